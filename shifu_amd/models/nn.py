@@ -1,0 +1,647 @@
+"""Encog-compatible MLP trainer (Shifu ``NN`` algorithm) on MI355X.
+
+Semantics follow the reference:
+  * network generation  ``DTrainUtils.generateNetwork``  (J/core/dtrain/DTrainUtils.java:303-386):
+    hidden activations from ``ActivationFunc``; output layer sigmoid for classification,
+    linear/relu/leakyrelu/swish for a linear target; every layer receives a bias neuron.
+  * gradient            ``SubGradient.process/processLevel`` (J/core/dtrain/nn/SubGradient.java:224-311):
+    delta = (ideal-actual)·(f'(out)+flatSpot)·significance, gradients are *ascent* directions
+    summed (not averaged) over all rows; flat spot 0.1 only for sigmoid layers
+    (J/core/dtrain/nn/AbstractNNWorker.java:605-609).
+  * update              ``Weight.calculateWeights`` (J/core/dtrain/Weight.java:194-343) - every rule adds.
+  * error               squared error averaged over records x outputs
+    (J/core/dtrain/nn/ParallelGradient.java:206-211).
+  * iteration 1 of the reference only syncs weights (J/core/dtrain/nn/AbstractNNWorker.java:525-527);
+    here initial weights are broadcast from rank 0 once at construction instead.
+
+MI355X design (not a translation): the whole local shard stays resident in HBM as bf16
+rows padded to a multiple of 128 columns with the bias neuron as a real column, each epoch
+streams it in row chunks through the hand-written MFMA kernels in ``ops/csrc/mlp_kernels.hip``
+(fused forward+activation, fused output/loss/delta row kernel, dgrad with fused derivative,
+TN wgrad via ``ds_read_b64_tr_b16``), sums the gradient in one fp32 buffer, all-reduces it once
+over RCCL with the error scalars in its tail, and applies the optimizer in one fused kernel on
+every rank (replicated optimizer, no parameter server).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..parallel import dist
+from ..utils.log import get_logger
+
+_log = get_logger("models.nn")
+
+ACT_IDS = {"sigmoid": 0, "tanh": 1, "linear": 2, "relu": 3, "leakyrelu": 4, "swish": 5,
+           "ptanh": 6, "log": 7, "sin": 8}
+ACT_DERIV_FROM_OUTPUT = {0, 1, 2, 3, 4, 6, 7}
+LOSS_IDS = {"squared": 0, "log": 1, "absolute": 2}
+RULE_IDS = {"B": 0, "Q": 1, "M": 2, "R": 3, "ADAM": 4, "ADAGRAD": 5, "RMSPROP": 6,
+            "MOMENTUM": 7, "NESTEROV": 8}
+PAD = 128
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def norm_act(name: str) -> str:
+    n = (name or "sigmoid").strip().lower()
+    return n if n in ACT_IDS else "sigmoid"   # DTrainUtils: unknown -> sigmoid
+
+
+# ------------------------------------------------------------------------------------------
+# activation math (torch, fp32) - the CPU oracle of common.h
+# ------------------------------------------------------------------------------------------
+def act_fwd(act: str, z: torch.Tensor) -> torch.Tensor:
+    if act == "sigmoid":
+        return torch.sigmoid(z)
+    if act == "tanh":
+        return torch.tanh(z)
+    if act == "linear":
+        return z
+    if act == "relu":
+        return torch.where(z <= 0, torch.zeros_like(z), z)
+    if act == "leakyrelu":
+        return torch.where(z <= 0, 0.01 * z, z)
+    if act == "swish":
+        return z * torch.sigmoid(z)
+    if act == "ptanh":
+        t = torch.tanh(z)
+        return torch.where(z > 0, t, 0.25 * t)
+    if act == "log":
+        return torch.where(z >= 0, torch.log1p(z.clamp(min=0)), -torch.log1p((-z).clamp(min=0)))
+    if act == "sin":
+        return torch.sin(z)
+    raise ValueError(act)
+
+
+def act_deriv(act: str, z: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+    if act == "sigmoid":
+        return a * (1 - a)
+    if act == "tanh":
+        return 1 - a * a
+    if act == "linear":
+        return torch.ones_like(a)
+    if act == "relu":
+        return (z > 0).to(a.dtype)
+    if act == "leakyrelu":
+        return torch.where(z <= 0, torch.full_like(a, 0.01), torch.ones_like(a))
+    if act == "swish":
+        s = torch.sigmoid(z)
+        return s + z * s * (1 - s)
+    if act == "ptanh":
+        return torch.where(z > 0, 1 - a * a, 0.25 * (1 - 16 * a * a))
+    if act == "log":
+        return torch.where(z >= 0, 1 / (1 + z.clamp(min=0)), 1 / (1 - z.clamp(max=0)))
+    if act == "sin":
+        return torch.cos(z)
+    raise ValueError(act)
+
+
+def flat_spot(act: str) -> float:
+    return 0.1 if act == "sigmoid" else 0.0
+
+
+@dataclass
+class MLPSpec:
+    n_in: int
+    hidden: list = field(default_factory=lambda: [50])
+    acts: list = field(default_factory=lambda: ["tanh"])
+    n_out: int = 1
+    out_act: str = "sigmoid"          # "sigmoid" (classification) or linear/relu/leakyrelu/swish
+    loss: str = "squared"
+
+    def __post_init__(self):
+        self.hidden = [int(h) for h in self.hidden]
+        acts = [norm_act(a) for a in (self.acts or [])]
+        while len(acts) < len(self.hidden):
+            acts.append(acts[-1] if acts else "sigmoid")
+        self.acts = acts[: len(self.hidden)]
+        self.out_act = norm_act(self.out_act)
+        self.loss = (self.loss or "squared").lower()
+        if self.loss not in LOSS_IDS:
+            self.loss = "squared"
+
+    @property
+    def layer_in(self):             # logical input width of each weight layer
+        return [self.n_in] + self.hidden
+
+    @property
+    def layer_out(self):
+        return self.hidden + [self.n_out]
+
+    @property
+    def layer_kpad(self):           # padded input width incl. bias column
+        return [round_up(i + 1, PAD) for i in self.layer_in]
+
+    def n_weights_encog(self) -> int:
+        return sum(o * (i + 1) for i, o in zip(self.layer_in, self.layer_out))
+
+
+class MLPParams:
+    """Flat fp32 parameter buffer with per-layer [out, in_pad] views (bias = column ``in``)."""
+
+    def __init__(self, spec: MLPSpec, device, dtype=torch.float32):
+        self.spec = spec
+        self.shapes = [(o, k) for o, k in zip(spec.layer_out, spec.layer_kpad)]
+        self.offsets = []
+        off = 0
+        for o, k in self.shapes:
+            self.offsets.append(off)
+            off += o * k
+        self.numel = off
+        self.flat = torch.zeros(off, dtype=dtype, device=device)
+
+    def views(self, flat=None):
+        flat = self.flat if flat is None else flat
+        return [flat[off: off + o * k].view(o, k) for off, (o, k) in zip(self.offsets, self.shapes)]
+
+    def valid_mask(self) -> torch.Tensor:
+        """1 for real weights (incl. bias column), 0 for padding."""
+        m = torch.zeros(self.numel, dtype=torch.bool)
+        for off, (o, k), i in zip(self.offsets, self.shapes, self.spec.layer_in):
+            m[off: off + o * k].view(o, k)[:, : i + 1] = True
+        return m
+
+    # ---- Encog flat layout (J/core/dtrain/dataset/FloatFlatNetwork.java:148-178) -----------
+    # layers output-first; block for (to=layer l+1 neurons, from=layer l incl. bias) is
+    # row-major [to][from+1], bias weight last.
+    def to_encog_flat(self) -> np.ndarray:
+        ws = self.views()
+        out = []
+        for l in reversed(range(len(ws))):
+            i = self.spec.layer_in[l]
+            out.append(ws[l][:, : i + 1].detach().double().cpu().numpy().reshape(-1))
+        return np.concatenate(out)
+
+    def from_encog_flat(self, flat: np.ndarray) -> None:
+        flat = np.asarray(flat, dtype=np.float64)
+        assert flat.size == self.spec.n_weights_encog(), (flat.size, self.spec.n_weights_encog())
+        ws = self.views()
+        pos = 0
+        with torch.no_grad():
+            self.flat.zero_()
+            for l in reversed(range(len(ws))):
+                i, o = self.spec.layer_in[l], self.spec.layer_out[l]
+                blk = torch.from_numpy(flat[pos: pos + o * (i + 1)].reshape(o, i + 1)).to(self.flat)
+                ws[l][:, : i + 1].copy_(blk)
+                pos += o * (i + 1)
+
+    def init_random(self, seed: int = 0, method: str = "default") -> None:
+        """Weight initialisers of ``DTrainUtils.generateNetwork`` (default / gaussian / xavier /
+        he / lecun).  "default" is a Nguyen-Widrow scaled uniform like Encog's reset()."""
+        g = torch.Generator().manual_seed(seed)
+        method = (method or "default").lower()
+        ws = self.views()
+        with torch.no_grad():
+            for l, w in enumerate(ws):
+                i, o = self.spec.layer_in[l], self.spec.layer_out[l]
+                if method == "gaussian":
+                    blk = torch.randn(o, i + 1, generator=g)
+                elif method == "xavier":
+                    blk = torch.randn(o, i + 1, generator=g) * math.sqrt(2.0 / (i + o))
+                elif method == "he":
+                    blk = torch.randn(o, i + 1, generator=g) * math.sqrt(2.0 / i)
+                elif method == "lecun":
+                    blk = torch.randn(o, i + 1, generator=g) * math.sqrt(1.0 / i)
+                else:
+                    blk = torch.rand(o, i + 1, generator=g) * 2 - 1
+                    beta = 0.7 * (o ** (1.0 / max(1, i)))
+                    nrm = blk[:, :i].norm(dim=1, keepdim=True).clamp(min=1e-12)
+                    blk[:, :i] = beta * blk[:, :i] / nrm
+                    blk[:, i] = (torch.rand(o, generator=g) * 2 - 1) * beta
+                w.zero_()
+                w[:, : i + 1].copy_(blk.to(w))
+
+
+@dataclass
+class TrainData:
+    """Resident (device) training shard: padded bf16/fp32 rows + targets + significance."""
+    x: torch.Tensor            # [N, K0] rows incl. bias column
+    y: torch.Tensor            # [N, n_out] fp32
+    s: torch.Tensor | None     # [N] fp32 significance
+    n: int
+
+
+class Optimizer:
+    """Replicated optimizer state + fused update (HIP kernel on GPU, torch on CPU)."""
+
+    def __init__(self, numel: int, device, propagation="R", learning_rate=0.1, momentum=0.5,
+                 adam_beta1=0.9, adam_beta2=0.999, learning_decay=0.0, reg=0.0, reg_level="NONE",
+                 fixed_mask=None):
+        prop = (propagation or "R").upper()
+        if prop not in RULE_IDS:
+            _log.warning("unknown propagation %s, using R", prop)
+            prop = "R"
+        self.prop = prop
+        self.rule = RULE_IDS[prop]
+        self.lr = float(learning_rate)
+        self.momentum = float(momentum)
+        self.beta1, self.beta2 = float(adam_beta1), float(adam_beta2)
+        self.learning_decay = float(learning_decay)
+        self.reg = float(reg)
+        self.reg_level = {"NONE": 0, "L1": 1, "L2": 2}.get(str(reg_level).upper(), 0)
+        self.device = device
+        z = lambda: torch.zeros(numel, dtype=torch.float32, device=device)  # noqa: E731
+        self.s0, self.s1 = z(), z()
+        self.s2 = torch.full((numel,), 0.1, dtype=torch.float32, device=device)  # RPROP update values
+        self.fixed = None if fixed_mask is None else fixed_mask.to(device=device, dtype=torch.uint8)
+        self.iteration = 0
+        self.num_train = 1.0
+
+    def state_dict(self):
+        return {"s0": self.s0.cpu(), "s1": self.s1.cpu(), "s2": self.s2.cpu(),
+                "iteration": self.iteration, "lr": self.lr}
+
+    def load_state_dict(self, d):
+        self.s0.copy_(d["s0"]); self.s1.copy_(d["s1"]); self.s2.copy_(d["s2"])
+        self.iteration = int(d["iteration"]); self.lr = float(d["lr"])
+
+    def step(self, w: torch.Tensor, g: torch.Tensor, num_train: float):
+        self.iteration += 1
+        if self.iteration > 1:
+            self.lr = self.lr * (1.0 - self.learning_decay)   # NNMaster.java:269
+        self.num_train = max(1.0, float(num_train))
+        qeps = 0.35 / self.num_train
+        qshrink = self.lr / (1.0 + self.lr)
+        if w.device.type == "cuda":
+            from ..ops import _native as nat
+            nat.call_hip("shifu_optimizer_step", w.data_ptr(), g.data_ptr(), self.s0.data_ptr(),
+                         self.s1.data_ptr(), self.s2.data_ptr(),
+                         None if self.fixed is None else self.fixed.data_ptr(), w.numel(), self.rule,
+                         self.reg_level, self.lr, self.momentum, self.beta1, self.beta2,
+                         self.learning_decay, self.reg, self.num_train, qeps, qshrink, 1e-4,
+                         self.iteration, nat.stream_of(w))
+            return
+        self._step_torch(w, g, qeps, qshrink)
+
+    def _step_torch(self, w, g, qeps, qshrink):
+        """CPU oracle of optimizer_kernel (fp32)."""
+        keep = None if self.fixed is None else self.fixed.bool()
+        w0 = w.clone()
+        s0, s1, s2, lr = self.s0, self.s1, self.s2, self.lr
+
+        def sgn(v):
+            return torch.where(v.abs() < 1e-7, torch.zeros_like(v), torch.sign(v))
+        rule = self.prop
+        delta = None
+        if rule == "B":
+            delta = g * lr + s0 * self.momentum
+            s0.copy_(delta)
+        elif rule == "M":
+            delta = torch.where(g.abs() < 1e-17, torch.zeros_like(g), torch.sign(g) * lr)
+        elif rule == "Q":
+            d, s, p = s0.clone(), -g + 1e-4 * w, -s1
+            ns = torch.zeros_like(g)
+            neg, pos, zero = d < 0, d > 0, d == 0
+            ns = ns + torch.where(neg & (s > 0), -qeps * s, torch.zeros_like(s))
+            quad = d * s / torch.where((p - s) == 0, torch.ones_like(s), p - s)
+            ns = ns + torch.where(neg, torch.where(s >= qshrink * p, lr * d, quad), torch.zeros_like(s))
+            ns = ns + torch.where(pos & (s < 0), -qeps * s, torch.zeros_like(s))
+            ns = ns + torch.where(pos, torch.where(s <= qshrink * p, lr * d, quad), torch.zeros_like(s))
+            ns = ns + torch.where(zero, -qeps * s, torch.zeros_like(s))
+            s0.copy_(ns)
+            s1.copy_(g)
+            delta = ns
+        elif rule == "R":
+            ch = sgn(g * s1)
+            up = torch.clamp(s2 * 1.2, max=50.0)
+            dn = torch.clamp(s2 * 0.5, min=1e-6)
+            delta = torch.where(ch > 0, sgn(g) * up, torch.where(ch < 0, -s0, sgn(g) * s2))
+            new_s2 = torch.where(ch > 0, up, torch.where(ch < 0, dn, s2))
+            new_s1 = torch.where(ch < 0, torch.zeros_like(g), g)
+            s2.copy_(new_s2)
+            s1.copy_(new_s1)
+            s0.copy_(delta)
+        elif rule == "ADAM":
+            s0.mul_(self.beta1).add_((1 - self.beta1) * g)
+            s1.mul_(self.beta2).add_((1 - self.beta2) * g * g)
+            mc = s0 / (1 - self.beta1 ** self.iteration)
+            vc = s1 / (1 - self.beta2 ** self.iteration)
+            w.add_(lr * mc / (vc.sqrt() + 1e-8))
+        elif rule == "ADAGRAD":
+            s0.add_(g * g)
+            w.add_(lr * g / (s0.sqrt() + 1e-8))
+        elif rule == "RMSPROP":
+            s0.add_(g * g)
+            s0.mul_(self.learning_decay).add_((1 - self.learning_decay) * g * g)
+            w.add_(lr * g / (s0.sqrt() + 1e-8))
+        elif rule == "MOMENTUM":
+            d = lr * g + self.momentum * s0
+            s0.copy_(d)
+            w.add_(d)
+        elif rule == "NESTEROV":
+            prev = s0.clone()
+            s0.copy_(self.momentum * prev + g * lr)
+            w.add_(self.momentum * prev - (1 + self.momentum) * s0)
+        if delta is not None:
+            if self.reg_level == 1 and self.reg != 0:
+                sh = self.reg / self.num_train
+                w.copy_(torch.sign(delta) * torch.clamp(delta.abs() - sh, min=0))
+            elif self.reg_level == 2:
+                w.add_(delta - self.reg * w / self.num_train)
+            else:
+                w.add_(delta)
+        if keep is not None:
+            w.copy_(torch.where(keep, w0, w))
+
+
+class MLPTrainer:
+    """Data-parallel full-batch (or mini-batch) MLP trainer."""
+
+    def __init__(self, spec: MLPSpec, device=None, propagation="R", learning_rate=0.1,
+                 momentum=0.5, adam_beta1=0.9, adam_beta2=0.999, learning_decay=0.0,
+                 reg=0.0, reg_level="NONE", seed=0, weight_init="default",
+                 chunk_rows=1 << 20, init_flat_encog=None, fixed_layers=None, wgrad_splits=None):
+        from ..utils.device import default_device
+        self.spec = spec
+        self.device = torch.device(device) if device is not None else default_device()
+        self.gpu = self.device.type == "cuda"
+        if self.gpu:
+            from ..ops import _native
+            _native.require_gpu_native()
+            if spec.layer_kpad[-1] > 512 or spec.n_out > 8:
+                raise ValueError("HIP output kernel supports last hidden width <= 511 and n_out <= 8")
+        self.params = MLPParams(spec, self.device)
+        if init_flat_encog is not None:
+            self.params.from_encog_flat(init_flat_encog)
+        else:
+            self.params.init_random(seed, weight_init)
+        dist.broadcast_(self.params.flat, 0)
+        self.valid = self.params.valid_mask().to(self.device)
+        # +2 tail slots: [error_sum, weight_sum] fused into the gradient all-reduce
+        self.gbuf = torch.zeros(self.params.numel + 2, dtype=torch.float32, device=self.device)
+        self.grad = self.gbuf[: self.params.numel]
+        fixed = None
+        if fixed_layers:
+            fixed = torch.zeros(self.params.numel, dtype=torch.bool)
+            for l in fixed_layers:      # FixedLayers: 1-based hidden layer ids (fine tuning)
+                li = int(l) - 1
+                if 0 <= li < len(self.params.shapes):
+                    o, k = self.params.shapes[li]
+                    fixed[self.params.offsets[li]: self.params.offsets[li] + o * k] = True
+        self.opt = Optimizer(self.params.numel, self.device, propagation, learning_rate, momentum,
+                             adam_beta1, adam_beta2, learning_decay, reg, reg_level, fixed)
+        self.chunk_rows = int(chunk_rows)
+        self.wgrad_splits = wgrad_splits
+        self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self._ws = None
+        self.last_error = float("nan")
+
+    # --------------------------------------------------------------------------------------
+    def prepare(self, x, y, s=None) -> TrainData:
+        """Host/device float rows -> resident padded rows (bias column = 1)."""
+        x = torch.as_tensor(x)
+        n, f = x.shape
+        assert f == self.spec.n_in, (f, self.spec.n_in)
+        k0 = self.spec.layer_kpad[0]
+        dt = torch.bfloat16 if self.gpu else torch.float32
+        xp = torch.zeros(n, k0, dtype=dt, device=self.device)
+        xp[:, :f] = x.to(self.device, dt)
+        xp[:, f] = 1
+        y = torch.as_tensor(y, dtype=torch.float32).reshape(n, -1).to(self.device)
+        assert y.shape[1] == self.spec.n_out
+        sd = None if s is None else torch.as_tensor(s, dtype=torch.float32).reshape(n).to(self.device)
+        return TrainData(xp, y.contiguous(), sd, n)
+
+    def _workspace(self, rows: int):
+        if self._ws is not None and self._ws["rows"] >= rows:
+            return self._ws
+        kp = self.spec.layer_kpad
+        L = len(self.spec.hidden)
+        ws = {"rows": rows, "acts": [], "deltas": [], "derivs": []}
+        for l in range(1, L + 1):
+            ws["acts"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device))
+            ws["deltas"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device))
+            need_d = ACT_IDS[self.spec.acts[l - 1]] not in ACT_DERIV_FROM_OUTPUT
+            ws["derivs"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device)
+                                if need_d else None)
+        self._ws = ws
+        return ws
+
+    def _weights_bf16(self):
+        """bf16 copies of the hidden-layer weights (+ transposed copies for dgrad)."""
+        ws = self.params.views()
+        kp = self.spec.layer_kpad
+        L = len(self.spec.hidden)
+        wb, wt = [], []
+        from ..ops import _native as nat
+        st = nat.stream_of(self.params.flat)
+        for l in range(L):
+            w = ws[l]
+            o, k = w.shape
+            b = torch.empty(o, k, dtype=torch.bfloat16, device=self.device)
+            nat.call_hip("shifu_cast_bf16", w.data_ptr(), k, b.data_ptr(), k, o, k, st)
+            wb.append(b)
+            if l >= 1:   # transposed copy for dgrad: [K_l, K_{l+1}] (columns >= o zero)
+                t = torch.empty(k, kp[l + 1], dtype=torch.bfloat16, device=self.device)
+                nat.call_hip("shifu_transpose_cast", w.data_ptr(), k, t.data_ptr(), o, k, kp[l + 1], st)
+                wt.append(t)
+            else:
+                wt.append(None)
+        return wb, wt
+
+    # --------------------------------------------------------------------------------------
+    def accumulate_gradients(self, data: TrainData, row_lo: int = 0, row_hi: int | None = None):
+        """Sum gradients/errors of rows [row_lo, row_hi) into self.grad / self.err_acc."""
+        row_hi = data.n if row_hi is None else row_hi
+        if self.gpu:
+            wb, wt = self._weights_bf16()
+            for r0 in range(row_lo, row_hi, self.chunk_rows):
+                r1 = min(row_hi, r0 + self.chunk_rows)
+                self._chunk_hip(data, r0, r1, wb, wt)
+        else:
+            for r0 in range(row_lo, row_hi, self.chunk_rows):
+                r1 = min(row_hi, r0 + self.chunk_rows)
+                self._chunk_torch(data, r0, r1)
+
+    def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt):
+        from ..ops import _native as nat
+        sp, kp = self.spec, self.spec.layer_kpad
+        L = len(sp.hidden)
+        mc = r1 - r0
+        ws = self._workspace(min(self.chunk_rows, data.n))
+        st = nat.stream_of(data.x)
+        gv = self.params.views(self.grad)
+        wv = self.params.views()
+        x = data.x[r0:r1]
+        acts = [x] + [a[:mc] for a in ws["acts"]]
+        dels = [None] + [d[:mc] for d in ws["deltas"]]
+        ders = [None] + [(d[:mc] if d is not None else None) for d in ws["derivs"]]
+        for l in range(L):
+            a_in, a_out = acts[l], acts[l + 1]
+            act = ACT_IDS[sp.acts[l]]
+            nat.call_hip("shifu_gemm_nt", a_in.data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
+                         a_out.data_ptr(), kp[l + 1], nat.ptr(ders[l + 1]), kp[l + 1], None, 0, None, 0,
+                         mc, kp[l + 1], kp[l], 0, act, sp.hidden[l], 1, flat_spot(sp.acts[l]), st)
+        # output layer + loss + last hidden delta + output wgrad
+        hid_act = ACT_IDS[sp.acts[L - 1]] if L else 2
+        y = data.y[r0:r1]
+        s = data.s[r0:r1] if data.s is not None else None
+        nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], nat.ptr(ders[L]), kp[L],
+                     wv[L].data_ptr(), y.data_ptr(), sp.n_out, nat.ptr(s),
+                     nat.ptr(dels[L]) if L else None, kp[L], gv[L].data_ptr(), self.err_acc.data_ptr(),
+                     None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act], hid_act,
+                     LOSS_IDS[sp.loss], flat_spot(sp.out_act), flat_spot(sp.acts[L - 1]) if L else 0.0, st)
+        splits = self.wgrad_splits
+        for l in range(L - 1, -1, -1):
+            # wgrad of layer l: G_l[h_l, K_l] += D_{l+1}^T A_l
+            if splits is None:
+                ntiles = math.ceil(sp.hidden[l] / 128) * (kp[l] // 128)
+                spl = max(1, min(mc // 256, 1024 // max(1, ntiles)))
+            else:
+                spl = splits
+            nat.call_hip("shifu_wgrad_tn", dels[l + 1].data_ptr(), kp[l + 1], acts[l].data_ptr(), kp[l],
+                         gv[l].data_ptr(), kp[l], mc, sp.hidden[l], kp[l], spl, st)
+            if l >= 1:
+                # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)
+                act = ACT_IDS[sp.acts[l - 1]]
+                nat.call_hip("shifu_gemm_nt", dels[l + 1].data_ptr(), kp[l + 1], wt[l].data_ptr(), kp[l + 1],
+                             kp[l], dels[l].data_ptr(), kp[l], None, 0, acts[l].data_ptr(), kp[l],
+                             nat.ptr(ders[l]), kp[l], mc, kp[l], kp[l + 1], 1, act, sp.hidden[l - 1], 0,
+                             flat_spot(sp.acts[l - 1]), st)
+
+    def _chunk_torch(self, data: TrainData, r0: int, r1: int):
+        """fp32 CPU oracle with exactly the HIP path's structure."""
+        sp, kp = self.spec, self.spec.layer_kpad
+        L = len(sp.hidden)
+        wv = self.params.views()
+        gv = self.params.views(self.grad)
+        x = data.x[r0:r1].float()
+        acts, zs = [x], [None]
+        for l in range(L):
+            z = acts[l] @ wv[l].t()
+            a = act_fwd(sp.acts[l], z)
+            ap = torch.zeros(a.shape[0], kp[l + 1], dtype=a.dtype)
+            ap[:, : sp.hidden[l]] = a
+            ap[:, sp.hidden[l]] = 1
+            acts.append(ap)
+            zs.append(z)
+        zo = acts[L] @ wv[L].t()
+        p = act_fwd(sp.out_act, zo)
+        y = data.y[r0:r1]
+        s = data.s[r0:r1].unsqueeze(1) if data.s is not None else torch.ones(r1 - r0, 1)
+        e = y - p
+        if sp.loss == "log":
+            dl = e * s
+            pc = p.clamp(1e-7, 1 - 1e-7)
+            if sp.n_out == 1:
+                err = -(torch.log(pc) * y + torch.log(1 - pc) * (1 - y)).sum()
+            else:
+                err = -(torch.log(pc) * y * s).sum()
+        elif sp.loss == "absolute":
+            dl = torch.where(y < p, torch.ones_like(p), -torch.ones_like(p)) * \
+                (act_deriv(sp.out_act, zo, p) + flat_spot(sp.out_act)) * s
+            err = (e.abs() * s).sum()
+        else:
+            dl = (act_deriv(sp.out_act, zo, p) + flat_spot(sp.out_act)) * e * s
+            err = ((e * s) ** 2).sum()
+        self.err_acc[0] += float(err)
+        self.err_acc[1] += float(s.sum())
+        gv[L].add_(dl.t() @ acts[L])
+        d = dl
+        for l in range(L - 1, -1, -1):
+            # delta of hidden layer l+1 (acts[l+1]) from the layer above
+            back = d @ wv[l + 1][:, : sp.hidden[l]]
+            dh = back * (act_deriv(sp.acts[l], zs[l + 1], acts[l + 1][:, : sp.hidden[l]]) + flat_spot(sp.acts[l]))
+            gv[l].add_(dh.t() @ acts[l])
+            d = dh
+
+    # --------------------------------------------------------------------------------------
+    def compute_gradients(self, data: TrainData, row_lo=0, row_hi=None):
+        """Local gradient pass + one fused all-reduce (grads ++ [err, wsum])."""
+        self.grad.zero_()
+        self.err_acc.zero_()
+        self.accumulate_gradients(data, row_lo, row_hi)
+        self.gbuf[-2:] = self.err_acc.to(torch.float32)
+        dist.all_reduce_(self.gbuf)
+        return self.gbuf
+
+    def step(self, data: TrainData, row_lo=0, row_hi=None, num_train_global: float | None = None) -> float:
+        """One epoch (iteration): full gradient over the shard, all-reduce, optimizer update.
+        Returns the global training error (squared error / (records x outputs))."""
+        gbuf = self.compute_gradients(data, row_lo, row_hi)
+        tail = gbuf[-2:].double().cpu() if not self.gpu else gbuf[-2:].double()
+        n_local = (data.n if row_hi is None else row_hi) - row_lo
+        if num_train_global is None:
+            t = torch.tensor([float(n_local)], dtype=torch.float64, device=self.device)
+            dist.all_reduce_(t)
+            num_train_global = float(t.item())
+        self.opt.step(self.params.flat, self.grad, num_train_global)
+        err = float(tail[0].item()) / max(1.0, num_train_global * self.spec.n_out)
+        self.last_error = err
+        return err
+
+    @torch.no_grad()
+    def evaluate(self, data: TrainData) -> float:
+        """Validation error (forward only), global over ranks."""
+        sp = self.spec
+        p = self.predict_rows(data.x)
+        y = data.y
+        s = data.s.unsqueeze(1) if data.s is not None else torch.ones_like(y[:, :1])
+        e = (y - p.to(y.dtype))
+        if sp.loss == "log":
+            pc = p.clamp(1e-7, 1 - 1e-7)
+            err = -(torch.log(pc) * y + torch.log(1 - pc) * (1 - y)).sum()
+        elif sp.loss == "absolute":
+            err = (e.abs() * s).sum()
+        else:
+            err = ((e * s) ** 2).sum()
+        t = torch.tensor([float(err), float(data.n)], dtype=torch.float64, device=self.device)
+        dist.all_reduce_(t)
+        return float(t[0] / max(1.0, t[1] * sp.n_out))
+
+    @torch.no_grad()
+    def predict_rows(self, xpad: torch.Tensor) -> torch.Tensor:
+        """Forward pass on padded rows -> [N, n_out] fp32 (HIP kernels on GPU)."""
+        sp, kp = self.spec, self.spec.layer_kpad
+        L = len(sp.hidden)
+        n = xpad.shape[0]
+        out = torch.empty(n, sp.n_out, dtype=torch.float32, device=self.device)
+        if not self.gpu:
+            wv = self.params.views()
+            a = xpad.float()
+            for l in range(L):
+                h = act_fwd(sp.acts[l], a @ wv[l].t())
+                ap = torch.zeros(n, kp[l + 1])
+                ap[:, : sp.hidden[l]] = h
+                ap[:, sp.hidden[l]] = 1
+                a = ap
+            return act_fwd(sp.out_act, a @ wv[L].t())
+        from ..ops import _native as nat
+        wb, _ = self._weights_bf16()
+        wv = self.params.views()
+        st = nat.stream_of(xpad)
+        ws = self._workspace(min(self.chunk_rows, n))
+        gscratch = torch.zeros(sp.n_out, kp[L], dtype=torch.float32, device=self.device)
+        escratch = torch.zeros(2, dtype=torch.float64, device=self.device)
+        ydummy = torch.zeros(min(self.chunk_rows, n), sp.n_out, dtype=torch.float32, device=self.device)
+        for r0 in range(0, n, self.chunk_rows):
+            r1 = min(n, r0 + self.chunk_rows)
+            mc = r1 - r0
+            acts = [xpad[r0:r1]] + [a[:mc] for a in ws["acts"]]
+            for l in range(L):
+                nat.call_hip("shifu_gemm_nt", acts[l].data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
+                             acts[l + 1].data_ptr(), kp[l + 1], None, 0, None, 0, None, 0, mc, kp[l + 1], kp[l],
+                             0, ACT_IDS[sp.acts[l]], sp.hidden[l], 1, 0.0, st)
+            nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], None, kp[L], wv[L].data_ptr(),
+                         ydummy.data_ptr(), sp.n_out, None, None, kp[L], gscratch.data_ptr(),
+                         escratch.data_ptr(), out[r0:r1].data_ptr(), sp.n_out, mc, kp[L], sp.layer_in[L],
+                         sp.n_out, ACT_IDS[sp.out_act], ACT_IDS[sp.acts[L - 1]] if L else 2, 0, 0.0, 0.0, st)
+        return out
+
+    # convenience ---------------------------------------------------------------------------
+    def encog_weights(self) -> np.ndarray:
+        return self.params.to_encog_flat()
+
+    def state_dict(self):
+        return {"flat": self.params.flat.detach().cpu(), "opt": self.opt.state_dict(),
+                "spec": self.spec.__dict__.copy()}
+
+    def load_state_dict(self, d):
+        self.params.flat.copy_(d["flat"].to(self.device))
+        self.opt.load_state_dict(d["opt"])

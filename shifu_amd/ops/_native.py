@@ -1,0 +1,133 @@
+"""Loader for the in-tree native libraries.
+
+* ``_lib/libshifu_hip.so`` - hand-written CDNA4 HIP kernels (built with
+  ``hipcc --offload-arch=gfx950``; sources ``shifu_amd/ops/csrc/*.hip``).
+* ``_lib/libshifu_rt.so``  - host C++ runtime (CSV parser, thread pool, binary IO;
+  sources ``shifu_amd/runtime/csrc/*.cpp``).
+
+Both are plain C ABIs loaded with :mod:`ctypes` so that device pointers / HIP streams are
+passed straight from torch tensors with no Python<->C++ ABI coupling.  On a GPU box a
+missing HIP library is a hard error (no silent eager fallback): callers on the GPU path use
+:func:`hip` which raises :class:`NativeUnavailable`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+LIB_DIR = Path(__file__).resolve().parent / "_lib"
+HIP_LIB = LIB_DIR / "libshifu_hip.so"
+RT_LIB = LIB_DIR / "libshifu_rt.so"
+
+_lock = threading.Lock()
+_hip = None
+_rt = None
+
+# argument codes: p=void*, l=int64, i=int32, f=float, d=double, s=hipStream_t
+_T = {"p": ctypes.c_void_p, "l": ctypes.c_long, "i": ctypes.c_int, "f": ctypes.c_float,
+      "d": ctypes.c_double, "s": ctypes.c_void_p, "P": ctypes.c_char_p}
+
+HIP_SIGNATURES = {
+    # mlp_kernels.hip
+    "shifu_gemm_nt": "plplipl" "plplpl" "iiiiiiif" "s",
+    "shifu_wgrad_tn": "plplpl" "iiiis",
+    "shifu_mlp_output": "plplppl" "pplpppl" "iiiiiii" "ff" "s",
+    "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
+    "shifu_cast_bf16": "plpliis",
+    "shifu_transpose_cast": "plpiiis",
+}
+
+RT_SIGNATURES = {}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def _bind(lib, sigs):
+    for name, sig in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            raise NativeUnavailable(f"symbol {name} missing from {lib._name}; rebuild with "
+                                    f"`python -m shifu_amd.build_native`")
+        fn.argtypes = [_T[c] for c in sig]
+        fn.restype = ctypes.c_int
+
+
+def register_hip(sigs: dict):
+    HIP_SIGNATURES.update(sigs)
+
+
+def register_rt(sigs: dict):
+    RT_SIGNATURES.update(sigs)
+
+
+def hip():
+    """The HIP kernel library (raises loudly when missing)."""
+    global _hip
+    if _hip is not None:
+        return _hip
+    with _lock:
+        if _hip is None:
+            if not HIP_LIB.exists():
+                raise NativeUnavailable(
+                    f"{HIP_LIB} not built: run `python -m shifu_amd.build_native` (hipcc gfx950)")
+            lib = ctypes.CDLL(str(HIP_LIB), mode=ctypes.RTLD_GLOBAL)
+            _bind(lib, HIP_SIGNATURES)
+            _hip = lib
+    return _hip
+
+
+def rt():
+    """The host C++ runtime library, or None if it is not built."""
+    global _rt
+    if _rt is not None:
+        return _rt
+    with _lock:
+        if _rt is None and RT_LIB.exists():
+            lib = ctypes.CDLL(str(RT_LIB))
+            _bind(lib, RT_SIGNATURES)
+            _rt = lib
+    return _rt
+
+
+def hip_available() -> bool:
+    try:
+        hip()
+        return True
+    except (NativeUnavailable, OSError):
+        return False
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"native call {name} failed with code {rc}")
+
+
+def call_hip(name: str, *args):
+    fn = getattr(hip(), name)
+    rc = fn(*args)
+    if rc != 0:
+        raise RuntimeError(f"HIP kernel launcher {name} returned {rc} (bad shape or HIP error)")
+    return rc
+
+
+def stream_of(t=None):
+    """Current torch HIP stream handle as an int (hipStream_t)."""
+    import torch
+    dev = t.device if t is not None else None
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def require_gpu_native():
+    """On a GPU run the HIP library must be present; raise otherwise."""
+    if os.environ.get("SHIFU_ALLOW_TORCH_FALLBACK") == "1":
+        return hip_available()
+    hip()
+    return True

@@ -1,0 +1,88 @@
+// Shared device helpers for the shifu_amd CDNA4 (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA 16x16x32 bf16 A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // MFMA 16x16 accumulator fragment
+typedef uint16_t bf16_t;                                     // raw bf16 bits
+
+#define SHIFU_API extern "C" __attribute__((visibility("default")))
+
+static constexpr int WAVE = 64;   // CDNA wavefront: 64 lanes, never 32
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even f32 -> bf16 (inputs are finite activations / deltas)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)(u >> 16);   // inf / nan passthrough
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// Activation functions, Encog/Shifu semantics (J/core/dtrain/DTrainUtils.java:303-386,
+// J/core/dtrain/nn/Activation*.java).  derivative(b = pre-activation sum, a = output).
+// ---------------------------------------------------------------------------------------
+enum Act : int {
+  ACT_SIGMOID = 0, ACT_TANH = 1, ACT_LINEAR = 2, ACT_RELU = 3, ACT_LEAKYRELU = 4,
+  ACT_SWISH = 5, ACT_PTANH = 6, ACT_LOG = 7, ACT_SIN = 8
+};
+
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
+    case ACT_TANH: return tanhf(x);
+    case ACT_LINEAR: return x;
+    case ACT_RELU: return x <= 0.f ? 0.f : x;
+    case ACT_LEAKYRELU: return x <= 0.f ? 0.01f * x : x;
+    case ACT_SWISH: return x / (1.f + __expf(-x));
+    case ACT_PTANH: return x > 0.f ? tanhf(x) : 0.25f * tanhf(x);   // ActivationPTANH.java:54-59
+    case ACT_LOG: return x >= 0.f ? __logf(1.f + x) : -__logf(1.f - x);
+    case ACT_SIN: return __sinf(x);
+  }
+  return x;
+}
+
+// true when derivative can be computed from the activation output alone
+__host__ __device__ __forceinline__ bool act_deriv_from_output(int act) {
+  return act == ACT_SIGMOID || act == ACT_TANH || act == ACT_LINEAR || act == ACT_RELU ||
+         act == ACT_LEAKYRELU || act == ACT_LOG || act == ACT_PTANH;
+}
+
+// derivative given output a (only valid when act_deriv_from_output(act))
+__device__ __forceinline__ float act_deriv_out(int act, float a) {
+  switch (act) {
+    case ACT_SIGMOID: return a * (1.f - a);
+    case ACT_TANH: return 1.f - a * a;
+    case ACT_LINEAR: return 1.f;
+    case ACT_RELU: return a <= 0.f ? 0.f : 1.f;
+    case ACT_LEAKYRELU: return a <= 0.f ? 0.01f : 1.f;
+    case ACT_LOG: { float b = a >= 0.f ? __expf(a) - 1.f : 1.f - __expf(-a);
+                    return b >= 0.f ? 1.f / (1.f + b) : 1.f / (1.f - b); }
+    case ACT_PTANH: return a > 0.f ? 1.f - a * a : 0.25f * (1.f - 16.f * a * a);
+  }
+  return 1.f;
+}
+
+// derivative given pre-activation b (general)
+__device__ __forceinline__ float act_deriv_pre(int act, float b) {
+  switch (act) {
+    case ACT_SWISH: { float s = 1.f / (1.f + __expf(-b)); return s + b * s * (1.f - s); }
+    case ACT_SIN: return __cosf(b);
+    default: return act_deriv_out(act, act_fwd(act, b));
+  }
+}

@@ -1,0 +1,101 @@
+"""HIP MLP kernels vs the fp32 PyTorch oracle (same bf16-rounded inputs)."""
+import pytest
+import torch
+
+from shifu_amd.models.nn import MLPSpec, MLPTrainer, TrainData
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(spec, n, seed=0, loss="squared"):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, spec.n_in, generator=g).bfloat16().float()
+    y = (torch.rand(n, spec.n_out, generator=g) > 0.5).float()
+    s = torch.rand(n, generator=g) + 0.5
+    return x, y, s
+
+
+@pytest.mark.parametrize("hidden,acts", [([64], ["sigmoid"]), ([96, 40], ["tanh", "sigmoid"]),
+                                         ([130, 70, 33], ["relu", "swish", "sigmoid"])])
+def test_gradients_match_cpu_oracle(hidden, acts):
+    spec = MLPSpec(n_in=75, hidden=hidden, acts=acts, n_out=1)
+    n = 3000
+    x, y, s = _mk(spec, n)
+    cpu = MLPTrainer(spec, device="cpu", seed=5, chunk_rows=1000)
+    gpu = MLPTrainer(spec, device="cuda", seed=5, chunk_rows=1024)
+    # make the oracle use exactly the bf16-rounded weights of the GPU path
+    cpu.params.flat.copy_(cpu.params.flat.bfloat16().float())
+    gpu.params.flat.copy_(cpu.params.flat.cuda())
+    dc, dg = cpu.prepare(x, y, s), gpu.prepare(x, y, s)
+    cpu.grad.zero_(); cpu.err_acc.zero_(); cpu.accumulate_gradients(dc)
+    gpu.grad.zero_(); gpu.err_acc.zero_(); gpu.accumulate_gradients(dg)
+    torch.cuda.synchronize()
+    gc, gg = cpu.grad, gpu.grad.cpu()
+    rel = (gc - gg).norm() / gc.norm()
+    assert rel < 3e-2, float(rel)
+    for vc, vg in zip(cpu.params.views(gc), gpu.params.views(gg)):
+        r = (vc - vg).norm() / vc.norm().clamp(min=1e-12)
+        assert r < 5e-2, float(r)
+    assert abs(float(cpu.err_acc[0]) - float(gpu.err_acc[0].cpu())) / float(cpu.err_acc[0]) < 1e-2
+    assert abs(float(cpu.err_acc[1]) - float(gpu.err_acc[1].cpu())) < 1e-2
+
+
+def test_gemm_nt_epilogue_exact_small():
+    """Identity-weight check with an ASYMMETRIC B: catches a transposed C write."""
+    from shifu_amd.ops import _native as nat
+    M, K, NB = 300, 128, 70
+    a = (torch.arange(M * K, dtype=torch.float32).reshape(M, K) % 7 - 3).bfloat16().cuda()
+    b = (torch.arange(NB * K, dtype=torch.float32).reshape(NB, K) % 5 - 2).bfloat16().cuda()
+    N = 128
+    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    nat.call_hip("shifu_gemm_nt", a.data_ptr(), K, b.data_ptr(), K, NB, c.data_ptr(), N, None, 0, None, 0,
+                 None, 0, M, N, K, 2, 2, NB, 0, 0.0, nat.stream_of(a))
+    ref = a.float() @ b.float().t()
+    torch.cuda.synchronize()
+    assert torch.allclose(c[:, :NB].float(), ref.bfloat16().float(), atol=0.5)
+    assert torch.all(c[:, NB:] == 0)
+
+
+def test_wgrad_tn_matches_torch():
+    from shifu_amd.ops import _native as nat
+    M, Nv, Kx = 5000, 150, 256
+    g = torch.Generator(device="cuda").manual_seed(0)
+    d = torch.randn(M, 256, generator=g, device="cuda").bfloat16()
+    d[:, Nv:] = 0
+    x = torch.randn(M, Kx, generator=g, device="cuda").bfloat16()
+    G = torch.zeros(Nv, Kx, device="cuda")
+    nat.call_hip("shifu_wgrad_tn", d.data_ptr(), 256, x.data_ptr(), Kx, G.data_ptr(), Kx, M, Nv, Kx, 7,
+                 nat.stream_of(d))
+    ref = d[:, :Nv].float().t() @ x.float()
+    torch.cuda.synchronize()
+    assert torch.allclose(G, ref, atol=1e-2, rtol=1e-3), float((G - ref).abs().max())
+
+
+def test_training_converges_on_gpu():
+    spec = MLPSpec(n_in=40, hidden=[64, 32], acts=["sigmoid", "sigmoid"], n_out=1)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(20000, 40, generator=g)
+    y = (x[:, :3].sum(1, keepdim=True) > 0).float()
+    tr = MLPTrainer(spec, device="cuda", seed=3, propagation="R", chunk_rows=8192)
+    data = tr.prepare(x, y)
+    errs = [tr.step(data) for _ in range(25)]
+    assert errs[-1] < 0.5 * errs[0], errs
+    p = tr.predict_rows(data.x).cpu()
+    acc = ((p > 0.5).float() == y).float().mean()
+    assert acc > 0.9, float(acc)
+
+
+def test_optimizer_kernel_matches_cpu():
+    from shifu_amd.models.nn import Optimizer
+    torch.manual_seed(0)
+    for rule in ["R", "B", "Q", "M", "ADAM", "ADAGRAD", "RMSPROP", "MOMENTUM", "NESTEROV"]:
+        oc = Optimizer(1000, "cpu", rule, learning_rate=0.05, learning_decay=0.1)
+        og = Optimizer(1000, "cuda", rule, learning_rate=0.05, learning_decay=0.1)
+        wc = torch.randn(1000)
+        wg = wc.clone().cuda()
+        for _ in range(4):
+            gr = torch.randn(1000)
+            oc.step(wc, gr, 100)
+            og.step(wg, gr.cuda(), 100)
+        torch.cuda.synchronize()
+        assert torch.allclose(wc, wg.cpu(), atol=1e-4, rtol=1e-4), rule

@@ -1,0 +1,153 @@
+"""CPU tests of the MLP engine semantics (the oracle the HIP kernels are checked against)."""
+import numpy as np
+import pytest
+import torch
+
+from shifu_amd.models.nn import (MLPParams, MLPSpec, MLPTrainer, Optimizer, act_deriv, act_fwd,
+                                 flat_spot)
+
+
+def _autograd_grads(tr: MLPTrainer, x, y, s=None):
+    """Reference gradient: -(dLoss/dW) where Loss = 0.5*sum(((y-p) s)^2)/s... computed with autograd
+    on the Encog formulation including the flat spot (flat spot is not a true derivative, so the
+    test uses tanh hidden layers (flat 0) and handles the sigmoid output flat spot analytically)."""
+    spec = tr.spec
+    ws = [w.clone().requires_grad_(True) for w in tr.params.views()]
+    a = tr.prepare(x, y).x.float()
+    for l in range(len(spec.hidden)):
+        z = a @ ws[l].t()
+        h = act_fwd(spec.acts[l], z)
+        pad = torch.zeros(a.shape[0], spec.layer_kpad[l + 1])
+        pad[:, spec.hidden[l]] = 1
+        hp = torch.cat([h, pad[:, spec.hidden[l]:]], 1)
+        a = hp
+    zo = a @ ws[-1].t()
+    return ws, zo, a
+
+
+def test_encog_flat_roundtrip():
+    spec = MLPSpec(n_in=7, hidden=[5, 3], acts=["sigmoid", "tanh"], n_out=2)
+    p = MLPParams(spec, "cpu")
+    p.init_random(3)
+    flat = p.to_encog_flat()
+    assert flat.size == spec.n_weights_encog() == 5 * 8 + 3 * 6 + 2 * 4
+    q = MLPParams(spec, "cpu")
+    q.from_encog_flat(flat)
+    assert torch.allclose(p.flat, q.flat)
+    # output-first ordering: first block is the output layer [2][3+1]
+    assert np.allclose(flat[:8], p.views()[2][:, :4].reshape(-1).numpy())
+
+
+def test_gradient_matches_autograd_linear_output():
+    """Hidden tanh + linear output + squared loss: Encog ascent gradient == -dL/dW for
+    L = 0.5 * sum((y - p)^2 s)."""
+    torch.manual_seed(0)
+    spec = MLPSpec(n_in=6, hidden=[8, 4], acts=["tanh", "tanh"], n_out=1, out_act="linear")
+    tr = MLPTrainer(spec, device="cpu", seed=1, chunk_rows=17)
+    x = torch.randn(50, 6)
+    y = torch.randn(50, 1)
+    data = tr.prepare(x, y)
+    tr.grad.zero_()
+    tr.err_acc.zero_()
+    tr.accumulate_gradients(data)
+    ws, zo, _ = _autograd_grads(tr, x, y)
+    loss = 0.5 * ((y - zo) ** 2).sum()
+    loss.backward()
+    for g_ours, w in zip(tr.params.views(tr.grad), ws):
+        assert torch.allclose(g_ours, -w.grad, atol=1e-4, rtol=1e-4)
+
+
+def test_sigmoid_flatspot_output_delta():
+    spec = MLPSpec(n_in=3, hidden=[], acts=[], n_out=1)
+    tr = MLPTrainer(spec, device="cpu", seed=1)
+    x = torch.randn(10, 3)
+    y = (torch.rand(10, 1) > 0.5).float()
+    data = tr.prepare(x, y)
+    tr.grad.zero_()
+    tr.err_acc.zero_()
+    tr.accumulate_gradients(data)
+    w = tr.params.views()[0]
+    p = torch.sigmoid(data.x @ w.t())
+    delta = (p * (1 - p) + 0.1) * (y - p)
+    g = delta.t() @ data.x
+    assert torch.allclose(tr.params.views(tr.grad)[0], g, atol=1e-5)
+
+
+def test_training_reduces_error_all_rules():
+    torch.manual_seed(0)
+    x = torch.randn(400, 5)
+    y = (x[:, :1] + 0.5 * x[:, 1:2] > 0).float()
+    for prop, lr in [("R", 0.1), ("B", 0.002), ("Q", 0.1), ("M", 0.002), ("ADAM", 0.01),
+                     ("ADAGRAD", 0.05), ("MOMENTUM", 0.001)]:
+        # NESTEROV is excluded on purpose: NesterovUpdate.java applies the descent-form update to
+        # Encog *ascent* gradients (sign flipped), so the reference's rule increases the loss;
+        # we reproduce it bit-for-bit (see test_optimizer_kernel_matches_cpu) rather than fix it.
+        spec = MLPSpec(n_in=5, hidden=[8], acts=["tanh"], n_out=1)
+        tr = MLPTrainer(spec, device="cpu", seed=2, propagation=prop, learning_rate=lr)
+        data = tr.prepare(x, y)
+        e0 = tr.step(data)
+        for _ in range(30):
+            e = tr.step(data)
+        assert e < e0, (prop, e0, e)
+
+
+def _rprop_ref(w, grads_seq):
+    """Direct port of Weight.updateWeightRLP (J/core/dtrain/Weight.java) in float64."""
+    n = len(w)
+    upd = np.full(n, 0.1)
+    last_d = np.zeros(n)
+    last_g = np.zeros(n)
+    w = w.copy()
+
+    def sign(v):
+        return 0 if abs(v) < 1e-7 else (1 if v > 0 else -1)
+    for g in grads_seq:
+        for i in range(n):
+            ch = sign(g[i] * last_g[i])
+            if ch > 0:
+                d = min(upd[i] * 1.2, 50)
+                wc = sign(g[i]) * d
+                upd[i] = d
+                last_g[i] = g[i]
+            elif ch < 0:
+                d = max(upd[i] * 0.5, 1e-6)
+                upd[i] = d
+                wc = -last_d[i]
+                last_g[i] = 0
+            else:
+                wc = sign(g[i]) * upd[i]
+                last_g[i] = g[i]
+            last_d[i] = wc
+            w[i] += wc
+    return w
+
+
+def test_rprop_matches_reference_port():
+    rng = np.random.default_rng(0)
+    w0 = rng.normal(size=20)
+    seq = [rng.normal(size=20) for _ in range(6)]
+    opt = Optimizer(20, "cpu", "R")
+    w = torch.tensor(w0, dtype=torch.float32)
+    for g in seq:
+        opt.step(w, torch.tensor(g, dtype=torch.float32), 100)
+    assert np.allclose(w.numpy(), _rprop_ref(w0, seq), atol=1e-5)
+
+
+def test_adam_matches_formula():
+    opt = Optimizer(3, "cpu", "ADAM", learning_rate=0.01)
+    w = torch.zeros(3)
+    g = torch.tensor([1.0, -2.0, 0.5])
+    opt.step(w, g, 10)
+    # first step: m=0.1g, v=0.001g^2, mc=g, vc=g^2 -> delta = lr * g/|g|
+    assert torch.allclose(w, 0.01 * torch.sign(g), atol=1e-6)
+
+
+@pytest.mark.parametrize("act", ["sigmoid", "tanh", "relu", "leakyrelu", "swish", "ptanh", "log", "sin", "linear"])
+def test_activation_derivatives(act):
+    z = torch.linspace(-3, 3, 101, dtype=torch.float64).requires_grad_(True)
+    a = act_fwd(act, z)
+    a.sum().backward()
+    d = act_deriv(act, z.detach(), a.detach())
+    mask = z.detach().abs() > 1e-3   # kinks at 0
+    assert torch.allclose(d[mask], z.grad[mask], atol=1e-6)
+    assert flat_spot(act) == (0.1 if act == "sigmoid" else 0.0)
