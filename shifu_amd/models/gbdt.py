@@ -1,0 +1,759 @@
+"""Gradient-boosted trees (GBT) and random forest (RF) on MI355X.
+
+Reference behaviour (Shifu ``GBT``/``RF``):
+  * rows are binned (``DTWorker.getBinIndex`` J/core/dtrain/dt/DTWorker.java:1001-1034);
+    categorical missing/unknown -> last bin (``:1148-1170``).
+  * level-wise growth to ``MaxDepth`` (root = level 1; children at level MaxDepth are leaves,
+    ``DTMaster.splitNodeForLevelWisedTree`` J/core/dtrain/dt/DTMaster.java:566-605).
+  * split search per (node, feature) = prefix scan over bins with ``MinInstancesPerNode`` /
+    ``MinInfoGain`` (``Impurity.computeImpurity`` J/core/dtrain/dt/Impurity.java:120-211);
+    categorical bins are ordered by mean target first.  Feature subsets are drawn per node
+    (``DTMaster.getSubsamplingFeatures`` :822-850).
+  * GBT: first tree fits the label and sets predict = leaf (weight 1.0); later trees fit
+    -dLoss/dpredict and add learningRate * leaf (``DTWorker.doCompute`` :620-670, ``Loss.java``).
+    Leaf value = weighted mean of the node's targets (no Newton step).
+  * RF: per-tree bagging weights (Poisson with replacement / Bernoulli), score = mean of trees.
+
+MI355X design: see ``ops/csrc/gbdt_kernels.hip`` (LDS histogram per (node, row range,
+32-feature group) work item, slab reduce + sibling subtraction + split scan, stable
+partition of a position->row permutation, tree application).  Multi-GPU: each rank owns a
+row shard; built-node histograms are all-reduced over RCCL (one bucket per level) and the
+split search is replicated deterministically, so no trees are ever broadcast.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..parallel import dist
+from ..utils.log import get_logger
+
+_log = get_logger("models.gbdt")
+
+NB = 256
+FG = 32
+IMPURITY_IDS = {"variance": 0, "friedmanmse": 1, "entropy": 2, "gini": 3}
+LOSS_IDS = {"squared": 0, "halfgradsquared": 1, "absolute": 2, "log": 3}
+
+
+def _strategy_count(strategy, n_feat: int, input_num: int, tree_num: int) -> int:
+    """Number of features a node samples (DTMaster.getSubsamplingFeatures); 0 = all."""
+    if strategy is None:
+        return n_feat
+    if isinstance(strategy, (int, float)) and not isinstance(strategy, bool):
+        return max(1, int(n_feat * float(strategy)))
+    s = str(strategy).strip().upper()
+    try:
+        v = float(s)
+        return max(1, int(n_feat * v))
+    except ValueError:
+        pass
+    if s == "HALF":
+        return n_feat // 2
+    if s == "ONETHIRD":
+        return n_feat // 3
+    if s == "TWOTHIRDS":
+        return n_feat * 2 // 3
+    if s == "SQRT":
+        return int(n_feat * math.sqrt(input_num) / input_num)
+    if s == "LOG2":
+        return int(n_feat * math.log(input_num) / math.log(2) / input_num)
+    if s == "AUTO":
+        return n_feat // 2 if tree_num > 1 else n_feat
+    return n_feat
+
+
+@dataclass
+class TreeConfig:
+    algorithm: str = "GBT"              # GBT | RF
+    tree_num: int = 100
+    max_depth: int = 7
+    min_instances_per_node: int = 5
+    min_info_gain: float = 0.0
+    impurity: str = "variance"
+    loss: str = "squared"
+    learning_rate: float = 0.05
+    feature_subset_strategy: object = "TWOTHIRDS"
+    bagging_sample_rate: float = 1.0
+    sample_with_replacement: bool = False
+    dropout_rate: float = 0.0
+    seed: int = 0
+    valid_tolerance: float = 0.0
+    early_stop: bool = False
+
+    def __post_init__(self):
+        self.algorithm = self.algorithm.upper()
+        self.impurity = (self.impurity or "variance").lower()
+        if self.impurity not in IMPURITY_IDS:
+            self.impurity = "variance"
+        self.loss = (self.loss or "squared").lower()
+        if self.loss not in LOSS_IDS:
+            self.loss = "squared"
+
+    @property
+    def is_gbt(self):
+        return self.algorithm == "GBT"
+
+
+class Tree:
+    """Heap-indexed tree (node id 1 = root, children 2i / 2i+1 as ``Node.leftIndex``)."""
+
+    def __init__(self, max_depth: int, weight: float = 1.0):
+        self.max_depth = max_depth
+        self.max_nodes = 1 << max_depth
+        m = self.max_nodes
+        self.feat = np.full(m, -1, dtype=np.int32)      # feature index (into the binned matrix)
+        self.thr = np.full(m, -1, dtype=np.int32)       # numeric: left iff bin <= thr
+        self.cat_left = np.zeros((m, 8), dtype=np.uint32)
+        self.value = np.zeros(m, dtype=np.float32)
+        self.wgt_cnt = np.zeros(m, dtype=np.float64)
+        self.gain = np.zeros(m, dtype=np.float32)
+        self.exists = np.zeros(m, dtype=bool)
+        self.weight = float(weight)                     # GBT: 1.0 for the first tree, else lr
+        self.features_used = []
+
+    def n_nodes(self) -> int:
+        return int(self.exists.sum())
+
+    def leaves(self):
+        return [i for i in range(1, self.max_nodes) if self.exists[i] and self.feat[i] < 0]
+
+    def device_arrays(self, device):
+        return (torch.from_numpy(self.feat).to(device), torch.from_numpy(self.thr).to(device),
+                torch.from_numpy(self.cat_left.view(np.int32)).to(device),
+                torch.from_numpy(self.value).to(device))
+
+    def predict_bins(self, bins: np.ndarray, is_cat: np.ndarray) -> np.ndarray:
+        """Host traversal (oracle for the HIP apply kernel)."""
+        n = bins.shape[0]
+        ids = np.ones(n, dtype=np.int64)
+        for _ in range(self.max_depth):
+            f = self.feat[ids]
+            active = f >= 0
+            if not active.any():
+                break
+            fa = np.where(active, f, 0)
+            b = bins[np.arange(n), fa].astype(np.int64)
+            catm = is_cat[fa].astype(bool)
+            bit = (self.cat_left[ids, b >> 5] >> (b & 31).astype(np.uint32)) & 1
+            left = np.where(catm, bit == 1, b <= self.thr[ids])
+            ids = np.where(active, np.where(left, 2 * ids, 2 * ids + 1), ids)
+        return self.value[ids]
+
+
+@dataclass
+class BinnedData:
+    """Resident binned shard: uint8 codes [N, Fp] (Fp multiple of 32) + targets/weights."""
+    bins: torch.Tensor
+    y: torch.Tensor
+    sig: torch.Tensor | None
+    nbins: np.ndarray               # [F] bins per feature (numeric: #boundaries, cat: #cats+1)
+    is_cat: np.ndarray              # [F] uint8
+    n_feat: int
+
+    @property
+    def n(self):
+        return self.bins.shape[0]
+
+    @property
+    def device(self):
+        return self.bins.device
+
+    @staticmethod
+    def from_codes(codes, y, nbins, is_cat=None, sig=None, device="cpu"):
+        codes = torch.as_tensor(codes)
+        n, f = codes.shape
+        fp = (f + FG - 1) // FG * FG
+        b = torch.zeros(n, fp, dtype=torch.uint8, device=device)
+        b[:, :f] = codes.to(device=device, dtype=torch.uint8)
+        y = torch.as_tensor(y, dtype=torch.float32).reshape(n).to(device)
+        s = None if sig is None else torch.as_tensor(sig, dtype=torch.float32).reshape(n).to(device)
+        nb = np.asarray(nbins, dtype=np.int32).reshape(f)
+        ic = np.zeros(f, np.uint8) if is_cat is None else np.asarray(is_cat, dtype=np.uint8).reshape(f)
+        return BinnedData(b, y, s, nb, ic, f)
+
+
+class TreeTrainer:
+    """Level-wise GBT/RF trainer over a resident binned shard."""
+
+    def __init__(self, cfg: TreeConfig, data: BinnedData, valid: BinnedData | None = None,
+                 items_per_node_group: int | None = None):
+        self.cfg = cfg
+        self.data = data
+        self.valid = valid
+        self.dev = data.device
+        self.gpu = self.dev.type == "cuda"
+        if self.gpu:
+            from ..ops import _native
+            _native.require_gpu_native()
+        self.F = data.n_feat
+        self.ngroups = (self.F + FG - 1) // FG
+        self.trees: list[Tree] = []
+        self.pred = torch.zeros(data.n, dtype=torch.float32, device=self.dev)
+        self.vpred = None if valid is None else torch.zeros(valid.n, dtype=torch.float32, device=valid.device)
+        self.nbins_t = torch.from_numpy(data.nbins.astype(np.int32)).to(self.dev)
+        self.is_cat_t = torch.from_numpy(data.is_cat.astype(np.uint8)).to(self.dev)
+        self.rng = np.random.default_rng(cfg.seed)
+        self.tgen = torch.Generator(device=self.dev).manual_seed(cfg.seed + 17 * dist.info().rank)
+        self.n_sub = _strategy_count(cfg.feature_subset_strategy, self.F, self.F, cfg.tree_num)
+        if self.n_sub <= 0 or self.n_sub > self.F:
+            self.n_sub = self.F
+        # work-item sizing: enough items to fill 256 CUs x 2 at the root
+        self.items_per_node_group = items_per_node_group
+        self.train_errors: list[float] = []
+        self.valid_errors: list[float] = []
+        self.timings = {"hist": 0.0, "split": 0.0, "partition": 0.0, "apply": 0.0}
+
+    # ------------------------------------------------------------------------------------
+    def _weights_for_tree(self) -> torch.Tensor:
+        c = self.cfg
+        n = self.data.n
+        sig = self.data.sig if self.data.sig is not None else torch.ones(n, device=self.dev)
+        rate = c.bagging_sample_rate
+        if c.sample_with_replacement or (not c.is_gbt and c.sample_with_replacement):
+            sub = torch.poisson(torch.full((n,), rate, device=self.dev), generator=self.tgen)
+        elif rate < 1.0:
+            sub = (torch.rand(n, device=self.dev, generator=self.tgen) <= rate).float()
+        else:
+            return sig.contiguous()
+        return (sig * sub).contiguous()
+
+    def _node_feature_mask(self, n_nodes: int) -> torch.Tensor | None:
+        if self.n_sub >= self.F:
+            return None
+        m = np.zeros((n_nodes, self.F), dtype=np.uint8)
+        for i in range(n_nodes):
+            m[i, self.rng.choice(self.F, self.n_sub, replace=False)] = 1
+        return torch.from_numpy(m).to(self.dev)
+
+    # ------------------------------------------------------------------------------------
+    def grow_tree(self, g: torch.Tensor, w: torch.Tensor, weight: float) -> Tree:
+        c = self.cfg
+        d = self.data
+        n = d.n
+        tree = Tree(c.max_depth, weight)
+        pos2row = torch.arange(n, dtype=torch.int32, device=self.dev)
+        pos_node = torch.zeros(n, dtype=torch.int32, device=self.dev)
+        # level-0 node: id 1, local range [0, n)
+        nodes = [{"id": 1, "start": 0, "end": n, "built": True, "parent": -1, "sibling": -1}]
+        hist_prev = None
+        # root stats for the root's own value
+        tot = dist.all_reduce_(torch.stack([w.double().sum(), (w.double() * g.double()).sum()]))
+        tw, ts = float(tot[0]), float(tot[1])
+        tree.exists[1] = True
+        tree.value[1] = ts / tw if tw != 0 else 0.0
+        tree.wgt_cnt[1] = tw
+        for level in range(1, c.max_depth):
+            if not nodes:
+                break
+            # slots: built nodes first (contiguous for the all-reduce), then derived; positions
+            # carry the partition's child index -> remap them to the new slot numbering
+            nodes.sort(key=lambda z: (not z["built"], z["id"]))
+            for s_, z in enumerate(nodes):
+                z["slot"] = s_
+            if level > 1:
+                remap = torch.full((len(nodes) + 1,), -1, dtype=torch.int32, device=self.dev)
+                for z in nodes:
+                    remap[z["pidx"]] = z["slot"]
+                pos_node = torch.where(pos_node >= 0, remap[pos_node.clamp(min=0).long()], pos_node)
+            slot_of = {z["id"]: z["slot"] for z in nodes}
+            for z in nodes:
+                if not z["built"]:
+                    z["sib_slot"] = slot_of[z["id"] ^ 1]
+            n_built = sum(1 for z in nodes if z["built"])
+            t0 = time.perf_counter()
+            hist = self._build_and_split(nodes, n_built, g, w, pos2row, hist_prev)
+            best = hist["best"]            # per slot: (feat, bin, gain, lw, ls, rw, rs, valid)
+            self.timings["split"] += time.perf_counter() - t0
+            # decisions ------------------------------------------------------------------
+            split_feat = np.full(len(nodes), -1, dtype=np.int32)
+            split_bin = np.full(len(nodes), -1, dtype=np.int32)
+            cat_left = np.zeros((len(nodes), 8), dtype=np.uint32)
+            children = []
+            last = level + 1 >= c.max_depth
+            for z in nodes:
+                s_ = z["slot"]
+                f, b, gain, lw, ls, rw, rs, ok = best[s_]
+                nid = z["id"]
+                if not ok:
+                    continue
+                f = int(f)
+                tree.feat[nid] = f
+                tree.gain[nid] = gain
+                tree.features_used.append(f)
+                if d.is_cat[f]:
+                    order = hist["cat_order"][s_][f]
+                    left_bins = order[: int(b) + 1]
+                    for lb in left_bins:
+                        cat_left[s_, lb >> 5] |= np.uint32(1 << (lb & 31))
+                    tree.cat_left[nid] = cat_left[s_]
+                    tree.thr[nid] = -1
+                else:
+                    tree.thr[nid] = int(b)
+                    split_bin[s_] = int(b)
+                split_feat[s_] = f
+                for cid, cw, cs in ((2 * nid, lw, ls), (2 * nid + 1, rw, rs)):
+                    tree.exists[cid] = True
+                    tree.value[cid] = cs / cw if cw != 0 else 0.0
+                    tree.wgt_cnt[cid] = cw
+                children.append((z, lw, rw))
+            if last or not children:
+                break
+            # partition rows of split nodes -----------------------------------------------
+            t0 = time.perf_counter()
+            pos2row, pos_node, ranges = self._partition(nodes, split_feat, split_bin, cat_left, pos2row, pos_node)
+            self.timings["partition"] += time.perf_counter() - t0
+            new_nodes = []
+            for z, lw, rw in children:
+                lo, mid, hi = ranges[z["slot"]]
+                # build the globally smaller child, derive the other (identical on all ranks)
+                left_built = lw <= rw
+                k = len(new_nodes)     # child index written by the partition scatter
+                new_nodes.append({"id": 2 * z["id"], "start": lo, "end": mid, "built": left_built,
+                                  "parent": z["slot"], "pidx": k})
+                new_nodes.append({"id": 2 * z["id"] + 1, "start": mid, "end": hi, "built": not left_built,
+                                  "parent": z["slot"], "pidx": k + 1})
+            hist_prev = hist["hist"]
+            nodes = new_nodes
+        return tree
+
+    # ------------------------------------------------------------------------------------
+    def _make_items(self, nodes, n_built):
+        """Work items (node_slot, lo, hi, group) for built nodes; chunked for parallelism."""
+        target_items = 2048
+        rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
+        items, node_items = [], {}
+        per = self.items_per_node_group
+        for z in nodes:
+            if not z["built"]:
+                continue
+            m = z["end"] - z["start"]
+            if m <= 0:
+                continue
+            if per is None:
+                share = m / max(1, rows_built)
+                k = max(1, int(round(target_items * share / self.ngroups)))
+                k = min(k, max(1, m // 4096), 64)
+            else:
+                k = per
+            step = (m + k - 1) // k
+            for gi in range(self.ngroups):
+                lst = node_items.setdefault((z["slot"], gi), [])
+                for j in range(k):
+                    lo = z["start"] + j * step
+                    hi = min(z["end"], lo + step)
+                    if lo >= hi:
+                        continue
+                    lst.append(len(items))
+                    items.append((z["slot"], lo, hi, gi))
+        return items, node_items
+
+    def _build_and_split(self, nodes, n_built, g, w, pos2row, hist_prev):
+        F = self.F
+        nn = len(nodes)
+        mask = self._node_feature_mask(nn)
+        imp = IMPURITY_IDS[self.cfg.impurity]
+        min_inst = float(self.cfg.min_instances_per_node)
+        min_gain = float(self.cfg.min_info_gain)
+        hist = torch.zeros(nn, F, NB, 2, dtype=torch.float32, device=self.dev)
+        if self.gpu:
+            best, cat_order = self._build_and_split_hip(nodes, n_built, g, w, pos2row, hist_prev, hist, mask,
+                                                        imp, min_inst, min_gain)
+        else:
+            best, cat_order = self._build_and_split_torch(nodes, n_built, g, w, pos2row, hist_prev, hist, mask,
+                                                          imp, min_inst, min_gain)
+        return {"hist": hist, "best": best, "cat_order": cat_order}
+
+    def _select_best(self, cand: torch.Tensor, nn: int):
+        """cand [nn, F, 8] -> per node best (lowest feature on ties)."""
+        gains = cand[:, :, 0].clone()
+        valid = cand[:, :, 6] > 0
+        gains[~valid] = -float("inf")
+        fbest = torch.argmax(gains, dim=1)                       # first max -> lowest feature
+        rows = cand[torch.arange(nn, device=cand.device), fbest]  # [nn, 8]
+        out = torch.cat([fbest.unsqueeze(1).float(), rows[:, 1:2], rows[:, 0:1], rows[:, 2:6], rows[:, 6:7]], 1)
+        out = out.cpu().double().numpy()
+        ok = valid.any(dim=1).cpu().numpy()
+        res = []
+        for i in range(nn):
+            f, b, gain, lw, ls, rw, rs, v = out[i]
+            res.append((int(f), int(b), float(gain), float(lw), float(ls), float(rw), float(rs), bool(ok[i])))
+        return res
+
+    def _build_and_split_hip(self, nodes, n_built, g, w, pos2row, hist_prev, hist, mask, imp, min_inst, min_gain):
+        from ..ops import _native as nat
+        d = self.data
+        F, nn = self.F, len(nodes)
+        st = nat.stream_of(d.bins)
+        items, node_items = self._make_items(nodes, n_built)
+        max_items = max([len(v) for v in node_items.values()] + [1])
+        ni = np.full((nn, self.ngroups, max_items), -1, dtype=np.int32)
+        for (slot, gi), lst in node_items.items():
+            ni[slot, gi, : len(lst)] = lst
+        ni_t = torch.from_numpy(ni).to(self.dev)
+        feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
+        cand = torch.zeros(nn, F, 8, dtype=torch.float32, device=self.dev)
+        cat_order = torch.zeros(nn, F, NB, dtype=torch.uint8, device=self.dev) if d.is_cat.any() else None
+        t0 = time.perf_counter()
+        if items:
+            it = torch.tensor(items, dtype=torch.int32, device=self.dev)
+            slab = torch.empty(len(items), FG, NB, 2, dtype=torch.float32, device=self.dev)
+            nat.call_hip("shifu_gbdt_hist", d.bins.data_ptr(), d.bins.shape[1], pos2row.data_ptr(), w.data_ptr(),
+                         g.data_ptr(), it.data_ptr(), len(items), slab.data_ptr(), F, st)
+        else:
+            slab = torch.zeros(1, FG, NB, 2, dtype=torch.float32, device=self.dev)
+        built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
+        derived = [z for z in nodes if not z["built"]]
+        if n_built:
+            nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, None, None, None,
+                         hist.data_ptr(), built.data_ptr(), n_built, feat_list.data_ptr(), F,
+                         self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), None, cand.data_ptr(), None, F, 0, imp,
+                         0, min_inst, min_gain, st)
+        self.timings["hist"] += time.perf_counter() - t0
+        # cross-rank reduction of the built-node histograms (one RCCL bucket per level)
+        if n_built:
+            dist.all_reduce_(hist[:n_built])
+        mptr = None if mask is None else mask.data_ptr()
+        cptr = None if cat_order is None else cat_order.data_ptr()
+        if n_built:
+            nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, None, None, None,
+                         hist.data_ptr(), built.data_ptr(), n_built, feat_list.data_ptr(), F,
+                         self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), mptr, cand.data_ptr(), cptr, F, 2, imp,
+                         1, min_inst, min_gain, st)
+        if derived:
+            dl = torch.tensor([z["slot"] for z in derived], dtype=torch.int32, device=self.dev)
+            par = np.zeros(nn, np.int32)
+            sib = np.zeros(nn, np.int32)
+            for z in derived:
+                par[z["slot"]] = z["parent"]
+                sib[z["slot"]] = z["sib_slot"]
+            par_t = torch.from_numpy(par).to(self.dev)
+            sib_t = torch.from_numpy(sib).to(self.dev)
+            nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, hist_prev.data_ptr(),
+                         par_t.data_ptr(), sib_t.data_ptr(), hist.data_ptr(), dl.data_ptr(), len(derived),
+                         feat_list.data_ptr(), F, self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), mptr,
+                         cand.data_ptr(), cptr, F, 1, imp, 1, min_inst, min_gain, st)
+        best = self._select_best(cand, nn)
+        co = None if cat_order is None else cat_order.cpu().numpy()
+        return best, co
+
+    def _build_and_split_torch(self, nodes, n_built, g, w, pos2row, hist_prev, hist, mask, imp, min_inst,
+                               min_gain):
+        """CPU oracle: same decomposition with torch ops (fp64 scan)."""
+        d = self.data
+        F, nn = self.F, len(nodes)
+        bins = d.bins[:, :F].long()
+        for z in nodes:
+            if not z["built"]:
+                continue
+            rows = pos2row[z["start"]: z["end"]].long()
+            if rows.numel() == 0:
+                continue
+            b = bins[rows]                                   # [m, F]
+            ww = w[rows].float()
+            gg = (w[rows] * g[rows]).float()
+            idx = (torch.arange(F).unsqueeze(0) * NB + b).reshape(-1)
+            hw = torch.zeros(F * NB, dtype=torch.float32)
+            hg = torch.zeros(F * NB, dtype=torch.float32)
+            hw.index_add_(0, idx, ww.unsqueeze(1).expand(-1, F).reshape(-1))
+            hg.index_add_(0, idx, gg.unsqueeze(1).expand(-1, F).reshape(-1))
+            hist[z["slot"], :, :, 0] = hw.view(F, NB)
+            hist[z["slot"], :, :, 1] = hg.view(F, NB)
+        if n_built:
+            dist.all_reduce_(hist[:n_built])
+        for z in nodes:
+            if not z["built"]:
+                hist[z["slot"]] = hist_prev[z["parent"]] - hist[z["sib_slot"]]
+                hist[z["slot"], :, :, 0].clamp_(min=0)
+        cand = torch.zeros(nn, F, 8, dtype=torch.float32)
+        cat_order = np.zeros((nn, F, NB), dtype=np.uint8) if d.is_cat.any() else None
+        H = hist.double()
+        for s_ in range(nn):
+            for f in range(F):
+                if mask is not None and not mask[s_, f]:
+                    continue
+                cw = H[s_, f, :, 0].clone()
+                cs = H[s_, f, :, 1].clone()
+                nb = int(d.nbins[f])
+                if d.is_cat[f]:
+                    keys = [(1e300 if b >= nb else (float(cs[b] / cw[b]) if cw[b] != 0 else 4.9e-324), b)
+                            for b in range(NB)]
+                    order = [b for _, b in sorted(keys)]
+                    cat_order[s_, f] = order
+                    cw, cs = cw[order], cs[order]
+                pw, ps = torch.cumsum(cw, 0), torch.cumsum(cs, 0)
+                tw, ts = float(pw[-1]), float(ps[-1])
+                best, bb = -1.0, -1
+                for b in range(nb - 1):
+                    lw, ls = float(pw[b]), float(ps[b])
+                    rw, rs = tw - lw, ts - ls
+                    if lw <= min_inst or rw <= min_inst:
+                        continue
+                    gain = _gain_py(imp, lw, ls, rw, rs)
+                    if not gain > min_gain:
+                        continue
+                    if gain > best:
+                        best, bb = gain, b
+                if bb >= 0:
+                    lw, ls = float(pw[bb]), float(ps[bb])
+                    cand[s_, f] = torch.tensor([best, bb, lw, ls, tw - lw, ts - ls, 1.0, tw])
+        return self._select_best(cand, nn), cat_order
+
+    # ------------------------------------------------------------------------------------
+    def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node):
+        d = self.data
+        nn = len(nodes)
+        n = d.n
+        starts = np.array([z["start"] for z in nodes], dtype=np.int64)
+        ends = np.array([z["end"] for z in nodes], dtype=np.int64)
+        # positions of unsplit nodes are never moved; mark non-split node positions -1
+        if self.gpu:
+            from ..ops import _native as nat
+            st = nat.stream_of(d.bins)
+            sf = torch.from_numpy(split_feat).to(self.dev)
+            sb = torch.from_numpy(split_bin).to(self.dev)
+            cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
+            flag = torch.empty(n, dtype=torch.int32, device=self.dev)
+            nat.call_hip("shifu_gbdt_partition_flag", d.bins.data_ptr(), d.bins.shape[1], pos2row.data_ptr(),
+                         pos_node.data_ptr(), sf.data_ptr(), sb.data_ptr(), cl.data_ptr(), self.is_cat_t.data_ptr(),
+                         flag.data_ptr(), n, st)
+            cum = torch.cumsum(flag, 0, dtype=torch.int32)
+            # per-node: #left = cum[end-1] - cum[start-1]
+            idx_end = torch.from_numpy(np.maximum(ends - 1, 0)).to(self.dev)
+            idx_start = torch.from_numpy(np.maximum(starts - 1, 0)).to(self.dev)
+            ce = cum[idx_end].cpu().numpy().astype(np.int64)
+            cb = cum[idx_start].cpu().numpy().astype(np.int64)
+            cb = np.where(starts > 0, cb, 0)
+            ce = np.where(ends > starts, ce, cb)
+            nleft = ce - cb
+            child_l = np.full(nn, -1, np.int32)
+            child_r = np.full(nn, -1, np.int32)
+            ranges = {}
+            k = 0
+            for z in nodes:
+                s_ = z["slot"]
+                if split_feat[s_] >= 0:
+                    child_l[s_], child_r[s_] = k, k + 1
+                    k += 2
+                ranges[s_] = (int(starts[s_]), int(starts[s_] + nleft[s_]), int(ends[s_]))
+            new_p2r = torch.empty_like(pos2row)
+            new_pn = torch.empty_like(pos_node)
+            t = lambda a, dt=np.int32: torch.from_numpy(np.ascontiguousarray(a.astype(dt))).to(self.dev)  # noqa
+            nat.call_hip("shifu_gbdt_partition_scatter", pos2row.data_ptr(), pos_node.data_ptr(), flag.data_ptr(),
+                         cum.data_ptr(), t(starts).data_ptr(), t(nleft).data_ptr(), t(cb).data_ptr(), sf.data_ptr(),
+                         t(child_l).data_ptr(), t(child_r).data_ptr(), new_p2r.data_ptr(), new_pn.data_ptr(), n, st)
+            # child slot ids follow the order of new_nodes built by the caller (left, right per split)
+            return new_p2r, new_pn, ranges
+        # CPU path
+        new_p2r = pos2row.clone()
+        new_pn = torch.full_like(pos_node, -1)
+        ranges = {}
+        k = 0
+        bins = d.bins
+        for z in nodes:
+            s_ = z["slot"]
+            lo, hi = z["start"], z["end"]
+            if split_feat[s_] < 0:
+                ranges[s_] = (lo, lo, hi)
+                continue
+            rows = pos2row[lo:hi].long()
+            f = int(split_feat[s_])
+            b = bins[rows, f].long()
+            if d.is_cat[f]:
+                words = torch.from_numpy(cat_left[s_].astype(np.int64))
+                left = ((words[b >> 5] >> (b & 31)) & 1) == 1
+            else:
+                left = b <= int(split_bin[s_])
+            lrows, rrows = rows[left], rows[~left]
+            new_p2r[lo: lo + lrows.numel()] = lrows.int()
+            new_p2r[lo + lrows.numel(): hi] = rrows.int()
+            new_pn[lo: lo + lrows.numel()] = k
+            new_pn[lo + lrows.numel(): hi] = k + 1
+            k += 2
+            ranges[s_] = (lo, lo + lrows.numel(), hi)
+        return new_p2r, new_pn, ranges
+
+    # ------------------------------------------------------------------------------------
+    def apply_tree(self, tree: Tree, data: BinnedData, pred: torch.Tensor, scale: float, set_mode: bool):
+        if data.device.type == "cuda":
+            from ..ops import _native as nat
+            feat, thr, cl, val = tree.device_arrays(data.device)
+            nat.call_hip("shifu_gbdt_apply_tree", data.bins.data_ptr(), data.bins.shape[1], None, feat.data_ptr(),
+                         thr.data_ptr(), cl.data_ptr(), val.data_ptr(),
+                         torch.from_numpy(data.is_cat.astype(np.uint8)).to(data.device).data_ptr(),
+                         pred.data_ptr(), float(scale), int(set_mode), None, data.n, tree.max_nodes,
+                         nat.stream_of(pred))
+        else:
+            v = torch.from_numpy(tree.predict_bins(data.bins.numpy(), data.is_cat)).float()
+            if set_mode:
+                pred.copy_(v)
+            else:
+                pred.add_(scale * v)
+
+    def _residual(self, pred, data: BinnedData, out):
+        """out = -dLoss/dpred; returns (sum s*err, sum s) global."""
+        loss = LOSS_IDS[self.cfg.loss]
+        err = torch.zeros(2, dtype=torch.float64, device=pred.device)
+        if pred.device.type == "cuda":
+            from ..ops import _native as nat
+            nat.call_hip("shifu_gbdt_residual", pred.data_ptr(), data.y.data_ptr(),
+                         None if data.sig is None else data.sig.data_ptr(), out.data_ptr(), err.data_ptr(),
+                         data.n, loss, nat.stream_of(pred))
+        else:
+            p, y = pred, data.y
+            s = data.sig if data.sig is not None else torch.ones_like(y)
+            if loss == 1:
+                gr, e = p - y, (p - y) ** 2
+            elif loss == 2:
+                gr, e = torch.where(y < p, torch.ones_like(p), -torch.ones_like(p)), (y - p).abs()
+            elif loss == 3:
+                gr = (2 - 4 * y) / torch.exp(4 * y * p - 2 * p)
+                e = torch.log1p(1 + torch.exp(2 * p - 4 * p * y))
+            else:
+                gr, e = 2 * (p - y), (p - y) ** 2
+            out.copy_(-gr)
+            err[0] = (s.double() * e.double()).sum()
+            err[1] = s.double().sum()
+        dist.all_reduce_(err)
+        return float(err[0] / max(err[1], 1e-12))
+
+    # ------------------------------------------------------------------------------------
+    def train(self, n_trees: int | None = None, callback=None):
+        c = self.cfg
+        n_trees = c.tree_num if n_trees is None else n_trees
+        d = self.data
+        out = torch.empty(d.n, dtype=torch.float32, device=self.dev)
+        vout = None if self.valid is None else torch.empty(self.valid.n, dtype=torch.float32, device=self.dev)
+        for _ in range(n_trees):
+            tid = len(self.trees)
+            w = self._weights_for_tree()
+            if c.is_gbt:
+                if tid == 0:
+                    g = d.y
+                else:
+                    g = out
+                tree = self.grow_tree(g, w, 1.0 if tid == 0 else c.learning_rate)
+                t0 = time.perf_counter()
+                self.apply_tree(tree, d, self.pred, tree.weight, tid == 0)
+                if self.valid is not None:
+                    self.apply_tree(tree, self.valid, self.vpred, tree.weight, tid == 0)
+                self.timings["apply"] += time.perf_counter() - t0
+                terr = self._residual(self.pred, d, out)
+                verr = self._residual(self.vpred, self.valid, vout) if self.valid is not None else float("nan")
+            else:
+                tree = self.grow_tree(d.y, w, 1.0)
+                self.apply_tree(tree, d, self.pred, 1.0, False)
+                if self.valid is not None:
+                    self.apply_tree(tree, self.valid, self.vpred, 1.0, False)
+                k = tid + 1
+                terr = self._residual(self.pred / k, d, out)
+                verr = self._residual(self.vpred / k, self.valid, vout) if self.valid is not None else float("nan")
+            self.trees.append(tree)
+            self.train_errors.append(terr)
+            self.valid_errors.append(verr)
+            if callback:
+                callback(tid, tree, terr, verr)
+        return self.trees
+
+    def predict(self, data: BinnedData) -> torch.Tensor:
+        p = torch.zeros(data.n, dtype=torch.float32, device=data.device)
+        for i, t in enumerate(self.trees):
+            if self.cfg.is_gbt:
+                self.apply_tree(t, data, p, t.weight, i == 0)
+            else:
+                self.apply_tree(t, data, p, 1.0, False)
+        if not self.cfg.is_gbt and self.trees:
+            p /= len(self.trees)
+        return p
+
+
+def _gain_py(imp, lw, ls, rw, rs):
+    c, s = lw + rw, ls + rs
+    if imp == 1:
+        dd = rw * ls - lw * rs
+        return dd * dd / (lw * rw * c)
+    if imp in (2, 3):
+        def ent(nn, p1):
+            if nn <= 0:
+                return 0.0
+            r1 = p1 / nn
+            r0 = 1 - r1
+            if imp == 3:
+                return -(r1 * r1 + r0 * r0)
+            e = 0.0
+            if r1 > 0:
+                e -= r1 * math.log2(r1)
+            if r0 > 0:
+                e -= r0 * math.log2(r0)
+            return e
+        return ent(c, s) - (lw / c) * ent(lw, ls) - (rw / c) * ent(rw, rs)
+    return (ls * ls / lw + rs * rs / rw - s * s / c) / c
+
+
+# ------------------------------------------------------------------------------------------
+# smoke + bench hooks
+# ------------------------------------------------------------------------------------------
+def synthetic_binned(n, f, device, seed=0, n_bins=256):
+    """uint8 codes [n, Fp] generated chunk-wise on the device (no int32 staging of the whole
+    matrix) + labels from a hidden rule on the first two features."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    fp = (f + FG - 1) // FG * FG
+    codes = torch.zeros(n, fp, dtype=torch.uint8, device=device)
+    y = torch.empty(n, dtype=torch.float32, device=device)
+    step = 1 << 21
+    for r0 in range(0, n, step):
+        r1 = min(n, r0 + step)
+        blk = torch.randint(0, n_bins, (r1 - r0, f), generator=g, device=device, dtype=torch.int32)
+        codes[r0:r1, :f] = blk.to(torch.uint8)
+        x0 = blk[:, 0].float() / n_bins
+        x1 = blk[:, 1].float() / n_bins
+        y[r0:r1] = ((x0 + 0.5 * x1 + 0.1 * torch.rand(r1 - r0, generator=g, device=device)) > 0.8).float()
+    nb = np.full(f, n_bins, np.int32)
+    return BinnedData(codes, y, None, nb, np.zeros(f, np.uint8), f)
+
+
+def smoke_gbdt(dev):
+    data = synthetic_binned(5000, 40, dev, seed=3, n_bins=64)
+    tr = TreeTrainer(TreeConfig("GBT", tree_num=3, max_depth=4, learning_rate=0.1,
+                                feature_subset_strategy="ALL"), data)
+    tr.train()
+    assert tr.train_errors[-1] <= tr.train_errors[0] + 1e-6, tr.train_errors
+    return tr.train_errors
+
+
+def bench_rounds(a, dev, info):
+    """GBDT config: 500 trees depth 7, 256-bin histograms, 100M rows x 1000 cols per GPU.
+    One step = one boosting round (one tree)."""
+    rows = a.rows
+    data = synthetic_binned(rows, a.cols, dev, seed=11 + info.rank)
+    cfg = TreeConfig("GBT", tree_num=500, max_depth=7, learning_rate=0.05,
+                     feature_subset_strategy="ALL", min_instances_per_node=5)
+    tr = TreeTrainer(cfg, data)
+    for _ in range(a.warmup):
+        tr.train(1)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    tr.train(a.steps)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce_(t, "max")
+    dt = float(t.item())
+    return {
+        "metric": "GBDT rounds/sec (boosting rounds, depth 7, 256 bins)",
+        "value": a.steps / dt, "unit": "rounds/s", "n_gpus": info.world_size, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32-hist/uint8-bins",
+        "data": "synthetic uint8 bin codes, labels from a hidden rule",
+        "config": {"model": "GBT 500 trees depth=7 256 bins", "global_batch": rows * info.world_size,
+                   "seq_len": None, "n_cols": a.cols, "parallelism": f"dp{info.world_size}"},
+        "timings_s": tr.timings, "train_error": tr.train_errors[-1],
+    }

@@ -37,6 +37,13 @@ HIP_SIGNATURES = {
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
     "shifu_cast_bf16": "plpliis",
     "shifu_transpose_cast": "plpiiis",
+    # gbdt_kernels.hip
+    "shifu_gbdt_hist": "plpppp" "ipi" "s",
+    "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "s",
+    "shifu_gbdt_partition_flag": "plppppppp" "l" "s",
+    "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "l" "s",
+    "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
+    "shifu_gbdt_residual": "pppp" "p" "li" "s",
 }
 
 RT_SIGNATURES = {}

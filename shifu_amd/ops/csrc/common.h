@@ -58,7 +58,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 }
 
 // true when derivative can be computed from the activation output alone
-__host__ __device__ __forceinline__ bool act_deriv_from_output(int act) {
+__host__ __device__ constexpr inline bool act_deriv_from_output(int act) {
   return act == ACT_SIGMOID || act == ACT_TANH || act == ACT_LINEAR || act == ACT_RELU ||
          act == ACT_LEAKYRELU || act == ACT_LOG || act == ACT_PTANH;
 }

@@ -1,0 +1,471 @@
+// Tree-ensemble (GBT / RF) kernels for MI355X (gfx950).
+//
+// Replaces the reference's DTWorker/DTMaster hot loops:
+//   histogram   DTWorker.doCompute stats loop          J/core/dtrain/dt/DTWorker.java:789-863
+//               Impurity.featureUpdate                 J/core/dtrain/dt/Impurity.java:238-242, 537-540
+//   split find  Impurity.computeImpurity (Variance / FriedmanMSE / Entropy / Gini)
+//                                                      J/core/dtrain/dt/Impurity.java:120-211, 269, 378, 563
+//   routing     DTWorker.predictNodeIndex              J/core/dtrain/dt/DTWorker.java:1036-1096
+//   GBT update  DTWorker.doCompute predict/output      J/core/dtrain/dt/DTWorker.java:620-670, Loss.java
+//
+// MI355X design:
+//   * bins are uint8 row-major [N][Fp] (Fp multiple of 32), rows grouped per node through a
+//     position->row permutation that is stably re-partitioned every level (rows of one node are
+//     a contiguous position range, so every histogram pass reads only that node's rows).
+//   * histograms keep only (sum w, sum w*g) per bin: for variance / friedman-mse / binary
+//     entropy / binary gini the best split depends on count and sum only (the sum-of-squares
+//     terms cancel in the variance gain), halving LDS atomic traffic.
+//   * a work item = (node, row range, 32-feature group); a block builds its item's histogram
+//     in LDS (32 x 256 x 2 fp32 = 64 KiB, feature-major planes with a 257-word stride) with
+//     ds_add_f32 and writes it to a per-item slab with plain coalesced stores (no global
+//     atomics); the split kernel sums the slabs in fp64, derives the larger sibling by
+//     parent - smaller (histogram subtraction) and scans the bins.
+//   * deterministic: slab order is fixed and ties break to the lowest feature, then bin, so
+//     every rank computes the identical split from the all-reduced histograms.
+#include "common.h"
+
+namespace {
+
+constexpr int NB = 256;        // max bins per feature (uint8 codes)
+constexpr int FG = 32;         // features per work-item group
+constexpr int HSTRIDE = 257;   // padded per-feature plane stride (words)
+
+struct HistArgs {
+  const uint8_t* bins; long ldb;     // [N][ldb]
+  const int* pos2row;                // [N] position -> row id
+  const float* w;                    // [N] per-row weight (significance x subsample)
+  const float* g;                    // [N] per-row target (label / pseudo residual)
+  const int* items;                  // [n_items][4] = {node, pos_lo, pos_hi, group}
+  float* slab;                       // [n_items][FG][NB][2]
+  int n_items, n_feat;
+};
+
+__global__ __launch_bounds__(256) void gbdt_hist_kernel(HistArgs a) {
+  __shared__ float hw[FG * HSTRIDE];
+  __shared__ float hg[FG * HSTRIDE];
+  const int item = blockIdx.x;
+  const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
+  for (int i = threadIdx.x; i < FG * HSTRIDE; i += 256) { hw[i] = 0.f; hg[i] = 0.f; }
+  __syncthreads();
+  const int half = threadIdx.x & 1;                 // which 16-feature half of the 32-B slice
+  const int f0 = grp * FG + half * 16;
+  const int nvalid = min(16, a.n_feat - f0);
+  // 128 rows in flight per block pass, 2 lanes per row, 16 B (16 features) per lane
+  for (int p = lo + (threadIdx.x >> 1); p < hi; p += 128) {
+    const int row = a.pos2row[p];
+    const float wv = a.w[row];
+    if (wv == 0.f) continue;
+    const float gv = wv * a.g[row];
+    const uint4 v = *(const uint4*)(a.bins + (size_t)row * a.ldb + f0);
+    const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      // stagger the feature order by lane so a wave's lanes spread over planes
+      const int jj = (j + (threadIdx.x >> 1)) & 15;
+      if (jj < nvalid) {
+        const uint32_t b = (words[jj >> 2] >> ((jj & 3) * 8)) & 0xff;
+        const int off = (half * 16 + jj) * HSTRIDE + b;
+        atomicAdd(&hw[off], wv);
+        atomicAdd(&hg[off], gv);
+      }
+    }
+  }
+  __syncthreads();
+  float* out = a.slab + (size_t)item * FG * NB * 2;
+  for (int i = threadIdx.x; i < FG * NB; i += 256) {
+    const int f = i / NB, b = i % NB;
+    float2 v;
+    v.x = hw[f * HSTRIDE + b];
+    v.y = hg[f * HSTRIDE + b];
+    *(float2*)(out + (size_t)i * 2) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Node histograms + split search.  One wave per (node, feature); 64 lanes x 4 bins.
+// mode 0: built node  -> hist = sum of its items' slabs
+// mode 1: derived node -> hist = parent_hist - sibling_hist (sibling built this level)
+// Writes hist (fp32, for the next level's subtraction) and the best split candidate.
+// ---------------------------------------------------------------------------------------
+enum Imp : int { IMP_VARIANCE = 0, IMP_FRIEDMAN = 1, IMP_ENTROPY = 2, IMP_GINI = 3 };
+
+struct SplitArgs {
+  const float* slab;            // [n_items][FG][NB][2]
+  const int* node_items;        // [n_nodes][n_groups][max_items] item ids (-1 padded) (mode 0)
+  int max_items;
+  const float* parent_hist;     // [n_parent][F][NB][2]                        (mode 1)
+  const int* node_parent;       // [n_nodes] parent slot in parent_hist        (mode 1)
+  const int* node_sibling;      // [n_nodes] sibling slot in hist              (mode 1)
+  float* hist;                  // [n_nodes][F][NB][2] out
+  const int* node_list;         // nodes processed by this launch
+  int n_list;
+  const int* feat_list;         // candidate features (subset)
+  int n_fsub;
+  const int* nbins;             // [F]
+  const uint8_t* is_cat;        // [F]
+  const uint8_t* feat_mask;     // [n_nodes][F] optional per-node feature subset (nullable)
+  float* cand;                  // [n_nodes][n_fsub][8]: gain, bin/k, lw, ls, rw, rs, valid, order_ref
+  uint8_t* cat_order;           // [n_nodes][n_fsub][NB] sorted bin order for categorical (nullable)
+  int F, mode, impurity, do_scan;
+  float min_inst, min_gain;
+};
+
+__device__ __forceinline__ double imp_gain(int imp, double lw, double ls, double rw, double rs) {
+  const double c = lw + rw, s = ls + rs;
+  switch (imp) {
+    case IMP_FRIEDMAN: { const double d = rw * ls - lw * rs; return d * d / (lw * rw * c); }
+    case IMP_ENTROPY: {
+      auto ent = [](double n, double p1) {   // binary classes: p1 = weight of class 1
+        if (n <= 0.0) return 0.0;
+        double r1 = p1 / n, r0 = 1.0 - r1, e = 0.0;
+        if (r1 > 0.0) e -= r1 * log2(r1);
+        if (r0 > 0.0) e -= r0 * log2(r0);
+        return e;
+      };
+      return ent(c, s) - (lw / c) * ent(lw, ls) - (rw / c) * ent(rw, rs);
+    }
+    case IMP_GINI: {
+      auto gin = [](double n, double p1) {
+        if (n <= 0.0) return 0.0;
+        double r1 = p1 / n, r0 = 1.0 - r1;
+        return -(r1 * r1 + r0 * r0);
+      };
+      return gin(c, s) - (lw / c) * gin(lw, ls) - (rw / c) * gin(rw, rs);
+    }
+    default:   // variance: (sL^2/cL + sR^2/cR - s^2/c) / c  (sum-of-squares terms cancel)
+      return (ls * ls / lw + rs * rs / rw - s * s / c) / c;
+  }
+}
+
+__global__ __launch_bounds__(256) void gbdt_split_kernel(SplitArgs a) {
+  __shared__ double skey[4][NB];
+  __shared__ int sidx[4][NB];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long gw = (long)blockIdx.x * 4 + wv;
+  if (gw >= (long)a.n_list * a.n_fsub) return;
+  const int node = a.node_list[gw / a.n_fsub];
+  const int fi = gw % a.n_fsub;
+  const int f = a.feat_list[fi];
+  float* cand = a.cand + ((size_t)node * a.n_fsub + fi) * 8;
+  float* h = a.hist + ((size_t)node * a.F + f) * NB * 2;
+  // ---- gather this (node, feature) histogram: 4 bins per lane --------------------------
+  double cw[4], cs[4];
+  const int b0 = lane * 4;
+  if (a.mode == 0) {
+    for (int k = 0; k < 4; ++k) { cw[k] = 0.0; cs[k] = 0.0; }
+    // node_items is laid out [node][group][max_items]: the items of this node's feature group
+    const int fg = f / FG, fl = f % FG;
+    const int n_groups = (a.F + FG - 1) / FG;
+    const int* its = a.node_items + ((size_t)node * n_groups + fg) * a.max_items;
+    for (int t = 0; t < a.max_items; ++t) {
+      const int it = its[t];
+      if (it < 0) break;
+      const float* sp = a.slab + (((size_t)it * FG + fl) * NB + b0) * 2;
+      const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
+      cw[0] += v0.x; cs[0] += v0.y; cw[1] += v0.z; cs[1] += v0.w;
+      cw[2] += v1.x; cs[2] += v1.y; cw[3] += v1.z; cs[3] += v1.w;
+    }
+  } else if (a.mode == 2) {        // already-reduced histogram (after the cross-rank all-reduce)
+    const float4 v0 = *(const float4*)(h + b0 * 2), v1 = *(const float4*)(h + b0 * 2 + 4);
+    cw[0] = v0.x; cs[0] = v0.y; cw[1] = v0.z; cs[1] = v0.w;
+    cw[2] = v1.x; cs[2] = v1.y; cw[3] = v1.z; cs[3] = v1.w;
+  } else {
+    const int par = a.node_parent[node], sib = a.node_sibling[node];
+    const float* ph = a.parent_hist + ((size_t)par * a.F + f) * NB * 2 + b0 * 2;
+    const float* sh = a.hist + ((size_t)sib * a.F + f) * NB * 2 + b0 * 2;
+    for (int k = 0; k < 4; ++k) {
+      cw[k] = (double)ph[2 * k] - (double)sh[2 * k];
+      cs[k] = (double)ph[2 * k + 1] - (double)sh[2 * k + 1];
+      if (cw[k] < 0.0) cw[k] = 0.0;    // fp32 subtraction noise on empty bins
+    }
+  }
+  if (a.mode != 2) {
+    float4 o0 = make_float4((float)cw[0], (float)cs[0], (float)cw[1], (float)cs[1]);
+    float4 o1 = make_float4((float)cw[2], (float)cs[2], (float)cw[3], (float)cs[3]);
+    *(float4*)(h + b0 * 2) = o0;
+    *(float4*)(h + b0 * 2 + 4) = o1;
+  }
+  if (!a.do_scan) return;
+  if (a.feat_mask && !a.feat_mask[(size_t)node * a.F + f]) {
+    if (lane == 0) { cand[0] = -1.f; cand[6] = 0.f; }
+    return;
+  }
+  const int nb = a.nbins[f];
+  const bool cat = a.is_cat[f] != 0;
+  // ---- categorical: order bins by mean target (ascending, stable by index) ----------------
+  int order[4] = {b0, b0 + 1, b0 + 2, b0 + 3};
+  if (cat) {
+    for (int k = 0; k < 4; ++k) {
+      const int b = b0 + k;
+      // Impurity.getCategoricalOrderList: empty bin -> Double.MIN_VALUE; bins >= nb sort last
+      double key = (b >= nb) ? 1e300 : (cw[k] != 0.0 ? cs[k] / cw[k] : 4.9e-324);
+      skey[wv][b] = key;
+      sidx[wv][b] = b;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // bitonic sort of 256 (key, idx) pairs, 4 per lane, lexicographic -> stable
+    for (int size = 2; size <= NB; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int k = 0; k < 2; ++k) {
+          const int t = lane + k * 64;          // 128 compare-exchange pairs
+          const int i = 2 * stride * (t / stride) + (t % stride);
+          const int j = i + stride;
+          const bool up = ((i & size) == 0);
+          const double ki = skey[wv][i], kj = skey[wv][j];
+          const int ii = sidx[wv][i], ij = sidx[wv][j];
+          const bool gt = (ki > kj) || (ki == kj && ii > ij);
+          if (gt == up) { skey[wv][i] = kj; skey[wv][j] = ki; sidx[wv][i] = ij; sidx[wv][j] = ii; }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    // gather stats in sorted order: need stats by bin -> stash in LDS keyed by bin
+    double tw[4], ts[4];
+    for (int k = 0; k < 4; ++k) { tw[k] = cw[k]; ts[k] = cs[k]; }
+    // write stats by bin into skey (reuse) after reading the order
+    for (int k = 0; k < 4; ++k) order[k] = sidx[wv][b0 + k];
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < 4; ++k) skey[wv][b0 + k] = tw[k];
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < 4; ++k) cw[k] = skey[wv][order[k]];
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < 4; ++k) skey[wv][b0 + k] = ts[k];
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < 4; ++k) cs[k] = skey[wv][order[k]];
+    if (a.cat_order) {
+      uint8_t* co = a.cat_order + ((size_t)node * a.n_fsub + fi) * NB;
+      for (int k = 0; k < 4; ++k) co[b0 + k] = (uint8_t)order[k];
+    }
+  }
+  // ---- inclusive prefix over the 256 (ordered) bins ---------------------------------------
+  double pw[4], ps[4];
+  pw[0] = cw[0]; ps[0] = cs[0];
+  for (int k = 1; k < 4; ++k) { pw[k] = pw[k - 1] + cw[k]; ps[k] = ps[k - 1] + cs[k]; }
+  double xw = pw[3], xs = ps[3];
+  for (int off = 1; off < 64; off <<= 1) {
+    const double uw = __shfl_up(xw, off, 64), us = __shfl_up(xs, off, 64);
+    if (lane >= off) { xw += uw; xs += us; }
+  }
+  const double ew = xw - pw[3], es = xs - ps[3];     // exclusive lane offset
+  const double tw = __shfl(xw, 63, 64), ts = __shfl(xs, 63, 64);
+  // candidates: left = ordered bins [0..b], b < nb - 1
+  double best = -1.0;
+  int bbin = -1;
+  double blw = 0, bls = 0;
+  for (int k = 0; k < 4; ++k) {
+    const int b = b0 + k;
+    if (b >= nb - 1) break;
+    const double lw = ew + pw[k], ls = es + ps[k];
+    const double rw = tw - lw, rs = ts - ls;
+    if (lw <= a.min_inst || rw <= a.min_inst) continue;
+    const double gain = imp_gain(a.impurity, lw, ls, rw, rs);
+    if (!(gain > a.min_gain)) continue;
+    if (gain > best) { best = gain; bbin = b; blw = lw; bls = ls; }
+  }
+  // wave argmax: max gain, ties -> lowest bin
+  for (int off = 32; off > 0; off >>= 1) {
+    const double og = __shfl_xor(best, off, 64);
+    const int ob = __shfl_xor(bbin, off, 64);
+    const double olw = __shfl_xor(blw, off, 64), ols = __shfl_xor(bls, off, 64);
+    const bool take = (og > best) || (og == best && ob >= 0 && (bbin < 0 || ob < bbin));
+    if (take) { best = og; bbin = ob; blw = olw; bls = ols; }
+  }
+  if (lane == 0) {
+    cand[0] = (float)best;
+    cand[1] = (float)bbin;
+    cand[2] = (float)blw;
+    cand[3] = (float)bls;
+    cand[4] = (float)(tw - blw);
+    cand[5] = (float)(ts - bls);
+    cand[6] = bbin >= 0 ? 1.f : 0.f;
+    cand[7] = (float)tw;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Partition: go-left flag per position for split nodes.  node_of_pos is computed by the
+// caller as a per-position node slot array (int16) maintained alongside pos2row.
+// split_feat < 0 -> node not split this level (rows stay, flag = 2 "keep").
+// ---------------------------------------------------------------------------------------
+struct PartArgs {
+  const uint8_t* bins; long ldb;
+  const int* pos2row;
+  const int* pos_node;          // [N] node slot of each position (current level)
+  const int* split_feat;        // [n_nodes]
+  const int* split_bin;         // [n_nodes] numeric: left iff bin <= split_bin
+  const uint32_t* cat_left;     // [n_nodes][8] categorical left bitset (bin b left iff bit set)
+  const uint8_t* is_cat;        // [F]
+  int* flag;                    // [N] out: 1 left, 0 right, for split nodes; 0 otherwise
+  long n;
+};
+
+__global__ void gbdt_partition_flag_kernel(PartArgs a) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.n) return;
+  const int node = a.pos_node[p];
+  const int f = node >= 0 ? a.split_feat[node] : -1;
+  int fl = 0;
+  if (f >= 0) {
+    const uint32_t b = a.bins[(size_t)a.pos2row[p] * a.ldb + f];
+    if (a.is_cat[f]) fl = (a.cat_left[node * 8 + (b >> 5)] >> (b & 31)) & 1;
+    else fl = (int)b <= a.split_bin[node] ? 1 : 0;
+  }
+  a.flag[p] = fl;
+}
+
+// scatter: positions of split nodes move to [start + rank_left] or [start + n_left + rank_right]
+struct ScatterArgs {
+  const int* pos2row; const int* pos_node; const int* flag; const int* cum;   // cum = inclusive cumsum(flag)
+  const int* node_start; const int* node_nleft; const int* node_cum0;          // per node: start pos, #left, cum before start
+  const int* split_feat;
+  const int* child_left; const int* child_right;                               // new node slots
+  int* new_pos2row; int* new_pos_node;
+  long n;
+};
+
+__global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.n) return;
+  const int node = a.pos_node[p];
+  if (node < 0 || a.split_feat[node] < 0) {        // unsplit / finished rows keep their place
+    a.new_pos2row[p] = a.pos2row[p];
+    a.new_pos_node[p] = -1;
+    return;
+  }
+  const int s = a.node_start[node];
+  const int before = a.cum[p] - a.node_cum0[node];           // #left in [s, p]
+  long np;
+  int child;
+  if (a.flag[p]) { np = s + before - 1; child = a.child_left[node]; }
+  else { np = s + a.node_nleft[node] + (int)(p - s) - before; child = a.child_right[node]; }
+  a.new_pos2row[np] = a.pos2row[p];
+  a.new_pos_node[np] = child;
+}
+
+// ---------------------------------------------------------------------------------------
+// Tree application: walk a heap-ordered tree (<= 2^depth nodes) per row over its bins.
+//   feat[id] < 0 -> leaf with value[id].  pred[row] += scale * value (or = value when set_mode).
+// Used for validation rows, continuous-training recovery and GBT predict update.
+// ---------------------------------------------------------------------------------------
+struct TreeArgs {
+  const uint8_t* bins; long ldb;
+  const int* rows;               // nullable: row ids (else 0..n-1)
+  const int* feat; const int* thr; const uint32_t* cat_left; const float* value; const uint8_t* is_cat;
+  float* pred; float scale; int set_mode;
+  int* leaf_out;                 // nullable: leaf node id per row
+  long n; int max_nodes;
+};
+
+__global__ void gbdt_apply_tree_kernel(TreeArgs a) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const long row = a.rows ? a.rows[i] : i;
+  int id = 1;
+  while (id < a.max_nodes && a.feat[id] >= 0) {
+    const int f = a.feat[id];
+    const uint32_t b = a.bins[(size_t)row * a.ldb + f];
+    bool left;
+    if (a.is_cat[f]) left = (a.cat_left[id * 8 + (b >> 5)] >> (b & 31)) & 1;
+    else left = (int)b <= a.thr[id];
+    id = left ? 2 * id : 2 * id + 1;
+  }
+  const float v = a.value[id];
+  if (a.set_mode) a.pred[row] = v; else a.pred[row] += a.scale * v;
+  if (a.leaf_out) a.leaf_out[row] = id;
+}
+
+// GBT residual refresh + error: output = -dLoss/dpredict (Loss.java), err += s * loss
+struct ResidArgs {
+  const float* pred; const float* y; const float* sig; float* out; double* err; long n; int loss;
+};
+__global__ void gbdt_residual_kernel(ResidArgs a) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  double e = 0.0, ws = 0.0;
+  if (i < a.n) {
+    const float p = a.pred[i], y = a.y[i], s = a.sig ? a.sig[i] : 1.f;
+    float grad, err;
+    switch (a.loss) {
+      case 1: grad = p - y; err = (p - y) * (p - y); break;                           // halfgradsquared
+      case 2: grad = (y < p) ? 1.f : -1.f; err = fabsf(y - p); break;                   // absolute
+      case 3: grad = (2.f - 4.f * y) / __expf(4.f * y * p - 2.f * p);                   // log
+              err = log1pf(1.f + __expf(2.f * p - 4.f * p * y)); break;
+      default: grad = 2.f * (p - y); err = (p - y) * (p - y); break;                    // squared
+    }
+    a.out[i] = -grad;
+    e = (double)s * err;
+    ws = s;
+  }
+  e = wave_sum_d(e);
+  ws = wave_sum_d(ws);
+  if ((threadIdx.x & 63) == 0) { atomicAdd(a.err, e); atomicAdd(a.err + 1, ws); }
+}
+
+}  // namespace
+
+#define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+SHIFU_API int shifu_gbdt_hist(const void* bins, long ldb, const int* pos2row, const float* w, const float* g,
+                              const int* items, int n_items, float* slab, int n_feat, hipStream_t stream) {
+  if (ldb % 16 || n_items <= 0) return -1;
+  HistArgs a{(const uint8_t*)bins, ldb, pos2row, w, g, items, slab, n_items, n_feat};
+  hipLaunchKernelGGL(gbdt_hist_kernel, dim3(n_items), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_gbdt_split(const float* slab, const int* node_items, int max_items, const float* parent_hist,
+                               const int* node_parent, const int* node_sibling, float* hist, const int* node_list,
+                               int n_list, const int* feat_list, int n_fsub, const int* nbins, const void* is_cat,
+                               const void* feat_mask, float* cand, void* cat_order, int F, int mode, int impurity,
+                               int do_scan, float min_inst, float min_gain, hipStream_t stream) {
+  if (n_list <= 0 || n_fsub <= 0) return 0;
+  SplitArgs a{slab, node_items, max_items, parent_hist, node_parent, node_sibling, hist, node_list, n_list,
+              feat_list, n_fsub, nbins, (const uint8_t*)is_cat, (const uint8_t*)feat_mask, cand,
+              (uint8_t*)cat_order, F, mode, impurity, do_scan, min_inst, min_gain};
+  const long waves = (long)n_list * n_fsub;
+  hipLaunchKernelGGL(gbdt_split_kernel, dim3((waves + 3) / 4), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long ldb, const int* pos2row, const int* pos_node,
+                                        const int* split_feat, const int* split_bin, const void* cat_left,
+                                        const void* is_cat, int* flag, long n, hipStream_t stream) {
+  PartArgs a{(const uint8_t*)bins, ldb, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
+             (const uint8_t*)is_cat, flag, n};
+  hipLaunchKernelGGL(gbdt_partition_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_gbdt_partition_scatter(const int* pos2row, const int* pos_node, const int* flag, const int* cum,
+                                           const int* node_start, const int* node_nleft, const int* node_cum0,
+                                           const int* split_feat, const int* child_left, const int* child_right,
+                                           int* new_pos2row, int* new_pos_node, long n, hipStream_t stream) {
+  ScatterArgs a{pos2row, pos_node, flag, cum, node_start, node_nleft, node_cum0, split_feat, child_left,
+                child_right, new_pos2row, new_pos_node, n};
+  hipLaunchKernelGGL(gbdt_partition_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_gbdt_apply_tree(const void* bins, long ldb, const int* rows, const int* feat, const int* thr,
+                                    const void* cat_left, const float* value, const void* is_cat, float* pred,
+                                    float scale, int set_mode, int* leaf_out, long n, int max_nodes,
+                                    hipStream_t stream) {
+  if (n <= 0) return 0;
+  TreeArgs a{(const uint8_t*)bins, ldb, rows, feat, thr, (const uint32_t*)cat_left, value, (const uint8_t*)is_cat,
+             pred, scale, set_mode, leaf_out, n, max_nodes};
+  hipLaunchKernelGGL(gbdt_apply_tree_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_gbdt_residual(const float* pred, const float* y, const float* sig, float* out, double* err,
+                                  long n, int loss, hipStream_t stream) {
+  if (n <= 0) return 0;
+  ResidArgs a{pred, y, sig, out, err, n, loss};
+  hipLaunchKernelGGL(gbdt_residual_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}

@@ -1,303 +1,9 @@
-// MLP training kernels for MI355X (gfx950 / CDNA4).
-//
-// Replaces the reference's per-row Java scalar loops
-//   forward  FloatFlatNetwork.compute/computeLayer  (J/core/dtrain/dataset/FloatFlatNetwork.java:69-223)
-//   backward SubGradient.process/processLevel         (J/core/dtrain/nn/SubGradient.java:224-311)
-//   update   Weight.calculateWeights + nn/update/*    (J/core/dtrain/Weight.java:194-343)
-// with row-tiled MFMA GEMMs.  Layout decisions (MI355X-first, not a translation):
-//   * Every layer is a pure GEMM: the Encog bias neuron is a real input column (value 1.0)
-//     stored right after the last feature, and K is zero-padded to a multiple of 64.  So
-//     W_l is [out_l, in_pad_l] with column in_l = bias (exactly Encog's flat layout per block).
-//   * Activations are bf16 row-major [rows, in_pad]; the forward epilogue writes act(z),
-//     the bias column (1.0) and zero padding in one pass.
-//   * dgrad is an NT GEMM against a per-step transposed bf16 copy of W, with the
-//     activation derivative (+ Encog flat spot) fused into the epilogue.
-//   * wgrad is a TN GEMM over the row axis (split-K over rows) using the gfx950
-//     ds_read_b64_tr_b16 transposed LDS read for both operands; fp32 atomics into the
-//     flat gradient buffer.
-//   * the output layer (n_out <= 8) + loss + output delta + last-hidden dgrad + output
-//     wgrad are one row kernel (memory-bound, one wave per row strip).
+// MLP row kernels for MI355X (gfx950): fused output layer/loss/delta, optimizer, weight casts.
+// See gemm_kernels.hip for the layer GEMMs.
 #include "common.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
-constexpr int TILE_BYTES = BM * BK * 2;   // 16 KiB per operand tile
-
-// XCD-aware bijective block remap: consecutive logical ids land on the same XCD
-// (blocks b, b+8, ... share an XCD under round-robin dispatch; speed only).
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
-// [128 rows][64 bf16] tile, 128-B rows, 16-B chunk XOR swizzle: rows 0..15 of a fragment
-// read land on 16 distinct 16-B slots of the 256-B bank row (conflict-free ds_read_b128).
-__device__ __forceinline__ int swz_nt(int row, int chunk) {
-  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
-}
-
-enum Epi : int { EPI_ACT = 0, EPI_DACT = 1, EPI_STORE = 2 };
-
-struct GemmArgs {
-  const bf16_t* A; long lda;   // [M, K] row-major
-  const bf16_t* B; long ldb;   // [NB, K] row-major (rows >= NB read as 0)
-  bf16_t* C; long ldc;         // [M, N] output
-  bf16_t* C2; long ldc2;       // EPI_ACT optional: f'(z)+flat (activations not derivable from output)
-  const bf16_t* H; long ldh;   // EPI_DACT: layer input activations (derivative from output)
-  const bf16_t* Hd; long ldhd; // EPI_DACT: stored derivative (when !act_deriv_from_output)
-  int M, N, K, NB, n_valid, act, bias_col;
-  float flat;
-};
-
-template <int EPI>
-__global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntn = (p.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-
-  uint4 ra[4], rb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * NTHR, row = idx >> 3, ch = idx & 7;
-      const int gm = m0 + row, gn = n0 + row;
-      ra[i] = gm < p.M ? *(const uint4*)(p.A + (size_t)gm * p.lda + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
-      rb[i] = gn < p.NB ? *(const uint4*)(p.B + (size_t)gn * p.ldb + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto swrite = [&](int buf) {
-    char* As = smem + buf * 2 * TILE_BYTES;
-    char* Bs = As + TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * NTHR, row = idx >> 3, ch = idx & 7;
-      *(uint4*)(As + swz_nt(row, ch)) = ra[i];
-      *(uint4*)(Bs + swz_nt(row, ch)) = rb[i];
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = p.K / BK;
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);        // issue next tile's HBM loads early
-    const char* As = smem + buf * 2 * TILE_BYTES;
-    const char* Bs = As + TILE_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = s * 4 + (lane >> 4);
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) af[j] = *(const bf16x8*)(As + swz_nt(wr * 64 + j * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) bfr[i] = *(const bf16x8*)(Bs + swz_nt(wc * 64 + i * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) swrite(buf ^ 1);
-    __syncthreads();
-  }
-
-  // Epilogue.  acc[i][j] holds D[n][m]: m = lane&15 (+16j), n = 4*(lane>>4) + r (+16i):
-  // each lane owns 4 consecutive output columns of one row -> one 8-byte store.
-  const bool dfo = act_deriv_from_output(p.act);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int nb = n0 + wc * 64 + i * 16 + (lane >> 4) * 4;
-    if (nb >= p.N) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + wr * 64 + j * 16 + (lane & 15);
-      if (m >= p.M) continue;
-      float o[4];
-      if constexpr (EPI == EPI_ACT) {
-        float d[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = nb + r;
-          const float z = acc[i][j][r];
-          if (n < p.n_valid) { o[r] = act_fwd(p.act, z); d[r] = act_deriv_pre(p.act, z) + p.flat; }
-          else { o[r] = (n == p.n_valid && p.bias_col) ? 1.f : 0.f; d[r] = 0.f; }
-        }
-        if (p.C2) {
-          uint2 w2;
-          w2.x = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
-          w2.y = (uint32_t)f2bf(d[2]) | ((uint32_t)f2bf(d[3]) << 16);
-          *(uint2*)(p.C2 + (size_t)m * p.ldc2 + nb) = w2;
-        }
-      } else if constexpr (EPI == EPI_DACT) {
-        float dv[4];
-        if (dfo) {
-          const uint2 h = *(const uint2*)(p.H + (size_t)m * p.ldh + nb);
-          const float hv[4] = {bf2f(h.x & 0xffff), bf2f(h.x >> 16), bf2f(h.y & 0xffff), bf2f(h.y >> 16)};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dv[r] = act_deriv_out(p.act, hv[r]) + p.flat;
-        } else {
-          const uint2 h = *(const uint2*)(p.Hd + (size_t)m * p.ldhd + nb);
-          dv[0] = bf2f(h.x & 0xffff); dv[1] = bf2f(h.x >> 16); dv[2] = bf2f(h.y & 0xffff); dv[3] = bf2f(h.y >> 16);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (nb + r < p.n_valid) ? acc[i][j][r] * dv[r] : 0.f;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r];
-      }
-      uint2 w;
-      w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-      w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-      *(uint2*)(p.C + (size_t)m * p.ldc + nb) = w;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// wgrad: G[n][k] += sum_m D[m][n] * X[m][k]   (TN GEMM over rows, split over m)
-// LDS images [64 m][128 cols] bf16, 256-B rows, quad XOR swizzle so that the 8 rows read
-// by one 32-lane half of ds_read_b64_tr_b16 hit 8 distinct bank groups.
-// ---------------------------------------------------------------------------------------
-constexpr int WT_BN = 128, WT_BK = 128, WT_BM = 64;   // n-tile, k-tile, rows per step
-constexpr int WT_TILE = WT_BM * 128 * 2;              // 16 KiB
-
-__device__ __forceinline__ int tr_h(int m) { return (m & 3) | (((m >> 3) & 1) << 2); }
-// byte offset of 8-byte quad q (4 bf16: cols 4q..4q+3) of row m
-__device__ __forceinline__ int swz_tn_quad(int m, int q) { return m * 256 + ((q ^ (tr_h(m) << 2)) << 3); }
-
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-// gfx950 ds_read_b64_tr_b16 (compiler builtin: hipcc counts its lgkmcnt itself)
-__device__ __forceinline__ s16x4 ds_read_tr16_b64(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
-}
-
-struct WgradArgs {
-  const bf16_t* D; long ldd;   // [M, Nd] deltas
-  const bf16_t* X; long ldx;   // [M, Kx] layer inputs
-  float* G; long ldg;          // [Nv, Kx] fp32 gradient (accumulated atomically)
-  int M, Nv, Kx, rows_per_split;
-};
-
-__global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tiles_n = (p.Nv + WT_BN - 1) / WT_BN, tiles_k = p.Kx / WT_BK;
-  const int ntiles = tiles_n * tiles_k;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = wg / ntiles, t = wg % ntiles;
-  const int n0 = (t / tiles_k) * WT_BN, k0 = (t % tiles_k) * WT_BK;
-  const int mbeg = split * p.rows_per_split;
-  const int mend = min(p.M, mbeg + p.rows_per_split);
-  if (mbeg >= mend) return;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wn = wid >> 1, wk = wid & 1;
-
-  uint4 rd[4], rx[4];
-  auto gload = [&](int mb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * NTHR, row = idx >> 4, ch = idx & 15;
-      const int gm = mb + row;
-      const bool ok = gm < mend;
-      const int gn = n0 + ch * 8;
-      rd[i] = (ok && gn < p.Nv) ? *(const uint4*)(p.D + (size_t)gm * p.ldd + gn) : make_uint4(0, 0, 0, 0);
-      rx[i] = ok ? *(const uint4*)(p.X + (size_t)gm * p.ldx + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto swrite = [&](int buf) {
-    char* Ds = smem + buf * 2 * WT_TILE;
-    char* Xs = Ds + WT_TILE;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * NTHR, row = idx >> 4, ch = idx & 15;
-      *(uint4*)(Ds + swz_tn_quad(row, ch * 2)) = rd[i];
-      *(uint4*)(Xs + swz_tn_quad(row, ch * 2)) = rx[i];
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // tr read addressing: group g = lane>>4; lane-in-group t = 4q+p supplies row (8g+q [+4]),
-  // quad (col_base/4 + p); lane receives column (col_base + t) of the 4 rows.
-  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-  const int nsteps = (mend - mbeg + WT_BM - 1) / WT_BM;
-  gload(mbeg);
-  swrite(0);
-  __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nsteps) gload(mbeg + (st + 1) * WT_BM);
-    const char* Ds = smem + buf * 2 * WT_TILE;
-    const char* Xs = Ds + WT_TILE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {          // two 32-row k-substeps
-      bf16x8 af[4], bfr[4];
-      const int mr = s * 32 + 8 * g + tq;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = (wn * 64 + i * 16) / 4 + tp;
-        const s16x4 lo = ds_read_tr16_b64(Ds + swz_tn_quad(mr, q));
-        const s16x4 hi = ds_read_tr16_b64(Ds + swz_tn_quad(mr + 4, q));
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = (wk * 64 + j * 16) / 4 + tp;
-        const s16x4 lo = ds_read_tr16_b64(Xs + swz_tn_quad(mr, q));
-        const s16x4 hi = ds_read_tr16_b64(Xs + swz_tn_quad(mr + 4, q));
-        bfr[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (st + 1 < nsteps) swrite(buf ^ 1);
-    __syncthreads();
-  }
-  // acc[i][j]: D_out[n][k]: k = lane&15 (+16j), n = 4*(lane>>4) + r (+16i)
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4 + r;
-      if (n >= p.Nv) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
-        atomicAdd(p.G + (size_t)n * p.ldg + k, acc[i][j][r]);
-      }
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// Output layer row kernel (n_out <= 8):
-//   z_o = sum_j H[m][j] W[o][j]   (bias = column kh_valid of H, value 1)
-//   p_o = act_out(z_o);  err += ((y-p)s)^2 (squared) | -(y ln p + (1-y) ln(1-p)) (log) | |y-p|s
-//   delta_o = (y-p)(f'(p)+flat_out)s  (squared, J/core/dtrain/nn/SubGradient.java:241-248)
-//           = (y-p)s                  (log)
-//           = sign-loss (absolute, AbsoluteErrorFunction)
-//   D[m][j] = (sum_o W[o][j] delta_o)(f'_hid(H[m][j]) + flat_hid)   j < kh_valid, else 0
-//   GW[o][j] += delta_o H[m][j]
-// One wave per row strip; each lane owns 8 columns (KH <= 512) - row read = 1 KiB per wave.
-// ---------------------------------------------------------------------------------------
 constexpr int OUT_MAX = 8;
 struct OutArgs {
   const bf16_t* H; long ldh;       // [M, KH]
@@ -313,80 +19,117 @@ struct OutArgs {
   float flat_out, flat_hid;
 };
 
-template <int NOUT>
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  f[0] = bf2f(v.x & 0xffff); f[1] = bf2f(v.x >> 16); f[2] = bf2f(v.y & 0xffff); f[3] = bf2f(v.y >> 16);
+  f[4] = bf2f(v.z & 0xffff); f[5] = bf2f(v.z >> 16); f[6] = bf2f(v.w & 0xffff); f[7] = bf2f(v.w >> 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
+  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  return v;
+}
+
+// LPR lanes per row (KH = 8*LPR), RPS = 64/LPR rows per wave step, U steps in flight.
+template <int NOUT, int LPR>
 __global__ __launch_bounds__(256) void mlp_output_kernel(OutArgs p) {
+  constexpr int RPS = 64 / LPR, U = 4;
+  const bool dfo = act_deriv_from_output(p.hid_act);   // wave-uniform
   const int lane = threadIdx.x & 63;
-  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int r0 = gw * p.rows_per_wave;
-  if (r0 >= p.M) return;
-  const int r1 = min(p.M, r0 + p.rows_per_wave);
-  const int cpl = p.KH / 64;                  // columns per lane: 1..8 (KH multiple of 64, <= 512)
-  const int c0 = lane * cpl;
-  float w[NOUT][8];
-  float gacc[NOUT][8];
-  _Pragma("unroll") for (int o = 0; o < NOUT; ++o)
+  const int sub = lane / LPR, li = lane % LPR;
+  const int c0 = li * 8;
+  const long gw = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+  float w[NOUT][8], gacc[NOUT][8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) { w[o][c] = c < cpl ? p.W[(size_t)o * p.KH + c0 + c] : 0.f; gacc[o][c] = 0.f; }
-  const bool dfo = act_deriv_from_output(p.hid_act);
+  for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { w[o][c] = p.W[(size_t)o * p.KH + c0 + c]; gacc[o][c] = 0.f; }
   double esum = 0.0, wsum = 0.0;
-  for (int m = r0; m < r1; ++m) {
-    float h[8];
-    const bf16_t* hp = p.H + (size_t)m * p.ldh + c0;
+  const long rows_per_iter = (long)RPS * U;
+  for (long base = gw * rows_per_iter; base < p.M; base += nw * rows_per_iter) {
+    uint4 hv[U], dv4[U];
+    float yv[U][NOUT], sv[U];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) h[c] = c < cpl ? bf2f(hp[c]) : 0.f;
-    const float s = p.S ? p.S[m] : 1.f;
-    float dlt[NOUT];
-    _Pragma("unroll") for (int o = 0; o < NOUT; ++o) {
-      float z = 0.f;
+    for (int u = 0; u < U; ++u) {          // issue every load of the U row-steps up front
+      const long m = base + u * RPS + sub;
+      const bool ok = m < p.M;
+      hv[u] = ok ? *(const uint4*)(p.H + (size_t)m * p.ldh + c0) : make_uint4(0, 0, 0, 0);
+      dv4[u] = (!dfo && ok && p.D) ? *(const uint4*)(p.Hd + (size_t)m * p.ldhd + c0) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) z += h[c] * w[o][c];
-      z = wave_sum(z);
-      const float a = act_fwd(p.out_act, z);
-      const float y = p.Y[(size_t)m * p.ldy + o];
-      const float e = y - a;
-      if (p.P && lane == 0) p.P[(size_t)m * p.ldp + o] = a;
-      if (p.loss == 1) {          // log
-        dlt[o] = e * s;
-        if (lane == 0) {
-          const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
-          esum += NOUT == 1 ? -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y)) : -(__logf(ac) * y * s);
-        }
-      } else if (p.loss == 2) {   // absolute
-        dlt[o] = (y < a ? 1.f : -1.f) * (act_deriv_out(p.out_act, a) + p.flat_out) * s;
-        if (lane == 0) esum += fabsf(e) * s;
-      } else {                    // squared (default)
-        dlt[o] = (act_deriv_pre(p.out_act, z) + p.flat_out) * e * s;
-        if (lane == 0) esum += (double)(e * s) * (e * s);
-      }
+      for (int o = 0; o < NOUT; ++o) yv[u][o] = ok ? p.Y[(size_t)m * p.ldy + o] : 0.f;
+      sv[u] = (ok && p.S) ? p.S[m] : 1.f;
     }
-    if (lane == 0) wsum += s;
-    // hidden deltas + output wgrad
-    float dsum[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) dsum[c] = 0.f;
-    _Pragma("unroll") for (int o = 0; o < NOUT; ++o)
+    for (int u = 0; u < U; ++u) {
+      const long m = base + u * RPS + sub;
+      const bool valid = m < p.M;
+      float h[8];
+      unpack8(hv[u], h);
+      const float s = sv[u];
+      float dlt[NOUT];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) { dsum[c] += w[o][c] * dlt[o]; gacc[o][c] += dlt[o] * h[c]; }
-    if (p.D) {
-      float dv[8];
-      if (dfo) {
+      for (int o = 0; o < NOUT; ++o) {
+        float z = 0.f;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) dv[c] = act_deriv_out(p.hid_act, h[c]) + p.flat_hid;
-      } else {
-        const bf16_t* dp = p.Hd + (size_t)m * p.ldhd + c0;
+        for (int c = 0; c < 8; ++c) z += h[c] * w[o][c];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) dv[c] = c < cpl ? bf2f(dp[c]) : 0.f;
+        for (int off = LPR / 2; off > 0; off >>= 1) z += __shfl_xor(z, off, 64);
+        const float a = act_fwd(p.out_act, z);
+        const float y = yv[u][o];
+        const float e = y - a;
+        if (p.P && valid && li == 0) p.P[(size_t)m * p.ldp + o] = a;
+        float contrib;
+        if (p.loss == 1) {          // log
+          dlt[o] = e * s;
+          const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
+          contrib = NOUT == 1 ? -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y)) : -(__logf(ac) * y * s);
+        } else if (p.loss == 2) {   // absolute
+          dlt[o] = (y < a ? 1.f : -1.f) * (act_deriv_out(p.out_act, a) + p.flat_out) * s;
+          contrib = fabsf(e) * s;
+        } else {                    // squared (default)
+          dlt[o] = (act_deriv_pre(p.out_act, z) + p.flat_out) * e * s;
+          contrib = (e * s) * (e * s);
+        }
+        if (!valid) dlt[o] = 0.f;
+        if (valid && li == 0) esum += contrib;
       }
-      bf16_t* outp = p.D + (size_t)m * p.ldd + c0;
+      if (valid && li == 0) wsum += s;
+      float dsum[8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (c < cpl) outp[c] = f2bf((c0 + c) < p.kh_valid ? dsum[c] * dv[c] : 0.f);
+      for (int c = 0; c < 8; ++c) dsum[c] = 0.f;
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { dsum[c] += w[o][c] * dlt[o]; gacc[o][c] += dlt[o] * h[c]; }
+      if (p.D && valid) {
+        float dv[8], outv[8];
+        if (dfo) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) dv[c] = act_deriv_out(p.hid_act, h[c]) + p.flat_hid;
+        } else {
+          unpack8(dv4[u], dv);
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) outv[c] = (c0 + c) < p.kh_valid ? dsum[c] * dv[c] : 0.f;
+        *(uint4*)(p.D + (size_t)m * p.ldd + c0) = pack8(outv);
+      }
     }
   }
-  _Pragma("unroll") for (int o = 0; o < NOUT; ++o)
+  // reduce gacc over the RPS row-groups of the wave (lanes with equal li), then one atomic per column
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (c < cpl) atomicAdd(p.GW + (size_t)o * p.KH + c0 + c, gacc[o][c]);
+  for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float v = gacc[o][c];
+#pragma unroll
+      for (int off = LPR; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+      if (sub == 0) atomicAdd(p.GW + (size_t)o * p.KH + c0 + c, v);
+    }
+  esum = wave_sum_d(esum);
+  wsum = wave_sum_d(wsum);
   if (lane == 0) {
     atomicAdd(p.err, esum);
     atomicAdd(p.err + 1, wsum);
@@ -486,51 +229,29 @@ __global__ void transpose_cast_kernel(const float* W, long ldw, bf16_t* O, int R
 // =======================================================================================
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
 
-SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc,
-                            void* C2, long ldc2, const void* H, long ldh, const void* Hd, long ldhd,
-                            int M, int N, int K, int epi, int act, int n_valid, int bias_col, float flat,
-                            hipStream_t stream) {
-  if (K % BK || N % 4 || ldc % 4 || lda % 8 || ldb % 8 || M <= 0 || N <= 0) return -1;
-  GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, (bf16_t*)C2, ldc2,
-             (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat};
-  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const size_t lds = 4 * TILE_BYTES;
-  if (epi == EPI_ACT) hipLaunchKernelGGL(gemm_nt_kernel<EPI_ACT>, dim3(grid), dim3(NTHR), lds, stream, p);
-  else if (epi == EPI_DACT) hipLaunchKernelGGL(gemm_nt_kernel<EPI_DACT>, dim3(grid), dim3(NTHR), lds, stream, p);
-  else hipLaunchKernelGGL(gemm_nt_kernel<EPI_STORE>, dim3(grid), dim3(NTHR), lds, stream, p);
-  CHECK_HIP(hipGetLastError());
-  return 0;
-}
-
-SHIFU_API int shifu_wgrad_tn(const void* D, long ldd, const void* X, long ldx, float* G, long ldg,
-                             int M, int Nv, int Kx, int splits, hipStream_t stream) {
-  if (Kx % WT_BK || ldd % 8 || ldx % 8 || M <= 0 || Nv <= 0) return -1;
-  if (splits < 1) splits = 1;
-  int rps = (M + splits - 1) / splits;
-  rps = ((rps + WT_BM - 1) / WT_BM) * WT_BM;
-  splits = (M + rps - 1) / rps;
-  WgradArgs p{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, G, ldg, M, Nv, Kx, rps};
-  const int ntiles = ((Nv + WT_BN - 1) / WT_BN) * (Kx / WT_BK);
-  hipLaunchKernelGGL(wgrad_tn_kernel, dim3(ntiles * splits), dim3(NTHR), 4 * WT_TILE, stream, p);
-  CHECK_HIP(hipGetLastError());
-  return 0;
-}
-
 SHIFU_API int shifu_mlp_output(const void* H, long ldh, const void* Hd, long ldhd, const float* W, const float* Y,
                                long ldy, const float* S, void* D, long ldd, float* GW, double* err, float* P,
                                long ldp, int M, int KH, int kh_valid, int n_out, int out_act, int hid_act, int loss,
                                float flat_out, float flat_hid, hipStream_t stream) {
   if (KH % 64 || KH > 512 || n_out < 1 || n_out > OUT_MAX || M <= 0) return -1;
-  const int rows_per_wave = 16;
+  if (D && !act_deriv_from_output(hid_act) && Hd == nullptr) return -3;
   OutArgs p{(const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, W, Y, ldy, S, (bf16_t*)D, ldd, GW, err, P, ldp,
-            M, KH, kh_valid, n_out, out_act, hid_act, loss, rows_per_wave, flat_out, flat_hid};
-  const long waves = (M + rows_per_wave - 1) / rows_per_wave;
+            M, KH, kh_valid, n_out, out_act, hid_act, loss, 0, flat_out, flat_hid};
+  const int lpr = KH / 8;
+  const long rows_per_wave_iter = (64 / lpr) * 4;
+  long waves = (M + rows_per_wave_iter - 1) / rows_per_wave_iter;
+  if (waves > 8192) waves = 8192;          // grid-stride: 2048 blocks x 4 waves
   const long blocks = (waves + 3) / 4;
+  // dispatch on (n_out, lanes-per-row)
+#define OUT_L(NO, L) hipLaunchKernelGGL((mlp_output_kernel<NO, L>), dim3(blocks), dim3(256), 0, stream, p)
+#define OUT_LPR(NO) switch (lpr) { case 8: OUT_L(NO, 8); break; case 16: OUT_L(NO, 16); break; \
+    case 32: OUT_L(NO, 32); break; case 64: OUT_L(NO, 64); break; default: return -1; }
   switch (n_out) {
-#define OUT_CASE(n) case n: hipLaunchKernelGGL(mlp_output_kernel<n>, dim3(blocks), dim3(256), 0, stream, p); break;
-    OUT_CASE(1) OUT_CASE(2) OUT_CASE(3) OUT_CASE(4) OUT_CASE(5) OUT_CASE(6) OUT_CASE(7) OUT_CASE(8)
-#undef OUT_CASE
+    case 1: OUT_LPR(1) break; case 2: OUT_LPR(2) break; case 3: OUT_LPR(3) break; case 4: OUT_LPR(4) break;
+    case 5: OUT_LPR(5) break; case 6: OUT_LPR(6) break; case 7: OUT_LPR(7) break; default: OUT_LPR(8) break;
   }
+#undef OUT_LPR
+#undef OUT_L
   CHECK_HIP(hipGetLastError());
   return 0;
 }
