@@ -244,6 +244,13 @@ class TreeTrainer:
         # root stats for the root's own value
         tot = dist.all_reduce_(torch.stack([w.double().sum(), (w.double() * g.double()).sum()]))
         tw, ts = float(tot[0]), float(tot[1])
+        # int64 fixed-point scales: every bin sum over all ranks stays below 2^62
+        mx = torch.stack([w.abs().max().double(), (w * g).abs().max().double(),
+                          torch.tensor(float(n), dtype=torch.float64, device=self.dev)])
+        dist.all_reduce_(mx, "max")
+        n_glob = float(mx[2]) * dist.info().world_size
+        self.scale_w = _fixed_scale(float(mx[0]), n_glob)
+        self.scale_g = _fixed_scale(float(mx[1]), n_glob)
         tree.exists[1] = True
         tree.value[1] = ts / tw if tw != 0 else 0.0
         tree.wgt_cnt[1] = tw
@@ -359,7 +366,7 @@ class TreeTrainer:
         imp = IMPURITY_IDS[self.cfg.impurity]
         min_inst = float(self.cfg.min_instances_per_node)
         min_gain = float(self.cfg.min_info_gain)
-        hist = torch.zeros(nn, F, NB, 2, dtype=torch.float32, device=self.dev)
+        hist = torch.zeros(nn, 2, F, NB, dtype=torch.int64, device=self.dev)
         if self.gpu:
             best, cat_order = self._build_and_split_hip(nodes, n_built, g, w, pos2row, hist_prev, hist, mask,
                                                         imp, min_inst, min_gain)
@@ -401,18 +408,18 @@ class TreeTrainer:
         t0 = time.perf_counter()
         if items:
             it = torch.tensor(items, dtype=torch.int32, device=self.dev)
-            slab = torch.empty(len(items), FG, NB, 2, dtype=torch.float32, device=self.dev)
-            nat.call_hip("shifu_gbdt_hist", d.bins.data_ptr(), d.bins.shape[1], pos2row.data_ptr(), w.data_ptr(),
-                         g.data_ptr(), it.data_ptr(), len(items), slab.data_ptr(), F, st)
+            slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
+            nat.call_hip("shifu_gbdt_hist", d.bins, d.bins.shape[1], pos2row, w, g, it, len(items), slab, F,
+                         self.scale_w, self.scale_g, st)
         else:
-            slab = torch.zeros(1, FG, NB, 2, dtype=torch.float32, device=self.dev)
+            slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
         built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
         derived = [z for z in nodes if not z["built"]]
         if n_built:
             nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, None, None, None,
                          hist.data_ptr(), built.data_ptr(), n_built, feat_list.data_ptr(), F,
                          self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), None, cand.data_ptr(), None, F, 0, imp,
-                         0, min_inst, min_gain, st)
+                         0, min_inst, min_gain, 1.0 / self.scale_w, 1.0 / self.scale_g, st)
         self.timings["hist"] += time.perf_counter() - t0
         # cross-rank reduction of the built-node histograms (one RCCL bucket per level)
         if n_built:
@@ -423,7 +430,7 @@ class TreeTrainer:
             nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, None, None, None,
                          hist.data_ptr(), built.data_ptr(), n_built, feat_list.data_ptr(), F,
                          self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), mptr, cand.data_ptr(), cptr, F, 2, imp,
-                         1, min_inst, min_gain, st)
+                         1, min_inst, min_gain, 1.0 / self.scale_w, 1.0 / self.scale_g, st)
         if derived:
             dl = torch.tensor([z["slot"] for z in derived], dtype=torch.int32, device=self.dev)
             par = np.zeros(nn, np.int32)
@@ -436,7 +443,8 @@ class TreeTrainer:
             nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, hist_prev.data_ptr(),
                          par_t.data_ptr(), sib_t.data_ptr(), hist.data_ptr(), dl.data_ptr(), len(derived),
                          feat_list.data_ptr(), F, self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), mptr,
-                         cand.data_ptr(), cptr, F, 1, imp, 1, min_inst, min_gain, st)
+                         cand.data_ptr(), cptr, F, 1, imp, 1, min_inst, min_gain, 1.0 / self.scale_w,
+                         1.0 / self.scale_g, st)
         best = self._select_best(cand, nn)
         co = None if cat_order is None else cat_order.cpu().numpy()
         return best, co
@@ -454,30 +462,30 @@ class TreeTrainer:
             if rows.numel() == 0:
                 continue
             b = bins[rows]                                   # [m, F]
-            ww = w[rows].float()
-            gg = (w[rows] * g[rows]).float()
+            qw = torch.round(w[rows].double() * self.scale_w).long()
+            qg = torch.round((w[rows] * g[rows]).float().double() * self.scale_g).long()
             idx = (torch.arange(F).unsqueeze(0) * NB + b).reshape(-1)
-            hw = torch.zeros(F * NB, dtype=torch.float32)
-            hg = torch.zeros(F * NB, dtype=torch.float32)
-            hw.index_add_(0, idx, ww.unsqueeze(1).expand(-1, F).reshape(-1))
-            hg.index_add_(0, idx, gg.unsqueeze(1).expand(-1, F).reshape(-1))
-            hist[z["slot"], :, :, 0] = hw.view(F, NB)
-            hist[z["slot"], :, :, 1] = hg.view(F, NB)
+            hw = torch.zeros(F * NB, dtype=torch.int64)
+            hg = torch.zeros(F * NB, dtype=torch.int64)
+            hw.index_add_(0, idx, qw.unsqueeze(1).expand(-1, F).reshape(-1))
+            hg.index_add_(0, idx, qg.unsqueeze(1).expand(-1, F).reshape(-1))
+            hist[z["slot"], 0] = hw.view(F, NB)
+            hist[z["slot"], 1] = hg.view(F, NB)
         if n_built:
             dist.all_reduce_(hist[:n_built])
         for z in nodes:
             if not z["built"]:
                 hist[z["slot"]] = hist_prev[z["parent"]] - hist[z["sib_slot"]]
-                hist[z["slot"], :, :, 0].clamp_(min=0)
         cand = torch.zeros(nn, F, 8, dtype=torch.float32)
         cat_order = np.zeros((nn, F, NB), dtype=np.uint8) if d.is_cat.any() else None
-        H = hist.double()
+        HW = hist[:, 0].double() * (1.0 / self.scale_w)
+        HG = hist[:, 1].double() * (1.0 / self.scale_g)
         for s_ in range(nn):
             for f in range(F):
                 if mask is not None and not mask[s_, f]:
                     continue
-                cw = H[s_, f, :, 0].clone()
-                cs = H[s_, f, :, 1].clone()
+                cw = HW[s_, f].clone()
+                cs = HG[s_, f].clone()
                 nb = int(d.nbins[f])
                 if d.is_cat[f]:
                     keys = [(1e300 if b >= nb else (float(cs[b] / cw[b]) if cw[b] != 0 else 4.9e-324), b)
@@ -543,9 +551,9 @@ class TreeTrainer:
             new_p2r = torch.empty_like(pos2row)
             new_pn = torch.empty_like(pos_node)
             t = lambda a, dt=np.int32: torch.from_numpy(np.ascontiguousarray(a.astype(dt))).to(self.dev)  # noqa
-            nat.call_hip("shifu_gbdt_partition_scatter", pos2row.data_ptr(), pos_node.data_ptr(), flag.data_ptr(),
-                         cum.data_ptr(), t(starts).data_ptr(), t(nleft).data_ptr(), t(cb).data_ptr(), sf.data_ptr(),
-                         t(child_l).data_ptr(), t(child_r).data_ptr(), new_p2r.data_ptr(), new_pn.data_ptr(), n, st)
+            # tensors (not .data_ptr() of temporaries) so every buffer outlives the launch
+            nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, flag, cum, t(starts), t(nleft), t(cb),
+                         sf, t(child_l), t(child_r), new_p2r, new_pn, n, st)
             # child slot ids follow the order of new_nodes built by the caller (left, right per split)
             return new_p2r, new_pn, ranges
         # CPU path
@@ -582,11 +590,9 @@ class TreeTrainer:
         if data.device.type == "cuda":
             from ..ops import _native as nat
             feat, thr, cl, val = tree.device_arrays(data.device)
-            nat.call_hip("shifu_gbdt_apply_tree", data.bins.data_ptr(), data.bins.shape[1], None, feat.data_ptr(),
-                         thr.data_ptr(), cl.data_ptr(), val.data_ptr(),
-                         torch.from_numpy(data.is_cat.astype(np.uint8)).to(data.device).data_ptr(),
-                         pred.data_ptr(), float(scale), int(set_mode), None, data.n, tree.max_nodes,
-                         nat.stream_of(pred))
+            ic = torch.from_numpy(data.is_cat.astype(np.uint8)).to(data.device)
+            nat.call_hip("shifu_gbdt_apply_tree", data.bins, data.bins.shape[1], None, feat, thr, cl, val, ic,
+                         pred, float(scale), int(set_mode), None, data.n, tree.max_nodes, nat.stream_of(pred))
         else:
             v = torch.from_numpy(tree.predict_bins(data.bins.numpy(), data.is_cat)).float()
             if set_mode:
@@ -669,6 +675,12 @@ class TreeTrainer:
         if not self.cfg.is_gbt and self.trees:
             p /= len(self.trees)
         return p
+
+
+def _fixed_scale(max_abs: float, n_rows: float) -> float:
+    """2^S such that n_rows * max_abs * 2^S < 2^62 (int64 histogram sums never overflow)."""
+    bound = max(max_abs, 1e-30) * max(n_rows, 1.0)
+    return float(2.0 ** min(60, math.floor(62 - math.log2(bound))))
 
 
 def _gain_py(imp, lw, ls, rw, rs):

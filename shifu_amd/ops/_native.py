@@ -38,8 +38,8 @@ HIP_SIGNATURES = {
     "shifu_cast_bf16": "plpliis",
     "shifu_transpose_cast": "plpiiis",
     # gbdt_kernels.hip
-    "shifu_gbdt_hist": "plpppp" "ipi" "s",
-    "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "s",
+    "shifu_gbdt_hist": "plpppp" "ipi" "dd" "s",
+    "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
     "shifu_gbdt_partition_flag": "plppppppp" "l" "s",
     "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "l" "s",
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
@@ -114,8 +114,15 @@ def check(rc: int, name: str):
 
 
 def call_hip(name: str, *args):
+    """Launch ``name``.  torch tensors may be passed directly: they are converted to device
+    pointers here and stay referenced until the launch has been enqueued (never pass
+    ``tmp().data_ptr()`` - the temporary is freed and its block re-issued by the caching
+    allocator before the kernel runs)."""
     fn = getattr(hip(), name)
-    rc = fn(*args)
+    keep = args
+    conv = [a.data_ptr() if hasattr(a, "data_ptr") else a for a in args]
+    rc = fn(*conv)
+    del keep
     if rc != 0:
         raise RuntimeError(f"HIP kernel launcher {name} returned {rc} (bad shape or HIP error)")
     return rc

@@ -28,7 +28,6 @@ namespace {
 
 constexpr int NB = 256;        // max bins per feature (uint8 codes)
 constexpr int FG = 32;         // features per work-item group
-constexpr int HSTRIDE = 257;   // padded per-feature plane stride (words)
 
 struct HistArgs {
   const uint8_t* bins; long ldb;     // [N][ldb]
@@ -36,48 +35,64 @@ struct HistArgs {
   const float* w;                    // [N] per-row weight (significance x subsample)
   const float* g;                    // [N] per-row target (label / pseudo residual)
   const int* items;                  // [n_items][4] = {node, pos_lo, pos_hi, group}
-  float* slab;                       // [n_items][FG][NB][2]
+  long long* slab;                   // [n_items][2][FG][NB] int64 fixed point
   int n_items, n_feat;
+  double scale_w, scale_g;           // fixed-point scales (2^S, chosen so sums cannot overflow)
 };
 
-__global__ __launch_bounds__(256) void gbdt_hist_kernel(HistArgs a) {
-  __shared__ float hw[FG * HSTRIDE];
-  __shared__ float hg[FG * HSTRIDE];
+// gfx950 measured (tools/microbench_lds_atomics.hip): ds_add_f32 ~100 G updates/s vs
+// ds_add_u32/u64 ~1.7 T/s.  So the LDS histogram is int64 fixed point: exact, order-independent
+// (bit-identical on every rank / every run) and 17x faster than float LDS atomics.
+constexpr int HT = 512;        // threads per histogram block (8 waves)
+constexpr int HU = 4;          // row slots in flight per thread
+constexpr int HP = 257;        // padded plane stride (u64 words)
+
+__global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];   // [2][FG][HP]
+  unsigned long long* hw = hsm;
+  unsigned long long* hg = hsm + FG * HP;
   const int item = blockIdx.x;
   const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
-  for (int i = threadIdx.x; i < FG * HSTRIDE; i += 256) { hw[i] = 0.f; hg[i] = 0.f; }
+  for (int i = threadIdx.x; i < 2 * FG * HP; i += HT) hsm[i] = 0ull;
   __syncthreads();
   const int half = threadIdx.x & 1;                 // which 16-feature half of the 32-B slice
-  const int f0 = grp * FG + half * 16;
-  const int nvalid = min(16, a.n_feat - f0);
-  // 128 rows in flight per block pass, 2 lanes per row, 16 B (16 features) per lane
-  for (int p = lo + (threadIdx.x >> 1); p < hi; p += 128) {
-    const int row = a.pos2row[p];
-    const float wv = a.w[row];
-    if (wv == 0.f) continue;
-    const float gv = wv * a.g[row];
-    const uint4 v = *(const uint4*)(a.bins + (size_t)row * a.ldb + f0);
-    const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+  const int f0 = grp * FG + half * 16;              // padded features (>= n_feat) land in unused planes
+  unsigned long long* pw = hw + half * 16 * HP;
+  unsigned long long* pg = hg + half * 16 * HP;
+  constexpr int RPP = HT / 2;                       // rows per slot pass
+  for (int p0 = lo + (threadIdx.x >> 1); p0 < hi; p0 += RPP * HU) {
+    int rows[HU];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      // stagger the feature order by lane so a wave's lanes spread over planes
-      const int jj = (j + (threadIdx.x >> 1)) & 15;
-      if (jj < nvalid) {
-        const uint32_t b = (words[jj >> 2] >> ((jj & 3) * 8)) & 0xff;
-        const int off = (half * 16 + jj) * HSTRIDE + b;
-        atomicAdd(&hw[off], wv);
-        atomicAdd(&hg[off], gv);
+    for (int u = 0; u < HU; ++u) { const int p = p0 + u * RPP; rows[u] = p < hi ? a.pos2row[p] : -1; }
+    float wv[HU], gv[HU];
+    uint4 bv[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int r = rows[u];
+      wv[u] = r >= 0 ? a.w[r] : 0.f;
+      gv[u] = r >= 0 ? a.g[r] : 0.f;
+      bv[u] = r >= 0 ? *(const uint4*)(a.bins + (size_t)r * a.ldb + f0) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      if (wv[u] == 0.f) continue;
+      const float wgf = wv[u] * gv[u];
+      const unsigned long long qw = (unsigned long long)__double2ll_rn((double)wv[u] * a.scale_w);
+      const unsigned long long qg = (unsigned long long)__double2ll_rn((double)wgf * a.scale_g);
+      const uint32_t words[4] = {bv[u].x, bv[u].y, bv[u].z, bv[u].w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (words[j >> 2] >> ((j & 3) * 8)) & 0xff;
+        atomicAdd(&pw[j * HP + b], qw);
+        atomicAdd(&pg[j * HP + b], qg);
       }
     }
   }
   __syncthreads();
-  float* out = a.slab + (size_t)item * FG * NB * 2;
-  for (int i = threadIdx.x; i < FG * NB; i += 256) {
-    const int f = i / NB, b = i % NB;
-    float2 v;
-    v.x = hw[f * HSTRIDE + b];
-    v.y = hg[f * HSTRIDE + b];
-    *(float2*)(out + (size_t)i * 2) = v;
+  long long* out = a.slab + (size_t)item * 2 * FG * NB;
+  for (int i = threadIdx.x; i < 2 * FG * NB; i += HT) {
+    const int st = i / (FG * NB), r = i % (FG * NB), f = r / NB, b = r % NB;
+    out[i] = (long long)hsm[st * FG * HP + f * HP + b];
   }
 }
 
@@ -90,13 +105,13 @@ __global__ __launch_bounds__(256) void gbdt_hist_kernel(HistArgs a) {
 enum Imp : int { IMP_VARIANCE = 0, IMP_FRIEDMAN = 1, IMP_ENTROPY = 2, IMP_GINI = 3 };
 
 struct SplitArgs {
-  const float* slab;            // [n_items][FG][NB][2]
+  const long long* slab;        // [n_items][2][FG][NB] int64 fixed point
   const int* node_items;        // [n_nodes][n_groups][max_items] item ids (-1 padded) (mode 0)
   int max_items;
-  const float* parent_hist;     // [n_parent][F][NB][2]                        (mode 1)
+  const long long* parent_hist; // [n_parent][2][F][NB]                        (mode 1)
   const int* node_parent;       // [n_nodes] parent slot in parent_hist        (mode 1)
   const int* node_sibling;      // [n_nodes] sibling slot in hist              (mode 1)
-  float* hist;                  // [n_nodes][F][NB][2] out
+  long long* hist;              // [n_nodes][2][F][NB] out (int64 fixed point)
   const int* node_list;         // nodes processed by this launch
   int n_list;
   const int* feat_list;         // candidate features (subset)
@@ -108,6 +123,7 @@ struct SplitArgs {
   uint8_t* cat_order;           // [n_nodes][n_fsub][NB] sorted bin order for categorical (nullable)
   int F, mode, impurity, do_scan;
   float min_inst, min_gain;
+  double inv_w, inv_g;          // 1 / fixed-point scales
 };
 
 __device__ __forceinline__ double imp_gain(int imp, double lw, double ls, double rw, double rs) {
@@ -147,12 +163,14 @@ __global__ __launch_bounds__(256) void gbdt_split_kernel(SplitArgs a) {
   const int fi = gw % a.n_fsub;
   const int f = a.feat_list[fi];
   float* cand = a.cand + ((size_t)node * a.n_fsub + fi) * 8;
-  float* h = a.hist + ((size_t)node * a.F + f) * NB * 2;
-  // ---- gather this (node, feature) histogram: 4 bins per lane --------------------------
-  double cw[4], cs[4];
+  const size_t plane = (size_t)a.F * NB;              // stat plane stride inside a node
+  long long* hw = a.hist + (size_t)node * 2 * plane + (size_t)f * NB;
+  long long* hg = hw + plane;
+  // ---- gather this (node, feature) histogram: 4 bins per lane (int64, exact) ----------
+  long long qw[4], qg[4];
   const int b0 = lane * 4;
   if (a.mode == 0) {
-    for (int k = 0; k < 4; ++k) { cw[k] = 0.0; cs[k] = 0.0; }
+    for (int k = 0; k < 4; ++k) { qw[k] = 0; qg[k] = 0; }
     // node_items is laid out [node][group][max_items]: the items of this node's feature group
     const int fg = f / FG, fl = f % FG;
     const int n_groups = (a.F + FG - 1) / FG;
@@ -160,32 +178,32 @@ __global__ __launch_bounds__(256) void gbdt_split_kernel(SplitArgs a) {
     for (int t = 0; t < a.max_items; ++t) {
       const int it = its[t];
       if (it < 0) break;
-      const float* sp = a.slab + (((size_t)it * FG + fl) * NB + b0) * 2;
-      const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
-      cw[0] += v0.x; cs[0] += v0.y; cw[1] += v0.z; cs[1] += v0.w;
-      cw[2] += v1.x; cs[2] += v1.y; cw[3] += v1.z; cs[3] += v1.w;
+      const long long* sw = a.slab + (size_t)it * 2 * FG * NB + (size_t)fl * NB + b0;
+      const long long* sg = sw + FG * NB;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { qw[k] += sw[k]; qg[k] += sg[k]; }
     }
   } else if (a.mode == 2) {        // already-reduced histogram (after the cross-rank all-reduce)
-    const float4 v0 = *(const float4*)(h + b0 * 2), v1 = *(const float4*)(h + b0 * 2 + 4);
-    cw[0] = v0.x; cs[0] = v0.y; cw[1] = v0.z; cs[1] = v0.w;
-    cw[2] = v1.x; cs[2] = v1.y; cw[3] = v1.z; cs[3] = v1.w;
-  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { qw[k] = hw[b0 + k]; qg[k] = hg[b0 + k]; }
+  } else {                         // derived sibling = parent - built sibling (exact in int64)
     const int par = a.node_parent[node], sib = a.node_sibling[node];
-    const float* ph = a.parent_hist + ((size_t)par * a.F + f) * NB * 2 + b0 * 2;
-    const float* sh = a.hist + ((size_t)sib * a.F + f) * NB * 2 + b0 * 2;
+    const long long* pw = a.parent_hist + (size_t)par * 2 * plane + (size_t)f * NB;
+    const long long* sw = a.hist + (size_t)sib * 2 * plane + (size_t)f * NB;
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
-      cw[k] = (double)ph[2 * k] - (double)sh[2 * k];
-      cs[k] = (double)ph[2 * k + 1] - (double)sh[2 * k + 1];
-      if (cw[k] < 0.0) cw[k] = 0.0;    // fp32 subtraction noise on empty bins
+      qw[k] = pw[b0 + k] - sw[b0 + k];
+      qg[k] = pw[plane + b0 + k] - sw[plane + b0 + k];
     }
   }
   if (a.mode != 2) {
-    float4 o0 = make_float4((float)cw[0], (float)cs[0], (float)cw[1], (float)cs[1]);
-    float4 o1 = make_float4((float)cw[2], (float)cs[2], (float)cw[3], (float)cs[3]);
-    *(float4*)(h + b0 * 2) = o0;
-    *(float4*)(h + b0 * 2 + 4) = o1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { hw[b0 + k] = qw[k]; hg[b0 + k] = qg[k]; }
   }
   if (!a.do_scan) return;
+  double cw[4], cs[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { cw[k] = (double)qw[k] * a.inv_w; cs[k] = (double)qg[k] * a.inv_g; }
   if (a.feat_mask && !a.feat_mask[(size_t)node * a.F + f]) {
     if (lane == 0) { cand[0] = -1.f; cand[6] = 0.f; }
     return;
@@ -378,10 +396,11 @@ __global__ void gbdt_apply_tree_kernel(TreeArgs a) {
 struct ResidArgs {
   const float* pred; const float* y; const float* sig; float* out; double* err; long n; int loss;
 };
-__global__ void gbdt_residual_kernel(ResidArgs a) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
+  // grid-stride + block reduction: one pair of f64 atomics per block (not per wave)
+  __shared__ double red[4][2];
   double e = 0.0, ws = 0.0;
-  if (i < a.n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (long)gridDim.x * blockDim.x) {
     const float p = a.pred[i], y = a.y[i], s = a.sig ? a.sig[i] : 1.f;
     float grad, err;
     switch (a.loss) {
@@ -392,12 +411,18 @@ __global__ void gbdt_residual_kernel(ResidArgs a) {
       default: grad = 2.f * (p - y); err = (p - y) * (p - y); break;                    // squared
     }
     a.out[i] = -grad;
-    e = (double)s * err;
-    ws = s;
+    e += (double)s * err;
+    ws += s;
   }
   e = wave_sum_d(e);
   ws = wave_sum_d(ws);
-  if ((threadIdx.x & 63) == 0) { atomicAdd(a.err, e); atomicAdd(a.err + 1, ws); }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[wv][0] = e; red[wv][1] = ws; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(a.err, red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+    atomicAdd(a.err + 1, red[0][1] + red[1][1] + red[2][1] + red[3][1]);
+  }
 }
 
 }  // namespace
@@ -405,23 +430,26 @@ __global__ void gbdt_residual_kernel(ResidArgs a) {
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 SHIFU_API int shifu_gbdt_hist(const void* bins, long ldb, const int* pos2row, const float* w, const float* g,
-                              const int* items, int n_items, float* slab, int n_feat, hipStream_t stream) {
-  if (ldb % 16 || n_items <= 0) return -1;
-  HistArgs a{(const uint8_t*)bins, ldb, pos2row, w, g, items, slab, n_items, n_feat};
-  hipLaunchKernelGGL(gbdt_hist_kernel, dim3(n_items), dim3(256), 0, stream, a);
+                              const int* items, int n_items, void* slab, int n_feat, double scale_w,
+                              double scale_g, hipStream_t stream) {
+  if (ldb % 32 || n_items <= 0) return -1;
+  HistArgs a{(const uint8_t*)bins, ldb, pos2row, w, g, items, (long long*)slab, n_items, n_feat, scale_w, scale_g};
+  hipLaunchKernelGGL(gbdt_hist_kernel, dim3(n_items), dim3(HT), 2 * FG * HP * 8, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
 
-SHIFU_API int shifu_gbdt_split(const float* slab, const int* node_items, int max_items, const float* parent_hist,
-                               const int* node_parent, const int* node_sibling, float* hist, const int* node_list,
+SHIFU_API int shifu_gbdt_split(const void* slab, const int* node_items, int max_items, const void* parent_hist,
+                               const int* node_parent, const int* node_sibling, void* hist, const int* node_list,
                                int n_list, const int* feat_list, int n_fsub, const int* nbins, const void* is_cat,
                                const void* feat_mask, float* cand, void* cat_order, int F, int mode, int impurity,
-                               int do_scan, float min_inst, float min_gain, hipStream_t stream) {
+                               int do_scan, float min_inst, float min_gain, double inv_w, double inv_g,
+                               hipStream_t stream) {
   if (n_list <= 0 || n_fsub <= 0) return 0;
-  SplitArgs a{slab, node_items, max_items, parent_hist, node_parent, node_sibling, hist, node_list, n_list,
-              feat_list, n_fsub, nbins, (const uint8_t*)is_cat, (const uint8_t*)feat_mask, cand,
-              (uint8_t*)cat_order, F, mode, impurity, do_scan, min_inst, min_gain};
+  SplitArgs a{(const long long*)slab, node_items, max_items, (const long long*)parent_hist, node_parent, node_sibling,
+              (long long*)hist, node_list, n_list, feat_list, n_fsub, nbins, (const uint8_t*)is_cat,
+              (const uint8_t*)feat_mask, cand, (uint8_t*)cat_order, F, mode, impurity, do_scan, min_inst, min_gain,
+              inv_w, inv_g};
   const long waves = (long)n_list * n_fsub;
   hipLaunchKernelGGL(gbdt_split_kernel, dim3((waves + 3) / 4), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
@@ -465,7 +493,9 @@ SHIFU_API int shifu_gbdt_residual(const float* pred, const float* y, const float
                                   long n, int loss, hipStream_t stream) {
   if (n <= 0) return 0;
   ResidArgs a{pred, y, sig, out, err, n, loss};
-  hipLaunchKernelGGL(gbdt_residual_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(gbdt_residual_kernel, dim3(blocks), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

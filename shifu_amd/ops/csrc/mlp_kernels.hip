@@ -118,21 +118,35 @@ __global__ __launch_bounds__(256) void mlp_output_kernel(OutArgs p) {
       }
     }
   }
-  // reduce gacc over the RPS row-groups of the wave (lanes with equal li), then one atomic per column
+  // Reduce the gradient partials: over the RPS row-groups of the wave (shuffles), then over the
+  // block's 4 waves (LDS), then ONE global atomic per column per block.  (Every block adding to
+  // the same few hundred addresses is what made a naive per-wave atomic version 8x slower.)
+  __shared__ float red[4][512];
+  __shared__ double ered[4][2];
+  const int wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int o = 0; o < NOUT; ++o)
+  for (int o = 0; o < NOUT; ++o) {
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       float v = gacc[o][c];
 #pragma unroll
       for (int off = LPR; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-      if (sub == 0) atomicAdd(p.GW + (size_t)o * p.KH + c0 + c, v);
+      if (sub == 0) red[wv][c0 + c] = v;
     }
+    __syncthreads();
+    for (int col = threadIdx.x; col < p.KH; col += blockDim.x) {
+      const float v = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+      atomicAdd(p.GW + (size_t)o * p.KH + col, v);
+    }
+    __syncthreads();
+  }
   esum = wave_sum_d(esum);
   wsum = wave_sum_d(wsum);
-  if (lane == 0) {
-    atomicAdd(p.err, esum);
-    atomicAdd(p.err + 1, wsum);
+  if (lane == 0) { ered[wv][0] = esum; ered[wv][1] = wsum; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(p.err, ered[0][0] + ered[1][0] + ered[2][0] + ered[3][0]);
+    atomicAdd(p.err + 1, ered[0][1] + ered[1][1] + ered[2][1] + ered[3][1]);
   }
 }
 
@@ -240,7 +254,7 @@ SHIFU_API int shifu_mlp_output(const void* H, long ldh, const void* Hd, long ldh
   const int lpr = KH / 8;
   const long rows_per_wave_iter = (64 / lpr) * 4;
   long waves = (M + rows_per_wave_iter - 1) / rows_per_wave_iter;
-  if (waves > 8192) waves = 8192;          // grid-stride: 2048 blocks x 4 waves
+  if (waves > 4096) waves = 4096;          // grid-stride: <= 1024 blocks x 4 waves
   const long blocks = (waves + 3) / 4;
   // dispatch on (n_out, lanes-per-row)
 #define OUT_L(NO, L) hipLaunchKernelGGL((mlp_output_kernel<NO, L>), dim3(blocks), dim3(256), 0, stream, p)
