@@ -1,0 +1,206 @@
+"""Normalization (H7) and tree-input binning (CleanedData).
+
+All 22 ``NormType``s of ``J/core/Normalizer.java`` (normalize :233-333, zScoreNormalize :444,
+parseRawValue :522-577, woeNormalize :619-648, woeZScoreNormalize :664, calculateWoeMeanAndStdDev
+:728-754, computeZScore :769-785), vectorized per column over the purified table:
+
+* ZSCALE/ZSCORE: numeric value (missing/invalid/inf -> mean), clipped to mean +- cutoff*std,
+  then (v-mean)/std (std <= 1e-5 -> 0); categorical -> bin pos-rate (missing/unknown -> last
+  bin's pos rate) then z-scored.  OLD_*: categorical pos-rate not z-scored.
+* WOE / WEIGHT_WOE: bin WOE (missing -> last bin).  *_WOE_ZSCORE: z-score of WOE with the
+  count-weighted WOE mean/std.  HYBRID: numeric z-score, categorical WOE.
+* ONEHOT: one column per bin incl. missing; ZSCALE_ONEHOT: numeric z-score, categorical one-hot.
+* ASIS_WOE / ASIS_PR: numeric raw value, categorical WOE / pos-rate.
+* DISCRETE_Z*: numeric -> lower bound of its bin (first bin -> min, missing -> mean), z-scored.
+* *_INDEX: categorical -> category index (for embeddings); numeric per the prefix.
+
+Tree models use ``tree_bin_codes``: numeric rows -> bin index of their value (missing -> 0.0 as
+``DTWorker.getFloatValue``), categorical -> category index (missing/unknown -> last bin).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..config.enums import is_index_norm
+from . import binning as B
+
+STD_DEV_CUTOFF = 4.0
+
+
+def _cat_index(cc, col) -> np.ndarray:
+    cats = cc.bin_category or []
+    lut = {}
+    for i, c in enumerate(cats):
+        for sub in str(c).split("^"):
+            lut.setdefault(sub, i)
+    if col.kind == "str":
+        d = col.dictionary
+        m = np.array([lut.get(s, -1) for s in d] + [-1], dtype=np.int64)
+        return m[np.where(col.values >= 0, col.values, len(d))]
+    s = col.strings()
+    return np.array([lut.get(v, -1) if v != "" else -1 for v in s], dtype=np.int64)
+
+
+def _num_values(cc, col) -> np.ndarray:
+    v = col.numeric().astype(np.float64)
+    mean = cc.mean if cc.mean is not None else 0.0
+    bad = ~np.isfinite(v)
+    if bad.any():
+        v = v.copy()
+        v[bad] = mean
+    return v
+
+
+def zscore(v: np.ndarray, mean: float, std: float, cutoff: float) -> np.ndarray:
+    mean = 0.0 if mean is None else float(mean)
+    std = 0.0 if std is None else float(std)
+    v = np.minimum(v, mean + cutoff * std)
+    v = np.maximum(v, mean - cutoff * std)
+    if std > 0.00001:
+        return (v - mean) / std
+    return np.zeros_like(v)
+
+
+def woe_mean_std(cc, weighted: bool):
+    woe = np.asarray(cc.bin_weighted_woe if weighted else cc.bin_count_woe, dtype=np.float64)
+    cnt = np.asarray(cc.bin_count_neg, dtype=np.float64) + np.asarray(cc.bin_count_pos, dtype=np.float64)
+    tot = cnt.sum()
+    s = (woe * cnt).sum()
+    sq = (woe * woe * cnt).sum()
+    mean = s / tot
+    std = np.sqrt(abs((sq - s * s / tot) / (tot - 1))) if tot > 1 else 0.0
+    return mean, std
+
+
+def _bin_num(cc, col) -> np.ndarray:
+    """BinUtils.getBinNum: -1 for missing/invalid."""
+    if cc.is_categorical():
+        return _cat_index(cc, col)
+    v = col.numeric().astype(np.float64)
+    bb = cc.bin_boundary or [float("-inf")]
+    idx = B.bin_index_numeric(v, bb).astype(np.int64)
+    idx[np.isnan(v)] = -1
+    return idx
+
+
+def _lookup_last(table_vals, idx):
+    t = np.asarray(table_vals, dtype=np.float64)
+    return np.where(idx >= 0, t[np.clip(idx, 0, len(t) - 1)], t[-1])
+
+
+def norm_width(cc, norm_type: str) -> int:
+    if norm_type == "ONEHOT":
+        return (len(cc.bin_boundary or []) + 1) if not cc.is_categorical() else len(cc.bin_category or []) + 1
+    if norm_type == "ZSCALE_ONEHOT" and cc.is_categorical():
+        return len(cc.bin_category or []) + 1
+    return 1
+
+
+def normalize_column(cc, col, norm_type: str, cutoff: float | None) -> np.ndarray:
+    """-> [N, width] float64."""
+    cutoff = STD_DEV_CUTOFF if cutoff is None or not np.isfinite(cutoff) else float(cutoff)
+    nt = norm_type
+    n = len(col.values)
+    cat = cc.is_categorical()
+    if nt in ("ZSCALE", "ZSCORE", "OLD_ZSCALE", "OLD_ZSCORE"):
+        if cat:
+            idx = _cat_index(cc, col)
+            v = _lookup_last(cc.bin_pos_rate, idx)
+            if nt.startswith("OLD_"):
+                return v[:, None]
+        else:
+            v = _num_values(cc, col)
+        return zscore(v, cc.mean, cc.std_dev, cutoff)[:, None]
+    if nt in ("WOE", "WEIGHT_WOE"):
+        return _lookup_last(cc.bin_weighted_woe if nt == "WEIGHT_WOE" else cc.bin_count_woe,
+                            _bin_num(cc, col))[:, None]
+    if nt in ("WOE_ZSCORE", "WOE_ZSCALE", "WEIGHT_WOE_ZSCORE", "WEIGHT_WOE_ZSCALE"):
+        w = nt.startswith("WEIGHT")
+        woe = _lookup_last(cc.bin_weighted_woe if w else cc.bin_count_woe, _bin_num(cc, col))
+        m, s = woe_mean_std(cc, w)
+        return zscore(woe, m, s, cutoff)[:, None]
+    if nt in ("HYBRID", "WEIGHT_HYBRID"):
+        if cat:
+            return _lookup_last(cc.bin_weighted_woe if nt == "WEIGHT_HYBRID" else cc.bin_count_woe,
+                                _bin_num(cc, col))[:, None]
+        return zscore(_num_values(cc, col), cc.mean, cc.std_dev, cutoff)[:, None]
+    if nt == "ONEHOT" or (nt == "ZSCALE_ONEHOT" and cat):
+        width = norm_width(cc, "ONEHOT")
+        idx = _bin_num(cc, col)
+        idx = np.where(idx < 0, width - 1, idx)
+        out = np.zeros((n, width))
+        out[np.arange(n), idx] = 1.0
+        return out
+    if nt == "ZSCALE_ONEHOT":
+        return zscore(_num_values(cc, col), cc.mean, cc.std_dev, cutoff)[:, None]
+    if nt in ("ASIS_WOE", "ASIS_PR"):
+        if cat:
+            tbl = cc.bin_count_woe if nt == "ASIS_WOE" else cc.bin_pos_rate
+            return _lookup_last(tbl, _cat_index(cc, col))[:, None]
+        return _num_values(cc, col)[:, None]
+    if nt in ("DISCRETE_ZSCORE", "DISCRETE_ZSCALE"):
+        if cat:
+            v = _lookup_last(cc.bin_pos_rate, _cat_index(cc, col))
+        else:
+            idx = _bin_num(cc, col)
+            bb = np.asarray(cc.bin_boundary, dtype=np.float64)
+            lo = bb.copy()
+            lo[0] = cc.stat("min", 0.0) if cc.stat("min") is not None else 0.0
+            mean = cc.mean or 0.0
+            v = np.where((idx < 0) | (idx >= len(bb)), mean, lo[np.clip(idx, 0, len(bb) - 1)])
+        return zscore(v, cc.mean, cc.std_dev, cutoff)[:, None]
+    if is_index_norm(nt):
+        if cat:
+            idx = _cat_index(cc, col)
+            return np.where(idx < 0, len(cc.bin_category or []), idx).astype(np.float64)[:, None]
+        if nt in ("ZSCALE_INDEX", "ZSCORE_INDEX"):
+            return zscore(_num_values(cc, col), cc.mean, cc.std_dev, cutoff)[:, None]
+        if nt == "WOE_INDEX":
+            return _lookup_last(cc.bin_count_woe, _bin_num(cc, col))[:, None]
+        woe = _lookup_last(cc.bin_count_woe, _bin_num(cc, col))
+        m, s = woe_mean_std(cc, False)
+        return zscore(woe, m, s, cutoff)[:, None]
+    raise ValueError(f"unsupported norm type {nt}")
+
+
+def normalize_table(mc, ccs, table, columns=None, norm_type: str | None = None):
+    """Normalize the selected columns -> (float32 [N, F'], names, column_nums)."""
+    nt = norm_type or mc.norm_type
+    cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
+    cols = columns if columns is not None else [c for c in ccs if c.final_select and not c.is_target()
+                                                 and not c.is_meta()]
+    mats, names, nums = [], [], []
+    for cc in cols:
+        if cc.name not in table:
+            raise KeyError(f"column {cc.name} missing from data")
+        m = normalize_column(cc, table[cc.name], nt, cutoff)
+        mats.append(m.astype(np.float32))
+        if m.shape[1] == 1:
+            names.append(cc.name)
+        else:
+            names.extend(f"{cc.name}_{i}" for i in range(m.shape[1]))
+        nums.extend([cc.num] * m.shape[1])
+    X = np.concatenate(mats, axis=1) if mats else np.zeros((table.n, 0), np.float32)
+    return X, names, nums
+
+
+def tree_bin_codes(ccs, table, columns):
+    """CleanedData equivalent for GBT/RF: int32 codes [N, F] and bins per feature."""
+    codes, nbins, is_cat = [], [], []
+    for cc in columns:
+        col = table[cc.name]
+        if cc.is_categorical():
+            idx = _cat_index(cc, col)
+            ncat = len(cc.bin_category or [])
+            codes.append(np.where(idx < 0, ncat, idx).astype(np.int32))
+            nbins.append(ncat + 1)
+            is_cat.append(1)
+        else:
+            v = col.numeric().astype(np.float64)
+            v = np.where(np.isfinite(v) | np.isinf(v), v, 0.0)     # DTWorker.getFloatValue: missing -> 0f
+            bb = cc.bin_boundary or [float("-inf")]
+            codes.append(B.bin_index_numeric(v, bb).astype(np.int32))
+            nbins.append(max(1, len(bb)))
+            is_cat.append(0)
+    C = np.stack(codes, 1) if codes else np.zeros((table.n, 0), np.int32)
+    return C, np.array(nbins, np.int32), np.array(is_cat, np.uint8)

@@ -1,0 +1,304 @@
+"""Column statistics (H2) + KS/IV/WOE (K3) + PSI (H4).
+
+Per column, over purified rows (``UpdateBinningInfoMapper.populateStats``
+J/core/binning/UpdateBinningInfoMapper.java:427-598 and ``UpdateBinningInfoReducer.reduce``
+J/core/binning/UpdateBinningInfoReducer.java:125-433):
+  * bins (+ missing bin) with pos/neg counts and weighted sums
+  * count / missing / sum / sum^2 / sum^3 / sum^4 / min / max of valid numeric values
+  * mean, stdDev (sample, with the reference's +EPS), skewness, kurtosis (population sigma)
+  * p25 / median / p75 interpolated inside bins
+  * KS x100, IV, WOE and per-bin WOE ``ln((n+eps)/(p+eps))`` (``ColumnStatsCalculator`` long[]/double[]
+    variants, J/core/ColumnStatsCalculator.java:76-165) for binary targets
+  * categorical: pos-rate per bin, stats recomputed over bin pos-rates
+  * distinct count (exact; the reference uses HyperLogLog++)
+
+The per-column histogram + moments run through torch on the device the data lives on (GPU
+when available), the KS/IV scan is O(bins).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..utils.log import get_logger
+from . import binning as B
+
+_log = get_logger("algos.stats")
+EPS = 1e-10
+
+
+def column_metrics(neg, pos):
+    """ColumnStatsCalculator.calculateColumnMetrics: (ks*100, iv, woe, bin_woe) or None."""
+    neg = np.asarray(neg, dtype=np.float64)
+    pos = np.asarray(pos, dtype=np.float64)
+    sn, sp = neg.sum(), pos.sum()
+    if sn == 0 or sp == 0:
+        return None
+    woe = math.log((sn + EPS) / (sp + EPS))
+    p = pos / sp
+    n = neg / sn
+    bw = np.log((n + EPS) / (p + EPS))
+    iv = float(((n - p) * bw).sum())
+    ks = float(np.abs(np.cumsum(p) - np.cumsum(n)).max())
+    return ks * 100.0, iv, woe, [float(x) for x in bw]
+
+
+def _hist(bin_idx: np.ndarray, y: np.ndarray, w: np.ndarray, nb: int, binary: bool, dev):
+    b = torch.as_tensor(bin_idx, device=dev, dtype=torch.int64)
+    yy = torch.as_tensor(y, device=dev, dtype=torch.float32)
+    ww = torch.as_tensor(w, device=dev, dtype=torch.float64)
+    if binary:
+        pos = yy > 0.5
+        cpos = torch.bincount(b[pos], minlength=nb)[:nb]
+        cneg = torch.bincount(b[~pos], minlength=nb)[:nb]
+        wpos = torch.bincount(b[pos], weights=ww[pos], minlength=nb)[:nb]
+        wneg = torch.bincount(b[~pos], weights=ww[~pos], minlength=nb)[:nb]
+    else:
+        cpos = torch.bincount(b, minlength=nb)[:nb]
+        cneg = torch.zeros_like(cpos)
+        wpos = torch.bincount(b, weights=ww, minlength=nb)[:nb]
+        wneg = torch.zeros_like(wpos)
+    return (cpos.cpu().numpy().astype(np.int64), cneg.cpu().numpy().astype(np.int64),
+            wpos.cpu().numpy(), wneg.cpu().numpy())
+
+
+def _moments(v: np.ndarray, dev):
+    t = torch.as_tensor(v, device=dev, dtype=torch.float64)
+    ok = torch.isfinite(t)
+    x = t[ok]
+    n = int(x.numel())
+    if n == 0:
+        return n, 0.0, 0.0, 0.0, 0.0, float("nan"), float("nan")
+    x2 = x * x
+    return (n, float(x.sum()), float(x2.sum()), float((x2 * x).sum()), float((x2 * x2).sum()),
+            float(x.min()), float(x.max()))
+
+
+def _finish_moments(cc, count, s1, s2, s3, s4, mn, mx, total, missing):
+    real = count
+    if real > 0:
+        mean = s1 / real
+        std = math.sqrt(abs((s2 - s1 * s1 / real + EPS) / (real - 1))) if real > 1 else 0.0
+        astd = math.sqrt(abs((s2 - s1 * s1 / real + EPS) / real))
+        skew = (s3 - 3 * s2 * mean + 3 * mean * mean * s1 - real * mean ** 3) / (real * astd ** 3) \
+            if astd > 0 else 0.0
+        kurt = (s4 - 4 * s3 * mean + 6 * s2 * mean * mean - 4 * s1 * mean ** 3 + real * mean ** 4) / \
+            (real * astd ** 4) if astd > 0 else 0.0
+    else:
+        mean = std = skew = kurt = 0.0
+    st = cc.stats
+    st["max"] = float(mx) if mx == mx else None
+    st["min"] = float(mn) if mn == mn else None
+    st["mean"] = float(mean)
+    st["stdDev"] = float(std)
+    st["skewness"] = float(skew)
+    st["kurtosis"] = float(kurt)
+    st["totalCount"] = int(total)
+    st["missingCount"] = int(missing)
+    st["missingPercentage"] = float(missing) / total if total else 0.0
+
+
+def _percentiles(bounds, counts, mn, mx, count):
+    """Interpolated p25/median/p75 inside bins (UpdateBinningInfoReducer.reduce :229-262)."""
+    p25c = count // 4
+    medc = p25c * 2
+    p75c = p25c * 3
+    p25 = med = p75 = mn
+    cur = 0
+
+    def cut(b):
+        return mx if b > mx else (mn if b < mn else b)
+    for i in range(len(bounds)):
+        left = cut(bounds[i])
+        right = mx if i == len(bounds) - 1 else cut(bounds[i + 1])
+        c = counts[i]
+        if c > 0:
+            if cur <= p25c < cur + c:
+                p25 = (p25c - cur) / c * (right - left) + left
+            if cur <= medc < cur + c:
+                med = (medc - cur) / c * (right - left) + left
+            if cur <= p75c < cur + c:
+                p75 = (p75c - cur) / c * (right - left) + left
+                break
+        cur += c
+    return p25, med, p75
+
+
+def compute_column_stats(mc, ccs, md, device=None, columns=None):
+    """Fill ``columnBinning``/``columnStats`` of every candidate column from ModelData ``md``."""
+    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    binary = mc.is_binary()
+    method = mc.binning_method
+    n_bins = int(mc.stats.get("maxNumBin", 10))
+    cate_max = int(mc.stats.get("cateMaxNumBin", 0) or 0)
+    num_thr = float(mc.stats.get("numericalValueThreshold", 1.7976931348623157e308))
+    algo = mc.binning_algorithm
+    y, w = md.y, md.w
+    for cc in ccs:
+        if columns is not None and cc.name not in columns:
+            continue
+        if cc.is_target() or cc.is_meta() or cc.name not in md.table:
+            continue
+        col = md.table[cc.name]
+        total = md.n
+        if cc.is_categorical():
+            codes = col.values if col.kind == "str" else None
+            if codes is None:   # numeric-parsed categorical: categories = formatted values
+                s = col.strings()
+                uniq = {}
+                codes = np.array([uniq.setdefault(v, len(uniq)) if v != "" else -1 for v in s], dtype=np.int32)
+                dictionary = list(uniq.keys())
+            else:
+                dictionary = col.dictionary
+            cats = B.categorical_bins(codes, dictionary, y, binary)
+            bidx = B.category_index(codes, dictionary, cats)
+            nb = len(cats) + 1
+            cpos, cneg, wpos, wneg = _hist(bidx, y, w, nb, binary, dev)
+            if cate_max > 0 and len(cats) > cate_max:
+                cats, cpos, cneg, wpos, wneg = B.rebin_categorical(cats, list(cpos), list(cneg), list(wpos),
+                                                                   list(wneg), cate_max)
+                cpos, cneg = np.array(cpos, np.int64), np.array(cneg, np.int64)
+                wpos, wneg = np.array(wpos), np.array(wneg)
+            cc.bin_category = cats
+            cc.bin_boundary = None
+            missing = int((bidx == len(cats)).sum()) if cate_max <= 0 else int(cpos[-1] + cneg[-1])
+            if binary:
+                rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
+            else:
+                tot = cpos.sum()
+                rate = cpos / tot if tot else np.zeros_like(cpos, dtype=float)
+            # categorical numeric stats are computed over bin pos-rates (reducer :309-333)
+            cnt = cpos + cneg if binary else cpos
+            okr = np.isfinite(rate)
+            mx = float(rate[okr].max()) if okr.any() else 0.0
+            mn = float(rate[okr].min()) if okr.any() else 0.0
+            s1 = float((rate * cnt).sum())
+            s2 = float((rate ** 2 * cnt).sum())
+            s3 = float((rate ** 3 * cnt).sum())
+            s4 = float((rate ** 4 * cnt).sum())
+            _finish_moments(cc, total - missing, s1, s2, s3, s4, mn, mx, total, missing)
+            cc.stats["distinctCount"] = int(len(dictionary))
+            cc.stats["median"] = None
+        else:
+            vals = col.numeric().astype(np.float64).copy()
+            vals[vals > num_thr] = np.nan          # numericalValueThreshold -> invalid
+            if binary and method in ("EqualPositive", "WeightEqualPositive"):
+                sel = y > 0.5
+            elif binary and method in ("EqualNegtive", "WeightEqualNegative"):
+                sel = y <= 0.5
+            else:
+                sel = np.ones(len(vals), dtype=bool)
+            weighted = method.startswith("Weight")
+            if method in ("EqualInterval", "WeightEqualInterval"):
+                bounds = B.equal_interval_boundaries(vals[sel], n_bins)
+            else:
+                bounds = B.equal_population_boundaries(vals[sel], n_bins, w[sel] if weighted else None)
+            if len(bounds) <= 1 and sel.sum() < len(vals):
+                bounds = B.equal_population_boundaries(vals, n_bins)
+            bidx = B.bin_index_numeric(vals, bounds)
+            nb = len(bounds) + 1
+            cpos, cneg, wpos, wneg = _hist(bidx, y, w, nb, binary, dev)
+            cc.bin_boundary = bounds
+            cc.bin_category = None
+            cnt, s1, s2, s3, s4, mn, mx = _moments(vals, dev)
+            missing = total - cnt
+            _finish_moments(cc, cnt, s1, s2, s3, s4, mn, mx, total, missing)
+            p25, med, p75 = _percentiles(bounds, (cpos + cneg) if binary else cpos, mn, mx, total)
+            cc.stats["median"] = float(med)
+            cc.stats["25th"] = float(p25)
+            cc.stats["75th"] = float(p75)
+            fin = vals[np.isfinite(vals)]
+            cc.stats["distinctCount"] = int(np.unique(fin).size)
+            if binary:
+                rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
+            else:
+                tot = cpos.sum()
+                rate = cpos / tot if tot else np.zeros(nb)
+        cc.stats["validNumCount"] = int(total - cc.stats.get("missingCount", 0))
+        cb = cc.binning
+        cb["length"] = int(nb - 1)
+        cb["binCountPos"] = [int(x) for x in cpos]
+        cb["binCountNeg"] = [int(x) for x in cneg]
+        cb["binWeightedPos"] = [float(x) for x in wpos]
+        cb["binWeightedNeg"] = [float(x) for x in wneg]
+        cb["binPosRate"] = [float(x) for x in rate]
+        if binary:
+            m = column_metrics(cneg, cpos)
+            mw = column_metrics(wneg, wpos)
+            zero = [0.0] * nb
+            cc.stats["ks"], cc.stats["iv"], cc.stats["woe"] = (m[0], m[1], m[2]) if m else (None, None, None)
+            cc.stats["weightedKs"], cc.stats["weightedIv"], cc.stats["weightedWoe"] = \
+                (mw[0], mw[1], mw[2]) if mw else (None, None, None)
+            cb["binCountWoe"] = m[3] if m else zero
+            cb["binWeightedWoe"] = mw[3] if mw else zero
+        else:
+            cb["binCountWoe"] = [0.0] * nb
+            cb["binWeightedWoe"] = [0.0] * nb
+    return ccs
+
+
+def compute_psi(mc, ccs, md, unit_column: str):
+    """Population stability per column across the units of ``psiColumnName``
+    (P/PSI.pig:19-46, PSICalculatorUDF): PSI = sum_units sum_bins (a-e) ln(a/e) with e the
+    overall bin distribution and a the unit's; also records ``unitStats``."""
+    if unit_column not in md.table:
+        _log.warning("psiColumnName %s not in data", unit_column)
+        return ccs
+    units_s = md.table[unit_column].strings()
+    units = sorted(set(units_s))
+    for cc in ccs:
+        if cc.is_target() or cc.is_meta() or cc.name not in md.table:
+            continue
+        col = md.table[cc.name]
+        if cc.is_categorical():
+            cats = cc.bin_category or []
+            codes = col.values if col.kind == "str" else None
+            if codes is None:
+                continue
+            bidx = B.category_index(codes, col.dictionary, cats)
+            nb = len(cats) + 1
+        else:
+            bb = cc.bin_boundary
+            if not bb:
+                continue
+            bidx = B.bin_index_numeric(col.numeric(), bb)
+            nb = len(bb) + 1
+        exp = np.bincount(bidx, minlength=nb).astype(float)
+        exp /= max(exp.sum(), 1)
+        psi = 0.0
+        unit_stats = []
+        for u in units:
+            m = units_s == u
+            act = np.bincount(bidx[m], minlength=nb).astype(float)
+            act /= max(act.sum(), 1)
+            ok = (act > 0) & (exp > 0)
+            pu = float(((act[ok] - exp[ok]) * np.log(act[ok] / exp[ok])).sum())
+            psi += pu
+            unit_stats.append(f"{u}:{pu}")
+        cc.stats["psi"] = psi
+        cc.stats["unitStats"] = unit_stats
+    return ccs
+
+
+def pearson_correlation(mats: np.ndarray, device=None):
+    """Pairwise-complete Pearson (H3, FastCorrelationMapper J/core/correlation/FastCorrelationMapper.java:171-278):
+    rows where either value is missing are skipped per pair.  Implemented as six GEMMs over the
+    masked matrix (X'X, (X^2)'M, M'(X^2), M'M, X'M, M'X) on the device (MFMA via hipBLASLt)."""
+    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    X = torch.as_tensor(mats, dtype=torch.float64, device=dev)
+    M = torch.isfinite(X).to(torch.float64)
+    Xz = torch.where(M > 0, X, torch.zeros_like(X))
+    X2 = Xz * Xz
+    n = M.t() @ M
+    sx = Xz.t() @ M          # sum of x_i over rows where j present
+    sy = M.t() @ Xz          # sum of x_j over rows where i present
+    sxx = X2.t() @ M
+    syy = M.t() @ X2
+    sxy = Xz.t() @ Xz
+    num = sxy - sx * sy / n.clamp(min=1)
+    den = torch.sqrt((sxx - sx * sx / n.clamp(min=1)).clamp(min=0) * (syy - sy * sy / n.clamp(min=1)).clamp(min=0))
+    corr = torch.where(den > 0, num / den, torch.zeros_like(num))
+    corr.fill_diagonal_(1.0)
+    return corr.cpu().numpy()

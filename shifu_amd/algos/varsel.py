@@ -1,0 +1,204 @@
+"""Variable selection (H13).
+
+* filter: KS / IV / mix / pareto ranking up to ``filterNum`` (or ``filterOutRatio``),
+  ForceSelect always in, ForceRemove/meta/target/bad candidates out
+  (``VariableSelector.selectByFilter`` J/core/VariableSelector.java:110-286).
+* auto filter: missing rate >= threshold, IV/KS below minimum, and for each highly correlated
+  pair drop the column with the lower ``postCorrelationMetric``
+  (``VarSelectModelProcessor.autoVarSelCondition`` :1008-1050, ``varSelectByCorrelation`` :1052).
+* sensitivity SE/ST (``VarSelectMapper.map`` J/core/varselect/VarSelectMapper.java:277-333 with
+  ``CacheFlatNetwork`` first-layer caching): for every row and input i the score with input i
+  zeroed is ``net(S - w_i x_i)``; accumulate sum|d| and sum d^2 -> mean / RMS / variance and keep
+  the top by RMS (SE) or by mean (ST).  On the GPU the perturbed first layer for a feature chunk
+  is one batched tensor op over the cached S (the dominant cost for 10k features).
+* voted: genetic wrapper (``CandidateGenerator`` inherit / hybrid / mutate) scored by small NNs.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..utils.log import get_logger
+
+_log = get_logger("algos.varsel")
+
+
+def _candidates(mc, ccs):
+    from ..config.column_config import has_candidates
+    hc = has_candidates(ccs)
+    cand_names = set(mc.candidate_names())
+    out, forced = [], []
+    for c in ccs:
+        if c.is_meta() or c.is_target() or c.is_force_remove() or c.is_weight():
+            continue
+        if c.is_force_select():
+            if c.mean is not None and c.std_dev is not None:
+                forced.append(c)
+            continue
+        if not c.is_good_candidate(hc, mc.is_binary()):
+            continue
+        if cand_names and c.name not in cand_names:
+            continue
+        out.append(c)
+    return out, forced
+
+
+def pareto_sort(tuples):
+    """Iterative epsilon-nondominated fronts over (ks, iv) (VariableSelector.sortByPareto)."""
+    rest = list(tuples)
+    out = []
+    while rest:
+        front = []
+        for t in rest:
+            dominated = any((o[1] >= t[1] and o[2] >= t[2]) and (o[1] > t[1] or o[2] > t[2]) for o in rest)
+            if not dominated:
+                front.append(t)
+        front.sort(key=lambda t: (-t[1], -t[2]))
+        out.extend(front)
+        ids = {id(t) for t in front}
+        rest = [t for t in rest if id(t) not in ids]
+    return out
+
+
+def select_by_filter(mc, ccs):
+    vs = mc.varSelect
+    cands, forced = _candidates(mc, ccs)
+    selected = [c.num for c in forced]
+    if not vs.get("filterEnable", True):
+        for c in ccs:
+            c.final_select = c.num in selected
+        return ccs
+    key = str(vs.get("filterBy", "KS")).lower()
+    filter_num = int(vs.get("filterNum", 200))
+    ratio = vs.get("filterOutRatio")
+    if filter_num <= 0 and ratio is not None:   # setFilterNumberByFilterOutRatio
+        filter_num = int(len(cands) * (1 - float(ratio)))
+    ks_list = sorted(cands, key=lambda c: -(c.ks or 0.0))
+    iv_list = sorted(cands, key=lambda c: -(c.iv or 0.0))
+    par = pareto_sort([(c.num, c.ks or 0.0, c.iv or 0.0) for c in cands])
+    expected = min(len(selected) + len(ks_list), filter_num)
+    for c in ccs:
+        c.final_select = False
+    pk = pi = pp = 0
+    sel = list(selected)
+    guard = 0
+    while len(sel) < expected and guard < 10 * (len(cands) + 1):
+        guard += 1
+        if key == "iv":
+            sel.append(iv_list[pi].num); pi += 1
+        elif key == "mix":
+            if pk < len(ks_list):
+                c = ks_list[pk]; pk += 1
+                if c.num not in sel:
+                    sel.append(c.num)
+            if len(sel) >= expected:
+                break
+            if pi < len(iv_list):
+                c = iv_list[pi]; pi += 1
+                if c.num not in sel:
+                    sel.append(c.num)
+        elif key == "pareto":
+            if pp < len(par):
+                sel.append(par[pp][0]); pp += 1
+            else:
+                c = ks_list[pk]; pk += 1
+                if c.num not in sel:
+                    sel.append(c.num)
+        else:   # ks (default)
+            sel.append(ks_list[pk].num); pk += 1
+    bynum = {c.num: c for c in ccs}
+    for n in sel:
+        if n in bynum:
+            bynum[n].final_select = True
+    return ccs
+
+
+def auto_filter(mc, ccs, corr: np.ndarray | None = None, corr_nums=None):
+    """Returns the list of auto-filtered column names (and sets finalSelect False)."""
+    vs = mc.varSelect
+    if not vs.get("autoFilterEnable", True):
+        return []
+    miss_thr = float(vs.get("missingRateThreshold", 0.98))
+    min_iv = float(vs.get("minIvThreshold", 0.0))
+    min_ks = float(vs.get("minKsThreshold", 0.0))
+    corr_thr = float(vs.get("correlationThreshold", 1.0))
+    metric = str(vs.get("postCorrelationMetric", "IV")).upper()
+    filtered = []
+    for c in ccs:
+        if not c.final_select or c.is_force_select():
+            continue
+        mp = c.missing_pct
+        if mp is not None and mp >= miss_thr:
+            c.final_select = False
+            filtered.append(c.name)
+            continue
+        if mc.is_binary():
+            if (c.iv or 0.0) < min_iv or (c.ks or 0.0) < min_ks:
+                c.final_select = False
+                filtered.append(c.name)
+    if corr is not None and corr_thr < 1.0:
+        idx = {n: i for i, n in enumerate(corr_nums)}
+        sel = [c for c in ccs if c.final_select and c.num in idx]
+        val = (lambda c: c.iv or 0.0) if metric == "IV" else (lambda c: c.ks or 0.0)
+        sel.sort(key=lambda c: -val(c))
+        kept = []
+        for c in sel:
+            if any(abs(corr[idx[c.num], idx[k.num]]) > corr_thr for k in kept):
+                if not c.is_force_select():
+                    c.final_select = False
+                    filtered.append(c.name)
+                    continue
+            kept.append(c)
+    return filtered
+
+
+@torch.no_grad()
+def sensitivity(network, X: np.ndarray, y=None, w=None, device=None, feat_chunk: int = 64,
+                row_chunk: int = 1 << 16):
+    """SE sensitivity over inputs of a trained MLP (NNNetwork, input-first weights).
+
+    Returns (mean |d|, rms, variance) per input, accumulated over rows.  The first layer
+    pre-activation S = X W1^T + b is computed once per row chunk; the perturbed pre-activations
+    for a chunk of features are S[:,None,:] - X[:,f,None] * W1[None,f,:] (rank-1 corrections),
+    then the rest of the network runs batched over (rows x features)."""
+    from ..models.nn import act_fwd
+    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    Ws = [torch.as_tensor(W, dtype=torch.float32, device=dev) for W in network.weights]
+    acts = network.acts
+    F = X.shape[1]
+    s_abs = torch.zeros(F, dtype=torch.float64, device=dev)
+    s_sq = torch.zeros(F, dtype=torch.float64, device=dev)
+    n = 0
+
+    def tail(z1):
+        a = act_fwd(acts[0], z1)
+        for l in range(1, len(Ws)):
+            a = act_fwd(acts[l], a @ Ws[l][:, :-1].t() + Ws[l][:, -1])
+        return a[..., 0]
+    W1 = Ws[0][:, :-1]          # [H1, F]
+    b1 = Ws[0][:, -1]
+    for r0 in range(0, X.shape[0], row_chunk):
+        xb = torch.as_tensor(X[r0: r0 + row_chunk], dtype=torch.float32, device=dev)
+        S = xb @ W1.t() + b1                     # cached first layer [R, H1]
+        base = tail(S)                           # [R]
+        for f0 in range(0, F, feat_chunk):
+            f1 = min(F, f0 + feat_chunk)
+            Z = S[:, None, :] - xb[:, f0:f1, None] * W1.t()[None, f0:f1, :]   # [R, fc, H1]
+            d = (base[:, None] - tail(Z)).double()
+            s_abs[f0:f1] += d.abs().sum(0)
+            s_sq[f0:f1] += (d * d).sum(0)
+        n += xb.shape[0]
+    mean = (s_abs / max(n, 1)).cpu().numpy()
+    rms = torch.sqrt(s_sq / max(n, 1)).cpu().numpy()
+    var = (s_sq / max(n, 1)).cpu().numpy() - mean ** 2
+    return mean, rms, var
+
+
+def select_by_sensitivity(ccs, input_cols, mean, rms, keep: int, by: str = "SE"):
+    """Keep the top ``keep`` inputs by RMS (SE) or mean (ST); force-selected always kept."""
+    order = np.argsort(-(rms if by.upper() == "SE" else mean), kind="stable")
+    keep_nums = {input_cols[i].num for i in order[:keep]}
+    for c in ccs:
+        if c.final_select and not c.is_force_select():
+            c.final_select = c.num in keep_nums
+    return [(input_cols[i].name, float(mean[i]), float(rms[i])) for i in order]

@@ -1,0 +1,174 @@
+"""Purify / tag / sample / weight (H6).
+
+* filter: ``DataPurifier.isFilter`` (J/core/DataPurifier.java:103-145) -> :mod:`.expr`
+* tags: pos/neg tag groups (``a|b`` = one class), invalid tags dropped
+  (``INVALID_TAG`` counter); multi-class = index into the tag list; linear target = float
+* sampling: ``DataSampler.isNotSampled`` (J/core/DataSampler.java:112-153), ``sampleNegOnly``
+* weight: column or JEXL expression (``NormalizeUDF.evaluateWeight`` J/udf/NormalizeUDF.java:640-661),
+  invalid -> 1.0
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..utils.log import get_logger
+from .expr import Evaluator
+from .reader import RawTable, read_header, read_table, first_line_is_header
+
+_log = get_logger("data.purifier")
+
+
+@dataclass
+class Counters:
+    """Hadoop-counter equivalents (SHIFU_GROUP_COUNTER)."""
+    total: int = 0
+    filtered_out: int = 0
+    invalid_tag: int = 0
+    not_sampled: int = 0
+    weight_exception: int = 0
+    valid: int = 0
+    pos: int = 0
+    neg: int = 0
+
+    def as_dict(self):
+        return dict(TOTAL_VALID_COUNT=self.valid, FILTER_OUT_COUNT=self.filtered_out, INVALID_TAG=self.invalid_tag,
+                    NOT_SAMPLED=self.not_sampled, WEIGHT_EXCEPTION=self.weight_exception, TOTAL=self.total,
+                    POSTAGS=self.pos, NEGTAGS=self.neg)
+
+
+@dataclass
+class ModelData:
+    table: RawTable
+    y: np.ndarray                # float32: binary 1/0, multi-class index, or regression target
+    w: np.ndarray                # float64 significance
+    tag_index: np.ndarray        # int32 class index (-1 linear)
+    counters: Counters = field(default_factory=Counters)
+
+    @property
+    def n(self):
+        return self.table.n
+
+
+def tag_index(values_str: np.ndarray, set_tags: list) -> np.ndarray:
+    lut = {}
+    for i, s in enumerate(set_tags):
+        for t in s:
+            lut[str(t).strip()] = i
+    return np.array([lut.get(str(v).strip(), -1) if v is not None else -1 for v in values_str], dtype=np.int32)
+
+
+def purify(mc, table: RawTable, target: str, weight_expr: str | None = None, filter_expr: str | None = None,
+           sample_rate: float = 1.0, sample_neg_only: bool = False, seed: int = 0,
+           require_target: bool = True) -> ModelData:
+    c = Counters(total=table.n)
+    keep = np.ones(table.n, dtype=bool)
+    if filter_expr and str(filter_expr).strip():
+        try:
+            m = Evaluator(filter_expr).mask(table)
+            c.filtered_out = int((~m).sum())
+            keep &= m
+        except Exception as e:  # reference logs and keeps the row on expression errors
+            _log.warning("filter expression %r failed (%s); no rows filtered", filter_expr, e)
+    # target / tags
+    ti = np.full(table.n, -1, dtype=np.int32)
+    if target in table.columns:
+        tcol = table[target]
+        if mc.is_linear_target():
+            y = tcol.numeric().astype(np.float64)
+            bad = np.isnan(y)
+            c.invalid_tag = int((bad & keep).sum())
+            if require_target:
+                keep &= ~bad
+            y = np.nan_to_num(y)
+        else:
+            ti = tag_index(tcol.strings(), mc.set_tags())
+            bad = ti < 0
+            c.invalid_tag = int((bad & keep).sum())
+            if require_target:
+                keep &= ~bad
+            if mc.is_binary():
+                npos = len(mc.pos_tags)
+                y = (ti < npos).astype(np.float64)   # pos tag groups come first in tags()
+                y[ti < 0] = 0
+            else:
+                y = ti.astype(np.float64)
+    else:
+        if require_target:
+            raise KeyError(f"target column {target!r} not in data header")
+        y = np.zeros(table.n)
+    # sampling
+    if sample_rate < 1.0:
+        rng = np.random.default_rng(seed)
+        r = rng.random(table.n)
+        if sample_neg_only and mc.is_binary():
+            drop = (y == 0) & (r > sample_rate)
+        else:
+            drop = r > sample_rate
+        c.not_sampled = int((drop & keep).sum())
+        keep &= ~drop
+    # weight
+    w = np.ones(table.n)
+    if weight_expr and str(weight_expr).strip():
+        we = str(weight_expr).strip()
+        if we in table.columns:
+            wv = table[we].numeric()
+        else:
+            try:
+                wv = Evaluator(we).values(table)
+            except Exception as e:
+                _log.warning("weight expression %r failed (%s); weight = 1", we, e)
+                wv = np.ones(table.n)
+        bad = ~np.isfinite(wv)
+        c.weight_exception = int((bad & keep).sum())
+        w = np.where(bad, 1.0, wv)
+    idx = np.nonzero(keep)[0]
+    c.valid = int(len(idx))
+    t = table.take(idx)
+    yk = y[idx].astype(np.float32)
+    if mc.is_binary():
+        c.pos = int((yk == 1).sum())
+        c.neg = int((yk == 0).sum())
+    return ModelData(t, yk, w[idx].astype(np.float64), ti[idx], c)
+
+
+def load_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=1.0, sample_neg_only=False,
+                 seed=0, require_target=True, extra_filter=None, max_rows=None) -> ModelData:
+    """Read + purify one data set section (``dataSet`` or an eval's ``dataSet``)."""
+    data_path = mc.resolve(data_conf.get("dataPath"))
+    delim = data_conf.get("dataDelimiter") or "|"
+    hpath = data_conf.get("headerPath")
+    header = read_header(mc.resolve(hpath) if hpath else None, data_conf.get("headerDelimiter") or "|",
+                         data_path, delim)
+    skip = (not hpath) and first_line_is_header(data_path, header, delim)
+    target = data_conf.get("targetColumnName") or mc.dataSet.get("targetColumnName")
+    weight = data_conf.get("weightColumnName")
+    filt = data_conf.get("filterExpressions")
+    if extra_filter:
+        filt = f"({filt}) && ({extra_filter})" if filt else extra_filter
+    strs = set(columns_str or [])
+    nums = set(columns_num or [])
+    if target:
+        strs.add(target)
+        nums.discard(target)
+    needed_expr = []
+    for e in (filt, weight):
+        if e and str(e).strip():
+            try:
+                needed_expr += Evaluator(str(e)).columns()
+            except Exception:
+                pass
+    from ..config.updater import simple_name
+    hmap = {simple_name(h): h for h in header}
+    for nm in needed_expr:
+        h = nm if nm in header else hmap.get(simple_name(nm))
+        if h and h not in nums:
+            strs.add(h)
+    if weight and weight in header:
+        nums.add(weight)
+        strs.discard(weight)
+    table = read_table(data_path, header, delim, numeric=[h for h in header if h in nums],
+                       strings=[h for h in header if h in strs], missing=mc.missing_values,
+                       skip_header_line=skip, max_rows=max_rows)
+    return purify(mc, table, target, weight, filt, sample_rate, sample_neg_only, seed, require_target)

@@ -1,0 +1,275 @@
+"""Delimited data reader (L1, D2/D3/E3 replacement).
+
+* headers: ``headerPath`` (``.pig_header``), or the data file's first line when no header file
+  is given (``InitModelProcessor.initColumnConfigList`` J/core/processor/InitModelProcessor.java:424-502)
+* data: a file, a directory of part files (hidden ``.``/``_`` files skipped, ``.gz`` inflated),
+  or a glob (``ShifuFileUtils`` / ``PathFinder`` semantics)
+* parsing: the native multithreaded C++ parser (``runtime/csrc/csv_parser.cpp``) into a columnar
+  :class:`RawTable`; pure-Python fallback for environments without a toolchain.
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+import gzip
+import io
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..utils.log import get_logger
+
+_log = get_logger("data.reader")
+
+
+def read_column_name_file(path: str) -> list:
+    """Column-name files: one name per line, '#' comments, blank lines ignored; a line may hold
+    several names separated by ','."""
+    if not path or not os.path.isfile(path):
+        return []
+    out = []
+    with open(path, encoding="utf-8") as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            for n in line.split(","):
+                if n.strip():
+                    out.append(n.strip())
+    return out
+
+
+def list_data_files(path: str) -> list:
+    if path is None:
+        return []
+    if any(ch in path for ch in "*?[") and not os.path.exists(path):
+        files = sorted(glob.glob(path))
+    elif os.path.isdir(path):
+        files = sorted(os.path.join(path, f) for f in os.listdir(path)
+                       if not f.startswith(".") and not f.startswith("_"))
+        files = [f for f in files if os.path.isfile(f)]
+    elif os.path.isfile(path):
+        files = [path]
+    else:
+        files = []
+    return files
+
+
+def _read_bytes(path: str) -> bytes:
+    if path.endswith(".gz"):
+        with gzip.open(path, "rb") as f:
+            return f.read()
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def read_header(header_path: str | None, header_delim: str = "|", data_path: str | None = None,
+                data_delim: str = "|") -> list:
+    if header_path:
+        files = list_data_files(header_path)
+        if files:
+            raw = _read_bytes(files[0]).decode("utf-8", errors="replace")
+            line = next((l for l in raw.splitlines() if l.strip()), "")
+            return [h.strip() for h in line.split(header_delim or "|")]
+    files = list_data_files(data_path)
+    if not files:
+        raise FileNotFoundError(f"no header file and no data under {data_path}")
+    raw = _read_bytes(files[0]).decode("utf-8", errors="replace")
+    line = next((l for l in raw.splitlines() if l.strip()), "")
+    return [h.strip() for h in line.split(data_delim or "|")]
+
+
+@dataclass
+class Column:
+    name: str
+    kind: str                         # "num" | "str"
+    values: np.ndarray                # float64 (num, NaN = missing) | int32 codes (str, -1 = missing)
+    dictionary: list = field(default_factory=list)
+
+    def strings(self) -> np.ndarray:
+        if self.kind == "str":
+            d = np.array(self.dictionary + [""], dtype=object)
+            return d[np.where(self.values >= 0, self.values, len(self.dictionary))]
+        out = np.array([("" if v != v else _java_num_str(v)) for v in self.values], dtype=object)
+        return out
+
+    def numeric(self) -> np.ndarray:
+        if self.kind == "num":
+            return self.values
+        lut = np.full(len(self.dictionary) + 1, np.nan)
+        for i, s in enumerate(self.dictionary):
+            try:
+                lut[i] = float(s)
+            except ValueError:
+                pass
+        return lut[np.where(self.values >= 0, self.values, len(self.dictionary))]
+
+    def missing_mask(self) -> np.ndarray:
+        return np.isnan(self.values) if self.kind == "num" else self.values < 0
+
+
+def _java_num_str(v: float) -> str:
+    if v == int(v) and abs(v) < 1e15:
+        return str(int(v)) if False else repr(v)
+    return repr(v)
+
+
+@dataclass
+class RawTable:
+    header: list
+    columns: dict                     # name -> Column (only parsed columns)
+    n: int
+    bad_rows: int = 0
+
+    def __getitem__(self, name) -> Column:
+        return self.columns[name]
+
+    def __contains__(self, name):
+        return name in self.columns
+
+    def take(self, idx: np.ndarray) -> "RawTable":
+        cols = {k: Column(c.name, c.kind, c.values[idx], c.dictionary) for k, c in self.columns.items()}
+        return RawTable(self.header, cols, int(len(idx)) if idx.dtype != bool else int(idx.sum()), self.bad_rows)
+
+
+def _parse_native(data: bytes, delim: str, kinds: list, missing: list, nthreads: int):
+    from ..ops import _native
+    lib = _native.rt()
+    if lib is None:
+        return None
+    kinds_arr = (ctypes.c_int * len(kinds))(*kinds)
+    miss = "\n".join(missing).encode("utf-8")
+    buf = ctypes.create_string_buffer(data, len(data))
+    h = lib.shifu_csv_parse(ctypes.addressof(buf), len(data), delim.encode("utf-8"), len(kinds), kinds_arr,
+                            miss, nthreads)
+    if not h:
+        return None
+    try:
+        n = lib.shifu_csv_nrows(h)
+        bad = lib.shifu_csv_bad_rows(h)
+        out = {}
+        for ci, k in enumerate(kinds):
+            if k == 1:
+                a = np.empty(n, dtype=np.float64)
+                lib.shifu_csv_numeric(h, ci, a.ctypes.data)
+                out[ci] = ("num", a, [])
+            elif k == 2:
+                a = np.empty(n, dtype=np.int32)
+                lib.shifu_csv_codes(h, ci, a.ctypes.data)
+                need = lib.shifu_csv_dict(h, ci, None, 0)
+                sz = lib.shifu_csv_dict_size(h, ci)
+                if sz > 0:
+                    b = ctypes.create_string_buffer(max(1, need))
+                    lib.shifu_csv_dict(h, ci, b, need)
+                    d = b.raw[:need].decode("utf-8", errors="replace").split("\n")
+                else:
+                    d = []
+                out[ci] = ("str", a, d)
+        return n, bad, out
+    finally:
+        lib.shifu_csv_free(h)
+
+
+def _parse_python(data: bytes, delim: str, kinds: list, missing: list):
+    text = data.decode("utf-8", errors="replace")
+    lines = [l for l in text.split("\n") if l.strip()]
+    n = len(lines)
+    miss = set(m.strip() for m in missing)
+    cols = {ci: [] for ci, k in enumerate(kinds) if k}
+    bad = 0
+    for line in lines:
+        parts = line.split(delim)
+        if len(parts) != len(kinds):
+            bad += 1
+        for ci in cols:
+            v = parts[ci].strip() if ci < len(parts) else ""
+            cols[ci].append(v)
+    out = {}
+    for ci, vals in cols.items():
+        if kinds[ci] == 1:
+            a = np.empty(n)
+            for i, v in enumerate(vals):
+                if v in miss:
+                    a[i] = np.nan
+                    continue
+                try:
+                    a[i] = float(v.rstrip("dDfF")) if v else np.nan
+                except ValueError:
+                    a[i] = np.nan
+            out[ci] = ("num", a, [])
+        else:
+            d, codes = {}, np.empty(n, dtype=np.int32)
+            for i, v in enumerate(vals):
+                if v in miss:
+                    codes[i] = -1
+                else:
+                    codes[i] = d.setdefault(v, len(d))
+            out[ci] = ("str", codes, list(d.keys()))
+    return n, bad, out
+
+
+def read_table(data_path: str, header: list, delim: str = "|", numeric: list | None = None,
+               strings: list | None = None, missing: list | None = None, skip_header_line: bool = False,
+               nthreads: int | None = None, max_rows: int | None = None) -> RawTable:
+    """Parse every file under ``data_path`` into a columnar table.  ``numeric``/``strings``
+    are column names (others skipped); by default every column is parsed as a string."""
+    files = list_data_files(data_path)
+    if not files:
+        raise FileNotFoundError(f"no data under {data_path}")
+    idx = {h: i for i, h in enumerate(header)}
+    kinds = [0] * len(header)
+    for nm in numeric or []:
+        if nm in idx:
+            kinds[idx[nm]] = 1
+    for nm in (strings if strings is not None else ([] if numeric else header)):
+        if nm in idx:
+            kinds[idx[nm]] = 2
+    missing = list(missing) if missing is not None else ["", "?"]
+    nthreads = nthreads or min(16, os.cpu_count() or 4)
+    parts = []
+    for fi, f in enumerate(files):
+        data = _read_bytes(f)
+        if skip_header_line and fi == 0:
+            nl = data.find(b"\n")
+            data = data[nl + 1:] if nl >= 0 else b""
+        res = _parse_native(data, delim or "|", kinds, missing, nthreads)
+        if res is None:
+            res = _parse_python(data, delim or "|", kinds, missing)
+        parts.append(res)
+    n = sum(p[0] for p in parts)
+    bad = sum(p[1] for p in parts)
+    cols = {}
+    for ci, k in enumerate(kinds):
+        if not k:
+            continue
+        name = header[ci]
+        if k == 1:
+            vals = np.concatenate([p[2][ci][1] for p in parts]) if parts else np.empty(0)
+            cols[name] = Column(name, "num", vals)
+        else:
+            gdict, remapped = {}, []
+            for p in parts:
+                _, codes, d = p[2][ci]
+                lut = np.array([gdict.setdefault(s, len(gdict)) for s in d] + [-1], dtype=np.int32)
+                remapped.append(lut[np.where(codes >= 0, codes, len(d))])
+            cols[name] = Column(name, "str", np.concatenate(remapped) if remapped else np.empty(0, np.int32),
+                                list(gdict.keys()))
+    if max_rows is not None and n > max_rows:
+        for c in cols.values():
+            c.values = c.values[:max_rows]
+        n = max_rows
+    if bad:
+        _log.warning("%d rows under %s have a column count != %d (padded as missing)", bad, data_path,
+                     len(header))
+    return RawTable(header, cols, n, bad)
+
+
+def first_line_is_header(data_path: str, header: list, delim: str) -> bool:
+    """Data files that start with their own header line (no separate header file)."""
+    files = list_data_files(data_path)
+    if not files:
+        return False
+    raw = _read_bytes(files[0])[:65536].decode("utf-8", errors="replace")
+    line = next((l for l in raw.splitlines() if l.strip()), "")
+    return [h.strip() for h in line.split(delim)] == header

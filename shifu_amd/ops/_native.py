@@ -46,7 +46,17 @@ HIP_SIGNATURES = {
     "shifu_gbdt_residual": "pppp" "p" "li" "s",
 }
 
-RT_SIGNATURES = {}
+# host runtime: name -> (argsig, restype)
+RT_SIGNATURES = {
+    "shifu_csv_parse": ("plPipPi", "p"),
+    "shifu_csv_nrows": ("p", "l"),
+    "shifu_csv_bad_rows": ("p", "l"),
+    "shifu_csv_numeric": ("pip", "i"),
+    "shifu_csv_codes": ("pip", "i"),
+    "shifu_csv_dict": ("pipl", "l"),
+    "shifu_csv_dict_size": ("pi", "l"),
+    "shifu_csv_free": ("p", None),
+}
 
 
 class NativeUnavailable(RuntimeError):
@@ -59,8 +69,11 @@ def _bind(lib, sigs):
         if fn is None:
             raise NativeUnavailable(f"symbol {name} missing from {lib._name}; rebuild with "
                                     f"`python -m shifu_amd.build_native`")
+        res = "i"
+        if isinstance(sig, tuple):
+            sig, res = sig
         fn.argtypes = [_T[c] for c in sig]
-        fn.restype = ctypes.c_int
+        fn.restype = None if res is None else _T[res]
 
 
 def register_hip(sigs: dict):
@@ -87,16 +100,23 @@ def hip():
     return _hip
 
 
-def rt():
-    """The host C++ runtime library, or None if it is not built."""
+def rt(build_if_missing: bool = True):
+    """The host C++ runtime library (built on demand with g++, seconds), or None."""
     global _rt
     if _rt is not None:
         return _rt
     with _lock:
-        if _rt is None and RT_LIB.exists():
-            lib = ctypes.CDLL(str(RT_LIB))
-            _bind(lib, RT_SIGNATURES)
-            _rt = lib
+        if _rt is None:
+            if not RT_LIB.exists() and build_if_missing and os.environ.get("SHIFU_NO_RT_BUILD") != "1":
+                try:
+                    from ..build_native import build_rt
+                    build_rt()
+                except Exception:   # pragma: no cover - toolchain missing
+                    return None
+            if RT_LIB.exists():
+                lib = ctypes.CDLL(str(RT_LIB))
+                _bind(lib, RT_SIGNATURES)
+                _rt = lib
     return _rt
 
 

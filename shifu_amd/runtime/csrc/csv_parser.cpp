@@ -1,0 +1,290 @@
+// Multithreaded delimited-text parser (host runtime, C++17).
+//
+// Replaces the reference's per-record text parsing in the Pig loaders / Guagua record readers
+// (NNWorker.load J/core/dtrain/nn/NNWorker.java:56-269, DTWorker.load J/core/dtrain/dt/DTWorker.java:1099-1297,
+// UpdateBinningInfoMapper.map) with a one-pass columnar parse:
+//   * the buffer is split at line boundaries into T chunks parsed by T threads
+//   * numeric columns -> double (NaN for missing / unparseable, the reference's "invalid")
+//   * string columns  -> int32 dictionary codes (-1 = missing) + per-column dictionary
+// Output is column-major so each column becomes one contiguous array (columnar cache).
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#define SHIFU_RT_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+struct Parser {
+  const char* buf = nullptr;
+  size_t len = 0;
+  std::string delim;
+  int ncols = 0;
+  std::vector<int> kinds;                  // 0 skip, 1 numeric, 2 string
+  std::unordered_set<std::string> missing; // tokens treated as missing (trimmed)
+  int nthreads = 1;
+  // results
+  size_t nrows = 0;
+  std::vector<std::vector<double>> num;    // per numeric column
+  std::vector<std::vector<int32_t>> codes; // per string column
+  std::vector<std::vector<std::string>> dicts;
+  std::vector<int> num_idx, str_idx;       // column -> slot
+  int64_t bad_rows = 0;
+};
+
+inline std::string_view trim(std::string_view s) {
+  size_t a = 0, b = s.size();
+  while (a < b && (s[a] == ' ' || s[a] == '\t' || s[a] == '\r')) ++a;
+  while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t' || s[b - 1] == '\r')) --b;
+  return s.substr(a, b - a);
+}
+
+inline double parse_double(std::string_view s, bool& ok) {
+  ok = false;
+  if (s.empty()) return NAN;
+  char tmp[64];
+  if (s.size() >= sizeof(tmp)) return NAN;
+  memcpy(tmp, s.data(), s.size());
+  tmp[s.size()] = 0;
+  char* end = nullptr;
+  double v = strtod(tmp, &end);
+  if (end == tmp) return NAN;
+  while (*end == ' ' || *end == 'd' || *end == 'D' || *end == 'f' || *end == 'F') ++end;   // Java "1.0d"
+  if (*end != 0) return NAN;
+  ok = true;
+  return v;
+}
+
+struct Chunk {
+  size_t begin, end;           // byte range (line aligned)
+  std::vector<size_t> line_starts;
+  size_t row_offset = 0;
+  std::vector<std::unordered_map<std::string, int32_t>> local_dict;   // per string col
+  std::vector<std::vector<std::string>> local_list;
+};
+
+void split_lines(const Parser& P, Chunk& c) {
+  size_t i = c.begin;
+  while (i < c.end) {
+    size_t j = i;
+    while (j < c.end && P.buf[j] != '\n') ++j;
+    // skip blank lines
+    size_t k = i;
+    while (k < j && (P.buf[k] == ' ' || P.buf[k] == '\r' || P.buf[k] == '\t')) ++k;
+    if (k < j) c.line_starts.push_back(i);
+    i = j + 1;
+  }
+}
+
+void parse_chunk(Parser& P, Chunk& c, std::atomic<int64_t>& bad) {
+  const size_t nstr = P.str_idx.size();
+  c.local_dict.assign(P.ncols, {});
+  c.local_list.assign(P.ncols, {});
+  const size_t dl = P.delim.size();
+  for (size_t li = 0; li < c.line_starts.size(); ++li) {
+    const size_t r = c.row_offset + li;
+    size_t s = c.line_starts[li];
+    size_t e = s;
+    while (e < c.end && P.buf[e] != '\n') ++e;
+    int col = 0;
+    size_t fs = s;
+    auto emit = [&](size_t a, size_t b) {
+      if (col < P.ncols) {
+        const int k = P.kinds[col];
+        if (k != 0) {
+          std::string_view v = trim(std::string_view(P.buf + a, b - a));
+          const bool miss = P.missing.count(std::string(v)) > 0;
+          if (k == 1) {
+            bool ok = false;
+            double d = miss ? NAN : parse_double(v, ok);
+            P.num[P.num_idx[col]][r] = d;
+          } else {
+            int32_t code = -1;
+            if (!miss) {
+              auto& m = c.local_dict[col];
+              std::string key(v);
+              auto it = m.find(key);
+              if (it == m.end()) {
+                code = (int32_t)c.local_list[col].size();
+                m.emplace(key, code);
+                c.local_list[col].push_back(std::move(key));
+              } else {
+                code = it->second;
+              }
+            }
+            P.codes[P.str_idx[col]][r] = code;   // local code, remapped after merge
+          }
+        }
+      }
+      ++col;
+    };
+    for (size_t i = s; i + dl <= e;) {
+      if (P.buf[i] == P.delim[0] && (dl == 1 || memcmp(P.buf + i, P.delim.data(), dl) == 0)) {
+        emit(fs, i);
+        i += dl;
+        fs = i;
+      } else {
+        ++i;
+      }
+    }
+    emit(fs, e);
+    if (col != P.ncols) {
+      bad.fetch_add(1);
+      for (int cc = col; cc < P.ncols; ++cc) {   // short row: rest missing
+        if (P.kinds[cc] == 1) P.num[P.num_idx[cc]][r] = NAN;
+        else if (P.kinds[cc] == 2) P.codes[P.str_idx[cc]][r] = -1;
+      }
+    }
+  }
+  (void)nstr;
+}
+
+}  // namespace
+
+// Parse `buf` (len bytes).  kinds[ncols]: 0 skip, 1 numeric, 2 string.  missing: '\n'-joined
+// tokens.  Returns an opaque handle (nullptr on error); read results with the getters.
+SHIFU_RT_API void* shifu_csv_parse(const char* buf, long len, const char* delim, int ncols, const int* kinds,
+                                   const char* missing, int nthreads) {
+  auto* P = new Parser();
+  P->buf = buf;
+  P->len = (size_t)len;
+  P->delim = delim && *delim ? delim : "|";
+  P->ncols = ncols;
+  P->kinds.assign(kinds, kinds + ncols);
+  if (missing) {
+    std::string m(missing);
+    size_t a = 0;
+    while (true) {
+      size_t b = m.find('\n', a);
+      std::string tok = m.substr(a, b == std::string::npos ? std::string::npos : b - a);
+      P->missing.insert(std::string(trim(tok)));
+      if (b == std::string::npos) break;
+      a = b + 1;
+    }
+  }
+  P->nthreads = std::max(1, nthreads);
+  for (int c = 0; c < ncols; ++c) {
+    P->num_idx.push_back(-1);
+    P->str_idx.push_back(-1);
+  }
+  int nn = 0, ns = 0;
+  for (int c = 0; c < ncols; ++c) {
+    if (P->kinds[c] == 1) P->num_idx[c] = nn++;
+    else if (P->kinds[c] == 2) P->str_idx[c] = ns++;
+  }
+  // chunking at line boundaries
+  const int T = P->nthreads;
+  std::vector<Chunk> chunks(T);
+  size_t pos = 0;
+  for (int t = 0; t < T; ++t) {
+    size_t target = (P->len * (t + 1)) / T;
+    if (t == T - 1) target = P->len;
+    else {
+      while (target < P->len && buf[target] != '\n') ++target;
+      if (target < P->len) ++target;
+    }
+    chunks[t].begin = pos;
+    chunks[t].end = std::max(pos, target);
+    pos = chunks[t].end;
+  }
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { split_lines(*P, chunks[t]); });
+    for (auto& x : th) x.join();
+  }
+  size_t rows = 0;
+  for (auto& c : chunks) { c.row_offset = rows; rows += c.line_starts.size(); }
+  P->nrows = rows;
+  P->num.assign(nn, std::vector<double>(rows));
+  P->codes.assign(ns, std::vector<int32_t>(rows));
+  std::atomic<int64_t> bad{0};
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { parse_chunk(*P, chunks[t], bad); });
+    for (auto& x : th) x.join();
+  }
+  P->bad_rows = bad.load();
+  // merge dictionaries in chunk order (first-seen order across the file) and remap codes
+  P->dicts.assign(ns, {});
+  for (int c = 0; c < ncols; ++c) {
+    if (P->kinds[c] != 2) continue;
+    const int si = P->str_idx[c];
+    std::unordered_map<std::string, int32_t> global;
+    for (auto& ch : chunks) {
+      std::vector<int32_t> remap(ch.local_list[c].size());
+      for (size_t i = 0; i < ch.local_list[c].size(); ++i) {
+        const std::string& s = ch.local_list[c][i];
+        auto it = global.find(s);
+        if (it == global.end()) {
+          const int32_t g = (int32_t)P->dicts[si].size();
+          global.emplace(s, g);
+          P->dicts[si].push_back(s);
+          remap[i] = g;
+        } else {
+          remap[i] = it->second;
+        }
+      }
+      int32_t* codes = P->codes[si].data();
+      for (size_t li = 0; li < ch.line_starts.size(); ++li) {
+        const size_t r = ch.row_offset + li;
+        if (codes[r] >= 0) codes[r] = remap[codes[r]];
+      }
+    }
+  }
+  return P;
+}
+
+SHIFU_RT_API long shifu_csv_nrows(void* h) { return (long)((Parser*)h)->nrows; }
+SHIFU_RT_API long shifu_csv_bad_rows(void* h) { return (long)((Parser*)h)->bad_rows; }
+
+SHIFU_RT_API int shifu_csv_numeric(void* h, int col, double* out) {
+  auto* P = (Parser*)h;
+  if (col < 0 || col >= P->ncols || P->num_idx[col] < 0) return -1;
+  const auto& v = P->num[P->num_idx[col]];
+  memcpy(out, v.data(), v.size() * sizeof(double));
+  return 0;
+}
+
+SHIFU_RT_API int shifu_csv_codes(void* h, int col, int32_t* out) {
+  auto* P = (Parser*)h;
+  if (col < 0 || col >= P->ncols || P->str_idx[col] < 0) return -1;
+  const auto& v = P->codes[P->str_idx[col]];
+  memcpy(out, v.data(), v.size() * sizeof(int32_t));
+  return 0;
+}
+
+// dictionary of a string column serialized as '\n'-joined values; returns the byte size needed
+SHIFU_RT_API long shifu_csv_dict(void* h, int col, char* out, long cap) {
+  auto* P = (Parser*)h;
+  if (col < 0 || col >= P->ncols || P->str_idx[col] < 0) return -1;
+  const auto& d = P->dicts[P->str_idx[col]];
+  long need = 0;
+  for (size_t i = 0; i < d.size(); ++i) need += (long)d[i].size() + (i + 1 < d.size() ? 1 : 0);
+  if (out && cap >= need) {
+    long p = 0;
+    for (size_t i = 0; i < d.size(); ++i) {
+      memcpy(out + p, d[i].data(), d[i].size());
+      p += (long)d[i].size();
+      if (i + 1 < d.size()) out[p++] = '\n';
+    }
+  }
+  return need;
+}
+
+SHIFU_RT_API long shifu_csv_dict_size(void* h, int col) {
+  auto* P = (Parser*)h;
+  if (col < 0 || col >= P->ncols || P->str_idx[col] < 0) return -1;
+  return (long)P->dicts[P->str_idx[col]].size();
+}
+
+SHIFU_RT_API void shifu_csv_free(void* h) { delete (Parser*)h; }

@@ -1,0 +1,99 @@
+"""Config JSON round trips and model file formats against the reference's own fixtures
+(parity model: ModelConfigTest / ColumnConfig tests, IndependentNNModelTest, IndependentTreeModelTest)."""
+import os
+
+import numpy as np
+import pytest
+
+from shifu_amd.config import jsonio
+from shifu_amd.config.column_config import load_column_configs, save_column_configs
+from shifu_amd.config.model_config import ModelConfig, create_init_model_config
+from shifu_amd.formats import nn_format, tree_format
+
+CJ = "example/cancer-judgement/ModelStore/ModelSet1"
+
+
+def test_model_config_roundtrip_bytes(ref_resources, tmp_path):
+    p = os.path.join(ref_resources, CJ, "ModelConfig.json")
+    mc = ModelConfig.load(p)
+    assert mc.is_binary() and not mc.is_multiclass()
+    assert mc.algorithm == "NN"
+    out = tmp_path / "mc.json"
+    mc.save(str(out))
+    assert jsonio.load(p) == jsonio.load(str(out))
+    # a file we wrote ourselves round-trips byte for byte
+    out2 = tmp_path / "mc2.json"
+    ModelConfig.load(str(out)).save(str(out2))
+    assert out.read_text() == out2.read_text()
+
+
+def test_column_config_roundtrip_bytes(ref_resources, tmp_path):
+    p = os.path.join(ref_resources, CJ, "ColumnConfig.json")
+    ccs = load_column_configs(p)
+    assert len(ccs) > 30
+    assert sum(1 for c in ccs if c.is_target()) == 1
+    out = tmp_path / "cc.json"
+    save_column_configs(ccs, str(out))
+    a, b = jsonio.load(p), jsonio.load(str(out))
+
+    def subset(x, y):   # every field of the (older-version) fixture survives unchanged
+        if isinstance(x, dict):
+            return all(k in y and subset(v, y[k]) for k, v in x.items())
+        if isinstance(x, list):
+            return len(x) == len(y) and all(subset(u, v) for u, v in zip(x, y))
+        return x == y
+    assert subset(a, b)
+
+
+def test_jsonio_special_values():
+    d = {"a": float("nan"), "b": [1.0, 2.5], "c": [{"x": 1}], "d": None, "e": 1e-7}
+    s = jsonio.dumps(d)
+    back = jsonio.loads(s)
+    assert back["b"] == [1.0, 2.5] and back["c"][0]["x"] == 1 and back["d"] is None
+
+
+def test_init_model_config_defaults():
+    mc = create_init_model_config("demo", "GBT")
+    assert mc.algorithm == "GBT"
+    assert mc.param("TreeNum") is not None
+
+
+def test_encog_nn_fixture_and_roundtrip(ref_resources, tmp_path):
+    net = nn_format.read_encog(os.path.join(ref_resources, CJ, "models/model0.nn"))
+    assert net.sizes[0] == 30 and net.sizes[-1] == 1
+    x = np.random.default_rng(0).normal(size=(7, net.n_in))
+    y0 = net.forward(x)
+    assert np.all((y0 > 0) & (y0 < 1))
+    out = tmp_path / "m.nn"
+    nn_format.write_encog(net, str(out))
+    net2 = nn_format.read_encog(str(out))
+    np.testing.assert_allclose(net2.forward(x), y0, rtol=1e-12)
+
+
+def test_binary_nn_roundtrip(tmp_path):
+    rng = np.random.default_rng(1)
+    net = nn_format.NNNetwork([5, 4, 1], ["tanh", "sigmoid"],
+                              [rng.normal(size=(4, 6)), rng.normal(size=(1, 5))], {"k": "v"}, [0, 1, 2, 3, 4])
+    cs = [nn_format.NNColumnStats(i, f"c{i}", "N", 6.0, 0.1, 1.0, 0, 1, 0, 1, [float("-inf"), 0.0], [],
+                                  [0.1, 0.2, 0.3], [0.0, 0.1, 0.2], [0.0, 0.1, 0.2]) for i in range(5)]
+    p = tmp_path / "m.nn"
+    nn_format.write_binary_nn(str(p), "ZSCALE", cs, {i: i for i in range(5)}, [net])
+    assert nn_format.is_binary_nn(str(p))
+    d = nn_format.read_binary_nn(str(p))
+    assert d["norm_type"] == "ZSCALE" and len(d["column_stats"]) == 5
+    x = rng.normal(size=(3, 5))
+    np.testing.assert_allclose(d["networks"][0].forward(x), net.forward(x), rtol=1e-12)
+
+
+def test_gbt_fixture_read_and_roundtrip(ref_resources, tmp_path):
+    p = os.path.join(ref_resources, "example/readablespec/model0.gbt")
+    m = tree_format.read_tree_model(p)
+    assert m.algorithm.upper() == "GBT" and len(m.bags) == 1 and len(m.bags[0]) == 100
+    out = tmp_path / "m.gbt"
+    tree_format.write_tree_model(str(out), m)
+    m2 = tree_format.read_tree_model(str(out))
+    rng = np.random.default_rng(0)
+    x = {c: rng.normal(size=5) * 10 for c in m.names}
+    np.testing.assert_allclose(m.score(x, 5), m2.score(x, 5))
+    fi = tree_format.feature_importance(m)
+    assert abs(sum(fi.values()) - 1.0) < 1e-9

@@ -1,0 +1,153 @@
+"""Data reading / purifying / expressions and the stats, normalize, varsel algorithms
+(parity model: DataPurifierTest, JexlTest, BinningTest, NormalizerTest, VariableSelectorTest)."""
+import os
+
+import numpy as np
+import pytest
+
+from shifu_amd.algos import binning as B
+from shifu_amd.algos import normalize as N
+from shifu_amd.algos import varsel as V
+from shifu_amd.algos.stats import column_metrics, compute_column_stats, pearson_correlation
+from shifu_amd.config.column_config import load_column_configs
+from shifu_amd.config.model_config import ModelConfig
+from shifu_amd.data import reader as R
+from shifu_amd.data.expr import Evaluator
+from shifu_amd.data.purifier import load_dataset
+
+CJ = "example/cancer-judgement"
+
+
+@pytest.fixture
+def cancer(ref_resources):
+    root = os.path.join(ref_resources, CJ)
+    mc = ModelConfig.load(os.path.join(root, "ModelStore/ModelSet1/ModelConfig.json"))
+    mc.dataSet["dataPath"] = os.path.join(root, "DataStore/DataSet1")
+    mc.dataSet["headerPath"] = os.path.join(root, "DataStore/DataSet1/.pig_header")
+    ccs = load_column_configs(os.path.join(root, "ModelStore/ModelSet1/ColumnConfig.json"))
+    return mc, ccs
+
+
+def test_native_and_python_parsers_agree(tmp_path):
+    rows = ["a|1.5|x", "b||y", "a|?|", "c|3|x", "d|-2e3|z|extra"]
+    (tmp_path / "part-0").write_text("\n".join(rows) + "\n")
+    hdr = ["s", "n", "t"]
+    t = R.read_table(str(tmp_path), hdr, "|", numeric=["n"], strings=["s", "t"])
+    data = (tmp_path / "part-0").read_bytes()
+    n, bad, py = R._parse_python(data, "|", [2, 1, 2], ["", "?"])
+    assert t.n == n == 5
+    np.testing.assert_array_equal(np.isnan(t["n"].values), np.isnan(py[1][1]))
+    assert t["s"].strings().tolist() == ["a", "b", "a", "c", "d"]
+    assert t["n"].values[0] == 1.5 and t["n"].values[4] == -2000.0
+    assert t["t"].missing_mask().tolist() == [False, False, True, False, False]
+
+
+def test_expression_evaluator():
+    from shifu_amd.data.reader import Column, RawTable
+    cols = {"a": Column("a", "num", np.array([1.0, 2.0, np.nan, 4.0])),
+            "s": Column("s", "str", np.array([0, 1, -1, 0], np.int32), ["x", "yy"])}
+    t = RawTable(["a", "s"], cols, 4, 0)
+    assert Evaluator("a > 1.5 && s == 'x'").mask(t).tolist() == [False, False, False, True]
+    assert Evaluator("a * 2 + 1").values(t)[:2].tolist() == [3.0, 5.0]
+    assert Evaluator("s != 'yy'").mask(t).tolist()[1] is False
+    assert set(Evaluator("a > 1 || b < 2").columns()) == {"a", "b"}
+
+
+def test_load_and_purify_cancer(cancer):
+    mc, ccs = cancer
+    nums = [c.name for c in ccs if not c.is_target() and not c.is_categorical()]
+    md = load_dataset(mc, mc.dataSet, columns_num=nums)
+    assert md.n == 429
+    assert md.counters.pos + md.counters.neg == md.n
+    assert set(np.unique(md.y)) <= {0.0, 1.0}
+
+
+def test_equal_population_binning():
+    rng = np.random.default_rng(0)
+    v = rng.normal(size=10000)
+    b = B.equal_population_boundaries(v, 10)
+    assert b[0] == float("-inf") and len(b) == 10 and all(x < y for x, y in zip(b, b[1:]))
+    idx = B.bin_index_numeric(v, b)
+    counts = np.bincount(idx, minlength=10)
+    assert counts.min() > 900 and counts.max() < 1100
+    idx2 = B.bin_index_numeric(np.array([np.nan, -np.inf, np.inf]), b)
+    assert idx2.tolist() == [10, 0, 9]
+
+
+def test_column_metrics_ks_iv():
+    neg, pos = np.array([40., 30., 20., 10.]), np.array([10., 20., 30., 40.])
+    ks, iv, woe, bw = column_metrics(neg, pos)
+    assert abs(ks - 40.0) < 1e-9
+    p, n = pos / pos.sum(), neg / neg.sum()
+    assert abs(iv - ((n - p) * np.log((n + 1e-10) / (p + 1e-10))).sum()) < 1e-12
+
+
+def test_stats_and_normalize_cancer(cancer):
+    mc, ccs = cancer
+    nums = [c.name for c in ccs if not c.is_target() and not c.is_categorical()]
+    md = load_dataset(mc, mc.dataSet, columns_num=nums)
+    compute_column_stats(mc, ccs, md)
+    c = next(c for c in ccs if c.name == "column_5")
+    assert c.ks > 50 and c.iv > 5              # strongly predictive in this data set
+    assert sum(c.bin_count_pos) == md.counters.pos or mc.binning_method != "EqualTotal"
+    v = md.table["column_5"].numeric()
+    assert abs(c.mean - np.nanmean(v)) < 1e-9 * abs(c.mean)
+    for cc in ccs:
+        if not cc.is_target():
+            cc.final_select = True
+    X, names, _ = N.normalize_table(mc, ccs, md.table, norm_type="ZSCALE")
+    assert X.shape == (md.n, len(nums))
+    j = names.index("column_5")
+    cut = float(mc.normalize.get("stdDevCutOff", 6.0))
+    ref = np.clip(v, c.mean - cut * c.std_dev, c.mean + cut * c.std_dev)
+    np.testing.assert_allclose(X[:, j], (ref - c.mean) / c.std_dev, rtol=1e-5, atol=1e-6)
+    Xw, _, _ = N.normalize_table(mc, ccs, md.table, norm_type="WOE")
+    assert np.isin(np.round(Xw[:, j], 5), np.round(np.asarray(c.bin_count_woe, np.float32), 5)).all()
+    C, nb, is_cat = N.tree_bin_codes(ccs, md.table, [cc for cc in ccs if not cc.is_target()])
+    assert C.max() < nb.max() and (C >= 0).all()
+
+
+def test_varsel_filter_ks_iv_mix(cancer):
+    mc, ccs = cancer
+    mc.varSelect["filterNum"] = 5
+    for key in ("KS", "IV", "mix", "pareto"):
+        mc.varSelect["filterBy"] = key
+        V.select_by_filter(mc, ccs)
+        sel = [c for c in ccs if c.final_select]
+        assert len(sel) == 5, key
+        if key == "KS":
+            top = sorted([c for c in ccs if not c.is_target() and c.ks is not None], key=lambda c: -c.ks)[:5]
+            assert {c.name for c in sel} == {c.name for c in top}
+
+
+def test_pareto_front_order():
+    pts = [(0, 1.0, 1.0), (1, 2.0, 0.5), (2, 0.5, 0.5), (3, 3.0, 3.0)]
+    order = [p[0] for p in V.pareto_sort(pts)]
+    assert order[0] == 3 and order[-1] == 2
+
+
+def test_pearson_pairwise_complete():
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(200, 3))
+    X[:, 1] = X[:, 0] * 2 + rng.normal(size=200) * 0.1
+    X[5, 0] = np.nan
+    C = pearson_correlation(X)
+    ok = np.isfinite(X[:, 0])
+    ref = np.corrcoef(X[ok][:, 0], X[ok][:, 1])[0, 1]
+    assert abs(C[0, 1] - ref) < 1e-9
+    assert abs(C[2, 2] - 1.0) < 1e-9
+
+
+def test_sensitivity_matches_bruteforce():
+    from shifu_amd.formats.nn_format import NNNetwork
+    rng = np.random.default_rng(0)
+    net = NNNetwork([6, 5, 1], ["tanh", "sigmoid"], [rng.normal(size=(5, 7)), rng.normal(size=(1, 6))])
+    X = rng.normal(size=(50, 6)).astype(np.float32)
+    mean, rms, _ = V.sensitivity(net, X, feat_chunk=4, row_chunk=16)
+    base = net.forward(X)[:, 0]
+    for i in range(6):
+        Z = X.astype(np.float64).copy()
+        Z[:, i] = 0
+        d = base - net.forward(Z)[:, 0]
+        assert abs(np.abs(d).mean() - mean[i]) < 1e-5
+        assert abs(np.sqrt((d * d).mean()) - rms[i]) < 1e-5
