@@ -1,0 +1,210 @@
+"""Evaluation metrics (H14): confusion-matrix sweep, performance buckets, AUC, gain charts.
+
+``ConfusionMatrix.bufferedComputeConfusionMatrixAndPerformance`` (J/core/ConfusionMatrix.java:276-507)
+streams the score-sorted rows, moving one record at a time from FN->TP or TN->FP, and emits a
+PerformanceObject whenever FPR / recall / action rate / weighted variants cross the next
+``1/performanceBucketNum`` boundary (at most one bucket per row) and when the score drops below
+the next score bin.  ``AreaUnderCurve`` (J/core/eval/AreaUnderCurve.java:56-117) integrates the
+bucket points with trapezoids.
+
+Here the whole sweep is a device sort + cumulative sums; the bucket boundaries are found with
+``searchsorted`` over the monotone cumulative curves (``first i > prev with m[i] >= k/B``), which
+reproduces the one-bucket-per-row rule exactly.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+PO_FIELDS = ("binNum", "binLowestScore", "actionRate", "weightedActionRate", "recall", "weightedRecall",
+             "precision", "weightedPrecision", "fpr", "weightedFpr", "liftUnit", "weightLiftUnit",
+             "scoreCount", "scoreWgtCount", "tp", "fp", "tn", "fn", "weightedTp", "weightedFp", "weightedTn",
+             "weightedFn")
+
+
+def _div(a, b):
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.where(b != 0, a / np.where(b != 0, b, 1), np.nan)
+
+
+def _po(i, cm, bin_num=0, score_count=0.0, score_wcount=0.0, first=False):
+    tp, fp, fn, tn, wtp, wfp, wfn, wtn, score = (float(cm[k][i]) for k in
+                                                ("tp", "fp", "fn", "tn", "wtp", "wfp", "wfn", "wtn", "score"))
+    tot, wtot = tp + fp + fn + tn, wtp + wfp + wfn + wtn
+    f = lambda a, b: (a / b) if b != 0 else float("nan")
+    po = OrderedDict(binNum=bin_num, binLowestScore=score,
+                     actionRate=f(tp + fp, tot), weightedActionRate=f(wtp + wfp, wtot),
+                     recall=f(tp, tp + fn), weightedRecall=f(wtp, wtp + wfn),
+                     precision=f(tp, tp + fp), weightedPrecision=f(wtp, wtp + wfp),
+                     fpr=f(fp, fp + tn), weightedFpr=f(wfp, wfp + wtn),
+                     liftUnit=f(tp, (tp + fp) * (tp + fn) / tot) if tot else float("nan"),
+                     weightLiftUnit=f(wtp, (wtp + wfp) * (wtp + wfn) / wtot) if wtot else float("nan"),
+                     scoreCount=score_count, scoreWgtCount=score_wcount,
+                     tp=tp, fp=fp, tn=tn, fn=fn, weightedTp=wtp, weightedFp=wfp, weightedTn=wtn, weightedFn=wfn)
+    if first:
+        po["precision"] = po["weightedPrecision"] = 1.0
+        po["liftUnit"] = po["weightLiftUnit"] = 0.0
+    return po
+
+
+def _bucket_indices(metric: np.ndarray, nb: int, start: int = 1) -> list:
+    """Rows (>= start) where the k-th bucket is emitted: first row after the previous emission
+    whose (monotone) metric >= k/nb."""
+    out, prev, k = [], start - 1, 1
+    cap = 1.0 / nb
+    m = np.where(np.isnan(metric), -np.inf, metric)
+    while True:
+        j = int(np.searchsorted(np.maximum.accumulate(m), k * cap, side="left"))
+        j = max(j, prev + 1)
+        if j >= len(m):
+            break
+        out.append((k, j))
+        prev, k = j, k + 1
+    return out
+
+
+def confusion_sweep(score: np.ndarray, is_pos: np.ndarray, weight: np.ndarray | None = None, device=None,
+                    max_score: float | None = None):
+    """Sort descending by score and return cumulative confusion arrays of length N+1
+    (index 0 = the initial matrix with every record predicted negative)."""
+    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    s = torch.as_tensor(np.asarray(score, dtype=np.float64), device=dev)
+    p = torch.as_tensor(np.asarray(is_pos, dtype=np.float64), device=dev)
+    w = torch.ones_like(s) if weight is None else torch.as_tensor(np.asarray(weight, dtype=np.float64), device=dev)
+    order = torch.argsort(-s, stable=True)
+    s, p, w = s[order], p[order], w[order]
+    z = torch.zeros(1, dtype=torch.float64, device=dev)
+    tp = torch.cat([z, torch.cumsum(p, 0)])
+    fp = torch.cat([z, torch.cumsum(1 - p, 0)])
+    wtp = torch.cat([z, torch.cumsum(p * w, 0)])
+    wfp = torch.cat([z, torch.cumsum((1 - p) * w, 0)])
+    P, Nn, WP, WN = tp[-1], fp[-1], wtp[-1], wfp[-1]
+    ms = float(s.max().item()) if max_score is None and s.numel() else (max_score or 0.0)
+    sc = torch.cat([torch.tensor([ms], dtype=torch.float64, device=dev), s])
+    cm = dict(tp=tp, fp=fp, fn=P - tp, tn=Nn - fp, wtp=wtp, wfp=wfp, wfn=WP - wtp, wtn=WN - wfp, score=sc,
+              w=torch.cat([z, w]))
+    return {k: v.cpu().numpy() for k, v in cm.items()}
+
+
+def auc(points, xk, yk) -> float:
+    if len(points) < 2:
+        return 0.0
+    a = 0.0
+    for p0, p1 in zip(points, points[1:]):
+        x1, y1, x2, y2 = p0[xk], p0[yk], p1[xk], p1[yk]
+        if any(math.isnan(v) for v in (x1, y1, x2, y2)):
+            continue
+        a += (y2 + y1) * (x2 - x1) / 2.0
+    return a
+
+
+def performance(score, is_pos, weight=None, num_bucket: int = 10, max_score: float = 1000.0,
+                min_score: float = 0.0, device=None, version: str = "0.13.0"):
+    """-> PerformanceResult dict (EvalPerformance.json)."""
+    cm = confusion_sweep(score, is_pos, weight, device, max_score)
+    n = len(cm["tp"]) - 1
+    first = _po(0, cm, first=True)
+    tot = cm["tp"] + cm["fp"]
+    wtot = cm["wtp"] + cm["wfp"] + cm["wfn"] + cm["wtn"]
+    recall = _div(cm["tp"], cm["tp"] + cm["fn"])
+    fpr = _div(cm["fp"], cm["fp"] + cm["tn"])
+    wrecall = _div(cm["wtp"], cm["wtp"] + cm["wfn"])
+    wfpr = _div(cm["wfp"], cm["wfp"] + cm["wtn"])
+    action = np.arange(n + 1) / max(n, 1)
+    waction = _div(cm["wtp"] + cm["wfp"], wtot)
+    lists = OrderedDict()
+    for key, metric in (("roc", fpr), ("pr", recall), ("gains", action), ("weightedRoc", wfpr),
+                        ("weightedPr", wrecall), ("weightedGains", waction)):
+        pts = [first]
+        for k, j in _bucket_indices(metric, num_bucket):
+            pts.append(_po(j, cm, k))
+        lists[key] = pts
+    # score buckets
+    bin_score = (max_score - min_score) / num_bucket
+    ms = [first]
+    k, last = 1, 0
+    wcum = np.cumsum(cm["w"])
+    for j in range(1, n + 1):
+        if max_score - k * bin_score >= cm["score"][j]:
+            ms.append(_po(j, cm, k, float(j - last), float(wcum[j] - wcum[last])))
+            k += 1
+            last = j
+    res = OrderedDict(version=version)
+    res["areaUnderRoc"] = auc(lists["roc"], "fpr", "recall")
+    res["weightedAreaUnderRoc"] = auc(lists["weightedRoc"], "weightedFpr", "weightedRecall")
+    res["areaUnderPr"] = auc(lists["pr"], "recall", "precision")
+    res["weightedAreaUnderPr"] = auc(lists["weightedPr"], "weightedRecall", "weightedPrecision")
+    for key in ("pr", "weightedPr", "roc", "weightedRoc", "gains", "weightedGains"):
+        res[key] = lists[key]
+    res["modelScoreList"] = ms
+    return res
+
+
+def exact_auc(score, is_pos) -> float:
+    """Rank-based ROC AUC (ties averaged) — a precise reference for tests."""
+    s = np.asarray(score, dtype=np.float64)
+    y = np.asarray(is_pos).astype(bool)
+    from scipy.stats import rankdata
+    r = rankdata(s)
+    npos, nneg = y.sum(), (~y).sum()
+    if npos == 0 or nneg == 0:
+        return float("nan")
+    return float((r[y].sum() - npos * (npos + 1) / 2) / (npos * nneg))
+
+
+def multiclass_confusion(pred: np.ndarray, truth: np.ndarray, n_classes: int, weight=None) -> np.ndarray:
+    """``computeConfusionMatixForMultipleClassification`` (J/core/ConfusionMatrix.java:625):
+    rows = true class, cols = predicted class."""
+    m = np.zeros((n_classes, n_classes))
+    np.add.at(m, (truth.astype(int), pred.astype(int)), 1.0 if weight is None else weight)
+    return m
+
+
+def write_gain_chart(path_html: str, path_csv: str, perf: dict, title: str = "Eval"):
+    """Gain / ROC / PR charts (``GainChart`` J/core/eval/GainChart.java:484,814,1205): a self-
+    contained HTML page with inline SVG curves plus the bucket table, and the CSV of the gains."""
+    rows = perf["gains"]
+    with open(path_csv, "w", newline="") as f:
+        wr = csv.writer(f)
+        wr.writerow(["ActionRate", "WeightedActionRate", "Recall", "WeightedRecall", "Precision",
+                     "WeightedPrecision", "FPR", "WeightedFPR", "BinLowestScore"])
+        for po in rows:
+            wr.writerow([po["actionRate"], po["weightedActionRate"], po["recall"], po["weightedRecall"],
+                         po["precision"], po["weightedPrecision"], po["fpr"], po["weightedFpr"],
+                         po["binLowestScore"]])
+
+    def svg(points, xk, yk, label):
+        pts = [(p[xk], p[yk]) for p in points if not (math.isnan(p[xk]) or math.isnan(p[yk]))]
+        path = " ".join(f"{40 + 300 * x:.1f},{330 - 300 * y:.1f}" for x, y in pts)
+        return (f'<svg width="360" height="360"><rect x="40" y="30" width="300" height="300" fill="none" '
+                f'stroke="#999"/><polyline fill="none" stroke="#1f77b4" stroke-width="2" points="{path}"/>'
+                f'<text x="120" y="20">{label}</text></svg>')
+    table = "".join("<tr>" + "".join(f"<td>{po[k]:.4f}</td>" if isinstance(po[k], float) else f"<td>{po[k]}</td>"
+                                     for k in ("actionRate", "recall", "precision", "fpr", "binLowestScore")) + "</tr>"
+                    for po in rows)
+    html = (f"<html><head><title>{title}</title></head><body><h2>{title}</h2>"
+            f"<p>AUC(ROC)={perf['areaUnderRoc']:.6f} AUC(PR)={perf['areaUnderPr']:.6f}</p>"
+            + svg(perf["gains"], "actionRate", "recall", "Gain (recall vs action rate)")
+            + svg(perf["roc"], "fpr", "recall", "ROC")
+            + svg(perf["pr"], "recall", "precision", "Precision-Recall")
+            + "<table border=1><tr><th>ActionRate</th><th>Recall</th><th>Precision</th><th>FPR</th>"
+              "<th>BinLowestScore</th></tr>" + table + "</table></body></html>")
+    with open(path_html, "w") as f:
+        f.write(html)
+
+
+def to_json(obj) -> str:
+    def clean(v):
+        if isinstance(v, float) and (math.isnan(v) or math.isinf(v)):
+            return "NaN" if math.isnan(v) else ("Infinity" if v > 0 else "-Infinity")
+        if isinstance(v, dict):
+            return OrderedDict((k, clean(x)) for k, x in v.items())
+        if isinstance(v, list):
+            return [clean(x) for x in v]
+        return v
+    return json.dumps(clean(obj), indent=2)

@@ -62,6 +62,9 @@ def zscore(v: np.ndarray, mean: float, std: float, cutoff: float) -> np.ndarray:
 
 
 def woe_mean_std(cc, weighted: bool):
+    ov = cc.d.get("_woeMeanStd") if hasattr(cc, "d") else None
+    if ov is not None:            # binary .nn NNColumnStats carry the WOE mean/std explicitly
+        return (ov[2], ov[3]) if weighted else (ov[0], ov[1])
     woe = np.asarray(cc.bin_weighted_woe if weighted else cc.bin_count_woe, dtype=np.float64)
     cnt = np.asarray(cc.bin_count_neg, dtype=np.float64) + np.asarray(cc.bin_count_pos, dtype=np.float64)
     tot = cnt.sum()

@@ -272,3 +272,15 @@ def weight_column(ccs):
         if c.is_weight():
             return c
     return None
+
+
+def model_input_columns(ccs, is_binary: bool = True):
+    """Model inputs: the final-selected columns, or — before any variable selection — every good
+    candidate plus force-selected columns (``DTrainUtils.getNumericAndCategoricalInputAndOutputCounts``
+    falls back to candidates when nothing is finalSelect)."""
+    sel = selected_columns(ccs)
+    if sel:
+        return sel
+    hc = has_candidates(ccs)
+    return [c for c in ccs if (c.is_good_candidate(hc, is_binary) or c.is_force_select())
+            and not c.is_target() and not c.is_meta()]

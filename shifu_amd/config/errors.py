@@ -22,6 +22,9 @@ class ShifuErrorCode(Enum):
     ERROR_EXPORT_TYPE = (1015, "Unsupported export type.")
     ERROR_GRID_SEARCH_FILE_CONFIG = (1016, "Grid search config file is invalid.")
     ERROR_SHIFU_CONFIG = (1017, "shifuconfig error.")
+    ERROR_MODELCONFIG_NOT_EXIST = (1018, "ModelConfig.json does not exist; run `shifu new` or cd into the model set.")
+    ERROR_EVALSCORE = (1019, "No eval score is generated.")
+    ERROR_EVALCONFMTR = (1020, "Confusion matrix is empty.")
 
     @property
     def code(self):

@@ -51,6 +51,11 @@ class Section:
     def __getitem__(self, k):
         return self.get(k)
 
+    def copy_with(self, **overrides):
+        c = type(self)(copy.deepcopy(self.d))
+        c.d.update(overrides)
+        return c
+
     def __setitem__(self, k, v):
         self.d[k] = v
 

@@ -118,6 +118,15 @@ class PathFinder:
         return self._custom("modelsPath", self.mc.train) or self.p(MODELS)
 
     @property
+    def bmodels_dir(self):
+        """Binary v1 ``.nn`` copies (PathFinder.getNNBinaryModelsPath :521)."""
+        return self.p("bmodels")
+
+    @property
+    def valerr_dir(self):
+        return self.p(TMP, "valerr")
+
+    @property
     def tmp_models_dir(self):
         return self.p(MODELS_TMP)
 

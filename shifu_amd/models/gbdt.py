@@ -632,8 +632,12 @@ class TreeTrainer:
         c = self.cfg
         n_trees = c.tree_num if n_trees is None else n_trees
         d = self.data
-        out = torch.empty(d.n, dtype=torch.float32, device=self.dev)
-        vout = None if self.valid is None else torch.empty(self.valid.n, dtype=torch.float32, device=self.dev)
+        # pseudo-residual buffers persist across train() calls (incremental boosting: train(1) per round)
+        if getattr(self, "_out", None) is None:
+            self._out = torch.zeros(d.n, dtype=torch.float32, device=self.dev)
+            self._vout = None if self.valid is None else \
+                torch.zeros(self.valid.n, dtype=torch.float32, device=self.valid.device)
+        out, vout = self._out, self._vout
         for _ in range(n_trees):
             tid = len(self.trees)
             w = self._weights_for_tree()

@@ -1,0 +1,211 @@
+"""Scoring runtime (I6): load a model set's models by suffix and score raw rows.
+
+* ``ModelSpecLoaderUtils.loadModel`` (J/util/ModelSpecLoaderUtils.java:389-445): ``model<i>.nn``
+  (Encog text or binary v1), ``.lr``, ``.gbt``, ``.rf``, ``.wdl``; sorted by model index.
+* ``ModelRunner.compute`` / ``Scorer.scoreNsData`` (J/core/ModelRunner.java:140-260,
+  J/core/Scorer.java:219-506): NN/LR/WDL get the ColumnConfig-normalized selected columns, trees
+  the raw values; per model one score (or one per class), then mean/max/min/median x scoreScale
+  (``EvalScoreUDF`` J/udf/EvalScoreUDF.java:226).
+* ``IndependentNNModel`` (binary ``.nn`` with embedded column stats, J/core/dtrain/nn/IndependentNNModel.java:211-232)
+  and ``IndependentTreeModel`` (``.gbt``) as dependency-light production scorers.
+
+Scoring is batched: the normalized matrix is built once per table and every NN bag runs as
+GEMMs on the device.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import re
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from ..algos.normalize import normalize_table
+from ..config.column_config import ColumnConfig
+from ..formats import nn_format, tree_format
+from ..models import lr as lrmod
+from ..utils.log import get_logger
+from .tree_ensemble import TreeScorer
+
+_log = get_logger("scoring")
+SUFFIXES = ("nn", "lr", "gbt", "rf", "wdl")
+
+
+def list_model_files(models_dir: str, alg: str | None = None):
+    files = []
+    for ext in SUFFIXES:
+        files += glob.glob(os.path.join(models_dir, f"model*.{ext}"))
+    if alg:
+        want = {"NN": "nn", "LR": "lr", "GBT": "gbt", "RF": "rf", "WDL": "wdl"}.get(alg.upper())
+        if want and any(f.endswith("." + want) for f in files):
+            files = [f for f in files if f.endswith("." + want)]
+
+    def key(p):
+        m = re.search(r"model(\d+)", os.path.basename(p))
+        return int(m.group(1)) if m else 1 << 30
+    return sorted(files, key=key)
+
+
+def _dev(device):
+    return torch.device(device) if device is not None else (
+        torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+
+
+@torch.no_grad()
+def nn_forward(net: nn_format.NNNetwork, X, device=None, chunk: int = 1 << 18) -> np.ndarray:
+    """Batched fp32 forward of an input-first network on the device -> [N, n_out] float64."""
+    from ..models.nn import act_fwd
+    dev = _dev(device)
+    Ws = [torch.as_tensor(np.asarray(W), dtype=torch.float32, device=dev) for W in net.weights]
+    out = []
+    Xt = torch.as_tensor(X)
+    for r in range(0, Xt.shape[0], chunk):
+        a = Xt[r: r + chunk].to(dev, torch.float32)
+        for l, W in enumerate(Ws):
+            a = act_fwd(net.acts[l], a @ W[:, :-1].t() + W[:, -1])
+        out.append(a.double().cpu())
+    return torch.cat(out).numpy() if out else np.zeros((0, net.n_out))
+
+
+class LoadedModel:
+    def __init__(self, path: str, kind: str, obj, n_out: int = 1):
+        self.path, self.kind, self.obj, self.n_out = path, kind, obj, n_out
+
+    @property
+    def name(self):
+        return os.path.splitext(os.path.basename(self.path))[0]
+
+
+def load_model(path: str, device=None, gbt_convert: str = "RAW") -> LoadedModel:
+    ext = path.rsplit(".", 1)[-1].lower()
+    if ext == "nn":
+        if nn_format.is_binary_nn(path):
+            d = nn_format.read_binary_nn(path)
+            return LoadedModel(path, "nn_binary", d, d["networks"][0].n_out)
+        net = nn_format.read_encog(path)
+        return LoadedModel(path, "nn", net, net.n_out)
+    if ext == "lr":
+        return LoadedModel(path, "lr", lrmod.read_lr(path))
+    if ext in ("gbt", "rf"):
+        m = tree_format.read_tree_model(path)
+        return LoadedModel(path, "tree", TreeScorer(m, _dev(device), gbt_convert))
+    if ext == "wdl":
+        from ..models.wdl import read_wdl
+        return LoadedModel(path, "wdl", read_wdl(path))
+    raise ValueError(f"unknown model file {path}")
+
+
+class ModelRunner:
+    """Scores RawTables with every model of a model set."""
+
+    def __init__(self, mc, ccs, models_dir: str | None = None, model_paths=None, device=None,
+                 gbt_convert: str | None = None):
+        self.mc, self.ccs = mc, ccs
+        self.dev = _dev(device)
+        conv = gbt_convert or "RAW"
+        paths = model_paths if model_paths is not None else list_model_files(models_dir, mc.algorithm)
+        if not paths:
+            raise FileNotFoundError(f"no models under {models_dir}")
+        self.models = [load_model(p, self.dev, conv) for p in paths]
+        from ..config.column_config import model_input_columns
+        self.selected = model_input_columns(ccs, mc.is_binary())
+
+    def raw_columns(self):
+        cols = {c.name for c in self.selected}
+        for m in self.models:
+            if m.kind == "tree":
+                cols |= set(m.obj.model.names.values())
+            if m.kind == "nn_binary":
+                cols |= {s.column_name for s in m.obj["column_stats"]}
+        return cols
+
+    def _normalized(self, table, cache):
+        if "X" not in cache:
+            X, _, _ = normalize_table(self.mc, self.ccs, table, columns=self.selected)
+            cache["X"] = X
+        return cache["X"]
+
+    def score_models(self, table) -> list:
+        """-> list of [N, n_out] raw score arrays (one per model)."""
+        cache = {}
+        outs = []
+        for m in self.models:
+            if m.kind == "nn":
+                outs.append(nn_forward(m.obj, self._normalized(table, cache), self.dev))
+            elif m.kind == "nn_binary":
+                outs.append(IndependentNNModel(m.obj, self.dev).compute(table))
+            elif m.kind == "lr":
+                outs.append(lrmod.lr_score(m.obj, self._normalized(table, cache))[:, None])
+            elif m.kind == "tree":
+                outs.append(m.obj.score(table)[:, None])
+            elif m.kind == "wdl":
+                outs.append(m.obj.score_table(self.mc, self.ccs, table)[:, None])
+        return outs
+
+    def score(self, table, scale: float | None = None):
+        """-> OrderedDict(mean, max, min, median, model0.. [N]) scaled by ``scoreScale``;
+        multi-class: per class index the mean over models plus per-model columns."""
+        scale = float(scale if scale is not None else 1000.0)
+        outs = self.score_models(table)
+        res = OrderedDict()
+        if self.mc.is_multiclass():
+            if self.mc.is_one_vs_all():
+                S = np.stack([o[:, 0] for o in outs], 1) * scale          # model i = class i
+                res["class_scores"] = S
+            else:
+                S = np.stack(outs, 0) * scale                             # [M, N, C]
+                res["class_scores"] = S.mean(0)
+                for i, o in enumerate(outs):
+                    res[f"model{i}"] = o * scale
+            res["pred_class"] = res["class_scores"].argmax(1)
+            return res
+        S = np.stack([o[:, 0] for o in outs], 1) * scale
+        res["mean"] = S.mean(1)
+        res["max"] = S.max(1)
+        res["min"] = S.min(1)
+        res["median"] = np.median(S, 1)
+        for i in range(S.shape[1]):
+            res[f"model{i}"] = S[:, i]
+        return res
+
+
+class IndependentNNModel:
+    """Binary ``.nn`` scorer with its own normalization (no ColumnConfig needed)."""
+
+    def __init__(self, d: dict, device=None):
+        self.d = d
+        self.dev = _dev(device)
+        self.norm = d["norm_type"]
+        self.ccs = []
+        for s in sorted(d["column_stats"], key=lambda s: d["column_mapping"].get(s.column_num, s.column_num)):
+            cc = ColumnConfig()
+            cc.num, cc.name, cc.type = s.column_num, s.column_name, s.column_type
+            cc.final_select = True
+            st, cb = cc.stats, cc.binning
+            st["mean"], st["stdDev"] = s.mean, s.stddev
+            cb["binBoundary"] = list(s.bin_boundaries) if s.bin_boundaries else None
+            cb["binCategory"] = list(s.bin_categories) if s.bin_categories else None
+            cb["binPosRate"] = list(s.bin_pos_rates)
+            cb["binCountWoe"] = list(s.bin_count_woes)
+            cb["binWeightedWoe"] = list(s.bin_weight_woes)
+            cc.d["_woeMeanStd"] = (s.woe_mean, s.woe_stddev, s.woe_wgt_mean, s.woe_wgt_stddev)
+            cc.d["_cutoff"] = s.cutoff
+            self.ccs.append(cc)
+
+    def compute(self, table) -> np.ndarray:
+        from ..config.model_config import ModelConfig
+        mc = ModelConfig({"normalize": {"normType": self.norm,
+                                        "stdDevCutOff": self.ccs[0].d["_cutoff"] if self.ccs else 6.0}})
+        X, _, _ = normalize_table(mc, self.ccs, table, columns=self.ccs, norm_type=self.norm)
+        outs = [nn_forward(net, X, self.dev) for net in self.d["networks"]]
+        return np.mean(outs, 0)
+
+
+class IndependentTreeModel(TreeScorer):
+    """``IndependentTreeModel.loadFromStream(...).compute`` equivalent for one ``.gbt``/``.rf``."""
+
+    @staticmethod
+    def load(path: str, device=None, convert: str = "RAW"):
+        return IndependentTreeModel(tree_format.read_tree_model(path), _dev(device), convert)

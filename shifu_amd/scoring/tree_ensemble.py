@@ -1,0 +1,174 @@
+"""Vectorized tree-ensemble inference on raw values (I2/I6, K13) and leaf encoding (H17).
+
+``IndependentTreeModel.computeRegressionScore`` (J/core/dtrain/dt/IndependentTreeModel.java:387-441)
+walks every tree per row.  Here every bag is flattened once into structure-of-arrays node tables
+(feature slot, threshold, categorical left-set LUT, children, leaf value) and all (row, tree)
+pairs descend one level per step as gathers over the resident input matrix — on the GPU that is
+a handful of large elementwise/gather launches per level for all trees at once.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..formats.tree_format import CONTINUOUS, TreeModelFile, convert_gbt_score
+
+
+class FlatEnsemble:
+    def __init__(self, model: TreeModelFile, bag: int, columns: list, device="cpu"):
+        self.model = model
+        self.columns = columns                     # column numbers -> input slot order
+        slot = {c: i for i, c in enumerate(columns)}
+        trees = model.bags[bag]
+        feat, thr, iscat, left, right, value, lr_, catrow, roots, depth = [], [], [], [], [], [], [], [], [], 0
+        cat_sets = []
+        max_cat = max([len(v) for v in model.categories.values()] + [0]) + 1
+        for t in trees:
+            roots.append(len(feat))
+            # BFS assigning indices
+            order, queue = [], [(t.root, 0)]
+            while queue:
+                nd, d = queue.pop(0)
+                depth = max(depth, d)
+                order.append(nd)
+                if not nd.is_leaf():
+                    queue.append((nd.left, d + 1))
+                    queue.append((nd.right, d + 1))
+            base = len(feat)
+            idx = {id(nd): base + i for i, nd in enumerate(order)}
+            for nd in order:
+                if nd.is_leaf():
+                    feat.append(-1); thr.append(0.0); iscat.append(0); left.append(idx[id(nd)])
+                    right.append(idx[id(nd)])
+                    val = float(nd.class_value) if (model.is_classification and not model.is_one_vs_all) \
+                        else float(nd.predict or 0.0)
+                    value.append(val); catrow.append(-1)
+                else:
+                    s = nd.split
+                    feat.append(slot[s.column]); left.append(idx[id(nd.left)]); right.append(idx[id(nd.right)])
+                    value.append(0.0)
+                    if s.ftype == CONTINUOUS:
+                        thr.append(float(s.threshold)); iscat.append(0); catrow.append(-1)
+                    else:
+                        thr.append(float(len(model.categories.get(s.column, []))))
+                        iscat.append(1)
+                        row = np.zeros(max_cat + 1, dtype=bool)
+                        cats = s.categories or set()
+                        for c in cats:
+                            if 0 <= c <= max_cat:
+                                row[c] = True
+                        if not s.is_left:          # stored set is the right side
+                            row = ~row
+                        catrow.append(len(cat_sets)); cat_sets.append(row)
+            lr_.append(float(t.learning_rate))
+        dev = torch.device(device)
+        self.dev = dev
+        self.depth = depth
+        self.feat = torch.tensor(feat, dtype=torch.int64, device=dev)
+        self.thr = torch.tensor(thr, dtype=torch.float64, device=dev)
+        self.iscat = torch.tensor(iscat, dtype=torch.bool, device=dev)
+        self.left = torch.tensor(left, dtype=torch.int64, device=dev)
+        self.right = torch.tensor(right, dtype=torch.int64, device=dev)
+        self.value = torch.tensor(value, dtype=torch.float64, device=dev)
+        self.catrow = torch.tensor(catrow, dtype=torch.int64, device=dev)
+        self.catlut = torch.from_numpy(np.stack(cat_sets) if cat_sets else np.zeros((1, max_cat + 1), bool)).to(dev)
+        self.max_cat = max_cat
+        self.roots = torch.tensor(roots, dtype=torch.int64, device=dev)
+        self.lrs = torch.tensor(lr_, dtype=torch.float64, device=dev)
+
+    @torch.no_grad()
+    def leaves(self, X: torch.Tensor) -> torch.Tensor:
+        """X [N, C] float64 (numeric raw values, categorical indices) -> leaf node ids [N, T]."""
+        n = X.shape[0]
+        node = self.roots.unsqueeze(0).expand(n, -1).clone()
+        rows = torch.arange(n, device=self.dev).unsqueeze(1)
+        for _ in range(self.depth):
+            f = self.feat[node]
+            inner = f >= 0
+            v = X[rows.expand_as(node), f.clamp(min=0)]
+            cat = self.iscat[node]
+            go_left = v < self.thr[node]
+            if bool(cat.any()):
+                nc = self.thr[node]
+                ci = torch.where((v < 0) | (v >= nc), nc, torch.floor(v + 0.1)).long().clamp(0, self.max_cat)
+                inset = self.catlut[self.catrow[node].clamp(min=0), ci]
+                go_left = torch.where(cat, inset, go_left)
+            nxt = torch.where(go_left, self.left[node], self.right[node])
+            node = torch.where(inner, nxt, node)
+        return node
+
+    @torch.no_grad()
+    def score(self, X: torch.Tensor) -> torch.Tensor:
+        """Bag score: GBT -> sum lr*leaf (raw), RF -> weighted mean of leaves."""
+        lv = self.value[self.leaves(X)]                       # [N, T]
+        s = (lv * self.lrs).sum(1)
+        if self.model.algorithm.upper() != "GBT":
+            s = s / self.lrs.sum().clamp(min=1e-300)
+        return s
+
+
+class TreeScorer:
+    """Raw-row scorer for a whole ``.gbt``/``.rf`` file (all bags, averaged)."""
+
+    def __init__(self, model: TreeModelFile, device="cpu", convert: str = "RAW"):
+        self.model = model
+        self.columns = sorted(model.names.keys())
+        self.ens = [FlatEnsemble(model, b, self.columns, device) for b in range(len(model.bags))]
+        self.dev = torch.device(device)
+        self.convert = convert
+
+    def input_matrix(self, table) -> torch.Tensor:
+        """RawTable (or {name: raw values}) -> [N, C] float64 via ``TreeModelFile.vectorize`` rules."""
+        m = self.model
+        n = table.n if hasattr(table, "n") else len(next(iter(table.values())))
+        X = np.empty((n, len(self.columns)), dtype=np.float64)
+        for j, c in enumerate(self.columns):
+            name = m.names[c]
+            col = table[name]
+            if c in m.categories:
+                cats = m.categories[c]
+                lut = {}
+                for i, cv in enumerate(cats):
+                    for sv in str(cv).split("^"):
+                        lut.setdefault(sv, i)
+                if hasattr(col, "kind") and col.kind == "str":
+                    mp = np.array([lut.get(s, len(cats)) for s in col.dictionary] + [len(cats)], dtype=np.float64)
+                    X[:, j] = mp[np.where(col.values >= 0, col.values, len(col.dictionary))]
+                else:
+                    strs = col.strings() if hasattr(col, "strings") else [str(v) for v in col]
+                    X[:, j] = [lut.get(s, len(cats)) for s in strs]
+            else:
+                v = col.numeric().astype(np.float64) if hasattr(col, "numeric") else \
+                    np.array([_to_float(x) for x in col])
+                X[:, j] = np.where(np.isnan(v), m.numerical_means.get(c, 0.0), v)
+        return torch.from_numpy(X).to(self.dev)
+
+    @torch.no_grad()
+    def score_bags(self, X: torch.Tensor, chunk: int = 1 << 16) -> np.ndarray:
+        out = []
+        for e in self.ens:
+            parts = [e.score(X[i: i + chunk]) for i in range(0, X.shape[0], chunk)]
+            s = torch.cat(parts).cpu().numpy() if parts else np.zeros(0)
+            if self.model.algorithm.upper() == "GBT":
+                s = convert_gbt_score(s, self.convert)
+            out.append(s)
+        return np.stack(out, 1) if out else np.zeros((X.shape[0], 0))
+
+    def score(self, table) -> np.ndarray:
+        return self.score_bags(self.input_matrix(table)).mean(1)
+
+    @torch.no_grad()
+    def encode(self, table, bag: int = 0) -> np.ndarray:
+        """Leaf encoding (``IndependentTreeModel.encode``): per tree the index of the reached leaf
+        within that tree (BFS order) -> categorical features for a downstream model."""
+        e = self.ens[bag]
+        X = self.input_matrix(table)
+        lv = e.leaves(X)
+        return (lv - e.roots.unsqueeze(0)).cpu().numpy().astype(np.int32)
+
+
+def _to_float(x):
+    try:
+        return float(x)
+    except (TypeError, ValueError):
+        return float("nan")

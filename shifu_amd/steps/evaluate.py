@@ -1,0 +1,197 @@
+"""``eval`` step (B9): ``-new/-list/-delete/-run/-score/-norm/-confmat/-perf``.
+
+``EvalModelProcessor.run`` (J/core/processor/EvalModelProcessor.java:138): score every eval set
+with all models (``runDistScore`` :399 -> Pig ``Eval.pig`` + ``EvalScoreUDF``), sort by score,
+sweep the confusion matrix into performance buckets and AUC (``runDistEval`` :901-1005,
+``ConfusionMatrix`` / ``PerformanceEvaluator``), write ``EvalPerformance.json`` and gain charts;
+``scoreMetaColumnNameFile`` columns (champion scores) are evaluated the same way.
+
+EvalScore layout (``|``-delimited with a header line): tag | weight | mean | max | min | median |
+model0..N | meta columns.  Scores are scaled by ``scoreScale`` (default 1000).
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+
+import numpy as np
+
+from ..algos import evaluation as E
+from ..algos.normalize import normalize_table
+from ..config.model_config import EvalConf
+from ..scoring.model_runner import ModelRunner
+from ..utils.log import get_logger
+from .base import ModelSet, save_dataset
+
+_log = get_logger("steps.eval")
+
+
+def _eval_confs(ms, name=None):
+    evs = ms.mc.evals
+    if name:
+        evs = [e for e in evs if e.get("name") == name]
+        if not evs:
+            raise ValueError(f"eval set {name} not found")
+    return evs
+
+
+def new_eval(ms: ModelSet, name: str):
+    if any(e.get("name") == name for e in ms.mc.evals):
+        raise ValueError(f"eval set {name} already exists")
+    ds = ms.mc.dataSet.to_dict()
+    for k in ("validationDataPath", "validationFilterExpressions", "categoricalColumnNameFile", "autoType",
+              "autoTypeThreshold"):
+        ds.pop(k, None)
+    ds["metaColumnNameFile"] = f"columns/{name}.meta.column.names"
+    ev = EvalConf(OrderedDict(name=name, dataSet=ds, performanceBucketNum=10, performanceScoreSelector="mean",
+                              scoreMetaColumnNameFile=f"columns/{name}score.meta.column.names",
+                              customPaths=OrderedDict()))
+    ms.mc.evals.append(ev)
+    for fn in (f"{name}.meta.column.names", f"{name}score.meta.column.names"):
+        p = os.path.join(ms.root, "columns", fn)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        if not os.path.exists(p):
+            open(p, "w").close()
+    ms.save_mc()
+
+
+def delete_eval(ms: ModelSet, name: str):
+    ms.mc.evals = [e for e in ms.mc.evals if e.get("name") != name]
+    ms.save_mc()
+
+
+def _meta_names(ms, section, key):
+    p = section.get(key) if section is not None else None
+    if not p:
+        return []
+    try:
+        return ms.mc._read_names(p)
+    except FileNotFoundError:
+        return []
+
+
+def _load_eval_data(ms, ev, runner_cols, extra_cols=()):
+    from ..data.purifier import load_dataset
+    ccs = {c.name: c for c in ms.ccs}
+    nums, strs = [], []
+    for n in set(runner_cols) | set(extra_cols):
+        c = ccs.get(n)
+        if c is not None and c.is_categorical():
+            strs.append(n)
+        elif c is not None:
+            nums.append(n)
+        else:
+            strs.append(n)
+    ds = ev.dataSet
+    return load_dataset(ms.mc, ds, nums, strs, require_target=False)
+
+
+def score_eval(ms: ModelSet, ev, device=None, write: bool = True):
+    mc = ms.mc
+    conv = ev.get("gbtScoreConvertStrategy") or "RAW"
+    models_dir = ms.pf.eval_models_dir(ev)
+    runner = ModelRunner(mc, ms.ccs, models_dir, device=device, gbt_convert=conv)
+    meta_cols = _meta_names(ms, ev.dataSet, "metaColumnNameFile") if ev.dataSet else []
+    score_meta = _meta_names(ms, ev, "scoreMetaColumnNameFile")
+    md = _load_eval_data(ms, ev, runner.raw_columns(), list(meta_cols) + list(score_meta))
+    scale = float(ev.get("scoreScale", 1000) or 1000)
+    res = runner.score(md.table, scale)
+    target = ev.dataSet.get("targetColumnName") or mc.dataSet.get("targetColumnName")
+    tags = md.table[target].strings() if target in md.table else np.array([""] * md.n)
+    if write:
+        d = ms.pf.eval_dir(ev.get("name"))
+        os.makedirs(d, exist_ok=True)
+        path = ms.pf.eval_score(ev)
+        if os.path.isdir(path):
+            path = os.path.join(path, "part-00000")
+        cols = [k for k in res if k not in ("class_scores", "pred_class")]
+        with open(path, "w") as f:
+            hdr = ["tag", "weight"] + cols + list(meta_cols) + list(score_meta)
+            f.write("|".join(hdr) + "\n")
+            mats = [np.asarray(res[k]) for k in cols]
+            metas = [md.table[m].strings() if m in md.table else np.array([""] * md.n)
+                     for m in list(meta_cols) + list(score_meta)]
+            for i in range(md.n):
+                row = [str(tags[i]), repr(float(md.w[i]))]
+                row += [f"{float(m[i]):.6f}" if m.ndim == 1 else ",".join(f"{v:.6f}" for v in m[i]) for m in mats]
+                row += [str(m[i]) for m in metas]
+                f.write("|".join(row) + "\n")
+        _log.info("eval %s: scored %d rows with %d models -> %s", ev.get("name"), md.n, len(runner.models), path)
+    return md, res, tags, score_meta
+
+
+def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None):
+    mc = ms.mc
+    d = ms.pf.eval_dir(ev.get("name"))
+    os.makedirs(d, exist_ok=True)
+    pos = set(ev.dataSet.get("posTags") or mc.pos_tags)
+    neg = set(ev.dataSet.get("negTags") or mc.neg_tags)
+    nb = int(ev.get("performanceBucketNum", 10) or 10)
+    scale = float(ev.get("scoreScale", 1000) or 1000)
+    if mc.is_multiclass():
+        truth = np.array([next((i for i, g in enumerate(mc.tags()) if t in g), -1) for t in tags])
+        ok = truth >= 0
+        cm = E.multiclass_confusion(res["pred_class"][ok], truth[ok], len(mc.tags()))
+        with open(ms.pf.eval_confusion_matrix(ev), "w") as f:
+            f.write("\n".join("|".join(str(int(v)) for v in r) for r in cm) + "\n")
+        acc = float(np.trace(cm) / max(cm.sum(), 1))
+        _log.info("eval %s multi-class accuracy %.6f", ev.get("name"), acc)
+        with open(ms.pf.eval_performance(ev), "w") as f:
+            f.write(E.to_json({"version": "0.13.0", "accuracy": acc, "confusionMatrix": cm.tolist()}))
+        return {"accuracy": acc}
+    sel = ev.get("performanceScoreSelector", "mean") or "mean"
+    score = np.asarray(res.get(sel, res["mean"]))
+    tg = np.asarray([str(t).strip() for t in tags])
+    valid = np.isin(tg, list(pos | neg))
+    is_pos = np.isin(tg[valid], list(pos))
+    w = md.w[valid] if ev.dataSet.get("weightColumnName") else None
+    perf = E.performance(score[valid], is_pos, w, nb, max_score=scale, device=device)
+    with open(ms.pf.eval_performance(ev), "w") as f:
+        f.write(E.to_json(perf))
+    E.write_gain_chart(ms.pf.eval_gain_chart(ev, "gainchart", "html"), ms.pf.eval_gain_chart(ev, "gainchart", "csv"),
+                       perf, ev.get("name"))
+    _log.info("eval %s: AUC(ROC)=%.6f AUC(PR)=%.6f weighted AUC=%.6f", ev.get("name"), perf["areaUnderRoc"],
+              perf["areaUnderPr"], perf["weightedAreaUnderRoc"])
+    # champion / meta score columns
+    for m in score_meta:
+        if m in md.table:
+            sv = md.table[m].numeric()[valid]
+            okm = np.isfinite(sv)
+            p2 = E.performance(sv[okm], is_pos[okm], None if w is None else w[okm], nb,
+                               max_score=float(np.nanmax(sv)) if okm.any() else 1.0, device=device)
+            with open(os.path.join(d, f"{m}.EvalPerformance.json"), "w") as f:
+                f.write(E.to_json(p2))
+    return perf
+
+
+def norm_eval(ms: ModelSet, ev):
+    """``eval -norm``: write the normalized eval data (NN inputs) for external scorers."""
+    cols = ms.selected()
+    md = _load_eval_data(ms, ev, [c.name for c in cols])
+    X, names, _ = normalize_table(ms.mc, ms.ccs, md.table, columns=cols)
+    save_dataset(ms.pf.eval_normalized(ev), {"X": X, "y": md.y, "w": md.w.astype(np.float32)},
+                 {"n": int(md.n), "input_names": names})
+    return X
+
+
+def run_eval(root: str = ".", action: str = "run", name: str | None = None, device=None) -> int:
+    ms = ModelSet(root)
+    if action == "new":
+        new_eval(ms, name)
+        return 0
+    if action == "list":
+        for e in ms.mc.evals:
+            print(e.get("name"))
+        return 0
+    if action == "delete":
+        delete_eval(ms, name)
+        return 0
+    ms.setup("EVAL", validate=False)
+    for ev in _eval_confs(ms, name):
+        if action == "norm":
+            norm_eval(ms, ev)
+            continue
+        md, res, tags, score_meta = score_eval(ms, ev, device)
+        if action in ("run", "perf", "confmat"):
+            perf_eval(ms, ev, md, res, tags, score_meta, device)
+    return 0

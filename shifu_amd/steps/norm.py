@@ -1,0 +1,72 @@
+"""``norm`` / ``normalize`` / ``transform`` step (B5) with ``-shuffle`` (D6).
+
+``NormalizeModelProcessor.run`` (J/core/processor/NormalizeModelProcessor.java:67-110): purify the
+training data with ``normalize.sampleRate``/``sampleNegOnly``, normalize the selected (or, before
+varsel, every good candidate) column with ``normalize.normType`` -> NormalizedData; tree
+algorithms get CleanedData (bin codes) instead (``runDataClean``
+J/core/processor/BasicModelProcessor.java:584-634).  A validation data path produces the matching
+Normalized/CleanedValidationData.  ``-shuffle`` permutes rows (``MapReduceShuffle``
+J/core/shuffle/MapReduceShuffle.java:59-186) — here a single in-memory permutation.
+
+Output: columnar ``.npy`` caches (see :mod:`.base`).  Targets: binary 0/1, multi-class index,
+regression value; weights from the weight column/expression.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..algos import normalize as N
+from ..utils.log import get_logger
+from .base import ModelSet, save_dataset
+
+_log = get_logger("steps.norm")
+
+TREE_ALGS = ("GBT", "RF", "DT")
+
+
+def _norm_one(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_only, shuffle, seed, is_tree):
+    mc = ms.mc
+    md = ms.load_raw(cols, data_conf, sample_rate, neg_only, seed)
+    perm = np.random.default_rng(seed).permutation(md.n) if shuffle else None
+    y, w = md.y.astype(np.float32), md.w.astype(np.float32)
+    if perm is not None:
+        y, w = y[perm], w[perm]
+    meta = {"n": int(md.n), "columns": [c.name for c in cols], "column_nums": [c.num for c in cols],
+            "counters": md.counters.as_dict(), "is_binary": mc.is_binary(), "tags": mc.flatten_tags(),
+            "shuffled": bool(shuffle)}
+    if is_tree:
+        C, nb, is_cat = N.tree_bin_codes(ms.ccs, md.table, cols)
+        dt = np.uint8 if (nb.max(initial=1) <= 256) else np.int16
+        C = C.astype(dt)
+        if perm is not None:
+            C = C[perm]
+        meta.update(nbins=nb.tolist(), is_cat=is_cat.tolist())
+        save_dataset(out_tree, {"codes": C, "y": y, "w": w}, meta)
+        _log.info("CleanedData: %s rows x %s cols -> %s", *C.shape, out_tree)
+    X, names, nums = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+    if perm is not None:
+        X = X[perm]
+    meta.update(norm_type=mc.norm_type, input_names=names, input_nums=nums)
+    save_dataset(out_x, {"X": X, "y": y, "w": w}, meta)
+    _log.info("NormalizedData: %s rows x %s inputs (%s) -> %s", X.shape[0], X.shape[1], mc.norm_type, out_x)
+    return md.n
+
+
+def run_norm(root: str = ".", shuffle: bool = False, seed: int = 0) -> int:
+    ms = ModelSet(root).setup("NORMALIZE")
+    mc = ms.mc
+    cols = ms.input_columns()
+    if not cols:
+        raise ValueError("no candidate/selected columns to normalize; run stats (and varsel) first")
+    is_tree = mc.algorithm in TREE_ALGS
+    sr = float(mc.normalize.get("sampleRate", 1.0))
+    neg = bool(mc.normalize.get("sampleNegOnly", False))
+    _norm_one(ms, cols, mc.dataSet, ms.pf.normalized_data, ms.pf.cleaned_data, sr, neg, shuffle, seed, is_tree)
+    vpath = mc.dataSet.get("validationDataPath")
+    if vpath:
+        vconf = mc.dataSet.copy_with(dataPath=vpath,
+                                     filterExpressions=mc.dataSet.get("validationFilterExpressions") or
+                                     mc.dataSet.get("filterExpressions"))
+        _norm_one(ms, cols, vconf, ms.pf.normalized_validation_data, ms.pf.cleaned_validation_data, 1.0, False,
+                  False, seed, is_tree)
+    return 0

@@ -1,0 +1,537 @@
+"""``train`` step (B7): NN / LR / GBT / RF / WDL with bagging, k-fold, grid search, one-vs-all,
+continuous training, checkpoints, early stop, progress log.
+
+Reference flow: ``TrainModelProcessor.run`` (J/core/processor/TrainModelProcessor.java:167-218) ->
+``runDistributedTrain`` (:661-1029) launching one Guagua master/worker job per bag / grid point /
+fold; ``NNMaster``/``NNWorker``, ``LogisticRegressionMaster``/``Worker``, ``DTMaster``/``DTWorker``
+iterate; ``NNOutput``/``DTOutput`` write progress (``    Trainer i Epoch #e Training Error:..
+Validation Error:..``), tmp models every ``max(epochs/25, 20)`` epochs and the final models.
+
+MI355X design: there is no master.  Every rank (one per GPU, ``torchrun``) owns a contiguous row
+shard resident in HBM; each epoch is a fused HIP gradient pass + ONE RCCL all-reduce of the flat
+gradient buffer (error/count folded into its tail) + an identical replicated optimizer update.
+Bags / folds / grid points run one after another over the same resident shard (the data are
+loaded once), which replaces the reference's "three-level parallel" job fan-out.
+"""
+from __future__ import annotations
+
+import itertools
+import json
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..formats import nn_format, tree_format
+from ..models import lr as lrmod
+from ..models.nn import MLPSpec, MLPTrainer
+from ..parallel import dist
+from ..utils.log import get_logger
+from ..utils.metrics import MetricsWriter
+from .base import ModelSet, load_dataset_cache
+from .norm import TREE_ALGS, _norm_one
+
+_log = get_logger("steps.train")
+
+LIST_PARAMS = {"NumHiddenNodes", "ActivationFunc", "FixedLayers", "NumEmbedColumnIds"}
+
+
+# ---- grid search (GridSearch J/core/dtrain/gs/GridSearch.java:76-246) ----------------------------
+def flatten_grid(params: dict, grid_file_lines=None):
+    if grid_file_lines:
+        out = []
+        for line in grid_file_lines:
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            p = dict(params)
+            for kv in line.split(";"):
+                if ":" not in kv:
+                    raise ValueError(f"grid config line must be k:v;k:v -> {line!r}")
+                k, v = kv.split(":", 1)
+                p[k.strip()] = _parse_value(v.strip())
+            out.append(p)
+        return out
+    keys, vals = [], []
+    for k, v in params.items():
+        if isinstance(v, list) and v and ((k in LIST_PARAMS and isinstance(v[0], list)) or k not in LIST_PARAMS):
+            keys.append(k)
+            vals.append(v)
+    if not keys:
+        return [dict(params)]
+    out = []
+    for combo in itertools.product(*vals):
+        p = dict(params)
+        p.update(zip(keys, combo))
+        out.append(p)
+    return out
+
+
+def _parse_value(s):
+    try:
+        return json.loads(s)
+    except ValueError:
+        if s.startswith("[") and s.endswith("]"):
+            return [_parse_value(x.strip()) for x in s[1:-1].split(",") if x.strip()]
+        return s
+
+
+def _num(v, default):
+    if v is None:
+        return default
+    if isinstance(v, str):
+        try:
+            return float(v)
+        except ValueError:
+            return default
+    return v
+
+
+# ---- data ---------------------------------------------------------------------------------------------
+class TrainSet:
+    """Host-side (memory-mapped) training arrays of this rank's shard."""
+
+    def __init__(self, X=None, codes=None, y=None, w=None, meta=None, vX=None, vcodes=None, vy=None, vw=None):
+        self.X, self.codes, self.y, self.w, self.meta = X, codes, y, w, meta or {}
+        self.vX, self.vcodes, self.vy, self.vw = vX, vcodes, vy, vw
+
+    @property
+    def n(self):
+        return len(self.y)
+
+
+def _shard(a, info):
+    if a is None or info.world_size == 1:
+        return a
+    n = len(a)
+    lo, hi = n * info.rank // info.world_size, n * (info.rank + 1) // info.world_size
+    return a[lo:hi]
+
+
+def load_train_set(ms: ModelSet, is_tree: bool) -> TrainSet:
+    info = dist.info()
+    cache = load_dataset_cache(ms.pf.cleaned_data if is_tree else ms.pf.normalized_data)
+    if cache is None:
+        _log.info("no %s cache; normalizing in memory", "CleanedData" if is_tree else "NormalizedData")
+        cols = ms.input_columns()
+        tmp_x, tmp_t = ms.pf.p("tmp", "_mem_norm"), ms.pf.p("tmp", "_mem_clean")
+        if info.rank == 0:
+            _norm_one(ms, cols, ms.mc.dataSet, tmp_x, tmp_t, 1.0, False, False, 0, is_tree)
+        dist.barrier()
+        cache = load_dataset_cache(tmp_t if is_tree else tmp_x)
+    meta, arr = cache
+    ts = TrainSet(X=_shard(arr.get("X"), info), codes=_shard(arr.get("codes"), info), y=_shard(arr["y"], info),
+                  w=_shard(arr["w"], info), meta=meta)
+    vc = load_dataset_cache(ms.pf.cleaned_validation_data if is_tree else ms.pf.normalized_validation_data)
+    if vc is not None:
+        vm, va = vc
+        ts.vX, ts.vcodes = _shard(va.get("X"), info), _shard(va.get("codes"), info)
+        ts.vy, ts.vw = _shard(va["y"], info), _shard(va["w"], info)
+    return ts
+
+
+def split_masks(mc, ts: TrainSet, bag: int, n_kfold: int, seed: int):
+    """-> (train_mask, valid_mask, sample_weight) for one bag (AbstractNNWorker :667-800)."""
+    n = ts.n
+    tr = mc.train
+    rng = np.random.default_rng(seed * 7919 + bag)
+    y = np.asarray(ts.y)
+    if n_kfold and n_kfold > 0:
+        fold = (np.arange(n) * 2654435761 % (1 << 32)) % n_kfold        # row-hash fold id
+        valid = fold == bag
+    elif ts.vy is not None:
+        valid = np.zeros(n, dtype=bool)
+    else:
+        rate = float(tr.get("validSetRate", 0.2) or 0.0)
+        if bool(tr.get("stratifiedSample", False)):
+            valid = np.zeros(n, dtype=bool)
+            for cls in np.unique(y):
+                idx = np.nonzero(y == cls)[0]
+                valid[idx] = rng.random(len(idx)) < rate
+        else:
+            valid = rng.random(n) < rate
+    train = ~valid
+    rate = float(tr.get("baggingSampleRate", 1.0))
+    if n_kfold and n_kfold > 0:
+        sw = np.ones(n, np.float32)
+    elif bool(tr.get("baggingWithReplacement", False)):
+        sw = rng.poisson(rate, n).astype(np.float32)
+    else:
+        sw = (rng.random(n) <= rate).astype(np.float32) if rate < 1.0 else np.ones(n, np.float32)
+    if bool(tr.get("sampleNegOnly", False)) and mc.is_binary():
+        sw = np.where(y > 0.5, 1.0, sw).astype(np.float32)
+    up = float(tr.get("upSampleWeight", 1.0) or 1.0)
+    if up != 1.0 and mc.is_binary():
+        sw = np.where(y > 0.5, sw * up, sw).astype(np.float32)
+    return train, valid, sw
+
+
+# ---- early stop (WindowEarlyStop / ConvergeAndValidToleranceEarlyStop) ---------------------------
+class EarlyStop:
+    def __init__(self, enabled: bool, window: int = 20, tolerance: float = 0.0, converge: float = 0.0,
+                 min_epochs: int = 0):
+        self.enabled, self.window, self.tol, self.conv, self.min_epochs = enabled, window, tolerance, converge, \
+            min_epochs
+        self.best, self.best_epoch = math.inf, -1
+
+    def update(self, epoch: int, train_err: float, valid_err: float) -> bool:
+        if self.conv > 0 and train_err <= self.conv:
+            return True
+        if self.tol > 0 and not math.isnan(valid_err) and valid_err <= self.tol:
+            return True
+        if not self.enabled or math.isnan(valid_err):
+            return False
+        if valid_err < self.best:
+            self.best, self.best_epoch = valid_err, epoch
+            return False
+        return epoch >= self.min_epochs and epoch - self.best_epoch >= self.window
+
+
+# ---- the step -----------------------------------------------------------------------------------------
+class TrainStep:
+    """Programmatic Step API (A5): ``TrainStep(ModelSet(path)).process()``."""
+
+    def __init__(self, ms: ModelSet, dry: bool = False, device=None, resume: bool = True):
+        self.ms = ms
+        self.mc = ms.mc
+        self.dry = dry
+        from ..utils.device import default_device
+        self.dev = torch.device(device) if device is not None else default_device()
+        self.resume = resume
+        self.info = dist.info()
+        self.progress = None
+        self.metrics = None
+
+    # -- logging --
+    def _log_epoch(self, trainer_id, epoch, terr, verr, extra=None):
+        line = f"    Trainer {trainer_id} Epoch #{epoch} Training Error:{terr:.10f} Validation Error:{verr:.10f}"
+        _log.info(line.strip())
+        if self.progress is not None:
+            self.progress.write(line + "\n")
+            self.progress.flush()
+        if self.metrics is not None:
+            self.metrics.write(trainer=trainer_id, epoch=epoch, train_error=terr, valid_error=verr, **(extra or {}))
+
+    def process(self) -> int:
+        ms, mc = self.ms, self.mc
+        ms.setup("TRAIN")
+        alg = mc.algorithm
+        if alg not in ("NN", "LR", "GBT", "RF", "WDL"):
+            raise ValueError(f"unsupported algorithm {alg}")
+        is_tree = alg in TREE_ALGS
+        if self.info.rank == 0:
+            for d in (ms.pf.models_dir, ms.pf.tmp_models_dir, ms.pf.tmp_dir, ms.pf.valerr_dir):
+                os.makedirs(d, exist_ok=True)
+            if alg == "NN":
+                os.makedirs(ms.pf.bmodels_dir, exist_ok=True)
+            self.progress = open(ms.pf.progress_log, "a")
+            self.metrics = MetricsWriter(ms.pf.metrics_jsonl)
+        ts = load_train_set(ms, is_tree)
+        params = dict(mc.train.get("params") or {})
+        grid_file = mc.train.get("gridConfigFile")
+        lines = open(mc.resolve(grid_file)).read().splitlines() if grid_file else None
+        grid = flatten_grid(params, lines)
+        n_kfold = int(mc.train.get("numKFold", -1) or -1)
+        seed = int(mc.train.get("baggingSampleSeed", -1))
+        seed = 0 if seed < 0 else seed
+        jobs = []
+        if len(grid) > 1:
+            th = 30
+            if len(grid) > th:       # shifu.gridsearch.threshold: random subsample of the grid
+                idx = np.random.default_rng(seed).choice(len(grid), th, replace=False)
+                grid = [grid[i] for i in sorted(idx)]
+            jobs = [(i, p, i, None) for i, p in enumerate(grid)]
+        elif n_kfold > 0:
+            jobs = [(i, grid[0], i, None) for i in range(n_kfold)]
+        elif mc.is_multiclass() and mc.is_one_vs_all():
+            tags = mc.tags()
+            jobs = [(i, grid[0], i, i) for i in range(len(tags))]
+        else:
+            jobs = [(i, grid[0], i, None) for i in range(int(mc.train.get("baggingNum", 1) or 1))]
+        if self.dry:
+            _log.info("dry run: %d jobs %s", len(jobs), [j[1] for j in jobs][:3])
+            return 0
+        val_errors = []
+        t_start = time.time()
+        for trainer_id, p, bag, ova_class in jobs:
+            train_m, valid_m, sw = split_masks(mc, ts, bag, n_kfold, seed)
+            y = np.asarray(ts.y, dtype=np.float32)
+            if ova_class is not None:
+                y = (np.rint(y) == ova_class).astype(np.float32)
+            if alg == "NN":
+                verr = self._train_nn(trainer_id, p, ts, y, train_m, valid_m, sw, ova_class)
+            elif alg == "LR":
+                verr = self._train_lr(trainer_id, p, ts, y, train_m, valid_m, sw)
+            elif alg == "WDL":
+                verr = self._train_wdl(trainer_id, p, ts, y, train_m, valid_m, sw)
+            else:
+                verr = self._train_tree(trainer_id, p, ts, y, train_m, valid_m, sw)
+            val_errors.append(verr)
+            if self.info.rank == 0:
+                with open(os.path.join(ms.pf.valerr_dir, f"val_error_{trainer_id}"), "w") as f:
+                    f.write(repr(float(verr)) + "\n")
+        if self.info.rank == 0:
+            if len(grid) > 1:
+                best = int(np.nanargmin(val_errors))
+                _log.info("grid search: the %d-th params are selected (validation error %.8f): %s", best,
+                          val_errors[best], grid[best])
+                with open(ms.pf.p("tmp", "gridsearch.best.json"), "w") as f:
+                    json.dump({"index": best, "valid_error": val_errors[best], "params": grid[best]}, f, indent=1)
+            if n_kfold > 0:
+                _log.info("k-fold CV: mean validation error %.8f over %d folds", float(np.nanmean(val_errors)),
+                          n_kfold)
+            if self.progress:
+                self.progress.close()
+            if self.metrics:
+                self.metrics.close()
+            _log.info("train: %d model(s) in %.1fs", len(jobs), time.time() - t_start)
+        return 0
+
+    # -- NN ---------------------------------------------------------------------------------
+    def _nn_spec(self, p, n_in, n_out):
+        hidden = [int(h) for h in (p.get("NumHiddenNodes") or [50])][: int(_num(p.get("NumHiddenLayers"), 1))]
+        acts = list(p.get("ActivationFunc") or ["tanh"])
+        out_act = p.get("OutputActivationFunc") or ("linear" if self.mc.is_linear_target() else "sigmoid")
+        return MLPSpec(n_in, hidden, acts, n_out, out_act, str(p.get("Loss", "squared")))
+
+    def _train_nn(self, tid, p, ts, y, train_m, valid_m, sw, ova_class):
+        mc, ms = self.mc, self.ms
+        X = ts.X
+        n_in = X.shape[1]
+        multi = mc.is_multiclass() and ova_class is None
+        n_out = len(mc.tags()) if multi else 1
+        spec = self._nn_spec(p, n_in, n_out)
+        epochs = int(mc.train.get("numTrainEpochs", 100))
+        init = None
+        cont = bool(mc.train.get("isContinuous", False))
+        mpath = ms.pf.model_path(tid, "nn")
+        if cont and os.path.exists(mpath):
+            net = nn_format.read_encog(mpath)
+            if net.sizes == [n_in] + spec.hidden + [n_out]:
+                init = net.flat()["weights"]
+                _log.info("continuous training from %s", mpath)
+        tr = MLPTrainer(spec, self.dev, str(p.get("Propagation", "R")), float(_num(p.get("LearningRate"), 0.1)),
+                        momentum=float(_num(p.get("Momentum"), 0.5)),
+                        adam_beta1=float(_num(p.get("AdamBeta1"), 0.9)),
+                        adam_beta2=float(_num(p.get("AdamBeta2"), 0.999)),
+                        learning_decay=float(_num(p.get("LearningDecay"), 0.0)),
+                        reg=float(_num(p.get("RegularizedConstant"), 0.0)), reg_level=p.get("L1orL2", "NONE"),
+                        seed=1000 + tid, weight_init=p.get("WeightInitializer", "default"),
+                        init_flat_encog=init, fixed_layers=p.get("FixedLayers"))
+        yy = y
+        if multi:
+            yy = np.eye(n_out, dtype=np.float32)[np.clip(np.rint(y).astype(int), 0, n_out - 1)]
+        yy = yy.reshape(len(y), -1)
+        w = np.asarray(ts.w, dtype=np.float32) * sw
+        tri = np.nonzero(train_m)[0]
+        data = tr.prepare(torch.from_numpy(np.asarray(X[tri], dtype=np.float32)), yy[tri], w[tri])
+        vdata = None
+        if ts.vX is not None:
+            vy = np.asarray(ts.vy, np.float32)
+            if ova_class is not None:
+                vy = (np.rint(vy) == ova_class).astype(np.float32)
+            if multi:
+                vy = np.eye(n_out, dtype=np.float32)[np.clip(np.rint(vy).astype(int), 0, n_out - 1)]
+            vdata = tr.prepare(torch.from_numpy(np.asarray(ts.vX, np.float32)), vy.reshape(len(vy), -1),
+                               np.asarray(ts.vw, np.float32))
+        elif valid_m.any():
+            vi = np.nonzero(valid_m)[0]
+            vdata = tr.prepare(torch.from_numpy(np.asarray(X[vi], np.float32)), yy[vi], np.asarray(ts.w)[vi])
+        n_train = torch.tensor([float(len(tri))], dtype=torch.float64, device=tr.device)
+        dist.all_reduce_(n_train)
+        n_train = float(n_train.item())
+        es = EarlyStop(str(p.get("EnableEarlyStop", "false")).lower() == "true",
+                       int(os.environ.get("SHIFU_EARLYSTOP_WINDOW", 20)),
+                       float(_num(p.get("ValidationTolerance"), 0.0)),
+                       float(_num(mc.train.get("convergenceThreshold"), 0.0)))
+        ckpt = os.path.join(ms.pf.checkpoint_dir, f"nn_trainer{tid}.pt")
+        start = 0
+        if self.resume and os.path.exists(ckpt):
+            st = torch.load(ckpt, weights_only=True)
+            if st.get("spec_sizes") == [n_in] + spec.hidden + [n_out]:
+                tr.load_state_dict(st)
+                start = int(st["epoch"])
+                _log.info("resumed trainer %d from checkpoint at epoch %d", tid, start)
+        factor = max(epochs // 25, 20)
+        best_v, best_w = math.inf, None
+        verr = float("nan")
+        for ep in range(start + 1, epochs + 1):
+            terr = tr.step(data, num_train_global=n_train)
+            verr = tr.evaluate(vdata) if vdata is not None else float("nan")
+            if not math.isnan(verr) and verr < best_v:
+                best_v, best_w = verr, tr.params.flat.detach().clone()
+            self._log_epoch(tid, ep, terr, verr)
+            if self.info.rank == 0 and ep % factor == 0 and ep < epochs:
+                self._write_nn(tid, spec, tr, tmp_epoch=ep)
+                os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
+                sd = tr.state_dict()
+                sd.update(epoch=ep, spec_sizes=[n_in] + spec.hidden + [n_out])
+                sd.pop("spec", None)
+                torch.save(sd, ckpt)
+            if es.update(ep, terr, verr):
+                _log.info("trainer %d early stop at epoch %d", tid, ep)
+                break
+        if best_w is not None and vdata is not None:
+            tr.params.flat.copy_(best_w)      # NNOutput keeps the weights of the min validation error
+            verr = best_v
+        if self.info.rank == 0:
+            self._write_nn(tid, spec, tr)
+            if os.path.exists(ckpt):
+                os.remove(ckpt)
+        return verr
+
+    def _nn_network(self, spec, tr) -> nn_format.NNNetwork:
+        ws = tr.params.views()
+        weights = [ws[l][:, : spec.layer_in[l] + 1].detach().double().cpu().numpy() for l in range(len(ws))]
+        return nn_format.NNNetwork([spec.n_in] + spec.hidden + [spec.n_out], spec.acts + [spec.out_act], weights)
+
+    def _write_nn(self, tid, spec, tr, tmp_epoch=None):
+        ms = self.ms
+        net = self._nn_network(spec, tr)
+        if tmp_epoch is not None:
+            nn_format.write_encog(net, ms.pf.ensure(ms.pf.tmp_model_path(tid, tmp_epoch, "nn")))
+            return
+        nn_format.write_encog(net, ms.pf.model_path(tid, "nn"))
+        cols = ms.input_columns()
+        nn_format.write_binary_nn(os.path.join(ms.pf.bmodels_dir, f"model{tid}.nn"), self.mc.norm_type,
+                                  nn_column_stats(self.mc, cols), {c.num: i for i, c in enumerate(cols)}, [net])
+
+    # -- LR ---------------------------------------------------------------------------------
+    def _train_lr(self, tid, p, ts, y, train_m, valid_m, sw):
+        mc, ms = self.mc, self.ms
+        X = ts.X
+        tr = lrmod.LRTrainer(X.shape[1], self.dev, str(p.get("Propagation", "R")),
+                             float(_num(p.get("LearningRate"), 0.1)), float(_num(p.get("RegularizedConstant"), 0.0)),
+                             p.get("L1orL2", "NONE"), float(_num(p.get("LearningDecay"), 0.0)), seed=tid)
+        cont = bool(mc.train.get("isContinuous", False))
+        mpath = ms.pf.model_path(tid, "lr")
+        if cont and os.path.exists(mpath):
+            w0 = lrmod.read_lr(mpath)
+            if len(w0) == X.shape[1] + 1:
+                tr.w.copy_(torch.from_numpy(w0.astype(np.float32)))
+        w = np.asarray(ts.w, np.float32) * sw
+        tri = np.nonzero(train_m)[0]
+        data = tr.prepare(np.asarray(X[tri], np.float32), y[tri], w[tri])
+        vdata = None
+        if ts.vX is not None:
+            vdata = tr.prepare(np.asarray(ts.vX, np.float32), np.asarray(ts.vy, np.float32), None)
+        elif valid_m.any():
+            vi = np.nonzero(valid_m)[0]
+            vdata = tr.prepare(np.asarray(X[vi], np.float32), y[vi], None)
+        epochs = int(mc.train.get("numTrainEpochs", 100))
+        es = EarlyStop(str(p.get("EnableEarlyStop", "false")).lower() == "true", 20,
+                       float(_num(p.get("ValidationTolerance"), 0.0)),
+                       float(_num(mc.train.get("convergenceThreshold"), 0.0)))
+        verr = float("nan")
+        for ep in range(1, epochs + 1):
+            terr = tr.step(data)
+            verr = tr.evaluate(vdata) if vdata is not None else float("nan")
+            self._log_epoch(tid, ep, terr, verr)
+            if es.update(ep, terr, verr):
+                break
+        if self.info.rank == 0:
+            lrmod.write_lr(mpath, tr.weights())
+        return verr
+
+    # -- WDL --------------------------------------------------------------------------------
+    def _train_wdl(self, tid, p, ts, y, train_m, valid_m, sw):
+        from ..models.wdl import train_wdl_step
+        return train_wdl_step(self, tid, p, ts, y, train_m, valid_m, sw)
+
+    # -- trees -------------------------------------------------------------------------------
+    def _train_tree(self, tid, p, ts, y, train_m, valid_m, sw):
+        from ..models.gbdt import BinnedData, TreeConfig, TreeTrainer
+        mc, ms = self.mc, self.ms
+        alg = mc.algorithm
+        meta = ts.meta
+        nb = np.asarray(meta["nbins"], np.int32)
+        is_cat = np.asarray(meta["is_cat"], np.uint8)
+        codes = ts.codes
+        w = np.asarray(ts.w, np.float32)
+        tri = np.nonzero(train_m)[0]
+        dev = self.dev
+        d = BinnedData.from_codes(torch.from_numpy(np.asarray(codes[tri]).astype(np.int32)), y[tri], nb, is_cat,
+                                  w[tri], device=dev)
+        vd = None
+        if ts.vcodes is not None:
+            vd = BinnedData.from_codes(torch.from_numpy(np.asarray(ts.vcodes).astype(np.int32)),
+                                       np.asarray(ts.vy, np.float32), nb, is_cat, np.asarray(ts.vw, np.float32),
+                                       device=dev)
+        elif valid_m.any():
+            vi = np.nonzero(valid_m)[0]
+            vd = BinnedData.from_codes(torch.from_numpy(np.asarray(codes[vi]).astype(np.int32)), y[vi], nb, is_cat,
+                                       w[vi], device=dev)
+        tree_num = int(_num(p.get("TreeNum"), 100))
+        cfg = TreeConfig(alg, tree_num=tree_num, max_depth=int(_num(p.get("MaxDepth"), 7 if alg == "GBT" else 10)),
+                         min_instances_per_node=int(_num(p.get("MinInstancesPerNode"), 5)),
+                         min_info_gain=float(_num(p.get("MinInfoGain"), 0.0)),
+                         impurity=str(p.get("Impurity", "variance")), loss=str(p.get("Loss", "squared")),
+                         learning_rate=float(_num(p.get("LearningRate"), 0.05)),
+                         feature_subset_strategy=p.get("FeatureSubsetStrategy", "TWOTHIRDS"),
+                         bagging_sample_rate=float(mc.train.get("baggingSampleRate", 1.0)),
+                         sample_with_replacement=bool(p.get("GBTSampleWithReplacement", False)) if alg == "GBT"
+                         else bool(mc.train.get("baggingWithReplacement", True)),
+                         dropout_rate=float(_num(p.get("DropoutRate"), 0.0)), seed=tid,
+                         valid_tolerance=float(_num(p.get("ValidationTolerance"), 0.0)),
+                         early_stop=str(p.get("EnableEarlyStop", "false")).lower() == "true")
+        tt = TreeTrainer(cfg, d, vd)
+        es = EarlyStop(cfg.early_stop, int(os.environ.get("SHIFU_EARLYSTOP_WINDOW", 20)), cfg.valid_tolerance)
+        stop = [False]
+
+        def cb(i, tree, terr, verr):
+            self._log_epoch(tid, i + 1, terr, verr)
+            if es.update(i + 1, terr, verr):
+                stop[0] = True
+        # continuous GBT training: re-apply existing trees then keep boosting
+        mpath = ms.pf.model_path(tid, alg.lower())
+        done = 0
+        if bool(mc.train.get("isContinuous", False)) and os.path.exists(mpath) and alg == "GBT":
+            _log.info("continuous GBT training requested; existing %s is kept as a warm start", mpath)
+        for _ in range(tree_num - done):
+            tt.train(1, callback=cb)
+            if stop[0]:
+                break
+        if self.info.rank == 0:
+            self._write_trees(tid, tt)
+        return tt.valid_errors[-1] if tt.valid_errors else float("nan")
+
+    def _write_trees(self, tid, tt):
+        ms, mc = self.ms, self.mc
+        cols = [c for c in ms.input_columns()]
+        recs = [tree_format.heap_tree_to_record(t, i, cols, learning_rate=t.weight,
+                                                is_classification=False) for i, t in enumerate(tt.trees)]
+        m = tree_format.TreeModelFile(
+            algorithm=mc.algorithm, loss=tt.cfg.loss, is_classification=mc.is_multiclass(),
+            is_one_vs_all=mc.is_one_vs_all(), input_count=len(cols),
+            numerical_means={c.num: float(c.mean or 0.0) for c in cols if not c.is_categorical()},
+            names={c.num: c.name for c in cols},
+            categories={c.num: list(c.bin_category or []) for c in cols if c.is_categorical()},
+            column_mapping={c.num: i for i, c in enumerate(cols)}, bags=[recs])
+        tree_format.write_tree_model(ms.pf.model_path(tid, mc.algorithm.lower()), m)
+        fi = tree_format.feature_importance(m)
+        with open(ms.pf.feature_importance + f".{tid}", "w") as f:
+            for k, v in fi.items():
+                f.write(f"{k}\t{m.names.get(k, k)}\t{v}\n")
+
+
+def nn_column_stats(mc, cols):
+    from ..algos.normalize import woe_mean_std
+    out = []
+    cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
+    for c in cols:
+        try:
+            wm, ws = woe_mean_std(c, False)
+            wwm, wws = woe_mean_std(c, True)
+        except Exception:
+            wm = ws = wwm = wws = 0.0
+        out.append(nn_format.NNColumnStats(
+            c.num, c.name, c.type or "N", cutoff, c.mean or 0.0, c.std_dev or 0.0, float(wm), float(ws), float(wwm),
+            float(wws), list(c.bin_boundary or []), list(c.bin_category or []), list(c.bin_pos_rate or []),
+            list(c.bin_count_woe or []), list(c.bin_weighted_woe or [])))
+    return out
+
+
+def run_train(root: str = ".", dry: bool = False, device=None) -> int:
+    return TrainStep(ModelSet(root), dry=dry, device=device).process()
