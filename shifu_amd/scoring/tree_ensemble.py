@@ -21,19 +21,20 @@ class FlatEnsemble:
         slot = {c: i for i, c in enumerate(columns)}
         trees = model.bags[bag]
         feat, thr, iscat, left, right, value, lr_, catrow, roots, depth = [], [], [], [], [], [], [], [], [], 0
-        cat_sets = []
+        cat_sets, paths = [], []
         max_cat = max([len(v) for v in model.categories.values()] + [0]) + 1
         for t in trees:
             roots.append(len(feat))
             # BFS assigning indices
-            order, queue = [], [(t.root, 0)]
+            order, queue = [], [(t.root, 0, "")]
             while queue:
-                nd, d = queue.pop(0)
+                nd, d, path = queue.pop(0)
                 depth = max(depth, d)
                 order.append(nd)
+                paths.append(path)
                 if not nd.is_leaf():
-                    queue.append((nd.left, d + 1))
-                    queue.append((nd.right, d + 1))
+                    queue.append((nd.left, d + 1, path + "L"))
+                    queue.append((nd.right, d + 1, path + "R"))
             base = len(feat)
             idx = {id(nd): base + i for i, nd in enumerate(order)}
             for nd in order:
@@ -75,6 +76,7 @@ class FlatEnsemble:
         self.max_cat = max_cat
         self.roots = torch.tensor(roots, dtype=torch.int64, device=dev)
         self.lrs = torch.tensor(lr_, dtype=torch.float64, device=dev)
+        self.paths = np.array(paths, dtype=object)     # L/R path from the root of every node
 
     @torch.no_grad()
     def leaves(self, X: torch.Tensor) -> torch.Tensor:
@@ -158,13 +160,18 @@ class TreeScorer:
         return self.score_bags(self.input_matrix(table)).mean(1)
 
     @torch.no_grad()
-    def encode(self, table, bag: int = 0) -> np.ndarray:
-        """Leaf encoding (``IndependentTreeModel.encode``): per tree the index of the reached leaf
-        within that tree (BFS order) -> categorical features for a downstream model."""
-        e = self.ens[bag]
+    def encode(self, table, depth: int | None = None) -> np.ndarray:
+        """Leaf-path encoding (``IndependentTreeModel.encode`` J/core/dtrain/dt/IndependentTreeModel.java:272-350):
+        per tree the L/R path to the reached leaf, right-padded with "L" to ``depth`` characters
+        -> [N, total trees] strings usable as categorical features of a downstream model."""
         X = self.input_matrix(table)
-        lv = e.leaves(X)
-        return (lv - e.roots.unsqueeze(0)).cpu().numpy().astype(np.int32)
+        cols = []
+        for e in self.ens:
+            d = depth or max(1, e.depth)
+            leaf = e.leaves(X).cpu().numpy()
+            pad = np.vectorize(lambda p: (p + "L" * d)[:d], otypes=[object])
+            cols.append(pad(e.paths[leaf]))
+        return np.concatenate(cols, 1) if cols else np.zeros((X.shape[0], 0), dtype=object)
 
 
 def _to_float(x):

@@ -85,6 +85,15 @@ class ModelSet:
         from ..config.column_config import model_input_columns
         return model_input_columns(self.ccs, self.mc.is_binary())
 
+    def norm_columns(self):
+        """Columns written by ``norm``: every good candidate plus force/final-selected ones
+        (Normalize.pig keeps candidates so varsel may run after norm; train then picks the
+        final-selected subset from the cache)."""
+        from ..config.column_config import has_candidates
+        hc = has_candidates(self.ccs)
+        return [c for c in self.ccs if not c.is_target() and not c.is_meta() and
+                (c.final_select or c.is_force_select() or c.is_good_candidate(hc, self.mc.is_binary()))]
+
     def load_raw(self, columns, data_conf=None, sample_rate=1.0, sample_neg_only=False, seed=0,
                  extra_filter=None, require_target=True):
         from ..data.purifier import load_dataset

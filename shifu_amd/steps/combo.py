@@ -1,0 +1,192 @@
+"""``combo -new/-init/-run/-eval`` (B11, H16): stacking of sub-models.
+
+``ComboModelProcessor.run`` (J/core/processor/ComboModelProcessor.java:80, ``runComboModels``
+:278-356): N sub-model sets with different algorithms train on the same data; their scores are
+joined to the raw rows; an assemble model set force-selects the sub-model score columns and runs
+the normal pipeline (init, stats, norm, varsel, train).  ``-eval`` scores the eval sets with every
+sub-model and evaluates the assemble model on the joined rows.
+
+Layout (under the parent model set): ``ComboTrain.json``, ``<name>_<ALG>_<i>/`` sub model sets,
+``<name>_assemble/`` with ``data/`` (training rows + score columns) and ``evaldata/<eval>/``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+
+import numpy as np
+
+from ..config.model_config import ModelConfig, create_params_by_alg
+from ..data.reader import first_line_is_header, read_header, read_table
+from ..scoring.model_runner import ModelRunner
+from ..utils.log import get_logger
+from .base import ModelSet
+
+_log = get_logger("steps.combo")
+
+
+def combo_new(root: str, algs: str, assemble_alg: str | None = None):
+    ms = ModelSet(root)
+    parts = [a.strip().upper() for a in algs.split(",") if a.strip()]
+    if assemble_alg is None:
+        assemble_alg = parts[-1] if len(parts) > 1 else "LR"
+        parts = parts[:-1] if len(parts) > 1 else parts
+    cfg = {"subTrains": [{"modelName": f"{ms.mc.name}_{a}_{i}", "algorithm": a} for i, a in enumerate(parts)],
+           "assemble": {"modelName": f"{ms.mc.name}_assemble", "algorithm": assemble_alg.upper()}}
+    with open(ms.pf.combo_config, "w") as f:
+        json.dump(cfg, f, indent=2)
+    return cfg
+
+
+def _load_cfg(ms):
+    with open(ms.pf.combo_config) as f:
+        return json.load(f)
+
+
+def _sub_dir(ms, name):
+    return os.path.join(ms.root, name)
+
+
+def combo_init(root: str):
+    ms = ModelSet(root)
+    cfg = _load_cfg(ms)
+    for sub in cfg["subTrains"] + [cfg["assemble"]]:
+        d = _sub_dir(ms, sub["modelName"])
+        os.makedirs(os.path.join(d, "columns"), exist_ok=True)
+        mc = ModelConfig.load(ms.pf.model_config)
+        mc.basic["name"] = sub["modelName"]
+        mc.train["algorithm"] = sub["algorithm"]
+        mc.train["params"] = create_params_by_alg(sub["algorithm"])
+        for k in ("dataPath", "headerPath"):       # absolute paths: sub sets live one level down
+            if mc.dataSet.get(k):
+                mc.dataSet[k] = mc.resolve(mc.dataSet.get(k))
+        for key in ("metaColumnNameFile", "categoricalColumnNameFile"):
+            v = mc.dataSet.get(key)
+            if v and os.path.exists(mc.resolve(v)):
+                mc.dataSet[key] = mc.resolve(v)
+        for ev in mc.evals:
+            for k in ("dataPath", "headerPath"):
+                if ev.dataSet.get(k):
+                    ev.dataSet[k] = mc.resolve(ev.dataSet.get(k))
+        for key in ("forceSelectColumnNameFile", "forceRemoveColumnNameFile", "candidateColumnNameFile"):
+            v = mc.varSelect.get(key)
+            if v and os.path.exists(mc.resolve(v)):
+                mc.varSelect[key] = mc.resolve(v)
+        mc.save(os.path.join(d, "ModelConfig.json"))
+        if os.path.exists(ms.pf.column_config) and sub is not cfg["assemble"]:
+            shutil.copyfile(ms.pf.column_config, os.path.join(d, "ColumnConfig.json"))
+    return cfg
+
+
+def _pipeline(root, steps=("init", "stats", "norm", "varsel", "train"), skip_init_if_cc=True):
+    from .create import run_init
+    from .norm import run_norm
+    from .stats import run_stats
+    from .train import run_train
+    from .varsel import run_varsel
+    if "init" in steps and not (skip_init_if_cc and os.path.exists(os.path.join(root, "ColumnConfig.json"))):
+        run_init(root)
+    if "stats" in steps:
+        run_stats(root)
+    if "norm" in steps:
+        run_norm(root)
+    if "varsel" in steps:
+        run_varsel(root)
+    if "train" in steps:
+        run_train(root)
+
+
+def _score_rows(ms_sub: ModelSet, data_conf):
+    """Raw rows of a data set + this sub-model's mean score (x1000)."""
+    mc = ms_sub.mc
+    runner = ModelRunner(mc, ms_sub.ccs, ms_sub.pf.models_dir)
+    path = mc.resolve(data_conf.get("dataPath"))
+    delim = data_conf.get("dataDelimiter") or "|"
+    hp = data_conf.get("headerPath")
+    header = read_header(mc.resolve(hp) if hp else None, data_conf.get("headerDelimiter") or "|", path, delim)
+    skip = (not hp) and first_line_is_header(path, header, delim)
+    cats = {c.name for c in ms_sub.ccs if c.is_categorical()}
+    need = runner.raw_columns()
+    t = read_table(path, header, delim, numeric=[h for h in header if h in need and h not in cats],
+                   strings=[h for h in header if h not in need or h in cats], missing=mc.missing_values,
+                   skip_header_line=skip)
+    raw = read_table(path, header, delim, strings=header, missing=mc.missing_values, skip_header_line=skip)
+    return header, raw, runner.score(t, 1000.0)["mean"]
+
+
+def _write_joined(out_dir, header, raw, score_cols):
+    os.makedirs(out_dir, exist_ok=True)
+    names = list(header) + list(score_cols.keys())
+    with open(os.path.join(out_dir, ".pig_header"), "w") as f:
+        f.write("|".join(names) + "\n")
+    cols = [raw[h].strings() for h in header] + [np.char.mod("%.6f", v) for v in score_cols.values()]
+    with open(os.path.join(out_dir, "part-00000"), "w") as f:
+        for i in range(raw.n):
+            f.write("|".join(str(c[i]) for c in cols) + "\n")
+
+
+def combo_run(root: str):
+    ms = ModelSet(root)
+    cfg = _load_cfg(ms)
+    subs = []
+    for sub in cfg["subTrains"]:
+        d = _sub_dir(ms, sub["modelName"])
+        _log.info("combo: training sub model %s (%s)", sub["modelName"], sub["algorithm"])
+        _pipeline(d)
+        subs.append((sub["modelName"], ModelSet(d)))
+    scores, header, raw = {}, None, None
+    for name, sms in subs:
+        header, raw, s = _score_rows(sms, sms.mc.dataSet)
+        scores[f"{name}_score"] = s
+    asm = cfg["assemble"]
+    ad = _sub_dir(ms, asm["modelName"])
+    data_dir = os.path.join(ad, "data")
+    _write_joined(data_dir, header, raw, scores)
+    ams = ModelSet(ad)
+    ams.mc.dataSet["dataPath"] = data_dir
+    ams.mc.dataSet["headerPath"] = os.path.join(data_dir, ".pig_header")
+    fs = os.path.join(ad, "columns", "forceselect.column.names")
+    with open(fs, "w") as f:
+        f.write("\n".join(scores.keys()) + "\n")
+    ams.mc.varSelect["forceSelectColumnNameFile"] = fs
+    ams.mc.varSelect["forceEnable"] = True
+    ams.save_mc()
+    _pipeline(ad, skip_init_if_cc=False)
+    return 0
+
+
+def combo_eval(root: str):
+    from .evaluate import run_eval
+    ms = ModelSet(root)
+    cfg = _load_cfg(ms)
+    asm = cfg["assemble"]
+    ad = _sub_dir(ms, asm["modelName"])
+    ams = ModelSet(ad)
+    for ev in ams.mc.evals:
+        scores, header, raw = {}, None, None
+        for sub in cfg["subTrains"]:
+            sms = ModelSet(_sub_dir(ms, sub["modelName"]))
+            sev = [e for e in sms.mc.evals if e.get("name") == ev.get("name")][0]
+            header, raw, s = _score_rows(sms, sev.dataSet)
+            scores[f"{sub['modelName']}_score"] = s
+        out = os.path.join(ad, "evaldata", ev.get("name"))
+        _write_joined(out, header, raw, scores)
+        ev.dataSet["dataPath"] = out
+        ev.dataSet["headerPath"] = os.path.join(out, ".pig_header")
+    ams.save_mc()
+    return run_eval(ad)
+
+
+def run_combo(root=".", action="run", algs: str | None = None) -> int:
+    if action == "new":
+        combo_new(root, algs or "NN,LR")
+    elif action == "init":
+        combo_init(root)
+    elif action == "run":
+        combo_run(root)
+    elif action == "eval":
+        combo_eval(root)
+    else:
+        raise ValueError(f"unknown combo action {action}")
+    return 0

@@ -55,7 +55,7 @@ def _norm_one(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_o
 def run_norm(root: str = ".", shuffle: bool = False, seed: int = 0) -> int:
     ms = ModelSet(root).setup("NORMALIZE")
     mc = ms.mc
-    cols = ms.input_columns()
+    cols = ms.norm_columns()
     if not cols:
         raise ValueError("no candidate/selected columns to normalize; run stats (and varsel) first")
     is_tree = mc.algorithm in TREE_ALGS

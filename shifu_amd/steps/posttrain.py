@@ -1,0 +1,73 @@
+"""``posttrain`` step (B8, H15): per-bin average model score (``binAvgScore``) and feature importance.
+
+``PostTrainModelProcessor.run`` (J/core/processor/PostTrainModelProcessor.java:86-113) scores the
+training data with the ensemble (``PostTrainMapper.map`` J/core/posttrain/PostTrainMapper.java:183-256),
+averages the score per (column, bin) and stores it in ``columnBinning.binAvgScore``; tree models
+also get gain-based feature importance (``runMRFeatureImportanceJob`` :301).  Reason codes
+(``Reasoner`` J/core/Reasoner.java:40-184) rank a row's variables by how far their bin's average
+score is below the column's best bin.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..algos.normalize import _bin_num
+from ..formats import tree_format
+from ..scoring.model_runner import ModelRunner, list_model_files
+from ..utils.log import get_logger
+from .base import ModelSet
+
+_log = get_logger("steps.posttrain")
+
+
+def run_posttrain(root: str = ".", device=None) -> int:
+    ms = ModelSet(root).setup("POSTTRAIN", validate=False)
+    mc = ms.mc
+    runner = ModelRunner(mc, ms.ccs, ms.pf.models_dir, device=device)
+    cols = runner.selected
+    names = runner.raw_columns()
+    byname = {c.name: c for c in ms.ccs}
+    md = ms.load_raw([byname[n] for n in names if n in byname])
+    res = runner.score(md.table, 1000.0)
+    score = np.asarray(res["mean"] if "mean" in res else res["class_scores"].max(1))
+    for c in cols:
+        if c.name not in md.table:
+            continue
+        b = _bin_num(c, md.table[c.name])
+        nb = c.n_bins()                        # incl. the missing bin (last)
+        b = np.where(b < 0, nb - 1, np.minimum(b, nb - 1))
+        s = np.bincount(b, weights=score, minlength=nb)
+        n = np.bincount(b, minlength=nb)
+        c.binning["binAvgScore"] = [int(round(v)) for v in np.where(n > 0, s / np.maximum(n, 1), 0.0)]
+    ms.save_cc()
+    # feature importance for tree models
+    fi_all = {}
+    for p in list_model_files(ms.pf.models_dir):
+        if p.endswith((".gbt", ".rf")):
+            for k, v in tree_format.feature_importance(tree_format.read_tree_model(p)).items():
+                fi_all[k] = fi_all.get(k, 0.0) + v
+    if fi_all:
+        tot = sum(fi_all.values())
+        nm = {c.num: c.name for c in ms.ccs}
+        with open(ms.pf.feature_importance, "w") as f:
+            for k, v in sorted(fi_all.items(), key=lambda kv: -kv[1]):
+                f.write(f"{k}\t{nm.get(k, k)}\t{v / tot}\n")
+    _log.info("posttrain: binAvgScore for %d columns", len(cols))
+    return 0
+
+
+def reason_codes(ccs, table, top_k: int = 3):
+    """Per row the ``top_k`` variable names whose bin average score is furthest below the
+    column's maximum bin average score (Reasoner semantics)."""
+    cols = [c for c in ccs if c.final_select and c.bin_avg_score and c.name in table]
+    if not cols:
+        return [[] for _ in range(table.n)]
+    gaps = []
+    for c in cols:
+        avg = np.asarray(c.bin_avg_score, dtype=np.float64)
+        b = _bin_num(c, table[c.name])
+        b = np.where(b < 0, len(avg) - 1, np.minimum(b, len(avg) - 1))
+        gaps.append(avg.max() - avg[b])
+    G = np.stack(gaps, 1)
+    order = np.argsort(-G, axis=1, kind="stable")[:, :top_k]
+    return [[cols[j].name for j in row] for row in order]

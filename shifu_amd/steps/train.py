@@ -110,11 +110,40 @@ def _shard(a, info):
     return a[lo:hi]
 
 
+def _subset_cache(meta, arr, want, is_tree):
+    """Column subset of a Normalized/CleanedData cache for the model inputs ``want`` (column
+    nums in ColumnConfig order); None if some wanted column is missing from the cache."""
+    if is_tree:
+        nums = meta["column_nums"]
+        pos = {n: i for i, n in enumerate(nums)}
+        if any(n not in pos for n in want):
+            return None
+        idx = [pos[n] for n in want]
+        if idx == list(range(len(nums))):
+            return meta, arr
+        meta = dict(meta, column_nums=list(want), nbins=[meta["nbins"][i] for i in idx],
+                    is_cat=[meta["is_cat"][i] for i in idx])
+        return meta, dict(arr, codes=np.asarray(arr["codes"])[:, idx])
+    inums = meta["input_nums"]
+    have = set(inums)
+    if any(n not in have for n in want):
+        return None
+    wanted = set(want)
+    idx = [i for i, n in enumerate(inums) if n in wanted]
+    if len(idx) == len(inums):
+        return meta, arr
+    meta = dict(meta, input_nums=[inums[i] for i in idx], input_names=[meta["input_names"][i] for i in idx])
+    return meta, dict(arr, X=np.asarray(arr["X"])[:, idx])
+
+
 def load_train_set(ms: ModelSet, is_tree: bool) -> TrainSet:
     info = dist.info()
+    want = [c.num for c in ms.input_columns()]
     cache = load_dataset_cache(ms.pf.cleaned_data if is_tree else ms.pf.normalized_data)
+    if cache is not None:
+        cache = _subset_cache(*cache, want, is_tree)
     if cache is None:
-        _log.info("no %s cache; normalizing in memory", "CleanedData" if is_tree else "NormalizedData")
+        _log.info("no usable %s cache; normalizing in memory", "CleanedData" if is_tree else "NormalizedData")
         cols = ms.input_columns()
         tmp_x, tmp_t = ms.pf.p("tmp", "_mem_norm"), ms.pf.p("tmp", "_mem_clean")
         if info.rank == 0:
@@ -125,6 +154,8 @@ def load_train_set(ms: ModelSet, is_tree: bool) -> TrainSet:
     ts = TrainSet(X=_shard(arr.get("X"), info), codes=_shard(arr.get("codes"), info), y=_shard(arr["y"], info),
                   w=_shard(arr["w"], info), meta=meta)
     vc = load_dataset_cache(ms.pf.cleaned_validation_data if is_tree else ms.pf.normalized_validation_data)
+    if vc is not None:
+        vc = _subset_cache(*vc, want, is_tree)
     if vc is not None:
         vm, va = vc
         ts.vX, ts.vcodes = _shard(va.get("X"), info), _shard(va.get("codes"), info)

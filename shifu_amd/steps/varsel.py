@@ -1,0 +1,247 @@
+"""``varsel`` step (B6): filter KS/IV/mix/pareto, SE/ST sensitivity (``-r N`` recursive), FI for
+trees, voted GA wrapper, auto-filter with history, ``-reset/-list/-autofilter/-recoverauto``.
+
+``VarSelectModelProcessor.run`` (J/core/processor/VarSelectModelProcessor.java:121-281):
+* binary targets: ``filterBy`` in KS/IV/MIX/PARETO -> ``VariableSelector.selectByFilter``; FI ->
+  tree feature importance; SE/ST -> ``distributedSEWrapper`` (:633-674: train an NN on the
+  candidates, then ``VarSelectMapper`` sensitivity + ``VarSelectReducer`` top-by-RMS keeping
+  ``filterNum`` or ``inputs*(1-filterOutRatio)``); V (voted) -> ``votedVariablesSelection``
+  (:403-438, GA over subsets scored by small NN validation error).
+* multi-class: force-selected (if any) else every good candidate.
+* then ``autoVarSelCondition`` (:1008-1050) + correlation filter; changes are appended to
+  ``varsel/varsel.history`` so ``-recoverauto`` can undo them.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..algos import normalize as N
+from ..algos import varsel as V
+from ..config.column_config import has_candidates
+from ..formats.nn_format import NNNetwork
+from ..models.nn import MLPSpec, MLPTrainer
+from ..utils.log import get_logger
+from .base import ModelSet
+
+_log = get_logger("steps.varsel")
+
+
+def _good(ms):
+    hc = has_candidates(ms.ccs)
+    return [c for c in ms.ccs if c.is_good_candidate(hc, ms.mc.is_binary()) or c.is_force_select()]
+
+
+def _history_append(ms, changes, reason):
+    os.makedirs(ms.pf.varsel_dir, exist_ok=True)
+    with open(ms.pf.varsel_history, "a") as f:
+        for c, old, new in changes:
+            f.write(f"{c.num},{c.name},{str(old).lower()},{str(new).lower()},{reason}\n")
+
+
+def _train_quick_nn(ms, cols, epochs, device=None, seed=0):
+    """Train the NN used for sensitivity analysis on the candidate columns; returns (net, X)."""
+    mc = ms.mc
+    md = ms.load_raw(cols)
+    X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+    p = mc.train.get("params") or {}
+    hidden = [int(h) for h in (p.get("NumHiddenNodes") or [50])][: int(p.get("NumHiddenLayers", 1) or 1)]
+    spec = MLPSpec(X.shape[1], hidden, list(p.get("ActivationFunc") or ["tanh"]), 1, "sigmoid")
+    from ..utils.device import default_device
+    dev = torch.device(device) if device is not None else default_device()
+    tr = MLPTrainer(spec, dev, str(p.get("Propagation", "R")), float(p.get("LearningRate", 0.1)), seed=seed)
+    data = tr.prepare(torch.from_numpy(X), md.y.reshape(-1, 1), md.w.astype(np.float32))
+    for _ in range(max(1, epochs)):
+        tr.step(data)
+    ws = tr.params.views()
+    net = NNNetwork([spec.n_in] + spec.hidden + [1], spec.acts + ["sigmoid"],
+                    [ws[l][:, : spec.layer_in[l] + 1].detach().double().cpu().numpy() for l in range(len(ws))])
+    return net, X, md
+
+
+def select_by_sensitivity(ms, by="SE", device=None, seed=0):
+    mc = ms.mc
+    cols = _good(ms)
+    if not cols:
+        return []
+    epochs = max(1, int(mc.train.get("numTrainEpochs", 100)) // 2)
+    net, X, md = _train_quick_nn(ms, cols, epochs, device, seed)
+    mean, rms, var = V.sensitivity(net, X, device=device)
+    filter_num = int(mc.varSelect.get("filterNum", 200) or 0)
+    keep = filter_num if filter_num > 0 else int(len(cols) * (1 - float(mc.varSelect.get("filterOutRatio", 0.05))))
+    order = np.argsort(-rms, kind="stable")          # VarSelectReducer sorts by RMS for SE and ST
+    keep_nums = {cols[i].num for i in order[:keep]}
+    for c in ms.ccs:
+        c.final_select = (c.num in keep_nums) or c.is_force_select()
+    return [(cols[i].num, cols[i].name, float(mean[i]), float(rms[i]), float(var[i])) for i in order]
+
+
+def select_by_fi(ms, device=None):
+    from ..models.gbdt import BinnedData, TreeConfig, TreeTrainer
+    from ..formats.tree_format import heap_tree_to_record
+    mc = ms.mc
+    cols = _good(ms)
+    md = ms.load_raw(cols)
+    C, nb, is_cat = N.tree_bin_codes(ms.ccs, md.table, cols)
+    from ..utils.device import default_device
+    dev = torch.device(device) if device is not None else default_device()
+    d = BinnedData.from_codes(torch.from_numpy(C), md.y, nb, is_cat, md.w.astype(np.float32), device=dev)
+    p = mc.train.get("params") or {}
+    cfg = TreeConfig(mc.algorithm if mc.algorithm in ("GBT", "RF") else "GBT",
+                     tree_num=min(int(float(p.get("TreeNum", 50))), 50), max_depth=int(p.get("MaxDepth", 6)),
+                     learning_rate=float(p.get("LearningRate", 0.05)), feature_subset_strategy="ALL")
+    tt = TreeTrainer(cfg, d)
+    tt.train()
+    imp = np.zeros(len(cols))
+    for t in tt.trees:
+        for nid in np.nonzero(t.exists)[0]:
+            f = int(t.feat[nid])
+            if f >= 0:
+                imp[f] += float(t.gain[nid]) * float(t.wgt_cnt[nid])
+    filter_num = int(mc.varSelect.get("filterNum", 200) or 0) or len(cols)
+    order = np.argsort(-imp, kind="stable")
+    keep = {cols[i].num for i in order[:filter_num] if imp[i] > 0}
+    for c in ms.ccs:
+        c.final_select = (c.num in keep) or c.is_force_select()
+    return [(cols[i].name, float(imp[i])) for i in order]
+
+
+def voted_selection(ms, device=None, population: int = 12, generations: int = 4, seed: int = 0):
+    """GA wrapper (``CandidateGenerator.nextGeneration`` J/core/dvarsel/wrapper/CandidateGenerator.java:113-200):
+    candidates are column subsets of size ``filterNum``; fitness = validation MSE of a small NN;
+    next generation = inherit the best half + hybrid (crossover) + mutate."""
+    mc = ms.mc
+    cols = _good(ms)
+    md = ms.load_raw(cols)
+    X, _, nums = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+    k = min(int(mc.varSelect.get("filterNum", 200) or len(cols)), len(cols))
+    rng = np.random.default_rng(seed)
+    n = X.shape[0]
+    va = rng.random(n) < 0.2
+    from ..utils.device import default_device
+    dev = torch.device(device) if device is not None else default_device()
+
+    def fitness(subset):
+        spec = MLPSpec(len(subset), [max(4, min(30, len(subset)))], ["tanh"], 1, "sigmoid")
+        tr = MLPTrainer(spec, dev, "R", 0.1, seed=int(rng.integers(1 << 30)))
+        tx = tr.prepare(torch.from_numpy(X[~va][:, subset]), md.y[~va].reshape(-1, 1))
+        vx = tr.prepare(torch.from_numpy(X[va][:, subset]), md.y[va].reshape(-1, 1))
+        for _ in range(20):
+            tr.step(tx)
+        return tr.evaluate(vx)
+    pop = [np.sort(rng.choice(len(cols), k, replace=False)) for _ in range(population)]
+    scored = []
+    for g in range(generations):
+        scored = sorted(((fitness(s), tuple(s)) for s in pop), key=lambda t: t[0])
+        _log.info("voted varsel generation %d best validation error %.6f", g, scored[0][0])
+        keep = [np.array(s) for _, s in scored[: population // 2]]
+        children = []
+        while len(keep) + len(children) < population:
+            a, b = rng.choice(len(keep), 2, replace=False)
+            pool = np.union1d(keep[a], keep[b])
+            child = np.sort(rng.choice(pool, k, replace=False))
+            if rng.random() < 0.3:             # mutate one gene
+                out = rng.integers(k)
+                rest = np.setdiff1d(np.arange(len(cols)), child)
+                if rest.size:
+                    child[out] = rng.choice(rest)
+                    child = np.sort(child)
+            children.append(child)
+        pop = keep + children
+    best = set(int(i) for i in scored[0][1])
+    for c in ms.ccs:
+        c.final_select = c.is_force_select()
+    for i in best:
+        cols[i].final_select = True
+    return [cols[i].name for i in sorted(best)]
+
+
+def run_auto_filter(ms):
+    before = {c.num: c.final_select for c in ms.ccs}
+    corr, corr_nums = None, None
+    thr = float(ms.mc.varSelect.get("correlationThreshold", 1.0) or 1.0)
+    if thr < 1.0 and os.path.exists(ms.pf.correlation_csv):
+        from .stats import read_correlation
+        names, corr = read_correlation(ms.pf.correlation_csv)
+        byname = {c.name: c.num for c in ms.ccs}
+        corr_nums = [byname.get(nm, -1) for nm in names]
+    removed = V.auto_filter(ms.mc, ms.ccs, corr, corr_nums)
+    changes = [(c, before[c.num], c.final_select) for c in ms.ccs if before[c.num] != c.final_select]
+    if changes:
+        _history_append(ms, changes, "auto")
+    _log.info("auto filter removed %d variables: %s", len(removed), removed[:20])
+    return removed
+
+
+def recover_auto(ms):
+    if not os.path.exists(ms.pf.varsel_history):
+        _log.warning("no varsel history")
+        return 0
+    byid = {c.num: c for c in ms.ccs}
+    n = 0
+    for line in open(ms.pf.varsel_history):
+        parts = line.strip().split(",")
+        if len(parts) < 5:
+            continue
+        c = byid.get(int(parts[0]))
+        old, new = parts[2] == "true", parts[3] == "true"
+        if c is not None and c.final_select == new:
+            c.final_select = old
+            n += 1
+    os.remove(ms.pf.varsel_history)
+    return n
+
+
+def run_varsel(root: str = ".", reset: bool = False, list_only: bool = False, autofilter: bool = False,
+               recover: bool = False, recursive: int = 1, device=None) -> int:
+    ms = ModelSet(root).setup("VARSELECT")
+    mc = ms.mc
+    if reset:
+        for c in ms.ccs:
+            c.final_select = False
+    elif list_only:
+        for c in ms.ccs:
+            if c.final_select:
+                print(c.name)
+        return 0
+    elif autofilter:
+        run_auto_filter(ms)
+    elif recover:
+        _log.info("recovered %d variables", recover_auto(ms))
+    else:
+        if mc.is_binary():
+            by = str(mc.varSelect.get("filterBy", "KS")).upper()
+            if by in ("KS", "IV", "MIX", "PARETO"):
+                V.select_by_filter(mc, ms.ccs)
+            elif by == "FI":
+                if mc.algorithm not in ("GBT", "RF"):
+                    raise ValueError("Filter by FI only works with GBT/RF")
+                select_by_fi(ms, device)
+            elif by in ("SE", "ST"):
+                if mc.algorithm not in ("NN", "LR"):
+                    raise ValueError("Filter by SE/ST only works with NN/LR")
+                os.makedirs(ms.pf.varsel_dir, exist_ok=True)
+                for i in range(max(1, recursive)):
+                    ms.save_cc()
+                    import shutil
+                    shutil.copyfile(ms.pf.column_config, ms.pf.varsel_cc_backup(i))
+                    res = select_by_sensitivity(ms, by, device, seed=i)
+                    with open(ms.pf.varsel_se(i), "w") as f:
+                        for num, name, mean, rms, var in res:
+                            f.write(f"{num}\t{name}\t{mean}\t{rms}\t{var}\n")
+            elif by in ("V", "VOTED"):
+                voted_selection(ms, device)
+            else:
+                raise ValueError(f"unknown filterBy {by}")
+        else:
+            forced = [c for c in ms.ccs if c.is_force_select()]
+            hc = has_candidates(ms.ccs)
+            for c in ms.ccs:
+                c.final_select = c.is_force_select() if forced else c.is_good_candidate(hc, False)
+        if bool(mc.varSelect.get("autoFilterEnable", True)):
+            run_auto_filter(ms)
+    ms.save_cc(backup=True)
+    _log.info("varsel: %d variables selected", sum(1 for c in ms.ccs if c.final_select))
+    return 0
