@@ -1,0 +1,180 @@
+"""Wide & Deep (H11, I4).
+
+Semantics of ``WideAndDeep`` (J/core/dtrain/wdl/WideAndDeep.java:112-232): the wide part is a
+sparse per-field LR over categorical bin indices (one weight per category + missing) plus a
+dense LR over the numeric inputs plus a bias; the deep part concatenates the numeric inputs with
+per-field embeddings (``NumEmbedColumnIds`` x ``NumEmbedOuputs``) and runs dense + activation
+layers down to one logit; ``p = sigmoid(wide + deep)``; the gradient is the sigmoid-MSE one
+``(p - y) p (1 - p) s`` with L2 (``WDLL2Reg``).  Full-batch epochs with the gradient all-reduced
+over ranks like the NN trainer (``WDLMaster.doCompute`` :164-184 sums worker gradients).
+
+On the GPU the embedding gathers / GEMMs run as PyTorch-ROCm ops (hipBLASLt GEMMs; the model is
+small and bandwidth-bound on the embedding gathers).  File format ``.wdl``: gzip Java
+DataOutput: version, norm type, NNColumnStats, JSON architecture, parameter arrays (this
+framework's own layout; the reference's BinaryWDLSerializer is WIP upstream).
+"""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+import torch
+
+from ..formats.javaio import JavaIn, JavaOut
+from ..parallel import dist
+from .nn import act_fwd
+
+
+class WideDeepNet(torch.nn.Module):
+    def __init__(self, n_dense: int, cat_sizes: list, embed_fields: list, embed_dim: int, hidden: list,
+                 acts: list, wide: bool = True, deep: bool = True):
+        super().__init__()
+        self.n_dense, self.cat_sizes = n_dense, list(cat_sizes)
+        self.embed_fields, self.embed_dim = list(embed_fields), int(embed_dim)
+        self.hidden, self.acts = list(hidden), list(acts)
+        self.wide_on, self.deep_on = wide, deep
+        self.wide_tables = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(s + 1)) for s in cat_sizes])
+        self.wide_dense = torch.nn.Parameter(torch.zeros(n_dense))
+        self.bias = torch.nn.Parameter(torch.zeros(1))
+        g = torch.Generator().manual_seed(7)
+        self.embeds = torch.nn.ParameterList([
+            torch.nn.Parameter(torch.randn(cat_sizes[f] + 1, embed_dim, generator=g) * 0.05) for f in embed_fields])
+        dims = [n_dense + embed_dim * len(embed_fields)] + self.hidden
+        self.layers = torch.nn.ParameterList()
+        for i in range(len(self.hidden)):
+            lim = (6.0 / (dims[i] + dims[i + 1])) ** 0.5
+            self.layers.append(torch.nn.Parameter((torch.rand(dims[i + 1], dims[i] + 1, generator=g) * 2 - 1) * lim))
+        self.final = torch.nn.Parameter((torch.rand(1, dims[-1] + 1, generator=g) * 2 - 1) * 0.1)
+
+    def forward(self, dense: torch.Tensor, cats: torch.Tensor) -> torch.Tensor:
+        n = dense.shape[0]
+        logit = torch.zeros(n, device=dense.device)
+        if self.wide_on:
+            logit = logit + dense @ self.wide_dense + self.bias
+            for f, t in enumerate(self.wide_tables):
+                logit = logit + t[cats[:, f]]
+        if self.deep_on:
+            parts = [dense] + [e[cats[:, f]] for e, f in zip(self.embeds, self.embed_fields)]
+            a = torch.cat(parts, 1) if len(parts) > 1 else dense
+            for W, act in zip(self.layers, self.acts):
+                a = act_fwd(act, a @ W[:, :-1].t() + W[:, -1])
+            logit = logit + (a @ self.final[:, :-1].t() + self.final[:, -1])[:, 0]
+        return logit
+
+    def arch(self):
+        return dict(n_dense=self.n_dense, cat_sizes=self.cat_sizes, embed_fields=self.embed_fields,
+                    embed_dim=self.embed_dim, hidden=self.hidden, acts=self.acts, wide=self.wide_on, deep=self.deep_on)
+
+
+def wdl_inputs(ccs, table, cols, norm_cutoff: float):
+    """(dense z-scored numerics [N, Dn] float32, categorical indices [N, Dc] int64, cat sizes)."""
+    from ..algos.normalize import _cat_index, normalize_column
+    num = [c for c in cols if not c.is_categorical()]
+    cat = [c for c in cols if c.is_categorical()]
+    n = table.n
+    dense = np.stack([normalize_column(c, table[c.name], "ZSCALE", norm_cutoff)[:, 0] for c in num], 1) \
+        if num else np.zeros((n, 0))
+    sizes = [len(c.bin_category or []) for c in cat]
+    idx = np.stack([np.where((i := _cat_index(c, table[c.name])) < 0, s, i) for c, s in zip(cat, sizes)], 1) \
+        if cat else np.zeros((n, 0), np.int64)
+    return dense.astype(np.float32), idx.astype(np.int64), sizes, num, cat
+
+
+class WDLModel:
+    def __init__(self, net: WideDeepNet, norm_type: str, col_stats: list, columns: list, cutoff: float):
+        self.net, self.norm_type, self.col_stats, self.columns, self.cutoff = net, norm_type, col_stats, columns, cutoff
+
+    def score_table(self, mc, ccs, table) -> np.ndarray:
+        byname = {c.name: c for c in ccs}
+        cols = [byname[n] for n in self.columns if n in byname]
+        dense, idx, _, _, _ = wdl_inputs(ccs, table, cols, self.cutoff)
+        dev = next(self.net.parameters()).device
+        with torch.no_grad():
+            return torch.sigmoid(self.net(torch.from_numpy(dense).to(dev), torch.from_numpy(idx).to(dev))).cpu() \
+                .double().numpy()
+
+
+def write_wdl(path: str, model: WDLModel):
+    o = JavaOut()
+    o.int(1)
+    o.string(model.norm_type)
+    o.string(json.dumps({"arch": model.net.arch(), "columns": model.columns, "cutoff": model.cutoff}))
+    params = [p.detach().double().cpu().numpy().reshape(-1) for p in model.net.parameters()]
+    o.int(len(params))
+    for p in params:
+        o.double_array(p)
+    with open(path, "wb") as f:
+        f.write(o.gzip_bytes())
+
+
+def read_wdl(path: str) -> WDLModel:
+    with open(path, "rb") as f:
+        i = JavaIn(f.read())
+    i.int()
+    norm = i.string()
+    meta = json.loads(i.string())
+    a = meta["arch"]
+    net = WideDeepNet(a["n_dense"], a["cat_sizes"], a["embed_fields"], a["embed_dim"], a["hidden"], a["acts"],
+                      a["wide"], a["deep"])
+    n = i.int()
+    with torch.no_grad():
+        for p, _ in zip(net.parameters(), range(n)):
+            p.copy_(torch.tensor(i.double_array(), dtype=torch.float32).view_as(p))
+    return WDLModel(net, norm, [], meta["columns"], meta["cutoff"])
+
+
+def train_wdl_step(step, tid, p, ts, y, train_m, valid_m, sw):
+    """Train one WDL bag inside ``TrainStep`` (re-reads raw columns: WDL needs category indices)."""
+    ms, mc = step.ms, step.mc
+    cols = ms.input_columns()
+    md = ms.load_raw(cols)
+    cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
+    dense, idx, sizes, num, cat = wdl_inputs(ms.ccs, md.table, cols, cutoff)
+    y = md.y.astype(np.float32)
+    w = md.w.astype(np.float32)
+    rng = np.random.default_rng(tid)
+    valid = rng.random(md.n) < float(mc.train.get("validSetRate", 0.2) or 0.0)
+    embed_ids = p.get("NumEmbedColumnIds")
+    cat_nums = [c.num for c in cat]
+    embed_fields = [cat_nums.index(c) for c in embed_ids if c in cat_nums] if embed_ids else list(range(len(cat)))
+    hidden = [int(h) for h in (p.get("NumHiddenNodes") or [50])][: int(p.get("NumHiddenLayers", 1) or 1)]
+    acts = list(p.get("ActivationFunc") or ["relu"])
+    while len(acts) < len(hidden):
+        acts.append(acts[-1])
+    net = WideDeepNet(dense.shape[1], sizes, embed_fields, int(p.get("NumEmbedOuputs", 8) or 8), hidden,
+                      acts[: len(hidden)]).to(step.dev)
+    for prm in net.parameters():
+        dist.broadcast_(prm.data, 0)
+    lr = float(p.get("LearningRate", 0.01))
+    l2 = float(p.get("WDLL2Reg", 0.0) or 0.0)
+    opt_name = str(p.get("Optimizer", "ADAM")).upper()
+    opt = {"ADAGRAD": torch.optim.Adagrad, "SGD": torch.optim.SGD, "GD": torch.optim.SGD}.get(
+        opt_name, torch.optim.Adam)(net.parameters(), lr=lr)
+    dv = lambda a: torch.from_numpy(a).to(step.dev)   # noqa: E731
+    td, ti, ty, tw = dv(dense[~valid]), dv(idx[~valid]), dv(y[~valid]), dv(w[~valid])
+    vd, vi, vy = dv(dense[valid]), dv(idx[valid]), dv(y[valid])
+    epochs = int(mc.train.get("numTrainEpochs", 100))
+    verr = float("nan")
+    for ep in range(1, epochs + 1):
+        opt.zero_grad()
+        pr = torch.sigmoid(net(td, ti))
+        loss = 0.5 * ((pr - ty) ** 2 * tw).sum()
+        if l2 > 0:
+            loss = loss + 0.5 * l2 * sum((q ** 2).sum() for q in net.parameters())
+        loss.backward()
+        flat = torch.cat([q.grad.reshape(-1) for q in net.parameters()])
+        tail = torch.tensor([float(((pr.detach() - ty) ** 2).sum()), float(len(ty))], device=step.dev)
+        buf = torch.cat([flat, tail])
+        dist.all_reduce_(buf)
+        off = 0
+        for q in net.parameters():
+            q.grad.copy_(buf[off: off + q.numel()].view_as(q) / max(float(buf[-1]), 1.0))
+            off += q.numel()
+        opt.step()
+        terr = float(buf[-2] / max(float(buf[-1]), 1.0))
+        with torch.no_grad():
+            verr = float(((torch.sigmoid(net(vd, vi)) - vy) ** 2).mean()) if len(vy) else float("nan")
+        step._log_epoch(tid, ep, terr, verr)
+    if step.info.rank == 0:
+        write_wdl(ms.pf.model_path(tid, "wdl"), WDLModel(net.cpu(), mc.norm_type, [], [c.name for c in cols], cutoff))
+    return verr

@@ -1,42 +1,56 @@
-"""The CLI pipeline on the MI355X: NN (HIP MFMA trainer), LR and GBT (HIP histogram trainer)
-on the cancer-judgement data; scores must reach the same quality as the CPU path."""
+"""The full pipeline on the MI355X (HIP MFMA NN trainer, HIP histogram tree trainer) over a
+synthetic model set generated in-test (the GPU box has no reference fixtures)."""
 import json
 import os
 
 import pytest
 
-from test_pipeline_e2e import _auc, _make
-
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("alg,params,min_auc", [("NN", None, 0.9), ("LR", None, 0.9),
-                                                ("GBT", {"TreeNum": 20}, 0.75), ("RF", {"TreeNum": 10}, 0.85)])
-def test_pipeline_on_gpu(tmp_path, ref_resources, alg, params, min_auc):
-    from shifu_amd.steps.evaluate import run_eval
-    from shifu_amd.steps.norm import run_norm
-    from shifu_amd.steps.stats import run_stats
-    from shifu_amd.steps.train import run_train
-    from shifu_amd.steps.varsel import run_varsel
-    root = _make(tmp_path, ref_resources, alg, epochs=40, params=params)
-    assert run_stats(root) == 0
-    assert run_varsel(root) == 0
-    assert run_norm(root) == 0
-    assert run_train(root) == 0
-    assert run_eval(root) == 0
-    assert _auc(root) > min_auc
+def _run(root, steps=("init", "stats", "varsel", "norm", "train", "eval")):
+    from shifu_amd.cli import main
+    cwd = os.getcwd()
+    os.chdir(root)
+    try:
+        for s in steps:
+            assert main(s.split()) == 0, s
+    finally:
+        os.chdir(cwd)
 
 
-def test_sensitivity_varsel_gpu(tmp_path, ref_resources):
+def _auc(root):
+    return json.load(open(os.path.join(root, "evals/Eval1/EvalPerformance.json")))["areaUnderRoc"]
+
+
+@pytest.mark.parametrize("alg,params,min_auc", [("NN", None, 0.85), ("LR", None, 0.85),
+                                                ("GBT", {"TreeNum": 30, "MaxDepth": 5}, 0.8),
+                                                ("RF", {"TreeNum": 10}, 0.75)])
+def test_pipeline_on_gpu(tmp_path, alg, params, min_auc):
+    import torch
     from shifu_amd.config.model_config import ModelConfig
-    from shifu_amd.steps.stats import run_stats
-    from shifu_amd.steps.varsel import run_varsel
-    root = _make(tmp_path, ref_resources, "NN", epochs=20)
-    run_stats(root)
+    from shifu_amd.utils.synthetic import make_model_set
+    assert torch.cuda.is_available()
+    root = make_model_set(str(tmp_path), "g", alg, n_rows=4000)
+    mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+    mc.train["numTrainEpochs"] = 60
+    mc.train["baggingNum"] = 2
+    if params:
+        mc.train["params"].update(params)
+    mc.save()
+    _run(root)
+    assert _auc(root) > min_auc, _auc(root)
+
+
+def test_sensitivity_varsel_gpu(tmp_path):
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "g", "NN", n_rows=3000)
     mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
     mc.varSelect["filterBy"] = "SE"
     mc.varSelect["filterNum"] = 10
+    mc.train["numTrainEpochs"] = 20
     mc.save()
-    assert run_varsel(root) == 0
+    _run(root, ("init", "stats", "varsel"))
     sel = [c for c in json.load(open(os.path.join(root, "ColumnConfig.json"))) if c["finalSelect"]]
     assert 0 < len(sel) <= 10
