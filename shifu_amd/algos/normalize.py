@@ -207,3 +207,124 @@ def tree_bin_codes(ccs, table, columns):
             is_cat.append(0)
     C = np.stack(codes, 1) if codes else np.zeros((table.n, 0), np.int32)
     return C, np.array(nbins, np.int32), np.array(is_cat, np.uint8)
+
+
+# ---- HIP path (K5 / K1') ---------------------------------------------------------------------------
+def _raw_matrix(cols, table):
+    """Column-major fp64 raw values: numeric value (NaN missing) or categorical index (-1 missing)."""
+    out = np.empty((len(cols), table.n), dtype=np.float64)
+    for j, cc in enumerate(cols):
+        col = table[cc.name]
+        out[j] = _cat_index(cc, col) if cc.is_categorical() else col.numeric().astype(np.float64)
+    return out
+
+
+def _gpu_spec(cc, nt, cutoff):
+    """Kernel spec for one width-1 column (None -> handled on the host, e.g. one-hot)."""
+    cat = cc.is_categorical()
+    mean, std = cc.mean or 0.0, cc.std_dev or 0.0
+    base = dict(mean=mean, std=std, cutoff=cutoff)
+    woe = lambda weighted: list(cc.bin_weighted_woe if weighted else cc.bin_count_woe)   # noqa: E731
+    if nt in ("ZSCALE", "ZSCORE", "OLD_ZSCALE", "OLD_ZSCORE"):
+        if cat:
+            return dict(base, mode="cat_table", table=list(cc.bin_pos_rate), zflag=0 if nt.startswith("OLD_") else 1,
+                        zmean=mean, zstd=std)
+        return dict(base, mode="zscore")
+    if nt in ("WOE", "WEIGHT_WOE"):
+        t = woe(nt == "WEIGHT_WOE")
+        return dict(base, mode="cat_table", table=t) if cat else dict(base, mode="num_table", table=t,
+                                                                      bounds=list(cc.bin_boundary))
+    if nt in ("WOE_ZSCORE", "WOE_ZSCALE", "WEIGHT_WOE_ZSCORE", "WEIGHT_WOE_ZSCALE"):
+        wt = nt.startswith("WEIGHT")
+        m, s = woe_mean_std(cc, wt)
+        d = dict(base, table=woe(wt), zflag=1, zmean=m, zstd=s)
+        return dict(d, mode="cat_table") if cat else dict(d, mode="num_table", bounds=list(cc.bin_boundary))
+    if nt in ("HYBRID", "WEIGHT_HYBRID"):
+        return dict(base, mode="cat_table", table=woe(nt == "WEIGHT_HYBRID")) if cat else dict(base, mode="zscore")
+    if nt == "ONEHOT" or (nt == "ZSCALE_ONEHOT" and cat):
+        return None
+    if nt == "ZSCALE_ONEHOT":
+        return dict(base, mode="zscore")
+    if nt in ("ASIS_WOE", "ASIS_PR"):
+        if cat:
+            return dict(base, mode="cat_table", table=list(cc.bin_count_woe if nt == "ASIS_WOE" else cc.bin_pos_rate))
+        return dict(base, mode="raw")
+    if nt in ("DISCRETE_ZSCORE", "DISCRETE_ZSCALE"):
+        if cat:
+            return dict(base, mode="cat_table", table=list(cc.bin_pos_rate), zflag=1, zmean=mean, zstd=std)
+        lo = list(np.asarray(cc.bin_boundary, dtype=np.float64))
+        lo[0] = cc.stat("min") if cc.stat("min") is not None else 0.0
+        return dict(base, mode="discrete", bounds=list(cc.bin_boundary), table=lo)
+    if is_index_norm(nt):
+        if cat:
+            return dict(base, mode="cat_index", ncat=len(cc.bin_category or []))
+        if nt in ("ZSCALE_INDEX", "ZSCORE_INDEX"):
+            return dict(base, mode="zscore")
+        if nt == "WOE_INDEX":
+            return dict(base, mode="num_table", table=woe(False), bounds=list(cc.bin_boundary))
+        m, s = woe_mean_std(cc, False)
+        return dict(base, mode="num_table", table=woe(False), bounds=list(cc.bin_boundary), zflag=1, zmean=m, zstd=s)
+    raise ValueError(f"unsupported norm type {nt}")
+
+
+def normalize_table_gpu(mc, ccs, table, columns=None, norm_type: str | None = None, device="cuda",
+                        return_device: bool = False):
+    """HIP normalization (one launch for every width-1 column); identical output to
+    :func:`normalize_table`.  ``return_device`` keeps X resident in HBM (training path)."""
+    import torch
+    from ..ops import stats_ops
+    nt = norm_type or mc.norm_type
+    cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
+    cols = columns if columns is not None else [c for c in ccs if c.final_select and not c.is_target()
+                                                 and not c.is_meta()]
+    specs, names, nums, host_cols = [], [], [], []
+    pos = 0
+    gpu_cols = []
+    for cc in cols:
+        if cc.name not in table:
+            raise KeyError(f"column {cc.name} missing from data")
+        s = _gpu_spec(cc, nt, cutoff)
+        if s is None:
+            width = norm_width(cc, "ONEHOT")
+            host_cols.append((cc, pos, width))
+            names.extend(f"{cc.name}_{i}" for i in range(width))
+            nums.extend([cc.num] * width)
+            pos += width
+        else:
+            s["out_col"] = pos
+            specs.append(s)
+            gpu_cols.append(cc)
+            names.append(cc.name)
+            nums.append(cc.num)
+            pos += 1
+    dev = torch.device(device)
+    out = torch.zeros(table.n, max(pos, 1), dtype=torch.float32, device=dev)
+    if gpu_cols:
+        vals = torch.as_tensor(_raw_matrix(gpu_cols, table), device=dev)
+        stats_ops.normalize(vals, specs, out)
+    for cc, p0, width in host_cols:
+        out[:, p0: p0 + width] = torch.as_tensor(normalize_column(cc, table[cc.name], nt, cutoff), dtype=torch.float32,
+                                                 device=dev)
+    out = out[:, :pos]
+    return (out if return_device else out.cpu().numpy()), names, nums
+
+
+def tree_bin_codes_gpu(ccs, table, columns, device="cuda"):
+    """HIP CleanedData codes (uint8, nbins <= 256)."""
+    import torch
+    from ..ops import stats_ops
+    nbins, is_cat, ncat, bounds = [], [], [], []
+    for cc in columns:
+        if cc.is_categorical():
+            k = len(cc.bin_category or [])
+            nbins.append(k + 1); is_cat.append(1); ncat.append(k); bounds.append(None)
+        else:
+            bb = cc.bin_boundary or [float("-inf")]
+            nbins.append(max(1, len(bb))); is_cat.append(0); ncat.append(0); bounds.append(bb)
+    if max(nbins, default=1) > 256:
+        return None
+    dev = torch.device(device)
+    vals = torch.as_tensor(_raw_matrix(columns, table), device=dev)
+    out = torch.zeros(table.n, max(1, len(columns)), dtype=torch.uint8, device=dev)
+    stats_ops.bin_codes(vals, is_cat, bounds, ncat, out)
+    return out.cpu().numpy().astype(np.int32), np.array(nbins, np.int32), np.array(is_cat, np.uint8)

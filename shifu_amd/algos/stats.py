@@ -126,116 +126,159 @@ def _percentiles(bounds, counts, mn, mx, count):
     return p25, med, p75
 
 
-def compute_column_stats(mc, ccs, md, device=None, columns=None):
-    """Fill ``columnBinning``/``columnStats`` of every candidate column from ModelData ``md``."""
-    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+def _finish_binning(cc, binary, nb, cpos, cneg, wpos, wneg, total):
+    """Write binning arrays + KS/IV/WOE for one column (shared by the CPU and HIP paths)."""
+    if binary:
+        rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
+    else:
+        tot = cpos.sum()
+        rate = cpos / tot if tot else np.zeros(nb)
+    cc.stats["validNumCount"] = int(total - cc.stats.get("missingCount", 0))
+    cb = cc.binning
+    cb["length"] = int(nb - 1)
+    cb["binCountPos"] = [int(x) for x in cpos]
+    cb["binCountNeg"] = [int(x) for x in cneg]
+    cb["binWeightedPos"] = [float(x) for x in wpos]
+    cb["binWeightedNeg"] = [float(x) for x in wneg]
+    cb["binPosRate"] = [float(x) for x in rate]
+    if binary:
+        m = column_metrics(cneg, cpos)
+        mw = column_metrics(wneg, wpos)
+        zero = [0.0] * nb
+        cc.stats["ks"], cc.stats["iv"], cc.stats["woe"] = (m[0], m[1], m[2]) if m else (None, None, None)
+        cc.stats["weightedKs"], cc.stats["weightedIv"], cc.stats["weightedWoe"] = \
+            (mw[0], mw[1], mw[2]) if mw else (None, None, None)
+        cb["binCountWoe"] = m[3] if m else zero
+        cb["binWeightedWoe"] = mw[3] if mw else zero
+    else:
+        cb["binCountWoe"] = [0.0] * nb
+        cb["binWeightedWoe"] = [0.0] * nb
+
+
+def _numeric_bounds(vals, y, w, binary, method, n_bins):
+    if binary and method in ("EqualPositive", "WeightEqualPositive"):
+        sel = y > 0.5
+    elif binary and method in ("EqualNegtive", "WeightEqualNegative"):
+        sel = y <= 0.5
+    else:
+        sel = np.ones(len(vals), dtype=bool)
+    weighted = method.startswith("Weight")
+    if method in ("EqualInterval", "WeightEqualInterval"):
+        bounds = B.equal_interval_boundaries(vals[sel], n_bins)
+    else:
+        bounds = B.equal_population_boundaries(vals[sel], n_bins, w[sel] if weighted else None)
+    if len(bounds) <= 1 and sel.sum() < len(vals):
+        bounds = B.equal_population_boundaries(vals, n_bins)
+    return bounds
+
+
+def _finish_numeric(cc, binary, bounds, cpos, cneg, wpos, wneg, mom, total, distinct):
+    cc.bin_boundary = bounds
+    cc.bin_category = None
+    cnt, s1, s2, s3, s4, mn, mx = mom
+    _finish_moments(cc, cnt, s1, s2, s3, s4, mn, mx, total, total - cnt)
+    p25, med, p75 = _percentiles(bounds, (cpos + cneg) if binary else cpos, mn, mx, total)
+    cc.stats["median"] = float(med)
+    cc.stats["25th"] = float(p25)
+    cc.stats["75th"] = float(p75)
+    cc.stats["distinctCount"] = int(distinct)
+    _finish_binning(cc, binary, len(bounds) + 1, cpos, cneg, wpos, wneg, total)
+
+
+def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int = 64):
+    """Fill ``columnBinning``/``columnStats`` of every candidate column from ModelData ``md``.
+
+    Numeric columns on the GPU go through the fused HIP kernel (K1+K2: bin search + pos/neg
+    histograms + fp64 moments for a batch of columns in one launch); the CPU path is the
+    oracle with identical semantics."""
+    from ..utils.device import is_gpu_available
+    dev = torch.device(device or ("cuda" if is_gpu_available() else "cpu"))
     binary = mc.is_binary()
     method = mc.binning_method
     n_bins = int(mc.stats.get("maxNumBin", 10))
     cate_max = int(mc.stats.get("cateMaxNumBin", 0) or 0)
     num_thr = float(mc.stats.get("numericalValueThreshold", 1.7976931348623157e308))
-    algo = mc.binning_algorithm
     y, w = md.y, md.w
+    total = md.n
+    numeric = []
     for cc in ccs:
         if columns is not None and cc.name not in columns:
             continue
         if cc.is_target() or cc.is_meta() or cc.name not in md.table:
             continue
         col = md.table[cc.name]
-        total = md.n
-        if cc.is_categorical():
-            codes = col.values if col.kind == "str" else None
-            if codes is None:   # numeric-parsed categorical: categories = formatted values
-                s = col.strings()
-                uniq = {}
-                codes = np.array([uniq.setdefault(v, len(uniq)) if v != "" else -1 for v in s], dtype=np.int32)
-                dictionary = list(uniq.keys())
-            else:
-                dictionary = col.dictionary
-            cats = B.categorical_bins(codes, dictionary, y, binary)
-            bidx = B.category_index(codes, dictionary, cats)
+        if not cc.is_categorical():
+            numeric.append(cc)
+            continue
+        codes = col.values if col.kind == "str" else None
+        if codes is None:   # numeric-parsed categorical: categories = formatted values
+            s = col.strings()
+            uniq = {}
+            codes = np.array([uniq.setdefault(v, len(uniq)) if v != "" else -1 for v in s], dtype=np.int32)
+            dictionary = list(uniq.keys())
+        else:
+            dictionary = col.dictionary
+        cats = B.categorical_bins(codes, dictionary, y, binary)
+        bidx = B.category_index(codes, dictionary, cats)
+        nb = len(cats) + 1
+        cpos, cneg, wpos, wneg = _hist(bidx, y, w, nb, binary, dev)
+        if cate_max > 0 and len(cats) > cate_max:
+            cats, cpos, cneg, wpos, wneg = B.rebin_categorical(cats, list(cpos), list(cneg), list(wpos),
+                                                               list(wneg), cate_max)
+            cpos, cneg = np.array(cpos, np.int64), np.array(cneg, np.int64)
+            wpos, wneg = np.array(wpos), np.array(wneg)
             nb = len(cats) + 1
-            cpos, cneg, wpos, wneg = _hist(bidx, y, w, nb, binary, dev)
-            if cate_max > 0 and len(cats) > cate_max:
-                cats, cpos, cneg, wpos, wneg = B.rebin_categorical(cats, list(cpos), list(cneg), list(wpos),
-                                                                   list(wneg), cate_max)
-                cpos, cneg = np.array(cpos, np.int64), np.array(cneg, np.int64)
-                wpos, wneg = np.array(wpos), np.array(wneg)
-            cc.bin_category = cats
-            cc.bin_boundary = None
-            missing = int((bidx == len(cats)).sum()) if cate_max <= 0 else int(cpos[-1] + cneg[-1])
-            if binary:
-                rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
-            else:
-                tot = cpos.sum()
-                rate = cpos / tot if tot else np.zeros_like(cpos, dtype=float)
-            # categorical numeric stats are computed over bin pos-rates (reducer :309-333)
-            cnt = cpos + cneg if binary else cpos
-            okr = np.isfinite(rate)
-            mx = float(rate[okr].max()) if okr.any() else 0.0
-            mn = float(rate[okr].min()) if okr.any() else 0.0
-            s1 = float((rate * cnt).sum())
-            s2 = float((rate ** 2 * cnt).sum())
-            s3 = float((rate ** 3 * cnt).sum())
-            s4 = float((rate ** 4 * cnt).sum())
-            _finish_moments(cc, total - missing, s1, s2, s3, s4, mn, mx, total, missing)
-            cc.stats["distinctCount"] = int(len(dictionary))
-            cc.stats["median"] = None
-        else:
-            vals = col.numeric().astype(np.float64).copy()
-            vals[vals > num_thr] = np.nan          # numericalValueThreshold -> invalid
-            if binary and method in ("EqualPositive", "WeightEqualPositive"):
-                sel = y > 0.5
-            elif binary and method in ("EqualNegtive", "WeightEqualNegative"):
-                sel = y <= 0.5
-            else:
-                sel = np.ones(len(vals), dtype=bool)
-            weighted = method.startswith("Weight")
-            if method in ("EqualInterval", "WeightEqualInterval"):
-                bounds = B.equal_interval_boundaries(vals[sel], n_bins)
-            else:
-                bounds = B.equal_population_boundaries(vals[sel], n_bins, w[sel] if weighted else None)
-            if len(bounds) <= 1 and sel.sum() < len(vals):
-                bounds = B.equal_population_boundaries(vals, n_bins)
-            bidx = B.bin_index_numeric(vals, bounds)
-            nb = len(bounds) + 1
-            cpos, cneg, wpos, wneg = _hist(bidx, y, w, nb, binary, dev)
-            cc.bin_boundary = bounds
-            cc.bin_category = None
-            cnt, s1, s2, s3, s4, mn, mx = _moments(vals, dev)
-            missing = total - cnt
-            _finish_moments(cc, cnt, s1, s2, s3, s4, mn, mx, total, missing)
-            p25, med, p75 = _percentiles(bounds, (cpos + cneg) if binary else cpos, mn, mx, total)
-            cc.stats["median"] = float(med)
-            cc.stats["25th"] = float(p25)
-            cc.stats["75th"] = float(p75)
-            fin = vals[np.isfinite(vals)]
-            cc.stats["distinctCount"] = int(np.unique(fin).size)
-            if binary:
-                rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
-            else:
-                tot = cpos.sum()
-                rate = cpos / tot if tot else np.zeros(nb)
-        cc.stats["validNumCount"] = int(total - cc.stats.get("missingCount", 0))
-        cb = cc.binning
-        cb["length"] = int(nb - 1)
-        cb["binCountPos"] = [int(x) for x in cpos]
-        cb["binCountNeg"] = [int(x) for x in cneg]
-        cb["binWeightedPos"] = [float(x) for x in wpos]
-        cb["binWeightedNeg"] = [float(x) for x in wneg]
-        cb["binPosRate"] = [float(x) for x in rate]
+        cc.bin_category = cats
+        cc.bin_boundary = None
+        missing = int((bidx == len(cats)).sum()) if cate_max <= 0 else int(cpos[-1] + cneg[-1])
         if binary:
-            m = column_metrics(cneg, cpos)
-            mw = column_metrics(wneg, wpos)
-            zero = [0.0] * nb
-            cc.stats["ks"], cc.stats["iv"], cc.stats["woe"] = (m[0], m[1], m[2]) if m else (None, None, None)
-            cc.stats["weightedKs"], cc.stats["weightedIv"], cc.stats["weightedWoe"] = \
-                (mw[0], mw[1], mw[2]) if mw else (None, None, None)
-            cb["binCountWoe"] = m[3] if m else zero
-            cb["binWeightedWoe"] = mw[3] if mw else zero
+            rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
         else:
-            cb["binCountWoe"] = [0.0] * nb
-            cb["binWeightedWoe"] = [0.0] * nb
+            tot = cpos.sum()
+            rate = cpos / tot if tot else np.zeros_like(cpos, dtype=float)
+        # categorical numeric stats are computed over bin pos-rates (reducer :309-333)
+        cnt = cpos + cneg if binary else cpos
+        okr = np.isfinite(rate)
+        mx = float(rate[okr].max()) if okr.any() else 0.0
+        mn = float(rate[okr].min()) if okr.any() else 0.0
+        s1 = float((rate * cnt).sum())
+        s2 = float((rate ** 2 * cnt).sum())
+        s3 = float((rate ** 3 * cnt).sum())
+        s4 = float((rate ** 4 * cnt).sum())
+        _finish_moments(cc, total - missing, s1, s2, s3, s4, mn, mx, total, missing)
+        cc.stats["distinctCount"] = int(len(dictionary))
+        cc.stats["median"] = None
+        _finish_binning(cc, binary, nb, cpos, cneg, wpos, wneg, total)
+    if not numeric:
+        return ccs
+    if dev.type == "cuda":
+        from ..ops import stats_ops
+        yt = torch.as_tensor(np.asarray(y, np.float32), device=dev)
+        wt = torch.as_tensor(np.asarray(w, np.float64), device=dev)
+        for b0 in range(0, len(numeric), gpu_batch):
+            batch = numeric[b0: b0 + gpu_batch]
+            host = [md.table[c.name].numeric().astype(np.float64) for c in batch]
+            bounds, distinct = [], []
+            for v in host:
+                v = v.copy()
+                v[v > num_thr] = np.nan
+                bounds.append(_numeric_bounds(v, y, w, binary, method, n_bins))
+                fin = v[np.isfinite(v)]
+                distinct.append(int(torch.unique(torch.as_tensor(fin, device=dev)).numel()) if fin.size else 0)
+            vals = torch.as_tensor(np.stack(host), device=dev)
+            res = stats_ops.column_stats(vals, yt, wt, bounds, binary, num_thr)
+            for c, bnd, (cpos, cneg, wpos, wneg, mom), dc in zip(batch, bounds, res, distinct):
+                _finish_numeric(c, binary, bnd, cpos, cneg, wpos, wneg, mom, total, dc)
+        return ccs
+    for cc in numeric:
+        vals = md.table[cc.name].numeric().astype(np.float64).copy()
+        vals[vals > num_thr] = np.nan          # numericalValueThreshold -> invalid
+        bounds = _numeric_bounds(vals, y, w, binary, method, n_bins)
+        bidx = B.bin_index_numeric(vals, bounds)
+        cpos, cneg, wpos, wneg = _hist(bidx, y, w, len(bounds) + 1, binary, dev)
+        fin = vals[np.isfinite(vals)]
+        _finish_numeric(cc, binary, bounds, cpos, cneg, wpos, wneg, _moments(vals, dev), total,
+                        np.unique(fin).size)
     return ccs
 
 

@@ -177,7 +177,23 @@ def sensitivity(network, X: np.ndarray, y=None, w=None, device=None, feat_chunk:
         return a[..., 0]
     W1 = Ws[0][:, :-1]          # [H1, F]
     b1 = Ws[0][:, -1]
-    for r0 in range(0, X.shape[0], row_chunk):
+    if dev.type == "cuda" and len(Ws) == 2 and Ws[1].shape[0] == 1 and W1.shape[0] <= 1024:
+        # HIP kernel (K14): S cached per row, rank-1 correction + activation + output neuron fused
+        from ..models.nn import ACT_IDS
+        from ..ops import stats_ops
+        acc = torch.zeros(F, 2, dtype=torch.float64, device=dev)
+        W1t = W1.t().contiguous()
+        W2 = Ws[1][0, :-1].contiguous()
+        b2 = float(Ws[1][0, -1])
+        for r0 in range(0, X.shape[0], row_chunk * 16):
+            xb = torch.as_tensor(X[r0: r0 + row_chunk * 16], dtype=torch.float32, device=dev).contiguous()
+            S = (xb @ W1.t() + b1).contiguous()
+            base = act_fwd(acts[1], act_fwd(acts[0], S) @ W2 + b2).contiguous()
+            stats_ops.sensitivity_1h(S, xb, W1t, W2, b2, base, ACT_IDS[acts[0]], ACT_IDS[acts[1]], acc)
+            n += xb.shape[0]
+        s_abs, s_sq = acc[:, 0], acc[:, 1]
+        row_chunk = X.shape[0] + 1     # skip the generic path
+    for r0 in (range(0, X.shape[0], row_chunk) if n == 0 else ()):
         xb = torch.as_tensor(X[r0: r0 + row_chunk], dtype=torch.float32, device=dev)
         S = xb @ W1.t() + b1                     # cached first layer [R, H1]
         base = tail(S)                           # [R]

@@ -5,10 +5,11 @@ and ``LogisticRegressionMaster`` (:227-299): p = sigmoid(w.x + b) (bias = last w
 gradient ``g_i += (y-p) x_i (p(1-p) + 0.1) s`` (the derivative-with-flat-spot variant), training
 error = mean (y-p)^2 (unweighted), then the shared ``Weight`` update rules (RPROP by default).
 
-MI355X mapping: the rows stay resident in HBM (bf16 when large); one epoch is two memory-bound
-GEMVs over the shard (``X w`` and ``X^T d``) via hipBLASLt plus a fused elementwise, then the
-[F+1(+2)] gradient buffer (with error/count tail) is all-reduced over RCCL and every rank applies
-the identical optimizer step (no parameter server).
+MI355X mapping: the rows stay resident in HBM (bf16 when large); one epoch is ONE memory-bound
+pass of the fused HIP kernel ``lr_grad_kernel`` (K9: dot, sigmoid, gradient accumulation in
+registers, block partials) over the shard; then the [F+1(+2)] gradient buffer (with error/count
+tail) is all-reduced over RCCL and every rank applies the identical optimizer step (no parameter
+server).  The torch two-GEMV path is the CPU oracle.
 """
 from __future__ import annotations
 
@@ -41,7 +42,13 @@ class LRTrainer:
         x = torch.as_tensor(x)
         n = x.shape[0]
         dt = torch.bfloat16 if (self.device.type == "cuda" and x.numel() > (1 << 30)) else torch.float32
-        xd = x.to(self.device, dt).contiguous()
+        if self.device.type == "cuda":      # pad rows to a 16-byte multiple for the vector loads of K9
+            fp = (x.shape[1] + 7) // 8 * 8
+            xp = torch.zeros(n, fp, dtype=dt, device=self.device)
+            xp[:, : x.shape[1]] = x.to(self.device, dt)
+            xd = xp[:, : x.shape[1]]
+        else:
+            xd = x.to(self.device, dt).contiguous()
         yd = torch.as_tensor(y, dtype=torch.float32).reshape(n).to(self.device)
         sd = torch.ones(n, device=self.device) if s is None else \
             torch.as_tensor(s, dtype=torch.float32).reshape(n).to(self.device)
@@ -55,7 +62,14 @@ class LRTrainer:
         x, y, s = data
         g = self.gbuf
         g.zero_()
-        for r0 in range(0, x.shape[0], chunk):
+        if self.device.type == "cuda":
+            from ..ops import stats_ops           # fused HIP pass (K9): dot + sigmoid + gradient
+            r = stats_ops.lr_grad(x, self.w, y, s)
+            if r is not None:
+                g[: self.n_in + 1] = r[0]
+                g[self.n_in + 1] = r[1].float()
+                chunk = 0
+        for r0 in (range(0, x.shape[0], chunk) if chunk else ()):
             xb, yb, sb = x[r0: r0 + chunk], y[r0: r0 + chunk], s[r0: r0 + chunk]
             p = self._score(xb)
             e = yb - p

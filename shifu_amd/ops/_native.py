@@ -44,6 +44,12 @@ HIP_SIGNATURES = {
     "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "l" "s",
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
     "shifu_gbdt_residual": "pppp" "p" "li" "s",
+    # stats_kernels.hip
+    "shifu_column_stats": "plppli" "ppii" "dd" "pipi" "s",
+    "shifu_normalize": "plli" "pppp" "pl" "s",
+    "shifu_bin_codes": "plli" "pp" "pl" "s",
+    "shifu_lr_grad": "plli" "i" "ppp" "pp" "i" "s",
+    "shifu_sensitivity": "plpl" "pp" "f" "p" "l" "iiiii" "p" "s",
 }
 
 # host runtime: name -> (argsig, restype)

@@ -1,0 +1,476 @@
+// Column statistics / normalization / LR / sensitivity kernels for MI355X (gfx950).
+//
+// Replaces the reference's per-row Java loops:
+//   K1+K2  bin index + per-column moments and pos/neg histograms
+//          UpdateBinningInfoMapper.populateStats  J/core/binning/UpdateBinningInfoMapper.java:427-615
+//          UpdateBinningInfoReducer.reduce         J/core/binning/UpdateBinningInfoReducer.java:125-433
+//   K5     normalization (z-score clip / WOE / pos-rate / discrete / index)
+//          Normalizer.normalize / zScoreNormalize / woeNormalize  J/core/Normalizer.java:233-785
+//   K1'    tree bin codes (CleanedData)         DTWorker.getBinIndex J/core/dtrain/dt/DTWorker.java:1001-1034
+//   K9     logistic-regression gradient         LogisticRegressionWorker.doCompute :302-352
+//   K14    sensitivity analysis (1 hidden layer) VarSelectMapper.map J/core/varselect/VarSelectMapper.java:277-333
+//          with CacheFlatNetwork's first-layer cache (S - x_i * W1[:, i])
+//
+// Design notes:
+//   * column-major raw values [F][ldv] fp64 (one column = one contiguous stream, exact double
+//     comparisons against double bin boundaries, same as the Java code); boundaries are staged in
+//     LDS per block and searched branch-free.
+//   * histograms: LDS-privatised integer counters (ds_add_u32 for counts, ds_add_u64 for fixed-
+//     point weights - integer LDS atomics are ~17x faster than ds_add_f32 on gfx950, see
+//     profiles/microbench_lds_atomics.txt) flushed once per block; moments are fp64 wave/block
+//     reductions written as per-block partials (no contended global atomics).
+//   * normalize / bin-codes transpose column-major input to row-major output through a 64x64
+//     LDS tile so both the loads and the stores are coalesced.
+//   * LR: one fused pass over the row-major shard - dot, sigmoid, gradient accumulation in
+//     registers (lane-strided vector loads), block partials reduced on the device.
+#include "common.h"
+
+#define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+namespace {
+
+constexpr int MAXB = 1024;          // max boundaries per column staged in LDS
+
+__device__ __forceinline__ int bin_search(const double* __restrict__ b, int nb, double v) {
+  // number of boundaries <= v, minus one (b[0] = -inf); clipped to [0, nb-1]
+  int lo = 0, hi = nb;                       // invariant: b[lo-1] <= v < b[hi]
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (b[mid] <= v) lo = mid + 1; else hi = mid;
+  }
+  int idx = lo - 1;
+  return idx < 0 ? 0 : (idx > nb - 1 ? nb - 1 : idx);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1+K2: per-column moments + pos/neg histograms
+// ---------------------------------------------------------------------------------------------
+struct StatsArgs {
+  const double* vals; long ldv;
+  const float* y; const double* w; long n;
+  const double* bounds; const int* boff;
+  int binary; double wscale; double num_thr;
+  unsigned long long* hist; int hstride;     // [F][hstride][4]: cpos, cneg, wpos, wneg (fixed point)
+  double* part; int nchunks; long rows_per_chunk;   // [F][nchunks][8]
+};
+
+__global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
+  __shared__ double sb[MAXB];
+  __shared__ unsigned int cp[MAXB + 1], cn[MAXB + 1];
+  __shared__ unsigned long long wp[MAXB + 1], wn[MAXB + 1];
+  __shared__ double red[4][8];
+  const int f = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const int b0 = a.boff[f], nb = a.boff[f + 1] - b0;
+  for (int i = tid; i < nb; i += 256) sb[i] = a.bounds[b0 + i];
+  for (int i = tid; i <= nb; i += 256) { cp[i] = 0; cn[i] = 0; wp[i] = 0ull; wn[i] = 0ull; }
+  __syncthreads();
+  const long r0 = (long)chunk * a.rows_per_chunk;
+  const long r1 = min(a.n, r0 + a.rows_per_chunk);
+  const double* col = a.vals + (long)f * a.ldv;
+  double cnt = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, mn = INFINITY, mx = -INFINITY;
+  for (long r = r0 + tid; r < r1; r += 256) {
+    double v = col[r];
+    if (v > a.num_thr) v = NAN;               // numericalValueThreshold -> invalid
+    int bin;
+    if (v != v) {
+      bin = nb;                               // missing bin
+    } else {
+      bin = bin_search(sb, nb, v);
+      if (isfinite(v)) {
+        double v2 = v * v;
+        cnt += 1.0; s1 += v; s2 += v2; s3 += v2 * v; s4 += v2 * v2;
+        mn = fmin(mn, v); mx = fmax(mx, v);
+      }
+    }
+    const bool pos = !a.binary || a.y[r] > 0.5f;
+    const unsigned long long q = (unsigned long long)__double2ll_rn(a.w[r] * a.wscale);
+    if (pos) { atomicAdd(&cp[bin], 1u); atomicAdd(&wp[bin], q); }
+    else     { atomicAdd(&cn[bin], 1u); atomicAdd(&wn[bin], q); }
+  }
+  // moments: wave then block reduction
+  cnt = wave_sum_d(cnt); s1 = wave_sum_d(s1); s2 = wave_sum_d(s2); s3 = wave_sum_d(s3); s4 = wave_sum_d(s4);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fmin(mn, __shfl_xor(mn, o, 64));
+    mx = fmax(mx, __shfl_xor(mx, o, 64));
+  }
+  const int wid = tid >> 6, lane = tid & 63;
+  if (lane == 0) {
+    red[wid][0] = cnt; red[wid][1] = s1; red[wid][2] = s2; red[wid][3] = s3; red[wid][4] = s4;
+    red[wid][5] = mn; red[wid][6] = mx;
+  }
+  __syncthreads();
+  if (tid < 8) {
+    double acc = red[0][tid];
+    for (int k = 1; k < 4; ++k) {
+      const double v = red[k][tid];
+      acc = tid == 5 ? fmin(acc, v) : (tid == 6 ? fmax(acc, v) : acc + v);
+    }
+    if (tid == 7) acc = 0.0;
+    a.part[((long)f * a.nchunks + chunk) * 8 + tid] = acc;
+  }
+  unsigned long long* h = a.hist + (long)f * a.hstride * 4;
+  for (int i = tid; i <= nb; i += 256) {
+    if (cp[i]) atomicAdd(&h[i * 4 + 0], (unsigned long long)cp[i]);
+    if (cn[i]) atomicAdd(&h[i * 4 + 1], (unsigned long long)cn[i]);
+    if (wp[i]) atomicAdd(&h[i * 4 + 2], wp[i]);
+    if (wn[i]) atomicAdd(&h[i * 4 + 3], wn[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K5: normalization, column-major fp64 in -> row-major fp32 out (LDS-tiled transpose)
+// ---------------------------------------------------------------------------------------------
+enum NormMode : int { NM_ZSCORE = 0, NM_NUM_TABLE = 1, NM_CAT_TABLE = 2, NM_RAW = 3, NM_DISCRETE = 4,
+                      NM_CAT_INDEX = 5 };
+
+struct NormArgs {
+  const double* vals; long ldv; long n; int F;
+  const int* ip;        // [F][8]: mode, out_col, bnd_off, nbnd, tbl_off, ntbl, zflag, 0
+  const double* dp;     // [F][8]: mean, std, cutoff, zmean, zstd, 0, 0, 0
+  const double* bounds; const double* tables;
+  float* out; long ldo;
+};
+
+__device__ __forceinline__ double zclip(double v, double mean, double std, double cutoff) {
+  v = fmin(v, mean + cutoff * std);
+  v = fmax(v, mean - cutoff * std);
+  return std > 0.00001 ? (v - mean) / std : 0.0;
+}
+
+__global__ void __launch_bounds__(256) normalize_kernel(NormArgs a) {
+  __shared__ float tile[64][65];
+  const long r0 = (long)blockIdx.x * 64;
+  const int f0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+  for (int k = ty; k < 64; k += 4) {
+    const int f = f0 + k;
+    const long r = r0 + tx;
+    float res = 0.f;
+    if (f < a.F && r < a.n) {
+      const int* ip = a.ip + f * 8;
+      const double* dp = a.dp + f * 8;
+      const double v = a.vals[(long)f * a.ldv + r];
+      const int mode = ip[0], nbnd = ip[3], ntbl = ip[5];
+      const double* bnd = a.bounds + ip[2];
+      const double* tbl = a.tables + ip[4];
+      double o;
+      switch (mode) {
+        case NM_ZSCORE: o = zclip(isfinite(v) ? v : dp[0], dp[0], dp[1], dp[2]); break;
+        case NM_NUM_TABLE: {
+          int bin = (v != v) ? -1 : bin_search(bnd, nbnd, v);
+          double t = tbl[bin < 0 ? ntbl - 1 : min(bin, ntbl - 1)];
+          o = ip[6] ? zclip(t, dp[3], dp[4], dp[2]) : t;
+          break;
+        }
+        case NM_CAT_TABLE: {
+          int idx = (v != v || v < 0) ? -1 : (int)v;
+          double t = tbl[(idx < 0 || idx >= ntbl) ? ntbl - 1 : idx];
+          o = ip[6] ? zclip(t, dp[3], dp[4], dp[2]) : t;
+          break;
+        }
+        case NM_RAW: o = isfinite(v) ? v : dp[0]; break;
+        case NM_DISCRETE: {
+          int bin = (v != v) ? -1 : bin_search(bnd, nbnd, v);
+          double lo = (bin < 0 || bin >= ntbl) ? dp[0] : tbl[bin];
+          o = zclip(lo, dp[0], dp[1], dp[2]);
+          break;
+        }
+        default: {   // NM_CAT_INDEX
+          int idx = (v != v || v < 0) ? -1 : (int)v;
+          o = (double)(idx < 0 ? ntbl : idx);
+        }
+      }
+      res = (float)o;
+    }
+    tile[k][tx] = res;
+  }
+  __syncthreads();
+  // store: thread (tx = column in tile, ty = row group) -> out[r][out_col]
+  for (int k = ty; k < 64; k += 4) {
+    const long r = r0 + k;
+    const int f = f0 + tx;
+    if (r < a.n && f < a.F) a.out[r * a.ldo + a.ip[f * 8 + 1]] = tile[tx][k];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1': tree bin codes (CleanedData): numeric missing -> bin of 0.0, categorical missing -> ncat
+// ---------------------------------------------------------------------------------------------
+struct CodeArgs {
+  const double* vals; long ldv; long n; int F;
+  const int* ip;        // [F][4]: is_cat, bnd_off, nbnd, ncat
+  const double* bounds;
+  uint8_t* out; long ldo;
+};
+
+__global__ void __launch_bounds__(256) bin_codes_kernel(CodeArgs a) {
+  __shared__ uint8_t tile[64][68];
+  const long r0 = (long)blockIdx.x * 64;
+  const int f0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int k = ty; k < 64; k += 4) {
+    const int f = f0 + k;
+    const long r = r0 + tx;
+    uint8_t c = 0;
+    if (f < a.F && r < a.n) {
+      const int* ip = a.ip + f * 4;
+      double v = a.vals[(long)f * a.ldv + r];
+      if (ip[0]) {
+        int idx = (v != v || v < 0) ? -1 : (int)v;
+        c = (uint8_t)((idx < 0 || idx >= ip[3]) ? ip[3] : idx);
+      } else {
+        if (v != v) v = 0.0;                 // DTWorker.getFloatValue: missing -> 0f
+        c = (uint8_t)bin_search(a.bounds + ip[1], ip[2], v);
+      }
+    }
+    tile[k][tx] = c;
+  }
+  __syncthreads();
+  for (int k = ty; k < 64; k += 4) {
+    const long r = r0 + k;
+    const int f = f0 + tx;
+    if (r < a.n && f < a.F) a.out[r * a.ldo + f] = tile[tx][k];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K9: logistic regression fused gradient (one pass over X)
+// ---------------------------------------------------------------------------------------------
+template <typename T> struct Vec;
+template <> struct Vec<float> { static constexpr int N = 4; };
+template <> struct Vec<bf16_t> { static constexpr int N = 8; };
+
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, float* o);
+template <>
+__device__ __forceinline__ void load_vec<float>(const float* p, float* o) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+template <>
+__device__ __forceinline__ void load_vec<bf16_t>(const bf16_t* p, float* o) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { o[2 * i] = __uint_as_float(u[i] << 16); o[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u); }
+}
+
+struct LrArgs {
+  const void* x; long ldx; long n; int F;
+  const float* w; const float* y; const float* s;
+  float* part; double* err_part;   // [nblk][F+1], [nblk]
+};
+
+template <typename T, int NK>
+__global__ void __launch_bounds__(256) lr_grad_kernel(LrArgs a) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float red[4][NK * 64 * V + 1];
+  __shared__ double ered[4];
+  const T* X = reinterpret_cast<const T*>(a.x);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float wv[NK][V], g[NK][V];
+#pragma unroll
+  for (int i = 0; i < NK; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (i * 64 + lane) * V + j;
+      wv[i][j] = c < a.F ? a.w[c] : 0.f;
+      g[i][j] = 0.f;
+    }
+  const float bias = a.w[a.F];
+  float gb = 0.f;
+  double err = 0.0;
+  const long wave_id = (long)blockIdx.x * 4 + wid, nwaves = (long)gridDim.x * 4;
+  for (long r = wave_id; r < a.n; r += nwaves) {
+    float xv[NK][V];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+      const int c0 = (i * 64 + lane) * V;
+      if (c0 + V <= a.ldx) load_vec<T>(X + r * a.ldx + c0, xv[i]);
+      else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) xv[i][j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if (c0 + j >= a.F) xv[i][j] = 0.f;
+        dot += xv[i][j] * wv[i][j];
+      }
+    }
+    dot = wave_sum(dot);
+    const float p = 1.f / (1.f + __expf(-(dot + bias)));
+    const float e = a.y[r] - p;
+    const float d = e * (p * (1.f - p) + 0.1f) * (a.s ? a.s[r] : 1.f);
+#pragma unroll
+    for (int i = 0; i < NK; ++i)
+#pragma unroll
+      for (int j = 0; j < V; ++j) g[i][j] += d * xv[i][j];
+    gb += d;
+    err += (double)e * e;
+  }
+#pragma unroll
+  for (int i = 0; i < NK; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[wid][(i * 64 + lane) * V + j] = g[i][j];
+  if (lane == 0) { red[wid][NK * 64 * V] = gb; ered[wid] = err; }
+  __syncthreads();
+  float* out = a.part + (long)blockIdx.x * (a.F + 1);
+  for (int c = tid; c < a.F; c += 256) out[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (tid == 0) {
+    const int B = NK * 64 * V;
+    out[a.F] = red[0][B] + red[1][B] + red[2][B] + red[3][B];
+    a.err_part[blockIdx.x] = ered[0] + ered[1] + ered[2] + ered[3];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K14: sensitivity, 1-hidden-layer network: per (row, input f)
+//   d = base[r] - act_o(b2 + sum_j W2[j] * act1(S[r][j] - x[r][f] * W1t[f][j]))
+//   accumulate sum |d|, sum d^2 per input
+// ---------------------------------------------------------------------------------------------
+constexpr int SFT = 32;    // inputs per block
+constexpr int SRT = 8;     // rows per step
+
+struct SensArgs {
+  const float* S; long lds; const float* X; long ldx; const float* W1t; const float* W2; float b2;
+  const float* base; long n; int F; int H; int act_o;
+  long rows_per_chunk; double* acc;   // [F][2]
+};
+
+template <int ACT1>
+__global__ void __launch_bounds__(256) sensitivity_kernel(SensArgs a) {
+  extern __shared__ float smem[];
+  const int H = a.H, HP = H + 1;
+  float* w1 = smem;                      // [SFT][HP]
+  float* w2 = w1 + SFT * HP;             // [H]
+  float* st = w2 + H;                    // [SRT][HP]
+  __shared__ double ra[SRT][SFT], rs[SRT][SFT];
+  const int tid = threadIdx.x, fl = tid % SFT, rl = tid / SFT;
+  const int f0 = blockIdx.y * SFT;
+  for (int i = tid; i < SFT * H; i += 256) {
+    const int ff = i / H, j = i % H;
+    w1[ff * HP + j] = (f0 + ff < a.F) ? a.W1t[(long)(f0 + ff) * H + j] : 0.f;
+  }
+  for (int j = tid; j < H; j += 256) w2[j] = a.W2[j];
+  const long r0 = (long)blockIdx.x * a.rows_per_chunk, r1 = min(a.n, r0 + a.rows_per_chunk);
+  double sa = 0.0, sq = 0.0;
+  const int f = f0 + fl;
+  for (long rb = r0; rb < r1; rb += SRT) {
+    __syncthreads();
+    for (int i = tid; i < SRT * H; i += 256) {
+      const int rr = i / H, j = i % H;
+      st[rr * HP + j] = (rb + rr < r1) ? a.S[(rb + rr) * a.lds + j] : 0.f;
+    }
+    __syncthreads();
+    const long r = rb + rl;
+    if (r < r1 && f < a.F) {
+      const float xf = a.X[r * a.ldx + f];
+      const float* sr = st + rl * HP;
+      const float* wr = w1 + fl * HP;
+      float acc = a.b2;
+      for (int j = 0; j < H; ++j) acc += w2[j] * act_fwd(ACT1, sr[j] - xf * wr[j]);
+      const float d = a.base[r] - act_fwd(a.act_o, acc);
+      sa += fabs((double)d);
+      sq += (double)d * d;
+    }
+  }
+  ra[rl][fl] = sa;
+  rs[rl][fl] = sq;
+  __syncthreads();
+  if (tid < SFT && f0 + tid < a.F) {
+    double x = 0.0, y = 0.0;
+    for (int k = 0; k < SRT; ++k) { x += ra[k][tid]; y += rs[k][tid]; }
+    atomicAdd(&a.acc[(long)(f0 + tid) * 2], x);
+    atomicAdd(&a.acc[(long)(f0 + tid) * 2 + 1], y);
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// C API
+// ---------------------------------------------------------------------------------------------
+SHIFU_API int shifu_column_stats(const double* vals, long ldv, const float* y, const double* w, long n, int F,
+                                 const double* bounds, const int* boff, int max_nb, int binary, double wscale,
+                                 double num_thr, void* hist, int hstride, double* part, int nchunks,
+                                 hipStream_t stream) {
+  if (max_nb > MAXB || hstride < max_nb + 1 || nchunks <= 0 || F <= 0) return -1;
+  StatsArgs a{vals, ldv, y, w, n, bounds, boff, binary, wscale, num_thr, (unsigned long long*)hist, hstride,
+              part, nchunks, (n + nchunks - 1) / nchunks};
+  hipLaunchKernelGGL(column_stats_kernel, dim3(nchunks, F), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_normalize(const double* vals, long ldv, long n, int F, const int* ip, const double* dp,
+                              const double* bounds, const double* tables, float* out, long ldo, hipStream_t stream) {
+  if (n <= 0 || F <= 0) return 0;
+  NormArgs a{vals, ldv, n, F, ip, dp, bounds, tables, out, ldo};
+  hipLaunchKernelGGL(normalize_kernel, dim3((n + 63) / 64, (F + 63) / 64), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_bin_codes(const double* vals, long ldv, long n, int F, const int* ip, const double* bounds,
+                              void* out, long ldo, hipStream_t stream) {
+  if (n <= 0 || F <= 0) return 0;
+  CodeArgs a{vals, ldv, n, F, ip, bounds, (uint8_t*)out, ldo};
+  hipLaunchKernelGGL(bin_codes_kernel, dim3((n + 63) / 64, (F + 63) / 64), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+static int lr_dispatch(int nk, dim3 g, hipStream_t s, const LrArgs& a) {
+  switch (nk) {
+    case 1: hipLaunchKernelGGL((lr_grad_kernel<T, 1>), g, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((lr_grad_kernel<T, 2>), g, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((lr_grad_kernel<T, 3>), g, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((lr_grad_kernel<T, 4>), g, dim3(256), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((lr_grad_kernel<T, 5>), g, dim3(256), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((lr_grad_kernel<T, 6>), g, dim3(256), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((lr_grad_kernel<T, 7>), g, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((lr_grad_kernel<T, 8>), g, dim3(256), 0, s, a); break;
+    default: return -2;
+  }
+  return 0;
+}
+
+// dtype: 0 = fp32 rows (ldx % 4 == 0), 1 = bf16 rows (ldx % 8 == 0); F <= 2048 / 4096
+SHIFU_API int shifu_lr_grad(const void* x, long ldx, long n, int F, int dtype, const float* w, const float* y,
+                            const float* s, float* part, double* err_part, int nblk, hipStream_t stream) {
+  const int V = dtype ? 8 : 4;
+  if (ldx % V || F <= 0 || nblk <= 0) return -1;
+  const int nk = (F + 64 * V - 1) / (64 * V);
+  LrArgs a{x, ldx, n, F, w, y, s, part, err_part};
+  int rc = dtype ? lr_dispatch<bf16_t>(nk, dim3(nblk), stream, a) : lr_dispatch<float>(nk, dim3(nblk), stream, a);
+  if (rc) return rc;
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_sensitivity(const float* S, long lds, const float* X, long ldx, const float* W1t, const float* W2,
+                                float b2, const float* base, long n, int F, int H, int act1, int act_o, int nchunks,
+                                double* acc, hipStream_t stream) {
+  if (H <= 0 || H > 1024 || n <= 0 || nchunks <= 0) return -1;
+  SensArgs a{S, lds, X, ldx, W1t, W2, b2, base, n, F, H, act_o, (n + nchunks - 1) / nchunks, acc};
+  const size_t sm = (size_t)(SFT * (H + 1) + H + SRT * (H + 1)) * sizeof(float);
+  if (sm > 150 * 1024) return -3;
+  dim3 g(nchunks, (F + SFT - 1) / SFT);
+  switch (act1) {
+    case ACT_SIGMOID: hipLaunchKernelGGL(sensitivity_kernel<ACT_SIGMOID>, g, dim3(256), sm, stream, a); break;
+    case ACT_TANH: hipLaunchKernelGGL(sensitivity_kernel<ACT_TANH>, g, dim3(256), sm, stream, a); break;
+    case ACT_LINEAR: hipLaunchKernelGGL(sensitivity_kernel<ACT_LINEAR>, g, dim3(256), sm, stream, a); break;
+    case ACT_RELU: hipLaunchKernelGGL(sensitivity_kernel<ACT_RELU>, g, dim3(256), sm, stream, a); break;
+    case ACT_LEAKYRELU: hipLaunchKernelGGL(sensitivity_kernel<ACT_LEAKYRELU>, g, dim3(256), sm, stream, a); break;
+    case ACT_SWISH: hipLaunchKernelGGL(sensitivity_kernel<ACT_SWISH>, g, dim3(256), sm, stream, a); break;
+    case ACT_PTANH: hipLaunchKernelGGL(sensitivity_kernel<ACT_PTANH>, g, dim3(256), sm, stream, a); break;
+    case ACT_LOG: hipLaunchKernelGGL(sensitivity_kernel<ACT_LOG>, g, dim3(256), sm, stream, a); break;
+    case ACT_SIN: hipLaunchKernelGGL(sensitivity_kernel<ACT_SIN>, g, dim3(256), sm, stream, a); break;
+    default: return -2;
+  }
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}

@@ -1,0 +1,139 @@
+"""Python side of ``stats_kernels.hip`` (K1/K2/K5/K9/K14): packs per-column parameters,
+launches the HIP kernels on the current stream and unpacks results.  Every function here
+requires the native library (``_native.require_gpu_native``) — there is no silent fallback;
+callers choose the CPU oracle explicitly when no GPU is present."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+NM = {"zscore": 0, "num_table": 1, "cat_table": 2, "raw": 3, "discrete": 4, "cat_index": 5}
+
+
+def _dev_tensor(a, dtype, dev):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).to(dev)
+
+
+def pack_bounds(bounds_list):
+    offs = [0]
+    flat = []
+    for b in bounds_list:
+        b = list(b) if b is not None and len(b) else [float("-inf")]
+        flat.extend(float(x) for x in b)
+        offs.append(len(flat))
+    return np.asarray(flat if flat else [0.0], np.float64), np.asarray(offs, np.int32)
+
+
+def column_stats(vals: torch.Tensor, y: torch.Tensor, w: torch.Tensor, bounds_list, binary: bool,
+                 num_thr: float = 1.7976931348623157e308, nchunks: int | None = None):
+    """vals [F, N] fp64 (column-major) on the GPU -> per column (cpos, cneg, wpos, wneg) numpy
+    arrays of length nb+1 (missing bin last) and moments (count, s1..s4, min, max)."""
+    nat.require_gpu_native()
+    F, N = vals.shape
+    dev = vals.device
+    bflat, boff = pack_bounds(bounds_list)
+    max_nb = int(np.max(np.diff(boff))) if F else 1
+    if max_nb > 1024:
+        raise ValueError("column_stats: more than 1024 bin boundaries per column")
+    hstride = max_nb + 1
+    wmax = float(w.abs().max().item()) if N else 1.0
+    wscale = 2.0 ** min(40, math.floor(62 - math.log2(max(wmax, 1e-30) * max(N, 1))))
+    nchunks = nchunks or max(1, min(256, (N + 65535) // 65536))
+    hist = torch.zeros(F * hstride * 4, dtype=torch.int64, device=dev)
+    part = torch.zeros(F * nchunks * 8, dtype=torch.float64, device=dev)
+    bt, ot = _dev_tensor(bflat, torch.float64, dev), _dev_tensor(boff, torch.int32, dev)
+    rc = nat.call_hip("shifu_column_stats", vals, vals.stride(0), y, w, N, F, bt, ot, max_nb, int(binary), wscale,
+                      float(num_thr), hist, hstride, part, nchunks, nat.stream_of(vals))
+    if rc:
+        raise RuntimeError(f"shifu_column_stats failed rc={rc}")
+    h = hist.view(F, hstride, 4).cpu().numpy()
+    p = part.view(F, nchunks, 8).cpu().numpy()
+    out = []
+    for f in range(F):
+        nb = int(boff[f + 1] - boff[f])
+        hh = h[f, : nb + 1]
+        mom = (int(p[f, :, 0].sum()), float(p[f, :, 1].sum()), float(p[f, :, 2].sum()), float(p[f, :, 3].sum()),
+               float(p[f, :, 4].sum()), float(p[f, :, 5].min()), float(p[f, :, 6].max()))
+        if mom[0] == 0:
+            mom = (0, 0.0, 0.0, 0.0, 0.0, float("nan"), float("nan"))
+        out.append((hh[:, 0].astype(np.int64), hh[:, 1].astype(np.int64), hh[:, 2] / wscale, hh[:, 3] / wscale, mom))
+    return out
+
+
+def normalize(vals: torch.Tensor, specs: list, out: torch.Tensor):
+    """vals [F, N] fp64; specs[f] = dict(mode, out_col, bounds, table, mean, std, cutoff, zflag,
+    zmean, zstd); out [N, ldo] fp32 (written in place)."""
+    nat.require_gpu_native()
+    F, N = vals.shape
+    dev = vals.device
+    ip = np.zeros((F, 8), np.int32)
+    dp = np.zeros((F, 8), np.float64)
+    bounds, tables = [], []
+    for f, s in enumerate(specs):
+        b = list(s.get("bounds") or [float("-inf")])
+        t = list(s.get("table") or [0.0])
+        nt = int(s["ncat"]) if s["mode"] == "cat_index" else len(t)
+        ip[f] = [NM[s["mode"]], s["out_col"], len(bounds), len(b), len(tables), nt, int(s.get("zflag", 0)), 0]
+        bounds.extend(b)
+        tables.extend(t)
+        dp[f, :5] = [s.get("mean", 0.0) or 0.0, s.get("std", 0.0) or 0.0, s.get("cutoff", 6.0),
+                     s.get("zmean", 0.0) or 0.0, s.get("zstd", 0.0) or 0.0]
+    rc = nat.call_hip("shifu_normalize", vals, vals.stride(0), N, F, _dev_tensor(ip, torch.int32, dev),
+                      _dev_tensor(dp, torch.float64, dev), _dev_tensor(np.asarray(bounds, np.float64), torch.float64, dev),
+                      _dev_tensor(np.asarray(tables, np.float64), torch.float64, dev), out, out.stride(0),
+                      nat.stream_of(vals))
+    if rc:
+        raise RuntimeError(f"shifu_normalize failed rc={rc}")
+    return out
+
+
+def bin_codes(vals: torch.Tensor, is_cat, bounds_list, ncat, out: torch.Tensor):
+    """Tree bin codes uint8 [N, ldo] from column-major fp64 values."""
+    nat.require_gpu_native()
+    F, N = vals.shape
+    dev = vals.device
+    bflat, boff = pack_bounds(bounds_list)
+    ip = np.zeros((F, 4), np.int32)
+    for f in range(F):
+        ip[f] = [int(is_cat[f]), boff[f], boff[f + 1] - boff[f], int(ncat[f])]
+    rc = nat.call_hip("shifu_bin_codes", vals, vals.stride(0), N, F, _dev_tensor(ip, torch.int32, dev),
+                      _dev_tensor(bflat, torch.float64, dev), out, out.stride(0), nat.stream_of(vals))
+    if rc:
+        raise RuntimeError(f"shifu_bin_codes failed rc={rc}")
+    return out
+
+
+def lr_grad(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, s: torch.Tensor | None, nblk: int = 1024):
+    """Fused LR gradient pass -> (grad [F+1] fp32 (ascent, bias last), sum squared error)."""
+    nat.require_gpu_native()
+    n, ldx = x.shape[0], x.stride(0)
+    F = w.numel() - 1
+    dtype = 1 if x.dtype == torch.bfloat16 else 0
+    lim = 4096 if dtype else 2048
+    if F > lim or ldx % (8 if dtype else 4):
+        return None
+    nblk = max(1, min(nblk, (n + 3) // 4))
+    part = torch.empty(nblk, F + 1, dtype=torch.float32, device=x.device)
+    ep = torch.empty(nblk, dtype=torch.float64, device=x.device)
+    rc = nat.call_hip("shifu_lr_grad", x, ldx, n, F, dtype, w, y, s, part, ep, nblk, nat.stream_of(x))
+    if rc:
+        raise RuntimeError(f"shifu_lr_grad failed rc={rc}")
+    return part.sum(0), ep.sum()
+
+
+def sensitivity_1h(S: torch.Tensor, X: torch.Tensor, W1t: torch.Tensor, W2: torch.Tensor, b2: float,
+                   base: torch.Tensor, act1: int, act_o: int, acc: torch.Tensor, nchunks: int | None = None):
+    """Accumulate sum|d| and sum d^2 per input into ``acc`` [F, 2] fp64 (1-hidden-layer nets)."""
+    nat.require_gpu_native()
+    n, H = S.shape
+    F = X.shape[1]
+    nchunks = nchunks or max(1, min(512, (n + 255) // 256))
+    rc = nat.call_hip("shifu_sensitivity", S, S.stride(0), X, X.stride(0), W1t, W2, float(b2), base, n, F, H,
+                      int(act1), int(act_o), nchunks, acc, nat.stream_of(S))
+    if rc:
+        raise RuntimeError(f"shifu_sensitivity failed rc={rc}")
+    return acc

@@ -16,6 +16,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..algos import normalize as N
+from ..utils.device import is_gpu_available
 from ..utils.log import get_logger
 from .base import ModelSet, save_dataset
 
@@ -34,8 +35,10 @@ def _norm_one(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_o
     meta = {"n": int(md.n), "columns": [c.name for c in cols], "column_nums": [c.num for c in cols],
             "counters": md.counters.as_dict(), "is_binary": mc.is_binary(), "tags": mc.flatten_tags(),
             "shuffled": bool(shuffle)}
+    gpu = is_gpu_available()
     if is_tree:
-        C, nb, is_cat = N.tree_bin_codes(ms.ccs, md.table, cols)
+        r = N.tree_bin_codes_gpu(ms.ccs, md.table, cols) if gpu else None
+        C, nb, is_cat = r if r is not None else N.tree_bin_codes(ms.ccs, md.table, cols)
         dt = np.uint8 if (nb.max(initial=1) <= 256) else np.int16
         C = C.astype(dt)
         if perm is not None:
@@ -43,7 +46,7 @@ def _norm_one(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_o
         meta.update(nbins=nb.tolist(), is_cat=is_cat.tolist())
         save_dataset(out_tree, {"codes": C, "y": y, "w": w}, meta)
         _log.info("CleanedData: %s rows x %s cols -> %s", *C.shape, out_tree)
-    X, names, nums = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+    X, names, nums = (N.normalize_table_gpu if gpu else N.normalize_table)(mc, ms.ccs, md.table, columns=cols)
     if perm is not None:
         X = X[perm]
     meta.update(norm_type=mc.norm_type, input_names=names, input_nums=nums)

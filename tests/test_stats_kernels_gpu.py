@@ -1,0 +1,115 @@
+"""HIP stats / normalize / bin-code / LR / sensitivity kernels vs the fp64 CPU oracles."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+NORMS = ["ZSCALE", "OLD_ZSCALE", "WOE", "WEIGHT_WOE", "WOE_ZSCORE", "WEIGHT_WOE_ZSCALE", "HYBRID", "ONEHOT",
+         "ZSCALE_ONEHOT", "ASIS_WOE", "ASIS_PR", "DISCRETE_ZSCORE", "ZSCALE_INDEX", "WOE_INDEX", "WOE_ZSCALE_INDEX"]
+
+
+@pytest.fixture(scope="module")
+def prepared(tmp_path_factory):
+    from shifu_amd.steps.base import ModelSet
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path_factory.mktemp("k")), "k", "NN", n_rows=5000)
+    from shifu_amd.cli import main
+    import os
+    cwd = os.getcwd()
+    os.chdir(root)
+    try:
+        assert main(["init"]) == 0
+    finally:
+        os.chdir(cwd)
+    ms = ModelSet(root)
+    cols = [c for c in ms.ccs if not c.is_target() and not c.is_meta() and not c.is_weight()]
+    md = ms.load_raw(cols)
+    return ms, cols, md
+
+
+def test_column_stats_gpu_matches_cpu(prepared):
+    import copy
+    from shifu_amd.algos.stats import compute_column_stats
+    ms, cols, md = prepared
+    a = copy.deepcopy(ms.ccs)
+    b = copy.deepcopy(ms.ccs)
+    compute_column_stats(ms.mc, a, md, device="cpu")
+    compute_column_stats(ms.mc, b, md, device="cuda")
+    for ca, cb in zip(a, b):
+        if ca.is_target() or ca.is_meta():
+            continue
+        assert ca.bin_boundary == cb.bin_boundary and ca.bin_category == cb.bin_category
+        assert ca.bin_count_pos == cb.bin_count_pos and ca.bin_count_neg == cb.bin_count_neg, ca.name
+        np.testing.assert_allclose(ca.bin_weighted_pos, cb.bin_weighted_pos, rtol=1e-9)
+        for k in ("mean", "stdDev", "min", "max", "skewness", "kurtosis", "ks", "iv", "median", "distinctCount"):
+            va, vb = ca.stats.get(k), cb.stats.get(k)
+            if va is None:
+                assert vb is None
+            else:
+                assert vb == pytest.approx(va, rel=1e-9, abs=1e-9), (ca.name, k)
+
+
+@pytest.mark.parametrize("nt", NORMS)
+def test_normalize_gpu_matches_cpu(prepared, nt):
+    import copy
+    from shifu_amd.algos.normalize import normalize_table, normalize_table_gpu
+    from shifu_amd.algos.stats import compute_column_stats
+    ms, cols, md = prepared
+    ccs = copy.deepcopy(ms.ccs)
+    compute_column_stats(ms.mc, ccs, md, device="cpu")
+    c2 = [c for c in ccs if c.name in {x.name for x in cols}]
+    X1, n1, _ = normalize_table(ms.mc, ccs, md.table, columns=c2, norm_type=nt)
+    X2, n2, _ = normalize_table_gpu(ms.mc, ccs, md.table, columns=c2, norm_type=nt)
+    assert n1 == n2
+    np.testing.assert_allclose(X2, X1, rtol=1e-6, atol=1e-6)
+
+
+def test_bin_codes_gpu_matches_cpu(prepared):
+    import copy
+    from shifu_amd.algos.normalize import tree_bin_codes, tree_bin_codes_gpu
+    from shifu_amd.algos.stats import compute_column_stats
+    ms, cols, md = prepared
+    ccs = copy.deepcopy(ms.ccs)
+    compute_column_stats(ms.mc, ccs, md, device="cpu")
+    c2 = [c for c in ccs if c.name in {x.name for x in cols}]
+    C1, nb1, ic1 = tree_bin_codes(ccs, md.table, c2)
+    C2, nb2, ic2 = tree_bin_codes_gpu(ccs, md.table, c2)
+    np.testing.assert_array_equal(C1, C2)
+    np.testing.assert_array_equal(nb1, nb2)
+
+
+@pytest.mark.parametrize("dtype,F", [(torch.float32, 37), (torch.float32, 1000), (torch.bfloat16, 1000)])
+def test_lr_grad_kernel(dtype, F):
+    from shifu_amd.ops import stats_ops
+    g = torch.Generator().manual_seed(0)
+    n = 20000
+    fp = (F + 7) // 8 * 8
+    xp = torch.zeros(n, fp, dtype=dtype, device="cuda")
+    xp[:, :F] = torch.randn(n, F, generator=g).to("cuda", dtype)
+    x = xp[:, :F]
+    w = (torch.randn(F + 1, generator=g) * 0.05).cuda()
+    y = (torch.rand(n, generator=g) > 0.5).float().cuda()
+    s = torch.rand(n, generator=g).cuda()
+    grad, err = stats_ops.lr_grad(x, w, y, s)
+    xf = x.float().double()
+    p = torch.sigmoid(xf @ w[:-1].double() + w[-1].double())
+    e = y.double() - p
+    d = e * (p * (1 - p) + 0.1) * s.double()
+    ref = torch.cat([d @ xf, d.sum()[None]])
+    torch.testing.assert_close(grad.double(), ref, rtol=2e-3, atol=2e-3)
+    assert float(err) == pytest.approx(float((e * e).sum()), rel=1e-4)
+
+
+@pytest.mark.parametrize("act", ["tanh", "sigmoid", "relu"])
+def test_sensitivity_kernel_matches_torch(act):
+    from shifu_amd.algos import varsel as V
+    from shifu_amd.formats.nn_format import NNNetwork
+    rng = np.random.default_rng(0)
+    F, H = 40, 24
+    net = NNNetwork([F, H, 1], [act, "sigmoid"], [rng.normal(size=(H, F + 1)) * 0.3, rng.normal(size=(1, H + 1))])
+    X = rng.normal(size=(3000, F)).astype(np.float32)
+    m1, r1, _ = V.sensitivity(net, X, device=torch.device("cpu"))
+    m2, r2, _ = V.sensitivity(net, X, device=torch.device("cuda"))
+    np.testing.assert_allclose(m2, m1, rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(r2, r1, rtol=2e-4, atol=1e-6)
