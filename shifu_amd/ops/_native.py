@@ -33,6 +33,8 @@ HIP_SIGNATURES = {
     # mlp_kernels.hip
     "shifu_gemm_nt": "plplipl" "plplpl" "iiiiiiif" "s",
     "shifu_wgrad_tn": "plplpl" "iiiis",
+    "shifu_gemm_set_stages": "i",
+    "shifu_gemm_set_big": "i",
     "shifu_mlp_output": "plplppl" "pplpppl" "iiiiiii" "ff" "s",
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
     "shifu_cast_bf16": "plpliis",

@@ -42,15 +42,27 @@ enum Act : int {
   ACT_SWISH = 5, ACT_PTANH = 6, ACT_LOG = 7, ACT_SIN = 8
 };
 
+// Fast transcendental forms (v_exp_f32 + v_rcp_f32): the outputs are rounded to bf16 (8-bit
+// mantissa) right after, so the ~1 ulp fp32 error of rcp/exp is invisible; tanh uses an odd
+// polynomial near 0 to avoid the 1 - 2/(e^2x + 1) cancellation.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_sigmoid(float x) { return fast_rcp(1.f + __expf(-x)); }
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float x2 = x * x;
+  const float poly = x * (1.f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * (-0.0539682540f + x2 * 0.0218694885f))));
+  const float big = 1.f - 2.f * fast_rcp(__expf(2.f * x) + 1.f);
+  return fabsf(x) < 0.3f ? poly : big;
+}
+
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
-    case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
-    case ACT_TANH: return tanhf(x);
+    case ACT_SIGMOID: return fast_sigmoid(x);
+    case ACT_TANH: return fast_tanh(x);
     case ACT_LINEAR: return x;
     case ACT_RELU: return x <= 0.f ? 0.f : x;
     case ACT_LEAKYRELU: return x <= 0.f ? 0.01f * x : x;
-    case ACT_SWISH: return x / (1.f + __expf(-x));
-    case ACT_PTANH: return x > 0.f ? tanhf(x) : 0.25f * tanhf(x);   // ActivationPTANH.java:54-59
+    case ACT_SWISH: return x * fast_sigmoid(x);
+    case ACT_PTANH: return x > 0.f ? fast_tanh(x) : 0.25f * fast_tanh(x);   // ActivationPTANH.java:54-59
     case ACT_LOG: return x >= 0.f ? __logf(1.f + x) : -__logf(1.f - x);
     case ACT_SIN: return __sinf(x);
   }

@@ -50,7 +50,10 @@ struct GemmArgs {
   float flat;
 };
 
-template <int EPI, int ACT>
+// STAGES = LDS buffers.  1: single 32 KiB buffer + register prefetch (two barriers per k-step,
+// up to 5 blocks = 5 waves/SIMD per CU -> the HBM/L2 latency of the next tile is hidden by the
+// other resident blocks); 2: classic LDS double buffer (64 KiB, 2 blocks per CU).
+template <int EPI, int ACT, int STAGES>
 __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntn = (p.N + BN - 1) / BN;
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
   swrite(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
+    const int buf = STAGES == 2 ? (kt & 1) : 0;
     if (kt + 1 < nk) gload((kt + 1) * BK);        // issue next tile's HBM loads early
     const char* As = smem + buf * 2 * TILE_BYTES;
     const char* Bs = As + TILE_BYTES;
@@ -109,13 +112,74 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) swrite(buf ^ 1);
+    if constexpr (STAGES == 1) __syncthreads();     // every wave is done reading the buffer
+    if (kt + 1 < nk) swrite(STAGES == 2 ? (buf ^ 1) : 0);
     __syncthreads();
   }
 
   // Epilogue.  acc[i][j] holds D[n][m]: m = lane&15 (+16j), n = 4*(lane>>4) + r (+16i):
-  // each lane owns 4 consecutive output columns of one row -> one 8-byte store.
+  // each lane owns 4 consecutive output columns of one row.
   constexpr bool dfo = act_deriv_from_output(ACT);
+  if constexpr ((EPI == EPI_ACT || EPI == EPI_DACT) && dfo || EPI == EPI_STORE) {
+    // Staged epilogue: phase 1 packs the tile (bf16) into LDS with a 16-B chunk XOR swizzle,
+    // phase 2 writes whole 256-B row segments with 16-B stores (and, for dgrad, reads the
+    // matching H row segment coalesced) instead of 16 rows x 32 B per wave instruction.
+    char* Cs = smem;                       // [128][256 B]; loop's last barrier freed the tiles
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;       // local column (multiple of 4)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ml = wr * 64 + j * 16 + (lane & 15);
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = acc[i][j][r];
+          if constexpr (EPI == EPI_ACT) {
+            const int n = n0 + nl + r;
+            o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
+          } else {
+            o[r] = z;
+          }
+        }
+        uint2 w;
+        w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+        w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        const int c = nl >> 3, half = (nl >> 2) & 1;
+        *(uint2*)(Cs + ml * 256 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
+      }
+    }
+    __syncthreads();
+    const int c = tid & 15;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int ml = pass * 16 + (tid >> 4);
+      const int m = m0 + ml, n = n0 + c * 8;
+      if (m >= p.M || n >= p.N) continue;
+      uint4 v = *(const uint4*)(Cs + ml * 256 + ((c ^ (ml & 15)) << 4));
+      if constexpr (EPI == EPI_DACT) {
+        const uint4 h = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+        const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
+        uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float a0 = bf2f(vv[q] & 0xffff), a1 = bf2f(vv[q] >> 16);
+          const float d0 = act_deriv_out(ACT, bf2f(hv[q] & 0xffff)) + p.flat;
+          const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
+          a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
+          a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
+          vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+        }
+        v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+      }
+      if (n + 8 <= p.N) {
+        *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
+      } else {                                             // N % 8 == 4 tail
+        *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
+      }
+    }
+    return;
+  } else {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int nb = n0 + wc * 64 + i * 16 + (lane >> 4) * 4;
@@ -131,37 +195,294 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
         for (int r = 0; r < 4; ++r) {
           const int n = nb + r;
           const float z = acc[i][j][r];
-          if (n < p.n_valid) { o[r] = act_fwd(ACT, z); if constexpr (!dfo) d[r] = act_deriv_pre(ACT, z) + p.flat; else d[r] = 0.f; }
+          if (n < p.n_valid) { o[r] = act_fwd(ACT, z); d[r] = act_deriv_pre(ACT, z) + p.flat; }
           else { o[r] = (n == p.n_valid && p.bias_col) ? 1.f : 0.f; d[r] = 0.f; }
         }
-        if constexpr (!dfo) {
-          uint2 w2;
-          w2.x = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
-          w2.y = (uint32_t)f2bf(d[2]) | ((uint32_t)f2bf(d[3]) << 16);
-          *(uint2*)(p.C2 + (size_t)m * p.ldc2 + nb) = w2;
-        }
-      } else if constexpr (EPI == EPI_DACT) {
-        float dv[4];
-        if constexpr (dfo) {
-          const uint2 h = *(const uint2*)(p.H + (size_t)m * p.ldh + nb);
-          const float hv[4] = {bf2f(h.x & 0xffff), bf2f(h.x >> 16), bf2f(h.y & 0xffff), bf2f(h.y >> 16)};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dv[r] = act_deriv_out(ACT, hv[r]) + p.flat;
-        } else {
-          const uint2 h = *(const uint2*)(p.Hd + (size_t)m * p.ldhd + nb);
-          dv[0] = bf2f(h.x & 0xffff); dv[1] = bf2f(h.x >> 16); dv[2] = bf2f(h.y & 0xffff); dv[3] = bf2f(h.y >> 16);
-        }
+        uint2 w2;
+        w2.x = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
+        w2.y = (uint32_t)f2bf(d[2]) | ((uint32_t)f2bf(d[3]) << 16);
+        *(uint2*)(p.C2 + (size_t)m * p.ldc2 + nb) = w2;
+      } else {   // EPI_DACT with a stored derivative (activations not derivable from the output)
+        const uint2 h = *(const uint2*)(p.Hd + (size_t)m * p.ldhd + nb);
+        const float dv[4] = {bf2f(h.x & 0xffff), bf2f(h.x >> 16), bf2f(h.y & 0xffff), bf2f(h.y >> 16)};
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = (nb + r < p.n_valid) ? acc[i][j][r] * dv[r] : 0.f;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r];
       }
       uint2 w;
       w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
       w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
       *(uint2*)(p.C + (size_t)m * p.ldc + nb) = w;
     }
+  }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Big-tile NT GEMM: 256 x 256 x 64 per 512-thread block (8 waves, 2 x 4, each wave 128 x 64).
+// Halves the L2->CU bytes per FLOP of the 128 x 128 kernel (128 FLOP/B), one LDS stage
+// (64 KiB) + register prefetch of the next k-tile; staged epilogue in two 128-row halves.
+// Dfo activations / dgrad / store only (the stored-derivative variants use gemm_nt_kernel).
+// ---------------------------------------------------------------------------------------
+constexpr int GB_M = 256, GB_N = 256, GB_T = 512;
+constexpr int GB_TILE = GB_M * BK * 2;       // 32 KiB per operand
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(GB_T, 1) void gemm_nt_big_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = (p.N + GB_N - 1) / GB_N;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * GB_M, n0 = (wg % ntn) * GB_N;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  char* As = smem;
+  char* Bs = smem + GB_TILE;
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + i * GB_T, row = idx >> 3, ch = idx & 7;
+      const int gm = m0 + row, gn = n0 + row;
+      ra[i] = gm < p.M ? *(const uint4*)(p.A + (size_t)gm * p.lda + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
+      rb[i] = gn < p.NB ? *(const uint4*)(p.B + (size_t)gn * p.ldb + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto swrite = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + i * GB_T, row = idx >> 3, ch = idx & 7;
+      *(uint4*)(As + swz_nt(row, ch)) = ra[i];
+      *(uint4*)(Bs + swz_nt(row, ch)) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  gload(0);
+  swrite();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = s * 4 + (lane >> 4);
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) af[j] = *(const bf16x8*)(As + swz_nt(wr * 128 + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bfr[i] = *(const bf16x8*)(Bs + swz_nt(wc * 64 + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (kt + 1 < nk) swrite();
+    __syncthreads();
+  }
+
+  // staged epilogue, two halves of 128 rows; LDS image [128 rows][512 B], 16-B chunk swizzle
+  char* Cs = smem;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wr == h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int ml = j * 16 + (lane & 15);
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z = acc[i][j][r];
+            if constexpr (EPI == EPI_ACT) {
+              const int n = n0 + nl + r;
+              o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
+            } else {
+              o[r] = z;
+            }
+          }
+          uint2 w;
+          w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+          w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+          const int c = nl >> 3, half = (nl >> 2) & 1;
+          *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
+        }
+      }
+    }
+    __syncthreads();
+    const int c = tid & 31;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int ml = pass * 16 + (tid >> 5);
+      const int m = m0 + h * 128 + ml, n = n0 + c * 8;
+      if (m < p.M && n < p.N) {
+        uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
+        if constexpr (EPI == EPI_DACT) {
+          const uint4 hh = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+          const uint32_t hv[4] = {hh.x, hh.y, hh.z, hh.w};
+          uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float a0 = bf2f(vv[q] & 0xffff), a1 = bf2f(vv[q] >> 16);
+            const float d0 = act_deriv_out(ACT, bf2f(hv[q] & 0xffff)) + p.flat;
+            const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
+            a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
+            a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
+            vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+          }
+          v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+        }
+        if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
+        else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Pipelined NT GEMM with LDS-DMA (global_load_lds_dwordx4): 256 x 256 tile, BK = 32, a ring of
+// 4 LDS stages (4 x 32 KiB) with 3 k-tiles in flight.  8 waves (2 M x 4 N, 128 x 64 each),
+// ONE raw s_barrier per k-step, counted vmcnt waits (never 0 inside the loop), no staging
+// VGPRs.  The LDS image is written linearly by the DMA (wave base + lane x 16 B); the 16-B
+// chunk swizzle chunk ^ ((row >> 2) & 3) is applied as the inverse permutation on the GLOBAL
+// source address and again on the ds_read address (an involution), which makes the 16-lane
+// groups of the fragment ds_read_b128 conflict-free on the 64-B rows.
+// ---------------------------------------------------------------------------------------
+constexpr int GP_M = 256, GP_N = 256, GP_K = 32, GP_T = 512, GP_ST = 4;
+constexpr int GP_OP = GP_M * GP_K * 2;          // 16 KiB per operand per stage
+constexpr int GP_STAGE = 2 * GP_OP;             // 32 KiB
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ int swz32(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(GP_T, 1) void gemm_nt_pipe_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = (p.N + GP_N - 1) / GP_N;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * GP_M, n0 = (wg % ntn) * GP_N;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nk = p.K / GP_K;
+
+  // per-lane global source rows/chunks of the 2 DMA instructions per operand (fixed per thread)
+  const bf16_t* srcA[2];
+  const bf16_t* srcB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int P = i * 8192 + wid * 1024 + lane * 16;      // physical byte in the operand image
+    const int row = P >> 6, pch = (P >> 4) & 3;
+    const int lch = pch ^ ((row >> 2) & 3);                // logical chunk stored at P
+    const int gm = min(m0 + row, p.M - 1), gn = min(n0 + row, p.NB - 1);
+    srcA[i] = p.A + (size_t)gm * p.lda + lch * 8;
+    srcB[i] = p.B + (size_t)gn * p.ldb + lch * 8;
+  }
+  auto issue = [&](int st) {
+    char* base = smem + (st & (GP_ST - 1)) * GP_STAGE;
+    const int k0 = st * GP_K;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[i] + k0), (lds_ptr_t)(base + i * 8192 + wid * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[i] + k0), (lds_ptr_t)(base + GP_OP + i * 8192 + wid * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire this k-tile's DMA (the younger ones stay in flight), then make every wave's land visible
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 3 < nk) issue(kt + 3);         // into the stage every wave finished reading last step
+    const char* As = smem + (kt & (GP_ST - 1)) * GP_STAGE;
+    const char* Bs = As + GP_OP;
+    const int ch = lane >> 4;
+    bf16x8 af[8], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bfr[i] = *(const bf16x8*)(Bs + swz32(wc * 64 + i * 16 + (lane & 15), ch));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) af[j] = *(const bf16x8*)(As + swz32(wr * 128 + j * 16 + (lane & 15), ch));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();             // every wave done reading the ring (DMA drained: vmcnt(0))
+  __builtin_amdgcn_sched_barrier(0);
+
+  // staged epilogue: whole 256 x 256 bf16 tile in LDS ([256][512 B], 16-B chunk ^ (row & 15))
+  char* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ml = wr * 128 + j * 16 + (lane & 15);
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = acc[i][j][r];
+        const int n = n0 + nl + r;
+        if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
+        else if constexpr (EPI == EPI_STORE) o[r] = n < p.NB ? z : 0.f;
+        else o[r] = z;
+      }
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+      w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+      const int c = nl >> 3, half = (nl >> 2) & 1;
+      *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
+    }
+  }
+  __syncthreads();
+  const int c = tid & 31;
+#pragma unroll 4
+  for (int pass = 0; pass < 16; ++pass) {
+    const int ml = pass * 16 + (tid >> 5);
+    const int m = m0 + ml, n = n0 + c * 8;
+    if (m >= p.M || n >= p.N) continue;
+    uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
+    if constexpr (EPI == EPI_DACT) {
+      const uint4 hh = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+      const uint32_t hv[4] = {hh.x, hh.y, hh.z, hh.w};
+      uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a0 = bf2f(vv[q] & 0xffff), a1 = bf2f(vv[q] >> 16);
+        const float d0 = act_deriv_out(ACT, bf2f(hv[q] & 0xffff)) + p.flat;
+        const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
+        a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
+        a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
+        vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+      }
+      v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
+    else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
   }
 }
 
@@ -191,6 +512,7 @@ struct WgradArgs {
   int M, Nv, Kx, rows_per_split;
 };
 
+template <int STAGES>
 __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles_n = (p.Nv + WT_BN - 1) / WT_BN, tiles_k = p.Kx / WT_BK;
@@ -241,7 +563,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
   swrite(0);
   __syncthreads();
   for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
+    const int buf = STAGES == 2 ? (st & 1) : 0;
     if (st + 1 < nsteps) gload(mbeg + (st + 1) * WT_BM);
     const char* Ds = smem + buf * 2 * WT_TILE;
     const char* Xs = Ds + WT_TILE;
@@ -269,7 +591,8 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (st + 1 < nsteps) swrite(buf ^ 1);
+    if constexpr (STAGES == 1) __syncthreads();
+    if (st + 1 < nsteps) swrite(STAGES == 2 ? (buf ^ 1) : 0);
     __syncthreads();
   }
   // acc[i][j]: D_out[n][k]: k = lane&15 (+16j), n = 4*(lane>>4) + r (+16i)
@@ -306,20 +629,59 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
 // =======================================================================================
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
 
+static int g_stages = 1;     // LDS stages of the MLP GEMMs (A/B switch for tuning; 1 = default)
+static int g_big = 0;        // large-M path: 0 = 128x128 kernel, 1 = 256x256 register-staged, 2 = 256x256 DMA ring
+SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
+SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b >= 0 && b <= 2) ? b : 0; return 0; }
+
 SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc,
                             void* C2, long ldc2, const void* H, long ldh, const void* Hd, long ldhd,
                             int M, int N, int K, int epi, int act, int n_valid, int bias_col, float flat,
                             hipStream_t stream) {
-  if (K % BK || N % 4 || ldc % 4 || lda % 8 || ldb % 8 || M <= 0 || N <= 0) return -1;
+  if (K % BK || N % 4 || ldc % 8 || lda % 8 || ldb % 8 || M <= 0 || N <= 0) return -1;
+  if (epi == EPI_DACT && H != nullptr && ldh % 8) return -1;     // 16-B row-segment loads of H
   GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, (bf16_t*)C2, ldc2,
              (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat};
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const size_t lds = 4 * TILE_BYTES;
+  const size_t lds = 2 * g_stages * TILE_BYTES;
   if (act < 0 || act > 8 || epi < 0 || epi > 2) return -2;
   if (epi == EPI_ACT && !act_deriv_from_output(act) && C2 == nullptr) return -3;
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;
-#define GEMM_L(E, A) hipLaunchKernelGGL((gemm_nt_kernel<E, A>), dim3(grid), dim3(NTHR), lds, stream, p)
+  const bool dfo_act = act_deriv_from_output(act);
+  if (g_big == 2 && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
+    const int gridp = ((M + GP_M - 1) / GP_M) * ((N + GP_N - 1) / GP_N);
+    const size_t ldsp = GP_ST * GP_STAGE;
+#define GEMMP_L(E, A) hipLaunchKernelGGL((gemm_nt_pipe_kernel<E, A>), dim3(gridp), dim3(GP_T), ldsp, stream, p)
+#define GEMMP_ACTS(E) switch (act) { case 0: GEMMP_L(E, 0); break; case 1: GEMMP_L(E, 1); break; \
+    case 2: GEMMP_L(E, 2); break; case 3: GEMMP_L(E, 3); break; case 4: GEMMP_L(E, 4); break; \
+    case 6: GEMMP_L(E, 6); break; default: GEMMP_L(E, 7); break; }
+    if (epi == EPI_ACT) { GEMMP_ACTS(EPI_ACT) }
+    else if (epi == EPI_DACT) { GEMMP_ACTS(EPI_DACT) }
+    else GEMMP_L(EPI_STORE, 2);
+#undef GEMMP_ACTS
+#undef GEMMP_L
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
+  if (g_big == 1 && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
+    const int gridb = ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
+    const size_t ldsb = 2 * GB_TILE;
+#define GEMMB_L(E, A) hipLaunchKernelGGL((gemm_nt_big_kernel<E, A>), dim3(gridb), dim3(GB_T), ldsb, stream, p)
+#define GEMMB_ACTS(E) switch (act) { case 0: GEMMB_L(E, 0); break; case 1: GEMMB_L(E, 1); break; \
+    case 2: GEMMB_L(E, 2); break; case 3: GEMMB_L(E, 3); break; case 4: GEMMB_L(E, 4); break; \
+    case 6: GEMMB_L(E, 6); break; default: GEMMB_L(E, 7); break; }
+    if (epi == EPI_ACT) { GEMMB_ACTS(EPI_ACT) }
+    else if (epi == EPI_DACT) { GEMMB_ACTS(EPI_DACT) }
+    else GEMMB_L(EPI_STORE, 2);
+#undef GEMMB_ACTS
+#undef GEMMB_L
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
+#define GEMM_L(E, A) do { if (g_stages == 2) \
+    hipLaunchKernelGGL((gemm_nt_kernel<E, A, 2>), dim3(grid), dim3(NTHR), lds, stream, p); \
+  else hipLaunchKernelGGL((gemm_nt_kernel<E, A, 1>), dim3(grid), dim3(NTHR), lds, stream, p); } while (0)
 #define GEMM_ACTS(E) switch (act) { case 0: GEMM_L(E, 0); break; case 1: GEMM_L(E, 1); break; \
     case 2: GEMM_L(E, 2); break; case 3: GEMM_L(E, 3); break; case 4: GEMM_L(E, 4); break; \
     case 5: GEMM_L(E, 5); break; case 6: GEMM_L(E, 6); break; case 7: GEMM_L(E, 7); break; \
@@ -342,7 +704,10 @@ SHIFU_API int shifu_wgrad_tn(const void* D, long ldd, const void* X, long ldx, f
   splits = (M + rps - 1) / rps;
   WgradArgs p{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, G, ldg, M, Nv, Kx, rps};
   const int ntiles = ((Nv + WT_BN - 1) / WT_BN) * (Kx / WT_BK);
-  hipLaunchKernelGGL(wgrad_tn_kernel, dim3(ntiles * splits), dim3(NTHR), 4 * WT_TILE, stream, p);
+  if (g_stages == 2)
+    hipLaunchKernelGGL(wgrad_tn_kernel<2>, dim3(ntiles * splits), dim3(NTHR), 4 * WT_TILE, stream, p);
+  else
+    hipLaunchKernelGGL(wgrad_tn_kernel<1>, dim3(ntiles * splits), dim3(NTHR), 2 * WT_TILE, stream, p);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

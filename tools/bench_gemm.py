@@ -1,0 +1,82 @@
+"""Micro-benchmark of the MLP HIP kernels at the bench shapes (1000-500-200-1, 1M-row chunk):
+forward GEMMs, dgrad, wgrad and the output kernel, timed with HIP events; prints TF/s."""
+import argparse
+import json
+
+import torch
+
+from shifu_amd.models.nn import ACT_IDS
+from shifu_amd.ops import _native as nat
+
+
+def timeit(fn, iters):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1 << 20)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--stages", type=int, default=1)
+    ap.add_argument("--big", type=int, default=1)
+    a = ap.parse_args()
+    nat.call_hip("shifu_gemm_set_stages", a.stages)
+    nat.call_hip("shifu_gemm_set_big", a.big)
+    M = a.rows
+    dev = torch.device("cuda")
+    bf = torch.bfloat16
+    X = torch.randn(M, 1024, device=dev).to(bf)
+    W1 = (torch.randn(500, 1024, device=dev) * 0.03).to(bf)
+    H1 = torch.empty(M, 512, device=dev, dtype=bf)
+    W2 = (torch.randn(200, 512, device=dev) * 0.05).to(bf)
+    H2 = torch.empty(M, 256, device=dev, dtype=bf)
+    W2t = (torch.randn(512, 256, device=dev) * 0.05).to(bf)
+    D2 = torch.randn(M, 256, device=dev).to(bf)
+    D1 = torch.empty(M, 512, device=dev, dtype=bf)
+    G1 = torch.zeros(500, 1024, device=dev)
+    G2 = torch.zeros(200, 512, device=dev)
+    st = nat.stream_of(X)
+    tanh = ACT_IDS["tanh"]
+    res = {}
+
+    def fwd1():
+        nat.call_hip("shifu_gemm_nt", X, 1024, W1, 1024, 500, H1, 512, None, 0, None, 0, None, 0, M, 512, 1024, 0,
+                     tanh, 500, 1, 0.0, st)
+
+    def fwd2():
+        nat.call_hip("shifu_gemm_nt", H1, 512, W2, 512, 200, H2, 256, None, 0, None, 0, None, 0, M, 256, 512, 0,
+                     tanh, 200, 1, 0.0, st)
+
+    def dgrad():
+        nat.call_hip("shifu_gemm_nt", D2, 256, W2t, 256, 512, D1, 512, None, 0, H1, 512, None, 0, M, 512, 256, 1,
+                     tanh, 500, 0, 0.0, st)
+
+    def spl(hidden, kpad):       # same split rule as MLPTrainer._chunk_hip
+        ntiles = -(-hidden // 128) * (kpad // 128)
+        return max(1, min(M // 256, 1024 // max(1, ntiles)))
+
+    def wgrad1():
+        nat.call_hip("shifu_wgrad_tn", D1, 512, X, 1024, G1, 1024, M, 500, 1024, spl(500, 1024), st)
+
+    def wgrad2():
+        nat.call_hip("shifu_wgrad_tn", D2, 256, H1, 512, G2, 512, M, 200, 512, spl(200, 512), st)
+
+    for name, fn, flops in (("fwd1", fwd1, 2 * M * 512 * 1024), ("fwd2", fwd2, 2 * M * 256 * 512),
+                            ("dgrad1", dgrad, 2 * M * 512 * 256), ("wgrad1", wgrad1, 2 * M * 512 * 1024),
+                            ("wgrad2", wgrad2, 2 * M * 256 * 512)):
+        ms = timeit(fn, a.iters)
+        res[name] = {"ms": round(ms, 4), "tflops": round(flops / ms / 1e9, 1)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
