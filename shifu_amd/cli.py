@@ -57,8 +57,10 @@ def main(argv=None) -> int:
     from .parallel import dist
     if cmd in ("train", "stats", "norm", "normalize", "transform", "varsel", "eval", "posttrain"):
         dist.init_from_env()
+    from .utils.trace import step_timer
     try:
-        return _dispatch(cmd, args)
+        with step_timer(cmd):
+            return _dispatch(cmd, args)
     except Exception as e:      # noqa: BLE001 - processors report errors and return non-zero
         if environment.get_bool("shifu.debug", False) or os.environ.get("SHIFU_DEBUG") == "1":
             raise

@@ -648,7 +648,14 @@ class TreeTrainer:
                     g = out
                 tree = self.grow_tree(g, w, 1.0 if tid == 0 else c.learning_rate)
                 t0 = time.perf_counter()
+                keep = None
+                if tid > 0 and c.dropout_rate > 0.0:
+                    # DTWorker :634-638: each row skips this tree's update with prob. DropoutRate
+                    keep = (torch.rand(d.n, device=self.dev, generator=self.tgen) >= c.dropout_rate).float()
+                    before = self.pred.clone()
                 self.apply_tree(tree, d, self.pred, tree.weight, tid == 0)
+                if keep is not None:
+                    self.pred.copy_(before + (self.pred - before) * keep)
                 if self.valid is not None:
                     self.apply_tree(tree, self.valid, self.vpred, tree.weight, tid == 0)
                 self.timings["apply"] += time.perf_counter() - t0
@@ -668,6 +675,40 @@ class TreeTrainer:
             if callback:
                 callback(tid, tree, terr, verr)
         return self.trees
+
+    # ---- checkpoint / resume (DTMaster.doCheckPoint :637-669 / recoverMasterStatus :1118-1154;
+    #      worker-side recoverGBTData :1452-1488 = replay the trees over the resident rows) -----------
+    def state_dict(self) -> dict:
+        trees = [{"max_depth": t.max_depth, "weight": t.weight, "feat": torch.from_numpy(t.feat),
+                  "thr": torch.from_numpy(t.thr), "cat_left": torch.from_numpy(t.cat_left.view(np.int32)),
+                  "value": torch.from_numpy(t.value), "wgt_cnt": torch.from_numpy(t.wgt_cnt),
+                  "gain": torch.from_numpy(t.gain), "exists": torch.from_numpy(t.exists),
+                  "features_used": list(map(int, t.features_used))} for t in self.trees]
+        return {"trees": trees, "train_errors": list(self.train_errors), "valid_errors": list(self.valid_errors),
+                "rng": self.rng.bit_generator.state, "tgen": self.tgen.get_state()}
+
+    def load_state_dict(self, st: dict) -> None:
+        self.trees = []
+        for d in st["trees"]:
+            t = Tree(int(d["max_depth"]), float(d["weight"]))
+            t.feat, t.thr = d["feat"].numpy().copy(), d["thr"].numpy().copy()
+            t.cat_left = d["cat_left"].numpy().copy().view(np.uint32)
+            t.value, t.wgt_cnt = d["value"].numpy().copy(), d["wgt_cnt"].numpy().copy()
+            t.gain, t.exists = d["gain"].numpy().copy(), d["exists"].numpy().copy()
+            t.features_used = list(d["features_used"])
+            self.trees.append(t)
+        self.train_errors, self.valid_errors = list(st["train_errors"]), list(st["valid_errors"])
+        self.rng.bit_generator.state = st["rng"]
+        self.tgen.set_state(st["tgen"])
+        # replay predictions and residuals
+        self.pred = self.predict(self.data) * (len(self.trees) if not self.cfg.is_gbt and self.trees else 1)
+        if self.valid is not None:
+            self.vpred = self.predict(self.valid) * (len(self.trees) if not self.cfg.is_gbt and self.trees else 1)
+        self._out = torch.zeros(self.data.n, dtype=torch.float32, device=self.dev)
+        self._vout = None if self.valid is None else torch.zeros(self.valid.n, dtype=torch.float32,
+                                                                   device=self.valid.device)
+        if self.cfg.is_gbt and self.trees:
+            self._residual(self.pred, self.data, self._out)
 
     def predict(self, data: BinnedData) -> torch.Tensor:
         p = torch.zeros(data.n, dtype=torch.float32, device=data.device)

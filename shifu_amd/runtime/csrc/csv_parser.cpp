@@ -251,7 +251,7 @@ SHIFU_RT_API int shifu_csv_numeric(void* h, int col, double* out) {
   auto* P = (Parser*)h;
   if (col < 0 || col >= P->ncols || P->num_idx[col] < 0) return -1;
   const auto& v = P->num[P->num_idx[col]];
-  memcpy(out, v.data(), v.size() * sizeof(double));
+  if (!v.empty()) memcpy(out, v.data(), v.size() * sizeof(double));   // (empty input: no rows)
   return 0;
 }
 
@@ -259,7 +259,7 @@ SHIFU_RT_API int shifu_csv_codes(void* h, int col, int32_t* out) {
   auto* P = (Parser*)h;
   if (col < 0 || col >= P->ncols || P->str_idx[col] < 0) return -1;
   const auto& v = P->codes[P->str_idx[col]];
-  memcpy(out, v.data(), v.size() * sizeof(int32_t));
+  if (!v.empty()) memcpy(out, v.data(), v.size() * sizeof(int32_t));
   return 0;
 }
 
@@ -273,7 +273,7 @@ SHIFU_RT_API long shifu_csv_dict(void* h, int col, char* out, long cap) {
   if (out && cap >= need) {
     long p = 0;
     for (size_t i = 0; i < d.size(); ++i) {
-      memcpy(out + p, d[i].data(), d[i].size());
+      if (!d[i].empty()) memcpy(out + p, d[i].data(), d[i].size());
       p += (long)d[i].size();
       if (i + 1 < d.size()) out[p++] = '\n';
     }

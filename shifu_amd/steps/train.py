@@ -28,7 +28,9 @@ from ..formats import nn_format, tree_format
 from ..models import lr as lrmod
 from ..models.nn import MLPSpec, MLPTrainer
 from ..parallel import dist
+from ..runtime.fault import check_finite, maybe_fault
 from ..utils.log import get_logger
+from ..utils.trace import trace_range
 from ..utils.metrics import MetricsWriter
 from .base import ModelSet, load_dataset_cache
 from .norm import TREE_ALGS, _norm_one
@@ -76,6 +78,18 @@ def _parse_value(s):
         if s.startswith("[") and s.endswith("]"):
             return [_parse_value(x.strip()) for x in s[1:-1].split(",") if x.strip()]
         return s
+
+
+def checkpoint_interval(params: dict, default: int) -> int:
+    """``CheckpointInterval`` param or ``-Dshifu.train.checkpoint.interval``; default = the
+    reference's tmp-model cadence max(epochs/25, 20) (DTrainUtils.tmpModelFactor :293-295)."""
+    from ..config import environment
+    v = params.get("CheckpointInterval") or environment.get("shifu.train.checkpoint.interval")
+    try:
+        v = int(float(v))
+    except (TypeError, ValueError):
+        v = 0
+    return v if v > 0 else default
 
 
 def _num(v, default):
@@ -379,18 +393,22 @@ class TrainStep:
                        float(_num(mc.train.get("convergenceThreshold"), 0.0)))
         ckpt = os.path.join(ms.pf.checkpoint_dir, f"nn_trainer{tid}.pt")
         start = 0
+        best_v, best_w = math.inf, None
         if self.resume and os.path.exists(ckpt):
             st = torch.load(ckpt, weights_only=True)
             if st.get("spec_sizes") == [n_in] + spec.hidden + [n_out]:
                 tr.load_state_dict(st)
                 start = int(st["epoch"])
+                best_v = float(st.get("best_v", math.inf))
+                best_w = st["best_w"].to(tr.device) if st.get("best_w") is not None else None
                 _log.info("resumed trainer %d from checkpoint at epoch %d", tid, start)
-        factor = max(epochs // 25, 20)
-        best_v, best_w = math.inf, None
+        factor = checkpoint_interval(p, max(epochs // 25, 20))
         verr = float("nan")
         for ep in range(start + 1, epochs + 1):
-            terr = tr.step(data, num_train_global=n_train)
-            verr = tr.evaluate(vdata) if vdata is not None else float("nan")
+            with trace_range(f"nn.epoch{ep}"):
+                terr = tr.step(data, num_train_global=n_train)
+                verr = tr.evaluate(vdata) if vdata is not None else float("nan")
+            check_finite("training error", terr, ep)
             if not math.isnan(verr) and verr < best_v:
                 best_v, best_w = verr, tr.params.flat.detach().clone()
             self._log_epoch(tid, ep, terr, verr)
@@ -398,9 +416,11 @@ class TrainStep:
                 self._write_nn(tid, spec, tr, tmp_epoch=ep)
                 os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
                 sd = tr.state_dict()
-                sd.update(epoch=ep, spec_sizes=[n_in] + spec.hidden + [n_out])
+                sd.update(epoch=ep, spec_sizes=[n_in] + spec.hidden + [n_out], best_v=best_v,
+                          best_w=None if best_w is None else best_w.cpu())
                 sd.pop("spec", None)
                 torch.save(sd, ckpt)
+            maybe_fault(ep, self.info.rank)
             if es.update(ep, terr, verr):
                 _log.info("trainer %d early stop at epoch %d", tid, ep)
                 break
@@ -515,17 +535,25 @@ class TrainStep:
             self._log_epoch(tid, i + 1, terr, verr)
             if es.update(i + 1, terr, verr):
                 stop[0] = True
-        # continuous GBT training: re-apply existing trees then keep boosting
-        mpath = ms.pf.model_path(tid, alg.lower())
-        done = 0
-        if bool(mc.train.get("isContinuous", False)) and os.path.exists(mpath) and alg == "GBT":
-            _log.info("continuous GBT training requested; existing %s is kept as a warm start", mpath)
-        for _ in range(tree_num - done):
+        ckpt = os.path.join(ms.pf.checkpoint_dir, f"tree_trainer{tid}.pt")
+        if self.resume and os.path.exists(ckpt):
+            tt.load_state_dict(torch.load(ckpt, weights_only=False))    # our own checkpoint file
+            _log.info("resumed trainer %d from checkpoint with %d trees", tid, len(tt.trees))
+        interval = checkpoint_interval(p, max(1, tree_num // 10))   # DTOutput: tmp models every treeNum/10
+        while len(tt.trees) < tree_num:
             tt.train(1, callback=cb)
+            n = len(tt.trees)
+            check_finite("training error", tt.train_errors[-1], n)
+            if self.info.rank == 0 and n % interval == 0 and n < tree_num:
+                os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
+                torch.save(tt.state_dict(), ckpt)
+            maybe_fault(n, self.info.rank)
             if stop[0]:
                 break
         if self.info.rank == 0:
             self._write_trees(tid, tt)
+            if os.path.exists(ckpt):
+                os.remove(ckpt)
         return tt.valid_errors[-1] if tt.valid_errors else float("nan")
 
     def _write_trees(self, tid, tt):

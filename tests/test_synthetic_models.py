@@ -85,3 +85,46 @@ def test_autotype_rebin_psi(tmp_path):
     assert nb > 5 and len(num3["columnBinning"]["binBoundary"]) == 5
     assert np.isclose(sum(num3["columnBinning"]["binCountPos"]) + sum(num3["columnBinning"]["binCountNeg"]),
                       1200 - 0, rtol=0.05)
+
+
+@pytest.mark.parametrize("alg", ["NN", "GBT"])
+def test_fault_injection_and_resume(tmp_path, alg):
+    """SHIFU_FAULT_AT_ITER kills the trainer right after a checkpoint; re-running resumes and
+    produces the same model as an uninterrupted run."""
+    import subprocess
+    import sys
+    from shifu_amd.utils.synthetic import make_model_set
+    roots = []
+    for name in ("a", "b"):
+        root = make_model_set(str(tmp_path), name, alg, n_rows=600)
+        mc = _mc(root)
+        mc.train["numTrainEpochs"] = 12
+        mc.train["baggingNum"] = 1
+        if alg == "GBT":
+            mc.train["params"].update({"TreeNum": 12, "MaxDepth": 3, "CheckpointInterval": 4})
+        else:
+            mc.train["params"]["CheckpointInterval"] = 4
+        mc.save()
+        _run(root, ["init", "stats", "norm"])
+        roots.append(root)
+    env = dict(os.environ, SHIFU_FORCE_CPU="1", SHIFU_FAULT_AT_ITER="8", PYTHONPATH=os.getcwd())
+    r = subprocess.run([sys.executable, "-m", "shifu_amd.cli", "train"], cwd=roots[0], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 17, r.stderr[-2000:]
+    assert os.path.exists(os.path.join(roots[0], "tmp/checkpoints"))
+    _run(roots[0], ["train"])                  # resumes from the iteration-8 checkpoint
+    _run(roots[1], ["train"])                  # uninterrupted reference
+    ext = "nn" if alg == "NN" else "gbt"
+    if alg == "NN":
+        from shifu_amd.formats.nn_format import read_encog
+        wa = read_encog(os.path.join(roots[0], f"models/model0.{ext}")).weights
+        wb = read_encog(os.path.join(roots[1], f"models/model0.{ext}")).weights
+        for x, y in zip(wa, wb):
+            np.testing.assert_allclose(x, y, rtol=1e-5, atol=1e-6)
+    else:
+        from shifu_amd.formats.tree_format import read_tree_model
+        ta, tb = read_tree_model(os.path.join(roots[0], "models/model0.gbt")), \
+            read_tree_model(os.path.join(roots[1], "models/model0.gbt"))
+        assert len(ta.bags[0]) == len(tb.bags[0]) == 12
+        x = {c: np.linspace(-3, 3, 50) for c in ta.names}
+        np.testing.assert_allclose(ta.score(x, 50), tb.score(x, 50), rtol=1e-5)
