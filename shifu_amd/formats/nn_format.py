@@ -24,6 +24,7 @@ ACT_CLASS = {"sigmoid": "ActivationSigmoid", "tanh": "ActivationTANH", "linear":
              "ptanh": "ActivationPTANH", "log": "ActivationLOG", "sin": "ActivationSIN"}
 CLASS_ACT = {v.lower(): k for k, v in ACT_CLASS.items()}
 ACT_PARAMS = {"relu": [0.0, 0.0], "leakyrelu": [0.0, 0.01]}
+SUBSET_PROP = "shifu.nn.feature.subset"     # input positions a feature-subsampled bag was trained on
 
 
 def act_from_class(name: str) -> str:
@@ -48,6 +49,13 @@ class NNNetwork:
     @property
     def n_out(self):
         return self.sizes[-1]
+
+    def input_subset(self):
+        """Input positions of a feature-subsampled network (None = all inputs)."""
+        if self.feature_set and len(self.feature_set) == self.n_in:
+            return list(self.feature_set)
+        v = (self.properties or {}).get(SUBSET_PROP)
+        return [int(t) for t in str(v).split(",") if t.strip()] if v else None
 
     # ---- Encog flat ---------------------------------------------------------------------
     def flat(self):

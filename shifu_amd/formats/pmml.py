@@ -118,6 +118,9 @@ def nn_pmml(net, cols, target, norm_type="ZSCALE", cutoff=STD_DEV_CUTOFF, model_
     _mining_schema(nn, cols, target)
     _output(nn)
     inputs = _transforms(nn, cols, norm_type, cutoff)
+    sub = net.input_subset()
+    if sub is not None and len(inputs) != net.n_in:
+        inputs = [inputs[i] for i in sub]
     ni = ET.SubElement(nn, "NeuralInputs", numberOfInputs=str(len(inputs)))
     prev = []
     for i, dn in enumerate(inputs):

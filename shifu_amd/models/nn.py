@@ -356,7 +356,8 @@ class MLPTrainer:
     def __init__(self, spec: MLPSpec, device=None, propagation="R", learning_rate=0.1,
                  momentum=0.5, adam_beta1=0.9, adam_beta2=0.999, learning_decay=0.0,
                  reg=0.0, reg_level="NONE", seed=0, weight_init="default",
-                 chunk_rows=1 << 20, init_flat_encog=None, fixed_layers=None, wgrad_splits=None):
+                 chunk_rows=1 << 20, init_flat_encog=None, fixed_layers=None, wgrad_splits=None,
+                 dropout_rate=0.0, fixed_bias=False):
         from ..utils.device import default_device
         self.spec = spec
         self.device = torch.device(device) if device is not None else default_device()
@@ -377,18 +378,33 @@ class MLPTrainer:
         self.gbuf = torch.zeros(self.params.numel + 2, dtype=torch.float32, device=self.device)
         self.grad = self.gbuf[: self.params.numel]
         fixed = None
+        if fixed_bias:                  # FixedBias: bias weights of every layer stay frozen
+            fixed = torch.zeros(self.params.numel, dtype=torch.bool)
+            for li, (o, k) in enumerate(self.params.shapes):
+                off = self.params.offsets[li]
+                fixed[off: off + o * k].view(o, k)[:, spec.layer_in[li]] = True
         if fixed_layers:
             fixed = torch.zeros(self.params.numel, dtype=torch.bool)
             for l in fixed_layers:      # FixedLayers: 1-based hidden layer ids (fine tuning)
                 li = int(l) - 1
                 if 0 <= li < len(self.params.shapes):
                     o, k = self.params.shapes[li]
+                    if fixed is None:
+                        fixed = torch.zeros(self.params.numel, dtype=torch.bool)
                     fixed[self.params.offsets[li]: self.params.offsets[li] + o * k] = True
         self.opt = Optimizer(self.params.numel, self.device, propagation, learning_rate, momentum,
                              adam_beta1, adam_beta2, learning_decay, reg, reg_level, fixed)
         self.chunk_rows = int(chunk_rows)
         self.wgrad_splits = wgrad_splits
         self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
+        # dropout (NNMaster.dropoutNodes :531-556, FloatFlatNetwork.computeLayer :205-215): each
+        # iteration drops hidden nodes with DropoutRate and inputs with 0.4*DropoutRate and scales
+        # kept outputs by 1/(1-rate).  Realised as a per-column scale of the NEXT layer's weights
+        # (identical forward/backward), the same mask on every rank (shared seed, no broadcast).
+        self.dropout_rate = float(dropout_rate or 0.0)
+        self._drop_gen = torch.Generator().manual_seed(seed * 7919 + 11)
+        self._wflat = self.params.flat
+        self._scale = None
         self._ws = None
         self.last_error = float("nan")
 
@@ -425,7 +441,7 @@ class MLPTrainer:
 
     def _weights_bf16(self):
         """bf16 copies of the hidden-layer weights (+ transposed copies for dgrad)."""
-        ws = self.params.views()
+        ws = self.params.views(self._wflat)
         kp = self.spec.layer_kpad
         L = len(self.spec.hidden)
         wb, wt = [], []
@@ -467,7 +483,7 @@ class MLPTrainer:
         ws = self._workspace(min(self.chunk_rows, data.n))
         st = nat.stream_of(data.x)
         gv = self.params.views(self.grad)
-        wv = self.params.views()
+        wv = self.params.views(self._wflat)
         x = data.x[r0:r1]
         acts = [x] + [a[:mc] for a in ws["acts"]]
         dels = [None] + [d[:mc] for d in ws["deltas"]]
@@ -509,7 +525,7 @@ class MLPTrainer:
         """fp32 CPU oracle with exactly the HIP path's structure."""
         sp, kp = self.spec, self.spec.layer_kpad
         L = len(sp.hidden)
-        wv = self.params.views()
+        wv = self.params.views(self._wflat)
         gv = self.params.views(self.grad)
         x = data.x[r0:r1].float()
         acts, zs = [x], [None]
@@ -552,13 +568,34 @@ class MLPTrainer:
             d = dh
 
     # --------------------------------------------------------------------------------------
+    def _dropout_scale(self) -> torch.Tensor:
+        sp = self.spec
+        scale = torch.ones(self.params.numel, dtype=torch.float32)
+        for l, (o, k) in enumerate(self.params.shapes):
+            n_src = sp.layer_in[l]                      # inputs (l = 0) or hidden layer l outputs
+            rate = self.dropout_rate * (0.4 if l == 0 else 1.0)
+            if rate <= 0:
+                continue
+            keep = (torch.rand(n_src, generator=self._drop_gen) >= rate).float() / (1.0 - rate)
+            off = self.params.offsets[l]
+            scale[off: off + o * k].view(o, k)[:, :n_src] *= keep
+        return scale.to(self.device)
+
     def compute_gradients(self, data: TrainData, row_lo=0, row_hi=None):
         """Local gradient pass + one fused all-reduce (grads ++ [err, wsum])."""
         self.grad.zero_()
         self.err_acc.zero_()
+        if self.dropout_rate > 0:
+            self._scale = self._dropout_scale()
+            self._wflat = self.params.flat * self._scale
+        else:
+            self._wflat = self.params.flat
         self.accumulate_gradients(data, row_lo, row_hi)
         self.gbuf[-2:] = self.err_acc.to(torch.float32)
         dist.all_reduce_(self.gbuf)
+        if self.dropout_rate > 0:
+            self.grad.mul_(self._scale)                 # d(loss)/dW of the scaled connections
+        self._wflat = self.params.flat
         return self.gbuf
 
     def step(self, data: TrainData, row_lo=0, row_hi=None, num_train_global: float | None = None) -> float:

@@ -61,6 +61,9 @@ def nn_forward(net: nn_format.NNNetwork, X, device=None, chunk: int = 1 << 18) -
     Ws = [torch.as_tensor(np.asarray(W), dtype=torch.float32, device=dev) for W in net.weights]
     out = []
     Xt = torch.as_tensor(X)
+    sub = net.input_subset()
+    if sub is not None and Xt.shape[1] != net.n_in:
+        Xt = Xt[:, torch.as_tensor(sub, dtype=torch.long)]
     for r in range(0, Xt.shape[0], chunk):
         a = Xt[r: r + chunk].to(dev, torch.float32)
         for l, W in enumerate(Ws):

@@ -343,7 +343,16 @@ class TrainStep:
 
     def _train_nn(self, tid, p, ts, y, train_m, valid_m, sw, ova_class):
         mc, ms = self.mc, self.ms
-        X = ts.X
+        X, vX = ts.X, ts.vX
+        # NN feature subsampling per bag (TrainModelProcessor :880-900 -> shifu.nn.feature.subset)
+        self._nn_subset = None
+        from ..models.gbdt import _strategy_count
+        k = _strategy_count(p.get("FeatureSubsetStrategy", "ALL"), X.shape[1], X.shape[1], 1)
+        if 0 < k < X.shape[1]:
+            cols = np.sort(np.random.default_rng(7 + tid).choice(X.shape[1], k, replace=False))
+            X = np.asarray(X)[:, cols]
+            vX = None if vX is None else np.asarray(vX)[:, cols]
+            self._nn_subset = cols
         n_in = X.shape[1]
         multi = mc.is_multiclass() and ova_class is None
         n_out = len(mc.tags()) if multi else 1
@@ -364,7 +373,9 @@ class TrainStep:
                         learning_decay=float(_num(p.get("LearningDecay"), 0.0)),
                         reg=float(_num(p.get("RegularizedConstant"), 0.0)), reg_level=p.get("L1orL2", "NONE"),
                         seed=1000 + tid, weight_init=p.get("WeightInitializer", "default"),
-                        init_flat_encog=init, fixed_layers=p.get("FixedLayers"))
+                        init_flat_encog=init, fixed_layers=p.get("FixedLayers"),
+                        dropout_rate=float(_num(p.get("DropoutRate"), 0.0)),
+                        fixed_bias=str(p.get("FixedBias", "false")).lower() == "true")
         yy = y
         if multi:
             yy = np.eye(n_out, dtype=np.float32)[np.clip(np.rint(y).astype(int), 0, n_out - 1)]
@@ -373,13 +384,13 @@ class TrainStep:
         tri = np.nonzero(train_m)[0]
         data = tr.prepare(torch.from_numpy(np.asarray(X[tri], dtype=np.float32)), yy[tri], w[tri])
         vdata = None
-        if ts.vX is not None:
+        if vX is not None:
             vy = np.asarray(ts.vy, np.float32)
             if ova_class is not None:
                 vy = (np.rint(vy) == ova_class).astype(np.float32)
             if multi:
                 vy = np.eye(n_out, dtype=np.float32)[np.clip(np.rint(vy).astype(int), 0, n_out - 1)]
-            vdata = tr.prepare(torch.from_numpy(np.asarray(ts.vX, np.float32)), vy.reshape(len(vy), -1),
+            vdata = tr.prepare(torch.from_numpy(np.asarray(vX, np.float32)), vy.reshape(len(vy), -1),
                                np.asarray(ts.vw, np.float32))
         elif valid_m.any():
             vi = np.nonzero(valid_m)[0]
@@ -404,9 +415,16 @@ class TrainStep:
                 _log.info("resumed trainer %d from checkpoint at epoch %d", tid, start)
         factor = checkpoint_interval(p, max(epochs // 25, 20))
         verr = float("nan")
+        # MiniBatchs=k: iteration i trains on slice (i-1) mod k of the rows (SubGradient :326-340)
+        mb = max(1, min(1000, int(_num(p.get("MiniBatchs"), 1))))
         for ep in range(start + 1, epochs + 1):
             with trace_range(f"nn.epoch{ep}"):
-                terr = tr.step(data, num_train_global=n_train)
+                if mb > 1:
+                    b = (ep - 1) % mb
+                    lo, hi = data.n * b // mb, data.n * (b + 1) // mb
+                    terr = tr.step(data, lo, hi)
+                else:
+                    terr = tr.step(data, num_train_global=n_train)
                 verr = tr.evaluate(vdata) if vdata is not None else float("nan")
             check_finite("training error", terr, ep)
             if not math.isnan(verr) and verr < best_v:
@@ -436,7 +454,12 @@ class TrainStep:
     def _nn_network(self, spec, tr) -> nn_format.NNNetwork:
         ws = tr.params.views()
         weights = [ws[l][:, : spec.layer_in[l] + 1].detach().double().cpu().numpy() for l in range(len(ws))]
-        return nn_format.NNNetwork([spec.n_in] + spec.hidden + [spec.n_out], spec.acts + [spec.out_act], weights)
+        net = nn_format.NNNetwork([spec.n_in] + spec.hidden + [spec.n_out], spec.acts + [spec.out_act], weights)
+        sub = getattr(self, "_nn_subset", None)
+        if sub is not None:            # input positions of the bag's feature subset
+            net.feature_set = [int(i) for i in sub]
+            net.properties = {nn_format.SUBSET_PROP: ",".join(str(int(i)) for i in sub)}
+        return net
 
     def _write_nn(self, tid, spec, tr, tmp_epoch=None):
         ms = self.ms
