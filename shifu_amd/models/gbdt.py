@@ -81,6 +81,7 @@ class TreeConfig:
     bagging_sample_rate: float = 1.0
     sample_with_replacement: bool = False
     dropout_rate: float = 0.0
+    max_leaves: int = 0                 # > 0: leaf budget, best (gain x weight) splits first
     seed: int = 0
     valid_tolerance: float = 0.0
     early_stop: bool = False
@@ -254,6 +255,7 @@ class TreeTrainer:
         tree.exists[1] = True
         tree.value[1] = ts / tw if tw != 0 else 0.0
         tree.wgt_cnt[1] = tw
+        n_leaves = 1
         for level in range(1, c.max_depth):
             if not nodes:
                 break
@@ -282,12 +284,21 @@ class TreeTrainer:
             cat_left = np.zeros((len(nodes), 8), dtype=np.uint32)
             children = []
             last = level + 1 >= c.max_depth
+            allowed = None
+            if c.max_leaves > 0:
+                # MaxLeaves (DTMaster :543-605, 1063-1071): split the candidates with the highest
+                # wgtCnt-ratio x gain first while the leaf budget lasts
+                cands = sorted((-(float(best[z["slot"]][2]) * float(tree.wgt_cnt[z["id"]])), z["slot"])
+                               for z in nodes if best[z["slot"]][7])
+                room = max(0, c.max_leaves - n_leaves)
+                allowed = {s_ for _, s_ in cands[:room]}
             for z in nodes:
                 s_ = z["slot"]
                 f, b, gain, lw, ls, rw, rs, ok = best[s_]
                 nid = z["id"]
-                if not ok:
+                if not ok or (allowed is not None and s_ not in allowed):
                     continue
+                n_leaves += 1
                 f = int(f)
                 tree.feat[nid] = f
                 tree.gain[nid] = gain

@@ -548,6 +548,7 @@ class TrainStep:
                          sample_with_replacement=bool(p.get("GBTSampleWithReplacement", False)) if alg == "GBT"
                          else bool(mc.train.get("baggingWithReplacement", True)),
                          dropout_rate=float(_num(p.get("DropoutRate"), 0.0)), seed=tid,
+                         max_leaves=int(_num(p.get("MaxLeaves"), 0)),
                          valid_tolerance=float(_num(p.get("ValidationTolerance"), 0.0)),
                          early_stop=str(p.get("EnableEarlyStop", "false")).lower() == "true")
         tt = TreeTrainer(cfg, d, vd)

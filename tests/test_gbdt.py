@@ -135,3 +135,19 @@ def test_gpu_many_items_and_feature_mask():
         v = t.predict_bins(host, data.is_cat)
         p = v if i == 0 else p + t.weight * v
     assert np.allclose(p, tr.pred.cpu().numpy(), atol=1e-4)
+
+
+def test_max_leaves_budget():
+    import numpy as np
+    import torch
+    from shifu_amd.models.gbdt import BinnedData, TreeConfig, TreeTrainer
+    rng = np.random.default_rng(3)
+    codes = rng.integers(0, 32, size=(3000, 8))
+    y = (codes[:, 0] + codes[:, 1] * 0.5 + rng.normal(size=3000) * 3 > 24).astype(np.float32)
+    d = BinnedData.from_codes(torch.from_numpy(codes), y, np.full(8, 32))
+    for ml in (3, 7, 12):
+        tt = TreeTrainer(TreeConfig("GBT", tree_num=2, max_depth=6, max_leaves=ml, feature_subset_strategy="ALL",
+                                    min_instances_per_node=1), d)
+        tt.train()
+        for t in tt.trees:
+            assert 2 <= len(t.leaves()) <= ml
