@@ -52,9 +52,26 @@ def update_column_flags(mc, ccs, step: str = "INIT"):
     hybrid = mc.hybrid_column_names()
     hyb = NSSet(list(hybrid.keys()))
     has_tags = bool(mc.tags())
+    segs = mc.segment_filter_expressions()
+    raw_names = {c.name for c in ccs[: len(ccs) // (len(segs) + 1)]} if segs else set()
     for c in ccs:
         name = c.name
         keep_type = c.type
+        if segs:                    # segment copy "<col>_<k>": flags/type follow the base column
+            from ..data.segments import split_name
+            base, k = split_name(name, len(segs), raw_names)
+            if k:
+                c.flag = None
+                if ns_equal(target, base) or (weight and ns_equal(weight, base)):
+                    c.flag = "ForceRemove"          # VarSelectModelProcessor :157-176 (shadow targets)
+                elif base in meta:
+                    c.flag = "Meta"
+                elif base in force_remove:
+                    c.flag = "ForceRemove"
+                c.type = "C" if base in cats else ("H" if base in hyb else "N")
+                if c.is_meta() or c.is_force_remove():
+                    c.final_select = False
+                continue
         c.flag = None
         if ns_equal(target, name):
             c.flag = "Target"

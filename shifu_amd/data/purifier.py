@@ -149,6 +149,19 @@ def load_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=
         filt = f"({filt}) && ({extra_filter})" if filt else extra_filter
     strs = set(columns_str or [])
     nums = set(columns_num or [])
+    seg_exprs = mc.segment_filter_expressions()
+    seg_names = []
+    if seg_exprs:                    # segment copies "<col>_<k>" are derived from their base column
+        from . import segments
+        raw = set(header)
+        seg_names = [n for n in list(nums) + list(strs) if segments.split_name(n, len(seg_exprs), raw)[1]]
+        base, expr_cols = segments.needed_base_columns(seg_names, seg_exprs, raw)
+        for n in seg_names:
+            b = segments.split_name(n, len(seg_exprs), raw)[0]
+            (nums if n in nums else strs).add(b)
+            nums.discard(n)
+            strs.discard(n)
+        strs |= {c for c in expr_cols if c in raw and c not in nums}
     if target:
         strs.add(target)
         nums.discard(target)
@@ -171,4 +184,7 @@ def load_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=
     table = read_table(data_path, header, delim, numeric=[h for h in header if h in nums],
                        strings=[h for h in header if h in strs], missing=mc.missing_values,
                        skip_header_line=skip, max_rows=max_rows)
+    if seg_names:
+        from . import segments
+        segments.expand(table, seg_names, seg_exprs, set(header))
     return purify(mc, table, target, weight, filt, sample_rate, sample_neg_only, seed, require_target)

@@ -55,6 +55,10 @@ class ModelSet:
             if not r:
                 raise ShifuException(ShifuErrorCode.ERROR_MODELCONFIG_NOT_VALIDATION, "; ".join(r.causes))
         check_algorithm_params(self.mc)
+        if step in ("NORMALIZE", "VARSELECT", "TRAIN", "EVAL") and self.mc.segment_filter_expressions() \
+                and self.mc.algorithm not in ("NN", "LR"):
+            raise ValueError("Segment expression is only supported in NN or LR model "
+                             "(BasicModelProcessor.setUp :140-155)")
         if update_flags and self.ccs:
             update_column_flags(self.mc, self.ccs, step)
         return self

@@ -81,6 +81,14 @@ def init_column_configs(ms: ModelSet, auto_type: bool | None = None):
         c.num = i
         c.name = norm_column_name(fld) if schema else str(i)
         ccs.append(c)
+    segs = mc.segment_filter_expressions()
+    base = list(ccs)
+    for k in range(1, len(segs) + 1):          # segment copies: num = k * size + i, name "<col>_<k>"
+        for c0 in base:
+            c = ColumnConfig()
+            c.num = k * len(base) + c0.num
+            c.name = f"{c0.name}_{k}"
+            ccs.append(c)
     update_column_flags(mc, ccs, "INIT")
     if not any(c.is_target() for c in ccs):
         raise ValueError(f"target column {target!r} not found in header")

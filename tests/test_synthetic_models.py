@@ -173,3 +173,30 @@ def test_dropout_gradient_matches_masked_network():
     for l in range(2):
         zero_cols = (sv[l] == 0)
         assert torch.all(gv[l][zero_cols] == 0)
+
+
+def test_segment_expansion_pipeline(tmp_path):
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "s", "NN", n_rows=1500)
+    with open(os.path.join(root, "columns", "segments.txt"), "w") as f:
+        f.write("cat_0 == 'k1'\nnum_0 > 0\n")
+    mc = _mc(root)
+    mc.dataSet["segExpressionFile"] = "columns/segments.txt"
+    mc.train["numTrainEpochs"] = 20
+    mc.train["baggingNum"] = 1
+    mc.varSelect["filterNum"] = 30
+    mc.save()
+    _run(root, ["init", "stats"])
+    ccs = json.load(open(os.path.join(root, "ColumnConfig.json")))
+    n = len(ccs) // 3
+    assert len(ccs) == 3 * n
+    byname = {c["columnName"]: c for c in ccs}
+    assert byname["diagnosis_1"]["columnFlag"] == "ForceRemove" and byname["id_2"]["columnFlag"] == "Meta"
+    assert byname["num_3_2"]["columnNum"] == 2 * n + byname["num_3"]["columnNum"]
+    # segment 2 (num_0 > 0) keeps about half the rows; the rest are missing in the copy
+    miss = byname["num_3_2"]["columnStats"]["missingCount"] - byname["num_3"]["columnStats"]["missingCount"]
+    assert 0.35 * 1500 < miss < 0.65 * 1500
+    assert byname["cat_0_1"]["columnBinning"]["binCategory"] == ["k1"]
+    _run(root, ["varsel", "norm", "train", "eval"])
+    auc = json.load(open(os.path.join(root, "evals/Eval1/EvalPerformance.json")))["areaUnderRoc"]
+    assert auc > 0.7
