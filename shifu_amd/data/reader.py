@@ -75,6 +75,9 @@ def read_header(header_path: str | None, header_delim: str = "|", data_path: str
     files = list_data_files(data_path)
     if not files:
         raise FileNotFoundError(f"no header file and no data under {data_path}")
+    if files[0].endswith(".parquet"):           # schema carries the header
+        import pyarrow.parquet as pq
+        return list(pq.read_schema(files[0]).names)
     raw = _read_bytes(files[0]).decode("utf-8", errors="replace")
     line = next((l for l in raw.splitlines() if l.strip()), "")
     return [h.strip() for h in line.split(data_delim or "|")]
@@ -209,6 +212,39 @@ def _parse_python(data: bytes, delim: str, kinds: list, missing: list):
     return n, bad, out
 
 
+def _parse_parquet(path: str, header: list, kinds: list, missing: list):
+    """Parquet part file (D3: GuaguaParquetRecordReader, column projection): only the requested
+    columns are read; numeric -> float64 (NaN missing), string -> dictionary codes."""
+    import pyarrow.parquet as pq
+    names = [h for h, k in zip(header, kinds) if k]
+    tbl = pq.read_table(path, columns=[n for n in names if n in pq.read_schema(path).names])
+    n = tbl.num_rows
+    miss = set(missing)
+    out = [None] * len(header)
+    for ci, (h, k) in enumerate(zip(header, kinds)):
+        if not k:
+            continue
+        if h not in tbl.column_names:
+            out[ci] = ("num", np.full(n, np.nan), []) if k == 1 else ("str", np.full(n, -1, np.int32), [])
+            continue
+        col = tbl.column(h).to_pylist()
+        if k == 1:
+            a = np.empty(n, dtype=np.float64)
+            for i, v in enumerate(col):
+                try:
+                    a[i] = float(v) if v is not None and str(v) not in miss else np.nan
+                except (TypeError, ValueError):
+                    a[i] = np.nan
+            out[ci] = ("num", a, [])
+        else:
+            d, codes = {}, np.empty(n, dtype=np.int32)
+            for i, v in enumerate(col):
+                s = "" if v is None else str(v)
+                codes[i] = -1 if s in miss else d.setdefault(s, len(d))
+            out[ci] = ("str", codes, list(d.keys()))
+    return n, 0, out
+
+
 def read_table(data_path: str, header: list, delim: str = "|", numeric: list | None = None,
                strings: list | None = None, missing: list | None = None, skip_header_line: bool = False,
                nthreads: int | None = None, max_rows: int | None = None) -> RawTable:
@@ -229,6 +265,9 @@ def read_table(data_path: str, header: list, delim: str = "|", numeric: list | N
     nthreads = nthreads or min(16, os.cpu_count() or 4)
     parts = []
     for fi, f in enumerate(files):
+        if f.endswith(".parquet"):
+            parts.append(_parse_parquet(f, header, kinds, missing))
+            continue
         data = _read_bytes(f)
         if skip_header_line and fi == 0:
             nl = data.find(b"\n")
@@ -268,7 +307,7 @@ def read_table(data_path: str, header: list, delim: str = "|", numeric: list | N
 def first_line_is_header(data_path: str, header: list, delim: str) -> bool:
     """Data files that start with their own header line (no separate header file)."""
     files = list_data_files(data_path)
-    if not files:
+    if not files or files[0].endswith(".parquet"):
         return False
     raw = _read_bytes(files[0])[:65536].decode("utf-8", errors="replace")
     line = next((l for l in raw.splitlines() if l.strip()), "")

@@ -151,3 +151,22 @@ def test_sensitivity_matches_bruteforce():
         d = base - net.forward(Z)[:, 0]
         assert abs(np.abs(d).mean() - mean[i]) < 1e-5
         assert abs(np.sqrt((d * d).mean()) - rms[i]) < 1e-5
+
+
+def test_parquet_input_matches_csv(tmp_path):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    rows = [("a", 1.5, "x"), ("b", None, "y"), ("a", 3.0, None), ("c", -2.0, "x")]
+    (tmp_path / "csv").mkdir()
+    (tmp_path / "csv" / "part-0").write_text("\n".join(f"{s}|{'' if n is None else n}|{'' if t is None else t}"
+                                                       for s, n, t in rows) + "\n")
+    (tmp_path / "pq").mkdir()
+    pq.write_table(pa.table({"s": [r[0] for r in rows], "n": [r[1] for r in rows], "t": [r[2] for r in rows]}),
+                   str(tmp_path / "pq" / "part-0.parquet"))
+    hdr = R.read_header(None, "|", str(tmp_path / "pq"))
+    assert hdr == ["s", "n", "t"]
+    a = R.read_table(str(tmp_path / "csv"), hdr, "|", numeric=["n"], strings=["s", "t"])
+    b = R.read_table(str(tmp_path / "pq"), hdr, "|", numeric=["n"], strings=["s", "t"])
+    np.testing.assert_array_equal(a["n"].values, b["n"].values)
+    assert a["s"].strings().tolist() == b["s"].strings().tolist()
+    assert a["t"].missing_mask().tolist() == b["t"].missing_mask().tolist()
