@@ -218,6 +218,61 @@ class MLPParams:
                 w[:, : i + 1].copy_(blk.to(w))
 
 
+class HostRows:
+    """Host-resident rows (numpy array / memmap / host tensor, fp32 or bf16) streamed to HBM.
+
+    ``chunks()`` yields device bf16 padded chunks [rows, K0] (bias column = 1): rows are copied into
+    a pinned staging buffer on the host, sent H2D on a dedicated copy stream into one of two
+    device buffers, cast/padded on the compute stream, and the copy of chunk i+1 overlaps the
+    GEMMs of chunk i (events order the buffer reuse)."""
+
+    def __init__(self, x, n_in: int):
+        self.x = x
+        self.n_in = n_in
+        self.shape = (int(np.shape(x)[0]), n_in)
+        self._bufs = None
+
+    def __len__(self):
+        return self.shape[0]
+
+    def _alloc(self, rows, k0, device):
+        if self._bufs is not None and self._bufs["rows"] >= rows and self._bufs["k0"] == k0:
+            return self._bufs
+        f = self.n_in
+        b = {"rows": rows, "k0": k0, "stream": torch.cuda.Stream(device),
+             "pin": [torch.empty(rows, f, dtype=torch.float32).pin_memory() for _ in range(2)],
+             "raw": [torch.empty(rows, f, dtype=torch.float32, device=device) for _ in range(2)],
+             "dev": [torch.zeros(rows, k0, dtype=torch.bfloat16, device=device) for _ in range(2)],
+             "copied": [torch.cuda.Event() for _ in range(2)], "used": [torch.cuda.Event() for _ in range(2)]}
+        for d in b["dev"]:
+            d[:, f] = 1                       # bias column; padding stays 0
+        self._bufs = b
+        return b
+
+    def chunks(self, lo, hi, chunk_rows, k0, device):
+        from ..ops import _native as nat
+        b = self._alloc(min(chunk_rows, hi - lo), k0, device)
+        cs, main = b["stream"], torch.cuda.current_stream(device)
+        starts = list(range(lo, hi, chunk_rows))
+        for i, r0 in enumerate(starts):
+            r1 = min(hi, r0 + chunk_rows)
+            m, k = r1 - r0, i % 2
+            b["copied"][k].synchronize() if i >= 2 else None      # pinned buffer k free again
+            src = self.x[r0:r1]
+            b["pin"][k][:m].copy_(torch.as_tensor(np.asarray(src, dtype=np.float32)) if not torch.is_tensor(src)
+                                  else src.float())
+            with torch.cuda.stream(cs):
+                if i >= 2:
+                    cs.wait_event(b["used"][k])                   # GEMMs of chunk i-2 done with buffer k
+                b["raw"][k][:m].copy_(b["pin"][k][:m], non_blocking=True)
+                b["copied"][k].record(cs)
+            main.wait_event(b["copied"][k])
+            dev = b["dev"][k][:m]
+            nat.call_hip("shifu_cast_bf16", b["raw"][k], self.n_in, dev, k0, m, self.n_in, nat.stream_of(dev))
+            yield r0, r1, dev
+            b["used"][k].record(main)
+
+
 @dataclass
 class TrainData:
     """Resident (device) training shard: padded bf16/fp32 rows + targets + significance."""
@@ -409,8 +464,22 @@ class MLPTrainer:
         self.last_error = float("nan")
 
     # --------------------------------------------------------------------------------------
-    def prepare(self, x, y, s=None) -> TrainData:
-        """Host/device float rows -> resident padded rows (bias column = 1)."""
+    def prepare(self, x, y, s=None, stream: bool | None = None) -> TrainData:
+        """Host/device float rows -> resident padded rows (bias column = 1).
+
+        ``stream=True`` (or rows that would not fit in ~80 % of free HBM) keeps the rows on the host
+        (numpy memmap / host tensor) and streams them through HBM chunk by chunk with the H2D copies
+        on a side stream overlapping compute (out-of-core rows for 1B x 10k)."""
+        if self.gpu:
+            nbytes = int(np.prod(np.shape(x))) * 2
+            if stream is None:
+                free = torch.cuda.mem_get_info(self.device)[0]
+                stream = nbytes > 0.8 * free
+            if stream:
+                n = int(np.shape(x)[0])
+                yd = torch.as_tensor(np.asarray(y, dtype=np.float32)).reshape(n, -1).to(self.device).contiguous()
+                sd = None if s is None else torch.as_tensor(np.asarray(s, dtype=np.float32)).reshape(n).to(self.device)
+                return TrainData(HostRows(x, self.spec.n_in), yd, sd, n)
         x = torch.as_tensor(x)
         n, f = x.shape
         assert f == self.spec.n_in, (f, self.spec.n_in)
@@ -465,6 +534,11 @@ class MLPTrainer:
     def accumulate_gradients(self, data: TrainData, row_lo: int = 0, row_hi: int | None = None):
         """Sum gradients/errors of rows [row_lo, row_hi) into self.grad / self.err_acc."""
         row_hi = data.n if row_hi is None else row_hi
+        if self.gpu and isinstance(data.x, HostRows):
+            wb, wt = self._weights_bf16()
+            for r0, r1, xd in data.x.chunks(row_lo, row_hi, self.chunk_rows, self.spec.layer_kpad[0], self.device):
+                self._chunk_hip(data, r0, r1, wb, wt, x_dev=xd)
+            return
         if self.gpu:
             wb, wt = self._weights_bf16()
             for r0 in range(row_lo, row_hi, self.chunk_rows):
@@ -475,16 +549,16 @@ class MLPTrainer:
                 r1 = min(row_hi, r0 + self.chunk_rows)
                 self._chunk_torch(data, r0, r1)
 
-    def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt):
+    def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None):
         from ..ops import _native as nat
         sp, kp = self.spec, self.spec.layer_kpad
         L = len(sp.hidden)
         mc = r1 - r0
         ws = self._workspace(min(self.chunk_rows, data.n))
-        st = nat.stream_of(data.x)
         gv = self.params.views(self.grad)
         wv = self.params.views(self._wflat)
-        x = data.x[r0:r1]
+        x = data.x[r0:r1] if x_dev is None else x_dev
+        st = nat.stream_of(x)
         acts = [x] + [a[:mc] for a in ws["acts"]]
         dels = [None] + [d[:mc] for d in ws["deltas"]]
         ders = [None] + [(d[:mc] if d is not None else None) for d in ws["derivs"]]
@@ -637,6 +711,10 @@ class MLPTrainer:
         """Forward pass on padded rows -> [N, n_out] fp32 (HIP kernels on GPU)."""
         sp, kp = self.spec, self.spec.layer_kpad
         L = len(sp.hidden)
+        if isinstance(xpad, HostRows):          # out-of-core rows: forward each streamed chunk
+            parts = [self.predict_rows(xd.clone()) for _, _, xd in
+                     xpad.chunks(0, len(xpad), self.chunk_rows, kp[0], self.device)]
+            return torch.cat(parts) if parts else torch.empty(0, sp.n_out, device=self.device)
         n = xpad.shape[0]
         out = torch.empty(n, sp.n_out, dtype=torch.float32, device=self.device)
         if not self.gpu:
