@@ -148,7 +148,11 @@ class Tree:
 
 @dataclass
 class BinnedData:
-    """Resident binned shard: uint8 codes [N, Fp] (Fp multiple of 32) + targets/weights."""
+    """Resident binned shard: uint8 codes in the group-blocked layout ``[G, N, 32]`` (32
+    features per group, G = ceil(F / 32), padding features code 0) + targets/weights.
+
+    Blocked rather than row-major so the histogram kernel streams each 32-feature group's
+    rows as contiguous 32-B records (see ``ops/csrc/gbdt_kernels.hip``)."""
     bins: torch.Tensor
     y: torch.Tensor
     sig: torch.Tensor | None
@@ -158,19 +162,39 @@ class BinnedData:
 
     @property
     def n(self):
-        return self.bins.shape[0]
+        return self.bins.shape[1]
 
     @property
     def device(self):
         return self.bins.device
 
+    @property
+    def group_stride(self) -> int:
+        """Bytes between consecutive feature groups of the blocked layout."""
+        return self.bins.shape[1] * FG
+
+    def codes(self) -> torch.Tensor:
+        """Row-major ``[N, F]`` view (a copy) of the codes - CPU paths and tests."""
+        g, n, _ = self.bins.shape
+        return self.bins.permute(1, 0, 2).reshape(n, g * FG)[:, : self.n_feat]
+
+    @staticmethod
+    def blocked(codes: torch.Tensor, device="cpu") -> torch.Tensor:
+        """Row-major codes [N, F] (any int dtype, any device) -> blocked uint8 [G, N, 32] on
+        ``device``, one group at a time (no full-size intermediate)."""
+        n, f = codes.shape
+        g = (f + FG - 1) // FG
+        b = torch.zeros(g, n, FG, dtype=torch.uint8, device=device)
+        for gi in range(g):
+            c0, c1 = gi * FG, min(f, (gi + 1) * FG)
+            b[gi, :, : c1 - c0] = codes[:, c0:c1].to(device=device, dtype=torch.uint8)
+        return b
+
     @staticmethod
     def from_codes(codes, y, nbins, is_cat=None, sig=None, device="cpu"):
         codes = torch.as_tensor(codes)
         n, f = codes.shape
-        fp = (f + FG - 1) // FG * FG
-        b = torch.zeros(n, fp, dtype=torch.uint8, device=device)
-        b[:, :f] = codes.to(device=device, dtype=torch.uint8)
+        b = BinnedData.blocked(codes, device)
         y = torch.as_tensor(y, dtype=torch.float32).reshape(n).to(device)
         s = None if sig is None else torch.as_tensor(sig, dtype=torch.float32).reshape(n).to(device)
         nb = np.asarray(nbins, dtype=np.int32).reshape(f)
@@ -208,6 +232,14 @@ class TreeTrainer:
         self.train_errors: list[float] = []
         self.valid_errors: list[float] = []
         self.timings = {"hist": 0.0, "split": 0.0, "partition": 0.0, "apply": 0.0}
+        self._root_level = False
+        self._codes_cache = None
+
+    def _codes(self) -> torch.Tensor:
+        """Row-major codes for the CPU paths (built once)."""
+        if self._codes_cache is None:
+            self._codes_cache = self.data.codes()
+        return self._codes_cache
 
     # ------------------------------------------------------------------------------------
     def _weights_for_tree(self) -> torch.Tensor:
@@ -245,13 +277,12 @@ class TreeTrainer:
         # root stats for the root's own value
         tot = dist.all_reduce_(torch.stack([w.double().sum(), (w.double() * g.double()).sum()]))
         tw, ts = float(tot[0]), float(tot[1])
-        # int64 fixed-point scales: every bin sum over all ranks stays below 2^62
-        mx = torch.stack([w.abs().max().double(), (w * g).abs().max().double(),
-                          torch.tensor(float(n), dtype=torch.float64, device=self.dev)])
+        # fixed-point scales (powers of two, identical on every rank): per row w*scale_w < 2^16 and
+        # |w*g*scale_g| < 2^23, the field widths of the packed LDS histogram entries
+        mx = torch.stack([w.abs().max().double(), (w * g).abs().max().double()])
         dist.all_reduce_(mx, "max")
-        n_glob = float(mx[2]) * dist.info().world_size
-        self.scale_w = _fixed_scale(float(mx[0]), n_glob)
-        self.scale_g = _fixed_scale(float(mx[1]), n_glob)
+        self.scale_w = _pack_scale(float(mx[0]), W_BITS)
+        self.scale_g = _pack_scale(float(mx[1]), G_BITS)
         tree.exists[1] = True
         tree.value[1] = ts / tw if tw != 0 else 0.0
         tree.wgt_cnt[1] = tw
@@ -274,6 +305,7 @@ class TreeTrainer:
                 if not z["built"]:
                     z["sib_slot"] = slot_of[z["id"] ^ 1]
             n_built = sum(1 for z in nodes if z["built"])
+            self._root_level = level == 1
             t0 = time.perf_counter()
             hist = self._build_and_split(nodes, n_built, g, w, pos2row, hist_prev)
             best = hist["best"]            # per slot: (feat, bin, gain, lw, ls, rw, rs, valid)
@@ -420,7 +452,8 @@ class TreeTrainer:
         if items:
             it = torch.tensor(items, dtype=torch.int32, device=self.dev)
             slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
-            nat.call_hip("shifu_gbdt_hist", d.bins, d.bins.shape[1], pos2row, w, g, it, len(items), slab, F,
+            p2r = None if self._root_level else pos2row      # root: positions are rows
+            nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, g, it, len(items), slab, F,
                          self.scale_w, self.scale_g, st)
         else:
             slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
@@ -465,7 +498,7 @@ class TreeTrainer:
         """CPU oracle: same decomposition with torch ops (fp64 scan)."""
         d = self.data
         F, nn = self.F, len(nodes)
-        bins = d.bins[:, :F].long()
+        bins = self._codes().long()
         for z in nodes:
             if not z["built"]:
                 continue
@@ -537,7 +570,7 @@ class TreeTrainer:
             sb = torch.from_numpy(split_bin).to(self.dev)
             cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
             flag = torch.empty(n, dtype=torch.int32, device=self.dev)
-            nat.call_hip("shifu_gbdt_partition_flag", d.bins.data_ptr(), d.bins.shape[1], pos2row.data_ptr(),
+            nat.call_hip("shifu_gbdt_partition_flag", d.bins.data_ptr(), d.group_stride, pos2row.data_ptr(),
                          pos_node.data_ptr(), sf.data_ptr(), sb.data_ptr(), cl.data_ptr(), self.is_cat_t.data_ptr(),
                          flag.data_ptr(), n, st)
             cum = torch.cumsum(flag, 0, dtype=torch.int32)
@@ -572,7 +605,7 @@ class TreeTrainer:
         new_pn = torch.full_like(pos_node, -1)
         ranges = {}
         k = 0
-        bins = d.bins
+        bins = self._codes()
         for z in nodes:
             s_ = z["slot"]
             lo, hi = z["start"], z["end"]
@@ -602,10 +635,10 @@ class TreeTrainer:
             from ..ops import _native as nat
             feat, thr, cl, val = tree.device_arrays(data.device)
             ic = torch.from_numpy(data.is_cat.astype(np.uint8)).to(data.device)
-            nat.call_hip("shifu_gbdt_apply_tree", data.bins, data.bins.shape[1], None, feat, thr, cl, val, ic,
+            nat.call_hip("shifu_gbdt_apply_tree", data.bins, data.group_stride, None, feat, thr, cl, val, ic,
                          pred, float(scale), int(set_mode), None, data.n, tree.max_nodes, nat.stream_of(pred))
         else:
-            v = torch.from_numpy(tree.predict_bins(data.bins.numpy(), data.is_cat)).float()
+            v = torch.from_numpy(tree.predict_bins(data.codes().numpy(), data.is_cat)).float()
             if set_mode:
                 pred.copy_(v)
             else:
@@ -733,10 +766,14 @@ class TreeTrainer:
         return p
 
 
-def _fixed_scale(max_abs: float, n_rows: float) -> float:
-    """2^S such that n_rows * max_abs * 2^S < 2^62 (int64 histogram sums never overflow)."""
-    bound = max(max_abs, 1e-30) * max(n_rows, 1.0)
-    return float(2.0 ** min(60, math.floor(62 - math.log2(bound))))
+W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histogram fields)
+
+
+def _pack_scale(max_abs: float, bits: int) -> float:
+    """Largest 2^S with max_abs * 2^S <= 2^bits - 1 (so the rounded value stays < 2^bits)."""
+    if not max_abs > 0 or not math.isfinite(max_abs):
+        return 1.0
+    return float(2.0 ** min(60, math.floor(math.log2((2.0 ** bits - 1) / max_abs))))
 
 
 def _gain_py(imp, lw, ls, rw, rs):
@@ -766,17 +803,19 @@ def _gain_py(imp, lw, ls, rw, rs):
 # smoke + bench hooks
 # ------------------------------------------------------------------------------------------
 def synthetic_binned(n, f, device, seed=0, n_bins=256):
-    """uint8 codes [n, Fp] generated chunk-wise on the device (no int32 staging of the whole
+    """uint8 codes (blocked [G, n, 32]) generated chunk-wise on the device (no int32 staging of the whole
     matrix) + labels from a hidden rule on the first two features."""
     g = torch.Generator(device=device).manual_seed(seed)
-    fp = (f + FG - 1) // FG * FG
-    codes = torch.zeros(n, fp, dtype=torch.uint8, device=device)
+    ng = (f + FG - 1) // FG
+    codes = torch.zeros(ng, n, FG, dtype=torch.uint8, device=device)
     y = torch.empty(n, dtype=torch.float32, device=device)
     step = 1 << 21
     for r0 in range(0, n, step):
         r1 = min(n, r0 + step)
         blk = torch.randint(0, n_bins, (r1 - r0, f), generator=g, device=device, dtype=torch.int32)
-        codes[r0:r1, :f] = blk.to(torch.uint8)
+        for gi in range(ng):
+            c0, c1 = gi * FG, min(f, (gi + 1) * FG)
+            codes[gi, r0:r1, : c1 - c0] = blk[:, c0:c1].to(torch.uint8)
         x0 = blk[:, 0].float() / n_bins
         x1 = blk[:, 1].float() / n_bins
         y[r0:r1] = ((x0 + 0.5 * x1 + 0.1 * torch.rand(r1 - r0, generator=g, device=device)) > 0.8).float()

@@ -9,17 +9,18 @@
 //   GBT update  DTWorker.doCompute predict/output      J/core/dtrain/dt/DTWorker.java:620-670, Loss.java
 //
 // MI355X design:
-//   * bins are uint8 row-major [N][Fp] (Fp multiple of 32), rows grouped per node through a
-//     position->row permutation that is stably re-partitioned every level (rows of one node are
-//     a contiguous position range, so every histogram pass reads only that node's rows).
+//   * bins are uint8, group-blocked [G][N][32] (32 features per group, G = Fp / 32); rows are
+//     grouped per node through a position->row permutation that is stably re-partitioned every
+//     level (rows of one node are a contiguous position range, so every histogram pass reads
+//     only that node's rows, each as one contiguous 32-B record per group).
 //   * histograms keep only (sum w, sum w*g) per bin: for variance / friedman-mse / binary
 //     entropy / binary gini the best split depends on count and sum only (the sum-of-squares
-//     terms cancel in the variance gain), halving LDS atomic traffic.
+//     terms cancel in the variance gain).  Both sums are int64 fixed point, packed into ONE
+//     LDS atomic per (row, feature) (see gbdt_hist_kernel).
 //   * a work item = (node, row range, 32-feature group); a block builds its item's histogram
-//     in LDS (32 x 256 x 2 fp32 = 64 KiB, feature-major planes with a 257-word stride) with
-//     ds_add_f32 and writes it to a per-item slab with plain coalesced stores (no global
-//     atomics); the split kernel sums the slabs in fp64, derives the larger sibling by
-//     parent - smaller (histogram subtraction) and scans the bins.
+//     in LDS and writes it to a per-item slab with coalesced stores (no global atomics); the
+//     split kernel sums the slabs, derives the larger sibling by parent - smaller (histogram
+//     subtraction) and scans the bins.
 //   * deterministic: slab order is fixed and ties break to the lowest feature, then bin, so
 //     every rank computes the identical split from the all-reduced histograms.
 #include "common.h"
@@ -30,69 +31,119 @@ constexpr int NB = 256;        // max bins per feature (uint8 codes)
 constexpr int FG = 32;         // features per work-item group
 
 struct HistArgs {
-  const uint8_t* bins; long ldb;     // [N][ldb]
-  const int* pos2row;                // [N] position -> row id
+  const uint8_t* bins; long gs;      // group-blocked bins [G][N][32]: gs = N * 32 bytes per group
+  const int* pos2row;                // [N] position -> row id (nullptr: identity, the root level)
   const float* w;                    // [N] per-row weight (significance x subsample)
   const float* g;                    // [N] per-row target (label / pseudo residual)
   const int* items;                  // [n_items][4] = {node, pos_lo, pos_hi, group}
   long long* slab;                   // [n_items][2][FG][NB] int64 fixed point
   int n_items, n_feat;
-  double scale_w, scale_g;           // fixed-point scales (2^S, chosen so sums cannot overflow)
+  float scale_w, scale_g;            // powers of two: w*scale_w < 2^16, |w*g*scale_g| < 2^23
 };
 
-// gfx950 measured (tools/microbench_lds_atomics.hip): ds_add_f32 ~100 G updates/s vs
-// ds_add_u32/u64 ~1.7 T/s.  So the LDS histogram is int64 fixed point: exact, order-independent
-// (bit-identical on every rank / every run) and 17x faster than float LDS atomics.
-constexpr int HT = 512;        // threads per histogram block (8 waves)
-constexpr int HU = 4;          // row slots in flight per thread
-constexpr int HP = 257;        // padded plane stride (u64 words)
+// Histogram build (measured on gfx950 with tools/microbench_hist.hip, 16M rows x 1024 features):
+//   * bins are stored group-blocked [G][N][32] so a block streams its group's 32-B row records
+//     contiguously (row-major [N][1024] made every 32-B slice fetch its own 128-B line:
+//     1.4 TB/s -> 4.1 TB/s);
+//   * one packed ds_add_u64 per (row, feature): (qw << 36) + qg with qg signed.  Over <= 4096
+//     rows a bin's sums stay inside their fields (qw < 2^16 -> 28 bits, |qg| < 2^23 -> 36 bits
+//     signed), so the block unpacks the LDS histogram into int64 registers every 4096 rows.
+//     Exact: identical sums to two separate int64 atomics;
+//   * LDS layout [half][bin][16 features] + a per-lane rotation of the 16 feature bytes: lane
+//     r of a 16-lane LDS group updates feature (j + r) & 15 at step j, so the group's 16 lanes
+//     always hit 16 distinct bank pairs whatever the bins are.
+constexpr int HT = 512;                       // threads per histogram block (8 waves)
+constexpr int HU = 4;                         // row slots in flight per thread
+constexpr int RPP = HT / 2;                   // rows per slot pass (2 threads x 16 B per row)
+constexpr int HFLUSH = 4096 / (RPP * HU);     // passes between unpacks (4096 rows)
+constexpr int HNE = 2 * NB * 16 / HT;         // LDS entries each thread unpacks (16)
+constexpr int PACK_G = 36;                    // low field bits (signed qg)
+
+__device__ __forceinline__ uint32_t pick(uint32_t a, uint32_t b, bool c) { return c ? b : a; }
+
+__device__ __forceinline__ void unpack_add(unsigned long long v, long long& aw, long long& ag) {
+  const long long gq = ((long long)(v << (64 - PACK_G))) >> (64 - PACK_G);
+  ag += gq;
+  aw += (long long)((v - (unsigned long long)gq) >> PACK_G);
+}
 
 __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];   // [2][FG][HP]
-  unsigned long long* hw = hsm;
-  unsigned long long* hg = hsm + FG * HP;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];   // [2][NB][16]
   const int item = blockIdx.x;
   const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
-  for (int i = threadIdx.x; i < 2 * FG * HP; i += HT) hsm[i] = 0ull;
+  for (int i = threadIdx.x; i < 2 * NB * 16; i += HT) hsm[i] = 0ull;
   __syncthreads();
-  const int half = threadIdx.x & 1;                 // which 16-feature half of the 32-B slice
-  const int f0 = grp * FG + half * 16;              // padded features (>= n_feat) land in unused planes
-  unsigned long long* pw = hw + half * 16 * HP;
-  unsigned long long* pg = hg + half * 16 * HP;
-  constexpr int RPP = HT / 2;                       // rows per slot pass
-  for (int p0 = lo + (threadIdx.x >> 1); p0 < hi; p0 += RPP * HU) {
+  const int half = threadIdx.x & 1, r = threadIdx.x & 15, t2 = threadIdx.x >> 1;
+  const uint8_t* gb = a.bins + (size_t)grp * a.gs + half * 16;
+  unsigned long long* base = hsm + half * NB * 16;
+  long long accw[HNE], accg[HNE];
+#pragma unroll
+  for (int k = 0; k < HNE; ++k) { accw[k] = 0; accg[k] = 0; }
+  int it = 0;
+  for (int p0 = lo; p0 < hi; p0 += RPP * HU) {        // block-uniform trip count (unpack barriers)
     int rows[HU];
 #pragma unroll
-    for (int u = 0; u < HU; ++u) { const int p = p0 + u * RPP; rows[u] = p < hi ? a.pos2row[p] : -1; }
+    for (int u = 0; u < HU; ++u) {
+      const int p = p0 + t2 + u * RPP;
+      rows[u] = p < hi ? (a.pos2row ? a.pos2row[p] : p) : -1;
+    }
     float wv[HU], gv[HU];
     uint4 bv[HU];
 #pragma unroll
     for (int u = 0; u < HU; ++u) {
-      const int r = rows[u];
-      wv[u] = r >= 0 ? a.w[r] : 0.f;
-      gv[u] = r >= 0 ? a.g[r] : 0.f;
-      bv[u] = r >= 0 ? *(const uint4*)(a.bins + (size_t)r * a.ldb + f0) : make_uint4(0, 0, 0, 0);
+      const int rr = rows[u];
+      wv[u] = rr >= 0 ? a.w[rr] : 0.f;
+      gv[u] = rr >= 0 ? a.g[rr] : 0.f;
+      bv[u] = rr >= 0 ? *(const uint4*)(gb + (size_t)rr * 32) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < HU; ++u) {
       if (wv[u] == 0.f) continue;
-      const float wgf = wv[u] * gv[u];
-      const unsigned long long qw = (unsigned long long)__double2ll_rn((double)wv[u] * a.scale_w);
-      const unsigned long long qg = (unsigned long long)__double2ll_rn((double)wgf * a.scale_g);
-      const uint32_t words[4] = {bv[u].x, bv[u].y, bv[u].z, bv[u].w};
+      const unsigned long long q = ((unsigned long long)__float2uint_rn(wv[u] * a.scale_w) << PACK_G) +
+                                   (unsigned long long)(long long)__float2int_rn(wv[u] * gv[u] * a.scale_g);
+      // rotate the 16 bytes left by r: byte j of R = feature (j + r) & 15
+      const uint32_t W[4] = {bv[u].x, bv[u].y, bv[u].z, bv[u].w};
+      uint32_t X[4], Y[4], R[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) X[k] = pick(W[k], W[(k + 1) & 3], r & 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Y[k] = pick(X[k], X[(k + 2) & 3], r & 8);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) R[k] = __builtin_amdgcn_alignbyte(Y[(k + 1) & 3], Y[k], r & 3);
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const uint32_t b = (words[j >> 2] >> ((j & 3) * 8)) & 0xff;
-        atomicAdd(&pw[j * HP + b], qw);
-        atomicAdd(&pg[j * HP + b], qg);
+        const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
+        atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
       }
+    }
+    if (++it == HFLUSH) {
+      it = 0;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < HNE; ++k) {
+        unpack_add(hsm[threadIdx.x + k * HT], accw[k], accg[k]);
+        hsm[threadIdx.x + k * HT] = 0ull;
+      }
+      __syncthreads();
     }
   }
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < HNE; ++k) unpack_add(hsm[threadIdx.x + k * HT], accw[k], accg[k]);
+  // transpose through LDS ([f][b] per statistic) for coalesced slab stores
   long long* out = a.slab + (size_t)item * 2 * FG * NB;
-  for (int i = threadIdx.x; i < 2 * FG * NB; i += HT) {
-    const int st = i / (FG * NB), r = i % (FG * NB), f = r / NB, b = r % NB;
-    out[i] = (long long)hsm[st * FG * HP + f * HP + b];
+  long long* tsm = (long long*)hsm;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < HNE; ++k) {
+      const int e = threadIdx.x + k * HT;
+      const int f = (e >> 12) * 16 + (e & 15), b = (e >> 4) & (NB - 1);
+      tsm[f * NB + b] = st ? accg[k] : accw[k];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < FG * NB; i += HT) out[st * FG * NB + i] = tsm[i];
   }
 }
 
@@ -306,7 +357,7 @@ __global__ __launch_bounds__(256) void gbdt_split_kernel(SplitArgs a) {
 // split_feat < 0 -> node not split this level (rows stay, flag = 2 "keep").
 // ---------------------------------------------------------------------------------------
 struct PartArgs {
-  const uint8_t* bins; long ldb;
+  const uint8_t* bins; long gs;   // group-blocked [G][N][32]
   const int* pos2row;
   const int* pos_node;          // [N] node slot of each position (current level)
   const int* split_feat;        // [n_nodes]
@@ -324,7 +375,7 @@ __global__ void gbdt_partition_flag_kernel(PartArgs a) {
   const int f = node >= 0 ? a.split_feat[node] : -1;
   int fl = 0;
   if (f >= 0) {
-    const uint32_t b = a.bins[(size_t)a.pos2row[p] * a.ldb + f];
+    const uint32_t b = a.bins[(size_t)(f >> 5) * a.gs + (size_t)a.pos2row[p] * 32 + (f & 31)];
     if (a.is_cat[f]) fl = (a.cat_left[node * 8 + (b >> 5)] >> (b & 31)) & 1;
     else fl = (int)b <= a.split_bin[node] ? 1 : 0;
   }
@@ -366,7 +417,7 @@ __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
 // Used for validation rows, continuous-training recovery and GBT predict update.
 // ---------------------------------------------------------------------------------------
 struct TreeArgs {
-  const uint8_t* bins; long ldb;
+  const uint8_t* bins; long gs;   // group-blocked [G][N][32]
   const int* rows;               // nullable: row ids (else 0..n-1)
   const int* feat; const int* thr; const uint32_t* cat_left; const float* value; const uint8_t* is_cat;
   float* pred; float scale; int set_mode;
@@ -381,7 +432,7 @@ __global__ void gbdt_apply_tree_kernel(TreeArgs a) {
   int id = 1;
   while (id < a.max_nodes && a.feat[id] >= 0) {
     const int f = a.feat[id];
-    const uint32_t b = a.bins[(size_t)row * a.ldb + f];
+    const uint32_t b = a.bins[(size_t)(f >> 5) * a.gs + (size_t)row * 32 + (f & 31)];
     bool left;
     if (a.is_cat[f]) left = (a.cat_left[id * 8 + (b >> 5)] >> (b & 31)) & 1;
     else left = (int)b <= a.thr[id];
@@ -429,12 +480,13 @@ __global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
 
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
 
-SHIFU_API int shifu_gbdt_hist(const void* bins, long ldb, const int* pos2row, const float* w, const float* g,
+SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, const int* pos2row, const float* w, const float* g,
                               const int* items, int n_items, void* slab, int n_feat, double scale_w,
                               double scale_g, hipStream_t stream) {
-  if (ldb % 32 || n_items <= 0) return -1;
-  HistArgs a{(const uint8_t*)bins, ldb, pos2row, w, g, items, (long long*)slab, n_items, n_feat, scale_w, scale_g};
-  hipLaunchKernelGGL(gbdt_hist_kernel, dim3(n_items), dim3(HT), 2 * FG * HP * 8, stream, a);
+  if (gs % 32 || n_items <= 0) return -1;
+  HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, items, (long long*)slab, n_items, n_feat,
+             (float)scale_w, (float)scale_g};
+  hipLaunchKernelGGL(gbdt_hist_kernel, dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -456,10 +508,10 @@ SHIFU_API int shifu_gbdt_split(const void* slab, const int* node_items, int max_
   return 0;
 }
 
-SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long ldb, const int* pos2row, const int* pos_node,
+SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const int* pos2row, const int* pos_node,
                                         const int* split_feat, const int* split_bin, const void* cat_left,
                                         const void* is_cat, int* flag, long n, hipStream_t stream) {
-  PartArgs a{(const uint8_t*)bins, ldb, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
+  PartArgs a{(const uint8_t*)bins, gs, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
              (const uint8_t*)is_cat, flag, n};
   hipLaunchKernelGGL(gbdt_partition_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
@@ -477,12 +529,12 @@ SHIFU_API int shifu_gbdt_partition_scatter(const int* pos2row, const int* pos_no
   return 0;
 }
 
-SHIFU_API int shifu_gbdt_apply_tree(const void* bins, long ldb, const int* rows, const int* feat, const int* thr,
+SHIFU_API int shifu_gbdt_apply_tree(const void* bins, long gs, const int* rows, const int* feat, const int* thr,
                                     const void* cat_left, const float* value, const void* is_cat, float* pred,
                                     float scale, int set_mode, int* leaf_out, long n, int max_nodes,
                                     hipStream_t stream) {
   if (n <= 0) return 0;
-  TreeArgs a{(const uint8_t*)bins, ldb, rows, feat, thr, (const uint32_t*)cat_left, value, (const uint8_t*)is_cat,
+  TreeArgs a{(const uint8_t*)bins, gs, rows, feat, thr, (const uint32_t*)cat_left, value, (const uint8_t*)is_cat,
              pred, scale, set_mode, leaf_out, n, max_nodes};
   hipLaunchKernelGGL(gbdt_apply_tree_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());

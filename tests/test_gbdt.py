@@ -62,7 +62,7 @@ def test_gbt_reduces_error_and_predict_consistent():
     # tree partition consistency: host traversal of every tree reproduces predictions
     acc = np.zeros(len(y), np.float32)
     for i, t in enumerate(tr.trees):
-        v = t.predict_bins(data.bins.numpy(), data.is_cat)
+        v = t.predict_bins(data.codes().numpy(), data.is_cat)
         acc = v if i == 0 else acc + t.weight * v
     assert np.allclose(acc, p.numpy(), atol=1e-5)
 
@@ -129,7 +129,7 @@ def test_gpu_many_items_and_feature_mask():
     tr = TreeTrainer(TreeConfig("GBT", tree_num=3, max_depth=7, feature_subset_strategy="TWOTHIRDS"), data)
     tr.train()
     assert tr.train_errors[-1] < tr.train_errors[0]
-    host = data.bins.cpu().numpy()
+    host = data.codes().cpu().numpy()
     p = np.zeros(data.n, np.float32)
     for i, t in enumerate(tr.trees):
         v = t.predict_bins(host, data.is_cat)
