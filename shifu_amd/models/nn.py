@@ -25,6 +25,7 @@ every rank (replicated optimizer, no parameter server).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -451,6 +452,7 @@ class MLPTrainer:
                              adam_beta1, adam_beta2, learning_decay, reg, reg_level, fixed)
         self.chunk_rows = int(chunk_rows)
         self.wgrad_splits = wgrad_splits
+        self.fused_tail = self._tail_eligible()
         self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
         # dropout (NNMaster.dropoutNodes :531-556, FloatFlatNetwork.computeLayer :205-215): each
         # iteration drops hidden nodes with DropoutRate and inputs with 0.4*DropoutRate and scales
@@ -549,6 +551,26 @@ class MLPTrainer:
                 r1 = min(row_hi, r0 + self.chunk_rows)
                 self._chunk_torch(data, r0, r1)
 
+    def _tail_supported(self) -> bool:
+        """Shapes the fused tail kernel (ops/csrc/mlp_tail.hip) covers: last hidden layer padded
+        width <= 256, n_out <= 8, output-only derivatives for the activations it differentiates."""
+        sp = self.spec
+        L = len(sp.hidden)
+        if self.device.type != "cuda" or L == 0:
+            return False
+        ok = sp.layer_kpad[L] <= 256 and sp.n_out <= 8 and ACT_IDS[sp.acts[L - 1]] in ACT_DERIV_FROM_OUTPUT
+        if L >= 2:
+            ok = ok and ACT_IDS[sp.acts[L - 2]] in ACT_DERIV_FROM_OUTPUT
+        return bool(ok)
+
+    def _tail_eligible(self) -> bool:
+        """Opt-in (SHIFU_FUSED_TAIL=1).  Measured on MI355X at the bench shape (1M-row chunk,
+        512/256 padded hidden widths): fused 2.09 ms vs 1.76 ms for the three unfused kernels -
+        at one 148-KiB block per CU its k-steps wait on HBM/L2 (SQ_WAIT_ANY 55 % of wave
+        cycles), which 5 resident 128x128 GEMM blocks per CU hide.  Kept, tested, for shapes
+        where launch count dominates."""
+        return os.environ.get("SHIFU_FUSED_TAIL", "0") == "1" and self._tail_supported()
+
     def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None):
         from ..ops import _native as nat
         sp, kp = self.spec, self.spec.layer_kpad
@@ -562,21 +584,33 @@ class MLPTrainer:
         acts = [x] + [a[:mc] for a in ws["acts"]]
         dels = [None] + [d[:mc] for d in ws["deltas"]]
         ders = [None] + [(d[:mc] if d is not None else None) for d in ws["derivs"]]
-        for l in range(L):
+        fused = self.fused_tail
+        y = data.y[r0:r1]
+        s = data.s[r0:r1] if data.s is not None else None
+        for l in range(L - 1 if fused else L):
             a_in, a_out = acts[l], acts[l + 1]
             act = ACT_IDS[sp.acts[l]]
             nat.call_hip("shifu_gemm_nt", a_in.data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
                          a_out.data_ptr(), kp[l + 1], nat.ptr(ders[l + 1]), kp[l + 1], None, 0, None, 0,
                          mc, kp[l + 1], kp[l], 0, act, sp.hidden[l], 1, flat_spot(sp.acts[l]), st)
-        # output layer + loss + last hidden delta + output wgrad
-        hid_act = ACT_IDS[sp.acts[L - 1]] if L else 2
-        y = data.y[r0:r1]
-        s = data.s[r0:r1] if data.s is not None else None
-        nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], nat.ptr(ders[L]), kp[L],
-                     wv[L].data_ptr(), y.data_ptr(), sp.n_out, nat.ptr(s),
-                     nat.ptr(dels[L]) if L else None, kp[L], gv[L].data_ptr(), self.err_acc.data_ptr(),
-                     None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act], hid_act,
-                     LOSS_IDS[sp.loss], flat_spot(sp.out_act), flat_spot(sp.acts[L - 1]) if L else 0.0, st)
+        if fused:
+            # last hidden layer forward + output layer + loss + deltas + backward GEMM, one kernel
+            lh = L - 1
+            bwd = L >= 2
+            nat.call_hip("shifu_mlp_tail", acts[lh], kp[lh], wb[lh], sp.hidden[lh], kp[lh], ACT_IDS[sp.acts[lh]],
+                         flat_spot(sp.acts[lh]), wv[L], kp[L], y, sp.n_out, s, sp.n_out, ACT_IDS[sp.out_act],
+                         LOSS_IDS[sp.loss], flat_spot(sp.out_act), dels[L], kp[L], gv[L], self.err_acc,
+                         int(bwd), wt[lh] if bwd else None, kp[L], dels[lh] if bwd else None, kp[lh],
+                         ACT_IDS[sp.acts[lh - 1]] if bwd else 0, sp.hidden[lh - 1] if bwd else 0,
+                         flat_spot(sp.acts[lh - 1]) if bwd else 0.0, mc, 0, st)
+        else:
+            # output layer + loss + last hidden delta + output wgrad
+            nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], nat.ptr(ders[L]), kp[L],
+                         wv[L].data_ptr(), y.data_ptr(), sp.n_out, nat.ptr(s),
+                         nat.ptr(dels[L]) if L else None, kp[L], gv[L].data_ptr(), self.err_acc.data_ptr(),
+                         None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act],
+                         ACT_IDS[sp.acts[L - 1]] if L else 2, LOSS_IDS[sp.loss], flat_spot(sp.out_act),
+                         flat_spot(sp.acts[L - 1]) if L else 0.0, st)
         splits = self.wgrad_splits
         for l in range(L - 1, -1, -1):
             # wgrad of layer l: G_l[h_l, K_l] += D_{l+1}^T A_l
@@ -587,7 +621,7 @@ class MLPTrainer:
                 spl = splits
             nat.call_hip("shifu_wgrad_tn", dels[l + 1].data_ptr(), kp[l + 1], acts[l].data_ptr(), kp[l],
                          gv[l].data_ptr(), kp[l], mc, sp.hidden[l], kp[l], spl, st)
-            if l >= 1:
+            if l >= 1 and not (fused and l == L - 1):
                 # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)
                 act = ACT_IDS[sp.acts[l - 1]]
                 nat.call_hip("shifu_gemm_nt", dels[l + 1].data_ptr(), kp[l + 1], wt[l].data_ptr(), kp[l + 1],

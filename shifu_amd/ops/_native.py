@@ -39,6 +39,8 @@ HIP_SIGNATURES = {
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
     "shifu_cast_bf16": "plpliis",
     "shifu_transpose_cast": "plpiiis",
+    # mlp_tail.hip
+    "shifu_mlp_tail": "plpiiif" "pipl" "piiif" "plpp" "i" "plpl" "iif" "ii" "s",
     # gbdt_kernels.hip
     "shifu_gbdt_hist": "plpppp" "ipi" "dd" "s",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",

@@ -348,6 +348,65 @@ __global__ __launch_bounds__(GB_T, 1) void gemm_nt_big_kernel(GemmArgs p) {
   }
 }
 
+// Staged epilogue of the 256 x 256 kernels (512 threads, 8 waves 2 M x 4 N, wave tile 128 x 64,
+// acc[n-sub 0..3][m-sub 0..7]): the whole bf16 tile goes through LDS ([256][512 B], 16-B chunk ^
+// (row & 15)) and leaves as 16-B row-segment stores (dgrad reads the matching H segments).
+// The caller guarantees every wave has finished reading the LDS staging buffers.
+template <int EPI, int ACT>
+__device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  char* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ml = wr * 128 + j * 16 + (lane & 15);
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = acc[i][j][r];
+        const int n = n0 + nl + r;
+        if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
+        else if constexpr (EPI == EPI_STORE) o[r] = n < p.NB ? z : 0.f;
+        else o[r] = z;
+      }
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+      w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+      const int c = nl >> 3, half = (nl >> 2) & 1;
+      *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
+    }
+  }
+  __syncthreads();
+  const int c = tid & 31;
+#pragma unroll 4
+  for (int pass = 0; pass < 16; ++pass) {
+    const int ml = pass * 16 + (tid >> 5);
+    const int m = m0 + ml, n = n0 + c * 8;
+    if (m >= p.M || n >= p.N) continue;
+    uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
+    if constexpr (EPI == EPI_DACT) {
+      const uint4 hh = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+      const uint32_t hv[4] = {hh.x, hh.y, hh.z, hh.w};
+      uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a0 = bf2f(vv[q] & 0xffff), a1 = bf2f(vv[q] >> 16);
+        const float d0 = act_deriv_out(ACT, bf2f(hv[q] & 0xffff)) + p.flat;
+        const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
+        a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
+        a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
+        vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+      }
+      v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
+    else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Pipelined NT GEMM with LDS-DMA (global_load_lds_dwordx4): 256 x 256 tile, BK = 32, a ring of
 // 4 LDS stages (4 x 32 KiB) with 3 k-tiles in flight.  8 waves (2 M x 4 N, 128 x 64 each),
@@ -434,56 +493,139 @@ __global__ __launch_bounds__(GP_T, 1) void gemm_nt_pipe_kernel(GemmArgs p) {
   __builtin_amdgcn_s_barrier();             // every wave done reading the ring (DMA drained: vmcnt(0))
   __builtin_amdgcn_sched_barrier(0);
 
-  // staged epilogue: whole 256 x 256 bf16 tile in LDS ([256][512 B], 16-B chunk ^ (row & 15))
-  char* Cs = smem;
+  epilogue_256<EPI, ACT>(p, acc, m0, n0, smem);
+}
+
+// ---------------------------------------------------------------------------------------
+// 8-phase NT GEMM (256 x 256 x 64, 8 waves 2 M x 4 N, wave tile 128 x 64, 1 block per CU).
+//
+// The schedule follows the CDNA4 "256^2 8-phase" recipe (cdna_hip_programming.md §5): one
+// iteration = 2 k-tiles = 8 phases; each phase is [ds_read fragments + one LDS-DMA half-tile
+// prefetch] s_barrier [16 MFMAs on one quadrant of the wave tile] s_barrier, and the two wave
+// rows run one barrier apart, so on every SIMD one wave's MFMAs overlap the other wave's
+// reads / DMA issue.  LDS = 2 k-tile buffers x 4 half-tiles (A rows 0-127 / 128-255, B rows
+// 0-127 / 128-255; 16 KiB each, [128 rows][128 B], 16-B chunk ^ ((row >> 1) & 7) swizzle that
+// the DMA applies on the GLOBAL source address).
+//
+// Per iteration (even k-tile 2i in buffer 0, odd 2i+1 in buffer 1), per wave:
+//   P1 DMA odd A-top(2i+1)   read A[mh0] B[nh0] (buf 0)  MFMA quadrant (0,0)
+//   P2 DMA odd A-bot(2i+1)   read B[nh1], lgkmcnt(0) before the barrier      (0,1)
+//   P3 DMA even B-0(2i+2)    read A[mh1]                                      (1,1)
+//   P4 DMA even B-1(2i+2)    vmcnt(4): odd buffer landed                      (1,0)
+//   P5-P8: the same on buffer 1 (DMA even A-top/A-bot(2i+2), odd B-0/B-1(2i+3)).
+// Write-after-read: a half-tile is re-staged >= 2 phases after its last ds_read (B: 1 phase,
+// its reads are retired before that phase's first barrier).  Read-after-DMA: the vmcnt(4) at
+// P4 / P8 (the two youngest half-tiles stay in flight) retires every DMA into the buffer read
+// in the next 3 phases, and a barrier separates the wait from the reads (no __syncthreads in
+// the loop: its fence would drain vmcnt to 0).  DMA past the last k-tile re-reads k-tile nk-1
+// into the buffer that is not read any more, so the counted waits stay exact.
+// ---------------------------------------------------------------------------------------
+constexpr int G8_T = 512, G8_HALF = 16384, G8_BUF = 4 * G8_HALF;
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = (p.N + 255) / 256;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * 256, n0 = (wg % ntn) * 256;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nk = p.K / 64;
+
+  // DMA sources: half-tile h (0 A-top, 1 A-bot, 2 B-0, 3 B-1), instruction i (2 per thread):
+  // LDS byte P = i*8192 + wid*1024 + lane*16 of the half-tile holds logical chunk lc of row P>>7.
+  long off[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ml = wr * 128 + j * 16 + (lane & 15);
-      float o[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = acc[i][j][r];
-        const int n = n0 + nl + r;
-        if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
-        else if constexpr (EPI == EPI_STORE) o[r] = n < p.NB ? z : 0.f;
-        else o[r] = z;
-      }
-      uint2 w;
-      w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-      w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-      const int c = nl >> 3, half = (nl >> 2) & 1;
-      *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
-    }
+  for (int i = 0; i < 2; ++i) {
+    const int P = i * 8192 + wid * 1024 + lane * 16;
+    const int row = P >> 7, lc = ((P >> 4) & 7) ^ ((row >> 1) & 7);
+    off[0][i] = (long)min(m0 + row, p.M - 1) * p.lda + lc * 8;
+    off[1][i] = (long)min(m0 + 128 + row, p.M - 1) * p.lda + lc * 8;
+    off[2][i] = (long)min(n0 + row, p.NB - 1) * p.ldb + lc * 8;
+    off[3][i] = (long)min(n0 + 128 + row, p.NB - 1) * p.ldb + lc * 8;
   }
-  __syncthreads();
-  const int c = tid & 31;
-#pragma unroll 4
-  for (int pass = 0; pass < 16; ++pass) {
-    const int ml = pass * 16 + (tid >> 5);
-    const int m = m0 + ml, n = n0 + c * 8;
-    if (m >= p.M || n >= p.N) continue;
-    uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
-    if constexpr (EPI == EPI_DACT) {
-      const uint4 hh = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
-      const uint32_t hv[4] = {hh.x, hh.y, hh.z, hh.w};
-      uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+  auto dma = [&](int h, int kt) {
+    char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
+    const int k0 = min(kt, nk - 1) * 64;
+    const bf16_t* src = h < 2 ? p.A : p.B;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float a0 = bf2f(vv[q] & 0xffff), a1 = bf2f(vv[q] >> 16);
-        const float d0 = act_deriv_out(ACT, bf2f(hv[q] & 0xffff)) + p.flat;
-        const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
-        a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
-        a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
-        vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
-      }
-      v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
-    }
-    if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
-    else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src + off[h][i] + k0), (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  const int lr = lane & 15, lq = lane >> 4;
+  auto readA = [&](int buf, int mh) {
+    const char* base = smem + buf * G8_BUF + wr * G8_HALF;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) af[t][c] = *(const bf16x8*)(base + swz_nt(mh * 64 + t * 16 + lr, c * 4 + lq));
+  };
+  auto readB = [&](int buf, int nh, bf16x8 (&bq)[2][2]) {
+    const char* base = smem + buf * G8_BUF + (2 + (wc >> 1)) * G8_HALF;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        bq[t][c] = *(const bf16x8*)(base + swz_nt((wc & 1) * 64 + nh * 32 + t * 16 + lr, c * 4 + lq));
+  };
+  auto mma = [&](int mh, int nh, bf16x8 (&bq)[2][2]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[nh * 2 + s_][mh * 4 + t] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s_][c], af[t][c], acc[nh * 2 + s_][mh * 4 + t], 0, 0, 0);
+  };
+#define G8_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
+                      __builtin_amdgcn_sched_barrier(0); } while (0)
+#define G8_MMA(mh, nh, bq, on) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    if (on) { __builtin_amdgcn_s_setprio(1); mma(mh, nh, bq); __builtin_amdgcn_s_setprio(0); } } while (0)
+
+  // prologue: even k-tile 0 complete, odd k-tile 1 B halves in flight
+  dma(2, 0); dma(3, 0); dma(0, 0); dma(1, 0);
+  dma(2, 1); dma(3, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  G8_BAR();
+  if (wr == 1) G8_BAR();                      // stagger the two wave rows by one barrier
+
+  for (int ke = 0; ke < nk; ke += 2) {
+    const int ko = ke + 1;
+    const bool odd_on = ko < nk;
+    // ---- even k-tile (buffer 0)
+    dma(0, ko); readB(0, 0, bf0); readA(0, 0);                                   // P1
+    G8_BAR(); G8_MMA(0, 0, bf0, true); G8_BAR();
+    dma(1, ko); readB(0, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P2
+    G8_BAR(); G8_MMA(0, 1, bf1, true); G8_BAR();
+    dma(2, ke + 2); readA(0, 1);                                                 // P3
+    G8_BAR(); G8_MMA(1, 1, bf1, true); G8_BAR();
+    dma(3, ke + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P4
+    G8_BAR(); G8_MMA(1, 0, bf0, true); G8_BAR();
+    // ---- odd k-tile (buffer 1)
+    dma(0, ke + 2); readB(1, 0, bf0); readA(1, 0);                               // P5
+    G8_BAR(); G8_MMA(0, 0, bf0, odd_on); G8_BAR();
+    dma(1, ke + 2); readB(1, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P6
+    G8_BAR(); G8_MMA(0, 1, bf1, odd_on); G8_BAR();
+    dma(2, ko + 2); readA(1, 1);                                                 // P7
+    G8_BAR(); G8_MMA(1, 1, bf1, odd_on); G8_BAR();
+    dma(3, ko + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P8
+    G8_BAR(); G8_MMA(1, 0, bf0, odd_on); G8_BAR();
   }
+  if (wr == 0) G8_BAR();                      // re-align the rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the trailing prefetches
+  G8_BAR();
+#undef G8_MMA
+#undef G8_BAR
+  epilogue_256<EPI, ACT>(p, acc, m0, n0, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -630,9 +772,10 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 static int g_stages = 1;     // LDS stages of the MLP GEMMs (A/B switch for tuning; 1 = default)
-static int g_big = 0;        // large-M path: 0 = 128x128 kernel, 1 = 256x256 register-staged, 2 = 256x256 DMA ring
+static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N >= 512, K >= 512; else 128x128),
+                             // 1 = 256x256 register-staged, 2 = 256x256 DMA ring, 3 = 8-phase, 4 = 128x128 only
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
-SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b >= 0 && b <= 2) ? b : 0; return 0; }
+SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b >= 0 && b <= 4) ? b : 0; return 0; }
 
 SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc,
                             void* C2, long ldc2, const void* H, long ldh, const void* Hd, long ldhd,
@@ -649,6 +792,22 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;
   const bool dfo_act = act_deriv_from_output(act);
+  const bool auto8 = g_big == 0 && M >= 65536 && N >= 512 && K >= 512;
+  if ((g_big == 3 || auto8) && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
+    const int grid8 = ((M + 255) / 256) * ((N + 255) / 256);
+    const size_t lds8 = 2 * G8_BUF;
+#define GEMM8_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_kernel<E, A>), dim3(grid8), dim3(G8_T), lds8, stream, p)
+#define GEMM8_ACTS(E) switch (act) { case 0: GEMM8_L(E, 0); break; case 1: GEMM8_L(E, 1); break; \
+    case 2: GEMM8_L(E, 2); break; case 3: GEMM8_L(E, 3); break; case 4: GEMM8_L(E, 4); break; \
+    case 6: GEMM8_L(E, 6); break; default: GEMM8_L(E, 7); break; }
+    if (epi == EPI_ACT) { GEMM8_ACTS(EPI_ACT) }
+    else if (epi == EPI_DACT) { GEMM8_ACTS(EPI_DACT) }
+    else GEMM8_L(EPI_STORE, 2);
+#undef GEMM8_ACTS
+#undef GEMM8_L
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
   if (g_big == 2 && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
     const int gridp = ((M + GP_M - 1) / GP_M) * ((N + GP_N - 1) / GP_N);
     const size_t ldsp = GP_ST * GP_STAGE;

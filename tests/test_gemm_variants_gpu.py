@@ -1,17 +1,18 @@
 """Every NT GEMM code path (128x128 register-staged, 256x256 register-staged, 256x256 LDS-DMA
-ring) against a torch fp32 reference, for the forward (act), dgrad (dact) and store epilogues."""
+ring, 256x256 8-phase) against a torch fp32 reference, for the forward (act), dgrad (dact) and store epilogues."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("epi", ["act", "dact", "store"])
-def test_gemm_nt_variants(variant, epi):
+@pytest.mark.parametrize("K", [320, 1024])
+def test_gemm_nt_variants(variant, epi, K):
     from shifu_amd.ops import _native as nat
     torch.manual_seed(0)
-    M, N, K, NB, nv = 70000 + 37, 512, 320, 500, 500
+    M, N, NB, nv = 70000 + 37, 512, 500, 500
     dev = "cuda"
     A = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
     B = (torch.randn(NB, K, device=dev) * 0.05).to(torch.bfloat16)

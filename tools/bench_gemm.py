@@ -70,7 +70,20 @@ def main():
     def wgrad2():
         nat.call_hip("shifu_wgrad_tn", D2, 256, H1, 512, G2, 512, M, 200, 512, spl(200, 512), st)
 
-    for name, fn, flops in (("fwd1", fwd1, 2 * M * 512 * 1024), ("fwd2", fwd2, 2 * M * 256 * 512),
+    Cs = torch.empty(M, 512, device=dev, dtype=bf)
+
+    def pure():                 # plain GEMM (store epilogue) at the forward-1 shape
+        nat.call_hip("shifu_gemm_nt", X, 1024, W1, 1024, 500, Cs, 512, None, 0, None, 0, None, 0, M, 512, 1024, 2,
+                     2, 500, 0, 0.0, st)
+
+    W1p = torch.zeros(512, 1024, device=dev, dtype=bf)
+    W1p[:500] = W1
+
+    def blaslt():               # hipBLASLt through torch at the same shape (library reference)
+        torch.mm(X, W1p.t(), out=Cs)
+
+    for name, fn, flops in (("pure_gemm", pure, 2 * M * 512 * 1024), ("torch_mm", blaslt, 2 * M * 512 * 1024),
+                            ("fwd1", fwd1, 2 * M * 512 * 1024), ("fwd2", fwd2, 2 * M * 256 * 512),
                             ("dgrad1", dgrad, 2 * M * 512 * 256), ("wgrad1", wgrad1, 2 * M * 512 * 1024),
                             ("wgrad2", wgrad2, 2 * M * 256 * 512)):
         ms = timeit(fn, a.iters)
