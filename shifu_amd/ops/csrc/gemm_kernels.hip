@@ -765,6 +765,148 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
 // ---------------------------------------------------------------------------------------
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// 8-phase TN wgrad: G[n][k] += sum_m D[m][n] X[m][k] over a split of rows, 256 (n) x 256 (k)
+// output tile, k-steps of 64 rows, the schedule of gemm_nt_8ph_kernel with D in the role of A
+// (wave tile 128 n) and X in the role of B (wave tile 64 k).  Half-tiles are [64 rows][128
+// cols] images (256-B rows, TN quad swizzle, filled by LDS-DMA with the swizzle applied on the
+// source address) read with ds_read_b64_tr_b16.  Rows are consumed in whole 64-row steps (the
+// host hands a tail of M % 64 rows to wgrad_tn_kernel); columns past the buffers are clamped on
+// load and their outputs dropped.
+// ---------------------------------------------------------------------------------------
+struct Wgrad8Args {
+  const bf16_t* D; long ldd;
+  const bf16_t* X; long ldx;
+  float* G; long ldg;
+  int Nv, Kx, rows_per_split, m_end;   // rows [0, m_end) with m_end % 64 == 0
+};
+
+__global__ __launch_bounds__(G8_T, 1) void wgrad_8ph_kernel(Wgrad8Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_n = (p.Nv + 255) / 256, tiles_k = (p.Kx + 255) / 256;
+  const int ntiles = tiles_n * tiles_k;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wg / ntiles, t = wg % ntiles;
+  const int n0 = (t / tiles_k) * 256, k0 = (t % tiles_k) * 256;
+  const int mbeg = split * p.rows_per_split;
+  const int mend = min(p.m_end, mbeg + p.rows_per_split);
+  if (mbeg >= mend) return;
+  const int nk = (mend - mbeg) / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid >> 2, wk = wid & 3;
+
+  // DMA sources (element offsets without the row step): half-tile h (0/1 D cols n0 + 128h,
+  // 2/3 X cols k0 + 128(h-2)), instruction i: LDS byte P = i*8192 + wid*1024 + lane*16
+  long off[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int P = i * 8192 + wid * 1024 + lane * 16;
+    const int row = P >> 8, pc = (P >> 4) & 15;
+    const int lc = pc ^ (tr_h(row) << 1);
+    const int cd0 = min(n0 + lc * 8, (int)p.ldd - 8), cd1 = min(n0 + 128 + lc * 8, (int)p.ldd - 8);
+    const int cx0 = min(k0 + lc * 8, (int)p.ldx - 8), cx1 = min(k0 + 128 + lc * 8, (int)p.ldx - 8);
+    off[0][i] = (long)(mbeg + row) * p.ldd + cd0;
+    off[1][i] = (long)(mbeg + row) * p.ldd + cd1;
+    off[2][i] = (long)(mbeg + row) * p.ldx + cx0;
+    off[3][i] = (long)(mbeg + row) * p.ldx + cx1;
+  }
+  auto dma = [&](int h, int kt) {
+    char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
+    const long r0 = (long)min(kt, nk - 1) * 64;
+    const bf16_t* src = h < 2 ? p.D + r0 * p.ldd : p.X + r0 * p.ldx;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src + off[h][i]), (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  auto frag = [&](const char* img, int col_base, int c) {
+    const int mr = c * 32 + 8 * g + tq, q = col_base / 4 + tp;
+    const s16x4 lo = ds_read_tr16_b64(img + swz_tn_quad(mr, q));
+    const s16x4 hi = ds_read_tr16_b64(img + swz_tn_quad(mr + 4, q));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto readD = [&](int buf, int nh) {
+    const char* img = smem + buf * G8_BUF + wn * G8_HALF;
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) af[t4][c] = frag(img, (nh * 4 + t4) * 16, c);
+  };
+  auto readX = [&](int buf, int kh, bf16x8 (&bq)[2][2]) {
+    const char* img = smem + buf * G8_BUF + (2 + (wk >> 1)) * G8_HALF;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) bq[s2][c] = frag(img, (wk & 1) * 64 + (kh * 2 + s2) * 16, c);
+  };
+  auto mma = [&](int nh, int kh, bf16x8 (&bq)[2][2]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4)
+          acc[nh * 4 + t4][kh * 2 + s2] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t4][c], bq[s2][c], acc[nh * 4 + t4][kh * 2 + s2], 0, 0, 0);
+  };
+#define G8_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
+                      __builtin_amdgcn_sched_barrier(0); } while (0)
+#define G8_MMA(nh, kh, bq, on) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    if (on) { __builtin_amdgcn_s_setprio(1); mma(nh, kh, bq); __builtin_amdgcn_s_setprio(0); } } while (0)
+
+  dma(2, 0); dma(3, 0); dma(0, 0); dma(1, 0);
+  dma(2, 1); dma(3, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  G8_BAR();
+  if (wn == 1) G8_BAR();
+
+  for (int ke = 0; ke < nk; ke += 2) {
+    const int ko = ke + 1;
+    const bool odd_on = ko < nk;
+    dma(0, ko); readX(0, 0, bf0); readD(0, 0);                                   // P1
+    G8_BAR(); G8_MMA(0, 0, bf0, true); G8_BAR();
+    dma(1, ko); readX(0, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P2
+    G8_BAR(); G8_MMA(0, 1, bf1, true); G8_BAR();
+    dma(2, ke + 2); readD(0, 1);                                                 // P3
+    G8_BAR(); G8_MMA(1, 1, bf1, true); G8_BAR();
+    dma(3, ke + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P4
+    G8_BAR(); G8_MMA(1, 0, bf0, true); G8_BAR();
+    dma(0, ke + 2); readX(1, 0, bf0); readD(1, 0);                               // P5
+    G8_BAR(); G8_MMA(0, 0, bf0, odd_on); G8_BAR();
+    dma(1, ke + 2); readX(1, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P6
+    G8_BAR(); G8_MMA(0, 1, bf1, odd_on); G8_BAR();
+    dma(2, ko + 2); readD(1, 1);                                                 // P7
+    G8_BAR(); G8_MMA(1, 1, bf1, odd_on); G8_BAR();
+    dma(3, ko + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P8
+    G8_BAR(); G8_MMA(1, 0, bf0, odd_on); G8_BAR();
+  }
+  if (wn == 0) G8_BAR();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef G8_MMA
+#undef G8_BAR
+  // acc[i][j]: G[n][k], k = k0 + 64 wk + 16 j + (lane & 15), n = n0 + 128 wn + 16 i + 4 (lane >> 4) + r
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
+      if (n >= p.Nv) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
+        if (k < p.Kx) atomicAdd(p.G + (size_t)n * p.ldg + k, acc[i][j][r]);
+      }
+    }
+}
+
 // =======================================================================================
 // C ABI (called through ctypes; host-side shape checks live in shifu_amd/ops/mlp.py and
 // are repeated here so a bad call fails loudly instead of faulting the GPU).
@@ -861,6 +1003,28 @@ SHIFU_API int shifu_wgrad_tn(const void* D, long ldd, const void* X, long ldx, f
   int rps = (M + splits - 1) / splits;
   rps = ((rps + WT_BM - 1) / WT_BM) * WT_BM;
   splits = (M + rps - 1) / rps;
+  // opt-in (set_big(3)): at the bench shape it measured 2.09 ms vs 1.39 ms for the 128x128
+  // kernel - the 8 output tiles sharing a row range drift apart by more than L2 holds, so each
+  // re-reads its rows from HBM (8 GB vs ~3 GB), while 5 smaller blocks per CU stay in step.
+  const bool use8 = g_big == 3;
+  if (use8 && M >= 65536 && Kx >= 256 && Nv >= 128 && ldd >= 8 && ldx >= 8) {
+    // 8-phase path over whole 64-row steps; ~256 blocks (one per CU), the M % 64 tail below
+    const int tiles8 = ((Nv + 255) / 256) * ((Kx + 255) / 256);
+    int sp8 = 256 / tiles8;
+    if (sp8 < 1) sp8 = 1;
+    const int m64 = M - M % 64;
+    int rps8 = (m64 / 64 + sp8 - 1) / sp8 * 64;
+    sp8 = (m64 + rps8 - 1) / rps8;
+    Wgrad8Args q{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, G, ldg, Nv, Kx, rps8, m64};
+    hipLaunchKernelGGL(wgrad_8ph_kernel, dim3(tiles8 * sp8), dim3(G8_T), 2 * G8_BUF, stream, q);
+    CHECK_HIP(hipGetLastError());
+    if (m64 == M) return 0;
+    D = (const bf16_t*)D + (size_t)m64 * ldd;
+    X = (const bf16_t*)X + (size_t)m64 * ldx;
+    M -= m64;
+    splits = 1;
+    rps = M;
+  }
   WgradArgs p{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, G, ldg, M, Nv, Kx, rps};
   const int ntiles = ((Nv + WT_BN - 1) / WT_BN) * (Kx / WT_BK);
   if (g_stages == 2)
