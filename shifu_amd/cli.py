@@ -8,6 +8,7 @@ RANK/LOCAL_RANK/WORLD_SIZE from the environment and joins the RCCL process group
 from __future__ import annotations
 
 import os
+import time
 import sys
 
 from . import __version__
@@ -58,16 +59,21 @@ def main(argv=None) -> int:
     if cmd in ("train", "stats", "norm", "normalize", "transform", "varsel", "eval", "posttrain"):
         dist.init_from_env()
     from .utils.trace import step_timer
+    from .utils.telemetry import record_usage
+    t0, rc = time.time(), 1
     try:
         with step_timer(cmd):
-            return _dispatch(cmd, args)
+            rc = _dispatch(cmd, args)
+            return rc
     except Exception as e:      # noqa: BLE001 - processors report errors and return non-zero
         if environment.get_bool("shifu.debug", False) or os.environ.get("SHIFU_DEBUG") == "1":
             raise
         _log.error("Error: %s: %s", type(e).__name__, e)
         return 1
     finally:
-        if dist.info().world_size > 1:
+        info = dist.info()
+        record_usage(cmd, args, rc if isinstance(rc, int) else 0, time.time() - t0, info.world_size, info.rank)
+        if info.world_size > 1:
             dist.shutdown()
 
 

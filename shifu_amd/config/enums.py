@@ -10,7 +10,7 @@ NORM_TYPES = ("OLD_ZSCORE", "OLD_ZSCALE", "ZSCORE", "ZSCALE", "WOE", "WEIGHT_WOE
               "WOE_ZSCORE", "WOE_ZSCALE", "WEIGHT_WOE_ZSCORE", "WEIGHT_WOE_ZSCALE", "ONEHOT", "ZSCALE_ONEHOT",
               "ASIS_WOE", "ASIS_PR", "DISCRETE_ZSCORE", "DISCRETE_ZSCALE", "ZSCALE_INDEX", "ZSCORE_INDEX",
               "WOE_INDEX", "WOE_ZSCALE_INDEX")
-ALGORITHMS = ("NN", "LR", "SVM", "DT", "RF", "GBT", "TENSORFLOW", "WDL")
+ALGORITHMS = ("NN", "LR", "SVM", "DT", "RF", "GBT", "TENSORFLOW", "WDL", "GENERIC")
 MULTI_CLASSIFICATION = ("NATIVE", "ONEVSALL", "ONEVSREST", "ONEVSONE")
 POST_CORRELATION_METRICS = ("IV", "KS", "SE")
 COLUMN_FLAGS = ("ForceSelect", "ForceRemove", "Candidate", "Meta", "Target", "Weight")

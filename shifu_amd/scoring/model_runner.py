@@ -6,6 +6,8 @@
   J/core/Scorer.java:219-506): NN/LR/WDL get the ColumnConfig-normalized selected columns, trees
   the raw values; per model one score (or one per class), then mean/max/min/median x scoreScale
   (``EvalScoreUDF`` J/udf/EvalScoreUDF.java:226).
+* generic models (``models/*.json`` GenericModelConfig, ``scoring/generic.py``) when the
+  algorithm is ``generic`` / ``tensorflow``.
 * ``IndependentNNModel`` (binary ``.nn`` with embedded column stats, J/core/dtrain/nn/IndependentNNModel.java:211-232)
   and ``IndependentTreeModel`` (``.gbt``) as dependency-light production scorers.
 
@@ -108,10 +110,18 @@ class ModelRunner:
         self.mc, self.ccs = mc, ccs
         self.dev = _dev(device)
         conv = gbt_convert or "RAW"
-        paths = model_paths if model_paths is not None else list_model_files(models_dir, mc.algorithm)
+        from .generic import GENERIC_ALGORITHMS, find_generic_models, load_generic
+        generic = str(mc.algorithm or "").lower() in GENERIC_ALGORITHMS
+        if model_paths is not None:
+            paths = model_paths
+        elif generic:
+            paths = find_generic_models(models_dir)
+        else:
+            paths = list_model_files(models_dir, mc.algorithm)
         if not paths:
             raise FileNotFoundError(f"no models under {models_dir}")
-        self.models = [load_model(p, self.dev, conv) for p in paths]
+        self.models = [LoadedModel(p, "generic", load_generic(p)) if p.endswith(".json")
+                       else load_model(p, self.dev, conv) for p in paths]
         from ..config.column_config import model_input_columns
         self.selected = model_input_columns(ccs, mc.is_binary())
 
@@ -122,6 +132,8 @@ class ModelRunner:
                 cols |= set(m.obj.model.names.values())
             if m.kind == "nn_binary":
                 cols |= {s.column_name for s in m.obj["column_stats"]}
+            if m.kind == "generic":
+                cols |= set(m.obj.input_names)
         return cols
 
     def _normalized(self, table, cache):
@@ -145,7 +157,24 @@ class ModelRunner:
                 outs.append(m.obj.score(table)[:, None])
             elif m.kind == "wdl":
                 outs.append(m.obj.score_table(self.mc, self.ccs, table)[:, None])
+            elif m.kind == "generic":
+                outs.append(m.obj.compute(self._generic_inputs(m.obj, table, cache)))
         return outs
+
+    def _generic_inputs(self, gm, table, cache):
+        """Normalized inputs in the generic model's ``inputnames`` order (default: selected)."""
+        names = gm.input_names
+        if not names:
+            return self._normalized(table, cache)
+        key = ("generic", tuple(names))
+        if key not in cache:
+            by_name = {c.name: c for c in self.ccs}
+            missing = [n for n in names if n not in by_name]
+            if missing:
+                raise KeyError(f"generic model inputs not in ColumnConfig: {missing[:5]}")
+            X, _, _ = normalize_table(self.mc, self.ccs, table, columns=[by_name[n] for n in names])
+            cache[key] = X
+        return cache[key]
 
     def score(self, table, scale: float | None = None):
         """-> OrderedDict(mean, max, min, median, model0.. [N]) scaled by ``scoreScale``;

@@ -127,14 +127,25 @@ def _write_joined(out_dir, header, raw, score_cols):
 
 
 def combo_run(root: str):
+    from ..config import environment
+    from ..runtime.executor import ExecutorManager, cli_task
     ms = ModelSet(root)
     cfg = _load_cfg(ms)
-    subs = []
+    # sub models train with retries (ExecutorManager); shifu.combo.parallel > 1 runs them side by
+    # side as child processes (ProcessManager), each with its own log under the sub model set
+    parallel = int(environment.get("shifu.combo.parallel", 1) or 1)
+    retries = int(environment.get("shifu.combo.retries", 1) or 0)
+    dirs = [_sub_dir(ms, sub["modelName"]) for sub in cfg["subTrains"]]
     for sub in cfg["subTrains"]:
-        d = _sub_dir(ms, sub["modelName"])
         _log.info("combo: training sub model %s (%s)", sub["modelName"], sub["algorithm"])
-        _pipeline(d)
-        subs.append((sub["modelName"], ModelSet(d)))
+    if parallel > 1:
+        steps = ["init", "stats", "norm", "varsel", "train"]
+        tasks = [cli_task([s for s in steps if not (s == "init" and os.path.exists(os.path.join(d, "ColumnConfig.json")))],
+                          d, os.path.join(d, "combo_sub.log")) for d in dirs]
+    else:
+        tasks = [(lambda d=d: _pipeline(d)) for d in dirs]
+    ExecutorManager(parallel, retries).run(tasks, [sub["modelName"] for sub in cfg["subTrains"]])
+    subs = [(sub["modelName"], ModelSet(d)) for sub, d in zip(cfg["subTrains"], dirs)]
     scores, header, raw = {}, None, None
     for name, sms in subs:
         header, raw, s = _score_rows(sms, sms.mc.dataSet)

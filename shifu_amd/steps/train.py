@@ -263,6 +263,10 @@ class TrainStep:
         ms, mc = self.ms, self.mc
         ms.setup("TRAIN")
         alg = mc.algorithm
+        if alg in ("GENERIC", "TENSORFLOW"):
+            raise ValueError(f"algorithm {alg}: generic models are trained outside shifu; put their "
+                             "GenericModelConfig JSON (+ artifacts) under models/ and run eval/export "
+                             "(scoring/generic.py)")
         if alg not in ("NN", "LR", "GBT", "RF", "WDL"):
             raise ValueError(f"unsupported algorithm {alg}")
         is_tree = alg in TREE_ALGS
