@@ -13,6 +13,8 @@ weights).  ``value`` = total rows processed per second over all ranks.
     python bench.py --gpus 1 --steps 5 --warmup 2
     torchrun --nproc-per-node 8 bench.py --gpus 8 ...
     python bench.py --model gbdt    # GBDT rounds/sec (500 trees depth 7, 256 bins) config
+    python bench.py --model varsel  # 10k-feature MLP + SE varselect config
+    python bench.py --model lr      # LR 100k-row CSV local (CPU plumbing) config
 """
 from __future__ import annotations
 
@@ -24,6 +26,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 # Derived reference throughput (CHANGES.txt:268): 20M rows x 200 epochs in
@@ -99,12 +102,107 @@ def bench_gbdt(a, dev, info):
     return bench_rounds(a, dev, info)
 
 
+def bench_varsel(a, dev, info):
+    """BASELINE config 5: 10k-feature MLP + sensitivity-analysis variable selection.  Each rank
+    holds ``--rows`` rows x 10000 features (bf16, HBM-resident: 2M rows = 40 GB), trains the
+    SE model (10000-500-1, sigmoid, RPROP full-batch epochs; ``--steps`` timed epochs) and then
+    runs one SE pass over every row (HIP kernel K14: cached first layer + rank-1 correction per
+    input), all-reducing the per-input sums over ranks.  value = rows through the job per second
+    (epochs x rows + one SE pass x rows, all ranks)."""
+    from shifu_amd.algos.varsel import sensitivity
+    from shifu_amd.formats.nn_format import NNNetwork
+    from shifu_amd.models.nn import MLPSpec, MLPTrainer, TrainData
+    from shifu_amd.parallel import dist
+    n_in = a.cols
+    spec = MLPSpec(n_in=n_in, hidden=[500], acts=["sigmoid"], n_out=1)
+    tr = MLPTrainer(spec, device=dev, propagation="R", learning_rate=0.1, seed=7, chunk_rows=a.chunk_rows)
+    x, y = make_synthetic(a.rows, n_in, spec.layer_kpad[0], dev, 4321 + info.rank)
+    data = TrainData(x, y, None, a.rows)
+    n_global = float(a.rows * info.world_size)
+    for _ in range(a.warmup):
+        tr.step(data, num_train_global=n_global)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+    dist.barrier(); sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.step(data, num_train_global=n_global)
+    sync(); dist.barrier()
+    t_train = time.perf_counter() - t0
+    ws = tr.params.views()
+    net = NNNetwork([n_in, 500, 1], ["sigmoid", "sigmoid"],
+                    [ws[l][:, : spec.layer_in[l] + 1].detach().double().cpu().numpy() for l in range(len(ws))])
+    dist.barrier(); sync()
+    t1 = time.perf_counter()
+    mean, rms, _ = sensitivity(net, x[:, :n_in], device=dev, row_chunk=1 << 12)
+    stats = torch.tensor(np.concatenate([mean, rms ** 2]) * a.rows, dtype=torch.float64, device=dev)
+    dist.all_reduce_(stats)
+    sync(); dist.barrier()
+    t_se = time.perf_counter() - t1
+    t = torch.tensor([t_train, t_se], dtype=torch.float64, device=dev)
+    dist.all_reduce_(t, "max")
+    t_train, t_se = float(t[0]), float(t[1])
+    rows_total = a.rows * info.world_size
+    value = rows_total * (a.steps + 1) / (t_train + t_se)
+    rms_all = np.sqrt(stats[n_in:].cpu().numpy() / rows_total)
+    return {
+        "metric": METRIC + " [config: 10k-feature MLP + SE varselect]",
+        "value": value, "unit": "rows/s", "n_gpus": info.world_size, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": (t_train + t_se) / (a.steps + 1) * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) features, hidden linear rule), random-init weights",
+        "config": {"model": f"MLP {n_in}-500-1 + SE sensitivity varselect", "global_batch": rows_total,
+                   "seq_len": None, "n_cols": n_in, "rows_per_gpu": a.rows, "parallelism": f"dp{info.world_size}"},
+        "train_ms_per_epoch": t_train / max(1, a.steps) * 1e3, "se_pass_ms": t_se * 1e3,
+        "se_input_pairs_per_s": rows_total * n_in / t_se, "top5_inputs_by_rms": np.argsort(-rms_all)[:5].tolist(),
+    }
+
+
+def bench_lr(a, dev, info):
+    """BASELINE config 1: logistic regression on a 100k-row CSV, local mode, CPU only (the
+    plumbing path): shifu init -> stats -> norm -> train on a generated model set.  One step =
+    one full pipeline run; value = pipeline runs per minute is not meaningful, so the line reports
+    the pipeline wall time (lower is better) and the LR training rows/s."""
+    import tempfile
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps import api
+    from shifu_amd.utils.synthetic import make_model_set
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    times, train_t = [], []
+    with tempfile.TemporaryDirectory(prefix="shifu_lr_bench_") as tmp:
+        root = make_model_set(tmp, "lrbench", "LR", n_rows=a.rows, n_num=20, n_cat=3)
+        mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+        mc.train["numTrainEpochs"] = 100
+        mc.train["baggingNum"] = 1
+        mc.save()
+        for i in range(a.warmup + a.steps):
+            t0 = time.perf_counter()
+            for cls in (api.InitStep, api.StatsStep, api.NormStep):
+                cls(root).process()
+            t1 = time.perf_counter()
+            api.TrainStep(root).process()
+            t2 = time.perf_counter()
+            if i >= a.warmup:
+                times.append(t2 - t0)
+                train_t.append(t2 - t1)
+    ms = sum(times) / len(times) * 1e3
+    return {
+        "metric": "LR local pipeline wall time (init+stats+norm+train, 100 epochs) [config: LR 100k-row CSV, CPU]",
+        "value": ms / 1e3, "unit": "s", "n_gpus": 0, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
+        "higher_is_better": False, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic CSV (20 numeric + 3 categorical columns)",
+        "config": {"model": "LR", "global_batch": a.rows, "seq_len": None, "parallelism": "local"},
+        "train_rows_epochs_per_s": a.rows * 100 / (sum(train_t) / len(train_t)),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr"])
     ap.add_argument("--rows", type=int, default=None, help="rows per GPU (default 100M on GPU)")
     ap.add_argument("--cols", type=int, default=1000)
     ap.add_argument("--chunk-rows", type=int, default=1 << 20)
@@ -115,11 +213,17 @@ def main():
     info = dist.init_from_env()
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+    if a.model == "varsel" and a.cols == 1000:
+        a.cols = 10_000
     if a.rows is None:
-        a.rows = 100_000_000 if gpu else 20_000
+        a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000}.get(a.model, 100_000_000 if gpu else 20_000)
     if a.model == "gbdt":
         res = bench_gbdt(a, dev, info)
         out = res
+    elif a.model == "varsel":
+        out = bench_varsel(a, dev, info)
+    elif a.model == "lr":
+        out = bench_lr(a, dev, info)
     else:
         dt, errs, flops_row = bench_mlp(a, dev, info)
         dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)

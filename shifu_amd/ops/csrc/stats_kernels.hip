@@ -330,8 +330,9 @@ __global__ void __launch_bounds__(256) lr_grad_kernel(LrArgs a) {
 //   d = base[r] - act_o(b2 + sum_j W2[j] * act1(S[r][j] - x[r][f] * W1t[f][j]))
 //   accumulate sum |d|, sum d^2 per input
 // ---------------------------------------------------------------------------------------------
-constexpr int SFT = 32;    // inputs per block
-constexpr int SRT = 8;     // rows per step
+constexpr int SFT = 32;    // inputs per block (8 per thread, 4 thread groups)
+constexpr int SRT = 64;    // rows per tile (one per thread group member)
+constexpr int SHC = 64;    // hidden units staged per chunk
 
 struct SensArgs {
   const float* S; long lds; const float* X; long ldx; const float* W1t; const float* W2; float b2;
@@ -339,49 +340,84 @@ struct SensArgs {
   long rows_per_chunk; double* acc;   // [F][2]
 };
 
+// Register-blocked: thread = 1 row x 8 inputs; per hidden unit j it reads S[r][j] (4 j per
+// ds_read_b128 from the row's LDS strip) and W1[j][8 inputs] (2 x ds_read_b128, same address for
+// the 64 row-threads of a group -> broadcast), then 8 x (fma, act, fma).  The activation's
+// v_exp/v_rcp (quarter rate) bound the loop instead of scalar LDS reads (the previous 1x1
+// version issued two ds_read_b32 per element).
 template <int ACT1>
 __global__ void __launch_bounds__(256) sensitivity_kernel(SensArgs a) {
-  extern __shared__ float smem[];
-  const int H = a.H, HP = H + 1;
-  float* w1 = smem;                      // [SFT][HP]
-  float* w2 = w1 + SFT * HP;             // [H]
-  float* st = w2 + H;                    // [SRT][HP]
-  __shared__ double ra[SRT][SFT], rs[SRT][SFT];
-  const int tid = threadIdx.x, fl = tid % SFT, rl = tid / SFT;
-  const int f0 = blockIdx.y * SFT;
-  for (int i = tid; i < SFT * H; i += 256) {
-    const int ff = i / H, j = i % H;
-    w1[ff * HP + j] = (f0 + ff < a.F) ? a.W1t[(long)(f0 + ff) * H + j] : 0.f;
-  }
-  for (int j = tid; j < H; j += 256) w2[j] = a.W2[j];
+  __shared__ __attribute__((aligned(16))) float st[SRT][SHC + 4];   // S strip per row
+  __shared__ __attribute__((aligned(16))) float w1[SHC][SFT];       // W1 chunk, inputs contiguous
+  __shared__ float w2s[SHC];
+  __shared__ double red[4][2][SFT];
+  const int tid = threadIdx.x, fg = tid & 3, rr = tid >> 2;
+  const int f0 = blockIdx.y * SFT, fb = f0 + fg * 8;
   const long r0 = (long)blockIdx.x * a.rows_per_chunk, r1 = min(a.n, r0 + a.rows_per_chunk);
-  double sa = 0.0, sq = 0.0;
-  const int f = f0 + fl;
+  double sa[8], sq[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sa[k] = 0.0; sq[k] = 0.0; }
   for (long rb = r0; rb < r1; rb += SRT) {
-    __syncthreads();
-    for (int i = tid; i < SRT * H; i += 256) {
-      const int rr = i / H, j = i % H;
-      st[rr * HP + j] = (rb + rr < r1) ? a.S[(rb + rr) * a.lds + j] : 0.f;
+    const long r = rb + rr;
+    const bool rok = r < r1;
+    float xv[8], acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      xv[k] = (rok && fb + k < a.F) ? a.X[r * a.ldx + fb + k] : 0.f;
+      acc[k] = 0.f;
     }
-    __syncthreads();
-    const long r = rb + rl;
-    if (r < r1 && f < a.F) {
-      const float xf = a.X[r * a.ldx + f];
-      const float* sr = st + rl * HP;
-      const float* wr = w1 + fl * HP;
-      float acc = a.b2;
-      for (int j = 0; j < H; ++j) acc += w2[j] * act_fwd(ACT1, sr[j] - xf * wr[j]);
-      const float d = a.base[r] - act_fwd(a.act_o, acc);
-      sa += fabs((double)d);
-      sq += (double)d * d;
+    for (int h0 = 0; h0 < a.H; h0 += SHC) {
+      const int hc = min(SHC, a.H - h0);
+      __syncthreads();
+      for (int i = tid; i < SRT * SHC; i += 256) {
+        const int row = i / SHC, j = i % SHC;
+        st[row][j] = (rb + row < r1 && j < hc) ? a.S[(rb + row) * a.lds + h0 + j] : 0.f;
+      }
+      for (int i = tid; i < SFT * SHC; i += 256) {
+        const int ff = i / SHC, j = i % SHC;
+        w1[j][ff] = (f0 + ff < a.F && j < hc) ? a.W1t[(long)(f0 + ff) * a.H + h0 + j] : 0.f;
+      }
+      for (int j = tid; j < SHC; j += 256) w2s[j] = j < hc ? a.W2[h0 + j] : 0.f;
+      __syncthreads();
+      for (int j = 0; j < hc; j += 4) {
+        const float4 s4 = *(const float4*)&st[rr][j];
+        const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float4 wa = *(const float4*)&w1[j + jj][fg * 8];
+          const float4 wb = *(const float4*)&w1[j + jj][fg * 8 + 4];
+          const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+          const float w2j = w2s[j + jj];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += w2j * act_fwd(ACT1, sv[jj] - xv[k] * wv[k]);
+        }
+      }
+    }
+    if (rok) {
+      const float bse = a.base[r];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const double d = (double)(bse - act_fwd(a.act_o, acc[k] + a.b2));
+        sa[k] += fabs(d);
+        sq[k] += d * d;
+      }
     }
   }
-  ra[rl][fl] = sa;
-  rs[rl][fl] = sq;
+  // reduce over the 64 rows of each input group: lanes l, l^4, l^8, ... share fg
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) { sa[k] += __shfl_xor(sa[k], o, 64); sq[k] += __shfl_xor(sq[k], o, 64); }
+  }
+  const int wv_ = tid >> 6, lane = tid & 63;
+  if (lane < 4) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { red[wv_][0][lane * 8 + k] = sa[k]; red[wv_][1][lane * 8 + k] = sq[k]; }
+  }
   __syncthreads();
   if (tid < SFT && f0 + tid < a.F) {
-    double x = 0.0, y = 0.0;
-    for (int k = 0; k < SRT; ++k) { x += ra[k][tid]; y += rs[k][tid]; }
+    const double x = red[0][0][tid] + red[1][0][tid] + red[2][0][tid] + red[3][0][tid];
+    const double y = red[0][1][tid] + red[1][1][tid] + red[2][1][tid] + red[3][1][tid];
     atomicAdd(&a.acc[(long)(f0 + tid) * 2], x);
     atomicAdd(&a.acc[(long)(f0 + tid) * 2 + 1], y);
   }
@@ -455,9 +491,11 @@ SHIFU_API int shifu_sensitivity(const float* S, long lds, const float* X, long l
                                 float b2, const float* base, long n, int F, int H, int act1, int act_o, int nchunks,
                                 double* acc, hipStream_t stream) {
   if (H <= 0 || H > 1024 || n <= 0 || nchunks <= 0) return -1;
-  SensArgs a{S, lds, X, ldx, W1t, W2, b2, base, n, F, H, act_o, (n + nchunks - 1) / nchunks, acc};
-  const size_t sm = (size_t)(SFT * (H + 1) + H + SRT * (H + 1)) * sizeof(float);
-  if (sm > 150 * 1024) return -3;
+  long rpc = (n + nchunks - 1) / nchunks;
+  rpc = (rpc + SRT - 1) / SRT * SRT;
+  nchunks = (int)((n + rpc - 1) / rpc);
+  SensArgs a{S, lds, X, ldx, W1t, W2, b2, base, n, F, H, act_o, rpc, acc};
+  const size_t sm = 0;
   dim3 g(nchunks, (F + SFT - 1) / SFT);
   switch (act1) {
     case ACT_SIGMOID: hipLaunchKernelGGL(sensitivity_kernel<ACT_SIGMOID>, g, dim3(256), sm, stream, a); break;
