@@ -35,6 +35,8 @@ HIP_SIGNATURES = {
     "shifu_wgrad_tn": "plplpl" "iiiis",
     "shifu_gemm_set_stages": "i",
     "shifu_gemm_set_big": "i",
+    "shifu_gemm_set_tune": "ii",
+    "shifu_mlp_set_out_waves": "i",
     "shifu_mlp_output": "plplppl" "pplpppl" "iiiiiii" "ff" "s",
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
     "shifu_cast_bf16": "plpliis",

@@ -14,12 +14,17 @@ static constexpr int WAVE = 64;   // CDNA wavefront: 64 lanes, never 32
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
-// round-to-nearest-even f32 -> bf16 (inputs are finite activations / deltas)
+// round-to-nearest-even f32 -> bf16 through the gfx950 hardware convert (v_cvt_pk_bf16_f32,
+// emitted by hipcc for a plain cast; keeps NaN a NaN).  pack_bf16x2 converts two values with one
+// instruction -- ~10x fewer VALU cycles per element than integer rounding on the f32 bits, which
+// matters in the GEMM epilogues (64K conversions per 256x256 tile).
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)(u >> 16);   // inf / nan passthrough
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

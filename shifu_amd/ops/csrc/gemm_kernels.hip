@@ -18,6 +18,7 @@
 //   * the output layer (n_out <= 8) + loss + output delta + last-hidden dgrad + output
 //     wgrad are one row kernel (memory-bound, one wave per row strip).
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
@@ -53,7 +54,7 @@ struct GemmArgs {
 // STAGES = LDS buffers.  1: single 32 KiB buffer + register prefetch (two barriers per k-step,
 // up to 5 blocks = 5 waves/SIMD per CU -> the HBM/L2 latency of the next tile is hidden by the
 // other resident blocks); 2: classic LDS double buffer (64 KiB, 2 blocks per CU).
-template <int EPI, int ACT, int STAGES>
+template <int EPI, int ACT, int STAGES, bool HPF = false>
 __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntn = (p.N + BN - 1) / BN;
@@ -88,6 +89,17 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // dgrad (HPF): the epilogue's H row segments are loaded before the k-loop, so their HBM
+  // latency overlaps the (short, K <= 256) main loop instead of trailing it.
+  uint4 hpre[HPF ? 8 : 1];
+  if constexpr (HPF) {
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int m = m0 + pass * 16 + (tid >> 4), n = n0 + (tid & 15) * 8;
+      hpre[pass] = (m < p.M && n + 8 <= p.N) ? *(const uint4*)(p.H + (size_t)m * p.ldh + n) : make_uint4(0, 0, 0, 0);
+    }
+  }
 
   const int nk = p.K / BK;
   gload(0);
@@ -143,8 +155,8 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
           }
         }
         uint2 w;
-        w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-        w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        w.x = pack_bf16x2(o[0], o[1]);
+        w.y = pack_bf16x2(o[2], o[3]);
         const int c = nl >> 3, half = (nl >> 2) & 1;
         *(uint2*)(Cs + ml * 256 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
       }
@@ -158,7 +170,9 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       if (m >= p.M || n >= p.N) continue;
       uint4 v = *(const uint4*)(Cs + ml * 256 + ((c ^ (ml & 15)) << 4));
       if constexpr (EPI == EPI_DACT) {
-        const uint4 h = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+        uint4 h;
+        if constexpr (HPF) h = (n + 8 <= p.N) ? hpre[pass] : *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+        else h = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
         const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
         uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -168,7 +182,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
           const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
           a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
           a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
-          vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+          vv[q] = pack_bf16x2(a0, a1);
         }
         v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
       }
@@ -199,8 +213,8 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
           else { o[r] = (n == p.n_valid && p.bias_col) ? 1.f : 0.f; d[r] = 0.f; }
         }
         uint2 w2;
-        w2.x = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
-        w2.y = (uint32_t)f2bf(d[2]) | ((uint32_t)f2bf(d[3]) << 16);
+        w2.x = pack_bf16x2(d[0], d[1]);
+        w2.y = pack_bf16x2(d[2], d[3]);
         *(uint2*)(p.C2 + (size_t)m * p.ldc2 + nb) = w2;
       } else {   // EPI_DACT with a stored derivative (activations not derivable from the output)
         const uint2 h = *(const uint2*)(p.Hd + (size_t)m * p.ldhd + nb);
@@ -209,8 +223,8 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
         for (int r = 0; r < 4; ++r) o[r] = (nb + r < p.n_valid) ? acc[i][j][r] * dv[r] : 0.f;
       }
       uint2 w;
-      w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-      w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+      w.x = pack_bf16x2(o[0], o[1]);
+      w.y = pack_bf16x2(o[2], o[3]);
       *(uint2*)(p.C + (size_t)m * p.ldc + nb) = w;
     }
   }
@@ -310,8 +324,8 @@ __global__ __launch_bounds__(GB_T, 1) void gemm_nt_big_kernel(GemmArgs p) {
             }
           }
           uint2 w;
-          w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-          w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+          w.x = pack_bf16x2(o[0], o[1]);
+          w.y = pack_bf16x2(o[2], o[3]);
           const int c = nl >> 3, half = (nl >> 2) & 1;
           *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
         }
@@ -336,7 +350,7 @@ __global__ __launch_bounds__(GB_T, 1) void gemm_nt_big_kernel(GemmArgs p) {
             const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
             a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
             a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
-            vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+            vv[q] = pack_bf16x2(a0, a1);
           }
           v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
         }
@@ -357,28 +371,34 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[4][
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   char* Cs = smem;
+  auto tile_write = [&](auto FULL) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+    for (int i = 0; i < 4; ++i) {
+      const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ml = wr * 128 + j * 16 + (lane & 15);
-      float o[4];
+      for (int j = 0; j < 8; ++j) {
+        const int ml = wr * 128 + j * 16 + (lane & 15);
+        float o[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = acc[i][j][r];
-        const int n = n0 + nl + r;
-        if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
-        else if constexpr (EPI == EPI_STORE) o[r] = n < p.NB ? z : 0.f;
-        else o[r] = z;
+        for (int r = 0; r < 4; ++r) {
+          const float z = acc[i][j][r];
+          const int n = n0 + nl + r;
+          if constexpr (decltype(FULL)::value) o[r] = EPI == EPI_ACT ? act_fwd(ACT, z) : z;
+          else if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
+          else if constexpr (EPI == EPI_STORE) o[r] = n < p.NB ? z : 0.f;
+          else o[r] = z;
+        }
+        uint2 w;
+        w.x = pack_bf16x2(o[0], o[1]);
+        w.y = pack_bf16x2(o[2], o[3]);
+        const int c = nl >> 3, half = (nl >> 2) & 1;
+        *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
       }
-      uint2 w;
-      w.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-      w.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-      const int c = nl >> 3, half = (nl >> 2) & 1;
-      *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
     }
-  }
+  };
+  const bool full = EPI == EPI_DACT || n0 + 256 <= (EPI == EPI_ACT ? p.n_valid : p.NB);
+  if (full) tile_write(std::integral_constant<bool, true>{});
+  else tile_write(std::integral_constant<bool, false>{});
   __syncthreads();
   const int c = tid & 31;
 #pragma unroll 4
@@ -398,7 +418,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[4][
         const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
         a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
         a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
-        vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+        vv[q] = pack_bf16x2(a0, a1);
       }
       v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     }
@@ -626,6 +646,194 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_kernel(GemmArgs p) {
 #undef G8_MMA
 #undef G8_BAR
   epilogue_256<EPI, ACT>(p, acc, m0, n0, smem);
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent 8-phase NT GEMM: the gemm_nt_8ph_kernel schedule run over a stream of output
+// tiles by one block per CU.  With K = 1024 a tile is only 16 k-tiles, and the standalone
+// kernel pays the DMA pipeline fill and a 128 KiB LDS-staged epilogue per tile with the MFMAs
+// idle.  Here the k-tile stream continues across tiles: the last iteration of tile t issues
+// the DMAs of tile t+1's k-tiles 0/1 (instead of dummy re-reads), and tile t's epilogue runs
+// from a separate 32 KiB LDS region (4 chunks of 64 rows) while those DMAs are in flight.
+// The epilogue's barriers are raw s_barrier (a __syncthreads fence would drain vmcnt to 0).
+// Tiles: block L (XCD-remapped) takes L, L + G, L + 2G, ...; tiles L and L+1 (the two N-tiles
+// of one 256-row M-tile) run concurrently on one XCD, so A rows are fetched from HBM once.
+// Requires K % 128 == 0 (an even number of k-tiles keeps the buffer parity across tiles).
+// ---------------------------------------------------------------------------------------
+constexpr int G8P_EPI = 2 * G8_BUF;              // epilogue region offset (after the 128 KiB ring)
+constexpr int G8P_LDS = 2 * G8_BUF + 32768;      // 160 KiB
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_persist_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = (p.N + 255) / 256;
+  const int ntiles = ((p.M + 255) / 256) * ntn;
+  const int G = gridDim.x;
+  const int L = xcd_remap(blockIdx.x, G);
+  if (L >= ntiles) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nk = p.K / 64;
+
+  // Per-thread DMA geometry (LDS byte P = i*8192 + wid*1024 + lane*16 of a half-tile holds
+  // logical 16-B chunk lc_i of row row_i); source addresses are formed per DMA from the
+  // (wave-uniform) tile origin so no per-tile offset tables occupy VGPRs.
+  int row_i[2], lc_i[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int P = i * 8192 + wid * 1024 + lane * 16;
+    row_i[i] = P >> 7;
+    lc_i[i] = ((P >> 4) & 7) ^ ((row_i[i] >> 1) & 7);
+  }
+  int t = L;
+  bool has_next = t + G < ntiles;
+  // k-tile kt of the stream: kt < nk -> this tile; kt >= nk -> next tile's kt - nk (or a dummy
+  // re-read of k-tile nk-1 when there is no next tile, which keeps the counted waits exact)
+  auto dma = [&](int h, int kt) {
+    char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
+    int tt = t, k = kt;
+    if (kt >= nk) {
+      if (has_next) { tt = t + G; k = kt - nk; } else k = nk - 1;
+    }
+    const bool isA = h < 2;
+    const int base = (isA ? (tt / ntn) * 256 : (tt % ntn) * 256) + (h & 1) * 128;
+    const int lim = (isA ? p.M : p.NB) - 1;
+    const long ld = isA ? p.lda : p.ldb;
+    const bf16_t* src = (isA ? p.A : p.B) + k * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src + (long)min(base + row_i[i], lim) * ld + lc_i[i] * 8),
+                                       (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
+  };
+
+  f32x4 acc[4][8];
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  const int lr = lane & 15, lq = lane >> 4;
+  auto readA = [&](int buf, int mh) {
+    const char* base = smem + buf * G8_BUF + wr * G8_HALF;
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) af[t4][c] = *(const bf16x8*)(base + swz_nt(mh * 64 + t4 * 16 + lr, c * 4 + lq));
+  };
+  auto readB = [&](int buf, int nh, bf16x8 (&bq)[2][2]) {
+    const char* base = smem + buf * G8_BUF + (2 + (wc >> 1)) * G8_HALF;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        bq[t2][c] = *(const bf16x8*)(base + swz_nt((wc & 1) * 64 + nh * 32 + t2 * 16 + lr, c * 4 + lq));
+  };
+  auto mma = [&](int mh, int nh, bf16x8 (&bq)[2][2]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4)
+          acc[nh * 2 + s_][mh * 4 + t4] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s_][c], af[t4][c], acc[nh * 2 + s_][mh * 4 + t4], 0, 0, 0);
+  };
+#define G8_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
+                      __builtin_amdgcn_sched_barrier(0); } while (0)
+#define G8_MMA(mh, nh, bq) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    __builtin_amdgcn_s_setprio(1); mma(mh, nh, bq); __builtin_amdgcn_s_setprio(0); } while (0)
+
+  dma(2, 0); dma(3, 0); dma(0, 0); dma(1, 0);
+  dma(2, 1); dma(3, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  G8_BAR();
+  if (wr == 1) G8_BAR();                      // stagger the two wave rows by one barrier
+
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ke = 0; ke < nk; ke += 2) {
+      const int ko = ke + 1;
+      dma(0, ko); readB(0, 0, bf0); readA(0, 0);                                   // P1
+      G8_BAR(); G8_MMA(0, 0, bf0); G8_BAR();
+      dma(1, ko); readB(0, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P2
+      G8_BAR(); G8_MMA(0, 1, bf1); G8_BAR();
+      dma(2, ke + 2); readA(0, 1);                                                 // P3
+      G8_BAR(); G8_MMA(1, 1, bf1); G8_BAR();
+      dma(3, ke + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P4
+      G8_BAR(); G8_MMA(1, 0, bf0); G8_BAR();
+      dma(0, ke + 2); readB(1, 0, bf0); readA(1, 0);                               // P5
+      G8_BAR(); G8_MMA(0, 0, bf0); G8_BAR();
+      dma(1, ke + 2); readB(1, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P6
+      G8_BAR(); G8_MMA(0, 1, bf1); G8_BAR();
+      dma(2, ko + 2); readA(1, 1);                                                 // P7
+      G8_BAR(); G8_MMA(1, 1, bf1); G8_BAR();
+      dma(3, ko + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P8
+      G8_BAR(); G8_MMA(1, 0, bf0); G8_BAR();
+    }
+    if (wr == 0) G8_BAR();                    // re-align the rows
+    const bool last = !has_next;
+    if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the dummy prefetches
+
+    // epilogue of tile t from the 32 KiB region: 4 chunks of 64 rows x 512 B (16-B chunk ^ row)
+    const int m0 = (t / ntn) * 256, n0 = (t % ntn) * 256;
+    char* Cs = smem + G8P_EPI;
+    // FULL: every column of the tile is a valid unit (no bias column / padding in it): the
+    // per-element range selects are skipped (wave-uniform branch, two instantiations)
+    auto chunk_write = [&](int q, auto FULL) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = (q & 1) * 4 + jj;
+          const int ml = jj * 16 + (lane & 15);
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z = acc[i][j][r];
+            const int n = n0 + nl + r;
+            if constexpr (decltype(FULL)::value) o[r] = EPI == EPI_ACT ? act_fwd(ACT, z) : z;
+            else if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
+            else o[r] = n < p.NB ? z : 0.f;
+          }
+          uint2 w;
+          w.x = pack_bf16x2(o[0], o[1]);
+          w.y = pack_bf16x2(o[2], o[3]);
+          const int c = nl >> 3, half = (nl >> 2) & 1;
+          *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
+        }
+      }
+    };
+    const bool full = n0 + 256 <= (EPI == EPI_ACT ? p.n_valid : p.NB);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (wr == (q >> 1)) {
+        if (full) chunk_write(q, std::integral_constant<bool, true>{});
+        else chunk_write(q, std::integral_constant<bool, false>{});
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      G8_BAR();
+      const int c = tid & 31;
+#pragma unroll
+      for (int pass = 0; pass < 4; ++pass) {
+        const int ml = pass * 16 + (tid >> 5);
+        const int m = m0 + q * 64 + ml, n = n0 + c * 8;
+        const uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
+        if (m < p.M && n < p.N) {
+          if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
+          else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      G8_BAR();
+    }
+    if (last) break;
+    // advance: the next tile's k-tiles 0 (complete) / 1 (B halves in flight) are staged
+    t += G;
+    has_next = t + G < ntiles;
+    if (wr == 1) G8_BAR();                    // re-stagger
+  }
+#undef G8_MMA
+#undef G8_BAR
 }
 
 // ---------------------------------------------------------------------------------------
@@ -916,8 +1124,23 @@ __global__ __launch_bounds__(G8_T, 1) void wgrad_8ph_kernel(Wgrad8Args p) {
 static int g_stages = 1;     // LDS stages of the MLP GEMMs (A/B switch for tuning; 1 = default)
 static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N >= 512, K >= 512; else 128x128),
                              // 1 = 256x256 register-staged, 2 = 256x256 DMA ring, 3 = 8-phase, 4 = 128x128 only
+static int g_persist = 0;    // auto path: 1 = persistent 8-phase kernel for the forward GEMMs
+static int g_dgrad_pf = 0;   // dgrad H prefetch (gemm_nt_kernel HPF); 0 = off (A/B switch)
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
-SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b >= 0 && b <= 4) ? b : 0; return 0; }
+SHIFU_API int shifu_gemm_set_tune(int key, int val) {
+  if (key == 0) { g_dgrad_pf = val; return 0; }
+  if (key == 1) { g_persist = val; return 0; }
+  return -1;
+}
+SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b >= 0 && b <= 5) ? b : 0; return 0; }
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
 
 SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc,
                             void* C2, long ldc2, const void* H, long ldh, const void* Hd, long ldhd,
@@ -947,6 +1170,21 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
     else GEMM8_L(EPI_STORE, 2);
 #undef GEMM8_ACTS
 #undef GEMM8_L
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
+  if ((g_big == 5 || (g_big == 0 && g_persist && auto8)) && M >= 65536 && N >= 256 && K % 128 == 0 &&
+      (epi == EPI_STORE || (epi == EPI_ACT && dfo_act && act != 6))) {   // ptanh: register spill, 8-phase
+    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    const int gridp = tiles < num_cus() ? tiles : num_cus();
+#define GEMMQ_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_persist_kernel<E, A>), dim3(gridp), dim3(G8_T), G8P_LDS, stream, p)
+#define GEMMQ_ACTS(E) switch (act) { case 0: GEMMQ_L(E, 0); break; case 1: GEMMQ_L(E, 1); break; \
+    case 2: GEMMQ_L(E, 2); break; case 3: GEMMQ_L(E, 3); break; case 4: GEMMQ_L(E, 4); break; \
+    case 6: GEMMQ_L(E, 6); break; default: GEMMQ_L(E, 7); break; }
+    if (epi == EPI_ACT) { GEMMQ_ACTS(EPI_ACT) }
+    else GEMMQ_L(EPI_STORE, 2);
+#undef GEMMQ_ACTS
+#undef GEMMQ_L
     CHECK_HIP(hipGetLastError());
     return 0;
   }
@@ -982,6 +1220,8 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   }
 #define GEMM_L(E, A) do { if (g_stages == 2) \
     hipLaunchKernelGGL((gemm_nt_kernel<E, A, 2>), dim3(grid), dim3(NTHR), lds, stream, p); \
+  else if (E == EPI_DACT && g_dgrad_pf && act_deriv_from_output(A)) \
+    hipLaunchKernelGGL((gemm_nt_kernel<E, A, 1, E == EPI_DACT && act_deriv_from_output(A)>), dim3(grid), dim3(NTHR), lds, stream, p); \
   else hipLaunchKernelGGL((gemm_nt_kernel<E, A, 1>), dim3(grid), dim3(NTHR), lds, stream, p); } while (0)
 #define GEMM_ACTS(E) switch (act) { case 0: GEMM_L(E, 0); break; case 1: GEMM_L(E, 1); break; \
     case 2: GEMM_L(E, 2); break; case 3: GEMM_L(E, 3); break; case 4: GEMM_L(E, 4); break; \

@@ -25,10 +25,10 @@ __device__ __forceinline__ void unpack8(const uint4 v, float* f) {
 }
 __device__ __forceinline__ uint4 pack8(const float* f) {
   uint4 v;
-  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
-  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
-  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  v.x = pack_bf16x2(f[0], f[1]);
+  v.y = pack_bf16x2(f[2], f[3]);
+  v.z = pack_bf16x2(f[4], f[5]);
+  v.w = pack_bf16x2(f[6], f[7]);
   return v;
 }
 
@@ -243,6 +243,9 @@ __global__ void transpose_cast_kernel(const float* W, long ldw, bf16_t* O, int R
 // =======================================================================================
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
 
+static long g_out_waves = 8192;   // output-kernel grid cap in waves (tuning knob)
+SHIFU_API int shifu_mlp_set_out_waves(int w) { g_out_waves = w >= 64 ? w : 4096; return 0; }
+
 SHIFU_API int shifu_mlp_output(const void* H, long ldh, const void* Hd, long ldhd, const float* W, const float* Y,
                                long ldy, const float* S, void* D, long ldd, float* GW, double* err, float* P,
                                long ldp, int M, int KH, int kh_valid, int n_out, int out_act, int hid_act, int loss,
@@ -254,7 +257,7 @@ SHIFU_API int shifu_mlp_output(const void* H, long ldh, const void* Hd, long ldh
   const int lpr = KH / 8;
   const long rows_per_wave_iter = (64 / lpr) * 4;
   long waves = (M + rows_per_wave_iter - 1) / rows_per_wave_iter;
-  if (waves > 4096) waves = 4096;          // grid-stride: <= 1024 blocks x 4 waves
+  if (waves > g_out_waves) waves = g_out_waves;   // grid-stride cap (blocks x 4 waves)
   const long blocks = (waves + 3) / 4;
   // dispatch on (n_out, lanes-per-row)
 #define OUT_L(NO, L) hipLaunchKernelGGL((mlp_output_kernel<NO, L>), dim3(blocks), dim3(256), 0, stream, p)

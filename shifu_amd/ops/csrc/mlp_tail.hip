@@ -233,8 +233,8 @@ __global__ __launch_bounds__(TT, 1) void mlp_tail_kernel(TailArgs p) {
           dv[r] = (nb + r) < p.nh ? ds * (act_deriv_out(p.act_h, acc[i][j][r]) + p.flat_h) : 0.f;
         }
         uint2 w2;
-        w2.x = (uint32_t)f2bf(dv[0]) | ((uint32_t)f2bf(dv[1]) << 16);
-        w2.y = (uint32_t)f2bf(dv[2]) | ((uint32_t)f2bf(dv[3]) << 16);
+        w2.x = pack_bf16x2(dv[0], dv[1]);
+        w2.y = pack_bf16x2(dv[2], dv[3]);
         const int kt = nb >> 6, ch = (nb & 63) >> 3, half = (nb >> 2) & 1;
         *(uint2*)(smem + L_DIMG + kt * 16384 + swz(ml, ch) + half * 8) = w2;
       }
@@ -300,8 +300,8 @@ __global__ __launch_bounds__(TT, 1) void mlp_tail_kernel(TailArgs p) {
         for (int j = 0; j < 4; ++j) {
           const int ml = wr * 64 + j * 16 + lr;
           uint2 w2;
-          w2.x = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
-          w2.y = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+          w2.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+          w2.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
           const int c = nl >> 3, half = (nl >> 2) & 1;
           *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w2;
         }
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(TT, 1) void mlp_tail_kernel(TailArgs p) {
           const float d1 = act_deriv_out(p.act_p, bf2f(hv[q] >> 16)) + p.flat_p;
           a0 = (n + 2 * q < p.np_valid) ? a0 * d0 : 0.f;
           a1 = (n + 2 * q + 1 < p.np_valid) ? a1 * d1 : 0.f;
-          vv[q] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+          vv[q] = pack_bf16x2(a0, a1);
         }
         *(uint4*)(p.Dp + (size_t)m * p.lddp + n) = make_uint4(vv[0], vv[1], vv[2], vv[3]);
       }

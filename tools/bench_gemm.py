@@ -28,6 +28,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--stages", type=int, default=1)
     ap.add_argument("--big", type=int, default=1)
+    ap.add_argument("--rounds", type=int, default=0)
+    ap.add_argument("--act", default="sigmoid")
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--ab", type=lambda t: (t.split("=")[0], int(t.split("=")[1])), nargs="*",
+                    help="interleaved A/B settings, e.g. dgrad_pf=0 dgrad_pf=1 out_waves=4096 out_waves=16384")
+    ap.add_argument("--tune", type=lambda t: tuple(int(x) for x in t.split("=")), nargs="*")
+    ap.add_argument("--out-waves", type=int, default=0)
     a = ap.parse_args()
     nat.call_hip("shifu_gemm_set_stages", a.stages)
     nat.call_hip("shifu_gemm_set_big", a.big)
@@ -45,7 +52,7 @@ def main():
     G1 = torch.zeros(500, 1024, device=dev)
     G2 = torch.zeros(200, 512, device=dev)
     st = nat.stream_of(X)
-    tanh = ACT_IDS["tanh"]
+    tanh = ACT_IDS[a.act]
     res = {}
 
     def fwd1():
@@ -82,12 +89,54 @@ def main():
     def blaslt():               # hipBLASLt through torch at the same shape (library reference)
         torch.mm(X, W1p.t(), out=Cs)
 
-    for name, fn, flops in (("pure_gemm", pure, 2 * M * 512 * 1024), ("torch_mm", blaslt, 2 * M * 512 * 1024),
+    G3 = torch.zeros(1, 256, device=dev)
+    Y = torch.rand(M, 1, device=dev)
+    W3 = (torch.randn(1, 256, device=dev) * 0.05)
+    err = torch.zeros(2, device=dev, dtype=torch.float64)
+
+    def output():
+        nat.call_hip("shifu_mlp_output", H2, 256, None, 0, W3, Y, 1, None, D2, 256, G3, err, None, 0,
+                     M, 256, 200, 1, ACT_IDS["sigmoid"], tanh, 0, 0.0, 0.0, st)
+
+    for k, v in (a.tune or []):
+        nat.call_hip("shifu_gemm_set_tune", k, v)
+    if a.out_waves:
+        nat.call_hip("shifu_mlp_set_out_waves", a.out_waves)
+    # A/B rounds inside one process (interleaved): knob settings from --ab
+    for rnd in range(a.rounds):
+        for setting in (a.ab or [None]):
+            if setting is not None:
+                kind, val = setting
+                if kind == "dgrad_pf":
+                    nat.call_hip("shifu_gemm_set_tune", 0, val)
+                    ms = timeit(dgrad, a.iters)
+                    res.setdefault(f"dgrad1_pf{val}", []).append(round(ms, 4))
+                elif kind == "persist":        # auto path, persistent 8-phase on/off
+                    nat.call_hip("shifu_gemm_set_big", 0)
+                    nat.call_hip("shifu_gemm_set_tune", 1, val)
+                    for nm, f in (("pure", pure), ("fwd1", fwd1), ("fwd2", fwd2)):
+                        ms = timeit(f, a.iters)
+                        res.setdefault(f"{nm}_persist{val}", []).append(round(ms, 4))
+                    nat.call_hip("shifu_gemm_set_tune", 1, 0)
+                    nat.call_hip("shifu_gemm_set_big", a.big)
+                elif kind == "out_waves":
+                    nat.call_hip("shifu_mlp_set_out_waves", val)
+                    ms = timeit(output, a.iters)
+                    res.setdefault(f"output_w{val}", []).append(round(ms, 4))
+    todo = (("output", output, 0),
+                            ("pure_gemm", pure, 2 * M * 512 * 1024), ("torch_mm", blaslt, 2 * M * 512 * 1024),
                             ("fwd1", fwd1, 2 * M * 512 * 1024), ("fwd2", fwd2, 2 * M * 256 * 512),
                             ("dgrad1", dgrad, 2 * M * 512 * 256), ("wgrad1", wgrad1, 2 * M * 512 * 1024),
-                            ("wgrad2", wgrad2, 2 * M * 256 * 512)):
+                            ("wgrad2", wgrad2, 2 * M * 256 * 512))
+    for name, fn, flops in todo:
+        if a.only and name not in a.only:
+            continue
         ms = timeit(fn, a.iters)
         res[name] = {"ms": round(ms, 4), "tflops": round(flops / ms / 1e9, 1)}
+        if name == "dgrad1":
+            res[name]["hbm_gbs"] = round((M * 256 * 2 + 2 * M * 512 * 2) / ms / 1e6, 1)
+        if name == "output":
+            res[name]["hbm_gbs"] = round((2 * M * 256 * 2 + M * 4) / ms / 1e6, 1)
     print(json.dumps(res))
 
 
