@@ -17,15 +17,16 @@ from .utils.log import get_logger, setup_logging
 
 USAGE = """Usage: shifu <command> [options]
   new <ModelSetName> [-t NN|LR|GBT|RF|WDL] [-m <description>]   create a model set
-  init [-autotype]                                             create ColumnConfig.json
-  stats [-c] [-p] [-rebin [-n <bins>] [-ivr <ratio>]]           column stats / correlation / psi / rebin
+  init [-autotype] | init -model                               create ColumnConfig.json | fill default train params
+  cp <src ModelSet> <dst ModelSet>                             copy a model set's ModelConfig.json
+  stats [-c] [-p] [-rebin [-vars v1,v2] [-n <bins>] [-ivr <ratio>] [-bic <min count>]]
   norm|normalize|transform [-shuffle]                          normalize training data
-  varsel [-reset|-list|-autofilter|-recoverauto] [-r <n>]      variable selection
-  train [-dry] [-shuffle]                                      train models
+  varsel|varselect [-reset|-list|-autofilter|-recoverauto] [-r <n>]  variable selection
+  train [-dry] [-debug] [-shuffle]                             train models
   posttrain                                                    bin average scores / feature importance
-  eval [-new <n>|-list|-delete <n>|-run [n]|-score [n]|-norm [n]|-confmat [n]|-perf [n]]
-  export -t pmml|columnstats|woemapping|bagging|baggingpmml|corr|woe [-c]
-  combo -new <algs>|-init|-run|-eval                           stacking of sub models
+  eval [-new <n>|-list|-delete <n>|-run [n]|-score [n] [-nosort]|-norm [n] [-strict]|-confmat [n]|-perf [n]]
+  export -t pmml|columnstats|woemapping|bagging|baggingpmml|corr|woe [-c] [-vars v1,v2] [-n <bins>] [-ivr <ratio>] [-bic <cnt>]
+  combo -new <algs>|-init|-run [-shuffle] [-resume]|-eval      stacking of sub models
   save [<name>] | switch <name> | show | list                  model-set branches
   encode [-run [<evalset>|*]] [-ref <modelset>]                tree leaf-path encoding
   test -filter [<evalset>|*] [-n <records>]                    dry-run filter expressions
@@ -87,19 +88,32 @@ def _dispatch(cmd, args) -> int:
             print(USAGE)
             return 1
         return run_new(args[0], _opt(args, "-t", "NN", True), _opt(args, "-m", None, True))
+    if cmd == "cp":
+        from .steps.create import copy_model_set
+        rest = [a for a in args if not a.startswith("-")]
+        if len(rest) < 2:
+            print(USAGE)
+            return 1
+        return copy_model_set(rest[0], rest[1])
     if cmd == "init":
-        from .steps.create import run_init
+        from .steps.create import init_model_params, run_init
+        if _opt(args, "-model"):
+            return init_model_params(".")
         return run_init(".", True if _opt(args, "-autotype") else None)
     if cmd == "stats":
         from .steps.stats import run_stats
         n = _opt(args, "-n", None, True)
         ivr = _opt(args, "-ivr", None, True)
-        return run_stats(".", bool(_opt(args, "-c")), bool(_opt(args, "-p")), bool(_opt(args, "-rebin")),
-                         int(n) if n else None, float(ivr) if ivr else 1.0)
+        bic = _opt(args, "-bic", None, True)
+        vars_ = _opt(args, "-vars", None, True)
+        return run_stats(".", bool(_opt(args, "-c") or _opt(args, "-correlation")),
+                         bool(_opt(args, "-p") or _opt(args, "-psi")), bool(_opt(args, "-rebin")),
+                         int(n) if n else None, float(ivr) if ivr else 1.0,
+                         min_inst_cnt=float(bic) if bic else 0, request_vars=vars_.split(",") if vars_ else None)
     if cmd in ("norm", "normalize", "transform"):
         from .steps.norm import run_norm
         return run_norm(".", shuffle=bool(_opt(args, "-shuffle")))
-    if cmd == "varsel":
+    if cmd in ("varsel", "varselect"):
         from .steps.varsel import run_varsel
         r = _opt(args, "-r", None, True)
         return run_varsel(".", bool(_opt(args, "-reset")), bool(_opt(args, "-list")), bool(_opt(args, "-autofilter")),
@@ -107,6 +121,9 @@ def _dispatch(cmd, args) -> int:
     if cmd == "train":
         from .steps.norm import run_norm
         from .steps.train import run_train
+        if _opt(args, "-debug"):
+            import logging
+            logging.getLogger("shifu_amd").setLevel(logging.DEBUG)
         if _opt(args, "-shuffle"):
             run_norm(".", shuffle=True)
         return run_train(".", dry=bool(_opt(args, "-dry")))
@@ -117,16 +134,22 @@ def _dispatch(cmd, args) -> int:
         from .steps.evaluate import run_eval
         for a in ("new", "list", "delete", "run", "score", "norm", "confmat", "perf"):
             if f"-{a}" in args:
-                return run_eval(".", a, _opt(args, f"-{a}", None, True))
-        return run_eval(".", "run", None)
+                return run_eval(".", a, _opt(args, f"-{a}", None, True), nosort=bool(_opt(args, "-nosort")),
+                                strict=bool(_opt(args, "-strict")))
+        return run_eval(".", "run", None)          # no option: every eval set
     if cmd == "export":
         from .steps.export import run_export
-        return run_export(".", _opt(args, "-t", "pmml", True), bool(_opt(args, "-c")))
+        vars_ = _opt(args, "-vars", None, True)
+        n, ivr, bic = _opt(args, "-n", None, True), _opt(args, "-ivr", None, True), _opt(args, "-bic", None, True)
+        return run_export(".", _opt(args, "-t", "pmml", True), bool(_opt(args, "-c")),
+                          request_vars=vars_.split(",") if vars_ else None, expected_bins=int(n) if n else 0,
+                          iv_keep_ratio=float(ivr) if ivr else 1.0, min_inst_cnt=float(bic) if bic else 0)
     if cmd == "combo":
         from .steps.combo import run_combo
         for a in ("new", "init", "run", "eval"):
             if f"-{a}" in args:
-                return run_combo(".", a, _opt(args, "-new", None, True) if a == "new" else None)
+                return run_combo(".", a, _opt(args, "-new", None, True) if a == "new" else None,
+                                 shuffle=bool(_opt(args, "-shuffle")), resume=bool(_opt(args, "-resume")))
         print(USAGE)
         return 1
     if cmd in ("save", "switch", "show", "list"):

@@ -79,7 +79,7 @@ def combo_init(root: str):
     return cfg
 
 
-def _pipeline(root, steps=("init", "stats", "norm", "varsel", "train"), skip_init_if_cc=True):
+def _pipeline(root, steps=("init", "stats", "norm", "varsel", "train"), skip_init_if_cc=True, shuffle=False):
     from .create import run_init
     from .norm import run_norm
     from .stats import run_stats
@@ -90,10 +90,12 @@ def _pipeline(root, steps=("init", "stats", "norm", "varsel", "train"), skip_ini
     if "stats" in steps:
         run_stats(root)
     if "norm" in steps:
-        run_norm(root)
+        run_norm(root, shuffle=shuffle)
     if "varsel" in steps:
         run_varsel(root)
     if "train" in steps:
+        if shuffle:
+            run_norm(root, shuffle=True)        # `train -shuffle` re-shuffles the normalized data
         run_train(root)
 
 
@@ -126,7 +128,12 @@ def _write_joined(out_dir, header, raw, score_cols):
             f.write("|".join(str(c[i]) for c in cols) + "\n")
 
 
-def combo_run(root: str):
+def _has_models(d: str) -> bool:
+    md = os.path.join(d, "models")
+    return os.path.isdir(md) and any(not f.startswith(".") for f in os.listdir(md))
+
+
+def combo_run(root: str, shuffle: bool = False, resume: bool = False):
     from ..config import environment
     from ..runtime.executor import ExecutorManager, cli_task
     ms = ModelSet(root)
@@ -138,13 +145,18 @@ def combo_run(root: str):
     dirs = [_sub_dir(ms, sub["modelName"]) for sub in cfg["subTrains"]]
     for sub in cfg["subTrains"]:
         _log.info("combo: training sub model %s (%s)", sub["modelName"], sub["algorithm"])
+    # -resume: sub models that already hold trained models are not trained again
+    todo = [(sub, d) for sub, d in zip(cfg["subTrains"], dirs) if not (resume and _has_models(d))]
+    if resume and len(todo) < len(dirs):
+        _log.info("combo -resume: %d of %d sub models already trained", len(dirs) - len(todo), len(dirs))
     if parallel > 1:
-        steps = ["init", "stats", "norm", "varsel", "train"]
+        steps = ["init", "stats", "norm -shuffle" if shuffle else "norm", "varsel",
+                 "train -shuffle" if shuffle else "train"]
         tasks = [cli_task([s for s in steps if not (s == "init" and os.path.exists(os.path.join(d, "ColumnConfig.json")))],
-                          d, os.path.join(d, "combo_sub.log")) for d in dirs]
+                          d, os.path.join(d, "combo_sub.log")) for _, d in todo]
     else:
-        tasks = [(lambda d=d: _pipeline(d)) for d in dirs]
-    ExecutorManager(parallel, retries).run(tasks, [sub["modelName"] for sub in cfg["subTrains"]])
+        tasks = [(lambda d=d: _pipeline(d, shuffle=shuffle)) for _, d in todo]
+    ExecutorManager(parallel, retries).run(tasks, [sub["modelName"] for sub, _ in todo])
     subs = [(sub["modelName"], ModelSet(d)) for sub, d in zip(cfg["subTrains"], dirs)]
     scores, header, raw = {}, None, None
     for name, sms in subs:
@@ -163,7 +175,7 @@ def combo_run(root: str):
     ams.mc.varSelect["forceSelectColumnNameFile"] = fs
     ams.mc.varSelect["forceEnable"] = True
     ams.save_mc()
-    _pipeline(ad, skip_init_if_cc=False)
+    _pipeline(ad, skip_init_if_cc=False, shuffle=True)   # assemble model: norm -shuffle / train -shuffle
     return 0
 
 
@@ -189,13 +201,13 @@ def combo_eval(root: str):
     return run_eval(ad)
 
 
-def run_combo(root=".", action="run", algs: str | None = None) -> int:
+def run_combo(root=".", action="run", algs: str | None = None, shuffle: bool = False, resume: bool = False) -> int:
     if action == "new":
         combo_new(root, algs or "NN,LR")
     elif action == "init":
         combo_init(root)
     elif action == "run":
-        combo_run(root)
+        combo_run(root, shuffle=shuffle, resume=resume)
     elif action == "eval":
         combo_eval(root)
     else:

@@ -151,3 +151,31 @@ def run_init(root: str = ".", auto_type: bool | None = None) -> int:
     save_column_configs(ms.ccs, ms.pf.column_config)
     _log.info("init: %d columns -> %s", len(ms.ccs), ms.pf.column_config)
     return 0
+
+
+def copy_model_set(src: str, dst: str) -> int:
+    """``shifu cp <src> <dst>`` (BasicModelProcessor.copyModelFiles :357-369): the source's
+    ModelConfig.json is written into ``dst`` with the model-set name = basename(dst) and the
+    creator = the current user."""
+    import getpass
+    from ..config.model_config import ModelConfig
+    mc = ModelConfig.load(os.path.join(src, "ModelConfig.json"))
+    os.makedirs(dst, exist_ok=True)
+    mc.basic["name"] = os.path.basename(os.path.normpath(dst))
+    try:
+        mc.basic["author"] = getpass.getuser()
+    except Exception:                     # noqa: BLE001 - no passwd entry in some containers
+        pass
+    mc.save(os.path.join(dst, "ModelConfig.json"))
+    _log.info("Model set %s copied to %s", src, dst)
+    return 0
+
+
+def init_model_params(root: str = ".") -> int:
+    """``shifu init -model`` (ShifuCLI.initializeModelParam :632-635 ->
+    checkAlgorithmParam): fill the default train.params of the configured algorithm."""
+    from .base import ModelSet, check_algorithm_params
+    ms = ModelSet(root)
+    check_algorithm_params(ms.mc)
+    ms.save_mc()
+    return 0

@@ -86,7 +86,7 @@ def _load_eval_data(ms, ev, runner_cols, extra_cols=()):
     return load_dataset(ms.mc, ds, nums, strs, require_target=False)
 
 
-def score_eval(ms: ModelSet, ev, device=None, write: bool = True):
+def score_eval(ms: ModelSet, ev, device=None, write: bool = True, nosort: bool = False):
     mc = ms.mc
     conv = ev.get("gbtScoreConvertStrategy") or "RAW"
     models_dir = ms.pf.eval_models_dir(ev)
@@ -111,7 +111,15 @@ def score_eval(ms: ModelSet, ev, device=None, write: bool = True):
             mats = [np.asarray(res[k]) for k in cols]
             metas = [md.table[m].strings() if m in md.table else np.array([""] * md.n)
                      for m in list(meta_cols) + list(score_meta)]
-            for i in range(md.n):
+            # rows leave sorted by score, descending (Eval.pig ORDER BY), except for
+            # classification or `eval -score -nosort` (EvalModelProcessor.java:432)
+            order = range(md.n)
+            if not (nosort or mc.is_multiclass()):
+                sel = ev.get("performanceScoreSelector", "mean") or "mean"
+                key = np.asarray(res.get(sel, res.get("mean")), dtype=np.float64)
+                if key.ndim == 1 and len(key) == md.n:
+                    order = np.argsort(-key, kind="stable")
+            for i in order:
                 row = [str(tags[i]), repr(float(md.w[i]))]
                 row += [f"{float(m[i]):.6f}" if m.ndim == 1 else ",".join(f"{v:.6f}" for v in m[i]) for m in mats]
                 row += [str(m[i]) for m in metas]
@@ -164,9 +172,23 @@ def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None):
     return perf
 
 
-def norm_eval(ms: ModelSet, ev):
-    """``eval -norm``: write the normalized eval data (NN inputs) for external scorers."""
+def norm_eval(ms: ModelSet, ev, strict: bool = False):
+    """``eval -norm [-strict]``: write the normalized eval data (NN inputs) for external scorers.
+    ``-strict``: every selected column must be present in the eval data (otherwise the missing
+    ones normalize as missing values)."""
     cols = ms.selected()
+    if strict:
+        from ..data.reader import read_header
+        ds = ev.dataSet
+
+        def _abs(x):
+            return x if not x or os.path.isabs(x) else os.path.join(ms.root, x)
+        hdr = set(read_header(_abs(ds.get("headerPath")), ds.get("headerDelimiter") or "|",
+                              _abs(ds.get("dataPath")), ds.get("dataDelimiter") or "|"))
+        if hdr:
+            missing = [c.name for c in cols if c.name not in hdr]
+            if missing:
+                raise ValueError(f"eval -norm -strict: selected columns missing from {ev.get('name')}: {missing}")
     md = _load_eval_data(ms, ev, [c.name for c in cols])
     X, names, _ = normalize_table(ms.mc, ms.ccs, md.table, columns=cols)
     save_dataset(ms.pf.eval_normalized(ev), {"X": X, "y": md.y, "w": md.w.astype(np.float32)},
@@ -174,7 +196,8 @@ def norm_eval(ms: ModelSet, ev):
     return X
 
 
-def run_eval(root: str = ".", action: str = "run", name: str | None = None, device=None) -> int:
+def run_eval(root: str = ".", action: str = "run", name: str | None = None, device=None, nosort: bool = False,
+             strict: bool = False) -> int:
     ms = ModelSet(root)
     if action == "new":
         new_eval(ms, name)
@@ -189,9 +212,9 @@ def run_eval(root: str = ".", action: str = "run", name: str | None = None, devi
     ms.setup("EVAL", validate=False)
     for ev in _eval_confs(ms, name):
         if action == "norm":
-            norm_eval(ms, ev)
+            norm_eval(ms, ev, strict)
             continue
-        md, res, tags, score_meta = score_eval(ms, ev, device)
+        md, res, tags, score_meta = score_eval(ms, ev, device, nosort=nosort)
         if action in ("run", "perf", "confmat"):
             perf_eval(ms, ev, md, res, tags, score_meta, device)
     return 0

@@ -23,13 +23,13 @@ _log = get_logger("steps.stats")
 
 def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, rebin: bool = False,
               expected_bins: int | None = None, iv_keep_ratio: float = 1.0, bin_avg_score_only: bool = False,
-              device=None) -> int:
+              device=None, min_inst_cnt: float = 0, request_vars: list[str] | None = None) -> int:
     ms = ModelSet(root).setup("STATS")
     mc = ms.mc
     cols = ms.stats_columns()
     if rebin:
-        do_rebin(ms, expected_bins or int(mc.stats.get("maxNumBin", 10)), iv_keep_ratio)
-        ms.save_cc(backup=True)
+        do_rebin(ms, expected_bins or 0, iv_keep_ratio, min_inst_cnt, request_vars)
+        ms.save_cc()
         return 0
     if correlation:                     # `stats -c` only computes correlation (stats must exist)
         run_correlation(ms, device)
@@ -69,19 +69,39 @@ def run_correlation(ms: ModelSet, device=None):
     X = np.stack(mats, 1) if mats else np.zeros((md.n, 0))
     C = S.pearson_correlation(X, device)
     path = ms.pf.correlation_csv
+    # StatsModelProcessor.computeCorrValue layout (:490-590): an index line, a name line, then one
+    # row per computed column: "<num>,<name>,<corr with every ColumnConfig column, ', '-joined>"
+    # (columns without a correlation - meta, target-less, not computed - read 0.0)
+    pos = {c.num: i for i, c in enumerate(cols)}
     with open(path, "w") as f:
-        f.write("," + ",".join(c.name for c in cols) + "\n")
+        f.write("ColumnIndex," + "".join(f",{c.num}" for c in ms.ccs) + "\n")
+        f.write(",ColumnName" + "".join(f",{c.name}" for c in ms.ccs) + "\n")
         for i, c in enumerate(cols):
-            f.write(c.name + "," + ",".join(repr(float(v)) for v in C[i]) + "\n")
+            vals = [repr(float(C[i, pos[o.num]])) if o.num in pos else "0.0" for o in ms.ccs]
+            f.write(f"{c.num},{c.name}," + ", ".join(vals) + "\n")
     _log.info("correlation: %d columns -> %s", len(cols), path)
     return C, [c.num for c in cols]
 
 
 def read_correlation(path: str):
+    """Parse ``correlation.csv``: returns (names of the computed rows, square matrix over them)."""
     with open(path) as f:
-        names = f.readline().rstrip("\n").split(",")[1:]
-        rows = [list(map(float, l.rstrip("\n").split(",")[1:])) for l in f if l.strip()]
-    return names, np.array(rows)
+        f.readline()
+        names_all = f.readline().rstrip("\n").split(",")[2:]
+        keys, names, rows = [], [], []
+        for line in f:
+            if not line.strip():
+                continue
+            parts = line.rstrip("\n").split(",")
+            keys.append(int(parts[0]))
+            names.append(parts[1])
+            rows.append([float(v) for v in parts[2:]])
+    if not rows:
+        return [], np.zeros((0, 0))
+    full = np.array(rows)
+    # row key -> column position in the all-column value list (ColumnConfig order = columnNum)
+    idx = [names_all.index(nm) if nm in names_all else k for k, nm in zip(keys, names)]
+    return names, full[:, idx]
 
 
 def _iv(pos, neg):
@@ -115,25 +135,49 @@ def rebin_numeric(bounds, cpos, cneg, wpos, wneg, target_bins: int, iv_keep_rati
     return b, cp + [miss[0]], cn + [miss[1]], wp + [miss[2]], wn + [miss[3]]
 
 
-def do_rebin(ms: ModelSet, target_bins: int, iv_keep_ratio: float = 1.0):
+def do_rebin(ms: ModelSet, target_bins: int, iv_keep_ratio: float = 1.0, min_inst_cnt: float = 0,
+             request_vars: list[str] | None = None):
+    """``stats -rebin`` (StatsModelProcessor.java:165-205, doReBin :670-760): re-bin from the
+    binning saved in ``tmp/ColumnConfig.json`` (created on the first rebin, so repeated rebins
+    always start from the original stats), for the requested good candidate columns, with the
+    IV-keeping dynamic merge of ``algos.dynamic_binning``."""
+    import json
+    import os
+    from ..algos.dynamic_binning import CATEGORICAL_GROUP_VAL_DELIMITER, dynamic_rebin
+    from ..config.column_config import save_column_configs
+    backup = ms.pf.p("tmp", "ColumnConfig.json")
+    if not os.path.exists(backup):
+        os.makedirs(os.path.dirname(backup), exist_ok=True)
+        save_column_configs(ms.ccs, backup)
+    else:
+        with open(backup) as f:
+            saved = {d["columnName"]: d.get("columnBinning") for d in json.load(f)}
+        for c in ms.ccs:
+            if saved.get(c.name) is not None:
+                c.d["columnBinning"] = saved[c.name]
     binary = ms.mc.is_binary()
-    for c in ms.stats_columns():
-        if c.bin_count_pos is None:
+    from ..config.column_config import has_candidates
+    has_cand = has_candidates(ms.ccs)
+    for c in ms.ccs:
+        if request_vars and c.name not in request_vars:
+            continue
+        if not c.is_good_candidate(has_cand, binary) or c.bin_count_pos is None:
             continue
         cp, cn = np.asarray(c.bin_count_pos), np.asarray(c.bin_count_neg)
         wp, wn = np.asarray(c.bin_weighted_pos), np.asarray(c.bin_weighted_neg)
-        if c.is_categorical():
-            cats = c.bin_category or []
-            if len(cats) <= target_bins:
-                continue
-            cats2, cp2, cn2, wp2, wn2 = rebin_categorical(cats, list(cp), list(cn), list(wp), list(wn), target_bins)
-            c.bin_category = cats2
+        cat = c.is_categorical()
+        keys = (c.bin_category if cat else c.bin_boundary) or []
+        if not keys:
+            continue
+        bins, miss = dynamic_rebin(cat, keys, cp, cn, wp, wn, target_bins or 0, iv_keep_ratio, min_inst_cnt)
+        if cat:
+            c.bin_category = [CATEGORICAL_GROUP_VAL_DELIMITER.join(b.values) for b in bins]
         else:
-            bb = c.bin_boundary or []
-            if len(bb) <= target_bins:
-                continue
-            bb2, cp2, cn2, wp2, wn2 = rebin_numeric(bb, cp, cn, wp, wn, target_bins, iv_keep_ratio)
-            c.bin_boundary = bb2
+            c.bin_boundary = [b.left for b in bins]
+        cp2 = [b.pos for b in bins] + [miss.pos]
+        cn2 = [b.neg for b in bins] + [miss.neg]
+        wp2 = [b.wpos for b in bins] + [miss.wpos]
+        wn2 = [b.wneg for b in bins] + [miss.wneg]
         cb = c.binning
         cb["binCountPos"], cb["binCountNeg"] = [int(x) for x in cp2], [int(x) for x in cn2]
         cb["binWeightedPos"], cb["binWeightedNeg"] = [float(x) for x in wp2], [float(x) for x in wn2]
