@@ -123,9 +123,14 @@ def load_generic(path: str) -> GenericModel:
 
 
 def find_generic_models(models_dir: str):
-    """``models/*.json`` generic model configs (sorted by name)."""
+    """``models/*.json`` generic model configs and ``models/<name>/GenericModelConfig.json``
+    model directories (the layout the reference's TF trainer writes; checkpoint directories
+    ``<name>-checkpoint-<epoch>`` are skipped), sorted by path."""
     import glob
-    return sorted(p for p in glob.glob(os.path.join(models_dir, "*.json")) if _is_generic_config(p))
+    cands = glob.glob(os.path.join(models_dir, "*.json"))
+    cands += [p for p in glob.glob(os.path.join(models_dir, "*", "GenericModelConfig.json"))
+              if "-checkpoint-" not in os.path.basename(os.path.dirname(p))]
+    return sorted(p for p in cands if _is_generic_config(p))
 
 
 def _is_generic_config(path: str) -> bool:

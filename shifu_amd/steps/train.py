@@ -259,14 +259,53 @@ class TrainStep:
         if self.metrics is not None:
             self.metrics.write(trainer=trainer_id, epoch=epoch, train_error=terr, valid_error=verr, **(extra or {}))
 
+    def _train_tensorflow(self) -> int:
+        """``algorithm: TENSORFLOW`` (TensorflowTrainer + train.py): a mini-batch DNN trained with
+        torch autograd, gradients all-reduced per batch over RCCL; saved as a generic model under
+        ``models/<ModelSetName>/`` (+ ``-checkpoint-<epoch>`` copies)."""
+        from ..models.dnn_sgd import save_generic, train_dnn
+        ms, mc = self.ms, self.mc
+        ts = load_train_set(ms, False)
+        if ts.X is None:
+            raise ValueError("TENSORFLOW training needs the normalized data (run `shifu norm`)")
+        params = dict(mc.train.get("params") or {})
+        seed = max(0, int(mc.train.get("baggingSampleSeed", -1)))
+        _, valid, sw = split_masks(mc, ts, 0, -1, seed)
+        dev = self.dev
+        names = [c.name for c in ms.input_columns()]
+        name = mc.basic.get("name") or "model"
+        out = os.path.join(ms.pf.models_dir, name)
+        rank0 = self.info.rank == 0
+        if rank0:
+            os.makedirs(ms.pf.models_dir, exist_ok=True)
+
+        def log_fn(ep, terr, verr):
+            if rank0:
+                _log.info("Epoch %d avg train error %.8f, avg validation error is %.8f.", ep, terr, verr)
+
+        def ckpt_fn(model, ep):
+            if rank0:
+                save_generic(model, f"{out}-checkpoint-{ep}", names, {"epoch": ep})
+        X = np.asarray(ts.X, dtype=np.float32)
+        model, hist = train_dnn(X, np.asarray(ts.y), np.asarray(sw), valid, params,
+                                int(mc.train.get("numTrainEpochs", 100) or 100), dev, seed, log_fn, ckpt_fn)
+        if rank0:
+            path = save_generic(model, out, names, {"epochs": len(hist),
+                                                    "trainError": hist[-1][1] if hist else None})
+            _log.info("TENSORFLOW model -> %s", path)
+        dist.barrier()
+        return 0
+
     def process(self) -> int:
         ms, mc = self.ms, self.mc
         ms.setup("TRAIN")
         alg = mc.algorithm
-        if alg in ("GENERIC", "TENSORFLOW"):
+        if alg == "GENERIC":
             raise ValueError(f"algorithm {alg}: generic models are trained outside shifu; put their "
                              "GenericModelConfig JSON (+ artifacts) under models/ and run eval/export "
                              "(scoring/generic.py)")
+        if alg == "TENSORFLOW":
+            return self._train_tensorflow()
         if alg not in ("NN", "LR", "GBT", "RF", "WDL"):
             raise ValueError(f"unsupported algorithm {alg}")
         is_tree = alg in TREE_ALGS
