@@ -255,25 +255,41 @@ def _load_network(i: JavaIn) -> NNNetwork:
     return NNNetwork.from_flat(feed, w, acts, widx, props, feats)
 
 
+def write_column_stats(o: JavaOut, cs: NNColumnStats):
+    """NNColumnStats.write (J/core/dtrain/nn/NNColumnStats.java:97-124)."""
+    o.int(cs.column_num)
+    o.string(cs.column_name)
+    o.byte(TYPE_BYTE.get(cs.column_type or "N", 1))
+    for v in (cs.cutoff, cs.mean, cs.stddev, cs.woe_mean, cs.woe_stddev, cs.woe_wgt_mean, cs.woe_wgt_stddev):
+        o.double(0.0 if v is None else v)
+    o.double_array(cs.bin_boundaries)
+    cats = cs.bin_categories or []
+    o.int(len(cats))
+    for c in cats:
+        o.string(c)
+    o.double_array(cs.bin_pos_rates)
+    o.double_array(cs.bin_count_woes)
+    o.double_array(cs.bin_weight_woes)
+
+
+def read_column_stats(i: JavaIn) -> NNColumnStats:
+    num = i.int()
+    name = i.string()
+    typ = BYTE_TYPE.get(i.byte(), "N")
+    vals = [i.double() for _ in range(7)]
+    bb = i.double_array()
+    cats = [i.string() for _ in range(i.int())]
+    pr, cw, ww = i.double_array(), i.double_array(), i.double_array()
+    return NNColumnStats(num, name, typ, *vals, bb, cats, pr, cw, ww)
+
+
 def write_binary_nn(path: str, norm_type: str, col_stats: list, column_mapping: dict, networks: list):
     o = JavaOut()
     o.int(1)
     o.string(norm_type)
     o.int(len(col_stats))
     for cs in col_stats:
-        o.int(cs.column_num)
-        o.string(cs.column_name)
-        o.byte(TYPE_BYTE.get(cs.column_type or "N", 1))
-        for v in (cs.cutoff, cs.mean, cs.stddev, cs.woe_mean, cs.woe_stddev, cs.woe_wgt_mean, cs.woe_wgt_stddev):
-            o.double(0.0 if v is None else v)
-        o.double_array(cs.bin_boundaries)
-        cats = cs.bin_categories or []
-        o.int(len(cats))
-        for c in cats:
-            o.string(c)
-        o.double_array(cs.bin_pos_rates)
-        o.double_array(cs.bin_count_woes)
-        o.double_array(cs.bin_weight_woes)
+        write_column_stats(o, cs)
     o.int(len(column_mapping))
     for k, v in column_mapping.items():
         o.int(k)
@@ -290,16 +306,7 @@ def read_binary_nn(path: str):
         i = JavaIn(f.read())
     version = i.int()
     norm = i.string()
-    stats = []
-    for _ in range(i.int()):
-        num = i.int()
-        name = i.string()
-        typ = BYTE_TYPE.get(i.byte(), "N")
-        vals = [i.double() for _ in range(7)]
-        bb = i.double_array()
-        cats = [i.string() for _ in range(i.int())]
-        pr, cw, ww = i.double_array(), i.double_array(), i.double_array()
-        stats.append(NNColumnStats(num, name, typ, *vals, bb, cats, pr, cw, ww))
+    stats = [read_column_stats(i) for _ in range(i.int())]
     mapping = {}
     for _ in range(i.int()):
         k = i.int()

@@ -9,9 +9,8 @@ layers down to one logit; ``p = sigmoid(wide + deep)``; the gradient is the sigm
 over ranks like the NN trainer (``WDLMaster.doCompute`` :164-184 sums worker gradients).
 
 On the GPU the embedding gathers / GEMMs run as PyTorch-ROCm ops (hipBLASLt GEMMs; the model is
-small and bandwidth-bound on the embedding gathers).  File format ``.wdl``: gzip Java
-DataOutput: version, norm type, NNColumnStats, JSON architecture, parameter arrays (this
-framework's own layout; the reference's BinaryWDLSerializer is WIP upstream).
+small and bandwidth-bound on the embedding gathers).  File format ``.wdl``: the reference's
+``BinaryWDLSerializer`` / ``IndependentWDLModel`` layout (``formats/wdl_format.py``).
 """
 from __future__ import annotations
 
@@ -95,32 +94,54 @@ class WDLModel:
 
 
 def write_wdl(path: str, model: WDLModel):
-    o = JavaOut()
-    o.int(1)
-    o.string(model.norm_type)
-    o.string(json.dumps({"arch": model.net.arch(), "columns": model.columns, "cutoff": model.cutoff}))
-    params = [p.detach().double().cpu().numpy().reshape(-1) for p in model.net.parameters()]
-    o.int(len(params))
-    for p in params:
-        o.double_array(p)
-    with open(path, "wb") as f:
-        f.write(o.gzip_bytes())
+    """Reference ``.wdl`` layout (``formats/wdl_format.py``, BinaryWDLSerializer :57-108)."""
+    from ..formats.wdl_format import WDLSpec, write_wdl_file
+    net = model.net
+    nums = {cs.column_name: cs.column_num for cs in model.col_stats}
+    types = {cs.column_name: cs.column_type for cs in model.col_stats}
+    num_names = [n for n in model.columns if types.get(n, "N") != "C"]
+    cat_names = [n for n in model.columns if types.get(n, "N") == "C"]
+    ids = lambda names: [int(nums.get(n, k)) for k, n in enumerate(names)]   # noqa: E731
+    dense_ids, wide_ids = ids(num_names), ids(cat_names)
+    f32 = lambda t: t.detach().float().cpu().numpy()   # noqa: E731
+    spec = WDLSpec(
+        n_dense=net.n_dense, dense_ids=dense_ids, embed_ids=[wide_ids[f] for f in net.embed_fields],
+        embed_outputs=[net.embed_dim] * len(net.embed_fields), wide_ids=wide_ids,
+        cate_sizes={cid: s + 1 for cid, s in zip(wide_ids, net.cat_sizes)}, hidden=list(net.hidden),
+        acts=list(net.acts), l2reg=float(getattr(model, "l2reg", 0.0)),
+        hidden_W=[f32(W[:, :-1]).T.copy() for W in net.layers], hidden_b=[f32(W[:, -1]) for W in net.layers],
+        final_W=f32(net.final[:, :-1]).T.copy(), final_b=f32(net.final[:, -1]),
+        embed_W=[f32(e) for e in net.embeds], wide_W=[f32(t) for t in net.wide_tables],
+        wide_dense=f32(net.wide_dense), bias=float(net.bias.detach()[0]), wide_on=net.wide_on, deep_on=net.deep_on)
+    write_wdl_file(path, model.norm_type, model.col_stats, spec)
 
 
 def read_wdl(path: str) -> WDLModel:
-    with open(path, "rb") as f:
-        i = JavaIn(f.read())
-    i.int()
-    norm = i.string()
-    meta = json.loads(i.string())
-    a = meta["arch"]
-    net = WideDeepNet(a["n_dense"], a["cat_sizes"], a["embed_fields"], a["embed_dim"], a["hidden"], a["acts"],
-                      a["wide"], a["deep"])
-    n = i.int()
+    from ..formats.wdl_format import read_wdl_file
+    _, norm, stats, sp = read_wdl_file(path)
+    byid = {cs.column_num: cs for cs in stats}
+    cat_sizes = [int(sp.cate_sizes.get(c, len(w) if w is not None else 1)) - 1
+                 for c, w in zip(sp.wide_ids, sp.wide_W or [None] * len(sp.wide_ids))]
+    embed_fields = [sp.wide_ids.index(c) for c in sp.embed_ids]
+    embed_dim = sp.embed_outputs[0] if sp.embed_outputs else (sp.embed_W[0].shape[1] if sp.embed_W else 8)
+    net = WideDeepNet(sp.n_dense, cat_sizes, embed_fields, embed_dim, list(sp.hidden), list(sp.acts),
+                      sp.wide_on, sp.deep_on)
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float32))   # noqa: E731
     with torch.no_grad():
-        for p, _ in zip(net.parameters(), range(n)):
-            p.copy_(torch.tensor(i.double_array(), dtype=torch.float32).view_as(p))
-    return WDLModel(net, norm, [], meta["columns"], meta["cutoff"])
+        if sp.wide_on:
+            for q, w in zip(net.wide_tables, sp.wide_W):
+                q.copy_(t(w))
+            net.wide_dense.copy_(t(sp.wide_dense))
+            net.bias.fill_(float(sp.bias or 0.0))
+        if sp.deep_on:
+            for q, w in zip(net.embeds, sp.embed_W):
+                q.copy_(t(w))
+            for q, W, b in zip(net.layers, sp.hidden_W, sp.hidden_b):
+                q.copy_(torch.cat([t(W).t(), t(b)[:, None]], 1))
+            net.final.copy_(torch.cat([t(sp.final_W).t(), t(sp.final_b)[:, None]], 1))
+    names = [byid[c].column_name for c in sp.dense_ids + sp.wide_ids if c in byid]
+    cutoff = stats[0].cutoff if stats else 6.0
+    return WDLModel(net, norm, stats, names, cutoff)
 
 
 def train_wdl_step(step, tid, p, ts, y, train_m, valid_m, sw):
@@ -176,5 +197,8 @@ def train_wdl_step(step, tid, p, ts, y, train_m, valid_m, sw):
             verr = float(((torch.sigmoid(net(vd, vi)) - vy) ** 2).mean()) if len(vy) else float("nan")
         step._log_epoch(tid, ep, terr, verr)
     if step.info.rank == 0:
-        write_wdl(ms.pf.model_path(tid, "wdl"), WDLModel(net.cpu(), mc.norm_type, [], [c.name for c in cols], cutoff))
+        from ..steps.train import nn_column_stats
+        m = WDLModel(net.cpu(), mc.norm_type, nn_column_stats(mc, cols), [c.name for c in cols], cutoff)
+        m.l2reg = l2
+        write_wdl(ms.pf.model_path(tid, "wdl"), m)
     return verr

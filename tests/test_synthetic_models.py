@@ -41,6 +41,26 @@ def test_wdl_pipeline(tmp_path):
     assert os.path.exists(os.path.join(root, "models/model0.wdl"))
     auc = json.load(open(os.path.join(root, "evals/Eval1/EvalPerformance.json")))["areaUnderRoc"]
     assert auc > 0.8
+    # reference BinaryWDLSerializer layout: gzip, version 1, reserved fields, norm type, column stats
+    import gzip
+    import struct
+    raw = gzip.open(os.path.join(root, "models/model0.wdl")).read()
+    assert struct.unpack(">i", raw[:4])[0] == 1
+    assert raw[4:20] == b"\0" * 16 and raw[20:22] == struct.pack(">h", 14) and raw[22:36] == b"Reserved field"
+    # read back -> identical scores
+    import torch
+    from shifu_amd.formats.wdl_format import read_wdl_file
+    from shifu_amd.models.wdl import read_wdl, write_wdl
+    m = read_wdl(os.path.join(root, "models/model0.wdl"))
+    _, norm, stats, spec = read_wdl_file(os.path.join(root, "models/model0.wdl"))
+    assert spec.hidden == [16] and spec.acts == ["relu"] and spec.n_dense == len(spec.dense_ids)
+    assert {cs.column_num for cs in stats} >= set(spec.dense_ids + spec.wide_ids)
+    p2 = os.path.join(str(tmp_path), "again.wdl")
+    write_wdl(p2, m)
+    m2 = read_wdl(p2)
+    for a, b in zip(m.net.parameters(), m2.net.parameters()):
+        torch.testing.assert_close(a, b)
+    assert m2.columns == m.columns
 
 
 @pytest.mark.parametrize("method", ["NATIVE", "ONEVSALL"])
