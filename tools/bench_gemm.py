@@ -119,6 +119,14 @@ def main():
                         res.setdefault(f"{nm}_persist{val}", []).append(round(ms, 4))
                     nat.call_hip("shifu_gemm_set_tune", 1, 0)
                     nat.call_hip("shifu_gemm_set_big", a.big)
+                elif kind in ("interleave", "interleave8"):   # wgrad row-split layout (big 0 / big 3)
+                    nat.call_hip("shifu_gemm_set_big", 3 if kind == "interleave8" else 0)
+                    nat.call_hip("shifu_gemm_set_tune", 2, val)
+                    for nm, f in (("wgrad1", wgrad1), ("wgrad2", wgrad2)):
+                        ms = timeit(f, a.iters)
+                        res.setdefault(f"{nm}_{kind}{val}", []).append(round(ms, 4))
+                    nat.call_hip("shifu_gemm_set_tune", 2, 0)
+                    nat.call_hip("shifu_gemm_set_big", a.big)
                 elif kind == "out_waves":
                     nat.call_hip("shifu_mlp_set_out_waves", val)
                     ms = timeit(output, a.iters)
