@@ -15,6 +15,8 @@
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import torch
 
@@ -43,21 +45,50 @@ def _candidates(mc, ccs):
     return out, forced
 
 
-def pareto_sort(tuples):
-    """Iterative epsilon-nondominated fronts over (ks, iv) (VariableSelector.sortByPareto)."""
-    rest = list(tuples)
-    out = []
-    while rest:
-        front = []
-        for t in rest:
-            dominated = any((o[1] >= t[1] and o[2] >= t[2]) and (o[1] > t[1] or o[2] > t[2]) for o in rest)
-            if not dominated:
-                front.append(t)
-        front.sort(key=lambda t: (-t[1], -t[2]))
-        out.extend(front)
-        ids = {id(t) for t in front}
-        rest = [t for t in rest if id(t) not in ids]
-    return out
+def pareto_sort(tuples, epsilons=None):
+    """``VariableSelector.sortByPareto`` (J/core/VariableSelector.java:296-404): an epsilon-box
+    archive over (ks, iv) tuples ``(num, ks, iv)`` in the reference's orientation (smaller box
+    coordinates dominate; same box -> the one nearer the box corner stays); ``epsilons`` from
+    ``varSelect.epsilons`` (default [0.01, 0.05]).  Returns the archive in insertion order."""
+    eps = list(epsilons) if epsilons else [0.01, 0.05]
+    arch = []                                  # [(box, tuple)]
+    for t in tuples:
+        vals = (t[1], t[2])
+        ebox = [math.floor((vals[0] if i == 0 else vals[1]) / e) for i, e in enumerate(eps)]
+        idx, keep = 0, True
+        while idx < len(arch):
+            abox, at = arch[idx]
+            adom = sdom = nondom = False
+            for i in range(len(eps)):
+                if abox[i] < ebox[i]:
+                    adom = True
+                    if sdom:
+                        nondom = True
+                        break
+                elif abox[i] > ebox[i]:
+                    sdom = True
+                    if adom:
+                        nondom = True
+                        break
+            if nondom:
+                idx += 1
+                continue
+            if adom:
+                keep = False
+                break
+            if sdom:
+                del arch[idx]
+                continue
+            corner = [b * e for b, e in zip(ebox, eps)]
+            sd = sum(((vals[0] if j == 0 else vals[1]) - corner[j]) ** 2 for j in range(len(eps)))
+            ad = sum(((at[1] if j == 0 else at[2]) - corner[j]) ** 2 for j in range(len(eps)))
+            if ad < sd:
+                keep = False
+                break
+            del arch[idx]
+        if keep:
+            arch.append((ebox, t))
+    return [t for _, t in arch]
 
 
 def select_by_filter(mc, ccs):
@@ -75,7 +106,7 @@ def select_by_filter(mc, ccs):
         filter_num = int(len(cands) * (1 - float(ratio)))
     ks_list = sorted(cands, key=lambda c: -(c.ks or 0.0))
     iv_list = sorted(cands, key=lambda c: -(c.iv or 0.0))
-    par = pareto_sort([(c.num, c.ks or 0.0, c.iv or 0.0) for c in cands])
+    par = pareto_sort([(c.num, c.ks or 0.0, c.iv or 0.0) for c in cands], mc.varSelect.get("epsilons"))
     expected = min(len(selected) + len(ks_list), filter_num)
     for c in ccs:
         c.final_select = False

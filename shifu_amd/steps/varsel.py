@@ -108,54 +108,29 @@ def select_by_fi(ms, device=None):
     return [(cols[i].name, float(imp[i])) for i in order]
 
 
-def voted_selection(ms, device=None, population: int = 12, generations: int = 4, seed: int = 0):
-    """GA wrapper (``CandidateGenerator.nextGeneration`` J/core/dvarsel/wrapper/CandidateGenerator.java:113-200):
-    candidates are column subsets of size ``filterNum``; fitness = validation MSE of a small NN;
-    next generation = inherit the best half + hybrid (crossover) + mutate."""
+def voted_selection(ms, device=None, seed: int = 0):
+    """``filterBy V``: genetic wrapper (``algos/ga_varsel.py``; WrapperMasterConductor +
+    CandidateGenerator + ValidationConductor) with the population trained as one batched GEMM."""
+    from ..algos.ga_varsel import voted_selection as ga
+    from ..parallel import dist
     mc = ms.mc
     cols = _good(ms)
     md = ms.load_raw(cols)
     X, _, nums = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
-    k = min(int(mc.varSelect.get("filterNum", 200) or len(cols)), len(cols))
-    rng = np.random.default_rng(seed)
-    n = X.shape[0]
-    va = rng.random(n) < 0.2
+    info = dist.info()
+    lo, hi = md.n * info.rank // info.world_size, md.n * (info.rank + 1) // info.world_size
     from ..utils.device import default_device
     dev = torch.device(device) if device is not None else default_device()
-
-    def fitness(subset):
-        spec = MLPSpec(len(subset), [max(4, min(30, len(subset)))], ["tanh"], 1, "sigmoid")
-        tr = MLPTrainer(spec, dev, "R", 0.1, seed=int(rng.integers(1 << 30)))
-        tx = tr.prepare(torch.from_numpy(X[~va][:, subset]), md.y[~va].reshape(-1, 1))
-        vx = tr.prepare(torch.from_numpy(X[va][:, subset]), md.y[va].reshape(-1, 1))
-        for _ in range(20):
-            tr.step(tx)
-        return tr.evaluate(vx)
-    pop = [np.sort(rng.choice(len(cols), k, replace=False)) for _ in range(population)]
-    scored = []
-    for g in range(generations):
-        scored = sorted(((fitness(s), tuple(s)) for s in pop), key=lambda t: t[0])
-        _log.info("voted varsel generation %d best validation error %.6f", g, scored[0][0])
-        keep = [np.array(s) for _, s in scored[: population // 2]]
-        children = []
-        while len(keep) + len(children) < population:
-            a, b = rng.choice(len(keep), 2, replace=False)
-            pool = np.union1d(keep[a], keep[b])
-            child = np.sort(rng.choice(pool, k, replace=False))
-            if rng.random() < 0.3:             # mutate one gene
-                out = rng.integers(k)
-                rest = np.setdiff1d(np.arange(len(cols)), child)
-                if rest.size:
-                    child[out] = rng.choice(rest)
-                    child = np.sort(child)
-            children.append(child)
-        pop = keep + children
-    best = set(int(i) for i in scored[0][1])
+    params = dict(mc.varSelect.get("params") or {})
+    nn_params = dict(mc.train.get("params") or {})
+    epochs = int(mc.train.get("numTrainEpochs", 100) or 100)
+    best, hist = ga(X[lo:hi], md.y[lo:hi], md.w[lo:hi], cols, params, nn_params, epochs,
+                    float(mc.train.get("validSetRate", 0.2) or 0.2), seed, dev,
+                    log=lambda it, e: _log.info("voted varsel generation %d best validation error %.6f", it, e))
+    chosen = {c.num for c in best}
     for c in ms.ccs:
-        c.final_select = c.is_force_select()
-    for i in best:
-        cols[i].final_select = True
-    return [cols[i].name for i in sorted(best)]
+        c.final_select = c.is_force_select() or c.num in chosen
+    return [c.name for c in best]
 
 
 def run_auto_filter(ms):

@@ -120,10 +120,15 @@ def test_varsel_filter_ks_iv_mix(cancer):
             assert {c.name for c in sel} == {c.name for c in top}
 
 
-def test_pareto_front_order():
+def test_pareto_epsilon_archive():
+    """VariableSelector.Archives.sortInto semantics: epsilon boxes floor(ks/0.01), floor(iv/0.05);
+    the smaller box dominates (the reference archive minimizes), mutually non-dominated boxes both
+    stay, same box -> the tuple nearer the box corner stays."""
     pts = [(0, 1.0, 1.0), (1, 2.0, 0.5), (2, 0.5, 0.5), (3, 3.0, 3.0)]
-    order = [p[0] for p in V.pareto_sort(pts)]
-    assert order[0] == 3 and order[-1] == 2
+    assert [p[0] for p in V.pareto_sort(pts)] == [2]
+    assert [p[0] for p in V.pareto_sort([(0, 1.0, 1.0), (1, 2.0, 0.5)])] == [0, 1]
+    # same box (eps 1.0): 0.1 is nearer the corner 0.0 than 0.9
+    assert [p[0] for p in V.pareto_sort([(0, 0.9, 0.9), (1, 0.1, 0.1)], [1.0, 1.0])] == [1]
 
 
 def test_pearson_pairwise_complete():
