@@ -82,6 +82,11 @@ class PathFinder:
         return self._custom("normalizedValidationDataPath") or self.p(TMP, "NormalizedValidationData")
 
     @property
+    def selected_raw_data(self):
+        """tmp/SelectedRawData (customPaths.selectedRawDataPath), PathFinder.getSelectedRawDataPath :323."""
+        return self._custom("selectedRawDataPath") or self.p(TMP, "SelectedRawData")
+
+    @property
     def cleaned_data(self):
         return self._custom("cleanedDataPath") or self.p(TMP, "CleanedData")
 

@@ -82,6 +82,9 @@ class TreeConfig:
     sample_with_replacement: bool = False
     dropout_rate: float = 0.0
     max_leaves: int = 0                 # > 0: leaf budget, best (gain x weight) splits first
+    max_batch_split: int = 0            # MaxBatchSplitSize: leaf-wise nodes split per level (0 = no cap)
+    max_stats_memory_mb: int = 0        # MaxStatsMemoryMB: node-batch bound of the reference (DTMaster
+                                        # :437-476); every level's histograms fit in HBM, so it only logs
     seed: int = 0
     valid_tolerance: float = 0.0
     early_stop: bool = False
@@ -323,6 +326,8 @@ class TreeTrainer:
                 cands = sorted((-(float(best[z["slot"]][2]) * float(tree.wgt_cnt[z["id"]])), z["slot"])
                                for z in nodes if best[z["slot"]][7])
                 room = max(0, c.max_leaves - n_leaves)
+                if c.max_batch_split > 0:   # DTMaster :360 intends this cap (its loop never counts)
+                    room = min(room, c.max_batch_split)
                 allowed = {s_ for _, s_ in cands[:room]}
             for z in nodes:
                 s_ = z["slot"]

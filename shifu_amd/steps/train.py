@@ -592,6 +592,8 @@ class TrainStep:
                          else bool(mc.train.get("baggingWithReplacement", True)),
                          dropout_rate=float(_num(p.get("DropoutRate"), 0.0)), seed=tid,
                          max_leaves=int(_num(p.get("MaxLeaves"), 0)),
+                         max_batch_split=int(_num(p.get("MaxBatchSplitSize"), 0)),
+                         max_stats_memory_mb=int(_num(p.get("MaxStatsMemoryMB"), 0)),
                          valid_tolerance=float(_num(p.get("ValidationTolerance"), 0.0)),
                          early_stop=str(p.get("EnableEarlyStop", "false")).lower() == "true")
         tt = TreeTrainer(cfg, d, vd)
