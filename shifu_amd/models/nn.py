@@ -453,6 +453,7 @@ class MLPTrainer:
         self.chunk_rows = int(chunk_rows)
         self.wgrad_splits = wgrad_splits
         self.fused_tail = self._tail_eligible()
+        self.fused_head = (not self.fused_tail) and self._head_eligible()
         self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
         # dropout (NNMaster.dropoutNodes :531-556, FloatFlatNetwork.computeLayer :205-215): each
         # iteration drops hidden nodes with DropoutRate and inputs with 0.4*DropoutRate and scales
@@ -563,6 +564,20 @@ class MLPTrainer:
             ok = ok and ACT_IDS[sp.acts[L - 2]] in ACT_DERIV_FROM_OUTPUT
         return bool(ok)
 
+    def _head_eligible(self) -> bool:
+        """Fused network head (gemm_kernels.hip: gemm_head_8ph_kernel): last hidden forward GEMM +
+        output layer + loss + deltas + output wgrad in one 8-phase GEMM epilogue, so the last
+        hidden activations never leave the chip.  n_out == 1, last hidden padded width <= 256,
+        an activation whose derivative follows from its output (not ptanh).  On by default on
+        the GPU (SHIFU_FUSED_HEAD=0 disables); large chunks only (the 8-phase tile is 256 rows)."""
+        sp = self.spec
+        L = len(sp.hidden)
+        if self.device.type != "cuda" or L == 0 or os.environ.get("SHIFU_FUSED_HEAD", "1") == "0":
+            return False
+        a = ACT_IDS[sp.acts[L - 1]]
+        return bool(sp.n_out == 1 and sp.layer_kpad[L] <= 256 and a in ACT_DERIV_FROM_OUTPUT and
+                    sp.acts[L - 1] != "ptanh" and sp.hidden[L - 1] <= 255)
+
     def _tail_eligible(self) -> bool:
         """Opt-in (SHIFU_FUSED_TAIL=1).  Measured on MI355X at the bench shape (1M-row chunk,
         512/256 padded hidden widths): fused 2.09 ms vs 1.76 ms for the three unfused kernels -
@@ -585,9 +600,10 @@ class MLPTrainer:
         dels = [None] + [d[:mc] for d in ws["deltas"]]
         ders = [None] + [(d[:mc] if d is not None else None) for d in ws["derivs"]]
         fused = self.fused_tail
+        head = self.fused_head and mc >= 65536
         y = data.y[r0:r1]
         s = data.s[r0:r1] if data.s is not None else None
-        for l in range(L - 1 if fused else L):
+        for l in range(L - 1 if (fused or head) else L):
             a_in, a_out = acts[l], acts[l + 1]
             act = ACT_IDS[sp.acts[l]]
             nat.call_hip("shifu_gemm_nt", a_in.data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
@@ -603,6 +619,14 @@ class MLPTrainer:
                          int(bwd), wt[lh] if bwd else None, kp[L], dels[lh] if bwd else None, kp[lh],
                          ACT_IDS[sp.acts[lh - 1]] if bwd else 0, sp.hidden[lh - 1] if bwd else 0,
                          flat_spot(sp.acts[lh - 1]) if bwd else 0.0, mc, 0, st)
+        elif head:
+            # last hidden forward + output layer + loss + deltas + output wgrad in one GEMM epilogue
+            lh = L - 1
+            nat.call_hip("shifu_gemm_head", acts[lh].data_ptr(), kp[lh], wb[lh].data_ptr(), kp[lh], sp.hidden[lh],
+                         dels[L].data_ptr(), kp[L], mc, kp[L], kp[lh], ACT_IDS[sp.acts[lh]], sp.hidden[lh],
+                         wv[L].data_ptr(), y.data_ptr(), nat.ptr(s), gv[L].data_ptr(), self.err_acc.data_ptr(),
+                         kp[L], ACT_IDS[sp.out_act], LOSS_IDS[sp.loss], flat_spot(sp.out_act),
+                         flat_spot(sp.acts[lh]), st)
         else:
             # output layer + loss + last hidden delta + output wgrad
             nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], nat.ptr(ders[L]), kp[L],

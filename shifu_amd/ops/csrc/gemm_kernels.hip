@@ -542,12 +542,8 @@ __global__ __launch_bounds__(GP_T, 1) void gemm_nt_pipe_kernel(GemmArgs p) {
 // ---------------------------------------------------------------------------------------
 constexpr int G8_T = 512, G8_HALF = 16384, G8_BUF = 4 * G8_HALF;
 
-template <int EPI, int ACT>
-__global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntn = (p.N + 255) / 256;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (wg / ntn) * 256, n0 = (wg % ntn) * 256;
+// The 8-phase k-loop of one 256 x 256 output tile (m0, n0) into acc (see the schedule above).
+__device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   const int nk = p.K / 64;
@@ -573,7 +569,6 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_kernel(GemmArgs p) {
       __builtin_amdgcn_global_load_lds((const void*)(src + off[h][i] + k0), (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
   };
 
-  f32x4 acc[4][8];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -645,7 +640,170 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_kernel(GemmArgs p) {
   G8_BAR();
 #undef G8_MMA
 #undef G8_BAR
+}
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = (p.N + 255) / 256;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * 256, n0 = (wg % ntn) * 256;
+  f32x4 acc[4][8];
+  gemm8_mainloop(p, acc, m0, n0, smem);
   epilogue_256<EPI, ACT>(p, acc, m0, n0, smem);
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused network head: last hidden layer forward (8-phase GEMM, the whole hidden width N <= 256
+// in one tile) + output layer (n_out = 1) + loss + output delta + last-hidden delta + output
+// wgrad, all in the epilogue.  A block owns complete rows, so the output dot product, the loss
+// and D = delta * w_out * (f'(a) + flat) are row-local; the last hidden activations never go to
+// HBM (the unfused path writes them and mlp_output_kernel reads them back).
+// Same per-row semantics as mlp_output_kernel (SubGradient.java:241-248 for the squared loss).
+// ---------------------------------------------------------------------------------------
+struct HeadArgs {
+  const float* W;        // [KH] fp32 output weights (bias weight at kh_valid, zeros after)
+  const float* Y;        // [M] targets
+  const float* S;        // [M] significance (nullable -> 1)
+  float* GW;             // [KH] output-weight gradient (atomic)
+  double* err;           // [2] error sum, weight sum (atomic)
+  int KH, out_act, loss;
+  float flat_out, flat_hid;
+};
+constexpr int HEAD_LDS = 2 * G8_BUF + 12288;    // ring / staging + row partials, deltas, gW partials
+
+template <int ACT>
+__global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, HeadArgs h) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * 256;
+  f32x4 acc[4][8];
+  gemm8_mainloop(p, acc, m0, 0, smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  float* red = (float*)(smem + 2 * G8_BUF);          // [2 wr][4 wc][128] row partials of z_out
+  float* dl = red + 1024;                            // [256] output deltas
+  float* gred = dl + 256;                            // [2 wr][256] output-wgrad partials
+  double* ered = (double*)(gred + 512);              // [8 waves][2]
+  const int nv = p.n_valid;
+  // 1. hidden activations (bf16-rounded, as the unfused path stores them) + this lane's w_out
+  float w3[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = wc * 64 + i * 16 + (lane >> 4) * 4 + r;
+      w3[i][r] = n < h.KH ? h.W[n] : 0.f;
+    }
+  float zp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = wc * 64 + i * 16 + (lane >> 4) * 4 + r;
+        float a = n < nv ? act_fwd(ACT, acc[i][j][r]) : (n == nv ? 1.f : 0.f);
+        a = bf2f(f2bf(a));
+        acc[i][j][r] = a;
+        t += a * w3[i][r];
+      }
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    zp[j] = t;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[(wr * 4 + wc) * 128 + j * 16 + lane] = zp[j];
+  }
+  __syncthreads();
+  // 2. per row: output, loss, delta (threads 0..255 = the tile's rows)
+  double e_c = 0.0, e_w = 0.0;
+  if (tid < 256) {
+    const int rw = tid >> 7, rl = tid & 127;
+    const float z = red[(rw * 4 + 0) * 128 + rl] + red[(rw * 4 + 1) * 128 + rl] + red[(rw * 4 + 2) * 128 + rl] +
+                    red[(rw * 4 + 3) * 128 + rl];
+    const int m = m0 + tid;
+    float dlt = 0.f;
+    if (m < p.M) {
+      const float y = h.Y[m], sg = h.S ? h.S[m] : 1.f;
+      const float a = act_fwd(h.out_act, z), e = y - a;
+      if (h.loss == 1) {
+        dlt = e * sg;
+        const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
+        e_c = -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
+      } else if (h.loss == 2) {
+        dlt = (y < a ? 1.f : -1.f) * (act_deriv_out(h.out_act, a) + h.flat_out) * sg;
+        e_c = fabsf(e) * sg;
+      } else {
+        dlt = (act_deriv_pre(h.out_act, z) + h.flat_out) * e * sg;
+        e_c = (double)(e * sg) * (e * sg);
+      }
+      e_w = sg;
+    }
+    dl[tid] = dlt;
+  }
+  e_c = wave_sum_d(e_c);
+  e_w = wave_sum_d(e_w);
+  if (lane == 0) { ered[wid * 2] = e_c; ered[wid * 2 + 1] = e_w; }
+  __syncthreads();
+  if (tid == 0) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int w = 0; w < 8; ++w) { a0 += ered[w * 2]; a1 += ered[w * 2 + 1]; }
+    atomicAdd(h.err, a0);
+    atomicAdd(h.err + 1, a1);
+  }
+  // 3. last-hidden deltas (bf16, staged through LDS) and the output-wgrad partials
+  char* Cs = smem;                                   // [256][512 B], 16-B chunk ^ (row & 15)
+  float gw[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gw[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ml = wr * 128 + j * 16 + (lane & 15);
+    const float d = dl[ml];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = acc[i][j][r];
+        gw[i][r] += d * a;
+        o[r] = (nl + r < nv) ? d * w3[i][r] * (act_deriv_out(ACT, a) + h.flat_hid) : 0.f;
+      }
+      uint2 w;
+      w.x = pack_bf16x2(o[0], o[1]);
+      w.y = pack_bf16x2(o[2], o[3]);
+      const int c = nl >> 3, half = (nl >> 2) & 1;
+      *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = gw[i][r];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if ((lane & 15) == 0) gred[wr * 256 + wc * 64 + i * 16 + (lane >> 4) * 4 + r] = v;
+    }
+  __syncthreads();
+  if (tid < 256 && tid < h.KH) atomicAdd(h.GW + tid, gred[tid] + gred[256 + tid]);
+  const int c = tid & 31;
+#pragma unroll 4
+  for (int pass = 0; pass < 16; ++pass) {
+    const int ml = pass * 16 + (tid >> 5);
+    const int m = m0 + ml, n = c * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
+    if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
+    else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1240,6 +1398,30 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   else GEMM_L(EPI_STORE, 2);
 #undef GEMM_ACTS
 #undef GEMM_L
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// Fused head (see gemm_head_8ph_kernel): A [M, K] last-hidden inputs, B [NB, K] last-hidden
+// weights (bf16), D out [M, N] deltas of the last hidden layer (N = padded width <= 256).
+SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, int NB, void* D, long ldd,
+                              int M, int N, int K, int act, int n_valid, const float* W, const float* Y,
+                              const float* S, float* GW, double* err, int KH, int out_act, int loss,
+                              float flat_out, float flat_hid, hipStream_t stream) {
+  if (K % 64 || N % 8 || N > 256 || KH > 256 || KH < n_valid + 1 || lda % 8 || ldb % 8 || ldd % 8 ||
+      M <= 0 || NB <= 0 || NB > 256)
+    return -1;
+  if (!act_deriv_from_output(act) || act == 6 || out_act < 0 || out_act > 8) return -2;
+  GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)D, ldd, nullptr, 0, nullptr, 0, nullptr, 0,
+             M, N, K, NB, n_valid, act, 1, 0.f};
+  HeadArgs h{W, Y, S, GW, err, KH, out_act, loss, flat_out, flat_hid};
+  const int grid = (M + 255) / 256;
+#define HEAD_L(A_) hipLaunchKernelGGL((gemm_head_8ph_kernel<A_>), dim3(grid), dim3(G8_T), HEAD_LDS, stream, p, h)
+  switch (act) {
+    case 0: HEAD_L(0); break; case 1: HEAD_L(1); break; case 2: HEAD_L(2); break;
+    case 3: HEAD_L(3); break; case 4: HEAD_L(4); break; default: HEAD_L(7); break;
+  }
+#undef HEAD_L
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -99,3 +99,29 @@ def test_optimizer_kernel_matches_cpu():
             og.step(wg, gr.cuda(), 100)
         torch.cuda.synchronize()
         assert torch.allclose(wc, wg.cpu(), atol=1e-4, rtol=1e-4), rule
+
+
+@pytest.mark.parametrize("hidden,acts,loss", [([300, 200], ["sigmoid", "sigmoid"], "squared"),
+                                              ([96, 130], ["relu", "tanh"], "log"),
+                                              ([64], ["sigmoid"], "absolute")])
+def test_fused_head_matches_unfused(hidden, acts, loss, monkeypatch):
+    """gemm_head_8ph_kernel (last hidden forward + output layer + loss + deltas + output wgrad in
+    one epilogue) against the unfused GEMM + mlp_output_kernel path: same gradients / errors."""
+    spec = MLPSpec(n_in=120, hidden=hidden, acts=acts, n_out=1, loss=loss)
+    n = 70000 + 77                       # >= 65536 rows per chunk: the fused head is used
+    x, y, s = _mk(spec, n, seed=3)
+    monkeypatch.setenv("SHIFU_FUSED_HEAD", "1")
+    a = MLPTrainer(spec, device="cuda", seed=9, chunk_rows=1 << 20)
+    monkeypatch.setenv("SHIFU_FUSED_HEAD", "0")
+    b = MLPTrainer(spec, device="cuda", seed=9, chunk_rows=1 << 20)
+    assert a.fused_head and not b.fused_head
+    b.params.flat.copy_(a.params.flat)
+    da, db = a.prepare(x, y, s), b.prepare(x, y, s)
+    for t, d in ((a, da), (b, db)):
+        t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
+    torch.cuda.synchronize()
+    for va, vb in zip(a.params.views(a.grad), b.params.views(b.grad)):
+        r = (va - vb).norm() / vb.norm().clamp(min=1e-12)
+        assert r < 1e-2, float(r)
+    assert abs(float(a.err_acc[0]) - float(b.err_acc[0])) / float(b.err_acc[0]) < 1e-4
+    assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
