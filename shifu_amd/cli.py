@@ -37,6 +37,17 @@ USAGE = """Usage: shifu <command> [options]
 
 _log = get_logger("cli")
 
+# verbs whose every rank takes part (row-sharded data, collectives inside); the other
+# multi-GPU verbs run on rank 0 alone under dist.local_only()
+DP_VERBS = ("train", "stats")
+
+
+def torch_status(rc: int):
+    import torch
+    from .parallel import dist as _d
+    dev = f"cuda:{torch.cuda.current_device()}" if _d.info().backend == "nccl" else "cpu"
+    return torch.tensor([int(rc or 0)], dtype=torch.int64, device=dev)
+
 
 def _opt(args, name, default=None, has_value=False):
     if name in args:
@@ -64,6 +75,17 @@ def main(argv=None) -> int:
     t0, rc = time.time(), 1
     try:
         with step_timer(cmd):
+            info0 = dist.info()
+            if info0.world_size > 1 and cmd not in DP_VERBS:
+                # not data-parallel (yet): rank 0 runs the step alone, the others wait for it
+                rc = 0
+                if info0.rank == 0:
+                    with dist.local_only():
+                        rc = _dispatch(cmd, args)
+                st = torch_status(rc)
+                dist.all_reduce_(st, "max")
+                rc = int(st.item())
+                return rc
             rc = _dispatch(cmd, args)
             return rc
     except Exception as e:      # noqa: BLE001 - processors report errors and return non-zero

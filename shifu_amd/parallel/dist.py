@@ -44,10 +44,33 @@ class DistInfo:
 
 
 _INFO = DistInfo()
+_LOCAL = 0      # > 0 inside local_only(): this rank runs a step alone, collectives are no-ops
 
 
 def info() -> DistInfo:
+    if _LOCAL:
+        return DistInfo(0, 1, _INFO.local_rank, _INFO.backend)
     return _INFO
+
+
+class local_only:
+    """Run a block on this rank alone (the other ranks skip it): ``info()`` reports a world of
+    one and barrier / all_reduce / broadcast / all_gather do nothing, so a step that is not
+    data-parallel can run on rank 0 while the group waits at the next real collective."""
+
+    def __enter__(self):
+        global _LOCAL
+        _LOCAL += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _LOCAL
+        _LOCAL -= 1
+        return False
+
+
+def _active() -> bool:
+    return not _LOCAL and tdist.is_initialized() and tdist.get_world_size() > 1
 
 
 def init_from_env(backend: str | None = None, timeout_s: int = 1800) -> DistInfo:
@@ -87,7 +110,7 @@ def shutdown() -> None:
 
 
 def barrier() -> None:
-    if tdist.is_initialized() and tdist.get_world_size() > 1:
+    if _active():
         if tdist.get_backend() == "nccl":
             tdist.barrier(device_ids=[torch.cuda.current_device()])
         else:
@@ -95,7 +118,7 @@ def barrier() -> None:
 
 
 def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-    if not (tdist.is_initialized() and tdist.get_world_size() > 1):
+    if not _active():
         return t
     rop = {"sum": tdist.ReduceOp.SUM, "max": tdist.ReduceOp.MAX, "min": tdist.ReduceOp.MIN}[op]
     tdist.all_reduce(t, op=rop)
@@ -103,14 +126,14 @@ def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    if tdist.is_initialized() and tdist.get_world_size() > 1:
+    if _active():
         tdist.broadcast(t, src=src)
     return t
 
 
 def all_gather_cat(t: torch.Tensor) -> torch.Tensor:
     """Gather variable-length 1-D tensors from all ranks and concatenate (rank order)."""
-    if not (tdist.is_initialized() and tdist.get_world_size() > 1):
+    if not _active():
         return t
     n = torch.tensor([t.numel()], device=t.device, dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(tdist.get_world_size())]
@@ -155,7 +178,7 @@ class BucketedAllReducer:
     def launch_from(self, start_elem: int):
         """Launch every not-yet-launched bucket whose range lies entirely at >= start_elem
         (buckets are launched from the END of the buffer, matching a back-to-front backward)."""
-        if not (tdist.is_initialized() and tdist.get_world_size() > 1):
+        if not _active():
             return
         for bi in range(len(self.bounds) - 1 - self._launched, -1, -1):
             lo, hi = self.bounds[bi]
@@ -166,7 +189,7 @@ class BucketedAllReducer:
             self._launched += 1
 
     def wait(self):
-        if not (tdist.is_initialized() and tdist.get_world_size() > 1):
+        if not _active():
             return
         if self._launched < len(self.bounds):
             self.launch_from(0)

@@ -64,9 +64,13 @@ class ModelSet:
         return self
 
     def save_mc(self):
+        if not _writer():
+            return
         self.mc.save(self.pf.model_config)
 
     def save_cc(self, backup: bool = False):
+        if not _writer():
+            return
         if backup and os.path.exists(self.pf.column_config):
             dst = self.pf.ensure(self.pf.backup_column_config(time.strftime("%Y%m%d%H%M%S")))
             shutil.copyfile(self.pf.column_config, dst)
@@ -105,6 +109,24 @@ class ModelSet:
         strs = [c.name for c in columns if c.is_categorical()]
         return load_dataset(self.mc, data_conf or self.mc.dataSet, nums, strs, sample_rate, sample_neg_only,
                             seed, require_target, extra_filter)
+
+
+def _writer() -> bool:
+    """Only rank 0 writes model-set files (every rank holds the same replicated state)."""
+    from ..parallel import dist
+    return dist.info().rank == 0
+
+
+def shard_model_data(md):
+    """This rank's contiguous row range of ``md`` (all of it for a single process)."""
+    from dataclasses import replace
+    from ..parallel import dist
+    i = dist.info()
+    if i.world_size <= 1:
+        return md
+    lo, hi = md.n * i.rank // i.world_size, md.n * (i.rank + 1) // i.world_size
+    idx = np.arange(lo, hi)
+    return replace(md, table=md.table.take(idx), y=md.y[idx], w=md.w[idx], tag_index=md.tag_index[idx])
 
 
 def check_algorithm_params(mc):

@@ -27,6 +27,14 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
     ms = ModelSet(root).setup("STATS")
     mc = ms.mc
     cols = ms.stats_columns()
+    from ..parallel import dist
+    if (rebin or correlation or psi) and dist.info().world_size > 1:
+        # rebin / correlation / PSI: rank 0 alone (the others wait at the verb's final barrier)
+        if dist.info().rank == 0:
+            with dist.local_only():
+                return run_stats(root, correlation, psi, rebin, expected_bins, iv_keep_ratio,
+                                 bin_avg_score_only, device, min_inst_cnt, request_vars)
+        return 0
     if rebin:
         do_rebin(ms, expected_bins or 0, iv_keep_ratio, min_inst_cnt, request_vars)
         ms.save_cc()
@@ -38,8 +46,23 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
         md = ms.load_raw(cols, sample_rate=float(mc.stats.get("sampleRate", 1.0)),
                          sample_neg_only=bool(mc.stats.get("sampleNegOnly", False)))
         _log.info("stats: %d valid rows (%s)", md.n, md.counters.as_dict())
-        S.compute_column_stats(mc, ms.ccs, md, device=device, columns={c.name for c in cols})
+        from ..parallel import dist
+        if dist.info().world_size > 1:
+            # data parallel: this rank's rows, partials merged with collectives (algos/dist_stats.py)
+            from ..algos.dist_stats import compute_column_stats_dp
+            from .base import shard_model_data
+            compute_column_stats_dp(mc, ms.ccs, shard_model_data(md), device=device,
+                                    columns={c.name for c in cols})
+        else:
+            S.compute_column_stats(mc, ms.ccs, md, device=device, columns={c.name for c in cols})
         ms.save_cc(backup=True)
+    if dist.info().world_size > 1:
+        dist.barrier()
+        if mc.stats.get("psiColumnName"):      # PSI over the unit column: rank 0 alone
+            if dist.info().rank == 0:
+                with dist.local_only():
+                    return run_stats(root, False, True, False, device=device)
+        return 0
     if psi or mc.stats.get("psiColumnName"):
         unit = mc.stats.get("psiColumnName")
         if unit:
