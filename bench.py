@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Headline benchmark (BASELINE.json): rows/sec (whole node) of Shifu NN training,
-MLP 1000-500-200-1 binary classifier, bf16, 100M rows x 1000 cols per MI355X.
+MLP 1000-500-200-1 binary classifier, bf16, 125M rows x 1000 cols per MI355X (256 GB of rows
+resident in HBM; 8 GPUs = the metric's 1B-row x 1k-col table).
 
 One step = one full training iteration of the reference's NN algorithm
 (``J/core/dtrain/nn/AbstractNNWorker.java:521-588`` + ``NNMaster.java:207-319``): forward +
@@ -203,7 +204,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr"])
-    ap.add_argument("--rows", type=int, default=None, help="rows per GPU (default 100M on GPU)")
+    ap.add_argument("--rows", type=int, default=None,
+                    help="rows per GPU (default 125M on GPU: 256 GB of bf16 rows resident in one MI355X's "
+                         "288 GB HBM, so 8 GPUs hold the metric's 1B-row x 1k-col table)")
     ap.add_argument("--cols", type=int, default=1000)
     ap.add_argument("--chunk-rows", type=int, default=1 << 20)
     ap.add_argument("--propagation", default="R")
@@ -216,7 +219,8 @@ def main():
     if a.model == "varsel" and a.cols == 1000:
         a.cols = 10_000
     if a.rows is None:
-        a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000}.get(a.model, 100_000_000 if gpu else 20_000)
+        a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000,
+                  "gbdt": 100_000_000 if gpu else 20_000}.get(a.model, 125_000_000 if gpu else 20_000)
     if a.model == "gbdt":
         res = bench_gbdt(a, dev, info)
         out = res
