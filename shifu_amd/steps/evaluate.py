@@ -95,9 +95,20 @@ def score_eval(ms: ModelSet, ev, device=None, write: bool = True, nosort: bool =
     score_meta = _meta_names(ms, ev, "scoreMetaColumnNameFile")
     md = _load_eval_data(ms, ev, runner.raw_columns(), list(meta_cols) + list(score_meta))
     scale = float(ev.get("scoreScale", 1000) or 1000)
+    from ..parallel import dist
+    info = dist.info()
+    if info.world_size > 1:
+        # data parallel scoring: every rank scores its row range, rank 0 gathers (Eval.pig's
+        # distributed scoring + ORDER BY collapsed onto rank 0 for the sorted output / metrics)
+        from .base import shard_model_data
+        md = shard_model_data(md)
     res = runner.score(md.table, scale)
     target = ev.dataSet.get("targetColumnName") or mc.dataSet.get("targetColumnName")
     tags = md.table[target].strings() if target in md.table else np.array([""] * md.n)
+    if info.world_size > 1:
+        md, res, tags = _gather_scores(md, res, tags, list(meta_cols) + list(score_meta))
+        if info.rank != 0:
+            return md, res, tags, score_meta
     if write:
         d = ms.pf.eval_dir(ev.get("name"))
         os.makedirs(d, exist_ok=True)
@@ -126,6 +137,51 @@ def score_eval(ms: ModelSet, ev, device=None, write: bool = True, nosort: bool =
                 f.write("|".join(row) + "\n")
         _log.info("eval %s: scored %d rows with %d models -> %s", ev.get("name"), md.n, len(runner.models), path)
     return md, res, tags, score_meta
+
+
+class _GCol:
+    def __init__(self, v):
+        self.v = v
+
+    def strings(self):
+        return self.v
+
+    def numeric(self):
+        out = np.full(len(self.v), np.nan)
+        for i, x in enumerate(self.v):
+            try:
+                out[i] = float(x)
+            except (TypeError, ValueError):
+                pass
+        return out
+
+
+class _GTable(dict):
+    def __getitem__(self, k):
+        return _GCol(dict.__getitem__(self, k))
+
+
+class _GatheredEval:
+    def __init__(self, n, w, cols):
+        self.n, self.w, self.table = n, w, _GTable(cols)
+
+
+def _gather_scores(md, res, tags, meta_names):
+    """All ranks' (tags, weights, score arrays, meta columns) -> one row set on rank 0 (rank order
+    = row order).  Other ranks get their own shard back."""
+    import torch.distributed as tdist
+    from ..parallel import dist
+    payload = (np.asarray(tags), np.asarray(md.w), {k: np.asarray(v) for k, v in res.items()},
+               {m: (md.table[m].strings() if m in md.table else np.array([""] * md.n)) for m in meta_names})
+    parts = [None] * dist.info().world_size
+    tdist.all_gather_object(parts, payload)
+    if dist.info().rank != 0:
+        return md, res, tags
+    tags = np.concatenate([p[0] for p in parts])
+    w = np.concatenate([p[1] for p in parts])
+    res = {k: np.concatenate([p[2][k] for p in parts]) for k in parts[0][2]}
+    cols = {m: np.concatenate([p[3][m] for p in parts]) for m in meta_names}
+    return _GatheredEval(len(tags), w, cols), res, tags
 
 
 def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None):
@@ -198,6 +254,13 @@ def norm_eval(ms: ModelSet, ev, strict: bool = False):
 
 def run_eval(root: str = ".", action: str = "run", name: str | None = None, device=None, nosort: bool = False,
              strict: bool = False) -> int:
+    from ..parallel import dist
+    if action in ("new", "list", "delete", "norm") and dist.info().world_size > 1:
+        # model-set edits and the normalized eval export: rank 0 alone
+        if dist.info().rank == 0:
+            with dist.local_only():
+                return run_eval(root, action, name, device, nosort, strict)
+        return 0
     ms = ModelSet(root)
     if action == "new":
         new_eval(ms, name)
@@ -215,6 +278,8 @@ def run_eval(root: str = ".", action: str = "run", name: str | None = None, devi
             norm_eval(ms, ev, strict)
             continue
         md, res, tags, score_meta = score_eval(ms, ev, device, nosort=nosort)
-        if action in ("run", "perf", "confmat"):
-            perf_eval(ms, ev, md, res, tags, score_meta, device)
+        from ..parallel import dist
+        if action in ("run", "perf", "confmat") and dist.info().rank == 0:
+            with dist.local_only():
+                perf_eval(ms, ev, md, res, tags, score_meta, device)
     return 0

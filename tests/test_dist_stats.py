@@ -102,3 +102,27 @@ def test_cli_pipeline_two_ranks(tmp_path):
     assert os.path.exists(os.path.join(root, "models", "model0.nn"))
     perf = json.load(open(os.path.join(root, "evals", "Eval1", "EvalPerformance.json")))
     assert perf["areaUnderRoc"] > 0.7
+    # the 2-rank (sharded scoring + gather) eval equals a single-process eval of the same models
+    def score_rows():
+        p = os.path.join(root, "evals", "Eval1", "EvalScore")
+        p = os.path.join(p, "part-00000") if os.path.isdir(p) else p
+        return open(p).read()
+    two = score_rows()
+    cwd = os.getcwd()
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    try:
+        os.chdir(root)
+        from shifu_amd.cli import main
+        assert main(["eval"]) == 0
+    finally:
+        os.chdir(cwd)
+    one = score_rows()
+    r1 = [l.split("|") for l in one.strip().split("\n")]
+    r2 = [l.split("|") for l in two.strip().split("\n")]
+    assert r1[0] == r2[0] and len(r1) == len(r2)
+    j = r1[0].index("mean")
+    m1, m2 = np.array([float(r[j]) for r in r1[1:]]), np.array([float(r[j]) for r in r2[1:]])
+    np.testing.assert_allclose(m1, m2, atol=1e-3)        # fp32 GEMM blocking differs by batch shape
+    assert sorted(r[0] for r in r1[1:]) == sorted(r[0] for r in r2[1:])
+    perf1 = json.load(open(os.path.join(root, "evals", "Eval1", "EvalPerformance.json")))
+    assert abs(perf1["areaUnderRoc"] - perf["areaUnderRoc"]) < 1e-3
