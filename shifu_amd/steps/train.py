@@ -28,7 +28,7 @@ from ..formats import nn_format, tree_format
 from ..models import lr as lrmod
 from ..models.nn import MLPSpec, MLPTrainer
 from ..parallel import dist
-from ..runtime.fault import check_finite, maybe_fault
+from ..runtime.fault import IterationWatchdog, check_finite, iteration_limit, maybe_fault
 from ..utils.log import get_logger
 from ..utils.trace import trace_range
 from ..utils.metrics import MetricsWriter
@@ -460,7 +460,9 @@ class TrainStep:
         verr = float("nan")
         # MiniBatchs=k: iteration i trains on slice (i-1) mod k of the rows (SubGradient :326-340)
         mb = max(1, min(1000, int(_num(p.get("MiniBatchs"), 1))))
+        wd = IterationWatchdog(iteration_limit(3600.0), "NN epoch").__enter__()
         for ep in range(start + 1, epochs + 1):
+            wd.tick()
             with trace_range(f"nn.epoch{ep}"):
                 if mb > 1:
                     b = (ep - 1) % mb
@@ -485,6 +487,7 @@ class TrainStep:
             if es.update(ep, terr, verr):
                 _log.info("trainer %d early stop at epoch %d", tid, ep)
                 break
+        wd.__exit__(None, None, None)
         if best_w is not None and vdata is not None:
             tr.params.flat.copy_(best_w)      # NNOutput keeps the weights of the min validation error
             verr = best_v
@@ -609,7 +612,9 @@ class TrainStep:
             tt.load_state_dict(torch.load(ckpt, weights_only=False))    # our own checkpoint file
             _log.info("resumed trainer %d from checkpoint with %d trees", tid, len(tt.trees))
         interval = checkpoint_interval(p, max(1, tree_num // 10))   # DTOutput: tmp models every treeNum/10
+        wd = IterationWatchdog(iteration_limit(800.0), "tree").__enter__()
         while len(tt.trees) < tree_num:
+            wd.tick()
             tt.train(1, callback=cb)
             n = len(tt.trees)
             check_finite("training error", tt.train_errors[-1], n)
@@ -619,6 +624,7 @@ class TrainStep:
             maybe_fault(n, self.info.rank)
             if stop[0]:
                 break
+        wd.__exit__(None, None, None)
         if self.info.rank == 0:
             self._write_trees(tid, tt)
             if os.path.exists(ckpt):
