@@ -208,7 +208,7 @@ def main():
                     help="rows per GPU (default 125M on GPU: 256 GB of bf16 rows resident in one MI355X's "
                          "288 GB HBM, so 8 GPUs hold the metric's 1B-row x 1k-col table)")
     ap.add_argument("--cols", type=int, default=1000)
-    ap.add_argument("--chunk-rows", type=int, default=1 << 20)
+    ap.add_argument("--chunk-rows", type=int, default=1 << 21)   # 2M-row chunks: +1.6% vs 1M (profiles/r1d)
     ap.add_argument("--propagation", default="R")
     a = ap.parse_args()
 
