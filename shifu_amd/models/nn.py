@@ -504,7 +504,9 @@ class MLPTrainer:
         ws = {"rows": rows, "acts": [], "deltas": [], "derivs": []}
         for l in range(1, L + 1):
             ws["acts"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device))
-            ws["deltas"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device))
+            # rows rounded up to 64: layer-1 deltas may be stored transposed + m-blocked
+            # ([rows/64][kp][64], see gemm_kernels.hip EPI_DACT_T)
+            ws["deltas"].append(torch.empty(round_up(rows, 64), kp[l], dtype=torch.bfloat16, device=self.device))
             need_d = ACT_IDS[self.spec.acts[l - 1]] not in ACT_DERIV_FROM_OUTPUT
             ws["derivs"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device)
                                 if need_d else None)
@@ -601,6 +603,14 @@ class MLPTrainer:
         ders = [None] + [(d[:mc] if d is not None else None) for d in ws["derivs"]]
         fused = self.fused_tail
         head = self.fused_head and mc >= 65536
+        # layer-1 deltas transposed + m-blocked (EPI_DACT_T), consumed by the layer-0 wgrad with
+        # ds_read_b128 for its D operand (shifu_wgrad_tn_dt).  Opt-in (SHIFU_DGRAD_T=1): measured at
+        # the bench shape (1M rows) dgrad 0.83 -> 0.82 ms but wgrad 1.43 -> 1.68 ms
+        # (profiles/r1d/microbench_dgrad_t.json), although ds_read_b128 moves twice the LDS bytes
+        # per cycle of ds_read_b64_tr_b16 (profiles/r1d/microbench_lds_tr.txt).
+        dtr = (L >= 2 and not fused and os.environ.get("SHIFU_DGRAD_T", "0") == "1"
+               and ACT_IDS[sp.acts[0]] in ACT_DERIV_FROM_OUTPUT)
+        ldt = kp[1]                      # D^T rows (m-blocked layout: block stride kp[1] * 64)
         y = data.y[r0:r1]
         s = data.s[r0:r1] if data.s is not None else None
         for l in range(L - 1 if (fused or head) else L):
@@ -643,15 +653,20 @@ class MLPTrainer:
                 spl = max(1, min(mc // 256, 1024 // max(1, ntiles)))
             else:
                 spl = splits
-            nat.call_hip("shifu_wgrad_tn", dels[l + 1].data_ptr(), kp[l + 1], acts[l].data_ptr(), kp[l],
-                         gv[l].data_ptr(), kp[l], mc, sp.hidden[l], kp[l], spl, st)
+            if l == 0 and dtr:
+                nat.call_hip("shifu_wgrad_tn_dt", dels[1].data_ptr(), ldt, acts[0].data_ptr(), kp[0],
+                             gv[0].data_ptr(), kp[0], mc, sp.hidden[0], kp[0], spl, st)
+            else:
+                nat.call_hip("shifu_wgrad_tn", dels[l + 1].data_ptr(), kp[l + 1], acts[l].data_ptr(), kp[l],
+                             gv[l].data_ptr(), kp[l], mc, sp.hidden[l], kp[l], spl, st)
             if l >= 1 and not (fused and l == L - 1):
-                # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)
+                # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)   (layer 1: written transposed)
                 act = ACT_IDS[sp.acts[l - 1]]
+                t = l == 1 and dtr
                 nat.call_hip("shifu_gemm_nt", dels[l + 1].data_ptr(), kp[l + 1], wt[l].data_ptr(), kp[l + 1],
-                             kp[l], dels[l].data_ptr(), kp[l], None, 0, acts[l].data_ptr(), kp[l],
-                             nat.ptr(ders[l]), kp[l], mc, kp[l], kp[l + 1], 1, act, sp.hidden[l - 1], 0,
-                             flat_spot(sp.acts[l - 1]), st)
+                             kp[l], dels[l].data_ptr(), ldt if t else kp[l], None, 0, acts[l].data_ptr(), kp[l],
+                             nat.ptr(ders[l]), kp[l], mc, kp[l], kp[l + 1], 3 if t else 1, act, sp.hidden[l - 1],
+                             0, flat_spot(sp.acts[l - 1]), st)
 
     def _chunk_torch(self, data: TrainData, r0: int, r1: int):
         """fp32 CPU oracle with exactly the HIP path's structure."""

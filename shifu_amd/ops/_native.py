@@ -33,6 +33,7 @@ HIP_SIGNATURES = {
     # mlp_kernels.hip
     "shifu_gemm_nt": "plplipl" "plplpl" "iiiiiiif" "s",
     "shifu_wgrad_tn": "plplpl" "iiiis",
+    "shifu_wgrad_tn_dt": "plplpl" "iiiis",
     "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "s",
     "shifu_gemm_set_stages": "i",
     "shifu_gemm_set_big": "i",

@@ -38,7 +38,20 @@ __device__ __forceinline__ int swz_nt(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-enum Epi : int { EPI_ACT = 0, EPI_DACT = 1, EPI_STORE = 2 };
+// 256-B-row LDS images read with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group):
+// quad XOR swizzle so that the 8 rows read by one 32-lane half hit 8 distinct bank groups.
+__device__ __forceinline__ int tr_h(int m) { return (m & 3) | (((m >> 3) & 1) << 2); }
+// byte offset of 8-byte quad q (4 bf16: cols 4q..4q+3) of row m
+__device__ __forceinline__ int swz_tn_quad(int m, int q) { return m * 256 + ((q ^ (tr_h(m) << 2)) << 3); }
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+// gfx950 ds_read_b64_tr_b16 (compiler builtin: hipcc counts its lgkmcnt itself)
+__device__ __forceinline__ s16x4 ds_read_tr16_b64(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+}
+
+enum Epi : int { EPI_ACT = 0, EPI_DACT = 1, EPI_STORE = 2, EPI_DACT_T = 3 };
 
 struct GemmArgs {
   const bf16_t* A; long lda;   // [M, K] row-major
@@ -122,7 +135,9 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = EPI == EPI_DACT_T   // transposed accumulator: lane = 4 consecutive rows of one column
+              ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[i][j], 0, 0, 0)
+              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
     }
     if constexpr (STAGES == 1) __syncthreads();     // every wave is done reading the buffer
     if (kt + 1 < nk) swrite(STAGES == 2 ? (buf ^ 1) : 0);
@@ -132,6 +147,67 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
   // Epilogue.  acc[i][j] holds D[n][m]: m = lane&15 (+16j), n = 4*(lane>>4) + r (+16i):
   // each lane owns 4 consecutive output columns of one row.
   constexpr bool dfo = act_deriv_from_output(ACT);
+  if constexpr (EPI == EPI_DACT_T) {
+    // dgrad written TRANSPOSED (C = D^T [N][ldc], rows = output columns): the swapped MFMA left
+    // lane l holding rows m = 4(l>>4) + r (+16j) of column n = l & 15 (+16i), i.e. 4 consecutive
+    // entries of one D^T row.  f'(H) for those 4 rows comes from the H tile staged in LDS and
+    // read back with ds_read_b64_tr_b16 (4 rows x 1 column per lane), then the D^T tile is staged
+    // [n][m] and leaves as 16-B row segments.  The wgrad that consumes D^T then reads its
+    // operand with ds_read_b128 instead of the half-rate transposed read.
+    char* Hs = smem;                                   // [128 m][256 B], TN quad swizzle (tr reads)
+    char* Ts = smem + 32768;                           // [128 n][256 B], 16-B chunk ^ (row & 15)
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int ml = pass * 16 + (tid >> 4), c = tid & 15;
+      const int m = min(m0 + ml, p.M - 1), n = min(n0 + c * 8, p.N - 8);     // clamped, no branch
+      *(uint4*)(Hs + swz_tn_quad(ml, c * 2)) = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+    }
+    __syncthreads();
+    const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nl = wc * 64 + i * 16;                 // this (i) block's first column
+      const int n = n0 + nl + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int mb = wr * 64 + j * 16 + 4 * g;       // the lane's 4 rows start here
+        const s16x4 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)(Hs + swz_tn_quad(wr * 64 + j * 16 + 4 * g + tq, nl / 4 + tp)));
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = act_deriv_out(ACT, bf2f((bf16_t)hv[r])) + p.flat;
+          o[r] = n < p.n_valid ? acc[i][j][r] * d : 0.f;
+        }
+        uint2 w;
+        w.x = pack_bf16x2(o[0], o[1]);
+        w.y = pack_bf16x2(o[2], o[3]);
+        const int trow = nl + (lane & 15), c = mb >> 3, half = (mb >> 2) & 1;
+        *(uint2*)(Ts + trow * 256 + ((c ^ (trow & 15)) << 4) + half * 8) = w;
+      }
+    }
+    __syncthreads();
+    // D^T is m-blocked: element (n, m) at (m / 64) * (ldc * 64) + n * 64 + m % 64 (ldc = number of
+    // D^T rows), so a 64-row block of every column is one contiguous 128-B run and a wgrad step
+    // reads one contiguous [n][64] slab (a plain [N][M] transpose puts every row ~M * 2 B apart:
+    // one TLB page per row)
+    const int c = tid & 15;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int nl = pass * 16 + (tid >> 4);
+      const int n = n0 + nl, m = m0 + c * 8;
+      if (n >= p.N || m >= p.M) continue;
+      const uint4 v = *(const uint4*)(Ts + nl * 256 + ((c ^ (nl & 15)) << 4));
+      bf16_t* dst = p.C + (size_t)(m >> 6) * ((size_t)p.ldc * 64) + (size_t)n * 64 + (m & 63);
+      if (m + 8 <= p.M) {
+        *(uint4*)dst = v;
+      } else {
+        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+        for (int q = 0; q < 8 && m + q < p.M; ++q) dst[q] = (bf16_t)((vv[q >> 1] >> ((q & 1) * 16)) & 0xffff);
+      }
+    }
+    return;
+  }
   if constexpr ((EPI == EPI_ACT || EPI == EPI_DACT) && dfo || EPI == EPI_STORE) {
     // Staged epilogue: phase 1 packs the tile (bf16) into LDS with a 16-B chunk XOR swizzle,
     // phase 2 writes whole 256-B row segments with 16-B stores (and, for dgrad, reads the
@@ -1002,16 +1078,6 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_persist_kernel(GemmArgs p
 constexpr int WT_BN = 128, WT_BK = 128, WT_BM = 64;   // n-tile, k-tile, rows per step
 constexpr int WT_TILE = WT_BM * 128 * 2;              // 16 KiB
 
-__device__ __forceinline__ int tr_h(int m) { return (m & 3) | (((m >> 3) & 1) << 2); }
-// byte offset of 8-byte quad q (4 bf16: cols 4q..4q+3) of row m
-__device__ __forceinline__ int swz_tn_quad(int m, int q) { return m * 256 + ((q ^ (tr_h(m) << 2)) << 3); }
-
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-// gfx950 ds_read_b64_tr_b16 (compiler builtin: hipcc counts its lgkmcnt itself)
-__device__ __forceinline__ s16x4 ds_read_tr16_b64(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
-}
 
 struct WgradArgs {
   const bf16_t* D; long ldd;   // [M, Nd] deltas
@@ -1021,7 +1087,10 @@ struct WgradArgs {
   int nsplit, interleave;      // interleave: split s takes the 64-row steps s, s+nsplit, ...
 };
 
-template <int STAGES>
+// DT: D arrives transposed (D^T [Nd][ldd], ldd >= M) - the A operand is then an NT image
+// [128 n][64 m] read with ds_read_b128 (full rate) instead of ds_read_b64_tr_b16 (measured at
+// less than half the LDS bandwidth on gfx950: tools/microbench_lds_tr.hip).
+template <int STAGES, bool DT = false>
 __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles_n = (p.Nv + WT_BN - 1) / WT_BN, tiles_k = p.Kx / WT_BK;
@@ -1045,8 +1114,27 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
       const int idx = tid + i * NTHR, row = idx >> 4, ch = idx & 15;
       const int gm = mb + row;
       const bool ok = gm < mend;
-      const int gn = n0 + ch * 8;
-      rd[i] = (ok && gn < p.Nv) ? *(const uint4*)(p.D + (size_t)gm * p.ldd + gn) : make_uint4(0, 0, 0, 0);
+      if constexpr (DT) {
+        // D^T m-blocked (see EPI_DACT_T): (n, m) at (m / 64) * (ldd * 64) + n * 64 + m % 64
+        // unconditional 16-B load (the buffer holds whole 64-row blocks and ldd >= Nv rows, so the
+        // address is in bounds) + register masking: a branch around the load would make hipcc
+        // wait vmcnt(0) per load and serialize the prefetch
+        const int dn = n0 + (idx >> 3), dm = mb + (idx & 7) * 8;      // D^T row n, 8 rows m
+        const int dnc = min(dn, (int)p.ldd - 1);
+        const uint4 v = *(const uint4*)(p.D + (size_t)(dm >> 6) * ((size_t)p.ldd * 64) + (size_t)dnc * 64 + (dm & 63));
+        const int valid = dn < p.Nv ? min(8, max(0, mend - dm)) : 0;               // leading valid rows
+        const uint32_t lo = valid >= 8 ? 0xffffffffu : 0u;
+        uint32_t q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t keep = (2 * e + 2 <= valid) ? 0xffffffffu : ((2 * e + 1 <= valid) ? 0x0000ffffu : 0u);
+          q[e] &= (keep | lo);
+        }
+        rd[i] = make_uint4(q[0], q[1], q[2], q[3]);
+      } else {
+        const int gn = n0 + ch * 8;
+        rd[i] = (ok && gn < p.Nv) ? *(const uint4*)(p.D + (size_t)gm * p.ldd + gn) : make_uint4(0, 0, 0, 0);
+      }
       rx[i] = ok ? *(const uint4*)(p.X + (size_t)gm * p.ldx + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
     }
   };
@@ -1056,7 +1144,8 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + i * NTHR, row = idx >> 4, ch = idx & 15;
-      *(uint4*)(Ds + swz_tn_quad(row, ch * 2)) = rd[i];
+      if constexpr (DT) *(uint4*)(Ds + swz_nt(idx >> 3, idx & 7)) = rd[i];
+      else *(uint4*)(Ds + swz_tn_quad(row, ch * 2)) = rd[i];
       *(uint4*)(Xs + swz_tn_quad(row, ch * 2)) = rx[i];
     }
   };
@@ -1085,10 +1174,14 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
       const int mr = s * 32 + 8 * g + tq;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int q = (wn * 64 + i * 16) / 4 + tp;
-        const s16x4 lo = ds_read_tr16_b64(Ds + swz_tn_quad(mr, q));
-        const s16x4 hi = ds_read_tr16_b64(Ds + swz_tn_quad(mr + 4, q));
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if constexpr (DT) {
+          af[i] = *(const bf16x8*)(Ds + swz_nt(wn * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4)));
+        } else {
+          const int q = (wn * 64 + i * 16) / 4 + tp;
+          const s16x4 lo = ds_read_tr16_b64(Ds + swz_tn_quad(mr, q));
+          const s16x4 hi = ds_read_tr16_b64(Ds + swz_tn_quad(mr + 4, q));
+          af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1318,11 +1411,23 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
              (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat};
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = 2 * g_stages * TILE_BYTES;
-  if (act < 0 || act > 8 || epi < 0 || epi > 2) return -2;
+  if (act < 0 || act > 8 || epi < 0 || epi > 3) return -2;
   if (epi == EPI_ACT && !act_deriv_from_output(act) && C2 == nullptr) return -3;
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;
   const bool dfo_act = act_deriv_from_output(act);
+  if (epi == EPI_DACT_T) {              // transposed dgrad (C = D^T [N][ldc]), 128 x 128 kernel
+    if (!dfo_act || H == nullptr || ldh % 8) return -3;
+#define GEMMT_L(A_) hipLaunchKernelGGL((gemm_nt_kernel<EPI_DACT_T, A_, 1>), dim3(grid), dim3(NTHR), 65536, stream, p)
+    switch (act) {
+      case 0: GEMMT_L(0); break; case 1: GEMMT_L(1); break; case 2: GEMMT_L(2); break;
+      case 3: GEMMT_L(3); break; case 4: GEMMT_L(4); break; case 6: GEMMT_L(6); break;
+      default: GEMMT_L(7); break;
+    }
+#undef GEMMT_L
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
   const bool auto8 = g_big == 0 && M >= 65536 && N >= 512 && K >= 512;
   if ((g_big == 3 || auto8) && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
     const int grid8 = ((M + 255) / 256) * ((N + 255) / 256);
@@ -1422,6 +1527,23 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
     case 3: HEAD_L(3); break; case 4: HEAD_L(4); break; default: HEAD_L(7); break;
   }
 #undef HEAD_L
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// wgrad with the deltas given transposed and m-blocked (ldd = number of D^T rows >= Nv, element
+// (n, m) at (m / 64) * ldd * 64 + n * 64 + m % 64; see EPI_DACT_T):
+// G[n][k] += sum_m D^T[n][m] X[m][k] with the D operand read at full LDS rate.
+SHIFU_API int shifu_wgrad_tn_dt(const void* DT, long ldd, const void* X, long ldx, float* G, long ldg,
+                                int M, int Nv, int Kx, int splits, hipStream_t stream) {
+  if (Kx % WT_BK || ldx % 8 || M <= 0 || Nv <= 0 || ldd < Nv) return -1;
+  if (splits < 1) splits = 1;
+  int rps = (M + splits - 1) / splits;
+  rps = ((rps + WT_BM - 1) / WT_BM) * WT_BM;
+  splits = (M + rps - 1) / rps;
+  WgradArgs p{(const bf16_t*)DT, ldd, (const bf16_t*)X, ldx, G, ldg, M, Nv, Kx, rps, splits, g_wg_interleave};
+  const int ntiles = ((Nv + WT_BN - 1) / WT_BN) * (Kx / WT_BK);
+  hipLaunchKernelGGL((wgrad_tn_kernel<1, true>), dim3(ntiles * splits), dim3(NTHR), 2 * WT_TILE, stream, p);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

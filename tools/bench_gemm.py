@@ -131,7 +131,18 @@ def main():
                     nat.call_hip("shifu_mlp_set_out_waves", val)
                     ms = timeit(output, a.iters)
                     res.setdefault(f"output_w{val}", []).append(round(ms, 4))
-    todo = (("output", output, 0),
+    nblk = (M + 63) // 64
+    D1T = torch.empty(nblk * 512 * 64, device=dev, dtype=bf)
+
+    def dgrad_t():
+        nat.call_hip("shifu_gemm_nt", D2, 256, W2t, 256, 512, D1T, 512, None, 0, H1, 512, None, 0, M, 512, 256, 3,
+                     tanh, 500, 0, 0.0, st)
+
+    def wgrad1_dt():
+        nat.call_hip("shifu_wgrad_tn_dt", D1T, 512, X, 1024, G1, 1024, M, 500, 1024, spl(500, 1024), st)
+
+    todo = (("dgrad1_t", dgrad_t, 2 * M * 512 * 256), ("wgrad1_dt", wgrad1_dt, 2 * M * 512 * 1024),
+            ("output", output, 0),
                             ("pure_gemm", pure, 2 * M * 512 * 1024), ("torch_mm", blaslt, 2 * M * 512 * 1024),
                             ("fwd1", fwd1, 2 * M * 512 * 1024), ("fwd2", fwd2, 2 * M * 256 * 512),
                             ("dgrad1", dgrad, 2 * M * 512 * 256), ("wgrad1", wgrad1, 2 * M * 512 * 1024),
