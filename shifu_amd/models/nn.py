@@ -605,7 +605,7 @@ class MLPTrainer:
         head = self.fused_head and mc >= 65536
         # layer-1 deltas transposed + m-blocked (EPI_DACT_T), consumed by the layer-0 wgrad with
         # ds_read_b128 for its D operand (shifu_wgrad_tn_dt).  Opt-in (SHIFU_DGRAD_T=1): measured at
-        # the bench shape (1M rows) dgrad 0.83 -> 0.82 ms but wgrad 1.43 -> 1.68 ms
+        # the bench shape (1M rows) dgrad 0.83 -> 0.82 ms but wgrad 1.46 -> 1.57 ms
         # (profiles/r1d/microbench_dgrad_t.json), although ds_read_b128 moves twice the LDS bytes
         # per cycle of ds_read_b64_tr_b16 (profiles/r1d/microbench_lds_tr.txt).
         dtr = (L >= 2 and not fused and os.environ.get("SHIFU_DGRAD_T", "0") == "1"

@@ -1108,6 +1108,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
   const int wn = wid >> 1, wk = wid & 1;
 
   uint4 rd[4], rx[4];
+  int dvalid[4] = {8, 8, 8, 8};
   auto gload = [&](int mb) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1119,18 +1120,12 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
         // unconditional 16-B load (the buffer holds whole 64-row blocks and ldd >= Nv rows, so the
         // address is in bounds) + register masking: a branch around the load would make hipcc
         // wait vmcnt(0) per load and serialize the prefetch
+        // (the mask is applied at LDS-write time: touching the loaded registers here would make
+        // hipcc wait for the prefetch right away)
         const int dn = n0 + (idx >> 3), dm = mb + (idx & 7) * 8;      // D^T row n, 8 rows m
         const int dnc = min(dn, (int)p.ldd - 1);
-        const uint4 v = *(const uint4*)(p.D + (size_t)(dm >> 6) * ((size_t)p.ldd * 64) + (size_t)dnc * 64 + (dm & 63));
-        const int valid = dn < p.Nv ? min(8, max(0, mend - dm)) : 0;               // leading valid rows
-        const uint32_t lo = valid >= 8 ? 0xffffffffu : 0u;
-        uint32_t q[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t keep = (2 * e + 2 <= valid) ? 0xffffffffu : ((2 * e + 1 <= valid) ? 0x0000ffffu : 0u);
-          q[e] &= (keep | lo);
-        }
-        rd[i] = make_uint4(q[0], q[1], q[2], q[3]);
+        rd[i] = *(const uint4*)(p.D + (size_t)(dm >> 6) * ((size_t)p.ldd * 64) + (size_t)dnc * 64 + (dm & 63));
+        dvalid[i] = dn < p.Nv ? min(8, max(0, mend - dm)) : 0;                      // leading valid rows
       } else {
         const int gn = n0 + ch * 8;
         rd[i] = (ok && gn < p.Nv) ? *(const uint4*)(p.D + (size_t)gm * p.ldd + gn) : make_uint4(0, 0, 0, 0);
@@ -1144,8 +1139,17 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + i * NTHR, row = idx >> 4, ch = idx & 15;
-      if constexpr (DT) *(uint4*)(Ds + swz_nt(idx >> 3, idx & 7)) = rd[i];
-      else *(uint4*)(Ds + swz_tn_quad(row, ch * 2)) = rd[i];
+      if constexpr (DT) {
+        uint32_t q[4] = {rd[i].x, rd[i].y, rd[i].z, rd[i].w};
+        if (dvalid[i] < 8) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            q[e] &= (2 * e + 2 <= dvalid[i]) ? 0xffffffffu : ((2 * e + 1 <= dvalid[i]) ? 0x0000ffffu : 0u);
+        }
+        *(uint4*)(Ds + swz_nt(idx >> 3, idx & 7)) = make_uint4(q[0], q[1], q[2], q[3]);
+      } else {
+        *(uint4*)(Ds + swz_tn_quad(row, ch * 2)) = rd[i];
+      }
       *(uint4*)(Xs + swz_tn_quad(row, ch * 2)) = rx[i];
     }
   };
