@@ -125,6 +125,17 @@ def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     return t
 
 
+def all_reduce_np(a, op: str = "sum"):
+    """All-reduce a host (numpy) array, staged through HBM when the backend is RCCL."""
+    if not _active():
+        return a
+    import numpy as np
+    dev = torch.device("cuda", torch.cuda.current_device()) if tdist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    all_reduce_(t, op)
+    return t.cpu().numpy()
+
+
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if _active():
         tdist.broadcast(t, src=src)

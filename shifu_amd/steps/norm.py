@@ -25,34 +25,68 @@ _log = get_logger("steps.norm")
 TREE_ALGS = ("GBT", "RF", "DT")
 
 
+def _write_shared(path: str, arrays: dict, meta: dict, lo: int, hi: int, n: int):
+    """Data-parallel cache write: rank 0 creates the full-size .npy files, every rank writes its
+    row range [lo, hi) in place (np.lib.format memmaps), rank 0 writes meta.json last."""
+    import json
+    import os
+    import shutil
+    from ..parallel import dist
+    if dist.info().rank == 0:
+        if os.path.isdir(path):
+            shutil.rmtree(path)
+        os.makedirs(path, exist_ok=True)
+        for k, v in arrays.items():
+            np.lib.format.open_memmap(os.path.join(path, f"{k}.npy"), mode="w+", dtype=v.dtype,
+                                      shape=(n,) + tuple(v.shape[1:])).flush()
+    dist.barrier()
+    for k, v in arrays.items():
+        mm = np.load(os.path.join(path, f"{k}.npy"), mmap_mode="r+")
+        mm[lo:hi] = v
+        mm.flush()
+        del mm
+    dist.barrier()
+    if dist.info().rank == 0:
+        with open(os.path.join(path, "meta.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+    dist.barrier()
+
+
 def _norm_one(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_only, shuffle, seed, is_tree):
+    """Normalize one data set into the NormalizedData / CleanedData caches.  Under more than one
+    rank every rank normalizes the output row range [n*r/R, n*(r+1)/R) (rows of the global
+    shuffle permutation when shuffling) and writes it in place: the caches are identical to the
+    single-process ones."""
+    from ..parallel import dist
     mc = ms.mc
     md = ms.load_raw(cols, data_conf, sample_rate, neg_only, seed)
-    perm = np.random.default_rng(seed).permutation(md.n) if shuffle else None
+    n = int(md.n)
+    perm = np.random.default_rng(seed).permutation(n) if shuffle else None
+    info = dist.info()
+    lo, hi = n * info.rank // info.world_size, n * (info.rank + 1) // info.world_size
+    if info.world_size > 1 or perm is not None:
+        idx = perm[lo:hi] if perm is not None else np.arange(lo, hi)
+        from dataclasses import replace
+        md = replace(md, table=md.table.take(idx), y=md.y[idx], w=md.w[idx], tag_index=md.tag_index[idx])
     y, w = md.y.astype(np.float32), md.w.astype(np.float32)
-    if perm is not None:
-        y, w = y[perm], w[perm]
-    meta = {"n": int(md.n), "columns": [c.name for c in cols], "column_nums": [c.num for c in cols],
+    meta = {"n": n, "columns": [c.name for c in cols], "column_nums": [c.num for c in cols],
             "counters": md.counters.as_dict(), "is_binary": mc.is_binary(), "tags": mc.flatten_tags(),
             "shuffled": bool(shuffle)}
     gpu = is_gpu_available()
+    save = (lambda p_, a_, m_: _write_shared(p_, a_, m_, lo, hi, n)) if info.world_size > 1 else save_dataset
     if is_tree:
         r = N.tree_bin_codes_gpu(ms.ccs, md.table, cols) if gpu else None
         C, nb, is_cat = r if r is not None else N.tree_bin_codes(ms.ccs, md.table, cols)
         dt = np.uint8 if (nb.max(initial=1) <= 256) else np.int16
         C = C.astype(dt)
-        if perm is not None:
-            C = C[perm]
         meta.update(nbins=nb.tolist(), is_cat=is_cat.tolist())
-        save_dataset(out_tree, {"codes": C, "y": y, "w": w}, meta)
-        _log.info("CleanedData: %s rows x %s cols -> %s", *C.shape, out_tree)
+        save(out_tree, {"codes": C, "y": y, "w": w}, meta)
+        _log.info("CleanedData: %s rows x %s cols -> %s", n, C.shape[1], out_tree)
     X, names, nums = (N.normalize_table_gpu if gpu else N.normalize_table)(mc, ms.ccs, md.table, columns=cols)
-    if perm is not None:
-        X = X[perm]
     meta.update(norm_type=mc.norm_type, input_names=names, input_nums=nums)
-    save_dataset(out_x, {"X": X, "y": y, "w": w}, meta)
-    _log.info("NormalizedData: %s rows x %s inputs (%s) -> %s", X.shape[0], X.shape[1], mc.norm_type, out_x)
-    return md.n
+    save(out_x, {"X": X, "y": y, "w": w}, meta)
+    _log.info("NormalizedData: %s rows x %s inputs (%s) -> %s", n, X.shape[1], mc.norm_type, out_x)
+    return n
 
 
 def run_norm(root: str = ".", shuffle: bool = False, seed: int = 0) -> int:

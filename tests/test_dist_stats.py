@@ -126,3 +126,29 @@ def test_cli_pipeline_two_ranks(tmp_path):
     assert sorted(r[0] for r in r1[1:]) == sorted(r[0] for r in r2[1:])
     perf1 = json.load(open(os.path.join(root, "evals", "Eval1", "EvalPerformance.json")))
     assert abs(perf1["areaUnderRoc"] - perf["areaUnderRoc"]) < 1e-3
+
+
+@pytest.mark.parametrize("alg,shuffle", [("NN", False), ("NN", True), ("GBT", False)])
+def test_norm_two_ranks_match_single(tmp_path, alg, shuffle):
+    """Data-parallel norm (each rank normalizes its output row range and writes it in place into
+    the shared .npy caches) == single-process norm, with and without -shuffle."""
+    from shifu_amd.steps.base import load_dataset_cache
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.norm import run_norm
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    a = make_model_set(str(tmp_path), "a", alg, n_rows=1203, n_num=5, n_cat=2)
+    run_init(a)
+    run_stats(a)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    run_norm(a, shuffle=shuffle)
+    verb = "norm -shuffle" if shuffle else "norm"
+    mp.start_processes(_rank_cli, args=(2, _port(), b, verb), nprocs=2, join=True, start_method="spawn")
+    sub = "CleanedData" if alg == "GBT" else "NormalizedData"
+    ma, xa = load_dataset_cache(os.path.join(a, "tmp", sub), mmap=False)
+    mb, xb = load_dataset_cache(os.path.join(b, "tmp", sub), mmap=False)
+    assert ma["n"] == mb["n"] and set(xa) == set(xb)
+    for k in xa:
+        np.testing.assert_array_equal(xa[k], xb[k], err_msg=k)
