@@ -235,6 +235,11 @@ def sensitivity(network, X: np.ndarray, y=None, w=None, device=None, feat_chunk:
             s_abs[f0:f1] += d.abs().sum(0)
             s_sq[f0:f1] += (d * d).sum(0)
         n += xb.shape[0]
+    from ..parallel import dist
+    if dist.info().world_size > 1:        # row-sharded SE: one all-reduce of the per-input sums
+        t = torch.cat([s_abs, s_sq, torch.tensor([float(n)], dtype=torch.float64, device=s_abs.device)])
+        dist.all_reduce_(t)
+        s_abs, s_sq, n = t[:F], t[F:2 * F], int(t[-1].item())
     mean = (s_abs / max(n, 1)).cpu().numpy()
     rms = torch.sqrt(s_sq / max(n, 1)).cpu().numpy()
     var = (s_sq / max(n, 1)).cpu().numpy() - mean ** 2

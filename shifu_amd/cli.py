@@ -39,7 +39,7 @@ _log = get_logger("cli")
 
 # verbs whose every rank takes part (row-sharded data, collectives inside); the other
 # multi-GPU verbs run on rank 0 alone under dist.local_only()
-DP_VERBS = ("train", "stats", "eval", "norm", "normalize", "transform")
+DP_VERBS = ("train", "stats", "eval", "norm", "normalize", "transform", "varsel", "posttrain")
 
 
 def torch_status(rc: int):

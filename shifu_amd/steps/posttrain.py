@@ -13,9 +13,10 @@ import numpy as np
 
 from ..algos.normalize import _bin_num
 from ..formats import tree_format
+from ..parallel import dist
 from ..scoring.model_runner import ModelRunner, list_model_files
 from ..utils.log import get_logger
-from .base import ModelSet
+from .base import ModelSet, _writer, shard_model_data
 
 _log = get_logger("steps.posttrain")
 
@@ -27,19 +28,30 @@ def run_posttrain(root: str = ".", device=None) -> int:
     cols = runner.selected
     names = runner.raw_columns()
     byname = {c.name: c for c in ms.ccs}
-    md = ms.load_raw([byname[n] for n in names if n in byname])
+    # data parallel: every rank scores its row shard; the per-(column, bin) score sums and counts
+    # are all-reduced once (the PostTrainMapper -> reducer shuffle), then every rank holds them
+    md = shard_model_data(ms.load_raw([byname[n] for n in names if n in byname]))
     res = runner.score(md.table, 1000.0)
     score = np.asarray(res["mean"] if "mean" in res else res["class_scores"].max(1))
-    for c in cols:
-        if c.name not in md.table:
-            continue
+    used = [c for c in cols if c.name in md.table]
+    parts = []
+    for c in used:
         b = _bin_num(c, md.table[c.name])
         nb = c.n_bins()                        # incl. the missing bin (last)
         b = np.where(b < 0, nb - 1, np.minimum(b, nb - 1))
-        s = np.bincount(b, weights=score, minlength=nb)
-        n = np.bincount(b, minlength=nb)
+        parts.append(np.stack([np.bincount(b, weights=score, minlength=nb),
+                               np.bincount(b, minlength=nb).astype(np.float64)]))
+    if used and dist.info().world_size > 1:
+        flat = dist.all_reduce_np(np.concatenate([p.reshape(-1) for p in parts]))
+        off = 0
+        for i, p in enumerate(parts):
+            parts[i] = flat[off:off + p.size].reshape(p.shape)
+            off += p.size
+    for c, (s, n) in zip(used, parts):
         c.binning["binAvgScore"] = [int(round(v)) for v in np.where(n > 0, s / np.maximum(n, 1), 0.0)]
     ms.save_cc()
+    if not _writer():
+        return 0
     # feature importance for tree models
     fi_all = {}
     for p in list_model_files(ms.pf.models_dir):

@@ -24,7 +24,8 @@ from ..config.column_config import has_candidates
 from ..formats.nn_format import NNNetwork
 from ..models.nn import MLPSpec, MLPTrainer
 from ..utils.log import get_logger
-from .base import ModelSet
+from ..parallel import dist
+from .base import ModelSet, _writer, shard_model_data
 
 _log = get_logger("steps.varsel")
 
@@ -35,6 +36,8 @@ def _good(ms):
 
 
 def _history_append(ms, changes, reason):
+    if not _writer():
+        return
     os.makedirs(ms.pf.varsel_dir, exist_ok=True)
     with open(ms.pf.varsel_history, "a") as f:
         for c, old, new in changes:
@@ -44,7 +47,7 @@ def _history_append(ms, changes, reason):
 def _train_quick_nn(ms, cols, epochs, device=None, seed=0):
     """Train the NN used for sensitivity analysis on the candidate columns; returns (net, X)."""
     mc = ms.mc
-    md = ms.load_raw(cols)
+    md = shard_model_data(ms.load_raw(cols))     # data parallel: each rank its row range
     X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
     p = mc.train.get("params") or {}
     hidden = [int(h) for h in (p.get("NumHiddenNodes") or [50])][: int(p.get("NumHiddenLayers", 1) or 1)]
@@ -83,7 +86,7 @@ def select_by_fi(ms, device=None):
     from ..formats.tree_format import heap_tree_to_record
     mc = ms.mc
     cols = _good(ms)
-    md = ms.load_raw(cols)
+    md = shard_model_data(ms.load_raw(cols))     # histograms all-reduced inside TreeTrainer
     C, nb, is_cat = N.tree_bin_codes(ms.ccs, md.table, cols)
     from ..utils.device import default_device
     dev = torch.device(device) if device is not None else default_device()
@@ -165,7 +168,9 @@ def recover_auto(ms):
         if c is not None and c.final_select == new:
             c.final_select = old
             n += 1
-    os.remove(ms.pf.varsel_history)
+    dist.barrier()                      # every rank has read the history before rank 0 drops it
+    if _writer():
+        os.remove(ms.pf.varsel_history)
     return n
 
 
@@ -178,7 +183,7 @@ def run_varsel(root: str = ".", reset: bool = False, list_only: bool = False, au
             c.final_select = False
     elif list_only:
         for c in ms.ccs:
-            if c.final_select:
+            if c.final_select and _writer():
                 print(c.name)
         return 0
     elif autofilter:
@@ -200,12 +205,14 @@ def run_varsel(root: str = ".", reset: bool = False, list_only: bool = False, au
                 os.makedirs(ms.pf.varsel_dir, exist_ok=True)
                 for i in range(max(1, recursive)):
                     ms.save_cc()
-                    import shutil
-                    shutil.copyfile(ms.pf.column_config, ms.pf.varsel_cc_backup(i))
+                    if _writer():
+                        import shutil
+                        shutil.copyfile(ms.pf.column_config, ms.pf.varsel_cc_backup(i))
                     res = select_by_sensitivity(ms, by, device, seed=i)
-                    with open(ms.pf.varsel_se(i), "w") as f:
-                        for num, name, mean, rms, var in res:
-                            f.write(f"{num}\t{name}\t{mean}\t{rms}\t{var}\n")
+                    if _writer():
+                        with open(ms.pf.varsel_se(i), "w") as f:
+                            for num, name, mean, rms, var in res:
+                                f.write(f"{num}\t{name}\t{mean}\t{rms}\t{var}\n")
             elif by in ("V", "VOTED"):
                 voted_selection(ms, device)
             else:

@@ -86,8 +86,8 @@ def _rank_cli(rank, world, port, root, verb):
 
 
 def test_cli_pipeline_two_ranks(tmp_path):
-    """stats (data parallel), norm / varsel (rank 0 alone under dist.local_only), train (data
-    parallel) and eval driven through the CLI by 2 gloo ranks, as `SHIFU_GPUS=2 shifu ...` does."""
+    """stats, norm, varsel, train, posttrain and eval (all data parallel) driven through the CLI by
+    2 gloo ranks, as `SHIFU_GPUS=2 shifu ...` does."""
     from shifu_amd.config.model_config import ModelConfig
     from shifu_amd.steps.create import run_init
     from shifu_amd.utils.synthetic import make_model_set
@@ -97,7 +97,7 @@ def test_cli_pipeline_two_ranks(tmp_path):
     mc.train["baggingNum"] = 1
     mc.save()
     run_init(root)
-    for verb in ("stats", "norm", "varsel", "train", "eval"):
+    for verb in ("stats", "norm", "varsel", "train", "posttrain", "eval"):
         mp.start_processes(_rank_cli, args=(2, _port(), root, verb), nprocs=2, join=True, start_method="spawn")
     assert os.path.exists(os.path.join(root, "models", "model0.nn"))
     perf = json.load(open(os.path.join(root, "evals", "Eval1", "EvalPerformance.json")))
@@ -152,3 +152,51 @@ def test_norm_two_ranks_match_single(tmp_path, alg, shuffle):
     assert ma["n"] == mb["n"] and set(xa) == set(xb)
     for k in xa:
         np.testing.assert_array_equal(xa[k], xb[k], err_msg=k)
+
+
+def test_varsel_se_and_posttrain_two_ranks_match_single(tmp_path):
+    """Row-sharded SE sensitivity (all-reduced per-input sums, gradients all-reduced in the quick
+    NN) and row-sharded posttrain (all-reduced per-bin score sums) == one process."""
+    from shifu_amd.config.column_config import load_column_configs
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.posttrain import run_posttrain
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.steps.train import run_train
+    from shifu_amd.steps.varsel import run_varsel
+    from shifu_amd.utils.synthetic import make_model_set
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=1100, n_num=7, n_cat=2)
+    mc = ModelConfig.load(os.path.join(a, "ModelConfig.json"))
+    mc.varSelect["filterBy"] = "SE"
+    mc.varSelect["filterNum"] = 5
+    mc.varSelect["autoFilterEnable"] = False
+    mc.train["numTrainEpochs"] = 12
+    mc.train["baggingNum"] = 1
+    mc.save()
+    run_init(a)
+    run_stats(a)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    run_varsel(a)
+    mp.start_processes(_rank_cli, args=(2, _port(), b, "varsel"), nprocs=2, join=True, start_method="spawn")
+    def se(root):
+        rows = [l.split("\t") for l in open(os.path.join(root, "varsel", "se.0")).read().strip().split("\n")]
+        return {r[1]: float(r[3]) for r in rows}
+    sa, sb = se(a), se(b)
+    assert sa.keys() == sb.keys()
+    np.testing.assert_allclose([sa[k] for k in sa], [sb[k] for k in sa], rtol=2e-3, atol=1e-6)
+    fa = sorted(c.name for c in load_column_configs(os.path.join(a, "ColumnConfig.json")) if c.final_select)
+    fb = sorted(c.name for c in load_column_configs(os.path.join(b, "ColumnConfig.json")) if c.final_select)
+    assert fa == fb and len(fa) == 5
+    # posttrain on the same model files
+    run_train(a)
+    shutil.rmtree(os.path.join(b, "models"), ignore_errors=True)
+    shutil.copytree(os.path.join(a, "models"), os.path.join(b, "models"))
+    run_posttrain(a)
+    mp.start_processes(_rank_cli, args=(2, _port(), b, "posttrain"), nprocs=2, join=True, start_method="spawn")
+    ba = {c.name: c.bin_avg_score for c in load_column_configs(os.path.join(a, "ColumnConfig.json")) if c.final_select}
+    bb = {c.name: c.bin_avg_score for c in load_column_configs(os.path.join(b, "ColumnConfig.json")) if c.final_select}
+    assert ba.keys() == bb.keys() and all(ba[k] for k in ba)
+    for k in ba:
+        assert np.max(np.abs(np.array(ba[k]) - np.array(bb[k]))) <= 1, k
