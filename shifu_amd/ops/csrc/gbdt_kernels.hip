@@ -24,6 +24,7 @@
 //   * deterministic: slab order is fixed and ties break to the lowest feature, then bin, so
 //     every rank computes the identical split from the all-reduced histograms.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -53,9 +54,7 @@ struct HistArgs {
 //     r of a 16-lane LDS group updates feature (j + r) & 15 at step j, so the group's 16 lanes
 //     always hit 16 distinct bank pairs whatever the bins are.
 constexpr int HT = 512;                       // threads per histogram block (8 waves)
-constexpr int HU = 4;                         // row slots in flight per thread
 constexpr int RPP = HT / 2;                   // rows per slot pass (2 threads x 16 B per row)
-constexpr int HFLUSH = 4096 / (RPP * HU);     // passes between unpacks (4096 rows)
 constexpr int HNE = 2 * NB * 16 / HT;         // LDS entries each thread unpacks (16)
 constexpr int PACK_G = 36;                    // low field bits (signed qg)
 
@@ -67,7 +66,9 @@ __device__ __forceinline__ void unpack_add(unsigned long long v, long long& aw, 
   aw += (long long)((v - (unsigned long long)gq) >> PACK_G);
 }
 
+template <bool PF, int HU>
 __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
+  constexpr int HFLUSH = 4096 / (RPP * HU);     // passes between unpacks (4096 rows)
   extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];   // [2][NB][16]
   const int item = blockIdx.x;
   const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
@@ -79,43 +80,27 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   long long accw[HNE], accg[HNE];
 #pragma unroll
   for (int k = 0; k < HNE; ++k) { accw[k] = 0; accg[k] = 0; }
-  int it = 0;
-  for (int p0 = lo; p0 < hi; p0 += RPP * HU) {        // block-uniform trip count (unpack barriers)
-    int rows[HU];
+  // one row slot: packed (w, w*g) fixed point added to the 16 features' bins of this half record
+  auto update = [&](float wv, float gv, const uint4& bv) {
+    if (wv == 0.f) return;
+    const unsigned long long q = ((unsigned long long)__float2uint_rn(wv * a.scale_w) << PACK_G) +
+                                 (unsigned long long)(long long)__float2int_rn(wv * gv * a.scale_g);
+    // rotate the 16 bytes left by r: byte j of R = feature (j + r) & 15
+    const uint32_t W[4] = {bv.x, bv.y, bv.z, bv.w};
+    uint32_t X[4], Y[4], R[4];
 #pragma unroll
-    for (int u = 0; u < HU; ++u) {
-      const int p = p0 + t2 + u * RPP;
-      rows[u] = p < hi ? (a.pos2row ? a.pos2row[p] : p) : -1;
+    for (int k = 0; k < 4; ++k) X[k] = pick(W[k], W[(k + 1) & 3], r & 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Y[k] = pick(X[k], X[(k + 2) & 3], r & 8);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) R[k] = __builtin_amdgcn_alignbyte(Y[(k + 1) & 3], Y[k], r & 3);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
+      atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
     }
-    float wv[HU], gv[HU];
-    uint4 bv[HU];
-#pragma unroll
-    for (int u = 0; u < HU; ++u) {
-      const int rr = rows[u];
-      wv[u] = rr >= 0 ? a.w[rr] : 0.f;
-      gv[u] = rr >= 0 ? a.g[rr] : 0.f;
-      bv[u] = rr >= 0 ? *(const uint4*)(gb + (size_t)rr * 32) : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < HU; ++u) {
-      if (wv[u] == 0.f) continue;
-      const unsigned long long q = ((unsigned long long)__float2uint_rn(wv[u] * a.scale_w) << PACK_G) +
-                                   (unsigned long long)(long long)__float2int_rn(wv[u] * gv[u] * a.scale_g);
-      // rotate the 16 bytes left by r: byte j of R = feature (j + r) & 15
-      const uint32_t W[4] = {bv[u].x, bv[u].y, bv[u].z, bv[u].w};
-      uint32_t X[4], Y[4], R[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) X[k] = pick(W[k], W[(k + 1) & 3], r & 4);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) Y[k] = pick(X[k], X[(k + 2) & 3], r & 8);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) R[k] = __builtin_amdgcn_alignbyte(Y[(k + 1) & 3], Y[k], r & 3);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
-        atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
-      }
-    }
+  };
+  auto flush = [&](int& it) {
     if (++it == HFLUSH) {
       it = 0;
       __syncthreads();
@@ -125,6 +110,61 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
         hsm[threadIdx.x + k * HT] = 0ull;
       }
       __syncthreads();
+    }
+  };
+  int it = 0;
+  constexpr int STEP = RPP * HU;
+  if constexpr (PF) {
+    // Software pipeline: pass i+1's loads (bins, w, g) and pass i+2's pos2row gather are issued
+    // before pass i's LDS atomics, so HBM latency hides behind the atomics.  Positions past `hi`
+    // are clamped to hi - 1 (valid memory, no branch around a load: a branch would make the
+    // compiler wait for the outstanding loads early) and get weight 0 when consumed.
+    auto row_of = [&](int p) { const int pc = min(p, hi - 1); return a.pos2row ? a.pos2row[pc] : pc; };
+    int rn[HU];
+    float wc[HU], gc[HU];
+    uint4 bc[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int rr = row_of(lo + t2 + u * RPP);
+      wc[u] = a.w[rr]; gc[u] = a.g[rr]; bc[u] = *(const uint4*)(gb + (size_t)rr * 32);
+    }
+#pragma unroll
+    for (int u = 0; u < HU; ++u) rn[u] = row_of(lo + STEP + t2 + u * RPP);
+    for (int p0 = lo; p0 < hi; p0 += STEP) {          // block-uniform trip count (unpack barriers)
+      float wn[HU], gn[HU];
+      uint4 bn[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        wn[u] = a.w[rn[u]]; gn[u] = a.g[rn[u]]; bn[u] = *(const uint4*)(gb + (size_t)rn[u] * 32);
+      }
+#pragma unroll
+      for (int u = 0; u < HU; ++u) rn[u] = row_of(p0 + 2 * STEP + t2 + u * RPP);
+#pragma unroll
+      for (int u = 0; u < HU; ++u) update(p0 + t2 + u * RPP < hi ? wc[u] : 0.f, gc[u], bc[u]);
+      flush(it);
+#pragma unroll
+      for (int u = 0; u < HU; ++u) { wc[u] = wn[u]; gc[u] = gn[u]; bc[u] = bn[u]; }
+    }
+  } else {
+    for (int p0 = lo; p0 < hi; p0 += STEP) {          // block-uniform trip count (unpack barriers)
+      int rows[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int p = p0 + t2 + u * RPP;
+        rows[u] = p < hi ? (a.pos2row ? a.pos2row[p] : p) : -1;
+      }
+      float wv[HU], gv[HU];
+      uint4 bv[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int rr = rows[u];
+        wv[u] = rr >= 0 ? a.w[rr] : 0.f;
+        gv[u] = rr >= 0 ? a.g[rr] : 0.f;
+        bv[u] = rr >= 0 ? *(const uint4*)(gb + (size_t)rr * 32) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < HU; ++u) update(wv[u], gv[u], bv[u]);
+      flush(it);
     }
   }
   __syncthreads();
@@ -486,7 +526,9 @@ SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, const int* pos2row, con
   if (gs % 32 || n_items <= 0) return -1;
   HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, items, (long long*)slab, n_items, n_feat,
              (float)scale_w, (float)scale_g};
-  hipLaunchKernelGGL(gbdt_hist_kernel, dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
+  static const int pf = [] { const char* e = getenv("SHIFU_HIST_PF"); return e ? atoi(e) : 1; }();
+  if (pf) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2>), dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
+  else hipLaunchKernelGGL((gbdt_hist_kernel<false, 4>), dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
