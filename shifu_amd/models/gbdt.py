@@ -23,6 +23,7 @@ split search is replicated deterministically, so no trees are ever broadcast (SU
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -237,6 +238,8 @@ class TreeTrainer:
         self.timings = {"hist": 0.0, "split": 0.0, "partition": 0.0, "apply": 0.0}
         self._root_level = False
         self._codes_cache = None
+        self._nmod, self._npos = 0, data.n
+        self._pending: list = []        # RF trees grown ahead in a forest batch
 
     def _codes(self) -> torch.Tensor:
         """Row-major codes for the CPU paths (built once)."""
@@ -262,40 +265,63 @@ class TreeTrainer:
         if self.n_sub >= self.F:
             return None
         m = np.zeros((n_nodes, self.F), dtype=np.uint8)
+        rngs = getattr(self, "_level_rngs", None) or [self.rng] * n_nodes
         for i in range(n_nodes):
-            m[i, self.rng.choice(self.F, self.n_sub, replace=False)] = 1
+            m[i, rngs[i].choice(self.F, self.n_sub, replace=False)] = 1
         return torch.from_numpy(m).to(self.dev)
 
     # ------------------------------------------------------------------------------------
-    def grow_tree(self, g: torch.Tensor, w: torch.Tensor, weight: float) -> Tree:
+    def grow_tree(self, g: torch.Tensor, w: torch.Tensor, weight: float, tid: int | None = None) -> Tree:
+        return self.grow_forest(g, [w], weight, [len(self.trees) if tid is None else tid])[0]
+
+    def grow_forest(self, g: torch.Tensor, ws: list, weight: float, tids: list) -> list:
+        """Grow ``len(ws)`` trees at the same time (RF tree parallelism, F5: DTWorker keeps a
+        per-tree subsample weight per row, J/core/dtrain/dt/DTWorker.java:1515-1575, and the master
+        grows every tree's todo nodes together).  Tree t's rows live at virtual positions
+        [t*N, (t+1)*N): pos2row holds t*N + row, the weights / targets are concatenated per tree
+        and the kernels read bins at (virtual row mod N).  Each level is ONE histogram launch over
+        every tree's built nodes and ONE histogram all-reduce.  Feature subsets come from a
+        per-tree generator, so a tree is identical whether it grows alone or in a batch."""
         c = self.cfg
         d = self.data
         n = d.n
-        tree = Tree(c.max_depth, weight)
-        pos2row = torch.arange(n, dtype=torch.int32, device=self.dev)
-        pos_node = torch.zeros(n, dtype=torch.int32, device=self.dev)
-        # level-0 node: id 1, local range [0, n)
-        nodes = [{"id": 1, "start": 0, "end": n, "built": True, "parent": -1, "sibling": -1}]
+        T = len(ws)
+        P = T * n
+        if P >= 2 ** 31:
+            raise ValueError("forest batch exceeds int32 positions; lower the batch")
+        self._nmod = n if T > 1 else 0
+        self._npos = P
+        w = ws[0] if T == 1 else torch.cat(ws)
+        gg = g if T == 1 else g.repeat(T)
+        trees = [Tree(c.max_depth, weight) for _ in range(T)]
+        rngs = [np.random.default_rng([c.seed, int(t)]) for t in tids]
+        pos2row = torch.arange(P, dtype=torch.int32, device=self.dev)
+        pos_node = (pos2row // max(1, n)).to(torch.int32) if T > 1 else torch.zeros(n, dtype=torch.int32,
+                                                                                        device=self.dev)
+        nodes = [{"tree": t, "id": 1, "start": t * n, "end": (t + 1) * n, "built": True, "parent": -1,
+                  "sibling": -1} for t in range(T)]
         hist_prev = None
-        # root stats for the root's own value
-        tot = dist.all_reduce_(torch.stack([w.double().sum(), (w.double() * g.double()).sum()]))
-        tw, ts = float(tot[0]), float(tot[1])
+        # root stats for each root's own value (one all-reduce for the batch)
+        tot = dist.all_reduce_(torch.stack([torch.stack([wt.double().sum(), (wt.double() * g.double()).sum()])
+                                            for wt in ws]))
         # fixed-point scales (powers of two, identical on every rank): per row w*scale_w < 2^16 and
         # |w*g*scale_g| < 2^23, the field widths of the packed LDS histogram entries
-        mx = torch.stack([w.abs().max().double(), (w * g).abs().max().double()])
+        mx = torch.stack([w.abs().max().double(), (w * gg).abs().max().double()])
         dist.all_reduce_(mx, "max")
         self.scale_w = _pack_scale(float(mx[0]), W_BITS)
         self.scale_g = _pack_scale(float(mx[1]), G_BITS)
-        tree.exists[1] = True
-        tree.value[1] = ts / tw if tw != 0 else 0.0
-        tree.wgt_cnt[1] = tw
-        n_leaves = 1
+        for t, tree in enumerate(trees):
+            tw, ts = float(tot[t, 0]), float(tot[t, 1])
+            tree.exists[1] = True
+            tree.value[1] = ts / tw if tw != 0 else 0.0
+            tree.wgt_cnt[1] = tw
+        n_leaves = [1] * T
         for level in range(1, c.max_depth):
             if not nodes:
                 break
             # slots: built nodes first (contiguous for the all-reduce), then derived; positions
             # carry the partition's child index -> remap them to the new slot numbering
-            nodes.sort(key=lambda z: (not z["built"], z["id"]))
+            nodes.sort(key=lambda z: (not z["built"], z["tree"], z["id"]))
             for s_, z in enumerate(nodes):
                 z["slot"] = s_
             if level > 1:
@@ -303,14 +329,15 @@ class TreeTrainer:
                 for z in nodes:
                     remap[z["pidx"]] = z["slot"]
                 pos_node = torch.where(pos_node >= 0, remap[pos_node.clamp(min=0).long()], pos_node)
-            slot_of = {z["id"]: z["slot"] for z in nodes}
+            slot_of = {(z["tree"], z["id"]): z["slot"] for z in nodes}
             for z in nodes:
                 if not z["built"]:
-                    z["sib_slot"] = slot_of[z["id"] ^ 1]
+                    z["sib_slot"] = slot_of[(z["tree"], z["id"] ^ 1)]
             n_built = sum(1 for z in nodes if z["built"])
             self._root_level = level == 1
+            self._level_rngs = [rngs[z["tree"]] for z in nodes]
             t0 = time.perf_counter()
-            hist = self._build_and_split(nodes, n_built, g, w, pos2row, hist_prev)
+            hist = self._build_and_split(nodes, n_built, gg, w, pos2row, hist_prev)
             best = hist["best"]            # per slot: (feat, bin, gain, lw, ls, rw, rs, valid)
             self.timings["split"] += time.perf_counter() - t0
             # decisions ------------------------------------------------------------------
@@ -322,20 +349,23 @@ class TreeTrainer:
             allowed = None
             if c.max_leaves > 0:
                 # MaxLeaves (DTMaster :543-605, 1063-1071): split the candidates with the highest
-                # wgtCnt-ratio x gain first while the leaf budget lasts
-                cands = sorted((-(float(best[z["slot"]][2]) * float(tree.wgt_cnt[z["id"]])), z["slot"])
-                               for z in nodes if best[z["slot"]][7])
-                room = max(0, c.max_leaves - n_leaves)
-                if c.max_batch_split > 0:   # DTMaster :360 intends this cap (its loop never counts)
-                    room = min(room, c.max_batch_split)
-                allowed = {s_ for _, s_ in cands[:room]}
+                # wgtCnt-ratio x gain first while each tree's leaf budget lasts
+                allowed = set()
+                for t in range(T):
+                    cands = sorted((-(float(best[z["slot"]][2]) * float(trees[t].wgt_cnt[z["id"]])), z["slot"])
+                                   for z in nodes if z["tree"] == t and best[z["slot"]][7])
+                    room = max(0, c.max_leaves - n_leaves[t])
+                    if c.max_batch_split > 0:   # DTMaster :360 intends this cap (its loop never counts)
+                        room = min(room, c.max_batch_split)
+                    allowed |= {s_ for _, s_ in cands[:room]}
             for z in nodes:
                 s_ = z["slot"]
                 f, b, gain, lw, ls, rw, rs, ok = best[s_]
                 nid = z["id"]
                 if not ok or (allowed is not None and s_ not in allowed):
                     continue
-                n_leaves += 1
+                tree = trees[z["tree"]]
+                n_leaves[z["tree"]] += 1
                 f = int(f)
                 tree.feat[nid] = f
                 tree.gain[nid] = gain
@@ -368,13 +398,14 @@ class TreeTrainer:
                 # build the globally smaller child, derive the other (identical on all ranks)
                 left_built = lw <= rw
                 k = len(new_nodes)     # child index written by the partition scatter
-                new_nodes.append({"id": 2 * z["id"], "start": lo, "end": mid, "built": left_built,
-                                  "parent": z["slot"], "pidx": k})
-                new_nodes.append({"id": 2 * z["id"] + 1, "start": mid, "end": hi, "built": not left_built,
-                                  "parent": z["slot"], "pidx": k + 1})
+                new_nodes.append({"tree": z["tree"], "id": 2 * z["id"], "start": lo, "end": mid,
+                                  "built": left_built, "parent": z["slot"], "pidx": k})
+                new_nodes.append({"tree": z["tree"], "id": 2 * z["id"] + 1, "start": mid, "end": hi,
+                                  "built": not left_built, "parent": z["slot"], "pidx": k + 1})
             hist_prev = hist["hist"]
             nodes = new_nodes
-        return tree
+        self._nmod, self._npos = 0, n
+        return trees
 
     # ------------------------------------------------------------------------------------
     def _make_items(self, nodes, n_built):
@@ -459,7 +490,7 @@ class TreeTrainer:
             slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
             p2r = None if self._root_level else pos2row      # root: positions are rows
             nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, g, it, len(items), slab, F,
-                         self.scale_w, self.scale_g, st)
+                         self.scale_w, self.scale_g, self._nmod, st)
         else:
             slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
         built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
@@ -510,7 +541,7 @@ class TreeTrainer:
             rows = pos2row[z["start"]: z["end"]].long()
             if rows.numel() == 0:
                 continue
-            b = bins[rows]                                   # [m, F]
+            b = bins[rows % d.n]                             # [m, F] (virtual rows of a forest batch)
             qw = torch.round(w[rows].double() * self.scale_w).long()
             qg = torch.round((w[rows] * g[rows]).float().double() * self.scale_g).long()
             idx = (torch.arange(F).unsqueeze(0) * NB + b).reshape(-1)
@@ -564,7 +595,7 @@ class TreeTrainer:
     def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node):
         d = self.data
         nn = len(nodes)
-        n = d.n
+        n = self._npos                   # positions (T * N for a forest batch)
         starts = np.array([z["start"] for z in nodes], dtype=np.int64)
         ends = np.array([z["end"] for z in nodes], dtype=np.int64)
         # positions of unsplit nodes are never moved; mark non-split node positions -1
@@ -577,7 +608,7 @@ class TreeTrainer:
             flag = torch.empty(n, dtype=torch.int32, device=self.dev)
             nat.call_hip("shifu_gbdt_partition_flag", d.bins.data_ptr(), d.group_stride, pos2row.data_ptr(),
                          pos_node.data_ptr(), sf.data_ptr(), sb.data_ptr(), cl.data_ptr(), self.is_cat_t.data_ptr(),
-                         flag.data_ptr(), n, st)
+                         flag.data_ptr(), n, self._nmod, st)
             cum = torch.cumsum(flag, 0, dtype=torch.int32)
             # per-node: #left = cum[end-1] - cum[start-1]
             idx_end = torch.from_numpy(np.maximum(ends - 1, 0)).to(self.dev)
@@ -619,7 +650,7 @@ class TreeTrainer:
                 continue
             rows = pos2row[lo:hi].long()
             f = int(split_feat[s_])
-            b = bins[rows, f].long()
+            b = bins[rows % d.n, f].long()
             if d.is_cat[f]:
                 words = torch.from_numpy(cat_left[s_].astype(np.int64))
                 left = ((words[b >> 5] >> (b & 31)) & 1) == 1
@@ -689,13 +720,13 @@ class TreeTrainer:
         out, vout = self._out, self._vout
         for _ in range(n_trees):
             tid = len(self.trees)
-            w = self._weights_for_tree()
             if c.is_gbt:
+                w = self._weights_for_tree()
                 if tid == 0:
                     g = d.y
                 else:
                     g = out
-                tree = self.grow_tree(g, w, 1.0 if tid == 0 else c.learning_rate)
+                tree = self.grow_tree(g, w, 1.0 if tid == 0 else c.learning_rate, tid)
                 t0 = time.perf_counter()
                 keep = None
                 if tid > 0 and c.dropout_rate > 0.0:
@@ -711,7 +742,15 @@ class TreeTrainer:
                 terr = self._residual(self.pred, d, out)
                 verr = self._residual(self.vpred, self.valid, vout) if self.valid is not None else float("nan")
             else:
-                tree = self.grow_tree(d.y, w, 1.0)
+                if not self._pending:
+                    # RF: the next trees grow together (their subsample weights drawn in tree order,
+                    # so the batch equals growing them one by one)
+                    t0 = time.perf_counter()
+                    b = self._forest_batch(max(1, c.tree_num - tid))
+                    ws = [self._weights_for_tree() for _ in range(b)]
+                    self._pending = self.grow_forest(d.y, ws, 1.0, list(range(tid, tid + b)))
+                    self.timings["forest"] = self.timings.get("forest", 0.0) + time.perf_counter() - t0
+                tree = self._pending.pop(0)
                 self.apply_tree(tree, d, self.pred, 1.0, False)
                 if self.valid is not None:
                     self.apply_tree(tree, self.valid, self.vpred, 1.0, False)
@@ -725,27 +764,43 @@ class TreeTrainer:
                 callback(tid, tree, terr, verr)
         return self.trees
 
+    def _forest_batch(self, remaining: int) -> int:
+        """Trees grown per RF batch: ``SHIFU_RF_BATCH`` (default 8), bounded by int32 positions
+        and by ~1/3 of free HBM (each tree needs ~40 B per row of position / weight buffers);
+        the minimum over ranks so every rank runs the same collectives."""
+        n = max(1, self.data.n)
+        b = min(int(os.environ.get("SHIFU_RF_BATCH", "8")), remaining, (2 ** 31 - 1) // n)
+        if self.gpu:
+            free, _ = torch.cuda.mem_get_info(self.dev)
+            b = min(b, int(free // 3 // (40 * n)))
+        t = torch.tensor([max(1, b)], dtype=torch.int64, device=self.dev)
+        dist.all_reduce_(t, "min")
+        return int(t.item())
+
     # ---- checkpoint / resume (DTMaster.doCheckPoint :637-669 / recoverMasterStatus :1118-1154;
     #      worker-side recoverGBTData :1452-1488 = replay the trees over the resident rows) -----------
     def state_dict(self) -> dict:
-        trees = [{"max_depth": t.max_depth, "weight": t.weight, "feat": torch.from_numpy(t.feat),
-                  "thr": torch.from_numpy(t.thr), "cat_left": torch.from_numpy(t.cat_left.view(np.int32)),
-                  "value": torch.from_numpy(t.value), "wgt_cnt": torch.from_numpy(t.wgt_cnt),
-                  "gain": torch.from_numpy(t.gain), "exists": torch.from_numpy(t.exists),
-                  "features_used": list(map(int, t.features_used))} for t in self.trees]
-        return {"trees": trees, "train_errors": list(self.train_errors), "valid_errors": list(self.valid_errors),
+        def enc(t):
+            return {"max_depth": t.max_depth, "weight": t.weight, "feat": torch.from_numpy(t.feat),
+                    "thr": torch.from_numpy(t.thr), "cat_left": torch.from_numpy(t.cat_left.view(np.int32)),
+                    "value": torch.from_numpy(t.value), "wgt_cnt": torch.from_numpy(t.wgt_cnt),
+                    "gain": torch.from_numpy(t.gain), "exists": torch.from_numpy(t.exists),
+                    "features_used": list(map(int, t.features_used))}
+        trees = [enc(t) for t in self.trees]
+        return {"trees": trees, "pending": [enc(t) for t in self._pending], "train_errors": list(self.train_errors), "valid_errors": list(self.valid_errors),
                 "rng": self.rng.bit_generator.state, "tgen": self.tgen.get_state()}
 
     def load_state_dict(self, st: dict) -> None:
-        self.trees = []
-        for d in st["trees"]:
+        def dec(d):
             t = Tree(int(d["max_depth"]), float(d["weight"]))
             t.feat, t.thr = d["feat"].numpy().copy(), d["thr"].numpy().copy()
             t.cat_left = d["cat_left"].numpy().copy().view(np.uint32)
             t.value, t.wgt_cnt = d["value"].numpy().copy(), d["wgt_cnt"].numpy().copy()
             t.gain, t.exists = d["gain"].numpy().copy(), d["exists"].numpy().copy()
             t.features_used = list(d["features_used"])
-            self.trees.append(t)
+            return t
+        self.trees = [dec(d) for d in st["trees"]]
+        self._pending = [dec(d) for d in st.get("pending", [])]
         self.train_errors, self.valid_errors = list(st["train_errors"]), list(st["valid_errors"])
         self.rng.bit_generator.state = st["rng"]
         self.tgen.set_state(st["tgen"])

@@ -40,6 +40,7 @@ struct HistArgs {
   long long* slab;                   // [n_items][2][FG][NB] int64 fixed point
   int n_items, n_feat;
   float scale_w, scale_g;            // powers of two: w*scale_w < 2^16, |w*g*scale_g| < 2^23
+  long nmod;                         // > 0: forest batch, pos2row holds tree * N + row -> bins row = v % N
 };
 
 // Histogram build (measured on gfx950 with tools/microbench_hist.hip, 16M rows x 1024 features):
@@ -77,6 +78,8 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   const int half = threadIdx.x & 1, r = threadIdx.x & 15, t2 = threadIdx.x >> 1;
   const uint8_t* gb = a.bins + (size_t)grp * a.gs + half * 16;
   unsigned long long* base = hsm + half * NB * 16;
+  // w / g are indexed by the (virtual) row id, the bins by the data row
+  auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * 32); };
   long long accw[HNE], accg[HNE];
 #pragma unroll
   for (int k = 0; k < HNE; ++k) { accw[k] = 0; accg[k] = 0; }
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
 #pragma unroll
     for (int u = 0; u < HU; ++u) {
       const int rr = row_of(lo + t2 + u * RPP);
-      wc[u] = a.w[rr]; gc[u] = a.g[rr]; bc[u] = *(const uint4*)(gb + (size_t)rr * 32);
+      wc[u] = a.w[rr]; gc[u] = a.g[rr]; bc[u] = rec(rr);
     }
 #pragma unroll
     for (int u = 0; u < HU; ++u) rn[u] = row_of(lo + STEP + t2 + u * RPP);
@@ -135,7 +138,7 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
       uint4 bn[HU];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
-        wn[u] = a.w[rn[u]]; gn[u] = a.g[rn[u]]; bn[u] = *(const uint4*)(gb + (size_t)rn[u] * 32);
+        wn[u] = a.w[rn[u]]; gn[u] = a.g[rn[u]]; bn[u] = rec(rn[u]);
       }
 #pragma unroll
       for (int u = 0; u < HU; ++u) rn[u] = row_of(p0 + 2 * STEP + t2 + u * RPP);
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
         const int rr = rows[u];
         wv[u] = rr >= 0 ? a.w[rr] : 0.f;
         gv[u] = rr >= 0 ? a.g[rr] : 0.f;
-        bv[u] = rr >= 0 ? *(const uint4*)(gb + (size_t)rr * 32) : make_uint4(0, 0, 0, 0);
+        bv[u] = rr >= 0 ? rec(rr) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < HU; ++u) update(wv[u], gv[u], bv[u]);
@@ -406,6 +409,7 @@ struct PartArgs {
   const uint8_t* is_cat;        // [F]
   int* flag;                    // [N] out: 1 left, 0 right, for split nodes; 0 otherwise
   long n;
+  long nmod;                    // > 0: forest batch (pos2row = tree * nmod + row)
 };
 
 __global__ void gbdt_partition_flag_kernel(PartArgs a) {
@@ -415,7 +419,8 @@ __global__ void gbdt_partition_flag_kernel(PartArgs a) {
   const int f = node >= 0 ? a.split_feat[node] : -1;
   int fl = 0;
   if (f >= 0) {
-    const uint32_t b = a.bins[(size_t)(f >> 5) * a.gs + (size_t)a.pos2row[p] * 32 + (f & 31)];
+    const long v = a.pos2row[p], row = a.nmod ? v % a.nmod : v;
+    const uint32_t b = a.bins[(size_t)(f >> 5) * a.gs + (size_t)row * 32 + (f & 31)];
     if (a.is_cat[f]) fl = (a.cat_left[node * 8 + (b >> 5)] >> (b & 31)) & 1;
     else fl = (int)b <= a.split_bin[node] ? 1 : 0;
   }
@@ -522,10 +527,10 @@ __global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
 
 SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, const int* pos2row, const float* w, const float* g,
                               const int* items, int n_items, void* slab, int n_feat, double scale_w,
-                              double scale_g, hipStream_t stream) {
+                              double scale_g, long nmod, hipStream_t stream) {
   if (gs % 32 || n_items <= 0) return -1;
   HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, items, (long long*)slab, n_items, n_feat,
-             (float)scale_w, (float)scale_g};
+             (float)scale_w, (float)scale_g, nmod};
   static const int pf = [] { const char* e = getenv("SHIFU_HIST_PF"); return e ? atoi(e) : 1; }();
   if (pf) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2>), dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
   else hipLaunchKernelGGL((gbdt_hist_kernel<false, 4>), dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
@@ -552,9 +557,9 @@ SHIFU_API int shifu_gbdt_split(const void* slab, const int* node_items, int max_
 
 SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const int* pos2row, const int* pos_node,
                                         const int* split_feat, const int* split_bin, const void* cat_left,
-                                        const void* is_cat, int* flag, long n, hipStream_t stream) {
+                                        const void* is_cat, int* flag, long n, long nmod, hipStream_t stream) {
   PartArgs a{(const uint8_t*)bins, gs, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
-             (const uint8_t*)is_cat, flag, n};
+             (const uint8_t*)is_cat, flag, n, nmod};
   hipLaunchKernelGGL(gbdt_partition_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;

@@ -151,3 +151,58 @@ def test_max_leaves_budget():
         tt.train()
         for t in tt.trees:
             assert 2 <= len(t.leaves()) <= ml
+
+
+def _rf_trees(data, batch, monkeypatch, **kw):
+    monkeypatch.setenv("SHIFU_RF_BATCH", str(batch))
+    cfg = dict(algorithm="RF", tree_num=5, max_depth=5, impurity="gini", sample_with_replacement=True,
+               feature_subset_strategy="HALF", seed=11, max_leaves=kw.get("max_leaves", 0))
+    tr = TreeTrainer(TreeConfig(**cfg), data)
+    tr.train()
+    return tr
+
+
+def _same_trees(ta, tb, atol=0.0):
+    assert len(ta.trees) == len(tb.trees)
+    for a, b in zip(ta.trees, tb.trees):
+        assert (a.feat == b.feat).all() and (a.thr == b.thr).all() and (a.exists == b.exists).all()
+        assert np.allclose(a.value, b.value, atol=atol) and (a.cat_left == b.cat_left).all()
+
+
+@pytest.mark.parametrize("max_leaves", [0, 9])
+def test_rf_forest_batch_equals_sequential(monkeypatch, max_leaves):
+    """F5 tree parallelism: RF trees grown together in one level loop (virtual positions
+    tree*N + row, one histogram pass + one all-reduce per level for the whole batch) are the
+    same trees as growing them one at a time."""
+    data, _, _ = _data(n=1400, f=7, nb=10, seed=4, cat_cols=(2,))
+    one = _rf_trees(data, 1, monkeypatch, max_leaves=max_leaves)
+    four = _rf_trees(data, 4, monkeypatch, max_leaves=max_leaves)   # batches of 4 + 1
+    _same_trees(one, four)
+    assert np.allclose(one.pred.numpy(), four.pred.numpy())
+
+
+def test_rf_forest_batch_checkpoint_keeps_pending(monkeypatch):
+    data, _, _ = _data(n=900, f=5, nb=8, seed=6)
+    ref = _rf_trees(data, 4, monkeypatch)
+    monkeypatch.setenv("SHIFU_RF_BATCH", "4")
+    cfg = dict(algorithm="RF", tree_num=5, max_depth=5, impurity="gini", sample_with_replacement=True,
+               feature_subset_strategy="HALF", seed=11)
+    a = TreeTrainer(TreeConfig(**cfg), data)
+    a.train(2)                                  # 2 trees used, 2 grown ahead and pending
+    st = a.state_dict()
+    b = TreeTrainer(TreeConfig(**cfg), data)
+    b.load_state_dict(st)
+    b.train(3)
+    _same_trees(ref, b)
+
+
+@pytest.mark.gpu
+def test_gpu_rf_forest_batch_matches_sequential(monkeypatch):
+    """HIP path: batch of 3 (+2) RF trees == the same trees grown one by one on the GPU (the
+    Poisson subsample weights come from the device generator, so the CPU oracle draws others)."""
+    data_c, codes, y = _data(n=30000, f=40, nb=64, seed=8, cat_cols=(5,))
+    data_g = BinnedData.from_codes(codes, y, data_c.nbins, data_c.is_cat, device="cuda")
+    t1 = _rf_trees(data_g, 1, monkeypatch)
+    t3 = _rf_trees(data_g, 3, monkeypatch)
+    _same_trees(t1, t3, atol=1e-6)
+    assert np.allclose(t1.pred.cpu().numpy(), t3.pred.cpu().numpy(), atol=1e-6)
