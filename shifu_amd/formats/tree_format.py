@@ -265,8 +265,16 @@ def write_tree_model(path: str, m: TreeModelFile):
     for k, v in m.column_mapping.items():
         o.int(k)
         o.int(v)
-    o.int(len(m.bags))
-    for bag in m.bags:
+    write_bags(o, m.bags)
+    with open(path, "wb") as f:
+        f.write(o.gzip_bytes())
+
+
+def write_bags(o: JavaOut, bags):
+    """int #bags, then per bag int #trees and ``TreeNode.write`` records (the ``.gbt`` tail and
+    the ``trees`` entry of the readable zip spec, IndependentTreeModelUtils.java:52-60)."""
+    o.int(len(bags))
+    for bag in bags:
         o.int(len(bag))
         for t in bag:
             o.int(t.tree_id)
@@ -278,8 +286,23 @@ def write_tree_model(path: str, m: TreeModelFile):
             o.int(len(t.features))
             for f in t.features:
                 o.int(f)
-    with open(path, "wb") as f:
-        f.write(o.gzip_bytes())
+
+
+def read_bags(i: JavaIn, version: int = TREE_FORMAT_VERSION, n_bags: int | None = None):
+    bags = []
+    nb = i.int() if n_bags is None else n_bags
+    for _ in range(nb):
+        trees = []
+        for _ in range(i.int()):
+            tid = i.int()
+            nn = i.int()
+            root = _read_node(i, version)
+            lr = i.double()
+            rw = i.double() if root.id == 1 else 0.0
+            feats = [i.int() for _ in range(i.int())]
+            trees.append(TreeRecord(tid, nn, root, lr, rw, feats))
+        bags.append(trees)
+    return bags
 
 
 def read_tree_model(path_or_bytes) -> TreeModelFile:
@@ -315,19 +338,7 @@ def read_tree_model(path_or_bytes) -> TreeModelFile:
     for _ in range(i.int()):
         k = i.int()
         mapping[k] = i.int()
-    bags = []
-    nb = 1 if version < 4 else i.int()
-    for _ in range(nb):
-        trees = []
-        for _ in range(i.int()):
-            tid = i.int()
-            nn = i.int()
-            root = _read_node(i, version)
-            lr = i.double()
-            rw = i.double() if root.id == 1 else 0.0
-            feats = [i.int() for _ in range(i.int())]
-            trees.append(TreeRecord(tid, nn, root, lr, rw, feats))
-        bags.append(trees)
+    bags = read_bags(i, version, 1 if version < 4 else None)
     return TreeModelFile(alg, loss, is_cls, ova, inputs, means, names, cats, mapping, bags, version)
 
 

@@ -24,6 +24,7 @@ import numpy as np
 from ..data.expr import Evaluator
 from ..data.reader import first_line_is_header, read_header, read_table
 from ..formats import tree_format
+from ..formats.javaio import JavaIn, JavaOut
 from ..scoring.tree_ensemble import TreeScorer
 from ..utils.log import get_logger
 from .base import ModelSet
@@ -165,68 +166,47 @@ def run_filter_test(root=".", target: str | None = None, n: int = 100) -> int:
 
 
 # ---- convert / analysis -------------------------------------------------------------------------------
-def _node_json(nd):
-    if nd is None:
-        return None
-    d = {"id": nd.id, "gain": nd.gain, "wgtCnt": nd.wgt_cnt, "predict": nd.predict, "classValue": nd.class_value}
-    if nd.split is not None:
-        s = nd.split
-        d["split"] = {"column": s.column, "type": "CONTINUOUS" if s.ftype == 1 else "CATEGORICAL",
-                      "threshold": s.threshold, "isLeft": s.is_left,
-                      "categories": sorted(s.categories) if s.categories else None}
-        d["left"] = _node_json(nd.left)
-        d["right"] = _node_json(nd.right)
-    return d
-
-
-def _node_from_json(d):
-    if d is None:
-        return None
-    nd = tree_format.Node(d["id"], d.get("gain", 0.0), d.get("wgtCnt", 0.0), None, d.get("predict"),
-                          d.get("classValue", 0))
-    s = d.get("split")
-    if s:
-        nd.split = tree_format.Split(s["column"], 1 if s["type"] == "CONTINUOUS" else 2, s.get("threshold", 0.0),
-                                     s.get("isLeft", True), set(s["categories"]) if s.get("categories") else None)
-        nd.left, nd.right = _node_from_json(d.get("left")), _node_from_json(d.get("right"))
-    return nd
-
-
 def gbt_to_zip(src: str, dst: str):
+    """Binary ``.gbt``/``.rf`` -> readable zip spec in the reference layout
+    (IndependentTreeModelUtils.convertBinaryToZipSpec, J/util/IndependentTreeModelUtils.java:38-70):
+    ``model.ini`` = the IndependentTreeModel bean as JSON with ``trees: null``, ``trees`` = int
+    #bags, per bag int #trees + ``TreeNode.write`` records (Java big-endian)."""
     m = tree_format.read_tree_model(src)
+    ini = {
+        "numNameMapping": {str(k): v for k, v in m.names.items()},
+        "categoricalColumnNameNames": {str(k): list(v) for k, v in m.categories.items()},
+        "columnCategoryIndexMapping": {str(k): {c: j for j, c in enumerate(v)} for k, v in m.categories.items()},
+        "columnNumIndexMapping": {str(k): v for k, v in m.column_mapping.items()},
+        "trees": None,
+        "weights": [[t.learning_rate for t in bag] for bag in m.bags],
+        "lossStr": m.loss,
+        "algorithm": m.algorithm,
+        "inputNode": m.input_count,
+        "numericalMeanMapping": {str(k): v for k, v in m.numerical_means.items()},
+        "gbtScoreConvertStrategy": "RAW",
+        "gbdt": m.algorithm.upper() == "GBT",
+        "classification": m.is_classification,
+        "convertToProb": False,
+    }
+    o = JavaOut()
+    tree_format.write_bags(o, m.bags)
     with zipfile.ZipFile(dst, "w", zipfile.ZIP_DEFLATED) as z:
-        ini = {"version": m.version, "algorithm": m.algorithm, "loss": m.loss,
-               "isClassification": m.is_classification, "isOneVsAll": m.is_one_vs_all,
-               "inputCount": m.input_count, "numericalMeans": {str(k): v for k, v in m.numerical_means.items()},
-               "columnNames": {str(k): v for k, v in m.names.items()},
-               "categories": {str(k): v for k, v in m.categories.items()},
-               "columnMapping": {str(k): v for k, v in m.column_mapping.items()}, "bags": len(m.bags)}
-        z.writestr("model.ini", json.dumps(ini, indent=1))
-        for b, bag in enumerate(m.bags):
-            for t in bag:
-                z.writestr(f"trees/bag{b}/tree{t.tree_id}.json",
-                           json.dumps({"treeId": t.tree_id, "learningRate": t.learning_rate,
-                                       "rootWgtCnt": t.root_wgt_cnt, "features": t.features,
-                                       "nodeNum": t.node_num, "root": _node_json(t.root)}))
+        z.writestr("model.ini", json.dumps(ini, indent=2))
+        z.writestr("trees", o.bytes())
 
 
 def zip_to_gbt(src: str, dst: str):
+    """Readable zip spec -> binary ``.gbt`` (convertZipSpecToBinary, :74-125)."""
     with zipfile.ZipFile(src) as z:
         ini = json.loads(z.read("model.ini"))
-        bags = [[] for _ in range(ini["bags"])]
-        for nm in sorted(z.namelist()):
-            if nm.startswith("trees/"):
-                b = int(nm.split("/")[1][3:])
-                d = json.loads(z.read(nm))
-                bags[b].append(tree_format.TreeRecord(d["treeId"], d["nodeNum"], _node_from_json(d["root"]),
-                                                      d["learningRate"], d.get("rootWgtCnt", 0.0),
-                                                      d.get("features", [])))
-        for bag in bags:
-            bag.sort(key=lambda t: t.tree_id)
-    ik = lambda dct: {int(k): v for k, v in dct.items()}   # noqa: E731
-    m = tree_format.TreeModelFile(ini["algorithm"], ini["loss"], ini["isClassification"], ini["isOneVsAll"],
-                                  ini["inputCount"], ik(ini["numericalMeans"]), ik(ini["columnNames"]),
-                                  ik(ini["categories"]), ik(ini["columnMapping"]), bags)
+        bags = tree_format.read_bags(JavaIn(z.read("trees")))
+    if not bags or not any(bags):
+        raise ValueError(f"{src}: no trees in the zip spec")
+    ik = lambda dct: {int(k): v for k, v in (dct or {}).items()}   # noqa: E731
+    m = tree_format.TreeModelFile(ini["algorithm"], ini.get("lossStr", "squared"), bool(ini.get("classification")),
+                                  bool(ini.get("oneVsAll", False)), int(ini["inputNode"]),
+                                  ik(ini.get("numericalMeanMapping")), ik(ini.get("numNameMapping")),
+                                  ik(ini.get("categoricalColumnNameNames")), ik(ini.get("columnNumIndexMapping")), bags)
     tree_format.write_tree_model(dst, m)
 
 

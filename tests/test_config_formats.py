@@ -5,6 +5,7 @@ import os
 import numpy as np
 import pytest
 
+from conftest import REF_TR
 from shifu_amd.config import jsonio
 from shifu_amd.config.column_config import load_column_configs, save_column_configs
 from shifu_amd.config.model_config import ModelConfig, create_init_model_config
@@ -97,3 +98,22 @@ def test_gbt_fixture_read_and_roundtrip(ref_resources, tmp_path):
     np.testing.assert_allclose(m.score(x, 5), m2.score(x, 5))
     fi = tree_format.feature_importance(m)
     assert abs(sum(fi.values()) - 1.0) < 1e-9
+
+
+def test_readable_zip_spec_matches_reference_bytes(tmp_path, ref_resources):
+    """convert -totreeb / -tozipb in the reference layout (IndependentTreeModelUtils): the
+    reference's own conversion outputs are the oracle -- model0.zip -> .gbt reproduces
+    model1.gbt's payload byte for byte, and model0.gbt -> zip reproduces model0.zip's ``trees``
+    entry byte for byte and its ``model.ini`` JSON."""
+    import gzip
+    import json
+    import zipfile
+    from shifu_amd.steps.misc import gbt_to_zip, zip_to_gbt
+    spec = os.path.join(REF_TR, "example", "readablespec")
+    zip_to_gbt(os.path.join(spec, "model0.zip"), str(tmp_path / "m.gbt"))
+    ours = gzip.decompress(open(tmp_path / "m.gbt", "rb").read())
+    assert ours == gzip.decompress(open(os.path.join(spec, "model1.gbt"), "rb").read())
+    gbt_to_zip(os.path.join(spec, "model0.gbt"), str(tmp_path / "m.zip"))
+    z1, z2 = zipfile.ZipFile(tmp_path / "m.zip"), zipfile.ZipFile(os.path.join(spec, "model0.zip"))
+    assert z1.read("trees") == z2.read("trees")
+    assert json.loads(z1.read("model.ini")) == json.loads(z2.read("model.ini"))
