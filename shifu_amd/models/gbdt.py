@@ -319,16 +319,11 @@ class TreeTrainer:
         for level in range(1, c.max_depth):
             if not nodes:
                 break
-            # slots: built nodes first (contiguous for the all-reduce), then derived; positions
-            # carry the partition's child index -> remap them to the new slot numbering
-            nodes.sort(key=lambda z: (not z["built"], z["tree"], z["id"]))
+            # slots: built nodes first (contiguous for the all-reduce), then derived, by (tree, id);
+            # the partition already wrote these slot ids into pos_node (no remap pass)
+            nodes.sort(key=_slot_key)
             for s_, z in enumerate(nodes):
                 z["slot"] = s_
-            if level > 1:
-                remap = torch.full((len(nodes) + 1,), -1, dtype=torch.int32, device=self.dev)
-                for z in nodes:
-                    remap[z["pidx"]] = z["slot"]
-                pos_node = torch.where(pos_node >= 0, remap[pos_node.clamp(min=0).long()], pos_node)
             slot_of = {(z["tree"], z["id"]): z["slot"] for z in nodes}
             for z in nodes:
                 if not z["built"]:
@@ -388,20 +383,26 @@ class TreeTrainer:
                 children.append((z, lw, rw))
             if last or not children:
                 break
-            # partition rows of split nodes -----------------------------------------------
-            t0 = time.perf_counter()
-            pos2row, pos_node, ranges = self._partition(nodes, split_feat, split_bin, cat_left, pos2row, pos_node)
-            self.timings["partition"] += time.perf_counter() - t0
+            # next level's nodes: build the globally smaller child, derive the other (identical on
+            # all ranks); their slots are fixed now so the partition scatter writes final slot ids
             new_nodes = []
             for z, lw, rw in children:
-                lo, mid, hi = ranges[z["slot"]]
-                # build the globally smaller child, derive the other (identical on all ranks)
                 left_built = lw <= rw
-                k = len(new_nodes)     # child index written by the partition scatter
-                new_nodes.append({"tree": z["tree"], "id": 2 * z["id"], "start": lo, "end": mid,
-                                  "built": left_built, "parent": z["slot"], "pidx": k})
-                new_nodes.append({"tree": z["tree"], "id": 2 * z["id"] + 1, "start": mid, "end": hi,
-                                  "built": not left_built, "parent": z["slot"], "pidx": k + 1})
+                new_nodes.append({"tree": z["tree"], "id": 2 * z["id"], "built": left_built, "parent": z["slot"]})
+                new_nodes.append({"tree": z["tree"], "id": 2 * z["id"] + 1, "built": not left_built,
+                                  "parent": z["slot"]})
+            for s_, nz in enumerate(sorted(new_nodes, key=_slot_key)):
+                nz["slot"] = s_
+            child_slots = {new_nodes[2 * i]["parent"]: (new_nodes[2 * i]["slot"], new_nodes[2 * i + 1]["slot"])
+                           for i in range(len(children))}
+            # partition rows of split nodes -----------------------------------------------
+            t0 = time.perf_counter()
+            pos2row, pos_node, ranges = self._partition(nodes, split_feat, split_bin, cat_left, pos2row, pos_node,
+                                                        child_slots)
+            self.timings["partition"] += time.perf_counter() - t0
+            for i, nz in enumerate(new_nodes):
+                lo, mid, hi = ranges[nz["parent"]]
+                nz["start"], nz["end"] = (lo, mid) if i % 2 == 0 else (mid, hi)
             hist_prev = hist["hist"]
             nodes = new_nodes
         self._nmod, self._npos = 0, n
@@ -592,7 +593,7 @@ class TreeTrainer:
         return self._select_best(cand, nn), cat_order
 
     # ------------------------------------------------------------------------------------
-    def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node):
+    def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots):
         d = self.data
         nn = len(nodes)
         n = self._npos                   # positions (T * N for a forest batch)
@@ -621,12 +622,10 @@ class TreeTrainer:
             child_l = np.full(nn, -1, np.int32)
             child_r = np.full(nn, -1, np.int32)
             ranges = {}
-            k = 0
             for z in nodes:
                 s_ = z["slot"]
                 if split_feat[s_] >= 0:
-                    child_l[s_], child_r[s_] = k, k + 1
-                    k += 2
+                    child_l[s_], child_r[s_] = child_slots[s_]
                 ranges[s_] = (int(starts[s_]), int(starts[s_] + nleft[s_]), int(ends[s_]))
             new_p2r = torch.empty_like(pos2row)
             new_pn = torch.empty_like(pos_node)
@@ -640,7 +639,6 @@ class TreeTrainer:
         new_p2r = pos2row.clone()
         new_pn = torch.full_like(pos_node, -1)
         ranges = {}
-        k = 0
         bins = self._codes()
         for z in nodes:
             s_ = z["slot"]
@@ -659,9 +657,8 @@ class TreeTrainer:
             lrows, rrows = rows[left], rows[~left]
             new_p2r[lo: lo + lrows.numel()] = lrows.int()
             new_p2r[lo + lrows.numel(): hi] = rrows.int()
-            new_pn[lo: lo + lrows.numel()] = k
-            new_pn[lo + lrows.numel(): hi] = k + 1
-            k += 2
+            new_pn[lo: lo + lrows.numel()] = child_slots[s_][0]
+            new_pn[lo + lrows.numel(): hi] = child_slots[s_][1]
             ranges[s_] = (lo, lo + lrows.numel(), hi)
         return new_p2r, new_pn, ranges
 
@@ -824,6 +821,11 @@ class TreeTrainer:
         if not self.cfg.is_gbt and self.trees:
             p /= len(self.trees)
         return p
+
+
+def _slot_key(z):
+    """Slot order of a level's nodes: built first (one contiguous all-reduce), then by tree, id."""
+    return (not z["built"], z["tree"], z["id"])
 
 
 W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histogram fields)
