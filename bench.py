@@ -256,6 +256,9 @@ def main():
             "baseline_note": "baseline = 1.48M rows/s derived from CHANGES.txt:268 (SURVEY §6)",
             "final_train_error": errs[-1] if errs else None,
         }
+        if gpu:      # HBM headroom per rank (RCCL buffers for N > 1 must fit beside the rows)
+            out["hbm_peak_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9
+            out["hbm_total_gb"] = torch.cuda.get_device_properties(dev).total_memory / 1e9
     if info.rank == 0:
         print(json.dumps(out), flush=True)
     dist.shutdown()
