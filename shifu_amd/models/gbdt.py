@@ -410,34 +410,42 @@ class TreeTrainer:
 
     # ------------------------------------------------------------------------------------
     def _make_items(self, nodes, n_built):
-        """Work items (node_slot, lo, hi, group) for built nodes; chunked for parallelism."""
+        """Work items [n, 4] = (node_slot, lo, hi, group) for the built nodes, chunked for
+        parallelism, and node_items [n_nodes, n_groups, max_items] (item ids, -1 padded).
+        Vectorized per node (numpy), order: node, group, chunk."""
         target_items = 2048
+        G = self.ngroups
         rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
-        items, node_items = [], {}
         per = self.items_per_node_group
+        blocks, ks = [], []
         for z in nodes:
-            if not z["built"]:
-                continue
             m = z["end"] - z["start"]
-            if m <= 0:
+            if not z["built"] or m <= 0:
                 continue
             if per is None:
-                share = m / max(1, rows_built)
-                k = max(1, int(round(target_items * share / self.ngroups)))
+                k = max(1, int(round(target_items * (m / max(1, rows_built)) / G)))
                 k = min(k, max(1, m // 4096), 64)
             else:
                 k = per
             step = (m + k - 1) // k
-            for gi in range(self.ngroups):
-                lst = node_items.setdefault((z["slot"], gi), [])
-                for j in range(k):
-                    lo = z["start"] + j * step
-                    hi = min(z["end"], lo + step)
-                    if lo >= hi:
-                        continue
-                    lst.append(len(items))
-                    items.append((z["slot"], lo, hi, gi))
-        return items, node_items
+            k = (m + step - 1) // step                      # chunks that are non-empty
+            lo = z["start"] + np.arange(k, dtype=np.int64) * step
+            hi = np.minimum(z["end"], lo + step)
+            b = np.empty((G, k, 4), dtype=np.int32)
+            b[:, :, 0] = z["slot"]
+            b[:, :, 1] = lo
+            b[:, :, 2] = hi
+            b[:, :, 3] = np.arange(G, dtype=np.int32)[:, None]
+            blocks.append((z["slot"], b.reshape(-1, 4)))
+            ks.append(k)
+        max_items = max(ks + [1])
+        ni = np.full((len(nodes), G, max_items), -1, dtype=np.int32)
+        off = 0
+        for (slot, b), k in zip(blocks, ks):
+            ni[slot, :, :k] = off + np.arange(G * k, dtype=np.int32).reshape(G, k)
+            off += G * k
+        items = np.concatenate([b for _, b in blocks]) if blocks else np.zeros((0, 4), np.int32)
+        return items, ni, max_items
 
     def _build_and_split(self, nodes, n_built, g, w, pos2row, hist_prev):
         F = self.F
@@ -463,11 +471,11 @@ class TreeTrainer:
         fbest = torch.argmax(gains, dim=1)                       # first max -> lowest feature
         rows = cand[torch.arange(nn, device=cand.device), fbest]  # [nn, 8]
         out = torch.cat([fbest.unsqueeze(1).float(), rows[:, 1:2], rows[:, 0:1], rows[:, 2:6], rows[:, 6:7]], 1)
-        out = out.cpu().double().numpy()
-        ok = valid.any(dim=1).cpu().numpy()
+        out = torch.cat([out, valid.any(dim=1, keepdim=True).float()], 1).cpu().double().numpy()   # one sync
+        ok = out[:, -1] > 0
         res = []
         for i in range(nn):
-            f, b, gain, lw, ls, rw, rs, v = out[i]
+            f, b, gain, lw, ls, rw, rs, v = out[i, :8]
             res.append((int(f), int(b), float(gain), float(lw), float(ls), float(rw), float(rs), bool(ok[i])))
         return res
 
@@ -476,18 +484,14 @@ class TreeTrainer:
         d = self.data
         F, nn = self.F, len(nodes)
         st = nat.stream_of(d.bins)
-        items, node_items = self._make_items(nodes, n_built)
-        max_items = max([len(v) for v in node_items.values()] + [1])
-        ni = np.full((nn, self.ngroups, max_items), -1, dtype=np.int32)
-        for (slot, gi), lst in node_items.items():
-            ni[slot, gi, : len(lst)] = lst
+        items, ni, max_items = self._make_items(nodes, n_built)
         ni_t = torch.from_numpy(ni).to(self.dev)
         feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
         cand = torch.zeros(nn, F, 8, dtype=torch.float32, device=self.dev)
         cat_order = torch.zeros(nn, F, NB, dtype=torch.uint8, device=self.dev) if d.is_cat.any() else None
         t0 = time.perf_counter()
-        if items:
-            it = torch.tensor(items, dtype=torch.int32, device=self.dev)
+        if len(items):
+            it = torch.from_numpy(items).to(self.dev)
             slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
             p2r = None if self._root_level else pos2row      # root: positions are rows
             nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, g, it, len(items), slab, F,
@@ -614,8 +618,8 @@ class TreeTrainer:
             # per-node: #left = cum[end-1] - cum[start-1]
             idx_end = torch.from_numpy(np.maximum(ends - 1, 0)).to(self.dev)
             idx_start = torch.from_numpy(np.maximum(starts - 1, 0)).to(self.dev)
-            ce = cum[idx_end].cpu().numpy().astype(np.int64)
-            cb = cum[idx_start].cpu().numpy().astype(np.int64)
+            cecb = torch.stack([cum[idx_end], cum[idx_start]]).cpu().numpy().astype(np.int64)   # one D2H sync
+            ce, cb = cecb[0], cecb[1]
             cb = np.where(starts > 0, cb, 0)
             ce = np.where(ends > starts, ce, cb)
             nleft = ce - cb
