@@ -609,7 +609,7 @@ class TrainStep:
                 stop[0] = True
         ckpt = os.path.join(ms.pf.checkpoint_dir, f"tree_trainer{tid}.pt")
         if self.resume and os.path.exists(ckpt):
-            tt.load_state_dict(torch.load(ckpt, weights_only=False))    # our own checkpoint file
+            tt.load_state_dict(torch.load(ckpt, weights_only=True))
             _log.info("resumed trainer %d from checkpoint with %d trees", tid, len(tt.trees))
         interval = checkpoint_interval(p, max(1, tree_num // 10))   # DTOutput: tmp models every treeNum/10
         wd = IterationWatchdog(iteration_limit(800.0), "tree").__enter__()
