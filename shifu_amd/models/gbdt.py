@@ -240,6 +240,7 @@ class TreeTrainer:
         self._codes_cache = None
         self._nmod, self._npos = 0, data.n
         self._pending: list = []        # RF trees grown ahead in a forest batch
+        self._fuse = None                # (pred, scale): GBT prediction update fused into the partition
 
     def _codes(self) -> torch.Tensor:
         """Row-major codes for the CPU paths (built once)."""
@@ -381,7 +382,19 @@ class TreeTrainer:
                     tree.value[cid] = cs / cw if cw != 0 else 0.0
                     tree.wgt_cnt[cid] = cw
                 children.append((z, lw, rw))
+            fuse = self._fuse if (self.gpu and T == 1) else None
+            if fuse is not None:
+                tree0 = trees[0]
+                nv = np.zeros((3, len(nodes)), dtype=np.float32)
+                for z in nodes:
+                    nv[0, z["slot"]] = tree0.value[z["id"]]
+                    if split_feat[z["slot"]] >= 0:
+                        nv[1, z["slot"]] = tree0.value[2 * z["id"]]
+                        nv[2, z["slot"]] = tree0.value[2 * z["id"] + 1]
+                leaf_vals = torch.from_numpy(nv).to(self.dev)
             if last or not children:
+                if fuse is not None:     # every remaining row gets its final leaf (child) value
+                    self._leaf_update(nodes, split_feat, split_bin, cat_left, pos2row, pos_node, leaf_vals, fuse)
                 break
             # next level's nodes: build the globally smaller child, derive the other (identical on
             # all ranks); their slots are fixed now so the partition scatter writes final slot ids
@@ -398,7 +411,7 @@ class TreeTrainer:
             # partition rows of split nodes -----------------------------------------------
             t0 = time.perf_counter()
             pos2row, pos_node, ranges = self._partition(nodes, split_feat, split_bin, cat_left, pos2row, pos_node,
-                                                        child_slots)
+                                                        child_slots, (leaf_vals, fuse) if fuse is not None else None)
             self.timings["partition"] += time.perf_counter() - t0
             for i, nz in enumerate(new_nodes):
                 lo, mid, hi = ranges[nz["parent"]]
@@ -597,7 +610,21 @@ class TreeTrainer:
         return self._select_best(cand, nn), cat_order
 
     # ------------------------------------------------------------------------------------
-    def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots):
+    def _leaf_update(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, leaf_vals, fuse):
+        """Final level of a fused GBT tree: pred[row] += scale * value of the row's leaf (split nodes:
+        the child its bin goes to), in the partition-flag kernel without a flag output."""
+        from ..ops import _native as nat
+        d = self.data
+        sf = torch.from_numpy(split_feat).to(self.dev)
+        sb = torch.from_numpy(split_bin).to(self.dev)
+        cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
+        pred, scale = fuse
+        self._leaf_done = True
+        nat.call_hip("shifu_gbdt_partition_flag", d.bins, d.group_stride, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
+                     None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale), 1,
+                     nat.stream_of(d.bins))
+
+    def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots, leaf=None):
         d = self.data
         nn = len(nodes)
         n = self._npos                   # positions (T * N for a forest batch)
@@ -611,9 +638,11 @@ class TreeTrainer:
             sb = torch.from_numpy(split_bin).to(self.dev)
             cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
             flag = torch.empty(n, dtype=torch.int32, device=self.dev)
-            nat.call_hip("shifu_gbdt_partition_flag", d.bins.data_ptr(), d.group_stride, pos2row.data_ptr(),
-                         pos_node.data_ptr(), sf.data_ptr(), sb.data_ptr(), cl.data_ptr(), self.is_cat_t.data_ptr(),
-                         flag.data_ptr(), n, self._nmod, st)
+            lv, (pred, scale) = leaf if leaf is not None else (None, (None, 0.0))
+            # non-split nodes' rows get their leaf value here (fused GBT prediction update)
+            nat.call_hip("shifu_gbdt_partition_flag", d.bins, d.group_stride, pos2row, pos_node, sf, sb, cl,
+                         self.is_cat_t, flag, n, self._nmod, pred, None if lv is None else lv[0], None, None,
+                         float(scale), 0, st)
             cum = torch.cumsum(flag, 0, dtype=torch.int32)
             # per-node: #left = cum[end-1] - cum[start-1]
             idx_end = torch.from_numpy(np.maximum(ends - 1, 0)).to(self.dev)
@@ -727,14 +756,25 @@ class TreeTrainer:
                     g = d.y
                 else:
                     g = out
-                tree = self.grow_tree(g, w, 1.0 if tid == 0 else c.learning_rate, tid)
+                scale = 1.0 if tid == 0 else c.learning_rate
+                fused = self.gpu and not (tid > 0 and c.dropout_rate > 0.0)
+                if fused:            # pred += scale * leaf value inside the partition passes
+                    if tid == 0:
+                        self.pred.zero_()
+                    self._fuse = (self.pred, scale)
+                    self._leaf_done = False
+                try:
+                    tree = self.grow_tree(g, w, scale, tid)
+                finally:
+                    self._fuse = None
                 t0 = time.perf_counter()
                 keep = None
                 if tid > 0 and c.dropout_rate > 0.0:
                     # DTWorker :634-638: each row skips this tree's update with prob. DropoutRate
                     keep = (torch.rand(d.n, device=self.dev, generator=self.tgen) >= c.dropout_rate).float()
                     before = self.pred.clone()
-                self.apply_tree(tree, d, self.pred, tree.weight, tid == 0)
+                if not fused or not self._leaf_done:      # (max_depth 1: no level pass ran)
+                    self.apply_tree(tree, d, self.pred, tree.weight, tid == 0)
                 if keep is not None:
                     self.pred.copy_(before + (self.pred - before) * keep)
                 if self.valid is not None:

@@ -407,9 +407,14 @@ struct PartArgs {
   const int* split_bin;         // [n_nodes] numeric: left iff bin <= split_bin
   const uint32_t* cat_left;     // [n_nodes][8] categorical left bitset (bin b left iff bit set)
   const uint8_t* is_cat;        // [F]
-  int* flag;                    // [N] out: 1 left, 0 right, for split nodes; 0 otherwise
+  int* flag;                    // [N] out: 1 left, 0 right, for split nodes; 0 otherwise (nullable)
   long n;
   long nmod;                    // > 0: forest batch (pos2row = tree * nmod + row)
+  // fused GBT prediction update (replaces walking every row through the finished tree):
+  // rows of nodes that stay leaves get pred += scale * node_val; on the final level rows of
+  // split nodes get the value of the child they go to
+  float* pred; const float* node_val; const float* child_l_val; const float* child_r_val;
+  float scale; int final_level;
 };
 
 __global__ void gbdt_partition_flag_kernel(PartArgs a) {
@@ -423,8 +428,12 @@ __global__ void gbdt_partition_flag_kernel(PartArgs a) {
     const uint32_t b = a.bins[(size_t)(f >> 5) * a.gs + (size_t)row * 32 + (f & 31)];
     if (a.is_cat[f]) fl = (a.cat_left[node * 8 + (b >> 5)] >> (b & 31)) & 1;
     else fl = (int)b <= a.split_bin[node] ? 1 : 0;
+    if (a.pred && a.final_level) a.pred[row] += a.scale * (fl ? a.child_l_val[node] : a.child_r_val[node]);
+  } else if (a.pred && node >= 0) {
+    const long v = a.pos2row[p];
+    a.pred[a.nmod ? v % a.nmod : v] += a.scale * a.node_val[node];
   }
-  a.flag[p] = fl;
+  if (a.flag) a.flag[p] = fl;
 }
 
 // scatter: positions of split nodes move to [start + rank_left] or [start + n_left + rank_right]
@@ -557,9 +566,13 @@ SHIFU_API int shifu_gbdt_split(const void* slab, const int* node_items, int max_
 
 SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const int* pos2row, const int* pos_node,
                                         const int* split_feat, const int* split_bin, const void* cat_left,
-                                        const void* is_cat, int* flag, long n, long nmod, hipStream_t stream) {
+                                        const void* is_cat, int* flag, long n, long nmod, float* pred,
+                                        const float* node_val, const float* child_l_val,
+                                        const float* child_r_val, float scale, int final_level,
+                                        hipStream_t stream) {
   PartArgs a{(const uint8_t*)bins, gs, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
-             (const uint8_t*)is_cat, flag, n, nmod};
+             (const uint8_t*)is_cat, flag, n, nmod, pred, node_val, child_l_val, child_r_val, scale,
+             final_level};
   hipLaunchKernelGGL(gbdt_partition_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
