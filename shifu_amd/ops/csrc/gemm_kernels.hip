@@ -239,6 +239,18 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
     }
     __syncthreads();
     const int c = tid & 15;
+    // dgrad: issue all 8 H row-segment loads of this thread before the passes (the accumulators
+    // are dead here, so the 8 x 16 B in flight cost no occupancy); rows clamped to M - 1 and
+    // columns to ldh - 8 keep every load in bounds without a branch around it
+    uint4 hreg[8];
+    if constexpr (EPI == EPI_DACT && !HPF) {
+      const int nh = min(n0 + c * 8, (int)p.ldh - 8);
+#pragma unroll
+      for (int pass = 0; pass < 8; ++pass) {
+        const int mh = min(m0 + pass * 16 + (tid >> 4), p.M - 1);
+        hreg[pass] = *(const uint4*)(p.H + (size_t)mh * p.ldh + nh);
+      }
+    }
 #pragma unroll
     for (int pass = 0; pass < 8; ++pass) {
       const int ml = pass * 16 + (tid >> 4);
@@ -248,7 +260,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       if constexpr (EPI == EPI_DACT) {
         uint4 h;
         if constexpr (HPF) h = (n + 8 <= p.N) ? hpre[pass] : *(const uint4*)(p.H + (size_t)m * p.ldh + n);
-        else h = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
+        else h = hreg[pass];
         const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
         uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
