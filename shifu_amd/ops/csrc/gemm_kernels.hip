@@ -213,6 +213,19 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
     // phase 2 writes whole 256-B row segments with 16-B stores (and, for dgrad, reads the
     // matching H row segment coalesced) instead of 16 rows x 32 B per wave instruction.
     char* Cs = smem;                       // [128][256 B]; loop's last barrier freed the tiles
+    const int c = tid & 15;
+    // dgrad: issue all 8 H row-segment loads of this thread up front, so they are in flight while
+    // the tile is staged through LDS (8 x 16 B per lane instead of one load per pass); rows clamped
+    // to M - 1 and columns to ldh - 8 keep every load in bounds without a branch around it
+    uint4 hreg[8];
+    if constexpr (EPI == EPI_DACT && !HPF) {
+      const int nh = min(n0 + c * 8, (int)p.ldh - 8);
+#pragma unroll
+      for (int pass = 0; pass < 8; ++pass) {
+        const int mh = min(m0 + pass * 16 + (tid >> 4), p.M - 1);
+        hreg[pass] = *(const uint4*)(p.H + (size_t)mh * p.ldh + nh);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;       // local column (multiple of 4)
@@ -238,19 +251,6 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       }
     }
     __syncthreads();
-    const int c = tid & 15;
-    // dgrad: issue all 8 H row-segment loads of this thread before the passes (the accumulators
-    // are dead here, so the 8 x 16 B in flight cost no occupancy); rows clamped to M - 1 and
-    // columns to ldh - 8 keep every load in bounds without a branch around it
-    uint4 hreg[8];
-    if constexpr (EPI == EPI_DACT && !HPF) {
-      const int nh = min(n0 + c * 8, (int)p.ldh - 8);
-#pragma unroll
-      for (int pass = 0; pass < 8; ++pass) {
-        const int mh = min(m0 + pass * 16 + (tid >> 4), p.M - 1);
-        hreg[pass] = *(const uint4*)(p.H + (size_t)mh * p.ldh + nh);
-      }
-    }
 #pragma unroll
     for (int pass = 0; pass < 8; ++pass) {
       const int ml = pass * 16 + (tid >> 4);
