@@ -764,10 +764,14 @@ template <int ACT>
 __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, HeadArgs h) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * 256;
-  f32x4 acc[4][8];
-  gemm8_mainloop(p, acc, m0, 0, smem);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
+  // the epilogue's per-row inputs (targets, significance) are loaded before the main loop so
+  // their HBM latency hides behind it (one block per CU: nothing else would cover it)
+  const int my = min(m0 + (tid & 255), p.M - 1);
+  const float y_pf = h.Y[my], s_pf = h.S ? h.S[my] : 1.f;
+  f32x4 acc[4][8];
+  gemm8_mainloop(p, acc, m0, 0, smem);
   float* red = (float*)(smem + 2 * G8_BUF);          // [2 wr][4 wc][128] row partials of z_out
   float* dl = red + 1024;                            // [256] output deltas
   float* gred = dl + 256;                            // [2 wr][256] output-wgrad partials
@@ -814,7 +818,7 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
     const int m = m0 + tid;
     float dlt = 0.f;
     if (m < p.M) {
-      const float y = h.Y[m], sg = h.S ? h.S[m] : 1.f;
+      const float y = y_pf, sg = s_pf;
       const float a = act_fwd(h.out_act, z), e = y - a;
       if (h.loss == 1) {
         dlt = e * sg;
