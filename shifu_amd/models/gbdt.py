@@ -467,7 +467,10 @@ class TreeTrainer:
         imp = IMPURITY_IDS[self.cfg.impurity]
         min_inst = float(self.cfg.min_instances_per_node)
         min_gain = float(self.cfg.min_info_gain)
-        hist = torch.zeros(nn, 2, F, NB, dtype=torch.int64, device=self.dev)
+        # GPU: the split kernel writes every (node, feature, bin) entry (built: mode 0, derived: mode 1),
+        # so no zero fill of the level's histograms (up to 64 nodes x 4 MB)
+        alloc = torch.empty if self.gpu else torch.zeros
+        hist = alloc(nn, 2, F, NB, dtype=torch.int64, device=self.dev)
         if self.gpu:
             best, cat_order = self._build_and_split_hip(nodes, n_built, g, w, pos2row, hist_prev, hist, mask,
                                                         imp, min_inst, min_gain)
