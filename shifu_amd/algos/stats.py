@@ -340,6 +340,10 @@ def pearson_correlation(mats: np.ndarray, device=None):
     sxx = X2.t() @ M
     syy = M.t() @ X2
     sxy = Xz.t() @ Xz
+    from ..parallel import dist
+    if dist.info().world_size > 1:       # row-sharded: the six F x F sums in one all-reduce
+        st = dist.all_reduce_(torch.stack([n, sx, sy, sxx, syy, sxy]))
+        n, sx, sy, sxx, syy, sxy = st.unbind(0)
     num = sxy - sx * sy / n.clamp(min=1)
     den = torch.sqrt((sxx - sx * sx / n.clamp(min=1)).clamp(min=0) * (syy - sy * sy / n.clamp(min=1)).clamp(min=0))
     corr = torch.where(den > 0, num / den, torch.zeros_like(num))

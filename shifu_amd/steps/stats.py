@@ -28,8 +28,9 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
     mc = ms.mc
     cols = ms.stats_columns()
     from ..parallel import dist
-    if (rebin or correlation or psi) and dist.info().world_size > 1:
-        # rebin / correlation / PSI: rank 0 alone (the others wait at the verb's final barrier)
+    if (rebin or psi) and not correlation and dist.info().world_size > 1:
+        # rebin / PSI: rank 0 alone (the others wait at the verb's final barrier); correlation is
+        # data parallel (row-sharded pairwise sums, one all-reduce)
         if dist.info().rank == 0:
             with dist.local_only():
                 return run_stats(root, correlation, psi, rebin, expected_bins, iv_keep_ratio,
@@ -80,7 +81,8 @@ def run_correlation(ms: ModelSet, device=None):
     written as ``correlation.csv`` (header row + one row per column, ``ColumnConfig`` order)."""
     mc = ms.mc
     cols = [c for c in ms.stats_columns() if c.bin_boundary or c.bin_category]
-    md = ms.load_raw(cols)
+    from .base import _writer, shard_model_data
+    md = shard_model_data(ms.load_raw(cols))
     mats = []
     for c in cols:
         col = md.table[c.name]
@@ -91,6 +93,8 @@ def run_correlation(ms: ModelSet, device=None):
             mats.append(v)
     X = np.stack(mats, 1) if mats else np.zeros((md.n, 0))
     C = S.pearson_correlation(X, device)
+    if not _writer():
+        return C, [c.num for c in cols]
     path = ms.pf.correlation_csv
     # StatsModelProcessor.computeCorrValue layout (:490-590): an index line, a name line, then one
     # row per computed column: "<num>,<name>,<corr with every ColumnConfig column, ', '-joined>"

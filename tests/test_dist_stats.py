@@ -200,3 +200,22 @@ def test_varsel_se_and_posttrain_two_ranks_match_single(tmp_path):
     assert ba.keys() == bb.keys() and all(ba[k] for k in ba)
     for k in ba:
         assert np.max(np.abs(np.array(ba[k]) - np.array(bb[k]))) <= 1, k
+
+
+def test_correlation_two_ranks_match_single(tmp_path):
+    """`stats -c` data parallel: row-sharded pairwise-complete sums all-reduced once == one process."""
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import read_correlation, run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=1301, n_num=6, n_cat=2)
+    run_init(a)
+    run_stats(a)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    run_stats(a, correlation=True)
+    mp.start_processes(_rank_cli, args=(2, _port(), b, "stats -c"), nprocs=2, join=True, start_method="spawn")
+    na, ca = read_correlation(os.path.join(a, "correlation.csv"))
+    nb, cb = read_correlation(os.path.join(b, "correlation.csv"))
+    assert na == nb and len(na) >= 6
+    np.testing.assert_allclose(ca, cb, atol=1e-10)
