@@ -285,10 +285,61 @@ def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int 
 def compute_psi(mc, ccs, md, unit_column: str):
     """Population stability per column across the units of ``psiColumnName``
     (P/PSI.pig:19-46, PSICalculatorUDF): PSI = sum_units sum_bins (a-e) ln(a/e) with e the
-    overall bin distribution and a the unit's; also records ``unitStats``."""
+    overall bin distribution and a the unit's; also records ``unitStats``.  Data parallel: the
+    unit set is the union over ranks and the (unit, bin) counts of every column are all-reduced
+    in one bucket (the PopulationCounterUDF -> PSICalculatorUDF shuffle)."""
+    from ..parallel import dist
     if unit_column not in md.table:
         _log.warning("psiColumnName %s not in data", unit_column)
         return ccs
+    units_s = md.table[unit_column].strings()
+    units = sorted(set(units_s))
+    if dist.info().world_size > 1:
+        units = sorted(set().union(*dist.all_gather_objects(units)))
+    uidx = {u: i for i, u in enumerate(units)}
+    ucode = np.array([uidx[u] for u in units_s], dtype=np.int64) if len(units_s) else np.zeros(0, np.int64)
+    cols, counts = [], []
+    for cc in ccs:
+        if cc.is_target() or cc.is_meta() or cc.name not in md.table:
+            continue
+        col = md.table[cc.name]
+        if cc.is_categorical():
+            cats = cc.bin_category or []
+            codes = col.values if col.kind == "str" else None
+            if codes is None:
+                continue
+            bidx = B.category_index(codes, col.dictionary, cats)
+            nb = len(cats) + 1
+        else:
+            bb = cc.bin_boundary
+            if not bb:
+                continue
+            bidx = B.bin_index_numeric(col.numeric(), bb)
+            nb = len(bb) + 1
+        cnt = np.bincount(ucode * nb + bidx, minlength=len(units) * nb).astype(np.float64)
+        cols.append((cc, nb))
+        counts.append(cnt)
+    if counts and dist.info().world_size > 1:
+        flat = dist.all_reduce_np(np.concatenate(counts))
+        off = 0
+        for i, c in enumerate(counts):
+            counts[i] = flat[off:off + c.size]
+            off += c.size
+    for (cc, nb), cnt in zip(cols, counts):
+        per_unit = cnt.reshape(len(units), nb)
+        exp = per_unit.sum(0)
+        exp = exp / max(exp.sum(), 1)
+        psi = 0.0
+        unit_stats = []
+        for ui, u in enumerate(units):
+            act = per_unit[ui] / max(per_unit[ui].sum(), 1)
+            ok = (act > 0) & (exp > 0)
+            pu = float(((act[ok] - exp[ok]) * np.log(act[ok] / exp[ok])).sum())
+            psi += pu
+            unit_stats.append(f"{u}:{pu}")
+        cc.stats["psi"] = psi
+        cc.stats["unitStats"] = unit_stats
+    return ccs
     units_s = md.table[unit_column].strings()
     units = sorted(set(units_s))
     for cc in ccs:

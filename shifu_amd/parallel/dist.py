@@ -136,6 +136,15 @@ def all_reduce_np(a, op: str = "sum"):
     return t.cpu().numpy()
 
 
+def all_gather_objects(obj) -> list:
+    """Every rank's (picklable, small) ``obj``, in rank order."""
+    if not _active():
+        return [obj]
+    out = [None] * tdist.get_world_size()
+    tdist.all_gather_object(out, obj)
+    return out
+
+
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if _active():
         tdist.broadcast(t, src=src)

@@ -28,9 +28,9 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
     mc = ms.mc
     cols = ms.stats_columns()
     from ..parallel import dist
-    if (rebin or psi) and not correlation and dist.info().world_size > 1:
-        # rebin / PSI: rank 0 alone (the others wait at the verb's final barrier); correlation is
-        # data parallel (row-sharded pairwise sums, one all-reduce)
+    if rebin and not correlation and dist.info().world_size > 1:
+        # rebin (ColumnConfig only, no data pass): rank 0 alone; correlation and PSI are data
+        # parallel (row-sharded sums / counts, one all-reduce each)
         if dist.info().rank == 0:
             with dist.local_only():
                 return run_stats(root, correlation, psi, rebin, expected_bins, iv_keep_ratio,
@@ -59,16 +59,12 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
         ms.save_cc(backup=True)
     if dist.info().world_size > 1:
         dist.barrier()
-        if mc.stats.get("psiColumnName"):      # PSI over the unit column: rank 0 alone
-            if dist.info().rank == 0:
-                with dist.local_only():
-                    return run_stats(root, False, True, False, device=device)
-        return 0
     if psi or mc.stats.get("psiColumnName"):
         unit = mc.stats.get("psiColumnName")
         if unit:
+            from .base import shard_model_data
             cc_unit = [c for c in ms.ccs if c.name == unit]
-            md = ms.load_raw(cols + cc_unit)
+            md = shard_model_data(ms.load_raw(cols + cc_unit))
             S.compute_psi(mc, ms.ccs, md, unit)
             ms.save_cc()
         else:

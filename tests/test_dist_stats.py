@@ -219,3 +219,33 @@ def test_correlation_two_ranks_match_single(tmp_path):
     nb, cb = read_correlation(os.path.join(b, "correlation.csv"))
     assert na == nb and len(na) >= 6
     np.testing.assert_allclose(ca, cb, atol=1e-10)
+
+
+def test_psi_two_ranks_match_single(tmp_path):
+    """`stats -p` data parallel: global unit set + all-reduced (unit, bin) counts == one process."""
+    from shifu_amd.config.column_config import load_column_configs
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=1250, n_num=5, n_cat=2)
+    mc = ModelConfig.load(os.path.join(a, "ModelConfig.json"))
+    mc.stats["psiColumnName"] = "cat_0"
+    mc.save()
+    run_init(a)
+    run_stats(a)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    from shifu_amd.config.column_config import save_column_configs
+    ccb = load_column_configs(os.path.join(b, "ColumnConfig.json"))
+    for c in ccb:                           # b's PSI must come from the 2-rank run
+        c.stats["psi"] = None
+    save_column_configs(ccb, os.path.join(b, "ColumnConfig.json"))
+    run_stats(a, psi=True)
+    mp.start_processes(_rank_cli, args=(2, _port(), b, "stats -p"), nprocs=2, join=True, start_method="spawn")
+    pa = {c.name: c.stats.get("psi") for c in load_column_configs(os.path.join(a, "ColumnConfig.json"))}
+    pb = {c.name: c.stats.get("psi") for c in load_column_configs(os.path.join(b, "ColumnConfig.json"))}
+    keys = [k for k in pa if pa[k] is not None]
+    assert keys and all(pb[k] is not None for k in keys)
+    np.testing.assert_allclose([pa[k] for k in keys], [pb[k] for k in keys], rtol=1e-9, atol=1e-12)
