@@ -173,8 +173,9 @@ def _gather_scores(md, res, tags, meta_names):
     from ..parallel import dist
     payload = (np.asarray(tags), np.asarray(md.w), {k: np.asarray(v) for k, v in res.items()},
                {m: (md.table[m].strings() if m in md.table else np.array([""] * md.n)) for m in meta_names})
-    parts = [None] * dist.info().world_size
-    tdist.all_gather_object(parts, payload)
+    # gathered on rank 0 only (the other ranks neither receive nor hold the full score set)
+    parts = [None] * dist.info().world_size if dist.info().rank == 0 else None
+    tdist.gather_object(payload, parts, dst=0)
     if dist.info().rank != 0:
         return md, res, tags
     tags = np.concatenate([p[0] for p in parts])
