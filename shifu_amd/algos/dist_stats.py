@@ -49,10 +49,7 @@ def _allreduce(t: torch.Tensor, op="sum") -> torch.Tensor:
 
 
 def _gather_objects(obj):
-    import torch.distributed as tdist
-    out = [None] * dist.info().world_size
-    tdist.all_gather_object(out, obj)
-    return out
+    return dist.all_gather_objects(obj)
 
 
 # ---- order-preserving float64 <-> int64 keys ----------------------------------------------------
