@@ -13,7 +13,11 @@ weights).  ``value`` = total rows processed per second over all ranks.
 
     python bench.py --gpus 1 --steps 5 --warmup 2
     torchrun --nproc-per-node 8 bench.py --gpus 8 ...
-    python bench.py --model gbdt    # GBDT rounds/sec (500 trees depth 7, 256 bins) config
+    python bench.py --model gbdt    # GBDT rounds/sec (500 trees depth 7, 256 bins) config alone
+
+The default line carries both halves of the metric: ``value`` = MLP rows/s, and after the MLP
+rows are freed the same process times ``--gbdt-steps`` boosting rounds on 100M x 1000 uint8 codes
+per GPU (``gbdt_rounds_per_s`` / ``gbdt_ms_per_round``; ``--gbdt-steps 0`` skips it).
     python bench.py --model varsel  # 10k-feature MLP + SE varselect config
     python bench.py --model lr      # LR 100k-row CSV local (CPU plumbing) config
 """
@@ -96,6 +100,29 @@ def bench_mlp(a, dev, info):
     log(f"[bench] train errors {['%.6f' % e for e in errs]}")
     flops_row = 2 * (a.cols * 500 + 500 * 200 + 200) * 2 + 2 * 500 * 200   # fwd+wgrad all, dgrad layer2
     return dt, errs, flops_row
+
+
+def gbdt_half(a, dev, info):
+    """The metric's second half ("+ GBDT rounds/sec"), timed in the same process after the MLP
+    rows are freed: BASELINE config 3 (GBT depth 7, 256-bin histograms, 100M rows x 1000 cols per
+    GPU, uint8 codes), ``--gbdt-steps`` boosting rounds after ``--gbdt-warmup`` untimed ones, each
+    bracketed like the MLP steps (barrier + synchronize, max over ranks)."""
+    import gc
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(dev)
+    from types import SimpleNamespace
+    rows = a.gbdt_rows or (100_000_000 if dev.type == "cuda" else 2_000)
+    g = SimpleNamespace(rows=rows, cols=a.cols, steps=a.gbdt_steps, warmup=a.gbdt_warmup)
+    t0 = time.time()
+    res = bench_gbdt(g, dev, info)
+    log(f"[bench] gbdt: {res['ms_per_step']:.1f} ms/round ({time.time() - t0:.1f}s incl. data generation)")
+    return {"gbdt_rounds_per_s": res["value"], "gbdt_ms_per_round": res["ms_per_step"],
+            "gbdt_steps": a.gbdt_steps, "gbdt_warmup": a.gbdt_warmup, "gbdt_train_error": res.get("train_error"),
+            "gbdt_config": {"model": res["config"]["model"], "rows_per_gpu": rows, "n_cols": a.cols,
+                            "global_rows": rows * info.world_size, "dtype": res["dtype"],
+                            "parallelism": res["config"]["parallelism"]}}
 
 
 def bench_gbdt(a, dev, info):
@@ -210,6 +237,10 @@ def main():
     ap.add_argument("--cols", type=int, default=1000)
     ap.add_argument("--chunk-rows", type=int, default=1 << 21)   # 2M-row chunks: +1.6% vs 1M (profiles/r1d)
     ap.add_argument("--propagation", default="R")
+    ap.add_argument("--gbdt-rows", type=int, default=None,
+                    help="rows per GPU of the GBDT half of the default line (default 100M on GPU)")
+    ap.add_argument("--gbdt-steps", type=int, default=5, help="timed boosting rounds (0 = MLP only)")
+    ap.add_argument("--gbdt-warmup", type=int, default=1)
     a = ap.parse_args()
 
     from shifu_amd.parallel import dist
@@ -259,6 +290,8 @@ def main():
         if gpu:      # HBM headroom per rank (RCCL buffers for N > 1 must fit beside the rows)
             out["hbm_peak_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9
             out["hbm_total_gb"] = torch.cuda.get_device_properties(dev).total_memory / 1e9
+        if a.gbdt_steps > 0:
+            out.update(gbdt_half(a, dev, info))
     if info.rank == 0:
         print(json.dumps(out), flush=True)
     dist.shutdown()
