@@ -452,6 +452,9 @@ class MLPTrainer:
                              adam_beta1, adam_beta2, learning_decay, reg, reg_level, fixed)
         self.chunk_rows = int(chunk_rows)
         self.wgrad_splits = wgrad_splits
+        # ring-pipelined TN wgrad (LDS-DMA ring 4 k-steps deep, fixed-order split reduction:
+        # bitwise reproducible); SHIFU_WGRAD_RING=0 restores the 128x128 split-K atomics kernel
+        self.wgrad_ring = os.environ.get("SHIFU_WGRAD_RING", "1") != "0"
         self.fused_tail = self._tail_eligible()
         self.fused_head = (not self.fused_tail) and self._head_eligible()
         self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
@@ -510,6 +513,13 @@ class MLPTrainer:
             need_d = ACT_IDS[self.spec.acts[l - 1]] not in ACT_DERIV_FROM_OUTPUT
             ws["derivs"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device)
                                 if need_d else None)
+        # fp32 split partials of the ring wgrad (ops/csrc/gemm_ring.hip): one buffer for every layer
+        ws["slab"] = None
+        if self.gpu and self.wgrad_ring:
+            from ..ops import _native as nat
+            need = max(nat.hip().shifu_wgrad_ring_ws(rows, self.spec.hidden[l], kp[l]) for l in range(L))
+            if need > 0:
+                ws["slab"] = torch.empty(need // 4, dtype=torch.float32, device=self.device)
         self._ws = ws
         return ws
 
@@ -653,7 +663,10 @@ class MLPTrainer:
                 spl = max(1, min(mc // 256, 1024 // max(1, ntiles)))
             else:
                 spl = splits
-            if l == 0 and dtr:
+            if self.wgrad_ring and ws["slab"] is not None and mc >= 4096 and not (l == 0 and dtr):
+                nat.call_hip("shifu_wgrad_ring", dels[l + 1], kp[l + 1], acts[l], kp[l], gv[l], kp[l],
+                             mc, sp.hidden[l], kp[l], ws["slab"], ws["slab"].numel() * 4, st)
+            elif l == 0 and dtr:
                 nat.call_hip("shifu_wgrad_tn_dt", dels[1].data_ptr(), ldt, acts[0].data_ptr(), kp[0],
                              gv[0].data_ptr(), kp[0], mc, sp.hidden[0], kp[0], spl, st)
             else:

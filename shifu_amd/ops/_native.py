@@ -43,6 +43,9 @@ HIP_SIGNATURES = {
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
     "shifu_cast_bf16": "plpliis",
     "shifu_transpose_cast": "plpiiis",
+    # gemm_ring.hip
+    "shifu_wgrad_ring": "plplpl" "iii" "pl" "s",
+    "shifu_wgrad_ring_ws": ("iii", "l"),
     # mlp_tail.hip
     "shifu_mlp_tail": "plpiiif" "pipl" "piiif" "plpp" "i" "plpl" "iif" "ii" "s",
     # gbdt_kernels.hip
