@@ -46,6 +46,10 @@ HIP_SIGNATURES = {
     # gemm_ring.hip
     "shifu_wgrad_ring": "plplpl" "iii" "pl" "s",
     "shifu_wgrad_ring_ws": ("iii", "l"),
+    "shifu_gemm_ring_nt": "plplipl" "iiiiiii" "s",
+    "shifu_ring_set_stamp": "p",
+    "shifu_ring_set_mf": "i",
+    "shifu_ring_set_dmamma": "i",
     # mlp_tail.hip
     "shifu_mlp_tail": "plpiiif" "pipl" "piiif" "plpp" "i" "plpl" "iif" "ii" "s",
     # gbdt_kernels.hip

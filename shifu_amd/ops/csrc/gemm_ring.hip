@@ -44,6 +44,7 @@ namespace {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;    // MFMA 32x32 accumulator fragment
 
 constexpr int RG_T = 512;
 constexpr int RG_NSLOT = 5;
@@ -67,6 +68,29 @@ __device__ __forceinline__ s16x4 rg_tr_read(uint32_t lds_addr) {
   return v;
 }
 
+template <int OFF>
+__device__ __forceinline__ s16x4 rg_tr_read_o(uint32_t lds_addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(lds_addr), "n"(OFF));
+  return v;
+}
+__device__ __forceinline__ bf16x8 rg_read_b128(uint32_t lds_addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ bf16x8 rg_read_b128_o(uint32_t lds_addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(lds_addr), "n"(OFF));
+  return v;
+}
+// 8-byte global store as inline asm: always exactly one instruction per call (the vmcnt counts
+// of the NT ring assume a fixed number of stores per tile)
+__device__ __forceinline__ void rg_store_b64(void* gaddr, uint2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off" :: "v"(gaddr), "v"(v) : "memory");
+}
+
 __device__ __forceinline__ int rg_f(int r) { return ((r & 3) << 2) | (((r >> 3) & 1) << 1); }
 // byte offset of the 8-byte quad holding columns col..col+3 (col % 4 == 0) of image row r
 __device__ __forceinline__ int rg_off(int r, int col) {
@@ -78,8 +102,12 @@ struct RingTNArgs {
   const bf16_t* X; long ldx;   // [M, ldx] layer inputs
   float* slab;                 // [S][NT * 256][KT * 256] fp32 partial sums
   int nsteps, S, NT, KT;       // nsteps = whole 32-row k-steps; split s takes steps s, s+S, ...
+  unsigned long long* dbg;     // STAMP builds only: per-wave segment cycle sums
 };
 
+// STAMP (diagnostic build, never the shipped path): s_memtime around every segment, per-wave sums
+// [dma issue, fragment read issue, waits, LD barrier, MFMA issue, MMA barrier] written at the end
+template <int MF, bool STAMP, bool DMA_IN_MMA>
 __global__ __launch_bounds__(RG_T, 2) void ring_tn_kernel(RingTNArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntiles = p.NT * p.KT;
@@ -91,99 +119,212 @@ __global__ __launch_bounds__(RG_T, 2) void ring_tn_kernel(RingTNArgs p) {
   const int wn = wid >> 2, wk = wid & 3;
   const bool lag = wid >= 4;
 
-  // ---- LDS-DMA sources: thread instr i (0/1) per image fills LDS bytes (i*8 + wid)*1024 + lane*16
-  const bf16_t* srcD[2];
-  const bf16_t* srcX[2];
+  // ---- LDS-DMA: thread instr i (0/1) per image fills LDS bytes (i*8 + wid)*1024 + lane*16;
+  // wave-uniform step base + per-lane 32-bit byte offsets (saddr form, no 64-bit math per step)
+  uint32_t offD[2], offX[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int P = (i * 8 + wid) * 1024 + lane * 16;
     const int row = P >> 9, lc = ((P >> 4) & 31) ^ rg_f(row);
-    const long r = (long)split * 32 + row;
-    srcD[i] = p.D + r * p.ldd + min(n0 + lc * 8, (int)p.ldd - 8);
-    srcX[i] = p.X + r * p.ldx + min(k0 + lc * 8, (int)p.ldx - 8);   // clamped columns: outputs dropped
+    offD[i] = (uint32_t)(row * p.ldd + min(n0 + lc * 8, (int)p.ldd - 8)) * 2u;
+    offX[i] = (uint32_t)(row * p.ldx + min(k0 + lc * 8, (int)p.ldx - 8)) * 2u;   // clamped columns: outputs dropped
   }
-  const long stepD = (long)p.S * 32 * p.ldd, stepX = (long)p.S * 32 * p.ldx;
-  auto dma = [&](int t, int slot) {
-    const long tc = min(t, T - 1);             // steps past the end re-read the last one (never read)
-    char* base = smem + slot * RG_SLOT + wid * 1024;
+  const size_t stepD = (size_t)p.S * 32 * p.ldd * 2, stepX = (size_t)p.S * 32 * p.ldx * 2;
+  const char* dD = (const char*)(p.D + (size_t)split * 32 * p.ldd);
+  const char* dX = (const char*)(p.X + (size_t)split * 32 * p.ldx);
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  int d_left = T - 1;                          // steps the DMA cursor may still advance
+  auto dma = [&](int slot) {
+    char* base = smem + slot * RG_SLOT + wid_u * 1024;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(srcD[i] + tc * stepD), (lds_ptr_t)(base + i * 8192), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(dD + offD[i]), (lds_ptr_t)(base + i * 8192), 16, 0, 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(srcX[i] + tc * stepX), (lds_ptr_t)(base + RG_IMG + i * 8192), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(dX + offX[i]), (lds_ptr_t)(base + RG_IMG + i * 8192), 16, 0, 0);
+    if (d_left > 0) { dD += stepD; dX += stepX; --d_left; }   // past the end: re-read the last step
+  };
+  // one of the 4 LDS-DMA instructions of a step (q = 0, 1: D halves; 2, 3: X halves); q == 3 advances
+  auto dma_piece = [&](int slot, int q) {
+    char* base = smem + slot * RG_SLOT + wid_u * 1024 + (q >> 1) * RG_IMG + (q & 1) * 8192;
+    if (q < 2) __builtin_amdgcn_global_load_lds((const void*)(dD + offD[q & 1]), (lds_ptr_t)base, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds((const void*)(dX + offX[q & 1]), (lds_ptr_t)base, 16, 0, 0);
+    if (q == 3 && d_left > 0) { dD += stepD; dX += stepX; --d_left; }
   };
 
-  f32x4 acc[8][4];
+  // accumulators: MF 16: acc16[i][j] (16 x 16 tiles, n block i, k block j); MF 32: acc32[b][c]
+  f32x4 acc16[MF == 16 ? 8 : 1][MF == 16 ? 4 : 1];
+  f32x16 acc32[MF == 32 ? 4 : 1][MF == 32 ? 2 : 1];
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc32[b][c][e] = 0.f;
+  }
 
-  // transposed fragment reads (T10): group g = lane >> 4 supplies rows 8g + tq (+4), lane 4tq+tp
-  // the quad at columns cb + 4tp; lane receives column cb + (lane & 15) of those rows
+  // transposed fragment reads (T10): a 16-lane group supplies 4 rows x 16 columns (lane 4tq+tp the
+  // quad at columns cb + 4tp of row tq) and lane t of the group receives column cb + t of the rows.
+  //   MF 16: group g = lane >> 4 -> rows 8g + tq (+4): lane holds A[n = lane & 15][m = 8g + 0..7]
+  //   MF 32: group G -> columns +16 (G & 1), rows 8 (G >> 1) + tq (+4) of k16 step s (+16 s):
+  //          lane holds A[n = lane & 31][m = 16 s + 8 (lane >> 5) + 0..7]
+  // Offsets are loop-invariant per lane (the XOR swizzle makes them non-additive in the fragment
+  // index); +2048 B = the 4 high rows, +8192 B = the second k16 step (swizzle unchanged by both).
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-  const int r_lo = 8 * g + tq, r_hi = r_lo + 4;
-  bf16x8 af[8], bfr[4];
+  const int r_lo = MF == 16 ? 8 * g + tq : 8 * (g >> 1) + tq;
+  const int cg = MF == 16 ? 0 : 16 * (g & 1);
+  constexpr int NA = MF == 16 ? 8 : 4, NB = MF == 16 ? 4 : 2, CW = MF == 16 ? 16 : 32;
+  uint32_t oD[NA], oX[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) oD[i] = rg_off(r_lo, wn * 128 + i * CW + cg + 4 * tp);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) oX[j] = RG_IMG + rg_off(r_lo, wk * 64 + j * CW + cg + 4 * tp);
   const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  auto frag = [&](uint32_t img, int cb) {
-    const s16x4 lo = rg_tr_read(img + rg_off(r_lo, cb + 4 * tp));
-    const s16x4 hi = rg_tr_read(img + rg_off(r_hi, cb + 4 * tp));
+  auto frag0 = [&](uint32_t a) {
+    const s16x4 lo = rg_tr_read_o<0>(a);
+    const s16x4 hi = rg_tr_read_o<2048>(a);
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   };
+  auto frag1 = [&](uint32_t a) {
+    const s16x4 lo = rg_tr_read_o<8192>(a);
+    const s16x4 hi = rg_tr_read_o<8192 + 2048>(a);
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  bf16x8 af[2][NA], bfr[2][NB];      // [k16 step] (MF 16 uses step 0 only: one K = 32 MFMA)
 
 #define RG_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
                       __builtin_amdgcn_sched_barrier(0); } while (0)
 
-  dma(0, 0); dma(1, 1); dma(2, 2); dma(3, 3);
+  dma(0); dma(1); dma(2); dma(3);
   asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   RG_BAR();
   if (lag) RG_BAR();
 
+  unsigned long long st_sum[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
+  auto stamp = [&](int k) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (k >= 0) st_sum[k] += now - st_prev;
+      st_prev = now;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   int slot = 0, dslot = 4;
   for (int t = 0; t < T; ++t) {
     // ---- LD segment
-    dma(t + 4, dslot);
-    const uint32_t Dimg = lds0 + slot * RG_SLOT;
-    const uint32_t Ximg = Dimg + RG_IMG;
+    stamp(-1);
+    if constexpr (!DMA_IN_MMA) dma(dslot);
+    stamp(0);
+    const uint32_t sb = lds0 + slot * RG_SLOT;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = frag(Ximg, wk * 64 + j * 16);
+    for (int j = 0; j < NB; ++j) bfr[0][j] = frag0(sb + oX[j]);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = frag(Dimg, wn * 128 + i * 16);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    for (int i = 0; i < NA; ++i) af[0][i] = frag0(sb + oD[i]);
+    if constexpr (MF == 32) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) bfr[1][j] = frag1(sb + oX[j]);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) af[1][i] = frag1(sb + oD[i]);
+    }
+    stamp(1);
+    if constexpr (DMA_IN_MMA) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stamp(2);
     RG_BAR();
+    stamp(3);
     // ---- MMA segment
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (MF == 16) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+          acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[0][j], acc16[i][j], 0, 0, 0);
+        if constexpr (DMA_IN_MMA) {
+          // the refill of slot (t+4)%5 = step t-1's slot: every wave finished its reads of step t-1
+          // before the barrier that ended its LD(t-1), which precedes this segment
+          if (i == 1 || i == 3 || i == 5 || i == 7) {
+            __builtin_amdgcn_sched_barrier(0);
+            dma_piece(dslot, i >> 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            acc32[b][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s2][b], bfr[s2][c], acc32[b][c], 0, 0, 0);
+          if constexpr (DMA_IN_MMA) {
+            if (b == 1 || b == 3) {
+              __builtin_amdgcn_sched_barrier(0);
+              dma_piece(dslot, s2 * 2 + (b >> 1));
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+    }
     __builtin_amdgcn_s_setprio(0);
+    stamp(4);
     RG_BAR();
+    stamp(5);
     slot = slot == RG_NSLOT - 1 ? 0 : slot + 1;
     dslot = dslot == RG_NSLOT - 1 ? 0 : dslot + 1;
   }
   if (!lag) RG_BAR();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #undef RG_BAR
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* d = p.dbg + ((size_t)blockIdx.x * 8 + wid) * 8;
+      for (int k = 0; k < 6; ++k) d[k] = st_sum[k];
+      d[6] = T;
+      d[7] = wg;
+    }
+  }
 
-  // ---- epilogue: this split's partial tile -> slab (acc[i][j][r]: n = 16i + 4(lane>>4) + r,
-  //      k = 16j + (lane & 15) within the wave tile)
+  // ---- epilogue: this split's partial tile -> slab
   const long lds = (long)p.KT * 256;
   float* out = p.slab + (size_t)split * ((size_t)p.NT * 256) * lds;
+  if constexpr (MF == 16) {
+    // acc16[i][j][r]: n = 16i + 4(lane>>4) + r, k = 16j + (lane & 15) within the wave tile
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
-        out[(size_t)n * lds + k] = acc[i][j][r];
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + wk * 64 + j * 16 + (lane & 15);
+          out[(size_t)n * lds + k] = acc16[i][j][r];
+        }
       }
-    }
+  } else {
+    // acc32[b][c][e]: n = 32b + (e & 3) + 8(e >> 2) + 4(lane >> 5), k = 32c + (lane & 31):
+    // every store is two 128-B row segments
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = n0 + wn * 128 + b * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int k = k0 + wk * 64 + c * 32 + (lane & 31);
+          out[(size_t)n * lds + k] = acc32[b][c][e];
+        }
+      }
+  }
 }
 
 // G[n][k] += sum_s slab[s][n][k] in fixed split order (n < Nv, k < Kx; Kx % 8 == 0)
@@ -202,6 +343,186 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// NT ring GEMM (forward layers): C[m][n] = act(sum_k A[m][k] B[n][k]) with the Encog bias column
+// (C[m][n_valid] = 1) and zero padding written by the epilogue (FloatFlatNetwork.java:148-178).
+// Same ring / stagger schedule as ring_tn_kernel, persistent over output tiles: block L takes tiles
+// L, L+G, ... (the two n-tiles of one 256-row m-tile are consecutive logical ids: one XCD, rows
+// fetched from HBM once), and the DMA stream runs straight across tile boundaries, so the next
+// tile's first k-steps land while the current one finishes (no per-tile pipeline fill).
+// Images: A [256 rows][32 k], B [256 rows][32 k], 64-B rows, chunk ^ ((r >> 4) & 1 | ((r >> 2) & 1) << 1):
+// conflict-free ds_read_b128 for the 16x16x32 (and 32x32x16) operand maps (brute-force checked over
+// the four ds_read_b128 lane groups).
+// Epilogue (after the MFMAs of a tile's last k-step): act + bf16 pack + 8-byte row stores.  Every
+// wave issues exactly RG_NT_STORES stores per tile (lanes outside the output write a dummy slot), so
+// the counted vmcnt of the next three LD segments can let the younger DMAs stay in flight.
+// ---------------------------------------------------------------------------------------------
+constexpr int RG_NT_STORES = 32;
+__device__ uint2 g_rg_dummy[64];     // 8-byte sinks for the stores of lanes outside the output
+
+__device__ __forceinline__ int nt_swz(int r) { return ((r >> 4) & 1) | (((r >> 2) & 1) << 1); }
+
+struct RingNTArgs {
+  const bf16_t* A; long lda;   // [M, K] row-major
+  const bf16_t* B; long ldb;   // [NB, K] row-major (rows >= NB read as row NB-1, outputs dropped)
+  bf16_t* C; long ldc;         // [M, N]
+  int M, N, K, NB, n_valid, bias_col;
+  int ntn, ntiles;             // n-tiles, total tiles
+};
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(RG_T, 2) void ring_nt_kernel(RingNTArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = gridDim.x;
+  const int L = rg_xcd_remap(blockIdx.x, G);
+  const int ks = p.K >> 5;                                  // k-steps per tile
+  const int U = ((p.ntiles - L + G - 1) / G) * ks;          // host: G <= ntiles -> U >= ks
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const bool lag = wid >= 4;
+
+  // DMA: thread instr i (0/1) per image fills LDS bytes (i*8 + wid)*1024 + lane*16 = row P >> 6
+  int drow[2], dch[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int P = (i * 8 + wid) * 1024 + lane * 16;
+    drow[i] = P >> 6;
+    dch[i] = (((P >> 4) & 3) ^ nt_swz(drow[i])) * 8;
+  }
+  // DMA cursor (tile id, k-step).  Per tile: wave-uniform base pointers of the tile's first rows
+  // and per-lane 32-bit byte offsets (rows clamped to the operand), so each LDS-DMA is a scalar base
+  // + vector offset (no 64-bit address math per step).
+  int d_tile = L, d_k = 0;
+  const char* dbaseA;
+  const char* dbaseB;
+  uint32_t offA[2], offB[2];
+  auto dma_tile = [&]() {
+    const int mt = d_tile / p.ntn, nt = d_tile - mt * p.ntn;
+    dbaseA = (const char*)(p.A + (size_t)mt * 256 * p.lda);
+    dbaseB = (const char*)(p.B + (size_t)nt * 256 * p.ldb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ml = min(mt * 256 + drow[i], p.M - 1) - mt * 256;
+      const int nl = min(nt * 256 + drow[i], p.NB - 1) - nt * 256;
+      offA[i] = (uint32_t)(ml * p.lda + dch[i]) * 2u;
+      offB[i] = (uint32_t)(nl * p.ldb + dch[i]) * 2u;
+    }
+  };
+  dma_tile();
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  auto dma = [&](int slot, bool live) {
+    char* base = smem + slot * RG_SLOT + wid_u * 1024;
+    const char* a = dbaseA + d_k * 64;
+    const char* b = dbaseB + d_k * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(a + offA[i]), (lds_ptr_t)(base + i * 8192), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b + offB[i]), (lds_ptr_t)(base + RG_IMG + i * 8192), 16, 0, 0);
+    if (live) {                                             // past the end: re-read the last step
+      if (++d_k == ks) { d_k = 0; d_tile += G; dma_tile(); }
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads: operand rows base + (lane & 15), 16-B chunk (lane >> 4) (+ swizzle).  Frag t
+  // of a 16-row block sits at t * 1024 + lane offset, and the lane offset only depends on t's
+  // parity (swizzle bit 0 = row bit 4), so two per-lane bases per operand + immediate offsets.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  const int fr = lane & 15, fc = lane >> 4;
+  auto lane_off = [&](int row) { return (uint32_t)(row * 64 + ((fc ^ nt_swz(row)) << 4)); };
+  const uint32_t oA0 = lane_off(wm * 128 + fr), oA1 = lane_off(wm * 128 + 16 + fr) - 1024;
+  const uint32_t oB0 = RG_IMG + lane_off(wn * 64 + fr), oB1 = RG_IMG + lane_off(wn * 64 + 16 + fr) - 1024;
+  bf16x8 af[8], bfr[4];
+
+#define RG_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
+                      __builtin_amdgcn_sched_barrier(0); } while (0)
+
+  int live_left = U;                                        // DMA steps still inside the stream
+  for (int s = 0; s < 4; ++s) { dma(s, live_left > 1); --live_left; }
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  RG_BAR();
+  if (lag) RG_BAR();
+
+  int slot = 0, dslot = 4, kstep = 0, tile = L, post_epi = 0;
+  for (int u = 0; u < U; ++u) {
+    // ---- LD segment
+    dma(dslot, live_left > 1); --live_left;
+    const uint32_t sb = lds0 + slot * RG_SLOT;
+    {
+      const uint32_t b0 = sb + oB0, b1 = sb + oB1, a0 = sb + oA0, a1 = sb + oA1;
+      bfr[0] = rg_read_b128_o<0>(b0);    bfr[1] = rg_read_b128_o<1024>(b1);
+      bfr[2] = rg_read_b128_o<2048>(b0); bfr[3] = rg_read_b128_o<3072>(b1);
+      af[0] = rg_read_b128_o<0>(a0);     af[1] = rg_read_b128_o<1024>(a1);
+      af[2] = rg_read_b128_o<2048>(a0);  af[3] = rg_read_b128_o<3072>(a1);
+      af[4] = rg_read_b128_o<4096>(a0);  af[5] = rg_read_b128_o<5120>(a1);
+      af[6] = rg_read_b128_o<6144>(a0);  af[7] = rg_read_b128_o<7168>(a1);
+    }
+    if (post_epi > 0) {                   // the last tile's 32 stores sit between older and younger DMAs
+      asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
+      --post_epi;
+    } else {
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    RG_BAR();
+    // ---- MMA segment
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][i], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (++kstep == ks) {
+      // ---- epilogue: acc[j][i] = D[n][m]: m = 16i + (lane & 15), n = 16j + 4(lane >> 4) + r
+      const int mt = tile / p.ntn, nt = tile - mt * p.ntn;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nb = nt * 256 + wn * 64 + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = mt * 256 + wm * 128 + i * 16 + fr;
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z = acc[j][i][r];
+            if constexpr (EPI == 0) {
+              // branch-free select (a ternary around act_fwd compiles to exec-masked branches)
+              const int n = nb + r;
+              const float a = act_fwd(ACT, z);
+              const float alt = (n == p.n_valid && p.bias_col) ? 1.f : 0.f;
+              const int keep = -(int)(n < p.n_valid);
+              o[r] = __int_as_float((__float_as_int(a) & keep) | (__float_as_int(alt) & ~keep));
+            } else {
+              o[r] = z;
+            }
+            acc[j][i][r] = 0.f;
+          }
+          const uint2 w = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+          uint2* dst = (m < p.M && nb < p.N) ? (uint2*)(p.C + (size_t)m * p.ldc + nb) : &g_rg_dummy[lane];
+          rg_store_b64(dst, w);
+        }
+      }
+      kstep = 0;
+      tile += G;
+      post_epi = 3;
+    }
+    RG_BAR();
+    slot = slot == RG_NSLOT - 1 ? 0 : slot + 1;
+    dslot = dslot == RG_NSLOT - 1 ? 0 : dslot + 1;
+  }
+  if (!lag) RG_BAR();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef RG_BAR
+}
+
 // tail rows (< 32) that do not fill a ring k-step: one thread per (n, k), fixed row order
 __global__ __launch_bounds__(256) void tail_tn_kernel(const bf16_t* __restrict__ D, long ldd,
                                                       const bf16_t* __restrict__ X, long ldx, int rows,
@@ -215,6 +536,14 @@ __global__ __launch_bounds__(256) void tail_tn_kernel(const bf16_t* __restrict__
 }
 
 }  // namespace
+
+static unsigned long long* g_rg_stamp = nullptr;    // diagnostic: STAMP build of the TN ring
+// Diagnostic switch: a device buffer of >= blocks * 8 * 8 u64 enables the STAMP build (nullptr: off).
+SHIFU_API int shifu_ring_set_stamp(void* buf) { g_rg_stamp = (unsigned long long*)buf; return 0; }
+static int g_rg_mf = 16;                            // MFMA shape of the TN ring (A/B switch: 16 or 32)
+static int g_rg_dmamma = 1;                         // TN ring: LDS-DMA issued inside the MMA segment
+SHIFU_API int shifu_ring_set_mf(int mf) { g_rg_mf = mf == 32 ? 32 : 16; return 0; }
+SHIFU_API int shifu_ring_set_dmamma(int v) { g_rg_dmamma = v; return 0; }
 
 static int rg_splits(int nsteps, int ntiles) {
   int S = 256 / ntiles;                      // one 160-KiB block per CU on the 256 CUs
@@ -241,8 +570,25 @@ SHIFU_API int shifu_wgrad_ring(const void* D, long ldd, const void* X, long ldx,
   const int S = rg_splits(nsteps, NT * KT);
   const long need = (long)S * NT * 256 * (long)KT * 256 * 4;
   if (ws == nullptr || ws_bytes < need || ((uintptr_t)ws & 15) || ((uintptr_t)G & 15)) return -1;
-  RingTNArgs p{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, (float*)ws, nsteps, S, NT, KT};
-  hipLaunchKernelGGL(ring_tn_kernel, dim3(S * NT * KT), dim3(RG_T), RG_LDS, stream, p);
+  RingTNArgs p{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, (float*)ws, nsteps, S, NT, KT, g_rg_stamp};
+  const dim3 grid(S * NT * KT);
+  if (g_rg_mf == 16) {
+    if (g_rg_dmamma) {
+      if (g_rg_stamp) hipLaunchKernelGGL((ring_tn_kernel<16, true, true>), grid, dim3(RG_T), RG_LDS, stream, p);
+      else hipLaunchKernelGGL((ring_tn_kernel<16, false, true>), grid, dim3(RG_T), RG_LDS, stream, p);
+    } else {
+      if (g_rg_stamp) hipLaunchKernelGGL((ring_tn_kernel<16, true, false>), grid, dim3(RG_T), RG_LDS, stream, p);
+      else hipLaunchKernelGGL((ring_tn_kernel<16, false, false>), grid, dim3(RG_T), RG_LDS, stream, p);
+    }
+  } else {
+    if (g_rg_dmamma) {
+      if (g_rg_stamp) hipLaunchKernelGGL((ring_tn_kernel<32, true, true>), grid, dim3(RG_T), RG_LDS, stream, p);
+      else hipLaunchKernelGGL((ring_tn_kernel<32, false, true>), grid, dim3(RG_T), RG_LDS, stream, p);
+    } else {
+      if (g_rg_stamp) hipLaunchKernelGGL((ring_tn_kernel<32, true, false>), grid, dim3(RG_T), RG_LDS, stream, p);
+      else hipLaunchKernelGGL((ring_tn_kernel<32, false, false>), grid, dim3(RG_T), RG_LDS, stream, p);
+    }
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const long sstride = (long)NT * 256 * KT * 256;
@@ -262,4 +608,40 @@ SHIFU_API int shifu_wgrad_ring(const void* D, long ldd, const void* X, long ldx,
     if (e != hipSuccess) return (int)e;
   }
   return 0;
+}
+
+static int rg_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// Forward NT GEMM through the persistent ring: C = act(A B^T) (epi 0: activation + bias column +
+// zero padding; epi 2: plain store).  K % 32 == 0; activations whose derivative follows from the
+// output only (no stored-derivative output).  Returns -1 on an unsupported shape (caller falls back).
+SHIFU_API int shifu_gemm_ring_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc,
+                                 int M, int N, int K, int epi, int act, int n_valid, int bias_col, hipStream_t stream) {
+  if (K % 32 || K < 32 || lda % 8 || ldb % 8 || ldc % 4 || N % 4 || M <= 0 || N <= 0 || NB <= 0 || lda < K ||
+      ldb < K || ldc < N || ((uintptr_t)C & 7))
+    return -1;
+  if (epi != 0 && epi != 2) return -1;
+  if (epi == 0 && (!act_deriv_from_output(act) || act < 0 || act > 8)) return -1;
+  const int ntn = (N + 255) / 256, ntiles = ((M + 255) / 256) * ntn;
+  const int grid = ntiles < rg_num_cus() ? ntiles : rg_num_cus();
+  RingNTArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, K, NB, n_valid, bias_col, ntn, ntiles};
+#define RNT_L(E, A_) hipLaunchKernelGGL((ring_nt_kernel<E, A_>), dim3(grid), dim3(RG_T), RG_LDS, stream, p)
+  if (epi == 2) RNT_L(2, 2);
+  else switch (act) {
+    case 0: RNT_L(0, 0); break; case 1: RNT_L(0, 1); break; case 2: RNT_L(0, 2); break;
+    case 3: RNT_L(0, 3); break; case 4: RNT_L(0, 4); break; case 6: RNT_L(0, 6); break;
+    default: RNT_L(0, 7); break;
+  }
+#undef RNT_L
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
 }

@@ -30,6 +30,18 @@ def ring(D, X, G, Nv, ws):
                  nat.stream_of(X))
 
 
+def ring_ld(D, X, G, Nv, ws):          # variant: DMA issued in the LD segment
+    nat.call_hip("shifu_ring_set_dmamma", 0)
+    ring(D, X, G, Nv, ws)
+    nat.call_hip("shifu_ring_set_dmamma", 1)
+
+
+def ring32(D, X, G, Nv, ws):           # variant: 32x32x16 MFMA
+    nat.call_hip("shifu_ring_set_mf", 32)
+    ring(D, X, G, Nv, ws)
+    nat.call_hip("shifu_ring_set_mf", 16)
+
+
 def old(D, X, G, Nv):
     M, Kx = X.shape[0], X.shape[1]
     ntiles = -(-Nv // 128) * (Kx // 128)
@@ -41,12 +53,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1 << 21)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only", nargs="*", default=None, help="timed cases to run (PMC passes)")
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--stamp", action="store_true", help="segment timestamps of the TN ring (diagnostic)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     bf = torch.bfloat16
     res = {}
     # ---- correctness (small M with a tail), both layer shapes
-    for name, (ldd, Nv, Kx) in {"l0": (512, 500, 1024), "l1": (256, 200, 512), "odd": (64, 30, 320)}.items():
+    checks = {} if a.no_check else {"l0": (512, 500, 1024), "l1": (256, 200, 512), "odd": (64, 30, 320)}
+    for name, (ldd, Nv, Kx) in checks.items():
         M = 65536 + 17
         D = (torch.rand(M, ldd, device=dev) * 2 - 1).to(bf)
         D[:, Nv:] = 0
@@ -60,6 +76,17 @@ def main():
         torch.cuda.synchronize()
         err = ((G - 0.5) - ref).abs().max().item() / ref.abs().max().item()
         res[f"check_{name}"] = {"max_rel_err": err, "bitwise_repro": bool(torch.equal(G, G2))}
+    # ---- NT forward ring: correctness (M not a multiple of 256, sigmoid + bias column + padding)
+    M = 70000 if not a.no_check else 256
+    X = (torch.rand(M, 1024, device=dev) * 2 - 1).to(bf)
+    W = ((torch.rand(500, 1024, device=dev) * 2 - 1) * 0.05).to(bf)
+    H = torch.full((M, 512), 7.0, device=dev, dtype=bf)
+    nat.call_hip("shifu_gemm_ring_nt", X, 1024, W, 1024, 500, H, 512, M, 512, 1024, 0, 0, 500, 1, nat.stream_of(X))
+    ref = torch.zeros(M, 512, device=dev)
+    ref[:, :500] = torch.sigmoid(X.float() @ W.float().t())
+    ref[:, 500] = 1
+    torch.cuda.synchronize()
+    res["check_nt_fwd"] = {"max_abs_err": (H.float() - ref).abs().max().item()}
     # ---- timing at the bench chunk
     M = a.rows
     X = (torch.rand(M, 1024, device=dev) * 2 - 1).to(bf)
@@ -71,14 +98,48 @@ def main():
     ws = torch.empty(max(nat.hip().shifu_wgrad_ring_ws(M, 500, 1024), nat.hip().shifu_wgrad_ring_ws(M, 200, 512)) // 4,
                      device=dev)
     fl0, fl1 = 2.0 * M * 512 * 1024, 2.0 * M * 256 * 512
+    W1 = ((torch.rand(500, 1024, device=dev) * 2 - 1) * 0.05).to(bf)
+    H1o = torch.empty(M, 512, device=dev, dtype=bf)
+    st = nat.stream_of(X)
+    flf = 2.0 * M * 512 * 1024
+
+    def fwd_old():
+        nat.call_hip("shifu_gemm_nt", X, 1024, W1, 1024, 500, H1o, 512, None, 0, None, 0, None, 0, M, 512, 1024, 0,
+                     0, 500, 1, 0.0, st)
+
+    def fwd_ring():
+        nat.call_hip("shifu_gemm_ring_nt", X, 1024, W1, 1024, 500, H1o, 512, M, 512, 1024, 0, 0, 500, 1, st)
+
+    def fwd_ring_store():
+        nat.call_hip("shifu_gemm_ring_nt", X, 1024, W1, 1024, 500, H1o, 512, M, 512, 1024, 2, 2, 500, 0, st)
+
     cases = {
+        "fwd1_old": (fwd_old, flf), "fwd1_ring": (fwd_ring, flf), "fwd1_ring_storeonly": (fwd_ring_store, flf),
         "wgrad0_old": (lambda: old(D1, X, G0, 500), fl0), "wgrad0_ring": (lambda: ring(D1, X, G0, 500, ws), fl0),
         "wgrad1_old": (lambda: old(D2, H1, G1, 200), fl1), "wgrad1_ring": (lambda: ring(D2, H1, G1, 200, ws), fl1),
+        "wgrad0_ring_dmald": (lambda: ring_ld(D1, X, G0, 500, ws), fl0),
+        "wgrad0_ring32": (lambda: ring32(D1, X, G0, 500, ws), fl0),
     }
     for r in range(a.rounds):
         for k, (fn, fl) in cases.items():
+            if a.only and k not in a.only:
+                continue
             ms = timeit(fn)
             res.setdefault(k, []).append([round(ms, 4), round(fl / ms / 1e9, 1)])
+    if a.stamp:              # diagnostic STAMP build of the TN ring: mean cycles per step per segment
+        for mf in (16, 32):
+            buf = torch.zeros(256 * 8 * 8, dtype=torch.int64, device=dev)
+            nat.call_hip("shifu_ring_set_mf", mf)
+            nat.call_hip("shifu_ring_set_stamp", buf)
+            ring(D1, X, G0, 500, ws)
+            torch.cuda.synchronize()
+            nat.call_hip("shifu_ring_set_stamp", None)
+            b = buf.view(256, 8, 8).double().cpu()
+            names = ["dma", "reads", "waits", "ld_bar", "mfma", "mma_bar"]
+            for half, sl in (("lead", slice(0, 4)), ("lag", slice(4, 8))):
+                v = b[:, sl, :6].sum(dim=(0, 1)) / b[:, sl, 6].sum()
+                res[f"stamp{mf}_{half}_cycles_per_step"] = {n: round(float(x), 1) for n, x in zip(names, v)}
+        nat.call_hip("shifu_ring_set_mf", 16)
     print(json.dumps(res))
 
 
