@@ -4,7 +4,8 @@ MapReduce shuffle (``UpdateBinningInfoMapper`` -> ``UpdateBinningInfoReducer``,
 J/core/binning/UpdateBinningInfoMapper.java:349-599, UpdateBinningInfoReducer.java:125-433).
 
 The result is the single-process result (``algos.stats.compute_column_stats``), not an
-approximation of it:
+approximation of it, with ONE exception (the distinct count of high-cardinality columns, last
+bullet):
 
 * numeric bin boundaries are the EXACT equal-population cuts over all ranks: the single-process
   rule (first distinct value whose cumulative count reaches j * total / bins, cut halfway to the
@@ -16,7 +17,10 @@ approximation of it:
 * histograms (count/weight x pos/neg) and moments are all_reduce(SUM); min/max all_reduce(MIN/MAX);
 * distinct counts: exact when the per-rank distinct sets are small enough to gather
   (<= ``DISTINCT_GATHER_CAP`` values each), otherwise a HyperLogLog (p = 14) merged with
-  all_reduce(MAX) of its registers (the reference uses HyperLogLogPlus(8) everywhere).
+  all_reduce(MAX) of its registers.  So for a column with more than ``DISTINCT_GATHER_CAP``
+  distinct values on some rank, ``distinctCount`` is an estimate (relative error ~0.8 %) and can
+  differ from the single-process exact count; the reference itself reports HyperLogLogPlus(8)
+  estimates for every column.
 """
 from __future__ import annotations
 

@@ -160,6 +160,7 @@ def normalize_column(cc, col, norm_type: str, cutoff: float | None) -> np.ndarra
             return zscore(_num_values(cc, col), cc.mean, cc.std_dev, cutoff)[:, None]
         if nt == "WOE_INDEX":
             return _lookup_last(cc.bin_count_woe, _bin_num(cc, col))[:, None]
+        # WOE_ZSCALE_INDEX (Normalizer.fullNormalize :305-315): z-scored WOE for numeric columns
         woe = _lookup_last(cc.bin_count_woe, _bin_num(cc, col))
         m, s = woe_mean_std(cc, False)
         return zscore(woe, m, s, cutoff)[:, None]

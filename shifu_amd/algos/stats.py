@@ -18,6 +18,7 @@ when available), the KS/IV scan is O(bins).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -282,12 +283,28 @@ def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int 
     return ccs
 
 
-def compute_psi(mc, ccs, md, unit_column: str):
-    """Population stability per column across the units of ``psiColumnName``
-    (P/PSI.pig:19-46, PSICalculatorUDF): PSI = sum_units sum_bins (a-e) ln(a/e) with e the
-    overall bin distribution and a the unit's; also records ``unitStats``.  Data parallel: the
-    unit set is the union over ranks and the (unit, bin) counts of every column are all-reduced
-    in one bucket (the PopulationCounterUDF -> PSICalculatorUDF shuffle)."""
+def compute_psi(mc, ccs, md, unit_column: str, unit_stats_path: str | None = None):
+    """Population stability per column across the units of ``psiColumnName`` (P/PSI.pig:19-46).
+
+    Reference parity:
+      * per (unit, column) counters = ``PopulationCounterUDF`` with ``NumericCounter`` /
+        ``CategoryCounter`` (J/udf/stats/*Counter.java): one count per bin + a missing bin, the
+        unit mean (sum of valid numeric values, or of the category's ``binPosRate`` for
+        categoricals, over ALL the unit's records incl. missing; NaN when every record is
+        missing), the missing rate and the record count;
+      * the EXPECTED distribution comes from the ColumnConfig stats pass:
+        ``(binCountNeg[i] + binCountPos[i]) / totalCount`` (``PSICalculatorUDF.exec`` :55-65),
+        not from the PSI pass's own rows;
+      * PSI = sum over units of sum_i (a_i - e_i) ln(a_i / e_i), accumulated with the UDF's
+        exact loop -- its bin index only advances on the terms it adds (a zero actual or
+        expected share, or an empty unit, skips the term WITHOUT advancing), reproduced as is;
+      * unit statistics ``unit^mean^missingRate^count`` (Java ``Double.toString``), sorted as
+        strings, joined by ``\u0001`` and written per column as ``columnNum|stats`` lines to
+        ``tmp/columnconfig.unitstats`` (MapReducerStatsWorker.runPSI :624-651); like the
+        reference, ColumnConfig gets ``psi`` only.
+    Data parallel: the unit set is the union over ranks and the (unit, bin) counts + unit value
+    sums of every column are all-reduced in one bucket (the PopulationCounter shuffle)."""
+    from ..config.jsonio import java_double_str
     from ..parallel import dist
     if unit_column not in md.table:
         _log.warning("psiColumnName %s not in data", unit_column)
@@ -296,6 +313,7 @@ def compute_psi(mc, ccs, md, unit_column: str):
     units = sorted(set(units_s))
     if dist.info().world_size > 1:
         units = sorted(set().union(*dist.all_gather_objects(units)))
+    U = len(units)
     uidx = {u: i for i, u in enumerate(units)}
     ucode = np.array([uidx[u] for u in units_s], dtype=np.int64) if len(units_s) else np.zeros(0, np.int64)
     cols, counts = [], []
@@ -306,73 +324,65 @@ def compute_psi(mc, ccs, md, unit_column: str):
         if cc.is_categorical():
             cats = cc.bin_category or []
             codes = col.values if col.kind == "str" else None
-            if codes is None:
+            if codes is None or not cats:
                 continue
             bidx = B.category_index(codes, col.dictionary, cats)
             nb = len(cats) + 1
+            rate = np.asarray(list(cc.bin_pos_rate or [0.0] * len(cats)) + [0.0], dtype=np.float64)
+            contrib = rate[np.clip(bidx, 0, nb - 1)]
+            contrib[bidx >= nb - 1] = 0.0
         else:
             bb = cc.bin_boundary
             if not bb:
                 continue
-            bidx = B.bin_index_numeric(col.numeric(), bb)
+            v = col.numeric()
+            bidx = B.bin_index_numeric(v, bb)
             nb = len(bb) + 1
-        cnt = np.bincount(ucode * nb + bidx, minlength=len(units) * nb).astype(np.float64)
+            contrib = np.where(np.isnan(v), 0.0, v)
+        cnt = np.bincount(ucode * nb + bidx, minlength=U * nb).astype(np.float64)
+        vsum = np.bincount(ucode, weights=contrib, minlength=U).astype(np.float64)
         cols.append((cc, nb))
-        counts.append(cnt)
+        counts.append(np.concatenate([cnt, vsum]))
     if counts and dist.info().world_size > 1:
         flat = dist.all_reduce_np(np.concatenate(counts))
         off = 0
         for i, c in enumerate(counts):
             counts[i] = flat[off:off + c.size]
             off += c.size
-    for (cc, nb), cnt in zip(cols, counts):
-        per_unit = cnt.reshape(len(units), nb)
-        exp = per_unit.sum(0)
-        exp = exp / max(exp.sum(), 1)
+    lines = []
+    for (cc, nb), buf in zip(cols, counts):
+        per_unit = buf[:U * nb].reshape(U, nb)
+        vsum = buf[U * nb:]
+        neg = list(cc.bin_count_neg or [])
+        pos = list(cc.bin_count_pos or [])
+        total_cnt = float(cc.stat("totalCount", 0) or 0)
+        expected = [0.0 if total_cnt == 0 else (float(neg[i]) + float(pos[i])) / total_cnt
+                    for i in range(min(len(neg), len(pos)))]
         psi = 0.0
         unit_stats = []
         for ui, u in enumerate(units):
-            act = per_unit[ui] / max(per_unit[ui].sum(), 1)
-            ok = (act > 0) & (exp > 0)
-            pu = float(((act[ok] - exp[ok]) * np.log(act[ok] / exp[ok])).sum())
-            psi += pu
-            unit_stats.append(f"{u}:{pu}")
+            sub = per_unit[ui]
+            total = float(sub.sum())
+            i = 0
+            for sv in sub:                       # PSICalculatorUDF.exec :75-95, index quirk kept
+                if total == 0 or i >= len(expected) or expected[i] == 0:
+                    continue
+                log_num = (sv / total) / expected[i]
+                if log_num <= 0:
+                    continue
+                psi += (sv / total - expected[i]) * math.log(log_num)
+                i += 1
+            miss = float(sub[nb - 1])
+            mean = float("nan") if (total == 0 or total == miss) else float(vsum[ui]) / total
+            mrate = miss / total if total != 0 else 0.0
+            unit_stats.append(f"{u}^{java_double_str(mean)}^{java_double_str(mrate)}^{int(total)}")
+        unit_stats.sort()
         cc.stats["psi"] = psi
-        cc.stats["unitStats"] = unit_stats
-    return ccs
-    units_s = md.table[unit_column].strings()
-    units = sorted(set(units_s))
-    for cc in ccs:
-        if cc.is_target() or cc.is_meta() or cc.name not in md.table:
-            continue
-        col = md.table[cc.name]
-        if cc.is_categorical():
-            cats = cc.bin_category or []
-            codes = col.values if col.kind == "str" else None
-            if codes is None:
-                continue
-            bidx = B.category_index(codes, col.dictionary, cats)
-            nb = len(cats) + 1
-        else:
-            bb = cc.bin_boundary
-            if not bb:
-                continue
-            bidx = B.bin_index_numeric(col.numeric(), bb)
-            nb = len(bb) + 1
-        exp = np.bincount(bidx, minlength=nb).astype(float)
-        exp /= max(exp.sum(), 1)
-        psi = 0.0
-        unit_stats = []
-        for u in units:
-            m = units_s == u
-            act = np.bincount(bidx[m], minlength=nb).astype(float)
-            act /= max(act.sum(), 1)
-            ok = (act > 0) & (exp > 0)
-            pu = float(((act[ok] - exp[ok]) * np.log(act[ok] / exp[ok])).sum())
-            psi += pu
-            unit_stats.append(f"{u}:{pu}")
-        cc.stats["psi"] = psi
-        cc.stats["unitStats"] = unit_stats
+        lines.append(f"{cc.num}|" + "\u0001".join(unit_stats))
+    if unit_stats_path and dist.info().rank == 0:
+        os.makedirs(os.path.dirname(unit_stats_path) or ".", exist_ok=True)
+        with open(unit_stats_path, "w", encoding="utf-8") as f:
+            f.write("".join(line + "\n" for line in lines))
     return ccs
 
 

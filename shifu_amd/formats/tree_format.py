@@ -7,6 +7,14 @@ the records ``TreeNode.write`` (:204-234), ``Node.write`` (J/core/dtrain/dt/Node
 ``SimpleBitSet.write`` (int byte-length + bytes, bit = value % 8 of byte value >> 3).
 Layout: SURVEY Appendix C.  Versions <= 3 (ungzipped, ``version < 4`` -> one bag, float wgtCnt
 for <= 2) are read with the same code path.
+
+Pre-versioned legacy layout (``read_legacy_tree_model``): the reference fixture
+``TR/example/wdbc/wdbcModelSetLocal/models/model0.gbt`` predates the version field; its strings
+are int-length framed (``StringUtils.writeString``), nodes carry impurity / a leaf flag / the
+weight-count ratio, splits carry the column name and the feature-type enum name.  The reference's
+own ``IndependentTreeModel.loadFromStream`` cannot read it (it expects ``readInt`` version +
+``readUTF``); the layout was recovered from the bytes (header, 13 nodes, root weight, 13 feature
+ids: exactly 1025 bytes) and is documented field by field on the reader.
 """
 from __future__ import annotations
 
@@ -305,8 +313,91 @@ def read_bags(i: JavaIn, version: int = TREE_FORMAT_VERSION, n_bags: int | None 
     return bags
 
 
+def _is_legacy(data: bytes) -> bool:
+    """Pre-versioned files start with the int-framed algorithm name ("GBT"/"RF") instead of a
+    version int followed by a readUTF string."""
+    if len(data) < 8 or data[:2] == b"\x1f\x8b":
+        return False
+    n = int.from_bytes(data[:4], "big")
+    return n in (2, 3) and data[4:4 + n] in (b"GBT", b"RF")
+
+
+def read_legacy_tree_model(data: bytes) -> TreeModelFile:
+    """Legacy (pre-versioned) tree model layout:
+
+      header : String algorithm, double learningRate, String loss, bool isClassification,
+               bool isOneVsAll, int treeNum
+      tree   : int treeId, int nodeNum, Node root, double rootWgtCnt, int nFeatures, int[] features
+      Node   : int id, double gain, double impurity, bool isLeaf, double wgtCntRatio,
+               bool hasSplit [Split], bool hasPredict [double predict, double classValue],
+               bool hasLeft [Node], bool hasRight [Node]
+      Split  : int columnNum, double threshold, String columnName, bool isLeft, UTF featureType
+               ("CONTINUOUS"/"CATEGORICAL"), int nCategories, String[] categories
+    (String = int byte length + UTF-8 bytes.)  Category strings become per-column category lists so
+    the model scores through the same ``TreeModelFile`` path as v4 files."""
+    i = JavaIn(bytes(data))
+
+    def jstr():
+        n = i.int()
+        return i._take(n).decode("utf-8") if n > 0 else ""
+
+    alg = jstr()
+    lr = i.double()
+    loss = jstr()
+    is_cls = i.bool()
+    ova = i.bool()
+    names, cats = {}, {}
+
+    def node():
+        nd = Node(i.int())
+        nd.gain = i.double()
+        i.double()                       # impurity
+        i.bool()                         # isLeaf (derivable from the children)
+        nd.wgt_cnt = i.double()          # weight-count ratio of the parent
+        if i.bool():
+            col = i.int()
+            thr = i.double()
+            names.setdefault(col, jstr())
+            is_left = i.bool()
+            ftype = i.utf()
+            ncat = i.int()
+            vals = [jstr() for _ in range(ncat)]
+            if ftype.upper().startswith("CAT"):
+                lst = cats.setdefault(col, [])
+                idx = set()
+                for v in vals:
+                    if v not in lst:
+                        lst.append(v)
+                    idx.add(lst.index(v))
+                nd.split = Split(col, CATEGORICAL, 0.0, is_left, idx)
+            else:
+                nd.split = Split(col, CONTINUOUS, thr, is_left)
+        if i.bool():
+            nd.predict = i.double()
+            nd.class_value = int(i.double())
+        if i.bool():
+            nd.left = node()
+        if i.bool():
+            nd.right = node()
+        return nd
+
+    trees = []
+    for _ in range(i.int()):
+        tid = i.int()
+        nn = i.int()
+        root = node()
+        rw = i.double()
+        feats = [i.int() for _ in range(i.int())]
+        trees.append(TreeRecord(tid, nn, root, lr, rw, feats))
+    cols = sorted({f for t in trees for f in t.features} | set(names))
+    mapping = {c: j for j, c in enumerate(cols)}
+    return TreeModelFile(alg, loss, is_cls, ova, len(cols), {}, names, cats, mapping, [trees], 0)
+
+
 def read_tree_model(path_or_bytes) -> TreeModelFile:
     data = path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray)) else open(path_or_bytes, "rb").read()
+    if _is_legacy(bytes(data)):
+        return read_legacy_tree_model(bytes(data))
     i = JavaIn(bytes(data))
     version = i.int()
     alg = i.utf()

@@ -249,6 +249,13 @@ class TreeTrainer:
         return self._codes_cache
 
     # ------------------------------------------------------------------------------------
+    def _reseed_rows(self, tree_index: int) -> None:
+        """Row-level randomness (bagging sub-samples, GBT dropout) is a pure function of (seed,
+        rank, first tree of the batch): a run resumed from a checkpoint draws exactly the streams
+        of an uninterrupted run, and every rank's shard draws its own (uncorrelated) stream."""
+        r = dist.info().rank
+        self.tgen.manual_seed((self.cfg.seed * 1_000_003 + r * 7_919 + tree_index * 104_729) % (1 << 63))
+
     def _weights_for_tree(self) -> torch.Tensor:
         c = self.cfg
         n = self.data.n
@@ -753,6 +760,7 @@ class TreeTrainer:
         out, vout = self._out, self._vout
         for _ in range(n_trees):
             tid = len(self.trees)
+            self._reseed_rows(tid)
             if c.is_gbt:
                 w = self._weights_for_tree()
                 if tid == 0:
@@ -791,7 +799,10 @@ class TreeTrainer:
                     # so the batch equals growing them one by one)
                     t0 = time.perf_counter()
                     b = self._forest_batch(max(1, c.tree_num - tid))
-                    ws = [self._weights_for_tree() for _ in range(b)]
+                    ws = []
+                    for k in range(b):          # per-tree streams: the batch == one-by-one growth
+                        self._reseed_rows(tid + k)
+                        ws.append(self._weights_for_tree())
                     self._pending = self.grow_forest(d.y, ws, 1.0, list(range(tid, tid + b)))
                     self.timings["forest"] = self.timings.get("forest", 0.0) + time.perf_counter() - t0
                 tree = self._pending.pop(0)
@@ -832,7 +843,7 @@ class TreeTrainer:
                     "features_used": list(map(int, t.features_used))}
         trees = [enc(t) for t in self.trees]
         return {"trees": trees, "pending": [enc(t) for t in self._pending], "train_errors": list(self.train_errors), "valid_errors": list(self.valid_errors),
-                "rng": self.rng.bit_generator.state, "tgen": self.tgen.get_state()}
+                "rng": self.rng.bit_generator.state}
 
     def load_state_dict(self, st: dict) -> None:
         def dec(d):
@@ -846,8 +857,7 @@ class TreeTrainer:
         self.trees = [dec(d) for d in st["trees"]]
         self._pending = [dec(d) for d in st.get("pending", [])]
         self.train_errors, self.valid_errors = list(st["train_errors"]), list(st["valid_errors"])
-        self.rng.bit_generator.state = st["rng"]
-        self.tgen.set_state(st["tgen"])
+        self.rng.bit_generator.state = st["rng"]       # row streams: _reseed_rows(tree index)
         # replay predictions and residuals
         self.pred = self.predict(self.data) * (len(self.trees) if not self.cfg.is_gbt and self.trees else 1)
         if self.valid is not None:

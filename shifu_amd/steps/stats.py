@@ -10,6 +10,8 @@ adjacent bins with the smallest IV loss down to ``-n`` bins (``-ivr`` keeps >= r
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from ..algos import normalize as N
@@ -65,7 +67,8 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
             from .base import shard_model_data
             cc_unit = [c for c in ms.ccs if c.name == unit]
             md = shard_model_data(ms.load_raw(cols + cc_unit))
-            S.compute_psi(mc, ms.ccs, md, unit)
+            S.compute_psi(mc, ms.ccs, md, unit,
+                          unit_stats_path=os.path.join(ms.pf.tmp_dir, "columnconfig.unitstats"))
             ms.save_cc()
         else:
             _log.warning("stats -p: stats.psiColumnName is empty")

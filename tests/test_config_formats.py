@@ -117,3 +117,31 @@ def test_readable_zip_spec_matches_reference_bytes(tmp_path, ref_resources):
     z1, z2 = zipfile.ZipFile(tmp_path / "m.zip"), zipfile.ZipFile(os.path.join(spec, "model0.zip"))
     assert z1.read("trees") == z2.read("trees")
     assert json.loads(z1.read("model.ini")) == json.loads(z2.read("model.ini"))
+
+
+def test_legacy_pre_versioned_gbt_fixture(ref_resources):
+    """The wdbc model set's model0.gbt predates the version field (int-framed strings, impurity +
+    leaf flag + weight ratio per node, column names in the splits).  Parsed completely (every byte
+    consumed, 13 nodes) and scored through the same TreeModelFile path; the expected leaf values
+    follow from the stored tree (root worst_concave_points < 0.14781, ...)."""
+    import numpy as np
+    from shifu_amd.formats.tree_format import read_tree_model, CONTINUOUS
+    path = os.path.join(REF_TR, "example", "wdbc", "wdbcModelSetLocal", "models", "model0.gbt")
+    m = read_tree_model(path)
+    assert m.algorithm == "GBT" and m.loss == "squared" and m.version == 0
+    t = m.bags[0][0]
+    assert t.node_num == 13 and t.root_wgt_cnt == 290.0 and len(t.features) == 13
+    assert t.root.split.column == 29 and t.root.split.ftype == CONTINUOUS
+    assert abs(t.root.split.threshold - 0.14781) < 1e-12 and m.names[29] == "worst_concave_points"
+
+    def count(nd):
+        return 0 if nd is None else 1 + count(nd.left) + count(nd.right)
+    assert count(t.root) == 13
+    x = {c: np.array([0.1, 0.2, 0.2]) for c in m.names}
+    x[15] = np.array([10.0, 10.0, 10.0])        # std_area
+    x[22] = np.array([20.0, 20.0, 10.0])        # worst_radius
+    # row 0: left, left (std_area < 31.68), left (worst_concavity < 0.378) -> leaf 8 (0.0)
+    # row 1: right (0.2 >= 0.14781), right (worst_radius >= 16.095) -> leaf 7 (1.0)
+    # row 2: right, left -> leaf 6 (0.714...)
+    s = m.score(x, 3)
+    np.testing.assert_allclose(s, [0.0, 0.1, 0.1 * 0.7142857142857143], rtol=1e-12)

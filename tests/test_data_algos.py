@@ -105,6 +105,12 @@ def test_stats_and_normalize_cancer(cancer):
     assert np.isin(np.round(Xw[:, j], 5), np.round(np.asarray(c.bin_count_woe, np.float32), 5)).all()
     C, nb, is_cat = N.tree_bin_codes(ccs, md.table, [cc for cc in ccs if not cc.is_target()])
     assert C.max() < nb.max() and (C >= 0).all()
+    # WOE_ZSCALE_INDEX on a numeric column = z-scored WOE (Normalizer.fullNormalize :305-315)
+    Xz, _, _ = N.normalize_table(mc, ccs, md.table, norm_type="WOE_ZSCALE_INDEX")
+    Xwz, _, _ = N.normalize_table(mc, ccs, md.table, norm_type="WOE_ZSCALE")
+    np.testing.assert_allclose(Xz[:, j], Xwz[:, j], rtol=1e-6)
+    m, sd = N.woe_mean_std(c, False)
+    np.testing.assert_allclose(Xz[:, j], N.zscore(Xw[:, j].astype(np.float64), m, sd, cut), rtol=1e-5, atol=1e-6)
 
 
 def test_varsel_filter_ks_iv_mix(cancer):

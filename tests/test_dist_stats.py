@@ -249,3 +249,78 @@ def test_psi_two_ranks_match_single(tmp_path):
     keys = [k for k in pa if pa[k] is not None]
     assert keys and all(pb[k] is not None for k in keys)
     np.testing.assert_allclose([pa[k] for k in keys], [pb[k] for k in keys], rtol=1e-9, atol=1e-12)
+    def unit_stats(root):            # {col: [(unit, mean, missing rate, count)]}
+        out = {}
+        for line in open(os.path.join(root, "tmp", "columnconfig.unitstats")).read().splitlines():
+            col, rest = line.split("|", 1)
+            out[col] = [(u, float(m), float(r), int(n)) for u, m, r, n in (x.split("^") for x in rest.split("\u0001"))]
+        return out
+    ua, ub = unit_stats(a), unit_stats(b)
+    assert ua.keys() == ub.keys() and ua
+    for k in ua:                    # value sums are all-reduced: equal up to summation order
+        assert [(u, n) for u, _, _, n in ua[k]] == [(u, n) for u, _, _, n in ub[k]]
+        np.testing.assert_allclose([x[1:3] for x in ua[k]], [x[1:3] for x in ub[k]], rtol=1e-12)
+
+
+def _java_psi(expected, per_unit_counts):
+    """PSICalculatorUDF.exec :70-97 transcribed literally (index advances only on added terms)."""
+    import math
+    psi = 0.0
+    for sub in per_unit_counts:
+        total = float(sum(sub))
+        i = 0
+        for s in sub:
+            if total == 0:
+                continue
+            elif expected[i] == 0:
+                continue
+            else:
+                log_num = (s / total) / expected[i]
+                if log_num <= 0:
+                    continue
+                psi += (s / total - expected[i]) * math.log(log_num)
+            i += 1
+    return psi
+
+
+def test_psi_reference_parity(tmp_path):
+    """PSI from the ColumnConfig stats' expected distribution + the UDF's loop, and unit stats
+    'unit^mean^missingRate^count' (sorted, \\u0001-joined) in tmp/columnconfig.unitstats."""
+    from shifu_amd.algos import binning as B
+    from shifu_amd.config.column_config import load_column_configs
+    from shifu_amd.config.jsonio import java_double_str
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps.base import ModelSet
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=900, n_num=4, n_cat=2)
+    mc = ModelConfig.load(os.path.join(a, "ModelConfig.json"))
+    mc.stats["psiColumnName"] = "cat_0"
+    mc.save()
+    run_init(a)
+    run_stats(a)
+    run_stats(a, psi=True)
+    ccs = load_column_configs(os.path.join(a, "ColumnConfig.json"))
+    ms = ModelSet(a)
+    md = ms.load_raw([c for c in ms.ccs if c.name in ("num_0", "cat_0")])
+    units_s = md.table["cat_0"].strings()
+    units = sorted(set(units_s))
+    cc = next(c for c in ccs if c.name == "num_0")
+    v = md.table["num_0"].numeric()
+    bidx = B.bin_index_numeric(v, cc.bin_boundary)
+    nb = len(cc.bin_boundary) + 1
+    per_unit = [np.bincount(bidx[units_s == u], minlength=nb) for u in units]
+    tot = float(cc.stat("totalCount"))
+    expected = [(n + p) / tot for n, p in zip(cc.bin_count_neg, cc.bin_count_pos)]
+    assert abs(cc.stats["psi"] - _java_psi(expected, per_unit)) < 1e-12
+    lines = dict(l.split("|", 1) for l in open(os.path.join(a, "tmp", "columnconfig.unitstats")).read().splitlines())
+    stats = lines[str(cc.num)].split("\u0001")
+    assert stats == sorted(stats) and len(stats) == len(units)
+    u0 = units[0]
+    m = units_s == u0
+    n0, miss = int(m.sum()), int(np.isnan(v[m]).sum())
+    mean = float("nan") if n0 == miss else float(np.nansum(v[m])) / n0
+    want = f"{u0}^{java_double_str(mean)}^{java_double_str(miss / n0)}^{n0}"
+    assert want in stats
