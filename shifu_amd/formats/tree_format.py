@@ -469,6 +469,53 @@ def heap_tree_to_record(tree, tree_id: int, columns, ccs_by_feature=None, learni
                       sorted({columns[f].num for f in tree.features_used}))
 
 
+def record_to_heap_tree(rec: TreeRecord, columns, min_depth: int = 1):
+    """Inverse of ``heap_tree_to_record`` for continuous training: a stored tree (column numbers,
+    raw-value thresholds) -> ``models.gbdt.Tree`` over the current binned features.  Node ids are
+    heap ids in both (``Node.leftIndex`` = 2 id).  A numeric threshold t maps to the last bin whose
+    upper boundary is <= t (exact when the ColumnConfig boundaries are the ones the model was
+    trained with); a categorical split's stored side maps to the left-bin bitset."""
+    from ..models.gbdt import Tree
+    pos = {c.num: j for j, c in enumerate(columns)}
+
+    def max_id(nd):
+        return 0 if nd is None else max(nd.id, max_id(nd.left), max_id(nd.right))
+    depth = max(min_depth, int(max_id(rec.root)).bit_length())
+    t = Tree(depth, float(rec.learning_rate))
+    used = set()
+
+    def put(nd):
+        if nd is None:
+            return
+        i = nd.id
+        t.exists[i] = True
+        t.gain[i] = nd.gain
+        t.wgt_cnt[i] = nd.wgt_cnt
+        s = nd.split
+        if s is not None and not (nd.left is None and nd.right is None) and s.column in pos:
+            f = pos[s.column]
+            cc = columns[f]
+            t.feat[i] = f
+            used.add(f)
+            if s.ftype == CATEGORICAL:
+                ncat = len(cc.bin_category or [])
+                stored = set(s.categories or set())
+                left = stored if s.is_left else set(range(ncat + 1)) - stored
+                for b in left:
+                    t.cat_left[i, b >> 5] |= np.uint32(1 << (b & 31))
+            else:
+                bb = np.asarray(cc.bin_boundary, dtype=np.float64)
+                thr = s.threshold
+                t.thr[i] = len(bb) - 1 if not np.isfinite(thr) else int(np.searchsorted(bb, thr, "right")) - 2
+            put(nd.left)
+            put(nd.right)
+        else:
+            t.value[i] = float(nd.predict or 0.0)
+    put(rec.root)
+    t.features_used = sorted(used)
+    return t
+
+
 def feature_importance(model: TreeModelFile) -> dict:
     """Gain-accumulated feature importance (TreeNode.computeFeatureImportance, scikit-learn style)."""
     imp = {}

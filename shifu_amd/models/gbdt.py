@@ -858,6 +858,18 @@ class TreeTrainer:
         self._pending = [dec(d) for d in st.get("pending", [])]
         self.train_errors, self.valid_errors = list(st["train_errors"]), list(st["valid_errors"])
         self.rng.bit_generator.state = st["rng"]       # row streams: _reseed_rows(tree index)
+        self._replay()
+
+    def continue_from(self, trees: list) -> None:
+        """GBT continuous training (DTMaster.init :1081-1104): start from an existing model's trees
+        (first tree weight 1.0, the others their learning rate); predictions and pseudo-residuals
+        are replayed over the shard, and the next tree is tree ``len(trees)`` at the current
+        learning rate."""
+        self.trees = list(trees)
+        self._pending = []
+        self._replay()
+
+    def _replay(self) -> None:
         # replay predictions and residuals
         self.pred = self.predict(self.data) * (len(self.trees) if not self.cfg.is_gbt and self.trees else 1)
         if self.valid is not None:

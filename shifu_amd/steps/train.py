@@ -611,6 +611,12 @@ class TrainStep:
         if self.resume and os.path.exists(ckpt):
             tt.load_state_dict(torch.load(ckpt, weights_only=True))
             _log.info("resumed trainer %d from checkpoint with %d trees", tid, len(tt.trees))
+        else:
+            existing = self._continuous_trees(tid, cfg)
+            if existing == -1:
+                return float("nan")
+            if existing:
+                tt.continue_from(existing)
         interval = checkpoint_interval(p, max(1, tree_num // 10))   # DTOutput: tmp models every treeNum/10
         wd = IterationWatchdog(iteration_limit(800.0), "tree").__enter__()
         while len(tt.trees) < tree_num:
@@ -630,6 +636,40 @@ class TrainStep:
             if os.path.exists(ckpt):
                 os.remove(ckpt)
         return tt.valid_errors[-1] if tt.valid_errors else float("nan")
+
+    def _continuous_trees(self, tid, cfg):
+        """``checkContinuousTraining`` (TrainModelProcessor.java:1149-1197) for trees: GBT only, the
+        existing model must be GBT with the same loss and fewer than TreeNum trees.  Returns the
+        existing trees as heap trees, [] (train from scratch) or -1 (already >= TreeNum trees:
+        this trainer is skipped, as the reference skips it)."""
+        mc, ms = self.mc, self.ms
+        if not bool(mc.train.get("isContinuous", False)):
+            return []
+        path = ms.pf.model_path(tid, mc.algorithm.lower())
+        if not os.path.exists(path):
+            _log.info("No existing model, model training will start from scratch.")
+            return []
+        if not cfg.is_gbt:
+            _log.warning("RF doesn't support continuous training")
+            return []
+        m = tree_format.read_tree_model(path)
+        if m.algorithm.upper() != "GBT":
+            _log.warning("Only GBT supports continuous training, while not GBT, will start from scratch")
+            return []
+        if m.loss.lower() != cfg.loss.lower():
+            _log.warning("Loss is changed, continuous training is disabled, will start from scratch")
+            return []
+        recs = [t for bag in m.bags for t in bag]
+        if not recs:
+            return []
+        if len(recs) >= cfg.tree_num:
+            _log.warning("Model with index %d with size of trees is over treeNum, such training will not be "
+                         "started.", tid)
+            return -1
+        cols = [c for c in ms.input_columns()]
+        trees = [tree_format.record_to_heap_tree(r, cols) for r in recs]
+        _log.info("continuous training of trainer %d from %s with %d existing trees", tid, path, len(trees))
+        return trees
 
     def _write_trees(self, tid, tt):
         ms, mc = self.ms, self.mc

@@ -220,3 +220,48 @@ def test_segment_expansion_pipeline(tmp_path):
     _run(root, ["varsel", "norm", "train", "eval"])
     auc = json.load(open(os.path.join(root, "evals/Eval1/EvalPerformance.json")))["areaUnderRoc"]
     assert auc > 0.7
+
+
+def test_gbt_continuous_training(tmp_path):
+    """isContinuous for GBT (TrainModelProcessor.checkContinuousTraining / DTMaster :1081-1104):
+    3 trees, then TreeNum 6 continues from the stored model (existing trees kept, predictions
+    replayed) and equals 6 trees trained straight; a changed loss restarts from scratch; an
+    existing model with >= TreeNum trees leaves the trainer untouched."""
+    from shifu_amd.formats.tree_format import read_tree_model
+    from shifu_amd.utils.synthetic import make_model_set
+    roots = []
+    for name in ("a", "b"):
+        root = make_model_set(str(tmp_path), name, "GBT", n_rows=800)
+        mc = _mc(root)
+        mc.train["baggingNum"] = 1
+        mc.train["validSetRate"] = 0.0
+        mc.train["params"].update({"TreeNum": 3 if name == "a" else 6, "MaxDepth": 3,
+                                   "FeatureSubsetStrategy": "ALL", "LearningRate": 0.2})
+        mc.save()
+        _run(root, ["init", "stats", "norm", "train"])
+        roots.append(root)
+    a, b = roots
+    mpath = os.path.join(a, "models/model0.gbt")
+    first = read_tree_model(mpath)
+    assert len(first.bags[0]) == 3
+    mc = _mc(a)
+    mc.train["isContinuous"] = True
+    mc.train["params"]["TreeNum"] = 6
+    mc.save()
+    _run(a, ["train"])
+    cont, straight = read_tree_model(mpath), read_tree_model(os.path.join(b, "models/model0.gbt"))
+    assert len(cont.bags[0]) == 6
+    x = {c: np.linspace(-3, 3, 64) for c in cont.names}
+    np.testing.assert_allclose(cont.score(x, 64), straight.score(x, 64), rtol=1e-5, atol=1e-6)
+    # >= TreeNum existing trees: skipped (model unchanged)
+    mtime = os.path.getmtime(mpath)
+    _run(a, ["train"])
+    assert os.path.getmtime(mpath) == mtime
+    # loss changed: from scratch (TreeNum trees, not appended)
+    mc = _mc(a)
+    mc.train["params"]["TreeNum"] = 8
+    mc.train["params"]["Loss"] = "absolute"
+    mc.save()
+    _run(a, ["train"])
+    assert len(read_tree_model(mpath).bags[0]) == 8
+    assert read_tree_model(mpath).loss == "absolute"
