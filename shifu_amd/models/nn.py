@@ -406,6 +406,48 @@ class Optimizer:
             w.copy_(torch.where(keep, w0, w))
 
 
+def can_grow(old_sizes, new_sizes) -> bool:
+    """``NNStructureComparator.compare(new, old) == 1`` (J/core/dtrain/nn/NNStructureComparator.java:
+    25-37) on input-first layer sizes: the new network has at least as many layers, and aligned from
+    the input end every non-output layer of the old network fits (>=) into the new one; the new
+    output is at least as wide."""
+    if len(new_sizes) < len(old_sizes) or new_sizes[-1] < old_sizes[-1]:
+        return False
+    return all(new_sizes[k] >= old_sizes[k] for k in range(len(old_sizes) - 1))
+
+
+def grow_weights(trainer: "MLPTrainer", old_weights, fixed_layers=None, fixed_bias: bool = True) -> int:
+    """``NNMaster.fitExistingModelIn`` (J/core/dtrain/nn/NNMaster.java:605-645): copy a smaller
+    existing network into the trainer's freshly initialised larger one, layers aligned from the
+    input end; each old weight matrix [out, in + 1] fills the top-left block of the new one and its
+    bias column moves to the new bias column.  Weights copied into a ``FixedLayers`` layer (1-based
+    from the input side; its bias too unless ``FixedBias`` is false) stay frozen.  Returns the
+    number of frozen weights."""
+    p = trainer.params
+    views = p.views()
+    mask = torch.zeros(p.numel, dtype=torch.bool)
+    fixed = set(int(x) for x in (fixed_layers or []))
+    with torch.no_grad():
+        for l, W in enumerate(old_weights):
+            W = torch.as_tensor(np.asarray(W), dtype=torch.float32)
+            o, i = W.shape[0], W.shape[1] - 1
+            k_new = trainer.spec.layer_in[l]
+            views[l][:o, :i] = W[:, :i].to(views[l].device)
+            views[l][:o, k_new] = W[:, i].to(views[l].device)
+            if l + 1 in fixed:
+                kp = p.shapes[l][1]
+                rows = torch.arange(o).unsqueeze(1) * kp + p.offsets[l]
+                mask[(rows + torch.arange(i).unsqueeze(0)).reshape(-1)] = True
+                if fixed_bias:
+                    mask[(torch.arange(o) * kp + p.offsets[l] + k_new)] = True
+    dist.broadcast_(p.flat, 0)
+    if mask.any():
+        prev = trainer.opt.fixed
+        m = mask.to(trainer.device)
+        trainer.opt.fixed = (m if prev is None else (prev.bool() | m)).to(torch.uint8)
+    return int(mask.sum())
+
+
 class MLPTrainer:
     """Data-parallel full-batch (or mini-batch) MLP trainer."""
 

@@ -26,7 +26,7 @@ import torch
 
 from ..formats import nn_format, tree_format
 from ..models import lr as lrmod
-from ..models.nn import MLPSpec, MLPTrainer
+from ..models.nn import MLPSpec, MLPTrainer, can_grow, grow_weights
 from ..parallel import dist
 from ..runtime.fault import IterationWatchdog, check_finite, iteration_limit, maybe_fault
 from ..utils.log import get_logger
@@ -402,13 +402,21 @@ class TrainStep:
         spec = self._nn_spec(p, n_in, n_out)
         epochs = int(mc.train.get("numTrainEpochs", 100))
         init = None
+        grow = None
         cont = bool(mc.train.get("isContinuous", False))
         mpath = ms.pf.model_path(tid, "nn")
         if cont and os.path.exists(mpath):
             net = nn_format.read_encog(mpath)
-            if net.sizes == [n_in] + spec.hidden + [n_out]:
+            sizes = [n_in] + spec.hidden + [n_out]
+            if net.sizes == sizes:
                 init = net.flat()["weights"]
                 _log.info("continuous training from %s", mpath)
+            elif can_grow(net.sizes, sizes):
+                grow = net               # NNMaster.fitExistingModelIn: the old net inside the new one
+                _log.info("continuous training from %s: existing %s grown into %s", mpath, net.sizes, sizes)
+            else:
+                _log.warning("!!! Model training parameters like hidden nodes, activation and others are not "
+                             "consistent with settings, model training will start from scratch.")
         tr = MLPTrainer(spec, self.dev, str(p.get("Propagation", "R")), float(_num(p.get("LearningRate"), 0.1)),
                         momentum=float(_num(p.get("Momentum"), 0.5)),
                         adam_beta1=float(_num(p.get("AdamBeta1"), 0.9)),
@@ -416,9 +424,16 @@ class TrainStep:
                         learning_decay=float(_num(p.get("LearningDecay"), 0.0)),
                         reg=float(_num(p.get("RegularizedConstant"), 0.0)), reg_level=p.get("L1orL2", "NONE"),
                         seed=1000 + tid, weight_init=p.get("WeightInitializer", "default"),
-                        init_flat_encog=init, fixed_layers=p.get("FixedLayers"),
+                        # FixedLayers / FixedBias act only when training continues from an existing
+                        # model (NNMaster.initOrRecoverParams :340-352): whole layers for the same
+                        # structure, the copied block for a grown one (grow_weights below)
+                        init_flat_encog=init, fixed_layers=p.get("FixedLayers") if init is not None else None,
                         dropout_rate=float(_num(p.get("DropoutRate"), 0.0)),
-                        fixed_bias=str(p.get("FixedBias", "false")).lower() == "true")
+                        fixed_bias=False)
+        if grow is not None:
+            nfix = grow_weights(tr, grow.weights, p.get("FixedLayers"),
+                                fixed_bias=str(p.get("FixedBias", "true")).lower() == "true")
+            _log.info("fitExistingModelIn: %d weights frozen", nfix)
         yy = y
         if multi:
             yy = np.eye(n_out, dtype=np.float32)[np.clip(np.rint(y).astype(int), 0, n_out - 1)]

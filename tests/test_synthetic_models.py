@@ -265,3 +265,33 @@ def test_gbt_continuous_training(tmp_path):
     _run(a, ["train"])
     assert len(read_tree_model(mpath).bags[0]) == 8
     assert read_tree_model(mpath).loss == "absolute"
+
+
+def test_nn_continuous_structure_growth(tmp_path):
+    """isContinuous with a larger network (NNMaster.fitExistingModelIn): the old 1-hidden-layer
+    weights sit in the top-left blocks of the new [8, 6]-hidden network, the old bias columns in
+    the new bias columns; FixedLayers [1] keeps the copied first-layer block (and its bias,
+    FixedBias default true) frozen through training while the rest moves."""
+    from shifu_amd.formats.nn_format import read_encog
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "g", "NN", n_rows=900)
+    mc = _mc(root)
+    mc.train["numTrainEpochs"] = 5
+    mc.train["baggingNum"] = 1
+    mc.train["params"].update({"NumHiddenLayers": 1, "NumHiddenNodes": [4], "ActivationFunc": ["Sigmoid"]})
+    mc.save()
+    _run(root, ["init", "stats", "norm", "train"])
+    old = read_encog(os.path.join(root, "models/model0.nn"))
+    mc = _mc(root)
+    mc.train["isContinuous"] = True
+    mc.train["params"].update({"NumHiddenLayers": 2, "NumHiddenNodes": [8, 6], "ActivationFunc": ["Sigmoid", "Sigmoid"],
+                               "FixedLayers": [1]})
+    mc.save()
+    _run(root, ["train"])
+    new = read_encog(os.path.join(root, "models/model0.nn"))
+    assert new.sizes == [old.sizes[0], 8, 6, 1]
+    W0o, W0n = old.weights[0], new.weights[0]
+    n_in = old.sizes[0]
+    np.testing.assert_allclose(W0n[:4, :n_in], W0o[:, :n_in], rtol=1e-6, atol=1e-7)   # frozen block
+    np.testing.assert_allclose(W0n[:4, n_in], W0o[:, n_in], rtol=1e-6, atol=1e-7)     # frozen bias
+    assert not np.allclose(new.weights[1][:1, :4], old.weights[1][:, :4])            # layer 2 trains
