@@ -386,27 +386,67 @@ def compute_psi(mc, ccs, md, unit_column: str, unit_stats_path: str | None = Non
     return ccs
 
 
-def pearson_correlation(mats: np.ndarray, device=None):
-    """Pairwise-complete Pearson (H3, FastCorrelationMapper J/core/correlation/FastCorrelationMapper.java:171-278):
-    rows where either value is missing are skipped per pair.  Implemented as six GEMMs over the
-    masked matrix (X'X, (X^2)'M, M'(X^2), M'M, X'M, M'X) on the device (MFMA via hipBLASLt)."""
-    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
-    X = torch.as_tensor(mats, dtype=torch.float64, device=dev)
-    M = torch.isfinite(X).to(torch.float64)
-    Xz = torch.where(M > 0, X, torch.zeros_like(X))
-    X2 = Xz * Xz
-    n = M.t() @ M
-    sx = Xz.t() @ M          # sum of x_i over rows where j present
-    sy = M.t() @ Xz          # sum of x_j over rows where i present
-    sxx = X2.t() @ M
-    syy = M.t() @ X2
-    sxy = Xz.t() @ Xz
-    from ..parallel import dist
-    if dist.info().world_size > 1:       # row-sharded: the six F x F sums in one all-reduce
-        st = dist.all_reduce_(torch.stack([n, sx, sy, sxx, syy, sxy]))
-        n, sx, sy, sxx, syy, sxy = st.unbind(0)
-    num = sxy - sx * sy / n.clamp(min=1)
-    den = torch.sqrt((sxx - sx * sx / n.clamp(min=1)).clamp(min=0) * (syy - sy * sy / n.clamp(min=1)).clamp(min=0))
-    corr = torch.where(den > 0, num / den, torch.zeros_like(num))
-    corr.fill_diagonal_(1.0)
-    return corr.cpu().numpy()
+class CorrAccumulator:
+    """Pairwise-complete Pearson sums (H3, FastCorrelationMapper J/core/correlation/
+    FastCorrelationMapper.java:171-278: rows where either value is missing are skipped per pair),
+    accumulated over row chunks on the device: per chunk four F x F GEMMs (hipBLASLt, fp64) of the
+    zero-filled values Xz, their squares and the validity mask M --
+        n = M'M,  sx = Xz'M (sum of x_i where j valid; sy = sx'),  sxx = (Xz*Xz)'M (syy = sxx'),
+        sxy = Xz'Xz
+    -- so the table never has to sit on the device (or in fp64 on the host) whole."""
+
+    def __init__(self, n_cols: int, device=None):
+        self.F = int(n_cols)
+        self.dev = torch.device(device) if device is not None else \
+            (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        self.sums = torch.zeros(4, self.F, self.F, dtype=torch.float64, device=self.dev)
+
+    def update(self, X) -> None:
+        X = torch.as_tensor(np.asarray(X), dtype=torch.float64).to(self.dev)
+        M = torch.isfinite(X).to(torch.float64)
+        Xz = torch.where(M > 0, X, torch.zeros_like(X))
+        self.sums[0].addmm_(M.t(), M)
+        self.sums[1].addmm_(Xz.t(), M)
+        self.sums[2].addmm_((Xz * Xz).t(), M)
+        self.sums[3].addmm_(Xz.t(), Xz)
+
+    @staticmethod
+    def _corr_rows(n, sx, sy, sxx, syy, sxy):
+        num = sxy - sx * sy / n.clamp(min=1)
+        den = torch.sqrt((sxx - sx * sx / n.clamp(min=1)).clamp(min=0) * (syy - sy * sy / n.clamp(min=1)).clamp(min=0))
+        return torch.where(den > 0, num / den, torch.zeros_like(num))
+
+    def finalize(self, dst: int = 0):
+        """Global correlation matrix on rank ``dst`` (numpy), None elsewhere.  Data parallel: the
+        six F x F sums (the four + the transposes that supply sy/syy) are REDUCE-SCATTERED by row
+        blocks -- each rank gets 1/R of the bytes an all-reduce would leave on every rank --, every
+        rank computes its block of correlation rows, and the blocks are gathered to ``dst``."""
+        from ..parallel import dist
+        F = self.F
+        n, sx, sxx, sxy = self.sums.unbind(0)
+        six = torch.stack([n, sx, sx.t(), sxx, sxx.t(), sxy])
+        blk = dist.reduce_scatter_rows(six)
+        a, b = dist.row_block(F)
+        rows = self._corr_rows(*blk.unbind(0))
+        idx = torch.arange(a, b, device=rows.device)
+        rows[idx - a, idx] = 1.0
+        full = dist.gather_rows_to(rows, F, dst)
+        return None if full is None else full.cpu().numpy()
+
+
+def pearson_correlation(mats, device=None, chunk_rows: int = 1 << 18, dst: int = 0):
+    """Pairwise-complete Pearson of the columns of ``mats`` ([N, F] array, NaN = missing, or an
+    iterable of such row chunks) -> [F, F] on rank ``dst`` (every rank when not distributed)."""
+    acc = None
+    chunks = [mats] if isinstance(mats, np.ndarray) or torch.is_tensor(mats) else mats
+    for X in chunks:
+        X = np.asarray(X) if not torch.is_tensor(X) else X
+        if acc is None:
+            acc = CorrAccumulator(X.shape[1], device)
+        for r0 in range(0, X.shape[0], chunk_rows):
+            acc.update(X[r0:r0 + chunk_rows])
+    if acc is None:
+        return np.zeros((0, 0))
+    return acc.finalize(dst)
+
+

@@ -111,6 +111,10 @@ class Column:
     def missing_mask(self) -> np.ndarray:
         return np.isnan(self.values) if self.kind == "num" else self.values < 0
 
+    def slice(self, a: int, b: int) -> "Column":
+        """Rows [a, b) (a view of the values, same dictionary)."""
+        return Column(self.name, self.kind, self.values[a:b], self.dictionary)
+
 
 def _java_num_str(v: float) -> str:
     if v == int(v) and abs(v) < 1e15:

@@ -166,6 +166,55 @@ def all_gather_cat(t: torch.Tensor) -> torch.Tensor:
     return torch.cat([o[: int(s.item())] for o, s in zip(outs, sizes)])
 
 
+def row_block(n: int, rank: int | None = None, world: int | None = None) -> tuple:
+    """[a, b) of ``n`` rows owned by ``rank`` in a block partition (blocks differ by <= 1 row)."""
+    i = info()
+    r = i.rank if rank is None else rank
+    w = i.world_size if world is None else world
+    q, m = divmod(n, w)
+    a = r * q + min(r, m)
+    return a, a + q + (1 if r < m else 0)
+
+
+def reduce_scatter_rows(t: torch.Tensor) -> torch.Tensor:
+    """Sum ``t`` [K, F, C] over ranks and return this rank's row block [K, b - a, C] (``row_block``
+    of F).  RCCL: one ``reduce_scatter_tensor`` over rank-major padded blocks (each rank receives
+    1/R of the bytes an all-reduce would leave everywhere); gloo (no reduce-scatter): all-reduce +
+    slice."""
+    if not _active():
+        return t
+    K, F, C = t.shape
+    w, r = tdist.get_world_size(), tdist.get_rank()
+    a, b = row_block(F, r, w)
+    if tdist.get_backend() != "nccl":
+        all_reduce_(t)
+        return t[:, a:b].contiguous()
+    fb = -(-F // w)
+    src = torch.zeros(w, K, fb, C, dtype=t.dtype, device=t.device)
+    for k in range(w):
+        ka, kb = row_block(F, k, w)
+        src[k, :, : kb - ka] = t[:, ka:kb]
+    out = torch.empty(K, fb, C, dtype=t.dtype, device=t.device)
+    tdist.reduce_scatter_tensor(out.reshape(-1), src.reshape(-1), op=tdist.ReduceOp.SUM)
+    return out[:, : b - a].contiguous()
+
+
+def gather_rows_to(t: torch.Tensor, n: int, dst: int = 0):
+    """Concatenate every rank's row block ``t`` [b - a, C] of an [n, C] matrix on rank ``dst``
+    (None elsewhere)."""
+    if not _active():
+        return t
+    w, r = tdist.get_world_size(), tdist.get_rank()
+    fb = -(-n // w)
+    pad = torch.zeros(fb, t.shape[1], dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    outs = [torch.zeros_like(pad) for _ in range(w)] if r == dst else None
+    tdist.gather(pad, outs, dst=dst)
+    if r != dst:
+        return None
+    return torch.cat([outs[k][: row_block(n, k, w)[1] - row_block(n, k, w)[0]] for k in range(w)])
+
+
 def all_reduce_max_scalar(x: float, device=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device or "cpu")
     all_reduce_(t, "max")

@@ -75,23 +75,50 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
     return 0
 
 
-def run_correlation(ms: ModelSet, device=None):
+def run_correlation(ms: ModelSet, device=None, chunk_rows: int = 1 << 18):
     """Pairwise-complete Pearson over numeric raw values (categoricals via their pos-rate encoding),
-    written as ``correlation.csv`` (header row + one row per column, ``ColumnConfig`` order)."""
+    written as ``correlation.csv`` (header row + one row per column, ``ColumnConfig`` order).
+
+    Rows stream through ``CorrAccumulator`` in ``chunk_rows`` chunks (only one chunk of fp64 values
+    exists at a time); data parallel: row shards, sums reduce-scattered by column blocks, rows
+    gathered to the writer.  ``shifu.stats.corr.reuse=true`` with a previous run's matrix for the
+    same columns under ``tmp/CorrelationPath`` skips the data pass (StatsModelProcessor :140-146,
+    dumpAndCalculateCorrelationResult)."""
+    import json
+    from ..config import environment
+    from ..parallel import dist
     mc = ms.mc
     cols = [c for c in ms.stats_columns() if c.bin_boundary or c.bin_category]
+    nums = [c.num for c in cols]
     from .base import _writer, shard_model_data
-    md = shard_model_data(ms.load_raw(cols))
-    mats = []
-    for c in cols:
-        col = md.table[c.name]
-        if c.is_categorical():
-            mats.append(N.normalize_column(c, col, "OLD_ZSCALE", None)[:, 0])
-        else:
-            v = col.numeric().astype(np.float64)
-            mats.append(v)
-    X = np.stack(mats, 1) if mats else np.zeros((md.n, 0))
-    C = S.pearson_correlation(X, device)
+    cache_dir = ms.pf.correlation_path
+    cache_m, cache_c = os.path.join(cache_dir, "corr.npy"), os.path.join(cache_dir, "columns.json")
+    C = None
+    if environment.get_bool("shifu.stats.corr.reuse", False) and os.path.exists(cache_m) and \
+            os.path.exists(cache_c) and json.load(open(cache_c)) == nums:
+        _log.info("correlation: reusing %s (shifu.stats.corr.reuse)", cache_m)
+        C = np.load(cache_m, allow_pickle=False)
+    else:
+        md = shard_model_data(ms.load_raw(cols))
+        acc = S.CorrAccumulator(len(cols), device)
+        for r0 in range(0, max(md.n, 1), chunk_rows):
+            r1 = min(md.n, r0 + chunk_rows)
+            if r1 <= r0:
+                break
+            mats = []
+            for c in cols:
+                col = md.table[c.name]
+                if c.is_categorical():
+                    mats.append(N.normalize_column(c, col.slice(r0, r1), "OLD_ZSCALE", None)[:, 0])
+                else:
+                    mats.append(col.numeric()[r0:r1].astype(np.float64))
+            acc.update(np.stack(mats, 1) if mats else np.zeros((r1 - r0, 0)))
+        C = acc.finalize(0)
+        if _writer() and C is not None:
+            os.makedirs(cache_dir, exist_ok=True)
+            np.save(cache_m, C)
+            with open(cache_c, "w") as f:
+                json.dump(nums, f)
     if not _writer():
         return C, [c.num for c in cols]
     path = ms.pf.correlation_csv

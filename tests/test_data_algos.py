@@ -181,3 +181,15 @@ def test_parquet_input_matches_csv(tmp_path):
     np.testing.assert_array_equal(a["n"].values, b["n"].values)
     assert a["s"].strings().tolist() == b["s"].strings().tolist()
     assert a["t"].missing_mask().tolist() == b["t"].missing_mask().tolist()
+
+
+def test_pearson_chunked_equals_whole():
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(301, 5))
+    X[:, 2] += X[:, 0]
+    X[rng.random(X.shape) < 0.1] = np.nan
+    np.testing.assert_allclose(pearson_correlation(X, chunk_rows=7), pearson_correlation(X), rtol=1e-12,
+                               atol=1e-14)
+    parts = [X[:100], X[100:250], X[250:]]
+    np.testing.assert_allclose(pearson_correlation(iter(parts), chunk_rows=64), pearson_correlation(X),
+                               rtol=1e-12, atol=1e-14)

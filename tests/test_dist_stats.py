@@ -324,3 +324,33 @@ def test_psi_reference_parity(tmp_path):
     mean = float("nan") if n0 == miss else float(np.nansum(v[m])) / n0
     want = f"{u0}^{java_double_str(mean)}^{java_double_str(miss / n0)}^{n0}"
     assert want in stats
+
+
+def test_correlation_reuse_skips_data_pass(tmp_path, monkeypatch):
+    """shifu.stats.corr.reuse=true with a cached matrix for the same columns rewrites
+    correlation.csv from the cache (a sentinel planted in the cache must come out)."""
+    from shifu_amd.config import environment
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import read_correlation, run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=700, n_num=4, n_cat=1)
+    run_init(a)
+    run_stats(a)
+    run_stats(a, correlation=True)
+    n1, c1 = read_correlation(os.path.join(a, "correlation.csv"))
+    cache = os.path.join(a, "tmp", "CorrelationPath", "corr.npy")
+    C = np.load(cache)
+    C[0, 1] = C[1, 0] = 0.123456
+    np.save(cache, C)
+    run_stats(a, correlation=True)                      # reuse off: recomputed
+    n2, c2 = read_correlation(os.path.join(a, "correlation.csv"))
+    np.testing.assert_allclose(c2, c1, rtol=1e-12)
+    np.save(cache, C)
+    environment.set_property("shifu.stats.corr.reuse", "true")
+    try:
+        run_stats(a, correlation=True)
+    finally:
+        environment.set_property("shifu.stats.corr.reuse", "false")
+    n3, c3 = read_correlation(os.path.join(a, "correlation.csv"))
+    assert n3 == n1 and abs(c3[0, 1] - 0.123456) < 1e-12
