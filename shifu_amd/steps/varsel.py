@@ -64,13 +64,39 @@ def _train_quick_nn(ms, cols, epochs, device=None, seed=0):
     return net, X, md
 
 
+def _reusable_se_model(ms, cols):
+    """``shifu.varsel.se.reuse=true`` (VarSelectModelProcessor.distributedSEWrapper :633-642): skip
+    training and analyse the current ``models/model0.nn`` when it was trained on these candidates
+    (same input width); otherwise None (train the sensitivity model)."""
+    from ..config import environment
+    if not environment.get_bool("shifu.varsel.se.reuse", False):
+        return None
+    from ..formats.nn_format import read_encog
+    path = ms.pf.model_path(0, "nn")
+    if not os.path.exists(path):
+        _log.warning("shifu.varsel.se.reuse: %s not found, training the SE model", path)
+        return None
+    net = read_encog(path)
+    if net.n_in != len(cols) or net.n_out != 1:
+        _log.warning("shifu.varsel.se.reuse: %s has %d inputs for %d candidates, training the SE model",
+                     path, net.n_in, len(cols))
+        return None
+    _log.info("shifu.varsel.se.reuse: sensitivity of the existing %s", path)
+    return net
+
+
 def select_by_sensitivity(ms, by="SE", device=None, seed=0):
     mc = ms.mc
     cols = _good(ms)
     if not cols:
         return []
     epochs = max(1, int(mc.train.get("numTrainEpochs", 100)) // 2)
-    net, X, md = _train_quick_nn(ms, cols, epochs, device, seed)
+    net = _reusable_se_model(ms, cols)
+    if net is not None:
+        md = shard_model_data(ms.load_raw(cols))
+        X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+    else:
+        net, X, md = _train_quick_nn(ms, cols, epochs, device, seed)
     mean, rms, var = V.sensitivity(net, X, device=device)
     filter_num = int(mc.varSelect.get("filterNum", 200) or 0)
     keep = filter_num if filter_num > 0 else int(len(cols) * (1 - float(mc.varSelect.get("filterOutRatio", 0.05))))

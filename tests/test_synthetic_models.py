@@ -295,3 +295,31 @@ def test_nn_continuous_structure_growth(tmp_path):
     np.testing.assert_allclose(W0n[:4, :n_in], W0o[:, :n_in], rtol=1e-6, atol=1e-7)   # frozen block
     np.testing.assert_allclose(W0n[:4, n_in], W0o[:, n_in], rtol=1e-6, atol=1e-7)     # frozen bias
     assert not np.allclose(new.weights[1][:1, :4], old.weights[1][:, :4])            # layer 2 trains
+
+
+def test_varsel_se_reuse_current_model(tmp_path, monkeypatch):
+    """shifu.varsel.se.reuse=true: SE ranks the candidates with the existing models/model0.nn
+    instead of training a sensitivity model (the trainer must not be called)."""
+    from shifu_amd.config import environment
+    from shifu_amd.steps import varsel as VS
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "se", "NN", n_rows=800)
+    mc = _mc(root)
+    mc.train["numTrainEpochs"] = 5
+    mc.train["baggingNum"] = 1
+    mc.varSelect["filterBy"] = "SE"
+    mc.varSelect["filterNum"] = 3
+    mc.save()
+    _run(root, ["init", "stats", "norm", "train"])
+
+    def boom(*a, **k):
+        raise AssertionError("sensitivity model retrained despite shifu.varsel.se.reuse")
+    monkeypatch.setattr(VS, "_train_quick_nn", boom)
+    environment.set_property("shifu.varsel.se.reuse", "true")
+    try:
+        _run(root, ["varsel"])
+    finally:
+        environment.set_property("shifu.varsel.se.reuse", "false")
+    from shifu_amd.config.column_config import load_column_configs
+    sel = [c for c in load_column_configs(os.path.join(root, "ColumnConfig.json")) if c.final_select]
+    assert len(sel) >= 3
