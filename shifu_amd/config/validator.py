@@ -1,6 +1,7 @@
-"""Per-step config validation (C3) - subset of ``ModelInspector.probe``
-(J/core/validator/ModelInspector.java:93, checkTrainSetting :451-938) plus
-``BasicModelProcessor.checkAlgorithmParam`` defaults (J/core/processor/BasicModelProcessor.java:404-494)."""
+"""Per-step config validation (C3): ``ModelInspector.probe`` (J/core/validator/ModelInspector.java:93-200):
+the meta-driven item checks of ``MetaFactory`` first (``config/meta.py``), then the step checks,
+``checkTrainSetting`` (:451-938) included, plus ``BasicModelProcessor.checkAlgorithmParam``
+defaults (J/core/processor/BasicModelProcessor.java:404-494)."""
 from __future__ import annotations
 
 import os
@@ -30,6 +31,11 @@ STEPS = ("INIT", "STATS", "VARSELECT", "NORMALIZE", "TRAIN", "POSTTRAIN", "EVAL"
 def probe(mc, step: str) -> ValidateResult:
     r = ValidateResult()
     step = step.upper()
+    from .meta import validate_config
+    for cause in validate_config(mc):         # checkMeta: a meta violation ends the probe
+        r.fail(cause)
+    if not r:
+        return r
     basic = mc.basic
     if not basic.get("name"):
         r.fail("basic.name must not be empty")
@@ -88,7 +94,25 @@ def check_train(mc, r: ValidateResult):
         r.fail("train.baggingSampleRate must be in (0, 1]")
     if int(t.get("numTrainEpochs", 100)) <= 0:
         r.fail("train.numTrainEpochs must be > 0")
+    if t.get("epochsPerIteration") is not None and int(t.get("epochsPerIteration")) <= 0:
+        r.fail("'epochsPerIteration' should be larger than 0 if set.")
+    if t.get("convergenceThreshold") is not None and float(t.get("convergenceThreshold")) < 0:
+        r.fail("'convergenceThreshold' should be larger than or equal to 0 if set.")
+    wtc = t.get("workerThreadCount")
+    if wtc is not None and (int(wtc) <= 0 or int(wtc) > 32):
+        r.fail("'workerThreadCount' should be in (0, 32] if set.")
+    if mc.is_multiclass():
+        method = str(t.get("multiClassifyMethod", "NATIVE")).upper()
+        if method in ("ONEVSALL", "ONEVSREST") and alg not in ("GBT", "RF", "NN"):
+            r.fail("OneVSAll multiple classification is only effective in gradient boosted trees (GBT) or "
+                   "random forest (RF) or Neural Network (NN) training method.")
+        if method == "NATIVE" and alg not in ("NN", "RF"):
+            r.fail("Native multiple classification is only effective in neural network (nn) or random forest "
+                   "(rf) training method.")
     p = mc.params or {}
+    from .meta import has_grid
+    if not has_grid(mc):
+        _check_params(alg, p, r)
     if alg == "NN":
         nl = p.get("NumHiddenLayers", 1)
         nodes = p.get("NumHiddenNodes", [])
@@ -127,3 +151,67 @@ def check_train(mc, r: ValidateResult):
     if kf > 20:
         r.fail("numKFold must be <= 20")
     return r
+
+
+def _f(v):
+    try:
+        return None if v is None else float(v)
+    except (TypeError, ValueError):
+        return None
+
+
+def _check_params(alg: str, p: dict, r: ValidateResult) -> None:
+    """Value ranges of ``checkTrainSetting`` (ModelInspector.java:527-938) for concrete params."""
+    lr = _f(p.get("LearningRate"))
+    if lr is not None and lr <= 0:
+        r.fail("Learning rate should be larger than 0.")
+    if alg == "NN":
+        ld = _f(p.get("LearningDecay"))
+        if ld is not None and (ld < 0 or ld >= 1):
+            r.fail("Learning decay should be in [0, 1) if set.")
+        mb = _f(p.get("MiniBatchs"))
+        if mb is not None and (mb <= 0 or mb > 1000):
+            r.fail("MiniBatchs should be in (0, 1000] if set.")
+        mom = _f(p.get("Momentum"))
+        if mom is not None and mom <= 0:
+            r.fail("Momentum should be larger than 0 if set.")
+        for k in ("AdamBeta1", "AdamBeta2"):
+            b = _f(p.get(k))
+            if b is not None and (b <= 0 or b >= 1):
+                r.fail(f"{k} should be in (0, 1) if set.")
+    if alg in ("NN", "GBT", "RF"):
+        dr = _f(p.get("DropoutRate"))
+        if dr is not None and (dr < 0 or dr >= 1):
+            r.fail("Dropout rate should be in [0, 1) if set.")
+    if alg in ("GBT", "RF"):
+        fss = p.get("FeatureSubsetStrategy")
+        if fss is None:
+            r.fail("'FeatureSubsetStrategy' should not be null for GBT/RF.")
+        else:
+            v = _f(fss)
+            if v is not None:
+                if v <= 0 or v > 1:
+                    r.fail("'FeatureSubsetStrategy' as a number should be in (0, 1].")
+            elif str(fss).upper() not in ("ALL", "HALF", "ONETHIRD", "TWOTHIRDS", "SQRT", "LOG2", "AUTO"):
+                r.fail(f"'FeatureSubsetStrategy' {fss} is not one of ALL, HALF, ONETHIRD, TWOTHIRDS, SQRT, "
+                       "LOG2, AUTO or a number in (0, 1].")
+        md, ml = p.get("MaxDepth"), p.get("MaxLeaves")
+        if md is None and ml is None:
+            r.fail("'MaxDepth' or 'MaxLeaves' should be set for GBT/RF.")
+        if ml is not None and int(ml) <= 0:
+            r.fail("'MaxLeaves' should be larger than 0 if set.")
+        vt = _f(p.get("ValidationTolerance"))
+        if vt is not None and (vt < 0 or vt >= 1):
+            r.fail("'ValidationTolerance' should be in [0, 1) if set.")
+        msm = p.get("MaxStatsMemoryMB")
+        if msm is not None and int(msm) <= 0:
+            r.fail("'MaxStatsMemoryMB' should be larger than 0 if set.")
+        mipn = p.get("MinInstancesPerNode")
+        if mipn is not None and int(mipn) <= 0:
+            r.fail("'MinInstancesPerNode' should be larger than 0 if set.")
+        tn = p.get("TreeNum")
+        if tn is not None and (int(tn) <= 0 or int(tn) > 10000):
+            r.fail("'TreeNum' should be in (0, 10000] if set.")
+        mig = _f(p.get("MinInfoGain"))
+        if mig is not None and mig < 0:
+            r.fail("'MinInfoGain' should be larger than or equal to 0 if set.")

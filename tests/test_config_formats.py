@@ -145,3 +145,41 @@ def test_legacy_pre_versioned_gbt_fixture(ref_resources):
     # row 2: right, left -> leaf 6 (0.714...)
     s = m.score(x, 3)
     np.testing.assert_allclose(s, [0.0, 0.1, 0.1 * 0.7142857142857143], rtol=1e-12)
+
+
+def test_meta_validation_rules(ref_resources):
+    """MetaFactory semantics: every reference fixture ModelConfig passes; typos in train.params,
+    out-of-option values, non-boolean flags, non-integer counts fail with the reference's
+    messages; a grid search exempts train#params#*; ModelInspector train ranges."""
+    import glob
+    import copy
+    from shifu_amd.config.meta import validate_config
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.config.validator import ValidateResult, check_train
+    files = glob.glob(os.path.join(ref_resources, "**", "ModelConfig.json"), recursive=True)
+    assert len(files) >= 5
+    for f in files:
+        assert validate_config(ModelConfig.load(f)) == [], f
+    mc = ModelConfig.load(os.path.join(ref_resources, "example/cancer-judgement/ModelStore/ModelSet1/ModelConfig.json"))
+    bad = copy.deepcopy(mc)
+    bad.train["params"]["Propagationn"] = "R"
+    assert validate_config(bad) == ["train#params#Propagationn - not found meta info."]
+    bad = copy.deepcopy(mc)
+    bad.normalize["normType"] = "ZZSCALE"
+    assert validate_config(bad)[0].startswith("normalize#normType - the value couldn't be found in the option")
+    bad = copy.deepcopy(mc)
+    bad.train["isContinuous"] = "yes"
+    assert validate_config(bad) == ["train#isContinuous - the value is illegal.  Only true/false are perimited."]
+    bad = copy.deepcopy(mc)
+    bad.train["baggingNum"] = "two"
+    assert validate_config(bad) == ["train#baggingNum - the value is not integer format."]
+    grid = copy.deepcopy(mc)
+    grid.train["params"]["LearningRate"] = [0.1, 0.2]
+    grid.train["params"]["Whatever"] = 1
+    assert validate_config(grid) == []
+    r = ValidateResult()
+    bad = copy.deepcopy(mc)
+    bad.train["params"]["LearningRate"] = 0
+    bad.train["params"]["DropoutRate"] = 1.0
+    check_train(bad, r)
+    assert not r and any("Learning rate" in c for c in r.causes) and any("Dropout" in c for c in r.causes)
