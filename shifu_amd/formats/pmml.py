@@ -109,11 +109,17 @@ def _output(model, name="FinalResult"):
     ET.SubElement(out, "OutputField", name=name, feature="predictedValue")
 
 
-def nn_pmml(net, cols, target, norm_type="ZSCALE", cutoff=STD_DEV_CUTOFF, model_name="model0"):
-    """One NN (input-first ``NNNetwork``) -> PMML NeuralNetwork."""
-    pmml = _root()
-    _data_dictionary(pmml, cols, target)
-    nn = ET.SubElement(pmml, "NeuralNetwork", modelName=model_name, functionName="regression",
+# activations PMML 4.2 can express exactly; the others (log, swish, leaky ReLU, ptanh) have no
+# PMML activationFunction, so such networks are refused instead of exported with wrong scores
+PMML_EXACT_ACTS = {"sigmoid", "tanh", "linear", "relu", "sin"}
+
+
+def _nn_element(parent, net, cols, target, norm_type, cutoff, model_name):
+    """NeuralNetwork element (MiningSchema, Output, LocalTransformations, layers) under ``parent``."""
+    bad = [a for a in net.acts if str(a).lower() not in PMML_EXACT_ACTS]
+    if bad:
+        raise ValueError(f"activation(s) {sorted(set(bad))} have no exact PMML 4.2 activationFunction")
+    nn = ET.SubElement(parent, "NeuralNetwork", modelName=model_name, functionName="regression",
                        activationFunction="logistic", numberOfLayers=str(len(net.weights)))
     _mining_schema(nn, cols, target)
     _output(nn)
@@ -145,6 +151,32 @@ def nn_pmml(net, cols, target, norm_type="ZSCALE", cutoff=STD_DEV_CUTOFF, model_
         o = ET.SubElement(no, "NeuralOutput", outputNeuron=nid)
         df = ET.SubElement(o, "DerivedField", optype="continuous", dataType="double")
         ET.SubElement(df, "FieldRef", field=target)
+    return nn
+
+
+def nn_pmml(net, cols, target, norm_type="ZSCALE", cutoff=STD_DEV_CUTOFF, model_name="model0"):
+    """One NN (input-first ``NNNetwork``) -> PMML NeuralNetwork."""
+    pmml = _root()
+    _data_dictionary(pmml, cols, target)
+    _nn_element(pmml, net, cols, target, norm_type, cutoff, model_name)
+    return pmml
+
+
+def nn_bagging_pmml(nets, cols, target, norm_type="ZSCALE", cutoff=STD_DEV_CUTOFF, model_name="model"):
+    """All bagging NNs as ONE PMML (``export -t baggingpmml``, PMMLTranslator.build with
+    isOutBaggingToOne, J/core/pmml/PMMLTranslator.java:122-159): a regression MiningModel whose
+    Segmentation averages one NeuralNetwork segment per bag (ids ``Segement<i>`` as the reference
+    names them), each with its own MiningSchema and LocalTransformations."""
+    pmml = _root()
+    _data_dictionary(pmml, cols, target)
+    mm = ET.SubElement(pmml, "MiningModel", modelName=model_name, functionName="regression")
+    _mining_schema(mm, cols, target)
+    _output(mm)
+    seg = ET.SubElement(mm, "Segmentation", multipleModelMethod="average")
+    for i, net in enumerate(nets):
+        s = ET.SubElement(seg, "Segment", id=f"Segement{i}")
+        ET.SubElement(s, "True")
+        _nn_element(s, net, cols, target, norm_type, cutoff, f"{model_name}{i}")
     return pmml
 
 
@@ -162,31 +194,53 @@ def lr_pmml(weights, cols, target, norm_type="ZSCALE", cutoff=STD_DEV_CUTOFF, mo
     return pmml
 
 
-def _tree_nodes(parent, nd, model, cols_by_num, pred_text):
-    el = ET.SubElement(parent, "Node", id=str(nd.id), score=repr(float(nd.predict or 0.0)))
-    ET.SubElement(el, pred_text[0]) if pred_text[0] == "True" else None
-    if pred_text[0] != "True":
-        el.append(pred_text[1])
-    if nd.is_leaf():
-        return
-    s = nd.split
+def _left_predicate(s, model):
+    """Predicate of the left child of a split, matching ``TreeModelFile.predict_node``: numeric
+    ``x < threshold`` (missing -> the column mean via the MiningField replacement); categorical
+    ``x in L`` where L = the stored set (isLeft) or its complement, OR ``isMissing`` when the
+    missing/unseen bin (index = #categories) is in L (unseen values are declared invalid ->
+    asMissing in the MiningSchema)."""
     name = model.names[s.column]
     if s.ftype == 1:
-        lp = ET.Element("SimplePredicate", field=name, operator="lessThan", value=repr(float(s.threshold)))
-        rp = ET.Element("SimplePredicate", field=name, operator="greaterOrEqual", value=repr(float(s.threshold)))
-    else:
-        cats = model.categories.get(s.column, [])
-        stored = sorted(s.categories or [])
-        vals = [cats[i] for i in stored if i < len(cats)]
-        inset = ET.Element("SimpleSetPredicate", field=name, booleanOperator="isIn")
-        arr = ET.SubElement(inset, "Array", n=str(len(vals)), type="string")
-        arr.text = " ".join(f'"{v}"' for v in vals)
-        notin = ET.Element("SimpleSetPredicate", field=name, booleanOperator="isNotIn")
-        arr2 = ET.SubElement(notin, "Array", n=str(len(vals)), type="string")
-        arr2.text = arr.text
-        lp, rp = (inset, notin) if s.is_left else (notin, inset)
-    _tree_nodes(el, nd.left, model, cols_by_num, ("P", lp))
-    _tree_nodes(el, nd.right, model, cols_by_num, ("P", rp))
+        return ET.Element("SimplePredicate", field=name, operator="lessThan", value=repr(float(s.threshold)))
+    cats = model.categories.get(s.column, [])
+    ncat = len(cats)
+    stored = set(s.categories or set())
+    left = stored if s.is_left else set(range(ncat + 1)) - stored
+    vals = [v for i in sorted(left) if i < ncat for v in str(cats[i]).split("^")]
+    inset = ET.Element("SimpleSetPredicate", field=name, booleanOperator="isIn")
+    arr = ET.SubElement(inset, "Array", n=str(len(vals)), type="string")
+    arr.text = " ".join('"' + v.replace('"', '\\"') + '"' for v in vals)
+    if ncat not in left:
+        return inset
+    comp = ET.Element("CompoundPredicate", booleanOperator="or")
+    comp.append(inset)
+    ET.SubElement(comp, "SimplePredicate", field=name, operator="isMissing")
+    return comp
+
+
+def _tree_nodes(parent, nd, model, pred):
+    el = ET.SubElement(parent, "Node", id=str(nd.id), score=repr(float(nd.predict or 0.0)))
+    el.append(pred if pred is not None else ET.Element("True"))
+    if nd.is_leaf():
+        return
+    _tree_nodes(el, nd.left, model, _left_predicate(nd.split, model))
+    _tree_nodes(el, nd.right, model, ET.Element("True"))      # first true child wins
+
+
+def _tree_mining_schema(model_el, cols, target, model):
+    """Missing numeric -> the stored column mean (IndependentTreeModel's numerical mean
+    replacement); values outside a categorical DataField's Value list are treated as missing."""
+    ms = ET.SubElement(model_el, "MiningSchema")
+    for c in cols:
+        f = ET.SubElement(ms, "MiningField", name=c.name, usageType="active",
+                          optype="categorical" if c.is_categorical() else "continuous")
+        if c.is_categorical():
+            f.set("invalidValueTreatment", "asMissing")
+        else:
+            f.set("missingValueReplacement", repr(float(model.numerical_means.get(c.num, c.mean or 0.0) or 0.0)))
+            f.set("invalidValueTreatment", "asMissing")
+    ET.SubElement(ms, "MiningField", name=target, usageType="target")
 
 
 def tree_pmml(model, cols, target, model_name="model0"):
@@ -199,15 +253,14 @@ def tree_pmml(model, cols, target, model_name="model0"):
     _output(mm)
     is_gbt = model.algorithm.upper() == "GBT"
     seg = ET.SubElement(mm, "Segmentation", multipleModelMethod="weightedSum" if is_gbt else "weightedAverage")
-    cols_by_num = {c.num: c for c in cols}
     k = 0
     for bag in model.bags:
         for t in bag:
             s = ET.SubElement(seg, "Segment", id=str(k), weight=repr(float(t.learning_rate)))
             ET.SubElement(s, "True")
             tm = ET.SubElement(s, "TreeModel", functionName="regression", splitCharacteristic="binarySplit")
-            _mining_schema(tm, cols, target)
-            _tree_nodes(tm, t.root, model, cols_by_num, ("True", None))
+            _tree_mining_schema(tm, cols, target, model)
+            _tree_nodes(tm, t.root, model, None)
             k += 1
     return pmml
 

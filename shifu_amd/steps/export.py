@@ -52,6 +52,30 @@ def export_pmml(ms, concise=False):
     return paths
 
 
+def export_bagging_pmml(ms):
+    """``export -t baggingpmml`` (ExportModelProcessor :173-187): every NN bag in ONE PMML
+    (``pmmls/<modelSetName>.pmml``, an averaging MiningModel); NN only, as in the reference."""
+    if str(ms.mc.algorithm).upper() != "NN":
+        _log.warning("Currently one bagging pmml model is only supported in NN algorithm.")
+        return None
+    from ..config.column_config import model_input_columns
+    cols = model_input_columns(ms.ccs, ms.mc.is_binary())
+    nets = []
+    for p in list_model_files(ms.pf.models_dir, "NN"):
+        if p.endswith(".nn"):
+            nets.append(nn_format.read_encog(p) if not nn_format.is_binary_nn(p)
+                        else nn_format.read_binary_nn(p)["networks"][0])
+    if not nets:
+        raise FileNotFoundError("no NN models to export")
+    cutoff = float(ms.mc.normalize.get("stdDevCutOff", 6.0))
+    doc = pmml.nn_bagging_pmml(nets, cols, _target(ms), ms.mc.norm_type, cutoff, ms.mc.name)
+    out = ms.pf.p("pmmls", f"{ms.mc.name}.pmml")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    pmml.write_pmml(doc, out)
+    _log.info("one bagging PMML (%d networks) -> %s", len(nets), out)
+    return out
+
+
 def export_bagging(ms):
     """Merge all NN bags into one binary ``.nn`` (BinaryNNSerializer with N networks)."""
     from ..config.column_config import model_input_columns
@@ -228,8 +252,10 @@ def run_export(root: str = ".", etype: str = "pmml", concise: bool = False, requ
     t = (etype or "pmml").lower()
     if t not in TYPES:
         raise ValueError(f"unsupported export type {etype}; one of {TYPES}")
-    if t in ("pmml", "baggingpmml"):
+    if t == "pmml":
         export_pmml(ms, concise)
+    elif t == "baggingpmml":
+        export_bagging_pmml(ms)
     elif t == "bagging":
         _log.info("merged bagging model -> %s", export_bagging(ms))
     elif t == "columnstats":
