@@ -185,3 +185,57 @@ def test_trainer_transposed_layer1_deltas_match(monkeypatch):
     torch.cuda.synchronize()
     for va, vb in zip(a.params.views(a.grad), b.params.views(b.grad)):
         assert float((va - vb).norm() / vb.norm().clamp(min=1e-12)) < 1e-2
+
+
+def test_bench_configuration_tracks_fp32_oracle():
+    """The exact bench trainer configuration (bench.py: n_in 1000, hidden 500/200 sigmoid, RPROP,
+    chunks >= 2^17 rows) so the 8-phase forward, the fused head, the ring wgrad (incl. the M % 32
+    tail) and dgrad all run, for 8 full-batch epochs against the fp32 torch oracle on the same
+    bf16-rounded rows and weights: the training-error trajectory agrees within 1e-2 relative and
+    the final weights stay close."""
+    spec = MLPSpec(n_in=1000, hidden=[500, 200], acts=["sigmoid", "sigmoid"], n_out=1)
+    n = (1 << 17) + 77
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, spec.n_in, generator=g).bfloat16().float()
+    wt = torch.randn(spec.n_in, 1, generator=g)
+    y = ((x @ wt) > 0).float()
+    cpu = MLPTrainer(spec, device="cpu", seed=7, chunk_rows=1 << 17)
+    gpu = MLPTrainer(spec, device="cuda", seed=7, chunk_rows=1 << 17)
+    assert gpu.fused_head and gpu.wgrad_ring
+    cpu.params.flat.copy_(cpu.params.flat.bfloat16().float())
+    gpu.params.flat.copy_(cpu.params.flat.cuda())
+    dc, dg = cpu.prepare(x, y), gpu.prepare(x, y)
+    # first full-batch gradient, layer by layer (RPROP only uses gradient signs afterwards, so
+    # weights of near-zero gradients legitimately drift apart between bf16 and fp32 runs)
+    cpu.grad.zero_(); cpu.err_acc.zero_(); cpu.accumulate_gradients(dc)
+    gpu.grad.zero_(); gpu.err_acc.zero_(); gpu.accumulate_gradients(dg)
+    torch.cuda.synchronize()
+    for vc, vg in zip(cpu.params.views(cpu.grad), gpu.params.views(gpu.grad.cpu())):
+        r = (vc - vg).norm() / vc.norm().clamp(min=1e-12)
+        assert r < 3e-2, float(r)
+    ec, eg = [], []
+    for _ in range(8):
+        ec.append(cpu.step(dc))
+        eg.append(gpu.step(dg))
+    torch.cuda.synchronize()
+    for a, b in zip(ec, eg):
+        assert abs(a - b) / a < 1e-2, (ec, eg)
+
+
+def test_ring_wgrad_bitwise_reproducible():
+    """The ring wgrad reduces split partials in a fixed order: two runs are bit-identical."""
+    from shifu_amd.ops import _native as nat
+    M, Nv, Kx = 300_000 + 13, 500, 1024
+    D = torch.randn(M, 512, device="cuda").bfloat16()
+    D[:, Nv:] = 0
+    X = torch.randn(M, Kx, device="cuda").bfloat16()
+    ws = torch.empty(nat.hip().shifu_wgrad_ring_ws(M, Nv, Kx) // 4, device="cuda")
+    outs = []
+    for _ in range(2):
+        G = torch.zeros(Nv, Kx, device="cuda")
+        nat.call_hip("shifu_wgrad_ring", D, 512, X, Kx, G, Kx, M, Nv, Kx, ws, ws.numel() * 4, nat.stream_of(X))
+        outs.append(G)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = D[:, :Nv].float().t() @ X.float()
+    assert ((outs[0] - ref).abs().max() / ref.abs().max()).item() < 1e-4
