@@ -20,6 +20,7 @@ rows are freed the same process times ``--gbdt-steps`` boosting rounds on 100M x
 per GPU (``gbdt_rounds_per_s`` / ``gbdt_ms_per_round``; ``--gbdt-steps 0`` skips it).
     python bench.py --model varsel  # 10k-feature MLP + SE varselect config
     python bench.py --model lr      # LR 100k-row CSV local (CPU plumbing) config
+    python bench.py --model stats   # stats (K4 exact cuts + histograms) 100M x 1000 per GPU
 """
 from __future__ import annotations
 
@@ -187,6 +188,101 @@ def bench_varsel(a, dev, info):
     }
 
 
+def _stats_batch(C, n, k0, dev, seed):
+    """Synthetic column batch [C, n] fp64 on the device: a mix of N(0,1) with ~2% missing,
+    log-normal heavy tails, low-cardinality integers and 2-decimal values (many ties)."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    v = torch.empty(C, n, dtype=torch.float64, device=dev)
+    v.normal_(generator=g)
+    for k in range(C):
+        t = (k0 + k) % 4
+        col = v[k]
+        if t == 0:
+            col.masked_fill_(col > 2.0, float("nan"))
+        elif t == 1:
+            col.mul_(2.0).exp_()
+        elif t == 2:
+            col.mul_(3.0).floor_()
+        else:
+            col.mul_(100.0).round_().div_(100.0)
+    return v
+
+
+def bench_stats(a, dev, info):
+    """``shifu stats`` over 100M rows x 1000 numeric columns per GPU (the reference's headline stats
+    job is 100M x 1600 in 30 min on a Hadoop cluster, CHANGES.txt:233-234).  One step = the full
+    per-column pass for every column: K4 exact equal-population cuts (qprep/qhist/qgather, 10 bins,
+    EqualPositive over a binary target), K1+K2 bin histograms + moments with those cuts, distinct
+    counts, and - for N > 1 - the all-reduces that merge the per-rank partials.  Columns are
+    processed in HBM-resident batches of 64 (51 GB of fp64 at 100M rows); each batch is generated
+    on the device before its timed section (generation time is reported, not counted).
+    value = rows x (all columns) per second over all ranks, i.e. full-table stats passes x rows."""
+    from shifu_amd.algos import quantile as Q
+    from shifu_amd.algos.stats import batch_histograms
+    from shifu_amd.parallel import dist
+    n, F, C = a.rows, a.cols, 64
+    g = torch.Generator(device=dev).manual_seed(99 + info.rank)
+    y = (torch.rand(n, generator=g, device=dev) < 0.3).float()
+    w = torch.ones(n, dtype=torch.float64, device=dev)
+    multi = info.world_size > 1
+    red = (lambda t, op: dist.all_reduce_(t, op)) if multi else None
+    cat = dist.all_gather_cat if multi else None
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    def one_pass(step):
+        t_stats = t_gen = 0.0
+        nb_total = 0
+        for b0 in range(0, F, C):
+            c = min(C, F - b0)
+            t0 = time.perf_counter()
+            v = _stats_batch(c, n, b0, dev, 1000 * step + b0 + 7 * info.rank)
+            sync()
+            dist.barrier()
+            t1 = time.perf_counter()
+            bounds, distinct = Q.column_cuts(v, y, w, 10, "EqualPositive", True, reduce=red, allgather=cat)
+            res = batch_histograms(v, y, w, bounds, True)
+            if multi:
+                h = np.concatenate([np.concatenate([r[0], r[1], r[2], r[3]]) for r in res])
+                dist.all_reduce_np(h)
+            sync()
+            dist.barrier()
+            t_stats += time.perf_counter() - t1
+            t_gen += t1 - t0
+            nb_total += sum(len(b) + 1 for b in bounds)
+            del v
+        return t_stats, t_gen, nb_total
+
+    for i in range(a.warmup):
+        ts, tg, nb = one_pass(i)
+        log(f"[bench] stats warmup {i}: {ts:.2f}s stats, {tg:.2f}s generation, {nb} bins")
+    times, gens = [], []
+    for i in range(a.steps):
+        ts, tg, nb = one_pass(100 + i)
+        times.append(ts)
+        gens.append(tg)
+        log(f"[bench] stats step {i}: {ts:.3f}s stats, {tg:.2f}s generation")
+    t = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
+    dist.all_reduce_(t, "max")
+    dt = float(t.item())
+    total_rows = n * info.world_size
+    value = total_rows * a.steps / dt
+    return {
+        "metric": "rows/sec (whole node) shifu stats: exact 10-bin equal-population cuts + bin histograms + "
+                  "moments + distinct counts over every column [config: 100M rows x 1000 numeric cols per GPU]",
+        "value": value, "unit": "rows/s", "n_gpus": info.world_size, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp64", "data": "synthetic, generated on the device per 64-column batch (not timed)",
+        "config": {"model": "stats (EqualPositive, maxNumBin 10, binary target)", "global_batch": total_rows,
+                   "seq_len": None, "n_cols": F, "rows_per_gpu": n, "parallelism": f"dp{info.world_size}"},
+        "column_rows_per_s": value * F, "generation_s_per_step": sum(gens) / len(gens),
+        "reference_note": "reference: 100M x 1600 stats in 30 min on a Hadoop cluster (CHANGES.txt:233-234) "
+                          "= 5.6e4 rows/s",
+    }
+
+
 def bench_lr(a, dev, info):
     """BASELINE config 1: logistic regression on a 100k-row CSV, local mode, CPU only (the
     plumbing path): shifu init -> stats -> norm -> train on a generated model set.  One step =
@@ -230,7 +326,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr", "stats"])
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per GPU (default 125M on GPU: 256 GB of bf16 rows resident in one MI355X's "
                          "288 GB HBM, so 8 GPUs hold the metric's 1B-row x 1k-col table)")
@@ -250,7 +346,7 @@ def main():
     if a.model == "varsel" and a.cols == 1000:
         a.cols = 10_000
     if a.rows is None:
-        a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000,
+        a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000, "stats": 100_000_000 if gpu else 5_000,
                   "gbdt": 100_000_000 if gpu else 20_000}.get(a.model, 125_000_000 if gpu else 20_000)
     if a.model == "gbdt":
         res = bench_gbdt(a, dev, info)
@@ -259,6 +355,10 @@ def main():
         out = bench_varsel(a, dev, info)
     elif a.model == "lr":
         out = bench_lr(a, dev, info)
+    elif a.model == "stats":
+        if not gpu and a.cols == 1000:
+            a.cols = 64
+        out = bench_stats(a, dev, info)
     else:
         dt, errs, flops_row = bench_mlp(a, dev, info)
         dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)

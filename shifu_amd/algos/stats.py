@@ -156,6 +156,54 @@ def _finish_binning(cc, binary, nb, cpos, cneg, wpos, wneg, total):
         cb["binWeightedWoe"] = [0.0] * nb
 
 
+# columns up to this many rows get an exact distinct count (one batched device sort); larger
+# ones keep the K4 histogram count (exact for low-cardinality columns) or the HLL estimate -- the
+# reference itself reports HyperLogLogPlus estimates for every column
+EXACT_DISTINCT_ROWS = 1 << 22
+
+
+def upload_columns(cols, dev) -> torch.Tensor:
+    """Host numeric columns -> one column-major [C, n] float64 device tensor (no host stack)."""
+    n = len(cols[0]) if cols else 0
+    out = torch.empty((len(cols), n), dtype=torch.float64, device=dev)
+    for k, v in enumerate(cols):
+        out[k].copy_(torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64)), non_blocking=False)
+    return out
+
+
+def exact_distinct(vals: torch.Tensor, num_thr: float) -> list:
+    """Distinct finite values per row of ``vals`` [C, n] (threshold -> invalid, -0.0 == 0.0)."""
+    v = torch.where(vals > num_thr, torch.full_like(vals, float("nan")), vals) + 0.0
+    v = torch.where(torch.isfinite(v), v, torch.full_like(v, float("inf")))
+    s, _ = torch.sort(v, dim=1)
+    fin = torch.isfinite(s)
+    if s.shape[1] == 0:
+        return [0] * s.shape[0]
+    first = fin[:, :1].long().sum(1)
+    chg = ((s[:, 1:] != s[:, :-1]) & fin[:, 1:]).long().sum(1)
+    return (first + chg).cpu().tolist()
+
+
+def batch_histograms(vals: torch.Tensor, y: torch.Tensor, w: torch.Tensor, bounds, binary: bool,
+                     num_thr: float = 1.7976931348623157e308):
+    """K1+K2 for a column batch ``vals`` [C, n]: per column (cpos, cneg, wpos, wneg, moments).
+    GPU: the HIP ``column_stats`` kernel; CPU: the torch/numpy oracle with the same layout."""
+    if vals.device.type == "cuda":
+        from ..ops import stats_ops
+        return stats_ops.column_stats(vals, y, w, bounds, binary, num_thr)
+    yn = y.cpu().numpy() if torch.is_tensor(y) else np.asarray(y)
+    wn = w.cpu().numpy() if torch.is_tensor(w) else np.asarray(w)
+    out = []
+    for c in range(vals.shape[0]):
+        v = vals[c].cpu().numpy().astype(np.float64, copy=True)
+        v[v > num_thr] = np.nan
+        bidx = B.bin_index_numeric(v, bounds[c])
+        cpos, cneg, wpos, wneg = _hist(bidx, yn, wn, len(bounds[c]) + 1, binary, torch.device("cpu"))
+        mom = _moments(v, torch.device("cpu"))
+        out.append((cpos, cneg, wpos, wneg, mom))
+    return out
+
+
 def _numeric_bounds(vals, y, w, binary, method, n_bins):
     if binary and method in ("EqualPositive", "WeightEqualPositive"):
         sel = y > 0.5
@@ -171,6 +219,35 @@ def _numeric_bounds(vals, y, w, binary, method, n_bins):
     if len(bounds) <= 1 and sel.sum() < len(vals):
         bounds = B.equal_population_boundaries(vals, n_bins)
     return bounds
+
+
+def finish_categorical(cc, cats, cpos, cneg, wpos, wneg, total, binary, cate_max, dict_size):
+    """Categorical column from its per-category histograms (last bin = missing/unknown):
+    ``cateMaxNumBin`` merge, pos-rate moments (UpdateBinningInfoReducer.reduce :309-333), binning."""
+    nb = len(cats) + 1
+    if cate_max > 0 and len(cats) > cate_max:
+        cats, cpos, cneg, wpos, wneg = B.rebin_categorical(cats, list(cpos), list(cneg), list(wpos),
+                                                           list(wneg), cate_max)
+        cpos, cneg = np.array(cpos, np.int64), np.array(cneg, np.int64)
+        wpos, wneg = np.array(wpos), np.array(wneg)
+        nb = len(cats) + 1
+    cc.bin_category = cats
+    cc.bin_boundary = None
+    missing = int(cpos[-1] + cneg[-1])
+    if binary:
+        rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
+    else:
+        tot = cpos.sum()
+        rate = cpos / tot if tot else np.zeros_like(cpos, dtype=float)
+    cnt = cpos + cneg if binary else cpos
+    okr = np.isfinite(rate)
+    mx = float(rate[okr].max()) if okr.any() else 0.0
+    mn = float(rate[okr].min()) if okr.any() else 0.0
+    _finish_moments(cc, total - missing, float((rate * cnt).sum()), float((rate ** 2 * cnt).sum()),
+                    float((rate ** 3 * cnt).sum()), float((rate ** 4 * cnt).sum()), mn, mx, total, missing)
+    cc.stats["distinctCount"] = int(dict_size)
+    cc.stats["median"] = None
+    _finish_binning(cc, binary, nb, cpos, cneg, wpos, wneg, total)
 
 
 def _finish_numeric(cc, binary, bounds, cpos, cneg, wpos, wneg, mom, total, distinct):
@@ -221,52 +298,23 @@ def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int 
             dictionary = col.dictionary
         cats = B.categorical_bins(codes, dictionary, y, binary)
         bidx = B.category_index(codes, dictionary, cats)
-        nb = len(cats) + 1
-        cpos, cneg, wpos, wneg = _hist(bidx, y, w, nb, binary, dev)
-        if cate_max > 0 and len(cats) > cate_max:
-            cats, cpos, cneg, wpos, wneg = B.rebin_categorical(cats, list(cpos), list(cneg), list(wpos),
-                                                               list(wneg), cate_max)
-            cpos, cneg = np.array(cpos, np.int64), np.array(cneg, np.int64)
-            wpos, wneg = np.array(wpos), np.array(wneg)
-            nb = len(cats) + 1
-        cc.bin_category = cats
-        cc.bin_boundary = None
-        missing = int((bidx == len(cats)).sum()) if cate_max <= 0 else int(cpos[-1] + cneg[-1])
-        if binary:
-            rate = np.where(cpos + cneg > 0, cpos / np.maximum(cpos + cneg, 1), 0.0)
-        else:
-            tot = cpos.sum()
-            rate = cpos / tot if tot else np.zeros_like(cpos, dtype=float)
-        # categorical numeric stats are computed over bin pos-rates (reducer :309-333)
-        cnt = cpos + cneg if binary else cpos
-        okr = np.isfinite(rate)
-        mx = float(rate[okr].max()) if okr.any() else 0.0
-        mn = float(rate[okr].min()) if okr.any() else 0.0
-        s1 = float((rate * cnt).sum())
-        s2 = float((rate ** 2 * cnt).sum())
-        s3 = float((rate ** 3 * cnt).sum())
-        s4 = float((rate ** 4 * cnt).sum())
-        _finish_moments(cc, total - missing, s1, s2, s3, s4, mn, mx, total, missing)
-        cc.stats["distinctCount"] = int(len(dictionary))
-        cc.stats["median"] = None
-        _finish_binning(cc, binary, nb, cpos, cneg, wpos, wneg, total)
+        cpos, cneg, wpos, wneg = _hist(bidx, y, w, len(cats) + 1, binary, dev)
+        finish_categorical(cc, cats, cpos, cneg, wpos, wneg, total, binary, cate_max, len(dictionary))
     if not numeric:
         return ccs
     if dev.type == "cuda":
+        # K4 on the device: exact cuts from the qprep/qhist/qgather passes (algos/quantile.py),
+        # then K1+K2 (column_stats) with those cuts -- no host sort, no per-column loop
         from ..ops import stats_ops
+        from . import quantile as Q
         yt = torch.as_tensor(np.asarray(y, np.float32), device=dev)
         wt = torch.as_tensor(np.asarray(w, np.float64), device=dev)
         for b0 in range(0, len(numeric), gpu_batch):
             batch = numeric[b0: b0 + gpu_batch]
-            host = [md.table[c.name].numeric().astype(np.float64) for c in batch]
-            bounds, distinct = [], []
-            for v in host:
-                v = v.copy()
-                v[v > num_thr] = np.nan
-                bounds.append(_numeric_bounds(v, y, w, binary, method, n_bins))
-                fin = v[np.isfinite(v)]
-                distinct.append(int(torch.unique(torch.as_tensor(fin, device=dev)).numel()) if fin.size else 0)
-            vals = torch.as_tensor(np.stack(host), device=dev)
+            vals = upload_columns([md.table[c.name].numeric() for c in batch], dev)
+            bounds, distinct = Q.column_cuts(vals, yt, wt, n_bins, method, binary, num_thr)
+            if total <= EXACT_DISTINCT_ROWS:
+                distinct = exact_distinct(vals, num_thr)
             res = stats_ops.column_stats(vals, yt, wt, bounds, binary, num_thr)
             for c, bnd, (cpos, cneg, wpos, wneg, mom), dc in zip(batch, bounds, res, distinct):
                 _finish_numeric(c, binary, bnd, cpos, cneg, wpos, wneg, mom, total, dc)

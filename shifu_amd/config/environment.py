@@ -26,6 +26,9 @@ DEFAULTS = {
     "shifu.tree.checkpoint.interval": "100",
     "shifu.combo.max.retry": "3",
     "shifu.stats.corr.reuse": "false",
+    "shifu.stats.streaming": "auto",
+    "shifu.stats.streamThresholdGB": "8",
+    "shifu.stats.chunkMB": "256",
     "shifu.varsel.se.reuse": "false",
     "shifu.tree.regeninput": "false",
 }

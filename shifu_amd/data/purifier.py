@@ -133,9 +133,25 @@ def purify(mc, table: RawTable, target: str, weight_expr: str | None = None, fil
     return ModelData(t, yk, w[idx].astype(np.float64), ti[idx], c)
 
 
-def load_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=1.0, sample_neg_only=False,
-                 seed=0, require_target=True, extra_filter=None, max_rows=None) -> ModelData:
-    """Read + purify one data set section (``dataSet`` or an eval's ``dataSet``)."""
+@dataclass
+class DatasetPlan:
+    """What to parse from one data set section and how to purify it (shared by the whole-table
+    loader and the streamed chunk reader, data/stream.py)."""
+    data_path: str
+    delim: str
+    header: list
+    skip_header_line: bool
+    target: str | None
+    weight: str | None
+    filt: str | None
+    nums: list
+    strs: list
+    seg_names: list
+    seg_exprs: list
+    missing: list
+
+
+def plan_dataset(mc, data_conf, columns_num=None, columns_str=None, extra_filter=None) -> DatasetPlan:
     data_path = mc.resolve(data_conf.get("dataPath"))
     delim = data_conf.get("dataDelimiter") or "|"
     hpath = data_conf.get("headerPath")
@@ -181,10 +197,24 @@ def load_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=
     if weight and weight in header:
         nums.add(weight)
         strs.discard(weight)
-    table = read_table(data_path, header, delim, numeric=[h for h in header if h in nums],
-                       strings=[h for h in header if h in strs], missing=mc.missing_values,
-                       skip_header_line=skip, max_rows=max_rows)
-    if seg_names:
+    return DatasetPlan(data_path, delim, header, skip, target, weight, filt, [h for h in header if h in nums],
+                       [h for h in header if h in strs], seg_names, seg_exprs, list(mc.missing_values))
+
+
+def finish_table(mc, plan: DatasetPlan, table, sample_rate=1.0, sample_neg_only=False, seed=0,
+                 require_target=True) -> ModelData:
+    """Segment expansion + purification of a parsed table (whole data set or one chunk)."""
+    if plan.seg_names:
         from . import segments
-        segments.expand(table, seg_names, seg_exprs, set(header))
-    return purify(mc, table, target, weight, filt, sample_rate, sample_neg_only, seed, require_target)
+        segments.expand(table, plan.seg_names, plan.seg_exprs, set(plan.header))
+    return purify(mc, table, plan.target, plan.weight, plan.filt, sample_rate, sample_neg_only, seed,
+                  require_target)
+
+
+def load_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=1.0, sample_neg_only=False,
+                 seed=0, require_target=True, extra_filter=None, max_rows=None) -> ModelData:
+    """Read + purify one data set section (``dataSet`` or an eval's ``dataSet``)."""
+    plan = plan_dataset(mc, data_conf, columns_num, columns_str, extra_filter)
+    table = read_table(plan.data_path, plan.header, plan.delim, numeric=plan.nums, strings=plan.strs,
+                       missing=plan.missing, skip_header_line=plan.skip_header_line, max_rows=max_rows)
+    return finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target)

@@ -64,23 +64,32 @@ def _read_bytes(path: str) -> bytes:
         return f.read()
 
 
+def _first_line(path: str, limit: int = 1 << 24) -> str:
+    """First non-blank line of a (possibly gzipped) text file, reading only what it needs."""
+    opener = gzip.open if path.endswith(".gz") else open
+    with opener(path, "rb") as f:
+        for _ in range(1 << 20):
+            line = f.readline(limit)
+            if not line:
+                return ""
+            if line.strip():
+                return line.decode("utf-8", errors="replace").rstrip("\r\n")
+    return ""
+
+
 def read_header(header_path: str | None, header_delim: str = "|", data_path: str | None = None,
                 data_delim: str = "|") -> list:
     if header_path:
         files = list_data_files(header_path)
         if files:
-            raw = _read_bytes(files[0]).decode("utf-8", errors="replace")
-            line = next((l for l in raw.splitlines() if l.strip()), "")
-            return [h.strip() for h in line.split(header_delim or "|")]
+            return [h.strip() for h in _first_line(files[0]).split(header_delim or "|")]
     files = list_data_files(data_path)
     if not files:
         raise FileNotFoundError(f"no header file and no data under {data_path}")
     if files[0].endswith(".parquet"):           # schema carries the header
         import pyarrow.parquet as pq
         return list(pq.read_schema(files[0]).names)
-    raw = _read_bytes(files[0]).decode("utf-8", errors="replace")
-    line = next((l for l in raw.splitlines() if l.strip()), "")
-    return [h.strip() for h in line.split(data_delim or "|")]
+    return [h.strip() for h in _first_line(files[0]).split(data_delim or "|")]
 
 
 @dataclass
@@ -249,14 +258,8 @@ def _parse_parquet(path: str, header: list, kinds: list, missing: list):
     return n, 0, out
 
 
-def read_table(data_path: str, header: list, delim: str = "|", numeric: list | None = None,
-               strings: list | None = None, missing: list | None = None, skip_header_line: bool = False,
-               nthreads: int | None = None, max_rows: int | None = None) -> RawTable:
-    """Parse every file under ``data_path`` into a columnar table.  ``numeric``/``strings``
-    are column names (others skipped); by default every column is parsed as a string."""
-    files = list_data_files(data_path)
-    if not files:
-        raise FileNotFoundError(f"no data under {data_path}")
+def column_kinds(header: list, numeric: list | None = None, strings: list | None = None) -> list:
+    """Per header column: 1 numeric, 2 string, 0 skipped (by default every column is a string)."""
     idx = {h: i for i, h in enumerate(header)}
     kinds = [0] * len(header)
     for nm in numeric or []:
@@ -265,21 +268,20 @@ def read_table(data_path: str, header: list, delim: str = "|", numeric: list | N
     for nm in (strings if strings is not None else ([] if numeric else header)):
         if nm in idx:
             kinds[idx[nm]] = 2
-    missing = list(missing) if missing is not None else ["", "?"]
-    nthreads = nthreads or min(16, os.cpu_count() or 4)
-    parts = []
-    for fi, f in enumerate(files):
-        if f.endswith(".parquet"):
-            parts.append(_parse_parquet(f, header, kinds, missing))
-            continue
-        data = _read_bytes(f)
-        if skip_header_line and fi == 0:
-            nl = data.find(b"\n")
-            data = data[nl + 1:] if nl >= 0 else b""
-        res = _parse_native(data, delim or "|", kinds, missing, nthreads)
-        if res is None:
-            res = _parse_python(data, delim or "|", kinds, missing)
-        parts.append(res)
+    return kinds
+
+
+def parse_block(data: bytes, delim: str, kinds: list, missing: list, nthreads: int):
+    """One in-memory block of complete lines -> (n, bad, {column index: (kind, values, dict)})."""
+    res = _parse_native(data, delim or "|", kinds, missing, nthreads)
+    if res is None:
+        res = _parse_python(data, delim or "|", kinds, missing)
+    return res
+
+
+def table_from_parts(header: list, kinds: list, parts: list, data_path: str = "") -> RawTable:
+    """Concatenate parsed parts (file order) into a RawTable; string dictionaries are merged in
+    first-appearance order."""
     n = sum(p[0] for p in parts)
     bad = sum(p[1] for p in parts)
     cols = {}
@@ -298,14 +300,40 @@ def read_table(data_path: str, header: list, delim: str = "|", numeric: list | N
                 remapped.append(lut[np.where(codes >= 0, codes, len(d))])
             cols[name] = Column(name, "str", np.concatenate(remapped) if remapped else np.empty(0, np.int32),
                                 list(gdict.keys()))
-    if max_rows is not None and n > max_rows:
-        for c in cols.values():
-            c.values = c.values[:max_rows]
-        n = max_rows
     if bad:
         _log.warning("%d rows under %s have a column count != %d (padded as missing)", bad, data_path,
                      len(header))
     return RawTable(header, cols, n, bad)
+
+
+def read_table(data_path: str, header: list, delim: str = "|", numeric: list | None = None,
+               strings: list | None = None, missing: list | None = None, skip_header_line: bool = False,
+               nthreads: int | None = None, max_rows: int | None = None) -> RawTable:
+    """Parse every file under ``data_path`` into a columnar table.  ``numeric``/``strings``
+    are column names (others skipped); by default every column is parsed as a string.
+    (Out-of-core / per-rank byte ranges: ``data/stream.py``.)"""
+    files = list_data_files(data_path)
+    if not files:
+        raise FileNotFoundError(f"no data under {data_path}")
+    kinds = column_kinds(header, numeric, strings)
+    missing = list(missing) if missing is not None else ["", "?"]
+    nthreads = nthreads or min(16, os.cpu_count() or 4)
+    parts = []
+    for fi, f in enumerate(files):
+        if f.endswith(".parquet"):
+            parts.append(_parse_parquet(f, header, kinds, missing))
+            continue
+        data = _read_bytes(f)
+        if skip_header_line and fi == 0:
+            nl = data.find(b"\n")
+            data = data[nl + 1:] if nl >= 0 else b""
+        parts.append(parse_block(data, delim, kinds, missing, nthreads))
+    t = table_from_parts(header, kinds, parts, data_path)
+    if max_rows is not None and t.n > max_rows:
+        for c in t.columns.values():
+            c.values = c.values[:max_rows]
+        t.n = max_rows
+    return t
 
 
 def first_line_is_header(data_path: str, header: list, delim: str) -> bool:
@@ -313,6 +341,4 @@ def first_line_is_header(data_path: str, header: list, delim: str) -> bool:
     files = list_data_files(data_path)
     if not files or files[0].endswith(".parquet"):
         return False
-    raw = _read_bytes(files[0])[:65536].decode("utf-8", errors="replace")
-    line = next((l for l in raw.splitlines() if l.strip()), "")
-    return [h.strip() for h in line.split(delim)] == header
+    return [h.strip() for h in _first_line(files[0]).split(delim)] == header

@@ -60,11 +60,15 @@ HIP_SIGNATURES = {
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
     "shifu_gbdt_residual": "pppp" "p" "li" "s",
     # stats_kernels.hip
-    "shifu_column_stats": "plppli" "ppii" "dd" "pipi" "s",
+    "shifu_column_stats": "plppli" "ppii" "dd" "pipii" "s",
     "shifu_normalize": "plli" "pppp" "pl" "s",
     "shifu_bin_codes": "plli" "pp" "pl" "s",
     "shifu_lr_grad": "plli" "i" "ppp" "pp" "i" "s",
     "shifu_sensitivity": "plpl" "pp" "f" "p" "l" "iiiii" "p" "s",
+    # quantile_kernels.hip
+    "shifu_qprep": "pllipid" "ppp" "s",
+    "shifu_qhist": "pllippid" "pip" "pdi" "pppppp" "s",
+    "shifu_qgather": "pllippid" "pip" "pd" "ppp" "pp" "s",
 }
 
 # host runtime: name -> (argsig, restype)

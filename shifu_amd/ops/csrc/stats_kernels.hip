@@ -52,17 +52,54 @@ struct StatsArgs {
   int binary; double wscale; double num_thr;
   unsigned long long* hist; int hstride;     // [F][hstride][4]: cpos, cneg, wpos, wneg (fixed point)
   double* part; int nchunks; long rows_per_chunk;   // [F][nchunks][8]
+  int unit_w;                                // every weight is 1: weight sums = counts
+  int max_nb;                                // max boundaries over the batch (sizes the LDS carve)
+  int priv;                                  // per-thread private counters (unit_w, few bins)
 };
 
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (unsigned long long)__shfl_xor((long long)v, o, 64);
+  return v;
+}
+
+// Grid: x = column (fastest, so the blocks resident together read the same rows of y and w from
+// L2), y = row chunk.  With few bins (the usual maxNumBin 10-30) and unit weights, every thread
+// counts into its own LDS column ([key][thread], conflict-free, no atomics) and the block reduces
+// the columns at the end; otherwise LDS atomics (u32 counts, u64 fixed-point weights).
+constexpr int PRIV_KEYS = 48;                 // 2 * (bins + missing) <= 48 -> private counters
+
+// dynamic LDS carve (bytes), shared by host and device
+__host__ __device__ inline long cs_lds_bytes(int max_nb, int priv, int unit_w) {
+  const long m1 = max_nb + 1;
+  long b = (long)max_nb * 8 + 2 * m1 * 4;      // bounds, cp, cn
+  b = (b + 15) & ~15L;
+  if (priv) b += 2 * m1 * 256 * 4;            // [2 (nb+1)][256] u32
+  else if (!unit_w) b += 2 * m1 * 8;          // wp, wn
+  return b;
+}
+
 __global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
-  __shared__ double sb[MAXB];
-  __shared__ unsigned int cp[MAXB + 1], cn[MAXB + 1];
-  __shared__ unsigned long long wp[MAXB + 1], wn[MAXB + 1];
+  extern __shared__ __align__(16) unsigned char smem[];
   __shared__ double red[4][8];
-  const int f = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const long m1 = a.max_nb + 1;
+  double* sb = (double*)smem;
+  unsigned int* cp = (unsigned int*)(sb + a.max_nb);
+  unsigned int* cn = cp + m1;
+  unsigned char* tail = smem + ((((long)a.max_nb * 8 + 2 * m1 * 4) + 15) & ~15L);
+  unsigned int* priv = (unsigned int*)tail;                       // [2 m1][256]
+  unsigned long long* wp = (unsigned long long*)tail;             // [m1]
+  unsigned long long* wn = wp + m1;
+  const int f = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int b0 = a.boff[f], nb = a.boff[f + 1] - b0;
+  const bool private_cnt = a.priv;
   for (int i = tid; i < nb; i += 256) sb[i] = a.bounds[b0 + i];
-  for (int i = tid; i <= nb; i += 256) { cp[i] = 0; cn[i] = 0; wp[i] = 0ull; wn[i] = 0ull; }
+  for (int i = tid; i <= nb; i += 256) {
+    cp[i] = 0; cn[i] = 0;
+    if (!private_cnt && !a.unit_w) { wp[i] = 0ull; wn[i] = 0ull; }
+  }
+  if (private_cnt)
+    for (int k = 0; k < 2 * (nb + 1); ++k) priv[k * 256 + tid] = 0u;
   __syncthreads();
   const long r0 = (long)chunk * a.rows_per_chunk;
   const long r1 = min(a.n, r0 + a.rows_per_chunk);
@@ -77,15 +114,32 @@ __global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
     } else {
       bin = bin_search(sb, nb, v);
       if (isfinite(v)) {
-        double v2 = v * v;
+        const double v2 = v * v;
         cnt += 1.0; s1 += v; s2 += v2; s3 += v2 * v; s4 += v2 * v2;
         mn = fmin(mn, v); mx = fmax(mx, v);
       }
     }
     const bool pos = !a.binary || a.y[r] > 0.5f;
-    const unsigned long long q = (unsigned long long)__double2ll_rn(a.w[r] * a.wscale);
-    if (pos) { atomicAdd(&cp[bin], 1u); atomicAdd(&wp[bin], q); }
-    else     { atomicAdd(&cn[bin], 1u); atomicAdd(&wn[bin], q); }
+    if (private_cnt) {
+      priv[(bin * 2 + (pos ? 1 : 0)) * 256 + tid] += 1u;
+    } else if (a.unit_w) {
+      atomicAdd(pos ? &cp[bin] : &cn[bin], 1u);
+    } else {
+      const unsigned long long q = (unsigned long long)__double2ll_rn(a.w[r] * a.wscale);
+      if (pos) { atomicAdd(&cp[bin], 1u); atomicAdd(&wp[bin], q); }
+      else     { atomicAdd(&cn[bin], 1u); atomicAdd(&wn[bin], q); }
+    }
+  }
+  if (private_cnt) {                          // one wave per key: sum the 256 thread columns
+    __syncthreads();
+    const int wid = tid >> 6;
+    for (int k = wid; k < 2 * (nb + 1); k += 4) {
+      const unsigned int* pk = priv + k * 256;
+      unsigned int t = pk[lane] + pk[lane + 64] + pk[lane + 128] + pk[lane + 192];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0) { if (k & 1) cp[k >> 1] = t; else cn[k >> 1] = t; }
+    }
   }
   // moments: wave then block reduction
   cnt = wave_sum_d(cnt); s1 = wave_sum_d(s1); s2 = wave_sum_d(s2); s3 = wave_sum_d(s3); s4 = wave_sum_d(s4);
@@ -94,7 +148,8 @@ __global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
     mn = fmin(mn, __shfl_xor(mn, o, 64));
     mx = fmax(mx, __shfl_xor(mx, o, 64));
   }
-  const int wid = tid >> 6, lane = tid & 63;
+  const int wid = tid >> 6;
+  __syncthreads();
   if (lane == 0) {
     red[wid][0] = cnt; red[wid][1] = s1; red[wid][2] = s2; red[wid][3] = s3; red[wid][4] = s4;
     red[wid][5] = mn; red[wid][6] = mx;
@@ -110,11 +165,14 @@ __global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
     a.part[((long)f * a.nchunks + chunk) * 8 + tid] = acc;
   }
   unsigned long long* h = a.hist + (long)f * a.hstride * 4;
+  const unsigned long long unit_q = (unsigned long long)__double2ll_rn(a.wscale);
   for (int i = tid; i <= nb; i += 256) {
+    const unsigned long long wpi = a.unit_w ? (unsigned long long)cp[i] * unit_q : wp[i];
+    const unsigned long long wni = a.unit_w ? (unsigned long long)cn[i] * unit_q : wn[i];
     if (cp[i]) atomicAdd(&h[i * 4 + 0], (unsigned long long)cp[i]);
     if (cn[i]) atomicAdd(&h[i * 4 + 1], (unsigned long long)cn[i]);
-    if (wp[i]) atomicAdd(&h[i * 4 + 2], wp[i]);
-    if (wn[i]) atomicAdd(&h[i * 4 + 3], wn[i]);
+    if (wpi) atomicAdd(&h[i * 4 + 2], wpi);
+    if (wni) atomicAdd(&h[i * 4 + 3], wni);
   }
 }
 
@@ -430,12 +488,15 @@ __global__ void __launch_bounds__(256) sensitivity_kernel(SensArgs a) {
 // ---------------------------------------------------------------------------------------------
 SHIFU_API int shifu_column_stats(const double* vals, long ldv, const float* y, const double* w, long n, int F,
                                  const double* bounds, const int* boff, int max_nb, int binary, double wscale,
-                                 double num_thr, void* hist, int hstride, double* part, int nchunks,
+                                 double num_thr, void* hist, int hstride, double* part, int nchunks, int unit_w,
                                  hipStream_t stream) {
-  if (max_nb > MAXB || hstride < max_nb + 1 || nchunks <= 0 || F <= 0) return -1;
+  if (max_nb > MAXB || hstride < max_nb + 1 || nchunks <= 0 || nchunks > 65535 || F <= 0) return -1;
+  const int priv = unit_w && 2 * (max_nb + 1) <= PRIV_KEYS;
   StatsArgs a{vals, ldv, y, w, n, bounds, boff, binary, wscale, num_thr, (unsigned long long*)hist, hstride,
-              part, nchunks, (n + nchunks - 1) / nchunks};
-  hipLaunchKernelGGL(column_stats_kernel, dim3(nchunks, F), dim3(256), 0, stream, a);
+              part, nchunks, (n + nchunks - 1) / nchunks, unit_w, max_nb, priv};
+  const long lds = cs_lds_bytes(max_nb, priv, unit_w);
+  if (lds > 150 * 1024) return -1;
+  hipLaunchKernelGGL(column_stats_kernel, dim3(F, nchunks), dim3(256), (unsigned)lds, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -46,8 +46,9 @@ def column_stats(vals: torch.Tensor, y: torch.Tensor, w: torch.Tensor, bounds_li
     hist = torch.zeros(F * hstride * 4, dtype=torch.int64, device=dev)
     part = torch.zeros(F * nchunks * 8, dtype=torch.float64, device=dev)
     bt, ot = _dev_tensor(bflat, torch.float64, dev), _dev_tensor(boff, torch.int32, dev)
+    unit_w = bool(N) and bool(torch.all(w[:N] == 1.0).item())
     rc = nat.call_hip("shifu_column_stats", vals, vals.stride(0), y, w, N, F, bt, ot, max_nb, int(binary), wscale,
-                      float(num_thr), hist, hstride, part, nchunks, nat.stream_of(vals))
+                      float(num_thr), hist, hstride, part, nchunks, int(unit_w), nat.stream_of(vals))
     if rc:
         raise RuntimeError(f"shifu_column_stats failed rc={rc}")
     h = hist.view(F, hstride, 4).cpu().numpy()

@@ -46,18 +46,21 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
         run_correlation(ms, device)
         return 0
     if not psi:
-        md = ms.load_raw(cols, sample_rate=float(mc.stats.get("sampleRate", 1.0)),
-                         sample_neg_only=bool(mc.stats.get("sampleNegOnly", False)))
-        _log.info("stats: %d valid rows (%s)", md.n, md.counters.as_dict())
         from ..parallel import dist
-        if dist.info().world_size > 1:
-            # data parallel: this rank's rows, partials merged with collectives (algos/dist_stats.py)
-            from ..algos.dist_stats import compute_column_stats_dp
-            from .base import shard_model_data
-            compute_column_stats_dp(mc, ms.ccs, shard_model_data(md), device=device,
-                                    columns={c.name for c in cols})
+        if _use_streaming(ms):
+            _stats_streamed(ms, cols, device)
         else:
-            S.compute_column_stats(mc, ms.ccs, md, device=device, columns={c.name for c in cols})
+            md = ms.load_raw(cols, sample_rate=float(mc.stats.get("sampleRate", 1.0)),
+                             sample_neg_only=bool(mc.stats.get("sampleNegOnly", False)))
+            _log.info("stats: %d valid rows (%s)", md.n, md.counters.as_dict())
+            if dist.info().world_size > 1:
+                # data parallel over an in-memory table (shifu.stats.streaming=false)
+                from ..algos.dist_stats import compute_column_stats_dp
+                from .base import shard_model_data
+                compute_column_stats_dp(mc, ms.ccs, shard_model_data(md), device=device,
+                                        columns={c.name for c in cols})
+            else:
+                S.compute_column_stats(mc, ms.ccs, md, device=device, columns={c.name for c in cols})
         ms.save_cc(backup=True)
     if dist.info().world_size > 1:
         dist.barrier()
@@ -73,6 +76,58 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
         else:
             _log.warning("stats -p: stats.psiColumnName is empty")
     return 0
+
+
+def _use_streaming(ms: ModelSet) -> bool:
+    """``shifu.stats.streaming``: true / false / auto (default).  auto streams when the data set is
+    larger than ``shifu.stats.streamThresholdGB`` (default 8) or the run is data parallel (every
+    rank then parses only its own byte range instead of the whole data set)."""
+    from ..config import environment
+    from ..data.purifier import plan_dataset
+    from ..data.stream import data_bytes
+    from ..parallel import dist
+    mode = str(environment.get("shifu.stats.streaming", "auto")).lower()
+    if mode in ("true", "1", "yes"):
+        return True
+    if mode in ("false", "0", "no"):
+        return False
+    if dist.info().world_size > 1:
+        return True
+    try:
+        nbytes = data_bytes(plan_dataset(ms.mc, ms.mc.dataSet))
+    except Exception:
+        return False
+    return nbytes > float(environment.get("shifu.stats.streamThresholdGB", 8)) * (1 << 30)
+
+
+def _stats_streamed(ms: ModelSet, cols, device=None) -> None:
+    """Stats over row chunks of this rank's byte range (algos/stats_stream.py)."""
+    import torch
+    from ..algos.stats_stream import compute_column_stats_streamed
+    from ..config import environment
+    from ..data import stream as DS
+    from ..data.purifier import plan_dataset
+    from ..parallel import dist
+    mc = ms.mc
+    info = dist.info()
+    plan = plan_dataset(mc, mc.dataSet, [c.name for c in cols if not c.is_categorical()],
+                        [c.name for c in cols if c.is_categorical()])
+    chunk = int(float(environment.get("shifu.stats.chunkMB", 256)) * (1 << 20))
+    rate = float(mc.stats.get("sampleRate", 1.0))
+    neg_only = bool(mc.stats.get("sampleNegOnly", False))
+
+    def chunks():
+        return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only)
+    multi = info.world_size > 1
+    if multi and device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if info.backend == "nccl" else "cpu"
+    n = compute_column_stats_streamed(
+        mc, ms.ccs, chunks, device=device, columns={c.name for c in cols},
+        reduce=(lambda t, op: dist.all_reduce_(t, op)) if multi else None,
+        allgather=dist.all_gather_cat if multi else None,
+        gather_objects=dist.all_gather_objects if multi else None)
+    _log.info("stats (streamed, %d MB chunks, rank %d/%d): %d valid rows", chunk >> 20, info.rank,
+              info.world_size, n)
 
 
 def run_correlation(ms: ModelSet, device=None, chunk_rows: int = 1 << 18):
