@@ -28,6 +28,7 @@ count as 0.
 from __future__ import annotations
 
 import math
+import weakref
 
 import numpy as np
 import torch
@@ -141,6 +142,7 @@ class QuantileEngine:
         else:
             self.mm = torch.tensor([_I64_MAX, _I64_MIN, _I64_MAX, _I64_MIN] * C, dtype=i64, device=dev).view(C, 4)
         self.scnt = torch.zeros(C, dtype=i64, device=dev)
+        self.smom = torch.zeros(C, 2, dtype=torch.float64, device=dev)      # selected sum, sum of squares
         self.hll = torch.zeros(C, HLL_M, dtype=torch.int32 if self.hip else i64, device=dev)
         self.wmax = 0.0
         self.stage = "a"
@@ -164,6 +166,17 @@ class QuantileEngine:
     def _stream(self):
         return self._nat.stream_of(self.mm)
 
+    def _sel(self, y, n):
+        """Packed selection bitmask of this chunk's rows for the kernels (None = every row)."""
+        if not self.sel_mode:
+            return None
+        ref = getattr(self, "_sel_ref", None)
+        if ref is None or ref[0]() is not y or ref[1] != n:       # weakref: no address aliasing
+            from ..ops.stats_ops import pack_sel
+            self._sel_bits = pack_sel(y[:n], self.sel_mode)
+            self._sel_ref = (weakref.ref(y), n)
+        return self._sel_bits
+
     # ---- pass A ------------------------------------------------------------------------------
     def pass_a(self, vals: torch.Tensor, y=None, w=None) -> None:
         n = self._check(vals, y, w)
@@ -174,8 +187,8 @@ class QuantileEngine:
             if bool(sm.any()):
                 self.wmax = max(self.wmax, float(w[:n][sm].clamp(min=0).max()))
         if self.hip:
-            self._nat.call_hip("shifu_qprep", vals, vals.stride(0), n, self.C, y if self.sel_mode else None,
-                               self.sel_mode, self.thr, self.mm, self.scnt, self.hll, self._stream())
+            self._nat.call_hip("shifu_qprep", vals, vals.stride(0), n, self.C, self._sel(y, n),
+                               self.sel_mode, self.thr, self.mm, self.scnt, self.hll, self.smom, self._stream())
             return
         v = _clean(vals, self.thr)
         fin = torch.isfinite(v)
@@ -187,6 +200,9 @@ class QuantileEngine:
         self.mm[:, 2] = torch.minimum(self.mm[:, 2], torch.where(fin, k, mx).amin(1))
         self.mm[:, 3] = torch.maximum(self.mm[:, 3], torch.where(fin, k, mn).amax(1))
         self.scnt += sel.sum(1)
+        vs = torch.where(sel, v, torch.zeros_like(v))
+        self.smom[:, 0] += vs.sum(1)
+        self.smom[:, 1] += (vs * vs).sum(1)
         for c in range(self.C):
             hll_update(self.hll[c], v[c][fin[c]])
 
@@ -201,6 +217,7 @@ class QuantileEngine:
         self.mm[:, 0], self.mm[:, 2] = mn[:, 0], mn[:, 1]
         self.mm[:, 1], self.mm[:, 3] = mx[:, 0], mx[:, 1]
         self._red(self.scnt, "sum")
+        self._red(self.smom, "sum")
         self._red(self.hll, "max")
         if self.weighted:
             t = torch.tensor([self.wmax], dtype=torch.float64, device=self.dev)
@@ -211,13 +228,20 @@ class QuantileEngine:
         self.lo, self.hi = _unskey_np(mm[:, 0]), _unskey_np(mm[:, 1])
         alo, ahi = _unskey_np(mm[:, 2]), _unskey_np(mm[:, 3])
         self.any_fin = mm[:, 2] <= mm[:, 3]
-        self.prm_np = np.zeros((self.C, 4), np.float64)
+        aprm = np.zeros((self.C, 2), np.float64)
+        smom = self.smom.cpu().numpy()
+        self.cols = [_Col() for _ in range(self.C)]
         for c in range(self.C):
-            if self.scnt_np[c] > 0:
-                self.prm_np[c, :2] = _mapping(self.lo[c], self.hi[c])
             if self.any_fin[c]:
-                self.prm_np[c, 2:] = _mapping(alo[c], ahi[c])
-        self.win_np = np.tile(np.array([_I64_MIN, _I64_MAX], np.int64), (self.C, 1))
+                aprm[c] = _lin_map(alo[c], ahi[c], NB)
+            if self.scnt_np[c] > 0:
+                n = float(self.scnt_np[c])
+                with np.errstate(all="ignore"):
+                    var = smom[c, 1] / n - (smom[c, 0] / n) ** 2
+                    span = self.hi[c] - self.lo[c]
+                    heavy = bool(np.isfinite(var) and np.isfinite(span) and span > HEAVY_RATIO * math.sqrt(max(var, 0.0)))
+                self.cols[c].windows = [_Win(int(mm[c, 0]), int(mm[c, 1]), 0, NB, key=heavy)]
+        self.aprm = torch.as_tensor(aprm, device=self.dev)
         nmax = max(int(self.scnt_np.max()) if self.C else 1, 1)
         if self.weighted:
             lim = 2.0 ** 61 / (max(self.wmax, 1e-300) * nmax * max(self.nb, 1))
@@ -233,16 +257,27 @@ class QuantileEngine:
         self.akmn = torch.full((C, NB), self._init_mn, dtype=i64, device=dev) if self.with_all else None
         self.akmx = torch.full((C, NB), self._init_mx, dtype=i64, device=dev) if self.with_all else None
         self.level = 1
-        self.cols = [_Col() for _ in range(C)]
         self.active = [c for c in range(C) if self.any_fin[c]]
         self.slots = []                       # (column, bucket) gathered in pass C
-        self._upload_level()
+        self._upload_windows()
         self.stage = "b"
 
-    def _upload_level(self):
-        self.prm = torch.as_tensor(self.prm_np, device=self.dev)
-        w = self.win_np ^ _I64_MIN if self.hip else self.win_np      # unsigned patterns for HIP
-        self.win = torch.as_tensor(np.ascontiguousarray(w), device=self.dev)
+    def _upload_windows(self):
+        wptr = np.zeros(self.C + 1, np.int32)
+        rows = []
+        for c in range(self.C):
+            ws = self.cols[c].windows
+            wptr[c + 1] = wptr[c] + len(ws)
+            rows += [w.record() for w in ws]
+        self.wptr_np = wptr
+        self.wins_np = rows
+        if self.hip:
+            arr = np.zeros(max(len(rows), 1), dtype=_QWIN)
+            for i, r in enumerate(rows):
+                arr[i] = (r[0] + (1 << 63), r[1] + (1 << 63), r[2], r[3], r[4], (r[5] + (1 << 63)) & ((1 << 64) - 1),
+                          r[6], r[7])
+            self.wins = torch.as_tensor(np.frombuffer(arr.tobytes(), np.uint8).copy(), device=self.dev)
+            self.wptr = torch.as_tensor(wptr, device=self.dev)
         self.colmap = torch.as_tensor(np.asarray(self.active or [0], np.int32), device=self.dev)
 
     # ---- pass B ------------------------------------------------------------------------------
@@ -252,45 +287,66 @@ class QuantileEngine:
             return
         with_all = self.with_all and self.level == 1
         if self.hip:
-            self._nat.call_hip("shifu_qhist", vals, vals.stride(0), n, self.C, y if self.sel_mode else None,
+            self._nat.call_hip("shifu_qhist", vals, vals.stride(0), n, self.C, self._sel(y, n),
                                w if self.weighted else None, self.sel_mode, self.thr, self.colmap, len(self.active),
-                               self.win, self.prm, self.wscale, int(with_all), self.cnt, self.wq, self.kmn, self.kmx,
-                               self.akmn, self.akmx, self._stream())
+                               self.wptr, self.wins, self.aprm, self.wscale, int(with_all), self.cnt, self.wq,
+                               self.kmn, self.kmx, self.akmn, self.akmx, self._stream())
             return
-        act = torch.as_tensor(self.active, device=vals.device)
-        v = _clean(vals[act], self.thr)
-        fin = torch.isfinite(v)
-        vz = torch.where(fin, v, torch.zeros_like(v))
-        k = skey(vz)
-        win = self.win[act]
-        sel = fin & _selmask(y, self.sel_mode, n, v.device)[None, :] & (k >= win[:, :1]) & (k <= win[:, 1:])
-        base = (act * NB)[:, None]
-        b = _bucket(vz, self.prm[act, 0], self.prm[act, 1]) + base
-        bs, ks = b[sel], k[sel]
-        self.cnt.view(-1).scatter_add_(0, bs, torch.ones_like(bs))
-        self.kmn.view(-1).scatter_reduce_(0, bs, ks, reduce="amin")
-        self.kmx.view(-1).scatter_reduce_(0, bs, ks, reduce="amax")
-        if self.weighted:
-            q = torch.round(w[:n].clamp(min=0) * self.wscale).long()[None, :].expand(len(self.active), n)[sel]
-            self.wq.view(-1).scatter_add_(0, bs, q)
-        if with_all:
-            ab = _bucket(vz, self.prm[act, 2], self.prm[act, 3]) + base
-            self.akmn.view(-1).scatter_reduce_(0, ab[fin], k[fin], reduce="amin")
-            self.akmx.view(-1).scatter_reduce_(0, ab[fin], k[fin], reduce="amax")
+        sm = _selmask(y, self.sel_mode, n, vals.device)
+        q_all = torch.round(w[:n].clamp(min=0) * self.wscale).long() if self.weighted else None
+        for c in self.active:
+            v = _clean(vals[c], self.thr)
+            fin = torch.isfinite(v)
+            vz = torch.where(fin, v, torch.zeros_like(v))
+            k = skey(vz)
+            sel = fin & sm
+            b = self._win_buckets(c, vz, k, sel)
+            take = b >= 0
+            bs, ks = b[take] + c * NB, k[take]
+            self.cnt.view(-1).scatter_add_(0, bs, torch.ones_like(bs))
+            self.kmn.view(-1).scatter_reduce_(0, bs, ks, reduce="amin")
+            self.kmx.view(-1).scatter_reduce_(0, bs, ks, reduce="amax")
+            if self.weighted:
+                self.wq.view(-1).scatter_add_(0, bs, q_all[take])
+            if with_all:
+                ab = _bucket(vz[None, :], self.aprm[c:c + 1, 0], self.aprm[c:c + 1, 1])[0] + c * NB
+                self.akmn.view(-1).scatter_reduce_(0, ab[fin], k[fin], reduce="amin")
+                self.akmx.view(-1).scatter_reduce_(0, ab[fin], k[fin], reduce="amax")
+
+    def _win_buckets(self, c, vz, k, sel):
+        """torch twin of the kernels' win_bucket: bucket index per row (-1 outside every window)."""
+        out = torch.full_like(k, -1)
+        for w in self.cols[c].windows:
+            m = sel & (k >= w.lo_key) & (k <= w.hi_key)
+            if not bool(m.any()):
+                continue
+            if w.msh < 0:
+                f = (vz[m] - w.mlo) * w.msc
+                f = torch.nan_to_num(f, nan=0.0, posinf=float(w.size), neginf=0.0)
+                b = torch.where(f <= 0, torch.zeros_like(f),
+                                torch.where(f >= w.size - 1, torch.full_like(f, w.size - 1), f)).long()
+            else:
+                d = k[m] - w.mklo
+                q = torch.bitwise_right_shift(d, w.msh)
+                if w.msh > 0:
+                    q = q & ((1 << (64 - w.msh)) - 1)
+                b = torch.where((q < 0) | (q > w.size - 1), torch.full_like(q, w.size - 1), q)
+            out[m] = w.base + b
+        return out
 
     def finish_b(self) -> str:
         """Merge this level's histograms and plan every active column: returns "B" when some
-        column refines into a narrower window (another pass B), "C" when values must be gathered,
+        column refines into narrower windows (another pass B), "C" when values must be gathered,
         "done" otherwise."""
         if self.hip:
             for t in (self.kmn, self.kmx) + ((self.akmn, self.akmx) if self.with_all and self.level == 1 else ()):
                 t ^= _I64_MIN
+        idx = self.active_t()
         if self.level == 1:
             self.local_cnt = self.cnt.clone()
         else:
-            self.local_cnt[self.active_t()] = self.cnt[self.active_t()]
+            self.local_cnt[idx] = self.cnt[idx]
         if self.reduce is not None:       # merge only this level's rows (finished rows are merged)
-            idx = self.active_t()
             for t, op in ((self.cnt, "sum"), (self.wq, "sum"), (self.kmn, "min"), (self.kmx, "max")):
                 if t is None:
                     continue
@@ -301,35 +357,42 @@ class QuantileEngine:
             self._red(self.akmn, "min")
             self._red(self.akmx, "max")
             self.akmn_np, self.akmx_np = self.akmn.cpu().numpy(), self.akmx.cpu().numpy()
-        act = self.active
         cnt = self.cnt.cpu().numpy()
         rank = self.wq.cpu().numpy() if self.weighted else cnt
         kmn, kmx = self.kmn.cpu().numpy(), self.kmx.cpu().numpy()
         if self.level == 1:
             self.h1 = (cnt.copy(), kmn.copy(), kmx.copy())
-        refine = []
-        for c in act:
-            if self._plan(c, cnt[c], rank[c], kmn[c], kmx[c]):
-                refine.append(c)
+        refine = [c for c in self.active if self._plan(c, cnt[c], rank[c], kmn[c], kmx[c])]
+        # keep the gather (one device sort of every gathered value) within budget: the columns
+        # with the largest gathers refine instead (one more histogram pass over those columns)
+        gathering = sorted((c for c in self.active if c not in refine and self.cols[c].gather
+                            and self.can_refine(self.cols[c])), key=lambda c: -self.cols[c].gather_size)
+        total = sum(self.cols[c].gather_size for c in self.active if self.cols[c].gather)
+        for c in gathering:
+            if total <= GATHER_BUDGET:
+                break
+            st = self.cols[c]
+            total -= st.gather_size
+            self.slots = [sb for sb in self.slots if sb[0] != c]
+            st.gather, st.singles = [], np.zeros(0)
+            self._refine(st)
+            refine.append(c)
         if refine:
+            refine.sort()
             self.level += 1
             self.active = refine
-            idx = torch.as_tensor(refine, device=self.dev)
-            self.cnt[idx] = 0
+            ridx = torch.as_tensor(refine, device=self.dev)
+            self.cnt[ridx] = 0
             if self.weighted:
-                self.wq[idx] = 0
-            if self.hip:      # kernels keep unsigned patterns; planned columns keep signed state
-                self.kmn[idx] = self._init_mn
-                self.kmx[idx] = self._init_mx
-            else:
-                self.kmn[idx] = _I64_MAX
-                self.kmx[idx] = _I64_MIN
-            if self.hip:      # the next finish_b flips every row: pre-flip the finished ones
+                self.wq[ridx] = 0
+            if self.hip:      # kernels keep unsigned patterns: reset refined rows, re-flip finished ones
                 keep = torch.ones(self.C, dtype=torch.bool, device=self.dev)
-                keep[idx] = False
+                keep[ridx] = False
                 self.kmn[keep] ^= _I64_MIN
                 self.kmx[keep] ^= _I64_MIN
-            self._upload_level()
+            self.kmn[ridx] = self._init_mn
+            self.kmx[ridx] = self._init_mx
+            self._upload_windows()
             return "B"
         self.active = []
         return self._plan_gather()
@@ -338,7 +401,7 @@ class QuantileEngine:
         return torch.as_tensor(self.active, device=self.dev)
 
     def _plan(self, c, cnt, rank, kmn, kmx) -> bool:
-        """One level of column ``c``; True when it refines into a narrower window."""
+        """One level of column ``c`` over its windows; True when it refines further."""
         st, nb = self.cols[c], self.nb
         ne_mask = cnt > 0
         multi = ne_mask & (kmn != kmx)
@@ -351,69 +414,76 @@ class QuantileEngine:
                 st.mode = INTERVAL
                 return False
             T = int(rank.sum())
-            st.pending = [(j, -((-j * T) // nb)) for j in range(1, nb)]      # ceil(j*T/nb), exact
+            st.windows[0].targets = [(j, -((-j * T) // nb)) for j in range(1, nb)]   # ceil(j*T/nb), exact
             if mu == 0 and ne <= nb:
                 st.mode, st.small = SMALL, _unskey_np(kmn[ne_mask])
                 return False
             st.mode = EQPOP if ne + mu > nb else AMBIG
-        # AMBIG: decide small vs equal-population once the distinct count is known
-        if st.mode == AMBIG:
+        if st.mode == AMBIG:              # small vs equal-population once the distinct count is known
             if len(st.outside) + ne + mu > nb:
                 st.mode = EQPOP
             elif mu == 0:
-                st.small = np.sort(np.concatenate([np.asarray(st.outside, np.float64),
-                                                   _unskey_np(kmn[ne_mask])]))
+                st.small = np.sort(np.concatenate([np.asarray(st.outside, np.float64), _unskey_np(kmn[ne_mask])]))
                 st.distinct = int(st.small.size)
                 if st.small.size <= nb:
                     st.mode = SMALL
                     return False
                 st.mode = EQPOP
-        # targets: single-valued buckets resolve here, the rest stay pending
-        cum = st.off + np.cumsum(rank)
-        nxt_ne = _next_nonempty(ne_mask)
-        pend = []
-        for j, s in st.pending:
-            b = int(np.searchsorted(cum, s, side="left"))
-            b = min(b, NB - 1)
-            if not ne_mask[b]:
-                b = int(nxt_ne[b])
-                if b < 0:                       # beyond the window (cannot happen for valid ranks)
-                    continue
-            if not multi[b]:
-                st.res[j] = (float(_unskey_np(kmn[b])), self._after_bucket(st, b, ne_mask, kmn, nxt_ne))
-            else:
-                before = int(cum[b - 1]) if b > 0 else st.off
-                pend.append((j, s, b, s - before))
-        st.pending = [(j, s) for j, s, _, _ in pend]
-        need = sorted({b for _, _, b, _ in pend})
-        if st.mode == AMBIG:
-            need = [int(b) for b in np.nonzero(multi)[0]]
-        if not need:
-            st.done = True
+        pend = []                         # (bucket, targets [(j, s, need)], off, after)
+        singles = []
+        for win in st.windows:
+            lo, hi = win.base, win.base + win.size
+            cum = win.off + np.cumsum(rank[lo:hi])
+            nem = ne_mask[lo:hi]
+            nxt = _next_nonempty(nem)
+            by_b = {}
+            for j, s in win.targets:
+                b = min(int(np.searchsorted(cum, s, side="left")), win.size - 1)
+                if not nem[b]:
+                    b = int(nxt[b])
+                    if b < 0:
+                        continue
+                if not multi[lo + b]:
+                    st.res[j] = (float(_unskey_np(kmn[lo + b])), _after(nxt, b, kmn[lo:hi], win.after))
+                else:
+                    by_b.setdefault(b, []).append((j, s))
+            bs = sorted(by_b)
+            if st.mode == AMBIG:
+                bs = [int(b) for b in np.nonzero(multi[lo:hi])[0]]
+                singles += list(_unskey_np(kmn[lo:hi][nem & ~multi[lo:hi]]))
+            for b in bs:
+                off = int(cum[b - 1]) if b > 0 else win.off
+                pend.append((lo + b, by_b.get(b, []), off, _after(nxt, b, kmn[lo:hi], win.after)))
+        if not pend:
             return False
-        if self.level < MAX_LEVEL and int(cnt[need].max()) > GATHER_CAP:
-            f, l = need[0], need[-1]
-            if st.mode == AMBIG:          # single values outside the new window stay known
-                outside = ne_mask & ~multi
-                outside[f:l + 1] = False
-                st.outside += list(_unskey_np(kmn[outside]))
-            st.off = int(cum[f - 1]) if f > 0 else st.off
-            st.after = self._after_bucket(st, l, ne_mask, kmn, nxt_ne)
-            self.win_np[c] = (kmn[f], kmx[l])
-            self.prm_np[c, :2] = _mapping(float(_unskey_np(kmn[f])), float(_unskey_np(kmx[l])))
+        st.pend, st.pend_singles = pend, singles
+        st.pend_kmn, st.pend_kmx = kmn, kmx
+        st.gather_size = int(sum(cnt[b] for b, _, _, _ in pend))
+        big = int(max(cnt[b] for b, _, _, _ in pend)) > GATHER_CAP
+        if big and self.can_refine(st):
+            self._refine(st)
             return True
-        # final level: gather the pending buckets (AMBIG: every multi bucket)
-        st.gather = [(b, [(j, nd) for j, _, bb, nd in pend if bb == b],
-                      self._after_bucket(st, b, ne_mask, kmn, nxt_ne)) for b in need]
-        st.singles = _unskey_np(kmn[ne_mask & ~multi])
-        self.slots += [(c, b) for b in need]
+        # final level: gather the pending buckets
+        st.gather = [(b, [(j, s - off) for j, s in tg], after) for b, tg, off, after in pend]
+        st.singles = np.asarray(singles, np.float64)
+        self.slots += [(c, b) for b, _, _, _ in pend]
         return False
 
-    @staticmethod
-    def _after_bucket(st, b, ne_mask, kmn, nxt_ne):
-        """first value above bucket ``b`` (next non-empty bucket of the window, else above it)."""
-        n = int(nxt_ne[b + 1]) if b + 1 < NB else -1
-        return float(_unskey_np(kmn[n])) if n >= 0 else st.after
+    def can_refine(self, st) -> bool:
+        return self.level < MAX_LEVEL and len(st.pend) <= MAX_WINDOWS
+
+    def _refine(self, st) -> None:
+        """Every pending bucket becomes a window of the next level (sharing the 2048 buckets)."""
+        pend, kmn, kmx = st.pend, st.pend_kmn, st.pend_kmx
+        size = NB // len(pend)
+        if st.mode == AMBIG:
+            st.outside += st.pend_singles
+        st.windows = []
+        for i, (b, tg, off, after) in enumerate(pend):
+            wlo, whi = float(_unskey_np(kmn[b])), float(_unskey_np(kmx[b]))
+            w = _Win(int(kmn[b]), int(kmx[b]), i * size, size, key=_spans_binades(wlo, whi))
+            w.off, w.after, w.targets = off, after, tg
+            st.windows.append(w)
 
     def _plan_gather(self) -> str:
         slots = sorted(self.slots)
@@ -433,10 +503,11 @@ class QuantileEngine:
         self.gq = torch.empty(max(M, 1), dtype=torch.int64, device=self.dev) if self.weighted else None
         self.scur = torch.zeros(max(len(slots), 1), dtype=torch.int32 if self.hip else torch.int64, device=self.dev)
         self.gcols = sorted({c for c, _ in slots})
+        self.active = self.gcols
+        self._upload_windows()
+        self.active = []
         self.gcolmap = torch.as_tensor(np.asarray(self.gcols or [0], np.int32), device=self.dev)
-        self.win = torch.as_tensor(np.ascontiguousarray(self.win_np ^ _I64_MIN if self.hip else self.win_np),
-                                   device=self.dev)
-        self.prm = torch.as_tensor(self.prm_np, device=self.dev)
+        self.two_phase = M > TWO_PHASE_GATHER
         self.stage = "c"
         return "C" if slots else "done"
 
@@ -446,35 +517,33 @@ class QuantileEngine:
         if n == 0 or not self.slots:
             return
         if self.hip:
-            self._nat.call_hip("shifu_qgather", vals, vals.stride(0), n, self.C, y if self.sel_mode else None,
+            self._nat.call_hip("shifu_qgather", vals, vals.stride(0), n, self.C, self._sel(y, n),
                                w if self.weighted else None, self.sel_mode, self.thr, self.gcolmap, len(self.gcols),
-                               self.win, self.prm, self.wscale, self.slot_t, self.sbase, self.scur, self.gv, self.gq,
-                               self._stream())
+                               self.wptr, self.wins, self.wscale, self.slot_t, self.sbase, self.scur, self.gv,
+                               self.gq, int(self.two_phase), self._stream())
             return
-        act = torch.as_tensor(self.gcols, device=vals.device)
-        v = _clean(vals[act], self.thr)
-        fin = torch.isfinite(v)
-        vz = torch.where(fin, v, torch.zeros_like(v))
-        k = skey(vz)
-        win = self.win[act]
-        sel = fin & _selmask(y, self.sel_mode, n, v.device)[None, :] & (k >= win[:, :1]) & (k <= win[:, 1:])
-        b = _bucket(vz, self.prm[act, 0], self.prm[act, 1])
-        s = torch.gather(self.slot_t[act].long(), 1, b)
-        take = sel & (s >= 0)
-        ss, vv = s[take], v[take]
-        if ss.numel() == 0:
-            return
-        order = torch.argsort(ss, stable=True)
-        ss, vv = ss[order], vv[order]
-        cnts = torch.bincount(ss, minlength=len(self.slots))
-        first = torch.cumsum(cnts, 0) - cnts
-        pos = torch.arange(ss.numel(), device=v.device) - first[ss]
-        at = self.sbase[ss] + self.scur[ss] + pos
-        self.gv[at] = vv
-        if self.weighted:
-            q = torch.round(w[:n].clamp(min=0) * self.wscale).long()[None, :].expand(len(self.gcols), n)[take][order]
-            self.gq[at] = q
-        self.scur += cnts
+        sm = _selmask(y, self.sel_mode, n, vals.device)
+        q_all = torch.round(w[:n].clamp(min=0) * self.wscale).long() if self.weighted else None
+        for c in self.gcols:
+            v = _clean(vals[c], self.thr)
+            fin = torch.isfinite(v)
+            vz = torch.where(fin, v, torch.zeros_like(v))
+            b = self._win_buckets(c, vz, skey(vz), fin & sm)
+            s = torch.where(b >= 0, self.slot_t[c].long()[b.clamp(min=0)], torch.full_like(b, -1))
+            take = s >= 0
+            ss, vv = s[take], v[take]
+            if ss.numel() == 0:
+                continue
+            order = torch.argsort(ss, stable=True)
+            ss, vv = ss[order], vv[order]
+            cnts = torch.bincount(ss, minlength=len(self.slots))
+            first = torch.cumsum(cnts, 0) - cnts
+            pos = torch.arange(ss.numel(), device=v.device) - first[ss]
+            at = self.sbase[ss] + self.scur[ss] + pos
+            self.gv[at] = vv
+            if self.weighted:
+                self.gq[at] = q_all[take][order]
+            self.scur += cnts
 
     # ---- resolution --------------------------------------------------------------------------
     def finish(self):
@@ -489,7 +558,9 @@ class QuantileEngine:
             if self.allgather is not None:
                 gv, seg = self.allgather(gv), self.allgather(seg)
                 gq = self.allgather(gq) if self.weighted else None
-            o1 = torch.argsort(gv, stable=True)
+            # segmented sort: one sort by (slot, value) through the order-preserving key
+            key = skey(gv)
+            o1 = torch.argsort(key)
             o2 = torch.argsort(seg[o1], stable=True)
             perm = o1[o2]
             V, SEG = gv[perm], seg[perm]
@@ -539,7 +610,7 @@ class QuantileEngine:
         for c, st in enumerate(self.cols):
             if self.interval or st.mode == INTERVAL:
                 bounds.append(self._interval(c))
-            elif st.mode == EMPTY:
+            elif st.mode in (EMPTY, None):
                 bounds.append([float("-inf")])
             elif st.mode == SMALL:
                 u = st.small
@@ -589,33 +660,77 @@ class QuantileEngine:
 
 
 MAX_LEVEL = 4
-GATHER_CAP = 1 << 18          # values per gathered bucket before a column refines instead
+MAX_WINDOWS = 128             # windows per column (MAXW in quantile_kernels.hip)
+GATHER_CAP = 1 << 17          # values per gathered bucket before a column refines instead
+GATHER_BUDGET = 4 << 20       # gathered values per engine (batch) before the largest refine
+TWO_PHASE_GATHER = 1 << 24    # above this many gathered values qgather reserves per block
+HEAVY_RATIO = 64.0            # range > 64 sigma: bucket in key space (heavy tails)
+
+_QWIN = np.dtype([("lo", "<u8"), ("hi", "<u8"), ("mlo", "<f8"), ("msc", "<f8"), ("msh", "<i8"), ("mklo", "<u8"),
+                  ("base", "<i4"), ("size", "<i4")])
+assert _QWIN.itemsize == 56
+
+
+class _Win:
+    """A key window [lo_key, hi_key] (signed keys) of one column mapped onto ``size`` buckets at
+    ``base``: linear in value, or in key space (heavy tails / windows spanning binades)."""
+
+    def __init__(self, lo_key: int, hi_key: int, base: int, size: int, key: bool = False):
+        self.lo_key, self.hi_key, self.base, self.size = int(lo_key), int(hi_key), int(base), int(size)
+        lo, hi = float(_unskey_np(np.int64(lo_key))), float(_unskey_np(np.int64(hi_key)))
+        if key:
+            self.msh, self.mklo = ((max(hi_key - lo_key, 0) // self.size).bit_length(), self.lo_key)
+            self.mlo, self.msc = 0.0, 0.0
+        else:
+            self.msh, self.mklo = -1, 0
+            self.mlo, self.msc = _lin_map(lo, hi, self.size)
+        self.off = 0
+        self.after = None
+        self.targets = []
+
+    def record(self):
+        return (self.lo_key, self.hi_key, self.mlo, self.msc, self.msh, self.mklo, self.base, self.size)
 
 
 class _Col:
-    """Per-column plan: mode, rank offset / first value above the current window, pending and
-    resolved targets, known values outside the window (AMBIG), gathered buckets."""
+    """Per-column plan: mode, windows of the current level, resolved targets, values known
+    outside the windows (AMBIG), gathered buckets."""
 
     def __init__(self):
         self.mode = None
-        self.off = 0
-        self.after = None
-        self.pending = []
+        self.windows = []
         self.res = {}
         self.outside = []
         self.gather = []
         self.singles = np.zeros(0)
         self.small = None
         self.distinct = None
-        self.done = False
+        self.pend = []
+        self.gather_size = 0
 
 
-def _mapping(lo: float, hi: float):
-    """(lo, scale) of the 2048-bucket linear map; scale 0 puts everything in bucket 0."""
+def _lin_map(lo: float, hi: float, size: int):
+    """(lo, scale) of a ``size``-bucket linear map; scale 0 puts everything in bucket 0."""
     if not (hi > lo):
         return lo, 0.0
     with np.errstate(all="ignore"):
-        return lo, (NB / 2) / (hi / 2 - lo / 2)
+        return lo, (size / 2) / (hi / 2 - lo / 2)
+
+
+def _after(nxt, b, kmn_w, outer):
+    """First value above bucket ``b`` of a window: the next non-empty bucket's min, else the
+    window's own ``after`` (the first value above the window)."""
+    n = int(nxt[b + 1]) if b + 1 < nxt.size else -1
+    return float(_unskey_np(kmn_w[n])) if n >= 0 else outer
+
+
+def _spans_binades(lo: float, hi: float) -> bool:
+    """A refinement window worth bucketing in key space: one sign and > 2^10 magnitude ratio (a
+    window straddling 0 stays linear: in key space the values near 0 would own most buckets)."""
+    if lo < 0.0 < hi:
+        return False
+    a, b = sorted((abs(lo), abs(hi)))
+    return b > 1024.0 * max(a, 1e-300)
 
 
 def _next_nonempty(ne_mask: np.ndarray) -> np.ndarray:

@@ -60,15 +60,16 @@ HIP_SIGNATURES = {
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
     "shifu_gbdt_residual": "pppp" "p" "li" "s",
     # stats_kernels.hip
-    "shifu_column_stats": "plppli" "ppii" "dd" "pipii" "s",
+    "shifu_column_stats": "plppli" "ppii" "dd" "pipiip" "s",
     "shifu_normalize": "plli" "pppp" "pl" "s",
     "shifu_bin_codes": "plli" "pp" "pl" "s",
     "shifu_lr_grad": "plli" "i" "ppp" "pp" "i" "s",
     "shifu_sensitivity": "plpl" "pp" "f" "p" "l" "iiiii" "p" "s",
     # quantile_kernels.hip
-    "shifu_qprep": "pllipid" "ppp" "s",
-    "shifu_qhist": "pllippid" "pip" "pdi" "pppppp" "s",
-    "shifu_qgather": "pllippid" "pip" "pd" "ppp" "pp" "s",
+    "shifu_pack_bits": "plip" "s",
+    "shifu_qprep": "pllipid" "pppp" "s",
+    "shifu_qhist": "pllippid" "pipp" "pdi" "pppppp" "s",
+    "shifu_qgather": "pllippid" "pipp" "d" "ppp" "ppi" "s",
 }
 
 # host runtime: name -> (argsig, restype)

@@ -103,3 +103,24 @@ __device__ __forceinline__ float act_deriv_pre(int act, float b) {
     default: return act_deriv_out(act, act_fwd(act, b));
   }
 }
+
+// Streaming row loop with U independent loads in flight per thread: the stats/quantile kernels
+// are HBM-bound single passes, and one outstanding 8-byte load per lane leaves far too few bytes
+// in flight per CU (Little's law at ~1 us HBM latency); loading U rows before processing any
+// keeps U x the bytes in flight.  f(r, v) is called for every row r in [r0, r1) of this thread.
+template <int U, typename F>
+__device__ __forceinline__ void for_rows(const double* __restrict__ col, long r0, long r1, int stride, F&& f) {
+  for (long rb = r0 + threadIdx.x; rb < r1; rb += (long)U * stride) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = rb + (long)u * stride;
+      v[u] = r < r1 ? col[r] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = rb + (long)u * stride;
+      if (r < r1) f(r, v[u]);
+    }
+  }
+}

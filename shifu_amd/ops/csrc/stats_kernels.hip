@@ -53,6 +53,7 @@ struct StatsArgs {
   unsigned long long* hist; int hstride;     // [F][hstride][4]: cpos, cneg, wpos, wneg (fixed point)
   double* part; int nchunks; long rows_per_chunk;   // [F][nchunks][8]
   int unit_w;                                // every weight is 1: weight sums = counts
+  const unsigned int* posbits;               // binary: bit r = (y[r] > 0.5), packed (1 bit per row)
   int max_nb;                                // max boundaries over the batch (sizes the LDS carve)
   int priv;                                  // per-thread private counters (unit_w, few bins)
 };
@@ -105,8 +106,7 @@ __global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
   const long r1 = min(a.n, r0 + a.rows_per_chunk);
   const double* col = a.vals + (long)f * a.ldv;
   double cnt = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, mn = INFINITY, mx = -INFINITY;
-  for (long r = r0 + tid; r < r1; r += 256) {
-    double v = col[r];
+  for_rows<4>(col, r0, r1, 256, [&](long r, double v) {
     if (v > a.num_thr) v = NAN;               // numericalValueThreshold -> invalid
     int bin;
     if (v != v) {
@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
         mn = fmin(mn, v); mx = fmax(mx, v);
       }
     }
-    const bool pos = !a.binary || a.y[r] > 0.5f;
+    const bool pos = !a.binary || ((a.posbits[r >> 5] >> (r & 31)) & 1u);
     if (private_cnt) {
       priv[(bin * 2 + (pos ? 1 : 0)) * 256 + tid] += 1u;
     } else if (a.unit_w) {
@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256) column_stats_kernel(StatsArgs a) {
       if (pos) { atomicAdd(&cp[bin], 1u); atomicAdd(&wp[bin], q); }
       else     { atomicAdd(&cn[bin], 1u); atomicAdd(&wn[bin], q); }
     }
-  }
+  });
   if (private_cnt) {                          // one wave per key: sum the 256 thread columns
     __syncthreads();
     const int wid = tid >> 6;
@@ -489,11 +489,12 @@ __global__ void __launch_bounds__(256) sensitivity_kernel(SensArgs a) {
 SHIFU_API int shifu_column_stats(const double* vals, long ldv, const float* y, const double* w, long n, int F,
                                  const double* bounds, const int* boff, int max_nb, int binary, double wscale,
                                  double num_thr, void* hist, int hstride, double* part, int nchunks, int unit_w,
-                                 hipStream_t stream) {
+                                 const unsigned int* posbits, hipStream_t stream) {
+  if (binary && !posbits) return -1;
   if (max_nb > MAXB || hstride < max_nb + 1 || nchunks <= 0 || nchunks > 65535 || F <= 0) return -1;
   const int priv = unit_w && 2 * (max_nb + 1) <= PRIV_KEYS;
   StatsArgs a{vals, ldv, y, w, n, bounds, boff, binary, wscale, num_thr, (unsigned long long*)hist, hstride,
-              part, nchunks, (n + nchunks - 1) / nchunks, unit_w, max_nb, priv};
+              part, nchunks, (n + nchunks - 1) / nchunks, unit_w, posbits, max_nb, priv};
   const long lds = cs_lds_bytes(max_nb, priv, unit_w);
   if (lds > 150 * 1024) return -1;
   hipLaunchKernelGGL(column_stats_kernel, dim3(F, nchunks), dim3(256), (unsigned)lds, stream, a);

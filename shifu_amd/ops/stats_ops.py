@@ -18,6 +18,30 @@ def _dev_tensor(a, dtype, dev):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).to(dev)
 
 
+def pack_bits(mask: torch.Tensor) -> torch.Tensor:
+    """bool [n] -> int32 words, bit r of word r // 32 = mask[r] (the kernels' row bitmasks)."""
+    n = mask.numel()
+    m = torch.zeros(((n + 31) // 32) * 32, dtype=torch.int64, device=mask.device)
+    m[:n] = mask.reshape(-1).to(torch.int64)
+    words = (m.view(-1, 32) << torch.arange(32, device=mask.device, dtype=torch.int64)).sum(1)
+    return torch.where(words >= (1 << 31), words - (1 << 32), words).to(torch.int32)
+
+
+def pack_sel(y: torch.Tensor, mode: int) -> torch.Tensor:
+    """Row bitmask of ``y > 0.5`` (mode 1) or its complement (mode 2): the HIP ballot kernel on the
+    GPU, :func:`pack_bits` on the CPU."""
+    n = y.numel()
+    if y.device.type != "cuda":
+        m = y.reshape(-1) > 0.5
+        return pack_bits(m if mode == 1 else ~m)
+    out = torch.empty((n + 31) // 32 + 1, dtype=torch.int32, device=y.device)
+    yf = y.reshape(-1)
+    if yf.dtype != torch.float32 or not yf.is_contiguous():
+        yf = yf.float().contiguous()
+    nat.call_hip("shifu_pack_bits", yf, n, int(mode), out, nat.stream_of(yf))
+    return out
+
+
 def pack_bounds(bounds_list):
     offs = [0]
     flat = []
@@ -47,8 +71,9 @@ def column_stats(vals: torch.Tensor, y: torch.Tensor, w: torch.Tensor, bounds_li
     part = torch.zeros(F * nchunks * 8, dtype=torch.float64, device=dev)
     bt, ot = _dev_tensor(bflat, torch.float64, dev), _dev_tensor(boff, torch.int32, dev)
     unit_w = bool(N) and bool(torch.all(w[:N] == 1.0).item())
+    posbits = pack_sel(y[:N], 1) if binary else None
     rc = nat.call_hip("shifu_column_stats", vals, vals.stride(0), y, w, N, F, bt, ot, max_nb, int(binary), wscale,
-                      float(num_thr), hist, hstride, part, nchunks, int(unit_w), nat.stream_of(vals))
+                      float(num_thr), hist, hstride, part, nchunks, int(unit_w), posbits, nat.stream_of(vals))
     if rc:
         raise RuntimeError(f"shifu_column_stats failed rc={rc}")
     h = hist.view(F, hstride, 4).cpu().numpy()

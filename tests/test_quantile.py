@@ -131,11 +131,13 @@ def test_kernel_state_equals_torch_passes():
     assert a.finish() == b.finish()
 
 
-@pytest.mark.parametrize("cap", [4, 64])
-def test_refinement_levels_equal_oracle_cpu(monkeypatch, cap):
-    """A tiny gather cap forces every multi-valued target bucket through windowed refinement
-    (and AMBIG columns through the outside-value bookkeeping) -- cuts stay exact."""
+@pytest.mark.parametrize("cap,budget", [(4, 1 << 30), (64, 1 << 30), (1 << 20, 50)])
+def test_refinement_levels_equal_oracle_cpu(monkeypatch, cap, budget):
+    """A tiny per-bucket gather cap (or a tiny per-batch gather budget) forces the multi-valued
+    target buckets through windowed refinement (and AMBIG columns through the outside-value
+    bookkeeping) -- cuts stay exact."""
     monkeypatch.setattr(Q, "GATHER_CAP", cap)
+    monkeypatch.setattr(Q, "GATHER_BUDGET", budget)
     rng = np.random.default_rng(cap)
     n = 4000
     V = _columns(n, rng)
@@ -155,3 +157,25 @@ def test_refinement_levels_equal_oracle_gpu(monkeypatch):
     w = rng.integers(1, 5, size=n).astype(float)
     _check(V, y, w, "cuda", 10)
     _check(V, y, w, "cuda", 10, chunk=20000)
+
+
+def test_pack_bits_matches_numpy():
+    from shifu_amd.ops.stats_ops import pack_bits
+    rng = np.random.default_rng(0)
+    for n in (1, 31, 32, 33, 1000):
+        m = rng.random(n) < 0.4
+        words = pack_bits(torch.from_numpy(m)).numpy().view(np.uint32)
+        ref = np.packbits(np.concatenate([m, np.zeros((-n) % 32, bool)]), bitorder="little").view("<u4")
+        assert np.array_equal(words, ref)
+
+
+@pytest.mark.gpu
+def test_pack_sel_kernel_matches_cpu():
+    from shifu_amd.ops.stats_ops import pack_sel
+    rng = np.random.default_rng(1)
+    for n in (1, 31, 63, 64, 65, 1000, 100003):
+        y = torch.from_numpy((rng.random(n) < 0.4).astype(np.float32))
+        for mode in (1, 2):
+            a = pack_sel(y, mode).numpy()
+            b = pack_sel(y.cuda(), mode).cpu().numpy()[: a.size]
+            assert np.array_equal(a, b), (n, mode)
