@@ -394,6 +394,17 @@ def read_legacy_tree_model(data: bytes) -> TreeModelFile:
     return TreeModelFile(alg, loss, is_cls, ova, len(cols), {}, names, cats, mapping, [trees], 0)
 
 
+def iter_nodes(root):
+    """Pre-order walk over a record tree."""
+    stack = [root] if root is not None else []
+    while stack:
+        nd = stack.pop()
+        yield nd
+        if not nd.is_leaf():
+            stack.append(nd.right)
+            stack.append(nd.left)
+
+
 def read_tree_model(path_or_bytes) -> TreeModelFile:
     data = path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray)) else open(path_or_bytes, "rb").read()
     if _is_legacy(bytes(data)):
@@ -461,7 +472,10 @@ def heap_tree_to_record(tree, tree_id: int, columns, ccs_by_feature=None, learni
             nd.right = build(2 * nid + 1)
         else:
             nd.predict = float(tree.value[nid])
-            nd.class_value = int(round(tree.value[nid])) if is_classification else 0
+            if getattr(tree, "classification", False):      # native multi-class RF leaf
+                nd.class_value = int(tree.class_value[nid])
+            else:
+                nd.class_value = int(round(tree.value[nid])) if is_classification else 0
         return nd
     root = build(1)
     lr = tree.weight if learning_rate is None else learning_rate

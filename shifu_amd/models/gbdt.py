@@ -89,6 +89,8 @@ class TreeConfig:
     seed: int = 0
     valid_tolerance: float = 0.0
     early_stop: bool = False
+    n_classes: int = 0                  # RF classification with Entropy/Gini over > 2 classes: native
+                                        # multi-class trees (per-class bin stats, Impurity.java:368-734)
 
     def __post_init__(self):
         self.algorithm = self.algorithm.upper()
@@ -103,6 +105,10 @@ class TreeConfig:
     def is_gbt(self):
         return self.algorithm == "GBT"
 
+    @property
+    def is_multiclass(self):
+        return (not self.is_gbt) and self.n_classes > 2 and self.impurity in ("entropy", "gini")
+
 
 class Tree:
     """Heap-indexed tree (node id 1 = root, children 2i / 2i+1 as ``Node.leftIndex``)."""
@@ -115,6 +121,8 @@ class Tree:
         self.thr = np.full(m, -1, dtype=np.int32)       # numeric: left iff bin <= thr
         self.cat_left = np.zeros((m, 8), dtype=np.uint32)
         self.value = np.zeros(m, dtype=np.float32)
+        self.class_value = np.zeros(m, dtype=np.float32)  # multi-class RF: argmax class per node
+        self.classification = False
         self.wgt_cnt = np.zeros(m, dtype=np.float64)
         self.gain = np.zeros(m, dtype=np.float32)
         self.exists = np.zeros(m, dtype=bool)
@@ -127,12 +135,12 @@ class Tree:
     def leaves(self):
         return [i for i in range(1, self.max_nodes) if self.exists[i] and self.feat[i] < 0]
 
-    def device_arrays(self, device):
+    def device_arrays(self, device, classes: bool = False):
         return (torch.from_numpy(self.feat).to(device), torch.from_numpy(self.thr).to(device),
                 torch.from_numpy(self.cat_left.view(np.int32)).to(device),
-                torch.from_numpy(self.value).to(device))
+                torch.from_numpy(self.class_value if classes else self.value).to(device))
 
-    def predict_bins(self, bins: np.ndarray, is_cat: np.ndarray) -> np.ndarray:
+    def predict_bins(self, bins: np.ndarray, is_cat: np.ndarray, classes: bool = False) -> np.ndarray:
         """Host traversal (oracle for the HIP apply kernel)."""
         n = bins.shape[0]
         ids = np.ones(n, dtype=np.int64)
@@ -147,7 +155,7 @@ class Tree:
             bit = (self.cat_left[ids, b >> 5] >> (b & 31).astype(np.uint32)) & 1
             left = np.where(catm, bit == 1, b <= self.thr[ids])
             ids = np.where(active, np.where(left, 2 * ids, 2 * ids + 1), ids)
-        return self.value[ids]
+        return (self.class_value if classes else self.value)[ids]
 
 
 @dataclass
@@ -257,6 +265,10 @@ class TreeTrainer:
         self.tgen.manual_seed((self.cfg.seed * 1_000_003 + r * 7_919 + tree_index * 104_729) % (1 << 63))
 
     def _weights_for_tree(self) -> torch.Tensor:
+        return self._subsample()[1]
+
+    def _subsample(self):
+        """(per-row bag weight or None when every row is in the bag, sig * bag weight)."""
         c = self.cfg
         n = self.data.n
         sig = self.data.sig if self.data.sig is not None else torch.ones(n, device=self.dev)
@@ -266,8 +278,8 @@ class TreeTrainer:
         elif rate < 1.0:
             sub = (torch.rand(n, device=self.dev, generator=self.tgen) <= rate).float()
         else:
-            return sig.contiguous()
-        return (sig * sub).contiguous()
+            return None, sig.contiguous()
+        return sub, (sig * sub).contiguous()
 
     def _node_feature_mask(self, n_nodes: int) -> torch.Tensor | None:
         if self.n_sub >= self.F:
@@ -323,6 +335,18 @@ class TreeTrainer:
             tree.exists[1] = True
             tree.value[1] = ts / tw if tw != 0 else 0.0
             tree.wgt_cnt[1] = tw
+        if self.cfg.is_multiclass:     # root Predict: P(class 1) and the majority class
+            C = self.cfg.n_classes
+            yl = g.round().long().clamp(0, C - 1)
+            ctot = torch.stack([torch.zeros(C, dtype=torch.float64, device=self.dev).index_add_(0, yl, wt.double())
+                                for wt in ws])
+            dist.all_reduce_(ctot)
+            ctot = ctot.cpu().numpy()
+            for t, tree in enumerate(trees):
+                sw = ctot[t].sum()
+                tree.classification = True
+                tree.value[1] = ctot[t, 1] / sw if sw > 0 else 0.0
+                tree.class_value[1] = float(np.argmax(ctot[t])) if sw > 0 else 0.0
         n_leaves = [1] * T
         for level in range(1, c.max_depth):
             if not nodes:
@@ -388,6 +412,8 @@ class TreeTrainer:
                     tree.exists[cid] = True
                     tree.value[cid] = cs / cw if cw != 0 else 0.0
                     tree.wgt_cnt[cid] = cw
+                if "class_lr" in hist:
+                    tree.class_value[2 * nid], tree.class_value[2 * nid + 1] = hist["class_lr"][s_]
                 children.append((z, lw, rw))
             fuse = self._fuse if (self.gpu and T == 1) else None
             if fuse is not None:
@@ -471,6 +497,8 @@ class TreeTrainer:
         F = self.F
         nn = len(nodes)
         mask = self._node_feature_mask(nn)
+        if self.cfg.is_multiclass:
+            return self._build_and_split_multi(nodes, n_built, g, w, pos2row, hist_prev, mask)
         imp = IMPURITY_IDS[self.cfg.impurity]
         min_inst = float(self.cfg.min_instances_per_node)
         min_gain = float(self.cfg.min_info_gain)
@@ -556,6 +584,121 @@ class TreeTrainer:
         best = self._select_best(cand, nn)
         co = None if cat_order is None else cat_order.cpu().numpy()
         return best, co
+
+    # ---- native multi-class RF (Entropy / Gini over C classes) ------------------------------
+    def _class_hist(self, nodes, n_built, gc, w, pos2row, hist_prev, hist):
+        """One class's (sum w, sum w*[y == c]) histograms of every node of the level: the packed
+        HIP histogram kernel + slab reduction for the built nodes (all-reduced across ranks),
+        parent - sibling for the derived ones."""
+        d = self.data
+        F = self.F
+        if self.gpu:
+            from ..ops import _native as nat
+            st = nat.stream_of(d.bins)
+            items, ni, max_items = self._make_items(nodes, n_built)
+            if n_built and len(items):
+                ni_t = torch.from_numpy(ni).to(self.dev)
+                it = torch.from_numpy(items).to(self.dev)
+                slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
+                p2r = None if self._root_level else pos2row
+                nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, gc, it, len(items), slab, F,
+                             self.scale_w, self.scale_g, self._nmod, st)
+                built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
+                feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
+                cand = torch.zeros(len(nodes), F, 8, dtype=torch.float32, device=self.dev)
+                nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, None, None, None,
+                             hist.data_ptr(), built.data_ptr(), n_built, feat_list.data_ptr(), F,
+                             self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), None, cand.data_ptr(), None, F, 0,
+                             IMPURITY_IDS["variance"], 0, 0.0, 0.0, 1.0 / self.scale_w, 1.0 / self.scale_g, st)
+            elif n_built:
+                hist[:n_built].zero_()
+        else:
+            bins = self._codes().long()
+            for z in nodes:
+                if not z["built"]:
+                    continue
+                hist[z["slot"]].zero_()
+                rows = pos2row[z["start"]: z["end"]].long()
+                if rows.numel() == 0:
+                    continue
+                b = bins[rows % d.n]
+                qw = torch.round(w[rows].double() * self.scale_w).long()
+                qg = torch.round((w[rows] * gc[rows]).float().double() * self.scale_g).long()
+                idx = (torch.arange(F).unsqueeze(0) * NB + b).reshape(-1)
+                hist[z["slot"], 0].view(-1).index_add_(0, idx, qw.unsqueeze(1).expand(-1, F).reshape(-1))
+                hist[z["slot"], 1].view(-1).index_add_(0, idx, qg.unsqueeze(1).expand(-1, F).reshape(-1))
+        if n_built:
+            dist.all_reduce_(hist[:n_built])
+        for z in nodes:
+            if not z["built"]:
+                hist[z["slot"]] = hist_prev[z["parent"]] - hist[z["sib_slot"]]
+
+    def _build_and_split_multi(self, nodes, n_built, g, w, pos2row, hist_prev, mask):
+        """``Entropy`` / ``Gini`` split search over per-class bin statistics
+        (Impurity.java:368-734): the class sums come from C runs of the packed histogram kernel
+        (target = one-hot of the class), the gain scan is vectorized over (node, feature, bin)."""
+        cfg, d = self.cfg, self.data
+        C, F, nn = cfg.n_classes, self.F, len(nodes)
+        yl = g.round().long()
+        hists = []
+        for c in range(C):
+            gc = (yl == c).float().contiguous()
+            h = torch.empty(nn, 2, F, NB, dtype=torch.int64, device=self.dev)
+            self._class_hist(nodes, n_built, gc, w, pos2row, None if hist_prev is None else hist_prev[c], h)
+            hists.append(h)
+        H = torch.stack([h[:, 1] for h in hists], -1).double() * (1.0 / self.scale_g)     # [nn, F, NB, C]
+        nb = self.nbins_t.long()
+        binr = torch.arange(NB, device=self.dev)
+        inb = binr[None, :] < nb[:, None]                                                 # [F, NB]
+        cat_order = None
+        if d.is_cat.any():
+            # categorical bins ordered by the class-1 rate of (class 0 + class 1) (Entropy /
+            # Gini getCategoricalOrderList); bins past the category count sort last
+            den = H[..., 0] + H[..., 1]
+            key = torch.where(den != 0, H[..., 1] / torch.where(den != 0, den, torch.ones_like(den)),
+                              torch.zeros_like(den))
+            key = torch.where(inb[None], key, torch.full_like(key, float("inf")))
+            iscat = torch.from_numpy(d.is_cat.astype(bool)).to(self.dev)
+            key = torch.where(iscat[None, :, None], key, binr.double()[None, None, :].expand_as(key))
+            order = torch.argsort(key, dim=2, stable=True)                                # [nn, F, NB]
+            H = torch.gather(H, 2, order[..., None].expand(-1, -1, -1, C))
+            cat_order = order.to(torch.uint8).cpu().numpy()
+        L = torch.cumsum(H, 2)
+        T = L[:, :, -1:, :]
+        R = T - L
+        lw, rw, tw = L.sum(-1), R.sum(-1), T.sum(-1)
+
+        def impurity(X, s):
+            p = X / torch.where(s > 0, s, torch.ones_like(s))[..., None]
+            if cfg.impurity == "gini":
+                return -(p * p).sum(-1)
+            return -torch.where(p > 0, p * torch.log2(torch.where(p > 0, p, torch.ones_like(p))),
+                                torch.zeros_like(p)).sum(-1)
+        gain = impurity(T, tw) - torch.where(tw > 0, lw / tw, torch.zeros_like(lw)) * impurity(L, lw) \
+            - torch.where(tw > 0, rw / tw, torch.zeros_like(rw)) * impurity(R, rw)
+        ok = (binr[None, None, :] < (nb[None, :, None] - 1)) & (lw > cfg.min_instances_per_node) & \
+            (rw > cfg.min_instances_per_node) & (gain > cfg.min_info_gain)
+        if mask is not None:
+            ok &= mask.bool()[:, :, None]
+        g_m = torch.where(ok, gain, torch.full_like(gain, -float("inf")))
+        bbest = torch.argmax(g_m, dim=2)                                                  # first max bin
+        gbest = torch.gather(g_m, 2, bbest[..., None])[..., 0]                            # [nn, F]
+        fbest = torch.argmax(gbest, dim=1)                                                # lowest feature
+        ar = torch.arange(nn, device=self.dev)
+        b_sel = bbest[ar, fbest]
+        g_sel = gbest[ar, fbest]
+        Lc = L[ar, fbest, b_sel]                                                          # [nn, C]
+        Rc = R[ar, fbest, b_sel]
+        res = torch.stack([fbest.double(), b_sel.double(), g_sel, Lc.sum(-1), Lc[:, 1], Rc.sum(-1), Rc[:, 1],
+                           torch.isfinite(g_sel).double(), Lc.argmax(-1).double(), Rc.argmax(-1).double()], 1)
+        res = res.cpu().numpy()
+        best, class_lr = [], []
+        for i in range(nn):
+            f, b, gn, lws, l1, rws, r1, v, cl, cr = res[i]
+            best.append((int(f), int(b), float(gn) if v else 0.0, float(lws), float(l1), float(rws), float(r1),
+                         bool(v)))
+            class_lr.append((float(cl), float(cr)))
+        return {"hist": hists, "best": best, "cat_order": cat_order, "class_lr": class_lr}
 
     def _build_and_split_torch(self, nodes, n_built, g, w, pos2row, hist_prev, hist, mask, imp, min_inst,
                                min_gain):
@@ -809,15 +952,58 @@ class TreeTrainer:
                 self.apply_tree(tree, d, self.pred, 1.0, False)
                 if self.valid is not None:
                     self.apply_tree(tree, self.valid, self.vpred, 1.0, False)
-                k = tid + 1
-                terr = self._residual(self.pred / k, d, out)
-                verr = self._residual(self.vpred / k, self.valid, vout) if self.valid is not None else float("nan")
+                terr, verr = self._rf_errors(tree, tid)
             self.trees.append(tree)
             self.train_errors.append(terr)
             self.valid_errors.append(verr)
             if callback:
                 callback(tid, tree, terr, verr)
         return self.trees
+
+    def _row_error(self, p: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """Per-row ``Loss.computeError`` (J/core/dtrain/dt/Loss.java and subclasses)."""
+        loss = LOSS_IDS[self.cfg.loss]
+        p, y = p.double(), y.double()
+        if loss == 2:
+            return (y - p).abs()
+        if loss == 3:
+            return torch.log1p(1 + torch.exp(2 * p - 4 * p * y))
+        return (p - y) ** 2
+
+    def _rf_errors(self, tree: Tree, tid: int):
+        """RF errors as DTWorker.doCompute accumulates them (J/core/dtrain/dt/DTWorker.java:582-751):
+        every tree scores every row with its own leaf ``predict``; an in-bag row adds
+        bag-weight * significance * error to the training error, an out-of-bag row (bag weight 0)
+        adds significance * error to the validation error, as does every validation-set row.  The
+        sums are cumulative over the trees (the reference re-scores all trees each iteration)."""
+        d = self.data
+        self._reseed_rows(tid)                    # this tree's bag weights (same stream as its growth)
+        sub, _ = self._subsample()
+        p = torch.empty(d.n, dtype=torch.float32, device=self.dev)
+        self.apply_tree(tree, d, p, 1.0, True)
+        e = self._row_error(p, d.y)
+        sig = d.sig.double() if d.sig is not None else torch.ones(d.n, dtype=torch.float64, device=self.dev)
+        acc = torch.zeros(6, dtype=torch.float64, device=self.dev)
+        if sub is None:
+            acc[0], acc[1] = (sig * e).sum(), sig.sum()
+        else:
+            sb = sub.double()
+            inb = sb > 0
+            acc[0], acc[1] = (sb * sig * e)[inb].sum(), (sb * sig)[inb].sum()
+            acc[2], acc[3] = (sig * e)[~inb].sum(), sig[~inb].sum()
+        if self.valid is not None:
+            v = self.valid
+            pv = torch.empty(v.n, dtype=torch.float32, device=v.device)
+            self.apply_tree(tree, v, pv, 1.0, True)
+            sv = v.sig.double() if v.sig is not None else torch.ones(v.n, dtype=torch.float64, device=v.device)
+            acc[4], acc[5] = (sv * self._row_error(pv, v.y)).sum().to(self.dev), sv.sum().to(self.dev)
+        dist.all_reduce_(acc)
+        self._rf_acc = acc if getattr(self, "_rf_acc", None) is None else self._rf_acc + acc
+        a = self._rf_acc.cpu().numpy()
+        terr = float(a[0] / a[1]) if a[1] > 0 else float("nan")
+        verr = float((a[2] + a[4]) / (a[3] + a[5])) if (a[3] + a[5]) > 0 else float("nan")
+        self.oob_error = float(a[2] / a[3]) if a[3] > 0 else float("nan")
+        return terr, verr
 
     def _forest_batch(self, remaining: int) -> int:
         """Trees grown per RF batch: ``SHIFU_RF_BATCH`` (default 8), bounded by int32 positions
@@ -839,6 +1025,7 @@ class TreeTrainer:
             return {"max_depth": t.max_depth, "weight": t.weight, "feat": torch.from_numpy(t.feat),
                     "thr": torch.from_numpy(t.thr), "cat_left": torch.from_numpy(t.cat_left.view(np.int32)),
                     "value": torch.from_numpy(t.value), "wgt_cnt": torch.from_numpy(t.wgt_cnt),
+                    "class_value": torch.from_numpy(t.class_value), "classification": bool(t.classification),
                     "gain": torch.from_numpy(t.gain), "exists": torch.from_numpy(t.exists),
                     "features_used": list(map(int, t.features_used))}
         trees = [enc(t) for t in self.trees]
@@ -853,12 +1040,25 @@ class TreeTrainer:
             t.value, t.wgt_cnt = d["value"].numpy().copy(), d["wgt_cnt"].numpy().copy()
             t.gain, t.exists = d["gain"].numpy().copy(), d["exists"].numpy().copy()
             t.features_used = list(d["features_used"])
+            if "class_value" in d:
+                t.class_value = d["class_value"].numpy().copy()
+                t.classification = bool(d["classification"])
             return t
         self.trees = [dec(d) for d in st["trees"]]
         self._pending = [dec(d) for d in st.get("pending", [])]
         self.train_errors, self.valid_errors = list(st["train_errors"]), list(st["valid_errors"])
         self.rng.bit_generator.state = st["rng"]       # row streams: _reseed_rows(tree index)
         self._replay()
+
+    def predict_class(self, data: BinnedData) -> torch.Tensor:
+        """Multi-class RF: majority vote of the trees' class values (ties -> lowest class)."""
+        C = self.cfg.n_classes
+        votes = torch.zeros(data.n, C, dtype=torch.float32, device=data.device)
+        cv = torch.empty(data.n, dtype=torch.float32, device=data.device)
+        for t in self.trees:
+            _apply_classes(self, t, data, cv)
+            votes.scatter_add_(1, cv.round().long().clamp(0, C - 1)[:, None], torch.ones_like(cv)[:, None])
+        return votes.argmax(1).float()
 
     def continue_from(self, trees: list) -> None:
         """GBT continuous training (DTMaster.init :1081-1104): start from an existing model's trees
@@ -879,8 +1079,14 @@ class TreeTrainer:
                                                                    device=self.valid.device)
         if self.cfg.is_gbt and self.trees:
             self._residual(self.pred, self.data, self._out)
+        if not self.cfg.is_gbt:          # cumulative in-bag / out-of-bag error sums
+            self._rf_acc = None
+            for i, t in enumerate(self.trees):
+                self._rf_errors(t, i)
 
     def predict(self, data: BinnedData) -> torch.Tensor:
+        if self.cfg.is_multiclass:
+            return self.predict_class(data)
         p = torch.zeros(data.n, dtype=torch.float32, device=data.device)
         for i, t in enumerate(self.trees):
             if self.cfg.is_gbt:
@@ -890,6 +1096,18 @@ class TreeTrainer:
         if not self.cfg.is_gbt and self.trees:
             p /= len(self.trees)
         return p
+
+
+def _apply_classes(tr: "TreeTrainer", t: Tree, data: BinnedData, out: torch.Tensor) -> None:
+    """out = the tree's class value per row (classification leaves)."""
+    if data.device.type == "cuda":
+        from ..ops import _native as nat
+        feat, thr, cl, val = t.device_arrays(data.device, classes=True)
+        ic = torch.from_numpy(data.is_cat.astype(np.uint8)).to(data.device)
+        nat.call_hip("shifu_gbdt_apply_tree", data.bins, data.group_stride, None, feat, thr, cl, val, ic,
+                     out, 1.0, 1, None, data.n, t.max_nodes, nat.stream_of(out))
+    else:
+        out.copy_(torch.from_numpy(t.predict_bins(data.codes().numpy(), data.is_cat, classes=True)).float())
 
 
 def _slot_key(z):

@@ -154,7 +154,11 @@ class ModelRunner:
             elif m.kind == "lr":
                 outs.append(lrmod.lr_score(m.obj, self._normalized(table, cache))[:, None])
             elif m.kind == "tree":
-                outs.append(m.obj.score(table)[:, None])
+                tm = m.obj.model
+                if self.mc.is_multiclass() and tm.is_classification and not tm.is_one_vs_all:
+                    outs.append(m.obj.class_votes(table, len(self.mc.tags())))
+                else:
+                    outs.append(m.obj.score(table)[:, None])
             elif m.kind == "wdl":
                 outs.append(m.obj.score_table(self.mc, self.ccs, table)[:, None])
             elif m.kind == "generic":

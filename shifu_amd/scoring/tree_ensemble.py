@@ -159,6 +159,20 @@ class TreeScorer:
     def score(self, table) -> np.ndarray:
         return self.score_bags(self.input_matrix(table)).mean(1)
 
+    def class_votes(self, table, n_classes: int, chunk: int = 1 << 16) -> np.ndarray:
+        """Native multi-class forests (classification leaves carry a class value): per row the
+        fraction of trees voting for each class, averaged over bags -> [N, n_classes]
+        (``computeClassificationScore`` returns every tree's class; the caller votes)."""
+        X = self.input_matrix(table)
+        out = np.zeros((X.shape[0], n_classes))
+        for e in self.ens:
+            for i in range(0, X.shape[0], chunk):
+                lv = e.value[e.leaves(X[i: i + chunk])].round().long().clamp(0, n_classes - 1)
+                cnt = torch.zeros(lv.shape[0], n_classes, dtype=torch.float64, device=lv.device)
+                cnt.scatter_add_(1, lv, torch.ones_like(lv, dtype=torch.float64))
+                out[i: i + chunk] += (cnt / max(lv.shape[1], 1)).cpu().numpy()
+        return out / max(len(self.ens), 1)
+
     @torch.no_grad()
     def encode(self, table, depth: int | None = None) -> np.ndarray:
         """Leaf-path encoding (``IndependentTreeModel.encode`` J/core/dtrain/dt/IndependentTreeModel.java:272-350):

@@ -613,7 +613,8 @@ class TrainStep:
                          max_batch_split=int(_num(p.get("MaxBatchSplitSize"), 0)),
                          max_stats_memory_mb=int(_num(p.get("MaxStatsMemoryMB"), 0)),
                          valid_tolerance=float(_num(p.get("ValidationTolerance"), 0.0)),
-                         early_stop=str(p.get("EnableEarlyStop", "false")).lower() == "true")
+                         early_stop=str(p.get("EnableEarlyStop", "false")).lower() == "true",
+                         n_classes=len(mc.tags()) if (mc.is_multiclass() and not mc.is_one_vs_all()) else 0)
         tt = TreeTrainer(cfg, d, vd)
         es = EarlyStop(cfg.early_stop, int(os.environ.get("SHIFU_EARLYSTOP_WINDOW", 20)), cfg.valid_tolerance)
         stop = [False]

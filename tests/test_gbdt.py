@@ -229,3 +229,122 @@ def test_resume_reproduces_uninterrupted_sampled_run():
         assert np.array_equal(ta.feat, tc.feat) and np.array_equal(ta.thr, tc.thr)
         np.testing.assert_allclose(ta.value, tc.value, rtol=1e-6)
     np.testing.assert_allclose(a.pred.numpy(), c.pred.numpy(), rtol=1e-5, atol=1e-6)
+
+
+# ---- native multi-class RF (Entropy / Gini over C classes) + RF out-of-bag errors ------------------
+def _mc_data(n=900, f=5, nb=10, C=3, seed=0, device="cpu", cat_cols=(1,)):
+    rng = np.random.default_rng(seed)
+    codes = rng.integers(0, nb, size=(n, f))
+    y = np.where(codes[:, 0] < 3, 0, np.where(codes[:, 1] % 3 == 0, 1, 2)).astype(np.float32)
+    y = np.where(rng.random(n) < 0.1, rng.integers(0, C, n), y).astype(np.float32)
+    is_cat = np.zeros(f, np.uint8)
+    for c in cat_cols:
+        is_cat[c] = 1
+    return BinnedData.from_codes(codes, y, np.full(f, nb), is_cat, device=device), codes, y
+
+
+def _mc_imp(counts, imp):
+    s = counts.sum()
+    if s == 0:
+        return 0.0
+    p = counts / s
+    if imp == "gini":
+        return -float((p * p).sum())
+    p = p[p > 0]
+    return -float((p * np.log2(p)).sum())
+
+
+def _mc_bruteforce(codes, y, C, nb, is_cat, imp, min_inst):
+    """Impurity.java Entropy/Gini computeImpurity: categorical bins ordered by class-1 rate of
+    (class 0 + class 1), numeric bins in order; best = max gain, first feature / bin on ties."""
+    best = (-np.inf, None, None, None)
+    for f in range(codes.shape[1]):
+        st = np.zeros((nb, C))
+        np.add.at(st, (codes[:, f], y.astype(int)), 1.0)
+        order = list(range(nb))
+        if is_cat[f]:
+            den = st[:, 0] + st[:, 1]
+            key = np.where(den != 0, st[:, 1] / np.where(den != 0, den, 1), 0.0)
+            order = sorted(range(nb), key=lambda b: (key[b], b))
+        tot = st.sum(0)
+        base = _mc_imp(tot, imp)
+        left = np.zeros(C)
+        for i in range(nb - 1):
+            left = left + st[order[i]]
+            right = tot - left
+            lw, rw = left.sum(), right.sum()
+            if lw <= min_inst or rw <= min_inst:
+                continue
+            gain = base - lw / tot.sum() * _mc_imp(left, imp) - rw / tot.sum() * _mc_imp(right, imp)
+            if gain > best[0] + 1e-12:
+                best = (gain, f, i, (int(np.argmax(left)), int(np.argmax(right))))
+    return best
+
+
+@pytest.mark.parametrize("imp", ["entropy", "gini"])
+def test_multiclass_root_split_matches_reference_rule(imp):
+    data, codes, y = _mc_data()
+    cfg = TreeConfig("RF", tree_num=1, max_depth=2, impurity=imp, feature_subset_strategy="ALL",
+                     min_instances_per_node=5, n_classes=3)
+    tr = TreeTrainer(cfg, data)
+    t = tr.train(1)[0]
+    gain, f, i, (cl, cr) = _mc_bruteforce(codes, y, 3, 10, data.is_cat, imp, 5)
+    assert t.feat[1] == f
+    assert abs(t.gain[1] - gain) < 1e-5
+    assert (t.class_value[2], t.class_value[3]) == (cl, cr)
+    assert t.classification and t.class_value[1] == np.argmax(np.bincount(y.astype(int), minlength=3))
+
+
+def test_multiclass_rf_votes_learn_the_rule():
+    data, codes, y = _mc_data(n=3000, seed=1)
+    cfg = TreeConfig("RF", tree_num=6, max_depth=5, impurity="gini", feature_subset_strategy="ALL",
+                     bagging_sample_rate=0.8, n_classes=3, seed=3)
+    tr = TreeTrainer(cfg, data)
+    tr.train()
+    pred = tr.predict(data).numpy()
+    assert (pred == y).mean() > 0.85
+    assert set(np.unique(pred)) <= {0.0, 1.0, 2.0}
+
+
+def test_rf_oob_errors_match_manual_accumulation():
+    data, codes, y = _data(n=800, seed=4)
+    cfg = TreeConfig("RF", tree_num=4, max_depth=3, impurity="variance", feature_subset_strategy="ALL",
+                     bagging_sample_rate=0.6, sample_with_replacement=False, seed=2)
+    tr = TreeTrainer(cfg, data)
+    tr.train()
+    num_in = den_in = num_oob = den_oob = 0.0
+    for i, t in enumerate(tr.trees):
+        tr._reseed_rows(i)
+        sub, _ = tr._subsample()
+        sub = sub.numpy()
+        p = t.predict_bins(codes, data.is_cat).astype(np.float64)
+        e = (p - y) ** 2
+        num_in += (sub * e)[sub > 0].sum()
+        den_in += sub[sub > 0].sum()
+        num_oob += e[sub == 0].sum()
+        den_oob += (sub == 0).sum()
+    assert abs(tr.train_errors[-1] - num_in / den_in) < 1e-6
+    assert abs(tr.valid_errors[-1] - num_oob / den_oob) < 1e-6
+    assert abs(tr.oob_error - num_oob / den_oob) < 1e-6
+    # resume replays the same cumulative sums
+    st = tr.state_dict()
+    tr2 = TreeTrainer(cfg, data)
+    tr2.load_state_dict(st)
+    assert abs(tr2.oob_error - tr.oob_error) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("imp", ["entropy", "gini"])
+def test_multiclass_gpu_matches_cpu(imp):
+    """Per-class histograms from the HIP kernel + the vectorized gain scan == the CPU oracle."""
+    cfg = dict(algorithm="RF", tree_num=3, max_depth=4, impurity=imp, feature_subset_strategy="ALL",
+               bagging_sample_rate=1.0, n_classes=3, seed=5)   # bags are device-RNG streams
+    dc, codes, y = _mc_data(n=5000, seed=7)
+    dg = BinnedData.from_codes(codes, y, dc.nbins, dc.is_cat, device="cuda")
+    tc, tg = TreeTrainer(TreeConfig(**cfg), dc), TreeTrainer(TreeConfig(**cfg), dg)
+    tc.train()
+    tg.train()
+    for a, b in zip(tc.trees, tg.trees):
+        assert np.array_equal(a.feat, b.feat) and np.array_equal(a.thr, b.thr)
+        assert np.array_equal(a.class_value, b.class_value)
+    assert np.array_equal(tc.predict(dc).numpy(), tg.predict(dg).cpu().numpy())

@@ -323,3 +323,25 @@ def test_varsel_se_reuse_current_model(tmp_path, monkeypatch):
     from shifu_amd.config.column_config import load_column_configs
     sel = [c for c in load_column_configs(os.path.join(root, "ColumnConfig.json")) if c.final_select]
     assert len(sel) >= 3
+
+
+def test_multiclass_rf_native(tmp_path):
+    """RF with Gini over 3 classes (no one-vs-all): native multi-class trees (class-value leaves,
+    Impurity.java Gini), vote scoring in eval."""
+    from shifu_amd.formats import tree_format
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "mcrf", "RF", n_rows=2000, n_classes=3)
+    mc = _mc(root)
+    mc.train["multiClassifyMethod"] = "NATIVE"
+    mc.train["baggingNum"] = 1
+    mc.train["params"]["Impurity"] = "gini"
+    mc.train["params"]["TreeNum"] = 8
+    mc.train["params"]["MaxDepth"] = 6
+    mc.save()
+    _run(root, ["init", "stats", "norm", "train", "eval"])
+    m = tree_format.read_tree_model(os.path.join(root, "models", "model0.rf"))
+    assert m.is_classification and not m.is_one_vs_all
+    leaves = [nd for t in m.bags[0] for nd in tree_format.iter_nodes(t.root) if nd.is_leaf()]
+    assert {nd.class_value for nd in leaves} <= {0, 1, 2} and len({nd.class_value for nd in leaves}) > 1
+    perf = json.load(open(os.path.join(root, "evals/Eval1/EvalPerformance.json")))
+    assert perf["accuracy"] > 0.55
