@@ -191,22 +191,30 @@ class BinnedData:
         return self.bins.permute(1, 0, 2).reshape(n, g * FG)[:, : self.n_feat]
 
     @staticmethod
-    def blocked(codes: torch.Tensor, device="cpu") -> torch.Tensor:
-        """Row-major codes [N, F] (any int dtype, any device) -> blocked uint8 [G, N, 32] on
-        ``device``, one group at a time (no full-size intermediate)."""
+    def blocked(codes, device="cpu", rows=None) -> torch.Tensor:
+        """Row-major codes [N, F] (torch or numpy incl. a uint8 memmap, any int dtype) -> blocked
+        uint8 [G, N', 32] on ``device``, one 32-feature group at a time (optionally only ``rows``):
+        host memory stays at one group slice, never an int32 copy of the whole matrix."""
         n, f = codes.shape
+        if rows is not None:
+            n = len(rows)
         g = (f + FG - 1) // FG
         b = torch.zeros(g, n, FG, dtype=torch.uint8, device=device)
         for gi in range(g):
             c0, c1 = gi * FG, min(f, (gi + 1) * FG)
-            b[gi, :, : c1 - c0] = codes[:, c0:c1].to(device=device, dtype=torch.uint8)
+            blk = codes[:, c0:c1] if rows is None else codes[rows, c0:c1]
+            if isinstance(blk, np.ndarray):
+                blk = torch.from_numpy(np.ascontiguousarray(blk, dtype=np.uint8))
+            b[gi, :, : c1 - c0] = blk.to(device=device, dtype=torch.uint8)
         return b
 
     @staticmethod
-    def from_codes(codes, y, nbins, is_cat=None, sig=None, device="cpu"):
-        codes = torch.as_tensor(codes)
-        n, f = codes.shape
-        b = BinnedData.blocked(codes, device)
+    def from_codes(codes, y, nbins, is_cat=None, sig=None, device="cpu", rows=None):
+        if not isinstance(codes, np.ndarray):
+            codes = torch.as_tensor(codes)
+        f = codes.shape[1]
+        n = codes.shape[0] if rows is None else len(rows)
+        b = BinnedData.blocked(codes, device, rows)
         y = torch.as_tensor(y, dtype=torch.float32).reshape(n).to(device)
         s = None if sig is None else torch.as_tensor(sig, dtype=torch.float32).reshape(n).to(device)
         nb = np.asarray(nbins, dtype=np.int32).reshape(f)
