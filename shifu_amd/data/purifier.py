@@ -59,9 +59,22 @@ def tag_index(values_str: np.ndarray, set_tags: list) -> np.ndarray:
     return np.array([lut.get(str(v).strip(), -1) if v is not None else -1 for v in values_str], dtype=np.int32)
 
 
+def row_uniform(seed: int, row0: int, n: int) -> np.ndarray:
+    """Uniform [0, 1) draws for raw rows row0 .. row0 + n - 1: a counter-based generator
+    (splitmix64 of seed and the global row index), so a row's sampling decision is the same whether
+    the data set is read whole, in chunks, or split over ranks by byte range."""
+    with np.errstate(over="ignore"):
+        x = (np.arange(row0, row0 + n, dtype=np.uint64) + np.uint64((int(seed) * 0x9E3779B97F4A7C15) % (1 << 64)))
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    return (x >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+
 def purify(mc, table: RawTable, target: str, weight_expr: str | None = None, filter_expr: str | None = None,
            sample_rate: float = 1.0, sample_neg_only: bool = False, seed: int = 0,
-           require_target: bool = True) -> ModelData:
+           require_target: bool = True, row_offset: int = 0) -> ModelData:
     c = Counters(total=table.n)
     keep = np.ones(table.n, dtype=bool)
     if filter_expr and str(filter_expr).strip():
@@ -100,8 +113,7 @@ def purify(mc, table: RawTable, target: str, weight_expr: str | None = None, fil
         y = np.zeros(table.n)
     # sampling
     if sample_rate < 1.0:
-        rng = np.random.default_rng(seed)
-        r = rng.random(table.n)
+        r = row_uniform(seed, row_offset, table.n)
         if sample_neg_only and mc.is_binary():
             drop = (y == 0) & (r > sample_rate)
         else:
@@ -202,13 +214,14 @@ def plan_dataset(mc, data_conf, columns_num=None, columns_str=None, extra_filter
 
 
 def finish_table(mc, plan: DatasetPlan, table, sample_rate=1.0, sample_neg_only=False, seed=0,
-                 require_target=True) -> ModelData:
-    """Segment expansion + purification of a parsed table (whole data set or one chunk)."""
+                 require_target=True, row_offset: int = 0) -> ModelData:
+    """Segment expansion + purification of a parsed table (whole data set or one chunk whose first
+    raw row is global row ``row_offset``)."""
     if plan.seg_names:
         from . import segments
         segments.expand(table, plan.seg_names, plan.seg_exprs, set(plan.header))
     return purify(mc, table, plan.target, plan.weight, plan.filt, sample_rate, sample_neg_only, seed,
-                  require_target)
+                  require_target, row_offset)
 
 
 def load_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=1.0, sample_neg_only=False,

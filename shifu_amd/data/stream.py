@@ -13,8 +13,9 @@ range of the part files (``UpdateBinningInfoMapper`` J/core/binning/UpdateBinnin
   the native parser and yields a purified :class:`ModelData` chunk, so host memory is bounded by
   one block plus its parsed columns, whatever the data set size.
 
-Sampling (``stats.sampleRate``) draws from a generator seeded by (seed, file, block offset), so
-every pass over the stream sees the same rows.
+Sampling (``*.sampleRate``) is a counter-based draw per global raw row (``purifier.row_uniform``):
+a row's decision is the same whole, chunked or split over ranks (plain-text files; gz / parquet
+units dealt round-robin keep their rank-local row numbering).
 """
 from __future__ import annotations
 
@@ -65,7 +66,10 @@ def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int):
         fh.seek(pos)
         carry = b""
         while pos < end:
-            blk = fh.read(chunk_bytes)
+            # never read (much) past the range: the line straddling `end` is completed by the
+            # small follow-up reads of the carry logic
+            want = min(chunk_bytes, max(end - pos - len(carry), 0) + (1 << 16))
+            blk = fh.read(want)
             if not blk:
                 if carry:
                     yield pos, carry
@@ -85,26 +89,22 @@ def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int):
             pos += len(lines)
 
 
-def iter_tables(plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
-                nthreads: int | None = None):
-    """Yield (key, RawTable) row chunks of this rank's share of the data set, in file order."""
+def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kinds: list, nthreads: int):
+    """Yield ((file index, offset), parsed part) for this rank's share, in file order."""
     files = list_data_files(plan.data_path)
     if not files:
         raise FileNotFoundError(f"no data under {plan.data_path}")
-    kinds = column_kinds(plan.header, plan.nums, plan.strs)
-    nthreads = nthreads or min(16, os.cpu_count() or 4)
     for fi, path, a, b in byte_ranges(files, rank, world):
         if a is None:                              # indivisible unit
             if path.endswith(".parquet"):
-                part = _parse_parquet(path, plan.header, kinds, plan.missing)
-            else:
-                with gzip.open(path, "rb") as fh:
-                    data = fh.read()
-                if plan.skip_header_line and fi == 0:
-                    nl = data.find(b"\n")
-                    data = data[nl + 1:] if nl >= 0 else b""
-                part = parse_block(data, plan.delim, kinds, plan.missing, nthreads)
-            yield (fi, 0), table_from_parts(plan.header, kinds, [part], path)
+                yield (fi, 0), _parse_parquet(path, plan.header, kinds, plan.missing)
+                continue
+            with gzip.open(path, "rb") as fh:
+                data = fh.read()
+            if plan.skip_header_line and fi == 0:
+                nl = data.find(b"\n")
+                data = data[nl + 1:] if nl >= 0 else b""
+            yield (fi, 0), parse_block(data, plan.delim, kinds, plan.missing, nthreads)
             continue
         for off, data in _lines_in_range(path, a, b, chunk_bytes):
             if plan.skip_header_line and fi == 0 and off == 0:
@@ -112,18 +112,60 @@ def iter_tables(plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank:
                 data = data[nl + 1:] if nl >= 0 else b""
                 if not data:
                     continue
-            part = parse_block(data, plan.delim, kinds, plan.missing, nthreads)
-            yield (fi, off), table_from_parts(plan.header, kinds, [part], path)
+            yield (fi, off), parse_block(data, plan.delim, kinds, plan.missing, nthreads)
+
+
+def iter_tables(plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
+                nthreads: int | None = None):
+    """Yield (key, RawTable) row chunks of this rank's share of the data set, in file order."""
+    kinds = column_kinds(plan.header, plan.nums, plan.strs)
+    nthreads = nthreads or min(16, os.cpu_count() or 4)
+    for key, part in _iter_parts(plan, chunk_bytes, rank, world, kinds, nthreads):
+        yield key, table_from_parts(plan.header, kinds, [part], plan.data_path)
+
+
+def count_rows(plan: DatasetPlan, rank: int = 0, world: int = 1, chunk_bytes: int = DEFAULT_CHUNK_BYTES) -> int:
+    """Raw data rows in this rank's share (a parse with no columns selected: row framing only)."""
+    kinds = [0] * len(plan.header)
+    return int(sum(p[0] for _, p in _iter_parts(plan, chunk_bytes, rank, world, kinds, min(16, os.cpu_count() or 4))))
+
+
+def rank_row_offset(plan: DatasetPlan, rank: int, world: int) -> int:
+    """Global raw-row index of this rank's first row (row counts all-gathered over ranks)."""
+    if world <= 1:
+        return 0
+    import torch
+    from ..parallel import dist
+    counts = dist.all_gather_objects(count_rows(plan, rank, world))
+    return int(sum(counts[:rank]))
 
 
 def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
                     sample_rate: float = 1.0, sample_neg_only: bool = False, seed: int = 0,
-                    require_target: bool = True):
-    """Yield purified :class:`ModelData` chunks of this rank's byte range."""
-    for (fi, off), table in iter_tables(plan, chunk_bytes, rank, world):
-        md = finish_table(mc, plan, table, sample_rate, sample_neg_only, [seed, fi, off], require_target)
+                    require_target: bool = True, row0: int = 0):
+    """Yield purified :class:`ModelData` chunks of this rank's byte range; ``row0`` = the global
+    raw-row index of the rank's first row (sampling draws are per global row)."""
+    r = row0
+    for _, table in iter_tables(plan, chunk_bytes, rank, world):
+        n = table.n
+        md = finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, r)
+        r += n
         if md.n:
             yield md
+
+
+def load_rank_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=1.0, sample_neg_only=False,
+                      seed=0, require_target=True, extra_filter=None, rank: int = 0, world: int = 1):
+    """This rank's rows only (its byte ranges, parsed block by block into one table) -- the
+    data-parallel replacement of parse-everything-then-slice; equals the rank's contiguous slice
+    of ``load_dataset`` over the whole data set, sampling included."""
+    from .purifier import plan_dataset
+    plan = plan_dataset(mc, data_conf, columns_num, columns_str, extra_filter)
+    row0 = rank_row_offset(plan, rank, world) if (world > 1 and sample_rate < 1.0) else 0
+    kinds = column_kinds(plan.header, plan.nums, plan.strs)
+    parts = [p for _, p in _iter_parts(plan, DEFAULT_CHUNK_BYTES, rank, world, kinds, min(16, os.cpu_count() or 4))]
+    table = table_from_parts(plan.header, kinds, parts, plan.data_path)
+    return finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, row0)
 
 
 def data_bytes(plan: DatasetPlan) -> int:

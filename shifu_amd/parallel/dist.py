@@ -166,6 +166,25 @@ def all_gather_cat(t: torch.Tensor) -> torch.Tensor:
     return torch.cat([o[: int(s.item())] for o, s in zip(outs, sizes)])
 
 
+def gather_cat(t: torch.Tensor, dst: int = 0):
+    """Concatenate every rank's variable-length 1-D ``t`` on rank ``dst`` (rank order); None on
+    the others (a tensor gather - no pickling, and only ``dst`` holds the full array)."""
+    if not _active():
+        return t
+    n = torch.tensor([t.numel()], device=t.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(tdist.get_world_size())]
+    tdist.all_gather(sizes, n)
+    mx = int(max(s.item() for s in sizes))
+    pad = torch.zeros(mx, dtype=t.dtype, device=t.device)
+    pad[: t.numel()] = t.reshape(-1)
+    r = tdist.get_rank()
+    outs = [torch.zeros_like(pad) for _ in sizes] if r == dst else None
+    tdist.gather(pad, outs, dst=dst)
+    if r != dst:
+        return None
+    return torch.cat([o[: int(s.item())] for o, s in zip(outs, sizes)])
+
+
 def row_block(n: int, rank: int | None = None, world: int | None = None) -> tuple:
     """[a, b) of ``n`` rows owned by ``rank`` in a block partition (blocks differ by <= 1 row)."""
     i = info()

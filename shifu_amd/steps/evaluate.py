@@ -83,6 +83,12 @@ def _load_eval_data(ms, ev, runner_cols, extra_cols=()):
         else:
             strs.append(n)
     ds = ev.dataSet
+    from ..parallel import dist
+    info = dist.info()
+    if info.world_size > 1:          # this rank's byte range only (no parse-all-then-slice)
+        from ..data.stream import load_rank_dataset
+        return load_rank_dataset(ms.mc, ds, nums, strs, require_target=False, rank=info.rank,
+                                 world=info.world_size)
     return load_dataset(ms.mc, ds, nums, strs, require_target=False)
 
 
@@ -97,18 +103,16 @@ def score_eval(ms: ModelSet, ev, device=None, write: bool = True, nosort: bool =
     scale = float(ev.get("scoreScale", 1000) or 1000)
     from ..parallel import dist
     info = dist.info()
-    if info.world_size > 1:
-        # data parallel scoring: every rank scores its row range, rank 0 gathers (Eval.pig's
-        # distributed scoring + ORDER BY collapsed onto rank 0 for the sorted output / metrics)
-        from .base import shard_model_data
-        md = shard_model_data(md)
+    # data parallel: every rank parsed and scores only its byte range; the sorted EvalScore is a
+    # merge of the ranks' locally sorted parts (Eval.pig's ORDER BY), the metrics come from a
+    # tensor gather of (score, label, weight) only
     res = runner.score(md.table, scale)
     target = ev.dataSet.get("targetColumnName") or mc.dataSet.get("targetColumnName")
     tags = md.table[target].strings() if target in md.table else np.array([""] * md.n)
     if info.world_size > 1:
-        md, res, tags = _gather_scores(md, res, tags, list(meta_cols) + list(score_meta))
-        if info.rank != 0:
-            return md, res, tags, score_meta
+        if write:
+            _write_scores_dp(ms, ev, md, res, tags, list(meta_cols) + list(score_meta), nosort)
+        return _gather_eval_numeric(ms, ev, md, res, tags, score_meta) + (score_meta,)
     if write:
         d = ms.pf.eval_dir(ev.get("name"))
         os.makedirs(d, exist_ok=True)
@@ -147,6 +151,8 @@ class _GCol:
         return self.v
 
     def numeric(self):
+        if isinstance(self.v, np.ndarray) and self.v.dtype.kind == "f":
+            return self.v
         out = np.full(len(self.v), np.nan)
         for i, x in enumerate(self.v):
             try:
@@ -164,6 +170,108 @@ class _GTable(dict):
 class _GatheredEval:
     def __init__(self, n, w, cols):
         self.n, self.w, self.table = n, w, _GTable(cols)
+
+
+def _score_rows(md, res, tags, metas, order):
+    cols = [k for k in res if k not in ("class_scores", "pred_class")]
+    mats = [np.asarray(res[k]) for k in cols]
+    for i in order:
+        row = [str(tags[i]), repr(float(md.w[i]))]
+        row += [f"{float(m[i]):.6f}" if m.ndim == 1 else ",".join(f"{v:.6f}" for v in m[i]) for m in mats]
+        row += [str(m[i]) for m in metas]
+        yield "|".join(row)
+
+
+def _write_scores_dp(ms, ev, md, res, tags, meta_names, nosort):
+    """Every rank writes its rows sorted by score (full-precision key prefix) to a temp part; rank
+    0 k-way merges the parts into EvalScore (stable: equal scores keep rank = row order, exactly the
+    single-process stable sort) while streaming, then removes the parts."""
+    import heapq
+    from ..parallel import dist
+    mc = ms.mc
+    info = dist.info()
+    d = ms.pf.eval_dir(ev.get("name"))
+    os.makedirs(d, exist_ok=True)
+    path = ms.pf.eval_score(ev)
+    if os.path.isdir(path):
+        path = os.path.join(path, "part-00000")
+    metas = [md.table[m].strings() if m in md.table else np.array([""] * md.n) for m in meta_names]
+    sort = not (nosort or mc.is_multiclass())
+    key = None
+    order = range(md.n)
+    if sort:
+        sel = ev.get("performanceScoreSelector", "mean") or "mean"
+        key = np.asarray(res.get(sel, res.get("mean")), dtype=np.float64)
+        if key.ndim == 1 and len(key) == md.n:
+            order = np.argsort(-key, kind="stable")
+        else:
+            key = None
+    part = f"{path}.rank{info.rank:05d}"
+    with open(part, "w") as f:
+        for i, line in zip(order, _score_rows(md, res, tags, metas, order)):
+            f.write((f"{float(-key[i])!r}\t" if key is not None else "") + line + "\n")
+    dist.barrier()
+    if info.rank == 0:
+        cols = [k for k in res if k not in ("class_scores", "pred_class")]
+        hdr = ["tag", "weight"] + cols + list(meta_names)
+        parts = [f"{path}.rank{r:05d}" for r in range(info.world_size)]
+        fhs = [open(p_) for p_ in parts]
+        with open(path, "w") as out:
+            out.write("|".join(hdr) + "\n")
+            if key is not None:
+                merged = heapq.merge(*fhs, key=lambda l: float(l.split("\t", 1)[0]))
+                for l in merged:
+                    out.write(l.split("\t", 1)[1])
+            else:
+                for fh in fhs:
+                    for l in fh:
+                        out.write(l)
+        for fh, p_ in zip(fhs, parts):
+            fh.close()
+            os.remove(p_)
+        _log.info("eval %s: merged %d rank parts -> %s", ev.get("name"), info.world_size, path)
+    dist.barrier()
+
+
+def _gather_eval_numeric(ms, ev, md, res, tags, score_meta):
+    """(score or predicted class, label code, weight, score-meta columns) of every rank -> rank 0
+    as tensors (dist.gather_cat); rank 0 gets an eval view with synthetic tag strings carrying
+    the same labels, the others their own shard."""
+    import torch
+    from ..parallel import dist
+    mc = ms.mc
+    info = dist.info()
+    dev = torch.device("cuda", torch.cuda.current_device()) if info.backend == "nccl" else torch.device("cpu")
+    tg = np.asarray([str(t).strip() for t in tags])
+    if mc.is_multiclass():
+        lab = np.array([next((i for i, g in enumerate(mc.tags()) if t in g), -1) for t in tg], np.int64)
+        score = np.asarray(res["pred_class"], np.float64)
+    else:
+        pos = set(ev.dataSet.get("posTags") or mc.pos_tags)
+        neg = set(ev.dataSet.get("negTags") or mc.neg_tags)
+        lab = np.where(np.isin(tg, list(pos)), 1, np.where(np.isin(tg, list(neg)), 0, -1)).astype(np.int64)
+        sel = ev.get("performanceScoreSelector", "mean") or "mean"
+        score = np.asarray(res.get(sel, res["mean"]), np.float64)
+    arrays = {"score": score, "lab": lab, "w": np.asarray(md.w, np.float64)}
+    for m in score_meta:
+        arrays["meta:" + m] = md.table[m].numeric() if m in md.table else np.full(md.n, np.nan)
+    got = {k: dist.gather_cat(torch.as_tensor(np.ascontiguousarray(v)).to(dev)) for k, v in arrays.items()}
+    if info.rank != 0:
+        return md, res, tags
+    got = {k: v.cpu().numpy() for k, v in got.items()}
+    lab = got["lab"]
+    if mc.is_multiclass():
+        names = [str(g[0]) for g in mc.tags()]
+        tags = np.array([names[k] if k >= 0 else "" for k in lab], dtype=object)
+        res = {"pred_class": got["score"].astype(np.int64)}
+    else:
+        pos = list(ev.dataSet.get("posTags") or mc.pos_tags)
+        neg = list(ev.dataSet.get("negTags") or mc.neg_tags)
+        tags = np.where(lab == 1, str(pos[0]) if pos else "1", np.where(lab == 0, str(neg[0]) if neg else "0", ""))
+        sel = ev.get("performanceScoreSelector", "mean") or "mean"
+        res = {sel: got["score"], "mean": got["score"]}
+    cols = {m: got["meta:" + m] for m in score_meta}
+    return _GatheredEval(len(lab), got["w"], cols), res, tags
 
 
 def _gather_scores(md, res, tags, meta_names):

@@ -25,9 +25,10 @@ _log = get_logger("steps.norm")
 TREE_ALGS = ("GBT", "RF", "DT")
 
 
-def _write_shared(path: str, arrays: dict, meta: dict, lo: int, hi: int, n: int):
+def _write_shared(path: str, arrays: dict, meta: dict, lo: int, hi: int, n: int, positions=None):
     """Data-parallel cache write: rank 0 creates the full-size .npy files, every rank writes its
-    row range [lo, hi) in place (np.lib.format memmaps), rank 0 writes meta.json last."""
+    rows in place (np.lib.format memmaps) -- at [lo, hi), or at ``positions`` (shuffled output),
+    rank 0 writes meta.json last."""
     import json
     import os
     import shutil
@@ -42,7 +43,10 @@ def _write_shared(path: str, arrays: dict, meta: dict, lo: int, hi: int, n: int)
     dist.barrier()
     for k, v in arrays.items():
         mm = np.load(os.path.join(path, f"{k}.npy"), mmap_mode="r+")
-        mm[lo:hi] = v
+        if positions is None:
+            mm[lo:hi] = v
+        else:
+            mm[positions] = v
         mm.flush()
         del mm
     dist.barrier()
@@ -59,21 +63,39 @@ def _norm_one(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_o
     single-process ones."""
     from ..parallel import dist
     mc = ms.mc
-    md = ms.load_raw(cols, data_conf, sample_rate, neg_only, seed)
-    n = int(md.n)
-    perm = np.random.default_rng(seed).permutation(n) if shuffle else None
     info = dist.info()
-    lo, hi = n * info.rank // info.world_size, n * (info.rank + 1) // info.world_size
-    if info.world_size > 1 or perm is not None:
-        idx = perm[lo:hi] if perm is not None else np.arange(lo, hi)
-        from dataclasses import replace
-        md = replace(md, table=md.table.take(idx), y=md.y[idx], w=md.w[idx], tag_index=md.tag_index[idx])
+    positions = None
+    if info.world_size > 1:
+        # this rank's byte range only (data/stream.py); its rows are the contiguous global row
+        # range [lo, hi) of the single-process table (same per-row sampling draws)
+        from ..data.stream import load_rank_dataset
+        md = load_rank_dataset(mc, data_conf, [c.name for c in cols if not c.is_categorical()],
+                               [c.name for c in cols if c.is_categorical()], sample_rate, neg_only, seed,
+                               rank=info.rank, world=info.world_size)
+        counts = dist.all_gather_objects(int(md.n))
+        n = int(sum(counts))
+        lo = int(sum(counts[: info.rank]))
+        hi = lo + int(md.n)
+        if shuffle:                  # row g lands at inv[g] (output[i] = row perm[i])
+            perm = np.random.default_rng(seed).permutation(n)
+            inv = np.empty(n, np.int64)
+            inv[perm] = np.arange(n)
+            positions = inv[lo:hi]
+    else:
+        md = ms.load_raw(cols, data_conf, sample_rate, neg_only, seed)
+        n = int(md.n)
+        lo, hi = 0, n
+        if shuffle:
+            idx = np.random.default_rng(seed).permutation(n)
+            from dataclasses import replace
+            md = replace(md, table=md.table.take(idx), y=md.y[idx], w=md.w[idx], tag_index=md.tag_index[idx])
     y, w = md.y.astype(np.float32), md.w.astype(np.float32)
     meta = {"n": n, "columns": [c.name for c in cols], "column_nums": [c.num for c in cols],
             "counters": md.counters.as_dict(), "is_binary": mc.is_binary(), "tags": mc.flatten_tags(),
             "shuffled": bool(shuffle)}
     gpu = is_gpu_available()
-    save = (lambda p_, a_, m_: _write_shared(p_, a_, m_, lo, hi, n)) if info.world_size > 1 else save_dataset
+    save = (lambda p_, a_, m_: _write_shared(p_, a_, m_, lo, hi, n, positions)) if info.world_size > 1 \
+        else save_dataset
     if is_tree:
         r = N.tree_bin_codes_gpu(ms.ccs, md.table, cols) if gpu else None
         C, nb, is_cat = r if r is not None else N.tree_bin_codes(ms.ccs, md.table, cols)

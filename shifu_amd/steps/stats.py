@@ -116,8 +116,10 @@ def _stats_streamed(ms: ModelSet, cols, device=None) -> None:
     rate = float(mc.stats.get("sampleRate", 1.0))
     neg_only = bool(mc.stats.get("sampleNegOnly", False))
 
+    row0 = DS.rank_row_offset(plan, info.rank, info.world_size) if rate < 1.0 else 0
+
     def chunks():
-        return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only)
+        return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only, row0=row0)
     multi = info.world_size > 1
     if multi and device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if info.backend == "nccl" else "cpu"

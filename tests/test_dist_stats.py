@@ -354,3 +354,43 @@ def test_correlation_reuse_skips_data_pass(tmp_path, monkeypatch):
         environment.set_property("shifu.stats.corr.reuse", "false")
     n3, c3 = read_correlation(os.path.join(a, "correlation.csv"))
     assert n3 == n1 and abs(c3[0, 1] - 0.123456) < 1e-12
+
+
+def _rank_norm_rss(rank, world, port, root, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIFU_FORCE_CPU="1")
+    from shifu_amd.parallel import dist
+    from shifu_amd.steps.norm import run_norm
+    dist.init_from_env("gloo")
+
+    def status(key):
+        for line in open("/proc/self/status"):
+            if line.startswith(key):
+                return int(line.split()[1]) * 1024
+    open("/proc/self/clear_refs", "w").write("5")
+    base = status("VmRSS:")
+    run_norm(root)
+    with open(f"{out}.{rank}", "w") as f:
+        f.write(str(status("VmHWM:") - base))
+    dist.barrier()
+    dist.shutdown()
+
+
+def test_norm_per_rank_host_memory(tmp_path):
+    """Data-parallel norm parses only each rank's byte range: per-rank peak host memory growth is
+    about 1/R of the single-process growth plus a fixed ~65 MB of buffers (2 ranks: < 0.72x)."""
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "m", "NN", n_rows=320_000, n_num=30, n_cat=2)
+    run_init(root)
+    os.environ["SHIFU_FORCE_CPU"] = "1"
+    run_stats(root)
+    out = str(tmp_path / "rss")
+    mp.start_processes(_rank_norm_rss, args=(1, _port(), root, out + "1"), nprocs=1, join=True, start_method="spawn")
+    mp.start_processes(_rank_norm_rss, args=(2, _port(), root, out + "2"), nprocs=2, join=True, start_method="spawn")
+    single = int(open(out + "1.0").read())
+    ranks = [int(open(f"{out}2.{r}").read()) for r in range(2)]
+    print("norm rss growth MB: 1 rank %.1f, 2 ranks %s" % (single / 1e6, [round(r / 1e6, 1) for r in ranks]))
+    assert max(ranks) < 0.72 * single, (single, ranks)
