@@ -475,6 +475,14 @@ class MLPTrainer:
         # +2 tail slots: [error_sum, weight_sum] fused into the gradient all-reduce
         self.gbuf = torch.zeros(self.params.numel + 2, dtype=torch.float32, device=self.device)
         self.grad = self.gbuf[: self.params.numel]
+        # > 8 MB of gradients under data parallelism: RCCL all-reduce of finished layers' buckets
+        # overlaps the last chunk's remaining backward (back-to-front, parallel/dist.py)
+        self._reducer = None
+        self._final_chunk = False
+        gbytes = self.params.numel * 4
+        if dist.info().world_size > 1 and (gbytes > (8 << 20) or os.environ.get("SHIFU_GRAD_OVERLAP") == "1"):
+            mb = float(os.environ.get("SHIFU_GRAD_BUCKET_MB", "16"))
+            self._reducer = dist.BucketedAllReducer(self.grad, int(mb * (1 << 20)))
         fixed = None
         if fixed_bias:                  # FixedBias: bias weights of every layer stay frozen
             fixed = torch.zeros(self.params.numel, dtype=torch.bool)
@@ -594,17 +602,27 @@ class MLPTrainer:
         if self.gpu and isinstance(data.x, HostRows):
             wb, wt = self._weights_bf16()
             for r0, r1, xd in data.x.chunks(row_lo, row_hi, self.chunk_rows, self.spec.layer_kpad[0], self.device):
+                self._final_chunk = r1 >= row_hi
                 self._chunk_hip(data, r0, r1, wb, wt, x_dev=xd)
             return
         if self.gpu:
             wb, wt = self._weights_bf16()
             for r0 in range(row_lo, row_hi, self.chunk_rows):
                 r1 = min(row_hi, r0 + self.chunk_rows)
+                self._final_chunk = r1 >= row_hi
                 self._chunk_hip(data, r0, r1, wb, wt)
         else:
             for r0 in range(row_lo, row_hi, self.chunk_rows):
                 r1 = min(row_hi, r0 + self.chunk_rows)
+                self._final_chunk = r1 >= row_hi
                 self._chunk_torch(data, r0, r1)
+
+    def _grad_ready(self, layer: int) -> None:
+        """Layer ``layer``'s gradient is final (last chunk's wgrad enqueued): launch the buckets that
+        lie entirely at or after its offset (the process-group stream waits for the compute
+        stream, so the all-reduce starts when the wgrad kernel has finished)."""
+        if self._reducer is not None and self._final_chunk:
+            self._reducer.launch_from(self.params.offsets[layer])
 
     def _tail_supported(self) -> bool:
         """Shapes the fused tail kernel (ops/csrc/mlp_tail.hip) covers: last hidden layer padded
@@ -697,6 +715,7 @@ class MLPTrainer:
                          None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act],
                          ACT_IDS[sp.acts[L - 1]] if L else 2, LOSS_IDS[sp.loss], flat_spot(sp.out_act),
                          flat_spot(sp.acts[L - 1]) if L else 0.0, st)
+        self._grad_ready(L)
         splits = self.wgrad_splits
         for l in range(L - 1, -1, -1):
             # wgrad of layer l: G_l[h_l, K_l] += D_{l+1}^T A_l
@@ -714,6 +733,7 @@ class MLPTrainer:
             else:
                 nat.call_hip("shifu_wgrad_tn", dels[l + 1].data_ptr(), kp[l + 1], acts[l].data_ptr(), kp[l],
                              gv[l].data_ptr(), kp[l], mc, sp.hidden[l], kp[l], spl, st)
+            self._grad_ready(l)
             if l >= 1 and not (fused and l == L - 1):
                 # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)   (layer 1: written transposed)
                 act = ACT_IDS[sp.acts[l - 1]]
@@ -761,12 +781,14 @@ class MLPTrainer:
         self.err_acc[0] += float(err)
         self.err_acc[1] += float(s.sum())
         gv[L].add_(dl.t() @ acts[L])
+        self._grad_ready(L)
         d = dl
         for l in range(L - 1, -1, -1):
             # delta of hidden layer l+1 (acts[l+1]) from the layer above
             back = d @ wv[l + 1][:, : sp.hidden[l]]
             dh = back * (act_deriv(sp.acts[l], zs[l + 1], acts[l + 1][:, : sp.hidden[l]]) + flat_spot(sp.acts[l]))
             gv[l].add_(dh.t() @ acts[l])
+            self._grad_ready(l)
             d = dh
 
     # --------------------------------------------------------------------------------------
@@ -794,7 +816,13 @@ class MLPTrainer:
             self._wflat = self.params.flat
         self.accumulate_gradients(data, row_lo, row_hi)
         self.gbuf[-2:] = self.err_acc.to(torch.float32)
-        dist.all_reduce_(self.gbuf)
+        if self._reducer is not None:
+            self._reducer.wait()                        # launches any bucket not yet in flight
+            tail = self.gbuf[-2:].clone()
+            dist.all_reduce_(tail)
+            self.gbuf[-2:] = tail
+        else:
+            dist.all_reduce_(self.gbuf)
         if self.dropout_rate > 0:
             self.grad.mul_(self._scale)                 # d(loss)/dW of the scaled connections
         self._wflat = self.params.flat

@@ -118,3 +118,36 @@ def _bucket_run(rank, world, port, out):
     if rank == 0:
         torch.save({"a": flat[:1000].clone(), "b": flat[1000:].view(7, 5).clone()}, out)
     dist.shutdown()
+
+
+def _mlp_overlap_run(rank, world, port, out, overlap):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIFU_FORCE_CPU="1")
+    if overlap:
+        os.environ["SHIFU_GRAD_OVERLAP"] = "1"
+        os.environ["SHIFU_GRAD_BUCKET_MB"] = "0.0002"        # ~200 B buckets: many per layer
+    from shifu_amd.models.nn import MLPSpec, MLPTrainer
+    from shifu_amd.parallel import dist
+    dist.init_from_env("gloo")
+    x, y = _data()
+    n = len(y)
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    tr = MLPTrainer(MLPSpec(x.shape[1], [16, 8], ["tanh", "sigmoid"], 1, "sigmoid"), "cpu", "R", 0.1, seed=3,
+                    chunk_rows=64)
+    assert (tr._reducer is not None) == bool(overlap)
+    d = tr.prepare(torch.from_numpy(x[lo:hi]), y[lo:hi].reshape(-1, 1))
+    errs = [tr.step(d, num_train_global=float(n)) for _ in range(4)]
+    if rank == 0:
+        torch.save({"w": tr.params.flat.clone(), "errs": errs}, out)
+    dist.shutdown()
+
+
+def test_mlp_bucketed_overlap_equals_single_allreduce(tmp_path):
+    """Buckets launched back-to-front during the last chunk's backward (BucketedAllReducer) give
+    bitwise the same training as one all-reduce after the backward."""
+    a, b = str(tmp_path / "o0.pt"), str(tmp_path / "o1.pt")
+    _spawn(_mlp_overlap_run, 2, a, False)
+    _spawn(_mlp_overlap_run, 2, b, True)
+    r1, r2 = torch.load(a, weights_only=True), torch.load(b, weights_only=True)
+    assert r1["errs"] == r2["errs"]
+    assert torch.equal(r1["w"], r2["w"])
