@@ -131,6 +131,23 @@ def bench_gbdt(a, dev, info):
     return bench_rounds(a, dev, info)
 
 
+class _Cycle:
+    """Rows [0, n) served from a host buffer of fewer rows (row r -> buffer row r mod len):
+    chunk slices never straddle the wrap (chunk size divides the buffer)."""
+
+    def __init__(self, buf, n):
+        self.buf, self.n = buf, n
+        self.shape = (n, buf.shape[1])
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, sl):
+        m = len(self.buf)
+        a = sl.start % m
+        return self.buf[a: a + (sl.stop - sl.start)]
+
+
 def bench_varsel(a, dev, info):
     """BASELINE config 5: 10k-feature MLP + sensitivity-analysis variable selection.  Each rank
     holds ``--rows`` rows x 10000 features (bf16, HBM-resident: 2M rows = 40 GB), trains the
@@ -140,24 +157,43 @@ def bench_varsel(a, dev, info):
     (epochs x rows + one SE pass x rows, all ranks)."""
     from shifu_amd.algos.varsel import sensitivity
     from shifu_amd.formats.nn_format import NNNetwork
-    from shifu_amd.models.nn import MLPSpec, MLPTrainer, TrainData
+    from shifu_amd.models.nn import HostRows, MLPSpec, MLPTrainer, TrainData
     from shifu_amd.parallel import dist
     n_in = a.cols
     spec = MLPSpec(n_in=n_in, hidden=[500], acts=["sigmoid"], n_out=1)
     tr = MLPTrainer(spec, device=dev, propagation="R", learning_rate=0.1, seed=7, chunk_rows=a.chunk_rows)
-    x, y = make_synthetic(a.rows, n_in, spec.layer_kpad[0], dev, 4321 + info.rank)
+    if a.stream:
+        # out-of-core: rows live in host memory and stream to HBM chunk by chunk (pinned staging,
+        # H2D on a copy stream overlapping the GEMMs / SE kernels).  The 288 GB-HBM box's host cap
+        # (270 GiB) cannot hold 20M x 10k bf16 (400 GB), so --rows are served from a host buffer of
+        # --host-rows rows cycled: every chunk is a real H2D copy, the row values repeat.
+        hb = min(a.rows, a.host_rows)
+        xd, yd = make_synthetic(hb, n_in, spec.layer_kpad[0], dev, 4321 + info.rank)
+        xh = xd[:, :n_in].cpu()
+        del xd
+        torch.cuda.empty_cache()
+        reps = -(-a.rows // hb)
+        x = HostRows(_Cycle(xh, a.rows), n_in)
+        y = yd.repeat(reps, 1)[: a.rows].contiguous()
+        if a.chunk_rows > hb or hb % a.chunk_rows:
+            raise SystemExit("--host-rows must be a multiple of --chunk-rows")
+    else:
+        x, y = make_synthetic(a.rows, n_in, spec.layer_kpad[0], dev, 4321 + info.rank)
     data = TrainData(x, y, None, a.rows)
     n_global = float(a.rows * info.world_size)
-    for _ in range(a.warmup):
+    log(f"[bench] varsel data ready ({'streamed from host' if a.stream else 'HBM-resident'})")
+    for i in range(a.warmup):
         tr.step(data, num_train_global=n_global)
+        log(f"[bench] varsel warmup epoch {i}")
 
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize()
     dist.barrier(); sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         tr.step(data, num_train_global=n_global)
+        log(f"[bench] varsel epoch {i}")
     sync(); dist.barrier()
     t_train = time.perf_counter() - t0
     ws = tr.params.views()
@@ -165,7 +201,8 @@ def bench_varsel(a, dev, info):
                     [ws[l][:, : spec.layer_in[l] + 1].detach().double().cpu().numpy() for l in range(len(ws))])
     dist.barrier(); sync()
     t1 = time.perf_counter()
-    mean, rms, _ = sensitivity(net, x[:, :n_in], device=dev, row_chunk=1 << 12)
+    mean, rms, _ = sensitivity(net, x if a.stream else x[:, :n_in], device=dev,
+                               row_chunk=(a.chunk_rows // 16) if a.stream else 1 << 12)
     stats = torch.tensor(np.concatenate([mean, rms ** 2]) * a.rows, dtype=torch.float64, device=dev)
     dist.all_reduce_(stats)
     sync(); dist.barrier()
@@ -182,7 +219,9 @@ def bench_varsel(a, dev, info):
         "ms_per_step": (t_train + t_se) / (a.steps + 1) * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) features, hidden linear rule), random-init weights",
         "config": {"model": f"MLP {n_in}-500-1 + SE sensitivity varselect", "global_batch": rows_total,
-                   "seq_len": None, "n_cols": n_in, "rows_per_gpu": a.rows, "parallelism": f"dp{info.world_size}"},
+                   "seq_len": None, "n_cols": n_in, "rows_per_gpu": a.rows, "parallelism": f"dp{info.world_size}",
+                   "streamed_from_host": bool(a.stream),
+                   "host_buffer_rows": min(a.rows, a.host_rows) if a.stream else None},
         "train_ms_per_epoch": t_train / max(1, a.steps) * 1e3, "se_pass_ms": t_se * 1e3,
         "se_input_pairs_per_s": rows_total * n_in / t_se, "top5_inputs_by_rms": np.argsort(-rms_all)[:5].tolist(),
     }
@@ -337,6 +376,8 @@ def main():
                     help="rows per GPU of the GBDT half of the default line (default 100M on GPU)")
     ap.add_argument("--gbdt-steps", type=int, default=5, help="timed boosting rounds (0 = MLP only)")
     ap.add_argument("--gbdt-warmup", type=int, default=1)
+    ap.add_argument("--stream", action="store_true", help="varsel: rows streamed from host memory (HostRows)")
+    ap.add_argument("--host-rows", type=int, default=2_000_000, help="varsel --stream: host buffer rows")
     a = ap.parse_args()
 
     from shifu_amd.parallel import dist

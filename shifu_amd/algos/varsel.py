@@ -184,57 +184,111 @@ def auto_filter(mc, ccs, corr: np.ndarray | None = None, corr_nums=None):
 
 
 @torch.no_grad()
-def sensitivity(network, X: np.ndarray, y=None, w=None, device=None, feat_chunk: int = 64,
-                row_chunk: int = 1 << 16):
+def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, row_chunk: int = 1 << 16,
+                deep_rows: int = 2048):
     """SE sensitivity over inputs of a trained MLP (NNNetwork, input-first weights).
 
-    Returns (mean |d|, rms, variance) per input, accumulated over rows.  The first layer
-    pre-activation S = X W1^T + b is computed once per row chunk; the perturbed pre-activations
-    for a chunk of features are S[:,None,:] - X[:,f,None] * W1[None,f,:] (rank-1 corrections),
-    then the rest of the network runs batched over (rows x features)."""
-    from ..models.nn import act_fwd
-    dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+    ``VarSelectMapper.map`` (J/core/varselect/VarSelectMapper.java:277-333) with
+    ``CacheFlatNetwork`` (J/core/dtrain/nn/CacheFlatNetwork.java:117-180): the first-layer
+    pre-activation S = X W1^T + b is computed once per row, an input's removal is the rank-1
+    correction S - x_f W1[:, f], and only the layers above are re-evaluated.  Returns
+    (mean |d|, rms, variance) per input, accumulated over rows.
+
+    ``X``: device tensor, host array, or :class:`models.nn.HostRows` (rows streamed to HBM on a
+    copy stream that overlaps the SE kernels).  GPU paths:
+    * 1 hidden layer (K14, ``sensitivity_kernel``): correction + activation + output neuron
+      fused, register-blocked (the v_exp/v_rcp issue rate bounds it -- see profiles/);
+    * deeper nets (K14b): ``se_perturb_kernel`` writes the perturbed first hidden layer of every
+      (row, input) pair as bf16 MLP rows, the remaining layers run as bf16 MFMA GEMMs
+      (hipBLASLt, fp32 accumulation) over R x feat_chunk pair rows at a time.
+    CPU: the fp32 torch oracle of the same decomposition."""
+    from ..models.nn import ACT_IDS, HostRows, act_fwd
+    dev = torch.device(device) if device is not None else \
+        (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
     Ws = [torch.as_tensor(W, dtype=torch.float32, device=dev) for W in network.weights]
     acts = network.acts
-    F = X.shape[1]
+    n_rows, F = (len(X), X.shape[1]) if not isinstance(X, HostRows) else X.shape
     s_abs = torch.zeros(F, dtype=torch.float64, device=dev)
     s_sq = torch.zeros(F, dtype=torch.float64, device=dev)
     n = 0
+    W1 = Ws[0][:, :-1]          # [H1, F]
+    b1 = Ws[0][:, -1]
+
+    def row_chunks(rc):
+        """device fp32 [m, F] row blocks (HostRows: pinned staging + H2D on a copy stream)."""
+        if isinstance(X, HostRows):
+            k0 = ((F + 1 + 127) // 128) * 128
+            for _, _, xd in X.chunks(0, n_rows, rc, k0, dev):
+                yield xd[:, :F].float()
+            return
+        for r0 in range(0, n_rows, rc):
+            xb = X[r0: r0 + rc]
+            yield (xb if torch.is_tensor(xb) else torch.as_tensor(np.asarray(xb), dtype=torch.float32)).to(
+                dev, dtype=torch.float32).contiguous()
 
     def tail(z1):
         a = act_fwd(acts[0], z1)
         for l in range(1, len(Ws)):
             a = act_fwd(acts[l], a @ Ws[l][:, :-1].t() + Ws[l][:, -1])
         return a[..., 0]
-    W1 = Ws[0][:, :-1]          # [H1, F]
-    b1 = Ws[0][:, -1]
+
     if dev.type == "cuda" and len(Ws) == 2 and Ws[1].shape[0] == 1 and W1.shape[0] <= 1024:
-        # HIP kernel (K14): S cached per row, rank-1 correction + activation + output neuron fused
-        from ..models.nn import ACT_IDS
+        # K14: S cached per row, rank-1 correction + activation + output neuron fused
         from ..ops import stats_ops
         acc = torch.zeros(F, 2, dtype=torch.float64, device=dev)
         W1t = W1.t().contiguous()
         W2 = Ws[1][0, :-1].contiguous()
         b2 = float(Ws[1][0, -1])
-        for r0 in range(0, X.shape[0], row_chunk * 16):
-            xb = torch.as_tensor(X[r0: r0 + row_chunk * 16], dtype=torch.float32, device=dev).contiguous()
+        for xb in row_chunks(row_chunk * 16):
             S = (xb @ W1.t() + b1).contiguous()
             base = act_fwd(acts[1], act_fwd(acts[0], S) @ W2 + b2).contiguous()
             stats_ops.sensitivity_1h(S, xb, W1t, W2, b2, base, ACT_IDS[acts[0]], ACT_IDS[acts[1]], acc)
             n += xb.shape[0]
         s_abs, s_sq = acc[:, 0], acc[:, 1]
-        row_chunk = X.shape[0] + 1     # skip the generic path
-    for r0 in (range(0, X.shape[0], row_chunk) if n == 0 else ()):
-        xb = torch.as_tensor(X[r0: r0 + row_chunk], dtype=torch.float32, device=dev)
-        S = xb @ W1.t() + b1                     # cached first layer [R, H1]
-        base = tail(S)                           # [R]
-        for f0 in range(0, F, feat_chunk):
-            f1 = min(F, f0 + feat_chunk)
-            Z = S[:, None, :] - xb[:, f0:f1, None] * W1.t()[None, f0:f1, :]   # [R, fc, H1]
-            d = (base[:, None] - tail(Z)).double()
-            s_abs[f0:f1] += d.abs().sum(0)
-            s_sq[f0:f1] += (d * d).sum(0)
-        n += xb.shape[0]
+    elif dev.type == "cuda" and Ws[-1].shape[0] == 1:
+        # K14b: perturbed first layer as bf16 rows -> MFMA GEMM tail
+        from ..ops import stats_ops
+        H1 = W1.shape[0]
+        hpad = ((H1 + 1 + 7) // 8) * 8
+        W1t = W1.t().contiguous()
+        Wb = [W.to(torch.bfloat16) for W in Ws]
+
+        def tail_bf16(A):                         # A [M, hpad] bf16 rows with bias column
+            k = H1 + 1
+            for l in range(1, len(Ws)):
+                z = (A[:, :k] @ Wb[l].t()).float()
+                a = act_fwd(acts[l], z)
+                if l == len(Ws) - 1:
+                    return a[:, 0]
+                k = a.shape[1] + 1
+                A = torch.cat([a, torch.ones(a.shape[0], 1, device=a.device)], 1).to(torch.bfloat16)
+            return A[:, 0].float()
+        act1 = ACT_IDS[acts[0]]
+        for xb in row_chunks(deep_rows):
+            R = xb.shape[0]
+            S = (xb @ W1.t() + b1).contiguous()
+            # unperturbed rows through the same kernel (x_f = 0 correction): base and perturbed
+            # activations share rounding, so an input with x_f = 0 gives d = 0 exactly
+            base = tail_bf16(stats_ops.se_perturb(S, torch.zeros(R, 1, device=dev), W1t[:1], 0, 1, act1, hpad))
+            buf = torch.empty(R * feat_chunk, hpad, dtype=torch.bfloat16, device=dev)
+            for f0 in range(0, F, feat_chunk):
+                fc = min(feat_chunk, F - f0)
+                P = stats_ops.se_perturb(S, xb, W1t, f0, fc, act1, hpad, buf[: R * fc])
+                d = (base[:, None] - tail_bf16(P).view(R, fc)).double()
+                s_abs[f0:f0 + fc] += d.abs().sum(0)
+                s_sq[f0:f0 + fc] += (d * d).sum(0)
+            n += R
+    else:
+        for xb in row_chunks(row_chunk):
+            S = xb @ W1.t() + b1                     # cached first layer [R, H1]
+            base = tail(S)                           # [R]
+            for f0 in range(0, F, feat_chunk):
+                f1 = min(F, f0 + feat_chunk)
+                Z = S[:, None, :] - xb[:, f0:f1, None] * W1.t()[None, f0:f1, :]   # [R, fc, H1]
+                d = (base[:, None] - tail(Z)).double()
+                s_abs[f0:f1] += d.abs().sum(0)
+                s_sq[f0:f1] += (d * d).sum(0)
+            n += xb.shape[0]
     from ..parallel import dist
     if dist.info().world_size > 1:        # row-sharded SE: one all-reduce of the per-input sums
         t = torch.cat([s_abs, s_sq, torch.tensor([float(n)], dtype=torch.float64, device=s_abs.device)])

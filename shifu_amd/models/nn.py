@@ -236,13 +236,19 @@ class HostRows:
     def __len__(self):
         return self.shape[0]
 
+    def _bf16_source(self) -> bool:
+        x = self.x
+        probe = x.buf if hasattr(x, "buf") else x
+        return torch.is_tensor(probe) and probe.dtype == torch.bfloat16
+
     def _alloc(self, rows, k0, device):
         if self._bufs is not None and self._bufs["rows"] >= rows and self._bufs["k0"] == k0:
             return self._bufs
         f = self.n_in
+        dt = torch.bfloat16 if self._bf16_source() else torch.float32   # bf16 rows travel as bf16
         b = {"rows": rows, "k0": k0, "stream": torch.cuda.Stream(device),
-             "pin": [torch.empty(rows, f, dtype=torch.float32).pin_memory() for _ in range(2)],
-             "raw": [torch.empty(rows, f, dtype=torch.float32, device=device) for _ in range(2)],
+             "pin": [torch.empty(rows, f, dtype=dt).pin_memory() for _ in range(2)],
+             "raw": [torch.empty(rows, f, dtype=dt, device=device) for _ in range(2)],
              "dev": [torch.zeros(rows, k0, dtype=torch.bfloat16, device=device) for _ in range(2)],
              "copied": [torch.cuda.Event() for _ in range(2)], "used": [torch.cuda.Event() for _ in range(2)]}
         for d in b["dev"]:
@@ -260,8 +266,9 @@ class HostRows:
             m, k = r1 - r0, i % 2
             b["copied"][k].synchronize() if i >= 2 else None      # pinned buffer k free again
             src = self.x[r0:r1]
-            b["pin"][k][:m].copy_(torch.as_tensor(np.asarray(src, dtype=np.float32)) if not torch.is_tensor(src)
-                                  else src.float())
+            pin = b["pin"][k][:m]
+            pin.copy_(torch.as_tensor(np.asarray(src, dtype=np.float32)) if not torch.is_tensor(src)
+                      else src.to(pin.dtype))
             with torch.cuda.stream(cs):
                 if i >= 2:
                     cs.wait_event(b["used"][k])                   # GEMMs of chunk i-2 done with buffer k
@@ -269,7 +276,10 @@ class HostRows:
                 b["copied"][k].record(cs)
             main.wait_event(b["copied"][k])
             dev = b["dev"][k][:m]
-            nat.call_hip("shifu_cast_bf16", b["raw"][k], self.n_in, dev, k0, m, self.n_in, nat.stream_of(dev))
+            if b["raw"][k].dtype == torch.bfloat16:
+                dev[:, : self.n_in].copy_(b["raw"][k][:m])
+            else:
+                nat.call_hip("shifu_cast_bf16", b["raw"][k], self.n_in, dev, k0, m, self.n_in, nat.stream_of(dev))
             yield r0, r1, dev
             b["used"][k].record(main)
 

@@ -65,6 +65,7 @@ HIP_SIGNATURES = {
     "shifu_bin_codes": "plli" "pp" "pl" "s",
     "shifu_lr_grad": "plli" "i" "ppp" "pp" "i" "s",
     "shifu_sensitivity": "plpl" "pp" "f" "p" "l" "iiiii" "p" "s",
+    "shifu_se_perturb": "plpl" "p" "ii" "iiii" "pl" "s",
     # quantile_kernels.hip
     "shifu_pack_bits": "plip" "s",
     "shifu_qprep": "pllipid" "pppp" "s",

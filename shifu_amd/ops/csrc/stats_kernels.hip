@@ -549,6 +549,45 @@ SHIFU_API int shifu_lr_grad(const void* x, long ldx, long n, int F, int dtype, c
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// K14b: SE for deeper nets -- the perturbed first hidden layer of (row, input) pairs, written as
+// bf16 MLP rows [R * fc][Hpad] (bias column H = 1, padding 0) so the remaining layers run as
+// MFMA GEMMs: out[(r*fc + f)][j] = act(S[r][j] - x[r][f0+f] * W1[j][f0+f]).  One thread per 2
+// hidden units (packed bf16x2 store); rows of the pair matrix are independent.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) se_perturb_kernel(const float* __restrict__ S, long lds,
+                                                         const float* __restrict__ X, long ldx,
+                                                         const float* __restrict__ W1t, int f0, int fc, int H,
+                                                         int Hpad, int act, uint32_t* __restrict__ out, long R) {
+  const long pair = (long)blockIdx.x;              // r * fc + f
+  const long r = pair / fc;
+  const int f = (int)(pair - r * fc);
+  if (r >= R) return;
+  const float xv = X[r * ldx + f0 + f];
+  const float* srow = S + r * lds;
+  const float* wrow = W1t + (long)(f0 + f) * H;
+  uint32_t* orow = out + pair * (Hpad / 2);
+  for (int j2 = threadIdx.x; j2 < Hpad / 2; j2 += blockDim.x) {
+    float v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = 2 * j2 + u;
+      v[u] = j < H ? act_fwd(act, srow[j] - xv * wrow[j]) : (j == H ? 1.f : 0.f);
+    }
+    orow[j2] = pack_bf16x2(v[0], v[1]);
+  }
+}
+
+SHIFU_API int shifu_se_perturb(const float* S, long lds, const float* X, long ldx, const float* W1t, int f0, int fc,
+                               int F, int H, int Hpad, int act, void* out, long R, hipStream_t stream) {
+  if (R <= 0 || fc <= 0) return 0;
+  if (Hpad % 2 || Hpad < H + 1 || f0 < 0 || f0 + fc > F || lds < H || ldx < F) return -1;
+  hipLaunchKernelGGL(se_perturb_kernel, dim3((unsigned)(R * fc)), dim3(256), 0, stream, S, lds, X, ldx, W1t, f0, fc,
+                     H, Hpad, act, (uint32_t*)out, R);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 SHIFU_API int shifu_sensitivity(const float* S, long lds, const float* X, long ldx, const float* W1t, const float* W2,
                                 float b2, const float* base, long n, int F, int H, int act1, int act_o, int nchunks,
                                 double* acc, hipStream_t stream) {

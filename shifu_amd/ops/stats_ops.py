@@ -151,6 +151,20 @@ def lr_grad(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, s: torch.Tensor |
     return part.sum(0), ep.sum()
 
 
+def se_perturb(S: torch.Tensor, X: torch.Tensor, W1t: torch.Tensor, f0: int, fc: int, act: int, hpad: int,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """Perturbed first hidden layer of every (row, input in [f0, f0+fc)) pair as bf16 MLP rows
+    [R*fc, hpad] (bias column = 1) for the MFMA tail of deep-net SE (K14b)."""
+    nat.require_gpu_native()
+    R, H = S.shape
+    F = X.shape[1]
+    if out is None:
+        out = torch.empty(R * fc, hpad, dtype=torch.bfloat16, device=S.device)
+    nat.call_hip("shifu_se_perturb", S, S.stride(0), X, X.stride(0), W1t, int(f0), int(fc), F, H, int(hpad),
+                 int(act), out, R, nat.stream_of(S))
+    return out
+
+
 def sensitivity_1h(S: torch.Tensor, X: torch.Tensor, W1t: torch.Tensor, W2: torch.Tensor, b2: float,
                    base: torch.Tensor, act1: int, act_o: int, acc: torch.Tensor, nchunks: int | None = None):
     """Accumulate sum|d| and sum d^2 per input into ``acc`` [F, 2] fp64 (1-hidden-layer nets)."""

@@ -113,3 +113,41 @@ def test_sensitivity_kernel_matches_torch(act):
     m2, r2, _ = V.sensitivity(net, X, device=torch.device("cuda"))
     np.testing.assert_allclose(m2, m1, rtol=2e-4, atol=1e-6)
     np.testing.assert_allclose(r2, r1, rtol=2e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("acts", [("sigmoid", "tanh", "sigmoid"), ("relu", "sigmoid", "sigmoid"),
+                                  ("tanh", "relu", "tanh", "sigmoid")])
+def test_deep_sensitivity_mfma_tail_matches_torch(acts):
+    """K14b (perturbed first layer as bf16 rows + MFMA GEMM tail) vs the fp32 torch oracle for 2-
+    and 3-hidden-layer nets: per-input SE within bf16 accuracy, same top inputs."""
+    from shifu_amd.algos import varsel as V
+    from shifu_amd.formats.nn_format import NNNetwork
+    rng = np.random.default_rng(1)
+    F = 50
+    sizes = [F] + [48, 24, 16][: len(acts) - 1] + [1]
+    Ws = [rng.normal(size=(sizes[i + 1], sizes[i] + 1)) * (0.8 / np.sqrt(sizes[i])) for i in range(len(sizes) - 1)]
+    Ws[0][:, :8] *= 4.0                                    # a few strongly used inputs
+    net = NNNetwork(sizes, list(acts), Ws)
+    X = rng.normal(size=(4000, F)).astype(np.float32)
+    m1, r1, _ = V.sensitivity(net, X, device=torch.device("cpu"))
+    m2, r2, _ = V.sensitivity(net, X, device=torch.device("cuda"), deep_rows=1024, feat_chunk=16)
+    np.testing.assert_allclose(r2, r1, rtol=3e-2, atol=2e-3 * r1.max())
+    np.testing.assert_allclose(m2, m1, rtol=3e-2, atol=1e-2 * m1.max())   # |d| keeps bf16 noise
+    assert set(np.argsort(-r1)[:8]) == set(np.argsort(-r2)[:8])
+
+
+def test_sensitivity_host_rows_stream_equals_resident():
+    """SE over HostRows (pinned staging + H2D on a copy stream overlapping the kernels) equals SE
+    over the same rows resident on the device (rows rounded to bf16, the staging precision)."""
+    from shifu_amd.algos import varsel as V
+    from shifu_amd.formats.nn_format import NNNetwork
+    from shifu_amd.models.nn import HostRows
+    rng = np.random.default_rng(2)
+    F, H = 64, 32
+    net = NNNetwork([F, H, 1], ["sigmoid", "sigmoid"], [rng.normal(size=(H, F + 1)) * 0.3,
+                                                        rng.normal(size=(1, H + 1))])
+    X = torch.from_numpy(rng.normal(size=(20000, F)).astype(np.float32)).to(torch.bfloat16).float().numpy()
+    m1, r1, _ = V.sensitivity(net, torch.from_numpy(X).cuda(), device=torch.device("cuda"), row_chunk=256)
+    m2, r2, _ = V.sensitivity(net, HostRows(X, F), device=torch.device("cuda"), row_chunk=256)
+    np.testing.assert_allclose(r2, r1, rtol=1e-6)
+    np.testing.assert_allclose(m2, m1, rtol=1e-6)
