@@ -58,6 +58,36 @@ def equal_population_boundaries(values: np.ndarray, n_bins: int, weights: np.nda
     return bounds
 
 
+def sketch_boundaries(values: np.ndarray, n_bins: int, algorithm: str, weights=None) -> list:
+    """Reference-parity cuts from the streaming sketches of ``stats.binningAlgorithm``
+    (runtime/csrc/binning_stream.cpp): SPDT / SPDTI -> ``EqualPopulationBinning``,
+    MunroPat / MunroPatI -> ``MunroPatBinning``; values in row order, NaN = missing."""
+    from ..ops import _native
+    lib = _native.rt()
+    if lib is None:
+        raise RuntimeError("binning parity mode needs the native runtime library (g++)")
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    cap = max(4 * n_bins + 8, 64)
+    out = np.empty(cap, np.float64)
+    algo = algorithm.upper()
+    if algo.startswith("SPDT"):
+        w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+        n = lib.shifu_spdt_bins(v.ctypes.data, None if w is None else w.ctypes.data, v.size, int(n_bins),
+                                out.ctypes.data, cap)
+    elif algo.startswith("MUNROPAT"):
+        n = lib.shifu_munropat_bins(v.ctypes.data, v.size, int(n_bins), out.ctypes.data, cap)
+    else:
+        raise ValueError(f"no streaming sketch for binning algorithm {algorithm!r}")
+    if n < 0:
+        raise ValueError(f"sketch binning failed ({algorithm}, bins={n_bins})")
+    if n > cap:
+        out = np.empty(n, np.float64)
+        n = lib.shifu_spdt_bins(v.ctypes.data, None, v.size, int(n_bins), out.ctypes.data, n) \
+            if algo.startswith("SPDT") else lib.shifu_munropat_bins(v.ctypes.data, v.size, int(n_bins),
+                                                                      out.ctypes.data, n)
+    return [float(x) for x in out[:n]]
+
+
 def equal_interval_boundaries(values: np.ndarray, n_bins: int) -> list:
     v = np.asarray(values, dtype=np.float64)
     v = v[np.isfinite(v)]

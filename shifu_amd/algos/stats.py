@@ -204,6 +204,19 @@ def batch_histograms(vals: torch.Tensor, y: torch.Tensor, w: torch.Tensor, bound
     return out
 
 
+def parity_algorithm(mc):
+    """``shifu.stats.binning.parity=true`` + binningAlgorithm SPDT/SPDTI/MunroPat/MunroPatI: the
+    reference's streaming-sketch cuts (BinningDataUDF semantics: every valid value of the column in
+    row order, unweighted, whatever the class) instead of the exact equal-population cuts."""
+    from ..config import environment
+    algo = str(mc.stats.get("binningAlgorithm", "SPDTI") or "SPDTI")
+    if not environment.get_bool("shifu.stats.binning.parity", False):
+        return None
+    if mc.binning_method in ("EqualInterval", "WeightEqualInterval"):
+        return None
+    return algo if algo.upper().startswith(("SPDT", "MUNROPAT")) else None
+
+
 def _numeric_bounds(vals, y, w, binary, method, n_bins):
     if binary and method in ("EqualPositive", "WeightEqualPositive"):
         sel = y > 0.5
@@ -278,6 +291,7 @@ def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int 
     num_thr = float(mc.stats.get("numericalValueThreshold", 1.7976931348623157e308))
     y, w = md.y, md.w
     total = md.n
+    parity = parity_algorithm(mc)
     numeric = []
     for cc in ccs:
         if columns is not None and cc.name not in columns:
@@ -313,6 +327,8 @@ def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int 
             batch = numeric[b0: b0 + gpu_batch]
             vals = upload_columns([md.table[c.name].numeric() for c in batch], dev)
             bounds, distinct = Q.column_cuts(vals, yt, wt, n_bins, method, binary, num_thr)
+            if parity:
+                bounds = [B.sketch_boundaries(md.table[c.name].numeric(), n_bins, parity) for c in batch]
             if total <= EXACT_DISTINCT_ROWS:
                 distinct = exact_distinct(vals, num_thr)
             res = stats_ops.column_stats(vals, yt, wt, bounds, binary, num_thr)
@@ -322,7 +338,8 @@ def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int 
     for cc in numeric:
         vals = md.table[cc.name].numeric().astype(np.float64).copy()
         vals[vals > num_thr] = np.nan          # numericalValueThreshold -> invalid
-        bounds = _numeric_bounds(vals, y, w, binary, method, n_bins)
+        bounds = B.sketch_boundaries(md.table[cc.name].numeric(), n_bins, parity) if parity else \
+            _numeric_bounds(vals, y, w, binary, method, n_bins)
         bidx = B.bin_index_numeric(vals, bounds)
         cpos, cneg, wpos, wneg = _hist(bidx, y, w, len(bounds) + 1, binary, dev)
         fin = vals[np.isfinite(vals)]

@@ -29,6 +29,7 @@ DEFAULTS = {
     "shifu.stats.streaming": "auto",
     "shifu.stats.streamThresholdGB": "8",
     "shifu.stats.chunkMB": "256",
+    "shifu.stats.binning.parity": "false",
     "shifu.varsel.se.reuse": "false",
     "shifu.tree.regeninput": "false",
 }

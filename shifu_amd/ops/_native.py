@@ -83,6 +83,8 @@ RT_SIGNATURES = {
     "shifu_csv_dict": ("pipl", "l"),
     "shifu_csv_dict_size": ("pi", "l"),
     "shifu_csv_free": ("p", None),
+    "shifu_spdt_bins": ("pplipl", "l"),
+    "shifu_munropat_bins": ("plipl", "l"),
 }
 
 

@@ -87,6 +87,8 @@ def _use_streaming(ms: ModelSet) -> bool:
     from ..data.stream import data_bytes
     from ..parallel import dist
     mode = str(environment.get("shifu.stats.streaming", "auto")).lower()
+    if S.parity_algorithm(ms.mc):            # reference sketches consume whole columns in row order
+        return False
     if mode in ("true", "1", "yes"):
         return True
     if mode in ("false", "0", "no"):

@@ -193,3 +193,56 @@ def test_pearson_chunked_equals_whole():
     parts = [X[:100], X[100:250], X[250:]]
     np.testing.assert_allclose(pearson_correlation(iter(parts), chunk_rows=64), pearson_correlation(X),
                                rtol=1e-12, atol=1e-14)
+
+
+def test_spdt_sketch_matches_reference_small_bin_rule():
+    """EqualPopulationBinningTest.testExtraSmallBins: 60 outliers next to 2 x 100000 values are
+    folded into a neighbour (< 0.3% of an average bin) -> 2 cut points; 61 -> 3."""
+    from shifu_amd.algos import binning as B
+    for n_out, want in ((60, 2), (61, 3)):
+        v = np.concatenate([np.full(100000, 5.0), np.full(100000, 8.0), np.full(n_out, -10.0)])
+        assert len(B.sketch_boundaries(v, 10, "SPDT")) == want
+
+
+def test_sketch_cuts_track_exact_quantiles():
+    from shifu_amd.algos import binning as B
+    rng = np.random.default_rng(0)
+    v = rng.normal(size=50000)
+    exact = np.array(B.equal_population_boundaries(v, 10)[1:])
+    spdt = np.array(B.sketch_boundaries(v, 10, "SPDTI")[1:])
+    mp = B.sketch_boundaries(v, 10, "MunroPat")
+    assert spdt.size == exact.size and np.abs(spdt - exact).max() < 0.02
+    # MunroPat: min + 8 interior quantiles + max -> -inf + 8 cuts (MunroPatBinning.binMerge)
+    assert mp[0] == -np.inf and len(mp) == 9
+    # the alternate-element collapse (lower element of each pair) biases the estimate low by a
+    # rank of ~1-3 %: compare ranks, not values
+    ranks = np.searchsorted(np.sort(v), np.array(mp[1:])) / v.size
+    assert np.abs(ranks - np.arange(1, 9) / 9).max() < 0.04
+    with_nan = np.concatenate([v, [np.nan] * 100])
+    assert B.sketch_boundaries(with_nan, 10, "SPDT") == B.sketch_boundaries(v, 10, "SPDT")
+
+
+def test_stats_binning_parity_mode(tmp_path, monkeypatch):
+    import json
+    import os
+    from shifu_amd.config import environment
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    from shifu_amd.algos import binning as B
+    from shifu_amd.data.purifier import load_dataset
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    root = make_model_set(str(tmp_path), "p", "NN", n_rows=3000, n_num=4, n_cat=1)
+    mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+    mc.stats["binningAlgorithm"] = "SPDTI"
+    mc.save()
+    run_init(root)
+    monkeypatch.setitem(environment.props(), "shifu.stats.binning.parity", "true")
+    run_stats(root)
+    ccs = json.load(open(os.path.join(root, "ColumnConfig.json")))
+    c = next(x for x in ccs if x["columnName"] == "num_0")
+    md = load_dataset(ModelConfig.load(os.path.join(root, "ModelConfig.json")),
+                      ModelConfig.load(os.path.join(root, "ModelConfig.json")).dataSet, ["num_0"], [])
+    want = B.sketch_boundaries(md.table["num_0"].numeric(), 10, "SPDTI")
+    assert c["columnBinning"]["binBoundary"][1:] == want[1:] and len(want) > 5
