@@ -204,7 +204,10 @@ class BinnedData:
             c0, c1 = gi * FG, min(f, (gi + 1) * FG)
             blk = codes[:, c0:c1] if rows is None else codes[rows, c0:c1]
             if isinstance(blk, np.ndarray):
-                blk = torch.from_numpy(np.ascontiguousarray(blk, dtype=np.uint8))
+                blk = np.ascontiguousarray(blk, dtype=np.uint8)
+                if not blk.flags.writeable:        # read-only memmap slice: torch wants writable memory
+                    blk = blk.copy()
+                blk = torch.from_numpy(blk)
             b[gi, :, : c1 - c0] = blk.to(device=device, dtype=torch.uint8)
         return b
 

@@ -515,8 +515,7 @@ class MLPTrainer:
         # ring-pipelined TN wgrad (LDS-DMA ring 4 k-steps deep, fixed-order split reduction:
         # bitwise reproducible); SHIFU_WGRAD_RING=0 restores the 128x128 split-K atomics kernel
         self.wgrad_ring = os.environ.get("SHIFU_WGRAD_RING", "1") != "0"
-        self.fused_tail = self._tail_eligible()
-        self.fused_head = (not self.fused_tail) and self._head_eligible()
+        self.fused_head = self._head_eligible()
         self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
         # dropout (NNMaster.dropoutNodes :531-556, FloatFlatNetwork.computeLayer :205-215): each
         # iteration drops hidden nodes with DropoutRate and inputs with 0.4*DropoutRate and scales
@@ -567,9 +566,7 @@ class MLPTrainer:
         ws = {"rows": rows, "acts": [], "deltas": [], "derivs": []}
         for l in range(1, L + 1):
             ws["acts"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device))
-            # rows rounded up to 64: layer-1 deltas may be stored transposed + m-blocked
-            # ([rows/64][kp][64], see gemm_kernels.hip EPI_DACT_T)
-            ws["deltas"].append(torch.empty(round_up(rows, 64), kp[l], dtype=torch.bfloat16, device=self.device))
+            ws["deltas"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device))
             need_d = ACT_IDS[self.spec.acts[l - 1]] not in ACT_DERIV_FROM_OUTPUT
             ws["derivs"].append(torch.empty(rows, kp[l], dtype=torch.bfloat16, device=self.device)
                                 if need_d else None)
@@ -634,18 +631,6 @@ class MLPTrainer:
         if self._reducer is not None and self._final_chunk:
             self._reducer.launch_from(self.params.offsets[layer])
 
-    def _tail_supported(self) -> bool:
-        """Shapes the fused tail kernel (ops/csrc/mlp_tail.hip) covers: last hidden layer padded
-        width <= 256, n_out <= 8, output-only derivatives for the activations it differentiates."""
-        sp = self.spec
-        L = len(sp.hidden)
-        if self.device.type != "cuda" or L == 0:
-            return False
-        ok = sp.layer_kpad[L] <= 256 and sp.n_out <= 8 and ACT_IDS[sp.acts[L - 1]] in ACT_DERIV_FROM_OUTPUT
-        if L >= 2:
-            ok = ok and ACT_IDS[sp.acts[L - 2]] in ACT_DERIV_FROM_OUTPUT
-        return bool(ok)
-
     def _head_eligible(self) -> bool:
         """Fused network head (gemm_kernels.hip: gemm_head_8ph_kernel): last hidden forward GEMM +
         output layer + loss + deltas + output wgrad in one 8-phase GEMM epilogue, so the last
@@ -660,14 +645,6 @@ class MLPTrainer:
         return bool(sp.n_out == 1 and sp.layer_kpad[L] <= 256 and a in ACT_DERIV_FROM_OUTPUT and
                     sp.acts[L - 1] != "ptanh" and sp.hidden[L - 1] <= 255)
 
-    def _tail_eligible(self) -> bool:
-        """Opt-in (SHIFU_FUSED_TAIL=1).  Measured on MI355X at the bench shape (1M-row chunk,
-        512/256 padded hidden widths): fused 2.09 ms vs 1.76 ms for the three unfused kernels -
-        at one 148-KiB block per CU its k-steps wait on HBM/L2 (SQ_WAIT_ANY 55 % of wave
-        cycles), which 5 resident 128x128 GEMM blocks per CU hide.  Kept, tested, for shapes
-        where launch count dominates."""
-        return os.environ.get("SHIFU_FUSED_TAIL", "0") == "1" and self._tail_supported()
-
     def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None):
         from ..ops import _native as nat
         sp, kp = self.spec, self.spec.layer_kpad
@@ -681,35 +658,16 @@ class MLPTrainer:
         acts = [x] + [a[:mc] for a in ws["acts"]]
         dels = [None] + [d[:mc] for d in ws["deltas"]]
         ders = [None] + [(d[:mc] if d is not None else None) for d in ws["derivs"]]
-        fused = self.fused_tail
         head = self.fused_head and mc >= 65536
-        # layer-1 deltas transposed + m-blocked (EPI_DACT_T), consumed by the layer-0 wgrad with
-        # ds_read_b128 for its D operand (shifu_wgrad_tn_dt).  Opt-in (SHIFU_DGRAD_T=1): measured at
-        # the bench shape (1M rows) dgrad 0.83 -> 0.82 ms but wgrad 1.46 -> 1.57 ms
-        # (profiles/r1d/microbench_dgrad_t.json), although ds_read_b128 moves twice the LDS bytes
-        # per cycle of ds_read_b64_tr_b16 (profiles/r1d/microbench_lds_tr.txt).
-        dtr = (L >= 2 and not fused and os.environ.get("SHIFU_DGRAD_T", "0") == "1"
-               and ACT_IDS[sp.acts[0]] in ACT_DERIV_FROM_OUTPUT)
-        ldt = kp[1]                      # D^T rows (m-blocked layout: block stride kp[1] * 64)
         y = data.y[r0:r1]
         s = data.s[r0:r1] if data.s is not None else None
-        for l in range(L - 1 if (fused or head) else L):
+        for l in range(L - 1 if head else L):
             a_in, a_out = acts[l], acts[l + 1]
             act = ACT_IDS[sp.acts[l]]
             nat.call_hip("shifu_gemm_nt", a_in.data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
                          a_out.data_ptr(), kp[l + 1], nat.ptr(ders[l + 1]), kp[l + 1], None, 0, None, 0,
                          mc, kp[l + 1], kp[l], 0, act, sp.hidden[l], 1, flat_spot(sp.acts[l]), st)
-        if fused:
-            # last hidden layer forward + output layer + loss + deltas + backward GEMM, one kernel
-            lh = L - 1
-            bwd = L >= 2
-            nat.call_hip("shifu_mlp_tail", acts[lh], kp[lh], wb[lh], sp.hidden[lh], kp[lh], ACT_IDS[sp.acts[lh]],
-                         flat_spot(sp.acts[lh]), wv[L], kp[L], y, sp.n_out, s, sp.n_out, ACT_IDS[sp.out_act],
-                         LOSS_IDS[sp.loss], flat_spot(sp.out_act), dels[L], kp[L], gv[L], self.err_acc,
-                         int(bwd), wt[lh] if bwd else None, kp[L], dels[lh] if bwd else None, kp[lh],
-                         ACT_IDS[sp.acts[lh - 1]] if bwd else 0, sp.hidden[lh - 1] if bwd else 0,
-                         flat_spot(sp.acts[lh - 1]) if bwd else 0.0, mc, 0, st)
-        elif head:
+        if head:
             # last hidden forward + output layer + loss + deltas + output wgrad in one GEMM epilogue
             lh = L - 1
             nat.call_hip("shifu_gemm_head", acts[lh].data_ptr(), kp[lh], wb[lh].data_ptr(), kp[lh], sp.hidden[lh],
@@ -734,23 +692,19 @@ class MLPTrainer:
                 spl = max(1, min(mc // 256, 1024 // max(1, ntiles)))
             else:
                 spl = splits
-            if self.wgrad_ring and ws["slab"] is not None and mc >= 4096 and not (l == 0 and dtr):
+            if self.wgrad_ring and ws["slab"] is not None and mc >= 4096:
                 nat.call_hip("shifu_wgrad_ring", dels[l + 1], kp[l + 1], acts[l], kp[l], gv[l], kp[l],
                              mc, sp.hidden[l], kp[l], ws["slab"], ws["slab"].numel() * 4, st)
-            elif l == 0 and dtr:
-                nat.call_hip("shifu_wgrad_tn_dt", dels[1].data_ptr(), ldt, acts[0].data_ptr(), kp[0],
-                             gv[0].data_ptr(), kp[0], mc, sp.hidden[0], kp[0], spl, st)
             else:
                 nat.call_hip("shifu_wgrad_tn", dels[l + 1].data_ptr(), kp[l + 1], acts[l].data_ptr(), kp[l],
                              gv[l].data_ptr(), kp[l], mc, sp.hidden[l], kp[l], spl, st)
             self._grad_ready(l)
-            if l >= 1 and not (fused and l == L - 1):
-                # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)   (layer 1: written transposed)
+            if l >= 1:
+                # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)
                 act = ACT_IDS[sp.acts[l - 1]]
-                t = l == 1 and dtr
                 nat.call_hip("shifu_gemm_nt", dels[l + 1].data_ptr(), kp[l + 1], wt[l].data_ptr(), kp[l + 1],
-                             kp[l], dels[l].data_ptr(), ldt if t else kp[l], None, 0, acts[l].data_ptr(), kp[l],
-                             nat.ptr(ders[l]), kp[l], mc, kp[l], kp[l + 1], 3 if t else 1, act, sp.hidden[l - 1],
+                             kp[l], dels[l].data_ptr(), kp[l], None, 0, acts[l].data_ptr(), kp[l],
+                             nat.ptr(ders[l]), kp[l], mc, kp[l], kp[l + 1], 1, act, sp.hidden[l - 1],
                              0, flat_spot(sp.acts[l - 1]), st)
 
     def _chunk_torch(self, data: TrainData, r0: int, r1: int):

@@ -33,7 +33,6 @@ HIP_SIGNATURES = {
     # mlp_kernels.hip
     "shifu_gemm_nt": "plplipl" "plplpl" "iiiiiiif" "s",
     "shifu_wgrad_tn": "plplpl" "iiiis",
-    "shifu_wgrad_tn_dt": "plplpl" "iiiis",
     "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "s",
     "shifu_gemm_set_stages": "i",
     "shifu_gemm_set_big": "i",
@@ -46,12 +45,9 @@ HIP_SIGNATURES = {
     # gemm_ring.hip
     "shifu_wgrad_ring": "plplpl" "iii" "pl" "s",
     "shifu_wgrad_ring_ws": ("iii", "l"),
-    "shifu_gemm_ring_nt": "plplipl" "iiiiiii" "s",
     "shifu_ring_set_stamp": "p",
     "shifu_ring_set_mf": "i",
     "shifu_ring_set_dmamma": "i",
-    # mlp_tail.hip
-    "shifu_mlp_tail": "plpiiif" "pipl" "piiif" "plpp" "i" "plpl" "iif" "ii" "s",
     # gbdt_kernels.hip
     "shifu_gbdt_hist": "plpppp" "ipi" "dd" "l" "s",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",

@@ -51,7 +51,7 @@ __device__ __forceinline__ s16x4 ds_read_tr16_b64(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
 }
 
-enum Epi : int { EPI_ACT = 0, EPI_DACT = 1, EPI_STORE = 2, EPI_DACT_T = 3 };
+enum Epi : int { EPI_ACT = 0, EPI_DACT = 1, EPI_STORE = 2 };
 
 struct GemmArgs {
   const bf16_t* A; long lda;   // [M, K] row-major
@@ -67,7 +67,7 @@ struct GemmArgs {
 // STAGES = LDS buffers.  1: single 32 KiB buffer + register prefetch (two barriers per k-step,
 // up to 5 blocks = 5 waves/SIMD per CU -> the HBM/L2 latency of the next tile is hidden by the
 // other resident blocks); 2: classic LDS double buffer (64 KiB, 2 blocks per CU).
-template <int EPI, int ACT, int STAGES, bool HPF = false>
+template <int EPI, int ACT, int STAGES>
 __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntn = (p.N + BN - 1) / BN;
@@ -103,16 +103,6 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // dgrad (HPF): the epilogue's H row segments are loaded before the k-loop, so their HBM
-  // latency overlaps the (short, K <= 256) main loop instead of trailing it.
-  uint4 hpre[HPF ? 8 : 1];
-  if constexpr (HPF) {
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int m = m0 + pass * 16 + (tid >> 4), n = n0 + (tid & 15) * 8;
-      hpre[pass] = (m < p.M && n + 8 <= p.N) ? *(const uint4*)(p.H + (size_t)m * p.ldh + n) : make_uint4(0, 0, 0, 0);
-    }
-  }
 
   const int nk = p.K / BK;
   gload(0);
@@ -135,9 +125,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = EPI == EPI_DACT_T   // transposed accumulator: lane = 4 consecutive rows of one column
-              ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], bfr[i], acc[i][j], 0, 0, 0)
-              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
     }
     if constexpr (STAGES == 1) __syncthreads();     // every wave is done reading the buffer
     if (kt + 1 < nk) swrite(STAGES == 2 ? (buf ^ 1) : 0);
@@ -147,67 +135,6 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
   // Epilogue.  acc[i][j] holds D[n][m]: m = lane&15 (+16j), n = 4*(lane>>4) + r (+16i):
   // each lane owns 4 consecutive output columns of one row.
   constexpr bool dfo = act_deriv_from_output(ACT);
-  if constexpr (EPI == EPI_DACT_T) {
-    // dgrad written TRANSPOSED (C = D^T [N][ldc], rows = output columns): the swapped MFMA left
-    // lane l holding rows m = 4(l>>4) + r (+16j) of column n = l & 15 (+16i), i.e. 4 consecutive
-    // entries of one D^T row.  f'(H) for those 4 rows comes from the H tile staged in LDS and
-    // read back with ds_read_b64_tr_b16 (4 rows x 1 column per lane), then the D^T tile is staged
-    // [n][m] and leaves as 16-B row segments.  The wgrad that consumes D^T then reads its
-    // operand with ds_read_b128 instead of the half-rate transposed read.
-    char* Hs = smem;                                   // [128 m][256 B], TN quad swizzle (tr reads)
-    char* Ts = smem + 32768;                           // [128 n][256 B], 16-B chunk ^ (row & 15)
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int ml = pass * 16 + (tid >> 4), c = tid & 15;
-      const int m = min(m0 + ml, p.M - 1), n = min(n0 + c * 8, p.N - 8);     // clamped, no branch
-      *(uint4*)(Hs + swz_tn_quad(ml, c * 2)) = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
-    }
-    __syncthreads();
-    const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nl = wc * 64 + i * 16;                 // this (i) block's first column
-      const int n = n0 + nl + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int mb = wr * 64 + j * 16 + 4 * g;       // the lane's 4 rows start here
-        const s16x4 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)(Hs + swz_tn_quad(wr * 64 + j * 16 + 4 * g + tq, nl / 4 + tp)));
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = act_deriv_out(ACT, bf2f((bf16_t)hv[r])) + p.flat;
-          o[r] = n < p.n_valid ? acc[i][j][r] * d : 0.f;
-        }
-        uint2 w;
-        w.x = pack_bf16x2(o[0], o[1]);
-        w.y = pack_bf16x2(o[2], o[3]);
-        const int trow = nl + (lane & 15), c = mb >> 3, half = (mb >> 2) & 1;
-        *(uint2*)(Ts + trow * 256 + ((c ^ (trow & 15)) << 4) + half * 8) = w;
-      }
-    }
-    __syncthreads();
-    // D^T is m-blocked: element (n, m) at (m / 64) * (ldc * 64) + n * 64 + m % 64 (ldc = number of
-    // D^T rows), so a 64-row block of every column is one contiguous 128-B run and a wgrad step
-    // reads one contiguous [n][64] slab (a plain [N][M] transpose puts every row ~M * 2 B apart:
-    // one TLB page per row)
-    const int c = tid & 15;
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int nl = pass * 16 + (tid >> 4);
-      const int n = n0 + nl, m = m0 + c * 8;
-      if (n >= p.N || m >= p.M) continue;
-      const uint4 v = *(const uint4*)(Ts + nl * 256 + ((c ^ (nl & 15)) << 4));
-      bf16_t* dst = p.C + (size_t)(m >> 6) * ((size_t)p.ldc * 64) + (size_t)n * 64 + (m & 63);
-      if (m + 8 <= p.M) {
-        *(uint4*)dst = v;
-      } else {
-        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-        for (int q = 0; q < 8 && m + q < p.M; ++q) dst[q] = (bf16_t)((vv[q >> 1] >> ((q & 1) * 16)) & 0xffff);
-      }
-    }
-    return;
-  }
   if constexpr ((EPI == EPI_ACT || EPI == EPI_DACT) && dfo || EPI == EPI_STORE) {
     // Staged epilogue: phase 1 packs the tile (bf16) into LDS with a 16-B chunk XOR swizzle,
     // phase 2 writes whole 256-B row segments with 16-B stores (and, for dgrad, reads the
@@ -218,7 +145,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
     // the tile is staged through LDS (8 x 16 B per lane instead of one load per pass); rows clamped
     // to M - 1 and columns to ldh - 8 keep every load in bounds without a branch around it
     uint4 hreg[8];
-    if constexpr (EPI == EPI_DACT && !HPF) {
+    if constexpr (EPI == EPI_DACT) {
       const int nh = min(n0 + c * 8, (int)p.ldh - 8);
 #pragma unroll
       for (int pass = 0; pass < 8; ++pass) {
@@ -258,9 +185,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       if (m >= p.M || n >= p.N) continue;
       uint4 v = *(const uint4*)(Cs + ml * 256 + ((c ^ (ml & 15)) << 4));
       if constexpr (EPI == EPI_DACT) {
-        uint4 h;
-        if constexpr (HPF) h = (n + 8 <= p.N) ? hpre[pass] : *(const uint4*)(p.H + (size_t)m * p.ldh + n);
-        else h = hreg[pass];
+        const uint4 h = hreg[pass];
         const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
         uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -316,137 +241,6 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       *(uint2*)(p.C + (size_t)m * p.ldc + nb) = w;
     }
   }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Big-tile NT GEMM: 256 x 256 x 64 per 512-thread block (8 waves, 2 x 4, each wave 128 x 64).
-// Halves the L2->CU bytes per FLOP of the 128 x 128 kernel (128 FLOP/B), one LDS stage
-// (64 KiB) + register prefetch of the next k-tile; staged epilogue in two 128-row halves.
-// Dfo activations / dgrad / store only (the stored-derivative variants use gemm_nt_kernel).
-// ---------------------------------------------------------------------------------------
-constexpr int GB_M = 256, GB_N = 256, GB_T = 512;
-constexpr int GB_TILE = GB_M * BK * 2;       // 32 KiB per operand
-
-template <int EPI, int ACT>
-__global__ __launch_bounds__(GB_T, 1) void gemm_nt_big_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntn = (p.N + GB_N - 1) / GB_N;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (wg / ntn) * GB_M, n0 = (wg % ntn) * GB_N;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  char* As = smem;
-  char* Bs = smem + GB_TILE;
-
-  uint4 ra[4], rb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * GB_T, row = idx >> 3, ch = idx & 7;
-      const int gm = m0 + row, gn = n0 + row;
-      ra[i] = gm < p.M ? *(const uint4*)(p.A + (size_t)gm * p.lda + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
-      rb[i] = gn < p.NB ? *(const uint4*)(p.B + (size_t)gn * p.ldb + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto swrite = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * GB_T, row = idx >> 3, ch = idx & 7;
-      *(uint4*)(As + swz_nt(row, ch)) = ra[i];
-      *(uint4*)(Bs + swz_nt(row, ch)) = rb[i];
-    }
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = p.K / BK;
-  gload(0);
-  swrite();
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload((kt + 1) * BK);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = s * 4 + (lane >> 4);
-      bf16x8 af[8], bfr[4];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) af[j] = *(const bf16x8*)(As + swz_nt(wr * 128 + j * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) bfr[i] = *(const bf16x8*)(Bs + swz_nt(wc * 64 + i * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();
-    if (kt + 1 < nk) swrite();
-    __syncthreads();
-  }
-
-  // staged epilogue, two halves of 128 rows; LDS image [128 rows][512 B], 16-B chunk swizzle
-  char* Cs = smem;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (wr == h) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int ml = j * 16 + (lane & 15);
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = acc[i][j][r];
-            if constexpr (EPI == EPI_ACT) {
-              const int n = n0 + nl + r;
-              o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
-            } else {
-              o[r] = z;
-            }
-          }
-          uint2 w;
-          w.x = pack_bf16x2(o[0], o[1]);
-          w.y = pack_bf16x2(o[2], o[3]);
-          const int c = nl >> 3, half = (nl >> 2) & 1;
-          *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
-        }
-      }
-    }
-    __syncthreads();
-    const int c = tid & 31;
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int ml = pass * 16 + (tid >> 5);
-      const int m = m0 + h * 128 + ml, n = n0 + c * 8;
-      if (m < p.M && n < p.N) {
-        uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
-        if constexpr (EPI == EPI_DACT) {
-          const uint4 hh = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
-          const uint32_t hv[4] = {hh.x, hh.y, hh.z, hh.w};
-          uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float a0 = bf2f(vv[q] & 0xffff), a1 = bf2f(vv[q] >> 16);
-            const float d0 = act_deriv_out(ACT, bf2f(hv[q] & 0xffff)) + p.flat;
-            const float d1 = act_deriv_out(ACT, bf2f(hv[q] >> 16)) + p.flat;
-            a0 = (n + 2 * q < p.n_valid) ? a0 * d0 : 0.f;
-            a1 = (n + 2 * q + 1 < p.n_valid) ? a1 * d1 : 0.f;
-            vv[q] = pack_bf16x2(a0, a1);
-          }
-          v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
-        }
-        if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
-        else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
-      }
-    }
-    __syncthreads();
   }
 }
 
@@ -515,95 +309,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[4][
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Pipelined NT GEMM with LDS-DMA (global_load_lds_dwordx4): 256 x 256 tile, BK = 32, a ring of
-// 4 LDS stages (4 x 32 KiB) with 3 k-tiles in flight.  8 waves (2 M x 4 N, 128 x 64 each),
-// ONE raw s_barrier per k-step, counted vmcnt waits (never 0 inside the loop), no staging
-// VGPRs.  The LDS image is written linearly by the DMA (wave base + lane x 16 B); the 16-B
-// chunk swizzle chunk ^ ((row >> 2) & 3) is applied as the inverse permutation on the GLOBAL
-// source address and again on the ds_read address (an involution), which makes the 16-lane
-// groups of the fragment ds_read_b128 conflict-free on the 64-B rows.
-// ---------------------------------------------------------------------------------------
-constexpr int GP_M = 256, GP_N = 256, GP_K = 32, GP_T = 512, GP_ST = 4;
-constexpr int GP_OP = GP_M * GP_K * 2;          // 16 KiB per operand per stage
-constexpr int GP_STAGE = 2 * GP_OP;             // 32 KiB
-
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-__device__ __forceinline__ int swz32(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
-
-template <int EPI, int ACT>
-__global__ __launch_bounds__(GP_T, 1) void gemm_nt_pipe_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntn = (p.N + GP_N - 1) / GP_N;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (wg / ntn) * GP_M, n0 = (wg % ntn) * GP_N;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int nk = p.K / GP_K;
-
-  // per-lane global source rows/chunks of the 2 DMA instructions per operand (fixed per thread)
-  const bf16_t* srcA[2];
-  const bf16_t* srcB[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int P = i * 8192 + wid * 1024 + lane * 16;      // physical byte in the operand image
-    const int row = P >> 6, pch = (P >> 4) & 3;
-    const int lch = pch ^ ((row >> 2) & 3);                // logical chunk stored at P
-    const int gm = min(m0 + row, p.M - 1), gn = min(n0 + row, p.NB - 1);
-    srcA[i] = p.A + (size_t)gm * p.lda + lch * 8;
-    srcB[i] = p.B + (size_t)gn * p.ldb + lch * 8;
-  }
-  auto issue = [&](int st) {
-    char* base = smem + (st & (GP_ST - 1)) * GP_STAGE;
-    const int k0 = st * GP_K;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_global_load_lds((const void*)(srcA[i] + k0), (lds_ptr_t)(base + i * 8192 + wid * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(srcB[i] + k0), (lds_ptr_t)(base + GP_OP + i * 8192 + wid * 1024),
-                                       16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 2) issue(2);
-  for (int kt = 0; kt < nk; ++kt) {
-    // retire this k-tile's DMA (the younger ones stay in flight), then make every wave's land visible
-    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + 3 < nk) issue(kt + 3);         // into the stage every wave finished reading last step
-    const char* As = smem + (kt & (GP_ST - 1)) * GP_STAGE;
-    const char* Bs = As + GP_OP;
-    const int ch = lane >> 4;
-    bf16x8 af[8], bfr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bfr[i] = *(const bf16x8*)(Bs + swz32(wc * 64 + i * 16 + (lane & 15), ch));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) af[j] = *(const bf16x8*)(As + swz32(wr * 128 + j * 16 + (lane & 15), ch));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();             // every wave done reading the ring (DMA drained: vmcnt(0))
-  __builtin_amdgcn_sched_barrier(0);
-
-  epilogue_256<EPI, ACT>(p, acc, m0, n0, smem);
-}
-
 // ---------------------------------------------------------------------------------------
 // 8-phase NT GEMM (256 x 256 x 64, 8 waves 2 M x 4 N, wave tile 128 x 64, 1 block per CU).
 //
@@ -899,194 +605,6 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
 }
 
 // ---------------------------------------------------------------------------------------
-// Persistent 8-phase NT GEMM: the gemm_nt_8ph_kernel schedule run over a stream of output
-// tiles by one block per CU.  With K = 1024 a tile is only 16 k-tiles, and the standalone
-// kernel pays the DMA pipeline fill and a 128 KiB LDS-staged epilogue per tile with the MFMAs
-// idle.  Here the k-tile stream continues across tiles: the last iteration of tile t issues
-// the DMAs of tile t+1's k-tiles 0/1 (instead of dummy re-reads), and tile t's epilogue runs
-// from a separate 32 KiB LDS region (4 chunks of 64 rows) while those DMAs are in flight.
-// The epilogue's barriers are raw s_barrier (a __syncthreads fence would drain vmcnt to 0).
-// Tiles: block L (XCD-remapped) takes L, L + G, L + 2G, ...; tiles L and L+1 (the two N-tiles
-// of one 256-row M-tile) run concurrently on one XCD, so A rows are fetched from HBM once.
-// Requires K % 128 == 0 (an even number of k-tiles keeps the buffer parity across tiles).
-// ---------------------------------------------------------------------------------------
-constexpr int G8P_EPI = 2 * G8_BUF;              // epilogue region offset (after the 128 KiB ring)
-constexpr int G8P_LDS = 2 * G8_BUF + 32768;      // 160 KiB
-
-template <int EPI, int ACT>
-__global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_persist_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntn = (p.N + 255) / 256;
-  const int ntiles = ((p.M + 255) / 256) * ntn;
-  const int G = gridDim.x;
-  const int L = xcd_remap(blockIdx.x, G);
-  if (L >= ntiles) return;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int nk = p.K / 64;
-
-  // Per-thread DMA geometry (LDS byte P = i*8192 + wid*1024 + lane*16 of a half-tile holds
-  // logical 16-B chunk lc_i of row row_i); source addresses are formed per DMA from the
-  // (wave-uniform) tile origin so no per-tile offset tables occupy VGPRs.
-  int row_i[2], lc_i[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int P = i * 8192 + wid * 1024 + lane * 16;
-    row_i[i] = P >> 7;
-    lc_i[i] = ((P >> 4) & 7) ^ ((row_i[i] >> 1) & 7);
-  }
-  int t = L;
-  bool has_next = t + G < ntiles;
-  // k-tile kt of the stream: kt < nk -> this tile; kt >= nk -> next tile's kt - nk (or a dummy
-  // re-read of k-tile nk-1 when there is no next tile, which keeps the counted waits exact)
-  auto dma = [&](int h, int kt) {
-    char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
-    int tt = t, k = kt;
-    if (kt >= nk) {
-      if (has_next) { tt = t + G; k = kt - nk; } else k = nk - 1;
-    }
-    const bool isA = h < 2;
-    const int base = (isA ? (tt / ntn) * 256 : (tt % ntn) * 256) + (h & 1) * 128;
-    const int lim = (isA ? p.M : p.NB) - 1;
-    const long ld = isA ? p.lda : p.ldb;
-    const bf16_t* src = (isA ? p.A : p.B) + k * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src + (long)min(base + row_i[i], lim) * ld + lc_i[i] * 8),
-                                       (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
-  };
-
-  f32x4 acc[4][8];
-  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
-  const int lr = lane & 15, lq = lane >> 4;
-  auto readA = [&](int buf, int mh) {
-    const char* base = smem + buf * G8_BUF + wr * G8_HALF;
-#pragma unroll
-    for (int t4 = 0; t4 < 4; ++t4)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) af[t4][c] = *(const bf16x8*)(base + swz_nt(mh * 64 + t4 * 16 + lr, c * 4 + lq));
-  };
-  auto readB = [&](int buf, int nh, bf16x8 (&bq)[2][2]) {
-    const char* base = smem + buf * G8_BUF + (2 + (wc >> 1)) * G8_HALF;
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        bq[t2][c] = *(const bf16x8*)(base + swz_nt((wc & 1) * 64 + nh * 32 + t2 * 16 + lr, c * 4 + lq));
-  };
-  auto mma = [&](int mh, int nh, bf16x8 (&bq)[2][2]) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int s_ = 0; s_ < 2; ++s_)
-#pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4)
-          acc[nh * 2 + s_][mh * 4 + t4] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s_][c], af[t4][c], acc[nh * 2 + s_][mh * 4 + t4], 0, 0, 0);
-  };
-#define G8_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
-                      __builtin_amdgcn_sched_barrier(0); } while (0)
-#define G8_MMA(mh, nh, bq) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-    __builtin_amdgcn_s_setprio(1); mma(mh, nh, bq); __builtin_amdgcn_s_setprio(0); } while (0)
-
-  dma(2, 0); dma(3, 0); dma(0, 0); dma(1, 0);
-  dma(2, 1); dma(3, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  G8_BAR();
-  if (wr == 1) G8_BAR();                      // stagger the two wave rows by one barrier
-
-  for (;;) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int ke = 0; ke < nk; ke += 2) {
-      const int ko = ke + 1;
-      dma(0, ko); readB(0, 0, bf0); readA(0, 0);                                   // P1
-      G8_BAR(); G8_MMA(0, 0, bf0); G8_BAR();
-      dma(1, ko); readB(0, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P2
-      G8_BAR(); G8_MMA(0, 1, bf1); G8_BAR();
-      dma(2, ke + 2); readA(0, 1);                                                 // P3
-      G8_BAR(); G8_MMA(1, 1, bf1); G8_BAR();
-      dma(3, ke + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P4
-      G8_BAR(); G8_MMA(1, 0, bf0); G8_BAR();
-      dma(0, ke + 2); readB(1, 0, bf0); readA(1, 0);                               // P5
-      G8_BAR(); G8_MMA(0, 0, bf0); G8_BAR();
-      dma(1, ke + 2); readB(1, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P6
-      G8_BAR(); G8_MMA(0, 1, bf1); G8_BAR();
-      dma(2, ko + 2); readA(1, 1);                                                 // P7
-      G8_BAR(); G8_MMA(1, 1, bf1); G8_BAR();
-      dma(3, ko + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P8
-      G8_BAR(); G8_MMA(1, 0, bf0); G8_BAR();
-    }
-    if (wr == 0) G8_BAR();                    // re-align the rows
-    const bool last = !has_next;
-    if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the dummy prefetches
-
-    // epilogue of tile t from the 32 KiB region: 4 chunks of 64 rows x 512 B (16-B chunk ^ row)
-    const int m0 = (t / ntn) * 256, n0 = (t % ntn) * 256;
-    char* Cs = smem + G8P_EPI;
-    // FULL: every column of the tile is a valid unit (no bias column / padding in it): the
-    // per-element range selects are skipped (wave-uniform branch, two instantiations)
-    auto chunk_write = [&](int q, auto FULL) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int j = (q & 1) * 4 + jj;
-          const int ml = jj * 16 + (lane & 15);
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = acc[i][j][r];
-            const int n = n0 + nl + r;
-            if constexpr (decltype(FULL)::value) o[r] = EPI == EPI_ACT ? act_fwd(ACT, z) : z;
-            else if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
-            else o[r] = n < p.NB ? z : 0.f;
-          }
-          uint2 w;
-          w.x = pack_bf16x2(o[0], o[1]);
-          w.y = pack_bf16x2(o[2], o[3]);
-          const int c = nl >> 3, half = (nl >> 2) & 1;
-          *(uint2*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4) + half * 8) = w;
-        }
-      }
-    };
-    const bool full = n0 + 256 <= (EPI == EPI_ACT ? p.n_valid : p.NB);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (wr == (q >> 1)) {
-        if (full) chunk_write(q, std::integral_constant<bool, true>{});
-        else chunk_write(q, std::integral_constant<bool, false>{});
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      G8_BAR();
-      const int c = tid & 31;
-#pragma unroll
-      for (int pass = 0; pass < 4; ++pass) {
-        const int ml = pass * 16 + (tid >> 5);
-        const int m = m0 + q * 64 + ml, n = n0 + c * 8;
-        const uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
-        if (m < p.M && n < p.N) {
-          if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
-          else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      G8_BAR();
-    }
-    if (last) break;
-    // advance: the next tile's k-tiles 0 (complete) / 1 (B halves in flight) are staged
-    t += G;
-    has_next = t + G < ntiles;
-    if (wr == 1) G8_BAR();                    // re-stagger
-  }
-#undef G8_MMA
-#undef G8_BAR
-}
-
-// ---------------------------------------------------------------------------------------
 // wgrad: G[n][k] += sum_m D[m][n] * X[m][k]   (TN GEMM over rows, split over m)
 // LDS images [64 m][128 cols] bf16, 256-B rows, quad XOR swizzle so that the 8 rows read
 // by one 32-lane half of ds_read_b64_tr_b16 hit 8 distinct bank groups.
@@ -1103,10 +621,7 @@ struct WgradArgs {
   int nsplit, interleave;      // interleave: split s takes the 64-row steps s, s+nsplit, ...
 };
 
-// DT: D arrives transposed (D^T [Nd][ldd], ldd >= M) - the A operand is then an NT image
-// [128 n][64 m] read with ds_read_b128 (full rate) instead of ds_read_b64_tr_b16 (measured at
-// less than half the LDS bandwidth on gfx950: tools/microbench_lds_tr.hip).
-template <int STAGES, bool DT = false>
+template <int STAGES>
 __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles_n = (p.Nv + WT_BN - 1) / WT_BN, tiles_k = p.Kx / WT_BK;
@@ -1124,28 +639,14 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
   const int wn = wid >> 1, wk = wid & 1;
 
   uint4 rd[4], rx[4];
-  int dvalid[4] = {8, 8, 8, 8};
   auto gload = [&](int mb) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + i * NTHR, row = idx >> 4, ch = idx & 15;
       const int gm = mb + row;
       const bool ok = gm < mend;
-      if constexpr (DT) {
-        // D^T m-blocked (see EPI_DACT_T): (n, m) at (m / 64) * (ldd * 64) + n * 64 + m % 64
-        // unconditional 16-B load (the buffer holds whole 64-row blocks and ldd >= Nv rows, so the
-        // address is in bounds) + register masking: a branch around the load would make hipcc
-        // wait vmcnt(0) per load and serialize the prefetch
-        // (the mask is applied at LDS-write time: touching the loaded registers here would make
-        // hipcc wait for the prefetch right away)
-        const int dn = n0 + (idx >> 3), dm = mb + (idx & 7) * 8;      // D^T row n, 8 rows m
-        const int dnc = min(dn, (int)p.ldd - 1);
-        rd[i] = *(const uint4*)(p.D + (size_t)(dm >> 6) * ((size_t)p.ldd * 64) + (size_t)dnc * 64 + (dm & 63));
-        dvalid[i] = dn < p.Nv ? min(8, max(0, mend - dm)) : 0;                      // leading valid rows
-      } else {
-        const int gn = n0 + ch * 8;
-        rd[i] = (ok && gn < p.Nv) ? *(const uint4*)(p.D + (size_t)gm * p.ldd + gn) : make_uint4(0, 0, 0, 0);
-      }
+      const int gn = n0 + ch * 8;
+      rd[i] = (ok && gn < p.Nv) ? *(const uint4*)(p.D + (size_t)gm * p.ldd + gn) : make_uint4(0, 0, 0, 0);
       rx[i] = ok ? *(const uint4*)(p.X + (size_t)gm * p.ldx + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
     }
   };
@@ -1155,17 +656,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + i * NTHR, row = idx >> 4, ch = idx & 15;
-      if constexpr (DT) {
-        uint32_t q[4] = {rd[i].x, rd[i].y, rd[i].z, rd[i].w};
-        if (dvalid[i] < 8) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            q[e] &= (2 * e + 2 <= dvalid[i]) ? 0xffffffffu : ((2 * e + 1 <= dvalid[i]) ? 0x0000ffffu : 0u);
-        }
-        *(uint4*)(Ds + swz_nt(idx >> 3, idx & 7)) = make_uint4(q[0], q[1], q[2], q[3]);
-      } else {
-        *(uint4*)(Ds + swz_tn_quad(row, ch * 2)) = rd[i];
-      }
+      *(uint4*)(Ds + swz_tn_quad(row, ch * 2)) = rd[i];
       *(uint4*)(Xs + swz_tn_quad(row, ch * 2)) = rx[i];
     }
   };
@@ -1194,14 +685,10 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
       const int mr = s * 32 + 8 * g + tq;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if constexpr (DT) {
-          af[i] = *(const bf16x8*)(Ds + swz_nt(wn * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4)));
-        } else {
-          const int q = (wn * 64 + i * 16) / 4 + tp;
-          const s16x4 lo = ds_read_tr16_b64(Ds + swz_tn_quad(mr, q));
-          const s16x4 hi = ds_read_tr16_b64(Ds + swz_tn_quad(mr + 4, q));
-          af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
+        const int q = (wn * 64 + i * 16) / 4 + tp;
+        const s16x4 lo = ds_read_tr16_b64(Ds + swz_tn_quad(mr, q));
+        const s16x4 hi = ds_read_tr16_b64(Ds + swz_tn_quad(mr + 4, q));
+        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1235,162 +722,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Output layer row kernel (n_out <= 8):
-//   z_o = sum_j H[m][j] W[o][j]   (bias = column kh_valid of H, value 1)
-//   p_o = act_out(z_o);  err += ((y-p)s)^2 (squared) | -(y ln p + (1-y) ln(1-p)) (log) | |y-p|s
-//   delta_o = (y-p)(f'(p)+flat_out)s  (squared, J/core/dtrain/nn/SubGradient.java:241-248)
-//           = (y-p)s                  (log)
-//           = sign-loss (absolute, AbsoluteErrorFunction)
-//   D[m][j] = (sum_o W[o][j] delta_o)(f'_hid(H[m][j]) + flat_hid)   j < kh_valid, else 0
-//   GW[o][j] += delta_o H[m][j]
-// One wave per row strip; each lane owns 8 columns (KH <= 512) - row read = 1 KiB per wave.
-// ---------------------------------------------------------------------------------------
 }  // namespace
-
-// ---------------------------------------------------------------------------------------
-// 8-phase TN wgrad: G[n][k] += sum_m D[m][n] X[m][k] over a split of rows, 256 (n) x 256 (k)
-// output tile, k-steps of 64 rows, the schedule of gemm_nt_8ph_kernel with D in the role of A
-// (wave tile 128 n) and X in the role of B (wave tile 64 k).  Half-tiles are [64 rows][128
-// cols] images (256-B rows, TN quad swizzle, filled by LDS-DMA with the swizzle applied on the
-// source address) read with ds_read_b64_tr_b16.  Rows are consumed in whole 64-row steps (the
-// host hands a tail of M % 64 rows to wgrad_tn_kernel); columns past the buffers are clamped on
-// load and their outputs dropped.
-// ---------------------------------------------------------------------------------------
-struct Wgrad8Args {
-  const bf16_t* D; long ldd;
-  const bf16_t* X; long ldx;
-  float* G; long ldg;
-  int Nv, Kx, rows_per_split, m_end;   // rows [0, m_end) with m_end % 64 == 0
-  int nsplit, interleave;              // interleave: split s takes the 64-row steps s, s+nsplit, ...
-};
-
-__global__ __launch_bounds__(G8_T, 1) void wgrad_8ph_kernel(Wgrad8Args p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tiles_n = (p.Nv + 255) / 256, tiles_k = (p.Kx + 255) / 256;
-  const int ntiles = tiles_n * tiles_k;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = wg / ntiles, t = wg % ntiles;
-  const int n0 = (t / tiles_k) * 256, k0 = (t % tiles_k) * 256;
-  const int mbeg = p.interleave ? 0 : split * p.rows_per_split;
-  const int mend = p.interleave ? p.m_end : min(p.m_end, mbeg + p.rows_per_split);
-  const int nk = p.interleave ? (p.m_end / 64 - split + p.nsplit - 1) / p.nsplit : (mend - mbeg) / 64;
-  if (mbeg >= mend || nk <= 0) return;
-  const long step0 = p.interleave ? split : 0, kstride = p.interleave ? p.nsplit : 1;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wn = wid >> 2, wk = wid & 3;
-
-  // DMA sources (element offsets without the row step): half-tile h (0/1 D cols n0 + 128h,
-  // 2/3 X cols k0 + 128(h-2)), instruction i: LDS byte P = i*8192 + wid*1024 + lane*16
-  long off[4][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int P = i * 8192 + wid * 1024 + lane * 16;
-    const int row = P >> 8, pc = (P >> 4) & 15;
-    const int lc = pc ^ (tr_h(row) << 1);
-    const int cd0 = min(n0 + lc * 8, (int)p.ldd - 8), cd1 = min(n0 + 128 + lc * 8, (int)p.ldd - 8);
-    const int cx0 = min(k0 + lc * 8, (int)p.ldx - 8), cx1 = min(k0 + 128 + lc * 8, (int)p.ldx - 8);
-    off[0][i] = (long)(mbeg + row) * p.ldd + cd0;
-    off[1][i] = (long)(mbeg + row) * p.ldd + cd1;
-    off[2][i] = (long)(mbeg + row) * p.ldx + cx0;
-    off[3][i] = (long)(mbeg + row) * p.ldx + cx1;
-  }
-  auto dma = [&](int h, int kt) {
-    char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
-    const long r0 = (step0 + (long)min(kt, nk - 1) * kstride) * 64;
-    const bf16_t* src = h < 2 ? p.D + r0 * p.ldd : p.X + r0 * p.ldx;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src + off[h][i]), (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
-  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-  auto frag = [&](const char* img, int col_base, int c) {
-    const int mr = c * 32 + 8 * g + tq, q = col_base / 4 + tp;
-    const s16x4 lo = ds_read_tr16_b64(img + swz_tn_quad(mr, q));
-    const s16x4 hi = ds_read_tr16_b64(img + swz_tn_quad(mr + 4, q));
-    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  auto readD = [&](int buf, int nh) {
-    const char* img = smem + buf * G8_BUF + wn * G8_HALF;
-#pragma unroll
-    for (int t4 = 0; t4 < 4; ++t4)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) af[t4][c] = frag(img, (nh * 4 + t4) * 16, c);
-  };
-  auto readX = [&](int buf, int kh, bf16x8 (&bq)[2][2]) {
-    const char* img = smem + buf * G8_BUF + (2 + (wk >> 1)) * G8_HALF;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) bq[s2][c] = frag(img, (wk & 1) * 64 + (kh * 2 + s2) * 16, c);
-  };
-  auto mma = [&](int nh, int kh, bf16x8 (&bq)[2][2]) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4)
-          acc[nh * 4 + t4][kh * 2 + s2] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t4][c], bq[s2][c], acc[nh * 4 + t4][kh * 2 + s2], 0, 0, 0);
-  };
-#define G8_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
-                      __builtin_amdgcn_sched_barrier(0); } while (0)
-#define G8_MMA(nh, kh, bq, on) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-    if (on) { __builtin_amdgcn_s_setprio(1); mma(nh, kh, bq); __builtin_amdgcn_s_setprio(0); } } while (0)
-
-  dma(2, 0); dma(3, 0); dma(0, 0); dma(1, 0);
-  dma(2, 1); dma(3, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  G8_BAR();
-  if (wn == 1) G8_BAR();
-
-  for (int ke = 0; ke < nk; ke += 2) {
-    const int ko = ke + 1;
-    const bool odd_on = ko < nk;
-    dma(0, ko); readX(0, 0, bf0); readD(0, 0);                                   // P1
-    G8_BAR(); G8_MMA(0, 0, bf0, true); G8_BAR();
-    dma(1, ko); readX(0, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // P2
-    G8_BAR(); G8_MMA(0, 1, bf1, true); G8_BAR();
-    dma(2, ke + 2); readD(0, 1);                                                 // P3
-    G8_BAR(); G8_MMA(1, 1, bf1, true); G8_BAR();
-    dma(3, ke + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P4
-    G8_BAR(); G8_MMA(1, 0, bf0, true); G8_BAR();
-    dma(0, ke + 2); readX(1, 0, bf0); readD(1, 0);                               // P5
-    G8_BAR(); G8_MMA(0, 0, bf0, odd_on); G8_BAR();
-    dma(1, ke + 2); readX(1, 1, bf1); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P6
-    G8_BAR(); G8_MMA(0, 1, bf1, odd_on); G8_BAR();
-    dma(2, ko + 2); readD(1, 1);                                                 // P7
-    G8_BAR(); G8_MMA(1, 1, bf1, odd_on); G8_BAR();
-    dma(3, ko + 2); asm volatile("s_waitcnt vmcnt(4)" ::: "memory");            // P8
-    G8_BAR(); G8_MMA(1, 0, bf0, odd_on); G8_BAR();
-  }
-  if (wn == 0) G8_BAR();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#undef G8_MMA
-#undef G8_BAR
-  // acc[i][j]: G[n][k], k = k0 + 64 wk + 16 j + (lane & 15), n = n0 + 128 wn + 16 i + 4 (lane >> 4) + r
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
-      if (n >= p.Nv) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
-        if (k < p.Kx) atomicAdd(p.G + (size_t)n * p.ldg + k, acc[i][j][r]);
-      }
-    }
-}
 
 // =======================================================================================
 // C ABI (called through ctypes; host-side shape checks live in shifu_amd/ops/mlp.py and
@@ -1400,26 +732,14 @@ __global__ __launch_bounds__(G8_T, 1) void wgrad_8ph_kernel(Wgrad8Args p) {
 
 static int g_stages = 1;     // LDS stages of the MLP GEMMs (A/B switch for tuning; 1 = default)
 static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N >= 512, K >= 512; else 128x128),
-                             // 1 = 256x256 register-staged, 2 = 256x256 DMA ring, 3 = 8-phase, 4 = 128x128 only
-static int g_persist = 0;    // auto path: 1 = persistent 8-phase kernel for the forward GEMMs
-static int g_dgrad_pf = 0;   // dgrad H prefetch (gemm_nt_kernel HPF): measured 0.89 -> 1.30 ms (VGPRs), off
+                             // 3 = 8-phase whenever M >= 64K and N >= 256, 4 = 128x128 only
 static int g_wg_interleave = 1;   // wgrad row splits: 1 interleaved 64-row steps (-3% wgrad1 at 1M rows), 0 contiguous
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
-  if (key == 0) { g_dgrad_pf = val; return 0; }
-  if (key == 1) { g_persist = val; return 0; }
   if (key == 2) { g_wg_interleave = val; return 0; }
   return -1;
 }
-SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b >= 0 && b <= 5) ? b : 0; return 0; }
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
+SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b == 3 || b == 4) ? b : 0; return 0; }
 
 SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc,
                             void* C2, long ldc2, const void* H, long ldh, const void* Hd, long ldhd,
@@ -1431,23 +751,11 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
              (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat};
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = 2 * g_stages * TILE_BYTES;
-  if (act < 0 || act > 8 || epi < 0 || epi > 3) return -2;
+  if (act < 0 || act > 8 || epi < 0 || epi > 2) return -2;
   if (epi == EPI_ACT && !act_deriv_from_output(act) && C2 == nullptr) return -3;
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;
   const bool dfo_act = act_deriv_from_output(act);
-  if (epi == EPI_DACT_T) {              // transposed dgrad (C = D^T [N][ldc]), 128 x 128 kernel
-    if (!dfo_act || H == nullptr || ldh % 8) return -3;
-#define GEMMT_L(A_) hipLaunchKernelGGL((gemm_nt_kernel<EPI_DACT_T, A_, 1>), dim3(grid), dim3(NTHR), 65536, stream, p)
-    switch (act) {
-      case 0: GEMMT_L(0); break; case 1: GEMMT_L(1); break; case 2: GEMMT_L(2); break;
-      case 3: GEMMT_L(3); break; case 4: GEMMT_L(4); break; case 6: GEMMT_L(6); break;
-      default: GEMMT_L(7); break;
-    }
-#undef GEMMT_L
-    CHECK_HIP(hipGetLastError());
-    return 0;
-  }
   const bool auto8 = g_big == 0 && M >= 65536 && N >= 512 && K >= 512;
   if ((g_big == 3 || auto8) && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
     const int grid8 = ((M + 255) / 256) * ((N + 255) / 256);
@@ -1464,55 +772,8 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
     CHECK_HIP(hipGetLastError());
     return 0;
   }
-  if ((g_big == 5 || (g_big == 0 && g_persist && auto8)) && M >= 65536 && N >= 256 && K % 128 == 0 &&
-      (epi == EPI_STORE || (epi == EPI_ACT && dfo_act && act != 6))) {   // ptanh: register spill, 8-phase
-    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-    const int gridp = tiles < num_cus() ? tiles : num_cus();
-#define GEMMQ_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_persist_kernel<E, A>), dim3(gridp), dim3(G8_T), G8P_LDS, stream, p)
-#define GEMMQ_ACTS(E) switch (act) { case 0: GEMMQ_L(E, 0); break; case 1: GEMMQ_L(E, 1); break; \
-    case 2: GEMMQ_L(E, 2); break; case 3: GEMMQ_L(E, 3); break; case 4: GEMMQ_L(E, 4); break; \
-    case 6: GEMMQ_L(E, 6); break; default: GEMMQ_L(E, 7); break; }
-    if (epi == EPI_ACT) { GEMMQ_ACTS(EPI_ACT) }
-    else GEMMQ_L(EPI_STORE, 2);
-#undef GEMMQ_ACTS
-#undef GEMMQ_L
-    CHECK_HIP(hipGetLastError());
-    return 0;
-  }
-  if (g_big == 2 && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
-    const int gridp = ((M + GP_M - 1) / GP_M) * ((N + GP_N - 1) / GP_N);
-    const size_t ldsp = GP_ST * GP_STAGE;
-#define GEMMP_L(E, A) hipLaunchKernelGGL((gemm_nt_pipe_kernel<E, A>), dim3(gridp), dim3(GP_T), ldsp, stream, p)
-#define GEMMP_ACTS(E) switch (act) { case 0: GEMMP_L(E, 0); break; case 1: GEMMP_L(E, 1); break; \
-    case 2: GEMMP_L(E, 2); break; case 3: GEMMP_L(E, 3); break; case 4: GEMMP_L(E, 4); break; \
-    case 6: GEMMP_L(E, 6); break; default: GEMMP_L(E, 7); break; }
-    if (epi == EPI_ACT) { GEMMP_ACTS(EPI_ACT) }
-    else if (epi == EPI_DACT) { GEMMP_ACTS(EPI_DACT) }
-    else GEMMP_L(EPI_STORE, 2);
-#undef GEMMP_ACTS
-#undef GEMMP_L
-    CHECK_HIP(hipGetLastError());
-    return 0;
-  }
-  if (g_big == 1 && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
-    const int gridb = ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N);
-    const size_t ldsb = 2 * GB_TILE;
-#define GEMMB_L(E, A) hipLaunchKernelGGL((gemm_nt_big_kernel<E, A>), dim3(gridb), dim3(GB_T), ldsb, stream, p)
-#define GEMMB_ACTS(E) switch (act) { case 0: GEMMB_L(E, 0); break; case 1: GEMMB_L(E, 1); break; \
-    case 2: GEMMB_L(E, 2); break; case 3: GEMMB_L(E, 3); break; case 4: GEMMB_L(E, 4); break; \
-    case 6: GEMMB_L(E, 6); break; default: GEMMB_L(E, 7); break; }
-    if (epi == EPI_ACT) { GEMMB_ACTS(EPI_ACT) }
-    else if (epi == EPI_DACT) { GEMMB_ACTS(EPI_DACT) }
-    else GEMMB_L(EPI_STORE, 2);
-#undef GEMMB_ACTS
-#undef GEMMB_L
-    CHECK_HIP(hipGetLastError());
-    return 0;
-  }
 #define GEMM_L(E, A) do { if (g_stages == 2) \
     hipLaunchKernelGGL((gemm_nt_kernel<E, A, 2>), dim3(grid), dim3(NTHR), lds, stream, p); \
-  else if (E == EPI_DACT && g_dgrad_pf && act_deriv_from_output(A)) \
-    hipLaunchKernelGGL((gemm_nt_kernel<E, A, 1, E == EPI_DACT && act_deriv_from_output(A)>), dim3(grid), dim3(NTHR), lds, stream, p); \
   else hipLaunchKernelGGL((gemm_nt_kernel<E, A, 1>), dim3(grid), dim3(NTHR), lds, stream, p); } while (0)
 #define GEMM_ACTS(E) switch (act) { case 0: GEMM_L(E, 0); break; case 1: GEMM_L(E, 1); break; \
     case 2: GEMM_L(E, 2); break; case 3: GEMM_L(E, 3); break; case 4: GEMM_L(E, 4); break; \
@@ -1551,22 +812,6 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
   return 0;
 }
 
-// wgrad with the deltas given transposed and m-blocked (ldd = number of D^T rows >= Nv, element
-// (n, m) at (m / 64) * ldd * 64 + n * 64 + m % 64; see EPI_DACT_T):
-// G[n][k] += sum_m D^T[n][m] X[m][k] with the D operand read at full LDS rate.
-SHIFU_API int shifu_wgrad_tn_dt(const void* DT, long ldd, const void* X, long ldx, float* G, long ldg,
-                                int M, int Nv, int Kx, int splits, hipStream_t stream) {
-  if (Kx % WT_BK || ldx % 8 || M <= 0 || Nv <= 0 || ldd < Nv) return -1;
-  if (splits < 1) splits = 1;
-  int rps = (M + splits - 1) / splits;
-  rps = ((rps + WT_BM - 1) / WT_BM) * WT_BM;
-  splits = (M + rps - 1) / rps;
-  WgradArgs p{(const bf16_t*)DT, ldd, (const bf16_t*)X, ldx, G, ldg, M, Nv, Kx, rps, splits, g_wg_interleave};
-  const int ntiles = ((Nv + WT_BN - 1) / WT_BN) * (Kx / WT_BK);
-  hipLaunchKernelGGL((wgrad_tn_kernel<1, true>), dim3(ntiles * splits), dim3(NTHR), 2 * WT_TILE, stream, p);
-  CHECK_HIP(hipGetLastError());
-  return 0;
-}
 
 SHIFU_API int shifu_wgrad_tn(const void* D, long ldd, const void* X, long ldx, float* G, long ldg,
                              int M, int Nv, int Kx, int splits, hipStream_t stream) {
@@ -1575,28 +820,6 @@ SHIFU_API int shifu_wgrad_tn(const void* D, long ldd, const void* X, long ldx, f
   int rps = (M + splits - 1) / splits;
   rps = ((rps + WT_BM - 1) / WT_BM) * WT_BM;
   splits = (M + rps - 1) / rps;
-  // opt-in (set_big(3)): at the bench shape it measured 2.09 ms vs 1.39 ms for the 128x128
-  // kernel - the 8 output tiles sharing a row range drift apart by more than L2 holds, so each
-  // re-reads its rows from HBM (8 GB vs ~3 GB), while 5 smaller blocks per CU stay in step.
-  const bool use8 = g_big == 3;
-  if (use8 && M >= 65536 && Kx >= 256 && Nv >= 128 && ldd >= 8 && ldx >= 8) {
-    // 8-phase path over whole 64-row steps; ~256 blocks (one per CU), the M % 64 tail below
-    const int tiles8 = ((Nv + 255) / 256) * ((Kx + 255) / 256);
-    int sp8 = 256 / tiles8;
-    if (sp8 < 1) sp8 = 1;
-    const int m64 = M - M % 64;
-    int rps8 = (m64 / 64 + sp8 - 1) / sp8 * 64;
-    sp8 = (m64 + rps8 - 1) / rps8;
-    Wgrad8Args q{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, G, ldg, Nv, Kx, rps8, m64, sp8, g_wg_interleave};
-    hipLaunchKernelGGL(wgrad_8ph_kernel, dim3(tiles8 * sp8), dim3(G8_T), 2 * G8_BUF, stream, q);
-    CHECK_HIP(hipGetLastError());
-    if (m64 == M) return 0;
-    D = (const bf16_t*)D + (size_t)m64 * ldd;
-    X = (const bf16_t*)X + (size_t)m64 * ldx;
-    M -= m64;
-    splits = 1;
-    rps = M;
-  }
   WgradArgs p{(const bf16_t*)D, ldd, (const bf16_t*)X, ldx, G, ldg, M, Nv, Kx, rps, splits, g_wg_interleave};
   const int ntiles = ((Nv + WT_BN - 1) / WT_BN) * (Kx / WT_BK);
   if (g_stages == 2)

@@ -343,186 +343,6 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// NT ring GEMM (forward layers): C[m][n] = act(sum_k A[m][k] B[n][k]) with the Encog bias column
-// (C[m][n_valid] = 1) and zero padding written by the epilogue (FloatFlatNetwork.java:148-178).
-// Same ring / stagger schedule as ring_tn_kernel, persistent over output tiles: block L takes tiles
-// L, L+G, ... (the two n-tiles of one 256-row m-tile are consecutive logical ids: one XCD, rows
-// fetched from HBM once), and the DMA stream runs straight across tile boundaries, so the next
-// tile's first k-steps land while the current one finishes (no per-tile pipeline fill).
-// Images: A [256 rows][32 k], B [256 rows][32 k], 64-B rows, chunk ^ ((r >> 4) & 1 | ((r >> 2) & 1) << 1):
-// conflict-free ds_read_b128 for the 16x16x32 (and 32x32x16) operand maps (brute-force checked over
-// the four ds_read_b128 lane groups).
-// Epilogue (after the MFMAs of a tile's last k-step): act + bf16 pack + 8-byte row stores.  Every
-// wave issues exactly RG_NT_STORES stores per tile (lanes outside the output write a dummy slot), so
-// the counted vmcnt of the next three LD segments can let the younger DMAs stay in flight.
-// ---------------------------------------------------------------------------------------------
-constexpr int RG_NT_STORES = 32;
-__device__ uint2 g_rg_dummy[64];     // 8-byte sinks for the stores of lanes outside the output
-
-__device__ __forceinline__ int nt_swz(int r) { return ((r >> 4) & 1) | (((r >> 2) & 1) << 1); }
-
-struct RingNTArgs {
-  const bf16_t* A; long lda;   // [M, K] row-major
-  const bf16_t* B; long ldb;   // [NB, K] row-major (rows >= NB read as row NB-1, outputs dropped)
-  bf16_t* C; long ldc;         // [M, N]
-  int M, N, K, NB, n_valid, bias_col;
-  int ntn, ntiles;             // n-tiles, total tiles
-};
-
-template <int EPI, int ACT>
-__global__ __launch_bounds__(RG_T, 2) void ring_nt_kernel(RingNTArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int G = gridDim.x;
-  const int L = rg_xcd_remap(blockIdx.x, G);
-  const int ks = p.K >> 5;                                  // k-steps per tile
-  const int U = ((p.ntiles - L + G - 1) / G) * ks;          // host: G <= ntiles -> U >= ks
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const bool lag = wid >= 4;
-
-  // DMA: thread instr i (0/1) per image fills LDS bytes (i*8 + wid)*1024 + lane*16 = row P >> 6
-  int drow[2], dch[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int P = (i * 8 + wid) * 1024 + lane * 16;
-    drow[i] = P >> 6;
-    dch[i] = (((P >> 4) & 3) ^ nt_swz(drow[i])) * 8;
-  }
-  // DMA cursor (tile id, k-step).  Per tile: wave-uniform base pointers of the tile's first rows
-  // and per-lane 32-bit byte offsets (rows clamped to the operand), so each LDS-DMA is a scalar base
-  // + vector offset (no 64-bit address math per step).
-  int d_tile = L, d_k = 0;
-  const char* dbaseA;
-  const char* dbaseB;
-  uint32_t offA[2], offB[2];
-  auto dma_tile = [&]() {
-    const int mt = d_tile / p.ntn, nt = d_tile - mt * p.ntn;
-    dbaseA = (const char*)(p.A + (size_t)mt * 256 * p.lda);
-    dbaseB = (const char*)(p.B + (size_t)nt * 256 * p.ldb);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int ml = min(mt * 256 + drow[i], p.M - 1) - mt * 256;
-      const int nl = min(nt * 256 + drow[i], p.NB - 1) - nt * 256;
-      offA[i] = (uint32_t)(ml * p.lda + dch[i]) * 2u;
-      offB[i] = (uint32_t)(nl * p.ldb + dch[i]) * 2u;
-    }
-  };
-  dma_tile();
-  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  auto dma = [&](int slot, bool live) {
-    char* base = smem + slot * RG_SLOT + wid_u * 1024;
-    const char* a = dbaseA + d_k * 64;
-    const char* b = dbaseB + d_k * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(a + offA[i]), (lds_ptr_t)(base + i * 8192), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b + offB[i]), (lds_ptr_t)(base + RG_IMG + i * 8192), 16, 0, 0);
-    if (live) {                                             // past the end: re-read the last step
-      if (++d_k == ks) { d_k = 0; d_tile += G; dma_tile(); }
-    }
-  };
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment reads: operand rows base + (lane & 15), 16-B chunk (lane >> 4) (+ swizzle).  Frag t
-  // of a 16-row block sits at t * 1024 + lane offset, and the lane offset only depends on t's
-  // parity (swizzle bit 0 = row bit 4), so two per-lane bases per operand + immediate offsets.
-  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  const int fr = lane & 15, fc = lane >> 4;
-  auto lane_off = [&](int row) { return (uint32_t)(row * 64 + ((fc ^ nt_swz(row)) << 4)); };
-  const uint32_t oA0 = lane_off(wm * 128 + fr), oA1 = lane_off(wm * 128 + 16 + fr) - 1024;
-  const uint32_t oB0 = RG_IMG + lane_off(wn * 64 + fr), oB1 = RG_IMG + lane_off(wn * 64 + 16 + fr) - 1024;
-  bf16x8 af[8], bfr[4];
-
-#define RG_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
-                      __builtin_amdgcn_sched_barrier(0); } while (0)
-
-  int live_left = U;                                        // DMA steps still inside the stream
-  for (int s = 0; s < 4; ++s) { dma(s, live_left > 1); --live_left; }
-  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  RG_BAR();
-  if (lag) RG_BAR();
-
-  int slot = 0, dslot = 4, kstep = 0, tile = L, post_epi = 0;
-  for (int u = 0; u < U; ++u) {
-    // ---- LD segment
-    dma(dslot, live_left > 1); --live_left;
-    const uint32_t sb = lds0 + slot * RG_SLOT;
-    {
-      const uint32_t b0 = sb + oB0, b1 = sb + oB1, a0 = sb + oA0, a1 = sb + oA1;
-      bfr[0] = rg_read_b128_o<0>(b0);    bfr[1] = rg_read_b128_o<1024>(b1);
-      bfr[2] = rg_read_b128_o<2048>(b0); bfr[3] = rg_read_b128_o<3072>(b1);
-      af[0] = rg_read_b128_o<0>(a0);     af[1] = rg_read_b128_o<1024>(a1);
-      af[2] = rg_read_b128_o<2048>(a0);  af[3] = rg_read_b128_o<3072>(a1);
-      af[4] = rg_read_b128_o<4096>(a0);  af[5] = rg_read_b128_o<5120>(a1);
-      af[6] = rg_read_b128_o<6144>(a0);  af[7] = rg_read_b128_o<7168>(a1);
-    }
-    if (post_epi > 0) {                   // the last tile's 32 stores sit between older and younger DMAs
-      asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
-      --post_epi;
-    } else {
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    RG_BAR();
-    // ---- MMA segment
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][i], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (++kstep == ks) {
-      // ---- epilogue: acc[j][i] = D[n][m]: m = 16i + (lane & 15), n = 16j + 4(lane >> 4) + r
-      const int mt = tile / p.ntn, nt = tile - mt * p.ntn;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nb = nt * 256 + wn * 64 + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int m = mt * 256 + wm * 128 + i * 16 + fr;
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = acc[j][i][r];
-            if constexpr (EPI == 0) {
-              // branch-free select (a ternary around act_fwd compiles to exec-masked branches)
-              const int n = nb + r;
-              const float a = act_fwd(ACT, z);
-              const float alt = (n == p.n_valid && p.bias_col) ? 1.f : 0.f;
-              const int keep = -(int)(n < p.n_valid);
-              o[r] = __int_as_float((__float_as_int(a) & keep) | (__float_as_int(alt) & ~keep));
-            } else {
-              o[r] = z;
-            }
-            acc[j][i][r] = 0.f;
-          }
-          const uint2 w = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
-          uint2* dst = (m < p.M && nb < p.N) ? (uint2*)(p.C + (size_t)m * p.ldc + nb) : &g_rg_dummy[lane];
-          rg_store_b64(dst, w);
-        }
-      }
-      kstep = 0;
-      tile += G;
-      post_epi = 3;
-    }
-    RG_BAR();
-    slot = slot == RG_NSLOT - 1 ? 0 : slot + 1;
-    dslot = dslot == RG_NSLOT - 1 ? 0 : dslot + 1;
-  }
-  if (!lag) RG_BAR();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#undef RG_BAR
-}
-
 // tail rows (< 32) that do not fill a ring k-step: one thread per (n, k), fixed row order
 __global__ __launch_bounds__(256) void tail_tn_kernel(const bf16_t* __restrict__ D, long ldd,
                                                       const bf16_t* __restrict__ X, long ldx, int rows,
@@ -608,40 +428,4 @@ SHIFU_API int shifu_wgrad_ring(const void* D, long ldd, const void* X, long ldx,
     if (e != hipSuccess) return (int)e;
   }
   return 0;
-}
-
-static int rg_num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-// Forward NT GEMM through the persistent ring: C = act(A B^T) (epi 0: activation + bias column +
-// zero padding; epi 2: plain store).  K % 32 == 0; activations whose derivative follows from the
-// output only (no stored-derivative output).  Returns -1 on an unsupported shape (caller falls back).
-SHIFU_API int shifu_gemm_ring_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc,
-                                 int M, int N, int K, int epi, int act, int n_valid, int bias_col, hipStream_t stream) {
-  if (K % 32 || K < 32 || lda % 8 || ldb % 8 || ldc % 4 || N % 4 || M <= 0 || N <= 0 || NB <= 0 || lda < K ||
-      ldb < K || ldc < N || ((uintptr_t)C & 7))
-    return -1;
-  if (epi != 0 && epi != 2) return -1;
-  if (epi == 0 && (!act_deriv_from_output(act) || act < 0 || act > 8)) return -1;
-  const int ntn = (N + 255) / 256, ntiles = ((M + 255) / 256) * ntn;
-  const int grid = ntiles < rg_num_cus() ? ntiles : rg_num_cus();
-  RingNTArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, K, NB, n_valid, bias_col, ntn, ntiles};
-#define RNT_L(E, A_) hipLaunchKernelGGL((ring_nt_kernel<E, A_>), dim3(grid), dim3(RG_T), RG_LDS, stream, p)
-  if (epi == 2) RNT_L(2, 2);
-  else switch (act) {
-    case 0: RNT_L(0, 0); break; case 1: RNT_L(0, 1); break; case 2: RNT_L(0, 2); break;
-    case 3: RNT_L(0, 3); break; case 4: RNT_L(0, 4); break; case 6: RNT_L(0, 6); break;
-    default: RNT_L(0, 7); break;
-  }
-#undef RNT_L
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : (int)e;
 }

@@ -1,12 +1,12 @@
-"""Every NT GEMM code path (128x128 register-staged, 256x256 register-staged, 256x256 LDS-DMA
-ring, 256x256 8-phase, persistent 8-phase) against a torch fp32 reference, for the forward (act), dgrad (dact) and store epilogues."""
+"""Every NT GEMM code path (auto dispatch, 256x256 8-phase forced, 128x128 register-staged forced)
+against a torch fp32 reference, for the forward (act), dgrad (dact) and store epilogues."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 3, 4])
 @pytest.mark.parametrize("epi", ["act", "dact", "store"])
 @pytest.mark.parametrize("K", [320, 1024])
 def test_gemm_nt_variants(variant, epi, K):
@@ -37,27 +37,4 @@ def test_gemm_nt_variants(variant, epi, K):
         ref[:, :nv] = z[:, :nv] * (1 - h * h)
     else:
         ref[:, :NB] = z
-    torch.testing.assert_close(C.float(), ref, rtol=2e-2, atol=2e-2)
-
-
-@pytest.mark.parametrize("M,N,K,nv", [(300001, 256, 512, 200), (65536 * 4, 512, 1024, 500), (131072 + 5, 768, 128, 700)])
-def test_gemm_persistent_many_tiles(M, N, K, nv):
-    """Persistent 8-phase kernel with several tiles per block (tile stream crosses tiles, the
-    next tile's k-tiles 0/1 are prefetched during the epilogue) vs torch fp32."""
-    from shifu_amd.ops import _native as nat
-    torch.manual_seed(1)
-    dev = "cuda"
-    A = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
-    B = (torch.randn(nv, K, device=dev) * 0.05).to(torch.bfloat16)
-    C = torch.full((M, N), 7.0, device=dev).to(torch.bfloat16)
-    nat.call_hip("shifu_gemm_set_big", 5)
-    try:
-        nat.call_hip("shifu_gemm_nt", A, K, B, K, nv, C, N, None, 0, None, 0, None, 0,
-                     M, N, K, 0, 0, nv, 1, 0.0, nat.stream_of(A))
-        torch.cuda.synchronize()
-    finally:
-        nat.call_hip("shifu_gemm_set_big", 0)
-    ref = torch.zeros(M, N, device=dev)
-    ref[:, :nv] = torch.sigmoid(A.float() @ B.float().t())
-    ref[:, nv] = 1.0
     torch.testing.assert_close(C.float(), ref, rtol=2e-2, atol=2e-2)

@@ -127,66 +127,6 @@ def test_fused_head_matches_unfused(hidden, acts, loss, monkeypatch):
     assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
 
 
-@pytest.mark.parametrize("M,N,K,nv", [(70000 + 37, 512, 256, 500), (1000 + 5, 128, 128, 100)])
-def test_dgrad_transposed_epilogue(M, N, K, nv):
-    """EPI_DACT_T (swapped-operand MFMA + tr-read of H + transposed staging) writes exactly the
-    transpose of the row-major dgrad (EPI_DACT)."""
-    from shifu_amd.ops import _native as nat
-    torch.manual_seed(2)
-    A = (torch.randn(M, K, device="cuda") * 0.3).bfloat16()
-    B = (torch.randn(N, K, device="cuda") * 0.1).bfloat16()
-    H = torch.rand(M, N, device="cuda").bfloat16()
-    C = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-    nblk = (M + 63) // 64
-    CT = torch.full((nblk, N, 64), 7.0, dtype=torch.bfloat16, device="cuda")    # m-blocked D^T
-    st = nat.stream_of(A)
-    for epi, out, ld in ((1, C, N), (3, CT, N)):
-        nat.call_hip("shifu_gemm_nt", A, K, B, K, N, out, ld, None, 0, H, N, None, 0, M, N, K, epi, 0, nv, 0,
-                     0.1, st)
-    torch.cuda.synchronize()
-    full = CT.permute(1, 0, 2).reshape(N, nblk * 64)[:, :M]
-    torch.testing.assert_close(full.t().float(), C.float(), rtol=1e-2, atol=1e-3)
-    ref = (A.float() @ B.float().t()) * (H.float() * (1 - H.float()) + 0.1)
-    ref[:, nv:] = 0
-    torch.testing.assert_close(C.float(), ref, rtol=2e-2, atol=2e-2)
-
-
-@pytest.mark.parametrize("M", [70000 + 37, 4096 + 3])
-def test_wgrad_dt_matches_torch(M):
-    from shifu_amd.ops import _native as nat
-    torch.manual_seed(4)
-    Nv, Kx = 500, 1024
-    nblk = (M + 63) // 64
-    full = torch.randn(512, nblk * 64, device="cuda").bfloat16()
-    full[:, M:] = 1e4                     # stale columns past M must not be read
-    DT = full.reshape(512, nblk, 64).permute(1, 0, 2).contiguous()      # m-blocked [blk][n][64]
-    X = torch.randn(M, Kx, device="cuda").bfloat16()
-    G0 = torch.randn(Nv, Kx, device="cuda")
-    G = G0.clone()
-    nat.call_hip("shifu_wgrad_tn_dt", DT, 512, X, Kx, G, Kx, M, Nv, Kx, 64, nat.stream_of(X))
-    torch.cuda.synchronize()
-    ref = G0 + full[:Nv, :M].float() @ X.float()
-    torch.testing.assert_close(G, ref, rtol=2e-3, atol=2e-2)
-
-
-def test_trainer_transposed_layer1_deltas_match(monkeypatch):
-    """SHIFU_DGRAD_T=1 (transposed layer-1 deltas + DT wgrad) gives the default path's gradients."""
-    spec = MLPSpec(n_in=200, hidden=[300, 90], acts=["sigmoid", "tanh"], n_out=1)
-    x, y, s = _mk(spec, 9000 + 13, seed=6)
-    monkeypatch.setenv("SHIFU_DGRAD_T", "1")
-    a = MLPTrainer(spec, device="cuda", seed=1, chunk_rows=4096)
-    da = a.prepare(x, y, s)
-    a.grad.zero_(); a.err_acc.zero_(); a.accumulate_gradients(da)
-    monkeypatch.setenv("SHIFU_DGRAD_T", "0")
-    b = MLPTrainer(spec, device="cuda", seed=1, chunk_rows=4096)
-    b.params.flat.copy_(a.params.flat)
-    db = b.prepare(x, y, s)
-    b.grad.zero_(); b.err_acc.zero_(); b.accumulate_gradients(db)
-    torch.cuda.synchronize()
-    for va, vb in zip(a.params.views(a.grad), b.params.views(b.grad)):
-        assert float((va - vb).norm() / vb.norm().clamp(min=1e-12)) < 1e-2
-
-
 def test_bench_configuration_tracks_fp32_oracle():
     """The exact bench trainer configuration (bench.py: n_in 1000, hidden 500/200 sigmoid, RPROP,
     chunks >= 2^17 rows) so the 8-phase forward, the fused head, the ring wgrad (incl. the M % 32

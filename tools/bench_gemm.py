@@ -27,12 +27,12 @@ def main():
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--stages", type=int, default=1)
-    ap.add_argument("--big", type=int, default=1)
+    ap.add_argument("--big", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=0)
     ap.add_argument("--act", default="sigmoid")
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--ab", type=lambda t: (t.split("=")[0], int(t.split("=")[1])), nargs="*",
-                    help="interleaved A/B settings, e.g. dgrad_pf=0 dgrad_pf=1 out_waves=4096 out_waves=16384")
+                    help="interleaved A/B settings, e.g. interleave=0 interleave=1 out_waves=4096 out_waves=16384")
     ap.add_argument("--tune", type=lambda t: tuple(int(x) for x in t.split("=")), nargs="*")
     ap.add_argument("--out-waves", type=int, default=0)
     a = ap.parse_args()
@@ -107,19 +107,7 @@ def main():
         for setting in (a.ab or [None]):
             if setting is not None:
                 kind, val = setting
-                if kind == "dgrad_pf":
-                    nat.call_hip("shifu_gemm_set_tune", 0, val)
-                    ms = timeit(dgrad, a.iters)
-                    res.setdefault(f"dgrad1_pf{val}", []).append(round(ms, 4))
-                elif kind == "persist":        # auto path, persistent 8-phase on/off
-                    nat.call_hip("shifu_gemm_set_big", 0)
-                    nat.call_hip("shifu_gemm_set_tune", 1, val)
-                    for nm, f in (("pure", pure), ("fwd1", fwd1), ("fwd2", fwd2)):
-                        ms = timeit(f, a.iters)
-                        res.setdefault(f"{nm}_persist{val}", []).append(round(ms, 4))
-                    nat.call_hip("shifu_gemm_set_tune", 1, 0)
-                    nat.call_hip("shifu_gemm_set_big", a.big)
-                elif kind in ("interleave", "interleave8"):   # wgrad row-split layout (big 0 / big 3)
+                if kind in ("interleave", "interleave8"):   # wgrad row-split layout (big 0 / big 3)
                     nat.call_hip("shifu_gemm_set_big", 3 if kind == "interleave8" else 0)
                     nat.call_hip("shifu_gemm_set_tune", 2, val)
                     for nm, f in (("wgrad1", wgrad1), ("wgrad2", wgrad2)):
@@ -131,18 +119,7 @@ def main():
                     nat.call_hip("shifu_mlp_set_out_waves", val)
                     ms = timeit(output, a.iters)
                     res.setdefault(f"output_w{val}", []).append(round(ms, 4))
-    nblk = (M + 63) // 64
-    D1T = torch.empty(nblk * 512 * 64, device=dev, dtype=bf)
-
-    def dgrad_t():
-        nat.call_hip("shifu_gemm_nt", D2, 256, W2t, 256, 512, D1T, 512, None, 0, H1, 512, None, 0, M, 512, 256, 3,
-                     tanh, 500, 0, 0.0, st)
-
-    def wgrad1_dt():
-        nat.call_hip("shifu_wgrad_tn_dt", D1T, 512, X, 1024, G1, 1024, M, 500, 1024, spl(500, 1024), st)
-
-    todo = (("dgrad1_t", dgrad_t, 2 * M * 512 * 256), ("wgrad1_dt", wgrad1_dt, 2 * M * 512 * 1024),
-            ("output", output, 0),
+    todo = (("output", output, 0),
                             ("pure_gemm", pure, 2 * M * 512 * 1024), ("torch_mm", blaslt, 2 * M * 512 * 1024),
                             ("fwd1", fwd1, 2 * M * 512 * 1024), ("fwd2", fwd2, 2 * M * 256 * 512),
                             ("dgrad1", dgrad, 2 * M * 512 * 256), ("wgrad1", wgrad1, 2 * M * 512 * 1024),

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc counter CSVs (tools/pmc_ring.sh layout <dir>/<case>/g*/...csv):
+"""Summarise rocprofv3 --pmc counter CSVs (layout <dir>/<case>/g*/...csv, one counter group per g* run):
 per case, the mean per-dispatch value of every counter of the kernels whose name contains the
 case's kernel pattern, plus derived ratios.
 
@@ -10,7 +10,7 @@ import glob
 import os
 import sys
 
-DEFAULT = {"fwd1_ring": "ring_nt_kernel", "fwd1_old": "gemm_nt_8ph", "wgrad0_ring": "ring_tn_kernel",
+DEFAULT = {"fwd1": "gemm_nt_8ph", "wgrad0_ring": "ring_tn_kernel",
            "wgrad0_old": "wgrad_tn_kernel", "wgrad1_ring": "ring_tn_kernel"}
 
 
