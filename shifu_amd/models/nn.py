@@ -525,7 +525,8 @@ class MLPTrainer:
         self._drop_gen = torch.Generator().manual_seed(seed * 7919 + 11)
         self._wflat = self.params.flat
         self._scale = None
-        self._ws = None
+        self._ws = {}                  # chunk lane -> activations / deltas / ring slab workspace
+        self._lane2 = None             # (side stream, gradient buffer) of the second chunk lane
         self.last_error = float("nan")
 
     # --------------------------------------------------------------------------------------
@@ -558,9 +559,10 @@ class MLPTrainer:
         sd = None if s is None else torch.as_tensor(s, dtype=torch.float32).reshape(n).to(self.device)
         return TrainData(xp, y.contiguous(), sd, n)
 
-    def _workspace(self, rows: int):
-        if self._ws is not None and self._ws["rows"] >= rows:
-            return self._ws
+    def _workspace(self, rows: int, lane: int = 0):
+        cur = self._ws.get(lane)
+        if cur is not None and cur["rows"] >= rows:
+            return cur
         kp = self.spec.layer_kpad
         L = len(self.spec.hidden)
         ws = {"rows": rows, "acts": [], "deltas": [], "derivs": []}
@@ -577,7 +579,7 @@ class MLPTrainer:
             need = max(nat.hip().shifu_wgrad_ring_ws(rows, self.spec.hidden[l], kp[l]) for l in range(L))
             if need > 0:
                 ws["slab"] = torch.empty(need // 4, dtype=torch.float32, device=self.device)
-        self._ws = ws
+        self._ws[lane] = ws
         return ws
 
     def _weights_bf16(self):
@@ -614,8 +616,11 @@ class MLPTrainer:
             return
         if self.gpu:
             wb, wt = self._weights_bf16()
-            for r0 in range(row_lo, row_hi, self.chunk_rows):
-                r1 = min(row_hi, r0 + self.chunk_rows)
+            chunks = [(r0, min(row_hi, r0 + self.chunk_rows)) for r0 in range(row_lo, row_hi, self.chunk_rows)]
+            if self._two_lanes(len(chunks)):
+                self._accumulate_two_lanes(data, chunks, wb, wt)
+                return
+            for r0, r1 in chunks:
                 self._final_chunk = r1 >= row_hi
                 self._chunk_hip(data, r0, r1, wb, wt)
         else:
@@ -623,6 +628,45 @@ class MLPTrainer:
                 r1 = min(row_hi, r0 + self.chunk_rows)
                 self._final_chunk = r1 >= row_hi
                 self._chunk_torch(data, r0, r1)
+
+    def _two_lanes(self, nchunks: int) -> bool:
+        """Chunks alternate between two HIP streams (SHIFU_CHUNK_LANES, default 2) when there are
+        at least two device-resident chunks and no per-layer all-reduce overlap is armed: chunk
+        c+1's forward GEMM (8-phase, one 128-KiB block per CU) then shares the chip with chunk c's
+        memory-bound dgrad / store-bound epilogues instead of waiting for them."""
+        return nchunks >= 2 and self._reducer is None and int(os.environ.get("SHIFU_CHUNK_LANES", "2")) >= 2
+
+    def _accumulate_two_lanes(self, data: TrainData, chunks, wb, wt):
+        """Even chunks on the current stream into self.grad, odd chunks on a side stream into a
+        second gradient buffer (own workspace, own ring slab), summed in a fixed order at the end:
+        deterministic run to run.  The error sums are double atomics (order-free up to rounding)."""
+        main = torch.cuda.current_stream(self.device)
+        if self._lane2 is None:
+            self._lane2 = (torch.cuda.Stream(self.device), torch.zeros_like(self.grad))
+        side, g2 = self._lane2
+        side.wait_stream(main)                     # bf16 weights, zeroed grads, the rows
+        with torch.cuda.stream(side):
+            g2.zero_()
+        g1 = self.grad
+        # stagger (opt-in; measured 299 vs 308M rows/s free-running): chunk i's forward starts once chunk i-1's forward is done, so each
+        # lane's forward (fwd GEMMs + head) overlaps the other lane's backward (wgrad/dgrad)
+        stagger = os.environ.get("SHIFU_CHUNK_STAGGER", "0") == "1"
+        fwd_done = None
+        for i, (r0, r1) in enumerate(chunks):
+            self._final_chunk = False
+            st = main if i % 2 == 0 else side
+            if stagger and fwd_done is not None:
+                st.wait_event(fwd_done)
+            ev = torch.cuda.Event() if stagger else None
+            with torch.cuda.stream(st):
+                self.grad = g1 if i % 2 == 0 else g2
+                try:
+                    self._chunk_hip(data, r0, r1, wb, wt, lane=i % 2, fwd_event=ev)
+                finally:
+                    self.grad = g1
+            fwd_done = ev
+        main.wait_stream(side)
+        self.grad.add_(g2)
 
     def _grad_ready(self, layer: int) -> None:
         """Layer ``layer``'s gradient is final (last chunk's wgrad enqueued): launch the buckets that
@@ -645,12 +689,12 @@ class MLPTrainer:
         return bool(sp.n_out == 1 and sp.layer_kpad[L] <= 256 and a in ACT_DERIV_FROM_OUTPUT and
                     sp.acts[L - 1] != "ptanh" and sp.hidden[L - 1] <= 255)
 
-    def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None):
+    def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None, lane: int = 0, fwd_event=None):
         from ..ops import _native as nat
         sp, kp = self.spec, self.spec.layer_kpad
         L = len(sp.hidden)
         mc = r1 - r0
-        ws = self._workspace(min(self.chunk_rows, data.n))
+        ws = self._workspace(min(self.chunk_rows, data.n), lane)
         gv = self.params.views(self.grad)
         wv = self.params.views(self._wflat)
         x = data.x[r0:r1] if x_dev is None else x_dev
@@ -683,6 +727,8 @@ class MLPTrainer:
                          None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act],
                          ACT_IDS[sp.acts[L - 1]] if L else 2, LOSS_IDS[sp.loss], flat_spot(sp.out_act),
                          flat_spot(sp.acts[L - 1]) if L else 0.0, st)
+        if fwd_event is not None:
+            fwd_event.record()                     # forward + head of this chunk enqueued
         self._grad_ready(L)
         splits = self.wgrad_splits
         for l in range(L - 1, -1, -1):

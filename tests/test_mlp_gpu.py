@@ -179,3 +179,24 @@ def test_ring_wgrad_bitwise_reproducible():
     assert torch.equal(outs[0], outs[1])
     ref = D[:, :Nv].float().t() @ X.float()
     assert ((outs[0] - ref).abs().max() / ref.abs().max()).item() < 1e-4
+
+
+def test_two_chunk_lanes_match_one_lane(monkeypatch):
+    """Chunks alternating over two HIP streams (own workspaces, second gradient buffer summed at
+    the end) give the single-stream gradients and errors (up to float summation order: the output
+    layer's gradient and the short tail chunk's wgrad use float atomics in either mode)."""
+    spec = MLPSpec(n_in=300, hidden=[256, 90], acts=["sigmoid", "sigmoid"], n_out=1)
+    x, y, s = _mk(spec, 5 * 65536 + 77, seed=11)
+    grads, errs = {}, {}
+    for lanes in ("1", "2", "2"):
+        monkeypatch.setenv("SHIFU_CHUNK_LANES", lanes)
+        t = MLPTrainer(spec, device="cuda", seed=3, chunk_rows=65536)
+        d = t.prepare(x, y, s)
+        t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
+        torch.cuda.synchronize()
+        if lanes in grads:
+            assert float((grads[lanes] - t.grad).norm() / t.grad.norm()) < 1e-5
+        grads[lanes], errs[lanes] = t.grad.clone(), t.err_acc.clone()
+    g1, g2 = grads["1"], grads["2"]
+    assert float((g1 - g2).norm() / g1.norm()) < 1e-5
+    torch.testing.assert_close(errs["2"], errs["1"], rtol=1e-9, atol=1e-9)
