@@ -172,7 +172,7 @@ def sensitivity_1h(S: torch.Tensor, X: torch.Tensor, W1t: torch.Tensor, W2: torc
     n, H = S.shape
     F = X.shape[1]
     if not nchunks:                     # >= ~2048 blocks over (row chunks x 32-input groups)
-        fblocks = (F + 31) // 32
+        fblocks = (F + 31) // 32                   # SFT = 32 inputs per block
         nchunks = max(1, min((n + 63) // 64, -(-2048 // fblocks)))
     rc = nat.call_hip("shifu_sensitivity", S, S.stride(0), X, X.stride(0), W1t, W2, float(b2), base, n, F, H,
                       int(act1), int(act_o), nchunks, acc, nat.stream_of(S))
