@@ -785,8 +785,8 @@ class TreeTrainer:
         pred, scale = fuse
         self._leaf_done = True
         nat.call_hip("shifu_gbdt_partition_flag", d.bins, d.group_stride, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
-                     None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale), 1,
-                     nat.stream_of(d.bins))
+                     None, None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale),
+                     1, nat.stream_of(d.bins))
 
     def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots, leaf=None):
         d = self.data
@@ -801,17 +801,22 @@ class TreeTrainer:
             sf = torch.from_numpy(split_feat).to(self.dev)
             sb = torch.from_numpy(split_bin).to(self.dev)
             cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
-            flag = torch.empty(n, dtype=torch.int32, device=self.dev)
+            # left bits, one 64-bit word per 64 positions + the words' popcounts (exclusive-scanned):
+            # the inclusive left count at p is wpre[p / 64] + popcount of the word's bits <= p
+            nw = (n + 63) // 64
+            fbits = torch.empty(nw, dtype=torch.int64, device=self.dev)
+            wcnt = torch.empty(nw, dtype=torch.int32, device=self.dev)
             lv, (pred, scale) = leaf if leaf is not None else (None, (None, 0.0))
             # non-split nodes' rows get their leaf value here (fused GBT prediction update)
             nat.call_hip("shifu_gbdt_partition_flag", d.bins, d.group_stride, pos2row, pos_node, sf, sb, cl,
-                         self.is_cat_t, flag, n, self._nmod, pred, None if lv is None else lv[0], None, None,
+                         self.is_cat_t, fbits, wcnt, n, self._nmod, pred, None if lv is None else lv[0], None, None,
                          float(scale), 0, st)
-            cum = torch.cumsum(flag, 0, dtype=torch.int32)
+            wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
             # per-node: #left = cum[end-1] - cum[start-1]
-            idx_end = torch.from_numpy(np.maximum(ends - 1, 0)).to(self.dev)
-            idx_start = torch.from_numpy(np.maximum(starts - 1, 0)).to(self.dev)
-            cecb = torch.stack([cum[idx_end], cum[idx_start]]).cpu().numpy().astype(np.int64)   # one D2H sync
+            idx = torch.from_numpy(np.concatenate([np.maximum(ends - 1, 0), np.maximum(starts - 1, 0)])).to(self.dev)
+            cum2 = torch.empty(2 * nn, dtype=torch.int32, device=self.dev)
+            nat.call_hip("shifu_gbdt_bitrank", fbits, wpre, idx, 2 * nn, cum2, st)
+            cecb = cum2.view(2, nn).cpu().numpy().astype(np.int64)   # one D2H sync
             ce, cb = cecb[0], cecb[1]
             cb = np.where(starts > 0, cb, 0)
             ce = np.where(ends > starts, ce, cb)
@@ -828,7 +833,7 @@ class TreeTrainer:
             new_pn = torch.empty_like(pos_node)
             t = lambda a, dt=np.int32: torch.from_numpy(np.ascontiguousarray(a.astype(dt))).to(self.dev)  # noqa
             # tensors (not .data_ptr() of temporaries) so every buffer outlives the launch
-            nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, flag, cum, t(starts), t(nleft), t(cb),
+            nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, fbits, wpre, t(starts), t(nleft), t(cb),
                          sf, t(child_l), t(child_r), new_p2r, new_pn, n, st)
             # child slot ids follow the order of new_nodes built by the caller (left, right per split)
             return new_p2r, new_pn, ranges

@@ -51,7 +51,8 @@ HIP_SIGNATURES = {
     # gbdt_kernels.hip
     "shifu_gbdt_hist": "plpppp" "ipi" "dd" "l" "s",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
-    "shifu_gbdt_partition_flag": "plppppppp" "ll" "pppp" "fi" "s",
+    "shifu_gbdt_partition_flag": "plpppppppp" "ll" "pppp" "fi" "s",
+    "shifu_gbdt_bitrank": "pppip" "s",
     "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "l" "s",
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
     "shifu_gbdt_residual": "pppp" "p" "li" "s",

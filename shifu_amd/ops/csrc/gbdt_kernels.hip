@@ -407,7 +407,10 @@ struct PartArgs {
   const int* split_bin;         // [n_nodes] numeric: left iff bin <= split_bin
   const uint32_t* cat_left;     // [n_nodes][8] categorical left bitset (bin b left iff bit set)
   const uint8_t* is_cat;        // [F]
-  int* flag;                    // [N] out: 1 left, 0 right, for split nodes; 0 otherwise (nullable)
+  // out (nullable): left bit of every position (1 left, 0 right / not split) as one 64-bit word
+  // per 64 positions (ballot), and the word's popcount -- 1/32 of an int32 flag array, and the
+  // scatter ranks positions from the bits plus an exclusive scan of the per-word counts
+  unsigned long long* fbits; int* wcnt;
   long n;
   long nmod;                    // > 0: forest batch (pos2row = tree * nmod + row)
   // fused GBT prediction update (replaces walking every row through the finished tree):
@@ -417,9 +420,8 @@ struct PartArgs {
   float scale; int final_level;
 };
 
-__global__ void gbdt_partition_flag_kernel(PartArgs a) {
-  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.n) return;
+// left bit of position p (+ the fused prediction update)
+__device__ __forceinline__ int partition_flag(const PartArgs& a, long p) {
   const int node = a.pos_node[p];
   const int f = node >= 0 ? a.split_feat[node] : -1;
   int fl = 0;
@@ -433,12 +435,25 @@ __global__ void gbdt_partition_flag_kernel(PartArgs a) {
     const long v = a.pos2row[p];
     a.pred[a.nmod ? v % a.nmod : v] += a.scale * a.node_val[node];
   }
-  if (a.flag) a.flag[p] = fl;
+  return fl;
+}
+
+__global__ void __launch_bounds__(256) gbdt_partition_flag_kernel(PartArgs a) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int fl = p < a.n ? partition_flag(a, p) : 0;
+  if (a.fbits) {
+    const unsigned long long m = __ballot(fl);
+    if ((threadIdx.x & 63) == 0 && p < a.n) {
+      a.fbits[p >> 6] = m;
+      a.wcnt[p >> 6] = __popcll(m);
+    }
+  }
 }
 
 // scatter: positions of split nodes move to [start + rank_left] or [start + n_left + rank_right]
 struct ScatterArgs {
-  const int* pos2row; const int* pos_node; const int* flag; const int* cum;   // cum = inclusive cumsum(flag)
+  const int* pos2row; const int* pos_node;
+  const unsigned long long* fbits; const int* wpre;                          // left bits, exclusive word prefix
   const int* node_start; const int* node_nleft; const int* node_cum0;          // per node: start pos, #left, cum before start
   const int* split_feat;
   const int* child_left; const int* child_right;                               // new node slots
@@ -456,10 +471,13 @@ __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
     return;
   }
   const int s = a.node_start[node];
-  const int before = a.cum[p] - a.node_cum0[node];           // #left in [s, p]
+  const unsigned long long m = a.fbits[p >> 6];
+  const int lane = (int)(p & 63);
+  const int cum = a.wpre[p >> 6] + __popcll(lane == 63 ? m : m & ((2ull << lane) - 1));   // inclusive
+  const int before = cum - a.node_cum0[node];                // #left in [s, p]
   long np;
   int child;
-  if (a.flag[p]) { np = s + before - 1; child = a.child_left[node]; }
+  if ((m >> lane) & 1) { np = s + before - 1; child = a.child_left[node]; }
   else { np = s + a.node_nleft[node] + (int)(p - s) - before; child = a.child_right[node]; }
   a.new_pos2row[np] = a.pos2row[p];
   a.new_pos_node[np] = child;
@@ -566,25 +584,45 @@ SHIFU_API int shifu_gbdt_split(const void* slab, const int* node_items, int max_
 
 SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const int* pos2row, const int* pos_node,
                                         const int* split_feat, const int* split_bin, const void* cat_left,
-                                        const void* is_cat, int* flag, long n, long nmod, float* pred,
+                                        const void* is_cat, void* fbits, int* wcnt, long n, long nmod, float* pred,
                                         const float* node_val, const float* child_l_val,
                                         const float* child_r_val, float scale, int final_level,
                                         hipStream_t stream) {
   PartArgs a{(const uint8_t*)bins, gs, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
-             (const uint8_t*)is_cat, flag, n, nmod, pred, node_val, child_l_val, child_r_val, scale,
+             (const uint8_t*)is_cat, (unsigned long long*)fbits, wcnt, n, nmod, pred, node_val, child_l_val,
+             child_r_val, scale,
              final_level};
   hipLaunchKernelGGL(gbdt_partition_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
 
-SHIFU_API int shifu_gbdt_partition_scatter(const int* pos2row, const int* pos_node, const int* flag, const int* cum,
+SHIFU_API int shifu_gbdt_partition_scatter(const int* pos2row, const int* pos_node, const void* fbits, const int* wpre,
                                            const int* node_start, const int* node_nleft, const int* node_cum0,
                                            const int* split_feat, const int* child_left, const int* child_right,
                                            int* new_pos2row, int* new_pos_node, long n, hipStream_t stream) {
-  ScatterArgs a{pos2row, pos_node, flag, cum, node_start, node_nleft, node_cum0, split_feat, child_left,
+  ScatterArgs a{pos2row, pos_node, (const unsigned long long*)fbits, wpre, node_start, node_nleft, node_cum0, split_feat, child_left,
                 child_right, new_pos2row, new_pos_node, n};
   hipLaunchKernelGGL(gbdt_partition_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// inclusive left count cum[idx[i]] from the bits + word prefix (per-node boundaries for the host)
+__global__ void gbdt_bitrank_kernel(const unsigned long long* fbits, const int* wpre, const long* idx, int m, int* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const long q = idx[i];
+  const unsigned long long w = fbits[q >> 6];
+  const int lane = (int)(q & 63);
+  out[i] = wpre[q >> 6] + __popcll(lane == 63 ? w : w & ((2ull << lane) - 1));
+}
+
+SHIFU_API int shifu_gbdt_bitrank(const void* fbits, const int* wpre, const long* idx, int m, int* out,
+                                 hipStream_t stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(gbdt_bitrank_kernel, dim3((m + 255) / 256), dim3(256), 0, stream,
+                     (const unsigned long long*)fbits, wpre, idx, m, out);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
