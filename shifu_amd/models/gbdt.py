@@ -927,7 +927,8 @@ class TreeTrainer:
                 else:
                     g = out
                 scale = 1.0 if tid == 0 else c.learning_rate
-                fused = self.gpu and not (tid > 0 and c.dropout_rate > 0.0)
+                fused = (self.gpu and not (tid > 0 and c.dropout_rate > 0.0)
+                         and os.environ.get("SHIFU_GBT_FUSED_PRED", "1") != "0")
                 if fused:            # pred += scale * leaf value inside the partition passes
                     if tid == 0:
                         self.pred.zero_()
