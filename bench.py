@@ -253,11 +253,12 @@ def bench_stats(a, dev, info):
     per-column pass for every column: K4 exact equal-population cuts (qprep/qhist/qgather, 10 bins,
     EqualPositive over a binary target), K1+K2 bin histograms + moments with those cuts, distinct
     counts, and - for N > 1 - the all-reduces that merge the per-rank partials.  Columns are
-    processed in HBM-resident batches of 64 (51 GB of fp64 at 100M rows); each batch is generated
-    on the device before its timed section (generation time is reported, not counted).
+    processed in HBM-resident batches of 64 (51 GB of fp64 at 100M rows), two batches in flight on
+    one GPU (as `shifu stats` runs them); the batches are generated on the device before their
+    timed section (generation time is reported, not counted).
     value = rows x (all columns) per second over all ranks, i.e. full-table stats passes x rows."""
     from shifu_amd.algos import quantile as Q
-    from shifu_amd.algos.stats import batch_histograms
+    from shifu_amd.algos.stats import batch_histograms, run_lanes
     from shifu_amd.parallel import dist
     n, F, C = a.rows, a.cols, 64
     g = torch.Generator(device=dev).manual_seed(99 + info.rank)
@@ -271,27 +272,36 @@ def bench_stats(a, dev, info):
         if dev.type == "cuda":
             torch.cuda.synchronize()
 
+    # column batches in flight together (algos/stats.run_lanes: one HIP stream + host thread per
+    # batch, so one batch's host planning overlaps the other's kernels), as `shifu stats` runs them
+    lanes = 1 if multi else int(os.environ.get("SHIFU_STATS_LANES", "2"))
+
+    def stats_of(v):
+        bounds, _ = Q.column_cuts(v, y, w, 10, "EqualPositive", True, reduce=red, allgather=cat)
+        return bounds, batch_histograms(v, y, w, bounds, True)
+
     def one_pass(step):
         t_stats = t_gen = 0.0
         nb_total = 0
-        for b0 in range(0, F, C):
-            c = min(C, F - b0)
+        starts = list(range(0, F, C))
+        for g0 in range(0, len(starts), lanes):
+            group = starts[g0: g0 + lanes]
             t0 = time.perf_counter()
-            v = _stats_batch(c, n, b0, dev, 1000 * step + b0 + 7 * info.rank)
+            vs = [_stats_batch(min(C, F - b0), n, b0, dev, 1000 * step + b0 + 7 * info.rank) for b0 in group]
             sync()
             dist.barrier()
             t1 = time.perf_counter()
-            bounds, distinct = Q.column_cuts(v, y, w, 10, "EqualPositive", True, reduce=red, allgather=cat)
-            res = batch_histograms(v, y, w, bounds, True)
-            if multi:
-                h = np.concatenate([np.concatenate([r[0], r[1], r[2], r[3]]) for r in res])
-                dist.all_reduce_np(h)
+            outs = run_lanes(stats_of, vs, dev, lanes)
+            for bounds, res in outs:
+                if multi:
+                    h = np.concatenate([np.concatenate([r[0], r[1], r[2], r[3]]) for r in res])
+                    dist.all_reduce_np(h)
+                nb_total += sum(len(b) + 1 for b in bounds)
             sync()
             dist.barrier()
             t_stats += time.perf_counter() - t1
             t_gen += t1 - t0
-            nb_total += sum(len(b) + 1 for b in bounds)
-            del v
+            del vs
         return t_stats, t_gen, nb_total
 
     for i in range(a.warmup):

@@ -204,6 +204,52 @@ def batch_histograms(vals: torch.Tensor, y: torch.Tensor, w: torch.Tensor, bound
     return out
 
 
+def run_lanes(fn, items, dev, lanes: int | None = None):
+    """``[fn(item) for item in items]`` with ``lanes`` column batches in flight (worker threads, one
+    HIP stream each): a batch's host planning between its K4 passes (~20 % of a 64-column batch at
+    100M rows, profiles/r2/stats_host_vs_device_per_batch_r2r.txt) overlaps the other batch's
+    kernels.  Single-process only (the data-parallel passes issue collectives, whose order must
+    match across ranks); ``SHIFU_STATS_LANES`` (default 2) sets the width."""
+    from ..parallel import dist
+    lanes = int(os.environ.get("SHIFU_STATS_LANES", "2")) if lanes is None else lanes
+    if lanes <= 1 or len(items) <= 1 or dev.type != "cuda" or dist.info().world_size > 1:
+        return [fn(it) for it in items]
+    import threading
+    main = torch.cuda.current_stream(dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(lanes)]
+    for st in streams:
+        st.wait_stream(main)                  # inputs produced on the caller's stream
+    results, errors = [None] * len(items), []
+    order = iter(range(len(items)))
+    lock = threading.Lock()
+
+    dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+
+    def worker(k):
+        try:
+            torch.cuda.set_device(dev_index)
+            with torch.cuda.stream(streams[k]):
+                while not errors:
+                    with lock:
+                        i = next(order, None)
+                    if i is None:
+                        return
+                    results[i] = fn(items[i])
+        except BaseException as e:            # re-raised on the caller's thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(k,), daemon=True) for k in range(min(lanes, len(items)))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for st in streams:
+        main.wait_stream(st)
+    if errors:
+        raise errors[0]
+    return results
+
+
 def parity_algorithm(mc):
     """``shifu.stats.binning.parity=true`` + binningAlgorithm SPDT/SPDTI/MunroPat/MunroPatI: the
     reference's streaming-sketch cuts (BinningDataUDF semantics: every valid value of the column in
@@ -323,15 +369,18 @@ def compute_column_stats(mc, ccs, md, device=None, columns=None, gpu_batch: int 
         from . import quantile as Q
         yt = torch.as_tensor(np.asarray(y, np.float32), device=dev)
         wt = torch.as_tensor(np.asarray(w, np.float64), device=dev)
-        for b0 in range(0, len(numeric), gpu_batch):
-            batch = numeric[b0: b0 + gpu_batch]
+
+        def one_batch(batch):
             vals = upload_columns([md.table[c.name].numeric() for c in batch], dev)
             bounds, distinct = Q.column_cuts(vals, yt, wt, n_bins, method, binary, num_thr)
             if parity:
                 bounds = [B.sketch_boundaries(md.table[c.name].numeric(), n_bins, parity) for c in batch]
             if total <= EXACT_DISTINCT_ROWS:
                 distinct = exact_distinct(vals, num_thr)
-            res = stats_ops.column_stats(vals, yt, wt, bounds, binary, num_thr)
+            return bounds, distinct, stats_ops.column_stats(vals, yt, wt, bounds, binary, num_thr)
+
+        batches = [numeric[b0: b0 + gpu_batch] for b0 in range(0, len(numeric), gpu_batch)]
+        for batch, (bounds, distinct, res) in zip(batches, run_lanes(one_batch, batches, dev)):
             for c, bnd, (cpos, cneg, wpos, wneg, mom), dc in zip(batch, bounds, res, distinct):
                 _finish_numeric(c, binary, bnd, cpos, cneg, wpos, wneg, mom, total, dc)
         return ccs

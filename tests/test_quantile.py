@@ -179,3 +179,29 @@ def test_pack_sel_kernel_matches_cpu():
             a = pack_sel(y, mode).numpy()
             b = pack_sel(y.cuda(), mode).cpu().numpy()[: a.size]
             assert np.array_equal(a, b), (n, mode)
+
+
+@pytest.mark.gpu
+def test_stats_lanes_equal_sequential():
+    """Column batches run two at a time on separate HIP streams (algos/stats.run_lanes, host
+    threads) give exactly the sequential cuts, distinct counts and bin histograms."""
+    from shifu_amd.algos.stats import batch_histograms, run_lanes
+    rng = np.random.default_rng(5)
+    n = 150_001
+    dev = torch.device("cuda")
+    batches = [torch.as_tensor(_columns(n, rng), device=dev) for _ in range(3)]
+    y = torch.as_tensor((rng.random(n) < 0.3).astype(np.float32), device=dev)
+    w = torch.as_tensor(rng.integers(1, 5, size=n).astype(float), device=dev)
+
+    def fn(v):
+        bounds, distinct = Q.column_cuts(v, y, w, 10, "EqualPositive", True)
+        return bounds, distinct, batch_histograms(v, y, w, bounds, True)
+
+    seq = run_lanes(fn, batches, dev, lanes=1)
+    par = run_lanes(fn, batches, dev, lanes=2)
+    for (b1, d1, h1), (b2, d2, h2) in zip(seq, par):
+        assert [list(b) for b in b1] == [list(b) for b in b2]
+        assert list(d1) == list(d2)
+        for r1, r2 in zip(h1, h2):
+            for a1, a2 in zip(r1, r2):
+                np.testing.assert_array_equal(np.asarray(a1), np.asarray(a2))
