@@ -648,8 +648,9 @@ class MLPTrainer:
         with torch.cuda.stream(side):
             g2.zero_()
         g1 = self.grad
-        # stagger (opt-in; measured 299 vs 308M rows/s free-running): chunk i's forward starts once chunk i-1's forward is done, so each
-        # lane's forward (fwd GEMMs + head) overlaps the other lane's backward (wgrad/dgrad)
+        # stagger (opt-in; measured 299 vs 308M rows/s free-running): chunk i's forward starts once
+        # chunk i-1's forward is done, so each lane's forward (fwd GEMMs + head) overlaps the other
+        # lane's backward (wgrad/dgrad)
         stagger = os.environ.get("SHIFU_CHUNK_STAGGER", "0") == "1"
         fwd_done = None
         for i, (r0, r1) in enumerate(chunks):
