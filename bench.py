@@ -21,6 +21,7 @@ per GPU (``gbdt_rounds_per_s`` / ``gbdt_ms_per_round``; ``--gbdt-steps 0`` skips
     python bench.py --model varsel  # 10k-feature MLP + SE varselect config
     python bench.py --model lr      # LR 100k-row CSV local (CPU plumbing) config
     python bench.py --model stats   # stats (K4 exact cuts + histograms) 100M x 1000 per GPU
+    python bench.py --model treeinfer   # eval scoring, 500-tree depth-7 GBT, 20M x 1000 fp64 rows
 """
 from __future__ import annotations
 
@@ -332,6 +333,53 @@ def bench_stats(a, dev, info):
     }
 
 
+def bench_treeinfer(a, dev, info):
+    """K13: eval-time scoring of a 500-tree depth-7 GBT (IndependentTreeModel.computeRegressionScore,
+    J/core/dtrain/dt/IndependentTreeModel.java:387-441) over rows x 1000 raw fp64 columns resident
+    in HBM (feature-major).  One step = every row scored by every tree (random-init trees with
+    random raw-value thresholds; synthetic N(0,1) inputs)."""
+    from shifu_amd.formats.tree_format import CONTINUOUS, Node, Split, TreeModelFile, TreeRecord
+    from shifu_amd.scoring.tree_ensemble import FlatEnsemble
+    rng = np.random.default_rng(7)
+    n_trees, depth, C = 500, 7, a.cols
+
+    def grow(d):
+        nd = Node(0)
+        if d == depth:
+            nd.predict = float(rng.normal())
+            return nd
+        nd.split = Split(int(rng.integers(0, C)), CONTINUOUS, threshold=float(rng.normal() * 0.5))
+        nd.left, nd.right = grow(d + 1), grow(d + 1)
+        return nd
+    cols = list(range(C))
+    m = TreeModelFile("GBT", "squared", False, False, C, {c: 0.0 for c in cols}, {c: f"c{c}" for c in cols}, {},
+                      {c: c for c in cols}, [[TreeRecord(t, 0, grow(0), 0.1) for t in range(n_trees)]])
+    ens = FlatEnsemble(m, 0, cols, dev)
+    XT = torch.empty(C, a.rows, dtype=torch.float64, device=dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    for c0 in range(0, C, 64):
+        XT[c0:c0 + 64].normal_(generator=g)
+    X = XT.t()                                  # [N, C] view of the feature-major matrix (no copy)
+    for _ in range(a.warmup):
+        ens.score(X)
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        s = ens.score(X)
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    dt = time.perf_counter() - t0
+    ms = dt / a.steps * 1e3
+    return {
+        "metric": "GBT scoring rows/s (500 trees depth 7, 1000 raw fp64 columns)", "value": a.rows / (ms / 1e3),
+        "unit": "rows/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp64",
+        "data": "synthetic N(0,1) inputs, random-init trees",
+        "config": {"model": "GBT 500 trees depth 7", "global_batch": a.rows, "seq_len": None, "n_cols": C,
+                   "parallelism": "single"},
+        "node_visits_per_s": a.rows * n_trees * depth / (ms / 1e3), "score_checksum": float(s.sum()),
+    }
+
+
 def bench_lr(a, dev, info):
     """BASELINE config 1: logistic regression on a 100k-row CSV, local mode, CPU only (the
     plumbing path): shifu init -> stats -> norm -> train on a generated model set.  One step =
@@ -375,7 +423,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr", "stats"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr", "stats", "treeinfer"])
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per GPU (default 125M on GPU: 256 GB of bf16 rows resident in one MI355X's "
                          "288 GB HBM, so 8 GPUs hold the metric's 1B-row x 1k-col table)")
@@ -398,6 +446,7 @@ def main():
         a.cols = 10_000
     if a.rows is None:
         a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000, "stats": 100_000_000 if gpu else 5_000,
+                  "treeinfer": 20_000_000 if gpu else 5_000,
                   "gbdt": 100_000_000 if gpu else 20_000}.get(a.model, 125_000_000 if gpu else 20_000)
     if a.model == "gbdt":
         res = bench_gbdt(a, dev, info)
@@ -406,6 +455,8 @@ def main():
         out = bench_varsel(a, dev, info)
     elif a.model == "lr":
         out = bench_lr(a, dev, info)
+    elif a.model == "treeinfer":
+        out = bench_treeinfer(a, dev, info)
     elif a.model == "stats":
         if not gpu and a.cols == 1000:
             a.cols = 64

@@ -430,6 +430,11 @@ def compute_psi(mc, ccs, md, unit_column: str, unit_stats_path: str | None = Non
     U = len(units)
     uidx = {u: i for i, u in enumerate(units)}
     ucode = np.array([uidx[u] for u in units_s], dtype=np.int64) if len(units_s) else np.zeros(0, np.int64)
+    from ..utils.device import default_device
+    dev = default_device()
+    if dev.type == "cuda":                     # K17 on the device: keyed_hist (scoring_kernels.hip)
+        from ..ops.stats_ops import keyed_hist
+        ucode_d = torch.as_tensor(ucode).to(dev)
     cols, counts = [], []
     for cc in ccs:
         if cc.is_target() or cc.is_meta() or cc.name not in md.table:
@@ -450,10 +455,19 @@ def compute_psi(mc, ccs, md, unit_column: str, unit_stats_path: str | None = Non
             if not bb:
                 continue
             v = col.numeric()
-            bidx = B.bin_index_numeric(v, bb)
             nb = len(bb) + 1
+            if dev.type == "cuda":
+                bidx = B.bin_index_torch(torch.as_tensor(np.asarray(v, np.float64)).to(dev),
+                                         torch.as_tensor(np.asarray(bb, np.float64)).to(dev))
+            else:
+                bidx = B.bin_index_numeric(v, bb)
             contrib = np.where(np.isnan(v), 0.0, v)
-        cnt = np.bincount(ucode * nb + bidx, minlength=U * nb).astype(np.float64)
+        if dev.type == "cuda":                 # exact integer (unit, bin) counts on the device
+            cnt = keyed_hist(ucode_d * nb + torch.as_tensor(bidx).to(dev), U * nb)[0][0].cpu().numpy()
+        else:
+            cnt = np.bincount(ucode * nb + bidx, minlength=U * nb).astype(np.float64)
+        # unit value sums stay an in-order fp64 host sum: they are printed at full double
+        # precision in the unit stats (Double.toString), so no fixed-point rounding here
         vsum = np.bincount(ucode, weights=contrib, minlength=U).astype(np.float64)
         cols.append((cc, nb))
         counts.append(np.concatenate([cnt, vsum]))

@@ -179,3 +179,38 @@ def sensitivity_1h(S: torch.Tensor, X: torch.Tensor, W1t: torch.Tensor, W2: torc
     if rc:
         raise RuntimeError(f"shifu_sensitivity failed rc={rc}")
     return acc
+
+
+def keyed_hist(keys: torch.Tensor, K: int, weights: torch.Tensor | None = None):
+    """Keyed counts (K17 PSI (unit, bin) counts, K18 post-train per-bin score sums) through
+    ``scoring_kernels.hip: keyed_hist_kernel``.
+
+    keys [F, N] or [N] int (rows with key < 0 or >= K are skipped; a 1-D key vector is shared by
+    every column of ``weights``); weights None, [N] (shared) or [F, N] fp64.
+    -> (counts [F, K] fp64, weighted sums [F, K] fp64 | None).  Weighted sums are accumulated as
+    int64 fixed point (scale from max |w| and N), so they are order-independent: identical run to
+    run and to a fixed-point host sum."""
+    nat.require_gpu_native()
+    dev = keys.device
+    shared_keys = keys.dim() == 1
+    N = keys.shape[-1]
+    F = 1 if shared_keys and (weights is None or weights.dim() == 1) else \
+        (weights.shape[0] if shared_keys else keys.shape[0])
+    k = keys.to(torch.int32).contiguous()
+    ks = 0 if shared_keys else N
+    w, ws, scale = None, 0, 0.0
+    if weights is not None:
+        w = weights.to(device=dev, dtype=torch.float64).contiguous()
+        ws = 0 if w.dim() == 1 else N
+        amax = float(w.abs().max()) if w.numel() else 0.0
+        if amax > 0:
+            # |sum| <= N * amax < 2^62  ->  scale = 2^(62 - ceil(log2(N * amax)))
+            scale = math.ldexp(1.0, 62 - max(1, math.ceil(math.log2(max(N, 1) * amax))))
+    cnt = torch.zeros(F, K, dtype=torch.int64, device=dev)
+    wsum = torch.zeros(F, K, dtype=torch.int64, device=dev) if w is not None else None
+    if N and K:
+        nat.call_hip("shifu_keyed_hist", k, ks, w, ws, N, F, int(K), scale, cnt, wsum, nat.stream_of(k))
+    c = cnt.to(torch.float64)
+    if wsum is None:
+        return c, None
+    return c, (wsum.to(torch.float64) / scale if scale else torch.zeros_like(c))

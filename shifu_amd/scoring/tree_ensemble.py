@@ -78,9 +78,36 @@ class FlatEnsemble:
         self.lrs = torch.tensor(lr_, dtype=torch.float64, device=dev)
         self.paths = np.array(paths, dtype=object)     # L/R path from the root of every node
 
+    # ---- HIP path (K13: scoring_kernels.hip tree_infer_kernel) ----------------------------
+    def _hip_tables(self):
+        if getattr(self, "_ht", None) is None:
+            node = torch.stack([self.feat, self.left, self.right,
+                                torch.where(self.iscat, self.catrow, torch.full_like(self.catrow, -1))], 1)
+            self._ht = (node.to(torch.int32).contiguous(), self.thr.contiguous(), self.value.contiguous(),
+                        self.catlut.to(torch.uint8).contiguous(), self.roots.to(torch.int32).contiguous(),
+                        self.lrs.contiguous())
+        return self._ht
+
+    def _hip_walk(self, X: torch.Tensor, want_leaves: bool):
+        """One kernel launch for all (row, tree) pairs of the chunk: -> (bag score, leaf ids | None)."""
+        from ..ops import _native
+        _native.require_gpu_native()
+        n, T = X.shape[0], int(self.roots.numel())
+        XT = X.to(torch.float64).t().contiguous()             # feature-major [C, N]: coalesced at the root
+        node, thr, value, lut, roots, lrs = self._hip_tables()
+        groups = max(1, min(T, -(-2048 // max(1, -(-n // 256)))))
+        groups = -(-T // -(-T // groups))                     # every group owns >= 1 tree
+        part = torch.empty(groups, n, dtype=torch.float64, device=X.device)
+        leaf = torch.empty(n, T, dtype=torch.int32, device=X.device) if want_leaves else None
+        _native.call_hip("shifu_tree_infer", XT, n, 1, n, node, thr, value, lut, lut.shape[1], roots, lrs, T,
+                         max(self.depth, 0), groups, part, leaf, _native.stream_of(X))
+        return part.sum(0), leaf
+
     @torch.no_grad()
     def leaves(self, X: torch.Tensor) -> torch.Tensor:
         """X [N, C] float64 (numeric raw values, categorical indices) -> leaf node ids [N, T]."""
+        if X.is_cuda and X.shape[0] and self.roots.numel():
+            return self._hip_walk(X, True)[1].long()
         n = X.shape[0]
         node = self.roots.unsqueeze(0).expand(n, -1).clone()
         rows = torch.arange(n, device=self.dev).unsqueeze(1)
@@ -102,8 +129,11 @@ class FlatEnsemble:
     @torch.no_grad()
     def score(self, X: torch.Tensor) -> torch.Tensor:
         """Bag score: GBT -> sum lr*leaf (raw), RF -> weighted mean of leaves."""
-        lv = self.value[self.leaves(X)]                       # [N, T]
-        s = (lv * self.lrs).sum(1)
+        if X.is_cuda and X.shape[0] and self.roots.numel():
+            s = self._hip_walk(X, False)[0]
+        else:
+            lv = self.value[self.leaves(X)]                   # [N, T]
+            s = (lv * self.lrs).sum(1)
         if self.model.algorithm.upper() != "GBT":
             s = s / self.lrs.sum().clamp(min=1e-300)
         return s
@@ -146,7 +176,8 @@ class TreeScorer:
         return torch.from_numpy(X).to(self.dev)
 
     @torch.no_grad()
-    def score_bags(self, X: torch.Tensor, chunk: int = 1 << 16) -> np.ndarray:
+    def score_bags(self, X: torch.Tensor, chunk: int | None = None) -> np.ndarray:
+        chunk = chunk or ((1 << 20) if X.is_cuda else (1 << 16))
         out = []
         for e in self.ens:
             parts = [e.score(X[i: i + chunk]) for i in range(0, X.shape[0], chunk)]

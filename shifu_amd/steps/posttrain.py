@@ -10,15 +10,50 @@ score is below the column's best bin.
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 from ..algos.normalize import _bin_num
 from ..formats import tree_format
 from ..parallel import dist
 from ..scoring.model_runner import ModelRunner, list_model_files
+from ..utils.device import default_device
 from ..utils.log import get_logger
 from .base import ModelSet, _writer, shard_model_data
 
 _log = get_logger("steps.posttrain")
+
+
+def _bin_score_sums_host(c, col, score):
+    b = _bin_num(c, col)
+    nb = c.n_bins()                            # incl. the missing bin (last)
+    b = np.where(b < 0, nb - 1, np.minimum(b, nb - 1))
+    return np.stack([np.bincount(b, weights=score, minlength=nb), np.bincount(b, minlength=nb).astype(np.float64)])
+
+
+def _bin_score_sums_gpu(used, table, score, dev, batch: int = 64):
+    """K18 on the device: numeric bin indices by ``torch.bucketize`` on the HBM copy of the
+    column, categorical through the host LUT, then one ``keyed_hist`` launch per column batch
+    (per-bin row counts + fixed-point score sums, ``scoring_kernels.hip``)."""
+    from ..algos.binning import bin_index_torch
+    from ..ops.stats_ops import keyed_hist
+    sc = torch.as_tensor(np.asarray(score, dtype=np.float64)).to(dev)
+    out = []
+    for i in range(0, len(used), batch):
+        cs = used[i: i + batch]
+        nbs = [c.n_bins() for c in cs]
+        keys = torch.empty(len(cs), sc.numel(), dtype=torch.int32, device=dev)
+        for j, c in enumerate(cs):
+            col = table[c.name]
+            if c.is_categorical():
+                b = torch.as_tensor(_bin_num(c, col)).to(dev)
+            else:
+                bb = torch.as_tensor(np.asarray(c.bin_boundary or [float("-inf")], np.float64)).to(dev)
+                b = bin_index_torch(torch.as_tensor(col.numeric().astype(np.float64)).to(dev), bb)
+            keys[j] = torch.where(b < 0, nbs[j] - 1, torch.clamp(b, max=nbs[j] - 1)).to(torch.int32)
+        cnt, ssum = keyed_hist(keys, max(nbs), sc)
+        cnt, ssum = cnt.cpu().numpy(), ssum.cpu().numpy()
+        out.extend(np.stack([ssum[j, :nb], cnt[j, :nb]]) for j, nb in enumerate(nbs))
+    return out
 
 
 def run_posttrain(root: str = ".", device=None) -> int:
@@ -34,13 +69,9 @@ def run_posttrain(root: str = ".", device=None) -> int:
     res = runner.score(md.table, 1000.0)
     score = np.asarray(res["mean"] if "mean" in res else res["class_scores"].max(1))
     used = [c for c in cols if c.name in md.table]
-    parts = []
-    for c in used:
-        b = _bin_num(c, md.table[c.name])
-        nb = c.n_bins()                        # incl. the missing bin (last)
-        b = np.where(b < 0, nb - 1, np.minimum(b, nb - 1))
-        parts.append(np.stack([np.bincount(b, weights=score, minlength=nb),
-                               np.bincount(b, minlength=nb).astype(np.float64)]))
+    dev = torch.device(device) if device is not None else default_device()
+    parts = _bin_score_sums_gpu(used, md.table, score, dev) if dev.type == "cuda" else \
+        [_bin_score_sums_host(c, md.table[c.name], score) for c in used]
     if used and dist.info().world_size > 1:
         flat = dist.all_reduce_np(np.concatenate([p.reshape(-1) for p in parts]))
         off = 0
