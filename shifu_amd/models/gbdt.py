@@ -282,7 +282,12 @@ class TreeTrainer:
         """(per-row bag weight or None when every row is in the bag, sig * bag weight)."""
         c = self.cfg
         n = self.data.n
-        sig = self.data.sig if self.data.sig is not None else torch.ones(n, device=self.dev)
+        if self.data.sig is not None:
+            sig = self.data.sig
+        else:                  # one persistent tensor: an unchanged weight vector keeps the root cache valid
+            if getattr(self, "_unit_w", None) is None or self._unit_w.numel() != n:
+                self._unit_w = torch.ones(n, device=self.dev)
+            sig = self._unit_w
         rate = c.bagging_sample_rate
         if c.sample_with_replacement or (not c.is_gbt and c.sample_with_replacement):
             sub = torch.poisson(torch.full((n,), rate, device=self.dev), generator=self.tgen)
@@ -554,10 +559,13 @@ class TreeTrainer:
         t0 = time.perf_counter()
         if len(items):
             it = torch.from_numpy(items).to(self.dev)
-            slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
-            p2r = None if self._root_level else pos2row      # root: positions are rows
-            nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, g, it, len(items), slab, F,
-                         self.scale_w, self.scale_g, self._nmod, st)
+            if self._root_level and self._nmod == 0 and ROOT_U32:
+                slab = self._root_slab(items, it, w, g, st)
+            else:
+                slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
+                p2r = None if self._root_level else pos2row      # root: positions are rows
+                nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, g, it, len(items), slab, F,
+                             self.scale_w, self.scale_g, self._nmod, 0, st)
         else:
             slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
         built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
@@ -596,6 +604,25 @@ class TreeTrainer:
         co = None if cat_order is None else cat_order.cpu().numpy()
         return best, co
 
+    def _root_slab(self, items, it, w, g, st):
+        """Root-level slabs from the two u32 histogram modes: sum w (mode 1) is built once and
+        kept while the weight tensor is the same unmodified object (no bagging sub-sample, the
+        usual GBT case), sum w*g (mode 2) is rebuilt every tree.  One u32 LDS atomic per (row,
+        feature) instead of the packed u64: about half the root level's histogram time."""
+        from ..ops import _native as nat
+        d = self.data
+        key = (w._version, self.scale_w, hash(items.tobytes()), d.bins.data_ptr())
+        c = getattr(self, "_root_cache", None)
+        if c is None or c[0] is not w or c[1] != key:
+            slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
+            nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, None, w, g, it, len(items), slab, self.F,
+                         self.scale_w, self.scale_g, 0, 1, st)
+            self._root_cache = (w, key, slab)          # holds w: its storage cannot be re-issued
+        slab = self._root_cache[2]
+        nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, None, w, g, it, len(items), slab, self.F,
+                     self.scale_w, self.scale_g, 0, 2, st)
+        return slab
+
     # ---- native multi-class RF (Entropy / Gini over C classes) ------------------------------
     def _class_hist(self, nodes, n_built, gc, w, pos2row, hist_prev, hist):
         """One class's (sum w, sum w*[y == c]) histograms of every node of the level: the packed
@@ -613,7 +640,7 @@ class TreeTrainer:
                 slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
                 p2r = None if self._root_level else pos2row
                 nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, gc, it, len(items), slab, F,
-                             self.scale_w, self.scale_g, self._nmod, st)
+                             self.scale_w, self.scale_g, self._nmod, 0, st)
                 built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
                 feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
                 cand = torch.zeros(len(nodes), F, 8, dtype=torch.float32, device=self.dev)
@@ -725,7 +752,10 @@ class TreeTrainer:
                 continue
             b = bins[rows % d.n]                             # [m, F] (virtual rows of a forest batch)
             qw = torch.round(w[rows].double() * self.scale_w).long()
-            qg = torch.round((w[rows] * g[rows]).float().double() * self.scale_g).long()
+            if self._root_level and self._nmod == 0 and ROOT_U32:    # the u32 root mode's coarser grid
+                qg = torch.round((w[rows] * g[rows]).float().double() * (self.scale_g / ROOT_G_DIV)).long() * ROOT_G_DIV
+            else:
+                qg = torch.round((w[rows] * g[rows]).float().double() * self.scale_g).long()
             idx = (torch.arange(F).unsqueeze(0) * NB + b).reshape(-1)
             hw = torch.zeros(F * NB, dtype=torch.int64)
             hg = torch.zeros(F * NB, dtype=torch.int64)
@@ -1133,6 +1163,10 @@ def _slot_key(z):
 
 
 W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histogram fields)
+# root level of a single-tree (non-forest) build: u32 histogram modes, w*g on a grid 2^3 coarser
+# (gbdt_kernels.hip GSH32); SHIFU_GBDT_ROOT_U32=0 keeps the packed u64 kernel everywhere
+ROOT_U32 = os.environ.get("SHIFU_GBDT_ROOT_U32", "1") != "0"
+ROOT_G_DIV = 8
 
 
 def _pack_scale(max_abs: float, bits: int) -> float:

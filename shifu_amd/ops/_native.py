@@ -49,7 +49,7 @@ HIP_SIGNATURES = {
     "shifu_ring_set_mf": "i",
     "shifu_ring_set_dmamma": "i",
     # gbdt_kernels.hip
-    "shifu_gbdt_hist": "plpppp" "ipi" "dd" "l" "s",
+    "shifu_gbdt_hist": "plpppp" "ipi" "dd" "l" "i" "s",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
     "shifu_gbdt_partition_flag": "plpppppppp" "ll" "pppp" "fi" "s",
     "shifu_gbdt_bitrank": "pppip" "s",

@@ -67,10 +67,20 @@ __device__ __forceinline__ void unpack_add(unsigned long long v, long long& aw, 
   aw += (long long)((v - (unsigned long long)gq) >> PACK_G);
 }
 
-template <bool PF, int HU>
+// Root-level u32 modes (MODE 1 = sum w only, MODE 2 = sum w*g only): LDS u32 atomics move half
+// the bytes of the packed u64 and run at ~2x its rate (profiles/microbench_lds_atomics.txt).  The
+// root's sum-w histogram does not change between boosting rounds while the row weights do not,
+// so the trainer builds it once (MODE 1) and re-builds only sum w*g (MODE 2) every round.  MODE 2
+// quantises w*g at scale_g / 2^GSH32 (|q| < 2^20; 2048 rows between unpacks keep a bin's sum
+// inside int32) and unpacks it shifted back to the scale_g grid, so the slab has the same units
+// as the packed kernel's and the histogram subtraction below the root stays exact.
+constexpr int GSH32 = 3;
+
+template <bool PF, int HU, int MODE>
 __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
-  constexpr int HFLUSH = 4096 / (RPP * HU);     // passes between unpacks (4096 rows)
+  constexpr int HFLUSH = (MODE == 0 ? 4096 : 2048) / (RPP * HU);   // passes between unpacks
   extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];   // [2][NB][16]
+  uint32_t* hsm32 = (uint32_t*)hsm;
   const int item = blockIdx.x;
   const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
   for (int i = threadIdx.x; i < 2 * NB * 16; i += HT) hsm[i] = 0ull;
@@ -78,6 +88,7 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   const int half = threadIdx.x & 1, r = threadIdx.x & 15, t2 = threadIdx.x >> 1;
   const uint8_t* gb = a.bins + (size_t)grp * a.gs + half * 16;
   unsigned long long* base = hsm + half * NB * 16;
+  uint32_t* base32 = hsm32 + half * NB * 16;
   // w / g are indexed by the (virtual) row id, the bins by the data row
   auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * 32); };
   long long accw[HNE], accg[HNE];
@@ -86,8 +97,15 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   // one row slot: packed (w, w*g) fixed point added to the 16 features' bins of this half record
   auto update = [&](float wv, float gv, const uint4& bv) {
     if (wv == 0.f) return;
-    const unsigned long long q = ((unsigned long long)__float2uint_rn(wv * a.scale_w) << PACK_G) +
-                                 (unsigned long long)(long long)__float2int_rn(wv * gv * a.scale_g);
+    unsigned long long q = 0;
+    uint32_t q32 = 0;
+    if constexpr (MODE == 0)
+      q = ((unsigned long long)__float2uint_rn(wv * a.scale_w) << PACK_G) +
+          (unsigned long long)(long long)__float2int_rn(wv * gv * a.scale_g);
+    else if constexpr (MODE == 1)
+      q32 = __float2uint_rn(wv * a.scale_w);
+    else
+      q32 = (uint32_t)__float2int_rn(wv * gv * a.scale_g);    // scale_g already / 2^GSH32
     // rotate the 16 bytes left by r: byte j of R = feature (j + r) & 15
     const uint32_t W[4] = {bv.x, bv.y, bv.z, bv.w};
     uint32_t X[4], Y[4], R[4];
@@ -100,8 +118,13 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
-      atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
+      if constexpr (MODE == 0) atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
+      else atomicAdd(&base32[(b << 4) | ((j + r) & 15)], q32);
     }
+  };
+  auto unpack32 = [&](uint32_t v, long long& aw, long long& ag) {
+    if constexpr (MODE == 1) aw += (long long)v;
+    else ag += (long long)(int32_t)v * (1ll << GSH32);
   };
   auto flush = [&](int& it) {
     if (++it == HFLUSH) {
@@ -109,8 +132,9 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < HNE; ++k) {
-        unpack_add(hsm[threadIdx.x + k * HT], accw[k], accg[k]);
-        hsm[threadIdx.x + k * HT] = 0ull;
+        const int e = threadIdx.x + k * HT;
+        if constexpr (MODE == 0) { unpack_add(hsm[e], accw[k], accg[k]); hsm[e] = 0ull; }
+        else { unpack32(hsm32[e], accw[k], accg[k]); hsm32[e] = 0u; }
       }
       __syncthreads();
     }
@@ -172,12 +196,16 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < HNE; ++k) unpack_add(hsm[threadIdx.x + k * HT], accw[k], accg[k]);
+  for (int k = 0; k < HNE; ++k) {
+    if constexpr (MODE == 0) unpack_add(hsm[threadIdx.x + k * HT], accw[k], accg[k]);
+    else unpack32(hsm32[threadIdx.x + k * HT], accw[k], accg[k]);
+  }
   // transpose through LDS ([f][b] per statistic) for coalesced slab stores
   long long* out = a.slab + (size_t)item * 2 * FG * NB;
   long long* tsm = (long long*)hsm;
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
+    if ((MODE == 1 && st == 1) || (MODE == 2 && st == 0)) continue;   // u32 modes own one half
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < HNE; ++k) {
@@ -554,13 +582,16 @@ __global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
 
 SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, const int* pos2row, const float* w, const float* g,
                               const int* items, int n_items, void* slab, int n_feat, double scale_w,
-                              double scale_g, long nmod, hipStream_t stream) {
-  if (gs % 32 || n_items <= 0) return -1;
+                              double scale_g, long nmod, int mode, hipStream_t stream) {
+  if (gs % 32 || n_items <= 0 || mode < 0 || mode > 2) return -1;
   HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, items, (long long*)slab, n_items, n_feat,
-             (float)scale_w, (float)scale_g, nmod};
+             (float)scale_w, (float)(mode == 2 ? scale_g / (1 << GSH32) : scale_g), nmod};
   static const int pf = [] { const char* e = getenv("SHIFU_HIST_PF"); return e ? atoi(e) : 1; }();
-  if (pf) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2>), dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
-  else hipLaunchKernelGGL((gbdt_hist_kernel<false, 4>), dim3(n_items), dim3(HT), 2 * NB * 16 * 8, stream, a);
+  const size_t lds = 2 * NB * 16 * 8;      // the u32 modes still use 64 KiB for the transposed store
+  if (mode == 1) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 1>), dim3(n_items), dim3(HT), lds, stream, a);
+  else if (mode == 2) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 2>), dim3(n_items), dim3(HT), lds, stream, a);
+  else if (pf) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 0>), dim3(n_items), dim3(HT), lds, stream, a);
+  else hipLaunchKernelGGL((gbdt_hist_kernel<false, 4, 0>), dim3(n_items), dim3(HT), lds, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

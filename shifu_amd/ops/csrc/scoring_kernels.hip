@@ -35,31 +35,56 @@ struct TreeInferArgs {
   int* leaf_out;                       // [n][T] leaf node ids (nullable)
 };
 
+// One (row, tree) walk is a chain of dependent loads (node -> input value -> next node), so a
+// thread walks TI trees at once, level by level: TI independent chains per lane keep TI x the
+// loads in flight (the kernel is latency-bound, not bandwidth-bound).  Leaves stay put, so the
+// level loop has a fixed trip count (the ensemble depth) and every lane exits.
+template <int TI>
 __global__ __launch_bounds__(256) void tree_infer_kernel(TreeInferArgs a) {
   const long row = (long)blockIdx.x * 256 + threadIdx.x;
   if (row >= a.n) return;
   const int t0 = blockIdx.y * a.tg, t1 = min(a.T, t0 + a.tg);
   const double* xr = a.X + row * a.sr;
   double acc = 0.0;
-  for (int t = t0; t < t1; ++t) {
-    int id = a.roots[t];
-    int4 nd = a.node[id];
-    for (int d = 0; d < a.depth && nd.x >= 0; ++d) {     // bounded: every lane exits
-      const double v = xr[(long)nd.x * a.sf];
-      const double th = a.thr[id];
-      bool left;
-      if (nd.w >= 0) {                                     // categorical: category-index LUT
-        int ci = (v < 0.0 || v >= th) ? (int)th : (int)floor(v + 0.1);
-        ci = min(max(ci, 0), a.lut_w - 1);
-        left = a.catlut[(long)nd.w * a.lut_w + ci] != 0;
-      } else {
-        left = v < th;
-      }
-      id = left ? nd.y : nd.z;
-      nd = a.node[id];
+  for (int tb = t0; tb < t1; tb += TI) {
+    int id[TI];
+    int4 nd[TI];
+#pragma unroll
+    for (int u = 0; u < TI; ++u) {
+      id[u] = a.roots[min(tb + u, t1 - 1)];          // a short last batch repeats its last tree
+      nd[u] = a.node[id[u]];
     }
-    if (a.leaf_out) a.leaf_out[row * a.T + t] = id;
-    acc += a.lrs[t] * a.value[id];
+    for (int d = 0; d < a.depth; ++d) {
+      double v[TI], th[TI];
+#pragma unroll
+      for (int u = 0; u < TI; ++u) {
+        const bool inner = nd[u].x >= 0;
+        v[u] = inner ? xr[(long)nd[u].x * a.sf] : 0.0;
+        th[u] = a.thr[id[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < TI; ++u) {
+        if (nd[u].x < 0) continue;
+        bool left;
+        if (nd[u].w >= 0) {                            // categorical: category-index LUT
+          int ci = (v[u] < 0.0 || v[u] >= th[u]) ? (int)th[u] : (int)floor(v[u] + 0.1);
+          ci = min(max(ci, 0), a.lut_w - 1);
+          left = a.catlut[(long)nd[u].w * a.lut_w + ci] != 0;
+        } else {
+          left = v[u] < th[u];
+        }
+        id[u] = left ? nd[u].y : nd[u].z;
+      }
+#pragma unroll
+      for (int u = 0; u < TI; ++u) nd[u] = a.node[id[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < TI; ++u) {
+      const int t = tb + u;
+      if (t >= t1) break;
+      if (a.leaf_out) a.leaf_out[row * a.T + t] = id[u];
+      acc += a.lrs[t] * a.value[id[u]];
+    }
   }
   if (a.part) a.part[(long)blockIdx.y * a.n + row] = acc;
 }
@@ -136,7 +161,7 @@ SHIFU_API int shifu_tree_infer(const double* X, long sf, long sr, long n, const 
   if ((long)(n_groups - 1) * tg >= T) return -1;          // every group owns >= 1 tree
   TreeInferArgs a{X, sf, sr, n, (const int4*)node, thr, value, (const uint8_t*)catlut, lut_w, roots, lrs,
                   T, depth, tg, part, leaf_out};
-  hipLaunchKernelGGL(tree_infer_kernel, dim3((unsigned)((n + 255) / 256), n_groups), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(tree_infer_kernel<4>, dim3((unsigned)((n + 255) / 256), n_groups), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -316,7 +316,6 @@ class TrainStep:
                 os.makedirs(ms.pf.bmodels_dir, exist_ok=True)
             self.progress = open(ms.pf.progress_log, "a")
             self.metrics = MetricsWriter(ms.pf.metrics_jsonl)
-        ts = load_train_set(ms, is_tree)
         params = dict(mc.train.get("params") or {})
         grid_file = mc.train.get("gridConfigFile")
         lines = open(mc.resolve(grid_file)).read().splitlines() if grid_file else None
@@ -341,25 +340,12 @@ class TrainStep:
         if self.dry:
             _log.info("dry run: %d jobs %s", len(jobs), [j[1] for j in jobs][:3])
             return 0
-        val_errors = []
         t_start = time.time()
-        for trainer_id, p, bag, ova_class in jobs:
-            train_m, valid_m, sw = split_masks(mc, ts, bag, n_kfold, seed)
-            y = np.asarray(ts.y, dtype=np.float32)
-            if ova_class is not None:
-                y = (np.rint(y) == ova_class).astype(np.float32)
-            if alg == "NN":
-                verr = self._train_nn(trainer_id, p, ts, y, train_m, valid_m, sw, ova_class)
-            elif alg == "LR":
-                verr = self._train_lr(trainer_id, p, ts, y, train_m, valid_m, sw)
-            elif alg == "WDL":
-                verr = self._train_wdl(trainer_id, p, ts, y, train_m, valid_m, sw)
-            else:
-                verr = self._train_tree(trainer_id, p, ts, y, train_m, valid_m, sw)
-            val_errors.append(verr)
-            if self.info.rank == 0:
-                with open(os.path.join(ms.pf.valerr_dir, f"val_error_{trainer_id}"), "w") as f:
-                    f.write(repr(float(verr)) + "\n")
+        if self._job_parallel(len(jobs), is_tree):
+            val_errors = self._run_jobs_parallel(jobs, is_tree, n_kfold, seed)
+        else:
+            ts = load_train_set(ms, is_tree)
+            val_errors = self._run_jobs(jobs, ts, n_kfold, seed)
         if self.info.rank == 0:
             if len(grid) > 1:
                 best = int(np.nanargmin(val_errors))
@@ -376,6 +362,74 @@ class TrainStep:
                 self.metrics.close()
             _log.info("train: %d model(s) in %.1fs", len(jobs), time.time() - t_start)
         return 0
+
+    # -- jobs -------------------------------------------------------------------------------
+    def _run_jobs(self, jobs, ts, n_kfold, seed):
+        mc, alg = self.mc, self.mc.algorithm
+        val_errors = []
+        for trainer_id, p, bag, ova_class in jobs:
+            train_m, valid_m, sw = split_masks(mc, ts, bag, n_kfold, seed)
+            y = np.asarray(ts.y, dtype=np.float32)
+            if ova_class is not None:
+                y = (np.rint(y) == ova_class).astype(np.float32)
+            if alg == "NN":
+                verr = self._train_nn(trainer_id, p, ts, y, train_m, valid_m, sw, ova_class)
+            elif alg == "LR":
+                verr = self._train_lr(trainer_id, p, ts, y, train_m, valid_m, sw)
+            elif alg == "WDL":
+                verr = self._train_wdl(trainer_id, p, ts, y, train_m, valid_m, sw)
+            else:
+                verr = self._train_tree(trainer_id, p, ts, y, train_m, valid_m, sw)
+            val_errors.append(verr)
+            if self.info.rank == 0:
+                with open(os.path.join(self.ms.pf.valerr_dir, f"val_error_{trainer_id}"), "w") as f:
+                    f.write(repr(float(verr)) + "\n")
+        return val_errors
+
+    def _job_parallel(self, n_jobs: int, is_tree: bool) -> bool:
+        """F6: bags / folds / grid points dealt over the ranks (``shifu.train.jobParallel``):
+        ``true`` / ``false``, or ``auto`` (default) = on when there are at least as many jobs as
+        ranks and the whole training cache fits in a quarter of one GPU's memory (every rank
+        then holds the full table and trains its jobs with no collectives -- the reference runs
+        one Guagua job per bag, TrainModelProcessor.runDistributedTrain :661-1029)."""
+        from ..config import environment
+        if self.info.world_size <= 1 or n_jobs <= 1:
+            return False
+        mode = str(environment.get("shifu.train.jobParallel", "auto")).lower()
+        if mode in ("false", "0", "off"):
+            return False
+        cache = load_dataset_cache(self.ms.pf.cleaned_data if is_tree else self.ms.pf.normalized_data)
+        if cache is None:                  # in-memory normalization is a collective path
+            return False
+        if mode in ("true", "1", "on"):
+            return True
+        if n_jobs < self.info.world_size:
+            return False
+        arr = cache[1]
+        nbytes = sum(int(np.asarray(arr[k]).nbytes) for k in ("X", "codes", "y", "w") if arr.get(k) is not None)
+        budget = (torch.cuda.get_device_properties(self.dev).total_memory if self.dev.type == "cuda"
+                  else 64 << 30) // 4
+        return nbytes <= budget
+
+    def _run_jobs_parallel(self, jobs, is_tree, n_kfold, seed):
+        """Every rank loads the whole training set and runs jobs rank, rank + R, ... alone
+        (``dist.local_only``: a world of one, so each job is exactly the single-process job and
+        its model / val_error files are written by the rank that trained it); the validation
+        errors are then gathered so rank 0 can pick the grid-search winner."""
+        info = self.info
+        mine = [j for k, j in enumerate(jobs) if k % info.world_size == info.rank]
+        _log.info("job-parallel training: rank %d runs %d of %d jobs", info.rank, len(mine), len(jobs))
+        with dist.local_only():
+            self.info = dist.info()
+            try:
+                ts = load_train_set(self.ms, is_tree)
+                errs = self._run_jobs(mine, ts, n_kfold, seed)
+            finally:
+                self.info = info
+        got = {}
+        for part in dist.all_gather_objects([(j[0], e) for j, e in zip(mine, errs)]):
+            got.update(dict(part))
+        return [got[j[0]] for j in jobs]
 
     # -- NN ---------------------------------------------------------------------------------
     def _nn_spec(self, p, n_in, n_out):

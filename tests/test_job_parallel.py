@@ -1,0 +1,58 @@
+"""F6: bags dealt over ranks (``shifu.train.jobParallel``).  Two gloo ranks each load the whole
+training cache and train bags rank, rank + 2, ... alone; every model must equal the one the
+single-process run trains for that bag (each job is exactly the world-of-one job)."""
+import os
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from tests.test_elastic_resume import _port
+from tests.test_synthetic_models import _mc, _run
+
+
+def _rank_train(rank, world, port, root):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIFU_FORCE_CPU="1")
+    os.chdir(root)
+    from shifu_amd.cli import main
+    rc = main(["train"])
+    if rc != 0:
+        raise SystemExit(rc)
+
+
+@pytest.mark.parametrize("alg", ["NN", "GBT"])
+def test_bags_dealt_over_ranks_equal_single_process(tmp_path, alg):
+    from shifu_amd.utils.synthetic import make_model_set
+    roots = []
+    for name in ("par", "seq"):
+        root = make_model_set(str(tmp_path), name, alg, n_rows=700)
+        mc = _mc(root)
+        mc.train["numTrainEpochs"] = 8
+        mc.train["baggingNum"] = 3
+        if alg == "GBT":
+            mc.train["params"].update({"TreeNum": 5, "MaxDepth": 3})
+        mc.save()
+        _run(root, ["init", "stats", "norm"])
+        roots.append(root)
+    par, seq = roots
+    mp.start_processes(_rank_train, args=(2, _port(), par), nprocs=2, join=True, start_method="spawn")
+    _run(seq, ["train"])
+    for b in range(3):
+        if alg == "NN":
+            from shifu_amd.formats.nn_format import read_encog
+            wa = read_encog(os.path.join(par, f"models/model{b}.nn")).weights
+            wb = read_encog(os.path.join(seq, f"models/model{b}.nn")).weights
+            for x, y in zip(wa, wb):
+                np.testing.assert_array_equal(x, y)
+        else:
+            from shifu_amd.formats.tree_format import read_tree_model
+            ta = read_tree_model(os.path.join(par, f"models/model{b}.gbt"))
+            tb = read_tree_model(os.path.join(seq, f"models/model{b}.gbt"))
+            x = {c: np.linspace(-3, 3, 40) for c in ta.names}
+            np.testing.assert_array_equal(ta.score(x, 40), tb.score(x, 40))
+    # every bag's validation error file exists in the parallel run
+    import glob
+    names = [sorted(os.path.basename(f) for f in glob.glob(os.path.join(r, "**", "val_error_*"), recursive=True))
+             for r in (par, seq)]
+    assert names[0] == names[1] == [f"val_error_{b}" for b in range(3)]

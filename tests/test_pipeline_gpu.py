@@ -54,3 +54,25 @@ def test_sensitivity_varsel_gpu(tmp_path):
     _run(root, ("init", "stats", "varsel"))
     sel = [c for c in json.load(open(os.path.join(root, "ColumnConfig.json"))) if c["finalSelect"]]
     assert 0 < len(sel) <= 10
+
+
+def test_posttrain_bin_avg_gpu_matches_cpu(tmp_path, monkeypatch):
+    """posttrain binAvgScore through the HIP tree-inference + keyed-count kernels (K13, K18)
+    equals the host numpy path on the same model set."""
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "g", "GBT", n_rows=4000)
+    mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+    mc.train["params"].update({"TreeNum": 10, "MaxDepth": 4})
+    mc.save()
+    _run(root, ("init", "stats", "norm", "train", "posttrain"))
+
+    def avg():
+        return {c["columnName"]: c["columnBinning"]["binAvgScore"]
+                for c in json.load(open(os.path.join(root, "ColumnConfig.json")))
+                if (c.get("columnBinning") or {}).get("binAvgScore")}
+    gpu = avg()
+    assert gpu and all(v for v in gpu.values())
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    _run(root, ("posttrain",))
+    assert avg() == gpu
