@@ -90,6 +90,170 @@ __global__ __launch_bounds__(256) void tree_infer_kernel(TreeInferArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Coded tree walk.  The scattered fp64 input reads above move a 64-B+ transaction per (row,
+// tree, level): at 500 trees x depth 7 that is ~1 TB per 5M rows, so the plain walk runs at
+// the HBM rate, not the tree rate.  Instead every input value is first replaced by its rank
+// among the ensemble's thresholds of that feature (u16 code: count of thresholds <= v, so
+// v < t_k <=> code <= k exactly; NaN -> 0xFFFF goes right like the fp64 compare), the rows'
+// codes are staged in LDS once (R rows x C codes, one coalesced read per row), and the walk
+// reads only LDS + the L2-resident node table.
+//   tree_code_kernel : 64-row x 64-feature tiles of the feature-major input, transposed
+//                      through LDS into row-major u16 codes (coalesced both ways)
+//   tree_walk_coded_kernel : R rows per block, TPR = 256 / R threads per row, thread sub walks
+//                      trees sub, sub + TPR, ... (2 at a time); per-row partial sums added in
+//                      sub order (deterministic)
+// ---------------------------------------------------------------------------------------
+struct TreeCodeArgs {
+  const double* XT; long ldx; long n; int C;  // feature-major: value (f, r) at XT[f * ldx + r]
+  const double* bnd; const int* boff;       // sorted unique thresholds of feature f: bnd[boff[f] .. boff[f+1])
+  const uint8_t* is_cat;                    // [C] categorical slot (value = category index)
+  uint16_t* codes;                          // [n][C]
+};
+
+constexpr int TC_LDS = 4096;                // thresholds of the tile's features staged in LDS (32 KiB)
+constexpr int TC_R = 256, TC_F = 32;        // tile: 256 rows (one per thread) x 32 features
+
+// Thread t owns row r0 + t of the tile: its 32 feature values are loaded 8 at a time (8 x 8 B in
+// flight per lane; a wave reads 512 contiguous bytes of one feature, the block 2 KiB), each is
+// ranked by a branchless upper-bound search over the LDS-staged thresholds (wave-uniform step
+// count: every lane of a wave is on the same feature), and the u16 codes are transposed
+// through LDS into 64-B row segments of the row-major output.
+__global__ __launch_bounds__(256) void tree_code_kernel(TreeCodeArgs a) {
+  __shared__ uint16_t tile[TC_R][TC_F + 2];
+  __shared__ double tb[TC_LDS];
+  // feature tile = blockIdx.x (fastest): the blocks in flight share a few row blocks, so every
+  // feature column is read as one sequential stream (few pages live, TLB-friendly) instead of
+  // each block opening 32 pages 8 B x N apart
+  const long r0 = (long)blockIdx.y * TC_R;
+  const int f0 = blockIdx.x * TC_F;
+  const int fend = min(a.C, f0 + TC_F);
+  const int b0 = a.boff[f0], nb = a.boff[fend] - b0;
+  const bool lds = nb <= TC_LDS;
+  if (lds)
+    for (int i = threadIdx.x; i < nb; i += 256) tb[i] = a.bnd[b0 + i];
+  __syncthreads();
+  // index the staged copy relative to b0 (never form tb - b0: an LDS address below the
+  // allocation does not survive the generic-pointer conversion)
+  auto thr_at = [&](int i) { return lds ? tb[i - b0] : a.bnd[i]; };
+  const long r = r0 + threadIdx.x;
+  const bool live = r < a.n;
+  auto load8 = [&](int g, double* v) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int f = f0 + g + k;
+      v[k] = (live && f < a.C) ? a.XT[(long)f * a.ldx + r] : 0.0;
+    }
+  };
+  double v[8], vn[8];
+  load8(0, v);
+  for (int g = 0; g < TC_F; g += 8) {
+    if (g + 8 < TC_F) load8(g + 8, vn);        // next group's loads in flight during this search
+    // the 8 searches advance together (8 independent LDS reads per step); a search whose
+    // feature has fewer thresholds just fails the bound check on the extra steps
+    int pos[8], base[8], L[8], lmax = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int f = min(f0 + g + k, a.C - 1);
+      base[k] = a.boff[f];
+      L[k] = a.boff[f + 1] - base[k];
+      pos[k] = 0;
+      lmax = max(lmax, L[k]);
+    }
+    for (int st = lmax ? 1 << (31 - __clz(lmax)) : 0; st > 0; st >>= 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (pos[k] + st <= L[k] && thr_at(base[k] + pos[k] + st - 1) <= v[k]) pos[k] += st;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int f = f0 + g + k;
+      uint16_t code = 0;
+      if (f < a.C) {
+        if (a.is_cat[f]) code = (v[k] >= 0.0) ? (uint16_t)fmin(floor(v[k] + 0.1), 65534.0) : (uint16_t)0xFFFF;
+        else code = (v[k] != v[k]) ? (uint16_t)0xFFFF : (uint16_t)pos[k];      // NaN goes right
+      }
+      tile[threadIdx.x][g + k] = code;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = vn[k];
+  }
+  __syncthreads();
+  const int nf = fend - f0;
+#pragma unroll 4
+  for (int i = 0; i < TC_R * TC_F / 256; ++i) {
+    const int e = threadIdx.x + 256 * i, rr = e / TC_F, fl = e % TC_F;
+    if (r0 + rr < a.n && fl < nf) a.codes[(r0 + rr) * a.C + f0 + fl] = tile[rr][fl];
+  }
+}
+
+struct TreeWalkArgs {
+  const uint16_t* codes; long n; int C;     // [n][C]
+  const int4* node;                         // {feat (-1 leaf), left, right, w}: w >= 0 numeric threshold code k
+                                            // (left iff code <= k), w < 0 categorical LUT row -w-1
+  const int* catnc;                         // [n_catrows] category count of the split's column
+  const double* value;
+  const uint8_t* catlut; int lut_w;
+  const int* roots; const double* lrs; int T, depth, tg, R;
+  double* part; long ldp;                   // partial score of group g, row r at part[g * ldp + r]
+  int* leaf_out;
+};
+
+__device__ __forceinline__ int walk_step(const TreeWalkArgs& a, const uint16_t* row, int4 nd) {
+  const uint32_t code = row[nd.x];
+  bool left;
+  if (nd.w >= 0) {
+    left = code <= (uint32_t)nd.w;
+  } else {
+    const int cr = -nd.w - 1, nc = a.catnc[cr];
+    int ci = (code == 0xFFFFu || (int)code >= nc) ? nc : (int)code;
+    ci = min(ci, a.lut_w - 1);
+    left = a.catlut[(long)cr * a.lut_w + ci] != 0;
+  }
+  return left ? nd.y : nd.z;
+}
+
+__global__ __launch_bounds__(256) void tree_walk_coded_kernel(TreeWalkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+  uint16_t* rows = (uint16_t*)wsm;                                  // [R][C]
+  double* red = (double*)(wsm + (((size_t)a.R * a.C * 2 + 15) & ~(size_t)15));   // [TPR][R]
+  const long rb = (long)blockIdx.x * a.R;
+  const int nr = (int)min((long)a.R, a.n - rb);
+  const uint16_t* src = a.codes + rb * a.C;
+  for (int i = threadIdx.x; i < nr * a.C; i += 256) rows[i] = src[i];
+  __syncthreads();
+  const int TPR = 256 / a.R, r = threadIdx.x % a.R, sub = threadIdx.x / a.R;
+  const int t0 = blockIdx.y * a.tg, t1 = min(a.T, t0 + a.tg);
+  const uint16_t* row = rows + r * a.C;
+  double acc = 0.0;
+  if (r < nr) {
+    for (int t = t0 + sub; t < t1; t += 2 * TPR) {
+      const int tb = min(t + TPR, t1 - 1);                          // second chain (repeats t when past the end)
+      int ia = a.roots[t], ib = a.roots[tb];
+      int4 na = a.node[ia], nb = a.node[ib];
+      for (int d = 0; d < a.depth; ++d) {                           // leaves stay put: fixed trip count
+        if (na.x >= 0) ia = walk_step(a, row, na);
+        if (nb.x >= 0) ib = walk_step(a, row, nb);
+        na = a.node[ia];
+        nb = a.node[ib];
+      }
+      if (a.leaf_out) a.leaf_out[(rb + r) * a.T + t] = ia;
+      acc += a.lrs[t] * a.value[ia];
+      if (t + TPR < t1) {
+        if (a.leaf_out) a.leaf_out[(rb + r) * a.T + t + TPR] = ib;
+        acc += a.lrs[t + TPR] * a.value[ib];
+      }
+    }
+  }
+  red[sub * a.R + r] = acc;
+  __syncthreads();
+  if (sub == 0 && r < nr && a.part) {
+    double s = 0.0;
+    for (int k = 0; k < TPR; ++k) s += red[k * a.R + r];
+    a.part[(long)blockIdx.y * a.ldp + rb + r] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Keyed counts: out_cnt[f][k] += 1, out_w[f][k] += round(w * scale) for every row with
 // 0 <= key < K.  keys[f * ks + r] (ks = 0: one key vector shared by every column),
 // w[f * ws + r] (ws = 0: shared weights; w == nullptr: no weighted sums).
@@ -176,6 +340,35 @@ SHIFU_API int shifu_keyed_hist(const int* keys, long ks, const double* w, long w
   if (bx < 1) bx = 1;
   KeyedArgs a{keys, ks, w, ws, n, K, scale, (unsigned long long*)cnt, (unsigned long long*)wsum};
   hipLaunchKernelGGL(keyed_hist_kernel, dim3((unsigned)bx, F), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_tree_code(const double* XT, long ldx, long n, int C, const double* bnd, const int* boff,
+                              const void* is_cat, void* codes, hipStream_t stream) {
+  if (n <= 0 || C <= 0) return 0;
+  if (C > 65535 * TC_F || ldx < n) return -1;
+  TreeCodeArgs a{XT, ldx, n, C, bnd, boff, (const uint8_t*)is_cat, (uint16_t*)codes};
+  if ((n + TC_R - 1) / TC_R > 65535) return -1;            // row blocks on grid y
+  hipLaunchKernelGGL(tree_code_kernel, dim3((C + TC_F - 1) / TC_F, (unsigned)((n + TC_R - 1) / TC_R)), dim3(256), 0,
+                     stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_tree_walk_coded(const void* codes, long n, int C, const void* node, const int* catnc,
+                                    const double* value, const void* catlut, int lut_w, const int* roots,
+                                    const double* lrs, int T, int depth, int R, int n_groups, double* part,
+                                    long ldp, int* leaf_out, hipStream_t stream) {
+  if (n <= 0 || T <= 0) return 0;
+  if (R < 1 || R > 256 || (R & (R - 1)) || (size_t)R * C * 2 > 65536 || n_groups < 1 || n_groups > T ||
+      lut_w < 1 || depth < 0 || ldp < n) return -1;
+  const int tg = (T + n_groups - 1) / n_groups;
+  if ((long)(n_groups - 1) * tg >= T) return -1;
+  TreeWalkArgs a{(const uint16_t*)codes, n, C, (const int4*)node, catnc, value, (const uint8_t*)catlut, lut_w,
+                 roots, lrs, T, depth, tg, R, part, ldp, leaf_out};
+  const size_t lds = (((size_t)R * C * 2 + 15) & ~(size_t)15) + 256 * sizeof(double);
+  hipLaunchKernelGGL(tree_walk_coded_kernel, dim3((unsigned)((n + R - 1) / R), n_groups), dim3(256), lds, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -13,6 +13,10 @@ import torch
 
 from ..formats.tree_format import CONTINUOUS, TreeModelFile, convert_gbt_score
 
+# GPU walk over u16 threshold-rank codes staged in LDS (SHIFU_TREE_CODED=0: fp64 input walk)
+import os as _os
+CODED_WALK = _os.environ.get("SHIFU_TREE_CODED", "1") != "0"
+
 
 class FlatEnsemble:
     def __init__(self, model: TreeModelFile, bag: int, columns: list, device="cpu"):
@@ -88,13 +92,73 @@ class FlatEnsemble:
                         self.lrs.contiguous())
         return self._ht
 
+    def _coded_tables(self, C: int):
+        """Tables of the coded walk (scoring_kernels.hip tree_code / tree_walk_coded): per input
+        slot the sorted unique thresholds the ensemble compares it with, node records whose 4th
+        field is the threshold's rank (numeric: left iff code <= rank) or -(LUT row + 1)
+        (categorical), and the category count per LUT row.  None when the coded walk cannot hold
+        the ensemble (> 65534 thresholds on one feature, or > 16384 inputs)."""
+        if getattr(self, "_ct", None) is not None or getattr(self, "_ct_none", False):
+            return self._ct
+        feat, thr = self.feat.cpu().numpy(), self.thr.cpu().numpy()
+        iscat, catrow = self.iscat.cpu().numpy(), self.catrow.cpu().numpy()
+        num = (feat >= 0) & ~iscat
+        order = np.lexsort((thr[num], feat[num]))
+        fs, ts = feat[num][order], thr[num][order]
+        keep = np.ones(len(fs), bool)
+        keep[1:] = (fs[1:] != fs[:-1]) | (ts[1:] != ts[:-1])
+        fs, ts = fs[keep], ts[keep]
+        boff = np.searchsorted(fs, np.arange(C + 1), side="left").astype(np.int32)
+        if C > 16384 or (len(boff) > 1 and np.diff(boff).max(initial=0) >= 65535):
+            self._ct_none = True
+            return None
+        w = np.zeros(len(feat), np.int64)
+        for i in np.nonzero(num)[0]:
+            f = feat[i]
+            w[i] = np.searchsorted(ts[boff[f]:boff[f + 1]], thr[i], side="left")
+        cat = (feat >= 0) & iscat
+        w[cat] = -(catrow[cat] + 1)
+        n_catrows = int(self.catlut.shape[0])
+        catnc = np.zeros(max(1, n_catrows), np.int32)
+        catnc[catrow[cat]] = thr[cat].astype(np.int64)
+        slot_cat = np.array([c in self.model.categories for c in self.columns], np.uint8)
+        dev = self.dev
+        node = torch.from_numpy(np.stack([feat, self.left.cpu().numpy(), self.right.cpu().numpy(), w], 1)
+                                .astype(np.int32)).to(dev)
+        self._ct = (torch.from_numpy(ts.astype(np.float64) if len(ts) else np.zeros(1)).to(dev),
+                    torch.from_numpy(boff).to(dev), torch.from_numpy(slot_cat).to(dev), node,
+                    torch.from_numpy(catnc).to(dev))
+        return self._ct
+
     def _hip_walk(self, X: torch.Tensor, want_leaves: bool):
         """One kernel launch for all (row, tree) pairs of the chunk: -> (bag score, leaf ids | None)."""
         from ..ops import _native
         _native.require_gpu_native()
         n, T = X.shape[0], int(self.roots.numel())
         XT = X.to(torch.float64).t().contiguous()             # feature-major [C, N]: coalesced at the root
+        C = XT.shape[0]
         node, thr, value, lut, roots, lrs = self._hip_tables()
+        ct = self._coded_tables(C) if CODED_WALK else None
+        if ct is not None:
+            bnd, boff, slot_cat, cnode, catnc = ct
+            R = 1 << max(0, min(8, int(np.floor(np.log2(16384 / max(C, 1))))))
+            rb = -(-n // R)
+            groups = max(1, min(T, -(-2048 // rb)))
+            groups = -(-T // -(-T // groups))
+            part = torch.empty(groups, n, dtype=torch.float64, device=X.device)
+            leaf = torch.empty(n, T, dtype=torch.int32, device=X.device) if want_leaves else None
+            step = min(65535 * 256, max(1, (1 << 31) // max(C, 1) // 2))   # codes chunk <= 2 GiB
+            codes = torch.empty(min(n, step), C, dtype=torch.int16, device=X.device)
+            for r0 in range(0, n, step):
+                m = min(n, r0 + step) - r0
+                # pointer offsets into the full-width buffers: no per-chunk copies
+                _native.call_hip("shifu_tree_code", XT.data_ptr() + r0 * 8, n, m, C, bnd, boff, slot_cat, codes,
+                                 _native.stream_of(X))
+                lv = None if leaf is None else leaf.data_ptr() + r0 * T * 4
+                _native.call_hip("shifu_tree_walk_coded", codes, m, C, cnode, catnc, value, lut, lut.shape[1],
+                                 roots, lrs, T, max(self.depth, 0), R, groups, part.data_ptr() + r0 * 8, n, lv,
+                                 _native.stream_of(X))
+            return part.sum(0), leaf
         groups = max(1, min(T, -(-2048 // max(1, -(-n // 256)))))
         groups = -(-T // -(-T // groups))                     # every group owns >= 1 tree
         part = torch.empty(groups, n, dtype=torch.float64, device=X.device)

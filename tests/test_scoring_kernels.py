@@ -58,16 +58,46 @@ def test_flat_ensemble_matches_record_walk():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("coded", [True, False])
 @pytest.mark.parametrize("algorithm,n,trees", [("GBT", 70_001, 60), ("RF", 5_000, 3), ("GBT", 257, 500)])
-def test_tree_infer_kernel_matches_torch(algorithm, n, trees):
+def test_tree_infer_kernel_matches_torch(algorithm, n, trees, coded, monkeypatch):
     from shifu_amd.ops import _native
+    from shifu_amd.scoring import tree_ensemble
     _native.require_gpu_native()
+    monkeypatch.setattr(tree_ensemble, "CODED_WALK", coded)
     m = _random_model(n_trees=trees, algorithm=algorithm, seed=n)
     X = _inputs(n, seed=trees)
     cpu, gpu = TreeScorer(m, device="cpu"), TreeScorer(m, device="cuda")
     Xd = X.cuda()
     np.testing.assert_array_equal(gpu.ens[0].leaves(Xd).cpu().numpy(), cpu.ens[0].leaves(X).numpy())
     np.testing.assert_allclose(gpu.score_bags(Xd), cpu.score_bags(X), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_coded_walk_wide_inputs():
+    """1000 numeric inputs (16 rows per block in LDS, 16 threads per row), NaN / +-inf inputs and
+    thresholds shared by several nodes: the coded walk equals the fp64 torch walk."""
+    from shifu_amd.formats.tree_format import CONTINUOUS, Node, Split, TreeModelFile, TreeRecord
+    rng = np.random.default_rng(11)
+    C = 1000
+    shared = rng.normal(size=50)
+
+    def grow(d):
+        nd = Node(0)
+        if d == 6:
+            nd.predict = float(rng.normal())
+            return nd
+        nd.split = Split(int(rng.integers(0, C)), CONTINUOUS, threshold=float(rng.choice(shared)))
+        nd.left, nd.right = grow(d + 1), grow(d + 1)
+        return nd
+    cols = list(range(C))
+    m = TreeModelFile("GBT", "squared", False, False, C, {c: 0.0 for c in cols}, {c: f"c{c}" for c in cols}, {},
+                      {c: c for c in cols}, [[TreeRecord(t, 0, grow(0), 0.1) for t in range(40)]])
+    X = torch.from_numpy(rng.choice(np.concatenate([shared, rng.normal(size=50), [np.nan, np.inf, -np.inf]]),
+                                    size=(3001, C)))
+    cpu, gpu = TreeScorer(m, device="cpu"), TreeScorer(m, device="cuda")
+    np.testing.assert_array_equal(gpu.ens[0].leaves(X.cuda()).cpu().numpy(), cpu.ens[0].leaves(X).numpy())
+    np.testing.assert_allclose(gpu.score_bags(X.cuda()), cpu.score_bags(X), rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.gpu
