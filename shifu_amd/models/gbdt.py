@@ -171,6 +171,9 @@ class BinnedData:
     nbins: np.ndarray               # [F] bins per feature (numeric: #boundaries, cat: #cats+1)
     is_cat: np.ndarray              # [F] uint8
     n_feat: int
+    # out-of-core: bins in pinned host memory, read by the kernels in place over the
+    # host link (the device address of the mapping); targets / weights / predictions stay in HBM
+    bins_dptr: int | None = None
 
     @property
     def n(self):
@@ -178,7 +181,13 @@ class BinnedData:
 
     @property
     def device(self):
-        return self.bins.device
+        return self.y.device
+
+    @property
+    def kbins(self):
+        """What the HIP kernels get for the bins: the HBM tensor, or the device address of the
+        pinned host copy."""
+        return self.bins if self.bins_dptr is None else self.bins_dptr
 
     @property
     def group_stride(self) -> int:
@@ -191,7 +200,25 @@ class BinnedData:
         return self.bins.permute(1, 0, 2).reshape(n, g * FG)[:, : self.n_feat]
 
     @staticmethod
-    def blocked(codes, device="cpu", rows=None) -> torch.Tensor:
+    def host_resident(codes, y, nbins, is_cat=None, sig=None, device="cuda", rows=None):
+        """Like :meth:`from_codes` but the blocked bins stay in pinned host memory (tables larger
+        than HBM): the kernels read them through the host mapping's device address
+        (``hipHostGetDevicePointer``; refused loudly if the runtime cannot map the buffer)."""
+        n, f = codes.shape
+        if rows is not None:
+            n = len(rows)
+        g = (f + FG - 1) // FG
+        b = torch.empty(g, n, FG, dtype=torch.uint8, pin_memory=True)
+        BinnedData.blocked(codes, "cpu", rows, out=b)
+        dptr = _host_device_pointer(b)
+        d = BinnedData.from_codes(np.zeros((0, f), np.uint8), np.zeros(0), nbins, is_cat, None, device)
+        d.bins, d.bins_dptr = b, dptr
+        d.y = torch.as_tensor(y, dtype=torch.float32).reshape(n).to(device)
+        d.sig = None if sig is None else torch.as_tensor(sig, dtype=torch.float32).reshape(n).to(device)
+        return d
+
+    @staticmethod
+    def blocked(codes, device="cpu", rows=None, out=None) -> torch.Tensor:
         """Row-major codes [N, F] (torch or numpy incl. a uint8 memmap, any int dtype) -> blocked
         uint8 [G, N', 32] on ``device``, one 32-feature group at a time (optionally only ``rows``):
         host memory stays at one group slice, never an int32 copy of the whole matrix."""
@@ -199,7 +226,9 @@ class BinnedData:
         if rows is not None:
             n = len(rows)
         g = (f + FG - 1) // FG
-        b = torch.zeros(g, n, FG, dtype=torch.uint8, device=device)
+        b = torch.zeros(g, n, FG, dtype=torch.uint8, device=device) if out is None else out
+        if out is not None and f % FG:
+            out[-1, :, f % FG:] = 0
         for gi in range(g):
             c0, c1 = gi * FG, min(f, (gi + 1) * FG)
             blk = codes[:, c0:c1] if rows is None else codes[rows, c0:c1]
@@ -550,7 +579,7 @@ class TreeTrainer:
         from ..ops import _native as nat
         d = self.data
         F, nn = self.F, len(nodes)
-        st = nat.stream_of(d.bins)
+        st = nat.stream_of(d.y)
         items, ni, max_items = self._make_items(nodes, n_built)
         ni_t = torch.from_numpy(ni).to(self.dev)
         feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
@@ -564,7 +593,7 @@ class TreeTrainer:
             else:
                 slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
                 p2r = None if self._root_level else pos2row      # root: positions are rows
-                nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, g, it, len(items), slab, F,
+                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, w, g, it, len(items), slab, F,
                              self.scale_w, self.scale_g, self._nmod, 0, st)
         else:
             slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
@@ -611,15 +640,15 @@ class TreeTrainer:
         feature) instead of the packed u64: about half the root level's histogram time."""
         from ..ops import _native as nat
         d = self.data
-        key = (w._version, self.scale_w, hash(items.tobytes()), d.bins.data_ptr())
+        key = (w._version, self.scale_w, hash(items.tobytes()), d.bins.data_ptr(), d.bins_dptr)
         c = getattr(self, "_root_cache", None)
         if c is None or c[0] is not w or c[1] != key:
             slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
-            nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, None, w, g, it, len(items), slab, self.F,
+            nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, it, len(items), slab, self.F,
                          self.scale_w, self.scale_g, 0, 1, st)
             self._root_cache = (w, key, slab)          # holds w: its storage cannot be re-issued
         slab = self._root_cache[2]
-        nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, None, w, g, it, len(items), slab, self.F,
+        nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, it, len(items), slab, self.F,
                      self.scale_w, self.scale_g, 0, 2, st)
         return slab
 
@@ -632,14 +661,14 @@ class TreeTrainer:
         F = self.F
         if self.gpu:
             from ..ops import _native as nat
-            st = nat.stream_of(d.bins)
+            st = nat.stream_of(d.y)
             items, ni, max_items = self._make_items(nodes, n_built)
             if n_built and len(items):
                 ni_t = torch.from_numpy(ni).to(self.dev)
                 it = torch.from_numpy(items).to(self.dev)
                 slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
                 p2r = None if self._root_level else pos2row
-                nat.call_hip("shifu_gbdt_hist", d.bins, d.group_stride, p2r, w, gc, it, len(items), slab, F,
+                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, w, gc, it, len(items), slab, F,
                              self.scale_w, self.scale_g, self._nmod, 0, st)
                 built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
                 feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
@@ -814,9 +843,9 @@ class TreeTrainer:
         cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
         pred, scale = fuse
         self._leaf_done = True
-        nat.call_hip("shifu_gbdt_partition_flag", d.bins, d.group_stride, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
+        nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
                      None, None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale),
-                     1, nat.stream_of(d.bins))
+                     1, nat.stream_of(d.y))
 
     def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots, leaf=None):
         d = self.data
@@ -827,7 +856,7 @@ class TreeTrainer:
         # positions of unsplit nodes are never moved; mark non-split node positions -1
         if self.gpu:
             from ..ops import _native as nat
-            st = nat.stream_of(d.bins)
+            st = nat.stream_of(d.y)
             sf = torch.from_numpy(split_feat).to(self.dev)
             sb = torch.from_numpy(split_bin).to(self.dev)
             cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
@@ -838,7 +867,7 @@ class TreeTrainer:
             wcnt = torch.empty(nw, dtype=torch.int32, device=self.dev)
             lv, (pred, scale) = leaf if leaf is not None else (None, (None, 0.0))
             # non-split nodes' rows get their leaf value here (fused GBT prediction update)
-            nat.call_hip("shifu_gbdt_partition_flag", d.bins, d.group_stride, pos2row, pos_node, sf, sb, cl,
+            nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, pos2row, pos_node, sf, sb, cl,
                          self.is_cat_t, fbits, wcnt, n, self._nmod, pred, None if lv is None else lv[0], None, None,
                          float(scale), 0, st)
             wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
@@ -900,7 +929,7 @@ class TreeTrainer:
             from ..ops import _native as nat
             feat, thr, cl, val = tree.device_arrays(data.device)
             ic = torch.from_numpy(data.is_cat.astype(np.uint8)).to(data.device)
-            nat.call_hip("shifu_gbdt_apply_tree", data.bins, data.group_stride, None, feat, thr, cl, val, ic,
+            nat.call_hip("shifu_gbdt_apply_tree", data.kbins, data.group_stride, None, feat, thr, cl, val, ic,
                          pred, float(scale), int(set_mode), None, data.n, tree.max_nodes, nat.stream_of(pred))
         else:
             v = torch.from_numpy(tree.predict_bins(data.codes().numpy(), data.is_cat)).float()
@@ -1151,7 +1180,7 @@ def _apply_classes(tr: "TreeTrainer", t: Tree, data: BinnedData, out: torch.Tens
         from ..ops import _native as nat
         feat, thr, cl, val = t.device_arrays(data.device, classes=True)
         ic = torch.from_numpy(data.is_cat.astype(np.uint8)).to(data.device)
-        nat.call_hip("shifu_gbdt_apply_tree", data.bins, data.group_stride, None, feat, thr, cl, val, ic,
+        nat.call_hip("shifu_gbdt_apply_tree", data.kbins, data.group_stride, None, feat, thr, cl, val, ic,
                      out, 1.0, 1, None, data.n, t.max_nodes, nat.stream_of(out))
     else:
         out.copy_(torch.from_numpy(t.predict_bins(data.codes().numpy(), data.is_cat, classes=True)).float())
@@ -1160,6 +1189,20 @@ def _apply_classes(tr: "TreeTrainer", t: Tree, data: BinnedData, out: torch.Tens
 def _slot_key(z):
     """Slot order of a level's nodes: built first (one contiguous all-reduce), then by tree, id."""
     return (not z["built"], z["tree"], z["id"])
+
+
+def _host_device_pointer(t: torch.Tensor) -> int:
+    """Device address of a pinned host tensor (hipHostGetDevicePointer on the HIP runtime torch
+    already loaded)."""
+    import ctypes
+    if not t.is_pinned():
+        raise RuntimeError("host-resident bins must be pinned")
+    lib = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    out = ctypes.c_void_p()
+    rc = lib.hipHostGetDevicePointer(ctypes.byref(out), ctypes.c_void_p(t.data_ptr()), 0)
+    if rc != 0 or not out.value:
+        raise RuntimeError(f"hipHostGetDevicePointer failed ({rc}): cannot map host-resident bins")
+    return int(out.value)
 
 
 W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histogram fields)

@@ -644,7 +644,13 @@ class TrainStep:
         # uint8 codes go to the device one 32-feature group at a time (no host int32 staging)
         codes_np = codes if isinstance(codes, np.ndarray) else np.asarray(codes)
         all_rows = len(tri) == codes_np.shape[0]
-        d = BinnedData.from_codes(codes_np, y[tri], nb, is_cat, w[tri], device=dev, rows=None if all_rows else tri)
+        if self._host_bins(len(tri), codes_np.shape[1]):
+            _log.info("tree bins stay in pinned host memory (%d rows x %d features)", len(tri), codes_np.shape[1])
+            d = BinnedData.host_resident(codes_np, y[tri], nb, is_cat, w[tri], device=dev,
+                                         rows=None if all_rows else tri)
+        else:
+            d = BinnedData.from_codes(codes_np, y[tri], nb, is_cat, w[tri], device=dev,
+                                      rows=None if all_rows else tri)
         vd = None
         if ts.vcodes is not None:
             vd = BinnedData.from_codes(np.asarray(ts.vcodes), np.asarray(ts.vy, np.float32), nb, is_cat,
@@ -706,6 +712,22 @@ class TrainStep:
             if os.path.exists(ckpt):
                 os.remove(ckpt)
         return tt.valid_errors[-1] if tt.valid_errors else float("nan")
+
+    def _host_bins(self, n_rows: int, n_feat: int) -> bool:
+        """Out-of-core trees: ``shifu.train.tree.hostBins`` = true / false / auto
+        (default: when the blocked uint8 bins would take more than 60 % of the GPU's free memory,
+        they stay in pinned host memory and the kernels read them over the host link)."""
+        from ..config import environment
+        if self.dev.type != "cuda":
+            return False
+        mode = str(environment.get("shifu.train.tree.hostBins", "auto")).lower()
+        if mode in ("true", "1", "on"):
+            return True
+        if mode in ("false", "0", "off"):
+            return False
+        need = n_rows * (-(-n_feat // 32) * 32)
+        free, _ = torch.cuda.mem_get_info(self.dev)
+        return need > 0.6 * free
 
     def _continuous_trees(self, tid, cfg):
         """``checkContinuousTraining`` (TrainModelProcessor.java:1149-1197) for trees: GBT only, the

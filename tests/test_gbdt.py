@@ -348,3 +348,26 @@ def test_multiclass_gpu_matches_cpu(imp):
         assert np.array_equal(a.feat, b.feat) and np.array_equal(a.thr, b.thr)
         assert np.array_equal(a.class_value, b.class_value)
     assert np.array_equal(tc.predict(dc).numpy(), tg.predict(dg).cpu().numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg", ["GBT", "RF"])
+def test_gpu_host_resident_bins_match_device(alg, monkeypatch):
+    """Out-of-core trees: bins in pinned host memory read by the kernels in place grow the same
+    trees and predictions as HBM-resident bins (RF also through the forest-batch path)."""
+    monkeypatch.setenv("SHIFU_RF_BATCH", "2")
+    data_c, codes, y = _data(n=20000, f=40, nb=64, seed=5, cat_cols=(3,))
+    dd = BinnedData.from_codes(codes, y, data_c.nbins, data_c.is_cat, device="cuda")
+    dh = BinnedData.host_resident(codes, y, data_c.nbins, data_c.is_cat, device="cuda")
+    assert dh.bins.device.type == "cpu" and dh.bins.is_pinned() and dh.bins_dptr
+    assert torch.equal(dh.bins, dd.bins.cpu())
+    cfg = dict(algorithm=alg, tree_num=4, max_depth=5, learning_rate=0.2, feature_subset_strategy="ALL")
+    if alg == "RF":
+        cfg.update(bagging_sample_rate=0.8, feature_subset_strategy="HALF")
+    ta, tb = TreeTrainer(TreeConfig(**cfg), dd), TreeTrainer(TreeConfig(**cfg), dh)
+    ta.train()
+    tb.train()
+    for a, b in zip(ta.trees, tb.trees):
+        assert (a.feat == b.feat).all() and (a.thr == b.thr).all()
+        assert np.array_equal(a.value, b.value)
+    assert torch.equal(ta.pred, tb.pred)
