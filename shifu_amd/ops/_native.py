@@ -66,7 +66,7 @@ HIP_SIGNATURES = {
     # scoring_kernels.hip
     "shifu_tree_infer": "plll" "ppp" "pi" "pp" "iii" "pp" "s",
     "shifu_keyed_hist": "plpl" "lii" "d" "pp" "s",
-    "shifu_tree_code": "plli" "ppp" "p" "s",
+    "shifu_tree_code": "plli" "ppp" "pi" "s",
     "shifu_tree_walk_coded": "pli" "pp" "p" "pi" "pp" "iiii" "pl" "p" "s",
     # quantile_kernels.hip
     "shifu_pack_bits": "plip" "s",

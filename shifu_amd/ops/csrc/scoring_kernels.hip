@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void tree_infer_kernel(TreeInferArgs a) {
 //   tree_code_kernel : 64-row x 64-feature tiles of the feature-major input, transposed
 //                      through LDS into row-major u16 codes (coalesced both ways)
 //   tree_walk_coded_kernel : R rows per block, TPR = 256 / R threads per row, thread sub walks
-//                      trees sub, sub + TPR, ... (2 at a time); per-row partial sums added in
+//                      trees sub, sub + TPR, ... (WCH at a time); per-row partial sums added in
 //                      sub order (deterministic)
 // ---------------------------------------------------------------------------------------
 struct TreeCodeArgs {
@@ -108,19 +108,21 @@ struct TreeCodeArgs {
   const double* bnd; const int* boff;       // sorted unique thresholds of feature f: bnd[boff[f] .. boff[f+1])
   const uint8_t* is_cat;                    // [C] categorical slot (value = category index)
   uint16_t* codes;                          // [n][C]
+  int tb_cap;                               // thresholds the dynamic LDS buffer holds (0: search in global)
 };
 
 constexpr int TC_LDS = 4096;                // thresholds of the tile's features staged in LDS (32 KiB)
 constexpr int TC_R = 256, TC_F = 32;        // tile: 256 rows (one per thread) x 32 features
+constexpr int TCG = 16;                     // features per load group (TCG x 8 B in flight per lane)
 
-// Thread t owns row r0 + t of the tile: its 32 feature values are loaded 8 at a time (8 x 8 B in
-// flight per lane; a wave reads 512 contiguous bytes of one feature, the block 2 KiB), each is
+// Thread t owns row r0 + t of the tile: its 32 feature values are loaded TCG at a time (TCG x 8 B in
+// flight per lane, the next group's loads issued before this group's searches; a wave reads 512 contiguous bytes of one feature, the block 2 KiB), each is
 // ranked by a branchless upper-bound search over the LDS-staged thresholds (wave-uniform step
 // count: every lane of a wave is on the same feature), and the u16 codes are transposed
 // through LDS into 64-B row segments of the row-major output.
 __global__ __launch_bounds__(256) void tree_code_kernel(TreeCodeArgs a) {
   __shared__ uint16_t tile[TC_R][TC_F + 2];
-  __shared__ double tb[TC_LDS];
+  extern __shared__ double tb[];            // [a.tb_cap]: sized by the host to the largest tile's list
   // feature tile = blockIdx.x (fastest): the blocks in flight share a few row blocks, so every
   // feature column is read as one sequential stream (few pages live, TLB-friendly) instead of
   // each block opening 32 pages 8 B x N apart
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(256) void tree_code_kernel(TreeCodeArgs a) {
   const int f0 = blockIdx.x * TC_F;
   const int fend = min(a.C, f0 + TC_F);
   const int b0 = a.boff[f0], nb = a.boff[fend] - b0;
-  const bool lds = nb <= TC_LDS;
+  const bool lds = nb <= a.tb_cap;
   if (lds)
     for (int i = threadIdx.x; i < nb; i += 256) tb[i] = a.bnd[b0 + i];
   __syncthreads();
@@ -137,22 +139,22 @@ __global__ __launch_bounds__(256) void tree_code_kernel(TreeCodeArgs a) {
   auto thr_at = [&](int i) { return lds ? tb[i - b0] : a.bnd[i]; };
   const long r = r0 + threadIdx.x;
   const bool live = r < a.n;
-  auto load8 = [&](int g, double* v) {
+  auto loadg = [&](int g, double* v) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < TCG; ++k) {
       const int f = f0 + g + k;
       v[k] = (live && f < a.C) ? a.XT[(long)f * a.ldx + r] : 0.0;
     }
   };
-  double v[8], vn[8];
-  load8(0, v);
-  for (int g = 0; g < TC_F; g += 8) {
-    if (g + 8 < TC_F) load8(g + 8, vn);        // next group's loads in flight during this search
-    // the 8 searches advance together (8 independent LDS reads per step); a search whose
+  double v[TCG], vn[TCG];
+  loadg(0, v);
+  for (int g = 0; g < TC_F; g += TCG) {
+    if (g + TCG < TC_F) loadg(g + TCG, vn);        // next group's loads in flight during this search
+    // the TCG searches advance together (TCG independent LDS reads per step); a search whose
     // feature has fewer thresholds just fails the bound check on the extra steps
-    int pos[8], base[8], L[8], lmax = 0;
+    int pos[TCG], base[TCG], L[TCG], lmax = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < TCG; ++k) {
       const int f = min(f0 + g + k, a.C - 1);
       base[k] = a.boff[f];
       L[k] = a.boff[f + 1] - base[k];
@@ -161,11 +163,11 @@ __global__ __launch_bounds__(256) void tree_code_kernel(TreeCodeArgs a) {
     }
     for (int st = lmax ? 1 << (31 - __clz(lmax)) : 0; st > 0; st >>= 1) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < TCG; ++k)
         if (pos[k] + st <= L[k] && thr_at(base[k] + pos[k] + st - 1) <= v[k]) pos[k] += st;
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < TCG; ++k) {
       const int f = f0 + g + k;
       uint16_t code = 0;
       if (f < a.C) {
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(256) void tree_code_kernel(TreeCodeArgs a) {
       tile[threadIdx.x][g + k] = code;
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = vn[k];
+    for (int k = 0; k < TCG; ++k) v[k] = vn[k];
   }
   __syncthreads();
   const int nf = fend - f0;
@@ -212,6 +214,8 @@ __device__ __forceinline__ int walk_step(const TreeWalkArgs& a, const uint16_t* 
   return left ? nd.y : nd.z;
 }
 
+constexpr int WCH = 4;                      // tree chains walked together per thread
+
 __global__ __launch_bounds__(256) void tree_walk_coded_kernel(TreeWalkArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
   uint16_t* rows = (uint16_t*)wsm;                                  // [R][C]
@@ -226,21 +230,29 @@ __global__ __launch_bounds__(256) void tree_walk_coded_kernel(TreeWalkArgs a) {
   const uint16_t* row = rows + r * a.C;
   double acc = 0.0;
   if (r < nr) {
-    for (int t = t0 + sub; t < t1; t += 2 * TPR) {
-      const int tb = min(t + TPR, t1 - 1);                          // second chain (repeats t when past the end)
-      int ia = a.roots[t], ib = a.roots[tb];
-      int4 na = a.node[ia], nb = a.node[ib];
-      for (int d = 0; d < a.depth; ++d) {                           // leaves stay put: fixed trip count
-        if (na.x >= 0) ia = walk_step(a, row, na);
-        if (nb.x >= 0) ib = walk_step(a, row, nb);
-        na = a.node[ia];
-        nb = a.node[ib];
+    for (int t = t0 + sub; t < t1; t += WCH * TPR) {
+      // WCH independent chains (trees t, t + TPR, ...): a chain past the group's end repeats the
+      // last tree and is not accumulated
+      int id[WCH];
+      int4 nd[WCH];
+#pragma unroll
+      for (int c = 0; c < WCH; ++c) {
+        id[c] = a.roots[min(t + c * TPR, t1 - 1)];
+        nd[c] = a.node[id[c]];
       }
-      if (a.leaf_out) a.leaf_out[(rb + r) * a.T + t] = ia;
-      acc += a.lrs[t] * a.value[ia];
-      if (t + TPR < t1) {
-        if (a.leaf_out) a.leaf_out[(rb + r) * a.T + t + TPR] = ib;
-        acc += a.lrs[t + TPR] * a.value[ib];
+      for (int d = 0; d < a.depth; ++d) {                           // leaves stay put: fixed trip count
+#pragma unroll
+        for (int c = 0; c < WCH; ++c)
+          if (nd[c].x >= 0) id[c] = walk_step(a, row, nd[c]);
+#pragma unroll
+        for (int c = 0; c < WCH; ++c) nd[c] = a.node[id[c]];
+      }
+#pragma unroll
+      for (int c = 0; c < WCH; ++c) {
+        const int tc = t + c * TPR;
+        if (tc >= t1) break;
+        if (a.leaf_out) a.leaf_out[(rb + r) * a.T + tc] = id[c];
+        acc += a.lrs[tc] * a.value[id[c]];
       }
     }
   }
@@ -345,13 +357,16 @@ SHIFU_API int shifu_keyed_hist(const int* keys, long ks, const double* w, long w
 }
 
 SHIFU_API int shifu_tree_code(const double* XT, long ldx, long n, int C, const double* bnd, const int* boff,
-                              const void* is_cat, void* codes, hipStream_t stream) {
+                              const void* is_cat, void* codes, int tb_cap, hipStream_t stream) {
   if (n <= 0 || C <= 0) return 0;
   if (C > 65535 * TC_F || ldx < n) return -1;
-  TreeCodeArgs a{XT, ldx, n, C, bnd, boff, (const uint8_t*)is_cat, (uint16_t*)codes};
+  // tb_cap: the largest 32-feature tile's threshold count (host-computed; tiles with more search in
+  // global memory), so the LDS footprint is what the ensemble needs, not the TC_LDS maximum
+  if (tb_cap < 0) return -1;
+  TreeCodeArgs a{XT, ldx, n, C, bnd, boff, (const uint8_t*)is_cat, (uint16_t*)codes, min(tb_cap, TC_LDS)};
   if ((n + TC_R - 1) / TC_R > 65535) return -1;            // row blocks on grid y
-  hipLaunchKernelGGL(tree_code_kernel, dim3((C + TC_F - 1) / TC_F, (unsigned)((n + TC_R - 1) / TC_R)), dim3(256), 0,
-                     stream, a);
+  hipLaunchKernelGGL(tree_code_kernel, dim3((C + TC_F - 1) / TC_F, (unsigned)((n + TC_R - 1) / TC_R)), dim3(256),
+                     (size_t)a.tb_cap * sizeof(double), stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -125,9 +125,11 @@ class FlatEnsemble:
         dev = self.dev
         node = torch.from_numpy(np.stack([feat, self.left.cpu().numpy(), self.right.cpu().numpy(), w], 1)
                                 .astype(np.int32)).to(dev)
+        tiles = np.minimum(np.arange(0, C + 32, 32), C)         # 32-feature tiles of the code kernel
+        tb_cap = int(np.diff(boff[np.unique(tiles)]).max(initial=0))
         self._ct = (torch.from_numpy(ts.astype(np.float64) if len(ts) else np.zeros(1)).to(dev),
                     torch.from_numpy(boff).to(dev), torch.from_numpy(slot_cat).to(dev), node,
-                    torch.from_numpy(catnc).to(dev))
+                    torch.from_numpy(catnc).to(dev), tb_cap)
         return self._ct
 
     def _hip_walk(self, X: torch.Tensor, want_leaves: bool):
@@ -140,7 +142,7 @@ class FlatEnsemble:
         node, thr, value, lut, roots, lrs = self._hip_tables()
         ct = self._coded_tables(C) if CODED_WALK else None
         if ct is not None:
-            bnd, boff, slot_cat, cnode, catnc = ct
+            bnd, boff, slot_cat, cnode, catnc, tb_cap = ct
             R = 1 << max(0, min(8, int(np.floor(np.log2(16384 / max(C, 1))))))
             rb = -(-n // R)
             groups = max(1, min(T, -(-2048 // rb)))
@@ -153,7 +155,7 @@ class FlatEnsemble:
                 m = min(n, r0 + step) - r0
                 # pointer offsets into the full-width buffers: no per-chunk copies
                 _native.call_hip("shifu_tree_code", XT.data_ptr() + r0 * 8, n, m, C, bnd, boff, slot_cat, codes,
-                                 _native.stream_of(X))
+                                 tb_cap, _native.stream_of(X))
                 lv = None if leaf is None else leaf.data_ptr() + r0 * T * 4
                 _native.call_hip("shifu_tree_walk_coded", codes, m, C, cnode, catnc, value, lut, lut.shape[1],
                                  roots, lrs, T, max(self.depth, 0), R, groups, part.data_ptr() + r0 * 8, n, lv,
