@@ -127,6 +127,47 @@ def _percentiles(bounds, counts, mn, mx, count):
     return p25, med, p75
 
 
+_DEFER = None      # list while a deferred_metrics block is open (K3 batched on the device)
+
+
+class deferred_metrics:
+    """K3 on the device: inside the block ``_finish_binning`` queues each column's (neg, pos)
+    bins; on exit ONE ``column_metrics_kernel`` launch computes KS / IV / WOE / per-bin WOE of the
+    counts and weighted bins of every queued column.  A no-op on the CPU (the host oracle
+    ``column_metrics`` runs per column)."""
+
+    def __init__(self, dev):
+        self.on = torch.device(dev).type == "cuda" if dev is not None else False
+        self.dev = dev
+
+    def __enter__(self):
+        global _DEFER
+        self.prev = _DEFER
+        if self.on:
+            _DEFER = []
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        global _DEFER
+        q = _DEFER if self.on else None
+        _DEFER = self.prev
+        if exc_type is None and q:
+            from ..ops.stats_ops import column_metrics_batch
+            res = column_metrics_batch([(c[2], c[4]) for c in q], [(c[1], c[3]) for c in q], self.dev)
+            for (cc, *_), (m, mw) in zip(q, res):
+                _apply_metrics(cc, len(_[0]), m, mw)
+        return False
+
+
+def _apply_metrics(cc, nb, m, mw):
+    zero = [0.0] * nb
+    cc.stats["ks"], cc.stats["iv"], cc.stats["woe"] = (m[0], m[1], m[2]) if m else (None, None, None)
+    cc.stats["weightedKs"], cc.stats["weightedIv"], cc.stats["weightedWoe"] = \
+        (mw[0], mw[1], mw[2]) if mw else (None, None, None)
+    cc.binning["binCountWoe"] = m[3] if m else zero
+    cc.binning["binWeightedWoe"] = mw[3] if mw else zero
+
+
 def _finish_binning(cc, binary, nb, cpos, cneg, wpos, wneg, total):
     """Write binning arrays + KS/IV/WOE for one column (shared by the CPU and HIP paths)."""
     if binary:
@@ -143,14 +184,11 @@ def _finish_binning(cc, binary, nb, cpos, cneg, wpos, wneg, total):
     cb["binWeightedNeg"] = [float(x) for x in wneg]
     cb["binPosRate"] = [float(x) for x in rate]
     if binary:
-        m = column_metrics(cneg, cpos)
-        mw = column_metrics(wneg, wpos)
-        zero = [0.0] * nb
-        cc.stats["ks"], cc.stats["iv"], cc.stats["woe"] = (m[0], m[1], m[2]) if m else (None, None, None)
-        cc.stats["weightedKs"], cc.stats["weightedIv"], cc.stats["weightedWoe"] = \
-            (mw[0], mw[1], mw[2]) if mw else (None, None, None)
-        cb["binCountWoe"] = m[3] if m else zero
-        cb["binWeightedWoe"] = mw[3] if mw else zero
+        if _DEFER is not None:         # K3 batched on the device at the end of the pass
+            _DEFER.append((cc, np.asarray(cpos, np.float64), np.asarray(cneg, np.float64),
+                           np.asarray(wpos, np.float64), np.asarray(wneg, np.float64)))
+            return
+        _apply_metrics(cc, nb, column_metrics(cneg, cpos), column_metrics(wneg, wpos))
     else:
         cb["binCountWoe"] = [0.0] * nb
         cb["binWeightedWoe"] = [0.0] * nb

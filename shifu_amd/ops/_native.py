@@ -63,6 +63,7 @@ HIP_SIGNATURES = {
     "shifu_lr_grad": "plli" "i" "ppp" "pp" "i" "s",
     "shifu_sensitivity": "plpl" "pp" "f" "p" "l" "iiiii" "p" "s",
     "shifu_se_perturb": "plpl" "p" "ii" "iiii" "pl" "s",
+    "shifu_column_metrics": "ppp" "il" "pp" "s",
     # scoring_kernels.hip
     "shifu_tree_infer": "plll" "ppp" "pi" "pp" "iii" "pp" "s",
     "shifu_keyed_hist": "plpl" "lii" "d" "pp" "s",

@@ -644,3 +644,70 @@ SHIFU_API int shifu_sensitivity(const float* S, long lds, const float* X, long l
   CHECK_HIP(hipGetLastError());
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// K3: KS / IV / WOE per column (ColumnStatsCalculator.calculateColumnMetrics,
+// J/core/ColumnStatsCalculator.java): one wave per (column, variant) -- variant 0 = bin counts,
+// 1 = weighted bins -- over the bins in 64-lane chunks: totals, per-bin WOE
+// ln((n_i + eps) / (p_i + eps)), IV = sum (n_i - p_i) * woe_i, KS = max |cum p - cum n| with the
+// cumulative sums carried across chunks by a wave scan.  All columns of a stats pass in one
+// launch (bins are variable-length: offsets).
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct MetricsArgs {
+  const double* neg; const double* pos;   // [2][total_bins]: counts, then weighted
+  const int* off; int F; long total;      // bins of column f: [off[f], off[f+1])
+  double* out;                            // [F][2][4]: ks * 100, iv, woe, valid
+  double* bin_woe;                        // [2][total_bins]
+};
+
+__global__ void __launch_bounds__(256) column_metrics_kernel(MetricsArgs a) {
+  const int wv = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wv >= 2 * a.F) return;
+  const int f = wv >> 1, var = wv & 1;
+  const double* ng = a.neg + var * a.total;
+  const double* ps = a.pos + var * a.total;
+  const int b0 = a.off[f], b1 = a.off[f + 1];
+  double sn = 0.0, sp = 0.0;
+  for (int b = b0 + lane; b < b1; b += 64) { sn += ng[b]; sp += ps[b]; }
+  sn = wave_sum_d(sn);
+  sp = wave_sum_d(sp);
+  double* o = a.out + ((long)f * 2 + var) * 4;
+  if (sn == 0.0 || sp == 0.0) {
+    if (lane == 0) { o[0] = 0.0; o[1] = 0.0; o[2] = 0.0; o[3] = 0.0; }
+    return;
+  }
+  const double EPS = 1e-10;
+  double iv = 0.0, ks = 0.0, cp = 0.0, cn = 0.0;     // cp / cn: cumulative sums before this chunk
+  for (int c0 = b0; c0 < b1; c0 += 64) {
+    const int b = c0 + lane;
+    const bool ok = b < b1;
+    const double p = ok ? ps[b] / sp : 0.0, n = ok ? ng[b] / sn : 0.0;
+    const double bw = log((n + EPS) / (p + EPS));
+    if (ok) { iv += (n - p) * bw; a.bin_woe[var * a.total + b] = bw; }
+    double sp_inc = p, sn_inc = n;                    // inclusive wave scans
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double tp = __shfl_up(sp_inc, d, 64), tn = __shfl_up(sn_inc, d, 64);
+      if (lane >= d) { sp_inc += tp; sn_inc += tn; }
+    }
+    if (ok) ks = fmax(ks, fabs((cp + sp_inc) - (cn + sn_inc)));
+    cp += __shfl(sp_inc, 63, 64);
+    cn += __shfl(sn_inc, 63, 64);
+  }
+  iv = wave_sum_d(iv);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) ks = fmax(ks, __shfl_xor(ks, d, 64));
+  if (lane == 0) { o[0] = ks * 100.0; o[1] = iv; o[2] = log((sn + EPS) / (sp + EPS)); o[3] = 1.0; }
+}
+}  // namespace
+
+SHIFU_API int shifu_column_metrics(const double* neg, const double* pos, const int* off, int F, long total,
+                                   double* out, double* bin_woe, hipStream_t stream) {
+  if (F <= 0) return 0;
+  MetricsArgs a{neg, pos, off, F, total, out, bin_woe};
+  const long waves = 2L * F;
+  hipLaunchKernelGGL(column_metrics_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}

@@ -214,3 +214,38 @@ def keyed_hist(keys: torch.Tensor, K: int, weights: torch.Tensor | None = None):
     if wsum is None:
         return c, None
     return c, (wsum.to(torch.float64) / scale if scale else torch.zeros_like(c))
+
+
+def column_metrics_batch(negs, poss, dev):
+    """K3 for many columns in one launch (``stats_kernels.hip: column_metrics_kernel``).
+
+    negs / poss: per column a pair (counts, weighted) of equal-length bin arrays.
+    -> per column ((ks*100, iv, woe, bin_woe) | None, same for the weighted bins)."""
+    nat.require_gpu_native()
+    F = len(negs)
+    if F == 0:
+        return []
+    lens = [len(n[0]) for n in negs]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    total = int(off[-1])
+    hn = np.zeros((2, max(1, total)))
+    hp = np.zeros((2, max(1, total)))
+    for k in range(F):
+        for v in range(2):
+            hn[v, off[k]:off[k + 1]] = negs[k][v]
+            hp[v, off[k]:off[k + 1]] = poss[k][v]
+    dn, dp = _dev_tensor(hn, torch.float64, dev), _dev_tensor(hp, torch.float64, dev)
+    doff = _dev_tensor(off, torch.int32, dev)
+    out = torch.zeros(F, 2, 4, dtype=torch.float64, device=dev)
+    bw = torch.zeros(2, max(1, total), dtype=torch.float64, device=dev)
+    nat.call_hip("shifu_column_metrics", dn, dp, doff, F, max(1, total), out, bw, nat.stream_of(dn))
+    out, bw = out.cpu().numpy(), bw.cpu().numpy()
+    res = []
+    for k in range(F):
+        pair = []
+        for v in range(2):
+            o = out[k, v]
+            pair.append((float(o[0]), float(o[1]), float(o[2]), [float(x) for x in bw[v, off[k]:off[k + 1]]])
+                        if o[3] > 0 else None)
+        res.append(tuple(pair))
+    return res

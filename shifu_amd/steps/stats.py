@@ -47,20 +47,9 @@ def run_stats(root: str = ".", correlation: bool = False, psi: bool = False, reb
         return 0
     if not psi:
         from ..parallel import dist
-        if _use_streaming(ms):
-            _stats_streamed(ms, cols, device)
-        else:
-            md = ms.load_raw(cols, sample_rate=float(mc.stats.get("sampleRate", 1.0)),
-                             sample_neg_only=bool(mc.stats.get("sampleNegOnly", False)))
-            _log.info("stats: %d valid rows (%s)", md.n, md.counters.as_dict())
-            if dist.info().world_size > 1:
-                # data parallel over an in-memory table (shifu.stats.streaming=false)
-                from ..algos.dist_stats import compute_column_stats_dp
-                from .base import shard_model_data
-                compute_column_stats_dp(mc, ms.ccs, shard_model_data(md), device=device,
-                                        columns={c.name for c in cols})
-            else:
-                S.compute_column_stats(mc, ms.ccs, md, device=device, columns={c.name for c in cols})
+        from ..utils.device import default_device
+        with S.deferred_metrics(device if device is not None else default_device()):
+            _stats_pass(ms, mc, cols, device)
         ms.save_cc(backup=True)
     if dist.info().world_size > 1:
         dist.barrier()
@@ -101,6 +90,24 @@ def _use_streaming(ms: ModelSet) -> bool:
         return False
     return nbytes > float(environment.get("shifu.stats.streamThresholdGB", 8)) * (1 << 30)
 
+
+
+def _stats_pass(ms, mc, cols, device) -> None:
+    from ..parallel import dist
+    if _use_streaming(ms):
+        _stats_streamed(ms, cols, device)
+    else:
+        md = ms.load_raw(cols, sample_rate=float(mc.stats.get("sampleRate", 1.0)),
+                         sample_neg_only=bool(mc.stats.get("sampleNegOnly", False)))
+        _log.info("stats: %d valid rows (%s)", md.n, md.counters.as_dict())
+        if dist.info().world_size > 1:
+            # data parallel over an in-memory table (shifu.stats.streaming=false)
+            from ..algos.dist_stats import compute_column_stats_dp
+            from .base import shard_model_data
+            compute_column_stats_dp(mc, ms.ccs, shard_model_data(md), device=device,
+                                    columns={c.name for c in cols})
+        else:
+            S.compute_column_stats(mc, ms.ccs, md, device=device, columns={c.name for c in cols})
 
 def _stats_streamed(ms: ModelSet, cols, device=None) -> None:
     """Stats over row chunks of this rank's byte range (algos/stats_stream.py)."""
