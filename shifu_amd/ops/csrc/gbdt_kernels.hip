@@ -78,7 +78,9 @@ constexpr int GSH32 = 3;
 
 template <bool PF, int HU, int MODE>
 __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
-  constexpr int HFLUSH = (MODE == 0 ? 4096 : 2048) / (RPP * HU);   // passes between unpacks
+  // passes between unpacks: 4096 rows; in the u32 modes each of the two LDS copies sees exactly
+  // half of them (2048), which keeps a bin's int32 sum in range
+  constexpr int HFLUSH = 4096 / (RPP * HU);
   extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];   // [2][NB][16]
   uint32_t* hsm32 = (uint32_t*)hsm;
   const int item = blockIdx.x;
@@ -88,7 +90,10 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   const int half = threadIdx.x & 1, r = threadIdx.x & 15, t2 = threadIdx.x >> 1;
   const uint8_t* gb = a.bins + (size_t)grp * a.gs + half * 16;
   unsigned long long* base = hsm + half * NB * 16;
-  uint32_t* base32 = hsm32 + half * NB * 16;
+  // u32 modes: two interleaved copies [half][bin][copy][16] (lane group parity picks the copy):
+  // the 4 lanes that update the same feature then spread over 4 banks unless their bins agree
+  // mod 2 (one 16-feature row per bin put them in 4 banks only when the bins differ mod 4)
+  uint32_t* base32 = hsm32 + half * NB * 32 + (((threadIdx.x >> 4) & 1) << 4);
   // w / g are indexed by the (virtual) row id, the bins by the data row
   auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * 32); };
   long long accw[HNE], accg[HNE];
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
     for (int j = 0; j < 16; ++j) {
       const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
       if constexpr (MODE == 0) atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
-      else atomicAdd(&base32[(b << 4) | ((j + r) & 15)], q32);
+      else atomicAdd(&base32[(b << 5) | ((j + r) & 15)], q32);
     }
   };
   auto unpack32 = [&](uint32_t v, long long& aw, long long& ag) {
@@ -134,7 +139,13 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
       for (int k = 0; k < HNE; ++k) {
         const int e = threadIdx.x + k * HT;
         if constexpr (MODE == 0) { unpack_add(hsm[e], accw[k], accg[k]); hsm[e] = 0ull; }
-        else { unpack32(hsm32[e], accw[k], accg[k]); hsm32[e] = 0u; }
+        else {
+          const int i0 = ((e >> 12) * NB + ((e >> 4) & (NB - 1))) * 32 + (e & 15);
+          unpack32(hsm32[i0], accw[k], accg[k]);
+          unpack32(hsm32[i0 + 16], accw[k], accg[k]);
+          hsm32[i0] = 0u;
+          hsm32[i0 + 16] = 0u;
+        }
       }
       __syncthreads();
     }
@@ -198,7 +209,11 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
 #pragma unroll
   for (int k = 0; k < HNE; ++k) {
     if constexpr (MODE == 0) unpack_add(hsm[threadIdx.x + k * HT], accw[k], accg[k]);
-    else unpack32(hsm32[threadIdx.x + k * HT], accw[k], accg[k]);
+    else {
+      const int e = threadIdx.x + k * HT, i0 = ((e >> 12) * NB + ((e >> 4) & (NB - 1))) * 32 + (e & 15);
+      unpack32(hsm32[i0], accw[k], accg[k]);
+      unpack32(hsm32[i0 + 16], accw[k], accg[k]);
+    }
   }
   // transpose through LDS ([f][b] per statistic) for coalesced slab stores
   long long* out = a.slab + (size_t)item * 2 * FG * NB;
