@@ -579,6 +579,13 @@ class MLPTrainer:
             need = max(nat.hip().shifu_wgrad_ring_ws(rows, self.spec.hidden[l], kp[l]) for l in range(L))
             if need > 0:
                 ws["slab"] = torch.empty(need // 4, dtype=torch.float32, device=self.device)
+        # head output-wgrad partials per 256-row tile + fixed-order reduction scratch (deterministic
+        # replacement of the per-tile atomics, ops/csrc/gemm_kernels.hip colsum_fixed)
+        ws["gw_slab"] = ws["gw_part"] = None
+        if self.gpu and self.fused_head:
+            tiles = -(-rows // 256)
+            ws["gw_slab"] = torch.empty(tiles * kp[L], dtype=torch.float32, device=self.device)
+            ws["gw_part"] = torch.empty(-(-tiles // 128) * kp[L], dtype=torch.float32, device=self.device)
         self._ws[lane] = ws
         return ws
 
@@ -719,7 +726,10 @@ class MLPTrainer:
                          dels[L].data_ptr(), kp[L], mc, kp[L], kp[lh], ACT_IDS[sp.acts[lh]], sp.hidden[lh],
                          wv[L].data_ptr(), y.data_ptr(), nat.ptr(s), gv[L].data_ptr(), self.err_acc.data_ptr(),
                          kp[L], ACT_IDS[sp.out_act], LOSS_IDS[sp.loss], flat_spot(sp.out_act),
-                         flat_spot(sp.acts[lh]), st)
+                         flat_spot(sp.acts[lh]), nat.ptr(ws["gw_slab"]), st)
+            if ws["gw_slab"] is not None:
+                nat.call_hip("shifu_colsum_fixed", ws["gw_slab"], -(-mc // 256), kp[L], ws["gw_part"],
+                             gv[L].data_ptr(), st)
         else:
             # output layer + loss + last hidden delta + output wgrad
             nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], nat.ptr(ders[L]), kp[L],

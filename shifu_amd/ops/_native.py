@@ -33,7 +33,9 @@ HIP_SIGNATURES = {
     # mlp_kernels.hip
     "shifu_gemm_nt": "plplipl" "plplpl" "iiiiiiif" "s",
     "shifu_wgrad_tn": "plplpl" "iiiis",
-    "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "s",
+    "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "p" "s",
+    "shifu_colsum_fixed": "pii" "pp" "s",
+    "shifu_colsum_ws": ("ii", "l"),
     "shifu_gemm_set_stages": "i",
     "shifu_gemm_set_big": "i",
     "shifu_gemm_set_tune": "ii",

@@ -459,7 +459,8 @@ struct HeadArgs {
   const float* W;        // [KH] fp32 output weights (bias weight at kh_valid, zeros after)
   const float* Y;        // [M] targets
   const float* S;        // [M] significance (nullable -> 1)
-  float* GW;             // [KH] output-weight gradient (atomic)
+  float* GW;             // [KH] output-weight gradient (atomic; unused when GWslab is set)
+  float* GWslab;         // [tiles][KH] per-tile partials (nullable): summed in fixed order afterwards
   double* err;           // [2] error sum, weight sum (atomic)
   int KH, out_act, loss;
   float flat_out, flat_hid;
@@ -591,7 +592,11 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
       if ((lane & 15) == 0) gred[wr * 256 + wc * 64 + i * 16 + (lane >> 4) * 4 + r] = v;
     }
   __syncthreads();
-  if (tid < 256 && tid < h.KH) atomicAdd(h.GW + tid, gred[tid] + gred[256 + tid]);
+  if (tid < 256 && tid < h.KH) {
+    const float v = gred[tid] + gred[256 + tid];
+    if (h.GWslab) h.GWslab[(size_t)(m0 >> 8) * h.KH + tid] = v;     // tile index = row block
+    else atomicAdd(h.GW + tid, v);
+  }
   const int c = tid & 31;
 #pragma unroll 4
   for (int pass = 0; pass < 16; ++pass) {
@@ -793,14 +798,14 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
 SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, int NB, void* D, long ldd,
                               int M, int N, int K, int act, int n_valid, const float* W, const float* Y,
                               const float* S, float* GW, double* err, int KH, int out_act, int loss,
-                              float flat_out, float flat_hid, hipStream_t stream) {
+                              float flat_out, float flat_hid, float* GWslab, hipStream_t stream) {
   if (K % 64 || N % 8 || N > 256 || KH > 256 || KH < n_valid + 1 || lda % 8 || ldb % 8 || ldd % 8 ||
       M <= 0 || NB <= 0 || NB > 256)
     return -1;
   if (!act_deriv_from_output(act) || act == 6 || out_act < 0 || out_act > 8) return -2;
   GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)D, ldd, nullptr, 0, nullptr, 0, nullptr, 0,
              M, N, K, NB, n_valid, act, 1, 0.f};
-  HeadArgs h{W, Y, S, GW, err, KH, out_act, loss, flat_out, flat_hid};
+  HeadArgs h{W, Y, S, GW, GWslab, err, KH, out_act, loss, flat_out, flat_hid};
   const int grid = (M + 255) / 256;
 #define HEAD_L(A_) hipLaunchKernelGGL((gemm_head_8ph_kernel<A_>), dim3(grid), dim3(G8_T), HEAD_LDS, stream, p, h)
   switch (act) {
@@ -808,6 +813,37 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
     case 3: HEAD_L(3); break; case 4: HEAD_L(4); break; default: HEAD_L(7); break;
   }
 #undef HEAD_L
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// Fixed-order column sums of per-tile partials: G[k] += sum_t slab[t][k] (t ascending within each
+// 128-tile block, blocks ascending in the second pass) -- the deterministic replacement of the
+// head's output-wgrad atomics.  part: [ceil(T / 128)][K] scratch.
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* slab, int T, int K, float* part) {
+  const int k = threadIdx.x;
+  if (k >= K) return;
+  const int t0 = blockIdx.x * 128, t1 = min(T, t0 + 128);
+  float s = 0.f;
+  for (int t = t0; t < t1; ++t) s += slab[(size_t)t * K + k];
+  part[(size_t)blockIdx.x * K + k] = s;
+}
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int B, int K, float* G) {
+  const int k = threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += part[(size_t)b * K + k];
+  G[k] += s;
+}
+
+SHIFU_API long shifu_colsum_ws(int T, int K) { return (long)((T + 127) / 128) * K * 4; }
+
+SHIFU_API int shifu_colsum_fixed(const float* slab, int T, int K, float* part, float* G, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (K <= 0 || K > 256) return -1;
+  const int B = (T + 127) / 128;
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(B), dim3(256), 0, stream, slab, T, K, part);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(1), dim3(256), 0, stream, part, B, K, G);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

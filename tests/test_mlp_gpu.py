@@ -200,3 +200,24 @@ def test_two_chunk_lanes_match_one_lane(monkeypatch):
     g1, g2 = grads["1"], grads["2"]
     assert float((g1 - g2).norm() / g1.norm()) < 1e-5
     torch.testing.assert_close(errs["2"], errs["1"], rtol=1e-9, atol=1e-9)
+
+
+def test_bench_configuration_gradient_bitwise_reproducible():
+    """The bench trainer path (8-phase forward, fused head, ring wgrad, dgrad; full chunks) gives
+    bit-identical gradients run to run: the head's output-layer wgrad goes through per-tile
+    partials + a fixed-order reduction (colsum_fixed) instead of float atomics."""
+    spec = MLPSpec(n_in=1000, hidden=[500, 200], acts=["sigmoid", "sigmoid"], n_out=1)
+    n = 2 << 17
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, spec.n_in, generator=g)
+    y = (x[:, :1] > 0).float()
+    t = MLPTrainer(spec, device="cuda", seed=7, chunk_rows=1 << 17)
+    assert t.fused_head and t.wgrad_ring
+    d = t.prepare(x, y)
+    grads = []
+    for _ in range(2):
+        t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
+        torch.cuda.synchronize()
+        grads.append(t.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    assert float(grads[0].abs().sum()) > 0
