@@ -2,11 +2,14 @@
 
 ``IndependentTreeModel.computeRegressionScore`` (J/core/dtrain/dt/IndependentTreeModel.java:387-441)
 walks every tree per row.  Here every bag is flattened once into structure-of-arrays node tables
-(feature slot, threshold, categorical left-set LUT, children, leaf value) and all (row, tree)
-pairs descend one level per step as gathers over the resident input matrix — on the GPU that is
-a handful of large elementwise/gather launches per level for all trees at once.
+(feature slot, threshold, categorical left-set LUT, children, leaf value).  On the CPU all (row,
+tree) pairs descend one level per step as torch gathers (the oracle); on the GPU the HIP kernels
+of ``ops/csrc/scoring_kernels.hip`` rank every input against the ensemble's thresholds (u16
+codes), stage the rows' codes in LDS and walk all trees per row there (``_hip_walk``).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -14,8 +17,7 @@ import torch
 from ..formats.tree_format import CONTINUOUS, TreeModelFile, convert_gbt_score
 
 # GPU walk over u16 threshold-rank codes staged in LDS (SHIFU_TREE_CODED=0: fp64 input walk)
-import os as _os
-CODED_WALK = _os.environ.get("SHIFU_TREE_CODED", "1") != "0"
+CODED_WALK = os.environ.get("SHIFU_TREE_CODED", "1") != "0"
 
 
 class FlatEnsemble:
