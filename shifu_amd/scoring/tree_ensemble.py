@@ -115,9 +115,10 @@ class FlatEnsemble:
             self._ct_none = True
             return None
         w = np.zeros(len(feat), np.int64)
-        for i in np.nonzero(num)[0]:
-            f = feat[i]
-            w[i] = np.searchsorted(ts[boff[f]:boff[f + 1]], thr[i], side="left")
+        ni = np.nonzero(num)[0]
+        for f in np.unique(feat[ni]):                  # one vectorized search per feature
+            idx = ni[feat[ni] == f]
+            w[idx] = np.searchsorted(ts[boff[f]:boff[f + 1]], thr[idx], side="left")
         cat = (feat >= 0) & iscat
         w[cat] = -(catrow[cat] + 1)
         n_catrows = int(self.catlut.shape[0])
