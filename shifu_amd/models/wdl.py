@@ -15,6 +15,7 @@ small and bandwidth-bound on the embedding gathers).  File format ``.wdl``: the 
 from __future__ import annotations
 
 import json
+import os
 
 import numpy as np
 import torch
@@ -22,6 +23,43 @@ import torch
 from ..formats.javaio import JavaIn, JavaOut
 from ..parallel import dist
 from .nn import act_fwd
+
+
+# GPU wide sums + deep input gathers in one pass (ops/csrc/wdl_kernels.hip); SHIFU_WDL_HIP=0: torch ops
+WDL_HIP = os.environ.get("SHIFU_WDL_HIP", "1") != "0"
+
+
+class _WdlGather(torch.autograd.Function):
+    """(dense, cats, wide tables, embedding tables) -> (wide sum per row, [dense | embeddings]) with
+    the HIP gather kernels; backward scatters into the concatenated tables."""
+
+    @staticmethod
+    def forward(ctx, dense, cats, wt, et, woff, eoff, efield, D, want_wide, want_deep):
+        from ..ops import _native as nat
+        n, nd = dense.shape
+        Fc, E = cats.shape[1], int(efield.numel())
+        wide = torch.empty(n, device=dense.device) if want_wide else None
+        A = torch.empty(n, nd + E * D, device=dense.device) if want_deep else None
+        nat.call_hip("shifu_wdl_gather", 0, dense, nd, cats, Fc, wt, woff, et, eoff, efield, E, D, wide, A,
+                     nd + E * D, None, None, n, nat.stream_of(dense))
+        ctx.save_for_backward(cats, woff, eoff, efield)
+        ctx.meta = (n, nd, Fc, E, D, wt.numel(), et.numel())
+        return (wide if wide is not None else dense.new_zeros(n)), (A if A is not None else dense.new_zeros(n, 0))
+
+    @staticmethod
+    def backward(ctx, g_wide, g_A):
+        from ..ops import _native as nat
+        cats, woff, eoff, efield = ctx.saved_tensors
+        n, nd, Fc, E, D, nw, ne = ctx.meta
+        dev = cats.device
+        dwt = torch.zeros(nw, device=dev)
+        det = torch.zeros(ne, device=dev)
+        gw = g_wide.contiguous() if g_wide is not None else None
+        gA = g_A.contiguous() if (g_A is not None and g_A.shape[1] == nd + E * D) else None
+        nat.call_hip("shifu_wdl_gather", 1, None, nd, cats, Fc, None, woff, None, eoff, efield, E, D, gw, gA,
+                     nd + E * D, dwt, det, n, nat.stream_of(cats))
+        ddense = gA[:, :nd] if gA is not None else None
+        return ddense, None, dwt, det, None, None, None, None, None, None
 
 
 class WideDeepNet(torch.nn.Module):
@@ -45,7 +83,37 @@ class WideDeepNet(torch.nn.Module):
             self.layers.append(torch.nn.Parameter((torch.rand(dims[i + 1], dims[i] + 1, generator=g) * 2 - 1) * lim))
         self.final = torch.nn.Parameter((torch.rand(1, dims[-1] + 1, generator=g) * 2 - 1) * 0.1)
 
+    def _hip_forward(self, dense, cats):
+        dev = dense.device
+        if getattr(self, "_offs", None) is None or self._offs[0].device != dev:
+            ws = [s + 1 for s in self.cat_sizes]
+            woff = torch.tensor(np.concatenate([[0], np.cumsum(ws)[:-1]]) if ws else [0], dtype=torch.int32)
+            es = [(self.cat_sizes[f] + 1) for f in self.embed_fields]
+            eoff = torch.tensor(np.concatenate([[0], np.cumsum(es)[:-1]]) if es else [0], dtype=torch.int32)
+            self._offs = (woff.to(dev), eoff.to(dev), torch.tensor(self.embed_fields or [0], dtype=torch.int32).to(dev))
+        woff, eoff, efield = self._offs
+        if not self.embed_fields:
+            efield = efield[:0]
+        wt = torch.cat(list(self.wide_tables)) if self.wide_on and len(self.wide_tables) else dense.new_zeros(1)
+        et = torch.cat([e.reshape(-1) for e in self.embeds]) if self.deep_on and len(self.embeds) else \
+            dense.new_zeros(1)
+        if not self.deep_on:
+            efield = efield[:0]
+        wide, A = _WdlGather.apply(dense.float().contiguous(), cats.long().contiguous(), wt, et, woff, eoff, efield,
+                                   self.embed_dim, self.wide_on and len(self.wide_tables) > 0, self.deep_on)
+        logit = torch.zeros(dense.shape[0], device=dev)
+        if self.wide_on:
+            logit = logit + dense @ self.wide_dense + self.bias + wide
+        if self.deep_on:
+            a = A
+            for W, act in zip(self.layers, self.acts):
+                a = act_fwd(act, a @ W[:, :-1].t() + W[:, -1])
+            logit = logit + (a @ self.final[:, :-1].t() + self.final[:, -1])[:, 0]
+        return logit
+
     def forward(self, dense: torch.Tensor, cats: torch.Tensor) -> torch.Tensor:
+        if dense.is_cuda and WDL_HIP and dense.shape[0]:
+            return self._hip_forward(dense, cats)
         n = dense.shape[0]
         logit = torch.zeros(n, device=dense.device)
         if self.wide_on:

@@ -1,0 +1,98 @@
+// Wide & Deep input kernels for MI355X (gfx950) (K20).
+//
+// Reference: WideAndDeep.forward / backward (J/core/dtrain/wdl/WideAndDeep.java:112-232):
+// the wide part sums one learned weight per (categorical field, category) -- a width-1
+// embedding bag -- and the deep part feeds [dense | per-field embeddings] to the MLP.
+//
+// MI355X design: the per-field gathers that PyTorch would run as one launch per field (plus a
+// concat) are one kernel that writes the deep input matrix row-major in a single coalesced pass
+// (one thread per output element: consecutive threads = consecutive columns of a row) and one
+// thread-per-row kernel for the wide sums; the backward scatters the gradients back into the
+// concatenated tables with fp32 atomics (embedding rows are shared by many rows of a batch).
+#include "common.h"
+
+namespace {
+
+struct WdlArgs {
+  const float* dense; int nd;                 // [n][nd]
+  const long* cats; int Fc;                   // [n][Fc] category index per field (< table rows)
+  const float* wtab; const int* woff;         // wide tables concatenated; field f at woff[f]
+  const float* etab; const int* eoff;         // embedding tables concatenated ([rows][D] each); e at eoff[e]
+  const int* efield; int E, D;                // embedding e reads field efield[e]
+  float* wide;                                // [n]           (fwd out / bwd in, nullable)
+  float* A; long lda;                         // [n][nd + E*D] (fwd out / bwd in, nullable)
+  float* dwtab; float* detab;                 // bwd out (accumulated)
+  long n;
+};
+
+__global__ __launch_bounds__(256) void wdl_wide_fwd_kernel(WdlArgs a) {
+  const long r = (long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= a.n) return;
+  float s = 0.f;
+  for (int f = 0; f < a.Fc; ++f) s += a.wtab[a.woff[f] + a.cats[r * a.Fc + f]];
+  a.wide[r] = s;
+}
+
+__global__ __launch_bounds__(256) void wdl_deep_fwd_kernel(WdlArgs a) {
+  const long w = a.nd + (long)a.E * a.D;
+  const long total = a.n * w;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / w;
+    const int c = (int)(i - r * w);
+    float v;
+    if (c < a.nd) {
+      v = a.dense[r * a.nd + c];
+    } else {
+      const int e = (c - a.nd) / a.D, d = (c - a.nd) - e * a.D;
+      v = a.etab[((long)a.eoff[e] + a.cats[r * a.Fc + a.efield[e]]) * a.D + d];
+    }
+    a.A[r * a.lda + c] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void wdl_wide_bwd_kernel(WdlArgs a) {
+  const long total = a.n * a.Fc;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / a.Fc;
+    const int f = (int)(i - r * a.Fc);
+    atomicAdd(&a.dwtab[a.woff[f] + a.cats[i]], a.wide[r]);
+  }
+}
+
+__global__ __launch_bounds__(256) void wdl_deep_bwd_kernel(WdlArgs a) {
+  const long ew = (long)a.E * a.D;
+  const long total = a.n * ew;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / ew;
+    const int c = (int)(i - r * ew), e = c / a.D, d = c - e * a.D;
+    atomicAdd(&a.detab[((long)a.eoff[e] + a.cats[r * a.Fc + a.efield[e]]) * a.D + d], a.A[r * a.lda + a.nd + c]);
+  }
+}
+
+long grid_of(long total) { long b = (total + 255) / 256; return b < 1 ? 1 : (b > 65536 ? 65536 : b); }
+
+}  // namespace
+
+#define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+// dir 0: forward (wide sums and/or deep input matrix), dir 1: backward (table gradients)
+SHIFU_API int shifu_wdl_gather(int dir, const float* dense, int nd, const long* cats, int Fc, const float* wtab,
+                               const int* woff, const float* etab, const int* eoff, const int* efield, int E, int D,
+                               float* wide, float* A, long lda, float* dwtab, float* detab, long n,
+                               hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (Fc < 0 || E < 0 || (E > 0 && D <= 0) || (A && lda < nd + (long)E * D)) return -1;
+  WdlArgs a{dense, nd, cats, Fc, wtab, woff, etab, eoff, efield, E, D, wide, A, lda, dwtab, detab, n};
+  if (dir == 0) {
+    if (wide && Fc > 0) hipLaunchKernelGGL(wdl_wide_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
+    if (A) hipLaunchKernelGGL(wdl_deep_fwd_kernel, dim3((unsigned)grid_of(n * (nd + (long)E * D))), dim3(256), 0,
+                              stream, a);
+  } else {
+    if (wide && dwtab && Fc > 0)
+      hipLaunchKernelGGL(wdl_wide_bwd_kernel, dim3((unsigned)grid_of(n * Fc)), dim3(256), 0, stream, a);
+    if (A && detab && E > 0)
+      hipLaunchKernelGGL(wdl_deep_bwd_kernel, dim3((unsigned)grid_of(n * (long)E * D)), dim3(256), 0, stream, a);
+  }
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
