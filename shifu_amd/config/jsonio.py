@@ -95,8 +95,22 @@ def load(path):
 
 
 def dump(obj, path):
-    with open(path, "w", encoding="utf-8") as f:
-        f.write(dumps(obj))
+    """Write atomically (temp file in the same directory + rename): ranks / processes that read
+    a ModelConfig / ColumnConfig while rank 0 rewrites it see the old or the new file, never a
+    truncated one."""
+    import os
+    import tempfile
+    d = os.path.dirname(os.path.abspath(path))
+    fd, tmp = tempfile.mkstemp(prefix=".tmp_", suffix=".json", dir=d)
+    try:
+        with os.fdopen(fd, "w", encoding="utf-8") as f:
+            f.write(dumps(obj))
+        os.chmod(tmp, os.stat(path).st_mode & 0o777 if os.path.exists(path) else 0o644)   # mkstemp is 0600
+        os.replace(tmp, path)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+        raise
 
 
 def to_double(v):
