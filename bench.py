@@ -33,6 +33,55 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+
+def _launch_ranks(argv) -> int | None:
+    """``--gpus N > 1`` without a torchrun environment: start N fresh worker processes (one per
+    GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, rendezvous on 127.0.0.1) and relay rank 0's JSON
+    line.  This parent never imports torch or touches the GPU and never execs: it only spawns
+    children and waits (the Guagua client's role, ``J/core/processor/TrainModelProcessor.java:
+    720-945``).  Returns the exit code, or None when this process should run the bench itself."""
+    if "WORLD_SIZE" in os.environ:
+        return None
+    n = 1
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            n = int(argv[i + 1])
+        elif a.startswith("--gpus="):
+            n = int(a.split("=", 1)[1])
+    if n <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out = procs[0].communicate()[0]
+    rc = procs[0].returncode
+    for p in procs[1:]:
+        try:
+            prc = p.wait(timeout=600 if rc == 0 else 30)
+        except subprocess.TimeoutExpired:
+            p.kill()                       # a peer stuck in a collective after a failure
+            prc = p.wait()
+        rc = rc or prc
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    if rc:
+        print(f"[bench] a rank failed (exit {rc})", file=sys.stderr, flush=True)
+    return rc
+
+
+if __name__ == "__main__":
+    _rc = _launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -93,15 +142,23 @@ def bench_mlp(a, dev, info):
         if dev.type == "cuda":
             torch.cuda.synchronize()
     dist.barrier(); sync()
+    tr.comm_events = []
     t0 = time.perf_counter()
     errs = []
     for i in range(a.steps):
         errs.append(tr.step(data, num_train_global=n_global))
-    sync(); dist.barrier()
+    sync()
+    t_local = time.perf_counter() - t0          # this rank's compute + its all-reduce waits
+    dist.barrier()
     dt = time.perf_counter() - t0
+    if dev.type == "cuda":
+        comm_ms = sum(e0.elapsed_time(e1) for e0, e1 in tr.comm_events)
+    else:
+        comm_ms = sum(e1 - e0 for e0, e1 in tr.comm_events) * 1e3
+    tr.comm_events = None
     log(f"[bench] train errors {['%.6f' % e for e in errs]}")
     flops_row = 2 * (a.cols * 500 + 500 * 200 + 200) * 2 + 2 * 500 * 200   # fwd+wgrad all, dgrad layer2
-    return dt, errs, flops_row
+    return dt, errs, flops_row, {"t_local": t_local, "comm_ms": comm_ms}
 
 
 def gbdt_half(a, dev, info):
@@ -360,23 +417,28 @@ def bench_treeinfer(a, dev, info):
     for c0 in range(0, C, 64):
         XT[c0:c0 + 64].normal_(generator=g)
     X = XT.t()                                  # [N, C] view of the feature-major matrix (no copy)
+    from shifu_amd.parallel import dist
     for _ in range(a.warmup):
         ens.score(X)
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         s = ens.score(X)
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
-    dt = time.perf_counter() - t0
-    ms = dt / a.steps * 1e3
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce_(t, "max")                  # every rank scores its own --rows (eval is row-sharded)
+    ms = float(t.item()) / a.steps * 1e3
+    total = a.rows * info.world_size
     return {
-        "metric": "GBT scoring rows/s (500 trees depth 7, 1000 raw fp64 columns)", "value": a.rows / (ms / 1e3),
-        "unit": "rows/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
+        "metric": "GBT scoring rows/s (500 trees depth 7, 1000 raw fp64 columns)", "value": total / (ms / 1e3),
+        "unit": "rows/s", "n_gpus": info.world_size, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp64",
         "data": "synthetic N(0,1) inputs, random-init trees",
-        "config": {"model": "GBT 500 trees depth 7", "global_batch": a.rows, "seq_len": None, "n_cols": C,
-                   "parallelism": "single"},
-        "node_visits_per_s": a.rows * n_trees * depth / (ms / 1e3), "score_checksum": float(s.sum()),
+        "config": {"model": "GBT 500 trees depth 7", "global_batch": total, "seq_len": None, "n_cols": C,
+                   "rows_per_gpu": a.rows, "parallelism": f"dp{info.world_size}"},
+        "node_visits_per_s": total * n_trees * depth / (ms / 1e3), "score_checksum": float(s.sum()),
     }
 
 
@@ -440,6 +502,8 @@ def main():
 
     from shifu_amd.parallel import dist
     info = dist.init_from_env()
+    if info.world_size != a.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={info.world_size}")
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
     if a.model == "varsel" and a.cols == 1000:
@@ -462,10 +526,13 @@ def main():
             a.cols = 64
         out = bench_stats(a, dev, info)
     else:
-        dt, errs, flops_row = bench_mlp(a, dev, info)
-        dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce_(dt_t, "max")
-        dt = float(dt_t.item())
+        dt, errs, flops_row, extra = bench_mlp(a, dev, info)
+        # max over ranks of the timed span; per-rank step-time spread and all-reduce time
+        tmax = torch.tensor([dt, extra["t_local"], extra["comm_ms"]], dtype=torch.float64, device=dev)
+        tmin = tmax.clone()
+        dist.all_reduce_(tmax, "max")
+        dist.all_reduce_(tmin, "min")
+        dt = float(tmax[0].item())
         ms = dt / a.steps * 1e3
         total_rows = a.rows * info.world_size
         value = total_rows * a.steps / dt
@@ -488,6 +555,9 @@ def main():
             "achieved_tflops": value * flops_row / 1e12,
             "baseline_note": "baseline = 1.48M rows/s derived from CHANGES.txt:268 (SURVEY §6)",
             "final_train_error": errs[-1] if errs else None,
+            "rank_step_ms_max": float(tmax[1]) / a.steps * 1e3, "rank_step_ms_min": float(tmin[1]) / a.steps * 1e3,
+            "allreduce_ms_per_step": float(tmax[2]) / a.steps,
+            "allreduce_ms_per_step_min_rank": float(tmin[2]) / a.steps,
         }
         if gpu:      # HBM headroom per rank (RCCL buffers for N > 1 must fit beside the rows)
             out["hbm_peak_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9

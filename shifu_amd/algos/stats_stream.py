@@ -191,6 +191,11 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
                         h[i] = h[i] + r[i]
                     _merge_moments(m, r[4])
     for bt in batches:
+        if bt.hist is None:     # no rows on this rank: zero partials shaped by the (global) cuts, so
+            # every rank sends same-sized buffers to the merging collectives
+            bt.hist = [[np.zeros(len(b) + 1, np.int64), np.zeros(len(b) + 1, np.int64),
+                        np.zeros(len(b) + 1, np.float64), np.zeros(len(b) + 1, np.float64)] for b in bt.bounds]
+            bt.mom = [[0, 0.0, 0.0, 0.0, 0.0, float("nan"), float("nan")] for _ in bt.bounds]
         _finish_batch(bt, binary, total, reduce, gather_objects, dev, n_bins)
     for cc in categorical:
         _finish_cat(cc, cat_state[cc.name], cat_missing[cc.name], binary, total, cate_max, gather_objects,
@@ -254,8 +259,7 @@ def _track_distinct(bt, vals, num_thr):
 def _finish_batch(bt, binary, total, reduce, gather_objects, dev, n_bins):
     # merge histograms / moments over ranks
     if reduce is not None:
-        flat = np.concatenate([np.concatenate([h[0], h[1], h[2], h[3]]).astype(np.float64) for h in bt.hist]) \
-            if bt.hist else np.zeros(1)
+        flat = np.concatenate([np.concatenate([h[0], h[1], h[2], h[3]]).astype(np.float64) for h in bt.hist])
         t = torch.as_tensor(flat, device=dev)
         reduce(t, "sum")
         flat = t.cpu().numpy()

@@ -100,12 +100,19 @@ def dump(obj, path):
     truncated one."""
     import os
     import tempfile
-    d = os.path.dirname(os.path.abspath(path))
+    path = os.path.realpath(path)              # a symlinked config: update the link's target
+    d = os.path.dirname(path)
     fd, tmp = tempfile.mkstemp(prefix=".tmp_", suffix=".json", dir=d)
     try:
         with os.fdopen(fd, "w", encoding="utf-8") as f:
             f.write(dumps(obj))
-        os.chmod(tmp, os.stat(path).st_mode & 0o777 if os.path.exists(path) else 0o644)   # mkstemp is 0600
+        if os.path.exists(path):
+            mode = os.stat(path).st_mode & 0o777
+        else:                                   # a new file: 0666 minus the process umask
+            um = os.umask(0)
+            os.umask(um)
+            mode = 0o666 & ~um
+        os.chmod(tmp, mode)                     # mkstemp creates 0600
         os.replace(tmp, path)
     except BaseException:
         if os.path.exists(tmp):

@@ -374,7 +374,9 @@ class TreeTrainer:
         mx = torch.stack([w.abs().max().double(), (w * gg).abs().max().double()])
         dist.all_reduce_(mx, "max")
         self.scale_w = _pack_scale(float(mx[0]), W_BITS)
-        self.scale_g = _pack_scale(float(mx[1]), G_BITS)
+        # margin 2^(GSH32+1): the root's u32 w*g mode quantises at scale_g / 2^GSH32, whose rounded
+        # |q| must stay < 2^20 - 1 so 2048 rows in one bin cannot reach 2^31 (gbdt_kernels.hip)
+        self.scale_g = _pack_scale(float(mx[1]), G_BITS, margin=2.0 ** (ROOT_GSH32 + 1))
         for t, tree in enumerate(trees):
             tw, ts = float(tot[t, 0]), float(tot[t, 1])
             tree.exists[1] = True
@@ -1209,14 +1211,15 @@ W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histo
 # root level of a single-tree (non-forest) build: u32 histogram modes, w*g on a grid 2^3 coarser
 # (gbdt_kernels.hip GSH32); SHIFU_GBDT_ROOT_U32=0 keeps the packed u64 kernel everywhere
 ROOT_U32 = os.environ.get("SHIFU_GBDT_ROOT_U32", "1") != "0"
-ROOT_G_DIV = 8
+ROOT_GSH32 = 3               # = gbdt_kernels.hip GSH32
+ROOT_G_DIV = 1 << ROOT_GSH32
 
 
-def _pack_scale(max_abs: float, bits: int) -> float:
-    """Largest 2^S with max_abs * 2^S <= 2^bits - 1 (so the rounded value stays < 2^bits)."""
+def _pack_scale(max_abs: float, bits: int, margin: float = 1.0) -> float:
+    """Largest 2^S with max_abs * 2^S <= 2^bits - margin (so the rounded value stays < 2^bits)."""
     if not max_abs > 0 or not math.isfinite(max_abs):
         return 1.0
-    return float(2.0 ** min(60, math.floor(math.log2((2.0 ** bits - 1) / max_abs))))
+    return float(2.0 ** min(60, math.floor(math.log2((2.0 ** bits - margin) / max_abs))))
 
 
 def _gain_py(imp, lw, ls, rw, rs):

@@ -25,6 +25,7 @@ every rank (replicated optimizer, no parameter server).
 from __future__ import annotations
 
 import math
+import time
 import os
 from dataclasses import dataclass, field
 
@@ -528,6 +529,7 @@ class MLPTrainer:
         self._ws = {}                  # chunk lane -> activations / deltas / ring slab workspace
         self._lane2 = None             # (side stream, gradient buffer) of the second chunk lane
         self.last_error = float("nan")
+        self.comm_events = None        # list -> (start, end) HIP events around each gradient all-reduce
 
     # --------------------------------------------------------------------------------------
     def prepare(self, x, y, s=None, stream: bool | None = None) -> TrainData:
@@ -837,6 +839,13 @@ class MLPTrainer:
             self._wflat = self.params.flat
         self.accumulate_gradients(data, row_lo, row_hi)
         self.gbuf[-2:] = self.err_acc.to(torch.float32)
+        ev0 = None
+        if self.comm_events is not None:
+            if self.gpu:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            else:
+                ev0 = time.perf_counter()
         if self._reducer is not None:
             self._reducer.wait()                        # launches any bucket not yet in flight
             tail = self.gbuf[-2:].clone()
@@ -844,6 +853,13 @@ class MLPTrainer:
             self.gbuf[-2:] = tail
         else:
             dist.all_reduce_(self.gbuf)
+        if ev0 is not None:                             # span of the (final) gradient all-reduce
+            if self.gpu:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
+            else:
+                ev1 = time.perf_counter()
+            self.comm_events.append((ev0, ev1))
         if self.dropout_rate > 0:
             self.grad.mul_(self._scale)                 # d(loss)/dW of the scaled connections
         self._wflat = self.params.flat

@@ -41,23 +41,25 @@ class _WdlGather(torch.autograd.Function):
         wide = torch.empty(n, device=dense.device) if want_wide else None
         A = torch.empty(n, nd + E * D, device=dense.device) if want_deep else None
         nat.call_hip("shifu_wdl_gather", 0, dense, nd, cats, Fc, wt, woff, et, eoff, efield, E, D, wide, A,
-                     nd + E * D, None, None, n, nat.stream_of(dense))
+                     nd + E * D, None, None, wt.numel(), et.numel(), n, nat.stream_of(dense))
         ctx.save_for_backward(cats, woff, eoff, efield)
-        ctx.meta = (n, nd, Fc, E, D, wt.numel(), et.numel())
+        ctx.meta = (n, nd, Fc, E, D, wt.numel(), et.numel(), bool(want_wide), bool(want_deep))
         return (wide if wide is not None else dense.new_zeros(n)), (A if A is not None else dense.new_zeros(n, 0))
 
     @staticmethod
     def backward(ctx, g_wide, g_A):
         from ..ops import _native as nat
         cats, woff, eoff, efield = ctx.saved_tensors
-        n, nd, Fc, E, D, nw, ne = ctx.meta
+        n, nd, Fc, E, D, nw, ne, want_wide, want_deep = ctx.meta
         dev = cats.device
-        dwt = torch.zeros(nw, device=dev)
-        det = torch.zeros(ne, device=dev)
-        gw = g_wide.contiguous() if g_wide is not None else None
-        gA = g_A.contiguous() if (g_A is not None and g_A.shape[1] == nd + E * D) else None
+        # an output that was not produced (the 1-element / 0-column placeholder) gets an
+        # autograd-materialised zero gradient: never scatter it into the placeholder tables
+        gw = g_wide.contiguous() if (want_wide and g_wide is not None) else None
+        gA = g_A.contiguous() if (want_deep and g_A is not None and g_A.shape[1] == nd + E * D) else None
+        dwt = torch.zeros(nw, device=dev) if gw is not None else None
+        det = torch.zeros(ne, device=dev) if gA is not None else None
         nat.call_hip("shifu_wdl_gather", 1, None, nd, cats, Fc, None, woff, None, eoff, efield, E, D, gw, gA,
-                     nd + E * D, dwt, det, n, nat.stream_of(cats))
+                     nd + E * D, dwt, det, nw, ne, n, nat.stream_of(cats))
         ddense = gA[:, :nd] if gA is not None else None
         return ddense, None, dwt, det, None, None, None, None, None, None
 

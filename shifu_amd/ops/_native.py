@@ -72,7 +72,7 @@ HIP_SIGNATURES = {
     "shifu_tree_code": "plli" "ppp" "pi" "s",
     "shifu_tree_walk_coded": "pli" "pp" "p" "pi" "pp" "iiii" "pl" "p" "s",
     # wdl_kernels.hip
-    "shifu_wdl_gather": "ipipipppppiipplppls",
+    "shifu_wdl_gather": "ipipipppppiipplppllls",
     # quantile_kernels.hip
     "shifu_pack_bits": "plip" "s",
     "shifu_qprep": "pllipid" "pppp" "s",

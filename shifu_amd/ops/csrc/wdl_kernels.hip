@@ -22,6 +22,8 @@ struct WdlArgs {
   float* wide;                                // [n]           (fwd out / bwd in, nullable)
   float* A; long lda;                         // [n][nd + E*D] (fwd out / bwd in, nullable)
   float* dwtab; float* detab;                 // bwd out (accumulated)
+  long nw, ne;                                // wide / embedding table sizes (floats): a table row
+                                              // index past them is skipped (read as 0, never written)
   long n;
 };
 
@@ -29,7 +31,10 @@ __global__ __launch_bounds__(256) void wdl_wide_fwd_kernel(WdlArgs a) {
   const long r = (long)blockIdx.x * 256 + threadIdx.x;
   if (r >= a.n) return;
   float s = 0.f;
-  for (int f = 0; f < a.Fc; ++f) s += a.wtab[a.woff[f] + a.cats[r * a.Fc + f]];
+  for (int f = 0; f < a.Fc; ++f) {
+    const long c = a.cats[r * a.Fc + f], k = a.woff[f] + c;
+    if (c >= 0 && k < a.nw) s += a.wtab[k];
+  }
   a.wide[r] = s;
 }
 
@@ -44,7 +49,8 @@ __global__ __launch_bounds__(256) void wdl_deep_fwd_kernel(WdlArgs a) {
       v = a.dense[r * a.nd + c];
     } else {
       const int e = (c - a.nd) / a.D, d = (c - a.nd) - e * a.D;
-      v = a.etab[((long)a.eoff[e] + a.cats[r * a.Fc + a.efield[e]]) * a.D + d];
+      const long c = a.cats[r * a.Fc + a.efield[e]], k = ((long)a.eoff[e] + c) * a.D + d;
+      v = (c >= 0 && k < a.ne) ? a.etab[k] : 0.f;
     }
     a.A[r * a.lda + c] = v;
   }
@@ -55,7 +61,8 @@ __global__ __launch_bounds__(256) void wdl_wide_bwd_kernel(WdlArgs a) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long r = i / a.Fc;
     const int f = (int)(i - r * a.Fc);
-    atomicAdd(&a.dwtab[a.woff[f] + a.cats[i]], a.wide[r]);
+    const long c = a.cats[i], k = a.woff[f] + c;
+    if (c >= 0 && k < a.nw) atomicAdd(&a.dwtab[k], a.wide[r]);
   }
 }
 
@@ -65,7 +72,8 @@ __global__ __launch_bounds__(256) void wdl_deep_bwd_kernel(WdlArgs a) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long r = i / ew;
     const int c = (int)(i - r * ew), e = c / a.D, d = c - e * a.D;
-    atomicAdd(&a.detab[((long)a.eoff[e] + a.cats[r * a.Fc + a.efield[e]]) * a.D + d], a.A[r * a.lda + a.nd + c]);
+    const long cat = a.cats[r * a.Fc + a.efield[e]], k = ((long)a.eoff[e] + cat) * a.D + d;
+    if (cat >= 0 && k < a.ne) atomicAdd(&a.detab[k], a.A[r * a.lda + a.nd + c]);
   }
 }
 
@@ -78,11 +86,12 @@ long grid_of(long total) { long b = (total + 255) / 256; return b < 1 ? 1 : (b >
 // dir 0: forward (wide sums and/or deep input matrix), dir 1: backward (table gradients)
 SHIFU_API int shifu_wdl_gather(int dir, const float* dense, int nd, const long* cats, int Fc, const float* wtab,
                                const int* woff, const float* etab, const int* eoff, const int* efield, int E, int D,
-                               float* wide, float* A, long lda, float* dwtab, float* detab, long n,
-                               hipStream_t stream) {
+                               float* wide, float* A, long lda, float* dwtab, float* detab, long nw, long ne,
+                               long n, hipStream_t stream) {
   if (n <= 0) return 0;
   if (Fc < 0 || E < 0 || (E > 0 && D <= 0) || (A && lda < nd + (long)E * D)) return -1;
-  WdlArgs a{dense, nd, cats, Fc, wtab, woff, etab, eoff, efield, E, D, wide, A, lda, dwtab, detab, n};
+  if (nw < 0 || ne < 0) return -1;
+  WdlArgs a{dense, nd, cats, Fc, wtab, woff, etab, eoff, efield, E, D, wide, A, lda, dwtab, detab, nw, ne, n};
   if (dir == 0) {
     if (wide && Fc > 0) hipLaunchKernelGGL(wdl_wide_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
     if (A) hipLaunchKernelGGL(wdl_deep_fwd_kernel, dim3((unsigned)grid_of(n * (nd + (long)E * D))), dim3(256), 0,

@@ -183,3 +183,21 @@ def test_meta_validation_rules(ref_resources):
     bad.train["params"]["DropoutRate"] = 1.0
     check_train(bad, r)
     assert not r and any("Learning rate" in c for c in r.causes) and any("Dropout" in c for c in r.causes)
+
+
+def test_jsonio_dump_follows_symlink_and_umask(tmp_path):
+    import os
+    from shifu_amd.config import jsonio
+    real = tmp_path / "real.json"
+    jsonio.dump({"a": 1}, str(real))
+    um = os.umask(0o027)
+    try:
+        jsonio.dump({"x": 2}, str(tmp_path / "new.json"))
+    finally:
+        os.umask(um)
+    assert (os.stat(tmp_path / "new.json").st_mode & 0o777) == 0o640
+    link = tmp_path / "link.json"
+    os.symlink(real, link)
+    jsonio.dump({"a": 3}, str(link))
+    assert os.path.islink(link)
+    assert jsonio.load(str(real))["a"] == 3

@@ -394,3 +394,49 @@ def test_norm_per_rank_host_memory(tmp_path):
     ranks = [int(open(f"{out}2.{r}").read()) for r in range(2)]
     print("norm rss growth MB: 1 rank %.1f, 2 ranks %s" % (single / 1e6, [round(r / 1e6, 1) for r in ranks]))
     assert max(ranks) < 0.72 * single, (single, ranks)
+
+
+def _rank_stats_one_empty(rank, world, port, root):
+    """Rank 1's byte range yields no valid rows (all filtered / no line start); rank 0 streams all."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIFU_FORCE_CPU="1")
+    from shifu_amd.config import environment
+    from shifu_amd.data import stream as DS
+    from shifu_amd.parallel import dist
+    from shifu_amd.steps.stats import run_stats
+    orig = DS.iter_model_data
+
+    def rows_of(mc, plan, chunk, r, w, *a, **k):
+        return iter(()) if r == 1 else orig(mc, plan, chunk, 0, 1, *a, **k)
+    DS.iter_model_data = rows_of
+    environment.props()["shifu.stats.streaming"] = "true"
+    environment.props()["shifu.stats.chunkMB"] = str(8 / 1024)
+    dist.init_from_env("gloo")
+    run_stats(root)
+    dist.barrier()
+    dist.shutdown()
+
+
+def test_streamed_stats_rank_without_rows(tmp_path, monkeypatch):
+    """a rank with no rows must still join every merge with same-sized partials."""
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    from shifu_amd.config import environment
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=1201, n_num=5, n_cat=2)
+    run_init(a)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    monkeypatch.setitem(environment.props(), "shifu.stats.streaming", "true")
+    run_stats(a)
+    mp.start_processes(_rank_stats_one_empty, args=(2, _port(), b), nprocs=2, join=True, start_method="spawn")
+    ca = json.load(open(os.path.join(a, "ColumnConfig.json")))
+    cb = json.load(open(os.path.join(b, "ColumnConfig.json")))
+    for x, y in zip(ca, cb):
+        assert x["columnBinning"].get("binBoundary") == y["columnBinning"].get("binBoundary"), x["columnName"]
+        assert x["columnBinning"].get("binCountPos") == y["columnBinning"].get("binCountPos"), x["columnName"]
+        for k in ("totalCount", "missingCount", "max", "min"):
+            assert x["columnStats"].get(k) == y["columnStats"].get(k), (x["columnName"], k)
+        if x["columnStats"].get("mean") is not None:
+            np.testing.assert_allclose(x["columnStats"]["mean"], y["columnStats"]["mean"], rtol=1e-9)

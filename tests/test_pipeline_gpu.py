@@ -81,18 +81,21 @@ def test_posttrain_bin_avg_gpu_matches_cpu(tmp_path, monkeypatch):
 @pytest.mark.parametrize("wide,deep", [(True, True), (True, False), (False, True)])
 def test_wdl_hip_gather_matches_torch(wide, deep, monkeypatch):
     """K20: the HIP wide-sum / deep-input gather (+ scatter backward) gives the torch path's
-    logits and parameter gradients."""
+    logits and parameter gradients.  The 40000-category field puts the wide offsets of the
+    deep-only case far past the 1-float placeholder table (the placeholder must never be
+    scattered into)."""
     import numpy as np
     import torch
     from shifu_amd.models import wdl
     torch.manual_seed(0)
-    net = wdl.WideDeepNet(5, [3, 40, 7], [0, 2], 4, [16], ["relu"], wide=wide, deep=deep).cuda()
+    sizes = [3, 40000, 7]
+    net = wdl.WideDeepNet(5, sizes, [0, 2], 4, [16], ["relu"], wide=wide, deep=deep).cuda()
     with torch.no_grad():
         for t in net.wide_tables:
             t.normal_()
     n = 3001
     dense = torch.randn(n, 5, device="cuda")
-    cats = torch.stack([torch.randint(0, s + 1, (n,)) for s in [3, 40, 7]], 1).cuda()
+    cats = torch.stack([torch.randint(0, s + 1, (n,)) for s in sizes], 1).cuda()
     out = {}
     for hip in (True, False):
         monkeypatch.setattr(wdl, "WDL_HIP", hip)
