@@ -306,7 +306,7 @@ class TrainStep:
                              "(scoring/generic.py)")
         if alg == "TENSORFLOW":
             return self._train_tensorflow()
-        if alg not in ("NN", "LR", "GBT", "RF", "WDL"):
+        if alg not in ("NN", "LR", "GBT", "RF", "WDL", "SVM"):
             raise ValueError(f"unsupported algorithm {alg}")
         is_tree = alg in TREE_ALGS
         if self.info.rank == 0:
@@ -378,6 +378,8 @@ class TrainStep:
                 verr = self._train_lr(trainer_id, p, ts, y, train_m, valid_m, sw)
             elif alg == "WDL":
                 verr = self._train_wdl(trainer_id, p, ts, y, train_m, valid_m, sw)
+            elif alg == "SVM":
+                verr = self._train_svm(trainer_id, p, ts, y, train_m, valid_m, sw)
             else:
                 verr = self._train_tree(trainer_id, p, ts, y, train_m, valid_m, sw)
             val_errors.append(verr)
@@ -622,6 +624,42 @@ class TrainStep:
                 break
         if self.info.rank == 0:
             lrmod.write_lr(mpath, tr.weights())
+        return verr
+
+    # -- SVM (legacy LOCAL, SVMTrainer.java:38-185) -----------------------------------------
+    def _train_svm(self, tid, p, ts, y, train_m, valid_m, sw):
+        """One C-SVC per bag on this process (the reference trains SVM locally only); rank 0 trains
+        and writes ``models/model<i>.svm``, the other ranks wait."""
+        from ..config import environment
+        from ..models import svm as S
+        mc, ms = self.mc, self.ms
+        verr = float("nan")
+        if self.info.rank == 0:
+            with dist.local_only():
+                X = np.asarray(ts.X, np.float32)
+                tri = np.nonzero(train_m & (sw > 0))[0]
+                cap = int(environment.get("shifu.svm.maxRows", 65536))
+                if len(tri) > cap:
+                    _log.warning("SVM: %d training rows > shifu.svm.maxRows=%d, training on a random subset",
+                                 len(tri), cap)
+                    tri = np.sort(np.random.default_rng(tid).choice(tri, cap, replace=False))
+                kern = S.kernel_name(p.get("Kernel", "linear"))
+                m = S.train_svm(X[tri], y[tri], kern, float(_num(p.get("Const"), 1.0)),
+                                float(_num(p.get("Gamma"), 1.0)), weights=sw[tri], device=self.dev,
+                                log=lambda s: _log.info("trainer %d: %s", tid, s))
+                if ts.vX is not None:
+                    vx, vy = np.asarray(ts.vX, np.float32), np.asarray(ts.vy, np.float64)
+                else:
+                    vi = np.nonzero(valid_m)[0]
+                    vx, vy = X[vi], y[vi].astype(np.float64)
+                if len(vy):
+                    verr = float(np.mean(m.predict(vx, self.dev) != vy))
+                tri_err = float(np.mean(m.predict(X[tri], self.dev) != y[tri])) if len(tri) else float("nan")
+                self._log_epoch(tid, 1, tri_err, verr)
+                S.write_svm(ms.pf.model_path(tid, "svm"), m, X.shape[1])
+                _log.info("Trainer #%d finish training: train error %.6f validation error %.6f (%s kernel)",
+                          tid, tri_err, verr, kern)
+        dist.barrier()
         return verr
 
     # -- WDL --------------------------------------------------------------------------------
