@@ -173,12 +173,13 @@ def gbdt_half(a, dev, info):
         torch.cuda.reset_peak_memory_stats(dev)
     from types import SimpleNamespace
     rows = a.gbdt_rows or (100_000_000 if dev.type == "cuda" else 2_000)
-    g = SimpleNamespace(rows=rows, cols=a.cols, steps=a.gbdt_steps, warmup=a.gbdt_warmup)
+    g = SimpleNamespace(rows=rows, cols=a.cols, steps=a.gbdt_steps, warmup=a.gbdt_warmup, levels=a.gbdt_levels)
     t0 = time.time()
     res = bench_gbdt(g, dev, info)
     log(f"[bench] gbdt: {res['ms_per_step']:.1f} ms/round ({time.time() - t0:.1f}s incl. data generation)")
     return {"gbdt_rounds_per_s": res["value"], "gbdt_ms_per_round": res["ms_per_step"],
             "gbdt_steps": a.gbdt_steps, "gbdt_warmup": a.gbdt_warmup, "gbdt_train_error": res.get("train_error"),
+            **({"gbdt_levels": res["levels"]} if res.get("levels") else {}),
             "gbdt_config": {"model": res["config"]["model"], "rows_per_gpu": rows, "n_cols": a.cols,
                             "global_rows": rows * info.world_size, "dtype": res["dtype"],
                             "parallelism": res["config"]["parallelism"]}}
@@ -496,6 +497,8 @@ def main():
                     help="rows per GPU of the GBDT half of the default line (default 100M on GPU)")
     ap.add_argument("--gbdt-steps", type=int, default=5, help="timed boosting rounds (0 = MLP only)")
     ap.add_argument("--gbdt-warmup", type=int, default=1)
+    ap.add_argument("--gbdt-levels", action="store_true",
+                    help="GBDT: per-level histogram table (rows, bytes, ms, TB/s; HIP events around each level)")
     ap.add_argument("--stream", action="store_true", help="varsel: rows streamed from host memory (HostRows)")
     ap.add_argument("--host-rows", type=int, default=2_000_000, help="varsel --stream: host buffer rows")
     a = ap.parse_args()
@@ -513,6 +516,7 @@ def main():
                   "treeinfer": 20_000_000 if gpu else 5_000,
                   "gbdt": 100_000_000 if gpu else 20_000}.get(a.model, 125_000_000 if gpu else 20_000)
     if a.model == "gbdt":
+        a.levels = a.gbdt_levels
         res = bench_gbdt(a, dev, info)
         out = res
     elif a.model == "varsel":

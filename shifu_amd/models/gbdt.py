@@ -36,7 +36,8 @@ from ..utils.log import get_logger
 _log = get_logger("models.gbdt")
 
 NB = 256
-FG = 32
+FG = 32                     # features per histogram work-item group (gbdt_kernels.hip FG)
+QF = 128                    # features per 128-B row record of the quad-blocked bins (QF)
 IMPURITY_IDS = {"variance": 0, "friedmanmse": 1, "entropy": 2, "gini": 3}
 LOSS_IDS = {"squared": 0, "halfgradsquared": 1, "absolute": 2, "log": 3}
 
@@ -191,13 +192,13 @@ class BinnedData:
 
     @property
     def group_stride(self) -> int:
-        """Bytes between consecutive feature groups of the blocked layout."""
-        return self.bins.shape[1] * FG
+        """Bytes between consecutive 128-feature record blocks of the quad-blocked layout."""
+        return self.bins.shape[1] * QF
 
     def codes(self) -> torch.Tensor:
         """Row-major ``[N, F]`` view (a copy) of the codes - CPU paths and tests."""
-        g, n, _ = self.bins.shape
-        return self.bins.permute(1, 0, 2).reshape(n, g * FG)[:, : self.n_feat]
+        q, n, _ = self.bins.shape
+        return self.bins.permute(1, 0, 2).reshape(n, q * QF)[:, : self.n_feat]
 
     @staticmethod
     def host_resident(codes, y, nbins, is_cat=None, sig=None, device="cuda", rows=None):
@@ -207,8 +208,7 @@ class BinnedData:
         n, f = codes.shape
         if rows is not None:
             n = len(rows)
-        g = (f + FG - 1) // FG
-        b = torch.empty(g, n, FG, dtype=torch.uint8, pin_memory=True)
+        b = torch.empty((f + QF - 1) // QF, n, QF, dtype=torch.uint8, pin_memory=True)
         BinnedData.blocked(codes, "cpu", rows, out=b)
         dptr = _host_device_pointer(b)
         d = BinnedData.from_codes(np.zeros((0, f), np.uint8), np.zeros(0), nbins, is_cat, None, device)
@@ -219,17 +219,18 @@ class BinnedData:
 
     @staticmethod
     def blocked(codes, device="cpu", rows=None, out=None) -> torch.Tensor:
-        """Row-major codes [N, F] (torch or numpy incl. a uint8 memmap, any int dtype) -> blocked
-        uint8 [G, N', 32] on ``device``, one 32-feature group at a time (optionally only ``rows``):
-        host memory stays at one group slice, never an int32 copy of the whole matrix."""
+        """Row-major codes [N, F] (torch or numpy incl. a uint8 memmap, any int dtype) -> quad-blocked
+        uint8 [Q, N', 128] on ``device`` (128 features of a row = one 128-B record), filled one
+        32-feature group at a time (optionally only ``rows``): host memory stays at one group
+        slice, never an int32 copy of the whole matrix."""
         n, f = codes.shape
         if rows is not None:
             n = len(rows)
-        g = (f + FG - 1) // FG
-        b = torch.zeros(g, n, FG, dtype=torch.uint8, device=device) if out is None else out
-        if out is not None and f % FG:
-            out[-1, :, f % FG:] = 0
-        for gi in range(g):
+        q = (f + QF - 1) // QF
+        b = torch.zeros(q, n, QF, dtype=torch.uint8, device=device) if out is None else out
+        if out is not None and f % QF:
+            out[-1, :, f % QF:] = 0
+        for gi in range((f + FG - 1) // FG):
             c0, c1 = gi * FG, min(f, (gi + 1) * FG)
             blk = codes[:, c0:c1] if rows is None else codes[rows, c0:c1]
             if isinstance(blk, np.ndarray):
@@ -237,7 +238,8 @@ class BinnedData:
                 if not blk.flags.writeable:        # read-only memmap slice: torch wants writable memory
                     blk = blk.copy()
                 blk = torch.from_numpy(blk)
-            b[gi, :, : c1 - c0] = blk.to(device=device, dtype=torch.uint8)
+            o = (gi % (QF // FG)) * FG
+            b[gi // (QF // FG), :, o: o + c1 - c0] = blk.to(device=device, dtype=torch.uint8)
         return b
 
     @staticmethod
@@ -284,6 +286,7 @@ class TreeTrainer:
         self.train_errors: list[float] = []
         self.valid_errors: list[float] = []
         self.timings = {"hist": 0.0, "split": 0.0, "partition": 0.0, "apply": 0.0}
+        self.level_stats = None        # list -> per-level histogram events (GPU), see bench_rounds
         self._root_level = False
         self._codes_cache = None
         self._nmod, self._npos = 0, data.n
@@ -358,6 +361,10 @@ class TreeTrainer:
         self._npos = P
         w = ws[0] if T == 1 else torch.cat(ws)
         gg = g if T == 1 else g.repeat(T)
+        # single GPU tree: (w, g) travel in position order with pos2row (the partition scatter moves
+        # them), so below the root the histogram reads them contiguously and gathers only the bins;
+        # at the root positions are rows
+        self._wg_pos = (w, gg) if (self.gpu and T == 1 and not c.is_multiclass) else None
         trees = [Tree(c.max_depth, weight) for _ in range(T)]
         rngs = [np.random.default_rng([c.seed, int(t)]) for t in tids]
         pos2row = torch.arange(P, dtype=torch.int32, device=self.dev)
@@ -409,6 +416,7 @@ class TreeTrainer:
                     z["sib_slot"] = slot_of[(z["tree"], z["id"] ^ 1)]
             n_built = sum(1 for z in nodes if z["built"])
             self._root_level = level == 1
+            self._level = level
             self._level_rngs = [rngs[z["tree"]] for z in nodes]
             t0 = time.perf_counter()
             hist = self._build_and_split(nodes, n_built, gg, w, pos2row, hist_prev)
@@ -524,19 +532,27 @@ class TreeTrainer:
             k = (m + step - 1) // step                      # chunks that are non-empty
             lo = z["start"] + np.arange(k, dtype=np.int64) * step
             hi = np.minimum(z["end"], lo + step)
-            b = np.empty((G, k, 4), dtype=np.int32)
-            b[:, :, 0] = z["slot"]
-            b[:, :, 1] = lo
-            b[:, :, 2] = hi
-            b[:, :, 3] = np.arange(G, dtype=np.int32)[:, None]
-            blocks.append((z["slot"], b.reshape(-1, 4)))
+            # order (quad, chunk, sub-group): the 4 groups of one 128-B record and row range are
+            # consecutive items (one XCD, gbdt_kernels.hip xcd_remap) and share every fetched line
+            Q = (G + 3) // 4
+            b = np.empty((Q, k, 4, 4), dtype=np.int32)
+            b[..., 0] = z["slot"]
+            b[..., 1] = lo[None, :, None]
+            b[..., 2] = hi[None, :, None]
+            grp = np.arange(Q, dtype=np.int32)[:, None, None] * 4 + np.arange(4, dtype=np.int32)[None, None, :]
+            b[..., 3] = grp
+            keep = (grp < G).repeat(k, axis=1).reshape(-1)
+            blocks.append((z["slot"], b.reshape(-1, 4)[keep]))
             ks.append(k)
         max_items = max(ks + [1])
         ni = np.full((len(nodes), G, max_items), -1, dtype=np.int32)
         off = 0
         for (slot, b), k in zip(blocks, ks):
-            ni[slot, :, :k] = off + np.arange(G * k, dtype=np.int32).reshape(G, k)
-            off += G * k
+            gi = b[:, 3]
+            # item id of (group, chunk): position of that row in b
+            chunk_of = np.searchsorted(np.unique(b[:, 1]), b[:, 1])
+            ni[slot, gi, chunk_of] = off + np.arange(len(b), dtype=np.int32)
+            off += len(b)
         items = np.concatenate([b for _, b in blocks]) if blocks else np.zeros((0, 4), np.int32)
         return items, ni, max_items
 
@@ -590,13 +606,24 @@ class TreeTrainer:
         t0 = time.perf_counter()
         if len(items):
             it = torch.from_numpy(items).to(self.dev)
+            ls = self.level_stats
+            if ls is not None:          # per-level histogram roofline (bench --gbdt-levels)
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
             if self._root_level and self._nmod == 0 and ROOT_U32:
                 slab = self._root_slab(items, it, w, g, st)
             else:
                 slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
                 p2r = None if self._root_level else pos2row      # root: positions are rows
-                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, w, g, it, len(items), slab, F,
-                             self.scale_w, self.scale_g, self._nmod, 0, st)
+                by_pos = p2r is not None and self._wg_pos is not None
+                wv, gv = self._wg_pos if by_pos else (w, g)
+                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, wv, gv, int(by_pos), it, len(items),
+                             slab, F, self.scale_w, self.scale_g, self._nmod, 0, st)
+            if ls is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
+                rows = int(sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"]))
+                ls.append({"level": self._level, "nodes_built": int(n_built), "rows": rows, "ev": (ev0, ev1)})
         else:
             slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
         built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
@@ -646,11 +673,11 @@ class TreeTrainer:
         c = getattr(self, "_root_cache", None)
         if c is None or c[0] is not w or c[1] != key:
             slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
-            nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, it, len(items), slab, self.F,
+            nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, 0, it, len(items), slab, self.F,
                          self.scale_w, self.scale_g, 0, 1, st)
             self._root_cache = (w, key, slab)          # holds w: its storage cannot be re-issued
         slab = self._root_cache[2]
-        nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, it, len(items), slab, self.F,
+        nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, 0, it, len(items), slab, self.F,
                      self.scale_w, self.scale_g, 0, 2, st)
         return slab
 
@@ -670,7 +697,7 @@ class TreeTrainer:
                 it = torch.from_numpy(items).to(self.dev)
                 slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
                 p2r = None if self._root_level else pos2row
-                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, w, gc, it, len(items), slab, F,
+                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, w, gc, 0, it, len(items), slab, F,
                              self.scale_w, self.scale_g, self._nmod, 0, st)
                 built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
                 feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
@@ -894,8 +921,13 @@ class TreeTrainer:
             new_pn = torch.empty_like(pos_node)
             t = lambda a, dt=np.int32: torch.from_numpy(np.ascontiguousarray(a.astype(dt))).to(self.dev)  # noqa
             # tensors (not .data_ptr() of temporaries) so every buffer outlives the launch
+            wg = self._wg_pos
+            nw_, ng_ = (torch.empty_like(wg[0]), torch.empty_like(wg[1])) if wg is not None else (None, None)
             nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, fbits, wpre, t(starts), t(nleft), t(cb),
-                         sf, t(child_l), t(child_r), new_p2r, new_pn, n, st)
+                         sf, t(child_l), t(child_r), new_p2r, new_pn, None if wg is None else wg[0],
+                         None if wg is None else wg[1], nw_, ng_, n, st)
+            if wg is not None:
+                self._wg_pos = (nw_, ng_)
             # child slot ids follow the order of new_nodes built by the caller (left, right per split)
             return new_p2r, new_pn, ranges
         # CPU path
@@ -1212,6 +1244,10 @@ W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histo
 # (gbdt_kernels.hip GSH32); SHIFU_GBDT_ROOT_U32=0 keeps the packed u64 kernel everywhere
 ROOT_U32 = os.environ.get("SHIFU_GBDT_ROOT_U32", "1") != "0"
 ROOT_GSH32 = 3               # = gbdt_kernels.hip GSH32
+# what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on
+# power-of-two grids (|w*g| < 2^23 of the grid, the root's u32 w*g mode 2^3 coarser), summed
+# exactly in int64 (so every rank and every run finds the same splits)
+HIST_DTYPE_LABEL = "int64 fixed-point hist (w 16-bit, w*g 23-bit grid; root w*g 20-bit)/uint8-bins"
 ROOT_G_DIV = 1 << ROOT_GSH32
 
 
@@ -1249,11 +1285,11 @@ def _gain_py(imp, lw, ls, rw, rs):
 # smoke + bench hooks
 # ------------------------------------------------------------------------------------------
 def synthetic_binned(n, f, device, seed=0, n_bins=256):
-    """uint8 codes (blocked [G, n, 32]) generated chunk-wise on the device (no int32 staging of the whole
+    """uint8 codes (quad-blocked [Q, n, 128]) generated chunk-wise on the device (no int32 staging of the whole
     matrix) + labels from a hidden rule on the first two features."""
     g = torch.Generator(device=device).manual_seed(seed)
     ng = (f + FG - 1) // FG
-    codes = torch.zeros(ng, n, FG, dtype=torch.uint8, device=device)
+    codes = torch.zeros((f + QF - 1) // QF, n, QF, dtype=torch.uint8, device=device)
     y = torch.empty(n, dtype=torch.float32, device=device)
     step = 1 << 21
     for r0 in range(0, n, step):
@@ -1261,7 +1297,8 @@ def synthetic_binned(n, f, device, seed=0, n_bins=256):
         blk = torch.randint(0, n_bins, (r1 - r0, f), generator=g, device=device, dtype=torch.int32)
         for gi in range(ng):
             c0, c1 = gi * FG, min(f, (gi + 1) * FG)
-            codes[gi, r0:r1, : c1 - c0] = blk[:, c0:c1].to(torch.uint8)
+            o = (gi % (QF // FG)) * FG
+            codes[gi // (QF // FG), r0:r1, o: o + c1 - c0] = blk[:, c0:c1].to(torch.uint8)
         x0 = blk[:, 0].float() / n_bins
         x1 = blk[:, 1].float() / n_bins
         y[r0:r1] = ((x0 + 0.5 * x1 + 0.1 * torch.rand(r1 - r0, generator=g, device=device)) > 0.8).float()
@@ -1291,12 +1328,31 @@ def bench_rounds(a, dev, info):
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dist.barrier()
+    if dev.type == "cuda" and getattr(a, "levels", False):
+        tr.level_stats = []
     t0 = time.perf_counter()
     tr.train(a.steps)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
+    levels = None
+    if tr.level_stats:               # per level: rows histogrammed, bytes of codes read, ms, TB/s
+        agg = {}
+        for e in tr.level_stats:
+            r = agg.setdefault(e["level"], {"level": e["level"], "rows": 0, "nodes_built": 0, "ms": 0.0})
+            r["rows"] += e["rows"]
+            r["nodes_built"] += e["nodes_built"]
+            r["ms"] += e["ev"][0].elapsed_time(e["ev"][1])
+        levels = []
+        for lv in sorted(agg):
+            r = agg[lv]
+            k = a.steps
+            gb = r["rows"] * (a.cols + 8) / k / 1e9         # codes + (w, g) per row touched
+            levels.append({"level": lv, "rows_per_round": r["rows"] // k, "nodes_built": r["nodes_built"] // k,
+                           "ms_per_round": round(r["ms"] / k, 3), "gb_per_round": round(gb, 2),
+                           "tb_per_s": round(gb / (r["ms"] / k), 2) if r["ms"] > 0 else None})
+        tr.level_stats = None
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     dist.all_reduce_(t, "max")
     dt = float(t.item())
@@ -1304,9 +1360,9 @@ def bench_rounds(a, dev, info):
         "metric": "GBDT rounds/sec (boosting rounds, depth 7, 256 bins)",
         "value": a.steps / dt, "unit": "rounds/s", "n_gpus": info.world_size, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32-hist/uint8-bins",
+        "vs_baseline": None, "dtype": HIST_DTYPE_LABEL,
         "data": "synthetic uint8 bin codes, labels from a hidden rule",
         "config": {"model": "GBT 500 trees depth=7 256 bins", "global_batch": rows * info.world_size,
                    "seq_len": None, "n_cols": a.cols, "parallelism": f"dp{info.world_size}"},
-        "timings_s": tr.timings, "train_error": tr.train_errors[-1],
+        "timings_s": tr.timings, "train_error": tr.train_errors[-1], "levels": levels,
     }

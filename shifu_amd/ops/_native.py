@@ -51,11 +51,11 @@ HIP_SIGNATURES = {
     "shifu_ring_set_mf": "i",
     "shifu_ring_set_dmamma": "i",
     # gbdt_kernels.hip
-    "shifu_gbdt_hist": "plpppp" "ipi" "dd" "l" "i" "s",
+    "shifu_gbdt_hist": "plppp" "i" "pipi" "dd" "l" "i" "s",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
     "shifu_gbdt_partition_flag": "plpppppppp" "ll" "pppp" "fi" "s",
     "shifu_gbdt_bitrank": "pppip" "s",
-    "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "l" "s",
+    "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "pppp" "l" "s",
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
     "shifu_gbdt_residual": "pppp" "p" "li" "s",
     # stats_kernels.hip

@@ -9,10 +9,15 @@
 //   GBT update  DTWorker.doCompute predict/output      J/core/dtrain/dt/DTWorker.java:620-670, Loss.java
 //
 // MI355X design:
-//   * bins are uint8, group-blocked [G][N][32] (32 features per group, G = Fp / 32); rows are
-//     grouped per node through a position->row permutation that is stably re-partitioned every
-//     level (rows of one node are a contiguous position range, so every histogram pass reads
-//     only that node's rows, each as one contiguous 32-B record per group).
+//   * bins are uint8, quad-blocked [Q][N][128]: 128 features of a row form one 128-B record (one
+//     L2 line), Q = Fp / 128; a histogram work item covers a 32-feature group = one 32-B quarter
+//     of the record.  Rows are grouped per node through a position->row permutation that is
+//     stably re-partitioned every level (rows of one node are a contiguous position range, so
+//     a histogram pass reads only that node's rows).  Below the root those rows are a sparse,
+//     ascending subset: each record read pulls its whole 128-B line, so the four groups of a
+//     quad are consecutive work items placed on ONE XCD (xcd_remap) and consume every line from
+//     that XCD's L2 -- the line-granularity gather that a [G][N][32] layout (a private 32-B slice
+//     per line and group) wastes 3/4 of (profiles/r3, per-level table).
 //   * histograms keep only (sum w, sum w*g) per bin: for variance / friedman-mse / binary
 //     entropy / binary gini the best split depends on count and sum only (the sum-of-squares
 //     terms cancel in the variance gain).  Both sums are int64 fixed point, packed into ONE
@@ -30,12 +35,26 @@ namespace {
 
 constexpr int NB = 256;        // max bins per feature (uint8 codes)
 constexpr int FG = 32;         // features per work-item group
+constexpr int QF = 128;        // features per row record (one 128-B line); 4 groups per record
+
+// XCD-aware bijective block remap: consecutive logical ids land on the same XCD (blocks b, b+8,
+// ... share an XCD under round-robin dispatch; speed only)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// byte offset of feature f of data row `row` in the quad-blocked layout (qs = N * 128)
+__device__ __forceinline__ size_t bin_off(long qs, long row, int f) {
+  return (size_t)(f >> 7) * qs + (size_t)row * QF + (f & (QF - 1));
+}
 
 struct HistArgs {
-  const uint8_t* bins; long gs;      // group-blocked bins [G][N][32]: gs = N * 32 bytes per group
+  const uint8_t* bins; long gs;      // quad-blocked bins [Q][N][128]: gs = N * 128 bytes per quad
   const int* pos2row;                // [N] position -> row id (nullptr: identity, the root level)
   const float* w;                    // [N] per-row weight (significance x subsample)
   const float* g;                    // [N] per-row target (label / pseudo residual)
+  int wg_by_pos;                     // 1: w / g are position-ordered (permuted with pos2row): contiguous reads
   const int* items;                  // [n_items][4] = {node, pos_lo, pos_hi, group}
   long long* slab;                   // [n_items][2][FG][NB] int64 fixed point
   int n_items, n_feat;
@@ -83,19 +102,20 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   constexpr int HFLUSH = 4096 / (RPP * HU);
   extern __shared__ __attribute__((aligned(16))) unsigned long long hsm[];   // [2][NB][16]
   uint32_t* hsm32 = (uint32_t*)hsm;
-  const int item = blockIdx.x;
+  const int item = xcd_remap(blockIdx.x, gridDim.x);     // a quad's 4 group items share an XCD
   const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
   for (int i = threadIdx.x; i < 2 * NB * 16; i += HT) hsm[i] = 0ull;
   __syncthreads();
   const int half = threadIdx.x & 1, r = threadIdx.x & 15, t2 = threadIdx.x >> 1;
-  const uint8_t* gb = a.bins + (size_t)grp * a.gs + half * 16;
+  const uint8_t* gb = a.bins + (size_t)(grp >> 2) * a.gs + (grp & 3) * FG + half * 16;
   unsigned long long* base = hsm + half * NB * 16;
   // u32 modes: two interleaved copies [half][bin][copy][16] (lane group parity picks the copy):
   // the 4 lanes that update the same feature then spread over 4 banks unless their bins agree
   // mod 2 (one 16-feature row per bin put them in 4 banks only when the bins differ mod 4)
   uint32_t* base32 = hsm32 + half * NB * 32 + (((threadIdx.x >> 4) & 1) << 4);
-  // w / g are indexed by the (virtual) row id, the bins by the data row
-  auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * 32); };
+  // w / g are indexed by the (virtual) row id -- or by position when wg_by_pos -- the bins by
+  // the data row
+  auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * QF); };
   long long accw[HNE], accg[HNE];
 #pragma unroll
   for (int k = 0; k < HNE; ++k) { accw[k] = 0; accg[k] = 0; }
@@ -158,13 +178,14 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
     // are clamped to hi - 1 (valid memory, no branch around a load: a branch would make the
     // compiler wait for the outstanding loads early) and get weight 0 when consumed.
     auto row_of = [&](int p) { const int pc = min(p, hi - 1); return a.pos2row ? a.pos2row[pc] : pc; };
+    auto wg_at = [&](int p, int rr) { return a.wg_by_pos ? min(p, hi - 1) : rr; };
     int rn[HU];
     float wc[HU], gc[HU];
     uint4 bc[HU];
 #pragma unroll
     for (int u = 0; u < HU; ++u) {
-      const int rr = row_of(lo + t2 + u * RPP);
-      wc[u] = a.w[rr]; gc[u] = a.g[rr]; bc[u] = rec(rr);
+      const int p = lo + t2 + u * RPP, rr = row_of(p), k = wg_at(p, rr);
+      wc[u] = a.w[k]; gc[u] = a.g[k]; bc[u] = rec(rr);
     }
 #pragma unroll
     for (int u = 0; u < HU; ++u) rn[u] = row_of(lo + STEP + t2 + u * RPP);
@@ -173,7 +194,8 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
       uint4 bn[HU];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
-        wn[u] = a.w[rn[u]]; gn[u] = a.g[rn[u]]; bn[u] = rec(rn[u]);
+        const int k = wg_at(p0 + STEP + t2 + u * RPP, rn[u]);
+        wn[u] = a.w[k]; gn[u] = a.g[k]; bn[u] = rec(rn[u]);
       }
 #pragma unroll
       for (int u = 0; u < HU; ++u) rn[u] = row_of(p0 + 2 * STEP + t2 + u * RPP);
@@ -195,9 +217,9 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
       uint4 bv[HU];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
-        const int rr = rows[u];
-        wv[u] = rr >= 0 ? a.w[rr] : 0.f;
-        gv[u] = rr >= 0 ? a.g[rr] : 0.f;
+        const int rr = rows[u], k = a.wg_by_pos ? p0 + t2 + u * RPP : rr;
+        wv[u] = rr >= 0 ? a.w[k] : 0.f;
+        gv[u] = rr >= 0 ? a.g[k] : 0.f;
         bv[u] = rr >= 0 ? rec(rr) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
@@ -443,7 +465,7 @@ __global__ __launch_bounds__(256) void gbdt_split_kernel(SplitArgs a) {
 // split_feat < 0 -> node not split this level (rows stay, flag = 2 "keep").
 // ---------------------------------------------------------------------------------------
 struct PartArgs {
-  const uint8_t* bins; long gs;   // group-blocked [G][N][32]
+  const uint8_t* bins; long gs;   // quad-blocked [Q][N][128]
   const int* pos2row;
   const int* pos_node;          // [N] node slot of each position (current level)
   const int* split_feat;        // [n_nodes]
@@ -470,7 +492,7 @@ __device__ __forceinline__ int partition_flag(const PartArgs& a, long p) {
   int fl = 0;
   if (f >= 0) {
     const long v = a.pos2row[p], row = a.nmod ? v % a.nmod : v;
-    const uint32_t b = a.bins[(size_t)(f >> 5) * a.gs + (size_t)row * 32 + (f & 31)];
+    const uint32_t b = a.bins[bin_off(a.gs, row, f)];
     if (a.is_cat[f]) fl = (a.cat_left[node * 8 + (b >> 5)] >> (b & 31)) & 1;
     else fl = (int)b <= a.split_bin[node] ? 1 : 0;
     if (a.pred && a.final_level) a.pred[row] += a.scale * (fl ? a.child_l_val[node] : a.child_r_val[node]);
@@ -501,6 +523,8 @@ struct ScatterArgs {
   const int* split_feat;
   const int* child_left; const int* child_right;                               // new node slots
   int* new_pos2row; int* new_pos_node;
+  // nullable: position-ordered per-row floats (w, g) moved with their rows (a pair of src / dst)
+  const float* w_src; const float* g_src; float* w_dst; float* g_dst;
   long n;
 };
 
@@ -511,6 +535,7 @@ __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
   if (node < 0 || a.split_feat[node] < 0) {        // unsplit / finished rows keep their place
     a.new_pos2row[p] = a.pos2row[p];
     a.new_pos_node[p] = -1;
+    if (a.w_dst) { a.w_dst[p] = a.w_src[p]; a.g_dst[p] = a.g_src[p]; }
     return;
   }
   const int s = a.node_start[node];
@@ -524,6 +549,7 @@ __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
   else { np = s + a.node_nleft[node] + (int)(p - s) - before; child = a.child_right[node]; }
   a.new_pos2row[np] = a.pos2row[p];
   a.new_pos_node[np] = child;
+  if (a.w_dst) { a.w_dst[np] = a.w_src[p]; a.g_dst[np] = a.g_src[p]; }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -532,7 +558,7 @@ __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
 // Used for validation rows, continuous-training recovery and GBT predict update.
 // ---------------------------------------------------------------------------------------
 struct TreeArgs {
-  const uint8_t* bins; long gs;   // group-blocked [G][N][32]
+  const uint8_t* bins; long gs;   // quad-blocked [Q][N][128]
   const int* rows;               // nullable: row ids (else 0..n-1)
   const int* feat; const int* thr; const uint32_t* cat_left; const float* value; const uint8_t* is_cat;
   float* pred; float scale; int set_mode;
@@ -547,7 +573,7 @@ __global__ void gbdt_apply_tree_kernel(TreeArgs a) {
   int id = 1;
   while (id < a.max_nodes && a.feat[id] >= 0) {
     const int f = a.feat[id];
-    const uint32_t b = a.bins[(size_t)(f >> 5) * a.gs + (size_t)row * 32 + (f & 31)];
+    const uint32_t b = a.bins[bin_off(a.gs, row, f)];
     bool left;
     if (a.is_cat[f]) left = (a.cat_left[id * 8 + (b >> 5)] >> (b & 31)) & 1;
     else left = (int)b <= a.thr[id];
@@ -596,10 +622,10 @@ __global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, const int* pos2row, const float* w, const float* g,
-                              const int* items, int n_items, void* slab, int n_feat, double scale_w,
-                              double scale_g, long nmod, int mode, hipStream_t stream) {
-  if (gs % 32 || n_items <= 0 || mode < 0 || mode > 2) return -1;
-  HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, items, (long long*)slab, n_items, n_feat,
+                              int wg_by_pos, const int* items, int n_items, void* slab, int n_feat,
+                              double scale_w, double scale_g, long nmod, int mode, hipStream_t stream) {
+  if (gs % QF || n_items <= 0 || mode < 0 || mode > 2 || (wg_by_pos && nmod)) return -1;
+  HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, wg_by_pos, items, (long long*)slab, n_items, n_feat,
              (float)scale_w, (float)(mode == 2 ? scale_g / (1 << GSH32) : scale_g), nmod};
   static const int pf = [] { const char* e = getenv("SHIFU_HIST_PF"); return e ? atoi(e) : 1; }();
   const size_t lds = 2 * NB * 16 * 8;      // the u32 modes still use 64 KiB for the transposed store
@@ -646,9 +672,12 @@ SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const int* po
 SHIFU_API int shifu_gbdt_partition_scatter(const int* pos2row, const int* pos_node, const void* fbits, const int* wpre,
                                            const int* node_start, const int* node_nleft, const int* node_cum0,
                                            const int* split_feat, const int* child_left, const int* child_right,
-                                           int* new_pos2row, int* new_pos_node, long n, hipStream_t stream) {
+                                           int* new_pos2row, int* new_pos_node, const float* w_src,
+                                           const float* g_src, float* w_dst, float* g_dst, long n,
+                                           hipStream_t stream) {
+  if ((w_dst != nullptr) != (g_dst != nullptr) || (w_dst && (!w_src || !g_src))) return -1;
   ScatterArgs a{pos2row, pos_node, (const unsigned long long*)fbits, wpre, node_start, node_nleft, node_cum0, split_feat, child_left,
-                child_right, new_pos2row, new_pos_node, n};
+                child_right, new_pos2row, new_pos_node, w_src, g_src, w_dst, g_dst, n};
   hipLaunchKernelGGL(gbdt_partition_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;

@@ -1,0 +1,80 @@
+"""Per-kernel time of one MLP training chunk at the bench shape (1000-500-200-1, sigmoid,
+2M-row chunk, one lane), measured with HIP events around every native call of
+``MLPTrainer._chunk_hip``; prints one JSON line (ms per kernel name and call index, total).
+
+    python tools/mlp_lab.py [--rows 2097152] [--iters 5] [--env KEY=VAL ...]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1 << 21)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--env", nargs="*", default=[])
+    ap.add_argument("--check", action="store_true", help="compare the chunk gradient with a second config")
+    a = ap.parse_args()
+    for kv in a.env:
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
+    import torch
+    from shifu_amd.models import nn as NN
+    from shifu_amd.ops import _native as nat
+    dev = torch.device("cuda")
+    spec = NN.MLPSpec(n_in=1000, hidden=[500, 200], acts=["sigmoid", "sigmoid"], n_out=1)
+    tr = NN.MLPTrainer(spec, device=dev, propagation="R", learning_rate=0.1, seed=7, chunk_rows=a.rows)
+    g = torch.Generator(device=dev).manual_seed(5)
+    k0 = spec.layer_kpad[0]
+    x = torch.empty(a.rows, k0, dtype=torch.bfloat16, device=dev)
+    x[:, :1000].normal_(generator=g)
+    x[:, 1000] = 1
+    x[:, 1001:] = 0
+    y = (torch.rand(a.rows, 1, generator=g, device=dev) > 0.5).float()
+    data = NN.TrainData(x, y, None, a.rows)
+    wb, wt = tr._weights_bf16()
+    real = nat.call_hip
+    rec = []
+
+    def timed(name, *args):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = real(name, *args)
+        e1.record()
+        rec.append((name, e0, e1))
+        return r
+    tr.grad.zero_()
+    tr._final_chunk = True
+    tr._chunk_hip(data, 0, a.rows, wb, wt)              # warm-up (workspace, code objects)
+    torch.cuda.synchronize()
+    nat.call_hip = timed
+    try:
+        tot = {}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        wall = 0.0
+        for _ in range(a.iters):
+            rec.clear()
+            e0.record()
+            tr._chunk_hip(data, 0, a.rows, wb, wt)
+            e1.record()
+            torch.cuda.synchronize()
+            wall += e0.elapsed_time(e1)
+            for i, (name, s0, s1) in enumerate(rec):
+                key = f"{i:02d}_{name}"
+                tot[key] = tot.get(key, 0.0) + s0.elapsed_time(s1)
+    finally:
+        nat.call_hip = real
+    out = {k: round(v / a.iters, 4) for k, v in sorted(tot.items())}
+    out["chunk_ms"] = round(wall / a.iters, 4)
+    out["rows"] = a.rows
+    out["rows_per_s_one_lane"] = round(a.rows / (wall / a.iters) * 1e3 / 1e6, 1)
+    out["env"] = a.env
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
