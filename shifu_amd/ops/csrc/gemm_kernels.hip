@@ -62,6 +62,7 @@ struct GemmArgs {
   const bf16_t* Hd; long ldhd; // EPI_DACT: stored derivative (when !act_deriv_from_output)
   int M, N, K, NB, n_valid, act, bias_col;
   float flat;
+  int dbg;                     // lab ablations (shifu_gemm_set_tune(9, v)); 0 in production
 };
 
 // STAGES = LDS buffers.  1: single 32 KiB buffer + register prefetch (two barriers per k-step,
@@ -444,6 +445,13 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_kernel(GemmArgs p) {
   const int m0 = (wg / ntn) * 256, n0 = (wg % ntn) * 256;
   f32x4 acc[4][8];
   gemm8_mainloop(p, acc, m0, n0, smem);
+  if (p.dbg & 2) {                                    // lab: main loop only (acc kept live)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" :: "v"(acc[i][j]));
+    return;
+  }
   epilogue_256<EPI, ACT>(p, acc, m0, n0, smem);
 }
 
@@ -479,6 +487,13 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
   const float y_pf = h.Y[my], s_pf = h.S ? h.S[my] : 1.f;
   f32x4 acc[4][8];
   gemm8_mainloop(p, acc, m0, 0, smem);
+  if (p.dbg & 2) {                                    // lab: main loop only (acc kept live)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" :: "v"(acc[i][j]));
+    return;
+  }
   float* red = (float*)(smem + 2 * G8_BUF);          // [2 wr][4 wc][128] row partials of z_out
   float* dl = red + 1024;                            // [256] output deltas
   float* gred = dl + 256;                            // [2 wr][256] output-wgrad partials
@@ -546,7 +561,7 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
   e_w = wave_sum_d(e_w);
   if (lane == 0) { ered[wid * 2] = e_c; ered[wid * 2 + 1] = e_w; }
   __syncthreads();
-  if (tid == 0) {
+  if (tid == 0 && !(p.dbg & 1)) {
     double a0 = 0.0, a1 = 0.0;
     for (int w = 0; w < 8; ++w) { a0 += ered[w * 2]; a1 += ered[w * 2 + 1]; }
     atomicAdd(h.err, a0);
@@ -739,9 +754,11 @@ static int g_stages = 1;     // LDS stages of the MLP GEMMs (A/B switch for tuni
 static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N >= 512, K >= 512; else 128x128),
                              // 3 = 8-phase whenever M >= 64K and N >= 256, 4 = 128x128 only
 static int g_wg_interleave = 1;   // wgrad row splits: 1 interleaved 64-row steps (-3% wgrad1 at 1M rows), 0 contiguous
+static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
   if (key == 2) { g_wg_interleave = val; return 0; }
+  if (key == 9) { g_dbg = val; return 0; }
   return -1;
 }
 SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b == 3 || b == 4) ? b : 0; return 0; }
@@ -753,7 +770,7 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   if (K % BK || N % 4 || ldc % 8 || lda % 8 || ldb % 8 || M <= 0 || N <= 0) return -1;
   if (epi == EPI_DACT && H != nullptr && ldh % 8) return -1;     // 16-B row-segment loads of H
   GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, (bf16_t*)C2, ldc2,
-             (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat};
+             (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat, g_dbg};
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = 2 * g_stages * TILE_BYTES;
   if (act < 0 || act > 8 || epi < 0 || epi > 2) return -2;
@@ -804,7 +821,7 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
     return -1;
   if (!act_deriv_from_output(act) || act == 6 || out_act < 0 || out_act > 8) return -2;
   GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)D, ldd, nullptr, 0, nullptr, 0, nullptr, 0,
-             M, N, K, NB, n_valid, act, 1, 0.f};
+             M, N, K, NB, n_valid, act, 1, 0.f, g_dbg};
   HeadArgs h{W, Y, S, GW, GWslab, err, KH, out_act, loss, flat_out, flat_hid};
   const int grid = (M + 255) / 256;
 #define HEAD_L(A_) hipLaunchKernelGGL((gemm_head_8ph_kernel<A_>), dim3(grid), dim3(G8_T), HEAD_LDS, stream, p, h)

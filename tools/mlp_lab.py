@@ -17,7 +17,8 @@ def main():
     ap.add_argument("--rows", type=int, default=1 << 21)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--env", nargs="*", default=[])
-    ap.add_argument("--check", action="store_true", help="compare the chunk gradient with a second config")
+    ap.add_argument("--dbg", type=int, nargs="*", default=[0],
+                    help="GEMM lab ablation bits per run (1: no head err atomics, 2: main loops only)")
     a = ap.parse_args()
     for kv in a.env:
         k, v = kv.split("=", 1)
@@ -51,6 +52,13 @@ def main():
     tr._final_chunk = True
     tr._chunk_hip(data, 0, a.rows, wb, wt)              # warm-up (workspace, code objects)
     torch.cuda.synchronize()
+    for dbg in a.dbg:
+        nat.call_hip("shifu_gemm_set_tune", 9, dbg)
+        run(a, tr, data, wb, wt, timed, real, rec, dbg, nat, torch)
+    nat.call_hip("shifu_gemm_set_tune", 9, 0)
+
+
+def run(a, tr, data, wb, wt, timed, real, rec, dbg, nat, torch):
     nat.call_hip = timed
     try:
         tot = {}
@@ -73,7 +81,8 @@ def main():
     out["rows"] = a.rows
     out["rows_per_s_one_lane"] = round(a.rows / (wall / a.iters) * 1e3 / 1e6, 1)
     out["env"] = a.env
-    print(json.dumps(out))
+    out["dbg"] = dbg
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
