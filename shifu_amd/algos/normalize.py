@@ -329,3 +329,167 @@ def tree_bin_codes_gpu(ccs, table, columns, device="cuda"):
     out = torch.zeros(table.n, max(1, len(columns)), dtype=torch.uint8, device=dev)
     stats_ops.bin_codes(vals, is_cat, bounds, ncat, out)
     return out.cpu().numpy().astype(np.int32), np.array(nbins, np.int32), np.array(is_cat, np.uint8)
+
+
+# ---- streamed norm: one plan, one fused kernel pass per chunk (K5) ------------------------------
+class NormPlan:
+    """Everything the per-chunk pass needs, built once for the ``norm`` columns: the width-1
+    columns' kernel specs (device tensors), the host-side one-hot columns, and the tree-code spec.
+    ``run(table)`` normalizes one chunk: on the GPU one ``norm_codes`` launch reads the raw values
+    once and writes the fp32 rows and/or the bf16 GEMM-ready rows (``kpad`` wide, bias column =
+    1 at ``width``) and/or the uint8 CleanedData codes; on the CPU the numpy oracle does the same."""
+
+    def __init__(self, mc, ccs, cols, norm_type: str | None = None, want_x: bool = True,
+                 want_codes: bool = False, x_dtype: str = "float32", device=None):
+        import torch
+        self.mc, self.cols = mc, list(cols)
+        self.nt = norm_type or mc.norm_type
+        self.cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
+        self.want_x, self.want_codes = want_x, want_codes
+        self.x_dtype = x_dtype
+        self.dev = torch.device(device) if device is not None else None
+        self.gpu = self.dev is not None and self.dev.type == "cuda"
+        specs, names, nums, host_cols, gpu_cols = [], [], [], [], []
+        pos = 0
+        for cc in self.cols:
+            s = _gpu_spec(cc, self.nt, self.cutoff)
+            if s is None:
+                width = norm_width(cc, self.nt if self.nt == "ONEHOT" else "ONEHOT")
+                host_cols.append((cc, pos, width))
+                names.extend(f"{cc.name}_{i}" for i in range(width))
+                nums.extend([cc.num] * width)
+                pos += width
+            else:
+                s["out_col"] = pos
+                specs.append(s)
+                gpu_cols.append(cc)
+                names.append(cc.name)
+                nums.append(cc.num)
+                pos += 1
+        self.width, self.names, self.nums = pos, names, nums
+        self.specs, self.gpu_cols, self.host_cols = specs, gpu_cols, host_cols
+        self.kpad = ((pos + 1 + 127) // 128) * 128            # bf16 rows: values + bias + zero padding
+        nb, ic, ncat, bounds = [], [], [], []
+        for cc in self.cols:
+            if cc.is_categorical():
+                k = len(cc.bin_category or [])
+                nb.append(k + 1); ic.append(1); ncat.append(k); bounds.append(None)
+            else:
+                bb = cc.bin_boundary or [float("-inf")]
+                nb.append(max(1, len(bb))); ic.append(0); ncat.append(0); bounds.append(bb)
+        self.nbins, self.is_cat = np.array(nb, np.int32), np.array(ic, np.uint8)
+        self.code_dtype = np.uint8 if self.nbins.max(initial=1) <= 256 else np.int16
+        self._ncat, self._cbounds = ncat, bounds
+        self._dev_specs = None
+        self._bufs = {}
+
+    def _device_specs(self):
+        import torch
+        from ..ops import stats_ops as so
+        if self._dev_specs is not None:
+            return self._dev_specs
+        F = len(self.gpu_cols)
+        ip = np.zeros((max(F, 1), 8), np.int32)
+        dp = np.zeros((max(F, 1), 8), np.float64)
+        bounds, tables = [], []
+        for f, s in enumerate(self.specs):
+            b = list(s.get("bounds") or [float("-inf")])
+            t = list(s.get("table") or [0.0])
+            nt = int(s["ncat"]) if s["mode"] == "cat_index" else len(t)
+            ip[f] = [so.NM[s["mode"]], s["out_col"], len(bounds), len(b), len(tables), nt, int(s.get("zflag", 0)), 0]
+            bounds.extend(b)
+            tables.extend(t)
+            dp[f, :5] = [s.get("mean", 0.0) or 0.0, s.get("std", 0.0) or 0.0, s.get("cutoff", 6.0),
+                         s.get("zmean", 0.0) or 0.0, s.get("zstd", 0.0) or 0.0]
+        cb, coff = so.pack_bounds(self._cbounds)
+        cip = np.zeros((len(self.cols), 4), np.int32)
+        for f in range(len(self.cols)):
+            cip[f] = [int(self.is_cat[f]), coff[f], coff[f + 1] - coff[f], int(self._ncat[f])]
+        t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(self.dev)   # noqa: E731
+        self._dev_specs = dict(ip=t(ip, torch.int32), dp=t(dp, torch.float64),
+                               bounds=t(np.asarray(bounds or [0.0], np.float64), torch.float64),
+                               tables=t(np.asarray(tables or [0.0], np.float64), torch.float64),
+                               cip=t(cip, torch.int32), cbounds=t(cb, torch.float64))
+        return self._dev_specs
+
+    def _buf(self, key, shape, dtype, init=None):
+        import torch
+        b = self._bufs.get(key)
+        if b is None or b.shape[0] < shape[0] or tuple(b.shape[1:]) != tuple(shape[1:]):
+            b = torch.zeros(shape, dtype=dtype, device=self.dev)
+            if init is not None:
+                init(b)
+            self._bufs[key] = b
+        return b[: shape[0]]
+
+    def run(self, table) -> dict:
+        """-> {"X": fp32 [n, width] | "Xb": uint16 (bf16 bits) [n, kpad], "codes": [n, F]} (numpy)."""
+        n = table.n
+        out = {}
+        bf16 = self.want_x and self.x_dtype == "bf16"
+        if not self.gpu:
+            if self.want_x:
+                X, _, _ = normalize_table(self.mc, None, table, columns=self.cols, norm_type=self.nt)
+                if bf16:
+                    import torch
+                    xb = np.zeros((n, self.kpad), np.uint16)
+                    xb[:, : self.width] = torch.from_numpy(np.ascontiguousarray(X)).to(torch.bfloat16) \
+                        .view(torch.int16).numpy().view(np.uint16)
+                    xb[:, self.width] = 0x3F80                       # bf16 1.0 (bias neuron)
+                    out["Xb"] = xb
+                else:
+                    out["X"] = X
+            if self.want_codes:
+                C, _, _ = tree_bin_codes(None, table, self.cols)
+                out["codes"] = C.astype(self.code_dtype)
+            return out
+        import torch
+        from ..ops import _native as nat
+        need_codes = self.want_codes and self.code_dtype == np.uint8
+        dev_cols = self.gpu_cols if not need_codes else self.cols
+        vals = torch.as_tensor(_raw_matrix(dev_cols, table), device=self.dev) if dev_cols else None
+        ds = self._device_specs()
+        outf = self._buf("f", (n, max(self.width, 1)), torch.float32) if (self.want_x and not bf16) else None
+        outb = self._buf("b", (n, self.kpad), torch.bfloat16,
+                         init=lambda b: b[:, self.width].fill_(1.0)) if bf16 else None
+        codes = self._buf("c", (n, max(1, len(self.cols))), torch.uint8) if need_codes else None
+        if vals is not None and n:
+            if need_codes and len(self.gpu_cols) != len(self.cols):
+                # one-hot columns present: the width-1 specs index the gpu columns only -> two passes
+                sub = torch.as_tensor(_raw_matrix(self.gpu_cols, table), device=self.dev)
+                rc = nat.call_hip("shifu_norm_codes", sub, sub.stride(0), n, len(self.gpu_cols), ds["ip"], ds["dp"],
+                                  ds["bounds"], ds["tables"], None, None, outf, 0 if outf is None else outf.stride(0),
+                                  outb, 0 if outb is None else outb.stride(0), None, 0, nat.stream_of(sub)) \
+                    if self.gpu_cols and (outf is not None or outb is not None) else 0
+                rc2 = nat.call_hip("shifu_norm_codes", vals, vals.stride(0), n, len(self.cols), None, None, None, None,
+                                   ds["cip"], ds["cbounds"], None, 0, None, 0, codes, codes.stride(0),
+                                   nat.stream_of(vals))
+                rc = rc or rc2
+            else:
+                want_v = outf is not None or outb is not None
+                rc = nat.call_hip("shifu_norm_codes", vals, vals.stride(0), n, vals.shape[0],
+                                  ds["ip"] if want_v else None, ds["dp"] if want_v else None, ds["bounds"], ds["tables"],
+                                  ds["cip"] if need_codes else None, ds["cbounds"] if need_codes else None,
+                                  outf, 0 if outf is None else outf.stride(0), outb,
+                                  0 if outb is None else outb.stride(0), codes,
+                                  0 if codes is None else codes.stride(0), nat.stream_of(vals))
+            if rc:
+                raise RuntimeError(f"shifu_norm_codes failed rc={rc}")
+        for cc, p0, width in self.host_cols:
+            oh = torch.as_tensor(normalize_column(cc, table[cc.name], self.nt, self.cutoff), dtype=torch.float32,
+                                 device=self.dev)
+            if outf is not None:
+                outf[:, p0: p0 + width] = oh
+            if outb is not None:
+                outb[:, p0: p0 + width] = oh.to(torch.bfloat16)
+        if outf is not None:
+            out["X"] = outf[:, : self.width].cpu().numpy()
+        if outb is not None:
+            out["Xb"] = outb.view(torch.int16).cpu().numpy().view(np.uint16)
+        if self.want_codes:
+            if codes is not None:
+                out["codes"] = codes.cpu().numpy()
+            else:
+                C, _, _ = tree_bin_codes(None, table, self.cols)
+                out["codes"] = C.astype(self.code_dtype)
+        return out

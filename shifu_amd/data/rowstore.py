@@ -1,0 +1,188 @@
+"""Out-of-core row stores for the step caches (NormalizedData / CleanedData / eval scores).
+
+SURVEY §5.7: ``norm`` and ``eval`` stream a rank's byte range chunk by chunk (the reference
+streams rows through Pig, ``P/Normalize.pig:35-46`` / ``P/Eval.pig:29-41``), so a cache is
+written without its row count known in advance and without the whole shard in host memory:
+
+* :class:`NpyAppender` appends row blocks to a ``.npy`` file whose header reserves room for the
+  final shape and is rewritten on close (a plain ``np.load``-able file, memory-mappable).
+* a data-parallel cache is one ``part-RRRRR/`` directory per rank plus a top-level
+  ``meta.json`` listing ``parts`` and their row counts; :class:`RowParts` presents the parts
+  of one array as a single row-indexable array (slices copy only the rows they touch), so
+  training's row shards and chunk streams read straight from the part files.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+HEADER_BYTES = 256          # reserved .npy header: magic + version + len + dict, padded to 256
+
+
+def _header(dtype: np.dtype, shape: tuple) -> bytes:
+    d = {"descr": np.lib.format.dtype_to_descr(np.dtype(dtype)), "fortran_order": False, "shape": tuple(shape)}
+    body = repr(d).encode("latin1")
+    head = b"\x93NUMPY\x01\x00"
+    room = HEADER_BYTES - len(head) - 2
+    if len(body) + 1 > room:
+        raise ValueError("npy header does not fit the reserved space")
+    body = body + b" " * (room - len(body) - 1) + b"\n"
+    return head + len(body).to_bytes(2, "little") + body
+
+
+class NpyAppender:
+    """Append ``[k, *row_shape]`` blocks of one dtype to ``path``; ``close()`` fixes the header."""
+
+    def __init__(self, path: str, dtype, row_shape: tuple = ()):
+        self.path, self.dtype, self.row_shape = path, np.dtype(dtype), tuple(row_shape)
+        self.rows = 0
+        self.f = open(path, "wb")
+        self.f.write(_header(self.dtype, (0,) + self.row_shape))
+
+    def append(self, a) -> None:
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        if a.shape[1:] != self.row_shape:
+            raise ValueError(f"{self.path}: row shape {a.shape[1:]} != {self.row_shape}")
+        self.f.write(a.tobytes(order="C"))
+        self.rows += a.shape[0]
+
+    def close(self) -> int:
+        if self.f is not None:
+            self.f.seek(0)
+            self.f.write(_header(self.dtype, (self.rows,) + self.row_shape))
+            self.f.close()
+            self.f = None
+        return self.rows
+
+    def abort(self) -> None:
+        if self.f is not None:
+            self.f.close()
+            self.f = None
+        if os.path.exists(self.path):
+            os.remove(self.path)
+
+
+class RowParts:
+    """Row-wise concatenation of memory-mapped part arrays (same dtype / trailing shape).
+
+    Supports ``len``, ``shape``, ``dtype``, ``ndim``, basic row slices (``a[lo:hi]``, ``a[lo:hi, cols]``),
+    integer / boolean row indexing, and ``np.asarray`` (which materialises every row)."""
+
+    def __init__(self, parts: list):
+        if not parts:
+            raise ValueError("RowParts needs at least one part")
+        self.parts = parts
+        self.offsets = np.cumsum([0] + [len(p) for p in parts])
+        self.dtype = parts[0].dtype
+        self.shape = (int(self.offsets[-1]),) + tuple(parts[0].shape[1:])
+        self.ndim = len(self.shape)
+
+    def __len__(self):
+        return self.shape[0]
+
+    @property
+    def nbytes(self) -> int:
+        return int(np.prod(self.shape)) * self.dtype.itemsize
+
+    def _rows(self, lo: int, hi: int):
+        out = []
+        for k, p in enumerate(self.parts):
+            a, b = max(lo, self.offsets[k]), min(hi, self.offsets[k + 1])
+            if a < b:
+                out.append(p[a - self.offsets[k]: b - self.offsets[k]])
+        return out
+
+    def __getitem__(self, idx):
+        rest = ()
+        if isinstance(idx, tuple):
+            idx, rest = idx[0], idx[1:]
+        if isinstance(idx, slice):
+            lo, hi, step = idx.indices(len(self))
+            if step != 1:
+                return self[np.arange(lo, hi, step)][(slice(None),) + rest] if rest else self[np.arange(lo, hi, step)]
+            blocks = self._rows(lo, hi)
+            if len(blocks) == 1:
+                out = blocks[0]
+            elif blocks:
+                out = np.concatenate(blocks)
+            else:
+                out = np.empty((0,) + self.shape[1:], self.dtype)
+        elif isinstance(idx, (int, np.integer)):
+            i = int(idx) + (len(self) if idx < 0 else 0)
+            k = int(np.searchsorted(self.offsets, i, side="right") - 1)
+            out = self.parts[k][i - self.offsets[k]]
+        else:
+            ix = np.asarray(idx)
+            if ix.dtype == bool:
+                ix = np.nonzero(ix)[0]
+            out = np.empty((len(ix),) + self.shape[1:], self.dtype)
+            k = np.searchsorted(self.offsets, ix, side="right") - 1
+            for pk in np.unique(k):
+                sel = k == pk
+                out[sel] = self.parts[pk][ix[sel] - self.offsets[pk]]
+        return out[(slice(None),) + rest] if rest else out
+
+    def __array__(self, dtype=None, copy=None):
+        a = self[0: len(self)]
+        a = np.array(a) if not isinstance(a, np.ndarray) or isinstance(a, np.memmap) else a
+        return a.astype(dtype) if dtype is not None else a
+
+
+def write_parts_meta(path: str, meta: dict, part_rows: list) -> None:
+    """Top-level meta.json of a partitioned cache (rank 0, after every rank closed its part)."""
+    parts = [{"dir": f"part-{r:05d}", "n": int(n)} for r, n in enumerate(part_rows)]
+    meta = dict(meta, n=int(sum(part_rows)), parts=parts)
+    tmp = os.path.join(path, ".meta.json.tmp")
+    with open(tmp, "w") as f:
+        json.dump(meta, f, indent=1)
+    os.replace(tmp, os.path.join(path, "meta.json"))
+
+
+def load_parts(path: str, meta: dict, mmap: bool = True) -> dict:
+    """name -> RowParts (or the single part's array) of a partitioned cache."""
+    arrays = {}
+    parts = [p for p in meta["parts"] if p["n"] > 0] or meta["parts"][:1]
+    names = sorted({fn[:-4] for p in parts for fn in os.listdir(os.path.join(path, p["dir"])) if fn.endswith(".npy")})
+    for name in names:
+        arrs = [np.load(os.path.join(path, p["dir"], f"{name}.npy"), mmap_mode="r" if mmap else None) for p in parts]
+        arrays[name] = arrs[0] if len(arrs) == 1 else RowParts(arrs)
+    return arrays
+
+
+class Bf16Rows:
+    """Float view of a bf16 GEMM-ready NormalizedData matrix (``Xb``: uint16 bf16 bits
+    [n, kpad], values in the first ``width`` columns, bias column 1.0 at ``width``).  Row /
+    column indexing returns float32 values of the ``width`` input columns; ``raw`` is the padded
+    bf16 matrix that the MLP trainer streams to HBM without any cast or padding pass."""
+
+    def __init__(self, raw, width: int):
+        self.raw, self.width = raw, int(width)
+        self.shape = (len(raw), self.width)
+        self.dtype = np.dtype(np.float32)
+        self.ndim = 2
+
+    def __len__(self):
+        return self.shape[0]
+
+    @property
+    def nbytes(self) -> int:
+        return self.shape[0] * self.width * 4
+
+    @staticmethod
+    def to_f32(u16) -> np.ndarray:
+        u = np.ascontiguousarray(u16, dtype=np.uint16)
+        return (u.astype(np.uint32) << 16).view(np.float32)
+
+    def __getitem__(self, idx):
+        rest = ()
+        if isinstance(idx, tuple):
+            idx, rest = idx[0], idx[1:]
+        rows = self.raw[idx]
+        out = self.to_f32(rows[..., : self.width])
+        return out[(slice(None),) + rest] if rest else out
+
+    def __array__(self, dtype=None, copy=None):
+        a = self[0: len(self)]
+        return a.astype(dtype) if dtype is not None else a

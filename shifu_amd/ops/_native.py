@@ -62,6 +62,7 @@ HIP_SIGNATURES = {
     "shifu_column_stats": "plppli" "ppii" "dd" "pipiip" "s",
     "shifu_normalize": "plli" "pppp" "pl" "s",
     "shifu_bin_codes": "plli" "pp" "pl" "s",
+    "shifu_norm_codes": "plli" "pppp" "pp" "pl" "pl" "pl" "s",
     "shifu_lr_grad": "plli" "i" "ppp" "pp" "i" "s",
     "shifu_sensitivity": "plpl" "pp" "f" "p" "l" "iiiii" "p" "s",
     "shifu_se_perturb": "plpl" "p" "ii" "iiii" "pl" "s",

@@ -293,6 +293,92 @@ __global__ void __launch_bounds__(256) bin_codes_kernel(CodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// K5 fused (streamed `norm`): one read of a chunk's raw values -> every NormalizedData /
+// CleanedData output of the chunk in the same pass: fp32 rows (the NormalizedData cache),
+// bf16 GEMM-ready rows (the MLP's padded layout: the caller's buffer holds the bias column and
+// the zero padding, the kernel fills the value columns) and uint8 tree codes.  Column-major fp64
+// in, row-major out through one LDS transpose tile per output; each output is optional.
+// ---------------------------------------------------------------------------------------------
+struct NormCodesArgs {
+  const double* vals; long ldv; long n; int F;
+  const int* ip; const double* dp; const double* bounds; const double* tables;   // as NormArgs
+  const int* cip; const double* cbounds;   // codes: [F][4] is_cat, bnd_off, nbnd, ncat (nullable)
+  float* outf; long ldf;                   // [n][ldf] fp32 at out_col (nullable)
+  bf16_t* outb; long ldb;                  // [n][ldb] bf16 at out_col (nullable)
+  uint8_t* codes; long ldc;                // [n][ldc] uint8 at column f (nullable)
+};
+
+__device__ __forceinline__ double norm_value(const int* ip, const double* dp, const double* bounds,
+                                             const double* tables, double v) {
+  const int mode = ip[0], nbnd = ip[3], ntbl = ip[5];
+  const double* bnd = bounds + ip[2];
+  const double* tbl = tables + ip[4];
+  switch (mode) {
+    case NM_ZSCORE: return zclip(isfinite(v) ? v : dp[0], dp[0], dp[1], dp[2]);
+    case NM_NUM_TABLE: {
+      const int bin = (v != v) ? -1 : bin_search(bnd, nbnd, v);
+      const double t = tbl[bin < 0 ? ntbl - 1 : min(bin, ntbl - 1)];
+      return ip[6] ? zclip(t, dp[3], dp[4], dp[2]) : t;
+    }
+    case NM_CAT_TABLE: {
+      const int idx = (v != v || v < 0) ? -1 : (int)v;
+      const double t = tbl[(idx < 0 || idx >= ntbl) ? ntbl - 1 : idx];
+      return ip[6] ? zclip(t, dp[3], dp[4], dp[2]) : t;
+    }
+    case NM_RAW: return isfinite(v) ? v : dp[0];
+    case NM_DISCRETE: {
+      const int bin = (v != v) ? -1 : bin_search(bnd, nbnd, v);
+      const double lo = (bin < 0 || bin >= ntbl) ? dp[0] : tbl[bin];
+      return zclip(lo, dp[0], dp[1], dp[2]);
+    }
+    default: {
+      const int idx = (v != v || v < 0) ? -1 : (int)v;
+      return (double)(idx < 0 ? ntbl : idx);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) norm_codes_kernel(NormCodesArgs a) {
+  __shared__ float tile[64][65];
+  __shared__ uint8_t ctile[64][68];
+  const long r0 = (long)blockIdx.x * 64;
+  const int f0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+  for (int k = ty; k < 64; k += 4) {
+    const int f = f0 + k;
+    const long r = r0 + tx;
+    float res = 0.f;
+    uint8_t c = 0;
+    if (f < a.F && r < a.n) {
+      double v = a.vals[(long)f * a.ldv + r];          // coalesced: consecutive rows of column f
+      if (a.outf || a.outb) res = (float)norm_value(a.ip + f * 8, a.dp + f * 8, a.bounds, a.tables, v);
+      if (a.codes) {
+        const int* cp = a.cip + f * 4;
+        if (cp[0]) {
+          const int idx = (v != v || v < 0) ? -1 : (int)v;
+          c = (uint8_t)((idx < 0 || idx >= cp[3]) ? cp[3] : idx);
+        } else {
+          if (v != v) v = 0.0;                         // DTWorker.getFloatValue: missing -> 0f
+          c = (uint8_t)bin_search(a.cbounds + cp[1], cp[2], v);
+        }
+      }
+    }
+    tile[k][tx] = res;
+    ctile[k][tx] = c;
+  }
+  __syncthreads();
+  for (int k = ty; k < 64; k += 4) {                   // thread (tx = column, ty = row group)
+    const long r = r0 + k;
+    const int f = f0 + tx;
+    if (r >= a.n || f >= a.F) continue;
+    const int oc = a.ip[f * 8 + 1];
+    if (a.outf) a.outf[r * a.ldf + oc] = tile[tx][k];
+    if (a.outb) a.outb[r * a.ldb + oc] = f2bf(tile[tx][k]);
+    if (a.codes) a.codes[r * a.ldc + f] = ctile[tx][k];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // K9: logistic regression fused gradient (one pass over X)
 // ---------------------------------------------------------------------------------------------
 template <typename T> struct Vec;
@@ -538,6 +624,20 @@ SHIFU_API int shifu_normalize(const double* vals, long ldv, long n, int F, const
   if (n <= 0 || F <= 0) return 0;
   NormArgs a{vals, ldv, n, F, ip, dp, bounds, tables, out, ldo};
   hipLaunchKernelGGL(normalize_kernel, dim3((n + 63) / 64, (F + 63) / 64), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_norm_codes(const double* vals, long ldv, long n, int F, const int* ip, const double* dp,
+                               const double* bounds, const double* tables, const int* cip, const double* cbounds,
+                               float* outf, long ldf, void* outb, long ldb, void* codes, long ldc,
+                               hipStream_t stream) {
+  if (n <= 0 || F <= 0) return 0;
+  if ((outf || outb) && (!ip || !dp)) return -1;
+  if (codes && (!cip || !cbounds || ldc < F)) return -1;
+  NormCodesArgs a{vals, ldv, n, F, ip, dp, bounds, tables, cip, cbounds, outf, ldf, (bf16_t*)outb, ldb,
+                  (uint8_t*)codes, ldc};
+  hipLaunchKernelGGL(norm_codes_kernel, dim3((n + 63) / 64, (F + 63) / 64), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -158,6 +158,12 @@ def load_dataset_cache(path: str, mmap: bool = True):
         return None
     with open(os.path.join(path, "meta.json")) as f:
         meta = json.load(f)
+    if meta.get("parts"):           # streamed per-rank parts (data/rowstore.py)
+        from ..data.rowstore import Bf16Rows, load_parts
+        arrs = load_parts(path, meta, mmap)
+        if "Xb" in arrs and "X" not in arrs:        # bf16 GEMM-ready rows (shifu.norm.dtype=bf16)
+            arrs["X"] = Bf16Rows(arrs.pop("Xb"), meta["x_width"])
+        return meta, arrs
     arrs = {}
     for fn in os.listdir(path):
         if fn.endswith(".npy"):

@@ -111,6 +111,164 @@ def _norm_one(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_o
     return n
 
 
+def _streaming(ms) -> bool:
+    """``shifu.norm.streaming``: ``true`` / ``false`` / ``auto`` (default: stream when this rank's
+    share of the data exceeds ``shifu.norm.inMemoryMB``, 1024)."""
+    from ..config import environment
+    from ..data.purifier import plan_dataset
+    from ..data.stream import data_bytes
+    from ..parallel import dist
+    mode = str(environment.get("shifu.norm.streaming", "auto")).lower()
+    if mode in ("true", "1", "on"):
+        return True
+    if mode in ("false", "0", "off"):
+        return False
+    try:
+        nbytes = data_bytes(plan_dataset(ms.mc, ms.mc.dataSet))
+    except (OSError, ValueError):
+        return False
+    return nbytes / max(1, dist.info().world_size) > float(environment.get("shifu.norm.inMemoryMB", 1024)) * (1 << 20)
+
+
+def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_rate, neg_only, shuffle, seed,
+                       is_tree):
+    """Out-of-core norm (the reference streams rows through ``P/Normalize.pig:35-46`` ->
+    ``NormalizeUDF.exec``): this rank's byte range is parsed chunk by chunk; each chunk goes through
+    ONE fused K5 launch (``NormPlan``: raw values read once -> fp32 or bf16 GEMM-ready rows + uint8
+    tree codes) and is appended to this rank's ``part-RRRRR`` of the caches (``data/rowstore.py``).
+    Host memory holds one chunk.  ``-shuffle`` then permutes the written parts out of core with the
+    single-process permutation (``_shuffle_parts``), so every output equals the in-memory norm."""
+    import os
+    import shutil
+    from ..config import environment
+    from ..data import stream as DS
+    from ..data.purifier import plan_dataset
+    from ..data.rowstore import NpyAppender, write_parts_meta
+    from ..parallel import dist
+    mc = ms.mc
+    info = dist.info()
+    plan = plan_dataset(mc, data_conf, [c.name for c in cols if not c.is_categorical()],
+                        [c.name for c in cols if c.is_categorical()])
+    chunk = int(float(environment.get("shifu.norm.chunkMB", 256)) * (1 << 20))
+    x_dtype = str(environment.get("shifu.norm.dtype", "float32")).lower()
+    x_dtype = "bf16" if x_dtype in ("bf16", "bfloat16") else "float32"
+    row0 = DS.rank_row_offset(plan, info.rank, info.world_size) if sample_rate < 1.0 else 0
+    dev = None
+    if is_gpu_available():
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+    nplan = N.NormPlan(mc, ms.ccs, cols, want_x=True, want_codes=is_tree, x_dtype=x_dtype, device=dev)
+    outs = [out_x] + ([out_tree] if is_tree else [])
+    if info.rank == 0:
+        for o in outs:
+            if os.path.isdir(o):
+                shutil.rmtree(o)
+            os.makedirs(o, exist_ok=True)
+    dist.barrier()
+    pdir = f"part-{info.rank:05d}"
+    for o in outs:
+        os.makedirs(os.path.join(o, pdir), exist_ok=True)
+    xname = "Xb" if x_dtype == "bf16" else "X"
+    apx = {xname: NpyAppender(os.path.join(out_x, pdir, f"{xname}.npy"), np.uint16 if x_dtype == "bf16" else np.float32,
+                              (nplan.kpad if x_dtype == "bf16" else nplan.width,)),
+           "y": NpyAppender(os.path.join(out_x, pdir, "y.npy"), np.float32),
+           "w": NpyAppender(os.path.join(out_x, pdir, "w.npy"), np.float32)}
+    apt = {}
+    if is_tree:
+        apt = {"codes": NpyAppender(os.path.join(out_tree, pdir, "codes.npy"), nplan.code_dtype, (len(cols),)),
+               "y": NpyAppender(os.path.join(out_tree, pdir, "y.npy"), np.float32),
+               "w": NpyAppender(os.path.join(out_tree, pdir, "w.npy"), np.float32)}
+    counters = {}
+    n_local = 0
+    try:
+        for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, sample_rate, neg_only, seed,
+                                     row0=row0):
+            res = nplan.run(md.table)
+            y, w = md.y.astype(np.float32), md.w.astype(np.float32)
+            apx[xname].append(res[xname])
+            apx["y"].append(y)
+            apx["w"].append(w)
+            if is_tree:
+                apt["codes"].append(res["codes"])
+                apt["y"].append(y)
+                apt["w"].append(w)
+            n_local += md.n
+            for k, v in md.counters.as_dict().items():
+                counters[k] = counters.get(k, 0) + v
+    finally:
+        for a in list(apx.values()) + list(apt.values()):
+            a.close()
+    got = dist.all_gather_objects((n_local, counters))
+    rows = [g[0] for g in got]
+    tot_counters = {}
+    for _, c in got:
+        for k, v in c.items():
+            tot_counters[k] = tot_counters.get(k, 0) + v
+    meta = {"columns": [c.name for c in cols], "column_nums": [c.num for c in cols], "counters": tot_counters,
+            "is_binary": mc.is_binary(), "tags": mc.flatten_tags(), "shuffled": bool(shuffle), "streamed": True}
+    metas = {out_x: dict(meta, norm_type=nplan.nt, input_names=nplan.names, input_nums=nplan.nums,
+                         x_dtype=x_dtype, **({"x_kpad": nplan.kpad, "x_width": nplan.width} if x_dtype == "bf16"
+                                             else {}))}
+    if is_tree:
+        tm = {"nbins": nplan.nbins.tolist(), "is_cat": nplan.is_cat.tolist()}
+        metas[out_tree] = dict(meta, **tm)
+        metas[out_x].update(tm)
+    dist.barrier()
+    for o in outs:
+        if shuffle:
+            _shuffle_parts(o, rows, seed)
+        if info.rank == 0:
+            write_parts_meta(o, metas[o], rows)
+    dist.barrier()
+    n = int(sum(rows))
+    _log.info("NormalizedData (streamed%s, %s, rank %d/%d): %d rows (%d here) x %d inputs (%s) -> %s",
+              ", shuffled" if shuffle else "", x_dtype, info.rank, info.world_size, n, n_local, nplan.width,
+              nplan.nt, out_x)
+    return n
+
+
+def _shuffle_parts(path: str, rows: list, seed: int) -> None:
+    """Out-of-core ``-shuffle`` of a partitioned cache: output row i = input row perm[i] with the
+    single-process permutation (``default_rng(seed).permutation(n)``); rank r writes output rows
+    [n r / R, n (r + 1) / R) as its new part, reading its rows by (sorted) memmap gathers in
+    blocks, then the new parts replace the old ones."""
+    import os
+    import shutil
+    from ..data.rowstore import NpyAppender, RowParts
+    from ..parallel import dist
+    info = dist.info()
+    n = int(sum(rows))
+    perm = np.random.default_rng(seed).permutation(n)
+    parts = [f"part-{r:05d}" for r in range(len(rows))]
+    names = sorted(fn[:-4] for fn in os.listdir(os.path.join(path, parts[info.rank])) if fn.endswith(".npy"))
+    lo, hi = n * info.rank // info.world_size, n * (info.rank + 1) // info.world_size
+    mine = perm[lo:hi]
+    newdir = os.path.join(path, f"shuf-{info.rank:05d}")
+    os.makedirs(newdir, exist_ok=True)
+    block = 1 << 20
+    for name in names:
+        arrs = [np.load(os.path.join(path, p, f"{name}.npy"), mmap_mode="r") for p in parts]
+        src = RowParts(arrs)
+        ap = NpyAppender(os.path.join(newdir, f"{name}.npy"), src.dtype, src.shape[1:])
+        try:
+            for b0 in range(0, len(mine), block):
+                idx = mine[b0: b0 + block]
+                order = np.argsort(idx, kind="stable")          # sequential-ish reads
+                got = src[idx[order]]
+                out = np.empty_like(got)
+                out[order] = got
+                ap.append(out)
+        finally:
+            ap.close()
+        del arrs, src
+    dist.barrier()
+    shutil.rmtree(os.path.join(path, parts[info.rank]))
+    os.replace(newdir, os.path.join(path, parts[info.rank]))
+    # the new part r holds output rows [lo, hi): rewrite the row counts the caller will publish
+    rows[:] = [n * (r + 1) // info.world_size - n * r // info.world_size for r in range(info.world_size)]
+    dist.barrier()
+
+
 def run_norm(root: str = ".", shuffle: bool = False, seed: int = 0) -> int:
     ms = ModelSet(root).setup("NORMALIZE")
     mc = ms.mc
@@ -120,12 +278,13 @@ def run_norm(root: str = ".", shuffle: bool = False, seed: int = 0) -> int:
     is_tree = mc.algorithm in TREE_ALGS
     sr = float(mc.normalize.get("sampleRate", 1.0))
     neg = bool(mc.normalize.get("sampleNegOnly", False))
-    _norm_one(ms, cols, mc.dataSet, ms.pf.normalized_data, ms.pf.cleaned_data, sr, neg, shuffle, seed, is_tree)
+    one = _norm_one_streamed if _streaming(ms) else _norm_one
+    one(ms, cols, mc.dataSet, ms.pf.normalized_data, ms.pf.cleaned_data, sr, neg, shuffle, seed, is_tree)
     vpath = mc.dataSet.get("validationDataPath")
     if vpath:
         vconf = mc.dataSet.copy_with(dataPath=vpath,
                                      filterExpressions=mc.dataSet.get("validationFilterExpressions") or
                                      mc.dataSet.get("filterExpressions"))
-        _norm_one(ms, cols, vconf, ms.pf.normalized_validation_data, ms.pf.cleaned_validation_data, 1.0, False,
-                  False, seed, is_tree)
+        one(ms, cols, vconf, ms.pf.normalized_validation_data, ms.pf.cleaned_validation_data, 1.0, False,
+            False, seed, is_tree)
     return 0

@@ -1,0 +1,154 @@
+"""Streamed (out-of-core) `norm` (steps/norm.py _norm_one_streamed + the fused K5 NormPlan pass):
+the per-rank part caches equal the in-memory NormalizedData / CleanedData -- single process and
+2 gloo ranks, with and without -shuffle; bf16 GEMM-ready rows are the fp32 rows rounded to bf16
+with the bias column; host memory stays bounded by the chunk size."""
+import json
+import os
+import shutil
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _set(mode, chunk_kb=None, dtype=None):
+    from shifu_amd.config import environment
+    environment.props()["shifu.norm.streaming"] = mode
+    if chunk_kb is not None:
+        environment.props()["shifu.norm.chunkMB"] = str(chunk_kb / 1024)
+    if dtype is not None:
+        environment.props()["shifu.norm.dtype"] = dtype
+
+
+def _model_set(tmp_path, alg, n_rows=1503):
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    a = make_model_set(str(tmp_path), "a", alg, n_rows=n_rows, n_num=6, n_cat=2)
+    run_init(a)
+    run_stats(a)
+    return a
+
+
+def _rank_norm(rank, world, port, root, shuffle):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIFU_FORCE_CPU="1")
+    from shifu_amd.parallel import dist
+    from shifu_amd.steps.norm import run_norm
+    _set("true", chunk_kb=16)
+    dist.init_from_env("gloo")
+    run_norm(root, shuffle=shuffle)
+    dist.barrier()
+    dist.shutdown()
+
+
+@pytest.mark.parametrize("alg,shuffle", [("NN", False), ("NN", True), ("GBT", False), ("GBT", True)])
+def test_streamed_norm_equals_in_memory(tmp_path, monkeypatch, alg, shuffle):
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    from shifu_amd.steps.base import load_dataset_cache
+    from shifu_amd.steps.norm import run_norm
+    a = _model_set(tmp_path, alg)
+    b, c = str(tmp_path / "b"), str(tmp_path / "c")
+    shutil.copytree(a, b)
+    shutil.copytree(a, c)
+    _set("false")
+    run_norm(a, shuffle=shuffle)
+    _set("true", chunk_kb=8)                    # many chunks
+    run_norm(b, shuffle=shuffle)
+    mp.start_processes(_rank_norm, args=(2, _port(), c, shuffle), nprocs=2, join=True, start_method="spawn")
+    _set("auto")
+    for sub in (["CleanedData", "NormalizedData"] if alg == "GBT" else ["NormalizedData"]):
+        ma, xa = load_dataset_cache(os.path.join(a, "tmp", sub), mmap=False)
+        for other in (b, c):
+            mb, xb = load_dataset_cache(os.path.join(other, "tmp", sub))
+            assert mb["n"] == ma["n"] and mb.get("streamed")
+            assert set(xa) <= set(xb), (set(xa), set(xb))
+            for k in xa:
+                np.testing.assert_array_equal(np.asarray(xb[k]), xa[k], err_msg=f"{sub} {k}")
+            for k in ("input_names", "input_nums", "nbins", "is_cat", "column_nums"):
+                if k in ma:
+                    assert mb[k] == ma[k], k
+
+
+def test_streamed_norm_bf16_rows(tmp_path, monkeypatch):
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    import torch
+    from shifu_amd.steps.base import load_dataset_cache
+    from shifu_amd.steps.norm import run_norm
+    a = _model_set(tmp_path, "NN")
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    _set("false")
+    run_norm(a)
+    _set("true", chunk_kb=8, dtype="bf16")
+    try:
+        run_norm(b)
+    finally:
+        _set("auto", dtype="float32")
+    ma, xa = load_dataset_cache(os.path.join(a, "tmp", "NormalizedData"), mmap=False)
+    mb, xb = load_dataset_cache(os.path.join(b, "tmp", "NormalizedData"))
+    X = xa["X"]
+    want = torch.from_numpy(X).to(torch.bfloat16).float().numpy()
+    np.testing.assert_array_equal(np.asarray(xb["X"]), want)
+    raw = xb["X"].raw
+    assert raw.shape == (len(X), mb["x_kpad"]) and mb["x_kpad"] % 128 == 0
+    assert np.all(raw[:, mb["x_width"]] == 0x3F80) and not raw[:, mb["x_width"] + 1:].any()
+
+
+_RSS = r"""
+import os, sys, json
+sys.path.insert(0, {root!r})
+os.environ["SHIFU_FORCE_CPU"] = "1"
+from shifu_amd.config import environment
+from shifu_amd.steps.norm import run_norm
+environment.props()["shifu.norm.streaming"] = {mode!r}
+environment.props()["shifu.norm.chunkMB"] = "2"
+def status(key):
+    for line in open("/proc/self/status"):
+        if line.startswith(key):
+            return int(line.split()[1])
+open("/proc/self/clear_refs", "w").write("5")
+base = status("VmRSS:")
+run_norm({root2!r})
+print(json.dumps({{"base_kb": base, "peak_kb": status("VmHWM:")}}))
+"""
+
+
+def _rss_growth(root, mode):
+    r = subprocess.run([sys.executable, "-c", _RSS.format(root=ROOT, mode=mode, root2=root)], capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    return (res["peak_kb"] - res["base_kb"]) * 1024
+
+
+def test_streamed_norm_host_memory_bounded_by_chunk(tmp_path):
+    """peak RSS growth of streamed norm is flat in the data size (2 MB chunks)."""
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    roots = {}
+    for n in (40_000, 120_000):
+        roots[n] = make_model_set(str(tmp_path / str(n)), "m", "NN", n_rows=n, n_num=40, n_cat=2)
+        run_init(roots[n])
+        os.environ["SHIFU_FORCE_CPU"] = "1"
+        run_stats(roots[n])
+    s_small, s_big = _rss_growth(roots[40_000], "true"), _rss_growth(roots[120_000], "true")
+    m_big = _rss_growth(roots[120_000], "false")
+    print("norm rss growth MB: streamed 40K %.1f, streamed 120K %.1f, in-memory 120K %.1f"
+          % (s_small / 1e6, s_big / 1e6, m_big / 1e6))
+    assert s_big - s_small < 24e6, (s_small, s_big)
+    assert s_big < 0.6 * m_big, (s_big, m_big)
