@@ -93,6 +93,9 @@ RT_SIGNATURES = {
     "shifu_csv_free": ("p", None),
     "shifu_spdt_bins": ("pplipl", "l"),
     "shifu_munropat_bins": ("plipl", "l"),
+    "shifu_format_rows": ("lipppppplp", "l"),
+    "shifu_merge_runs": ("ippppP", "l"),
+    "shifu_gather_lines": ("ppplPp", "l"),
 }
 
 

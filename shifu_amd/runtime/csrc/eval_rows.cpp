@@ -1,0 +1,159 @@
+// EvalScore text rows for the streamed `eval` (B9): the reference writes EvalScore through Pig
+// (P/Eval.pig:29-41: EvalScoreUDF.exec J/udf/EvalScoreUDF.java:226, then ORDER BY score DESC).
+// Here every rank scores its byte range chunk by chunk; this file formats a chunk's columns into
+// '|'-joined lines in one native pass (no per-row Python), and k-way merges the ranks' sorted
+// line runs into one EvalScore (stable: ties keep rank order = the single-process row order).
+//
+// Number formats match the Python writer they replace byte for byte:
+//   FIXED6  f"{x:.6f}"   (std::to_chars fixed, precision 6: correctly rounded, like CPython)
+//   REPR    repr(float)  (shortest round-trip digits, CPython's fixed/scientific switch)
+//   REPR_OR_EMPTY  the same, '' for NaN (a numeric tag / meta column's missing value)
+//   DICT    dictionary string of an int32 code ('' for a missing code < 0)
+#include <charconv>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <queue>
+#include <vector>
+
+#define SHIFU_RT_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+enum Kind : int { FIXED6 = 0, REPR = 1, DICT = 2, REPR_OR_EMPTY = 3 };
+
+int put_fixed6(char* p, double x) {
+  if (std::isnan(x)) { std::memcpy(p, "nan", 3); return 3; }
+  if (std::isinf(x)) { if (x < 0) { std::memcpy(p, "-inf", 4); return 4; } std::memcpy(p, "inf", 3); return 3; }
+  auto r = std::to_chars(p, p + 400, x, std::chars_format::fixed, 6);
+  return (int)(r.ptr - p);
+}
+
+// CPython float_repr_style 'short': repr(x) = shortest digits; fixed when -4 <= exp10 < 16
+int put_repr(char* p, double x) {
+  if (std::isnan(x)) { std::memcpy(p, "nan", 3); return 3; }
+  if (std::isinf(x)) { if (x < 0) { std::memcpy(p, "-inf", 4); return 4; } std::memcpy(p, "inf", 3); return 3; }
+  char* q = p;
+  if (std::signbit(x)) { *q++ = '-'; x = -x; }
+  if (x == 0.0) { std::memcpy(q, "0.0", 3); return (int)(q - p) + 3; }
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof buf, x, std::chars_format::scientific);
+  *r.ptr = 0;
+  // buf = d[.ddd]e[+-]XX
+  char digits[32];
+  int nd = 0;
+  const char* s = buf;
+  for (; *s && *s != 'e'; ++s)
+    if (*s != '.') digits[nd++] = *s;
+  const int e = std::atoi(s + 1);
+  if (e >= -4 && e < 16) {
+    if (e >= 0) {
+      for (int i = 0; i <= e; ++i) *q++ = i < nd ? digits[i] : '0';
+      *q++ = '.';
+      if (nd > e + 1) for (int i = e + 1; i < nd; ++i) *q++ = digits[i];
+      else *q++ = '0';
+    } else {
+      *q++ = '0'; *q++ = '.';
+      for (int i = 0; i < -e - 1; ++i) *q++ = '0';
+      for (int i = 0; i < nd; ++i) *q++ = digits[i];
+    }
+  } else {
+    *q++ = digits[0];
+    if (nd > 1) { *q++ = '.'; for (int i = 1; i < nd; ++i) *q++ = digits[i]; }
+    *q++ = 'e';
+    *q++ = e < 0 ? '-' : '+';
+    const int ae = e < 0 ? -e : e;
+    if (ae < 10) *q++ = '0';
+    q += std::snprintf(q, 8, "%d", ae);
+  }
+  return (int)(q - p);
+}
+
+}  // namespace
+
+// Format n rows of ncols columns into '|'-joined, '\n'-terminated lines.
+//   kinds[c]: FIXED6 / REPR / REPR_OR_EMPTY (cols[c] -> double[n]) or DICT (cols[c] -> int32[n],
+//   dict_blob[c] + dict_off[c][k..k+1] = string k, dict_n[c] strings).
+//   line_end[i] = byte offset just past row i's '\n'.  Returns bytes written, or -1 if cap is short.
+SHIFU_RT_API long shifu_format_rows(long n, int ncols, const int* kinds, const void* const* cols,
+                                    const char* const* dict_blob, const long* const* dict_off,
+                                    const long* dict_n, char* out, long cap, long* line_end) {
+  long pos = 0;
+  for (long i = 0; i < n; ++i) {
+    for (int c = 0; c < ncols; ++c) {
+      if (cap - pos < 512) return -1;
+      if (c) out[pos++] = '|';
+      const int k = kinds[c];
+      if (k == DICT) {
+        const int code = ((const int32_t*)cols[c])[i];
+        if (code >= 0 && code < dict_n[c]) {
+          const long a = dict_off[c][code], b = dict_off[c][code + 1];
+          if (cap - pos < (b - a) + 512) return -1;
+          std::memcpy(out + pos, dict_blob[c] + a, (size_t)(b - a));
+          pos += b - a;
+        }
+      } else {
+        const double v = ((const double*)cols[c])[i];
+        if (k == FIXED6) pos += put_fixed6(out + pos, v);
+        else if (k == REPR || !std::isnan(v)) pos += put_repr(out + pos, v);
+      }
+    }
+    out[pos++] = '\n';
+    line_end[i] = pos;
+  }
+  return pos;
+}
+
+// k-way merge of R sorted runs of lines into `out_path` (appending).  Run r: lines blob + line_end
+// offsets (ascending) + keys (the run's order: descending key); ties go to the lower run index,
+// so runs = ranks in order reproduces a stable single-process sort.  Returns lines written or -1.
+SHIFU_RT_API long shifu_merge_runs(int R, const char* const* blobs, const long* const* ends, const double* const* keys,
+                                   const long* counts, const char* out_path) {
+  FILE* f = std::fopen(out_path, "ab");
+  if (!f) return -1;
+  std::vector<char> buf(1 << 22);
+  std::setvbuf(f, buf.data(), _IOFBF, buf.size());
+  struct Head { double key; int run; };
+  auto worse = [](const Head& a, const Head& b) {        // priority: larger key, then lower run
+    return a.key < b.key || (a.key == b.key && a.run > b.run);
+  };
+  std::priority_queue<Head, std::vector<Head>, decltype(worse)> pq(worse);
+  std::vector<long> at(R, 0);
+  for (int r = 0; r < R; ++r)
+    if (counts[r] > 0) pq.push({keys[r][0], r});
+  long written = 0;
+  while (!pq.empty()) {
+    const Head h = pq.top();
+    pq.pop();
+    const int r = h.run;
+    const long i = at[r]++;
+    const long a = i ? ends[r][i - 1] : 0, b = ends[r][i];
+    if (std::fwrite(blobs[r] + a, 1, (size_t)(b - a), f) != (size_t)(b - a)) { std::fclose(f); return -1; }
+    ++written;
+    if (at[r] < counts[r]) pq.push({keys[r][at[r]], r});
+  }
+  if (std::fclose(f) != 0) return -1;
+  return written;
+}
+
+// Reorder one run's lines: write lines order[0], order[1], ... of (blob, line_end) to out_path and
+// their new end offsets to new_end (the rank-local ORDER BY before the k-way merge).
+SHIFU_RT_API long shifu_gather_lines(const char* blob, const long* ends, const long* order, long n,
+                                     const char* out_path, long* new_end) {
+  FILE* f = std::fopen(out_path, "wb");
+  if (!f) return -1;
+  std::vector<char> buf(1 << 22);
+  std::setvbuf(f, buf.data(), _IOFBF, buf.size());
+  long pos = 0;
+  for (long i = 0; i < n; ++i) {
+    const long j = order[i];
+    const long a = j ? ends[j - 1] : 0, b = ends[j];
+    if (std::fwrite(blob + a, 1, (size_t)(b - a), f) != (size_t)(b - a)) { std::fclose(f); return -1; }
+    pos += b - a;
+    new_end[i] = pos;
+  }
+  if (std::fclose(f) != 0) return -1;
+  return pos;
+}

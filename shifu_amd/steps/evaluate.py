@@ -92,6 +92,236 @@ def _load_eval_data(ms, ev, runner_cols, extra_cols=()):
     return load_dataset(ms.mc, ds, nums, strs, require_target=False)
 
 
+# ---- streamed eval -------------------------------------------------------------------
+FIXED6, REPR, DICT, REPR_OR_EMPTY = 0, 1, 2, 3
+
+
+def format_rows(fields, n: int):
+    """EvalScore lines of ``n`` rows in one native pass (runtime/csrc/eval_rows.cpp).  ``fields``:
+    (kind, values[, dictionary]) per column -> (bytes, int64 line ends)."""
+    import ctypes
+    from ..ops import _native
+    lib = _native.rt()
+    ncols = len(fields)
+    keep, cols, blobs, offs, dn = [], [], [], [], []
+    kinds = []
+    for f in fields:
+        kind, v = f[0], f[1]
+        if kind == DICT:
+            v = np.ascontiguousarray(v, dtype=np.int32)
+            enc = [str(x).encode("utf-8") for x in f[2]]
+            blob = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8)
+            off = np.zeros(len(enc) + 1, np.int64)
+            off[1:] = np.cumsum([len(e) for e in enc]) if enc else []
+            keep += [v, blob, off]
+            blobs.append(blob.ctypes.data)
+            offs.append(off.ctypes.data)
+            dn.append(len(enc))
+        else:
+            v = np.ascontiguousarray(v, dtype=np.float64)
+            keep.append(v)
+            blobs.append(None)
+            offs.append(None)
+            dn.append(0)
+        cols.append(v.ctypes.data)
+        kinds.append(kind)
+    ka = (ctypes.c_int * ncols)(*kinds)
+    ca = (ctypes.c_void_p * ncols)(*cols)
+    ba = (ctypes.c_void_p * ncols)(*blobs)
+    oa = (ctypes.c_void_p * ncols)(*offs)
+    na = (ctypes.c_long * ncols)(*dn)
+    ends = np.zeros(n, np.int64)
+    cap = max(1024, n * (ncols * 26 + 16))
+    while True:
+        buf = ctypes.create_string_buffer(cap)
+        got = lib.shifu_format_rows(n, ncols, ka, ca, ba, oa, na, buf, cap, ends.ctypes.data)
+        if got >= 0:
+            return buf.raw[:got], ends
+        cap *= 2
+
+
+def _text_field(table, name, n):
+    """A tag / meta column as a formatter field ('' where missing / absent)."""
+    if name not in table:
+        return (DICT, np.full(n, -1, np.int32), [])
+    col = table[name]
+    if col.kind == "str":
+        return (DICT, col.values, col.dictionary)
+    return (REPR_OR_EMPTY, col.values)
+
+
+def _eval_streaming(ms, ev) -> bool:
+    """``shifu.eval.streaming``: true / false / auto (default: stream when this rank's share of the
+    eval data exceeds ``shifu.eval.inMemoryMB``, 1024)."""
+    from ..config import environment
+    from ..data.purifier import plan_dataset
+    from ..data.stream import data_bytes
+    from ..parallel import dist
+    mode = str(environment.get("shifu.eval.streaming", "auto")).lower()
+    if mode in ("true", "1", "on"):
+        return True
+    if mode in ("false", "0", "off") or ms.mc.is_multiclass():
+        return False
+    try:
+        nbytes = data_bytes(plan_dataset(ms.mc, ev.dataSet))
+    except (OSError, ValueError):
+        return False
+    return nbytes / max(1, dist.info().world_size) > float(environment.get("shifu.eval.inMemoryMB", 1024)) * (1 << 20)
+
+
+class _StreamedEval:
+    """Rank 0's view of every rank's streamed numeric eval parts (memory-mapped; ``perf_eval`` input)."""
+
+    def __init__(self, n, w, cols):
+        self.n, self.w, self.table = n, w, _GTable(cols)
+
+
+def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, nosort):
+    """Out-of-core eval (the reference streams Eval.pig: EvalScoreUDF per row, then ORDER BY): this
+    rank's byte range is scored chunk by chunk; each chunk's EvalScore lines are formatted natively
+    and appended to the rank's run with the numeric (score, label, weight, score-meta) columns;
+    each rank then orders its run by score (stable) and rank 0 k-way merges the runs into
+    EvalScore (byte-identical to the in-memory writer) and reads the numeric parts memory-mapped
+    for the confusion sweep.  Host memory: one chunk (+ rank 0's numeric columns for metrics)."""
+    import shutil
+    from ..config import environment
+    from ..data import stream as DS
+    from ..data.purifier import plan_dataset
+    from ..data.rowstore import NpyAppender, RowParts
+    from ..ops import _native
+    from ..parallel import dist
+    mc = ms.mc
+    info = dist.info()
+    ccs = {c.name: c for c in ms.ccs}
+    names = set(runner.raw_columns()) | set(meta_cols) | set(score_meta)
+    nums = [n for n in names if n in ccs and not ccs[n].is_categorical()]
+    strs = [n for n in names if n not in nums]
+    target = ev.dataSet.get("targetColumnName") or mc.dataSet.get("targetColumnName")
+    if target and target not in strs and target not in nums:
+        strs.append(target)
+    plan = plan_dataset(mc, ev.dataSet, nums, strs)
+    chunk = int(float(environment.get("shifu.eval.chunkMB", 256)) * (1 << 20))
+    sel = ev.get("performanceScoreSelector", "mean") or "mean"
+    pos = set(str(t) for t in (ev.dataSet.get("posTags") or mc.pos_tags))
+    neg = set(str(t) for t in (ev.dataSet.get("negTags") or mc.neg_tags))
+    d = ms.pf.eval_dir(ev.get("name"))
+    os.makedirs(d, exist_ok=True)
+    path = ms.pf.eval_score(ev)
+    if os.path.isdir(path):
+        path = os.path.join(path, "part-00000")
+    tmp = os.path.join(d, ".parts")
+    if info.rank == 0 and os.path.isdir(tmp):
+        shutil.rmtree(tmp)
+    dist.barrier()
+    pdir = os.path.join(tmp, f"part-{info.rank:05d}")
+    os.makedirs(pdir, exist_ok=True)
+    aps = {k: NpyAppender(os.path.join(pdir, f"{k}.npy"), dt) for k, dt in
+           (("key", np.float64), ("lab", np.int8), ("w", np.float64), ("ends", np.int64))}
+    for m in score_meta:
+        aps["meta:" + m] = NpyAppender(os.path.join(pdir, f"meta_{len(aps)}.npy"), np.float64)
+    meta_file = {m: os.path.basename(aps["meta:" + m].path)[:-4] for m in score_meta}
+    lines = open(os.path.join(pdir, "lines.bin"), "wb")
+    off, n_local, cols = 0, 0, None
+    try:
+        for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, require_target=False):
+            res = runner.score(md.table, scale)
+            if cols is None:
+                cols = [k for k in res if k not in ("class_scores", "pred_class")]
+            n = md.n
+            if write:
+                fields = [_text_field(md.table, target, n), (REPR, md.w)] + [(FIXED6, res[k]) for k in cols] + \
+                         [_text_field(md.table, m, n) for m in list(meta_cols) + list(score_meta)]
+                blob, ends = format_rows(fields, n)
+                lines.write(blob)
+                aps["ends"].append(ends + off)
+                off += len(blob)
+            key = np.asarray(res.get(sel, res["mean"]), dtype=np.float64)
+            aps["key"].append(key)
+            tcol = md.table[target] if target in md.table else None
+            if tcol is None:
+                lab = np.full(n, -1, np.int8)
+            elif tcol.kind == "str":
+                dl = np.array([1 if str(t).strip() in pos else (0 if str(t).strip() in neg else -1)
+                               for t in tcol.dictionary] + [-1], np.int8)
+                lab = dl[np.where(tcol.values >= 0, tcol.values, len(tcol.dictionary))]
+            else:
+                st = np.asarray([str(t).strip() for t in tcol.strings()])
+                lab = np.where(np.isin(st, list(pos)), 1, np.where(np.isin(st, list(neg)), 0, -1)).astype(np.int8)
+            aps["lab"].append(lab)
+            aps["w"].append(np.asarray(md.w, np.float64))
+            for m in score_meta:
+                aps["meta:" + m].append(md.table[m].numeric() if m in md.table else np.full(n, np.nan))
+            n_local += n
+    finally:
+        lines.close()
+        for a in aps.values():
+            a.close()
+    got = dist.all_gather_objects((n_local, cols))
+    cols = next((c for _, c in got if c is not None), cols) or []
+    sort = not nosort
+    lib = _native.rt()
+    if write and sort and n_local:
+        key = np.load(os.path.join(pdir, "key.npy"), mmap_mode="r")
+        k = np.nan_to_num(np.asarray(key), nan=-np.inf)
+        order = np.argsort(-k, kind="stable").astype(np.int64)
+        blob = np.memmap(os.path.join(pdir, "lines.bin"), dtype=np.uint8, mode="r") if off else np.zeros(1, np.uint8)
+        ends = np.ascontiguousarray(np.load(os.path.join(pdir, "ends.npy")))
+        new_end = np.zeros(n_local, np.int64)
+        rc = lib.shifu_gather_lines(blob.ctypes.data, ends.ctypes.data, order.ctypes.data, n_local,
+                                    os.path.join(pdir, "sorted.bin").encode(), new_end.ctypes.data)
+        if rc < 0:
+            raise OSError("eval: writing the sorted score run failed")
+        np.save(os.path.join(pdir, "sorted_ends.npy"), new_end)
+        np.save(os.path.join(pdir, "sorted_key.npy"), np.ascontiguousarray(k[order]))
+        del blob
+    dist.barrier()
+    counts = [g[0] for g in got]
+    parts = [os.path.join(tmp, f"part-{r:05d}") for r in range(info.world_size)]
+    if write and info.rank == 0:
+        hdr = ["tag", "weight"] + cols + list(meta_cols) + list(score_meta)
+        with open(path, "w") as f:
+            f.write("|".join(hdr) + "\n")
+        live = [(p_, c) for p_, c in zip(parts, counts) if c]
+        if sort and live:
+            import ctypes
+            keep = []
+            bl, en, ky = [], [], []
+            for p_, c in live:
+                b = np.memmap(os.path.join(p_, "sorted.bin"), dtype=np.uint8, mode="r")
+                e = np.ascontiguousarray(np.load(os.path.join(p_, "sorted_ends.npy")))
+                kk = np.ascontiguousarray(np.load(os.path.join(p_, "sorted_key.npy")))
+                keep += [b, e, kk]
+                bl.append(b.ctypes.data)
+                en.append(e.ctypes.data)
+                ky.append(kk.ctypes.data)
+            R = len(live)
+            rc = lib.shifu_merge_runs(R, (ctypes.c_void_p * R)(*bl), (ctypes.c_void_p * R)(*en),
+                                      (ctypes.c_void_p * R)(*ky), (ctypes.c_long * R)(*[c for _, c in live]),
+                                      path.encode())
+            if rc != sum(c for _, c in live):
+                raise OSError("eval: merging the score runs failed")
+        else:
+            with open(path, "ab") as f:
+                for p_, c in live:
+                    with open(os.path.join(p_, "lines.bin"), "rb") as src:
+                        shutil.copyfileobj(src, f, 1 << 22)
+        _log.info("eval %s: scored %d rows on %d rank(s) with %d models (streamed) -> %s", ev.get("name"),
+                  sum(counts), info.world_size, len(runner.models), path)
+    # metrics inputs on rank 0: the numeric parts, memory-mapped in rank order
+    live = [p_ for p_, c in zip(parts, counts) if c] or parts[:1]
+    if info.rank != 0:
+        return None
+
+    def col(name):
+        arrs = [np.load(os.path.join(p_, f"{name}.npy"), mmap_mode="r") for p_ in live]
+        return arrs[0] if len(arrs) == 1 else RowParts(arrs)
+    keyc, labc, wc = col("key"), col("lab"), col("w")
+    metas = {m: np.asarray(col(meta_file[m])) for m in score_meta}
+    view = _StreamedEval(len(keyc), np.asarray(wc), metas)
+    res = {sel: np.asarray(keyc), "mean": np.asarray(keyc)}
+    return view, res, None, np.asarray(labc), tmp
+
+
 def score_eval(ms: ModelSet, ev, device=None, write: bool = True, nosort: bool = False):
     mc = ms.mc
     conv = ev.get("gbtScoreConvertStrategy") or "RAW"
@@ -274,26 +504,9 @@ def _gather_eval_numeric(ms, ev, md, res, tags, score_meta):
     return _GatheredEval(len(lab), got["w"], cols), res, tags
 
 
-def _gather_scores(md, res, tags, meta_names):
-    """All ranks' (tags, weights, score arrays, meta columns) -> one row set on rank 0 (rank order
-    = row order).  Other ranks get their own shard back."""
-    import torch.distributed as tdist
-    from ..parallel import dist
-    payload = (np.asarray(tags), np.asarray(md.w), {k: np.asarray(v) for k, v in res.items()},
-               {m: (md.table[m].strings() if m in md.table else np.array([""] * md.n)) for m in meta_names})
-    # gathered on rank 0 only (the other ranks neither receive nor hold the full score set)
-    parts = [None] * dist.info().world_size if dist.info().rank == 0 else None
-    tdist.gather_object(payload, parts, dst=0)
-    if dist.info().rank != 0:
-        return md, res, tags
-    tags = np.concatenate([p[0] for p in parts])
-    w = np.concatenate([p[1] for p in parts])
-    res = {k: np.concatenate([p[2][k] for p in parts]) for k in parts[0][2]}
-    cols = {m: np.concatenate([p[3][m] for p in parts]) for m in meta_names}
-    return _GatheredEval(len(tags), w, cols), res, tags
-
-
-def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None):
+def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None, lab=None):
+    """``lab`` (optional, numeric labels of the streamed eval): binary 1 pos / 0 neg / -1 neither,
+    multi-class the tag-group index; replaces the per-row tag strings."""
     mc = ms.mc
     d = ms.pf.eval_dir(ev.get("name"))
     os.makedirs(d, exist_ok=True)
@@ -302,7 +515,8 @@ def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None):
     nb = int(ev.get("performanceBucketNum", 10) or 10)
     scale = float(ev.get("scoreScale", 1000) or 1000)
     if mc.is_multiclass():
-        truth = np.array([next((i for i, g in enumerate(mc.tags()) if t in g), -1) for t in tags])
+        truth = np.asarray(lab) if lab is not None else \
+            np.array([next((i for i, g in enumerate(mc.tags()) if t in g), -1) for t in tags])
         ok = truth >= 0
         cm = E.multiclass_confusion(res["pred_class"][ok], truth[ok], len(mc.tags()))
         with open(ms.pf.eval_confusion_matrix(ev), "w") as f:
@@ -314,10 +528,15 @@ def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None):
         return {"accuracy": acc}
     sel = ev.get("performanceScoreSelector", "mean") or "mean"
     score = np.asarray(res.get(sel, res["mean"]))
-    tg = np.asarray([str(t).strip() for t in tags])
-    valid = np.isin(tg, list(pos | neg))
-    is_pos = np.isin(tg[valid], list(pos))
-    w = md.w[valid] if ev.dataSet.get("weightColumnName") else None
+    if lab is not None:
+        lab = np.asarray(lab)
+        valid = lab >= 0
+        is_pos = lab[valid] == 1
+    else:
+        tg = np.asarray([str(t).strip() for t in tags])
+        valid = np.isin(tg, list(pos | neg))
+        is_pos = np.isin(tg[valid], list(pos))
+    w = np.asarray(md.w)[valid] if ev.dataSet.get("weightColumnName") else None
     perf = E.performance(score[valid], is_pos, w, nb, max_score=scale, device=device)
     with open(ms.pf.eval_performance(ev), "w") as f:
         f.write(E.to_json(perf))
@@ -386,8 +605,24 @@ def run_eval(root: str = ".", action: str = "run", name: str | None = None, devi
         if action == "norm":
             norm_eval(ms, ev, strict)
             continue
-        md, res, tags, score_meta = score_eval(ms, ev, device, nosort=nosort)
         from ..parallel import dist
+        if _eval_streaming(ms, ev):
+            runner = ModelRunner(ms.mc, ms.ccs, ms.pf.eval_models_dir(ev), device=device,
+                                 gbt_convert=ev.get("gbtScoreConvertStrategy") or "RAW")
+            meta_cols = _meta_names(ms, ev.dataSet, "metaColumnNameFile") if ev.dataSet else []
+            score_meta = _meta_names(ms, ev, "scoreMetaColumnNameFile")
+            out = _score_eval_streamed(ms, ev, runner, meta_cols, score_meta,
+                                       float(ev.get("scoreScale", 1000) or 1000), True, nosort)
+            if out is not None and action in ("run", "perf", "confmat"):
+                view, res, _, lab, tmp = out
+                with dist.local_only():
+                    perf_eval(ms, ev, view, res, None, score_meta, device, lab=lab)
+            dist.barrier()
+            if dist.info().rank == 0 and out is not None:
+                import shutil
+                shutil.rmtree(out[4], ignore_errors=True)
+            continue
+        md, res, tags, score_meta = score_eval(ms, ev, device, nosort=nosort)
         if action in ("run", "perf", "confmat") and dist.info().rank == 0:
             with dist.local_only():
                 perf_eval(ms, ev, md, res, tags, score_meta, device)
