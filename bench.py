@@ -22,6 +22,7 @@ per GPU (``gbdt_rounds_per_s`` / ``gbdt_ms_per_round``; ``--gbdt-steps 0`` skips
     python bench.py --model lr      # LR 100k-row CSV local (CPU plumbing) config
     python bench.py --model stats   # stats (K4 exact cuts + histograms) 100M x 1000 per GPU
     python bench.py --model treeinfer   # eval scoring, 500-tree depth-7 GBT, 20M x 1000 fp64 rows
+    python bench.py --model pipeline    # CLI steps on disk data, 2M x 1600 per GPU (reference: 20M x 1600)
 """
 from __future__ import annotations
 
@@ -443,6 +444,130 @@ def bench_treeinfer(a, dev, info):
     }
 
 
+REF_PIPELINE_MIN = {"stats": 20.0, "eval": 13.0, "varsel_train_200ep": 45.0, "varsel_se": 25.0}
+REF_PIPELINE_ROWS = 20_000_000
+
+
+def bench_pipeline(a, dev, info):
+    """The reference's only published numbers are CLI step wall times on 20M rows x 1600 variables
+    (CHANGES.txt:233-237, 264-268): stats 20 min, eval 13 min, varsel SE 70 min = 45 min of
+    200-epoch NN training + 25 min of sensitivity.  This runs the same CLI steps (Step API, the
+    code `shifu <verb>` runs) on a generated '|'-delimited data set on disk (native generator,
+    runtime/csrc/gen_csv.cpp, planted sparse rule on 20 of the columns) and times each step:
+    init, stats, norm, varsel (filterBy SE: trains numTrainEpochs/2 epochs then the SE pass),
+    train (numTrainEpochs = --steps epochs of the default NN) and eval (an eval set as large as
+    the training set).  Epoch counts below 200 are timed and the 200-epoch figure is projected
+    linearly from the per-epoch time (labelled); the 20M-row projection scales each
+    data-proportional step linearly (labelled).  value = rows/s of the whole pipeline."""
+    import ctypes
+    import shutil
+    import tempfile
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.ops import _native
+    from shifu_amd.parallel import dist
+    from shifu_amd.steps import api
+    from shifu_amd.steps.create import create_model_set
+    rows, F = a.rows, a.cols
+    epochs = max(2, a.steps)
+    work = a.workdir or os.path.join(tempfile.gettempdir(), "shifu_pipeline_bench")
+    root = os.path.join(work, "pipe")
+    t_gen = 0.0
+    if info.rank == 0:
+        shutil.rmtree(work, ignore_errors=True)
+        os.makedirs(work)
+        root = create_model_set("pipe", "NN", parent=work)
+        lib = _native.rt()
+        t0 = time.perf_counter()
+        for name, seed in (("DataSet1", 11), ("EvalSet1", 12)):
+            d = os.path.join(root, "data", name)
+            os.makedirs(d, exist_ok=True)
+            rc = lib.shifu_gen_csv(d.encode(), rows, F, 3, seed, 0.02, 20, min(16, os.cpu_count() or 4))
+            if rc:
+                raise RuntimeError("data generation failed (disk full?)")
+            hdr = ["id", "diagnosis", "wgt"] + [f"num_{j}" for j in range(F)] + [f"cat_{j}" for j in range(3)]
+            with open(os.path.join(d, ".pig_header"), "w") as f:
+                f.write("|".join(hdr) + "\n")
+        t_gen = time.perf_counter() - t0
+        mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+        for sec, key in ((mc.dataSet, "DataSet1"), (mc.evals[0].dataSet, "EvalSet1")):
+            d = os.path.join(root, "data", key)
+            sec["dataPath"], sec["headerPath"] = d, os.path.join(d, ".pig_header")
+            sec["targetColumnName"], sec["posTags"], sec["negTags"] = "diagnosis", ["M"], ["B"]
+            sec["weightColumnName"] = "wgt"
+        with open(os.path.join(root, "columns", "meta.column.names"), "w") as f:
+            f.write("id\n")
+        with open(os.path.join(root, "columns", "categorical.column.names"), "w") as f:
+            f.write("cat_0\ncat_1\ncat_2\n")
+        mc.varSelect["filterBy"] = "SE"
+        mc.varSelect["filterNum"] = 200
+        mc.varSelect["autoFilterEnable"] = False
+        mc.train["numTrainEpochs"] = epochs
+        mc.train["baggingNum"] = 1
+        mc.train["validSetRate"] = 0.1
+        mc.save()
+        gb = sum(os.path.getsize(os.path.join(root, "data", "DataSet1", f))
+                 for f in os.listdir(os.path.join(root, "data", "DataSet1")))
+        log(f"[bench] pipeline data: {rows} rows x {F} numeric + 3 categorical, {gb / 1e9:.1f} GB text, "
+            f"generated in {t_gen:.1f}s -> {root}")
+    root = dist.all_gather_objects(root)[0]
+    times = {}
+
+    def step(name, fn):
+        dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce_(t, "max")
+        times[name] = float(t.item())
+        log(f"[bench] pipeline {name}: {times[name]:.1f}s")
+    step("init", lambda: api.InitStep(root).process())
+    step("stats", lambda: api.StatsStep(root).process())
+    step("norm", lambda: api.NormStep(root).process())
+    step("varsel", lambda: api.VarSelStep(root).process())
+    step("train", lambda: api.TrainStep(root).process())
+    step("eval", lambda: api.EvalStep(root).process())
+    recall = None
+    if info.rank == 0:
+        import numpy as np
+        from shifu_amd.config.column_config import load_column_configs
+        strong = np.zeros(20, np.int32)
+        k = _native.rt().shifu_gen_strong_cols(F, 20, strong.ctypes.data)
+        want = {f"num_{j}" for j in strong[:k]}
+        se = [l.split("\t") for l in open(os.path.join(root, "varsel", "se.0")).read().strip().split("\n")]
+        top = [r[1] for r in se[:k]]
+        recall = len(want & set(top)) / max(1, k)
+        perf = json.load(open(os.path.join(root, "evals", "Eval1", "EvalPerformance.json")))
+    total = sum(times.values())
+    scale20 = REF_PIPELINE_ROWS / float(rows * info.world_size)
+    proj = {k: v * scale20 / 60.0 for k, v in times.items()}
+    ep_train = times["train"] / epochs
+    out = {
+        "metric": "rows/sec (whole pipeline init+stats+norm+varsel(SE)+train+eval, CLI steps on disk data)",
+        "value": rows * info.world_size / total, "unit": "rows/s", "n_gpus": info.world_size, "steps": epochs,
+        "warmup": 0, "ms_per_step": total * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16 NN GEMMs / fp64 stats", "data": f"synthetic '|'-delimited text on disk, {rows} rows x {F} numeric "
+        "+ 3 categorical per GPU, planted rule on 20 columns (native generator)",
+        "config": {"model": f"default NN {F}-50-1 (tanh), SE varsel filterNum 200", "global_batch": rows * info.world_size,
+                   "seq_len": None, "n_cols": F, "rows_per_gpu": rows, "parallelism": f"dp{info.world_size}"},
+        "step_seconds": {k: round(v, 2) for k, v in times.items()}, "generation_s": round(t_gen, 1),
+        "train_epoch_s": round(ep_train, 3),
+        "projected_20M_rows_minutes (linear in rows, labelled projection)": {k: round(v, 2) for k, v in proj.items()},
+        "projected_20M_train_200_epochs_minutes (per-epoch x 200, labelled projection)":
+            round(ep_train * 200 * scale20 / 60.0, 2),
+        "reference_minutes_20M_x_1600 (CHANGES.txt:233-237,264-268)": REF_PIPELINE_MIN,
+        "se_recall_of_planted_columns": recall,
+        "eval_auc": perf["areaUnderRoc"] if info.rank == 0 else None,
+    }
+    if info.rank == 0 and not a.keep:
+        shutil.rmtree(work, ignore_errors=True)
+    return out
+
+
 def bench_lr(a, dev, info):
     """BASELINE config 1: logistic regression on a 100k-row CSV, local mode, CPU only (the
     plumbing path): shifu init -> stats -> norm -> train on a generated model set.  One step =
@@ -486,7 +611,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr", "stats", "treeinfer"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr", "stats", "treeinfer", "pipeline"])
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per GPU (default 125M on GPU: 256 GB of bf16 rows resident in one MI355X's "
                          "288 GB HBM, so 8 GPUs hold the metric's 1B-row x 1k-col table)")
@@ -501,6 +626,8 @@ def main():
                     help="GBDT: per-level histogram table (rows, bytes, ms, TB/s; HIP events around each level)")
     ap.add_argument("--stream", action="store_true", help="varsel: rows streamed from host memory (HostRows)")
     ap.add_argument("--host-rows", type=int, default=2_000_000, help="varsel --stream: host buffer rows")
+    ap.add_argument("--workdir", default=None, help="pipeline: where the generated model set lives")
+    ap.add_argument("--keep", action="store_true", help="pipeline: keep the generated model set")
     a = ap.parse_args()
 
     from shifu_amd.parallel import dist
@@ -511,9 +638,11 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
     if a.model == "varsel" and a.cols == 1000:
         a.cols = 10_000
+    if a.model == "pipeline" and a.cols == 1000:
+        a.cols = 1600 if gpu else 40
     if a.rows is None:
         a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000, "stats": 100_000_000 if gpu else 5_000,
-                  "treeinfer": 20_000_000 if gpu else 5_000,
+                  "treeinfer": 20_000_000 if gpu else 5_000, "pipeline": 2_000_000 if gpu else 4_000,
                   "gbdt": 100_000_000 if gpu else 20_000}.get(a.model, 125_000_000 if gpu else 20_000)
     if a.model == "gbdt":
         a.levels = a.gbdt_levels
@@ -525,6 +654,8 @@ def main():
         out = bench_lr(a, dev, info)
     elif a.model == "treeinfer":
         out = bench_treeinfer(a, dev, info)
+    elif a.model == "pipeline":
+        out = bench_pipeline(a, dev, info)
     elif a.model == "stats":
         if not gpu and a.cols == 1000:
             a.cols = 64

@@ -96,6 +96,8 @@ RT_SIGNATURES = {
     "shifu_format_rows": ("lipppppplp", "l"),
     "shifu_merge_runs": ("ippppP", "l"),
     "shifu_gather_lines": ("ppplPp", "l"),
+    "shifu_gen_csv": ("Pliildii", "i"),
+    "shifu_gen_strong_cols": ("iip", "i"),
 }
 
 
