@@ -18,7 +18,7 @@ weights).  ``value`` = total rows processed per second over all ranks.
 The default line carries both halves of the metric: ``value`` = MLP rows/s, and after the MLP
 rows are freed the same process times ``--gbdt-steps`` boosting rounds on 100M x 1000 uint8 codes
 per GPU (``gbdt_rounds_per_s`` / ``gbdt_ms_per_round``; ``--gbdt-steps 0`` skips it).
-    python bench.py --model varsel  # 10k-feature MLP + SE varselect config
+    python bench.py --model varsel  # 10k-feature MLP + SE varselect config (sparse planted rule, recall@20)
     python bench.py --model lr      # LR 100k-row CSV local (CPU plumbing) config
     python bench.py --model stats   # stats (K4 exact cuts + histograms) 100M x 1000 per GPU
     python bench.py --model treeinfer   # eval scoring, 500-tree depth-7 GBT, 20M x 1000 fp64 rows
@@ -97,13 +97,27 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def make_synthetic(rows, n_in, k0, device, seed):
-    """bf16 rows [rows, k0]: N(0,1) features, bias column = 1, zero padding; labels from a
-    random hidden linear rule so the task is learnable."""
+def strong_inputs(n_in, k):
+    """The ``k`` inputs of a sparse planted rule (spread over the columns, fixed for every rank)."""
+    step = max(1, n_in // k)
+    return list(range(0, step * k, step))[:k]
+
+
+def make_synthetic(rows, n_in, k0, device, seed, sparse_k=0):
+    """bf16 rows [rows, k0]: N(0,1) features, bias column = 1, zero padding; labels from a hidden
+    linear rule so the task is learnable -- dense (every input) or, ``sparse_k`` > 0, only over the
+    ``strong_inputs`` (alternating signs, decaying weights), which a sensitivity analysis must
+    recover."""
     g = torch.Generator(device=device).manual_seed(seed)
     x = torch.empty(rows, k0, dtype=torch.bfloat16, device=device)
     y = torch.empty(rows, 1, dtype=torch.float32, device=device)
-    wt = torch.randn(n_in, 1, generator=g, device=device, dtype=torch.float32).to(torch.bfloat16)
+    wt = torch.randn(n_in, 1, generator=torch.Generator(device=device).manual_seed(99), device=device,
+                     dtype=torch.float32)
+    if sparse_k:
+        wt.zero_()
+        for q, j in enumerate(strong_inputs(n_in, sparse_k)):
+            wt[j, 0] = (1.0 if q % 2 == 0 else -1.0) / (1.0 + 0.15 * q)
+    wt = wt.to(torch.bfloat16)
     step = 1 << 22
     for r0 in range(0, rows, step):
         r1 = min(rows, r0 + step)
@@ -208,6 +222,9 @@ class _Cycle:
         return self.buf[a: a + (sl.stop - sl.start)]
 
 
+SE_K = 20     # planted strong inputs of the SE bench
+
+
 def bench_varsel(a, dev, info):
     """BASELINE config 5: 10k-feature MLP + sensitivity-analysis variable selection.  Each rank
     holds ``--rows`` rows x 10000 features (bf16, HBM-resident: 2M rows = 40 GB), trains the
@@ -228,7 +245,7 @@ def bench_varsel(a, dev, info):
         # (270 GiB) cannot hold 20M x 10k bf16 (400 GB), so --rows are served from a host buffer of
         # --host-rows rows cycled: every chunk is a real H2D copy, the row values repeat.
         hb = min(a.rows, a.host_rows)
-        xd, yd = make_synthetic(hb, n_in, spec.layer_kpad[0], dev, 4321 + info.rank)
+        xd, yd = make_synthetic(hb, n_in, spec.layer_kpad[0], dev, 4321 + info.rank, sparse_k=SE_K)
         xh = xd[:, :n_in].cpu()
         del xd
         torch.cuda.empty_cache()
@@ -238,7 +255,7 @@ def bench_varsel(a, dev, info):
         if a.chunk_rows > hb or hb % a.chunk_rows:
             raise SystemExit("--host-rows must be a multiple of --chunk-rows")
     else:
-        x, y = make_synthetic(a.rows, n_in, spec.layer_kpad[0], dev, 4321 + info.rank)
+        x, y = make_synthetic(a.rows, n_in, spec.layer_kpad[0], dev, 4321 + info.rank, sparse_k=SE_K)
     data = TrainData(x, y, None, a.rows)
     n_global = float(a.rows * info.world_size)
     log(f"[bench] varsel data ready ({'streamed from host' if a.stream else 'HBM-resident'})")
@@ -273,6 +290,13 @@ def bench_varsel(a, dev, info):
     rows_total = a.rows * info.world_size
     value = rows_total * (a.steps + 1) / (t_train + t_se)
     rms_all = np.sqrt(stats[n_in:].cpu().numpy() / rows_total)
+    # the result must be meaningful: non-degenerate RMS and the planted inputs ranked on top
+    strong = set(strong_inputs(n_in, SE_K))
+    top = np.argsort(-rms_all, kind="stable")[:SE_K]
+    recall = len(strong & set(int(i) for i in top)) / SE_K
+    distinct = int(np.unique(np.round(rms_all, 12)).size)
+    if distinct < n_in // 2 or not np.isfinite(rms_all).all() or float(rms_all.max()) <= 0.0:
+        raise SystemExit(f"degenerate SE result: {distinct} distinct RMS values over {n_in} inputs")
     return {
         "metric": METRIC + " [config: 10k-feature MLP + SE varselect]",
         "value": value, "unit": "rows/s", "n_gpus": info.world_size, "steps": a.steps, "warmup": a.warmup,
@@ -284,6 +308,7 @@ def bench_varsel(a, dev, info):
                    "host_buffer_rows": min(a.rows, a.host_rows) if a.stream else None},
         "train_ms_per_epoch": t_train / max(1, a.steps) * 1e3, "se_pass_ms": t_se * 1e3,
         "se_input_pairs_per_s": rows_total * n_in / t_se, "top5_inputs_by_rms": np.argsort(-rms_all)[:5].tolist(),
+        "planted_rule": f"sparse, {SE_K} of {n_in} inputs", "recall_at_k": recall, "distinct_rms_values": distinct,
     }
 
 

@@ -129,11 +129,17 @@ def performance(score, is_pos, weight=None, num_bucket: int = 10, max_score: flo
     ms = [first]
     k, last = 1, 0
     wcum = np.cumsum(cm["w"])
-    for j in range(1, n + 1):
-        if max_score - k * bin_score >= cm["score"][j]:
-            ms.append(_po(j, cm, k, float(j - last), float(wcum[j] - wcum[last])))
-            k += 1
-            last = j
+    # emissions (binary searches on the descending scores, not a per-row loop): bucket k closes at
+    # the first row after the previous emission whose score <= max_score - k * bin_score
+    neg = -np.asarray(cm["score"][1:], dtype=np.float64)          # ascending
+    while last < n:
+        thr = max_score - k * bin_score
+        j = max(int(np.searchsorted(neg, -thr, side="left")) + 1, last + 1)
+        if j > n:
+            break
+        ms.append(_po(j, cm, k, float(j - last), float(wcum[j] - wcum[last])))
+        k += 1
+        last = j
     res = OrderedDict(version=version)
     res["areaUnderRoc"] = auc(lists["roc"], "fpr", "recall")
     res["weightedAreaUnderRoc"] = auc(lists["weightedRoc"], "weightedFpr", "weightedRecall")

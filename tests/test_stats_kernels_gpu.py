@@ -153,6 +153,27 @@ def test_sensitivity_host_rows_stream_equals_resident():
     np.testing.assert_allclose(m2, m1, rtol=1e-6)
 
 
+def test_sensitivity_stream_equals_resident_wide():
+    """the streamed SE path at the bench's width class (F = 4096 inputs, H = 500)
+    equals the resident one, and a sparse planted dependence is ranked on top by both."""
+    from shifu_amd.algos import varsel as V
+    from shifu_amd.formats.nn_format import NNNetwork
+    from shifu_amd.models.nn import HostRows
+    rng = np.random.default_rng(5)
+    F, H, n = 4096, 500, 8192
+    W1 = rng.normal(size=(H, F + 1)) * (0.5 / np.sqrt(F))
+    strong = np.arange(0, F, F // 16)[:16]
+    W1[:, strong] *= 40.0
+    net = NNNetwork([F, H, 1], ["sigmoid", "sigmoid"], [W1, rng.normal(size=(1, H + 1)) * 0.3])
+    X = torch.from_numpy(rng.normal(size=(n, F)).astype(np.float32)).to(torch.bfloat16).float().numpy()
+    m1, r1, _ = V.sensitivity(net, torch.from_numpy(X).cuda(), device=torch.device("cuda"), row_chunk=1024)
+    m2, r2, _ = V.sensitivity(net, HostRows(X, F), device=torch.device("cuda"), row_chunk=1024)
+    np.testing.assert_allclose(r2, r1, rtol=1e-6)
+    np.testing.assert_allclose(m2, m1, rtol=1e-6)
+    assert set(np.argsort(-r1)[:16]) == set(strong.tolist())
+    assert np.unique(r1).size > F // 2                  # not a degenerate (all-tied) result
+
+
 @pytest.mark.gpu
 def test_column_metrics_kernel_matches_host():
     """K3: KS / IV / WOE / per-bin WOE of many columns in one launch == the host
