@@ -36,6 +36,9 @@ HIP_SIGNATURES = {
     "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "p" "s",
     "shifu_colsum_fixed": "pii" "pp" "s",
     "shifu_colsum_ws": ("ii", "l"),
+    # sort_kernels.hip
+    "shifu_sort_ws": ("l", "l"),
+    "shifu_sort_desc": "plpps",
     "shifu_gemm_set_stages": "i",
     "shifu_gemm_set_big": "i",
     "shifu_gemm_set_tune": "ii",

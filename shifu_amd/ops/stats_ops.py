@@ -249,3 +249,19 @@ def column_metrics_batch(negs, poss, dev):
                         if o[3] > 0 else None)
         res.append(tuple(pair))
     return res
+
+
+def sort_desc(x: torch.Tensor) -> torch.Tensor:
+    """K16: stable descending order of fp64 scores on the device (hand-written LSD radix sort,
+    ops/csrc/sort_kernels.hip): int32 row ids, ties in row order, NaN last."""
+    nat.require_gpu_native()
+    x = x.to(torch.float64).contiguous()
+    n = x.numel()
+    order = torch.empty(n, dtype=torch.int32, device=x.device)
+    if n == 0:
+        return order
+    ws = torch.empty(int(nat.hip().shifu_sort_ws(n)), dtype=torch.uint8, device=x.device)
+    rc = nat.call_hip("shifu_sort_desc", x, n, order, ws, nat.stream_of(x))
+    if rc:
+        raise RuntimeError(f"shifu_sort_desc failed rc={rc}")
+    return order
