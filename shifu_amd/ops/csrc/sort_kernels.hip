@@ -26,8 +26,9 @@ constexpr int TILE = RT * SLOTS;        // 4096 keys per tile
 constexpr int NDIG = 256;
 
 __device__ __forceinline__ uint64_t desc_key(double x) {
-  if (x != x) x = -__builtin_inf();     // NaN scores sort with -inf (last)
   uint64_t u = __double_as_longlong(x);
+  // NaN scores sort with -inf (last): an integer test (a float x != x may be folded away)
+  if ((u & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) u = 0xfff0000000000000ull;
   u = (u >> 63) ? ~u : (u | 0x8000000000000000ull);   // ascending order of x
   return ~u;                                           // descending
 }

@@ -26,7 +26,7 @@ def test_radix_sort_desc_matches_stable_argsort(n, kind):
         x[::13] = np.nan
         x[::17] = -np.inf
     got = sort_desc(torch.from_numpy(x).cuda()).cpu().numpy()
-    k = np.nan_to_num(x, nan=-np.inf)
+    k = np.where(np.isnan(x), -np.inf, x)                 # NaN ranks with -inf (last)
     k = np.where(k == 0.0, 0.0, k)                 # -0.0 == 0.0 ties: keep row order
     want = np.argsort(-k, kind="stable")
     if kind == "neg":     # the radix key orders -0.0 below +0.0; compare as values + stability per value

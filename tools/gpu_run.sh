@@ -2,7 +2,7 @@
 #   gpurun --timeout 1200 -- bash tools/gpu_run.sh TAG step [step ...]
 # Steps (each under its own timeout; the first failure ends the run):
 #   tests            full `pytest -m gpu` suite
-#   tests:<k-expr>   GPU tests matching a -k expression
+#   tests:<k-expr>   GPU tests matching a -k expression ("=" stands for a space: tests:a=or=b)
 #   smoke            __graft_entry__.smoke()
 #   bench            default bench line (MLP + GBDT halves)
 #   bench:<args>     bench.py with extra args, e.g. bench:--model=gbdt (use '=' not spaces)
@@ -28,7 +28,7 @@ for step in "$@"; do
   case $kind in
     tests)
       if [ -n "$arg" ]; then
-        timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu -k "$arg" > "$log" 2>&1
+        timeout -k 10 900 python -u -m pytest -x -v -rA --timeout 300 --timeout-method thread tests -m gpu -k "$args" > "$log" 2>&1
       else
         timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > "$log" 2>&1
       fi ;;
