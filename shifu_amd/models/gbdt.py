@@ -677,8 +677,17 @@ class TreeTrainer:
                          self.scale_w, self.scale_g, 0, 1, st)
             self._root_cache = (w, key, slab)          # holds w: its storage cannot be re-issued
         slab = self._root_cache[2]
-        nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, 0, it, len(items), slab, self.F,
-                     self.scale_w, self.scale_g, 0, 2, st)
+        if ROOT_QUAD:
+            # sum w*g over whole 128-B records: one block per (row range, quad) consumes every
+            # line it fetches (gbdt_kernels.hip gbdt_root_quad_kernel)
+            first = np.nonzero(items[:, 3] % 4 == 0)[0]
+            q = np.stack([first, items[first, 1], items[first, 2], items[first, 3] // 4], 1).astype(np.int32)
+            qt = torch.from_numpy(np.ascontiguousarray(q)).to(self.dev)
+            nat.call_hip("shifu_gbdt_hist_root_quad", d.kbins, d.group_stride, w, g, qt, len(q), slab,
+                         self.ngroups, self.scale_g, st)
+        else:
+            nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, 0, it, len(items), slab, self.F,
+                         self.scale_w, self.scale_g, 0, 2, st)
         return slab
 
     # ---- native multi-class RF (Entropy / Gini over C classes) ------------------------------
@@ -1244,6 +1253,8 @@ W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histo
 # (gbdt_kernels.hip GSH32); SHIFU_GBDT_ROOT_U32=0 keeps the packed u64 kernel everywhere
 ROOT_U32 = os.environ.get("SHIFU_GBDT_ROOT_U32", "1") != "0"
 ROOT_GSH32 = 3               # = gbdt_kernels.hip GSH32
+# root sum w*g over whole quad records (SHIFU_GBDT_ROOT_QUAD=0: the per-group items)
+ROOT_QUAD = os.environ.get("SHIFU_GBDT_ROOT_QUAD", "1") != "0"
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on
 # power-of-two grids (|w*g| < 2^23 of the grid, the root's u32 w*g mode 2^3 coarser), summed
 # exactly in int64 (so every rank and every run finds the same splits)

@@ -617,9 +617,120 @@ __global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Root level, sum w*g (MODE 2) over WHOLE 128-B records: one block builds the u32 histograms of
+// all 128 features of a quad for its row range (128 x 256 u32 = 128 KiB of LDS), 8 threads per
+// row each reading 16 B, so every fetched line is consumed by the CU that fetched it (the
+// per-group items read a quarter of each line, 4x the L2->L1 traffic of the dense root pass).
+// Bank = feature mod 64 ((bin * 128 + f) * 4 B); at step j lane (row slot r8, segment s)
+// updates feature 16 s + ((j + rot) & 15) with rot = r8 + 8 (s >> 2): the 64 lanes of a wave
+// hit 64 distinct banks whatever the bins are.  Sums stay exact: |q| < 2^20 - 1 on the root's
+// coarser grid and 2048 rows between the int64 unpacks.
+// ---------------------------------------------------------------------------------------
+constexpr int RQ_T = 512;
+constexpr int RQ_E = QF * NB / RQ_T;           // u32 entries each thread unpacks (64)
+
+struct RootQuadArgs {
+  const uint8_t* bins; long gs;              // quad-blocked [Q][N][128]
+  const float* w; const float* g;
+  const int* qitems;                         // [n][4] = {first item, lo, hi, quad}
+  long long* slab;                           // [n_items][2][FG][NB]: this kernel writes the w*g half
+  int n_groups;                              // 32-feature groups (G) = items per full quad
+  float scale_g;                             // already / 2^GSH32
+};
+
+__global__ __launch_bounds__(RQ_T, 1) void gbdt_root_quad_kernel(RootQuadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hq[];    // [NB][128]
+  const int qi = xcd_remap(blockIdx.x, gridDim.x);
+  const int first = a.qitems[qi * 4], lo = a.qitems[qi * 4 + 1], hi = a.qitems[qi * 4 + 2],
+            quad = a.qitems[qi * 4 + 3];
+  for (int i = threadIdx.x; i < QF * NB; i += RQ_T) hq[i] = 0u;
+  __syncthreads();
+  const int seg = threadIdx.x & 7, rs = threadIdx.x >> 3;        // 64 row slots x 8 segments
+  const int rot = ((threadIdx.x >> 3) & 7) + ((seg >> 2) << 3);
+  const uint8_t* qb = a.bins + (size_t)quad * a.gs + seg * 16;
+  long long acc[RQ_E];
+#pragma unroll
+  for (int k = 0; k < RQ_E; ++k) acc[k] = 0;
+  auto flush = [&]() {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RQ_E; ++k) {
+      const int e = threadIdx.x + k * RQ_T;
+      acc[k] += (long long)(int32_t)hq[e];
+      hq[e] = 0u;
+    }
+    __syncthreads();
+  };
+  int passes = 0;
+  // software pipeline: next pass's record / w / g loaded before this pass's atomics
+  auto load = [&](int r, uint4& b, float& q) {
+    const int rc = min(r, hi - 1);
+    b = *(const uint4*)(qb + (size_t)rc * QF);
+    q = r < hi ? a.w[rc] * a.g[rc] * a.scale_g : 0.f;
+  };
+  uint4 bc; float qc;
+  load(lo + rs, bc, qc);
+  for (int r0 = lo; r0 < hi; r0 += 64) {                        // block-uniform trip count
+    uint4 bn; float qn;
+    load(r0 + 64 + rs, bn, qn);
+    const uint32_t q32 = (uint32_t)__float2int_rn(qc);
+    if (qc != 0.f) {
+      // rotate the 16 bytes left by rot: byte j of R = feature byte (j + rot) & 15
+      const uint32_t W[4] = {bc.x, bc.y, bc.z, bc.w};
+      uint32_t X[4], Y[4], R[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) X[k] = pick(W[k], W[(k + 1) & 3], rot & 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Y[k] = pick(X[k], X[(k + 2) & 3], rot & 8);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) R[k] = __builtin_amdgcn_alignbyte(Y[(k + 1) & 3], Y[k], rot & 3);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
+        atomicAdd(&hq[(b << 7) | (seg << 4) | ((j + rot) & 15)], q32);
+      }
+    }
+    if (++passes == 2048 / 64) { passes = 0; flush(); }
+    bc = bn; qc = qn;
+  }
+  flush();
+  // slabs: sub-group s of the quad -> item first + s, [1][fl][b] = feature 32 s + fl, bin b.
+  // Thread t owns feature t & 127 and bins (t >> 7) + 4 k; transposed through LDS (64 features
+  // x 256 bins of int64 = 128 KiB per half) so the slab rows leave as coalesced stores.
+  const int nsub = min(4, a.n_groups - quad * 4);
+  long long* tq = (long long*)hq;
+  const int f_own = threadIdx.x & 127;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if ((f_own >> 6) == h) {
+#pragma unroll
+      for (int k = 0; k < RQ_E; ++k) tq[(f_own & 63) * NB + (threadIdx.x >> 7) + 4 * k] = acc[k];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * NB; i += RQ_T) {
+      const int f = h * 64 + (i >> 8), s = f >> 5;
+      if (s < nsub) a.slab[((size_t)(first + s) * 2 + 1) * FG * NB + (size_t)(f & 31) * NB + (i & 255)] = tq[i];
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+// Root sum w*g over whole quad records (gbdt_root_quad_kernel); qitems [n][4] = {first item, lo,
+// hi, quad}, the items of a quad's groups consecutive in the slab.
+SHIFU_API int shifu_gbdt_hist_root_quad(const void* bins, long gs, const float* w, const float* g, const int* qitems,
+                                        int n_qitems, void* slab, int n_groups, double scale_g, hipStream_t stream) {
+  if (gs % QF || n_qitems <= 0 || n_groups <= 0) return -1;
+  RootQuadArgs a{(const uint8_t*)bins, gs, w, g, qitems, (long long*)slab, n_groups,
+                 (float)(scale_g / (1 << GSH32))};
+  hipLaunchKernelGGL(gbdt_root_quad_kernel, dim3(n_qitems), dim3(RQ_T), QF * NB * 4, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
 
 SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, const int* pos2row, const float* w, const float* g,
                               int wg_by_pos, const int* items, int n_items, void* slab, int n_feat,

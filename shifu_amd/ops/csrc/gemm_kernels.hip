@@ -337,15 +337,11 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // ---------------------------------------------------------------------------------------
 constexpr int G8_T = 512, G8_HALF = 16384, G8_BUF = 4 * G8_HALF;
 
-// The 8-phase k-loop of one 256 x 256 output tile (m0, n0) into acc (see the schedule above).
-__device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, char* smem) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int nk = p.K / 64;
-
-  // DMA sources: half-tile h (0 A-top, 1 A-bot, 2 B-0, 3 B-1), instruction i (2 per thread):
-  // LDS byte P = i*8192 + wid*1024 + lane*16 of the half-tile holds logical chunk lc of row P>>7.
-  long off[4][2];
+// Per-thread LDS-DMA source offsets of tile (m0, n0): half-tile h (0 A-top, 1 A-bot, 2 B-0, 3 B-1),
+// instruction i (2 per thread): LDS byte P = i*8192 + wid*1024 + lane*16 of the half-tile holds
+// logical chunk lc of row P>>7 (the swizzle is applied on the GLOBAL source address).
+__device__ __forceinline__ void gemm8_src(const GemmArgs& p, int m0, int n0, long (&off)[4][2]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int P = i * 8192 + wid * 1024 + lane * 16;
@@ -355,14 +351,34 @@ __device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4
     off[2][i] = (long)min(n0 + row, p.NB - 1) * p.ldb + lc * 8;
     off[3][i] = (long)min(n0 + 128 + row, p.NB - 1) * p.ldb + lc * 8;
   }
-  auto dma = [&](int h, int kt) {
-    char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
-    const int k0 = min(kt, nk - 1) * 64;
-    const bf16_t* src = h < 2 ? p.A : p.B;
+}
+
+__device__ __forceinline__ void gemm8_dma(const GemmArgs& p, const long (&off)[4][2], char* smem, int h, int kt) {
+  const int wid = threadIdx.x >> 6;
+  const int nk = p.K / 64;
+  char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
+  const int k0 = min(kt, nk - 1) * 64;
+  const bf16_t* src = h < 2 ? p.A : p.B;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src + off[h][i] + k0), (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
-  };
+  for (int i = 0; i < 2; ++i)
+    __builtin_amdgcn_global_load_lds((const void*)(src + off[h][i] + k0), (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
+}
+
+// prologue DMAs of a tile: even k-tile 0 complete, odd k-tile 1 B halves (12 vector-memory ops)
+__device__ __forceinline__ void gemm8_prologue(const GemmArgs& p, const long (&off)[4][2], char* smem) {
+  gemm8_dma(p, off, smem, 2, 0); gemm8_dma(p, off, smem, 3, 0); gemm8_dma(p, off, smem, 0, 0);
+  gemm8_dma(p, off, smem, 1, 0); gemm8_dma(p, off, smem, 2, 1); gemm8_dma(p, off, smem, 3, 1);
+}
+
+// The 8-phase k-loop of one 256 x 256 output tile into acc (see the schedule above), after its
+// prologue DMAs.  extra16: the caller issued 16 vector-memory ops after the prologue (a persistent
+// kernel's epilogue stores of the previous tile), which the first wait leaves in flight.
+__device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8], const long (&off)[4][2],
+                                           char* smem, bool extra16 = false) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nk = p.K / 64;
+  auto dma = [&](int h, int kt) { gemm8_dma(p, off, smem, h, kt); };
 
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -401,10 +417,10 @@ __device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4
 #define G8_MMA(mh, nh, bq, on) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
     if (on) { __builtin_amdgcn_s_setprio(1); mma(mh, nh, bq); __builtin_amdgcn_s_setprio(0); } } while (0)
 
-  // prologue: even k-tile 0 complete, odd k-tile 1 B halves in flight
-  dma(2, 0); dma(3, 0); dma(0, 0); dma(1, 0);
-  dma(2, 1); dma(3, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  // even k-tile 0 landed (its 8 DMAs are the oldest), odd k-tile 1 B halves stay in flight (and
+  // extra16: the 16 epilogue stores a persistent kernel issued after the prologue)
+  if (extra16) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   G8_BAR();
   if (wr == 1) G8_BAR();                      // stagger the two wave rows by one barrier
 
@@ -435,6 +451,119 @@ __device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4
   G8_BAR();
 #undef G8_MMA
 #undef G8_BAR
+}
+
+__device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0, char* smem) {
+  long off[4][2];
+  gemm8_src(p, m0, n0, off);
+  gemm8_prologue(p, off, smem);
+  gemm8_loop(p, acc, off, smem);
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent 8-phase forward (EPI_ACT / EPI_STORE): one block per CU walks its tiles; the next
+// tile's prologue DMAs are issued BEFORE the current tile's epilogue, which stages the bf16 tile
+// through the LDS that the prologue does not touch (buffer 1's A halves + the 32 KiB above the
+// ring) in two 128-row rounds and leaves as 16 bounds-checked buffer stores per thread -- so the
+// next tile's first loads, its launch, and this tile's stores overlap instead of serialising
+// (the fixed per-tile cost of gemm_nt_8ph_kernel: profiles/r3/mlp_lab_ablation_r3d.jsonl).
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) int v4i_t;
+
+template <int EPI, int ACT>
+__device__ __forceinline__ void epilogue_256_persist(const GemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0,
+                                                     char* smem) {
+  // the thread id through an opaque asm: the per-lane staging / store addresses are then computed
+  // here, not hoisted out of the persistent tile loop (where they would stay live across the
+  // k-loop and spill)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  // bounds-checked stores (rows >= M dropped by the hardware): the store count is the same on
+  // every tile, which keeps the next loop's counted vmcnt exact
+  const int rows = min(256, p.M - m0);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.C + (size_t)m0 * p.ldc), (short)0, rows * (int)p.ldc * 2, 0x00020000);
+  const bool full = n0 + 256 <= (EPI == EPI_ACT ? p.n_valid : p.NB);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (wr == half) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int ml = j * 16 + (lane & 15);                        // row within the half
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z = acc[i][j][r];
+            const int n = n0 + nl + r;
+            if (full) o[r] = EPI == EPI_ACT ? act_fwd(ACT, z) : z;
+            else if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
+            else o[r] = n < p.NB ? z : 0.f;
+          }
+          uint2 w;
+          w.x = pack_bf16x2(o[0], o[1]);
+          w.y = pack_bf16x2(o[2], o[3]);
+          const int c = nl >> 3, hb = (nl >> 2) & 1;
+          char* region = smem + (ml < 64 ? G8_BUF : 2 * G8_BUF);       // buf1 A halves | above the ring
+          *(uint2*)(region + (ml & 63) * 512 + ((c ^ (ml & 15)) << 4) + hb * 8) = w;
+        }
+      }
+    }
+    // raw barriers: a __syncthreads() would make hipcc drain the next tile's prologue DMAs
+    // (vmcnt(0)) -- only the LDS writes need to be complete (lgkmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int c = tid & 31;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int ml = pass * 16 + (tid >> 5);
+      const char* region = smem + (ml < 64 ? G8_BUF : 2 * G8_BUF);
+      const v4i_t v = *(const v4i_t*)(region + (ml & 63) * 512 + ((c ^ (ml & 15)) << 4));
+      const int m = half * 128 + ml;                                  // row within the tile
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)((size_t)m * p.ldc * 2 + (size_t)(n0 + c * 8) * 2), 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // staging reads done before reuse
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_persist_kernel(GemmArgs p, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = (p.N + 255) / 256;
+  // tile t -> (m, n); logical block lb (XCD-remapped) walks t = lb, lb + G, ...: tiles t, t + 1
+  // (the two column tiles of a row block) run on one XCD and share the A rows in its L2
+  const int G = gridDim.x;
+  int t = xcd_remap(blockIdx.x, G);
+  if (t >= ntiles) return;
+  f32x4 acc[4][8];
+  {
+    long o0[4][2];
+    gemm8_src(p, (t / ntn) * 256, (t % ntn) * 256, o0);
+    gemm8_prologue(p, o0, smem);
+  }
+  bool first = true;
+  for (;;) {
+    {
+      long off[4][2];
+      gemm8_src(p, (t / ntn) * 256, (t % ntn) * 256, off);
+      gemm8_loop(p, acc, off, smem, !first);          // 16 stores of the previous epilogue in flight
+    }
+    const int tn = t + G;
+    if (tn < ntiles) {     // next tile's prologue first: lands in buffer 0 + buffer 1's B halves
+      long o2[4][2];
+      gemm8_src(p, (tn / ntn) * 256, (tn % ntn) * 256, o2);
+      gemm8_prologue(p, o2, smem);
+    }
+    epilogue_256_persist<EPI, ACT>(p, acc, (t / ntn) * 256, (t % ntn) * 256, smem);
+    if (tn >= ntiles) return;
+    t = tn;
+    first = false;
+  }
 }
 
 template <int EPI, int ACT>
@@ -755,10 +884,12 @@ static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N 
                              // 3 = 8-phase whenever M >= 64K and N >= 256, 4 = 128x128 only
 static int g_wg_interleave = 1;   // wgrad row splits: 1 interleaved 64-row steps (-3% wgrad1 at 1M rows), 0 contiguous
 static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
+static int g_fwd_persist = 1;     // persistent 8-phase forward (tune key 10; 0 = one tile per block)
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
   if (key == 2) { g_wg_interleave = val; return 0; }
   if (key == 9) { g_dbg = val; return 0; }
+  if (key == 10) { g_fwd_persist = val; return 0; }
   return -1;
 }
 SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b == 3 || b == 4) ? b : 0; return 0; }
@@ -782,6 +913,23 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   if ((g_big == 3 || auto8) && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
     const int grid8 = ((M + 255) / 256) * ((N + 255) / 256);
     const size_t lds8 = 2 * G8_BUF;
+    if (g_fwd_persist && epi != EPI_DACT && M * (long)ldc * 2 < (1l << 31)) {
+      // persistent forward: one block per CU (LDS = the ring + 32 KiB of epilogue staging)
+      int dev = 0, ncu = 256;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      const int gridp = grid8 < ncu ? grid8 : ncu;
+      const size_t ldsp = 2 * G8_BUF + 32768;
+#define GEMMP_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_persist_kernel<E, A>), dim3(gridp), dim3(G8_T), ldsp, stream, p, grid8)
+      if (epi == EPI_ACT) {
+        switch (act) { case 0: GEMMP_L(EPI_ACT, 0); break; case 1: GEMMP_L(EPI_ACT, 1); break;
+          case 2: GEMMP_L(EPI_ACT, 2); break; case 3: GEMMP_L(EPI_ACT, 3); break; case 4: GEMMP_L(EPI_ACT, 4); break;
+          case 6: GEMMP_L(EPI_ACT, 6); break; default: GEMMP_L(EPI_ACT, 7); break; }
+      } else GEMMP_L(EPI_STORE, 2);
+#undef GEMMP_L
+      CHECK_HIP(hipGetLastError());
+      return 0;
+    }
 #define GEMM8_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_kernel<E, A>), dim3(grid8), dim3(G8_T), lds8, stream, p)
 #define GEMM8_ACTS(E) switch (act) { case 0: GEMM8_L(E, 0); break; case 1: GEMM8_L(E, 1); break; \
     case 2: GEMM8_L(E, 2); break; case 3: GEMM8_L(E, 3); break; case 4: GEMM8_L(E, 4); break; \

@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--rows", type=int, default=1 << 21)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--env", nargs="*", default=[])
+    ap.add_argument("--tune", nargs="*", default=[],
+                    help="GEMM tune settings applied per run, e.g. 10=0 10=1 (key 10: persistent forward)")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0],
                     help="GEMM lab ablation bits per run (1: no head err atomics, 2: main loops only)")
     a = ap.parse_args()
@@ -52,9 +54,13 @@ def main():
     tr._final_chunk = True
     tr._chunk_hip(data, 0, a.rows, wb, wt)              # warm-up (workspace, code objects)
     torch.cuda.synchronize()
-    for dbg in a.dbg:
-        nat.call_hip("shifu_gemm_set_tune", 9, dbg)
-        run(a, tr, data, wb, wt, timed, real, rec, dbg, nat, torch)
+    for tune in (a.tune or [None]):
+        if tune is not None:
+            k, v = (int(x) for x in tune.split("="))
+            nat.call_hip("shifu_gemm_set_tune", k, v)
+        for dbg in a.dbg:
+            nat.call_hip("shifu_gemm_set_tune", 9, dbg)
+            run(a, tr, data, wb, wt, timed, real, rec, f"{dbg} tune {tune}", nat, torch)
     nat.call_hip("shifu_gemm_set_tune", 9, 0)
 
 
