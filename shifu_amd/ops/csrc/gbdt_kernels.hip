@@ -657,7 +657,7 @@ __global__ __launch_bounds__(RQ_T, 1) void gbdt_root_quad_kernel(RootQuadArgs a)
 #pragma unroll
     for (int k = 0; k < RQ_E; ++k) {
       const int e = threadIdx.x + k * RQ_T;
-      acc[k] += (long long)(int32_t)hq[e];
+      acc[k] += (long long)(int32_t)hq[e] * (1ll << GSH32);     // back on the scale_g grid (MODE 2)
       hq[e] = 0u;
     }
     __syncthreads();
