@@ -627,7 +627,7 @@ __global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
 // hit 64 distinct banks whatever the bins are.  Sums stay exact: |q| < 2^20 - 1 on the root's
 // coarser grid and 2048 rows between the int64 unpacks.
 // ---------------------------------------------------------------------------------------
-constexpr int RQ_T = 512;
+constexpr int RQ_T = 1024;                   // 16 waves: 128 rows per pass
 constexpr int RQ_E = QF * NB / RQ_T;           // u32 entries each thread unpacks (64)
 
 struct RootQuadArgs {
@@ -640,13 +640,14 @@ struct RootQuadArgs {
 };
 
 __global__ __launch_bounds__(RQ_T, 1) void gbdt_root_quad_kernel(RootQuadArgs a) {
+  constexpr int RPQ = RQ_T / 8;               // rows per pass
   extern __shared__ __attribute__((aligned(16))) uint32_t hq[];    // [NB][128]
   const int qi = xcd_remap(blockIdx.x, gridDim.x);
   const int first = a.qitems[qi * 4], lo = a.qitems[qi * 4 + 1], hi = a.qitems[qi * 4 + 2],
             quad = a.qitems[qi * 4 + 3];
   for (int i = threadIdx.x; i < QF * NB; i += RQ_T) hq[i] = 0u;
   __syncthreads();
-  const int seg = threadIdx.x & 7, rs = threadIdx.x >> 3;        // 64 row slots x 8 segments
+  const int seg = threadIdx.x & 7, rs = threadIdx.x >> 3;        // RPQ row slots x 8 segments
   const int rot = ((threadIdx.x >> 3) & 7) + ((seg >> 2) << 3);
   const uint8_t* qb = a.bins + (size_t)quad * a.gs + seg * 16;
   long long acc[RQ_E];
@@ -671,9 +672,9 @@ __global__ __launch_bounds__(RQ_T, 1) void gbdt_root_quad_kernel(RootQuadArgs a)
   };
   uint4 bc; float qc;
   load(lo + rs, bc, qc);
-  for (int r0 = lo; r0 < hi; r0 += 64) {                        // block-uniform trip count
+  for (int r0 = lo; r0 < hi; r0 += RPQ) {                       // block-uniform trip count
     uint4 bn; float qn;
-    load(r0 + 64 + rs, bn, qn);
+    load(r0 + RPQ + rs, bn, qn);
     const uint32_t q32 = (uint32_t)__float2int_rn(qc);
     if (qc != 0.f) {
       // rotate the 16 bytes left by rot: byte j of R = feature byte (j + rot) & 15
@@ -691,7 +692,7 @@ __global__ __launch_bounds__(RQ_T, 1) void gbdt_root_quad_kernel(RootQuadArgs a)
         atomicAdd(&hq[(b << 7) | (seg << 4) | ((j + rot) & 15)], q32);
       }
     }
-    if (++passes == 2048 / 64) { passes = 0; flush(); }
+    if (++passes == 2048 / RPQ) { passes = 0; flush(); }
     bc = bn; qc = qn;
   }
   flush();
@@ -705,7 +706,7 @@ __global__ __launch_bounds__(RQ_T, 1) void gbdt_root_quad_kernel(RootQuadArgs a)
   for (int h = 0; h < 2; ++h) {
     if ((f_own >> 6) == h) {
 #pragma unroll
-      for (int k = 0; k < RQ_E; ++k) tq[(f_own & 63) * NB + (threadIdx.x >> 7) + 4 * k] = acc[k];
+      for (int k = 0; k < RQ_E; ++k) tq[(f_own & 63) * NB + (threadIdx.x >> 7) + (RQ_T / 128) * k] = acc[k];
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * NB; i += RQ_T) {

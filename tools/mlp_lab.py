@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--env", nargs="*", default=[])
     ap.add_argument("--tune", nargs="*", default=[],
-                    help="GEMM tune settings applied per run, e.g. 10=0 10=1 (key 10: persistent forward)")
+                    help="GEMM tune settings applied per run, e.g. 10:0 10:1 (key 10: persistent forward)")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0],
                     help="GEMM lab ablation bits per run (1: no head err atomics, 2: main loops only)")
     a = ap.parse_args()
@@ -56,7 +56,7 @@ def main():
     torch.cuda.synchronize()
     for tune in (a.tune or [None]):
         if tune is not None:
-            k, v = (int(x) for x in tune.split("="))
+            k, v = (int(x) for x in tune.split(":"))
             nat.call_hip("shifu_gemm_set_tune", k, v)
         for dbg in a.dbg:
             nat.call_hip("shifu_gemm_set_tune", 9, dbg)
