@@ -617,7 +617,7 @@ class TreeTrainer:
                 p2r = None if self._root_level else pos2row      # root: positions are rows
                 by_pos = p2r is not None and self._wg_pos is not None
                 wv, gv = self._wg_pos if by_pos else (w, g)
-                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, wv, gv, int(by_pos), it, len(items),
+                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, QF, p2r, wv, gv, int(by_pos), it, len(items),
                              slab, F, self.scale_w, self.scale_g, self._nmod, 0, st)
             if ls is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
@@ -662,6 +662,30 @@ class TreeTrainer:
         co = None if cat_order is None else cat_order.cpu().numpy()
         return best, co
 
+    def _root_bins(self):
+        """A [G][N][32] copy of the (quad-blocked) bins for the dense root pass, made once when HBM
+        has room for it (SHIFU_GBDT_ROOT_G32=0: never): the per-group root items then stream
+        contiguous 32-B slices, where the quad records would make each CU fetch whole 128-B lines
+        for a quarter of their bytes (profiles/r3, per-level tables).  None: use the quad records."""
+        d = self.data
+        if not ROOT_G32 or d.bins_dptr is not None or d.bins.device.type != "cuda":
+            return None
+        c = getattr(self, "_g32", None)
+        if c is None:
+            G, n = self.ngroups, d.n
+            need = G * n * FG
+            free = torch.cuda.mem_get_info(self.dev)[0]
+            if free < need * 1.1 + (6 << 30):
+                _log.info("GBDT root: no room for the [G][N][32] bins copy (%.1f GB); quad records", need / 1e9)
+                self._g32 = False
+                return None
+            b = torch.empty(G, n, FG, dtype=torch.uint8, device=self.dev)
+            for gi in range(G):
+                o = (gi % (QF // FG)) * FG
+                b[gi] = d.bins[gi // (QF // FG), :, o: o + FG]
+            self._g32 = c = b
+        return c if c is not False else None
+
     def _root_slab(self, items, it, w, g, st):
         """Root-level slabs from the two u32 histogram modes: sum w (mode 1) is built once and
         kept while the weight tensor is the same unmodified object (no bagging sub-sample, the
@@ -673,11 +697,17 @@ class TreeTrainer:
         c = getattr(self, "_root_cache", None)
         if c is None or c[0] is not w or c[1] != key:
             slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
-            nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, 0, it, len(items), slab, self.F,
-                         self.scale_w, self.scale_g, 0, 1, st)
+            rb = self._root_bins()
+            nat.call_hip("shifu_gbdt_hist", rb if rb is not None else d.kbins,
+                         d.n * FG if rb is not None else d.group_stride, FG if rb is not None else QF, None, w, g, 0,
+                         it, len(items), slab, self.F, self.scale_w, self.scale_g, 0, 1, st)
             self._root_cache = (w, key, slab)          # holds w: its storage cannot be re-issued
         slab = self._root_cache[2]
-        if ROOT_QUAD:
+        rb = self._root_bins()
+        if rb is not None:           # dense root pass over the [G][N][32] copy (every line fully used)
+            nat.call_hip("shifu_gbdt_hist", rb, d.n * FG, FG, None, w, g, 0, it, len(items), slab, self.F,
+                         self.scale_w, self.scale_g, 0, 2, st)
+        elif ROOT_QUAD:
             # sum w*g over whole 128-B records: one block per (row range, quad) consumes every
             # line it fetches (gbdt_kernels.hip gbdt_root_quad_kernel)
             first = np.nonzero(items[:, 3] % 4 == 0)[0]
@@ -686,7 +716,7 @@ class TreeTrainer:
             nat.call_hip("shifu_gbdt_hist_root_quad", d.kbins, d.group_stride, w, g, qt, len(q), slab,
                          self.ngroups, self.scale_g, st)
         else:
-            nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, None, w, g, 0, it, len(items), slab, self.F,
+            nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, QF, None, w, g, 0, it, len(items), slab, self.F,
                          self.scale_w, self.scale_g, 0, 2, st)
         return slab
 
@@ -706,7 +736,7 @@ class TreeTrainer:
                 it = torch.from_numpy(items).to(self.dev)
                 slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
                 p2r = None if self._root_level else pos2row
-                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, p2r, w, gc, 0, it, len(items), slab, F,
+                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, QF, p2r, w, gc, 0, it, len(items), slab, F,
                              self.scale_w, self.scale_g, self._nmod, 0, st)
                 built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
                 feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
@@ -1253,8 +1283,10 @@ W_BITS, G_BITS = 16, 23     # per-row fixed-point magnitude bounds (packed histo
 # (gbdt_kernels.hip GSH32); SHIFU_GBDT_ROOT_U32=0 keeps the packed u64 kernel everywhere
 ROOT_U32 = os.environ.get("SHIFU_GBDT_ROOT_U32", "1") != "0"
 ROOT_GSH32 = 3               # = gbdt_kernels.hip GSH32
-# root sum w*g over whole quad records (SHIFU_GBDT_ROOT_QUAD=0: the per-group items)
+# root sum w*g over whole quad records when there is no [G][N][32] copy (SHIFU_GBDT_ROOT_QUAD=0:
+# the per-group items); SHIFU_GBDT_ROOT_G32=0 never makes the copy
 ROOT_QUAD = os.environ.get("SHIFU_GBDT_ROOT_QUAD", "1") != "0"
+ROOT_G32 = os.environ.get("SHIFU_GBDT_ROOT_G32", "1") != "0"
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on
 # power-of-two grids (|w*g| < 2^23 of the grid, the root's u32 w*g mode 2^3 coarser), summed
 # exactly in int64 (so every rank and every run finds the same splits)

@@ -54,7 +54,7 @@ HIP_SIGNATURES = {
     "shifu_ring_set_mf": "i",
     "shifu_ring_set_dmamma": "i",
     # gbdt_kernels.hip
-    "shifu_gbdt_hist": "plppp" "i" "pipi" "dd" "l" "i" "s",
+    "shifu_gbdt_hist": "pli" "ppp" "i" "pipi" "dd" "l" "i" "s",
     "shifu_gbdt_hist_root_quad": "plpppipids",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
     "shifu_gbdt_partition_flag": "plpppppppp" "ll" "pppp" "fi" "s",

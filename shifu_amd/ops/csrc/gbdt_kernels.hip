@@ -55,6 +55,8 @@ struct HistArgs {
   const float* w;                    // [N] per-row weight (significance x subsample)
   const float* g;                    // [N] per-row target (label / pseudo residual)
   int wg_by_pos;                     // 1: w / g are position-ordered (permuted with pos2row): contiguous reads
+  int rec;                           // row record bytes: 128 (quad-blocked) or 32 (group-blocked [G][N][32]
+                                     // copy the dense root pass streams; gs = N * rec)
   const int* items;                  // [n_items][4] = {node, pos_lo, pos_hi, group}
   long long* slab;                   // [n_items][2][FG][NB] int64 fixed point
   int n_items, n_feat;
@@ -107,7 +109,8 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   for (int i = threadIdx.x; i < 2 * NB * 16; i += HT) hsm[i] = 0ull;
   __syncthreads();
   const int half = threadIdx.x & 1, r = threadIdx.x & 15, t2 = threadIdx.x >> 1;
-  const uint8_t* gb = a.bins + (size_t)(grp >> 2) * a.gs + (grp & 3) * FG + half * 16;
+  const int gpr = a.rec / FG;                                   // groups per record (4 or 1)
+  const uint8_t* gb = a.bins + (size_t)(grp / gpr) * a.gs + (grp % gpr) * FG + half * 16;
   unsigned long long* base = hsm + half * NB * 16;
   // u32 modes: two interleaved copies [half][bin][copy][16] (lane group parity picks the copy):
   // the 4 lanes that update the same feature then spread over 4 banks unless their bins agree
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   uint32_t* base32 = hsm32 + half * NB * 32 + (((threadIdx.x >> 4) & 1) << 4);
   // w / g are indexed by the (virtual) row id -- or by position when wg_by_pos -- the bins by
   // the data row
-  auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * QF); };
+  auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * a.rec); };
   long long accw[HNE], accg[HNE];
 #pragma unroll
   for (int k = 0; k < HNE; ++k) { accw[k] = 0; accg[k] = 0; }
@@ -733,11 +736,12 @@ SHIFU_API int shifu_gbdt_hist_root_quad(const void* bins, long gs, const float* 
   return 0;
 }
 
-SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, const int* pos2row, const float* w, const float* g,
-                              int wg_by_pos, const int* items, int n_items, void* slab, int n_feat,
+SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, int rec, const int* pos2row, const float* w,
+                              const float* g, int wg_by_pos, const int* items, int n_items, void* slab, int n_feat,
                               double scale_w, double scale_g, long nmod, int mode, hipStream_t stream) {
-  if (gs % QF || n_items <= 0 || mode < 0 || mode > 2 || (wg_by_pos && nmod)) return -1;
-  HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, wg_by_pos, items, (long long*)slab, n_items, n_feat,
+  if ((rec != QF && rec != FG) || gs % rec || n_items <= 0 || mode < 0 || mode > 2 || (wg_by_pos && nmod))
+    return -1;
+  HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, wg_by_pos, rec, items, (long long*)slab, n_items, n_feat,
              (float)scale_w, (float)(mode == 2 ? scale_g / (1 << GSH32) : scale_g), nmod};
   static const int pf = [] { const char* e = getenv("SHIFU_HIST_PF"); return e ? atoi(e) : 1; }();
   const size_t lds = 2 * NB * 16 * 8;      // the u32 modes still use 64 KiB for the transposed store
