@@ -493,7 +493,10 @@ def bench_pipeline(a, dev, info):
     from shifu_amd.steps import api
     from shifu_amd.steps.create import create_model_set
     rows, F = a.rows, a.cols
+    rows_eval = max(1000, rows // 4)          # disk: the eval set is a quarter of the training set
     epochs = max(2, a.steps)
+    from shifu_amd.config import environment
+    environment.props()["shifu.norm.dtype"] = "bf16"     # GEMM-ready NormalizedData (half the bytes)
     work = a.workdir or os.path.join(tempfile.gettempdir(), "shifu_pipeline_bench")
     root = os.path.join(work, "pipe")
     t_gen = 0.0
@@ -503,10 +506,10 @@ def bench_pipeline(a, dev, info):
         root = create_model_set("pipe", "NN", parent=work)
         lib = _native.rt()
         t0 = time.perf_counter()
-        for name, seed in (("DataSet1", 11), ("EvalSet1", 12)):
+        for name, seed, nr in (("DataSet1", 11, rows), ("EvalSet1", 12, rows_eval)):
             d = os.path.join(root, "data", name)
             os.makedirs(d, exist_ok=True)
-            rc = lib.shifu_gen_csv(d.encode(), rows, F, 3, seed, 0.02, 20, min(16, os.cpu_count() or 4))
+            rc = lib.shifu_gen_csv(d.encode(), nr, F, 3, seed, 0.02, 20, min(16, os.cpu_count() or 4))
             if rc:
                 raise RuntimeError("data generation failed (disk full?)")
             hdr = ["id", "diagnosis", "wgt"] + [f"num_{j}" for j in range(F)] + [f"cat_{j}" for j in range(3)]
@@ -569,14 +572,15 @@ def bench_pipeline(a, dev, info):
         perf = json.load(open(os.path.join(root, "evals", "Eval1", "EvalPerformance.json")))
     total = sum(times.values())
     scale20 = REF_PIPELINE_ROWS / float(rows * info.world_size)
-    proj = {k: v * scale20 / 60.0 for k, v in times.items()}
+    proj = {k: v * (REF_PIPELINE_ROWS / float(rows_eval * info.world_size) if k == "eval" else scale20) / 60.0
+            for k, v in times.items()}
     ep_train = times["train"] / epochs
     out = {
         "metric": "rows/sec (whole pipeline init+stats+norm+varsel(SE)+train+eval, CLI steps on disk data)",
         "value": rows * info.world_size / total, "unit": "rows/s", "n_gpus": info.world_size, "steps": epochs,
         "warmup": 0, "ms_per_step": total * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "bf16 NN GEMMs / fp64 stats", "data": f"synthetic '|'-delimited text on disk, {rows} rows x {F} numeric "
-        "+ 3 categorical per GPU, planted rule on 20 columns (native generator)",
+        "dtype": "bf16 NN GEMMs / fp64 stats", "data": f"synthetic '|'-delimited text on disk, {rows} training + "
+        f"{rows_eval} eval rows x {F} numeric + 3 categorical per GPU, planted rule on 20 columns (native generator)",
         "config": {"model": f"default NN {F}-50-1 (tanh), SE varsel filterNum 200", "global_batch": rows * info.world_size,
                    "seq_len": None, "n_cols": F, "rows_per_gpu": rows, "parallelism": f"dp{info.world_size}"},
         "step_seconds": {k: round(v, 2) for k, v in times.items()}, "generation_s": round(t_gen, 1),
