@@ -469,6 +469,146 @@ def bench_treeinfer(a, dev, info):
     }
 
 
+def bench_corr(a, dev, info):
+    """K15: ``shifu stats -correlation`` sums (pairwise-complete Pearson, FastCorrelationMapper
+    J/core/correlation/FastCorrelationMapper.java:171-278) over rows x cols fp64 values per GPU
+    with 2% missing cells.  One step = every row through CorrAccumulator.update (int8 digit-plane
+    GEMMs, method i8) + finalize (fold, reduce-scatter of the six sums, correlation rows, gather).
+    Rows are drawn from a pool of device-resident 64K-row chunks (generated before the timed
+    section) that is cycled through -- the pass is compute bound, so reuse does not flatter it.
+    Also reported: the fp64 torch-addmm path (hipBLASLt fp64 GEMMs) over one pool pass, and the
+    max |corr_i8 - corr_fp64| over the pool (same shift)."""
+    from shifu_amd.algos.stats import CORR_CHUNK, CorrAccumulator
+    from shifu_amd.parallel import dist
+    n, F = a.rows, a.cols
+    CH = CORR_CHUNK if dev.type == "cuda" else 1024
+    npool = max(1, min(16, int(16e9 // (CH * F * 8)), -(-n // CH)))
+    g = torch.Generator(device=dev).manual_seed(5 + info.rank)
+    pool = []
+    for k in range(npool):
+        z = torch.randn(CH, F + 1, generator=g, device=dev, dtype=torch.float64)
+        x = z[:, 1:] + 0.6 * z[:, :-1]                         # neighbouring columns correlated
+        x[:, ::7] += 1000.0                                    # large-mean columns (shifted away)
+        x[torch.rand(CH, F, generator=g, device=dev) < 0.02] = float("nan")
+        pool.append(x.contiguous())
+        del z
+    shift = torch.zeros(F, dtype=torch.float64)
+    shift[::7] = 1000.0
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def one_pass(method, rows):
+        acc = CorrAccumulator(F, dev, shift=shift.numpy(), method=method)
+        k = 0
+        for r0 in range(0, rows, CH):
+            x = pool[k % npool]
+            acc.update(x[: min(CH, rows - r0)])
+            k += 1
+        return acc.finalize(0)
+
+    for _ in range(a.warmup):
+        one_pass("i8" if dev.type == "cuda" else "fp64", n)
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        C = one_pass("i8" if dev.type == "cuda" else "fp64", n)
+    sync()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce_(t, "max")
+    dt = float(t.item())
+    total = n * info.world_size
+    value = total * a.steps / dt
+    out = {
+        "metric": "correlation rows/s (whole node): pairwise-complete Pearson sums + finalize over every column pair",
+        "value": value, "unit": "rows/s", "n_gpus": info.world_size, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp64 values; exact int8 digit GEMMs (S=6 x 7-bit digits)" if dev.type == "cuda" else "fp64",
+        "data": f"synthetic N(0,1) with neighbour correlation, 2% missing, every 7th column mean 1000; "
+                f"{npool} device-resident 64K-row chunks cycled",
+        "config": {"model": "stats -correlation", "global_batch": total, "seq_len": None, "n_cols": F,
+                   "rows_per_gpu": n, "parallelism": f"dp{info.world_size}"},
+        "column_pair_updates_per_s": value * F * F,
+    }
+    if dev.type == "cuda":
+        # the previous path (four fp64 addmm per chunk) over one pool pass, and the agreement
+        rows_ref = npool * CH
+        sync()
+        t1 = time.perf_counter()
+        Cref = one_pass("fp64", rows_ref)
+        sync()
+        t_ref = time.perf_counter() - t1
+        Ci8 = one_pass("i8", rows_ref)
+        if info.rank == 0:
+            out["fp64_addmm_rows_per_s"] = rows_ref * info.world_size / t_ref
+            out["speedup_vs_fp64_addmm"] = value / out["fp64_addmm_rows_per_s"]
+            out["max_abs_diff_vs_fp64"] = float(np.nanmax(np.abs(Ci8 - Cref)))
+            out["corr_checksum"] = float(np.nansum(C))
+    return out
+
+
+def bench_eval(a, dev, info):
+    """K16 ``shifu eval`` performance pass (EvalModelProcessor -> ConfusionMatrix
+    .bufferedComputeConfusionMatrixAndPerformance, J/core/ConfusionMatrix.java:276-507) over
+    rows scored (score, tag, weight) records per GPU: stable descending radix sort on the device
+    (ops/csrc/sort_kernels.hip), cumulative confusion sweep, ROC / PR / gains bucket searches and
+    the score buckets -- the EvalPerformance.json of that eval set.  Each rank evaluates its own
+    eval set (N GPUs = N eval sets in parallel).  Reported also: the sort alone."""
+    from shifu_amd.algos import evaluation as E
+    from shifu_amd.parallel import dist
+    n = a.rows
+    g = torch.Generator(device=dev).manual_seed(11 + info.rank)
+    z = torch.randn(n, generator=g, device=dev, dtype=torch.float64)
+    y = (torch.rand(n, generator=g, device=dev, dtype=torch.float64) < torch.sigmoid(1.5 * z - 1.0)).double()
+    score = torch.round(1000.0 * torch.sigmoid(z + 0.3 * torch.randn(n, generator=g, device=dev,
+                                                                      dtype=torch.float64)))   # integer scores: ties
+    w = 0.5 + torch.rand(n, generator=g, device=dev, dtype=torch.float64)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    res = None
+    for _ in range(a.warmup):
+        res = E.performance(score, y, w, 10, max_score=1000.0, device=dev)
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = E.performance(score, y, w, 10, max_score=1000.0, device=dev)
+    sync()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce_(t, "max")
+    dt = float(t.item())
+    total = n * info.world_size
+    out = {
+        "metric": "eval performance rows/s (whole node): sort + confusion sweep + ROC/PR/gains/score buckets",
+        "value": total * a.steps / dt, "unit": "rows/s", "n_gpus": info.world_size, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp64",
+        "data": "synthetic scored records (integer scores 0..1000 -> heavy ties, logistic tags, U(0.5,1.5) weights)",
+        "config": {"model": "eval performance (10 buckets)", "global_batch": total, "seq_len": None,
+                   "rows_per_gpu": n, "parallelism": f"dp{info.world_size} (one eval set per rank)"},
+        "auc": res["areaUnderRoc"] if res else None,
+    }
+    if dev.type == "cuda":
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            E.order_desc(score)
+        sync()
+        out["sort_rows_per_s"] = 3 * n / (time.perf_counter() - t1)
+        t1 = time.perf_counter()
+        torch.argsort(-score, stable=True)
+        sync()
+        out["torch_stable_argsort_rows_per_s"] = n / (time.perf_counter() - t1)
+    return out
+
+
 REF_PIPELINE_MIN = {"stats": 20.0, "eval": 13.0, "varsel_train_200ep": 45.0, "varsel_se": 25.0}
 REF_PIPELINE_ROWS = 20_000_000
 
@@ -640,7 +780,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr", "stats", "treeinfer", "pipeline"])
+    ap.add_argument("--model", default="mlp", choices=["mlp", "gbdt", "varsel", "lr", "stats", "treeinfer", "pipeline", "corr", "eval"])
     ap.add_argument("--rows", type=int, default=None,
                     help="rows per GPU (default 125M on GPU: 256 GB of bf16 rows resident in one MI355X's "
                          "288 GB HBM, so 8 GPUs hold the metric's 1B-row x 1k-col table)")
@@ -669,9 +809,12 @@ def main():
         a.cols = 10_000
     if a.model == "pipeline" and a.cols == 1000:
         a.cols = 1600 if gpu else 40
+    if a.model == "corr" and a.cols == 1000:
+        a.cols = 1600 if gpu else 40
     if a.rows is None:
         a.rows = {"varsel": 2_000_000 if gpu else 2_000, "lr": 100_000, "stats": 100_000_000 if gpu else 5_000,
                   "treeinfer": 20_000_000 if gpu else 5_000, "pipeline": 2_000_000 if gpu else 4_000,
+                  "corr": 20_000_000 if gpu else 5_000, "eval": 100_000_000 if gpu else 20_000,
                   "gbdt": 100_000_000 if gpu else 20_000}.get(a.model, 125_000_000 if gpu else 20_000)
     if a.model == "gbdt":
         a.levels = a.gbdt_levels
@@ -685,6 +828,10 @@ def main():
         out = bench_treeinfer(a, dev, info)
     elif a.model == "pipeline":
         out = bench_pipeline(a, dev, info)
+    elif a.model == "corr":
+        out = bench_corr(a, dev, info)
+    elif a.model == "eval":
+        out = bench_eval(a, dev, info)
     elif a.model == "stats":
         if not gpu and a.cols == 1000:
             a.cols = 64

@@ -52,31 +52,56 @@ def _po(i, cm, bin_num=0, score_count=0.0, score_wcount=0.0, first=False):
     return po
 
 
-def _bucket_indices(metric: np.ndarray, nb: int, start: int = 1) -> list:
+def _bucket_indices(metric, nb: int, start: int = 1) -> list:
     """Rows (>= start) where the k-th bucket is emitted: first row after the previous emission
-    whose (monotone) metric >= k/nb."""
+    whose (monotone) metric >= k/nb.  ``metric``: numpy array or (device) tensor; one running max
+    and one binary search per bucket."""
+    m = torch.as_tensor(metric)
+    m = torch.where(torch.isnan(m), torch.full_like(m, -math.inf), m).cummax(0).values
     out, prev, k = [], start - 1, 1
     cap = 1.0 / nb
-    m = np.where(np.isnan(metric), -np.inf, metric)
+    n = m.numel()
     while True:
-        j = int(np.searchsorted(np.maximum.accumulate(m), k * cap, side="left"))
+        j = int(torch.searchsorted(m, torch.tensor([k * cap], dtype=m.dtype, device=m.device)).item())
         j = max(j, prev + 1)
-        if j >= len(m):
+        if j >= n:
             break
         out.append((k, j))
         prev, k = j, k + 1
     return out
 
 
-def confusion_sweep(score: np.ndarray, is_pos: np.ndarray, weight: np.ndarray | None = None, device=None,
-                    max_score: float | None = None):
-    """Sort descending by score and return cumulative confusion arrays of length N+1
-    (index 0 = the initial matrix with every record predicted negative)."""
+def order_desc(key, device=None):
+    """Stable descending order of scores (ties keep row order, NaN last): K16's radix sort on the
+    GPU (ops/csrc/sort_kernels.hip; int64 numpy array, or a device tensor for a device input),
+    numpy's stable argsort on the host."""
     dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
-    s = torch.as_tensor(np.asarray(score, dtype=np.float64), device=dev)
-    p = torch.as_tensor(np.asarray(is_pos, dtype=np.float64), device=dev)
-    w = torch.ones_like(s) if weight is None else torch.as_tensor(np.asarray(weight, dtype=np.float64), device=dev)
-    order = torch.argsort(-s, stable=True)
+    if torch.is_tensor(key) and key.device.type == "cuda":
+        from ..ops.stats_ops import sort_desc
+        return sort_desc(key).long()
+    k = np.asarray(key, dtype=np.float64)
+    if torch.device(dev).type == "cuda" and k.size >= 4096:
+        from ..ops.stats_ops import sort_desc
+        return sort_desc(torch.from_numpy(np.ascontiguousarray(k)).to(dev)).long().cpu().numpy()
+    return np.argsort(-k, kind="stable").astype(np.int64)
+
+
+def _as_dev(x, dev):
+    if torch.is_tensor(x):
+        return x.to(dev, torch.float64)
+    return torch.as_tensor(np.asarray(x, dtype=np.float64), device=dev)
+
+
+def confusion_sweep_t(score, is_pos, weight=None, device=None, max_score: float | None = None) -> dict:
+    """Sort descending by score and return cumulative confusion tensors of length N+1 on the
+    device (index 0 = the initial matrix with every record predicted negative).  Inputs: numpy
+    arrays or tensors (device-resident scores are not copied through the host)."""
+    dev = device or (score.device if torch.is_tensor(score) else
+                     (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")))
+    s = _as_dev(score, dev)
+    p = _as_dev(is_pos, dev)
+    w = torch.ones_like(s) if weight is None else _as_dev(weight, dev)
+    order = order_desc(s) if s.device.type == "cuda" else torch.argsort(-s, stable=True)
     s, p, w = s[order], p[order], w[order]
     z = torch.zeros(1, dtype=torch.float64, device=dev)
     tp = torch.cat([z, torch.cumsum(p, 0)])
@@ -86,9 +111,13 @@ def confusion_sweep(score: np.ndarray, is_pos: np.ndarray, weight: np.ndarray | 
     P, Nn, WP, WN = tp[-1], fp[-1], wtp[-1], wfp[-1]
     ms = float(s.max().item()) if max_score is None and s.numel() else (max_score or 0.0)
     sc = torch.cat([torch.tensor([ms], dtype=torch.float64, device=dev), s])
-    cm = dict(tp=tp, fp=fp, fn=P - tp, tn=Nn - fp, wtp=wtp, wfp=wfp, wfn=WP - wtp, wtn=WN - wfp, score=sc,
-              w=torch.cat([z, w]))
-    return {k: v.cpu().numpy() for k, v in cm.items()}
+    return dict(tp=tp, fp=fp, fn=P - tp, tn=Nn - fp, wtp=wtp, wfp=wfp, wfn=WP - wtp, wtn=WN - wfp, score=sc,
+                w=torch.cat([z, w]))
+
+
+def confusion_sweep(score, is_pos, weight=None, device=None, max_score: float | None = None):
+    """``confusion_sweep_t`` as host numpy arrays."""
+    return {k: v.cpu().numpy() for k, v in confusion_sweep_t(score, is_pos, weight, device, max_score).items()}
 
 
 def auc(points, xk, yk) -> float:
@@ -105,41 +134,51 @@ def auc(points, xk, yk) -> float:
 
 def performance(score, is_pos, weight=None, num_bucket: int = 10, max_score: float = 1000.0,
                 min_score: float = 0.0, device=None, version: str = "0.13.0"):
-    """-> PerformanceResult dict (EvalPerformance.json)."""
-    cm = confusion_sweep(score, is_pos, weight, device, max_score)
-    n = len(cm["tp"]) - 1
-    first = _po(0, cm, first=True)
-    tot = cm["tp"] + cm["fp"]
+    """-> PerformanceResult dict (EvalPerformance.json).  The sweep, the curves and the bucket
+    searches stay on the device; only the emitted rows' confusion values come to the host."""
+    cm = confusion_sweep_t(score, is_pos, weight, device, max_score)
+    n = cm["tp"].numel() - 1
+
+    def div(a, b):
+        return torch.where(b != 0, a / torch.where(b != 0, b, torch.ones_like(b)), torch.full_like(a, math.nan))
     wtot = cm["wtp"] + cm["wfp"] + cm["wfn"] + cm["wtn"]
-    recall = _div(cm["tp"], cm["tp"] + cm["fn"])
-    fpr = _div(cm["fp"], cm["fp"] + cm["tn"])
-    wrecall = _div(cm["wtp"], cm["wtp"] + cm["wfn"])
-    wfpr = _div(cm["wfp"], cm["wfp"] + cm["wtn"])
-    action = np.arange(n + 1) / max(n, 1)
-    waction = _div(cm["wtp"] + cm["wfp"], wtot)
-    lists = OrderedDict()
-    for key, metric in (("roc", fpr), ("pr", recall), ("gains", action), ("weightedRoc", wfpr),
-                        ("weightedPr", wrecall), ("weightedGains", waction)):
-        pts = [first]
-        for k, j in _bucket_indices(metric, num_bucket):
-            pts.append(_po(j, cm, k))
-        lists[key] = pts
-    # score buckets
+    curves = (("roc", div(cm["fp"], cm["fp"] + cm["tn"])), ("pr", div(cm["tp"], cm["tp"] + cm["fn"])),
+              ("gains", torch.arange(n + 1, dtype=torch.float64, device=cm["tp"].device) / max(n, 1)),
+              ("weightedRoc", div(cm["wfp"], cm["wfp"] + cm["wtn"])),
+              ("weightedPr", div(cm["wtp"], cm["wtp"] + cm["wfn"])),
+              ("weightedGains", div(cm["wtp"] + cm["wfp"], wtot)))
+    marks = {key: _bucket_indices(metric, num_bucket) for key, metric in curves}
+    del curves, wtot
+    # score buckets: bucket k closes at the first row after the previous emission whose score
+    # <= max_score - k * bin_score (binary searches on the descending scores)
     bin_score = (max_score - min_score) / num_bucket
-    ms = [first]
-    k, last = 1, 0
-    wcum = np.cumsum(cm["w"])
-    # emissions (binary searches on the descending scores, not a per-row loop): bucket k closes at
-    # the first row after the previous emission whose score <= max_score - k * bin_score
-    neg = -np.asarray(cm["score"][1:], dtype=np.float64)          # ascending
+    neg = -cm["score"][1:]                                           # ascending; NaN scores last
+    neg = torch.where(torch.isnan(neg), torch.full_like(neg, math.inf), neg)
+    wcum = torch.cumsum(cm["w"], 0)
+    emits, k, last = [], 1, 0
     while last < n:
         thr = max_score - k * bin_score
-        j = max(int(np.searchsorted(neg, -thr, side="left")) + 1, last + 1)
+        j = max(int(torch.searchsorted(neg, torch.tensor([-thr], dtype=neg.dtype, device=neg.device)).item()) + 1,
+                last + 1)
         if j > n:
             break
-        ms.append(_po(j, cm, k, float(j - last), float(wcum[j] - wcum[last])))
+        emits.append((k, j, last))
         k += 1
         last = j
+    # one gather of every emitted row
+    idx = sorted({0} | {j for v in marks.values() for _, j in v} | {j for _, j, _ in emits} |
+                 {l for _, _, l in emits})
+    it = torch.tensor(idx, dtype=torch.long, device=cm["tp"].device)
+    keys = ("tp", "fp", "fn", "tn", "wtp", "wfp", "wfn", "wtn", "score")
+    host = torch.stack([cm[c][it] for c in keys] + [wcum[it]]).cpu().numpy()
+    pos = {j: q for q, j in enumerate(idx)}
+    hcm = {c: host[r] for r, c in enumerate(keys)}
+    hw = host[len(keys)]
+    first = _po(0, hcm, first=True)
+    lists = OrderedDict()
+    for key in ("roc", "pr", "gains", "weightedRoc", "weightedPr", "weightedGains"):
+        lists[key] = [first] + [_po(pos[j], hcm, kk) for kk, j in marks[key]]
+    ms = [first] + [_po(pos[j], hcm, kk, float(j - l), float(hw[pos[j]] - hw[pos[l]])) for kk, j, l in emits]
     res = OrderedDict(version=version)
     res["areaUnderRoc"] = auc(lists["roc"], "fpr", "recall")
     res["weightedAreaUnderRoc"] = auc(lists["weightedRoc"], "weightedFpr", "weightedRecall")

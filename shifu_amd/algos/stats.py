@@ -552,29 +552,145 @@ def compute_psi(mc, ccs, md, unit_column: str, unit_stats_path: str | None = Non
     return ccs
 
 
+CORR_CHUNK = 65536      # rows per int8-digit GEMM launch (int32 bound: 7 pairs x 64^2 x 2^16 < 2^31)
+
+
+def corr_job_list(S: int) -> list:
+    """The K15 GEMM jobs for S digits: (name, [(A plane, B plane), ...], A scale row, B scale row,
+    digit weight exponent, symmetric).  Planes: 0 mask, 1..S digits of u / 2^ex, S+1..2S digits of
+    u^2 / 2^ey; scale rows 0 (ones), 1 (2^ex), 2 (2^ey).  A job's pairs share the weight
+    2^-wexp, so they sum in one int32 accumulator: sxy_d is the digit diagonal s + t = d."""
+    X, Y = (lambda s: 1 + s), (lambda s: 1 + S + s)
+    jobs = [("n", [(0, 0)], 0, 0, 0, True)]
+    jobs += [(f"sx{s}", [(X(s), 0)], 1, 0, 7 * (s + 1), False) for s in range(S)]
+    jobs += [(f"sxx{s}", [(Y(s), 0)], 2, 0, 7 * (s + 1), False) for s in range(S)]
+    jobs += [(f"sxy{d}", [(X(s), X(d - s)) for s in range(d + 1)], 1, 1, 7 * (d + 2), True) for d in range(S)]
+    return jobs
+
+
 class CorrAccumulator:
     """Pairwise-complete Pearson sums (H3, FastCorrelationMapper J/core/correlation/
     FastCorrelationMapper.java:171-278: rows where either value is missing are skipped per pair),
-    accumulated over row chunks on the device: per chunk four F x F GEMMs (hipBLASLt, fp64) of the
-    zero-filled values Xz, their squares and the validity mask M --
-        n = M'M,  sx = Xz'M (sum of x_i where j valid; sy = sx'),  sxx = (Xz*Xz)'M (syy = sxx'),
-        sxy = Xz'Xz
-    -- so the table never has to sit on the device (or in fp64 on the host) whole."""
+    accumulated over row chunks on the device, of the shifted values u = x - c (``shift`` c per
+    column -- e.g. the stats step's means; Pearson is shift invariant and the shift keeps the
+    final ``sxy - sx*sy/n`` free of cancellation), zero-filled where missing, and the mask M:
+        n = M'M,  sx = U'M (sum of u_i where j valid; sy = sx'),  sxx = (U*U)'M (syy = sxx'),
+        sxy = U'U
+    so the table never has to sit on the device (or in fp64 on the host) whole.
 
-    def __init__(self, n_cols: int, device=None):
+    ``method="i8"`` (default on the GPU, K15): every sum is an EXACT integer GEMM on the int8 MFMA
+    (ops/csrc/corr_kernels.hip digit planes + gemm_kernels.hip corr_i8_kernel): u / 2^ex and
+    u^2 / 2^ey are split into ``slices`` S balanced base-128 digits (S x 7 bits of each value,
+    relative to its column's chunk maximum), products of digit planes are summed in int32 and
+    flushed per 64K-row chunk into fp64 with their exact power-of-two weights; the symmetric n and
+    sxy run their upper tiles only.  ~2S + S(S+1)/4 int8 GEMMs at 2x the bf16 MFMA rate replace
+    four fp64 GEMMs at 1/32 of it.  ``method="fp64"``: four torch fp64 ``addmm`` per chunk (CPU,
+    and the oracle of the GPU tests)."""
+
+    def __init__(self, n_cols: int, device=None, shift=None, method: str | None = None, slices: int | None = None):
+        from ..config import environment
         self.F = int(n_cols)
         self.dev = torch.device(device) if device is not None else \
             (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
-        self.sums = torch.zeros(4, self.F, self.F, dtype=torch.float64, device=self.dev)
+        self.shift = None if shift is None else \
+            torch.as_tensor(np.asarray(shift, dtype=np.float64), device=self.dev).reshape(self.F).contiguous()
+        method = method or environment.get("shifu.stats.corr.method", "auto")
+        if method == "auto":
+            method = "i8" if self.dev.type == "cuda" and self.F > 0 else "fp64"
+        if method not in ("i8", "fp64"):
+            raise ValueError(f"unknown correlation method {method!r}")
+        if method == "i8" and self.dev.type != "cuda":
+            raise ValueError("correlation method i8 needs a GPU")
+        self.method = method
+        if method == "fp64":
+            self.sums = torch.zeros(4, self.F, self.F, dtype=torch.float64, device=self.dev)
+            return
+        from ..ops import _native as nat
+        nat.require_gpu_native()
+        self.S = int(slices or environment.get_int("shifu.stats.corr.slices", 6))
+        if not 4 <= self.S <= 7:
+            raise ValueError("shifu.stats.corr.slices must be in 4..7")
+        self._build_jobs(nat)
+        self.J = torch.zeros(len(self.job_names), self.F, self.F, dtype=torch.float64, device=self.dev)
+        self._planes = None
+        self._scale = torch.empty(3, self.F, dtype=torch.float64, device=self.dev)
+        self._maxbits = torch.empty(self.F, dtype=torch.int64, device=self.dev)
 
+    # -- i8 path -----------------------------------------------------------------------------
+    def _build_jobs(self, nat):
+        """Job table (gemm_kernels.hip CorrJob) and the (job, tile m, tile n) launch order."""
+        jobs = corr_job_list(self.S)
+        self.job_names = [j[0] for j in jobs]
+        self.job_sym = [j[5] for j in jobs]
+        rec = np.zeros((len(jobs), 4 + 14), dtype=np.int32)
+        for k, (_, pairs, ka, kb, wexp, _) in enumerate(jobs):
+            rec[k, :4] = (len(pairs), ka, kb, wexp)
+            for q, (a, b) in enumerate(pairs):
+                rec[k, 4 + q], rec[k, 11 + q] = a, b
+        assert rec.shape[1] * 4 == nat.hip().shifu_corr_job_bytes()
+        self._jobs = torch.from_numpy(rec).to(self.dev)
+        T = -(-self.F // 256)
+        items = []
+        for k, (_, pairs, _, _, _, sym) in enumerate(jobs):
+            for tm in range(T):
+                for tn in range(tm if sym else 0, T):
+                    items.append((len(pairs), k, tm, tn))
+        # heaviest first (longest K), then job / tile order so consecutive blocks share operand rows
+        items.sort(key=lambda t: (-t[0], t[1], t[2], t[3]))
+        self._items = torch.tensor([(k, tm, tn, 0) for _, k, tm, tn in items], dtype=torch.int32, device=self.dev)
+        self.n_items = len(items)
+
+    def _update_i8(self, X: torch.Tensor) -> None:
+        from ..ops import _native as nat
+        n, F = X.shape
+        if n == 0:
+            return
+        kpad = max(128, 1 << (n - 1).bit_length())
+        P = 1 + 2 * self.S
+        if self._planes is None or self._planes.numel() < P * F * kpad:
+            self._planes = torch.empty(P * F * kpad, dtype=torch.int8, device=self.dev)
+        st = nat.stream_of(X)
+        nat.call_hip("shifu_corr_planes", X, X.stride(0), n, F, self.shift, self.S, kpad, self._planes, F * kpad,
+                     self._scale, self._maxbits, st)
+        nat.call_hip("shifu_corr_gemm", self._planes, F * kpad, kpad, F, self._jobs, self._items, self.n_items,
+                     self._scale, self.J, F * F, st)
+
+    def _fold(self) -> torch.Tensor:
+        """[4, F, F] fp64 sums (n, sx, sxx, sxy) from the per-job buffers."""
+        T = torch.arange(self.F, device=self.dev) // 256
+        lower = T[:, None] > T[None, :]
+
+        def mirror(U):
+            return torch.where(lower, U.t(), U)
+        J, names = self.J, self.job_names
+        pick = lambda pre: [J[k] for k, nm in enumerate(names) if nm.rstrip("0123456789") == pre]
+        n = mirror(J[names.index("n")])
+        sx = torch.stack(pick("sx")).sum(0)
+        sxx = torch.stack(pick("sxx")).sum(0)
+        sxy = mirror(torch.stack(pick("sxy")).sum(0))
+        return torch.stack([n, sx, sxx, sxy])
+
+    # -- common ------------------------------------------------------------------------------
     def update(self, X) -> None:
-        X = torch.as_tensor(np.asarray(X), dtype=torch.float64).to(self.dev)
-        M = torch.isfinite(X).to(torch.float64)
-        Xz = torch.where(M > 0, X, torch.zeros_like(X))
+        if not torch.is_tensor(X):
+            X = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float64))
+        if self.method == "i8":
+            for r0 in range(0, X.shape[0], CORR_CHUNK):
+                xs = X[r0:r0 + CORR_CHUNK].to(self.dev, torch.float64, non_blocking=True)
+                self._update_i8(xs if xs.stride(1) == 1 else xs.contiguous())
+            return
+        X = X.to(self.dev, torch.float64)
+        M = torch.isfinite(X)
+        U = torch.where(M, X - self.shift if self.shift is not None else X, torch.zeros((), dtype=X.dtype, device=X.device))
+        M = M.to(torch.float64)
         self.sums[0].addmm_(M.t(), M)
-        self.sums[1].addmm_(Xz.t(), M)
-        self.sums[2].addmm_((Xz * Xz).t(), M)
-        self.sums[3].addmm_(Xz.t(), Xz)
+        self.sums[1].addmm_(U.t(), M)
+        self.sums[2].addmm_((U * U).t(), M)
+        self.sums[3].addmm_(U.t(), U)
+
+    def raw_sums(self) -> torch.Tensor:
+        """This rank's [4, F, F] fp64 (n, sx, sxx, sxy) of the shifted values."""
+        return self._fold() if self.method == "i8" else self.sums
 
     @staticmethod
     def _corr_rows(n, sx, sy, sxx, syy, sxy):
@@ -584,31 +700,39 @@ class CorrAccumulator:
 
     def finalize(self, dst: int = 0):
         """Global correlation matrix on rank ``dst`` (numpy), None elsewhere.  Data parallel: the
-        six F x F sums (the four + the transposes that supply sy/syy) are REDUCE-SCATTERED by row
-        blocks -- each rank gets 1/R of the bytes an all-reduce would leave on every rank --, every
-        rank computes its block of correlation rows, and the blocks are gathered to ``dst``."""
+        six F x F sums (the four + the transposes that supply sy/syy), laid out row-major as
+        [F][6][F] so that a rank's row block is one contiguous slab, are REDUCE-SCATTERED -- each
+        rank gets 1/R of the bytes an all-reduce would leave on every rank --, every rank computes
+        its block of correlation rows, and the blocks are gathered to ``dst``."""
         from ..parallel import dist
         F = self.F
-        n, sx, sxx, sxy = self.sums.unbind(0)
-        six = torch.stack([n, sx, sx.t(), sxx, sxx.t(), sxy])
-        blk = dist.reduce_scatter_rows(six)
+        n, sx, sxx, sxy = self.raw_sums().unbind(0)
+        six = torch.stack([n, sx, sx.t(), sxx, sxx.t(), sxy], dim=1)      # [F, 6, F]
+        if self.method == "i8":
+            self.J = None                                                  # free the job sums
+        blk = dist.reduce_scatter_rows(six, dim0=True)                     # [b - a, 6, F]
         a, b = dist.row_block(F)
-        rows = self._corr_rows(*blk.unbind(0))
+        rows = self._corr_rows(*blk.unbind(1))
         idx = torch.arange(a, b, device=rows.device)
         rows[idx - a, idx] = 1.0
         full = dist.gather_rows_to(rows, F, dst)
         return None if full is None else full.cpu().numpy()
 
 
-def pearson_correlation(mats, device=None, chunk_rows: int = 1 << 18, dst: int = 0):
+def pearson_correlation(mats, device=None, chunk_rows: int = 1 << 18, dst: int = 0, method: str | None = None):
     """Pairwise-complete Pearson of the columns of ``mats`` ([N, F] array, NaN = missing, or an
     iterable of such row chunks) -> [F, F] on rank ``dst`` (every rank when not distributed)."""
+    from ..parallel import dist
     acc = None
     chunks = [mats] if isinstance(mats, np.ndarray) or torch.is_tensor(mats) else mats
     for X in chunks:
         X = np.asarray(X) if not torch.is_tensor(X) else X
         if acc is None:
-            acc = CorrAccumulator(X.shape[1], device)
+            shift = None
+            if not dist._active() and len(X):       # single process: center on the first chunk's means
+                Xt = torch.as_tensor(X[:CORR_CHUNK], dtype=torch.float64)
+                shift = torch.nan_to_num(torch.nanmean(torch.where(torch.isfinite(Xt), Xt, torch.nan), 0)).cpu().numpy()
+            acc = CorrAccumulator(X.shape[1], device, shift=shift, method=method)
         for r0 in range(0, X.shape[0], chunk_rows):
             acc.update(X[r0:r0 + chunk_rows])
     if acc is None:

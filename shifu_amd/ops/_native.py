@@ -36,6 +36,10 @@ HIP_SIGNATURES = {
     "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "p" "s",
     "shifu_colsum_fixed": "pii" "pp" "s",
     "shifu_colsum_ws": ("ii", "l"),
+    # corr_kernels.hip + gemm_kernels.hip corr_i8_kernel (K15)
+    "shifu_corr_planes": "plii" "p" "ii" "pl" "pp" "s",
+    "shifu_corr_gemm": "plii" "ppi" "p" "pl" "s",
+    "shifu_corr_job_bytes": ("", "i"),
     # sort_kernels.hip
     "shifu_sort_ws": ("l", "l"),
     "shifu_sort_desc": "plpps",

@@ -63,6 +63,12 @@ struct GemmArgs {
   int M, N, K, NB, n_valid, act, bias_col;
   float flat;
   int dbg;                     // lab ablations (shifu_gemm_set_tune(9, v)); 0 in production
+  // segmented K (corr_i8_kernel): k-tiles [q * seg_nk, (q + 1) * seg_nk) read A rows from
+  // A + segA[q] * seg_stride and B rows from B + segB[q] * seg_stride (plane pairs summed in one
+  // pipeline).  Held as wave-uniform values and picked with a select chain: a load (or a dynamic
+  // index into a private array) inside the pipeline would be a vector-memory op that breaks the
+  // counted vmcnt waits.
+  int segA[7], segB[7]; long seg_stride; int seg_shift;   // seg_nk = 1 << seg_shift
 };
 
 // STAGES = LDS buffers.  1: single 32 KiB buffer + register prefetch (two barriers per k-step,
@@ -336,54 +342,74 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // into the buffer that is not read any more, so the counted waits stay exact.
 // ---------------------------------------------------------------------------------------
 constexpr int G8_T = 512, G8_HALF = 16384, G8_BUF = 4 * G8_HALF;
+typedef __attribute__((ext_vector_type(4))) int v4i_t;
 
 // Per-thread LDS-DMA source offsets of tile (m0, n0): half-tile h (0 A-top, 1 A-bot, 2 B-0, 3 B-1),
 // instruction i (2 per thread): LDS byte P = i*8192 + wid*1024 + lane*16 of the half-tile holds
 // logical chunk lc of row P>>7 (the swizzle is applied on the GLOBAL source address).
-__device__ __forceinline__ void gemm8_src(const GemmArgs& p, int m0, int n0, long (&off)[4][2]) {
+template <typename OffT = long>
+__device__ __forceinline__ void gemm8_src(const GemmArgs& p, int m0, int n0, OffT (&off)[4][2]) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int P = i * 8192 + wid * 1024 + lane * 16;
     const int row = P >> 7, lc = ((P >> 4) & 7) ^ ((row >> 1) & 7);
-    off[0][i] = (long)min(m0 + row, p.M - 1) * p.lda + lc * 8;
-    off[1][i] = (long)min(m0 + 128 + row, p.M - 1) * p.lda + lc * 8;
-    off[2][i] = (long)min(n0 + row, p.NB - 1) * p.ldb + lc * 8;
-    off[3][i] = (long)min(n0 + 128 + row, p.NB - 1) * p.ldb + lc * 8;
+    off[0][i] = (OffT)((long)min(m0 + row, p.M - 1) * p.lda + lc * 8);
+    off[1][i] = (OffT)((long)min(m0 + 128 + row, p.M - 1) * p.lda + lc * 8);
+    off[2][i] = (OffT)((long)min(n0 + row, p.NB - 1) * p.ldb + lc * 8);
+    off[3][i] = (OffT)((long)min(n0 + 128 + row, p.NB - 1) * p.ldb + lc * 8);
   }
 }
 
-__device__ __forceinline__ void gemm8_dma(const GemmArgs& p, const long (&off)[4][2], char* smem, int h, int kt) {
+template <bool SEG = false, typename OffT = long>
+__device__ __forceinline__ void gemm8_dma(const GemmArgs& p, const OffT (&off)[4][2], char* smem, int h, int kt) {
   const int wid = threadIdx.x >> 6;
   const int nk = p.K / 64;
   char* dst = smem + (kt & 1) * G8_BUF + h * G8_HALF + wid * 1024;
-  const int k0 = min(kt, nk - 1) * 64;
+  int k0 = min(kt, nk - 1) * 64;
   const bf16_t* src = h < 2 ? p.A : p.B;
+  if constexpr (SEG) {                 // wave-uniform shifts + scalar loads (no division: VALU)
+    const int kk = min(kt, nk - 1), q = kk >> p.seg_shift;
+    k0 = (kk & ((1 << p.seg_shift) - 1)) * 64;
+    int pl = h < 2 ? p.segA[0] : p.segB[0];
+#pragma unroll
+    for (int i = 1; i < 7; ++i) pl = q == i ? (h < 2 ? p.segA[i] : p.segB[i]) : pl;
+    src += (long)pl * p.seg_stride;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
     __builtin_amdgcn_global_load_lds((const void*)(src + off[h][i] + k0), (lds_ptr_t)(dst + i * 8192), 16, 0, 0);
 }
 
 // prologue DMAs of a tile: even k-tile 0 complete, odd k-tile 1 B halves (12 vector-memory ops)
-__device__ __forceinline__ void gemm8_prologue(const GemmArgs& p, const long (&off)[4][2], char* smem) {
-  gemm8_dma(p, off, smem, 2, 0); gemm8_dma(p, off, smem, 3, 0); gemm8_dma(p, off, smem, 0, 0);
-  gemm8_dma(p, off, smem, 1, 0); gemm8_dma(p, off, smem, 2, 1); gemm8_dma(p, off, smem, 3, 1);
+template <bool SEG = false, typename OffT = long>
+__device__ __forceinline__ void gemm8_prologue(const GemmArgs& p, const OffT (&off)[4][2], char* smem) {
+  gemm8_dma<SEG>(p, off, smem, 2, 0); gemm8_dma<SEG>(p, off, smem, 3, 0); gemm8_dma<SEG>(p, off, smem, 0, 0);
+  gemm8_dma<SEG>(p, off, smem, 1, 0); gemm8_dma<SEG>(p, off, smem, 2, 1); gemm8_dma<SEG>(p, off, smem, 3, 1);
 }
 
 // The 8-phase k-loop of one 256 x 256 output tile into acc (see the schedule above), after its
 // prologue DMAs.  extra16: the caller issued 16 vector-memory ops after the prologue (a persistent
 // kernel's epilogue stores of the previous tile), which the first wait leaves in flight.
-__device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8], const long (&off)[4][2],
-                                           char* smem, bool extra16 = false) {
+// I8: the operands are int8 (a k-tile = 128 int8 per row = the same 128 B that hold 64 bf16, so the
+// staging is unchanged; p.K / p.lda stay in 2-byte units) and every MFMA is
+// v_mfma_i32_16x16x64_i8 -- acc then holds int32 bits.  A and B fragments take the same 16 bytes
+// of a row, so the hardware's k order inside the 64 does not matter.  zero = false accumulates
+// onto acc (several operand pairs summed into one tile).
+template <bool I8 = false, typename OffT = long>
+__device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8], const OffT (&off)[4][2],
+                                           char* smem, bool extra16 = false, bool zero = true) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   const int nk = p.K / 64;
-  auto dma = [&](int h, int kt) { gemm8_dma(p, off, smem, h, kt); };
+  auto dma = [&](int h, int kt) { gemm8_dma<I8, OffT>(p, off, smem, h, kt); };
 
+  if (zero) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   bf16x8 af[4][2], bf0[2][2], bf1[2][2];
   const int lr = lane & 15, lq = lane >> 4;
@@ -408,9 +434,15 @@ __device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8]
 #pragma unroll
       for (int s_ = 0; s_ < 2; ++s_)
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          acc[nh * 2 + s_][mh * 4 + t] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s_][c], af[t][c], acc[nh * 2 + s_][mh * 4 + t], 0, 0, 0);
+        for (int t = 0; t < 4; ++t) {
+          f32x4& a_ = acc[nh * 2 + s_][mh * 4 + t];
+          if constexpr (I8)
+            a_ = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                     __builtin_bit_cast(v4i_t, bq[s_][c]), __builtin_bit_cast(v4i_t, af[t][c]),
+                     __builtin_bit_cast(v4i_t, a_), 0, 0, 0));
+          else
+            a_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s_][c], af[t][c], a_, 0, 0, 0);
+        }
   };
 #define G8_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
                       __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -468,8 +500,6 @@ __device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4
 // next tile's first loads, its launch, and this tile's stores overlap instead of serialising
 // (the fixed per-tile cost of gemm_nt_8ph_kernel: profiles/r3/mlp_lab_ablation_r3d.jsonl).
 // ---------------------------------------------------------------------------------------
-typedef __attribute__((ext_vector_type(4))) int v4i_t;
-
 template <int EPI, int ACT>
 __device__ __forceinline__ void epilogue_256_persist(const GemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0,
                                                      char* smem) {
@@ -871,6 +901,79 @@ __global__ __launch_bounds__(NTHR) void wgrad_tn_kernel(WgradArgs p) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// K15 pairwise-complete correlation sums (CorrAccumulator, shifu_amd/algos/stats.py; the
+// reference's FastCorrelationMapper J/core/correlation/FastCorrelationMapper.java:171-278 adds
+// fp64 products row by row).  corr_kernels.hip writes, per row chunk, int8 DIGIT PLANES
+// [P][F][kpad] (feature-major, rows contiguous): the validity mask m and S balanced base-128
+// digits of the column-scaled shifted value u = (x - c) / 2^ex and of u^2 / 2^ey.  Every sum is
+// then an exact integer NT GEMM over the chunk's rows on v_mfma_i32_16x16x64_i8 (the 8-phase
+// pipeline above, 2x the bf16 rate): a JOB is a list of (A plane, B plane) pairs that share one
+// power-of-two weight (e.g. the digit diagonal s + t = d of u_i u_j), accumulated in int32
+// (|digit| <= 64, <= 7 pairs: < 2^31 for chunks <= 64K rows), and flushed once per tile into its
+// own fp64 [F][F] sum with the exact scale 2^(ea_i + eb_j - wexp).  Symmetric jobs (m'm, u'u)
+// run the upper tiles only.
+// ---------------------------------------------------------------------------------------
+struct CorrJob {
+  int npairs, ka, kb, wexp;    // ka / kb: scale row (0 ones, 1 2^ex, 2 2^ey); weight 2^-wexp
+  int pa[7], pb[7];            // plane indices (npairs <= 7)
+};
+struct CorrArgs {
+  const int8_t* planes; long plane_stride; int kpad, F;
+  const CorrJob* jobs; const int4* items;   // item: {job, tile m, tile n, -}
+  const double* scale;                       // [3][F]
+  double* out; long out_stride;              // [jobs][F][F]
+};
+
+__global__ __launch_bounds__(G8_T, 1) void corr_i8_kernel(CorrArgs c) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int4 it4 = c.items[blockIdx.x];
+  const int job = __builtin_amdgcn_readfirstlane(it4.x);
+  const int4 it{job, __builtin_amdgcn_readfirstlane(it4.y), __builtin_amdgcn_readfirstlane(it4.z), 0};
+  const CorrJob& jb = c.jobs[job];
+  const int m0 = it.y * 256, n0 = it.z * 256;
+  // the job's plane pairs are consecutive K segments of one pipeline
+  GemmArgs p{};
+  p.A = p.B = (const bf16_t*)c.planes;
+  p.lda = p.ldb = c.kpad / 2;
+  p.seg_shift = __builtin_ctz(c.kpad / 128);
+  const int npairs = __builtin_amdgcn_readfirstlane(jb.npairs);
+  p.K = npairs * (c.kpad / 2);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    p.segA[i] = __builtin_amdgcn_readfirstlane(jb.pa[i]);
+    p.segB[i] = __builtin_amdgcn_readfirstlane(jb.pb[i]);
+  }
+  p.seg_stride = c.plane_stride / 2;
+  p.M = p.NB = p.N = c.F;
+  f32x4 acc[4][8];
+  int off[4][2];                      // 32-bit DMA offsets: a plane is < 2 GiB (host check)
+  gemm8_src<int>(p, m0, n0, off);
+  gemm8_prologue<true, int>(p, off, smem);
+  gemm8_loop<true, int>(p, acc, off, smem);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const double* sa = c.scale + (long)jb.ka * c.F;
+  const double* sb = c.scale + (long)jb.kb * c.F;
+  const double w = __builtin_ldexp(1.0, -jb.wexp);
+  double* o = c.out + (long)it.x * c.out_stride;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = m0 + wr * 128 + j * 16 + (lane & 15);
+    if (m >= c.F) continue;
+    const double am = sa[m] * w;
+    double* row = o + (long)m * c.F;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nb = n0 + wc * 64 + i * 16 + (lane >> 4) * 4;
+      const v4i_t v = __builtin_bit_cast(v4i_t, acc[i][j]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (nb + r < c.F) row[nb + r] += (double)v[r] * am * sb[nb + r];
+    }
+  }
+}
 }  // namespace
 
 // =======================================================================================
@@ -1031,3 +1134,22 @@ SHIFU_API int shifu_wgrad_tn(const void* D, long ldd, const void* X, long ldx, f
   return 0;
 }
 
+// K15 correlation sums: one launch per row chunk over n_items (job, tile) items (ordered by the
+// caller); planes [P][F][kpad] int8, kpad a power of two in [128, 65536] (int32 accumulation
+// bound: 7 pairs x 64^2 x 65536 < 2^31).
+SHIFU_API int shifu_corr_gemm(const void* planes, long plane_stride, int kpad, int F, const void* jobs,
+                              const void* items, int n_items, const double* scale, double* out,
+                              long out_stride, hipStream_t stream) {
+  if (kpad < 128 || (kpad & (kpad - 1)) || kpad > 65536 || F <= 0 || plane_stride < (long)F * kpad || plane_stride % 2 ||
+      n_items < 0 ||
+      out_stride < (long)F * F)
+    return -1;
+  if (n_items == 0) return 0;
+  if ((long)F * kpad >= (1l << 31)) return -1;
+  CorrArgs c{(const int8_t*)planes, plane_stride, kpad, F, (const CorrJob*)jobs, (const int4*)items, scale,
+             out, out_stride};
+  hipLaunchKernelGGL(corr_i8_kernel, dim3(n_items), dim3(G8_T), 2 * G8_BUF, stream, c);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+SHIFU_API int shifu_corr_job_bytes() { return (int)sizeof(CorrJob); }

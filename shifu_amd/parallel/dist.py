@@ -195,20 +195,36 @@ def row_block(n: int, rank: int | None = None, world: int | None = None) -> tupl
     return a, a + q + (1 if r < m else 0)
 
 
-def reduce_scatter_rows(t: torch.Tensor) -> torch.Tensor:
-    """Sum ``t`` [K, F, C] over ranks and return this rank's row block [K, b - a, C] (``row_block``
-    of F).  RCCL: one ``reduce_scatter_tensor`` over rank-major padded blocks (each rank receives
-    1/R of the bytes an all-reduce would leave everywhere); gloo (no reduce-scatter): all-reduce +
-    slice."""
+def reduce_scatter_rows(t: torch.Tensor, dim0: bool = False) -> torch.Tensor:
+    """Sum ``t`` over ranks and return this rank's row block (``row_block`` of F).
+
+    ``t`` is [K, F, C] (block [K, b - a, C]) or, with ``dim0``, [F, K, C] (block [b - a, K, C]):
+    there a rank's rows are one contiguous slab, so when R divides F the tensor goes to RCCL's
+    ``reduce_scatter_tensor`` as it is (no padded rank-major copy; each rank receives 1/R of the
+    bytes an all-reduce would leave everywhere).  gloo (no reduce-scatter): all-reduce + slice."""
     if not _active():
         return t
-    K, F, C = t.shape
     w, r = tdist.get_world_size(), tdist.get_rank()
+    F = t.shape[1] if not dim0 else t.shape[0]
     a, b = row_block(F, r, w)
     if tdist.get_backend() != "nccl":
         all_reduce_(t)
-        return t[:, a:b].contiguous()
+        return (t[a:b] if dim0 else t[:, a:b]).contiguous()
     fb = -(-F // w)
+    if dim0 and F % w == 0:
+        t = t.contiguous()
+        out = torch.empty((fb,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        tdist.reduce_scatter_tensor(out.reshape(-1), t.reshape(-1), op=tdist.ReduceOp.SUM)
+        return out
+    if dim0:
+        src = torch.zeros((w, fb) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        for k in range(w):
+            ka, kb = row_block(F, k, w)
+            src[k, : kb - ka] = t[ka:kb]
+        out = torch.empty((fb,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        tdist.reduce_scatter_tensor(out.reshape(-1), src.reshape(-1), op=tdist.ReduceOp.SUM)
+        return out[: b - a].contiguous()
+    K, _, C = t.shape
     src = torch.zeros(w, K, fb, C, dtype=t.dtype, device=t.device)
     for k in range(w):
         ka, kb = row_block(F, k, w)

@@ -263,7 +263,7 @@ def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, no
     if write and sort and n_local:
         key = np.load(os.path.join(pdir, "key.npy"), mmap_mode="r")
         k = np.nan_to_num(np.asarray(key), nan=-np.inf)
-        order = np.argsort(-k, kind="stable").astype(np.int64)
+        order = E.order_desc(k)
         blob = np.memmap(os.path.join(pdir, "lines.bin"), dtype=np.uint8, mode="r") if off else np.zeros(1, np.uint8)
         ends = np.ascontiguousarray(np.load(os.path.join(pdir, "ends.npy")))
         new_end = np.zeros(n_local, np.int64)
@@ -363,7 +363,7 @@ def score_eval(ms: ModelSet, ev, device=None, write: bool = True, nosort: bool =
                 sel = ev.get("performanceScoreSelector", "mean") or "mean"
                 key = np.asarray(res.get(sel, res.get("mean")), dtype=np.float64)
                 if key.ndim == 1 and len(key) == md.n:
-                    order = np.argsort(-key, kind="stable")
+                    order = E.order_desc(key)
             for i in order:
                 row = [str(tags[i]), repr(float(md.w[i]))]
                 row += [f"{float(m[i]):.6f}" if m.ndim == 1 else ",".join(f"{v:.6f}" for v in m[i]) for m in mats]
@@ -433,7 +433,7 @@ def _write_scores_dp(ms, ev, md, res, tags, meta_names, nosort):
         sel = ev.get("performanceScoreSelector", "mean") or "mean"
         key = np.asarray(res.get(sel, res.get("mean")), dtype=np.float64)
         if key.ndim == 1 and len(key) == md.n:
-            order = np.argsort(-key, kind="stable")
+            order = E.order_desc(key)
         else:
             key = None
     part = f"{path}.rank{info.rank:05d}"

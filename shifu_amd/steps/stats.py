@@ -166,7 +166,10 @@ def run_correlation(ms: ModelSet, device=None, chunk_rows: int = 1 << 18):
         C = np.load(cache_m, allow_pickle=False)
     else:
         md = shard_model_data(ms.load_raw(cols))
-        acc = S.CorrAccumulator(len(cols), device)
+        # center on the stats step's means (the same on every rank; Pearson is shift invariant)
+        shift = [0.0 if c.is_categorical() or not isinstance(c.mean, (int, float)) or not np.isfinite(c.mean)
+                 else float(c.mean) for c in cols]
+        acc = S.CorrAccumulator(len(cols), device, shift=shift)
         for r0 in range(0, max(md.n, 1), chunk_rows):
             r1 = min(md.n, r0 + chunk_rows)
             if r1 <= r0:
