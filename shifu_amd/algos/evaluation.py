@@ -72,18 +72,22 @@ def _bucket_indices(metric, nb: int, start: int = 1) -> list:
 
 
 def order_desc(key, device=None):
-    """Stable descending order of scores (ties keep row order, NaN last): K16's radix sort on the
-    GPU (ops/csrc/sort_kernels.hip; int64 numpy array, or a device tensor for a device input),
-    numpy's stable argsort on the host."""
+    """Stable descending order of scores: ties keep row order, NaN ranks with -inf (last).  K16's
+    radix sort on the GPU (ops/csrc/sort_kernels.hip) for a device tensor or, when a GPU is
+    present, for a large host array; a stable argsort otherwise.  Returns the input's kind
+    (device tensor / numpy int64)."""
+    if torch.is_tensor(key):
+        if key.device.type == "cuda":
+            from ..ops.stats_ops import sort_desc
+            return sort_desc(key).long()
+        k = key.to(torch.float64)
+        return torch.argsort(-torch.where(torch.isnan(k), torch.full_like(k, -math.inf), k), stable=True)
     dev = device or (torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
-    if torch.is_tensor(key) and key.device.type == "cuda":
-        from ..ops.stats_ops import sort_desc
-        return sort_desc(key).long()
     k = np.asarray(key, dtype=np.float64)
     if torch.device(dev).type == "cuda" and k.size >= 4096:
         from ..ops.stats_ops import sort_desc
         return sort_desc(torch.from_numpy(np.ascontiguousarray(k)).to(dev)).long().cpu().numpy()
-    return np.argsort(-k, kind="stable").astype(np.int64)
+    return np.argsort(-np.where(np.isnan(k), -np.inf, k), kind="stable").astype(np.int64)
 
 
 def _as_dev(x, dev):
@@ -101,7 +105,7 @@ def confusion_sweep_t(score, is_pos, weight=None, device=None, max_score: float 
     s = _as_dev(score, dev)
     p = _as_dev(is_pos, dev)
     w = torch.ones_like(s) if weight is None else _as_dev(weight, dev)
-    order = order_desc(s) if s.device.type == "cuda" else torch.argsort(-s, stable=True)
+    order = order_desc(s)
     s, p, w = s[order], p[order], w[order]
     z = torch.zeros(1, dtype=torch.float64, device=dev)
     tp = torch.cat([z, torch.cumsum(p, 0)])

@@ -15,6 +15,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import numpy as np
@@ -248,12 +250,45 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
     elif dev.type == "cuda" and Ws[-1].shape[0] == 1:
         # K14b: perturbed first layer as bf16 rows -> MFMA GEMM tail
         from ..ops import stats_ops
+        from ..ops import _native as nat
         H1 = W1.shape[0]
-        hpad = ((H1 + 1 + 7) // 8) * 8
+        pad64 = lambda k: ((k + 63) // 64) * 64
+        hpad = pad64(H1 + 1)
         W1t = W1.t().contiguous()
         Wb = [W.to(torch.bfloat16) for W in Ws]
+        # own MFMA GEMMs (gemm_kernels.hip shifu_gemm_nt, EPI_ACT): each layer's activation, bias
+        # column and zero padding are written by the GEMM epilogue as the next layer's bf16 rows;
+        # W_l padded to [out_l, pad64(in_l + 1)] with the bias weight at column in_l (the Encog
+        # flat layout).  SHIFU_SE_TAIL=torch: the previous torch bf16 matmul + cat tail.
+        hip_tail = os.environ.get("SHIFU_SE_TAIL", "hip") != "torch"
+        Wp, kin = [None], [hpad]
+        for l in range(1, len(Ws)):
+            o, i1 = Ws[l].shape
+            w = torch.zeros(o, pad64(i1), dtype=torch.bfloat16, device=dev)
+            w[:, :i1] = Wb[l]
+            Wp.append(w)
+            kin.append(pad64(o + 1) if l < len(Ws) - 1 else 64)
+        bufs = {}
 
         def tail_bf16(A):                         # A [M, hpad] bf16 rows with bias column
+            if hip_tail:
+                M = A.shape[0]
+                st = nat.stream_of(A)
+                for l in range(1, len(Ws)):
+                    last = l == len(Ws) - 1
+                    N, act = kin[l], ACT_IDS[acts[l]]
+                    key = (l, M)
+                    if key not in bufs:
+                        bufs[key] = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+                    C = bufs[key]
+                    C2 = None
+                    if act in (5, 8):             # swish / sin: derivative not derivable from output
+                        C2 = bufs.setdefault(("d", l, M), torch.empty(M, N, dtype=torch.bfloat16, device=dev))
+                    nat.call_hip("shifu_gemm_nt", A, kin[l - 1], Wp[l], kin[l - 1], Ws[l].shape[0], C, N, C2, N,
+                                 None, 0, None, 0, M, N, kin[l - 1], 0, act, Ws[l].shape[0], 0 if last else 1, 0.0,
+                                 st)
+                    A = C
+                return A[:, 0].float()
             k = H1 + 1
             for l in range(1, len(Ws)):
                 z = (A[:, :k] @ Wb[l].t()).float()

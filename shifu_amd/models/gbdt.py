@@ -911,8 +911,9 @@ class TreeTrainer:
         cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
         pred, scale = fuse
         self._leaf_done = True
-        nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
-                     None, None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale),
+        rb = self._root_bins()
+        nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, d.n * FG if rb is not None else 0,
+                     pos2row, pos_node, sf, sb, cl, self.is_cat_t, None, None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale),
                      1, nat.stream_of(d.y))
 
     def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots, leaf=None):
@@ -935,8 +936,9 @@ class TreeTrainer:
             wcnt = torch.empty(nw, dtype=torch.int32, device=self.dev)
             lv, (pred, scale) = leaf if leaf is not None else (None, (None, 0.0))
             # non-split nodes' rows get their leaf value here (fused GBT prediction update)
-            nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, pos2row, pos_node, sf, sb, cl,
-                         self.is_cat_t, fbits, wcnt, n, self._nmod, pred, None if lv is None else lv[0], None, None,
+            rb = self._root_bins()        # 32-B records when the root's [G][N][32] copy exists
+            nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, d.n * FG if rb is not None else 0,
+                         pos2row, pos_node, sf, sb, cl, self.is_cat_t, fbits, wcnt, n, self._nmod, pred, None if lv is None else lv[0], None, None,
                          float(scale), 0, st)
             wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
             # per-node: #left = cum[end-1] - cum[start-1]

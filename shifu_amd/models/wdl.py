@@ -8,8 +8,8 @@ layers down to one logit; ``p = sigmoid(wide + deep)``; the gradient is the sigm
 ``(p - y) p (1 - p) s`` with L2 (``WDLL2Reg``).  Full-batch epochs with the gradient all-reduced
 over ranks like the NN trainer (``WDLMaster.doCompute`` :164-184 sums worker gradients).
 
-On the GPU the embedding gathers / GEMMs run as PyTorch-ROCm ops (hipBLASLt GEMMs; the model is
-small and bandwidth-bound on the embedding gathers).  File format ``.wdl``: the reference's
+On the GPU the wide sums and the deep input gathers are one HIP pass (``wdl_kernels.hip``), and
+the deep tower's GEMMs run on the MLP's hand-written bf16 MFMA kernels (``_DeepMFMA``).  File format ``.wdl``: the reference's
 ``BinaryWDLSerializer`` / ``IndependentWDLModel`` layout (``formats/wdl_format.py``).
 """
 from __future__ import annotations
@@ -64,6 +64,110 @@ class _WdlGather(torch.autograd.Function):
         return ddense, None, dwt, det, None, None, None, None, None, None
 
 
+# deep layers on the hand-written bf16 MFMA GEMMs (gemm_kernels.hip); SHIFU_WDL_DEEP=torch: fp32 torch
+WDL_DEEP_HIP = os.environ.get("SHIFU_WDL_DEEP", "hip") != "torch"
+_P = 128                                  # row widths padded to 128 (gemm_nt K % 64, wgrad_tn K % 128)
+
+
+def _pad(k: int) -> int:
+    return ((k + _P - 1) // _P) * _P
+
+
+def _deriv_from_out(act: str, a: torch.Tensor) -> torch.Tensor:
+    """f'(z) from the activation output a = f(z) (common.h act_deriv_out)."""
+    if act == "sigmoid":
+        return a * (1 - a)
+    if act == "tanh":
+        return 1 - a * a
+    if act == "linear":
+        return torch.ones_like(a)
+    if act == "relu":
+        return (a > 0).to(a.dtype)
+    if act == "leakyrelu":
+        return torch.where(a <= 0, torch.full_like(a, 0.01), torch.ones_like(a))
+    if act == "ptanh":
+        return torch.where(a > 0, 1 - a * a, 0.25 * (1 - 16 * a * a))
+    if act == "log":
+        return torch.exp(-a.abs())
+    raise ValueError(act)
+
+
+class _DeepMFMA(torch.autograd.Function):
+    """Deep tower (dense + activation layers, then the linear output neuron) with every GEMM on
+    the MLP's own kernels: forward ``shifu_gemm_nt`` EPI_ACT (activation, bias column and zero
+    padding written by the epilogue as the next layer's bf16 rows -- no per-layer cat), backward
+    ``shifu_gemm_nt`` EPI_DACT (dgrad x f'(a) fused) and ``shifu_wgrad_tn`` (fp32 weight
+    gradients).  bf16 activations / deltas, fp32 accumulation (the NN trainer's precision);
+    WideAndDeep.java:163-232 semantics (no flat spot)."""
+
+    @staticmethod
+    def forward(ctx, A, final, acts, *Ws):
+        from ..ops import _native as nat
+        from .nn import ACT_IDS
+        dev, n = A.device, A.shape[0]
+        st = nat.stream_of(A)
+        dims = [A.shape[1]] + [W.shape[0] for W in Ws]
+        kp = [_pad(d + 1) for d in dims]
+        X = torch.zeros(n, kp[0], dtype=torch.bfloat16, device=dev)
+        X[:, : dims[0]] = A
+        X[:, dims[0]] = 1.0
+        xs, ders, wbs = [X], [], []
+        for l, (W, act) in enumerate(zip(Ws, acts)):
+            wb = torch.zeros(dims[l + 1], kp[l], dtype=torch.bfloat16, device=dev)
+            wb[:, : dims[l] + 1] = W
+            C = torch.empty(n, kp[l + 1], dtype=torch.bfloat16, device=dev)
+            aid = ACT_IDS[act]
+            C2 = None if aid in (0, 1, 2, 3, 4, 6, 7) else torch.empty_like(C)
+            nat.call_hip("shifu_gemm_nt", xs[-1], kp[l], wb, kp[l], dims[l + 1], C, kp[l + 1], C2, kp[l + 1], None, 0,
+                         None, 0, n, kp[l + 1], kp[l], 0, aid, dims[l + 1], 1, 0.0, st)
+            xs.append(C)
+            ders.append(C2)
+            wbs.append(wb)
+        hL = xs[-1][:, : dims[-1] + 1].float()                   # [n, h_L + 1] incl. the bias column
+        out = hL @ final[0]
+        ctx.save_for_backward(final, hL, *xs, *Ws)
+        ctx.meta = (list(acts), dims, kp, ders, wbs, len(Ws))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ..ops import _native as nat
+        from .nn import ACT_IDS
+        acts, dims, kp, ders, wbs, L = ctx.meta
+        saved = ctx.saved_tensors
+        final, hL = saved[0], saved[1]
+        xs, Ws = saved[2: 3 + L], saved[3 + L:]
+        n, dev = hL.shape[0], hL.device
+        st = nat.stream_of(hL)
+        g = g.contiguous().float()
+        g_final = (g @ hL)[None, :]
+        # output delta -> last hidden layer delta (elementwise; the output neuron is linear)
+        aL = hL[:, : dims[-1]]
+        dl = ders[-1][:, : dims[-1]].float() if ders[-1] is not None else _deriv_from_out(acts[-1], aL)
+        D = torch.zeros(n, kp[-1], dtype=torch.bfloat16, device=dev)
+        D[:, : dims[-1]] = (g[:, None] * final[0, : dims[-1]][None, :]) * dl
+        gWs = [None] * L
+        for l in range(L - 1, -1, -1):
+            G = torch.zeros(dims[l + 1], kp[l], dtype=torch.float32, device=dev)
+            nat.call_hip("shifu_wgrad_tn", D, kp[l + 1], xs[l], kp[l], G, kp[l], n, dims[l + 1], kp[l],
+                         max(1, min(n // 256, 256)), st)
+            gWs[l] = G[:, : dims[l] + 1]
+            # delta of the layer below (or the input gradient): D W_l through W_l^T as B rows
+            wt = torch.zeros(kp[l], kp[l + 1], dtype=torch.bfloat16, device=dev)
+            wt[: dims[l] + 1, : dims[l + 1]] = Ws[l].t()
+            Dn = torch.empty(n, kp[l], dtype=torch.bfloat16, device=dev)
+            if l > 0:
+                aid = ACT_IDS[acts[l - 1]]
+                nat.call_hip("shifu_gemm_nt", D, kp[l + 1], wt, kp[l + 1], kp[l], Dn, kp[l], None, 0,
+                             xs[l], kp[l], ders[l - 1], kp[l], n, kp[l], kp[l + 1], 1, aid, dims[l], 0, 0.0, st)
+            else:
+                nat.call_hip("shifu_gemm_nt", D, kp[1], wt, kp[1], kp[0], Dn, kp[0], None, 0, None, 0, None, 0,
+                             n, kp[0], kp[1], 2, 2, dims[0], 0, 0.0, st)
+            D = Dn
+        dA = D[:, : dims[0]].float()
+        return (dA, g_final, None, *gWs)
+
+
 class WideDeepNet(torch.nn.Module):
     def __init__(self, n_dense: int, cat_sizes: list, embed_fields: list, embed_dim: int, hidden: list,
                  acts: list, wide: bool = True, deep: bool = True):
@@ -107,10 +211,13 @@ class WideDeepNet(torch.nn.Module):
         if self.wide_on:
             logit = logit + dense @ self.wide_dense + self.bias + wide
         if self.deep_on:
-            a = A
-            for W, act in zip(self.layers, self.acts):
-                a = act_fwd(act, a @ W[:, :-1].t() + W[:, -1])
-            logit = logit + (a @ self.final[:, :-1].t() + self.final[:, -1])[:, 0]
+            if WDL_DEEP_HIP and len(self.layers):
+                logit = logit + _DeepMFMA.apply(A, self.final, tuple(self.acts), *self.layers)
+            else:
+                a = A
+                for W, act in zip(self.layers, self.acts):
+                    a = act_fwd(act, a @ W[:, :-1].t() + W[:, -1])
+                logit = logit + (a @ self.final[:, :-1].t() + self.final[:, -1])[:, 0]
         return logit
 
     def forward(self, dense: torch.Tensor, cats: torch.Tensor) -> torch.Tensor:

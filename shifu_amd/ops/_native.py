@@ -61,7 +61,7 @@ HIP_SIGNATURES = {
     "shifu_gbdt_hist": "pli" "ppp" "i" "pipi" "dd" "l" "i" "s",
     "shifu_gbdt_hist_root_quad": "plpppipids",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
-    "shifu_gbdt_partition_flag": "plpppppppp" "ll" "pppp" "fi" "s",
+    "shifu_gbdt_partition_flag": "plpl" "pppppppp" "ll" "pppp" "fi" "s",
     "shifu_gbdt_bitrank": "pppip" "s",
     "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "pppp" "l" "s",
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",

@@ -469,6 +469,9 @@ __global__ __launch_bounds__(256) void gbdt_split_kernel(SplitArgs a) {
 // ---------------------------------------------------------------------------------------
 struct PartArgs {
   const uint8_t* bins; long gs;   // quad-blocked [Q][N][128]
+  // nullable: the [G][N][32] copy of the same bins (the dense root pass's); a row's split-feature
+  // byte is then read from its 32-B record instead of a 128-B quad record (1/4 of the lines)
+  const uint8_t* bins32; long gs32;
   const int* pos2row;
   const int* pos_node;          // [N] node slot of each position (current level)
   const int* split_feat;        // [n_nodes]
@@ -495,7 +498,7 @@ __device__ __forceinline__ int partition_flag(const PartArgs& a, long p) {
   int fl = 0;
   if (f >= 0) {
     const long v = a.pos2row[p], row = a.nmod ? v % a.nmod : v;
-    const uint32_t b = a.bins[bin_off(a.gs, row, f)];
+    const uint32_t b = a.bins32 ? a.bins32[(f >> 5) * a.gs32 + row * 32 + (f & 31)] : a.bins[bin_off(a.gs, row, f)];
     if (a.is_cat[f]) fl = (a.cat_left[node * 8 + (b >> 5)] >> (b & 31)) & 1;
     else fl = (int)b <= a.split_bin[node] ? 1 : 0;
     if (a.pred && a.final_level) a.pred[row] += a.scale * (fl ? a.child_l_val[node] : a.child_r_val[node]);
@@ -770,13 +773,14 @@ SHIFU_API int shifu_gbdt_split(const void* slab, const int* node_items, int max_
   return 0;
 }
 
-SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const int* pos2row, const int* pos_node,
+SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const void* bins32, long gs32,
+                                        const int* pos2row, const int* pos_node,
                                         const int* split_feat, const int* split_bin, const void* cat_left,
                                         const void* is_cat, void* fbits, int* wcnt, long n, long nmod, float* pred,
                                         const float* node_val, const float* child_l_val,
                                         const float* child_r_val, float scale, int final_level,
                                         hipStream_t stream) {
-  PartArgs a{(const uint8_t*)bins, gs, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
+  PartArgs a{(const uint8_t*)bins, gs, (const uint8_t*)bins32, gs32, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
              (const uint8_t*)is_cat, (unsigned long long*)fbits, wcnt, n, nmod, pred, node_val, child_l_val,
              child_r_val, scale,
              final_level};

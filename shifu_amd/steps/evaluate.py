@@ -11,6 +11,7 @@ model0..N | meta columns.  Scores are scaled by ``scoreScale`` (default 1000).
 """
 from __future__ import annotations
 
+import math
 import os
 from collections import OrderedDict
 
@@ -176,7 +177,7 @@ class _StreamedEval:
         self.n, self.w, self.table = n, w, _GTable(cols)
 
 
-def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, nosort):
+def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, nosort, local_metrics=False):
     """Out-of-core eval (the reference streams Eval.pig: EvalScoreUDF per row, then ORDER BY): this
     rank's byte range is scored chunk by chunk; each chunk's EvalScore lines are formatted natively
     and appended to the rank's run with the numeric (score, label, weight, score-meta) columns;
@@ -307,9 +308,12 @@ def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, no
                         shutil.copyfileobj(src, f, 1 << 22)
         _log.info("eval %s: scored %d rows on %d rank(s) with %d models (streamed) -> %s", ev.get("name"),
                   sum(counts), info.world_size, len(runner.models), path)
-    # metrics inputs on rank 0: the numeric parts, memory-mapped in rank order
+    # metrics inputs on rank 0: the numeric parts, memory-mapped in rank order (local_metrics:
+    # every rank its own part, for the collective EvalPerformance of algos/eval_dist.py)
     live = [p_ for p_, c in zip(parts, counts) if c] or parts[:1]
-    if info.rank != 0:
+    if local_metrics:
+        live = [pdir]
+    elif info.rank != 0:
         return None
 
     def col(name):
@@ -504,10 +508,18 @@ def _gather_eval_numeric(ms, ev, md, res, tags, score_meta):
     return _GatheredEval(len(lab), got["w"], cols), res, tags
 
 
-def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None, lab=None):
+def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None, lab=None, collective: bool = False):
     """``lab`` (optional, numeric labels of the streamed eval): binary 1 pos / 0 neg / -1 neither,
-    multi-class the tag-group index; replaces the per-row tag strings."""
+    multi-class the tag-group index; replaces the per-row tag strings.  ``collective``: every
+    rank passes its own rows and the metrics are the exact global ones (algos/eval_dist.py,
+    binary only); rank 0 writes the files."""
+    from ..parallel import dist
     mc = ms.mc
+    if collective:
+        from ..algos import eval_dist
+        perf_fn, writer = eval_dist.performance, dist.info().rank == 0
+    else:
+        perf_fn, writer = E.performance, True
     d = ms.pf.eval_dir(ev.get("name"))
     os.makedirs(d, exist_ok=True)
     pos = set(ev.dataSet.get("posTags") or mc.pos_tags)
@@ -537,22 +549,27 @@ def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None, lab=N
         valid = np.isin(tg, list(pos | neg))
         is_pos = np.isin(tg[valid], list(pos))
     w = np.asarray(md.w)[valid] if ev.dataSet.get("weightColumnName") else None
-    perf = E.performance(score[valid], is_pos, w, nb, max_score=scale, device=device)
-    with open(ms.pf.eval_performance(ev), "w") as f:
-        f.write(E.to_json(perf))
-    E.write_gain_chart(ms.pf.eval_gain_chart(ev, "gainchart", "html"), ms.pf.eval_gain_chart(ev, "gainchart", "csv"),
-                       perf, ev.get("name"))
-    _log.info("eval %s: AUC(ROC)=%.6f AUC(PR)=%.6f weighted AUC=%.6f", ev.get("name"), perf["areaUnderRoc"],
-              perf["areaUnderPr"], perf["weightedAreaUnderRoc"])
+    perf = perf_fn(score[valid], is_pos, w, nb, max_score=scale, device=device)
+    if writer:
+        with open(ms.pf.eval_performance(ev), "w") as f:
+            f.write(E.to_json(perf))
+        E.write_gain_chart(ms.pf.eval_gain_chart(ev, "gainchart", "html"),
+                           ms.pf.eval_gain_chart(ev, "gainchart", "csv"), perf, ev.get("name"))
+        _log.info("eval %s: AUC(ROC)=%.6f AUC(PR)=%.6f weighted AUC=%.6f", ev.get("name"), perf["areaUnderRoc"],
+                  perf["areaUnderPr"], perf["weightedAreaUnderRoc"])
     # champion / meta score columns
     for m in score_meta:
         if m in md.table:
             sv = md.table[m].numeric()[valid]
             okm = np.isfinite(sv)
-            p2 = E.performance(sv[okm], is_pos[okm], None if w is None else w[okm], nb,
-                               max_score=float(np.nanmax(sv)) if okm.any() else 1.0, device=device)
-            with open(os.path.join(d, f"{m}.EvalPerformance.json"), "w") as f:
-                f.write(E.to_json(p2))
+            mx = float(np.nanmax(sv[okm])) if okm.any() else -math.inf
+            if collective:
+                mx = dist.all_reduce_max_scalar(mx)
+            p2 = perf_fn(sv[okm], is_pos[okm], None if w is None else w[okm], nb,
+                         max_score=mx if math.isfinite(mx) else 1.0, device=device)
+            if writer:
+                with open(os.path.join(d, f"{m}.EvalPerformance.json"), "w") as f:
+                    f.write(E.to_json(p2))
     return perf
 
 
@@ -611,9 +628,15 @@ def run_eval(root: str = ".", action: str = "run", name: str | None = None, devi
                                  gbt_convert=ev.get("gbtScoreConvertStrategy") or "RAW")
             meta_cols = _meta_names(ms, ev.dataSet, "metaColumnNameFile") if ev.dataSet else []
             score_meta = _meta_names(ms, ev, "scoreMetaColumnNameFile")
+            from ..config import environment
+            coll = dist.info().world_size > 1 and not ms.mc.is_multiclass() and \
+                environment.get_bool("shifu.eval.distPerf", True)
             out = _score_eval_streamed(ms, ev, runner, meta_cols, score_meta,
-                                       float(ev.get("scoreScale", 1000) or 1000), True, nosort)
-            if out is not None and action in ("run", "perf", "confmat"):
+                                       float(ev.get("scoreScale", 1000) or 1000), True, nosort, local_metrics=coll)
+            if coll and action in ("run", "perf", "confmat"):
+                view, res, _, lab, tmp = out          # this rank's rows: exact global metrics, no gather
+                perf_eval(ms, ev, view, res, None, score_meta, device, lab=lab, collective=True)
+            elif out is not None and action in ("run", "perf", "confmat"):
                 view, res, _, lab, tmp = out
                 with dist.local_only():
                     perf_eval(ms, ev, view, res, None, score_meta, device, lab=lab)

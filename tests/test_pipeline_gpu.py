@@ -97,6 +97,7 @@ def test_wdl_hip_gather_matches_torch(wide, deep, monkeypatch):
     dense = torch.randn(n, 5, device="cuda")
     cats = torch.stack([torch.randint(0, s + 1, (n,)) for s in sizes], 1).cuda()
     out = {}
+    monkeypatch.setattr(wdl, "WDL_DEEP_HIP", False)       # fp32 deep tower: the gather is under test
     for hip in (True, False):
         monkeypatch.setattr(wdl, "WDL_HIP", hip)
         net.zero_grad()
@@ -109,6 +110,36 @@ def test_wdl_hip_gather_matches_torch(wide, deep, monkeypatch):
             assert a is None or float(a.abs().max()) == 0.0
         else:
             torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("acts", [["relu"], ["tanh", "sigmoid"], ["swish", "leakyrelu"]])
+def test_wdl_deep_mfma_matches_fp32(acts, monkeypatch):
+    """K20: the deep tower on the hand-written bf16 MFMA GEMMs (gemm_nt EPI_ACT / EPI_DACT +
+    wgrad_tn) against the fp32 torch tower: logits and every parameter gradient within bf16
+    accuracy (relative to each tensor's scale)."""
+    import torch
+    from shifu_amd.models import wdl
+    torch.manual_seed(1)
+    sizes = [3, 500, 7]
+    hidden = [40, 24][: len(acts)]
+    net = wdl.WideDeepNet(5, sizes, [0, 1, 2], 6, hidden, acts).cuda()
+    n = 5000
+    dense = torch.randn(n, 5, device="cuda")
+    cats = torch.stack([torch.randint(0, s + 1, (n,)) for s in sizes], 1).cuda()
+    out = {}
+    for deep_hip in (True, False):
+        monkeypatch.setattr(wdl, "WDL_DEEP_HIP", deep_hip)
+        net.zero_grad()
+        logit = net(dense, cats)
+        ((logit.sigmoid() - 0.3) ** 2).sum().backward()
+        out[deep_hip] = (logit.detach().clone(), [None if p.grad is None else p.grad.clone() for p in net.parameters()])
+    a, b = out[True][0], out[False][0]
+    assert float((a - b).abs().max()) <= 3e-2 * max(1.0, float(b.abs().max()))
+    for ga, gb in zip(out[True][1], out[False][1]):
+        if gb is None:
+            continue
+        scale = max(float(gb.abs().max()), 1e-6)
+        assert float((ga - gb).abs().max()) <= 5e-2 * scale
 
 
 def test_wdl_pipeline_on_gpu(tmp_path):

@@ -33,3 +33,30 @@ def test_radix_sort_desc_matches_stable_argsort(n, kind):
         np.testing.assert_array_equal(x[got], x[want])
         return
     np.testing.assert_array_equal(got, want)
+
+
+def test_device_performance_equals_host():
+    """E.performance on device tensors (radix-sort order, device curves and bucket searches) ==
+    the host run (numpy inputs, CPU torch): same buckets, same rows, same values."""
+    import json
+    from shifu_amd.algos import evaluation as E
+    rng = np.random.default_rng(3)
+    n = 300_000
+    s = np.round(rng.random(n) * 1000.0)                   # integer scores: heavy ties
+    y = (rng.random(n) < 0.25).astype(np.float64)
+    w = rng.random(n) * 2.0
+    host = E.performance(s, y, w, 10, max_score=1000.0, device=torch.device("cpu"))
+    dev = E.performance(torch.from_numpy(s).cuda(), torch.from_numpy(y).cuda(), torch.from_numpy(w).cuda(), 10,
+                        max_score=1000.0)
+    # counts are exact; weighted sums differ only by the device scan's summation order
+    def close(a, b):
+        if isinstance(a, dict):
+            return a.keys() == b.keys() and all(close(a[k], b[k]) for k in a)
+        if isinstance(a, list):
+            return len(a) == len(b) and all(close(x, y) for x, y in zip(a, b))
+        if isinstance(a, float):
+            return (np.isnan(a) and np.isnan(b)) or abs(a - b) <= 1e-12 * max(1.0, abs(a))
+        return a == b
+    assert close(json.loads(json.dumps(host)), json.loads(json.dumps(dev)))
+    o = E.order_desc(s)                                     # host array on a GPU box: device sort
+    assert np.array_equal(o, np.argsort(-s, kind="stable"))
