@@ -606,6 +606,24 @@ def bench_eval(a, dev, info):
         torch.argsort(-score, stable=True)
         sync()
         out["torch_stable_argsort_rows_per_s"] = n / (time.perf_counter() - t1)
+        # NN scoring (the eval's model pass) of the headline 1000-500-200-1 net: fp32 (default,
+        # parity) vs bf16 on the trainer's own MFMA kernels
+        from shifu_amd.formats.nn_format import NNNetwork
+        from shifu_amd.scoring.model_runner import nn_forward
+        rng = np.random.default_rng(0)
+        sizes = [1000, 500, 200, 1]
+        net = NNNetwork(sizes, ["sigmoid", "sigmoid", "sigmoid"],
+                        [rng.normal(size=(sizes[i + 1], sizes[i] + 1)) * 0.05 for i in range(3)])
+        ns = min(n, 4_000_000)
+        X = torch.randn(ns, 1000, generator=g, device=dev, dtype=torch.float32)
+        for prec in ("fp32", "bf16"):
+            nn_forward(net, X[:65536], dev, precision=prec)
+            sync()
+            t1 = time.perf_counter()
+            sc = nn_forward(net, X, dev, precision=prec)
+            sync()
+            out[f"nn_scoring_rows_per_s_{prec}"] = ns / (time.perf_counter() - t1)
+            out[f"nn_scoring_checksum_{prec}"] = float(sc.sum())
     return out
 
 

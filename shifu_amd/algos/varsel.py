@@ -275,7 +275,11 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
                 M = A.shape[0]
                 st = nat.stream_of(A)
                 for l in range(1, len(Ws)):
-                    last = l == len(Ws) - 1
+                    if l == len(Ws) - 1:          # output neuron: fp32 dot over the bf16 rows (a
+                        k = Ws[l].shape[1]        # bf16-rounded output would put a noise floor on d)
+                        z = A[:, :k].float() @ Ws[l][0]
+                        return act_fwd(acts[l], z)
+                    last = False
                     N, act = kin[l], ACT_IDS[acts[l]]
                     key = (l, M)
                     if key not in bufs:

@@ -289,6 +289,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[4][
   if (full) tile_write(std::integral_constant<bool, true>{});
   else tile_write(std::integral_constant<bool, false>{});
   __syncthreads();
+  if (p.dbg & 8) return;                             // lab: no global tile stores
   const int c = tid & 31;
 #pragma unroll 4
   for (int pass = 0; pass < 16; ++pass) {
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = wc * 64 + i * 16 + (lane >> 4) * 4 + r;
-      w3[i][r] = n < h.KH ? h.W[n] : 0.f;
+      w3[i][r] = (p.dbg & 16) ? 0.01f : (n < h.KH ? h.W[n] : 0.f);    // lab 16: no global loads
     }
   float zp[8];
 #pragma unroll
@@ -726,6 +727,7 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
     atomicAdd(h.err, a0);
     atomicAdd(h.err + 1, a1);
   }
+  if (p.dbg & 4) return;                             // lab: stages 1-2 only
   // 3. last-hidden deltas (bf16, staged through LDS) and the output-wgrad partials
   char* Cs = smem;                                   // [256][512 B], 16-B chunk ^ (row & 15)
   float gw[4][4];
@@ -771,6 +773,7 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
     if (h.GWslab) h.GWslab[(size_t)(m0 >> 8) * h.KH + tid] = v;     // tile index = row block
     else atomicAdd(h.GW + tid, v);
   }
+  if (p.dbg & 8) return;                             // lab: no global D stores
   const int c = tid & 31;
 #pragma unroll 4
   for (int pass = 0; pass < 16; ++pass) {

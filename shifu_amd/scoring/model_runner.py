@@ -55,11 +55,58 @@ def _dev(device):
         torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
 
 
+def _nn_forward_bf16(net, Xt, dev, chunk):
+    """bf16 forward on the trainer's hand-written MFMA GEMMs (gemm_kernels.hip shifu_gemm_nt,
+    EPI_ACT: activation + bias column + zero padding in the epilogue), fp32 accumulation."""
+    from ..models.nn import ACT_IDS
+    from ..ops import _native as nat
+    pad = lambda k: ((k + 127) // 128) * 128
+    dims = [net.weights[0].shape[1] - 1] + [W.shape[0] for W in net.weights]
+    kp = [pad(d + 1) for d in dims]
+    Wb = []
+    for l, W in enumerate(net.weights):
+        w = torch.zeros(dims[l + 1], kp[l], dtype=torch.bfloat16, device=dev)
+        w[:, : dims[l] + 1] = torch.as_tensor(np.asarray(W), dtype=torch.float32)
+        Wb.append(w)
+    out = []
+    for r in range(0, Xt.shape[0], chunk):
+        xb = Xt[r: r + chunk].to(dev, torch.float32)
+        m = xb.shape[0]
+        a = torch.zeros(m, kp[0], dtype=torch.bfloat16, device=dev)
+        a[:, : dims[0]] = xb
+        a[:, dims[0]] = 1.0
+        st = nat.stream_of(a)
+        for l in range(len(Wb)):
+            act = ACT_IDS[net.acts[l]]
+            c = torch.empty(m, kp[l + 1], dtype=torch.bfloat16, device=dev)
+            c2 = torch.empty_like(c) if act in (5, 8) else None
+            last = l == len(Wb) - 1
+            nat.call_hip("shifu_gemm_nt", a, kp[l], Wb[l], kp[l], dims[l + 1], c, kp[l + 1], c2, kp[l + 1], None, 0,
+                         None, 0, m, kp[l + 1], kp[l], 0, act, dims[l + 1], 0 if last else 1, 0.0, st)
+            a = c
+        out.append(a[:, : dims[-1]].double().cpu())
+    return torch.cat(out).numpy() if out else np.zeros((0, net.n_out))
+
+
 @torch.no_grad()
-def nn_forward(net: nn_format.NNNetwork, X, device=None, chunk: int = 1 << 18) -> np.ndarray:
-    """Batched fp32 forward of an input-first network on the device -> [N, n_out] float64."""
+def nn_forward(net: nn_format.NNNetwork, X, device=None, chunk: int = 1 << 18, precision: str | None = None) -> np.ndarray:
+    """Batched forward of an input-first network on the device -> [N, n_out] float64.
+
+    fp32 by default (``shifu.eval.nnPrecision=fp32``): torch fp32 GEMMs, scores agree with the
+    reference's float scoring (IndependentNNModel) to ~1e-6 -- eval / posttrain / SE base scores
+    are written as text and compared across runs.  ``bf16``: the trainer's own MFMA kernels
+    (``_nn_forward_bf16``), ~3 significant digits, for throughput-bound scoring."""
     from ..models.nn import act_fwd
     dev = _dev(device)
+    if precision is None:
+        from ..config import environment
+        precision = environment.get("shifu.eval.nnPrecision", "fp32")
+    if precision == "bf16" and dev.type == "cuda":
+        Xt = torch.as_tensor(X)
+        sub = net.input_subset()
+        if sub is not None and Xt.shape[1] != net.n_in:
+            Xt = Xt[:, torch.as_tensor(sub, dtype=torch.long)]
+        return _nn_forward_bf16(net, Xt, dev, chunk)
     Ws = [torch.as_tensor(np.asarray(W), dtype=torch.float32, device=dev) for W in net.weights]
     out = []
     Xt = torch.as_tensor(X)

@@ -221,3 +221,21 @@ def test_bench_configuration_gradient_bitwise_reproducible():
         grads.append(t.grad.clone())
     assert torch.equal(grads[0], grads[1])
     assert float(grads[0].abs().sum()) > 0
+
+
+def test_nn_scoring_bf16_close_to_fp32():
+    """shifu.eval.nnPrecision=bf16: scoring on the trainer's MFMA kernels agrees with the fp32
+    scoring path to bf16 accuracy (incl. an input-subset net and a swish layer)."""
+    import numpy as np
+    import torch
+    from shifu_amd.formats.nn_format import NNNetwork
+    from shifu_amd.scoring.model_runner import nn_forward
+    rng = np.random.default_rng(4)
+    sizes = [70, 40, 12, 2]
+    net = NNNetwork(sizes, ["tanh", "swish", "sigmoid"],
+                    [rng.normal(size=(sizes[i + 1], sizes[i] + 1)) * 0.3 for i in range(3)])
+    X = rng.normal(size=(20000, 70)).astype(np.float32)
+    a = nn_forward(net, X, torch.device("cuda"), precision="fp32")
+    b = nn_forward(net, X, torch.device("cuda"), precision="bf16")
+    assert a.shape == b.shape == (20000, 2)
+    assert np.abs(a - b).max() <= 2e-2

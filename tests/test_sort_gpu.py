@@ -55,7 +55,8 @@ def test_device_performance_equals_host():
         if isinstance(a, list):
             return len(a) == len(b) and all(close(x, y) for x, y in zip(a, b))
         if isinstance(a, float):
-            return (np.isnan(a) and np.isnan(b)) or abs(a - b) <= 1e-12 * max(1.0, abs(a))
+            # fn / tn = totals - prefix: absolute error ~1e-16 of the total weight (3e5 here)
+            return (np.isnan(a) and np.isnan(b)) or abs(a - b) <= 1e-12 * max(1.0, abs(a)) + 1e-9
         return a == b
     assert close(json.loads(json.dumps(host)), json.loads(json.dumps(dev)))
     o = E.order_desc(s)                                     # host array on a GPU box: device sort

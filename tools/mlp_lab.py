@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--tune", nargs="*", default=[],
                     help="GEMM tune settings applied per run, e.g. 10:0 10:1 (key 10: persistent forward)")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0],
-                    help="GEMM lab ablation bits per run (1: no head err atomics, 2: main loops only)")
+                    help="GEMM lab ablation bits per run (1: no head err atomics, 2: main loops only, 4: head "
+                         "stages 1-2 only, 8: no head / 8-phase tile stores, 16: head w_out without loads)")
     a = ap.parse_args()
     for kv in a.env:
         k, v = kv.split("=", 1)
