@@ -156,9 +156,13 @@ def _parse_native(data: bytes, delim: str, kinds: list, missing: list, nthreads:
         return None
     kinds_arr = (ctypes.c_int * len(kinds))(*kinds)
     miss = "\n".join(missing).encode("utf-8")
-    buf = ctypes.create_string_buffer(data, len(data))
-    h = lib.shifu_csv_parse(ctypes.addressof(buf), len(data), delim.encode("utf-8"), len(kinds), kinds_arr,
-                            miss, nthreads)
+    if isinstance(data, bytes):              # immutable: parse it in place (no copy of the block)
+        buf = data
+        addr = ctypes.cast(ctypes.c_char_p(data), ctypes.c_void_p).value
+    else:
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        addr = ctypes.addressof(buf)
+    h = lib.shifu_csv_parse(addr, len(data), delim.encode("utf-8"), len(kinds), kinds_arr, miss, nthreads)
     if not h:
         return None
     try:

@@ -32,6 +32,12 @@ struct Parser {
   int ncols = 0;
   std::vector<int> kinds;                  // 0 skip, 1 numeric, 2 string
   std::unordered_set<std::string> missing; // tokens treated as missing (trimmed)
+  std::vector<std::string> miss_list;      // the same, scanned by length + memcmp (no per-field hash)
+  bool is_missing(std::string_view v) const {
+    for (const auto& t : miss_list)
+      if (t.size() == v.size() && (v.empty() || memcmp(t.data(), v.data(), v.size()) == 0)) return true;
+    return false;
+  }
   int nthreads = 1;
   // results
   size_t nrows = 0;
@@ -49,9 +55,47 @@ inline std::string_view trim(std::string_view s) {
   return s.substr(a, b - a);
 }
 
+// Clinger's fast path: [+-]digits[.digits] with <= 19 significant digits whose integer value is
+// < 2^53 and <= 22 fraction digits is m / 10^k with both operands exact doubles, so ONE IEEE
+// division gives the correctly rounded value -- bit-identical to strtod -- without strtod's
+// locale / generic machinery (the common shape of the numeric text: "%.5f"-like fields).
+// Anything else (exponents, more digits, inf/nan words, Java "1.0d") takes the strtod path.
+static const double kPow10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+inline bool parse_decimal_fast(std::string_view s, double& out) {
+  size_t i = 0;
+  const size_t n = s.size();
+  bool neg = false;
+  if (i < n && (s[i] == '-' || s[i] == '+')) { neg = s[i] == '-'; ++i; }
+  uint64_t m = 0;
+  int nd = 0, frac = 0;
+  bool any = false, dot = false;
+  for (; i < n; ++i) {
+    const char c = s[i];
+    if (c >= '0' && c <= '9') {
+      any = true;
+      if (m == 0 && c == '0') { if (dot) ++frac; continue; }     // leading zeros
+      if (++nd > 19) return false;
+      m = m * 10 + (uint64_t)(c - '0');
+      if (dot) ++frac;
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      return false;
+    }
+  }
+  if (!any || m >= (1ull << 53) || frac > 22) return false;
+  const double v = frac ? (double)m / kPow10[frac] : (double)m;
+  out = neg ? -v : v;
+  return true;
+}
+
 inline double parse_double(std::string_view s, bool& ok) {
   ok = false;
   if (s.empty()) return NAN;
+  double fast;
+  if (parse_decimal_fast(s, fast)) { ok = true; return fast; }
   char tmp[64];
   if (s.size() >= sizeof(tmp)) return NAN;
   memcpy(tmp, s.data(), s.size());
@@ -76,8 +120,8 @@ struct Chunk {
 void split_lines(const Parser& P, Chunk& c) {
   size_t i = c.begin;
   while (i < c.end) {
-    size_t j = i;
-    while (j < c.end && P.buf[j] != '\n') ++j;
+    const char* nl = (const char*)memchr(P.buf + i, '\n', c.end - i);
+    const size_t j = nl ? (size_t)(nl - P.buf) : c.end;
     // skip blank lines
     size_t k = i;
     while (k < j && (P.buf[k] == ' ' || P.buf[k] == '\r' || P.buf[k] == '\t')) ++k;
@@ -86,67 +130,114 @@ void split_lines(const Parser& P, Chunk& c) {
   }
 }
 
-void parse_chunk(Parser& P, Chunk& c, std::atomic<int64_t>& bad) {
-  const size_t nstr = P.str_idx.size();
-  c.local_dict.assign(P.ncols, {});
-  c.local_list.assign(P.ncols, {});
+// One line: fields are tokenised and numeric fields converted in the same left-to-right pass.  A
+// numeric field of the common shape ([+-]digits[.digits], <= 19 significant digits, < 2^53,
+// <= 22 fraction digits) is accumulated while it is scanned and finished with one division
+// (Clinger's fast path, == strtod); an empty field is missing; anything else (spaces, missing
+// tokens, exponents, Java "1.0d", strings) is re-scanned to its delimiter and takes the general
+// path (trim, missing tokens, strtod / dictionary).
+void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<int64_t>& bad) {
+  const char d0 = P.delim[0];
   const size_t dl = P.delim.size();
-  for (size_t li = 0; li < c.line_starts.size(); ++li) {
-    const size_t r = c.row_offset + li;
-    size_t s = c.line_starts[li];
-    size_t e = s;
-    while (e < c.end && P.buf[e] != '\n') ++e;
-    int col = 0;
-    size_t fs = s;
-    auto emit = [&](size_t a, size_t b) {
-      if (col < P.ncols) {
-        const int k = P.kinds[col];
-        if (k != 0) {
-          std::string_view v = trim(std::string_view(P.buf + a, b - a));
-          const bool miss = P.missing.count(std::string(v)) > 0;
-          if (k == 1) {
-            bool ok = false;
-            double d = miss ? NAN : parse_double(v, ok);
-            P.num[P.num_idx[col]][r] = d;
-          } else {
-            int32_t code = -1;
-            if (!miss) {
-              auto& m = c.local_dict[col];
-              std::string key(v);
-              auto it = m.find(key);
-              if (it == m.end()) {
-                code = (int32_t)c.local_list[col].size();
-                m.emplace(key, code);
-                c.local_list[col].push_back(std::move(key));
-              } else {
-                code = it->second;
-              }
-            }
-            P.codes[P.str_idx[col]][r] = code;   // local code, remapped after merge
-          }
+  const char* buf = P.buf;
+  int col = 0;
+  size_t p = s;
+  auto field_end = [&](size_t a) -> size_t {     // first delimiter at or after a (or e)
+    if (dl == 1) {
+      const void* q = memchr(buf + a, d0, e - a);
+      return q ? (size_t)((const char*)q - buf) : e;
+    }
+    for (size_t i = a; i + dl <= e; ++i)
+      if (buf[i] == d0 && memcmp(buf + i, P.delim.data(), dl) == 0) return i;
+    return e;
+  };
+  auto general = [&](size_t a, size_t b) {
+    const int k = P.kinds[col];
+    std::string_view v = trim(std::string_view(buf + a, b - a));
+    const bool miss = P.is_missing(v);
+    if (k == 1) {
+      bool ok = false;
+      P.num[P.num_idx[col]][r] = miss ? NAN : parse_double(v, ok);
+    } else {
+      int32_t code = -1;
+      if (!miss) {
+        auto& m = c.local_dict[col];
+        std::string key(v);
+        auto it = m.find(key);
+        if (it == m.end()) {
+          code = (int32_t)c.local_list[col].size();
+          m.emplace(key, code);
+          c.local_list[col].push_back(std::move(key));
+        } else {
+          code = it->second;
         }
       }
-      ++col;
-    };
-    for (size_t i = s; i + dl <= e;) {
-      if (P.buf[i] == P.delim[0] && (dl == 1 || memcmp(P.buf + i, P.delim.data(), dl) == 0)) {
-        emit(fs, i);
-        i += dl;
-        fs = i;
-      } else {
-        ++i;
-      }
+      P.codes[P.str_idx[col]][r] = code;   // local code, remapped after merge
     }
-    emit(fs, e);
-    if (col != P.ncols) {
-      bad.fetch_add(1);
-      for (int cc = col; cc < P.ncols; ++cc) {   // short row: rest missing
-        if (P.kinds[cc] == 1) P.num[P.num_idx[cc]][r] = NAN;
-        else if (P.kinds[cc] == 2) P.codes[P.str_idx[cc]][r] = -1;
+  };
+  while (true) {
+    const int k = col < P.ncols ? P.kinds[col] : 0;
+    size_t b;                                      // field end
+    if (k == 1 && dl == 1) {
+      size_t i = p;
+      bool neg = false;
+      if (i < e && (buf[i] == '-' || buf[i] == '+')) { neg = buf[i] == '-'; ++i; }
+      uint64_t m = 0;
+      int nd = 0, frac = 0;
+      bool any = false, dot = false, fast = true;
+      for (; i < e; ++i) {
+        const char ch = buf[i];
+        const unsigned dgt = (unsigned)(ch - '0');
+        if (dgt < 10) {
+          any = true;
+          if (m == 0 && dgt == 0) { frac += dot; continue; }
+          if (++nd > 19) { fast = false; break; }
+          m = m * 10 + dgt;
+          frac += dot;
+        } else if (ch == '.' && !dot) {
+          dot = true;
+        } else {
+          if (ch != d0) fast = false;
+          break;
+        }
       }
+      if (fast && i == p) {                        // empty field: missing (token or not)
+        b = i;
+        P.num[P.num_idx[col]][r] = NAN;
+      } else if (fast && any && m < (1ull << 53) && frac <= 22) {
+        b = i;
+        const double v = frac ? (double)m / kPow10[frac] : (double)m;
+        P.num[P.num_idx[col]][r] = neg ? -v : v;
+      } else {
+        b = field_end(p);
+        general(p, b);
+      }
+    } else {
+      b = field_end(p);
+      if (k != 0) general(p, b);
+    }
+    ++col;
+    if (b >= e) break;
+    p = b + dl;
+  }
+  if (col != P.ncols) {
+    bad.fetch_add(1);
+    for (int cc = col; cc < P.ncols; ++cc) {   // short row: rest missing
+      if (P.kinds[cc] == 1) P.num[P.num_idx[cc]][r] = NAN;
+      else if (P.kinds[cc] == 2) P.codes[P.str_idx[cc]][r] = -1;
     }
   }
-  (void)nstr;
+}
+
+void parse_chunk(Parser& P, Chunk& c, std::atomic<int64_t>& bad) {
+  c.local_dict.assign(P.ncols, {});
+  c.local_list.assign(P.ncols, {});
+  for (size_t li = 0; li < c.line_starts.size(); ++li) {
+    const size_t s = c.line_starts[li];
+    const size_t e = li + 1 < c.line_starts.size() ? c.line_starts[li + 1] - 1 : c.end;
+    const char* nl = (const char*)memchr(P.buf + s, '\n', e - s);   // blank lines were skipped
+    parse_line(P, c, s, nl ? (size_t)(nl - P.buf) : e, c.row_offset + li, bad);
+  }
 }
 
 }  // namespace
@@ -172,6 +263,7 @@ SHIFU_RT_API void* shifu_csv_parse(const char* buf, long len, const char* delim,
       a = b + 1;
     }
   }
+  P->miss_list.assign(P->missing.begin(), P->missing.end());
   P->nthreads = std::max(1, nthreads);
   for (int c = 0; c < ncols; ++c) {
     P->num_idx.push_back(-1);
