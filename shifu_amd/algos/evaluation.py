@@ -54,15 +54,18 @@ def _po(i, cm, bin_num=0, score_count=0.0, score_wcount=0.0, first=False):
 
 def _bucket_indices(metric, nb: int, start: int = 1) -> list:
     """Rows (>= start) where the k-th bucket is emitted: first row after the previous emission
-    whose (monotone) metric >= k/nb.  ``metric``: numpy array or (device) tensor; one running max
-    and one binary search per bucket."""
+    whose metric >= k/nb.  ``metric``: numpy array or (device) tensor.  The first row whose
+    running max reaches k/nb is the first row whose value does (NaN never does), so each bucket
+    is one compare + first-true argmax -- no running-max scan of the whole curve."""
     m = torch.as_tensor(metric)
-    m = torch.where(torch.isnan(m), torch.full_like(m, -math.inf), m).cummax(0).values
     out, prev, k = [], start - 1, 1
     cap = 1.0 / nb
     n = m.numel()
     while True:
-        j = int(torch.searchsorted(m, torch.tensor([k * cap], dtype=m.dtype, device=m.device)).item())
+        hit = m >= k * cap
+        j = int(torch.argmax(hit.to(torch.uint8)).item()) if n else 0
+        if n == 0 or not bool(hit[j]):
+            j = n
         j = max(j, prev + 1)
         if j >= n:
             break

@@ -44,18 +44,46 @@ def _history_append(ms, changes, reason):
             f.write(f"{c.num},{c.name},{str(old).lower()},{str(new).lower()},{reason}\n")
 
 
-def _train_quick_nn(ms, cols, epochs, device=None, seed=0):
-    """Train the NN used for sensitivity analysis on the candidate columns; returns (net, X)."""
+def _normalized_rows(ms, cols):
+    """This rank's (X fp32 [n, len(cols)], y, w) from the norm step's NormalizedData when it holds
+    exactly the candidate columns (the usual init -> stats -> norm -> varsel order); None otherwise.
+    The reference's SE job reads the normalized training data too (VarSelectMapper); reading it
+    here avoids a second parse + normalisation of the raw text."""
+    from .base import load_dataset_cache
+    from .train import _shard
+    cache = load_dataset_cache(ms.pf.normalized_data)
+    if cache is None:
+        return None
+    meta, arr = cache
+    if meta.get("input_nums") != [c.num for c in cols] or "X" not in arr or "y" not in arr:
+        return None
+    info = dist.info()
+    X = np.asarray(_shard(arr["X"], info), dtype=np.float32)
+    y = np.asarray(_shard(arr["y"], info), dtype=np.float32).reshape(len(X), -1)[:, :1]
+    w = np.asarray(_shard(arr["w"], info), dtype=np.float32) if "w" in arr else np.ones(len(X), np.float32)
+    _log.info("varsel: sensitivity rows from NormalizedData (%d x %d)", X.shape[0], X.shape[1])
+    return X, y, w
+
+
+def _train_quick_nn(ms, cols, epochs, device=None, seed=0, rows=None):
+    """Train the NN used for sensitivity analysis on the candidate columns; returns (net, X, md).
+    ``rows``: (X, y, w) already normalized (``_normalized_rows``); else the raw data is loaded
+    and normalized here."""
     mc = ms.mc
-    md = shard_model_data(ms.load_raw(cols))     # data parallel: each rank its row range
-    X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+    md = None
+    if rows is not None:
+        X, y, w = rows
+    else:
+        md = shard_model_data(ms.load_raw(cols))     # data parallel: each rank its row range
+        X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+        y, w = md.y.reshape(-1, 1), md.w.astype(np.float32)
     p = mc.train.get("params") or {}
     hidden = [int(h) for h in (p.get("NumHiddenNodes") or [50])][: int(p.get("NumHiddenLayers", 1) or 1)]
     spec = MLPSpec(X.shape[1], hidden, list(p.get("ActivationFunc") or ["tanh"]), 1, "sigmoid")
     from ..utils.device import default_device
     dev = torch.device(device) if device is not None else default_device()
     tr = MLPTrainer(spec, dev, str(p.get("Propagation", "R")), float(p.get("LearningRate", 0.1)), seed=seed)
-    data = tr.prepare(torch.from_numpy(X), md.y.reshape(-1, 1), md.w.astype(np.float32))
+    data = tr.prepare(torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)), y, w)
     for _ in range(max(1, epochs)):
         tr.step(data)
     ws = tr.params.views()
@@ -92,11 +120,15 @@ def select_by_sensitivity(ms, by="SE", device=None, seed=0):
         return []
     epochs = max(1, int(mc.train.get("numTrainEpochs", 100)) // 2)
     net = _reusable_se_model(ms, cols)
+    rows = _normalized_rows(ms, cols)
     if net is not None:
-        md = shard_model_data(ms.load_raw(cols))
-        X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
+        if rows is not None:
+            X = rows[0]
+        else:
+            md = shard_model_data(ms.load_raw(cols))
+            X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
     else:
-        net, X, md = _train_quick_nn(ms, cols, epochs, device, seed)
+        net, X, md = _train_quick_nn(ms, cols, epochs, device, seed, rows=rows)
     mean, rms, var = V.sensitivity(net, X, device=device)
     filter_num = int(mc.varSelect.get("filterNum", 200) or 0)
     keep = filter_num if filter_num > 0 else int(len(cols) * (1 - float(mc.varSelect.get("filterOutRatio", 0.05))))
