@@ -140,18 +140,78 @@ def rank_row_offset(plan: DatasetPlan, rank: int, world: int) -> int:
     return int(sum(counts[:rank]))
 
 
+class _Raised:
+    def __init__(self, exc):
+        self.exc = exc
+
+
+def prefetched(gen_fn, depth: int = 2):
+    """Run the generator ``gen_fn()`` on a background thread, ``depth`` items ahead of the
+    consumer: the next chunk's file read + native parse (both release the GIL) overlap the
+    consumer's uploads and kernels on the current one.  Exceptions re-raise in the consumer;
+    closing the consumer stops the producer."""
+    import queue
+    import threading
+    if depth <= 0:
+        yield from gen_fn()
+        return
+    q = queue.Queue(maxsize=depth)
+    stop = threading.Event()
+    end = object()
+
+    def put(item):
+        while not stop.is_set():
+            try:
+                q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def run():
+        try:
+            for item in gen_fn():
+                if not put(item):
+                    return
+            put(end)
+        except BaseException as e:          # noqa: BLE001 - handed to the consumer
+            put(_Raised(e))
+    t = threading.Thread(target=run, name="shifu-prefetch", daemon=True)
+    t.start()
+    try:
+        while True:
+            item = q.get()
+            if item is end:
+                break
+            if isinstance(item, _Raised):
+                raise item.exc
+            yield item
+    finally:
+        stop.set()
+        while t.is_alive():
+            try:
+                q.get_nowait()
+            except queue.Empty:
+                t.join(0.05)
+
+
 def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
                     sample_rate: float = 1.0, sample_neg_only: bool = False, seed: int = 0,
                     require_target: bool = True, row0: int = 0):
     """Yield purified :class:`ModelData` chunks of this rank's byte range; ``row0`` = the global
-    raw-row index of the rank's first row (sampling draws are per global row)."""
-    r = row0
-    for _, table in iter_tables(plan, chunk_bytes, rank, world):
-        n = table.n
-        md = finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, r)
-        r += n
-        if md.n:
-            yield md
+    raw-row index of the rank's first row (sampling draws are per global row).  Chunks are
+    produced ``shifu.data.prefetch`` (default 1) ahead on a background thread."""
+    from ..config import environment
+
+    def produce():
+        r = row0
+        for _, table in iter_tables(plan, chunk_bytes, rank, world):
+            n = table.n
+            md = finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, r)
+            r += n
+            if md.n:
+                yield md
+    yield from prefetched(produce, int(environment.get("shifu.data.prefetch", 1)))
 
 
 def load_rank_dataset(mc, data_conf, columns_num=None, columns_str=None, sample_rate=1.0, sample_neg_only=False,

@@ -378,7 +378,7 @@ def _rank_norm_rss(rank, world, port, root, out):
 
 def test_norm_per_rank_host_memory(tmp_path):
     """Data-parallel norm parses only each rank's byte range: per-rank peak host memory growth is
-    about 1/R of the single-process growth plus a fixed ~65 MB of buffers (2 ranks: < 0.72x)."""
+    about 1/R of the single-process growth plus a fixed ~65 MB of buffers (2 ranks: < 0.5x + 80 MB)."""
     from shifu_amd.config.model_config import ModelConfig
     from shifu_amd.steps.create import run_init
     from shifu_amd.steps.stats import run_stats
@@ -393,7 +393,7 @@ def test_norm_per_rank_host_memory(tmp_path):
     single = int(open(out + "1.0").read())
     ranks = [int(open(f"{out}2.{r}").read()) for r in range(2)]
     print("norm rss growth MB: 1 rank %.1f, 2 ranks %s" % (single / 1e6, [round(r / 1e6, 1) for r in ranks]))
-    assert max(ranks) < 0.72 * single, (single, ranks)
+    assert max(ranks) < 0.5 * single + 80e6, (single, ranks)
 
 
 def _rank_stats_one_empty(rank, world, port, root):
