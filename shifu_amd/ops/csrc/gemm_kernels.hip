@@ -288,28 +288,17 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[4][
   const bool full = EPI == EPI_DACT || n0 + 256 <= (EPI == EPI_ACT ? p.n_valid : p.NB);
   if (full) tile_write(std::integral_constant<bool, true>{});
   else tile_write(std::integral_constant<bool, false>{});
-  const int c = tid & 31;
-  // dgrad: this thread's 16 H row segments are loaded now -- the accumulators are dead, so the
-  // 64 VGPRs are free -- and their HBM latency overlaps the staging barrier instead of being
-  // exposed pass by pass in the store loop
-  uint4 hpre[EPI == EPI_DACT ? 16 : 1];
-  if constexpr (EPI == EPI_DACT) {
-#pragma unroll
-    for (int pass = 0; pass < 16; ++pass) {
-      const int m = min(m0 + pass * 16 + (tid >> 5), p.M - 1), n = min(n0 + c * 8, p.N - 8);
-      hpre[pass] = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
-    }
-  }
   __syncthreads();
   if (p.dbg & 8) return;                             // lab: no global tile stores
-#pragma unroll
+  const int c = tid & 31;
+#pragma unroll 4
   for (int pass = 0; pass < 16; ++pass) {
     const int ml = pass * 16 + (tid >> 5);
     const int m = m0 + ml, n = n0 + c * 8;
     if (m >= p.M || n >= p.N) continue;
     uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
     if constexpr (EPI == EPI_DACT) {
-      const uint4 hh = hpre[pass];
+      const uint4 hh = *(const uint4*)(p.H + (size_t)m * p.ldh + n);
       const uint32_t hv[4] = {hh.x, hh.y, hh.z, hh.w};
       uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
