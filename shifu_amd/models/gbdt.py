@@ -69,6 +69,16 @@ def _strategy_count(strategy, n_feat: int, input_num: int, tree_num: int) -> int
     return n_feat
 
 
+def _h2d(a, dev):
+    """Host array -> device tensor through pinned memory with a non-blocking copy: a pageable
+    ``.to(device)`` waits for every kernel queued on the stream, so the per-level bookkeeping
+    arrays of the tree builder would drain the GPU pipeline a dozen times per level."""
+    t = torch.as_tensor(np.ascontiguousarray(a))
+    if torch.device(dev).type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 @dataclass
 class TreeConfig:
     algorithm: str = "GBT"              # GBT | RF
@@ -274,8 +284,8 @@ class TreeTrainer:
         self.trees: list[Tree] = []
         self.pred = torch.zeros(data.n, dtype=torch.float32, device=self.dev)
         self.vpred = None if valid is None else torch.zeros(valid.n, dtype=torch.float32, device=valid.device)
-        self.nbins_t = torch.from_numpy(data.nbins.astype(np.int32)).to(self.dev)
-        self.is_cat_t = torch.from_numpy(data.is_cat.astype(np.uint8)).to(self.dev)
+        self.nbins_t = _h2d(data.nbins.astype(np.int32), self.dev)
+        self.is_cat_t = _h2d(data.is_cat.astype(np.uint8), self.dev)
         self.rng = np.random.default_rng(cfg.seed)
         self.tgen = torch.Generator(device=self.dev).manual_seed(cfg.seed + 17 * dist.info().rank)
         self.n_sub = _strategy_count(cfg.feature_subset_strategy, self.F, self.F, cfg.tree_num)
@@ -336,7 +346,7 @@ class TreeTrainer:
         rngs = getattr(self, "_level_rngs", None) or [self.rng] * n_nodes
         for i in range(n_nodes):
             m[i, rngs[i].choice(self.F, self.n_sub, replace=False)] = 1
-        return torch.from_numpy(m).to(self.dev)
+        return _h2d(m, self.dev)
 
     # ------------------------------------------------------------------------------------
     def grow_tree(self, g: torch.Tensor, w: torch.Tensor, weight: float, tid: int | None = None) -> Tree:
@@ -479,7 +489,7 @@ class TreeTrainer:
                     if split_feat[z["slot"]] >= 0:
                         nv[1, z["slot"]] = tree0.value[2 * z["id"]]
                         nv[2, z["slot"]] = tree0.value[2 * z["id"] + 1]
-                leaf_vals = torch.from_numpy(nv).to(self.dev)
+                leaf_vals = _h2d(nv, self.dev)
             if last or not children:
                 if fuse is not None:     # every remaining row gets its final leaf (child) value
                     self._leaf_update(nodes, split_feat, split_bin, cat_left, pos2row, pos_node, leaf_vals, fuse)
@@ -599,13 +609,13 @@ class TreeTrainer:
         F, nn = self.F, len(nodes)
         st = nat.stream_of(d.y)
         items, ni, max_items = self._make_items(nodes, n_built)
-        ni_t = torch.from_numpy(ni).to(self.dev)
+        ni_t = _h2d(ni, self.dev)
         feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
         cand = torch.zeros(nn, F, 8, dtype=torch.float32, device=self.dev)
         cat_order = torch.zeros(nn, F, NB, dtype=torch.uint8, device=self.dev) if d.is_cat.any() else None
         t0 = time.perf_counter()
         if len(items):
-            it = torch.from_numpy(items).to(self.dev)
+            it = _h2d(items, self.dev)
             ls = self.level_stats
             if ls is not None:          # per-level histogram roofline (bench --gbdt-levels)
                 ev0 = torch.cuda.Event(enable_timing=True)
@@ -626,7 +636,7 @@ class TreeTrainer:
                 ls.append({"level": self._level, "nodes_built": int(n_built), "rows": rows, "ev": (ev0, ev1)})
         else:
             slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
-        built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
+        built = _h2d(np.asarray([z["slot"] for z in nodes if z["built"]], np.int32), self.dev)
         derived = [z for z in nodes if not z["built"]]
         if n_built:
             nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, None, None, None,
@@ -645,14 +655,14 @@ class TreeTrainer:
                          self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), mptr, cand.data_ptr(), cptr, F, 2, imp,
                          1, min_inst, min_gain, 1.0 / self.scale_w, 1.0 / self.scale_g, st)
         if derived:
-            dl = torch.tensor([z["slot"] for z in derived], dtype=torch.int32, device=self.dev)
+            dl = _h2d(np.asarray([z["slot"] for z in derived], np.int32), self.dev)
             par = np.zeros(nn, np.int32)
             sib = np.zeros(nn, np.int32)
             for z in derived:
                 par[z["slot"]] = z["parent"]
                 sib[z["slot"]] = z["sib_slot"]
-            par_t = torch.from_numpy(par).to(self.dev)
-            sib_t = torch.from_numpy(sib).to(self.dev)
+            par_t = _h2d(par, self.dev)
+            sib_t = _h2d(sib, self.dev)
             nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, hist_prev.data_ptr(),
                          par_t.data_ptr(), sib_t.data_ptr(), hist.data_ptr(), dl.data_ptr(), len(derived),
                          feat_list.data_ptr(), F, self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), mptr,
@@ -712,7 +722,7 @@ class TreeTrainer:
             # line it fetches (gbdt_kernels.hip gbdt_root_quad_kernel)
             first = np.nonzero(items[:, 3] % 4 == 0)[0]
             q = np.stack([first, items[first, 1], items[first, 2], items[first, 3] // 4], 1).astype(np.int32)
-            qt = torch.from_numpy(np.ascontiguousarray(q)).to(self.dev)
+            qt = _h2d(np.ascontiguousarray(q), self.dev)
             nat.call_hip("shifu_gbdt_hist_root_quad", d.kbins, d.group_stride, w, g, qt, len(q), slab,
                          self.ngroups, self.scale_g, st)
         else:
@@ -732,13 +742,13 @@ class TreeTrainer:
             st = nat.stream_of(d.y)
             items, ni, max_items = self._make_items(nodes, n_built)
             if n_built and len(items):
-                ni_t = torch.from_numpy(ni).to(self.dev)
-                it = torch.from_numpy(items).to(self.dev)
+                ni_t = _h2d(ni, self.dev)
+                it = _h2d(items, self.dev)
                 slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
                 p2r = None if self._root_level else pos2row
                 nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, QF, p2r, w, gc, 0, it, len(items), slab, F,
                              self.scale_w, self.scale_g, self._nmod, 0, st)
-                built = torch.tensor([z["slot"] for z in nodes if z["built"]], dtype=torch.int32, device=self.dev)
+                built = _h2d(np.asarray([z["slot"] for z in nodes if z["built"]], np.int32), self.dev)
                 feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
                 cand = torch.zeros(len(nodes), F, 8, dtype=torch.float32, device=self.dev)
                 nat.call_hip("shifu_gbdt_split", slab.data_ptr(), ni_t.data_ptr(), max_items, None, None, None,
@@ -793,7 +803,7 @@ class TreeTrainer:
             key = torch.where(den != 0, H[..., 1] / torch.where(den != 0, den, torch.ones_like(den)),
                               torch.zeros_like(den))
             key = torch.where(inb[None], key, torch.full_like(key, float("inf")))
-            iscat = torch.from_numpy(d.is_cat.astype(bool)).to(self.dev)
+            iscat = _h2d(d.is_cat.astype(bool), self.dev)
             key = torch.where(iscat[None, :, None], key, binr.double()[None, None, :].expand_as(key))
             order = torch.argsort(key, dim=2, stable=True)                                # [nn, F, NB]
             H = torch.gather(H, 2, order[..., None].expand(-1, -1, -1, C))
@@ -906,9 +916,9 @@ class TreeTrainer:
         the child its bin goes to), in the partition-flag kernel without a flag output."""
         from ..ops import _native as nat
         d = self.data
-        sf = torch.from_numpy(split_feat).to(self.dev)
-        sb = torch.from_numpy(split_bin).to(self.dev)
-        cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
+        sf = _h2d(split_feat, self.dev)
+        sb = _h2d(split_bin, self.dev)
+        cl = _h2d(cat_left.view(np.int32), self.dev)
         pred, scale = fuse
         self._leaf_done = True
         rb = self._root_bins()
@@ -926,9 +936,9 @@ class TreeTrainer:
         if self.gpu:
             from ..ops import _native as nat
             st = nat.stream_of(d.y)
-            sf = torch.from_numpy(split_feat).to(self.dev)
-            sb = torch.from_numpy(split_bin).to(self.dev)
-            cl = torch.from_numpy(cat_left.view(np.int32)).to(self.dev)
+            sf = _h2d(split_feat, self.dev)
+            sb = _h2d(split_bin, self.dev)
+            cl = _h2d(cat_left.view(np.int32), self.dev)
             # left bits, one 64-bit word per 64 positions + the words' popcounts (exclusive-scanned):
             # the inclusive left count at p is wpre[p / 64] + popcount of the word's bits <= p
             nw = (n + 63) // 64
@@ -942,7 +952,7 @@ class TreeTrainer:
                          float(scale), 0, st)
             wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
             # per-node: #left = cum[end-1] - cum[start-1]
-            idx = torch.from_numpy(np.concatenate([np.maximum(ends - 1, 0), np.maximum(starts - 1, 0)])).to(self.dev)
+            idx = _h2d(np.concatenate([np.maximum(ends - 1, 0), np.maximum(starts - 1, 0)]), self.dev)
             cum2 = torch.empty(2 * nn, dtype=torch.int32, device=self.dev)
             nat.call_hip("shifu_gbdt_bitrank", fbits, wpre, idx, 2 * nn, cum2, st)
             cecb = cum2.view(2, nn).cpu().numpy().astype(np.int64)   # one D2H sync
@@ -960,7 +970,7 @@ class TreeTrainer:
                 ranges[s_] = (int(starts[s_]), int(starts[s_] + nleft[s_]), int(ends[s_]))
             new_p2r = torch.empty_like(pos2row)
             new_pn = torch.empty_like(pos_node)
-            t = lambda a, dt=np.int32: torch.from_numpy(np.ascontiguousarray(a.astype(dt))).to(self.dev)  # noqa
+            t = lambda a, dt=np.int32: _h2d(np.ascontiguousarray(a.astype(dt)), self.dev)  # noqa
             # tensors (not .data_ptr() of temporaries) so every buffer outlives the launch
             wg = self._wg_pos
             nw_, ng_ = (torch.empty_like(wg[0]), torch.empty_like(wg[1])) if wg is not None else (None, None)
