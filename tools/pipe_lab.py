@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--cols", type=int, default=1600)
     ap.add_argument("--steps", nargs="*", default=["stats", "norm"])
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--stream", action="store_true", help="force the streamed stats / norm paths")
     a = ap.parse_args()
     from shifu_amd.config import environment
     from shifu_amd.config.model_config import ModelConfig
@@ -30,6 +31,9 @@ def main():
     from shifu_amd.steps import api
     from shifu_amd.steps.create import create_model_set
     environment.props()["shifu.norm.dtype"] = "bf16"
+    if a.stream:
+        environment.props()["shifu.stats.streaming"] = "true"
+        environment.props()["shifu.norm.streaming"] = "true"
     work = os.path.join(tempfile.gettempdir(), "shifu_pipe_lab")
     shutil.rmtree(work, ignore_errors=True)
     os.makedirs(work)
