@@ -236,24 +236,56 @@ def _merge_moments(m, r):
 def _track_distinct(bt, vals, num_thr):
     """Exact value sets while the data set is small enough for the in-memory rule
     (<= stats.EXACT_DISTINCT_ROWS rows) and the set itself stays <= DISTINCT_SET_CAP values (so the
-    sets never outgrow a few chunks); a column that overflows falls back to the K4 estimate."""
+    sets never outgrow a few chunks); a column that overflows falls back to the K4 estimate.
+    GPU: batched over the batch's columns -- the current sets ([C, K] sorted, +inf padded) and the chunk
+    ([C, n], non-finite -> +inf) are sorted together per row, duplicates become +inf and a second
+    sort compacts the new sets -- two sorts per chunk and batch instead of a unique per column."""
     bt.rows_seen += vals.shape[1]
+    C = vals.shape[0]
     if bt.rows_seen > S.EXACT_DISTINCT_ROWS:
         bt.distinct_sets = [None] * len(bt.cols)
         bt.overflow = [True] * len(bt.cols)
+        bt._dset = None
         return
-    for k in range(vals.shape[0]):
-        if bt.overflow[k]:
-            continue
-        v = vals[k]
-        v = torch.where(v > num_thr, torch.full_like(v, float("nan")), v) + 0.0
-        u = torch.unique(v[torch.isfinite(v)])
-        cur = bt.distinct_sets[k]
-        u = u if cur is None else torch.unique(torch.cat([cur, u]))
-        if u.numel() > DISTINCT_SET_CAP:
+    if all(bt.overflow):
+        return
+    if vals.device.type != "cuda":                 # host: per-column sets (no padded [C, K] copies)
+        for k in range(C):
+            if bt.overflow[k]:
+                continue
+            v = vals[k]
+            v = torch.where(v > num_thr, torch.full_like(v, float("nan")), v) + 0.0
+            u = torch.unique(v[torch.isfinite(v)])
+            cur = bt.distinct_sets[k]
+            u = u if cur is None else torch.unique(torch.cat([cur, u]))
+            if u.numel() > DISTINCT_SET_CAP:
+                bt.overflow[k] = True
+                u = None
+            bt.distinct_sets[k] = u
+        return
+    inf = float("inf")
+    v = torch.where(vals > num_thr, torch.full_like(vals, float("nan")), vals) + 0.0
+    v = torch.where(torch.isfinite(v), v, torch.full_like(v, inf))
+    ovf = torch.tensor(bt.overflow, dtype=torch.bool, device=v.device)
+    v = torch.where(ovf[:, None], torch.full_like(v, inf), v)
+    cur = getattr(bt, "_dset", None)
+    comb = v if cur is None else torch.cat([cur, v], 1)
+    srt, _ = torch.sort(comb, dim=1)
+    dup = torch.zeros_like(srt, dtype=torch.bool)
+    dup[:, 1:] = srt[:, 1:] == srt[:, :-1]
+    srt = torch.where(dup, torch.full_like(srt, inf), srt)
+    srt, _ = torch.sort(srt, dim=1)
+    cnt = torch.isfinite(srt).sum(1)
+    new_ovf = (cnt > DISTINCT_SET_CAP).cpu().numpy()
+    cnt_h = cnt.cpu().numpy()
+    for k in range(C):
+        if new_ovf[k]:
             bt.overflow[k] = True
-            u = None
-        bt.distinct_sets[k] = u
+    keep = [int(cnt_h[k]) for k in range(C) if not bt.overflow[k]]
+    width = max(keep) if keep else 0
+    bt._dset = srt[:, :max(width, 1)].contiguous()
+    bt._dcnt = cnt_h
+    bt.distinct_sets = [None if bt.overflow[k] else bt._dset[k, : int(cnt_h[k])] for k in range(C)]
 
 
 def _finish_batch(bt, binary, total, reduce, gather_objects, dev, n_bins):
