@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--env", nargs="*", default=[])
     ap.add_argument("--tune", nargs="*", default=[],
                     help="GEMM tune settings applied per run, e.g. 10:0 10:1 (key 10: persistent forward)")
+    ap.add_argument("--big", type=int, nargs="*", default=[0],
+                    help="shifu_gemm_set_big per run (0 auto, 3 8-phase whenever M >= 64K and N >= 256, 4 128x128)")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0],
                     help="GEMM lab ablation bits per run (1: no head err atomics, 2: main loops only, 4: head "
                          "stages 1-2 only, 8: no head / 8-phase tile stores, 16: head w_out without loads)")
@@ -59,9 +61,11 @@ def main():
         if tune is not None:
             k, v = (int(x) for x in tune.split(":"))
             nat.call_hip("shifu_gemm_set_tune", k, v)
-        for dbg in a.dbg:
-            nat.call_hip("shifu_gemm_set_tune", 9, dbg)
-            run(a, tr, data, wb, wt, timed, real, rec, f"{dbg} tune {tune}", nat, torch)
+        for big in a.big:
+            nat.call_hip("shifu_gemm_set_big", big)
+            for dbg in a.dbg:
+                nat.call_hip("shifu_gemm_set_tune", 9, dbg)
+                run(a, tr, data, wb, wt, timed, real, rec, f"{dbg} tune {tune} big {big}", nat, torch)
     nat.call_hip("shifu_gemm_set_tune", 9, 0)
 
 
