@@ -421,6 +421,12 @@ class TrainStep:
         info = self.info
         mine = [j for k, j in enumerate(jobs) if k % info.world_size == info.rank]
         _log.info("job-parallel training: rank %d runs %d of %d jobs", info.rank, len(mine), len(jobs))
+        # ranks > 0 log their jobs' epochs to per-rank files that rank 0 appends to the progress
+        # log / metrics stream afterwards (the logs then cover every job, as in the sequential path)
+        pf = self.ms.pf
+        if info.rank:
+            self.progress = open(pf.progress_log + f".rank{info.rank:05d}", "w")
+            self.metrics = MetricsWriter(pf.metrics_jsonl + f".rank{info.rank:05d}")
         with dist.local_only():
             self.info = dist.info()
             try:
@@ -428,9 +434,28 @@ class TrainStep:
                 errs = self._run_jobs(mine, ts, n_kfold, seed)
             finally:
                 self.info = info
+                if info.rank:
+                    self.progress.close()
+                    self.metrics.close()
+                    self.progress = self.metrics = None
         got = {}
         for part in dist.all_gather_objects([(j[0], e) for j, e in zip(mine, errs)]):
             got.update(dict(part))
+        if info.rank == 0:
+            for r in range(1, info.world_size):
+                for path, fh in ((pf.progress_log, self.progress), (pf.metrics_jsonl, self.metrics)):
+                    src = path + f".rank{r:05d}"
+                    if not os.path.exists(src) or fh is None:
+                        continue
+                    with open(src) as f:
+                        data = f.read()
+                    if isinstance(fh, MetricsWriter):
+                        fh.write_raw(data)
+                    else:
+                        fh.write(data)
+                    os.remove(src)
+            if self.progress is not None:
+                self.progress.flush()
         return [got[j[0]] for j in jobs]
 
     # -- NN ---------------------------------------------------------------------------------

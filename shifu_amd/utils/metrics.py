@@ -28,6 +28,11 @@ class MetricsWriter:
         kv.setdefault("ts", time.time())
         self._fh.write(json.dumps(kv, default=float) + "\n")
 
+    def write_raw(self, text: str):
+        """Append already-serialised JSONL lines (another rank's stream)."""
+        if self.enabled and text:
+            self._fh.write(text if text.endswith("\n") else text + "\n")
+
     def close(self):
         if self._fh:
             self._fh.close()

@@ -56,3 +56,13 @@ def test_bags_dealt_over_ranks_equal_single_process(tmp_path, alg):
     names = [sorted(os.path.basename(f) for f in glob.glob(os.path.join(r, "**", "val_error_*"), recursive=True))
              for r in (par, seq)]
     assert names[0] == names[1] == [f"val_error_{b}" for b in range(3)]
+    # the progress log / metrics stream cover every bag (ranks > 0 log to side files rank 0 appends)
+    from shifu_amd.steps.base import ModelSet
+    for r in (par, seq):
+        pf = ModelSet(r).pf
+        log = open(pf.progress_log).read()
+        assert all(f"Trainer {b} Epoch #" in log for b in range(3)), r
+        assert not glob.glob(pf.progress_log + ".rank*")
+        import json
+        trainers = {json.loads(l)["trainer"] for l in open(pf.metrics_jsonl)}
+        assert trainers == {0, 1, 2}, (r, trainers)
