@@ -1,0 +1,562 @@
+// Fused row-block MLP step for two hidden layers (the headline 1000-500-200-1 net), gfx950.
+//
+// One 256-thread block (4 waves, one per SIMD) owns 128 rows; each wave owns 32 complete rows.
+// Per row block, everything between reading X and writing the deltas happens on the chip:
+//   GEMM1  Z1 = W1 . X^T            (k = inputs, 32-wide LDS slices of W1 and X)
+//          H1 = act1(Z1), bias column, bf16           -> stored once (wgrad2 reads it)
+//   GEMM2  Z2 = W2 . H1^T           (H1 straight from the accumulators: no LDS, no HBM)
+//          A2 = act2(Z2); out = A2 . w3; loss; output delta; output-wgrad partials
+//          D2 = delta * w3 * (act2'(A2) + flat)      -> stored once (wgrad2 reads it)
+//   GEMM3  D1 = (W2^T . D2^T) * (act1'(H1) + flat)    -> stored once (wgrad1 reads it)
+// The unfused path (gemm_nt fwd + gemm_head + gemm_nt dgrad) writes H1, reads it back twice and
+// reads D2 back once: 5 GB of HBM traffic per 2M rows that this kernel does not make.
+// Same per-row math as the reference's forward/backward (FloatFlatNetwork.java:148-178,
+// SubGradient.java:224-311) and as gemm_head_8ph_kernel + EPI_DACT (gemm_kernels.hip).
+//
+// MFMA 32x32x16 bf16 with the weights as the A operand and the rows as the B operand, so an
+// accumulator tile C[n][m] has the row m on the lane (m = lane & 31) and 16 outputs n in the
+// registers (n = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)).  GEMM2 / GEMM3 sum over that
+// register index, so H1 / D2 feed them as B operands without moving a value (the k order inside
+// a 16-step is permuted: W2p / W2tp hold W2 with that permutation, see fused_w2_prep_kernel).
+//
+// Pipeline: 3-stage LDS ring of 40 KiB slices (GEMM1: W1 [512][32] + X [128][32]; GEMM2: W2p
+// [256][32]; GEMM3: W2tp [256][32] per output half), filled by LDS-DMA two slices ahead; the
+// wait before a slice is a counted vmcnt (ops issued after that slice's DMAs, stores included:
+// loads, stores and LDS-DMA retire in issue order), never a drain.
+#include "common.h"
+#include <type_traits>
+
+namespace {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) int v4i_t;
+
+constexpr int FT = 256;                 // threads per block
+constexpr int FS = 40960;               // ring stage bytes
+constexpr int FNS = 3;                  // ring stages
+constexpr int F_GW = FS * FNS;          // per-wave [32 m][32 n] fp32 transpose scratch (4 x 4 KiB)
+constexpr int F_W3 = F_GW + 4 * 4096;   // w3 [256] fp32
+constexpr int F_GS = F_W3 + 1024;       // per-wave output-wgrad partials [4][256] fp32
+constexpr int F_ER = F_GS + 4096;       // per-wave error sums [4][2] fp64
+constexpr int F_Y = F_ER + 64;          // targets, significance [2][128] fp32
+constexpr int F_LDS = F_Y + 1024;
+constexpr int NT1 = 16, NT2 = 8;        // 32-wide tiles of H1 (512) and of the last hidden layer (256)
+
+struct FusedArgs {
+  const bf16_t* X; long ldx;            // [M][K0] rows (bias column and zero padding included)
+  const bf16_t* W1; long ldw1;          // [512][K0] (rows past nv1 zero)
+  const bf16_t* W2p;                    // [256][512] W2, k permuted within 16-blocks, zero rows >= nv2
+  const bf16_t* W2tp;                   // [512][256] W2^T, k permuted within 16-blocks
+  const float* w3;                      // [KH] output weights (bias weight at nv2)
+  const float* Y; const float* S;       // [M] targets, significance (nullable)
+  bf16_t* H1; long ldh1;                // out [M][512]
+  bf16_t* D2; long ldd2;                // out [M][256]
+  bf16_t* D1; long ldd1;                // out [M][512]
+  float* gw_slab;                       // [tiles][KH] output-wgrad partials per 128-row tile
+  double* err;                          // [2] error sum, weight sum
+  int M, K0, n1rows, nv1, nv2, KH, out_act, loss;
+  float flat1, flat2, flat_out;
+  unsigned long long* stamps;           // lab: per block [8] s_memtime at phase ends (nullable)
+};
+
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+#define WV(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); return;
+    WV(0) WV(1) WV(2) WV(3) WV(4) WV(5) WV(6) WV(7) WV(8) WV(9) WV(10) WV(11) WV(12) WV(13) WV(14) WV(15)
+    WV(16) WV(17) WV(18) WV(19) WV(20) WV(21) WV(22) WV(23) WV(24) WV(25) WV(26) WV(27) WV(28) WV(29) WV(30)
+    WV(31) WV(32) WV(33) WV(34) WV(35) WV(36) WV(37) WV(38) WV(39) WV(40) WV(41) WV(42) WV(43) WV(44) WV(45)
+    WV(46) WV(47) WV(48) WV(49) WV(50) WV(51) WV(52) WV(53) WV(54) WV(55) WV(56) WV(57) WV(58) WV(59) WV(60)
+    WV(61) WV(62)
+#undef WV
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); return;
+  }
+}
+
+// LDS-DMA of 16 B per lane (saddr form: SGPR base + VGPR byte offset) into LDS byte lds + 16 *
+// lane, and a plain dword load -- both as inline asm: hipcc's wait-count pass cannot count
+// across its own LDS-DMA builtin and falls back to lgkmcnt(0) before every fragment read of the
+// pipelined loops.  The ring waits (wait_vm) cover both; M0 is set right before each DMA.
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16(const void* sbase, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" :: "v"(voff), "s"(sbase), "s"(lds)
+               : "memory", "m0");
+}
+__device__ __forceinline__ float ldg_f32(const float* ptr) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(ptr) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* ptr) { return (uint32_t)(uintptr_t)(lds_ptr_t)ptr; }
+
+#define F_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
+                     __builtin_amdgcn_sched_barrier(0); } while (0)
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// bf16x8 fragment from 8 floats (round to nearest even)
+__device__ __forceinline__ bf16x8 pack8(const float* v) {
+  v4i_t u;
+  u[0] = (int)pack_bf16x2(v[0], v[1]);
+  u[1] = (int)pack_bf16x2(v[2], v[3]);
+  u[2] = (int)pack_bf16x2(v[4], v[5]);
+  u[3] = (int)pack_bf16x2(v[6], v[7]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+// a wave-uniform value the compiler must re-read at each use: stops it from computing the
+// per-element bound masks once and keeping hundreds of them live (spilled) across the GEMMs
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+__device__ __forceinline__ int opaque_v(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// Bias / padding select for output n = 32 t + nl of a layer with nv valid outputs (lim = nv -
+// 32 t, wave-uniform): tiles wholly below nv take the activation as is, the one tile holding nv
+// compares the lane-local index nl (one of 16 per lane), tiles above are zero / bias.
+__device__ __forceinline__ float bias_sel(float a, int nl, int lim) {
+  return nl < lim ? a : (nl == lim ? 1.f : 0.f);
+}
+__device__ __forceinline__ float elem(const bf16x8& f, int j) { return bf2f((bf16_t)f[j]); }
+
+// Row-per-lane bf16 store of one k-step fragment (8 outputs n = 16s + {0..3, 8..11} + 4h of a
+// 32-wide tile): permlane32_swap pairs the halves so each lane writes 16 contiguous bytes.
+__device__ __forceinline__ void store_frag(const __amdgpu_buffer_rsrc_t& rs, const bf16x8& f, int voff) {
+  v4i_t u = __builtin_bit_cast(v4i_t, f);
+  auto r0 = __builtin_amdgcn_permlane32_swap((unsigned)u[0], (unsigned)u[2], false, false);
+  auto r1 = __builtin_amdgcn_permlane32_swap((unsigned)u[1], (unsigned)u[3], false, false);
+  v4i_t o;
+  o[0] = (int)r0[0]; o[1] = (int)r1[0]; o[2] = (int)r0[1]; o[3] = (int)r1[1];
+  __builtin_amdgcn_raw_buffer_store_b128(o, rs, voff, 0, 0);
+}
+
+// Software-pipelined MFMA chain over N (fragment, accumulator) items: the LDS read of item
+// k + D is issued before the MFMA of item k, and sched_group_barriers pin that interleave (left
+// alone, hipcc reads each fragment right before its MFMA and waits lgkmcnt(0) in between).
+template <int N, int D, typename RdF, typename MmF>
+__device__ __forceinline__ void mfma_pipe(RdF rd, MmF mm) {
+  bf16x8 f[N];
+#pragma unroll
+  for (int k = 0; k < D; ++k) f[k] = rd(k);
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (k + D < N) f[k + D] = rd(k + D);
+    mm(k, f[k]);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if (k + D < N) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  }
+}
+
+template <int ACT1, int ACT2>
+__global__ __launch_bounds__(FT, 1) void mlp_fused2_kernel(FusedArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int tile = blockIdx.x;
+  // every kernel argument in SGPRs before the ring starts: a scalar load still in flight inside
+  // the pipelined loops would force lgkmcnt(0) (scalar loads retire out of order) before every
+  // fragment read
+  asm volatile("" :: "s"(p.X), "s"(p.W1), "s"(p.W2p), "s"(p.W2tp), "s"(p.w3), "s"(p.Y), "s"(p.S));
+  asm volatile("" :: "s"(p.H1), "s"(p.D2), "s"(p.D1), "s"(p.gw_slab), "s"(p.err), "s"(p.ldx), "s"(p.ldw1));
+  asm volatile("" :: "s"(p.ldh1), "s"(p.ldd2), "s"(p.ldd1), "s"(p.M), "s"(p.K0), "s"(p.nv1), "s"(p.nv2));
+  asm volatile("" :: "s"(p.KH), "s"(p.out_act), "s"(p.loss), "s"(p.flat1), "s"(p.flat2), "s"(p.flat_out));
+  const long m0 = (long)tile * 128;
+  const int rows = (int)min(128l, (long)p.M - m0);
+  const int NQ1 = p.K0 / 32;
+
+
+  // ---- LDS-DMA source offsets (elements).  Thread tid fills LDS byte P = i * 4096 + tid * 16
+  // of a slice: row i * 64 + (tid >> 2), 16-B chunk (tid & 3) ^ ((tid >> 4) & 3) of the row
+  // (the XOR swizzle of the ds_read side, applied on the source address).  One VGPR offset per
+  // operand; the row-group term i * 64 * ld is wave-uniform (scalar base).  W1 is padded to 512
+  // rows by the host, so only the X rows of a partial last block are clamped.
+  // Stage layout: GEMM1 = X [128][32] at 0 + W1 [512][32] at 8 KiB; GEMM2/3 = [256][32] at 0;
+  // bytes [16 KiB, 40 KiB) of every stage are free once GEMM1 is done (H1 stash, below).
+  const int drow = tid >> 2, dch = ((tid & 3) ^ ((tid >> 4) & 3)) * 8;
+  const bf16_t* Xt = p.X + m0 * p.ldx;
+  const uint32_t offW1 = (drow * (int)p.ldw1 + dch) * 2;
+  const uint32_t offX0 = (min(drow, rows - 1) * (int)p.ldx + dch) * 2;
+  const uint32_t offX1 = (min(64 + drow, rows - 1) * (int)p.ldx + dch) * 2;
+  const uint32_t offW2 = (drow * 512 + dch) * 2, offW2t = (drow * 256 + dch) * 2;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem) + w * 1024);
+
+  auto dma = [&](int q) {     // slice q -> stage q % 3 (wave-uniform)
+    const uint32_t st = lds0 + (q % FNS) * FS;
+    if (q < NQ1) {
+      const int k0 = q * 32;
+      dma16(Xt + k0, offX0, st);
+      dma16(Xt + k0, offX1, st + 4096);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dma16(p.W1 + (long)i * 64 * p.ldw1 + k0, offW1, st + 8192 + i * 4096);
+    } else if (q < NQ1 + 16) {
+      const int k0 = (q - NQ1) * 32;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma16(p.W2p + i * 64 * 512 + k0, offW2, st + i * 4096);
+    } else {
+      const int j = q - NQ1 - 16, k0 = (j & 7) * 32;
+      const bf16_t* src = p.W2tp + (j >> 3) * 256 * 256;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma16(src + i * 64 * 256 + k0, offW2t, st + i * 4096);
+    }
+  };
+  const int NQ = NQ1 + 32;
+
+  // per-row inputs and w3 ride between the DMAs of slices 0 and 1: step 0's wait (slice 0 in,
+  // 10 younger ops allowed) covers them, so staging them in LDS costs no drain of the ring
+  unsigned long long t_st[8] = {};
+  auto stamp = [&](int i) { if (p.stamps) t_st[i] = __builtin_amdgcn_s_memtime(); };
+  stamp(0);
+  dma(0);
+  const int my = (int)min(m0 + 32 * w + r, (long)p.M - 1);
+  const float y_in = ldg_f32(p.Y + my);
+  const float s_in = ldg_f32((p.S ? p.S : p.Y) + my);
+  const float w3_in = ldg_f32(p.w3 + min(tid, p.KH - 1));
+  dma(1);
+  float* w3s = (float*)(smem + F_W3);
+  float* ys = (float*)(smem + F_Y);
+
+  // per-lane ds_read offsets: row 32t + r, chunk c -> r * 64 + ((c ^ ((r >> 2) & 3)) << 4) (+ t * 2048)
+  int coff[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) coff[c] = r * 64 + ((c ^ ((r >> 2) & 3)) << 4);
+  const int xrow = (32 * w + r) * 64;      // this wave's X rows inside a GEMM1 slice
+
+  // step q: wait until slice q has landed (nw = vector-memory ops this wave issued after slice
+  // q's DMAs: the DMAs of q + 1 plus any epilogue stores since), barrier (every wave's part of
+  // slice q is in, every wave is past slice q - 1 so stage (q + 2) % 3 is free), DMAs of q + 2.
+  auto step_begin = [&](int q, int nw) {
+    wait_vm(nw);
+    F_BAR();
+    if (q + 2 < NQ) dma(q + 2);
+  };
+
+  // ================= GEMM1: Z1[n1][m] over k = K0 =================
+  f32x16 acc1[NT1];
+#pragma unroll
+  for (int t = 0; t < NT1; ++t) acc1[t] = f32x16{};
+  for (int q = 0; q < NQ1; ++q) {
+    if (q + 1 < NQ1) step_begin(q, 10);
+    else step_begin(q, 4);
+    if (q == 0) {   // visible to every wave after step 1's barrier (first read: head epilogue)
+      w3s[tid] = tid < p.KH ? w3_in : 0.f;
+      if (h == 0) { ys[32 * w + r] = y_in; ys[128 + 32 * w + r] = p.S ? s_in : 1.f; }
+    }
+    const char* st = smem + (q % FNS) * FS;
+    bf16x8 b[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) b[s] = *(const bf16x8*)(st + xrow + ((((2 * s + h) ^ ((r >> 2) & 3))) << 4));
+    mfma_pipe<2 * NT1, 6>(
+        [&](int k) { return *(const bf16x8*)(st + 8192 + (k & 15) * 2048 + coff[2 * (k >> 4) + h]); },
+        [&](int k, const bf16x8& a) { acc1[k & 15] = mfma32(a, b[k >> 4], acc1[k & 15]); });
+  }
+
+  stamp(1);
+  // ---- epilogue 1: H1 = act1(Z1) (+ bias column, zero padding), bf16.  Tiles 0..7 stay in
+  // registers as B fragments; tiles 8..15 go to the free upper 24 KiB of the three stages (a
+  // barrier first: every wave is done with the last GEMM1 slice there) and come back as LDS
+  // reads in GEMM2's second half and GEMM3's second half -- 64 VGPRs instead of 128 live.
+  F_BAR();
+  auto stash = [&](int t, int s) -> char* {
+    const int idx = ((w * 16 + (t - 8) * 2 + s) * 64 + lane);
+    return smem + (idx / 1536) * FS + 16384 + (idx % 1536) * 16;
+  };
+  bf16x8 H1b[8][2];
+  {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.H1 + m0 * p.ldh1), (short)0, rows * (int)p.ldh1 * 2, 0x00020000);
+    const int vrow = (32 * w + r) * (int)p.ldh1 * 2 + h * 16;
+    const int nv = opaque(p.nv1), h4 = opaque_v(4 * h);
+#pragma unroll
+    for (int t = 0; t < NT1; ++t) {
+      const int lim = nv - 32 * t;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int reg = 8 * s + j;
+          const float a = act_fwd(ACT1, acc1[t][reg]);
+          v[j] = lim >= 32 ? a : bias_sel(a, (reg & 3) + 8 * (reg >> 2) + h4, lim);
+        }
+        const bf16x8 f = pack8(v);
+        store_frag(rs, f, vrow + (32 * t + 16 * s) * 2);
+        if (t < 8) H1b[t][s] = f;
+        else *(bf16x8*)stash(t, s) = f;
+      }
+    }
+  }
+
+  stamp(2);
+  // ================= GEMM2: Z2[n2][m] over k = n1 (512) =================
+  f32x16 acc2[NT2];
+#pragma unroll
+  for (int t = 0; t < NT2; ++t) acc2[t] = f32x16{};
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int q = NQ1 + j;
+    step_begin(q, (j < 2 ? 2 * NT1 : 0) + 4);
+    const char* st = smem + (q % FNS) * FS;
+    bf16x8 hb[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) hb[s] = j < 8 ? H1b[j & 7][s] : *(const bf16x8*)stash(j, s);
+    mfma_pipe<2 * NT2, 4>(
+        [&](int k) { return *(const bf16x8*)(st + (k & 7) * 2048 + coff[2 * (k >> 3) + h]); },
+        [&](int k, const bf16x8& a) { acc2[k & 7] = mfma32(a, hb[k >> 3], acc2[k & 7]); });
+  }
+
+  stamp(3);
+  // ---- head epilogue: A2, output, loss, delta, D2, output-wgrad partials
+  // A2 (bf16 values, as the unfused path stores them) kept packed: 64 VGPRs instead of 128
+  float zo = 0.f;
+  bf16x8 A2b[NT2][2];
+  const int nv2e = opaque(p.nv2), h4e = opaque_v(4 * h);
+#pragma unroll
+  for (int t = 0; t < NT2; ++t)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float v[8];
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        const int g = 2 * s + gg;
+        const float4 w4 = *(const float4*)(w3s + 32 * t + 8 * g + 4 * h);
+        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int lim = nv2e - 32 * t;
+          const float af = act_fwd(ACT2, acc2[t][4 * g + k]);
+          const float a = bf2f(f2bf(lim >= 32 ? af : bias_sel(af, 8 * g + k + h4e, lim)));
+          v[4 * gg + k] = a;
+          zo += a * wv[k];
+        }
+      }
+      A2b[t][s] = pack8(v);
+    }
+  zo += __shfl_xor(zo, 32, 64);               // the row's other 128 outputs live in lane ^ 32
+  const long mrow = m0 + 32 * w + r;
+  const bool valid = mrow < p.M;
+  float dlt = 0.f;
+  double e_c = 0.0, e_w = 0.0;
+  if (valid) {
+    const float y = ys[32 * w + r], sg = ys[128 + 32 * w + r];
+    const float a = act_fwd(p.out_act, zo), e = y - a;
+    if (p.loss == 1) {
+      dlt = e * sg;
+      const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
+      e_c = -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
+    } else if (p.loss == 2) {
+      dlt = (y < a ? 1.f : -1.f) * (act_deriv_out(p.out_act, a) + p.flat_out) * sg;
+      e_c = fabsf(e) * sg;
+    } else {
+      dlt = (act_deriv_pre(p.out_act, zo) + p.flat_out) * e * sg;
+      e_c = (double)(e * sg) * (e * sg);
+    }
+    e_w = sg;
+  }
+  if (h) { e_c = 0.0; e_w = 0.0; }            // each row counted once
+  e_c = wave_sum_d(e_c);
+  e_w = wave_sum_d(e_w);
+  double* ers = (double*)(smem + F_ER);
+  if (lane == 0) { ers[2 * w] = e_c; ers[2 * w + 1] = e_w; }
+
+  bf16x8 D2b[NT2][2];
+  float* gws = (float*)(smem + F_GW + w * 4096);       // [32 m][32 n] fp32, 16-B chunks swizzled
+  float gacc[NT2];
+  const int nv2d = opaque(p.nv2), h4d = opaque_v(4 * h);
+#pragma unroll
+  for (int t = 0; t < NT2; ++t) {
+    const int lim = nv2d - 32 * t;
+    // output-wgrad partial of this tile: sum over the wave's 32 rows of dlt * a2 (fixed order)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = (2 * g + h) ^ ((r >> 1) & 7);
+      float4 v;
+      const bf16x8& af = A2b[t][g >> 1];
+      const int j0 = 4 * (g & 1);
+      v.x = dlt * elem(af, j0); v.y = dlt * elem(af, j0 + 1);
+      v.z = dlt * elem(af, j0 + 2); v.w = dlt * elem(af, j0 + 3);
+      *(float4*)(gws + r * 32 + ch * 4) = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      const int n = r;                        // column n of the tile, rows 16 h .. 16 h + 15
+      float sacc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = 16 * h + ((i + h) & 15);
+        sacc += gws[m * 32 + ((((n >> 2) ^ ((m >> 1) & 7))) << 2) + (n & 3)];
+      }
+      sacc += __shfl_xor(sacc, 32, 64);
+      gacc[t] = sacc;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // D2 = dlt * w3 * (act2'(a2) + flat2)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float v[8];
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        const int g = 2 * s + gg;
+        const float4 w4 = *(const float4*)(w3s + 32 * t + 8 * g + 4 * h);
+        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d = dlt * wv[k] * (act_deriv_out(ACT2, elem(A2b[t][s], 4 * gg + k)) + p.flat2);
+          v[4 * gg + k] = (lim >= 32 || 8 * g + k + h4d < lim) ? d : 0.f;
+        }
+      }
+      D2b[t][s] = pack8(v);
+    }
+  }
+  float* gsum = (float*)(smem + F_GS);
+  if (h == 0) {
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) gsum[w * 256 + 32 * t + r] = gacc[t];
+  }
+  {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.D2 + m0 * p.ldd2), (short)0, rows * (int)p.ldd2 * 2, 0x00020000);
+    const int vrow = (32 * w + r) * (int)p.ldd2 * 2 + h * 16;
+#pragma unroll
+    for (int t = 0; t < NT2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) store_frag(rs, D2b[t][s], vrow + (32 * t + 16 * s) * 2);
+  }
+
+  // ================= GEMM3: D1[n1][m] = sum_n2 W2^T[n1][n2] D2[m][n2], two 256-wide halves ====
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.D1 + m0 * p.ldd1), (short)0, rows * (int)p.ldd1 * 2, 0x00020000);
+  const int vrow1 = (32 * w + r) * (int)p.ldd1 * 2 + h * 16;
+  // one instance per half (compile-time HH: every register-array index stays a constant)
+  auto gemm3_half = [&](auto HHc) {
+    constexpr int HH = decltype(HHc)::value;
+    f32x16 acc3[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc3[t] = f32x16{};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int q = NQ1 + 16 + HH * 8 + j;
+      // 16 stores (D2 before half 0, D1 half 0 before half 1) sit after slices q0, q0 + 1
+      step_begin(q, (j < 2 ? 16 : 0) + (HH == 1 && j == 7 ? 0 : 4));
+      const char* st = smem + (q % FNS) * FS;
+      mfma_pipe<16, 4>(
+          [&](int k) { return *(const bf16x8*)(st + (k & 7) * 2048 + coff[2 * (k >> 3) + h]); },
+          [&](int k, const bf16x8& a) { acc3[k & 7] = mfma32(a, D2b[j][k >> 3], acc3[k & 7]); });
+    }
+    const int nv1d = opaque(p.nv1), h4g = opaque_v(4 * h);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      constexpr int T0 = HH * 8;
+      const int lim = nv1d - 32 * (T0 + t);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 hf = HH == 0 ? H1b[t][s] : *(const bf16x8*)stash(8 + t, s);
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int reg = 8 * s + j;
+          const float d = acc3[t][reg] * (act_deriv_out(ACT1, elem(hf, j)) + p.flat1);
+          v[j] = (lim >= 32 || (reg & 3) + 8 * (reg >> 2) + h4g < lim) ? d : 0.f;
+        }
+        store_frag(rs1, pack8(v), vrow1 + (32 * (T0 + t) + 16 * s) * 2);
+      }
+    }
+  };
+  stamp(4);
+  gemm3_half(std::integral_constant<int, 0>{});
+  stamp(5);
+  gemm3_half(std::integral_constant<int, 1>{});
+  stamp(6);
+
+  // ---- block totals: output-wgrad partials (fixed wave order) and the error sums
+  F_BAR();
+  if (p.stamps && tid == 0) {
+    t_st[7] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p.stamps[(long)tile * 8 + i] = t_st[i];
+  }
+  if (tid < p.KH)
+    p.gw_slab[(long)tile * p.KH + tid] = gsum[tid] + gsum[256 + tid] + gsum[512 + tid] + gsum[768 + tid];
+  if (tid == 0) {
+    atomicAdd(p.err, ers[0] + ers[2] + ers[4] + ers[6]);
+    atomicAdd(p.err + 1, ers[1] + ers[3] + ers[5] + ers[7]);
+  }
+}
+
+// W2 [o][512] fp32 -> W2p [256][512] (k permuted within 16-blocks) and W2tp [512][256]
+// (transposed, k = n2 permuted within 16-blocks); rows / columns >= o are zero.
+// Permutation: position 8 hh + j of a 16-block holds index 8 (j >> 2) + 4 hh + (j & 3).
+__global__ void fused_w2_prep_kernel(const float* W2, long ldw, int o, bf16_t* W2p, bf16_t* W2tp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 256 * 512) return;
+  {
+    const int n2 = i >> 9, pos = i & 511;
+    const int blk = pos >> 4, pp = pos & 15, hh = pp >> 3, j = pp & 7;
+    const int n1 = blk * 16 + 8 * (j >> 2) + 4 * hh + (j & 3);
+    W2p[i] = n2 < o ? f2bf(W2[(long)n2 * ldw + n1]) : (bf16_t)0;
+  }
+  {
+    const int n1 = i >> 8, pos = i & 255;
+    const int blk = pos >> 4, pp = pos & 15, hh = pp >> 3, j = pp & 7;
+    const int n2 = blk * 16 + 8 * (j >> 2) + 4 * hh + (j & 3);
+    W2tp[i] = n2 < o ? f2bf(W2[(long)n2 * ldw + n1]) : (bf16_t)0;
+  }
+}
+
+}  // namespace
+
+#define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+// W2p / W2tp: bf16 [256 * 512] each (see fused_w2_prep_kernel).
+SHIFU_API int shifu_fused_w2_prep(const float* W2, long ldw, int o, void* W2p, void* W2tp, hipStream_t stream) {
+  if (o <= 0 || o > 255 || ldw < 512) return -1;
+  hipLaunchKernelGGL(fused_w2_prep_kernel, dim3(512), dim3(256), 0, stream, W2, ldw, o, (bf16_t*)W2p,
+                     (bf16_t*)W2tp);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_mlp_fused2_tiles(int M) { return (M + 127) / 128; }
+
+// lab: per-block phase time stamps (s_memtime at start, GEMM1 end, epilogue-1 end, GEMM2 end,
+// head end, GEMM3 halves, totals) into [tiles][8] u64; nullptr turns it off
+static unsigned long long* g_f2_stamps = nullptr;
+SHIFU_API void shifu_mlp_fused2_set_stamps(void* p) { g_f2_stamps = (unsigned long long*)p; }
+
+// Shapes: K0 % 32 == 0, layer-1 width (incl. bias) padded to 512 (256 < nv1 + 1 <= 512 not
+// required: rows past nv1 are written as bias / zeros), last hidden padded to 256 (nv2 <= 255),
+// one output; activations whose derivative follows from the output (not ptanh).
+SHIFU_API int shifu_mlp_fused2(const void* X, long ldx, int M, int K0, const void* W1, long ldw1, int n1rows,
+                               int nv1, const void* W2p, const void* W2tp, int nv2, const float* w3, int KH,
+                               const float* Y, const float* S, void* H1, long ldh1, void* D2, long ldd2, void* D1,
+                               long ldd1, float* gw_slab, double* err, int act1, int act2, int out_act, int loss,
+                               float flat1, float flat2, float flat_out, hipStream_t stream) {
+  if (M <= 0 || K0 <= 0 || K0 % 32 || ldx < K0 || ldx % 8 || ldw1 < K0 || ldw1 % 8 || n1rows <= 0 ||
+      n1rows > 512 || nv1 < 1 || nv1 > 511 || nv2 < 1 || nv2 > 255 || KH < nv2 + 1 || KH > 256 ||
+      ldh1 < 512 || ldh1 % 8 || ldd2 < 256 || ldd2 % 8 || ldd1 < 512 || ldd1 % 8)
+    return -1;
+  if (n1rows != 512) return -1;            // W1 padded to 512 rows (zero rows past nv1)
+  if ((long)128 * ldx >= (1l << 31) || (long)512 * ldw1 >= (1l << 31) || (long)128 * ldd1 * 2 >= (1l << 31))
+    return -1;
+  if (out_act < 0 || out_act > 8) return -2;
+  FusedArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W1, ldw1, (const bf16_t*)W2p, (const bf16_t*)W2tp, w3, Y, S,
+              (bf16_t*)H1, ldh1, (bf16_t*)D2, ldd2, (bf16_t*)D1, ldd1, gw_slab, err,
+              M, K0, n1rows, nv1, nv2, KH, out_act, loss, flat1, flat2, flat_out, g_f2_stamps};
+  const int grid = (M + 127) / 128;
+#define FL(A1, A2) hipLaunchKernelGGL((mlp_fused2_kernel<A1, A2>), dim3(grid), dim3(FT), F_LDS, stream, a)
+  if (act1 == 0 && act2 == 0) FL(0, 0);
+  else if (act1 == 1 && act2 == 1) FL(1, 1);
+  else if (act1 == 3 && act2 == 3) FL(3, 3);
+  else if (act1 == 3 && act2 == 0) FL(3, 0);
+  else return -2;
+#undef FL
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}

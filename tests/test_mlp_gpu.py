@@ -239,3 +239,36 @@ def test_nn_scoring_bf16_close_to_fp32():
     b = nn_forward(net, X, torch.device("cuda"), precision="bf16")
     assert a.shape == b.shape == (20000, 2)
     assert np.abs(a - b).max() <= 2e-2
+
+
+@pytest.mark.parametrize("hidden,acts,loss,n", [([500, 200], ["sigmoid", "sigmoid"], "squared", 70000 + 77),
+                                                ([450, 192], ["tanh", "tanh"], "log", 3 * 4096 + 5),
+                                                ([511, 255], ["relu", "sigmoid"], "absolute", 131072),
+                                                ([500, 200], ["sigmoid", "sigmoid"], "squared", 100)])
+def test_fused_mlp_step_matches_per_layer_kernels(hidden, acts, loss, n, monkeypatch):
+    """mlp_fused2_kernel (layer-1 fwd + layer-2 fwd + output/loss/deltas + layer-1 dgrad in one
+    row-block kernel, H1 / D2 kept on chip) against the per-layer kernels (8-phase forward, fused
+    head, dgrad GEMM): same gradients (bf16 intermediates, different fp32 summation order), same
+    error sums.  Covers a partial last row block, several chunks and a chunk below one block."""
+    spec = MLPSpec(n_in=1000, hidden=hidden, acts=acts, n_out=1, loss=loss)
+    x, y, s = _mk(spec, n, seed=21)
+    monkeypatch.setenv("SHIFU_FUSED_MLP", "1")
+    a = MLPTrainer(spec, device="cuda", seed=4, chunk_rows=65536)
+    monkeypatch.setenv("SHIFU_FUSED_MLP", "0")
+    b = MLPTrainer(spec, device="cuda", seed=4, chunk_rows=65536)
+    assert a.fused2 and not b.fused2
+    b.params.flat.copy_(a.params.flat)
+    da, db = a.prepare(x, y, s), b.prepare(x, y, s)
+    for t, d in ((a, da), (b, db)):
+        t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
+    torch.cuda.synchronize()
+    for va, vb in zip(a.params.views(a.grad), b.params.views(b.grad)):
+        r = (va - vb).norm() / vb.norm().clamp(min=1e-12)
+        assert r < 1e-2, float(r)
+    assert abs(float(a.err_acc[0]) - float(b.err_acc[0])) / float(b.err_acc[0]) < 1e-4
+    assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
+    # and bit-identical run to run (fixed-order output-wgrad partials, no float atomics)
+    g1 = a.grad.clone()
+    a.grad.zero_(); a.accumulate_gradients(da)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, a.grad)
