@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1 << 21)
     ap.add_argument("--iters", type=int, default=3)
     a = ap.parse_args()
+    os.environ["SHIFU_FUSED_MLP"] = "1"
     import torch
     from shifu_amd.models import nn as NN
     from shifu_amd.ops import _native as nat
