@@ -137,12 +137,16 @@ def purify(mc, table: RawTable, target: str, weight_expr: str | None = None, fil
         w = np.where(bad, 1.0, wv)
     idx = np.nonzero(keep)[0]
     c.valid = int(len(idx))
-    t = table.take(idx)
-    yk = y[idx].astype(np.float32)
+    if c.valid == table.n:
+        # every row kept (the common case): no copy of the table (a full gather of every column
+        # was ~7 % of a streamed stats / norm pass at 2M x 1600)
+        t, yk, wk, tk = table, y.astype(np.float32), w.astype(np.float64, copy=False), ti
+    else:
+        t, yk, wk, tk = table.take(idx), y[idx].astype(np.float32), w[idx].astype(np.float64), ti[idx]
     if mc.is_binary():
         c.pos = int((yk == 1).sum())
         c.neg = int((yk == 0).sum())
-    return ModelData(t, yk, w[idx].astype(np.float64), ti[idx], c)
+    return ModelData(t, yk, wk, tk, c)
 
 
 @dataclass

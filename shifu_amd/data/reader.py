@@ -294,7 +294,10 @@ def table_from_parts(header: list, kinds: list, parts: list, data_path: str = ""
             continue
         name = header[ci]
         if k == 1:
-            vals = np.concatenate([p[2][ci][1] for p in parts]) if parts else np.empty(0)
+            if len(parts) == 1:             # one parsed block: its array as is (no copy)
+                vals = parts[0][2][ci][1]
+            else:
+                vals = np.concatenate([p[2][ci][1] for p in parts]) if parts else np.empty(0)
             cols[name] = Column(name, "num", vals)
         else:
             gdict, remapped = {}, []
