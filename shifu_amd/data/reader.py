@@ -159,6 +159,9 @@ def _parse_native(data: bytes, delim: str, kinds: list, missing: list, nthreads:
     if isinstance(data, bytes):              # immutable: parse it in place (no copy of the block)
         buf = data
         addr = ctypes.cast(ctypes.c_char_p(data), ctypes.c_void_p).value
+    elif isinstance(data, memoryview) and not data.readonly and data.contiguous and len(data):
+        buf = data                           # a block of a read buffer (data/stream.py): in place
+        addr = ctypes.addressof(ctypes.c_char.from_buffer(data))
     else:
         buf = ctypes.create_string_buffer(bytes(data), len(data))
         addr = ctypes.addressof(buf)
@@ -192,7 +195,7 @@ def _parse_native(data: bytes, delim: str, kinds: list, missing: list, nthreads:
 
 
 def _parse_python(data: bytes, delim: str, kinds: list, missing: list):
-    text = data.decode("utf-8", errors="replace")
+    text = bytes(data).decode("utf-8", errors="replace")
     lines = [l for l in text.split("\n") if l.strip()]
     n = len(lines)
     miss = set(m.strip() for m in missing)

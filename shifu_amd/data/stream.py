@@ -26,6 +26,7 @@ from .purifier import DatasetPlan, finish_table
 from .reader import column_kinds, list_data_files, parse_block, table_from_parts, _parse_parquet
 
 DEFAULT_CHUNK_BYTES = 256 << 20
+PREFETCH_READ = int(os.environ.get("SHIFU_READ_PREFETCH", "2"))   # blocks read ahead of the parse
 
 
 def _units(files):
@@ -54,39 +55,58 @@ def byte_ranges(files, rank: int = 0, world: int = 1):
     return sorted(out)
 
 
-def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int):
-    """Yield (offset, bytes) blocks of complete lines whose first byte lies in [start, end)."""
-    with open(path, "rb") as fh:
+def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int = 1):
+    """Yield (offset, block) blocks of complete lines whose first byte lies in [start, end).
+
+    Blocks are memoryviews into ``nbuf`` rotating buffers, filled with ``readinto`` (no copy of
+    the text; the old ``carry + read()`` / slicing made two copies of every block): a block stays
+    valid until ``nbuf - 1`` further blocks have been produced (1: until the next is requested)."""
+    bufs = [None] * max(1, nbuf)
+    k = 0
+    with open(path, "rb", buffering=0) as fh:
         pos = start
         if start > 0:
             fh.seek(start - 1)
             if fh.read(1) != b"\n":           # mid-line: that line belongs to the previous range
-                rest = fh.readline()
-                pos = start + len(rest)
+                with open(path, "rb") as fl:
+                    fl.seek(start)
+                    pos = start + len(fl.readline())
         fh.seek(pos)
         carry = b""
         while pos < end:
             # never read (much) past the range: the line straddling `end` is completed by the
             # small follow-up reads of the carry logic
             want = min(chunk_bytes, max(end - pos - len(carry), 0) + (1 << 16))
-            blk = fh.read(want)
-            if not blk:
+            need = len(carry) + want
+            buf = bufs[k]
+            if buf is None or len(buf) < need:
+                buf = bufs[k] = bytearray(max(need, chunk_bytes + (1 << 16)))
+            mv = memoryview(buf)
+            c = len(carry)
+            mv[:c] = carry
+            got = 0
+            while got < want:                  # a raw read may return short
+                r = fh.readinto(mv[c + got: c + want])
+                if not r:
+                    break
+                got += r
+            filled = c + got
+            if got == 0:
                 if carry:
-                    yield pos, carry
+                    yield pos, mv[:c]
                 return
-            buf = carry + blk
-            cut = buf.rfind(b"\n")
+            cut = buf.rfind(b"\n", 0, filled)
             if cut < 0:
-                carry = buf
+                carry = bytes(mv[:filled])     # one line longer than the block: read on
                 continue
-            lines, carry = buf[:cut + 1], buf[cut + 1:]
-            if pos + len(lines) > end:            # stop after the line that starts before `end`
-                i = lines.find(b"\n", max(0, end - pos - 1))
-                lines = lines[:i + 1]
-                yield pos, lines
+            carry = bytes(mv[cut + 1:filled])
+            k = (k + 1) % len(bufs)
+            if pos + cut + 1 > end:           # stop after the line that starts before `end`
+                i = buf.find(b"\n", max(0, end - pos - 1), filled)
+                yield pos, mv[:i + 1]
                 return
-            yield pos, lines
-            pos += len(lines)
+            yield pos, mv[:cut + 1]
+            pos += cut + 1
 
 
 def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kinds: list, nthreads: int):
@@ -106,11 +126,16 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
                 data = data[nl + 1:] if nl >= 0 else b""
             yield (fi, 0), parse_block(data, plan.delim, kinds, plan.missing, nthreads)
             continue
-        for off, data in _lines_in_range(path, a, b, chunk_bytes):
+        # the file reads run one thread ahead of the parse (readinto and the native parser both
+        # release the GIL); PREFETCH_READ + 3 buffers cover the queue, the block being parsed and
+        # the one being filled
+        blocks = (prefetched(lambda: _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + 3), PREFETCH_READ)
+                  if PREFETCH_READ > 0 else _lines_in_range(path, a, b, chunk_bytes))
+        for off, data in blocks:
             if plan.skip_header_line and fi == 0 and off == 0:
-                nl = data.find(b"\n")
+                nl = bytes(data[: 1 << 20]).find(b"\n")
                 data = data[nl + 1:] if nl >= 0 else b""
-                if not data:
+                if not len(data):
                     continue
             yield (fi, off), parse_block(data, plan.delim, kinds, plan.missing, nthreads)
 

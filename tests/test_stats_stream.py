@@ -41,7 +41,7 @@ def test_byte_ranges_partition_rows(tmp_path, world, chunk):
                 got += [(fi, 0, l) for l in gzip.open(path, "rt").read().splitlines()]
                 continue
             for off, blk in DS._lines_in_range(path, a, b, chunk):
-                got += [(fi, off, l) for l in blk.decode().splitlines()]
+                got += [(fi, off, l) for l in bytes(blk).decode().splitlines()]
     got.sort(key=lambda t: (t[0], t[1]))
     assert [g[2] for g in got] == rows + gz
 
