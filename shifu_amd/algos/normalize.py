@@ -216,7 +216,33 @@ def _raw_matrix(cols, table):
     out = np.empty((len(cols), table.n), dtype=np.float64)
     for j, cc in enumerate(cols):
         col = table[cc.name]
-        out[j] = _cat_index(cc, col) if cc.is_categorical() else col.numeric().astype(np.float64)
+        out[j] = _cat_index(cc, col) if cc.is_categorical() else col.numeric()
+    return out
+
+
+def _raw_matrix_dev(cols, table, dev):
+    """:func:`_raw_matrix` on ``dev``.  The numeric columns that are rows of the parser's block
+    matrix are uploaded in place (the block's spanned rows as one copy, placed by a device-side
+    gather); only the others (categorical indices, filtered tables) go through a host gather."""
+    import torch
+    from ..data.reader import numeric_rows
+    num_j = [j for j, cc in enumerate(cols) if not cc.is_categorical() and table[cc.name].kind == "num"]
+    hit = numeric_rows([table[cols[j].name].values for j in num_j]) if len(num_j) > 1 else None
+    if hit is None:
+        return torch.as_tensor(_raw_matrix(cols, table), device=dev)
+    base, idx = hit
+    lo, hi = int(idx.min()), int(idx.max()) + 1
+    blk = torch.as_tensor(base[lo:hi], device=dev)                  # one H2D copy, no host gather
+    if len(num_j) == len(cols) and np.array_equal(idx, np.arange(lo, hi)):
+        return blk
+    out = torch.empty((len(cols), table.n), dtype=torch.float64, device=dev)
+    jt = torch.as_tensor(np.asarray(num_j, np.int64), device=dev)
+    out.index_copy_(0, jt, blk.index_select(0, torch.as_tensor(idx - lo, device=dev)))
+    in_blk = set(num_j)
+    rest = [j for j in range(len(cols)) if j not in in_blk]
+    if rest:
+        host = _raw_matrix([cols[j] for j in rest], table)
+        out.index_copy_(0, torch.as_tensor(np.asarray(rest, np.int64), device=dev), torch.as_tensor(host, device=dev))
     return out
 
 
@@ -301,7 +327,7 @@ def normalize_table_gpu(mc, ccs, table, columns=None, norm_type: str | None = No
     dev = torch.device(device)
     out = torch.zeros(table.n, max(pos, 1), dtype=torch.float32, device=dev)
     if gpu_cols:
-        vals = torch.as_tensor(_raw_matrix(gpu_cols, table), device=dev)
+        vals = _raw_matrix_dev(gpu_cols, table, dev)
         stats_ops.normalize(vals, specs, out)
     for cc, p0, width in host_cols:
         out[:, p0: p0 + width] = torch.as_tensor(normalize_column(cc, table[cc.name], nt, cutoff), dtype=torch.float32,
@@ -325,7 +351,7 @@ def tree_bin_codes_gpu(ccs, table, columns, device="cuda"):
     if max(nbins, default=1) > 256:
         return None
     dev = torch.device(device)
-    vals = torch.as_tensor(_raw_matrix(columns, table), device=dev)
+    vals = _raw_matrix_dev(columns, table, dev)
     out = torch.zeros(table.n, max(1, len(columns)), dtype=torch.uint8, device=dev)
     stats_ops.bin_codes(vals, is_cat, bounds, ncat, out)
     return out.cpu().numpy().astype(np.int32), np.array(nbins, np.int32), np.array(is_cat, np.uint8)
@@ -447,7 +473,7 @@ class NormPlan:
         from ..ops import _native as nat
         need_codes = self.want_codes and self.code_dtype == np.uint8
         dev_cols = self.gpu_cols if not need_codes else self.cols
-        vals = torch.as_tensor(_raw_matrix(dev_cols, table), device=self.dev) if dev_cols else None
+        vals = _raw_matrix_dev(dev_cols, table, self.dev) if dev_cols else None
         ds = self._device_specs()
         outf = self._buf("f", (n, max(self.width, 1)), torch.float32) if (self.want_x and not bf16) else None
         outb = self._buf("b", (n, self.kpad), torch.bfloat16,
@@ -456,7 +482,7 @@ class NormPlan:
         if vals is not None and n:
             if need_codes and len(self.gpu_cols) != len(self.cols):
                 # one-hot columns present: the width-1 specs index the gpu columns only -> two passes
-                sub = torch.as_tensor(_raw_matrix(self.gpu_cols, table), device=self.dev)
+                sub = _raw_matrix_dev(self.gpu_cols, table, self.dev)
                 rc = nat.call_hip("shifu_norm_codes", sub, sub.stride(0), n, len(self.gpu_cols), ds["ip"], ds["dp"],
                                   ds["bounds"], ds["tables"], None, None, outf, 0 if outf is None else outf.stride(0),
                                   outb, 0 if outb is None else outb.stride(0), None, 0, nat.stream_of(sub)) \

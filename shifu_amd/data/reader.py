@@ -172,11 +172,17 @@ def _parse_native(data: bytes, delim: str, kinds: list, missing: list, nthreads:
         n = lib.shifu_csv_nrows(h)
         bad = lib.shifu_csv_bad_rows(h)
         out = {}
+        # numeric columns land in the rows of ONE column-major matrix: each column is a row view,
+        # and consumers that need several columns as a matrix (normalize, stats uploads) can use
+        # the rows in place (see ``numeric_rows``) instead of gathering them
+        num_ci = [ci for ci, k in enumerate(kinds) if k == 1]
+        M = np.empty((len(num_ci), n), dtype=np.float64)
+        for r, ci in enumerate(num_ci):
+            lib.shifu_csv_numeric(h, ci, M[r].ctypes.data)
+            out[ci] = ("num", M[r], [])
         for ci, k in enumerate(kinds):
             if k == 1:
-                a = np.empty(n, dtype=np.float64)
-                lib.shifu_csv_numeric(h, ci, a.ctypes.data)
-                out[ci] = ("num", a, [])
+                continue
             elif k == 2:
                 a = np.empty(n, dtype=np.int32)
                 lib.shifu_csv_codes(h, ci, a.ctypes.data)
@@ -263,6 +269,27 @@ def _parse_parquet(path: str, header: list, kinds: list, missing: list):
                 codes[i] = -1 if s in miss else d.setdefault(s, len(d))
             out[ci] = ("str", codes, list(d.keys()))
     return n, 0, out
+
+
+def numeric_rows(arrays: list):
+    """If every array is a full row of one C-contiguous 2-D float64 matrix (the parser's
+    column-major block, see ``_parse_native``) -> (matrix, row indices); else None."""
+    if not arrays:
+        return None
+    base = arrays[0].base
+    if not isinstance(base, np.ndarray) or base.ndim != 2 or base.dtype != np.float64 \
+            or not base.flags.c_contiguous or base.shape[1] != len(arrays[0]):
+        return None
+    p0, rb = base.ctypes.data, base.strides[0]
+    idx = np.empty(len(arrays), dtype=np.int64)
+    for j, a in enumerate(arrays):
+        if a.base is not base or a.dtype != np.float64 or a.ndim != 1 or a.strides[0] != 8:
+            return None
+        off = a.ctypes.data - p0
+        if off % rb or len(a) != base.shape[1]:
+            return None
+        idx[j] = off // rb
+    return base, idx
 
 
 def column_kinds(header: list, numeric: list | None = None, strings: list | None = None) -> list:

@@ -45,7 +45,7 @@ class NpyAppender:
         a = np.ascontiguousarray(a, dtype=self.dtype)
         if a.shape[1:] != self.row_shape:
             raise ValueError(f"{self.path}: row shape {a.shape[1:]} != {self.row_shape}")
-        self.f.write(a.tobytes(order="C"))
+        self.f.write(memoryview(a.reshape(-1).view(np.uint8)) if a.size else b"")   # no tobytes() copy
         self.rows += a.shape[0]
 
     def close(self) -> int:

@@ -26,7 +26,7 @@ from .purifier import DatasetPlan, finish_table
 from .reader import column_kinds, list_data_files, parse_block, table_from_parts, _parse_parquet
 
 DEFAULT_CHUNK_BYTES = 256 << 20
-PREFETCH_READ = int(os.environ.get("SHIFU_READ_PREFETCH", "2"))   # blocks read ahead of the parse
+PREFETCH_READ = int(os.environ.get("SHIFU_READ_PREFETCH", "1"))   # blocks read ahead of the parse
 
 
 def _units(files):
@@ -80,7 +80,7 @@ def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int
             need = len(carry) + want
             buf = bufs[k]
             if buf is None or len(buf) < need:
-                buf = bufs[k] = bytearray(max(need, chunk_bytes + (1 << 16)))
+                buf = bufs[k] = bytearray(need + (1 << 16))   # sized to the block: small ranges stay small
             mv = memoryview(buf)
             c = len(carry)
             mv[:c] = carry
@@ -126,10 +126,11 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
                 data = data[nl + 1:] if nl >= 0 else b""
             yield (fi, 0), parse_block(data, plan.delim, kinds, plan.missing, nthreads)
             continue
-        # the file reads run one thread ahead of the parse (readinto and the native parser both
-        # release the GIL); PREFETCH_READ + 3 buffers cover the queue, the block being parsed and
-        # the one being filled
-        blocks = (prefetched(lambda: _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + 3), PREFETCH_READ)
+        # the file reads run on their own thread, PREFETCH_READ blocks ahead of the parse (readinto
+        # and the native parser both release the GIL).  PREFETCH_READ + 2 buffers: the block being
+        # parsed (its parse copies everything out before the next block is requested), the queued
+        # ones and the one being filled
+        blocks = (prefetched(lambda: _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + 2), PREFETCH_READ)
                   if PREFETCH_READ > 0 else _lines_in_range(path, a, b, chunk_bytes))
         for off, data in blocks:
             if plan.skip_header_line and fi == 0 and off == 0:

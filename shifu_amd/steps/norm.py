@@ -180,21 +180,34 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
                "w": NpyAppender(os.path.join(out_tree, pdir, "w.npy"), np.float32)}
     counters = {}
     n_local = 0
+
+    def write(res, y, w):
+        apx[xname].append(res[xname])
+        apx["y"].append(y)
+        apx["w"].append(w)
+        if is_tree:
+            apt["codes"].append(res["codes"])
+            apt["y"].append(y)
+            apt["w"].append(w)
+
+    # the cache writes of chunk i (file writes release the GIL) run on a writer thread while
+    # chunk i+1 is normalized; one write in flight keeps the part files in row order
+    from concurrent.futures import ThreadPoolExecutor
+    pending = None
     try:
-        for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, sample_rate, neg_only, seed,
-                                     row0=row0):
-            res = nplan.run(md.table)
-            y, w = md.y.astype(np.float32), md.w.astype(np.float32)
-            apx[xname].append(res[xname])
-            apx["y"].append(y)
-            apx["w"].append(w)
-            if is_tree:
-                apt["codes"].append(res["codes"])
-                apt["y"].append(y)
-                apt["w"].append(w)
-            n_local += md.n
-            for k, v in md.counters.as_dict().items():
-                counters[k] = counters.get(k, 0) + v
+        with ThreadPoolExecutor(1, thread_name_prefix="shifu-norm-write") as ex:
+            for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, sample_rate, neg_only, seed,
+                                         row0=row0):
+                res = nplan.run(md.table)
+                y, w = md.y.astype(np.float32), md.w.astype(np.float32)
+                if pending is not None:
+                    pending.result()
+                pending = ex.submit(write, res, y, w)
+                n_local += md.n
+                for k, v in md.counters.as_dict().items():
+                    counters[k] = counters.get(k, 0) + v
+            if pending is not None:
+                pending.result()
     finally:
         for a in list(apx.values()) + list(apt.values()):
             a.close()

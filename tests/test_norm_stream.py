@@ -152,3 +152,46 @@ def test_streamed_norm_host_memory_bounded_by_chunk(tmp_path):
           % (s_small / 1e6, s_big / 1e6, m_big / 1e6))
     assert s_big - s_small < 24e6, (s_small, s_big)
     assert s_big < 0.6 * m_big, (s_big, m_big)
+
+
+def test_block_matrix_rows_upload_in_place():
+    """The parser's numeric columns are rows of one block matrix; the normalize upload uses them
+    in place (contiguous run, permuted gather, sliced/filtered fallback) and equals the gather."""
+    import numpy as np
+    import torch
+    from shifu_amd.algos.normalize import _raw_matrix, _raw_matrix_dev
+    from shifu_amd.data.reader import numeric_rows, parse_block, table_from_parts
+
+    rng = np.random.default_rng(3)
+    header = [f"c{i}" for i in range(6)]
+    vals = rng.normal(size=(50, 6)).round(3)
+    text = "\n".join("|".join("" if (r * 7 + c) % 11 == 0 else ("ab"[r % 2] if c == 2 else repr(vals[r, c]))
+                              for c in range(6))
+                     for r in range(50)).encode() + b"\n"
+    kinds = [1, 1, 2, 1, 1, 1]
+    part = parse_block(bytearray(text), "|", kinds, ["", "?"], 2)
+    t = table_from_parts(header, kinds, [part])
+
+    class CC:
+        def __init__(self, name, cat=False):
+            self.name, self.cat = name, cat
+            self.bin_category = ["a", "b"]
+
+        def is_categorical(self):
+            return self.cat
+
+    native = numeric_rows([t["c0"].values, t["c1"].values]) is not None
+    for names in (["c3", "c4", "c5"], ["c5", "c0", "c4"], ["c1"]):
+        cols = [CC(n) for n in names]
+        if len(cols) > 1:
+            cols.insert(1, CC("c2", cat=True))          # a host-side categorical row among them
+        want = _raw_matrix(cols, t)
+        got = _raw_matrix_dev(cols, t, torch.device("cpu")).numpy()
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+        np.testing.assert_array_equal(np.nan_to_num(got), np.nan_to_num(want))
+    if native:
+        base, idx = numeric_rows([t[n].values for n in ("c4", "c0")])
+        assert base.shape == (5, 50) and list(idx) == [3, 0]
+    sub = t.take(np.arange(10))
+    assert numeric_rows([sub["c0"].values]) is None            # filtered rows: generic path
+    assert numeric_rows([t["c0"].values[:10]]) is None          # row slices are not full rows
