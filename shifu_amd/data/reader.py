@@ -165,20 +165,21 @@ def _parse_native(data: bytes, delim: str, kinds: list, missing: list, nthreads:
     else:
         buf = ctypes.create_string_buffer(bytes(data), len(data))
         addr = ctypes.addressof(buf)
-    h = lib.shifu_csv_parse(addr, len(data), delim.encode("utf-8"), len(kinds), kinds_arr, miss, nthreads)
+    h = lib.shifu_csv_scan(addr, len(data), delim.encode("utf-8"), len(kinds), kinds_arr, miss, nthreads)
     if not h:
         return None
     try:
         n = lib.shifu_csv_nrows(h)
-        bad = lib.shifu_csv_bad_rows(h)
-        out = {}
-        # numeric columns land in the rows of ONE column-major matrix: each column is a row view,
-        # and consumers that need several columns as a matrix (normalize, stats uploads) can use
-        # the rows in place (see ``numeric_rows``) instead of gathering them
+        # numeric columns are parsed straight into the rows of ONE column-major matrix: each
+        # column is a row view, and consumers that need several columns as a matrix (normalize,
+        # stats uploads) use the rows in place (see ``numeric_rows``) instead of gathering them
         num_ci = [ci for ci, k in enumerate(kinds) if k == 1]
         M = np.empty((len(num_ci), n), dtype=np.float64)
+        if lib.shifu_csv_fill(h, M.ctypes.data if M.size else None, max(n, 1)) != 0:
+            return None
+        bad = lib.shifu_csv_bad_rows(h)
+        out = {}
         for r, ci in enumerate(num_ci):
-            lib.shifu_csv_numeric(h, ci, M[r].ctypes.data)
             out[ci] = ("num", M[r], [])
         for ci, k in enumerate(kinds):
             if k == 1:

@@ -97,6 +97,8 @@ HIP_SIGNATURES = {
 # host runtime: name -> (argsig, restype)
 RT_SIGNATURES = {
     "shifu_csv_parse": ("plPipPi", "p"),
+    "shifu_csv_scan": ("plPipPi", "p"),
+    "shifu_csv_fill": ("ppl", "i"),
     "shifu_csv_nrows": ("p", "l"),
     "shifu_csv_bad_rows": ("p", "l"),
     "shifu_csv_numeric": ("pip", "i"),

@@ -7,6 +7,9 @@
 //   * numeric columns -> double (NaN for missing / unparseable, the reference's "invalid")
 //   * string columns  -> int32 dictionary codes (-1 = missing) + per-column dictionary
 // Output is column-major so each column becomes one contiguous array (columnar cache).
+// Two-phase use (shifu_csv_scan + shifu_csv_fill) writes the numeric columns straight into the
+// caller's [n_numeric][ld] block: no internal per-column vectors, no serial zero-fill + copy-out
+// (the destination's pages are first touched by the parsing threads).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -41,7 +44,9 @@ struct Parser {
   int nthreads = 1;
   // results
   size_t nrows = 0;
-  std::vector<std::vector<double>> num;    // per numeric column
+  std::vector<std::vector<double>> num;    // per numeric column (internal storage, shifu_csv_parse)
+  std::vector<double*> numptr;             // per numeric column: where its rows are written
+  std::vector<struct Chunk>* chunks = nullptr;
   std::vector<std::vector<int32_t>> codes; // per string column
   std::vector<std::vector<std::string>> dicts;
   std::vector<int> num_idx, str_idx;       // column -> slot
@@ -157,7 +162,7 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
     const bool miss = P.is_missing(v);
     if (k == 1) {
       bool ok = false;
-      P.num[P.num_idx[col]][r] = miss ? NAN : parse_double(v, ok);
+      P.numptr[P.num_idx[col]][r] = miss ? NAN : parse_double(v, ok);
     } else {
       int32_t code = -1;
       if (!miss) {
@@ -203,11 +208,11 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
       }
       if (fast && i == p) {                        // empty field: missing (token or not)
         b = i;
-        P.num[P.num_idx[col]][r] = NAN;
+        P.numptr[P.num_idx[col]][r] = NAN;
       } else if (fast && any && m < (1ull << 53) && frac <= 22) {
         b = i;
         const double v = frac ? (double)m / kPow10[frac] : (double)m;
-        P.num[P.num_idx[col]][r] = neg ? -v : v;
+        P.numptr[P.num_idx[col]][r] = neg ? -v : v;
       } else {
         b = field_end(p);
         general(p, b);
@@ -223,7 +228,7 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
   if (col != P.ncols) {
     bad.fetch_add(1);
     for (int cc = col; cc < P.ncols; ++cc) {   // short row: rest missing
-      if (P.kinds[cc] == 1) P.num[P.num_idx[cc]][r] = NAN;
+      if (P.kinds[cc] == 1) P.numptr[P.num_idx[cc]][r] = NAN;
       else if (P.kinds[cc] == 2) P.codes[P.str_idx[cc]][r] = -1;
     }
   }
@@ -242,10 +247,11 @@ void parse_chunk(Parser& P, Chunk& c, std::atomic<int64_t>& bad) {
 
 }  // namespace
 
-// Parse `buf` (len bytes).  kinds[ncols]: 0 skip, 1 numeric, 2 string.  missing: '\n'-joined
-// tokens.  Returns an opaque handle (nullptr on error); read results with the getters.
-SHIFU_RT_API void* shifu_csv_parse(const char* buf, long len, const char* delim, int ncols, const int* kinds,
-                                   const char* missing, int nthreads) {
+// Phase 1: split `buf` (len bytes) at line boundaries over `nthreads` threads and count the
+// rows.  kinds[ncols]: 0 skip, 1 numeric, 2 string.  missing: '\n'-joined tokens.  Returns an
+// opaque handle (nullptr on error); shifu_csv_nrows gives the row count for sizing the output.
+SHIFU_RT_API void* shifu_csv_scan(const char* buf, long len, const char* delim, int ncols, const int* kinds,
+                                  const char* missing, int nthreads) {
   auto* P = new Parser();
   P->buf = buf;
   P->len = (size_t)len;
@@ -276,7 +282,8 @@ SHIFU_RT_API void* shifu_csv_parse(const char* buf, long len, const char* delim,
   }
   // chunking at line boundaries
   const int T = P->nthreads;
-  std::vector<Chunk> chunks(T);
+  P->chunks = new std::vector<Chunk>(T);
+  auto& chunks = *P->chunks;
   size_t pos = 0;
   for (int t = 0; t < T; ++t) {
     size_t target = (P->len * (t + 1)) / T;
@@ -297,18 +304,39 @@ SHIFU_RT_API void* shifu_csv_parse(const char* buf, long len, const char* delim,
   size_t rows = 0;
   for (auto& c : chunks) { c.row_offset = rows; rows += c.line_starts.size(); }
   P->nrows = rows;
-  P->num.assign(nn, std::vector<double>(rows));
+  return P;
+}
+
+// Phase 2: parse every row.  num_out: the numeric columns (in column order) as the rows of a
+// [n_numeric][ld] double block (ld >= nrows), or nullptr for internal storage (then read them
+// with shifu_csv_numeric).  String columns -> codes + dictionaries (shifu_csv_codes / _dict).
+SHIFU_RT_API int shifu_csv_fill(void* h, double* num_out, long ld) {
+  auto* P = (Parser*)h;
+  if (!P || !P->chunks) return -1;
+  auto& chunks = *P->chunks;
+  const size_t rows = P->nrows;
+  int nn = 0, ns = 0;
+  for (int c = 0; c < P->ncols; ++c) nn += P->kinds[c] == 1, ns += P->kinds[c] == 2;
+  P->numptr.assign(nn, nullptr);
+  if (num_out) {
+    if (ld < (long)rows) return -2;
+    for (int i = 0; i < nn; ++i) P->numptr[i] = num_out + (size_t)i * (size_t)ld;
+  } else {
+    P->num.assign(nn, std::vector<double>(rows));
+    for (int i = 0; i < nn; ++i) P->numptr[i] = P->num[i].data();
+  }
   P->codes.assign(ns, std::vector<int32_t>(rows));
   std::atomic<int64_t> bad{0};
   {
     std::vector<std::thread> th;
+    const int T = (int)chunks.size();
     for (int t = 0; t < T; ++t) th.emplace_back([&, t] { parse_chunk(*P, chunks[t], bad); });
     for (auto& x : th) x.join();
   }
   P->bad_rows = bad.load();
   // merge dictionaries in chunk order (first-seen order across the file) and remap codes
   P->dicts.assign(ns, {});
-  for (int c = 0; c < ncols; ++c) {
+  for (int c = 0; c < P->ncols; ++c) {
     if (P->kinds[c] != 2) continue;
     const int si = P->str_idx[c];
     std::unordered_map<std::string, int32_t> global;
@@ -333,7 +361,23 @@ SHIFU_RT_API void* shifu_csv_parse(const char* buf, long len, const char* delim,
       }
     }
   }
-  return P;
+  for (auto& ch : chunks) {                     // release the per-chunk line tables / local dicts
+    std::vector<size_t>().swap(ch.line_starts);
+    ch.local_dict.clear();
+    ch.local_list.clear();
+  }
+  return 0;
+}
+
+// One-call form: scan + fill into internal storage.
+SHIFU_RT_API void* shifu_csv_parse(const char* buf, long len, const char* delim, int ncols, const int* kinds,
+                                   const char* missing, int nthreads) {
+  void* h = shifu_csv_scan(buf, len, delim, ncols, kinds, missing, nthreads);
+  if (h && shifu_csv_fill(h, nullptr, 0) != 0) {
+    delete (Parser*)h;
+    return nullptr;
+  }
+  return h;
 }
 
 SHIFU_RT_API long shifu_csv_nrows(void* h) { return (long)((Parser*)h)->nrows; }
@@ -342,8 +386,8 @@ SHIFU_RT_API long shifu_csv_bad_rows(void* h) { return (long)((Parser*)h)->bad_r
 SHIFU_RT_API int shifu_csv_numeric(void* h, int col, double* out) {
   auto* P = (Parser*)h;
   if (col < 0 || col >= P->ncols || P->num_idx[col] < 0) return -1;
-  const auto& v = P->num[P->num_idx[col]];
-  if (!v.empty()) memcpy(out, v.data(), v.size() * sizeof(double));   // (empty input: no rows)
+  const double* v = P->numptr.empty() ? nullptr : P->numptr[P->num_idx[col]];
+  if (v && P->nrows && v != out) memcpy(out, v, P->nrows * sizeof(double));   // (empty input: no rows)
   return 0;
 }
 
@@ -379,4 +423,9 @@ SHIFU_RT_API long shifu_csv_dict_size(void* h, int col) {
   return (long)P->dicts[P->str_idx[col]].size();
 }
 
-SHIFU_RT_API void shifu_csv_free(void* h) { delete (Parser*)h; }
+SHIFU_RT_API void shifu_csv_free(void* h) {
+  auto* P = (Parser*)h;
+  if (!P) return;
+  delete P->chunks;
+  delete P;
+}
