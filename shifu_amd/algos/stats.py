@@ -228,8 +228,13 @@ def upload_columns(cols, dev) -> torch.Tensor:
     if st["ev"][i] is not None:
         st["ev"][i].synchronize()                 # the copy that last read this buffer is done
     host = buf[: C * n].numpy().reshape(C, n)
-    for k, v in enumerate(cols):
-        host[k] = v
+    from ..data.reader import numeric_rows
+    hit = numeric_rows(cols)
+    if hit is not None and np.array_equal(hit[1], np.arange(hit[1][0], hit[1][0] + C)):
+        host[:] = hit[0][hit[1][0]: hit[1][0] + C]     # a run of the parser's block rows: one memcpy
+    else:
+        for k, v in enumerate(cols):
+            host[k] = v
     out.copy_(buf[: C * n].view(C, n), non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
