@@ -2,7 +2,8 @@
 the same synthetic text data, runs init, then each requested step under cProfile, and prints the
 step's wall time plus the top functions by cumulative time.
 
-    python tools/pipe_lab.py [--rows 500000] [--cols 1600] [--steps stats norm varsel] [--top 25]
+    python tools/pipe_lab.py [--rows 500000] [--cols 1600] [--steps stats norm varsel train eval] [--top 25]
+(eval runs on an eval set of --rows / 4 rows, as in the pipeline bench)
 """
 import argparse
 import cProfile
@@ -43,14 +44,20 @@ def main():
     t0 = time.perf_counter()
     if _native.rt().shifu_gen_csv(d.encode(), a.rows, a.cols, 3, 11, 0.02, 20, 16):
         raise SystemExit("generation failed")
+    e = os.path.join(root, "data", "EvalSet1")
+    os.makedirs(e)
+    if "eval" in a.steps and _native.rt().shifu_gen_csv(e.encode(), max(1, a.rows // 4), a.cols, 3, 12, 0.02, 20, 16):
+        raise SystemExit("generation failed")
     print(f"generated {a.rows} x {a.cols} in {time.perf_counter() - t0:.1f}s", flush=True)
-    with open(os.path.join(d, ".pig_header"), "w") as f:
-        f.write("|".join(["id", "diagnosis", "wgt"] + [f"num_{j}" for j in range(a.cols)] +
-                         [f"cat_{j}" for j in range(3)]) + "\n")
+    for dd in (d, e):
+        with open(os.path.join(dd, ".pig_header"), "w") as f:
+            f.write("|".join(["id", "diagnosis", "wgt"] + [f"num_{j}" for j in range(a.cols)] +
+                             [f"cat_{j}" for j in range(3)]) + "\n")
     mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
-    mc.dataSet["dataPath"], mc.dataSet["headerPath"] = d, os.path.join(d, ".pig_header")
-    mc.dataSet["targetColumnName"], mc.dataSet["posTags"], mc.dataSet["negTags"] = "diagnosis", ["M"], ["B"]
-    mc.dataSet["weightColumnName"] = "wgt"
+    for sec, dd in ((mc.dataSet, d), (mc.evals[0].dataSet, e)):
+        sec["dataPath"], sec["headerPath"] = dd, os.path.join(dd, ".pig_header")
+        sec["targetColumnName"], sec["posTags"], sec["negTags"] = "diagnosis", ["M"], ["B"]
+        sec["weightColumnName"] = "wgt"
     with open(os.path.join(root, "columns", "meta.column.names"), "w") as f:
         f.write("id\n")
     with open(os.path.join(root, "columns", "categorical.column.names"), "w") as f:
@@ -60,7 +67,11 @@ def main():
     mc.train["numTrainEpochs"] = 10
     mc.save()
     api.InitStep(root).process()
-    steps = {"stats": api.StatsStep, "norm": api.NormStep, "varsel": api.VarSelStep, "train": api.TrainStep}
+    mc.varSelect["autoFilterEnable"] = False
+    mc.train["baggingNum"] = 1
+    mc.save()
+    steps = {"stats": api.StatsStep, "norm": api.NormStep, "varsel": api.VarSelStep, "train": api.TrainStep,
+             "eval": api.EvalStep}
     for name in a.steps:
         pr = cProfile.Profile()
         t0 = time.perf_counter()
