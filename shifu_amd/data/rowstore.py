@@ -154,11 +154,15 @@ def load_parts(path: str, meta: dict, mmap: bool = True) -> dict:
 class Bf16Rows:
     """Float view of a bf16 GEMM-ready NormalizedData matrix (``Xb``: uint16 bf16 bits
     [n, kpad], values in the first ``width`` columns, bias column 1.0 at ``width``).  Row /
-    column indexing returns float32 values of the ``width`` input columns; ``raw`` is the padded
-    bf16 matrix that the MLP trainer streams to HBM without any cast or padding pass."""
+    column indexing returns float32 values of the input columns; ``raw`` is the padded
+    bf16 matrix that the MLP trainer streams to HBM without any cast or padding pass.
+    ``cols``: the raw columns this view exposes (a model's input subset, :meth:`subset`);
+    :meth:`device_rows` moves the bf16 bits to the GPU as they are (no host fp32 expansion)."""
 
-    def __init__(self, raw, width: int):
-        self.raw, self.width = raw, int(width)
+    def __init__(self, raw, width: int, cols=None):
+        self.raw = raw
+        self.cols = None if cols is None else np.asarray(cols, dtype=np.int64)
+        self.width = int(width) if self.cols is None else len(self.cols)
         self.shape = (len(raw), self.width)
         self.dtype = np.dtype(np.float32)
         self.ndim = 2
@@ -175,12 +179,44 @@ class Bf16Rows:
         u = np.ascontiguousarray(u16, dtype=np.uint16)
         return (u.astype(np.uint32) << 16).view(np.float32)
 
+    def subset(self, idx) -> "Bf16Rows":
+        """The view of input columns ``idx`` (positions in this view)."""
+        base = np.arange(self.width) if self.cols is None else self.cols
+        return Bf16Rows(self.raw, len(idx), base[np.asarray(idx, dtype=np.int64)])
+
+    def device_rows(self, device, rows=None, block: int = 1 << 18):
+        """bf16 torch tensor [len(rows), width] on ``device``: the raw bits are uploaded in row
+        blocks (``rows``: optional SORTED row index array, gathered on the device) and the
+        columns picked on the device."""
+        import torch
+        n = len(self.raw)
+        out = torch.empty((n if rows is None else len(rows), self.width), dtype=torch.bfloat16, device=device)
+        cols_d = None if self.cols is None else torch.as_tensor(self.cols, device=device)
+        ridx = None if rows is None else np.asarray(rows, dtype=np.int64)
+        lo_out = 0
+        for r0 in range(0, n, block):
+            r1 = min(n, r0 + block)
+            if ridx is not None:
+                a, b = np.searchsorted(ridx, r0), np.searchsorted(ridx, r1)
+                if a == b:
+                    continue
+                sel = ridx[a:b]
+                r0, r1 = int(sel[0]), int(sel[-1]) + 1
+            blk = torch.as_tensor(np.ascontiguousarray(self.raw[r0:r1]).view(np.int16), device=device)
+            blk = blk.view(torch.bfloat16)
+            if ridx is not None:
+                blk = blk.index_select(0, torch.as_tensor(sel - r0, device=device))
+            blk = blk[:, : self.width] if cols_d is None else blk.index_select(1, cols_d)
+            out[lo_out: lo_out + len(blk)] = blk
+            lo_out += len(blk)
+        return out
+
     def __getitem__(self, idx):
         rest = ()
         if isinstance(idx, tuple):
             idx, rest = idx[0], idx[1:]
         rows = self.raw[idx]
-        out = self.to_f32(rows[..., : self.width])
+        out = self.to_f32(rows[..., : self.width] if self.cols is None else rows[..., self.cols])
         return out[(slice(None),) + rest] if rest else out
 
     def __array__(self, dtype=None, copy=None):

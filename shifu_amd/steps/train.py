@@ -147,6 +147,9 @@ def _subset_cache(meta, arr, want, is_tree):
     if len(idx) == len(inums):
         return meta, arr
     meta = dict(meta, input_nums=[inums[i] for i in idx], input_names=[meta["input_names"][i] for i in idx])
+    from ..data.rowstore import Bf16Rows
+    if isinstance(arr["X"], Bf16Rows):          # bf16 cache: a column view, nothing expanded on the host
+        return meta, dict(arr, X=arr["X"].subset(idx))
     return meta, dict(arr, X=np.asarray(arr["X"])[:, idx])
 
 
@@ -521,7 +524,15 @@ class TrainStep:
         yy = yy.reshape(len(y), -1)
         w = np.asarray(ts.w, dtype=np.float32) * sw
         tri = np.nonzero(train_m)[0]
-        data = tr.prepare(torch.from_numpy(np.asarray(X[tri], dtype=np.float32)), yy[tri], w[tri])
+        from ..data.rowstore import Bf16Rows
+
+        def rows_of(A, idx):
+            # bf16 NormalizedData goes to HBM as its bf16 bits (rows / columns gathered on the
+            # device); anything else as fp32 host rows
+            if isinstance(A, Bf16Rows) and tr.gpu:
+                return A.device_rows(tr.device, rows=idx)
+            return torch.from_numpy(np.asarray(A[idx] if idx is not None else A, dtype=np.float32))
+        data = tr.prepare(rows_of(X, tri), yy[tri], w[tri])
         vdata = None
         if vX is not None:
             vy = np.asarray(ts.vy, np.float32)
@@ -529,11 +540,10 @@ class TrainStep:
                 vy = (np.rint(vy) == ova_class).astype(np.float32)
             if multi:
                 vy = np.eye(n_out, dtype=np.float32)[np.clip(np.rint(vy).astype(int), 0, n_out - 1)]
-            vdata = tr.prepare(torch.from_numpy(np.asarray(vX, np.float32)), vy.reshape(len(vy), -1),
-                               np.asarray(ts.vw, np.float32))
+            vdata = tr.prepare(rows_of(vX, None), vy.reshape(len(vy), -1), np.asarray(ts.vw, np.float32))
         elif valid_m.any():
             vi = np.nonzero(valid_m)[0]
-            vdata = tr.prepare(torch.from_numpy(np.asarray(X[vi], np.float32)), yy[vi], np.asarray(ts.w)[vi])
+            vdata = tr.prepare(rows_of(X, vi), yy[vi], np.asarray(ts.w)[vi])
         n_train = torch.tensor([float(len(tri))], dtype=torch.float64, device=tr.device)
         dist.all_reduce_(n_train)
         n_train = float(n_train.item())

@@ -44,7 +44,7 @@ def _history_append(ms, changes, reason):
             f.write(f"{c.num},{c.name},{str(old).lower()},{str(new).lower()},{reason}\n")
 
 
-def _normalized_rows(ms, cols):
+def _normalized_rows(ms, cols, device=None):
     """This rank's (X fp32 [n, len(cols)], y, w) from the norm step's NormalizedData when it holds
     exactly the candidate columns (the usual init -> stats -> norm -> varsel order); None otherwise.
     The reference's SE job reads the normalized training data too (VarSelectMapper); reading it
@@ -58,7 +58,16 @@ def _normalized_rows(ms, cols):
     if meta.get("input_nums") != [c.num for c in cols] or "X" not in arr or "y" not in arr:
         return None
     info = dist.info()
-    X = np.asarray(_shard(arr["X"], info), dtype=np.float32)
+    from ..data.rowstore import Bf16Rows
+    from ..utils.device import default_device
+    dev = torch.device(device) if device is not None else default_device()
+    if isinstance(arr["X"], Bf16Rows) and dev.type == "cuda":
+        # bf16 cache on a GPU: the rank's rows go to HBM as bf16 bits (no host fp32 expansion)
+        n = len(arr["X"])
+        lo, hi = n * info.rank // info.world_size, n * (info.rank + 1) // info.world_size
+        X = arr["X"].device_rows(dev, rows=np.arange(lo, hi) if (lo, hi) != (0, n) else None)
+    else:
+        X = np.asarray(_shard(arr["X"], info), dtype=np.float32)
     y = np.asarray(_shard(arr["y"], info), dtype=np.float32).reshape(len(X), -1)[:, :1]
     w = np.asarray(_shard(arr["w"], info), dtype=np.float32) if "w" in arr else np.ones(len(X), np.float32)
     _log.info("varsel: sensitivity rows from NormalizedData (%d x %d)", X.shape[0], X.shape[1])
@@ -83,7 +92,7 @@ def _train_quick_nn(ms, cols, epochs, device=None, seed=0, rows=None):
     from ..utils.device import default_device
     dev = torch.device(device) if device is not None else default_device()
     tr = MLPTrainer(spec, dev, str(p.get("Propagation", "R")), float(p.get("LearningRate", 0.1)), seed=seed)
-    data = tr.prepare(torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)), y, w)
+    data = tr.prepare(X if torch.is_tensor(X) else torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)), y, w)
     for _ in range(max(1, epochs)):
         tr.step(data)
     ws = tr.params.views()
@@ -120,7 +129,7 @@ def select_by_sensitivity(ms, by="SE", device=None, seed=0):
         return []
     epochs = max(1, int(mc.train.get("numTrainEpochs", 100)) // 2)
     net = _reusable_se_model(ms, cols)
-    rows = _normalized_rows(ms, cols)
+    rows = _normalized_rows(ms, cols, device)
     if net is not None:
         if rows is not None:
             X = rows[0]

@@ -195,3 +195,83 @@ def test_block_matrix_rows_upload_in_place():
     sub = t.take(np.arange(10))
     assert numeric_rows([sub["c0"].values]) is None            # filtered rows: generic path
     assert numeric_rows([t["c0"].values[:10]]) is None          # row slices are not full rows
+
+
+def test_bf16rows_subset_and_device_rows():
+    """Column subsets of the bf16 NormalizedData view and the bf16-bits upload (rows gathered,
+    columns picked on the device) equal the host fp32 expansion."""
+    import numpy as np
+    import torch
+    from shifu_amd.data.rowstore import Bf16Rows
+
+    rng = np.random.default_rng(5)
+    n, width, kpad = 1000, 37, 128
+    x = torch.from_numpy(rng.normal(size=(n, width)).astype(np.float32)).to(torch.bfloat16)
+    raw = np.zeros((n, kpad), np.uint16)
+    raw[:, :width] = x.view(torch.int16).numpy().view(np.uint16)
+    raw[:, width] = 0x3F80
+    v = Bf16Rows(raw, width)
+    full = np.asarray(v)
+    np.testing.assert_array_equal(full, x.float().numpy())
+    idx = [3, 0, 36, 10]
+    sub = v.subset(idx)
+    assert sub.shape == (n, 4)
+    np.testing.assert_array_equal(np.asarray(sub), full[:, idx])
+    np.testing.assert_array_equal(sub[5:9], full[5:9][:, idx])
+    rows = np.sort(rng.choice(n, 300, replace=False))
+    for view, want in ((v, full), (sub, full[:, idx])):
+        d = view.device_rows(torch.device("cpu"), block=128)
+        assert d.dtype == torch.bfloat16
+        np.testing.assert_array_equal(d.float().numpy(), want)
+        d = view.device_rows(torch.device("cpu"), rows=rows, block=128)
+        np.testing.assert_array_equal(d.float().numpy(), want[rows])
+    np.testing.assert_array_equal(np.asarray(sub.subset([1, 2])), full[:, [0, 36]])
+
+
+@pytest.mark.gpu
+def test_bf16_cache_varsel_train_gpu_match_host_expansion(tmp_path, monkeypatch):
+    """varsel (SE) and NN train read the bf16 NormalizedData as bf16 bits uploaded to HBM
+    (Bf16Rows.device_rows); the result equals the host fp32 expansion route."""
+    import torch
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.data import rowstore
+    from shifu_amd.steps.norm import run_norm
+    from shifu_amd.steps.train import run_train
+    from shifu_amd.steps.varsel import run_varsel
+    a = _model_set(tmp_path, "NN", n_rows=6000)
+    mc = ModelConfig.load(os.path.join(a, "ModelConfig.json"))
+    mc.varSelect["filterBy"], mc.varSelect["filterNum"] = "SE", 5
+    mc.varSelect["autoFilterEnable"] = False
+    mc.train["numTrainEpochs"], mc.train["baggingNum"] = 6, 1
+    mc.save()
+    _set("true", chunk_kb=64, dtype="bf16")
+    try:
+        run_norm(a)
+    finally:
+        _set("auto", dtype="float32")
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    calls = []
+    orig = rowstore.Bf16Rows.device_rows
+
+    def spy(self, device, rows=None, block=1 << 18):
+        calls.append(len(self) if rows is None else len(rows))
+        return orig(self, device, rows, block)
+    monkeypatch.setattr(rowstore.Bf16Rows, "device_rows", spy)
+    run_varsel(a)
+    run_train(a)
+    assert len(calls) >= 2, calls                       # varsel rows + train rows went as bf16
+
+    def host(self, device, rows=None, block=1 << 18):   # the previous route: fp32 on the host
+        x = np.asarray(self) if rows is None else self[rows]
+        return torch.from_numpy(np.ascontiguousarray(x)).to(device, torch.bfloat16)
+    monkeypatch.setattr(rowstore.Bf16Rows, "device_rows", host)
+    run_varsel(b)
+    run_train(b)
+    sa = open(os.path.join(a, "varsel", "se.0")).read().split("\n")
+    sb = open(os.path.join(b, "varsel", "se.0")).read().split("\n")
+    assert [l.split("\t")[:2] for l in sa] == [l.split("\t")[:2] for l in sb]
+    from shifu_amd.formats.nn_format import read_encog
+    na, nb = read_encog(os.path.join(a, "models", "model0.nn")), read_encog(os.path.join(b, "models", "model0.nn"))
+    for wa, wb in zip(na.weights, nb.weights):
+        np.testing.assert_allclose(wa, wb, rtol=0, atol=1e-6)
