@@ -185,9 +185,27 @@ class ModelRunner:
 
     def _normalized(self, table, cache):
         if "X" not in cache:
-            X, _, _ = normalize_table(self.mc, self.ccs, table, columns=self.selected)
-            cache["X"] = X
+            plan = self._norm_plan()
+            if plan is not None:
+                # the norm step's fused K5 pass (the same kernel that wrote the training rows): one
+                # launch per chunk instead of a host numpy pass per column
+                cache["X"] = plan.run(table)["X"]
+            else:
+                X, _, _ = normalize_table(self.mc, self.ccs, table, columns=self.selected)
+                cache["X"] = X
         return cache["X"]
+
+    def _norm_plan(self):
+        """GPU NormPlan of the selected columns (``shifu.eval.gpuNorm``, default true on a GPU;
+        within 1e-6 of the fp64 host oracle, tests/test_stats_kernels_gpu.py); None on the CPU."""
+        if getattr(self, "_nplan", False) is False:
+            self._nplan = None
+            from ..config import environment
+            if self.dev.type == "cuda" and environment.get_bool("shifu.eval.gpuNorm", True):
+                from ..algos.normalize import NormPlan
+                self._nplan = NormPlan(self.mc, self.ccs, self.selected, want_x=True, x_dtype="float32",
+                                       device=self.dev)
+        return self._nplan
 
     def score_models(self, table) -> list:
         """-> list of [N, n_out] raw score arrays (one per model)."""
