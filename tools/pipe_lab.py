@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", nargs="*", default=["stats", "norm"])
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--stream", action="store_true", help="force the streamed stats / norm paths")
+    ap.add_argument("--prefetch", type=int, default=None, help="shifu.data.prefetch (parsed chunks queued ahead)")
     a = ap.parse_args()
     from shifu_amd.config import environment
     from shifu_amd.config.model_config import ModelConfig
@@ -32,6 +33,8 @@ def main():
     from shifu_amd.steps import api
     from shifu_amd.steps.create import create_model_set
     environment.props()["shifu.norm.dtype"] = "bf16"
+    if a.prefetch is not None:
+        environment.props()["shifu.data.prefetch"] = str(a.prefetch)
     if a.stream:
         environment.props()["shifu.stats.streaming"] = "true"
         environment.props()["shifu.norm.streaming"] = "true"
