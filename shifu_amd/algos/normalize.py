@@ -232,12 +232,16 @@ def _raw_matrix_dev(cols, table, dev):
         return torch.as_tensor(_raw_matrix(cols, table), device=dev)
     base, idx = hit
     lo, hi = int(idx.min()), int(idx.max()) + 1
-    blk = torch.as_tensor(base[lo:hi], device=dev)                  # one H2D copy, no host gather
-    if len(num_j) == len(cols) and np.array_equal(idx, np.arange(lo, hi)):
-        return blk
+    if hi - lo <= 2 * len(idx):
+        blk = torch.as_tensor(base[lo:hi], device=dev)              # one H2D copy, no host gather
+        if len(num_j) == len(cols) and np.array_equal(idx, np.arange(lo, hi)):
+            return blk
+        blk = blk.index_select(0, torch.as_tensor(idx - lo, device=dev))
+    else:                                   # a sparse pick of a wide block: gather just those rows
+        blk = torch.as_tensor(base[idx], device=dev)
     out = torch.empty((len(cols), table.n), dtype=torch.float64, device=dev)
     jt = torch.as_tensor(np.asarray(num_j, np.int64), device=dev)
-    out.index_copy_(0, jt, blk.index_select(0, torch.as_tensor(idx - lo, device=dev)))
+    out.index_copy_(0, jt, blk)
     in_blk = set(num_j)
     rest = [j for j in range(len(cols)) if j not in in_blk]
     if rest:

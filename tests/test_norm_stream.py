@@ -181,7 +181,7 @@ def test_block_matrix_rows_upload_in_place():
             return self.cat
 
     native = numeric_rows([t["c0"].values, t["c1"].values]) is not None
-    for names in (["c3", "c4", "c5"], ["c5", "c0", "c4"], ["c1"]):
+    for names in (["c3", "c4", "c5"], ["c5", "c0", "c4"], ["c1"], ["c5", "c0"]):
         cols = [CC(n) for n in names]
         if len(cols) > 1:
             cols.insert(1, CC("c2", cat=True))          # a host-side categorical row among them
