@@ -21,6 +21,8 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
+from ..utils.trace import trace_range
+
 PO_FIELDS = ("binNum", "binLowestScore", "actionRate", "weightedActionRate", "recall", "weightedRecall",
              "precision", "weightedPrecision", "fpr", "weightedFpr", "liftUnit", "weightLiftUnit",
              "scoreCount", "scoreWgtCount", "tp", "fp", "tn", "fn", "weightedTp", "weightedFp", "weightedTn",
@@ -108,13 +110,15 @@ def confusion_sweep_t(score, is_pos, weight=None, device=None, max_score: float 
     s = _as_dev(score, dev)
     p = _as_dev(is_pos, dev)
     w = torch.ones_like(s) if weight is None else _as_dev(weight, dev)
-    order = order_desc(s)
-    s, p, w = s[order], p[order], w[order]
-    z = torch.zeros(1, dtype=torch.float64, device=dev)
-    tp = torch.cat([z, torch.cumsum(p, 0)])
-    fp = torch.cat([z, torch.cumsum(1 - p, 0)])
-    wtp = torch.cat([z, torch.cumsum(p * w, 0)])
-    wfp = torch.cat([z, torch.cumsum((1 - p) * w, 0)])
+    with trace_range("eval.sort"):
+        order = order_desc(s)
+        s, p, w = s[order], p[order], w[order]
+    with trace_range("eval.sweep"):
+        z = torch.zeros(1, dtype=torch.float64, device=dev)
+        tp = torch.cat([z, torch.cumsum(p, 0)])
+        fp = torch.cat([z, torch.cumsum(1 - p, 0)])
+        wtp = torch.cat([z, torch.cumsum(p * w, 0)])
+        wfp = torch.cat([z, torch.cumsum((1 - p) * w, 0)])
     P, Nn, WP, WN = tp[-1], fp[-1], wtp[-1], wfp[-1]
     ms = float(s.max().item()) if max_score is None and s.numel() else (max_score or 0.0)
     sc = torch.cat([torch.tensor([ms], dtype=torch.float64, device=dev), s])

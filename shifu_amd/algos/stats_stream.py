@@ -33,6 +33,7 @@ import os
 import numpy as np
 import torch
 
+from ..utils.trace import trace_range
 from ..utils.log import get_logger
 from . import binning as B
 from . import quantile as Q
@@ -123,10 +124,11 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
         if sm:
             unselected += int((~Q._selmask(y, sm, md.n, y.device)).sum())
         vals_all = []
-        for bt in batches:
-            v = upload(md, bt)
-            bt.eng.pass_a(v, y, w)
-            _track_distinct(bt, v, num_thr)
+        for bi, bt in enumerate(batches):
+            with trace_range(f"stats.passA.batch{bi}"):
+                v = upload(md, bt)
+                bt.eng.pass_a(v, y, w)
+                _track_distinct(bt, v, num_thr)
             vals_all.append(v)
         for cc in categorical:
             _cat_update(cc, md, binary, cat_state[cc.name], cat_missing[cc.name])
@@ -152,7 +154,8 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
         bt.eng.finish_a()
 
     # ---- passes B (one per refinement level) and C --------------------------------------------
-    _run_cut_passes([bt.eng for bt in batches], stream)
+    with trace_range("stats.cut_passes"):
+        _run_cut_passes([bt.eng for bt in batches], stream)
     for bt in batches:
         bt.bounds, bt.distinct = bt.eng.finish()
     # class-restricted cuts that degenerate are redone over all rows, unweighted (reference rule)

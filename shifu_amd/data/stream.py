@@ -135,6 +135,8 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
         for off, data in blocks:
             if plan.skip_header_line and fi == 0 and off == 0:
                 nl = bytes(data[: 1 << 20]).find(b"\n")
+                if nl < 0 and len(data) > (1 << 20):      # a header line wider than 1 MiB
+                    nl = bytes(data).find(b"\n")
                 data = data[nl + 1:] if nl >= 0 else b""
                 if not len(data):
                     continue

@@ -32,6 +32,7 @@ import torch
 
 from ..parallel import dist
 from ..utils.log import get_logger
+from ..utils.trace import trace_range
 
 _log = get_logger("models.gbdt")
 
@@ -297,6 +298,11 @@ class TreeTrainer:
         self.valid_errors: list[float] = []
         self.timings = {"hist": 0.0, "split": 0.0, "partition": 0.0, "apply": 0.0}
         self.level_stats = None        # list -> per-level histogram events (GPU), see bench_rounds
+        # always-on phase accounting (DTWorker's per-phase nanoTime logs, DTWorker.java:581-687):
+        # rows histogrammed so far, and per tree the level table + histogram all-reduce time
+        self.hist_rows_total = 0
+        self.last_tree_stats = None
+        self._ar_events = []
         self._root_level = False
         self._codes_cache = None
         self._nmod, self._npos = 0, data.n
@@ -412,6 +418,8 @@ class TreeTrainer:
                 tree.value[1] = ctot[t, 1] / sw if sw > 0 else 0.0
                 tree.class_value[1] = float(np.argmax(ctot[t])) if sw > 0 else 0.0
         n_leaves = [1] * T
+        level_log = []
+        self.last_tree_stats = {"levels": level_log}
         for level in range(1, c.max_depth):
             if not nodes:
                 break
@@ -429,9 +437,15 @@ class TreeTrainer:
             self._level = level
             self._level_rngs = [rngs[z["tree"]] for z in nodes]
             t0 = time.perf_counter()
-            hist = self._build_and_split(nodes, n_built, gg, w, pos2row, hist_prev)
-            best = hist["best"]            # per slot: (feat, bin, gain, lw, ls, rw, rs, valid)
+            lv_rows = int(sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"]))
+            self.hist_rows_total += lv_rows
+            with trace_range(f"gbdt.level{level}.hist_split"):
+                hist = self._build_and_split(nodes, n_built, gg, w, pos2row, hist_prev)
+                best = hist["best"]            # per slot: (feat, bin, gain, lw, ls, rw, rs, valid)
             self.timings["split"] += time.perf_counter() - t0
+            lv_stat = {"level": level, "nodes": len(nodes), "built": int(n_built), "hist_rows": lv_rows,
+                       "hist_split_ms": (time.perf_counter() - t0) * 1e3}
+            level_log.append(lv_stat)
             # decisions ------------------------------------------------------------------
             split_feat = np.full(len(nodes), -1, dtype=np.int32)
             split_bin = np.full(len(nodes), -1, dtype=np.int32)
@@ -508,9 +522,12 @@ class TreeTrainer:
                            for i in range(len(children))}
             # partition rows of split nodes -----------------------------------------------
             t0 = time.perf_counter()
-            pos2row, pos_node, ranges = self._partition(nodes, split_feat, split_bin, cat_left, pos2row, pos_node,
-                                                        child_slots, (leaf_vals, fuse) if fuse is not None else None)
+            with trace_range(f"gbdt.level{level}.partition"):
+                pos2row, pos_node, ranges = self._partition(nodes, split_feat, split_bin, cat_left, pos2row,
+                                                            pos_node, child_slots,
+                                                            (leaf_vals, fuse) if fuse is not None else None)
             self.timings["partition"] += time.perf_counter() - t0
+            lv_stat["partition_ms"] = (time.perf_counter() - t0) * 1e3
             for i, nz in enumerate(new_nodes):
                 lo, mid, hi = ranges[nz["parent"]]
                 nz["start"], nz["end"] = (lo, mid) if i % 2 == 0 else (mid, hi)
@@ -565,6 +582,35 @@ class TreeTrainer:
             off += len(b)
         items = np.concatenate([b for _, b in blocks]) if blocks else np.zeros((0, 4), np.int32)
         return items, ni, max_items
+
+    def _hist_allreduce(self, h: torch.Tensor) -> None:
+        """All-reduce one level's built-node histograms (one bucket per level), timed: HIP events
+        on the GPU (read when the tree is done), host wall time on the CPU (gloo is synchronous)."""
+        if dist.info().world_size <= 1:
+            return
+        with trace_range("gbdt.hist_allreduce"):
+            if h.is_cuda:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                dist.all_reduce_(h)
+                e1.record()
+                self._ar_events.append((e0, e1))
+            else:
+                t0 = time.perf_counter()
+                dist.all_reduce_(h)
+                self._ar_events.append((time.perf_counter() - t0) * 1e3)
+
+    def _allreduce_ms(self) -> float:
+        """Histogram all-reduce time since the last call (synchronises on pending events)."""
+        ms = 0.0
+        for e in self._ar_events:
+            if isinstance(e, tuple):
+                e[1].synchronize()
+                ms += e[0].elapsed_time(e[1])
+            else:
+                ms += e
+        self._ar_events = []
+        return ms
 
     def _build_and_split(self, nodes, n_built, g, w, pos2row, hist_prev):
         F = self.F
@@ -646,7 +692,7 @@ class TreeTrainer:
         self.timings["hist"] += time.perf_counter() - t0
         # cross-rank reduction of the built-node histograms (one RCCL bucket per level)
         if n_built:
-            dist.all_reduce_(hist[:n_built])
+            self._hist_allreduce(hist[:n_built])
         mptr = None if mask is None else mask.data_ptr()
         cptr = None if cat_order is None else cat_order.data_ptr()
         if n_built:
@@ -773,7 +819,7 @@ class TreeTrainer:
                 hist[z["slot"], 0].view(-1).index_add_(0, idx, qw.unsqueeze(1).expand(-1, F).reshape(-1))
                 hist[z["slot"], 1].view(-1).index_add_(0, idx, qg.unsqueeze(1).expand(-1, F).reshape(-1))
         if n_built:
-            dist.all_reduce_(hist[:n_built])
+            self._hist_allreduce(hist[:n_built])
         for z in nodes:
             if not z["built"]:
                 hist[z["slot"]] = hist_prev[z["parent"]] - hist[z["sib_slot"]]
@@ -871,7 +917,7 @@ class TreeTrainer:
             hist[z["slot"], 0] = hw.view(F, NB)
             hist[z["slot"], 1] = hg.view(F, NB)
         if n_built:
-            dist.all_reduce_(hist[:n_built])
+            self._hist_allreduce(hist[:n_built])
         for z in nodes:
             if not z["built"]:
                 hist[z["slot"]] = hist_prev[z["parent"]] - hist[z["sib_slot"]]
@@ -1063,6 +1109,8 @@ class TreeTrainer:
         out, vout = self._out, self._vout
         for _ in range(n_trees):
             tid = len(self.trees)
+            t_tree = time.perf_counter()
+            rows0 = self.hist_rows_total
             self._reseed_rows(tid)
             if c.is_gbt:
                 w = self._weights_for_tree()
@@ -1117,6 +1165,11 @@ class TreeTrainer:
             self.trees.append(tree)
             self.train_errors.append(terr)
             self.valid_errors.append(verr)
+            st = self.last_tree_stats if c.is_gbt else None
+            self.last_tree_stats = {"tree": tid, "ms": (time.perf_counter() - t_tree) * 1e3,
+                                    "hist_rows": self.hist_rows_total - rows0,
+                                    "allreduce_ms": self._allreduce_ms(),
+                                    "levels": (st or {}).get("levels", [])}
             if callback:
                 callback(tid, tree, terr, verr)
         return self.trees
@@ -1339,10 +1392,18 @@ def _gain_py(imp, lw, ls, rw, rs):
 # ------------------------------------------------------------------------------------------
 # smoke + bench hooks
 # ------------------------------------------------------------------------------------------
-def synthetic_binned(n, f, device, seed=0, n_bins=256):
+def synthetic_binned(n, f, device, seed=0, n_bins=256, labels="favourable"):
     """uint8 codes (quad-blocked [Q, n, 128]) generated chunk-wise on the device (no int32 staging of the whole
-    matrix) + labels from a hidden rule on the first two features."""
+    matrix) + labels.  ``favourable``: a hidden rule on the first two features (later splits peel off
+    small minorities: few rows histogrammed below the root).  ``balanced``: a dense random linear
+    rule over ALL codes thresholded at its median (the codes are iid uniform, so the median of the
+    symmetric score is its mean): every split lands near a feature's median bin and the smaller
+    child of each node holds about half its rows -- the worst case for the histogram work."""
     g = torch.Generator(device=device).manual_seed(seed)
+    wv = None
+    if labels == "balanced":
+        wv = torch.randn(f, generator=g, device=device, dtype=torch.float32)
+        thr = float(wv.sum()) * (n_bins - 1) / 2.0
     ng = (f + FG - 1) // FG
     codes = torch.zeros((f + QF - 1) // QF, n, QF, dtype=torch.uint8, device=device)
     y = torch.empty(n, dtype=torch.float32, device=device)
@@ -1354,9 +1415,13 @@ def synthetic_binned(n, f, device, seed=0, n_bins=256):
             c0, c1 = gi * FG, min(f, (gi + 1) * FG)
             o = (gi % (QF // FG)) * FG
             codes[gi // (QF // FG), r0:r1, o: o + c1 - c0] = blk[:, c0:c1].to(torch.uint8)
-        x0 = blk[:, 0].float() / n_bins
-        x1 = blk[:, 1].float() / n_bins
-        y[r0:r1] = ((x0 + 0.5 * x1 + 0.1 * torch.rand(r1 - r0, generator=g, device=device)) > 0.8).float()
+        if wv is not None:
+            sc = blk.float() @ wv
+            y[r0:r1] = (sc + 0.05 * sc.abs().mean() * torch.randn(r1 - r0, generator=g, device=device) > thr).float()
+        else:
+            x0 = blk[:, 0].float() / n_bins
+            x1 = blk[:, 1].float() / n_bins
+            y[r0:r1] = ((x0 + 0.5 * x1 + 0.1 * torch.rand(r1 - r0, generator=g, device=device)) > 0.8).float()
     nb = np.full(f, n_bins, np.int32)
     return BinnedData(codes, y, None, nb, np.zeros(f, np.uint8), f)
 
@@ -1374,23 +1439,27 @@ def bench_rounds(a, dev, info):
     """GBDT config: 500 trees depth 7, 256-bin histograms, 100M rows x 1000 cols per GPU.
     One step = one boosting round (one tree)."""
     rows = a.rows
-    data = synthetic_binned(rows, a.cols, dev, seed=11 + info.rank)
+    labels = getattr(a, "labels", "favourable")
+    data = synthetic_binned(rows, a.cols, dev, seed=11 + info.rank, labels=labels)
     cfg = TreeConfig("GBT", tree_num=500, max_depth=7, learning_rate=0.05,
                      feature_subset_strategy="ALL", min_instances_per_node=5)
     tr = TreeTrainer(cfg, data)
-    for _ in range(a.warmup):
+    late = int(getattr(a, "late", 0) or 0)
+    for _ in range(a.warmup + late):    # --gbdt-late: time a later window (rounds late+w .. late+w+k)
         tr.train(1)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dist.barrier()
     if dev.type == "cuda" and getattr(a, "levels", False):
         tr.level_stats = []
+    rows0 = tr.hist_rows_total
     t0 = time.perf_counter()
     tr.train(a.steps)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
+    hist_rows = (tr.hist_rows_total - rows0) / max(1, a.steps)
     levels = None
     if tr.level_stats:               # per level: rows histogrammed, bytes of codes read, ms, TB/s
         agg = {}
@@ -1416,7 +1485,10 @@ def bench_rounds(a, dev, info):
         "value": a.steps / dt, "unit": "rounds/s", "n_gpus": info.world_size, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": HIST_DTYPE_LABEL,
-        "data": "synthetic uint8 bin codes, labels from a hidden rule",
+        "data": f"synthetic uint8 bin codes, {labels} labels "
+                + ("(dense linear rule over all codes at its median)" if labels == "balanced"
+                   else "(hidden rule on two features)"),
+        "labels": labels, "hist_rows_per_round": hist_rows, "late_rounds": late,
         "config": {"model": "GBT 500 trees depth=7 256 bins", "global_batch": rows * info.world_size,
                    "seq_len": None, "n_cols": a.cols, "parallelism": f"dp{info.world_size}"},
         "timings_s": tr.timings, "train_error": tr.train_errors[-1], "levels": levels,

@@ -33,7 +33,7 @@ class LRTrainer:
             torch.as_tensor(np.asarray(init, dtype=np.float32))
         self.w = w.to(self.device).contiguous()
         dist.broadcast_(self.w, 0)
-        self.gbuf = torch.zeros(n_in + 3, dtype=torch.float32, device=self.device)
+        self.gbuf = torch.zeros(n_in + 1, dtype=torch.float32, device=self.device)
         self.opt = Optimizer(n_in + 1, self.device, propagation, learning_rate, momentum, adam_beta1, adam_beta2,
                              learning_decay, reg, reg_level, None)
         self.last_error = float("nan")
@@ -62,12 +62,14 @@ class LRTrainer:
         x, y, s = data
         g = self.gbuf
         g.zero_()
+        # [error sum, row count] in fp64 (an fp32 count rounds past 2^24 rows)
+        tail = torch.zeros(2, dtype=torch.float64, device=self.device)
         if self.device.type == "cuda":
             from ..ops import stats_ops           # fused HIP pass (K9): dot + sigmoid + gradient
             r = stats_ops.lr_grad(x, self.w, y, s)
             if r is not None:
                 g[: self.n_in + 1] = r[0]
-                g[self.n_in + 1] = r[1].float()
+                tail[0] = r[1].double()
                 chunk = 0
         for r0 in (range(0, x.shape[0], chunk) if chunk else ()):
             xb, yb, sb = x[r0: r0 + chunk], y[r0: r0 + chunk], s[r0: r0 + chunk]
@@ -76,12 +78,13 @@ class LRTrainer:
             d = e * (p * (1 - p) + FLAT_SPOT) * sb
             g[: self.n_in] += (d.to(xb.dtype) @ xb).float()
             g[self.n_in] += d.sum()
-            g[self.n_in + 1] += (e * e).sum()
-        g[self.n_in + 2] = float(x.shape[0])
-        dist.all_reduce_(g)
-        n = float(g[self.n_in + 2].item())
+            tail[0] += (e.double() * e.double()).sum()
+        tail[1] = float(x.shape[0])
+        dist.all_reduce_(g[: self.n_in + 1])
+        dist.all_reduce_(tail)
+        n = float(tail[1].item())
         self.opt.step(self.w, g[: self.n_in + 1], n)
-        self.last_error = float(g[self.n_in + 1].item()) / max(n, 1.0)
+        self.last_error = float(tail[0].item()) / max(n, 1.0)
         return self.last_error
 
     @torch.no_grad()

@@ -33,6 +33,7 @@ import numpy as np
 import torch
 
 from ..parallel import dist
+from ..utils.trace import trace_range
 from ..utils.log import get_logger
 
 _log = get_logger("models.nn")
@@ -483,7 +484,7 @@ class MLPTrainer:
             self.params.init_random(seed, weight_init)
         dist.broadcast_(self.params.flat, 0)
         self.valid = self.params.valid_mask().to(self.device)
-        # +2 tail slots: [error_sum, weight_sum] fused into the gradient all-reduce
+        # +2 tail slots: an fp32 copy of [error_sum, weight_sum] (reduced in fp64 as self.err_acc)
         self.gbuf = torch.zeros(self.params.numel + 2, dtype=torch.float32, device=self.device)
         self.grad = self.gbuf[: self.params.numel]
         # > 8 MB of gradients under data parallelism: RCCL all-reduce of finished layers' buckets
@@ -909,7 +910,6 @@ class MLPTrainer:
         else:
             self._wflat = self.params.flat
         self.accumulate_gradients(data, row_lo, row_hi)
-        self.gbuf[-2:] = self.err_acc.to(torch.float32)
         ev0 = None
         if self.comm_events is not None:
             if self.gpu:
@@ -917,13 +917,15 @@ class MLPTrainer:
                 ev0.record()
             else:
                 ev0 = time.perf_counter()
-        if self._reducer is not None:
-            self._reducer.wait()                        # launches any bucket not yet in flight
-            tail = self.gbuf[-2:].clone()
-            dist.all_reduce_(tail)
-            self.gbuf[-2:] = tail
-        else:
-            dist.all_reduce_(self.gbuf)
+        with trace_range("nn.grad_allreduce"):
+            if self._reducer is not None:
+                self._reducer.wait()                    # launches any bucket not yet in flight
+            else:
+                dist.all_reduce_(self.grad)
+            # [error sum, weight sum] stay fp64 end to end: an fp32 tail rounds the
+            # weight sum once a rank holds > 2^24 rows (the bench's 125M rows per rank)
+            dist.all_reduce_(self.err_acc)
+        self.gbuf[-2:] = self.err_acc.to(torch.float32)     # fp32 view for callers of the flat buffer
         if ev0 is not None:                             # span of the (final) gradient all-reduce
             if self.gpu:
                 ev1 = torch.cuda.Event(enable_timing=True)
@@ -939,8 +941,8 @@ class MLPTrainer:
     def step(self, data: TrainData, row_lo=0, row_hi=None, num_train_global: float | None = None) -> float:
         """One epoch (iteration): full gradient over the shard, all-reduce, optimizer update.
         Returns the global training error (squared error / (records x outputs))."""
-        gbuf = self.compute_gradients(data, row_lo, row_hi)
-        tail = gbuf[-2:].double().cpu() if not self.gpu else gbuf[-2:].double()
+        self.compute_gradients(data, row_lo, row_hi)
+        tail = self.err_acc
         n_local = (data.n if row_hi is None else row_hi) - row_lo
         if num_train_global is None:
             t = torch.tensor([float(n_local)], dtype=torch.float64, device=self.device)

@@ -29,6 +29,7 @@ __device__ __forceinline__ uint64_t desc_key(double x) {
   uint64_t u = __double_as_longlong(x);
   // NaN scores sort with -inf (last): an integer test (a float x != x may be folded away)
   if ((u & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) u = 0xfff0000000000000ull;
+  if (u == 0x8000000000000000ull) u = 0;               // -0.0 ties with +0.0 (stable row order)
   u = (u >> 63) ? ~u : (u | 0x8000000000000000ull);   // ascending order of x
   return ~u;                                           // descending
 }

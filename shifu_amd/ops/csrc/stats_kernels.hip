@@ -371,9 +371,11 @@ __global__ void __launch_bounds__(256) norm_codes_kernel(NormCodesArgs a) {
     const long r = r0 + k;
     const int f = f0 + tx;
     if (r >= a.n || f >= a.F) continue;
-    const int oc = a.ip[f * 8 + 1];
-    if (a.outf) a.outf[r * a.ldf + oc] = tile[tx][k];
-    if (a.outb) a.outb[r * a.ldb + oc] = f2bf(tile[tx][k]);
+    if (a.outf || a.outb) {                          // a codes-only launch has no ip table
+      const int oc = a.ip[f * 8 + 1];
+      if (a.outf) a.outf[r * a.ldf + oc] = tile[tx][k];
+      if (a.outb) a.outb[r * a.ldb + oc] = f2bf(tile[tx][k]);
+    }
     if (a.codes) a.codes[r * a.ldc + f] = ctile[tx][k];
   }
 }

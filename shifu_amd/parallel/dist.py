@@ -83,7 +83,9 @@ def init_from_env(backend: str | None = None, timeout_s: int = 1800) -> DistInfo
     if use_gpu:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1 and not tdist.is_initialized():
-        be = backend or ("nccl" if use_gpu else "gloo")
+        # SHIFU_DIST_BACKEND=gloo: host-transport collectives on a GPU box (tests of the device
+        # contract with several ranks on one GPU; RCCL refuses two ranks per device)
+        be = backend or os.environ.get("SHIFU_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {}
         if be == "nccl" and use_gpu:
@@ -109,6 +111,37 @@ def shutdown() -> None:
         tdist.destroy_process_group()
 
 
+def coll_device() -> torch.device:
+    """Device a collective's tensors must live on: the rank's GPU under RCCL (``nccl`` cannot
+    reduce host tensors), the host under gloo."""
+    if tdist.is_initialized() and tdist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _compute_device_type() -> str:
+    return "cuda" if torch.cuda.is_available() and os.environ.get("SHIFU_FORCE_CPU") != "1" else "cpu"
+
+
+def _stage_device() -> torch.device:
+    """Where host values are staged for a collective: the collective device, or the rank's GPU
+    under the device-collective guard (a gloo run on a GPU box then follows RCCL's contract)."""
+    if os.environ.get("SHIFU_ASSERT_DEVICE_COLLECTIVES") == "1" and _compute_device_type() == "cuda":
+        return torch.device("cuda", torch.cuda.current_device())
+    return coll_device()
+
+
+def _check(t: torch.Tensor, what: str) -> None:
+    """SHIFU_ASSERT_DEVICE_COLLECTIVES=1: every tensor handed to a collective must be on the
+    device RCCL would need (the rank's GPU whenever there is one), whatever the backend -- so a
+    gloo run on a GPU box (or a CPU run) catches a host tensor that would make RCCL raise."""
+    if os.environ.get("SHIFU_ASSERT_DEVICE_COLLECTIVES") != "1":
+        return
+    want = _compute_device_type()
+    if t.device.type != want:
+        raise AssertionError(f"{what}: collective over a {t.device.type} tensor (rank compute device: {want})")
+
+
 def barrier() -> None:
     if _active():
         if tdist.get_backend() == "nccl":
@@ -120,6 +153,7 @@ def barrier() -> None:
 def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     if not _active():
         return t
+    _check(t, "all_reduce")
     rop = {"sum": tdist.ReduceOp.SUM, "max": tdist.ReduceOp.MAX, "min": tdist.ReduceOp.MIN}[op]
     tdist.all_reduce(t, op=rop)
     return t
@@ -130,8 +164,7 @@ def all_reduce_np(a, op: str = "sum"):
     if not _active():
         return a
     import numpy as np
-    dev = torch.device("cuda", torch.cuda.current_device()) if tdist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(_stage_device())
     all_reduce_(t, op)
     return t.cpu().numpy()
 
@@ -147,6 +180,7 @@ def all_gather_objects(obj) -> list:
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if _active():
+        _check(t, "broadcast")
         tdist.broadcast(t, src=src)
     return t
 
@@ -155,6 +189,7 @@ def all_gather_cat(t: torch.Tensor) -> torch.Tensor:
     """Gather variable-length 1-D tensors from all ranks and concatenate (rank order)."""
     if not _active():
         return t
+    _check(t, "all_gather_cat")
     n = torch.tensor([t.numel()], device=t.device, dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(tdist.get_world_size())]
     tdist.all_gather(sizes, n)
@@ -171,6 +206,7 @@ def gather_cat(t: torch.Tensor, dst: int = 0):
     the others (a tensor gather - no pickling, and only ``dst`` holds the full array)."""
     if not _active():
         return t
+    _check(t, "gather_cat")
     n = torch.tensor([t.numel()], device=t.device, dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(tdist.get_world_size())]
     tdist.all_gather(sizes, n)
@@ -204,6 +240,7 @@ def reduce_scatter_rows(t: torch.Tensor, dim0: bool = False) -> torch.Tensor:
     bytes an all-reduce would leave everywhere).  gloo (no reduce-scatter): all-reduce + slice."""
     if not _active():
         return t
+    _check(t, "reduce_scatter_rows")
     w, r = tdist.get_world_size(), tdist.get_rank()
     F = t.shape[1] if not dim0 else t.shape[0]
     a, b = row_block(F, r, w)
@@ -239,6 +276,7 @@ def gather_rows_to(t: torch.Tensor, n: int, dst: int = 0):
     (None elsewhere)."""
     if not _active():
         return t
+    _check(t, "gather_rows_to")
     w, r = tdist.get_world_size(), tdist.get_rank()
     fb = -(-n // w)
     pad = torch.zeros(fb, t.shape[1], dtype=t.dtype, device=t.device)
@@ -251,7 +289,10 @@ def gather_rows_to(t: torch.Tensor, n: int, dst: int = 0):
 
 
 def all_reduce_max_scalar(x: float, device=None) -> float:
-    t = torch.tensor([x], dtype=torch.float64, device=device or "cpu")
+    """Max of a host scalar over ranks (staged on the collective device: RCCL needs HBM)."""
+    if not _active():
+        return float(x)
+    t = torch.tensor([x], dtype=torch.float64, device=device if device is not None else _stage_device())
     all_reduce_(t, "max")
     return float(t.item())
 
@@ -288,6 +329,7 @@ class BucketedAllReducer:
             lo, hi = self.bounds[bi]
             if lo < start_elem:
                 break
+            _check(self.flat, "bucketed all_reduce")
             h = tdist.all_reduce(self.flat[lo:hi], op=tdist.ReduceOp.SUM, async_op=True)
             self._handles.append(h)
             self._launched += 1

@@ -36,6 +36,8 @@ struct Parser {
   std::vector<int> kinds;                  // 0 skip, 1 numeric, 2 string
   std::unordered_set<std::string> missing; // tokens treated as missing (trimmed)
   std::vector<std::string> miss_list;      // the same, scanned by length + memcmp (no per-field hash)
+  bool numeric_missing = false;            // some missing token is itself a decimal ("-999", "0"):
+                                           // the inline numeric fast path must check the token list
   bool is_missing(std::string_view v) const {
     for (const auto& t : miss_list)
       if (t.size() == v.size() && (v.empty() || memcmp(t.data(), v.data(), v.size()) == 0)) return true;
@@ -209,7 +211,8 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
       if (fast && i == p) {                        // empty field: missing (token or not)
         b = i;
         P.numptr[P.num_idx[col]][r] = NAN;
-      } else if (fast && any && m < (1ull << 53) && frac <= 22) {
+      } else if (fast && any && m < (1ull << 53) && frac <= 22 &&
+                 !(P.numeric_missing && P.is_missing(std::string_view(buf + p, i - p)))) {
         b = i;
         const double v = frac ? (double)m / kPow10[frac] : (double)m;
         P.numptr[P.num_idx[col]][r] = neg ? -v : v;
@@ -270,6 +273,10 @@ SHIFU_RT_API void* shifu_csv_scan(const char* buf, long len, const char* delim, 
     }
   }
   P->miss_list.assign(P->missing.begin(), P->missing.end());
+  for (const auto& t : P->miss_list) {
+    double v;
+    if (!t.empty() && parse_decimal_fast(t, v)) P->numeric_missing = true;
+  }
   P->nthreads = std::max(1, nthreads);
   for (int c = 0; c < ncols; ++c) {
     P->num_idx.push_back(-1);

@@ -263,7 +263,8 @@ def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, no
     lib = _native.rt()
     if write and sort and n_local:
         key = np.load(os.path.join(pdir, "key.npy"), mmap_mode="r")
-        k = np.nan_to_num(np.asarray(key), nan=-np.inf)
+        k = np.asarray(key)
+        k = np.where(np.isnan(k), -np.inf, k)          # NaN ranks with -inf; +-inf stay unclamped
         order = E.order_desc(k)
         blob = np.memmap(os.path.join(pdir, "lines.bin"), dtype=np.uint8, mode="r") if off else np.zeros(1, np.uint8)
         ends = np.ascontiguousarray(np.load(os.path.join(pdir, "ends.npy")))

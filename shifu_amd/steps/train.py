@@ -262,6 +262,25 @@ class TrainStep:
         if self.metrics is not None:
             self.metrics.write(trainer=trainer_id, epoch=epoch, train_error=terr, valid_error=verr, **(extra or {}))
 
+    def _epoch_extra(self, tr, rows: float, secs: float) -> dict:
+        """Per-epoch throughput fields of the metrics stream: whole-job training rows
+        per second, gradient all-reduce milliseconds, HBM in use / peak on this rank."""
+        ar = 0.0
+        for e0, e1 in tr.comm_events or []:
+            if isinstance(e0, float):
+                ar += (e1 - e0) * 1e3
+            else:
+                e1.synchronize()
+                ar += e0.elapsed_time(e1)
+        if tr.comm_events is not None:
+            tr.comm_events.clear()
+        out = {"rows_per_s": round(rows / secs, 1) if secs > 0 else None, "epoch_ms": round(secs * 1e3, 3),
+               "allreduce_ms": round(ar, 3)}
+        if tr.device.type == "cuda":
+            out["hbm_gb"] = round(torch.cuda.memory_allocated(tr.device) / 1e9, 3)
+            out["hbm_peak_gb"] = round(torch.cuda.max_memory_allocated(tr.device) / 1e9, 3)
+        return out
+
     def _train_tensorflow(self) -> int:
         """``algorithm: TENSORFLOW`` (TensorflowTrainer + train.py): a mini-batch DNN trained with
         torch autograd, gradients all-reduced per batch over RCCL; saved as a generic model under
@@ -567,20 +586,25 @@ class TrainStep:
         # MiniBatchs=k: iteration i trains on slice (i-1) mod k of the rows (SubGradient :326-340)
         mb = max(1, min(1000, int(_num(p.get("MiniBatchs"), 1))))
         wd = IterationWatchdog(iteration_limit(3600.0), "NN epoch").__enter__()
+        tr.comm_events = []                    # (start, end) of each gradient all-reduce -> allreduce_ms
         for ep in range(start + 1, epochs + 1):
             wd.tick()
+            t_ep = time.perf_counter()
             with trace_range(f"nn.epoch{ep}"):
                 if mb > 1:
                     b = (ep - 1) % mb
                     lo, hi = data.n * b // mb, data.n * (b + 1) // mb
                     terr = tr.step(data, lo, hi)
+                    rows_ep = n_train / mb
                 else:
                     terr = tr.step(data, num_train_global=n_train)
+                    rows_ep = n_train
+                t_train = time.perf_counter() - t_ep     # step() ends with a host read of the error
                 verr = tr.evaluate(vdata) if vdata is not None else float("nan")
             check_finite("training error", terr, ep)
             if not math.isnan(verr) and verr < best_v:
                 best_v, best_w = verr, tr.params.flat.detach().clone()
-            self._log_epoch(tid, ep, terr, verr)
+            self._log_epoch(tid, ep, terr, verr, extra=self._epoch_extra(tr, rows_ep, t_train))
             if self.info.rank == 0 and ep % factor == 0 and ep < epochs:
                 self._write_nn(tid, spec, tr, tmp_epoch=ep)
                 os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
@@ -753,7 +777,18 @@ class TrainStep:
         stop = [False]
 
         def cb(i, tree, terr, verr):
-            self._log_epoch(tid, i + 1, terr, verr)
+            st = tt.last_tree_stats or {}
+            lv = st.get("levels") or []
+            if lv:          # DTWorker-style phase line (DTWorker.java:581-687, 858-884)
+                _log.debug("tree %d: %.1f ms, hist rows %d, hist allreduce %.2f ms, levels %s", i + 1,
+                           st.get("ms", 0.0), st.get("hist_rows", 0), st.get("allreduce_ms", 0.0),
+                           " ".join(f"L{e['level']}:{e['hist_rows']}r/{e['hist_split_ms']:.1f}"
+                                    f"+{e.get('partition_ms', 0.0):.1f}ms" for e in lv))
+            self._log_epoch(tid, i + 1, terr, verr,
+                            extra={"tree_ms": round(st.get("ms", 0.0), 3), "hist_rows": st.get("hist_rows", 0),
+                                   "allreduce_ms": round(st.get("allreduce_ms", 0.0), 3),
+                                   "levels": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in e.items()}
+                                              for e in lv]})
             if es.update(i + 1, terr, verr):
                 stop[0] = True
         ckpt = os.path.join(ms.pf.checkpoint_dir, f"tree_trainer{tid}.pt")
@@ -770,7 +805,8 @@ class TrainStep:
         wd = IterationWatchdog(iteration_limit(800.0), "tree").__enter__()
         while len(tt.trees) < tree_num:
             wd.tick()
-            tt.train(1, callback=cb)
+            with trace_range(f"gbdt.tree{len(tt.trees) + 1}"):
+                tt.train(1, callback=cb)
             n = len(tt.trees)
             check_finite("training error", tt.train_errors[-1], n)
             if self.info.rank == 0 and n % interval == 0 and n < tree_num:

@@ -34,3 +34,19 @@ def test_bench_gpus1_single_process():
     out = _run(["--gpus", "1", "--rows", "2000", "--cols", "64", "--steps", "1", "--warmup", "0",
                 "--gbdt-steps", "0"])
     assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1"
+
+
+def test_bench_launcher_fails_fast_when_a_rank_dies():
+    """one rank exits at init -> the launcher stops the others and returns non-zero
+    promptly (not after the 1800 s process-group timeout)."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(SHIFU_FORCE_CPU="1", SHIFU_BENCH_FAIL_RANK="1")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--rows", "4000", "--cols", "64",
+                        "--steps", "2", "--warmup", "1", "--gbdt-steps", "0"], capture_output=True, text=True,
+                       env=env, timeout=120, cwd=ROOT)
+    dt = time.monotonic() - t0
+    assert p.returncode != 0, p.stdout
+    assert dt < 30, dt
+    assert "a rank failed" in p.stderr

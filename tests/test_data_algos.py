@@ -42,6 +42,23 @@ def test_native_and_python_parsers_agree(tmp_path):
     assert t["t"].missing_mask().tolist() == [False, False, True, False, False]
 
 
+def test_native_parser_numeric_missing_token(tmp_path):
+    """A missing token that is itself a decimal ("-999", "0") must read as missing on the native
+    parser's inline numeric fast path too (UpdateBinningInfoMapper checks missingOrInvalidValues
+    before parsing); "-999.0" is a different token and stays a number."""
+    rows = ["-999|1", "-999.0|0", "5|-999", "0|2.5", "-999|"]
+    (tmp_path / "part-0").write_text("\n".join(rows) + "\n")
+    miss = ["", "?", "-999", "0"]
+    t = R.read_table(str(tmp_path), ["a", "b"], "|", numeric=["a", "b"], missing=miss)
+    data = (tmp_path / "part-0").read_bytes()
+    n, bad, py = R._parse_python(data, "|", [1, 1], miss)
+    assert t.n == n == 5
+    for ci, c in enumerate(["a", "b"]):
+        np.testing.assert_array_equal(t[c].values, py[ci][1])
+    assert np.isnan(t["a"].values[[0, 3, 4]]).all() and t["a"].values[1] == -999.0
+    assert np.isnan(t["b"].values[[1, 2, 4]]).all() and t["b"].values[3] == 2.5
+
+
 def test_expression_evaluator():
     from shifu_amd.data.reader import Column, RawTable
     cols = {"a": Column("a", "num", np.array([1.0, 2.0, np.nan, 4.0])),

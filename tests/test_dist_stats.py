@@ -128,6 +128,55 @@ def test_cli_pipeline_two_ranks(tmp_path):
     assert abs(perf1["areaUnderRoc"] - perf["areaUnderRoc"]) < 1e-3
 
 
+def _rank_cli_guarded(rank, world, port, root, verb, gpu):
+    """One CLI verb on one rank with SHIFU_ASSERT_DEVICE_COLLECTIVES=1 (every collective tensor on
+    the rank's compute device, RCCL's contract).  gpu: both ranks share cuda:0 over gloo."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SHIFU_ASSERT_DEVICE_COLLECTIVES="1", SHIFU_DIST_BACKEND="gloo")
+    if not gpu:
+        os.environ["SHIFU_FORCE_CPU"] = "1"
+    os.chdir(root)
+    from shifu_amd.cli import main
+    rc = main(verb.split())
+    if rc != 0:
+        raise SystemExit(rc)
+
+
+def _guarded_pipeline(tmp_path, gpu):
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "g", "NN", n_rows=900, n_num=6, n_cat=2)
+    mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+    mc.train["numTrainEpochs"] = 8
+    mc.train["baggingNum"] = 1
+    mc.evals[0]["scoreMetaColumnNameFile"] = "columns/Eval1score.meta.column.names"
+    mc.save()
+    with open(os.path.join(root, "columns", "Eval1score.meta.column.names"), "w") as f:
+        f.write("id\n")                                 # a champion score column: the max goes over ranks
+    run_init(root)
+    for verb in ("stats", "norm", "varsel", "train", "posttrain", "eval"):
+        mp.start_processes(_rank_cli_guarded, args=(2, _port(), root, verb, gpu), nprocs=2, join=True,
+                           start_method="spawn")
+    assert os.path.exists(os.path.join(root, "evals", "Eval1", "id.EvalPerformance.json"))
+    return root
+
+
+def test_cli_two_ranks_device_collective_guard(tmp_path):
+    """the data-parallel verbs incl. eval with score meta columns under the
+    device-collective guard (host run: the guard's contract is the host device)."""
+    _guarded_pipeline(tmp_path, gpu=False)
+
+
+@pytest.mark.gpu
+def test_cli_two_ranks_device_collectives_gpu(tmp_path):
+    """The same two ranks on one GPU (gloo transport, guard on): a collective over a host tensor,
+    which RCCL would reject (the r3 eval champion-score crash), raises here."""
+    import torch
+    assert torch.cuda.is_available()
+    _guarded_pipeline(tmp_path, gpu=True)
+
+
 @pytest.mark.parametrize("alg,shuffle", [("NN", False), ("NN", True), ("GBT", False)])
 def test_norm_two_ranks_match_single(tmp_path, alg, shuffle):
     """Data-parallel norm (each rank normalizes its output row range and writes it in place into

@@ -275,3 +275,49 @@ def test_bf16_cache_varsel_train_gpu_match_host_expansion(tmp_path, monkeypatch)
     na, nb = read_encog(os.path.join(a, "models", "model0.nn")), read_encog(os.path.join(b, "models", "model0.nn"))
     for wa, wb in zip(na.weights, nb.weights):
         np.testing.assert_allclose(wa, wb, rtol=0, atol=1e-6)
+
+
+def _set_norm_type(root, norm_type):
+    from shifu_amd.config.model_config import ModelConfig
+    mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+    mc.normalize["normType"] = norm_type
+    mc.save()
+
+
+@pytest.mark.parametrize("norm_type", ["ONEHOT", "ZSCALE_ONEHOT"])
+def test_streamed_gbt_onehot_norm_equals_in_memory(tmp_path, monkeypatch, norm_type):
+    """Tree model + one-hot norm types (host one-hot columns beside a codes-only K5 launch)."""
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    _check_gbt_onehot(tmp_path, norm_type)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm_type", ["ONEHOT", "ZSCALE_ONEHOT"])
+def test_streamed_gbt_onehot_norm_gpu_equals_in_memory(tmp_path, norm_type):
+    """the codes-only norm_codes_kernel launch (ip == nullptr) of a streamed GBT norm
+    with host one-hot columns runs on the GPU and equals the in-memory CleanedData."""
+    import torch
+    assert torch.cuda.is_available()
+    _check_gbt_onehot(tmp_path, norm_type)
+
+
+def _check_gbt_onehot(tmp_path, norm_type):
+    from shifu_amd.steps.base import load_dataset_cache
+    from shifu_amd.steps.norm import run_norm
+    a = _model_set(tmp_path, "GBT")
+    _set_norm_type(a, norm_type)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    _set("false")
+    run_norm(a)
+    _set("true", chunk_kb=8)
+    try:
+        run_norm(b)
+    finally:
+        _set("auto")
+    for sub in ("CleanedData", "NormalizedData"):
+        ma, xa = load_dataset_cache(os.path.join(a, "tmp", sub), mmap=False)
+        mb, xb = load_dataset_cache(os.path.join(b, "tmp", sub))
+        assert mb["n"] == ma["n"] and mb.get("streamed")
+        for k in xa:
+            np.testing.assert_array_equal(np.asarray(xb[k]), xa[k], err_msg=f"{norm_type} {sub} {k}")

@@ -29,10 +29,7 @@ def test_radix_sort_desc_matches_stable_argsort(n, kind):
     k = np.where(np.isnan(x), -np.inf, x)                 # NaN ranks with -inf (last)
     k = np.where(k == 0.0, 0.0, k)                 # -0.0 == 0.0 ties: keep row order
     want = np.argsort(-k, kind="stable")
-    if kind == "neg":     # the radix key orders -0.0 below +0.0; compare as values + stability per value
-        np.testing.assert_array_equal(x[got], x[want])
-        return
-    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, want)              # -0.0 / +0.0 ties in row order too
 
 
 def test_device_performance_equals_host():
