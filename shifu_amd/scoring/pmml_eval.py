@@ -13,7 +13,9 @@ here, so this module implements the elements the exporter writes, from the PMML 
 * NeuralNetwork (NeuralInputs, NeuralLayer with per-layer ``activationFunction``, Neuron bias +
   Con weights, NeuralOutputs), RegressionModel (NumericPredictor, intercept,
   ``normalizationMethod`` logit/none), TreeModel (Node, first-true-child, ``score``), MiningModel
-  ``Segmentation`` (sum / weightedSum / average / weightedAverage).
+  ``Segmentation`` (sum / weightedSum / average / weightedAverage); ``Constant`` / ``Apply``
+  expressions and the ``Output`` element (predictedValue / transformedValue) of reference-written
+  PMML (``src/test/resources/dttest/model/golf0*.pmml``).
 Records are dicts {field name: raw value (str / float / None)}.
 """
 from __future__ import annotations
@@ -142,6 +144,33 @@ class PMMLModel:
                 if ok_lo and ok_hi:
                     return _num(b.get("binValue"))
             return _num(e.get("defaultValue"))
+        if t == "Constant":
+            v = _num(e.text)
+            return v if v is not None else (e.text or "").strip()
+        if t == "Apply":
+            args = [self._expr(c, vals) for c in e if _strip(c.tag) != "Extension"]
+            fn = e.get("function")
+            if any(a is None for a in args) and fn not in ("isMissing", "isNotMissing", "if"):
+                return _num(e.get("mapMissingTo"))
+            f2 = {"+": lambda a, b: a + b, "-": lambda a, b: a - b, "*": lambda a, b: a * b,
+                  "/": lambda a, b: a / b if b != 0 else None, "pow": lambda a, b: a ** b,
+                  "min": min, "max": max}
+            if fn in f2:
+                r = args[0]
+                for a in args[1:]:
+                    r = f2[fn](r, a)
+                return r
+            f1 = {"log10": math.log10, "ln": math.log, "exp": math.exp, "sqrt": math.sqrt, "abs": abs,
+                  "floor": math.floor, "ceil": math.ceil, "round": round}
+            if fn in f1:
+                return float(f1[fn](args[0]))
+            if fn == "isMissing":
+                return args[0] is None
+            if fn == "isNotMissing":
+                return args[0] is not None
+            if fn == "if":
+                return args[1] if args[0] else (args[2] if len(args) > 2 else None)
+            raise ValueError(f"unsupported PMML function {fn}")
         raise ValueError(f"unsupported PMML expression {t}")
 
     # ---- models -------------------------------------------------------------------------
@@ -242,6 +271,36 @@ class PMMLModel:
     def evaluate(self, records) -> np.ndarray:
         """[N] predictions for a list of records ({field: raw value})."""
         return np.array([self._eval(self.model, r) for r in records], dtype=np.float64)
+
+    def output_fields(self) -> list:
+        out = _kid(self.model, "Output")
+        return [f.get("name") for f in _kids(out, "OutputField")] if out is not None else []
+
+    def evaluate_outputs(self, records) -> dict:
+        """The model's ``Output`` fields per record: ``predictedValue`` (the raw prediction) and
+        ``transformedValue`` (its expression, e.g. Shifu's RawResult x 1000 NormContinuous,
+        PMMLTranslator's score scaling) -> {name: [N] array}.  Without an Output element:
+        {"predicted": evaluate(records)}."""
+        out = _kid(self.model, "Output")
+        if out is None:
+            return {"predicted": self.evaluate(records)}
+        fields = _kids(out, "OutputField")
+        res = {f.get("name"): np.empty(len(records)) for f in fields}
+        for i, r in enumerate(records):
+            y = self._eval(self.model, r)
+            vals = {}
+            for f in fields:
+                feat = f.get("feature", "predictedValue")
+                if feat == "predictedValue":
+                    v = y
+                elif feat == "transformedValue":
+                    ex = [c for c in f if _strip(c.tag) != "Extension"]
+                    v = self._expr(ex[0], vals) if ex else y
+                else:
+                    raise ValueError(f"unsupported OutputField feature {feat}")
+                vals[f.get("name")] = v
+                res[f.get("name")][i] = np.nan if v is None else float(v)
+        return res
 
 
 def records_from_table(table, names) -> list:
