@@ -18,10 +18,16 @@ parameter server + ``SyncReplicasOptimizer`` in DIST mode):
 * every ``CheckpointInterval`` epochs a checkpoint model, and the final model, saved with a
   ``GenericModelConfig.json`` (train.py:349-363) under ``models/<ModelSetName>/``.
 
-MI355X realization: the rows stay resident in HBM, each rank owns a row shard, and every
-mini-batch's gradient is all-reduced (one fused flat buffer) before the replicated optimizer
-step - synchronous SGD with no parameter server (F9 -> F1).  The saved model is a
-``safetensors_mlp`` generic model (``scoring/generic.py``), scored on the GPU by ``eval``.
+MI355X realization (``train_dnn``): the network runs on the framework's own MLP engine
+(``models/nn.py`` MLPTrainer: bf16 rows resident in HBM -- no fp32 copy of the shard -- and the
+hand-written MFMA forward / dgrad / wgrad kernels), with the Encog flat spot off, tf.nn.leaky_relu
+(alpha 0.2) as activation id 9, and the TF update rules of ``optimizer_kernel``
+(``shifu_optimizer_step_tf``: ADAM, plain gradient descent, RMSProp rho 0.9) applied to the batch's
+mean-loss gradient plus the L2 term in one fused pass.  Each rank owns a row shard and every
+mini-batch's gradient is all-reduced before the replicated update -- synchronous SGD with no
+parameter server (F9 -> F1).  ``train_dnn_autograd`` is the torch-autograd formulation of the same
+objective, kept as the test oracle.  The saved model is a ``safetensors_mlp`` generic model
+(``scoring/generic.py``), scored on the GPU by ``eval``.
 """
 from __future__ import annotations
 
@@ -119,9 +125,9 @@ def save_generic(model: DNN, out_dir: str, input_names, meta: dict | None = None
     return path
 
 
-def train_dnn(X: np.ndarray, y: np.ndarray, w: np.ndarray, valid: np.ndarray, params: dict, epochs: int,
-              device, seed: int = 0, log_fn=None, checkpoint_fn=None, grad_hook=None):
-    """Train on this rank's rows; returns (model, [(epoch, train_err, valid_err)])."""
+def train_dnn_autograd(X: np.ndarray, y: np.ndarray, w: np.ndarray, valid: np.ndarray, params: dict, epochs: int,
+                       device, seed: int = 0, log_fn=None, checkpoint_fn=None, grad_hook=None):
+    """torch-autograd oracle of ``train_dnn`` (same batches, objective and optimizer)."""
     hidden = [int(h) for h in (params.get("NumHiddenNodes") or [])]
     acts = list(params.get("ActivationFunc") or [])
     lr = float(params.get("LearningRate", 0.1))
@@ -190,3 +196,136 @@ def train_dnn(X: np.ndarray, y: np.ndarray, w: np.ndarray, valid: np.ndarray, pa
         if checkpoint_fn and ckpt > 0 and ep % ckpt == 0:
             checkpoint_fn(model, ep)
     return model, hist
+
+
+# ------------------------------------------------------------------------------------------------
+# the TENSORFLOW algorithm on the framework's MLP engine
+# ------------------------------------------------------------------------------------------------
+_TF_RULES = {"adam": 4, "gradientdescent": 7, "rmsprop": 9}    # optimizer_kernel rule ids
+
+
+def _mlp_act(name):
+    n, _ = _act(name)
+    return "leakyrelu_tf" if n == "leakyrelu" else n
+
+
+def _tf_step_torch(rule, w, g, s0, s1, lr, gscale, l2, l2mask, it):
+    """CPU oracle of optimizer_kernel's TF path (fp32; Encog ascent direction g)."""
+    g = g * gscale - l2 * w * l2mask
+    if rule == 4:
+        s0.mul_(0.9).add_(0.1 * g)
+        s1.mul_(0.999).add_(0.001 * g * g)
+        w.add_(lr * (s0 / (1 - 0.9 ** it)) / ((s1 / (1 - 0.999 ** it)).sqrt() + 1e-8))
+    elif rule == 9:
+        s0.mul_(0.9).add_(0.1 * g * g)
+        w.add_(lr * g / (s0.sqrt() + 1e-10))
+    else:
+        w.add_(lr * g)
+
+
+def train_dnn(X, y: np.ndarray, w: np.ndarray, valid: np.ndarray, params: dict, epochs: int,
+              device, seed: int = 0, log_fn=None, checkpoint_fn=None, grad_hook=None):
+    """Train on this rank's rows with the MLP engine; returns (DNN module, [(epoch, train_err,
+    valid_err)]).  Batches, initialisation, objective and update equal ``train_dnn_autograd``."""
+    from .nn import MLPSpec, MLPTrainer
+    hidden = [int(h) for h in (params.get("NumHiddenNodes") or [])]
+    acts = list(params.get("ActivationFunc") or [])
+    lr = float(params.get("LearningRate", 0.1))
+    batch = int(params.get("MiniBatchs", 10) or 10)
+    ckpt = int(params.get("CheckpointInterval", 0) or 0)
+    loss = (params.get("TF.loss") or "squared").lower()
+    loss = loss if loss in ("squared", "absolute", "log") else "squared"
+    rule = _TF_RULES.get((params.get("TF.optimizer") or "adam").lower(), 4)
+    device = torch.device(device)
+    n_in = int(np.shape(X)[1])
+    ref = DNN(n_in, hidden, acts, params.get("WeightInitializer"), seed)      # the TF initialisation
+    spec = MLPSpec(n_in, hidden, [_mlp_act(a) for a in acts[: len(hidden)]] or ["sigmoid"], 1, "sigmoid", loss,
+                   flat=False)
+    if len(spec.acts) < len(hidden):
+        spec.acts += [_mlp_act(None)] * (len(hidden) - len(spec.acts))
+    tr = MLPTrainer(spec, device=device, propagation="R", seed=seed, chunk_rows=max(1 << 16, batch))
+    with torch.no_grad():
+        for l, wv in enumerate(tr.params.views()):
+            i = spec.layer_in[l]
+            wv.zero_()
+            wv[:, :i].copy_(ref.W[l].detach())
+            wv[:, i].copy_(ref.b[l].detach())
+    dist.broadcast_(tr.params.flat, 0)
+    l2mask = torch.zeros(tr.params.numel, dtype=torch.uint8)
+    for off, (o, k), i in zip(tr.params.offsets, tr.params.shapes, spec.layer_in):
+        l2mask[off: off + o * k].view(o, k)[:, :i] = 1                          # weights, not biases
+    l2mask = l2mask.to(device)
+    s0 = torch.zeros(tr.params.numel, dtype=torch.float32, device=device)
+    s1 = torch.zeros_like(s0)
+    vmask = np.asarray(valid, dtype=bool)
+    tri, vai = np.nonzero(~vmask)[0], np.nonzero(vmask)[0]
+    yv = np.asarray(y, dtype=np.float32).reshape(-1)
+    wv_ = np.asarray(w, dtype=np.float32).reshape(-1)
+
+    def rows(idx):
+        # bf16 NormalizedData (data/rowstore.Bf16Rows) goes to HBM as its bf16 bits, rows gathered
+        # on the device; other inputs as fp32 host rows (prepare() casts them to bf16 on the GPU)
+        if hasattr(X, "device_rows") and device.type == "cuda":
+            return X.device_rows(device, rows=None if len(idx) == len(yv) else idx)
+        return torch.from_numpy(np.asarray(X if len(idx) == len(yv) else X[idx], dtype=np.float32))
+    data = tr.prepare(rows(tri), yv[tri].reshape(-1, 1), wv_[tri])
+    vdata = tr.prepare(rows(vai), yv[vai].reshape(-1, 1), wv_[vai]) if len(vai) else None
+    n_tr = len(tri)
+    n_batches = max(1, n_tr // batch)
+    if dist.info().world_size > 1:          # every rank runs the same number of synchronous steps
+        t = torch.tensor([n_batches], dtype=torch.float64, device=device)
+        dist.all_reduce_(t, "max")
+        n_batches = int(t.item())
+    bounds = [(int(a[0]), int(a[-1]) + 1) if len(a) else (0, 0)
+              for a in np.array_split(np.arange(n_tr), n_batches)]
+    # SUM_BY_NONZERO_WEIGHTS over the GLOBAL batch: per-batch counts of non-zero weights, summed once
+    nz = (wv_[tri] != 0).astype(np.float64)
+    cnts = torch.tensor([nz[a:b].sum() for a, b in bounds], dtype=torch.float64, device=device)
+    dist.all_reduce_(cnts)
+    cnts = cnts.clamp(min=1).cpu().numpy()
+    sign = {"squared": 2.0, "log": 1.0, "absolute": -1.0}[loss]   # Encog delta -> -d(mean loss)/dW
+    hist, it = [], 0
+    from ..ops import _native as nat
+    for ep in range(1, epochs + 1):
+        terr_sum, tcnt = 0.0, 0.0
+        for bi, (a, b) in enumerate(bounds):
+            it += 1
+            tr.compute_gradients(data, a, b)
+            gscale = sign / float(cnts[bi])
+            if grad_hook:
+                grad_hook(tr)
+            if device.type == "cuda":
+                nat.call_hip("shifu_optimizer_step_tf", tr.params.flat, tr.grad, s0, s1, tr.params.numel, rule,
+                             lr, 0.9, 0.999, 0.9, gscale, 0.01, l2mask, it, nat.stream_of(tr.params.flat))
+            else:
+                _tf_step_torch(rule, tr.params.flat, tr.grad, s0, s1, lr, gscale, 0.01, l2mask.float(), it)
+            terr_sum += float(tr.err_acc[0])
+            tcnt += float(cnts[bi])
+        terr = terr_sum / max(tcnt, 1.0)
+        v = torch.zeros(2, dtype=torch.float64, device=device)
+        if vdata is not None:
+            with torch.no_grad():
+                p = tr.predict_rows(vdata.x)[:, :1].float()
+                vs, vc = _loss(loss, p, vdata.y[:, :1].float(), vdata.s.reshape(-1, 1).float())
+                v = torch.stack([vs.double(), vc.double()])
+        dist.all_reduce_(v)
+        verr = float(v[0] / v[1].clamp(min=1)) if float(v[1]) > 0 else float("nan")
+        hist.append((ep, terr, verr))
+        if log_fn:
+            log_fn(ep, terr, verr)
+        if checkpoint_fn and ckpt > 0 and ep % ckpt == 0:
+            checkpoint_fn(_to_dnn(tr, ref), ep)
+    return _to_dnn(tr, ref), hist
+
+
+def _to_dnn(tr, ref: DNN) -> DNN:
+    """The MLP engine's weights as the DNN module (save_generic's layout: W[l] [out, in], b[l])."""
+    m = DNN.__new__(DNN)
+    torch.nn.Module.__init__(m)
+    m.W, m.b = torch.nn.ParameterList(), torch.nn.ParameterList()
+    for l, wv in enumerate(tr.params.views()):
+        i = tr.spec.layer_in[l]
+        m.W.append(torch.nn.Parameter(wv[:, :i].detach().float().cpu().clone()))
+        m.b.append(torch.nn.Parameter(wv[:, i].detach().float().cpu().clone()))
+    m.act_names, m.acts = list(ref.act_names), list(ref.acts)
+    return m

@@ -39,8 +39,9 @@ from ..utils.log import get_logger
 _log = get_logger("models.nn")
 
 ACT_IDS = {"sigmoid": 0, "tanh": 1, "linear": 2, "relu": 3, "leakyrelu": 4, "swish": 5,
-           "ptanh": 6, "log": 7, "sin": 8}
-ACT_DERIV_FROM_OUTPUT = {0, 1, 2, 3, 4, 6, 7}
+           "ptanh": 6, "log": 7, "sin": 8,
+           "leakyrelu_tf": 9}          # tf.nn.leaky_relu, alpha 0.2 (TENSORFLOW algorithm)
+ACT_DERIV_FROM_OUTPUT = {0, 1, 2, 3, 4, 6, 7, 9}
 LOSS_IDS = {"squared": 0, "log": 1, "absolute": 2}
 RULE_IDS = {"B": 0, "Q": 1, "M": 2, "R": 3, "ADAM": 4, "ADAGRAD": 5, "RMSPROP": 6,
             "MOMENTUM": 7, "NESTEROV": 8}
@@ -70,6 +71,8 @@ def act_fwd(act: str, z: torch.Tensor) -> torch.Tensor:
         return torch.where(z <= 0, torch.zeros_like(z), z)
     if act == "leakyrelu":
         return torch.where(z <= 0, 0.01 * z, z)
+    if act == "leakyrelu_tf":
+        return torch.where(z <= 0, 0.2 * z, z)
     if act == "swish":
         return z * torch.sigmoid(z)
     if act == "ptanh":
@@ -93,6 +96,8 @@ def act_deriv(act: str, z: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
         return (z > 0).to(a.dtype)
     if act == "leakyrelu":
         return torch.where(z <= 0, torch.full_like(a, 0.01), torch.ones_like(a))
+    if act == "leakyrelu_tf":
+        return torch.where(z <= 0, torch.full_like(a, 0.2), torch.ones_like(a))
     if act == "swish":
         s = torch.sigmoid(z)
         return s + z * s * (1 - s)
@@ -117,6 +122,7 @@ class MLPSpec:
     n_out: int = 1
     out_act: str = "sigmoid"          # "sigmoid" (classification) or linear/relu/leakyrelu/swish
     loss: str = "squared"
+    flat: bool = True                 # Encog's sigmoid flat spot (+0.1 on f'); False for TENSORFLOW
 
     def __post_init__(self):
         self.hidden = [int(h) for h in self.hidden]
@@ -140,6 +146,9 @@ class MLPSpec:
     @property
     def layer_kpad(self):           # padded input width incl. bias column
         return [round_up(i + 1, PAD) for i in self.layer_in]
+
+    def flat_spot(self, act: str) -> float:
+        return flat_spot(act) if self.flat else 0.0
 
     def n_weights_encog(self) -> int:
         return sum(o * (i + 1) for i, o in zip(self.layer_in, self.layer_out))
@@ -755,7 +764,7 @@ class MLPTrainer:
         nat.call_hip("shifu_mlp_fused2", x, kp[0], mc, kp[0], w1, kp[0], 512, sp.hidden[0], w2p, w2tp,
                      sp.hidden[1], wv[2], kp[2], y, s, h1, kp[1], d2, kp[2], d1, kp[1], slab, self.err_acc,
                      ACT_IDS[sp.acts[0]], ACT_IDS[sp.acts[1]], ACT_IDS[sp.out_act], LOSS_IDS[sp.loss],
-                     flat_spot(sp.acts[0]), flat_spot(sp.acts[1]), flat_spot(sp.out_act), st)
+                     sp.flat_spot(sp.acts[0]), sp.flat_spot(sp.acts[1]), sp.flat_spot(sp.out_act), st)
         nat.call_hip("shifu_colsum_fixed", slab, tiles, kp[2], part, gv[2], st)
         self._grad_ready(2)
         for l, dl, al in ((1, d2, h1), (0, d1, x)):
@@ -792,15 +801,15 @@ class MLPTrainer:
             act = ACT_IDS[sp.acts[l]]
             nat.call_hip("shifu_gemm_nt", a_in.data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
                          a_out.data_ptr(), kp[l + 1], nat.ptr(ders[l + 1]), kp[l + 1], None, 0, None, 0,
-                         mc, kp[l + 1], kp[l], 0, act, sp.hidden[l], 1, flat_spot(sp.acts[l]), st)
+                         mc, kp[l + 1], kp[l], 0, act, sp.hidden[l], 1, sp.flat_spot(sp.acts[l]), st)
         if head:
             # last hidden forward + output layer + loss + deltas + output wgrad in one GEMM epilogue
             lh = L - 1
             nat.call_hip("shifu_gemm_head", acts[lh].data_ptr(), kp[lh], wb[lh].data_ptr(), kp[lh], sp.hidden[lh],
                          dels[L].data_ptr(), kp[L], mc, kp[L], kp[lh], ACT_IDS[sp.acts[lh]], sp.hidden[lh],
                          wv[L].data_ptr(), y.data_ptr(), nat.ptr(s), gv[L].data_ptr(), self.err_acc.data_ptr(),
-                         kp[L], ACT_IDS[sp.out_act], LOSS_IDS[sp.loss], flat_spot(sp.out_act),
-                         flat_spot(sp.acts[lh]), nat.ptr(ws["gw_slab"]), st)
+                         kp[L], ACT_IDS[sp.out_act], LOSS_IDS[sp.loss], sp.flat_spot(sp.out_act),
+                         sp.flat_spot(sp.acts[lh]), nat.ptr(ws["gw_slab"]), st)
             if ws["gw_slab"] is not None:
                 nat.call_hip("shifu_colsum_fixed", ws["gw_slab"], -(-mc // 256), kp[L], ws["gw_part"],
                              gv[L].data_ptr(), st)
@@ -810,8 +819,8 @@ class MLPTrainer:
                          wv[L].data_ptr(), y.data_ptr(), sp.n_out, nat.ptr(s),
                          nat.ptr(dels[L]) if L else None, kp[L], gv[L].data_ptr(), self.err_acc.data_ptr(),
                          None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act],
-                         ACT_IDS[sp.acts[L - 1]] if L else 2, LOSS_IDS[sp.loss], flat_spot(sp.out_act),
-                         flat_spot(sp.acts[L - 1]) if L else 0.0, st)
+                         ACT_IDS[sp.acts[L - 1]] if L else 2, LOSS_IDS[sp.loss], sp.flat_spot(sp.out_act),
+                         sp.flat_spot(sp.acts[L - 1]) if L else 0.0, st)
         if fwd_event is not None:
             fwd_event.record()                     # forward + head of this chunk enqueued
         self._grad_ready(L)
@@ -836,7 +845,7 @@ class MLPTrainer:
                 nat.call_hip("shifu_gemm_nt", dels[l + 1].data_ptr(), kp[l + 1], wt[l].data_ptr(), kp[l + 1],
                              kp[l], dels[l].data_ptr(), kp[l], None, 0, acts[l].data_ptr(), kp[l],
                              nat.ptr(ders[l]), kp[l], mc, kp[l], kp[l + 1], 1, act, sp.hidden[l - 1],
-                             0, flat_spot(sp.acts[l - 1]), st)
+                             0, sp.flat_spot(sp.acts[l - 1]), st)
 
     def _chunk_torch(self, data: TrainData, r0: int, r1: int):
         """fp32 CPU oracle with exactly the HIP path's structure."""
@@ -868,10 +877,10 @@ class MLPTrainer:
                 err = -(torch.log(pc) * y * s).sum()
         elif sp.loss == "absolute":
             dl = torch.where(y < p, torch.ones_like(p), -torch.ones_like(p)) * \
-                (act_deriv(sp.out_act, zo, p) + flat_spot(sp.out_act)) * s
+                (act_deriv(sp.out_act, zo, p) + sp.flat_spot(sp.out_act)) * s
             err = (e.abs() * s).sum()
         else:
-            dl = (act_deriv(sp.out_act, zo, p) + flat_spot(sp.out_act)) * e * s
+            dl = (act_deriv(sp.out_act, zo, p) + sp.flat_spot(sp.out_act)) * e * s
             err = ((e * s) ** 2).sum()
         self.err_acc[0] += float(err)
         self.err_acc[1] += float(s.sum())
@@ -881,7 +890,7 @@ class MLPTrainer:
         for l in range(L - 1, -1, -1):
             # delta of hidden layer l+1 (acts[l+1]) from the layer above
             back = d @ wv[l + 1][:, : sp.hidden[l]]
-            dh = back * (act_deriv(sp.acts[l], zs[l + 1], acts[l + 1][:, : sp.hidden[l]]) + flat_spot(sp.acts[l]))
+            dh = back * (act_deriv(sp.acts[l], zs[l + 1], acts[l + 1][:, : sp.hidden[l]]) + sp.flat_spot(sp.acts[l]))
             gv[l].add_(dh.t() @ acts[l])
             self._grad_ready(l)
             d = dh

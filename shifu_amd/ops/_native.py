@@ -54,6 +54,7 @@ HIP_SIGNATURES = {
     "shifu_mlp_set_out_waves": "i",
     "shifu_mlp_output": "plplppl" "pplpppl" "iiiiiii" "ff" "s",
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
+    "shifu_optimizer_step_tf": "pppp" "li" "ffff" "ff" "p" "is",
     "shifu_cast_bf16": "plpliis",
     "shifu_transpose_cast": "plpiiis",
     # gemm_ring.hip

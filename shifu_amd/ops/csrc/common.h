@@ -44,7 +44,8 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // ---------------------------------------------------------------------------------------
 enum Act : int {
   ACT_SIGMOID = 0, ACT_TANH = 1, ACT_LINEAR = 2, ACT_RELU = 3, ACT_LEAKYRELU = 4,
-  ACT_SWISH = 5, ACT_PTANH = 6, ACT_LOG = 7, ACT_SIN = 8
+  ACT_SWISH = 5, ACT_PTANH = 6, ACT_LOG = 7, ACT_SIN = 8,
+  ACT_LEAKYRELU_TF = 9            // tf.nn.leaky_relu (alpha 0.2): the TENSORFLOW algorithm's leakyrelu
 };
 
 // Fast transcendental forms (v_exp_f32 + v_rcp_f32): the outputs are rounded to bf16 (8-bit
@@ -70,6 +71,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
     case ACT_PTANH: return x > 0.f ? fast_tanh(x) : 0.25f * fast_tanh(x);   // ActivationPTANH.java:54-59
     case ACT_LOG: return x >= 0.f ? __logf(1.f + x) : -__logf(1.f - x);
     case ACT_SIN: return __sinf(x);
+    case ACT_LEAKYRELU_TF: return x <= 0.f ? 0.2f * x : x;
   }
   return x;
 }
@@ -77,7 +79,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 // true when derivative can be computed from the activation output alone
 __host__ __device__ constexpr inline bool act_deriv_from_output(int act) {
   return act == ACT_SIGMOID || act == ACT_TANH || act == ACT_LINEAR || act == ACT_RELU ||
-         act == ACT_LEAKYRELU || act == ACT_LOG || act == ACT_PTANH;
+         act == ACT_LEAKYRELU || act == ACT_LOG || act == ACT_PTANH || act == ACT_LEAKYRELU_TF;
 }
 
 // derivative given output a (only valid when act_deriv_from_output(act))
@@ -91,6 +93,7 @@ __device__ __forceinline__ float act_deriv_out(int act, float a) {
     case ACT_LOG: { float b = a >= 0.f ? __expf(a) - 1.f : 1.f - __expf(-a);
                     return b >= 0.f ? 1.f / (1.f + b) : 1.f / (1.f - b); }
     case ACT_PTANH: return a > 0.f ? 1.f - a * a : 0.25f * (1.f - 16.f * a * a);
+    case ACT_LEAKYRELU_TF: return a <= 0.f ? 0.2f : 1.f;
   }
   return 1.f;
 }

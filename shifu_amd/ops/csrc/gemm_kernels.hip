@@ -355,8 +355,10 @@ __device__ __forceinline__ void gemm8_src(const GemmArgs& p, int m0, int n0, Off
   for (int i = 0; i < 2; ++i) {
     const int P = i * 8192 + wid * 1024 + lane * 16;
     const int row = P >> 7, lc = ((P >> 4) & 7) ^ ((row >> 1) & 7);
-    off[0][i] = (OffT)((long)min(m0 + row, p.M - 1) * p.lda + lc * 8);
-    off[1][i] = (OffT)((long)min(m0 + 128 + row, p.M - 1) * p.lda + lc * 8);
+    int ma = min(m0 + row, p.M - 1), mb = min(m0 + 128 + row, p.M - 1);
+    if (p.dbg & 32) { ma &= 4095; mb &= 4095; }        // lab: A rows from a 4096-row (L2-resident) window
+    off[0][i] = (OffT)((long)ma * p.lda + lc * 8);
+    off[1][i] = (OffT)((long)mb * p.lda + lc * 8);
     off[2][i] = (OffT)((long)min(n0 + row, p.NB - 1) * p.ldb + lc * 8);
     off[3][i] = (OffT)((long)min(n0 + 128 + row, p.NB - 1) * p.ldb + lc * 8);
   }
@@ -448,7 +450,7 @@ __device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8]
 #define G8_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
                       __builtin_amdgcn_sched_barrier(0); } while (0)
 #define G8_MMA(mh, nh, bq, on) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-    if (on) { __builtin_amdgcn_s_setprio(1); mma(mh, nh, bq); __builtin_amdgcn_s_setprio(0); } } while (0)
+    if ((on) && !(p.dbg & 64)) { __builtin_amdgcn_s_setprio(1); mma(mh, nh, bq); __builtin_amdgcn_s_setprio(0); } } while (0)
 
   // even k-tile 0 landed (its 8 DMAs are the oldest), odd k-tile 1 B halves stay in flight (and
   // extra16: the 16 epilogue stores a persistent kernel issued after the prologue)
@@ -590,7 +592,16 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_persist_kernel(GemmArgs p
       gemm8_src(p, (tn / ntn) * 256, (tn % ntn) * 256, o2);
       gemm8_prologue(p, o2, smem);
     }
-    epilogue_256_persist<EPI, ACT>(p, acc, (t / ntn) * 256, (t % ntn) * 256, smem);
+    if (p.dbg & 2) {                                  // lab: main loop only (acc kept live)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" :: "v"(acc[i][j]));
+    } else if (p.dbg & 128) {
+      epilogue_256_persist<EPI_STORE, 2>(p, acc, (t / ntn) * 256, (t % ntn) * 256, smem);   // lab: no activation
+    } else {
+      epilogue_256_persist<EPI, ACT>(p, acc, (t / ntn) * 256, (t % ntn) * 256, smem);
+    }
     if (tn >= ntiles) return;
     t = tn;
     first = false;
@@ -1010,7 +1021,7 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
              (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat, g_dbg};
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = 2 * g_stages * TILE_BYTES;
-  if (act < 0 || act > 8 || epi < 0 || epi > 2) return -2;
+  if (act < 0 || act > 9 || epi < 0 || epi > 2) return -2;
   if (epi == EPI_ACT && !act_deriv_from_output(act) && C2 == nullptr) return -3;
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;
@@ -1030,7 +1041,8 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
       if (epi == EPI_ACT) {
         switch (act) { case 0: GEMMP_L(EPI_ACT, 0); break; case 1: GEMMP_L(EPI_ACT, 1); break;
           case 2: GEMMP_L(EPI_ACT, 2); break; case 3: GEMMP_L(EPI_ACT, 3); break; case 4: GEMMP_L(EPI_ACT, 4); break;
-          case 6: GEMMP_L(EPI_ACT, 6); break; default: GEMMP_L(EPI_ACT, 7); break; }
+          case 6: GEMMP_L(EPI_ACT, 6); break; case 9: GEMMP_L(EPI_ACT, 9); break;
+          default: GEMMP_L(EPI_ACT, 7); break; }
       } else GEMMP_L(EPI_STORE, 2);
 #undef GEMMP_L
       CHECK_HIP(hipGetLastError());
@@ -1039,7 +1051,7 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
 #define GEMM8_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_kernel<E, A>), dim3(grid8), dim3(G8_T), lds8, stream, p)
 #define GEMM8_ACTS(E) switch (act) { case 0: GEMM8_L(E, 0); break; case 1: GEMM8_L(E, 1); break; \
     case 2: GEMM8_L(E, 2); break; case 3: GEMM8_L(E, 3); break; case 4: GEMM8_L(E, 4); break; \
-    case 6: GEMM8_L(E, 6); break; default: GEMM8_L(E, 7); break; }
+    case 6: GEMM8_L(E, 6); break; case 9: GEMM8_L(E, 9); break; default: GEMM8_L(E, 7); break; }
     if (epi == EPI_ACT) { GEMM8_ACTS(EPI_ACT) }
     else if (epi == EPI_DACT) { GEMM8_ACTS(EPI_DACT) }
     else GEMM8_L(EPI_STORE, 2);
@@ -1054,7 +1066,7 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
 #define GEMM_ACTS(E) switch (act) { case 0: GEMM_L(E, 0); break; case 1: GEMM_L(E, 1); break; \
     case 2: GEMM_L(E, 2); break; case 3: GEMM_L(E, 3); break; case 4: GEMM_L(E, 4); break; \
     case 5: GEMM_L(E, 5); break; case 6: GEMM_L(E, 6); break; case 7: GEMM_L(E, 7); break; \
-    default: GEMM_L(E, 8); break; }
+    case 9: GEMM_L(E, 9); break; default: GEMM_L(E, 8); break; }
   if (epi == EPI_ACT) { GEMM_ACTS(EPI_ACT) }
   else if (epi == EPI_DACT) { GEMM_ACTS(EPI_DACT) }
   else GEMM_L(EPI_STORE, 2);
@@ -1073,7 +1085,7 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
   if (K % 64 || N % 8 || N > 256 || KH > 256 || KH < n_valid + 1 || lda % 8 || ldb % 8 || ldd % 8 ||
       M <= 0 || NB <= 0 || NB > 256)
     return -1;
-  if (!act_deriv_from_output(act) || act == 6 || out_act < 0 || out_act > 8) return -2;
+  if (!act_deriv_from_output(act) || act == 6 || out_act < 0 || out_act > 9) return -2;
   GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)D, ldd, nullptr, 0, nullptr, 0, nullptr, 0,
              M, N, K, NB, n_valid, act, 1, 0.f, g_dbg};
   HeadArgs h{W, Y, S, GW, GWslab, err, KH, out_act, loss, flat_out, flat_hid};
@@ -1081,7 +1093,7 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
 #define HEAD_L(A_) hipLaunchKernelGGL((gemm_head_8ph_kernel<A_>), dim3(grid), dim3(G8_T), HEAD_LDS, stream, p, h)
   switch (act) {
     case 0: HEAD_L(0); break; case 1: HEAD_L(1); break; case 2: HEAD_L(2); break;
-    case 3: HEAD_L(3); break; case 4: HEAD_L(4); break; default: HEAD_L(7); break;
+    case 3: HEAD_L(3); break; case 4: HEAD_L(4); break; case 9: HEAD_L(9); break; default: HEAD_L(7); break;
   }
 #undef HEAD_L
   CHECK_HIP(hipGetLastError());

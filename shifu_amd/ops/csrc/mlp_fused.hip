@@ -545,7 +545,7 @@ SHIFU_API int shifu_mlp_fused2(const void* X, long ldx, int M, int K0, const voi
   if (n1rows != 512) return -1;            // W1 padded to 512 rows (zero rows past nv1)
   if ((long)128 * ldx >= (1l << 31) || (long)512 * ldw1 >= (1l << 31) || (long)128 * ldd1 * 2 >= (1l << 31))
     return -1;
-  if (out_act < 0 || out_act > 8) return -2;
+  if (out_act < 0 || out_act > 9) return -2;
   FusedArgs a{(const bf16_t*)X, ldx, (const bf16_t*)W1, ldw1, (const bf16_t*)W2p, (const bf16_t*)W2tp, w3, Y, S,
               (bf16_t*)H1, ldh1, (bf16_t*)D2, ldd2, (bf16_t*)D1, ldd1, gw_slab, err,
               M, K0, n1rows, nv1, nv2, KH, out_act, loss, flat1, flat2, flat_out, g_f2_stamps};

@@ -155,12 +155,17 @@ __global__ __launch_bounds__(256) void mlp_output_kernel(OutArgs p) {
 // J/core/dtrain/nn/update/*.java).  Gradients are Encog ascent directions: every rule ADDS.
 // ---------------------------------------------------------------------------------------
 enum Rule : int { R_BACKPROP = 0, R_QUICK = 1, R_MANHATTAN = 2, R_RPROP = 3, R_ADAM = 4, R_ADAGRAD = 5,
-                  R_RMSPROP = 6, R_MOMENTUM = 7, R_NESTEROV = 8 };
+                  R_RMSPROP = 6, R_MOMENTUM = 7, R_NESTEROV = 8,
+                  R_RMSPROP_TF = 9 };   // tf.train.RMSPropOptimizer: c = rho c + (1 - rho) g^2 (train.py)
 struct OptArgs {
   float* w; const float* g; float* s0; float* s1; float* s2; const uint8_t* fixed;
   long n; int rule, reg_level;     // reg_level 0 none, 1 L1, 2 L2 (legacy rules only)
   float lr, momentum, beta1, beta2, decay_rate, reg, num_train, q_eps, q_shrink, q_decay;
   int iteration;
+  // TENSORFLOW algorithm (models/dnn_sgd.py): the accumulated Encog-direction gradient is scaled to
+  // the mean loss of the batch (gscale) and the L2 term of tf.contrib.layers.l2_regularizer is
+  // folded in on the weight entries (l2mask: 1 for weights, 0 for biases / padding)
+  float gscale, l2; const uint8_t* l2mask;
 };
 
 __device__ __forceinline__ int sgn_tol(float v) { return fabsf(v) < 1e-7f ? 0 : (v > 0.f ? 1 : -1); }
@@ -169,8 +174,9 @@ __global__ void optimizer_kernel(OptArgs a) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   if (a.fixed && a.fixed[i]) return;
-  const float g = a.g[i];
   float w = a.w[i];
+  float g = a.g[i] * a.gscale;
+  if (a.l2mask && a.l2mask[i]) g -= a.l2 * w;
   float delta = 0.f;
   switch (a.rule) {
     case R_BACKPROP: delta = g * a.lr + a.s0[i] * a.momentum; a.s0[i] = delta; break;
@@ -204,6 +210,10 @@ __global__ void optimizer_kernel(OptArgs a) {
       a.w[i] = w + a.lr * g / (sqrtf(c) + 1e-8f); return;
     }
     case R_MOMENTUM: { const float d = a.lr * g + a.momentum * a.s0[i]; a.s0[i] = d; a.w[i] = w + d; return; }
+    case R_RMSPROP_TF: {
+      const float c = a.decay_rate * a.s0[i] + (1.f - a.decay_rate) * g * g; a.s0[i] = c;
+      a.w[i] = w + a.lr * g / (sqrtf(c) + 1e-10f); return;
+    }
     case R_NESTEROV: {
       const float prev = a.s0[i]; const float ld = a.momentum * prev + g * a.lr; a.s0[i] = ld;
       a.w[i] = w + a.momentum * prev - (1.f + a.momentum) * ld; return;
@@ -278,7 +288,20 @@ SHIFU_API int shifu_optimizer_step(float* w, const float* g, float* s0, float* s
                                    float beta2, float decay_rate, float reg, float num_train, float q_eps,
                                    float q_shrink, float q_decay, int iteration, hipStream_t stream) {
   OptArgs a{w, g, s0, s1, s2, fixed, n, rule, reg_level, lr, momentum, beta1, beta2, decay_rate, reg, num_train,
-            q_eps, q_shrink, q_decay, iteration};
+            q_eps, q_shrink, q_decay, iteration, 1.f, 0.f, nullptr};
+  hipLaunchKernelGGL(optimizer_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// TENSORFLOW-algorithm update: g' = gscale * g - l2 * w * l2mask, then `rule` (ADAM / momentum-free
+// gradient descent / RMSPROP_TF) with the TF hyper-parameters.
+SHIFU_API int shifu_optimizer_step_tf(float* w, const float* g, float* s0, float* s1, long n, int rule, float lr,
+                                      float beta1, float beta2, float decay_rate, float gscale, float l2,
+                                      const uint8_t* l2mask, int iteration, hipStream_t stream) {
+  if (rule != R_ADAM && rule != R_MOMENTUM && rule != R_RMSPROP_TF) return -1;
+  OptArgs a{w, g, s0, s1, nullptr, nullptr, n, rule, 0, lr, 0.f, beta1, beta2, decay_rate, 0.f, 1.f,
+            0.f, 0.f, 0.f, iteration, gscale, l2, l2mask};
   hipLaunchKernelGGL(optimizer_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;

@@ -282,8 +282,8 @@ class TrainStep:
         return out
 
     def _train_tensorflow(self) -> int:
-        """``algorithm: TENSORFLOW`` (TensorflowTrainer + train.py): a mini-batch DNN trained with
-        torch autograd, gradients all-reduced per batch over RCCL; saved as a generic model under
+        """``algorithm: TENSORFLOW`` (TensorflowTrainer + train.py): a mini-batch DNN trained on the
+        MLP engine's MFMA kernels, gradients all-reduced per batch over RCCL; saved as a generic model under
         ``models/<ModelSetName>/`` (+ ``-checkpoint-<epoch>`` copies)."""
         from ..models.dnn_sgd import save_generic, train_dnn
         ms, mc = self.ms, self.mc
@@ -308,8 +308,7 @@ class TrainStep:
         def ckpt_fn(model, ep):
             if rank0:
                 save_generic(model, f"{out}-checkpoint-{ep}", names, {"epoch": ep})
-        X = np.asarray(ts.X, dtype=np.float32)
-        model, hist = train_dnn(X, np.asarray(ts.y), np.asarray(sw), valid, params,
+        model, hist = train_dnn(ts.X, np.asarray(ts.y), np.asarray(sw), valid, params,
                                 int(mc.train.get("numTrainEpochs", 100) or 100), dev, seed, log_fn, ckpt_fn)
         if rank0:
             path = save_generic(model, out, names, {"epochs": len(hist),

@@ -104,3 +104,47 @@ def test_dnn_sgd_two_ranks_match_single(tmp_path):
     for a, b, c in zip(r0, r1, m.parameters()):
         torch.testing.assert_close(a, b)
         torch.testing.assert_close(a, c.detach(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("opt,loss,act", [("adam", "squared", "sigmoid"), ("rmsprop", "log", "tanh"),
+                                          ("gradientdescent", "absolute", "relu"),
+                                          ("adam", "log", "leakyrelu")])
+def test_mlp_engine_matches_autograd_oracle(opt, loss, act):
+    """The MLP-engine TENSORFLOW trainer (own kernels' CPU oracle, no flat spot, TF leaky slope,
+    optimizer_kernel's TF rules) trains the same weights as torch autograd + torch.optim."""
+    from shifu_amd.models.dnn_sgd import train_dnn, train_dnn_autograd
+    g = np.random.default_rng(4)
+    X = g.normal(size=(300, 9)).astype(np.float32)
+    y = (X[:, 0] - X[:, 3] > 0).astype(np.float32)
+    w = (g.random(300) < 0.9).astype(np.float32) * 1.5         # some zero weights: nonzero-count mean
+    valid = g.random(300) < 0.2
+    p = {"NumHiddenNodes": [8, 5], "ActivationFunc": [act, act], "LearningRate": 0.02, "MiniBatchs": 32,
+         "TF.optimizer": opt, "TF.loss": loss}
+    m1, h1 = train_dnn(X, y, w, valid, p, 3, torch.device("cpu"), seed=7)
+    m2, h2 = train_dnn_autograd(X, y, w, valid, p, 3, torch.device("cpu"), seed=7)
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose([v for _, _, v in h1], [v for _, _, v in h2], rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_mlp_engine_tf_gpu_tracks_autograd():
+    """On the GPU the TENSORFLOW trainer runs the bf16 MFMA kernels + shifu_optimizer_step_tf; it
+    tracks the fp32 autograd oracle within bf16 rounding over a few epochs."""
+    from shifu_amd.models.dnn_sgd import train_dnn, train_dnn_autograd
+    from shifu_amd.ops import _native
+    _native.require_gpu_native()
+    g = np.random.default_rng(4)
+    X = g.normal(size=(4000, 30)).astype(np.float32)
+    y = (X[:, 0] - X[:, 3] > 0).astype(np.float32)
+    w = np.ones(4000, np.float32)
+    valid = g.random(4000) < 0.2
+    p = {"NumHiddenNodes": [32, 16], "ActivationFunc": ["tanh", "leakyrelu"], "LearningRate": 0.01,
+         "MiniBatchs": 256, "TF.optimizer": "adam", "TF.loss": "log"}
+    m1, h1 = train_dnn(X, y, w, valid, p, 4, torch.device("cuda"), seed=2)
+    m2, h2 = train_dnn_autograd(X, y, w, valid, p, 4, torch.device("cpu"), seed=2)
+    v1, v2 = [v for _, _, v in h1], [v for _, _, v in h2]
+    assert v1[-1] < v1[0]
+    np.testing.assert_allclose(v1, v2, rtol=0.05)
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        assert float((a.detach() - b.detach()).abs().max()) < 0.05
