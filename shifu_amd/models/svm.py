@@ -26,6 +26,7 @@ framework's files back for scoring.
 from __future__ import annotations
 
 import math
+import os
 import time
 
 import numpy as np
@@ -35,6 +36,7 @@ KERNELS = {"leaner kernel": "linear", "linear": "linear", "poly kernel": "poly",
            "sigmoid kernel": "sigmoid", "sigmoid": "sigmoid", "radialbasisfunction": "rbf", "rbf": "rbf"}
 LIBSVM_KERNEL_IDS = {"linear": 0, "poly": 1, "rbf": 2, "sigmoid": 3}
 TAU = 1e-12
+SMO_BATCH = 2048          # SMO iterations per GPU launch (svm_kernels.hip)
 
 
 def kernel_name(k) -> str:
@@ -120,12 +122,30 @@ def train_svm(X, y, kernel="linear", C=1.0, gamma=1.0, degree=3, coef0=0.0, eps=
     Cv = torch.as_tensor(C * cw, dtype=torch.float64, device=dev)
     alpha = torch.zeros(n, dtype=torch.float64, device=dev)
     G = torch.full((n,), -1.0, dtype=torch.float64, device=dev)        # gradient of 0.5 a'Qa - e'a
-    Kd = torch.diagonal(K).double()
+    Kd = torch.diagonal(K).double().contiguous()
     inf = torch.tensor(float("inf"), dtype=torch.float64, device=dev)
     max_iter = max_iter or max(10_000_000, 100 * n)
     t0 = time.time()
     it = 0
-    while it < max_iter:
+    if dev.type == "cuda" and os.environ.get("SHIFU_SVM_HOST_LOOP") != "1":
+        # ops/csrc/svm_kernels.hip: SMO_BATCH iterations per launch inside one workgroup, one host
+        # synchronisation per batch (the convergence flag) instead of ~8 per iteration
+        from ..ops import _native as nat
+        state = torch.zeros(2, dtype=torch.int64, device=dev)
+        gap = torch.zeros(1, dtype=torch.float64, device=dev)
+        st = nat.stream_of(K)
+        next_log = 20000
+        while it < max_iter:
+            k = int(min(SMO_BATCH, max_iter - it))
+            nat.call_hip("shifu_svm_smo", K, n, Y, Cv, Kd, alpha, G, n, k, float(eps), TAU, state, gap, st)
+            done, conv = (int(v) for v in state.cpu())
+            it = done
+            if conv:
+                break
+            if log is not None and it >= next_log:
+                log(f"SVM SMO iteration {it}: gap {float(gap.item()):.3g} ({time.time() - t0:.1f}s)")
+                next_log += 20000
+    while it < max_iter and (dev.type != "cuda" or os.environ.get("SHIFU_SVM_HOST_LOOP") == "1"):
         # WSS3: i = argmax_{I_up} -y G ; j = argmin over I_low of the second-order gain
         up = ((Y > 0) & (alpha < Cv)) | ((Y < 0) & (alpha > 0))
         low = ((Y > 0) & (alpha > 0)) | ((Y < 0) & (alpha < Cv))

@@ -57,6 +57,8 @@ HIP_SIGNATURES = {
     "shifu_optimizer_step_tf": "pppp" "li" "ffff" "ff" "p" "is",
     "shifu_cast_bf16": "plpliis",
     "shifu_transpose_cast": "plpiiis",
+    # svm_kernels.hip
+    "shifu_svm_smo": "pl" "ppp" "pp" "ii" "dd" "pp" "s",
     # gemm_ring.hip
     "shifu_wgrad_ring": "plplpl" "iii" "pl" "s",
     "shifu_wgrad_ring_ws": ("iii", "l"),
