@@ -186,6 +186,46 @@ def auto_filter(mc, ccs, corr: np.ndarray | None = None, corr_nums=None):
 
 
 @torch.no_grad()
+def first_layer_fp32(xb: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, fl_cache: dict | None = None):
+    """S = X W1^T + b1 in fp32.  GPU: ONE own-MFMA GEMM (gemm_kernels.hip, EPI_F32 tile) over
+    split-bf16 operands concatenated along K -- [xh | xh | xl | 1 | 1] . [Wh | Wl | Wh | bh | bl]^T,
+    hi = bf16(v), lo = bf16(v - hi) -- whose bf16 products are exact and accumulate in fp32:
+    the fp32 product to ~2^-17 relative (the Xl Wl term dropped), like K15's split digits.
+    ``fl_cache`` keeps the split weights and the operand buffer across row chunks."""
+    dev = xb.device
+    F, H1a = W1.shape[1], W1.shape[0]
+    fl_cache = {} if fl_cache is None else fl_cache
+    if dev.type != "cuda":
+        return xb @ W1.t() + b1
+    from ..ops import _native as nat
+    R = xb.shape[0]
+    kp = ((3 * F + 2 + 63) // 64) * 64
+    nh = ((H1a + 7) // 8) * 8
+    if fl_cache.get("B") is None:
+        wh = W1.to(torch.bfloat16)
+        wl = (W1 - wh.float()).to(torch.bfloat16)
+        bh = b1.to(torch.bfloat16)
+        bl = (b1 - bh.float()).to(torch.bfloat16)
+        B = torch.zeros(H1a, kp, dtype=torch.bfloat16, device=dev)
+        B[:, :F], B[:, F:2 * F], B[:, 2 * F:3 * F] = wh, wl, wh
+        B[:, 3 * F], B[:, 3 * F + 1] = bh, bl
+        fl_cache["B"] = B
+    A = fl_cache.get("A")
+    if A is None or A.shape[0] < R:
+        A = torch.zeros(R, kp, dtype=torch.bfloat16, device=dev)
+        A[:, 3 * F: 3 * F + 2] = 1.0
+        fl_cache["A"] = A
+    A = A[:R]
+    xh = xb.to(torch.bfloat16)
+    A[:, :F] = xh
+    A[:, F:2 * F] = xh
+    A[:, 2 * F:3 * F] = (xb - xh.float()).to(torch.bfloat16)
+    S = torch.empty(R, nh, dtype=torch.float32, device=dev)
+    nat.call_hip("shifu_gemm_nt", A, kp, fl_cache["B"], kp, H1a, S, nh, None, 0, None, 0, None, 0,
+                 R, nh, kp, 3, 2, H1a, 0, 0.0, nat.stream_of(A))
+    return S[:, :H1a]
+
+
 def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, row_chunk: int = 1 << 16,
                 deep_rows: int = 2048):
     """SE sensitivity over inputs of a trained MLP (NNNetwork, input-first weights).
@@ -201,8 +241,10 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
     * 1 hidden layer (K14, ``sensitivity_kernel``): correction + activation + output neuron
       fused, register-blocked (the v_exp/v_rcp issue rate bounds it -- see profiles/);
     * deeper nets (K14b): ``se_perturb_kernel`` writes the perturbed first hidden layer of every
-      (row, input) pair as bf16 MLP rows, the remaining layers run as bf16 MFMA GEMMs
-      (hipBLASLt, fp32 accumulation) over R x feat_chunk pair rows at a time.
+      (row, input) pair as bf16 MLP rows, the remaining layers run as the framework's own bf16
+      MFMA GEMMs (``shifu_gemm_nt``, fp32 accumulation) over R x feat_chunk pair rows at a time;
+    * both: the cached first layer S is one own-MFMA GEMM over split-bf16 operands with an fp32
+      tile epilogue (``first_layer``), fp32-accurate to ~2^-17.
     CPU: the fp32 torch oracle of the same decomposition."""
     from ..models.nn import ACT_IDS, HostRows, act_fwd
     dev = torch.device(device) if device is not None else \
@@ -228,6 +270,12 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
             yield (xb if torch.is_tensor(xb) else torch.as_tensor(np.asarray(xb), dtype=torch.float32)).to(
                 dev, dtype=torch.float32).contiguous()
 
+    fl_cache = {}
+
+    def first_layer(xb):
+        return first_layer_fp32(xb, W1, b1, fl_cache)
+
+
     def tail(z1):
         a = act_fwd(acts[0], z1)
         for l in range(1, len(Ws)):
@@ -242,7 +290,7 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
         W2 = Ws[1][0, :-1].contiguous()
         b2 = float(Ws[1][0, -1])
         for xb in row_chunks(row_chunk * 16):
-            S = (xb @ W1.t() + b1).contiguous()
+            S = first_layer(xb).contiguous()
             base = act_fwd(acts[1], act_fwd(acts[0], S) @ W2 + b2).contiguous()
             stats_ops.sensitivity_1h(S, xb, W1t, W2, b2, base, ACT_IDS[acts[0]], ACT_IDS[acts[1]], acc)
             n += xb.shape[0]
@@ -305,7 +353,7 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
         act1 = ACT_IDS[acts[0]]
         for xb in row_chunks(deep_rows):
             R = xb.shape[0]
-            S = (xb @ W1.t() + b1).contiguous()
+            S = first_layer(xb).contiguous()
             # unperturbed rows through the same kernel (x_f = 0 correction): base and perturbed
             # activations share rounding, so an input with x_f = 0 gives d = 0 exactly
             base = tail_bf16(stats_ops.se_perturb(S, torch.zeros(R, 1, device=dev), W1t[:1], 0, 1, act1, hpad))

@@ -51,7 +51,8 @@ __device__ __forceinline__ s16x4 ds_read_tr16_b64(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
 }
 
-enum Epi : int { EPI_ACT = 0, EPI_DACT = 1, EPI_STORE = 2 };
+enum Epi : int { EPI_ACT = 0, EPI_DACT = 1, EPI_STORE = 2,
+                 EPI_F32 = 3 };   // fp32 output tile (split-bf16 fp32-accurate products: algos/varsel.py)
 
 struct GemmArgs {
   const bf16_t* A; long lda;   // [M, K] row-major
@@ -213,6 +214,19 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
       }
     }
     return;
+  } else if constexpr (EPI == EPI_F32) {
+    // each lane owns 4 consecutive output columns of one row: one 16-B store (C is float, ldc floats)
+    float* Cf = (float*)p.C;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nb = n0 + wc * 64 + i * 16 + (lane >> 4) * 4;
+      if (nb >= p.N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wr * 64 + j * 16 + (lane & 15);
+        if (m < p.M) *(float4*)(Cf + (size_t)m * p.ldc + nb) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
   } else {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1021,7 +1035,14 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
              (const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, M, N, K, NB, n_valid, act, bias_col, flat, g_dbg};
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = 2 * g_stages * TILE_BYTES;
-  if (act < 0 || act > 9 || epi < 0 || epi > 2) return -2;
+  if (act < 0 || act > 9 || epi < 0 || epi > 3) return -2;
+  if (epi == EPI_F32) {             // fp32 tile out: the 128 x 128 kernel (ldc counted in floats)
+    if (ldc % 4) return -1;
+    if (g_stages == 2) hipLaunchKernelGGL((gemm_nt_kernel<EPI_F32, 2, 2>), dim3(grid), dim3(NTHR), lds, stream, p);
+    else hipLaunchKernelGGL((gemm_nt_kernel<EPI_F32, 2, 1>), dim3(grid), dim3(NTHR), lds, stream, p);
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
   if (epi == EPI_ACT && !act_deriv_from_output(act) && C2 == nullptr) return -3;
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;

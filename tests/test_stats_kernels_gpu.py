@@ -200,3 +200,19 @@ def test_column_metrics_kernel_matches_host():
                 continue
             np.testing.assert_allclose(g[:3], ref[:3], rtol=1e-12, atol=1e-12)
             np.testing.assert_allclose(g[3], ref[3], rtol=1e-12, atol=1e-12)
+
+
+def test_se_first_layer_split_bf16_gemm_fp32_accurate():
+    """The SE cached first layer S = X W1^T + b1 on the own MFMA GEMM (split-bf16 operands, EPI_F32
+    tile) is fp32-accurate: within ~1e-5 of the fp64 product (a plain bf16 GEMM is ~1e-2 off)."""
+    from shifu_amd.algos import varsel as V
+    rng = np.random.default_rng(7)
+    F, H = 333, 50
+    W = rng.normal(size=(H, F + 1)) * 0.2
+    X = rng.normal(size=(5000, F)).astype(np.float32)
+    Wt = torch.tensor(W, dtype=torch.float32, device="cuda")
+    S = V.first_layer_fp32(torch.from_numpy(X).cuda(), Wt[:, :F], Wt[:, F]).double().cpu().numpy()
+    ref = X.astype(np.float64) @ W[:, :F].astype(np.float32).astype(np.float64).T + \
+        W[:, F].astype(np.float32).astype(np.float64)
+    err = np.abs(S - ref).max() / np.abs(ref).max()
+    assert err < 2e-5, err

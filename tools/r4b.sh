@@ -6,7 +6,7 @@ set -o pipefail
 out=gpurun_out/r4b
 mkdir -p $out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_dist_stats.py tests/test_sort_gpu.py tests/test_norm_stream.py tests/test_tensorflow_alg.py > $out/gpu_tests_new.txt 2>&1 || { tail -30 $out/gpu_tests_new.txt; exit 1; }
+  tests/test_dist_stats.py tests/test_sort_gpu.py tests/test_norm_stream.py tests/test_tensorflow_alg.py tests/test_svm.py tests/test_stats_kernels_gpu.py > $out/gpu_tests_new.txt 2>&1 || { tail -30 $out/gpu_tests_new.txt; exit 1; }
 tail -3 $out/gpu_tests_new.txt
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --gbdt-levels > $out/bench_default.json 2> $out/bench_default.err || { tail -20 $out/bench_default.err; exit 1; }
 cat $out/bench_default.json | cut -c1-600
