@@ -23,6 +23,7 @@
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
+#include <immintrin.h>
 
 #define SHIFU_RT_API extern "C" __attribute__((visibility("default")))
 
@@ -116,6 +117,59 @@ inline double parse_double(std::string_view s, bool& ok) {
   return v;
 }
 
+// SSSE3 / SSE4.1 form of the same fast path for fields of <= 16 bytes that lie inside the buffer:
+// one 16-byte load gives the delimiter, dot, sign and digit masks; a table shuffle right-aligns the
+// digits around the dot; two madd steps fold 16 digits into two 8-digit halves.  The mantissa m
+// and the fraction length are exactly the scalar loop's, so the value (m / 10^frac, one IEEE
+// division) is bit-identical.  Returns false (caller takes the scalar path) for anything else.
+struct DigitShuffles {
+  alignas(16) int8_t m[2][17][17][16];   // [sign][integer digits][fraction digits]
+  DigitShuffles() {
+    for (int s0 = 0; s0 < 2; ++s0)
+      for (int di = 0; di <= 16; ++di)
+        for (int df = 0; df <= 16; ++df) {
+          const int nd = di + df;
+          for (int j = 0; j < 16; ++j) {
+            const int t = j - (16 - nd);
+            m[s0][di][df][j] = (nd > 16 || t < 0) ? (int8_t)0x80 : (int8_t)(s0 + t + (t >= di ? 1 : 0));
+          }
+        }
+  }
+};
+static const DigitShuffles kShuf;
+
+__attribute__((target("ssse3,sse4.1,popcnt,bmi")))
+inline bool parse_field_simd(const char* p, size_t avail, char d0, double& out, size_t& flen) {
+  if (avail < 16) return false;
+  const __m128i v = _mm_loadu_si128((const __m128i*)p);
+  const unsigned md = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(v, _mm_set1_epi8(d0))) |
+                      (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(v, _mm_set1_epi8('\n')));
+  if (!md) return false;                                  // field longer than 15 bytes
+  const int L = __builtin_ctz(md);
+  if (L == 0) return false;                               // empty field: the caller's missing rule
+  const int s0 = (p[0] == '-' || p[0] == '+') ? 1 : 0;
+  const __m128i x = _mm_sub_epi8(v, _mm_set1_epi8('0'));
+  const unsigned mdig = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_min_epu8(x, _mm_set1_epi8(9)), x));
+  const unsigned mdot = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(v, _mm_set1_epi8('.')));
+  const unsigned field = ((1u << L) - 1) & ~((1u << s0) - 1);
+  const unsigned dg = mdig & field, dt = mdot & field;
+  if ((dg | dt) != field || !dg || (dt & (dt - 1))) return false;
+  const int nd = __builtin_popcount(dg);
+  int di = nd, df = 0;
+  if (dt) { const int pd = __builtin_ctz(dt); di = pd - s0; df = L - pd - 1; }
+  const __m128i d = _mm_shuffle_epi8(x, _mm_load_si128((const __m128i*)kShuf.m[s0][di][df]));
+  const __m128i t1 = _mm_maddubs_epi16(d, _mm_setr_epi8(10, 1, 10, 1, 10, 1, 10, 1, 10, 1, 10, 1, 10, 1, 10, 1));
+  const __m128i t2 = _mm_madd_epi16(t1, _mm_setr_epi16(100, 1, 100, 1, 100, 1, 100, 1));
+  const __m128i t3 = _mm_packus_epi32(t2, t2);
+  const __m128i t4 = _mm_madd_epi16(t3, _mm_setr_epi16(10000, 1, 10000, 1, 10000, 1, 10000, 1));
+  const uint64_t m = (uint64_t)(uint32_t)_mm_cvtsi128_si32(t4) * 100000000ull +
+                     (uint32_t)_mm_extract_epi32(t4, 1);
+  const double val = df ? (double)m / kPow10[df] : (double)m;
+  out = (s0 && p[0] == '-') ? -val : val;
+  flen = (size_t)L;
+  return true;
+}
+
 struct Chunk {
   size_t begin, end;           // byte range (line aligned)
   std::vector<size_t> line_starts;
@@ -143,7 +197,9 @@ void split_lines(const Parser& P, Chunk& c) {
 // (Clinger's fast path, == strtod); an empty field is missing; anything else (spaces, missing
 // tokens, exponents, Java "1.0d", strings) is re-scanned to its delimiter and takes the general
 // path (trim, missing tokens, strtod / dictionary).
-void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<int64_t>& bad) {
+// Numeric values go to row_out[slot] (a row of the caller's row-major tile); string codes straight
+// to their column (one int per row, sequential).
+void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, double* row_out, std::atomic<int64_t>& bad) {
   const char d0 = P.delim[0];
   const size_t dl = P.delim.size();
   const char* buf = P.buf;
@@ -164,7 +220,7 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
     const bool miss = P.is_missing(v);
     if (k == 1) {
       bool ok = false;
-      P.numptr[P.num_idx[col]][r] = miss ? NAN : parse_double(v, ok);
+      row_out[P.num_idx[col]] = miss ? NAN : parse_double(v, ok);
     } else {
       int32_t code = -1;
       if (!miss) {
@@ -185,7 +241,14 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
   while (true) {
     const int k = col < P.ncols ? P.kinds[col] : 0;
     size_t b;                                      // field end
-    if (k == 1 && dl == 1) {
+    double sv;
+    size_t sl;
+    if (k == 1 && dl == 1 && p < e &&
+        parse_field_simd(buf + p, P.len - p, d0, sv, sl) && p + sl <= e &&
+        !(P.numeric_missing && P.is_missing(std::string_view(buf + p, sl)))) {
+      b = p + sl;
+      row_out[P.num_idx[col]] = sv;
+    } else if (k == 1 && dl == 1) {
       size_t i = p;
       bool neg = false;
       if (i < e && (buf[i] == '-' || buf[i] == '+')) { neg = buf[i] == '-'; ++i; }
@@ -210,12 +273,12 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
       }
       if (fast && i == p) {                        // empty field: missing (token or not)
         b = i;
-        P.numptr[P.num_idx[col]][r] = NAN;
+        row_out[P.num_idx[col]] = NAN;
       } else if (fast && any && m < (1ull << 53) && frac <= 22 &&
                  !(P.numeric_missing && P.is_missing(std::string_view(buf + p, i - p)))) {
         b = i;
         const double v = frac ? (double)m / kPow10[frac] : (double)m;
-        P.numptr[P.num_idx[col]][r] = neg ? -v : v;
+        row_out[P.num_idx[col]] = neg ? -v : v;
       } else {
         b = field_end(p);
         general(p, b);
@@ -231,20 +294,39 @@ void parse_line(Parser& P, Chunk& c, size_t s, size_t e, size_t r, std::atomic<i
   if (col != P.ncols) {
     bad.fetch_add(1);
     for (int cc = col; cc < P.ncols; ++cc) {   // short row: rest missing
-      if (P.kinds[cc] == 1) P.numptr[P.num_idx[cc]][r] = NAN;
+      if (P.kinds[cc] == 1) row_out[P.num_idx[cc]] = NAN;
       else if (P.kinds[cc] == 2) P.codes[P.str_idx[cc]][r] = -1;
     }
   }
 }
 
+// Lines are parsed TILE rows at a time into a row-major [TILE][n_numeric] scratch tile, which is
+// then written out column by column (TILE consecutive doubles per column).  Writing each field
+// straight to its column touched one page and one cache line per field (n_numeric pages per row:
+// a DTLB miss per value at 1600 columns); the tile keeps the parse in L2 and the column writes
+// contiguous.
+constexpr int TILE = 32;
+
 void parse_chunk(Parser& P, Chunk& c, std::atomic<int64_t>& bad) {
   c.local_dict.assign(P.ncols, {});
   c.local_list.assign(P.ncols, {});
-  for (size_t li = 0; li < c.line_starts.size(); ++li) {
-    const size_t s = c.line_starts[li];
-    const size_t e = li + 1 < c.line_starts.size() ? c.line_starts[li + 1] - 1 : c.end;
-    const char* nl = (const char*)memchr(P.buf + s, '\n', e - s);   // blank lines were skipped
-    parse_line(P, c, s, nl ? (size_t)(nl - P.buf) : e, c.row_offset + li, bad);
+  const size_t nn = P.numptr.size();
+  std::vector<double> tile(std::max<size_t>(1, nn) * TILE);
+  const size_t nl_total = c.line_starts.size();
+  for (size_t l0 = 0; l0 < nl_total; l0 += TILE) {
+    const size_t l1 = std::min(nl_total, l0 + TILE);
+    for (size_t li = l0; li < l1; ++li) {
+      const size_t s = c.line_starts[li];
+      const size_t e = li + 1 < nl_total ? c.line_starts[li + 1] - 1 : c.end;
+      const char* nl = (const char*)memchr(P.buf + s, '\n', e - s);   // blank lines were skipped
+      parse_line(P, c, s, nl ? (size_t)(nl - P.buf) : e, c.row_offset + li, tile.data() + (li - l0) * nn, bad);
+    }
+    const size_t rows = l1 - l0, r0 = c.row_offset + l0;
+    for (size_t k = 0; k < nn; ++k) {
+      double* dst = P.numptr[k] + r0;
+      const double* src = tile.data() + k;
+      for (size_t i = 0; i < rows; ++i) dst[i] = src[i * nn];
+    }
   }
 }
 
