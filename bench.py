@@ -752,6 +752,7 @@ def bench_pipeline(a, dev, info):
     step("stats", lambda: api.StatsStep(root).process())
     step("norm", lambda: api.NormStep(root).process())
     step("varsel", lambda: api.VarSelStep(root).process())
+    from shifu_amd.steps.varsel import PHASES as SE_PHASES
     step("train", lambda: api.TrainStep(root).process())
     step("eval", lambda: api.EvalStep(root).process())
     recall = None
@@ -795,13 +796,19 @@ def bench_pipeline(a, dev, info):
         "step_seconds": {k: round(v, 2) for k, v in times.items()}, "generation_s": round(t_gen, 1),
         "train_epoch_s (median epoch interval, metrics.jsonl)": round(ep_train, 4),
         "train_setup_s": round(train_setup, 2),
-        "projected_20M_rows_minutes (linear in rows, labelled projection)": {k: round(v, 2) for k, v in proj.items()},
-        "projected_20M_train_200_epochs_minutes ((setup + 200 x epoch) x rows, labelled projection)":
-            round((train_setup + ep_train * 200) * scale20 / 60.0, 2),
+        "varsel_phases_s (SE: rows load, NN training, sensitivity)": {k: (round(v, 2) if isinstance(v, float) else v)
+                                                                      for k, v in SE_PHASES.items()},
+        "step_minutes": {k: round(v / 60.0, 2) for k, v in times.items()},
         "reference_minutes_20M_x_1600 (CHANGES.txt:233-237,264-268)": REF_PIPELINE_MIN,
+        "measured_at_reference_shape": bool(rows * info.world_size >= REF_PIPELINE_ROWS and F >= 1600 and epochs >= 400),
         "se_recall_of_planted_columns": recall,
         "eval_auc": perf["areaUnderRoc"] if info.rank == 0 else None,
     }
+    if not out["measured_at_reference_shape"]:        # smaller runs: labelled linear projections
+        out["projected_20M_rows_minutes (linear in rows, labelled projection)"] = {k: round(v, 2)
+                                                                                  for k, v in proj.items()}
+        out["projected_20M_train_200_epochs_minutes ((setup + 200 x epoch) x rows, labelled projection)"] = \
+            round((train_setup + ep_train * 200) * scale20 / 60.0, 2)
     if info.rank == 0 and not a.keep:
         shutil.rmtree(work, ignore_errors=True)
     return out

@@ -14,6 +14,7 @@ trees, voted GA wrapper, auto-filter with history, ``-reset/-list/-autofilter/-r
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import torch
@@ -24,6 +25,7 @@ from ..config.column_config import has_candidates
 from ..formats.nn_format import NNNetwork
 from ..models.nn import MLPSpec, MLPTrainer
 from ..utils.log import get_logger
+from ..utils.trace import trace_range
 from ..parallel import dist
 from .base import ModelSet, _writer, shard_model_data
 
@@ -122,14 +124,26 @@ def _reusable_se_model(ms, cols):
     return net
 
 
+PHASES: dict = {}          # last SE run: load / training / sensitivity seconds (bench.py pipeline)
+
+
+def _sync(device):
+    if torch.cuda.is_available() and (device is None or torch.device(device).type == "cuda"):
+        torch.cuda.synchronize()
+
+
 def select_by_sensitivity(ms, by="SE", device=None, seed=0):
     mc = ms.mc
     cols = _good(ms)
     if not cols:
         return []
     epochs = max(1, int(mc.train.get("numTrainEpochs", 100)) // 2)
+    t0 = time.perf_counter()
     net = _reusable_se_model(ms, cols)
-    rows = _normalized_rows(ms, cols, device)
+    trained = net is None
+    with trace_range("varsel.load_rows"):
+        rows = _normalized_rows(ms, cols, device)
+    t1 = time.perf_counter()
     if net is not None:
         if rows is not None:
             X = rows[0]
@@ -137,8 +151,18 @@ def select_by_sensitivity(ms, by="SE", device=None, seed=0):
             md = shard_model_data(ms.load_raw(cols))
             X, _, _ = N.normalize_table(mc, ms.ccs, md.table, columns=cols)
     else:
-        net, X, md = _train_quick_nn(ms, cols, epochs, device, seed, rows=rows)
-    mean, rms, var = V.sensitivity(net, X, device=device)
+        with trace_range("varsel.se_train"):
+            net, X, md = _train_quick_nn(ms, cols, epochs, device, seed, rows=rows)
+    _sync(device)
+    t2 = time.perf_counter()
+    with trace_range("varsel.sensitivity"):
+        mean, rms, var = V.sensitivity(net, X, device=device)
+    _sync(device)
+    t3 = time.perf_counter()
+    # phase split of the SE job (the reference's 70 min = 45 min of training + 25 min of sensitivity)
+    PHASES.update(load_s=t1 - t0, train_s=t2 - t1, train_epochs=epochs if trained else 0, sensitivity_s=t3 - t2)
+    _log.info("varsel SE phases: rows %.2fs, training %.2fs (%d epochs), sensitivity %.2fs",
+              t1 - t0, t2 - t1, epochs, t3 - t2)
     filter_num = int(mc.varSelect.get("filterNum", 200) or 0)
     keep = filter_num if filter_num > 0 else int(len(cols) * (1 - float(mc.varSelect.get("filterOutRatio", 0.05))))
     order = np.argsort(-rms, kind="stable")          # VarSelectReducer sorts by RMS for SE and ST
