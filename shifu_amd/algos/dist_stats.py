@@ -39,10 +39,7 @@ HLL_P = 14
 
 
 def _dev():
-    i = dist.info()
-    if i.backend == "nccl":
-        return torch.device("cuda", torch.cuda.current_device())
-    return torch.device("cpu")
+    return dist.coll_device()
 
 
 def _allreduce(t: torch.Tensor, op="sum") -> torch.Tensor:

@@ -69,7 +69,8 @@ def _cache_budget(dev) -> int:
 
 def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None, batch: int = 64,
                                   reduce=None, allgather=None, gather_objects=None):
-    """``chunks_fn()`` -> a fresh iterator of ModelData chunks (this rank's rows).  Fills the same
+    """``chunks_fn(resume=None, with_keys=False)`` -> a fresh iterator of ModelData chunks (this
+    rank's rows; ``with_keys``: (key, chunk) pairs, ``resume``: start at a key's block).  Fills the same
     ColumnConfig fields as ``compute_column_stats``; returns the merged row count."""
     from ..utils.device import is_gpu_available
     dev = torch.device(device or ("cuda" if is_gpu_available() else "cpu"))
@@ -104,12 +105,15 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
         return (torch.as_tensor(np.asarray(md.y, np.float32), device=dev),
                 torch.as_tensor(np.asarray(md.w, np.float64), device=dev))
 
+    resume = [None]          # key of the first chunk that did not fit the device cache
+
     def stream():
-        """(y, w, [vals per batch]) per chunk -- from the device cache when the pass-A stream fit."""
-        if cache_ok and cache:
-            yield from cache
+        """(y, w, [vals per batch]) per chunk: the chunks that fit the HBM budget come from the
+        device cache, the rest is re-read and re-parsed from the first uncached block on."""
+        yield from cache
+        if resume[0] is None:
             return
-        for md in chunks_fn():
+        for md in chunks_fn(resume=resume[0]):
             y, w = yw(md)
             yield y, w, [upload(md, bt) for bt in batches]
 
@@ -118,7 +122,7 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
     cat_state = {cc.name: ({}, []) for cc in categorical}     # name -> (cat -> idx, [counts rows])
     cat_missing = {cc.name: np.zeros(4) for cc in categorical}
     first = True
-    for md in chunks_fn():
+    for key, md in chunks_fn(with_keys=True):
         total += md.n
         y, w = yw(md)
         if sm:
@@ -137,9 +141,9 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
             if cached_bytes + nbytes <= budget:
                 cache.append((y, w, vals_all))
                 cached_bytes += nbytes
-            else:
+            else:                  # keep the cached prefix; later passes resume at this block
                 cache_ok = False
-                cache.clear()
+                resume[0] = key
         del vals_all
         first = False
     if first:
@@ -148,8 +152,9 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
     if reduce is not None:
         reduce(t, "sum")
     total, unselected = int(t[0].item()), int(t[1].item())
-    _log.info("stats stream: %d rows, %d numeric batches, device cache %s (%.1f GB)", total, len(batches),
-              "on" if cache_ok and cache else "off", cached_bytes / 1e9)
+    _log.info("stats stream: %d rows, %d numeric batches, device cache %d chunks (%.1f GB)%s", total,
+              len(batches), len(cache), cached_bytes / 1e9,
+              "" if resume[0] is None else ", later passes re-parse from block %s" % (resume[0][:2],))
     for bt in batches:
         bt.eng.finish_a()
 

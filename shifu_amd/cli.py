@@ -45,7 +45,7 @@ DP_VERBS = ("train", "stats", "eval", "norm", "normalize", "transform", "varsel"
 def torch_status(rc: int):
     import torch
     from .parallel import dist as _d
-    dev = f"cuda:{torch.cuda.current_device()}" if _d.info().backend == "nccl" else "cpu"
+    dev = _d.coll_device() if _d.info().world_size > 1 else "cpu"
     return torch.tensor([int(rc or 0)], dtype=torch.int64, device=dev)
 
 

@@ -109,12 +109,22 @@ def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int
             pos += cut + 1
 
 
-def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kinds: list, nthreads: int):
-    """Yield ((file index, offset), parsed part) for this rank's share, in file order."""
+def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kinds: list, nthreads: int,
+                resume=None):
+    """Yield ((file index, offset), parsed part) for this rank's share, in file order.  ``resume``
+    = (file index, offset) of a block yielded by an earlier pass: start there (earlier blocks are
+    neither read nor parsed; an offset is always a line start)."""
     files = list_data_files(plan.data_path)
     if not files:
         raise FileNotFoundError(f"no data under {plan.data_path}")
     for fi, path, a, b in byte_ranges(files, rank, world):
+        if resume is not None:
+            if fi < resume[0]:
+                continue
+            if fi == resume[0] and a is not None:
+                a = max(a, resume[1])
+                if a >= b:
+                    continue
         if a is None:                              # indivisible unit
             if path.endswith(".parquet"):
                 yield (fi, 0), _parse_parquet(path, plan.header, kinds, plan.missing)
@@ -144,11 +154,11 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
 
 
 def iter_tables(plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
-                nthreads: int | None = None):
+                nthreads: int | None = None, resume=None):
     """Yield (key, RawTable) row chunks of this rank's share of the data set, in file order."""
     kinds = column_kinds(plan.header, plan.nums, plan.strs)
     nthreads = nthreads or min(16, os.cpu_count() or 4)
-    for key, part in _iter_parts(plan, chunk_bytes, rank, world, kinds, nthreads):
+    for key, part in _iter_parts(plan, chunk_bytes, rank, world, kinds, nthreads, resume):
         yield key, table_from_parts(plan.header, kinds, [part], plan.data_path)
 
 
@@ -225,20 +235,26 @@ def prefetched(gen_fn, depth: int = 2):
 
 def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
                     sample_rate: float = 1.0, sample_neg_only: bool = False, seed: int = 0,
-                    require_target: bool = True, row0: int = 0):
+                    require_target: bool = True, row0: int = 0, resume=None, with_keys: bool = False):
     """Yield purified :class:`ModelData` chunks of this rank's byte range; ``row0`` = the global
     raw-row index of the rank's first row (sampling draws are per global row).  Chunks are
-    produced ``shifu.data.prefetch`` (default 1) ahead on a background thread."""
+    produced ``shifu.data.prefetch`` (default 1) ahead on a background thread.
+
+    ``with_keys``: yield (key, md) with key = (file index, offset, raw row index of the block),
+    which a later pass hands back as ``resume`` to start at that block (stats passes whose first
+    blocks are cached in HBM re-parse only the rest)."""
     from ..config import environment
 
     def produce():
-        r = row0
-        for _, table in iter_tables(plan, chunk_bytes, rank, world):
+        r = row0 if resume is None else resume[2]
+        for key, table in iter_tables(plan, chunk_bytes, rank, world,
+                                      resume=None if resume is None else resume[:2]):
             n = table.n
             md = finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, r)
+            k = (key[0], key[1], r)
             r += n
             if md.n:
-                yield md
+                yield (k, md) if with_keys else md
     yield from prefetched(produce, int(environment.get("shifu.data.prefetch", 1)))
 
 

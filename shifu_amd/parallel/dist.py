@@ -113,8 +113,10 @@ def shutdown() -> None:
 
 def coll_device() -> torch.device:
     """Device a collective's tensors must live on: the rank's GPU under RCCL (``nccl`` cannot
-    reduce host tensors), the host under gloo."""
-    if tdist.is_initialized() and tdist.get_backend() == "nccl":
+    reduce host tensors), the host under gloo -- except under SHIFU_ASSERT_DEVICE_COLLECTIVES=1 on
+    a GPU box, where gloo runs follow RCCL's contract so the guard sees the RCCL device choices."""
+    if tdist.is_initialized() and (tdist.get_backend() == "nccl" or (
+            os.environ.get("SHIFU_ASSERT_DEVICE_COLLECTIVES") == "1" and _compute_device_type() == "cuda")):
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 
@@ -124,10 +126,7 @@ def _compute_device_type() -> str:
 
 
 def _stage_device() -> torch.device:
-    """Where host values are staged for a collective: the collective device, or the rank's GPU
-    under the device-collective guard (a gloo run on a GPU box then follows RCCL's contract)."""
-    if os.environ.get("SHIFU_ASSERT_DEVICE_COLLECTIVES") == "1" and _compute_device_type() == "cuda":
-        return torch.device("cuda", torch.cuda.current_device())
+    """Where host values are staged for a collective (see coll_device)."""
     return coll_device()
 
 

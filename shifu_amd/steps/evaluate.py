@@ -476,7 +476,7 @@ def _gather_eval_numeric(ms, ev, md, res, tags, score_meta):
     from ..parallel import dist
     mc = ms.mc
     info = dist.info()
-    dev = torch.device("cuda", torch.cuda.current_device()) if info.backend == "nccl" else torch.device("cpu")
+    dev = dist.coll_device()
     tg = np.asarray([str(t).strip() for t in tags])
     if mc.is_multiclass():
         lab = np.array([next((i for i, g in enumerate(mc.tags()) if t in g), -1) for t in tg], np.int64)

@@ -127,11 +127,12 @@ def _stats_streamed(ms: ModelSet, cols, device=None) -> None:
 
     row0 = DS.rank_row_offset(plan, info.rank, info.world_size) if rate < 1.0 else 0
 
-    def chunks():
-        return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only, row0=row0)
+    def chunks(resume=None, with_keys=False):
+        return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only, row0=row0,
+                                  resume=resume, with_keys=with_keys)
     multi = info.world_size > 1
     if multi and device is None:
-        device = torch.device("cuda", torch.cuda.current_device()) if info.backend == "nccl" else "cpu"
+        device = dist.coll_device()
     n = compute_column_stats_streamed(
         mc, ms.ccs, chunks, device=device, columns={c.name for c in cols},
         reduce=(lambda t, op: dist.all_reduce_(t, op)) if multi else None,

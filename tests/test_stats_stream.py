@@ -59,8 +59,12 @@ def _model_set(tmp_path, method):
     return a
 
 
-@pytest.mark.parametrize("method", ["EqualPositive", "EqualTotal", "WeightEqualPositive", "EqualInterval"])
-def test_streamed_stats_equal_in_memory(tmp_path, monkeypatch, method):
+@pytest.mark.parametrize("method,cache_gb", [("EqualPositive", None), ("EqualTotal", None),
+                                             ("WeightEqualPositive", None), ("EqualInterval", None),
+                                             ("EqualPositive", "0.00004"), ("EqualTotal", "0.00004")])
+def test_streamed_stats_equal_in_memory(tmp_path, monkeypatch, method, cache_gb):
+    """cache_gb: an HBM-cache budget that holds only the first chunks -- later passes take the
+    cached prefix and re-parse from the first uncached block (data/stream.py resume)."""
     import shutil
     from shifu_amd.config import environment
     from shifu_amd.steps.stats import run_stats
@@ -72,7 +76,20 @@ def test_streamed_stats_equal_in_memory(tmp_path, monkeypatch, method):
     run_stats(a)
     monkeypatch.setitem(environment.props(), "shifu.stats.streaming", "true")
     monkeypatch.setitem(environment.props(), "shifu.stats.chunkMB", str(8 / 1024))      # 8 KB chunks
+    if cache_gb is not None:
+        monkeypatch.setenv("SHIFU_STATS_CACHE_GB", cache_gb)
+        from shifu_amd.data import stream as DS
+        resumed = []
+        orig = DS.iter_model_data
+
+        def spy(*a, **k):
+            if k.get("resume") is not None:
+                resumed.append(k["resume"])
+            return orig(*a, **k)
+        monkeypatch.setattr(DS, "iter_model_data", spy)
     run_stats(b)
+    if cache_gb is not None:
+        assert resumed and all(r[1] > 0 or r[0] > 0 for r in resumed), resumed   # a partial prefix was cached
     ca = json.load(open(os.path.join(a, "ColumnConfig.json")))
     cb = json.load(open(os.path.join(b, "ColumnConfig.json")))
     for x, y in zip(ca, cb):
