@@ -1131,6 +1131,8 @@ class TreeTrainer:
                 finally:
                     self._fuse = None
                 t0 = time.perf_counter()
+                rng = trace_range("gbdt.apply_residual")
+                rng.__enter__()
                 keep = None
                 if tid > 0 and c.dropout_rate > 0.0:
                     # DTWorker :634-638: each row skips this tree's update with prob. DropoutRate
@@ -1145,6 +1147,7 @@ class TreeTrainer:
                 self.timings["apply"] += time.perf_counter() - t0
                 terr = self._residual(self.pred, d, out)
                 verr = self._residual(self.vpred, self.valid, vout) if self.valid is not None else float("nan")
+                rng.__exit__(None, None, None)
             else:
                 if not self._pending:
                     # RF: the next trees grow together (their subsample weights drawn in tree order,

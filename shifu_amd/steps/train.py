@@ -365,7 +365,8 @@ class TrainStep:
         if self._job_parallel(len(jobs), is_tree):
             val_errors = self._run_jobs_parallel(jobs, is_tree, n_kfold, seed)
         else:
-            ts = load_train_set(ms, is_tree)
+            with trace_range("train.load_data"):
+                ts = load_train_set(ms, is_tree)
             val_errors = self._run_jobs(jobs, ts, n_kfold, seed)
         if self.info.rank == 0:
             if len(grid) > 1:
@@ -740,6 +741,8 @@ class TrainStep:
         # uint8 codes go to the device one 32-feature group at a time (no host int32 staging)
         codes_np = codes if isinstance(codes, np.ndarray) else np.asarray(codes)
         all_rows = len(tri) == codes_np.shape[0]
+        rng = trace_range("train.upload_bins")
+        rng.__enter__()
         if self._host_bins(len(tri), codes_np.shape[1]):
             _log.info("tree bins stay in pinned host memory (%d rows x %d features)", len(tri), codes_np.shape[1])
             d = BinnedData.host_resident(codes_np, y[tri], nb, is_cat, w[tri], device=dev,
@@ -754,6 +757,7 @@ class TrainStep:
         elif valid_m.any():
             vi = np.nonzero(valid_m)[0]
             vd = BinnedData.from_codes(codes_np, y[vi], nb, is_cat, w[vi], device=dev, rows=vi)
+        rng.__exit__(None, None, None)
         tree_num = int(_num(p.get("TreeNum"), 100))
         cfg = TreeConfig(alg, tree_num=tree_num, max_depth=int(_num(p.get("MaxDepth"), 7 if alg == "GBT" else 10)),
                          min_instances_per_node=int(_num(p.get("MinInstancesPerNode"), 5)),
@@ -816,7 +820,8 @@ class TrainStep:
                 break
         wd.__exit__(None, None, None)
         if self.info.rank == 0:
-            self._write_trees(tid, tt)
+            with trace_range("train.write_model"):
+                self._write_trees(tid, tt)
             if os.path.exists(ckpt):
                 os.remove(ckpt)
         return tt.valid_errors[-1] if tt.valid_errors else float("nan")
