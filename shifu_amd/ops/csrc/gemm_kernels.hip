@@ -332,6 +332,7 @@ __device__ __forceinline__ void epilogue_256(const GemmArgs& p, f32x4 (&acc)[4][
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int v2u32_t;
 // ---------------------------------------------------------------------------------------
 // 8-phase NT GEMM (256 x 256 x 64, 8 waves 2 M x 4 N, wave tile 128 x 64, 1 block per CU).
 //
@@ -415,7 +416,7 @@ __device__ __forceinline__ void gemm8_prologue(const GemmArgs& p, const OffT (&o
 // onto acc (several operand pairs summed into one tile).
 template <bool I8 = false, typename OffT = long>
 __device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8], const OffT (&off)[4][2],
-                                           char* smem, bool extra16 = false, bool zero = true) {
+                                           char* smem, bool extra16 = false, bool zero = true, int extra = -1) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   const int nk = p.K / 64;
@@ -468,7 +469,11 @@ __device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8]
 
   // even k-tile 0 landed (its 8 DMAs are the oldest), odd k-tile 1 B halves stay in flight (and
   // extra16: the 16 epilogue stores a persistent kernel issued after the prologue)
-  if (extra16) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  // (extra: the number of vector-memory ops a persistent kernel issued after the prologue -- 16
+  // epilogue stores of the forward, 32 of the head -- which this first wait leaves in flight)
+  const int ex = extra >= 0 ? extra : (extra16 ? 16 : 0);
+  if (ex == 32) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+  else if (ex == 16) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   G8_BAR();
   if (wr == 1) G8_BAR();                      // stagger the two wave rows by one barrier
@@ -812,6 +817,185 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
 }
 
 // ---------------------------------------------------------------------------------------
+// Persistent fused head: one block per CU walks row tiles t = lb, lb + G, ...; the next tile's
+// prologue DMAs are issued BEFORE this tile's epilogue (as the persistent forward does), and the
+// last-hidden deltas leave straight from the accumulator registers as 32 bounds-checked 8-B buffer
+// stores per lane (no LDS staging: the ring holds the next tile's first k-tile), which drain while
+// the next tile's main loop runs.  The epilogue's row partials / deltas / output-wgrad partials
+// live above the ring.  Same per-row semantics and the same fixed-point-free fp32 math as
+// gemm_head_8ph_kernel (its stage 1-3 arithmetic, in the same order).
+// ---------------------------------------------------------------------------------------
+constexpr int HEADP_STORES = 32;      // D stores per lane per tile (4 column blocks x 8 row blocks)
+
+template <int ACT>
+__device__ __forceinline__ void head_epilogue_regs(const GemmArgs& p, const HeadArgs& h, f32x4 (&acc)[4][8],
+                                                   int m0, float y_pf, float s_pf, char* smem) {
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));        // keep per-lane addressing local to the epilogue
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  float* red = (float*)(smem + 2 * G8_BUF);          // [2 wr][4 wc][128] row partials of z_out
+  float* dl = red + 1024;                            // [256] output deltas
+  float* gred = dl + 256;                            // [2 wr][256] output-wgrad partials
+  double* ered = (double*)(gred + 512);              // [8 waves][2]
+  const int nv = p.n_valid;
+  float w3[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = wc * 64 + i * 16 + (lane >> 4) * 4 + r;
+      w3[i][r] = n < h.KH ? h.W[n] : 0.f;
+    }
+  float zp[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = wc * 64 + i * 16 + (lane >> 4) * 4 + r;
+        float a = n < nv ? act_fwd(ACT, acc[i][j][r]) : (n == nv ? 1.f : 0.f);
+        a = bf2f(f2bf(a));
+        acc[i][j][r] = a;
+        t += a * w3[i][r];
+      }
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    zp[j] = t;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[(wr * 4 + wc) * 128 + j * 16 + lane] = zp[j];
+  }
+  // raw barriers: __syncthreads() would make hipcc drain the next tile's prologue DMAs
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  double e_c = 0.0, e_w = 0.0;
+  if (tid < 256) {
+    const int rw = tid >> 7, rl = tid & 127;
+    const float z = red[(rw * 4 + 0) * 128 + rl] + red[(rw * 4 + 1) * 128 + rl] + red[(rw * 4 + 2) * 128 + rl] +
+                    red[(rw * 4 + 3) * 128 + rl];
+    const int m = m0 + tid;
+    float dlt = 0.f;
+    if (m < p.M) {
+      const float y = y_pf, sg = s_pf;
+      const float a = act_fwd(h.out_act, z), e = y - a;
+      if (h.loss == 1) {
+        dlt = e * sg;
+        const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
+        e_c = -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
+      } else if (h.loss == 2) {
+        dlt = (y < a ? 1.f : -1.f) * (act_deriv_out(h.out_act, a) + h.flat_out) * sg;
+        e_c = fabsf(e) * sg;
+      } else {
+        dlt = (act_deriv_pre(h.out_act, z) + h.flat_out) * e * sg;
+        e_c = (double)(e * sg) * (e * sg);
+      }
+      e_w = sg;
+    }
+    dl[tid] = dlt;
+  }
+  e_c = wave_sum_d(e_c);
+  e_w = wave_sum_d(e_w);
+  if (lane == 0) { ered[wid * 2] = e_c; ered[wid * 2 + 1] = e_w; }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // D = delta_out * w_out * (f'(a) + flat) straight from registers: lane owns 4 consecutive
+  // columns of one row per (i, j); columns >= N get an out-of-range offset (dropped by the
+  // buffer bounds check: the store count stays uniform for the next tile's counted vmcnt)
+  const int rows = min(256, p.M - m0);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.C + (size_t)m0 * p.ldc), (short)0, rows * (int)p.ldc * 2, 0x00020000);
+  float gw[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gw[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ml = wr * 128 + j * 16 + (lane & 15);
+    const float d = dl[ml];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = acc[i][j][r];
+        gw[i][r] += d * a;
+        o[r] = (nl + r < nv) ? d * w3[i][r] * (act_deriv_out(ACT, a) + h.flat_hid) : 0.f;
+      }
+      const uint32_t lo = pack_bf16x2(o[0], o[1]), hi = pack_bf16x2(o[2], o[3]);
+      const int off = nl < p.N ? (int)((ml * p.ldc + nl) * 2) : 0x7ffffff0;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, (uint2){lo, hi}), rs, off, 0, 0);
+    }
+  }
+  if (tid == 0) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int w = 0; w < 8; ++w) { a0 += ered[w * 2]; a1 += ered[w * 2 + 1]; }
+    atomicAdd(h.err, a0);
+    atomicAdd(h.err + 1, a1);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = gw[i][r];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if ((lane & 15) == 0) gred[wr * 256 + wc * 64 + i * 16 + (lane >> 4) * 4 + r] = v;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (tid < 256 && tid < h.KH) {
+    const float v = gred[tid] + gred[256 + tid];
+    if (h.GWslab) h.GWslab[(size_t)(m0 >> 8) * h.KH + tid] = v;     // tile index = row block
+    else atomicAdd(h.GW + tid, v);
+  }
+  // the row partials / deltas above the ring are rewritten by the next tile's epilogue only after
+  // its main loop, whose barriers order every wave's reads of this tile's values before it
+}
+
+template <int ACT>
+__global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_persist_kernel(GemmArgs p, HeadArgs h, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = gridDim.x;
+  int t = xcd_remap(blockIdx.x, G);
+  if (t >= ntiles) return;
+  {
+    long o0[4][2];
+    gemm8_src(p, t * 256, 0, o0);
+    gemm8_prologue(p, o0, smem);
+  }
+  bool first = true;
+  for (;;) {
+    const int m0 = t * 256;
+    const int my = min(m0 + (int)(threadIdx.x & 255), p.M - 1);
+    const float y_pf = h.Y[my], s_pf = h.S ? h.S[my] : 1.f;
+    f32x4 acc[4][8];
+    {
+      long off[4][2];
+      gemm8_src(p, m0, 0, off);
+      gemm8_loop(p, acc, off, smem, !first, true, first ? 0 : HEADP_STORES);
+    }
+    const int tn = t + G;
+    if (tn < ntiles) {        // next tile's prologue first: lands in buffer 0 + buffer 1's B halves
+      long o2[4][2];
+      gemm8_src(p, tn * 256, 0, o2);
+      gemm8_prologue(p, o2, smem);
+    }
+    head_epilogue_regs<ACT>(p, h, acc, m0, y_pf, s_pf, smem);
+    if (tn >= ntiles) return;
+    t = tn;
+    first = false;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // wgrad: G[n][k] += sum_m D[m][n] * X[m][k]   (TN GEMM over rows, split over m)
 // LDS images [64 m][128 cols] bf16, 256-B rows, quad XOR swizzle so that the 8 rows read
 // by one 32-lane half of ds_read_b64_tr_b16 hit 8 distinct bank groups.
@@ -1016,11 +1200,13 @@ static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N 
 static int g_wg_interleave = 1;   // wgrad row splits: 1 interleaved 64-row steps (-3% wgrad1 at 1M rows), 0 contiguous
 static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
 static int g_fwd_persist = 1;     // persistent 8-phase forward (tune key 10; 0 = one tile per block)
+static int g_head_persist = 1;    // persistent fused head (tune key 11; 0 = one row tile per block)
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
   if (key == 2) { g_wg_interleave = val; return 0; }
   if (key == 9) { g_dbg = val; return 0; }
   if (key == 10) { g_fwd_persist = val; return 0; }
+  if (key == 11) { g_head_persist = val; return 0; }
   return -1;
 }
 SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b == 3 || b == 4) ? b : 0; return 0; }
@@ -1111,6 +1297,21 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
              M, N, K, NB, n_valid, act, 1, 0.f, g_dbg};
   HeadArgs h{W, Y, S, GW, GWslab, err, KH, out_act, loss, flat_out, flat_hid};
   const int grid = (M + 255) / 256;
+  if (g_head_persist && !g_dbg && (long)M * ldd * 2 < (1l << 31)) {
+    int dev = 0, ncu = 256;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int gridp = grid < ncu ? grid : ncu;
+#define HEADP_L(A_) hipLaunchKernelGGL((gemm_head_8ph_persist_kernel<A_>), dim3(gridp), dim3(G8_T), HEAD_LDS, stream, \
+                                       p, h, grid)
+    switch (act) {
+      case 0: HEADP_L(0); break; case 1: HEADP_L(1); break; case 2: HEADP_L(2); break;
+      case 3: HEADP_L(3); break; case 4: HEADP_L(4); break; case 9: HEADP_L(9); break; default: HEADP_L(7); break;
+    }
+#undef HEADP_L
+    CHECK_HIP(hipGetLastError());
+    return 0;
+  }
 #define HEAD_L(A_) hipLaunchKernelGGL((gemm_head_8ph_kernel<A_>), dim3(grid), dim3(G8_T), HEAD_LDS, stream, p, h)
   switch (act) {
     case 0: HEAD_L(0); break; case 1: HEAD_L(1); break; case 2: HEAD_L(2); break;

@@ -127,6 +127,29 @@ def test_fused_head_matches_unfused(hidden, acts, loss, monkeypatch):
     assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
 
 
+@pytest.mark.parametrize("n", [70000 + 77, 300000])
+def test_persistent_head_bitwise_equals_per_tile_head(n):
+    """gemm_head_8ph_persist_kernel (next tile's prologue before the epilogue, deltas stored from
+    registers) computes exactly the per-tile head's gradients (same per-element arithmetic); only
+    the fp64 error atomics may differ in summation order."""
+    from shifu_amd.ops import _native as nat
+    spec = MLPSpec(n_in=120, hidden=[300, 200], acts=["sigmoid", "sigmoid"], n_out=1)
+    x, y, s = _mk(spec, n, seed=4)
+    res = []
+    for persist in (0, 1):
+        nat.call_hip("shifu_gemm_set_tune", 11, persist)
+        try:
+            t = MLPTrainer(spec, device="cuda", seed=9, chunk_rows=1 << 20)
+            d = t.prepare(x, y, s)
+            t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
+            torch.cuda.synchronize()
+            res.append((t.grad.clone(), t.err_acc.clone()))
+        finally:
+            nat.call_hip("shifu_gemm_set_tune", 11, 1)
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
+
+
 def test_bench_configuration_tracks_fp32_oracle():
     """The exact bench trainer configuration (bench.py: n_in 1000, hidden 500/200 sigmoid, RPROP,
     chunks >= 2^17 rows) so the 8-phase forward, the fused head, the ring wgrad (incl. the M % 32

@@ -1,12 +1,20 @@
 #!/bin/bash
-# r4c: (1) the CLI pipeline at the largest reference-width shape the box's disk holds (3M training +
+# r4c: (0) MLP GPU tests incl. the persistent head (now default) + head A/B in the lab + the MLP bench;
+# (1) the CLI pipeline at the largest reference-width shape the box's disk holds (3M training +
 # 0.75M eval rows x 1600 columns, 400 epochs: varsel SE trains 200 epochs over all 1600 candidates);
 # (2) a roctx marker trace of `shifu train` (GBT) with its range summary.
 set -o pipefail
 out=gpurun_out/r4c
 mkdir -p $out
 root=$(pwd)
-(df -h /tmp; free -g) > $out/box_info.txt 2>&1
+timeout -k 10 400 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_mlp_gpu.py > $out/gpu_tests_mlp.txt 2>&1
+rc=$?
+tail -4 $out/gpu_tests_mlp.txt
+if [ $rc -ne 0 ]; then echo "mlp tests rc $rc: stopping"; exit $rc; fi
+timeout -k 10 300 python tools/mlp_lab.py --iters 5 --tune 11:0 11:1 > $out/mlp_lab_head_persist.jsonl 2> $out/mlp_lab.err || exit 1
+cat $out/mlp_lab_head_persist.jsonl
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --gbdt-steps 0 > $out/bench_mlp.json 2> $out/bench_mlp.err || exit 1
+cut -c1-300 $out/bench_mlp.json
 timeout -k 10 900 python bench.py --model pipeline --rows 3000000 --pipeline-epochs 400 --workdir /tmp/shifu_pipe \
   > $out/bench_pipeline_3Mx1600.json 2> $out/bench_pipeline_3Mx1600.err || { tail -30 $out/bench_pipeline_3Mx1600.err; exit 1; }
 cut -c1-600 $out/bench_pipeline_3Mx1600.json
