@@ -484,6 +484,8 @@ class MLPTrainer:
         if self.gpu:
             from ..ops import _native
             _native.require_gpu_native()
+            if "SHIFU_HEAD_PERSIST" in os.environ:     # persistent fused head A/B (gemm_kernels.hip)
+                _native.call_hip("shifu_gemm_set_tune", 11, int(os.environ["SHIFU_HEAD_PERSIST"] == "1"))
             if spec.layer_kpad[-1] > 512 or spec.n_out > 8:
                 raise ValueError("HIP output kernel supports last hidden width <= 511 and n_out <= 8")
         self.params = MLPParams(spec, self.device)

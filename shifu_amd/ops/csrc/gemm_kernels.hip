@@ -1200,7 +1200,8 @@ static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N 
 static int g_wg_interleave = 1;   // wgrad row splits: 1 interleaved 64-row steps (-3% wgrad1 at 1M rows), 0 contiguous
 static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
 static int g_fwd_persist = 1;     // persistent 8-phase forward (tune key 10; 0 = one tile per block)
-static int g_head_persist = 1;    // persistent fused head (tune key 11; 0 = one row tile per block)
+static int g_head_persist = 0;    // persistent fused head (tune key 11 / SHIFU_HEAD_PERSIST=1; measured
+                                  // 1.13 vs 1.10 ms per 2M-row chunk: off by default, profiles/r4)
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
   if (key == 2) { g_wg_interleave = val; return 0; }

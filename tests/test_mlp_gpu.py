@@ -145,7 +145,7 @@ def test_persistent_head_bitwise_equals_per_tile_head(n):
             torch.cuda.synchronize()
             res.append((t.grad.clone(), t.err_acc.clone()))
         finally:
-            nat.call_hip("shifu_gemm_set_tune", 11, 1)
+            nat.call_hip("shifu_gemm_set_tune", 11, 0)
     assert torch.equal(res[0][0], res[1][0])
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
 

@@ -32,7 +32,14 @@ def main():
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
-    rows = list(con.execute("select name, start, end, category from regions"))
+    rows = []
+    for name, s, e, cat, ext in con.execute("select name, start, end, category, extdata from regions"):
+        # roctx ranges: the region is the API call (roctxThreadRangeA), the range text its message
+        try:
+            msg = json.loads(ext or "{}").get("message")
+        except ValueError:
+            msg = None
+        rows.append((msg or name, s, e, cat))
     tops = [(s, e) for n, s, e, _ in rows if n == a.top]
     if not tops:
         names = sorted({n for n, *_ in rows})
