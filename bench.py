@@ -644,7 +644,8 @@ def bench_eval(a, dev, info):
         sync()
         out["torch_stable_argsort_rows_per_s"] = n / (time.perf_counter() - t1)
         # NN scoring (the eval's model pass) of the headline 1000-500-200-1 net: fp32 (default,
-        # parity) vs bf16 on the trainer's own MFMA kernels
+        # parity: split-bf16 on the own MFMA GEMM), the vendor fp32 GEMM, and bf16 on the
+        # trainer's own MFMA kernels
         from shifu_amd.formats.nn_format import NNNetwork
         from shifu_amd.scoring.model_runner import nn_forward
         rng = np.random.default_rng(0)
@@ -653,7 +654,11 @@ def bench_eval(a, dev, info):
                         [rng.normal(size=(sizes[i + 1], sizes[i] + 1)) * 0.05 for i in range(3)])
         ns = min(n, 4_000_000)
         X = torch.randn(ns, 1000, generator=g, device=dev, dtype=torch.float32)
-        for prec in ("fp32", "bf16"):
+        a64 = X[:16384].double().cpu().numpy()
+        for W in net.weights:                                   # fp64 oracle of the first rows
+            a64 = 1.0 / (1.0 + np.exp(-(a64 @ W[:, :-1].T + W[:, -1])))
+        ref64 = a64
+        for prec in ("fp32", "fp32_torch", "bf16"):
             nn_forward(net, X[:65536], dev, precision=prec)
             sync()
             t1 = time.perf_counter()
@@ -661,6 +666,7 @@ def bench_eval(a, dev, info):
             sync()
             out[f"nn_scoring_rows_per_s_{prec}"] = ns / (time.perf_counter() - t1)
             out[f"nn_scoring_checksum_{prec}"] = float(sc.sum())
+            out[f"nn_scoring_maxabs_vs_fp64_{prec}"] = float(np.abs(sc[:16384] - ref64).max())
     return out
 
 

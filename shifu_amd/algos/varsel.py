@@ -188,42 +188,17 @@ def auto_filter(mc, ccs, corr: np.ndarray | None = None, corr_nums=None):
 @torch.no_grad()
 def first_layer_fp32(xb: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, fl_cache: dict | None = None):
     """S = X W1^T + b1 in fp32.  GPU: ONE own-MFMA GEMM (gemm_kernels.hip, EPI_F32 tile) over
-    split-bf16 operands concatenated along K -- [xh | xh | xl | 1 | 1] . [Wh | Wl | Wh | bh | bl]^T,
-    hi = bf16(v), lo = bf16(v - hi) -- whose bf16 products are exact and accumulate in fp32:
-    the fp32 product to ~2^-17 relative (the Xl Wl term dropped), like K15's split digits.
-    ``fl_cache`` keeps the split weights and the operand buffer across row chunks."""
-    dev = xb.device
-    F, H1a = W1.shape[1], W1.shape[0]
-    fl_cache = {} if fl_cache is None else fl_cache
-    if dev.type != "cuda":
+    split-bf16 operands concatenated along K (``ops/gemm_ops.linear_fp32``, 3 part products
+    hi*hi + hi*mid + mid*hi, exact in the fp32 accumulator): the fp32 product to ~2^-17 relative,
+    like K15's split digits.  ``fl_cache`` keeps the split weights and the operand buffer across
+    row chunks."""
+    if xb.device.type != "cuda":
         return xb @ W1.t() + b1
-    from ..ops import _native as nat
-    R = xb.shape[0]
-    kp = ((3 * F + 2 + 63) // 64) * 64
-    nh = ((H1a + 7) // 8) * 8
-    if fl_cache.get("B") is None:
-        wh = W1.to(torch.bfloat16)
-        wl = (W1 - wh.float()).to(torch.bfloat16)
-        bh = b1.to(torch.bfloat16)
-        bl = (b1 - bh.float()).to(torch.bfloat16)
-        B = torch.zeros(H1a, kp, dtype=torch.bfloat16, device=dev)
-        B[:, :F], B[:, F:2 * F], B[:, 2 * F:3 * F] = wh, wl, wh
-        B[:, 3 * F], B[:, 3 * F + 1] = bh, bl
-        fl_cache["B"] = B
-    A = fl_cache.get("A")
-    if A is None or A.shape[0] < R:
-        A = torch.zeros(R, kp, dtype=torch.bfloat16, device=dev)
-        A[:, 3 * F: 3 * F + 2] = 1.0
-        fl_cache["A"] = A
-    A = A[:R]
-    xh = xb.to(torch.bfloat16)
-    A[:, :F] = xh
-    A[:, F:2 * F] = xh
-    A[:, 2 * F:3 * F] = (xb - xh.float()).to(torch.bfloat16)
-    S = torch.empty(R, nh, dtype=torch.float32, device=dev)
-    nat.call_hip("shifu_gemm_nt", A, kp, fl_cache["B"], kp, H1a, S, nh, None, 0, None, 0, None, 0,
-                 R, nh, kp, 3, 2, H1a, 0, 0.0, nat.stream_of(A))
-    return S[:, :H1a]
+    from ..ops.gemm_ops import SplitWeights, linear_fp32
+    fl_cache = {} if fl_cache is None else fl_cache
+    if fl_cache.get("sw") is None:
+        fl_cache["sw"] = SplitWeights(W1, b1, terms=3)
+    return linear_fp32(xb, W1, b1, sw=fl_cache["sw"])
 
 
 def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, row_chunk: int = 1 << 16,

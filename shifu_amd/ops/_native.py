@@ -56,6 +56,7 @@ HIP_SIGNATURES = {
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
     "shifu_optimizer_step_tf": "pppp" "li" "ffff" "ff" "p" "is",
     "shifu_cast_bf16": "plpliis",
+    "shifu_split_bf16_rows": "plli" "pl" "ii" "s",
     "shifu_transpose_cast": "plpiiis",
     # svm_kernels.hip
     "shifu_svm_smo": "pl" "ppp" "pp" "ii" "dd" "pp" "s",

@@ -76,6 +76,19 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
   return x;
 }
 
+// fp32-accurate forms (libm expf/tanhf/log1pf/sinf) for outputs kept in fp32 (split-bf16 scoring)
+__device__ __forceinline__ float act_fwd_precise(int act, float x) {
+  switch (act) {
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+    case ACT_TANH: return tanhf(x);
+    case ACT_SWISH: return x / (1.f + expf(-x));
+    case ACT_PTANH: return x > 0.f ? tanhf(x) : 0.25f * tanhf(x);
+    case ACT_LOG: return x >= 0.f ? log1pf(x) : -log1pf(-x);
+    case ACT_SIN: return sinf(x);
+  }
+  return act_fwd(act, x);
+}
+
 // true when derivative can be computed from the activation output alone
 __host__ __device__ constexpr inline bool act_deriv_from_output(int act) {
   return act == ACT_SIGMOID || act == ACT_TANH || act == ACT_LINEAR || act == ACT_RELU ||

@@ -216,6 +216,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
     return;
   } else if constexpr (EPI == EPI_F32) {
     // each lane owns 4 consecutive output columns of one row: one 16-B store (C is float, ldc floats)
+    // act != LINEAR applies the activation with the accurate libm forms (fp32 scoring: ops/gemm_ops.py)
     float* Cf = (float*)p.C;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -224,7 +225,12 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = m0 + wr * 64 + j * 16 + (lane & 15);
-        if (m < p.M) *(float4*)(Cf + (size_t)m * p.ldc + nb) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (p.act != ACT_LINEAR) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = act_fwd_precise(p.act, o[e]);
+        }
+        if (m < p.M) *(float4*)(Cf + (size_t)m * p.ldc + nb) = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
   } else {
@@ -1391,3 +1397,67 @@ SHIFU_API int shifu_corr_gemm(const void* planes, long plane_stride, int kpad, i
   return 0;
 }
 SHIFU_API int shifu_corr_job_bytes() { return (int)sizeof(CorrJob); }
+
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 operand builder for the fp32-accurate GEMM (ops/gemm_ops.py): x [M, K] fp32 (ld ldx)
+// -> A[:, t*K : (t+1)*K] = part_{xsel(t)}(x) for the T term pairs, parts hi = bf16(x),
+// mid = bf16(x - hi), lo = bf16(x - hi - mid) (residuals exact in fp32).  One pass: each lane
+// reads V consecutive floats once and writes its V bf16 per term (the torch form takes ~10
+// elementwise passes).  xsel packs 2 bits per term.
+// ---------------------------------------------------------------------------------------------
+template <int V>
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ x, long ldx, long M, int K,
+                                                          bf16_t* __restrict__ A, long lda, int T, int xsel) {
+  const int KV = K / V;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= M * KV) return;
+  const long r = idx / KV;
+  const int k = (int)(idx - r * KV) * V;
+  float v[V];
+  if constexpr (V == 4) {
+    const float4 q = *(const float4*)(x + r * ldx + k);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    v[0] = x[r * ldx + k];
+  }
+  bf16_t part[3][V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    float rem = v[e];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      part[q][e] = f2bf(rem);
+      rem -= bf2f(part[q][e]);
+    }
+  }
+  bf16_t* dst = A + r * lda + k;
+  for (int t = 0; t < T; ++t) {
+    const int s = (xsel >> (2 * t)) & 3;
+    if constexpr (V == 4) {
+      const bf16_t* p = s == 0 ? part[0] : (s == 1 ? part[1] : part[2]);
+      *(uint2*)(dst + (long)t * K) = make_uint2((uint32_t)p[0] | ((uint32_t)p[1] << 16),
+                                                (uint32_t)p[2] | ((uint32_t)p[3] << 16));
+    } else {
+      dst[(long)t * K] = s == 0 ? part[0][0] : (s == 1 ? part[1][0] : part[2][0]);
+    }
+  }
+}
+
+SHIFU_API int shifu_split_bf16_rows(const float* x, long ldx, long M, int K, void* A, long lda, int T, int xsel,
+                                    hipStream_t stream) {
+  if (M <= 0 || K <= 0) return 0;
+  if (T < 1 || T > 15 || ldx < K || lda < (long)T * K) return -1;
+  const bool vec = (K % 4 == 0) && (ldx % 4 == 0) && (lda % 4 == 0) && ((uintptr_t)x % 16 == 0) &&
+                   ((uintptr_t)A % 8 == 0);
+  const long n = M * (vec ? K / 4 : K);
+  const long blocks = (n + 255) / 256;
+  if (blocks > 0x7fffffffL) return -1;
+  if (vec)
+    hipLaunchKernelGGL(split_rows_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, stream, x, ldx, M, K,
+                       (bf16_t*)A, lda, T, xsel);
+  else
+    hipLaunchKernelGGL(split_rows_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, x, ldx, M, K,
+                       (bf16_t*)A, lda, T, xsel);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}

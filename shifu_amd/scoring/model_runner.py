@@ -92,31 +92,37 @@ def _nn_forward_bf16(net, Xt, dev, chunk):
 def nn_forward(net: nn_format.NNNetwork, X, device=None, chunk: int = 1 << 18, precision: str | None = None) -> np.ndarray:
     """Batched forward of an input-first network on the device -> [N, n_out] float64.
 
-    fp32 by default (``shifu.eval.nnPrecision=fp32``): torch fp32 GEMMs, scores agree with the
-    reference's float scoring (IndependentNNModel) to ~1e-6 -- eval / posttrain / SE base scores
-    are written as text and compared across runs.  ``bf16``: the trainer's own MFMA kernels
-    (``_nn_forward_bf16``), ~3 significant digits, for throughput-bound scoring."""
-    from ..models.nn import act_fwd
+    fp32 by default (``shifu.eval.nnPrecision=fp32``): scores agree with the reference's float
+    scoring (IndependentNNModel) to ~1e-6 -- eval / posttrain / SE base scores are written as text
+    and compared across runs.  On a GPU this runs on the framework's own MFMA GEMM over
+    split-bf16 operands (``ops/gemm_ops.linear_fp32``, 6 part products = fp32 accuracy, activation
+    in the fp32 tile epilogue); ``fp32_torch`` keeps the vendor fp32 GEMM (the oracle, and the CPU
+    path).  ``bf16``: the trainer's own MFMA kernels (``_nn_forward_bf16``), ~3 significant
+    digits, for throughput-bound scoring."""
+    from ..models.nn import ACT_IDS, act_fwd
     dev = _dev(device)
     if precision is None:
         from ..config import environment
         precision = environment.get("shifu.eval.nnPrecision", "fp32")
-    if precision == "bf16" and dev.type == "cuda":
-        Xt = torch.as_tensor(X)
-        sub = net.input_subset()
-        if sub is not None and Xt.shape[1] != net.n_in:
-            Xt = Xt[:, torch.as_tensor(sub, dtype=torch.long)]
-        return _nn_forward_bf16(net, Xt, dev, chunk)
-    Ws = [torch.as_tensor(np.asarray(W), dtype=torch.float32, device=dev) for W in net.weights]
-    out = []
     Xt = torch.as_tensor(X)
     sub = net.input_subset()
     if sub is not None and Xt.shape[1] != net.n_in:
         Xt = Xt[:, torch.as_tensor(sub, dtype=torch.long)]
+    if precision == "bf16" and dev.type == "cuda":
+        return _nn_forward_bf16(net, Xt, dev, chunk)
+    Ws = [torch.as_tensor(np.asarray(W), dtype=torch.float32, device=dev) for W in net.weights]
+    own = precision == "fp32" and dev.type == "cuda"
+    if own:
+        from ..ops.gemm_ops import SplitWeights, linear_fp32
+        sws = [SplitWeights(W[:, :-1], W[:, -1].contiguous(), terms=6) for W in Ws]
+    out = []
     for r in range(0, Xt.shape[0], chunk):
         a = Xt[r: r + chunk].to(dev, torch.float32)
         for l, W in enumerate(Ws):
-            a = act_fwd(net.acts[l], a @ W[:, :-1].t() + W[:, -1])
+            if own:
+                a = linear_fp32(a, None, None, sw=sws[l], act=ACT_IDS[net.acts[l]])
+            else:
+                a = act_fwd(net.acts[l], a @ W[:, :-1].t() + W[:, -1])
         out.append(a.double().cpu())
     return torch.cat(out).numpy() if out else np.zeros((0, net.n_out))
 

@@ -80,6 +80,40 @@ def test_native_parser_simd_fast_path_randomized():
             np.testing.assert_array_equal(nat[2][c][1], py[c][1], err_msg=f"column {c} missing {miss}")
 
 
+def test_native_parser_skipped_column_runs_randomized():
+    """Runs of unparsed columns are jumped with the 16-byte delimiter count (nth_delim): random
+    column subsets over ragged rows (short, long, blank, long fields > 16 bytes) give the same
+    values, string codes and bad-row count as the python parser."""
+    import random
+    rng = random.Random(7)
+    C = 41
+    toks = ["", "1.5", "-2", "abc", "x" * 40, "3.25", "?", "1e3", " 7 "]
+    rows = []
+    for _ in range(2000):
+        k = C + rng.choice([0, 0, 0, 0, -1, -7, 3, -C + 1])
+        rows.append("|".join(rng.choice(toks) for _ in range(max(k, 1))))
+        if rng.random() < 0.02:
+            rows.append("  \t")
+    data = ("\n".join(rows) + "\n").encode()
+    for trial in range(12):
+        kinds = [rng.choice([0, 0, 0, 1, 2]) for _ in range(C)]
+        if trial == 0:
+            kinds = [0] * C
+            kinds[rng.randrange(C)] = 1
+        n, bad, py = R._parse_python(data, "|", kinds, ["", "?"])
+        nat = R._parse_native(bytearray(data), "|", kinds, ["", "?"], 3)
+        if nat is None:
+            pytest.skip("native runtime not built")
+        assert nat[0] == n and nat[1] == bad, (trial, nat[:2], n, bad)
+        for c, k in enumerate(kinds):
+            if k == 1:
+                np.testing.assert_array_equal(nat[2][c][1], py[c][1], err_msg=f"trial {trial} column {c}")
+            elif k == 2:
+                a = np.array(nat[2][c][2] + [None], dtype=object)[nat[2][c][1]]
+                b = np.array(py[c][2] + [None], dtype=object)[py[c][1]]
+                assert list(a) == list(b), (trial, c)
+
+
 def test_expression_evaluator():
     from shifu_amd.data.reader import Column, RawTable
     cols = {"a": Column("a", "num", np.array([1.0, 2.0, np.nan, 4.0])),
