@@ -707,12 +707,22 @@ def bench_pipeline(a, dev, info):
         root = create_model_set("pipe", "NN", parent=work)
         lib = _native.rt()
         t0 = time.perf_counter()
+        rep = max(1, a.pipeline_replicate)
         for name, seed, nr in (("DataSet1", 11, rows), ("EvalSet1", 12, rows_eval)):
             d = os.path.join(root, "data", name)
             os.makedirs(d, exist_ok=True)
-            rc = lib.shifu_gen_csv(d.encode(), nr, F, 3, seed, 0.02, 20, min(16, os.cpu_count() or 4))
+            # --pipeline-replicate R: one generated part of rows/R rows, listed R times (symlinks):
+            # the reference's 20M x 1600 text (268 GB) does not fit the box's disk
+            g = d if rep == 1 else os.path.join(work, "gen_" + name)
+            os.makedirs(g, exist_ok=True)
+            rc = lib.shifu_gen_csv(g.encode(), -(-nr // rep), F, 3, seed, 0.02, 20, min(16, os.cpu_count() or 4))
             if rc:
                 raise RuntimeError("data generation failed (disk full?)")
+            if rep > 1:
+                parts = sorted(f for f in os.listdir(g) if not f.startswith((".", "_")))
+                for r_ in range(rep):
+                    for f in parts:
+                        os.symlink(os.path.join(g, f), os.path.join(d, f"r{r_:02d}-{f}"))
             hdr = ["id", "diagnosis", "wgt"] + [f"num_{j}" for j in range(F)] + [f"cat_{j}" for j in range(3)]
             with open(os.path.join(d, ".pig_header"), "w") as f:
                 f.write("|".join(hdr) + "\n")
@@ -734,6 +744,12 @@ def bench_pipeline(a, dev, info):
         mc.train["baggingNum"] = 1
         mc.train["validSetRate"] = 0.1
         mc.save()
+        if a.pipeline_tmp:                   # NormalizedData etc. on another filesystem (e.g. /dev/shm)
+            tdir = os.path.join(a.pipeline_tmp, "shifu_pipe_tmp")
+            shutil.rmtree(tdir, ignore_errors=True)
+            os.makedirs(tdir)
+            shutil.rmtree(os.path.join(root, "tmp"), ignore_errors=True)
+            os.symlink(tdir, os.path.join(root, "tmp"))
         gb = sum(os.path.getsize(os.path.join(root, "data", "DataSet1", f))
                  for f in os.listdir(os.path.join(root, "data", "DataSet1")))
         log(f"[bench] pipeline data: {rows} rows x {F} numeric + 3 categorical, {gb / 1e9:.1f} GB text, "
@@ -796,7 +812,9 @@ def bench_pipeline(a, dev, info):
         "train_epochs": epochs,
         "warmup": 0, "ms_per_step": total * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "bf16 NN GEMMs / fp64 stats", "data": f"synthetic '|'-delimited text on disk, {rows} training + "
-        f"{rows_eval} eval rows x {F} numeric + 3 categorical per GPU, planted rule on 20 columns (native generator)",
+        f"{rows_eval} eval rows x {F} numeric + 3 categorical per GPU, planted rule on 20 columns (native generator)"
+        + (f"; each set is one generated part listed {a.pipeline_replicate} times (symlinks: the box's disk cannot "
+           f"hold the full-size text)" if a.pipeline_replicate > 1 else ""),
         "config": {"model": f"default NN {F}-50-1 (tanh), SE varsel filterNum 200", "global_batch": rows * info.world_size,
                    "seq_len": None, "n_cols": F, "rows_per_gpu": rows, "parallelism": f"dp{info.world_size}"},
         "step_seconds": {k: round(v, 2) for k, v in times.items()}, "generation_s": round(t_gen, 1),
@@ -817,6 +835,8 @@ def bench_pipeline(a, dev, info):
             round((train_setup + ep_train * 200) * scale20 / 60.0, 2)
     if info.rank == 0 and not a.keep:
         shutil.rmtree(work, ignore_errors=True)
+        if a.pipeline_tmp:
+            shutil.rmtree(os.path.join(a.pipeline_tmp, "shifu_pipe_tmp"), ignore_errors=True)
     return out
 
 
@@ -885,6 +905,9 @@ def main():
     ap.add_argument("--host-rows", type=int, default=2_000_000, help="varsel --stream: host buffer rows")
     ap.add_argument("--workdir", default=None, help="pipeline: where the generated model set lives")
     ap.add_argument("--keep", action="store_true", help="pipeline: keep the generated model set")
+    ap.add_argument("--pipeline-replicate", type=int, default=1,
+                    help="pipeline: generate rows/R rows and list the part R times (disk-limited boxes)")
+    ap.add_argument("--pipeline-tmp", default=None, help="pipeline: put the model set's tmp/ (NormalizedData) here")
     ap.add_argument("--pipeline-epochs", type=int, default=40,
                     help="pipeline: numTrainEpochs of the NN (varsel SE trains half of them)")
     a = ap.parse_args()

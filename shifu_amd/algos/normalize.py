@@ -225,8 +225,20 @@ def _raw_matrix_dev(cols, table, dev):
     matrix are uploaded in place (the block's spanned rows as one copy, placed by a device-side
     gather); only the others (categorical indices, filtered tables) go through a host gather."""
     import torch
+    from ..data.gpu_parse import device_rows
     from ..data.reader import numeric_rows
     num_j = [j for j, cc in enumerate(cols) if not cc.is_categorical() and table[cc.name].kind == "num"]
+    blk = device_rows([table[cols[j].name] for j in num_j], dev) if num_j else None
+    if blk is not None:                      # GPU-parsed columns (K0): already in HBM
+        if len(num_j) == len(cols):
+            return blk
+        out = torch.empty((len(cols), table.n), dtype=torch.float64, device=dev)
+        out.index_copy_(0, torch.as_tensor(np.asarray(num_j, np.int64), device=dev), blk)
+        in_blk = set(num_j)
+        rest = [j for j in range(len(cols)) if j not in in_blk]
+        host = _raw_matrix([cols[j] for j in rest], table)
+        out.index_copy_(0, torch.as_tensor(np.asarray(rest, np.int64), device=dev), torch.as_tensor(host, device=dev))
+        return out
     hit = numeric_rows([table[cols[j].name].values for j in num_j]) if len(num_j) > 1 else None
     if hit is None:
         return torch.as_tensor(_raw_matrix(cols, table), device=dev)
@@ -370,9 +382,10 @@ class NormPlan:
     1 at ``width``) and/or the uint8 CleanedData codes; on the CPU the numpy oracle does the same."""
 
     def __init__(self, mc, ccs, cols, norm_type: str | None = None, want_x: bool = True,
-                 want_codes: bool = False, x_dtype: str = "float32", device=None):
+                 want_codes: bool = False, x_dtype: str = "float32", device=None, pinned_out: int = 0):
         import torch
         self.mc, self.cols = mc, list(cols)
+        self.pinned_out, self._pins, self._pin_i = int(pinned_out), {}, {}
         self.nt = norm_type or mc.norm_type
         self.cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
         self.want_x, self.want_codes = want_x, want_codes
@@ -442,6 +455,34 @@ class NormPlan:
                                cip=t(cip, torch.int32), cbounds=t(cb, torch.float64))
         return self._dev_specs
 
+    def _host(self, key, t):
+        """D2H of one output.  ``pinned_out`` = k: into the next of k rotating page-locked buffers
+        (DMA rate instead of a pageable copy; the returned array is overwritten k calls later --
+        the streamed norm keeps at most one chunk in its writer)."""
+        import torch
+        if not self.pinned_out:
+            return t.cpu().numpy()
+        i = self._pin_i[key] = (self._pin_i.get(key, -1) + 1) % self.pinned_out
+        buf = self._pins.get((key, i))
+        if buf is None or buf.numel() < t.numel():
+            buf = self._pins[(key, i)] = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
+        h = buf[: t.numel()].view(t.shape)
+        h.copy_(t)
+        return h.numpy()
+
+    def _onehot_specs(self):
+        """Device [F][5] (is_cat, bnd_off, nbnd, width, out_col) + packed numeric boundaries."""
+        import torch
+        if getattr(self, "_oh", None) is None:
+            ip, bounds = np.zeros((len(self.host_cols), 5), np.int32), []
+            for f, (cc, p0, width) in enumerate(self.host_cols):
+                bb = [] if cc.is_categorical() else list(cc.bin_boundary or [float("-inf")])
+                ip[f] = [int(cc.is_categorical()), len(bounds), len(bb), width, p0]
+                bounds.extend(bb)
+            self._oh = (torch.as_tensor(ip).to(self.dev),
+                        torch.as_tensor(np.asarray(bounds or [0.0], np.float64)).to(self.dev))
+        return self._oh
+
     def _buf(self, key, shape, dtype, init=None):
         import torch
         b = self._bufs.get(key)
@@ -452,8 +493,9 @@ class NormPlan:
             self._bufs[key] = b
         return b[: shape[0]]
 
-    def run(self, table) -> dict:
-        """-> {"X": fp32 [n, width] | "Xb": uint16 (bf16 bits) [n, kpad], "codes": [n, F]} (numpy)."""
+    def run(self, table, keep_device: bool = False) -> dict:
+        """-> {"X": fp32 [n, width] | "Xb": uint16 (bf16 bits) [n, kpad], "codes": [n, F]} (numpy;
+        ``keep_device`` on a GPU: "X" as a device tensor -- a fresh copy, not the reused buffer)."""
         n = table.n
         out = {}
         bf16 = self.want_x and self.x_dtype == "bf16"
@@ -505,20 +547,22 @@ class NormPlan:
                                   0 if codes is None else codes.stride(0), nat.stream_of(vals))
             if rc:
                 raise RuntimeError(f"shifu_norm_codes failed rc={rc}")
-        for cc, p0, width in self.host_cols:
-            oh = torch.as_tensor(normalize_column(cc, table[cc.name], self.nt, self.cutoff), dtype=torch.float32,
-                                 device=self.dev)
-            if outf is not None:
-                outf[:, p0: p0 + width] = oh
-            if outb is not None:
-                outb[:, p0: p0 + width] = oh.to(torch.bfloat16)
+        if self.host_cols and n and (outf is not None or outb is not None):
+            # one-hot columns: one K5 one-hot launch (raw values / category indices -> 0/1 blocks)
+            ohv = _raw_matrix_dev([cc for cc, _, _ in self.host_cols], table, self.dev)
+            oip, obnd = self._onehot_specs()
+            rc = nat.call_hip("shifu_onehot", ohv, ohv.stride(0), n, len(self.host_cols), oip, obnd,
+                              outf, 0 if outf is None else outf.stride(0), outb, 0 if outb is None else outb.stride(0),
+                              nat.stream_of(ohv))
+            if rc:
+                raise RuntimeError(f"shifu_onehot failed rc={rc}")
         if outf is not None:
-            out["X"] = outf[:, : self.width].cpu().numpy()
+            out["X"] = outf[:, : self.width].clone() if keep_device else self._host("X", outf[:, : self.width])
         if outb is not None:
-            out["Xb"] = outb.view(torch.int16).cpu().numpy().view(np.uint16)
+            out["Xb"] = self._host("Xb", outb.view(torch.int16)).view(np.uint16)
         if self.want_codes:
             if codes is not None:
-                out["codes"] = codes.cpu().numpy()
+                out["codes"] = self._host("codes", codes)
             else:
                 C, _, _ = tree_bin_codes(None, table, self.cols)
                 out["codes"] = C.astype(self.code_dtype)

@@ -97,6 +97,11 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
     cache, cached_bytes, cache_ok = [], 0, True
 
     def upload(md, bt):
+        from ..data.gpu_parse import device_rows
+        if dev.type == "cuda":          # GPU-parsed columns (K0): already in HBM
+            v = device_rows([md.table.columns.get(c.name) for c in bt.cols], dev)
+            if v is not None:
+                return v
         vals = S.upload_columns([md.table[c.name].numeric() if c.name in md.table
                                  else np.full(md.n, np.nan) for c in bt.cols], dev)
         return vals

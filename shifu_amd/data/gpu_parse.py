@@ -1,0 +1,199 @@
+"""GPU parse of text blocks (K0, host side of ``ops/csrc/csv_kernels.hip``).
+
+SURVEY §7.1 choice 2 asks that the raw text stop being re-tokenized on the host for every step
+(``stats``, ``norm``, ``eval``; the reference re-reads text per step: ``P/Normalize.pig:35-46``).
+On a GPU run the bulk numeric columns of each block are parsed on the device instead:
+
+1. the block reader (``data/stream._lines_in_range``) fills page-locked buffers with parallel
+   preads, so a block goes to HBM as ONE DMA (``torch`` copy from pinned memory);
+2. the host parser (``runtime/csrc/csv_parser.cpp``) runs over the same bytes with only the few
+   "meta" columns requested (target, weight, filter / categorical columns): it frames the rows,
+   counts bad rows and builds the string dictionaries, skipping the unparsed column runs with a
+   16-byte delimiter count;
+3. ``shifu_csv_gpu_parse`` tokenizes and converts every bulk numeric field (one wave per line) into
+   a column-major fp64 block in HBM; fields outside the Clinger fast path come back as a short list
+   the host finishes with its own strtod path (``shifu_parse_fields``), blank lines are dropped.
+
+The result is bit-identical to the host parse (tests/test_gpu_parse.py).  Parsed columns stay in
+HBM as :class:`DeviceBlock` rows: ``stats`` batches and the ``norm`` K5 pass read them in place
+(``device_rows``); anything that asks for host values gets one D2H copy of the block.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ..utils.log import get_logger
+
+_log = get_logger("data.gpu_parse")
+
+FB_CAP = 1 << 20          # fallback fields per block before the whole block is parsed on the host
+MAX_TOKENS, TOKEN_BYTES = 8, 15
+
+
+class DeviceBlock:
+    """Numeric columns of one parsed block: ``D`` [k, n] fp64 in HBM; a host copy on demand."""
+    __slots__ = ("D", "_host")
+
+    def __init__(self, D):
+        self.D = D
+        self._host = None
+
+    def host(self) -> np.ndarray:
+        if self._host is None:
+            self._host = self.D.cpu().numpy()
+        return self._host
+
+    def take(self, idx) -> "DeviceBlock":
+        import torch
+        idx = np.asarray(idx)
+        if idx.dtype == bool:
+            idx = np.flatnonzero(idx)
+        return DeviceBlock(self.D.index_select(1, torch.as_tensor(idx, dtype=torch.long, device=self.D.device)))
+
+
+class DevRef:
+    """Row ``row`` of a :class:`DeviceBlock` (one column's values)."""
+    __slots__ = ("block", "row")
+
+    def __init__(self, block: DeviceBlock, row: int):
+        self.block, self.row = block, row
+
+    def host(self) -> np.ndarray:
+        return self.block.host()[self.row]
+
+    def tensor(self):
+        return self.block.D[self.row]
+
+    def __len__(self):
+        return int(self.block.D.shape[1])
+
+
+def device_rows(cols, dev):
+    """[C, n] fp64 device tensor of the columns when all of them are rows of ONE device block on
+    ``dev`` (a view for a consecutive run, else one gather), else None."""
+    import torch
+    refs = [getattr(c, "dev", None) if c is not None else None for c in cols]
+    if not refs or any(r is None for r in refs):
+        return None
+    blk = refs[0].block
+    want = torch.device(dev)
+    if want.type == "cuda" and want.index is None:
+        want = torch.device("cuda", torch.cuda.current_device())
+    if any(r.block is not blk for r in refs) or blk.D.device != want:
+        return None
+    rows = [r.row for r in refs]
+    if rows == list(range(rows[0], rows[0] + len(rows))):
+        return blk.D[rows[0]: rows[0] + len(rows)]
+    return blk.D.index_select(0, torch.as_tensor(rows, dtype=torch.long, device=blk.D.device))
+
+
+def enabled(dev) -> bool:
+    """``shifu.data.gpuParse`` (default auto: on for a CUDA device with the HIP library present)."""
+    from ..config import environment
+    mode = str(environment.get("shifu.data.gpuParse", "auto")).lower()
+    if mode in ("false", "0", "off") or dev is None:
+        return False
+    import torch
+    if torch.device(dev).type != "cuda":
+        return False
+    from ..ops import _native as nat
+    if mode in ("true", "1", "on"):
+        nat.hip()
+        return True
+    return nat.hip_available() and nat.rt() is not None
+
+
+class GpuBlockParser:
+    """Parses blocks with the numeric header columns ``gpu_cols`` on the device and the rest of
+    ``kinds`` on the host.  ``usable`` is False when the data set's format needs the host parser
+    throughout (multi-byte delimiter, more / longer missing tokens than the kernel holds)."""
+
+    def __init__(self, kinds: list, gpu_cols: list, delim: str, missing: list, dev):
+        import torch
+        self.dev = torch.device(dev)
+        self.kinds = list(kinds)
+        self.gpu_cols = sorted(c for c in gpu_cols if kinds[c] == 1)
+        self.kinds_host = list(kinds)
+        for c in self.gpu_cols:
+            self.kinds_host[c] = 0
+        toks = []
+        for t in missing:
+            t = str(t).strip()
+            if t and t not in toks:
+                toks.append(t)
+        enc = [t.encode("utf-8") for t in toks]
+        d = (delim or "|").encode("utf-8")
+        self.usable = (len(d) == 1 and d != b"\n" and len(enc) <= MAX_TOKENS and
+                       all(len(t) <= TOKEN_BYTES and b"\0" not in t for t in enc) and bool(self.gpu_cols))
+        self.delim, self.missing = delim or "|", list(missing)
+        self.dbyte = d[0] if len(d) == 1 else 0
+        self.toks = b"".join(t + b"\0" for t in enc)
+        self.ntok = len(enc)
+        slot = np.full(len(kinds), -1, np.int32)
+        slot[self.gpu_cols] = np.arange(len(self.gpu_cols), dtype=np.int32)
+        self.slot = torch.as_tensor(slot, device=self.dev)
+        self.fb = torch.empty(4 * FB_CAP, dtype=torch.long, device=self.dev)
+        self.fb_n = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.stats = {"blocks": 0, "fallback_fields": 0, "host_blocks": 0}
+
+    def parse(self, data, nthreads: int):
+        """``data``: a memoryview of complete lines inside a page-locked uint8 ndarray (or any
+        buffer: then it is staged) -> the host parser's (n, bad, {column: (kind, values, dict)})
+        with the GPU columns as ``("num", DevRef, [])``."""
+        import torch
+        from ..ops import _native as nat
+        from .reader import parse_block
+        with torch.cuda.device(self.dev):          # a reader thread: HIP's current device = ours
+            return self._parse(data, nthreads)
+
+    def _parse(self, data, nthreads: int):
+        import torch
+        from ..ops import _native as nat
+        from .reader import parse_block
+        L = len(data)
+        n, bad, out = parse_block(data, self.delim, self.kinds_host, self.missing, nthreads)
+        self.stats["blocks"] += 1
+        if L == 0 or n == 0:
+            blk = DeviceBlock(torch.empty((len(self.gpu_cols), 0), dtype=torch.float64, device=self.dev))
+            out.update({c: ("num", DevRef(blk, j), []) for j, c in enumerate(self.gpu_cols)})
+            return n, bad, out
+        host = np.frombuffer(data, dtype=np.uint8)
+        src = torch.from_numpy(host)
+        dbuf = torch.empty(L + 64, dtype=torch.uint8, device=self.dev)
+        dbuf[:L].copy_(src)
+        d = dbuf[:L]
+        ends = torch.nonzero(d == 10).flatten()
+        if int(host[-1]) != 10:
+            ends = torch.cat([ends, torch.tensor([L], dtype=torch.long, device=self.dev)])
+        nl = int(ends.numel())
+        starts = torch.zeros(nl, dtype=torch.long, device=self.dev)
+        if nl > 1:
+            starts[1:] = ends[:-1] + 1
+        vals = torch.empty((len(self.gpu_cols), nl), dtype=torch.float64, device=self.dev)
+        lflags = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        self.fb_n.zero_()
+        nat.call_hip("shifu_csv_gpu_parse", dbuf, starts, ends, nl, self.slot, len(self.kinds), vals, nl, lflags,
+                     self.fb, FB_CAP, self.fb_n, self.dbyte, self.ntok, self.toks, nat.stream_of(dbuf))
+        nfb = int(self.fb_n.item())
+        if nfb > FB_CAP:                         # a mostly non-decimal block: host parse throughout
+            self.stats["host_blocks"] += 1
+            return parse_block(data, self.delim, self.kinds, self.missing, nthreads)
+        if nfb:
+            self.stats["fallback_fields"] += nfb
+            fb = self.fb[: 4 * nfb].view(nfb, 4).cpu().numpy()
+            fv = np.empty(nfb, np.float64)
+            addr = ctypes.addressof(ctypes.c_char.from_buffer(data)) if not data.readonly else \
+                np.frombuffer(data, np.uint8).ctypes.data
+            nat.rt().shifu_parse_fields(addr, fb.ctypes.data, nfb, fv.ctypes.data)
+            fbt = torch.as_tensor(fb, device=self.dev)
+            vals[fbt[:, 1], fbt[:, 0]] = torch.as_tensor(fv, device=self.dev)
+        blank = (lflags & 1).bool()
+        if bool(blank.any()):
+            vals = vals[:, torch.nonzero(~blank).flatten()]
+        if vals.shape[1] != n:
+            raise RuntimeError(f"GPU parse framed {vals.shape[1]} rows, host parser {n}")
+        blk = DeviceBlock(vals)
+        out.update({c: ("num", DevRef(blk, j), []) for j, c in enumerate(self.gpu_cols)})
+        return n, bad, out

@@ -92,12 +92,29 @@ def read_header(header_path: str | None, header_delim: str = "|", data_path: str
     return [h.strip() for h in _first_line(files[0]).split(data_delim or "|")]
 
 
-@dataclass
 class Column:
-    name: str
-    kind: str                         # "num" | "str"
-    values: np.ndarray                # float64 (num, NaN = missing) | int32 codes (str, -1 = missing)
-    dictionary: list = field(default_factory=list)
+    """One parsed column: ``values`` float64 (num, NaN = missing) | int32 codes (str, -1 =
+    missing).  A numeric column parsed on the GPU (data/gpu_parse.py) carries ``dev`` (its row of
+    a device block) and materializes host ``values`` only when asked."""
+    __slots__ = ("name", "kind", "_values", "dictionary", "dev")
+
+    def __init__(self, name: str, kind: str, values=None, dictionary=None, dev=None):
+        self.name, self.kind, self._values = name, kind, values
+        self.dictionary = dictionary if dictionary is not None else []
+        self.dev = dev
+
+    @property
+    def values(self) -> np.ndarray:
+        if self._values is None and self.dev is not None:
+            self._values = self.dev.host()
+        return self._values
+
+    @values.setter
+    def values(self, v):
+        self._values, self.dev = v, None
+
+    def __len__(self):
+        return len(self.dev) if self._values is None and self.dev is not None else len(self._values)
 
     def strings(self) -> np.ndarray:
         if self.kind == "str":
@@ -145,7 +162,16 @@ class RawTable:
         return name in self.columns
 
     def take(self, idx: np.ndarray) -> "RawTable":
-        cols = {k: Column(c.name, c.kind, c.values[idx], c.dictionary) for k, c in self.columns.items()}
+        cols, blocks = {}, {}
+        for k, c in self.columns.items():
+            if c._values is None and c.dev is not None:      # GPU-parsed: gather each block once
+                from .gpu_parse import DevRef
+                b = c.dev.block
+                if id(b) not in blocks:
+                    blocks[id(b)] = b.take(idx)
+                cols[k] = Column(c.name, c.kind, dev=DevRef(blocks[id(b)], c.dev.row))
+            else:
+                cols[k] = Column(c.name, c.kind, c.values[idx], c.dictionary)
         return RawTable(self.header, cols, int(len(idx)) if idx.dtype != bool else int(idx.sum()), self.bad_rows)
 
 
@@ -325,10 +351,14 @@ def table_from_parts(header: list, kinds: list, parts: list, data_path: str = ""
             continue
         name = header[ci]
         if k == 1:
-            if len(parts) == 1:             # one parsed block: its array as is (no copy)
-                vals = parts[0][2][ci][1]
+            if len(parts) == 1 and not isinstance(parts[0][2][ci][1], np.ndarray):
+                cols[name] = Column(name, "num", dev=parts[0][2][ci][1])   # GPU-parsed (DevRef)
+                continue
+            arrs = [p[2][ci][1] if isinstance(p[2][ci][1], np.ndarray) else p[2][ci][1].host() for p in parts]
+            if len(arrs) == 1:              # one parsed block: its array as is (no copy)
+                vals = arrs[0]
             else:
-                vals = np.concatenate([p[2][ci][1] for p in parts]) if parts else np.empty(0)
+                vals = np.concatenate(arrs) if arrs else np.empty(0)
             cols[name] = Column(name, "num", vals)
         else:
             gdict, remapped = {}, []

@@ -55,23 +55,86 @@ def byte_ranges(files, rank: int = 0, world: int = 1):
     return sorted(out)
 
 
-def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int = 1):
+READ_THREADS = int(os.environ.get("SHIFU_READ_THREADS", "4"))   # parallel preads per block
+
+
+def _pread_into(fd: int, mv, off: int, want: int) -> int:
+    """Fill ``mv[:want]`` from file offset ``off`` -> bytes read (short only at end of file).
+    Blocks of >= 32 MB are read as READ_THREADS concurrent preads (page-cache copies run at a few
+    GB/s per thread; one block of a 1600-column text is ~256 MB)."""
+    def one(a, b):
+        got = 0
+        while a + got < b:
+            r = os.preadv(fd, [mv[a + got: b]], off + a + got)
+            if not r:
+                break
+            got += r
+        return got
+    nt = READ_THREADS if want >= (32 << 20) else 1
+    if nt <= 1:
+        return one(0, want)
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = [want * i // nt for i in range(nt + 1)]
+    with ThreadPoolExecutor(nt) as ex:
+        got = list(ex.map(lambda i: one(cuts[i], cuts[i + 1]), range(nt)))
+    total = 0
+    for i, g in enumerate(got):
+        total += g
+        if g < cuts[i + 1] - cuts[i]:
+            break
+    return total
+
+
+def _find_nl(buf, lo: int, hi: int, last: bool) -> int:
+    """First (``last``: last) '\n' in buf[lo:hi] -> index or -1 (bytearray or uint8 ndarray)."""
+    if isinstance(buf, bytearray):
+        return buf.rfind(b"\n", lo, hi) if last else buf.find(b"\n", lo, hi)
+    import numpy as np
+    step = 1 << 16
+    if last:
+        b = hi
+        while b > lo:
+            a = max(lo, b - step)
+            idx = np.flatnonzero(buf[a:b] == 10)
+            if len(idx):
+                return a + int(idx[-1])
+            b, step = a, step * 2
+    else:
+        a = lo
+        while a < hi:
+            b = min(hi, a + step)
+            idx = np.flatnonzero(buf[a:b] == 10)
+            if len(idx):
+                return a + int(idx[0])
+            a, step = b, step * 2
+    return -1
+
+
+def _new_buf(n: int, pinned: bool):
+    if not pinned:
+        return bytearray(n)
+    import torch
+    # the ndarray's base holds the tensor's storage: views of a block keep its pages alive
+    return torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy()
+
+
+def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int = 1, pinned: bool = False):
     """Yield (offset, block) blocks of complete lines whose first byte lies in [start, end).
 
-    Blocks are memoryviews into ``nbuf`` rotating buffers, filled with ``readinto`` (no copy of
-    the text; the old ``carry + read()`` / slicing made two copies of every block): a block stays
-    valid until ``nbuf - 1`` further blocks have been produced (1: until the next is requested)."""
+    Blocks are memoryviews into ``nbuf`` rotating buffers, filled by (parallel) preads (no copy of
+    the text): a block stays valid until ``nbuf - 1`` further blocks have been produced (1: until
+    the next is requested).  ``pinned``: the buffers are page-locked host memory (uint8 ndarrays
+    of pinned torch tensors) so a GPU parse can DMA a block straight to HBM."""
     bufs = [None] * max(1, nbuf)
     k = 0
-    with open(path, "rb", buffering=0) as fh:
+    fd = os.open(path, os.O_RDONLY)
+    try:
         pos = start
         if start > 0:
-            fh.seek(start - 1)
-            if fh.read(1) != b"\n":           # mid-line: that line belongs to the previous range
+            if os.pread(fd, 1, start - 1) != b"\n":     # mid-line: that line belongs to the previous range
                 with open(path, "rb") as fl:
                     fl.seek(start)
                     pos = start + len(fl.readline())
-        fh.seek(pos)
         carry = b""
         while pos < end:
             # never read (much) past the range: the line straddling `end` is completed by the
@@ -80,40 +143,42 @@ def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int
             need = len(carry) + want
             buf = bufs[k]
             if buf is None or len(buf) < need:
-                buf = bufs[k] = bytearray(need + (1 << 16))   # sized to the block: small ranges stay small
+                buf = bufs[k] = _new_buf(need + (1 << 16), pinned)   # sized to the block
             mv = memoryview(buf)
             c = len(carry)
             mv[:c] = carry
-            got = 0
-            while got < want:                  # a raw read may return short
-                r = fh.readinto(mv[c + got: c + want])
-                if not r:
-                    break
-                got += r
+            got = _pread_into(fd, mv[c:], pos + c, want)
             filled = c + got
             if got == 0:
                 if carry:
                     yield pos, mv[:c]
                 return
-            cut = buf.rfind(b"\n", 0, filled)
+            cut = _find_nl(buf, 0, filled, last=True)
             if cut < 0:
                 carry = bytes(mv[:filled])     # one line longer than the block: read on
                 continue
             carry = bytes(mv[cut + 1:filled])
             k = (k + 1) % len(bufs)
             if pos + cut + 1 > end:           # stop after the line that starts before `end`
-                i = buf.find(b"\n", max(0, end - pos - 1), filled)
+                i = _find_nl(buf, max(0, end - pos - 1), filled, last=False)
                 yield pos, mv[:i + 1]
                 return
             yield pos, mv[:cut + 1]
             pos += cut + 1
+    finally:
+        os.close(fd)
 
 
 def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kinds: list, nthreads: int,
-                resume=None):
+                resume=None, gpu=None):
     """Yield ((file index, offset), parsed part) for this rank's share, in file order.  ``resume``
     = (file index, offset) of a block yielded by an earlier pass: start there (earlier blocks are
-    neither read nor parsed; an offset is always a line start)."""
+    neither read nor parsed; an offset is always a line start).  ``gpu``: a
+    :class:`~.gpu_parse.GpuBlockParser` -- plain-text blocks are read into page-locked buffers and
+    its columns parsed on the device."""
+    pinned = gpu is not None and gpu.usable
+    parse = (lambda data: gpu.parse(data, nthreads)) if pinned else \
+        (lambda data: parse_block(data, plan.delim, kinds, plan.missing, nthreads))
     files = list_data_files(plan.data_path)
     if not files:
         raise FileNotFoundError(f"no data under {plan.data_path}")
@@ -140,8 +205,9 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
         # and the native parser both release the GIL).  PREFETCH_READ + 2 buffers: the block being
         # parsed (its parse copies everything out before the next block is requested), the queued
         # ones and the one being filled
-        blocks = (prefetched(lambda: _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + 2), PREFETCH_READ)
-                  if PREFETCH_READ > 0 else _lines_in_range(path, a, b, chunk_bytes))
+        blocks = (prefetched(lambda: _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + 2, pinned=pinned),
+                             PREFETCH_READ)
+                  if PREFETCH_READ > 0 else _lines_in_range(path, a, b, chunk_bytes, pinned=pinned))
         for off, data in blocks:
             if plan.skip_header_line and fi == 0 and off == 0:
                 nl = bytes(data[: 1 << 20]).find(b"\n")
@@ -150,15 +216,44 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
                 data = data[nl + 1:] if nl >= 0 else b""
                 if not len(data):
                     continue
-            yield (fi, off), parse_block(data, plan.delim, kinds, plan.missing, nthreads)
+            yield (fi, off), parse(data)
+
+
+def gpu_parser(plan: DatasetPlan, gpu_cols, dev):
+    """A GpuBlockParser for the numeric plan columns named in ``gpu_cols`` (minus the weight and
+    the filter / segment expression inputs, which the purifier reads on the host), or None when
+    GPU parsing is off (``shifu.data.gpuParse``) or nothing qualifies."""
+    if not gpu_cols or dev is None or plan.seg_names:
+        return None
+    from . import gpu_parse as G
+    if not G.enabled(dev):
+        return None
+    kinds = column_kinds(plan.header, plan.nums, plan.strs)
+    skip = set()
+    if plan.weight:
+        skip.add(plan.weight)
+    from .expr import Evaluator
+    for e in (plan.filt, plan.weight):
+        if e and str(e).strip():
+            try:
+                skip |= set(Evaluator(str(e)).columns())
+            except Exception:
+                pass
+    want = set(gpu_cols) - skip
+    idx = [i for i, h in enumerate(plan.header) if h in want and kinds[i] == 1]
+    if not idx:
+        return None
+    p = G.GpuBlockParser(kinds, idx, plan.delim, plan.missing, dev)
+    return p if p.usable else None
 
 
 def iter_tables(plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
-                nthreads: int | None = None, resume=None):
-    """Yield (key, RawTable) row chunks of this rank's share of the data set, in file order."""
+                nthreads: int | None = None, resume=None, gpu=None):
+    """Yield (key, RawTable) row chunks of this rank's share of the data set, in file order
+    (``gpu``: see :func:`_iter_parts`)."""
     kinds = column_kinds(plan.header, plan.nums, plan.strs)
     nthreads = nthreads or min(16, os.cpu_count() or 4)
-    for key, part in _iter_parts(plan, chunk_bytes, rank, world, kinds, nthreads, resume):
+    for key, part in _iter_parts(plan, chunk_bytes, rank, world, kinds, nthreads, resume, gpu):
         yield key, table_from_parts(plan.header, kinds, [part], plan.data_path)
 
 
@@ -235,20 +330,25 @@ def prefetched(gen_fn, depth: int = 2):
 
 def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTES, rank: int = 0, world: int = 1,
                     sample_rate: float = 1.0, sample_neg_only: bool = False, seed: int = 0,
-                    require_target: bool = True, row0: int = 0, resume=None, with_keys: bool = False):
+                    require_target: bool = True, row0: int = 0, resume=None, with_keys: bool = False,
+                    gpu_cols=None, dev=None):
     """Yield purified :class:`ModelData` chunks of this rank's byte range; ``row0`` = the global
     raw-row index of the rank's first row (sampling draws are per global row).  Chunks are
     produced ``shifu.data.prefetch`` (default 1) ahead on a background thread.
 
     ``with_keys``: yield (key, md) with key = (file index, offset, raw row index of the block),
     which a later pass hands back as ``resume`` to start at that block (stats passes whose first
-    blocks are cached in HBM re-parse only the rest)."""
+    blocks are cached in HBM re-parse only the rest).
+
+    ``gpu_cols`` + ``dev``: those numeric columns are parsed on the GPU (data/gpu_parse.py) and
+    stay in HBM as device-block rows (``gpu_parse.device_rows``)."""
     from ..config import environment
+    gp = gpu_parser(plan, gpu_cols, dev)
 
     def produce():
         r = row0 if resume is None else resume[2]
         for key, table in iter_tables(plan, chunk_bytes, rank, world,
-                                      resume=None if resume is None else resume[:2]):
+                                      resume=None if resume is None else resume[:2], gpu=gp):
             n = table.n
             md = finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, r)
             k = (key[0], key[1], r)

@@ -27,7 +27,7 @@ _rt = None
 
 # argument codes: p=void*, l=int64, i=int32, f=float, d=double, s=hipStream_t
 _T = {"p": ctypes.c_void_p, "l": ctypes.c_long, "i": ctypes.c_int, "f": ctypes.c_float,
-      "d": ctypes.c_double, "s": ctypes.c_void_p, "P": ctypes.c_char_p}
+      "d": ctypes.c_double, "s": ctypes.c_void_p, "P": ctypes.c_char_p, "L": ctypes.c_long}
 
 HIP_SIGNATURES = {
     # mlp_kernels.hip
@@ -57,6 +57,8 @@ HIP_SIGNATURES = {
     "shifu_optimizer_step_tf": "pppp" "li" "ffff" "ff" "p" "is",
     "shifu_cast_bf16": "plpliis",
     "shifu_split_bf16_rows": "plli" "pl" "ii" "s",
+    # csv_kernels.hip
+    "shifu_csv_gpu_parse": "pppl" "pi" "pl" "p" "pip" "iiP" "s",
     "shifu_transpose_cast": "plpiiis",
     # svm_kernels.hip
     "shifu_svm_smo": "pl" "ppp" "pp" "ii" "dd" "pp" "s",
@@ -80,6 +82,7 @@ HIP_SIGNATURES = {
     "shifu_normalize": "plli" "pppp" "pl" "s",
     "shifu_bin_codes": "plli" "pp" "pl" "s",
     "shifu_norm_codes": "plli" "pppp" "pp" "pl" "pl" "pl" "s",
+    "shifu_onehot": "plli" "pp" "pl" "pl" "s",
     "shifu_lr_grad": "plli" "i" "ppp" "pp" "i" "s",
     "shifu_sensitivity": "plpl" "pp" "f" "p" "l" "iiiii" "p" "s",
     "shifu_se_perturb": "plpl" "p" "ii" "iiii" "pl" "s",
@@ -117,6 +120,7 @@ RT_SIGNATURES = {
     "shifu_gather_lines": ("ppplPp", "l"),
     "shifu_gen_csv": ("Pliildii", "i"),
     "shifu_gen_strong_cols": ("iip", "i"),
+    "shifu_parse_fields": ("ppLp", "l"),
 }
 
 

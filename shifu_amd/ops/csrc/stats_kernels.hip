@@ -813,3 +813,44 @@ SHIFU_API int shifu_column_metrics(const double* neg, const double* pos, const i
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
+
+// ---------------------------------------------------------------------------------------------
+// K5 one-hot columns (ONEHOT, and ZSCALE_ONEHOT's categoricals): raw values column-major fp64
+// [F][ldv] (categorical index, -1 / NaN missing) -> `width` 0/1 outputs per column at out_col,
+// the missing / unknown slot last (normalize_column's ONEHOT branch).  ip [F][5]: is_cat,
+// bnd_off, nbnd, width, out_col.  One thread per (row, column); the column-major read is
+// coalesced over rows.
+// ---------------------------------------------------------------------------------------------
+struct OneHotArgs {
+  const double* vals; long ldv; long n; int F;
+  const int* ip; const double* bounds;
+  float* outf; long ldf; bf16_t* outb; long ldb;
+};
+
+__global__ void __launch_bounds__(256) onehot_kernel(OneHotArgs a) {
+  const long r = (long)blockIdx.x * 256 + threadIdx.x;
+  const int f = blockIdx.y;
+  if (r >= a.n) return;
+  const int* p = a.ip + f * 5;
+  const double v = a.vals[(long)f * a.ldv + r];
+  int idx;
+  if (p[0]) idx = (v != v || v < 0) ? -1 : (int)v;
+  else idx = (v != v) ? -1 : bin_search(a.bounds + p[1], p[2], v);
+  const int width = p[3], oc = p[4];
+  if (idx < 0 || idx >= width) idx = width - 1;
+  for (int j = 0; j < width; ++j) {
+    const float o = j == idx ? 1.f : 0.f;
+    if (a.outf) a.outf[r * a.ldf + oc + j] = o;
+    if (a.outb) a.outb[r * a.ldb + oc + j] = f2bf(o);
+  }
+}
+
+SHIFU_API int shifu_onehot(const double* vals, long ldv, long n, int F, const int* ip, const double* bounds,
+                           float* outf, long ldf, void* outb, long ldb, hipStream_t stream) {
+  if (n <= 0 || F <= 0) return 0;
+  if (F > 65535 || !ip || ldv < n) return -1;
+  OneHotArgs a{vals, ldv, n, F, ip, bounds, outf, ldf, (bf16_t*)outb, ldb};
+  hipLaunchKernelGGL(onehot_kernel, dim3((unsigned)((n + 255) / 256), F), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}

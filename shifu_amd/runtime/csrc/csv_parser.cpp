@@ -560,3 +560,15 @@ SHIFU_RT_API void shifu_csv_free(void* h) {
   delete P->chunks;
   delete P;
 }
+
+// The GPU field parser's fallback list (ops/csrc/csv_kernels.hip): n entries (line, slot, start,
+// end) of trimmed, non-missing fields its Clinger fast path did not take -> the same strtod path
+// the host parser's general branch uses, so GPU-parsed blocks equal host-parsed ones bit for bit.
+SHIFU_RT_API long shifu_parse_fields(const char* buf, const long* fb, long n, double* out) {
+  for (long k = 0; k < n; ++k) {
+    const long a = fb[4 * k + 2], b = fb[4 * k + 3];
+    bool ok = false;
+    out[k] = parse_double(std::string_view(buf + a, (size_t)(b - a)), ok);
+  }
+  return n;
+}

@@ -189,7 +189,18 @@ class ModelRunner:
                 cols |= set(m.obj.input_names)
         return cols
 
+    def _normalized_dev(self, table, cache):
+        """The normalized rows left in HBM when the K5 pass made them (NN scoring reads them in
+        place: no D2H + H2D round trip of [n, width] fp32), else the host rows."""
+        if "X" not in cache and "Xd" not in cache:
+            plan = self._norm_plan()
+            if plan is not None:
+                cache["Xd"] = plan.run(table, keep_device=True)["X"]
+        return cache["Xd"] if "Xd" in cache else self._normalized(table, cache)
+
     def _normalized(self, table, cache):
+        if "X" not in cache and "Xd" in cache:
+            cache["X"] = cache["Xd"].cpu().numpy()
         if "X" not in cache:
             plan = self._norm_plan()
             if plan is not None:
@@ -219,7 +230,7 @@ class ModelRunner:
         outs = []
         for m in self.models:
             if m.kind == "nn":
-                outs.append(nn_forward(m.obj, self._normalized(table, cache), self.dev))
+                outs.append(nn_forward(m.obj, self._normalized_dev(table, cache), self.dev))
             elif m.kind == "nn_binary":
                 outs.append(IndependentNNModel(m.obj, self.dev).compute(table))
             elif m.kind == "lr":

@@ -224,7 +224,13 @@ def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, no
     lines = open(os.path.join(pdir, "lines.bin"), "wb")
     off, n_local, cols = 0, 0, None
     try:
-        for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, require_target=False):
+        # the models' numeric inputs are parsed on the GPU (K0) and normalized where they land
+        gpu_cols = None
+        if getattr(runner, "dev", None) is not None and runner.dev.type == "cuda":
+            host_side = set(meta_cols) | set(score_meta) | {target}
+            gpu_cols = [n for n in runner.raw_columns() if n in nums and n not in host_side]
+        for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, require_target=False,
+                                     gpu_cols=gpu_cols, dev=_cuda_index(runner.dev) if gpu_cols else None):
             res = runner.score(md.table, scale)
             if cols is None:
                 cols = [k for k in res if k not in ("class_scores", "pred_class")]
@@ -596,6 +602,12 @@ def norm_eval(ms: ModelSet, ev, strict: bool = False):
     save_dataset(ms.pf.eval_normalized(ev), {"X": X, "y": md.y, "w": md.w.astype(np.float32)},
                  {"n": int(md.n), "input_names": names})
     return X
+
+
+def _cuda_index(dev):
+    import torch
+    d = torch.device(dev)
+    return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
 
 
 def run_eval(root: str = ".", action: str = "run", name: str | None = None, device=None, nosort: bool = False,

@@ -157,7 +157,9 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     if is_gpu_available():
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
-    nplan = N.NormPlan(mc, ms.ccs, cols, want_x=True, want_codes=is_tree, x_dtype=x_dtype, device=dev)
+    # two rotating pinned output buffers: chunk i is written while chunk i + 1 is normalized
+    nplan = N.NormPlan(mc, ms.ccs, cols, want_x=True, want_codes=is_tree, x_dtype=x_dtype, device=dev,
+                       pinned_out=2 if dev is not None else 0)
     outs = [out_x] + ([out_tree] if is_tree else [])
     if info.rank == 0:
         for o in outs:
@@ -196,8 +198,9 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     pending = None
     try:
         with ThreadPoolExecutor(1, thread_name_prefix="shifu-norm-write") as ex:
+            gpu_cols = [c.name for c in cols if not c.is_categorical()] if dev is not None else None
             for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, sample_rate, neg_only, seed,
-                                         row0=row0):
+                                         row0=row0, gpu_cols=gpu_cols, dev=dev):
                 res = nplan.run(md.table)
                 y, w = md.y.astype(np.float32), md.w.astype(np.float32)
                 if pending is not None:

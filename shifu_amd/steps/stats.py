@@ -109,6 +109,20 @@ def _stats_pass(ms, mc, cols, device) -> None:
         else:
             S.compute_column_stats(mc, ms.ccs, md, device=device, columns={c.name for c in cols})
 
+def _parse_device(device):
+    """The CUDA device (with its index) a streamed step computes on, or None on the CPU."""
+    import torch
+    from ..utils.device import is_gpu_available
+    if device is None:
+        if not is_gpu_available():
+            return None
+        device = "cuda"
+    d = torch.device(device)
+    if d.type != "cuda":
+        return None
+    return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
+
+
 def _stats_streamed(ms: ModelSet, cols, device=None) -> None:
     """Stats over row chunks of this rank's byte range (algos/stats_stream.py)."""
     import torch
@@ -126,13 +140,16 @@ def _stats_streamed(ms: ModelSet, cols, device=None) -> None:
     neg_only = bool(mc.stats.get("sampleNegOnly", False))
 
     row0 = DS.rank_row_offset(plan, info.rank, info.world_size) if rate < 1.0 else 0
-
-    def chunks(resume=None, with_keys=False):
-        return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only, row0=row0,
-                                  resume=resume, with_keys=with_keys)
     multi = info.world_size > 1
     if multi and device is None:
         device = dist.coll_device()
+    # the candidate numeric columns are parsed on the GPU and binned where they land (K0 -> K4)
+    pdev = _parse_device(device)
+    gpu_cols = [c.name for c in cols if not c.is_categorical() and not c.is_target() and not c.is_meta()]
+
+    def chunks(resume=None, with_keys=False):
+        return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only, row0=row0,
+                                  resume=resume, with_keys=with_keys, gpu_cols=gpu_cols, dev=pdev)
     n = compute_column_stats_streamed(
         mc, ms.ccs, chunks, device=device, columns={c.name for c in cols},
         reduce=(lambda t, op: dist.all_reduce_(t, op)) if multi else None,

@@ -292,19 +292,21 @@ def test_streamed_gbt_onehot_norm_equals_in_memory(tmp_path, monkeypatch, norm_t
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("norm_type", ["ONEHOT", "ZSCALE_ONEHOT"])
-def test_streamed_gbt_onehot_norm_gpu_equals_in_memory(tmp_path, norm_type):
+@pytest.mark.parametrize("norm_type,alg", [("ONEHOT", "GBT"), ("ZSCALE_ONEHOT", "GBT"), ("ONEHOT", "NN"),
+                                           ("ZSCALE_ONEHOT", "NN")])
+def test_streamed_gbt_onehot_norm_gpu_equals_in_memory(tmp_path, norm_type, alg):
     """the codes-only norm_codes_kernel launch (ip == nullptr) of a streamed GBT norm
-    with host one-hot columns runs on the GPU and equals the in-memory CleanedData."""
+    runs on the GPU and equals the in-memory CleanedData; the one-hot columns come from the K5
+    one-hot kernel (shifu_onehot) and equal the host expansion."""
     import torch
     assert torch.cuda.is_available()
-    _check_gbt_onehot(tmp_path, norm_type)
+    _check_gbt_onehot(tmp_path, norm_type, alg)
 
 
-def _check_gbt_onehot(tmp_path, norm_type):
+def _check_gbt_onehot(tmp_path, norm_type, alg="GBT"):
     from shifu_amd.steps.base import load_dataset_cache
     from shifu_amd.steps.norm import run_norm
-    a = _model_set(tmp_path, "GBT")
+    a = _model_set(tmp_path, alg)
     _set_norm_type(a, norm_type)
     b = str(tmp_path / "b")
     shutil.copytree(a, b)
@@ -315,7 +317,7 @@ def _check_gbt_onehot(tmp_path, norm_type):
         run_norm(b)
     finally:
         _set("auto")
-    for sub in ("CleanedData", "NormalizedData"):
+    for sub in (("CleanedData", "NormalizedData") if alg == "GBT" else ("NormalizedData",)):
         ma, xa = load_dataset_cache(os.path.join(a, "tmp", sub), mmap=False)
         mb, xb = load_dataset_cache(os.path.join(b, "tmp", sub))
         assert mb["n"] == ma["n"] and mb.get("streamed")

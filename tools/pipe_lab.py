@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--stream", action="store_true", help="force the streamed stats / norm paths")
     ap.add_argument("--prefetch", type=int, default=None, help="shifu.data.prefetch (parsed chunks queued ahead)")
+    ap.add_argument("--props", nargs="*", default=[], help="extra shifu properties k=v (e.g. shifu.data.gpuParse=false)")
     a = ap.parse_args()
     from shifu_amd.config import environment
     from shifu_amd.config.model_config import ModelConfig
@@ -35,6 +36,9 @@ def main():
     environment.props()["shifu.norm.dtype"] = "bf16"
     if a.prefetch is not None:
         environment.props()["shifu.data.prefetch"] = str(a.prefetch)
+    for kv in a.props:
+        k, v = kv.split("=", 1)
+        environment.props()[k] = v
     if a.stream:
         environment.props()["shifu.stats.streaming"] = "true"
         environment.props()["shifu.norm.streaming"] = "true"
