@@ -191,7 +191,15 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
                     bt.bounds[k] = b
 
     # ---- pass D: bin histograms + moments ------------------------------------------------------
+    bcache = {}
+    acc = [None] * len(batches)      # GPU: per batch [counts, weight sums, moments] arrays
     for y, w, vl in stream():
+        if dev.type == "cuda":       # every batch of the chunk: one weight scan, two D2H copies
+            from ..ops import stats_ops
+            multi = stats_ops.column_stats_multi(vl, y, w, [bt.bounds for bt in batches], binary, num_thr, bcache)
+            for i, (cnt, wsum, mom, boff) in enumerate(multi):
+                acc[i] = _acc_chunk(acc[i], cnt, wsum, mom, boff)
+            continue
         for bt, v in zip(batches, vl):
             res = S.batch_histograms(v, y, w, bt.bounds, binary, num_thr)
             if bt.hist is None:
@@ -203,6 +211,9 @@ def compute_column_stats_streamed(mc, ccs, chunks_fn, device=None, columns=None,
                     for i in range(4):
                         h[i] = h[i] + r[i]
                     _merge_moments(m, r[4])
+    for bt, a in zip(batches, acc):
+        if a is not None:
+            bt.hist, bt.mom = _acc_lists(a)
     for bt in batches:
         if bt.hist is None:     # no rows on this rank: zero partials shaped by the (global) cuts, so
             # every rank sends same-sized buffers to the merging collectives
@@ -231,6 +242,35 @@ def _run_cut_passes(engs, stream):
             for e, v in zip(engs, vl):
                 if state[id(e)] == "C":
                     e.pass_c(v, y, w)
+
+
+def _acc_chunk(a, cnt, wsum, mom, boff):
+    """Vectorized form of the per-column merge below for one chunk's batch arrays (the same
+    elementwise float adds in chunk order, so the totals are bit-identical)."""
+    if a is None:
+        return [cnt.copy(), wsum.copy(), mom.copy(), boff]
+    a[0] += cnt
+    a[1] += wsum
+    m = a[2]
+    take = mom[:, 0] != 0
+    new = take & (m[:, 0] == 0)
+    upd = take & ~new
+    m[new] = mom[new]
+    m[upd, :5] += mom[upd, :5]
+    m[upd, 5] = np.minimum(m[upd, 5], mom[upd, 5])
+    m[upd, 6] = np.maximum(m[upd, 6], mom[upd, 6])
+    return a
+
+
+def _acc_lists(a):
+    """Accumulated batch arrays -> the per-column hist / moment lists of the host path."""
+    cnt, wsum, mom, boff = a
+    hist, moms = [], []
+    for f in range(cnt.shape[0]):
+        k = int(boff[f + 1] - boff[f]) + 1
+        hist.append([cnt[f, :k, 0].copy(), cnt[f, :k, 1].copy(), wsum[f, :k, 0].copy(), wsum[f, :k, 1].copy()])
+        moms.append([int(mom[f, 0])] + [float(x) for x in mom[f, 1:]])
+    return hist, moms
 
 
 def _merge_moments(m, r):

@@ -1,0 +1,18 @@
+#!/bin/bash
+# r4h: text-path stage throughputs (parse_lab), stats GPU tests after the pass-D batching, the
+# 3M x 1600 pipeline again, then the reference's 20M x 1600 shape (one 2.5M-row part listed 8
+# times; the NormalizedData cache on /dev/shm: the box's disk is 79 GB).
+set -o pipefail
+out=gpurun_out/r4h
+mkdir -p $out
+(while sleep 50; do date +%T >> $out/heartbeat.txt; done) &
+hb=$!
+trap "kill $hb" EXIT
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_stats_stream.py tests/test_gpu_parse.py > $out/gpu_tests.txt 2>&1 || { tail -40 $out/gpu_tests.txt; exit 1; }
+tail -2 $out/gpu_tests.txt
+timeout -k 10 300 python tools/parse_lab.py --rows 1000000 --cols 1600 > $out/parse_lab_1M.txt 2>&1 || { tail -30 $out/parse_lab_1M.txt; exit 1; }
+tail -1 $out/parse_lab_1M.txt
+timeout -k 10 400 python bench.py --model pipeline --rows 3000000 --cols 1600 --pipeline-epochs 400 > $out/bench_pipeline_3M.json 2> $out/bench_pipeline_3M.err || { tail -30 $out/bench_pipeline_3M.err; exit 1; }
+python -c "import json; d=json.loads(open('$out/bench_pipeline_3M.json').read().strip().splitlines()[-1]); print(d['step_seconds'], d['value'])"
+timeout -k 10 900 python bench.py --model pipeline --rows 20000000 --cols 1600 --pipeline-epochs 400 --pipeline-replicate 8 --pipeline-tmp /dev/shm > $out/bench_pipeline_20M.json 2> $out/bench_pipeline_20M.err || { tail -30 $out/bench_pipeline_20M.err; exit 1; }
+python -c "import json; d=json.loads(open('$out/bench_pipeline_20M.json').read().strip().splitlines()[-1]); print(d['step_seconds'], d['value'], d.get('eval_auc'), d.get('se_recall_of_planted_columns'))"
