@@ -62,8 +62,9 @@ def _cache_budget(dev) -> int:
     if env is not None:
         return int(float(env) * (1 << 30))
     if dev.type == "cuda":
-        free, _ = torch.cuda.mem_get_info(dev)
-        return int(free * 0.5)
+        from ..utils.device import free_hbm
+        free = free_hbm(dev)
+        return int(free * 0.7)
     return 0
 
 

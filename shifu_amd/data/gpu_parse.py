@@ -134,6 +134,13 @@ class GpuBlockParser:
         slot = np.full(len(kinds), -1, np.int32)
         slot[self.gpu_cols] = np.arange(len(self.gpu_cols), dtype=np.int32)
         self.slot = torch.as_tensor(slot, device=self.dev)
+        # the host-parsed columns: the kernel hands back their field bounds, the host parses just
+        # those bytes (one short line per row) instead of scanning the whole block
+        self.host_cols = [c for c, k in enumerate(self.kinds_host) if k]
+        self.kinds_mini = [self.kinds_host[c] for c in self.host_cols] + [0]
+        mslot = np.full(len(kinds), -1, np.int32)
+        mslot[self.host_cols] = np.arange(len(self.host_cols), dtype=np.int32)
+        self.mslot = torch.as_tensor(mslot, device=self.dev) if self.host_cols else None
         self.fb = torch.empty(4 * FB_CAP, dtype=torch.long, device=self.dev)
         self.fb_n = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.stats = {"blocks": 0, "fallback_fields": 0, "host_blocks": 0}
@@ -153,16 +160,12 @@ class GpuBlockParser:
         from ..ops import _native as nat
         from .reader import parse_block
         L = len(data)
-        n, bad, out = parse_block(data, self.delim, self.kinds_host, self.missing, nthreads)
         self.stats["blocks"] += 1
-        if L == 0 or n == 0:
-            blk = DeviceBlock(torch.empty((len(self.gpu_cols), 0), dtype=torch.float64, device=self.dev))
-            out.update({c: ("num", DevRef(blk, j), []) for j, c in enumerate(self.gpu_cols)})
-            return n, bad, out
+        if L == 0:
+            return self._host_framing(data, nthreads, None)
         host = np.frombuffer(data, dtype=np.uint8)
-        src = torch.from_numpy(host)
         dbuf = torch.empty(L + 64, dtype=torch.uint8, device=self.dev)
-        dbuf[:L].copy_(src)
+        dbuf[:L].copy_(torch.from_numpy(host))
         d = dbuf[:L]
         ends = torch.nonzero(d == 10).flatten()
         if int(host[-1]) != 10:
@@ -173,27 +176,60 @@ class GpuBlockParser:
             starts[1:] = ends[:-1] + 1
         vals = torch.empty((len(self.gpu_cols), nl), dtype=torch.float64, device=self.dev)
         lflags = torch.empty(nl, dtype=torch.int32, device=self.dev)
+        nh = len(self.host_cols)
+        moffs = torch.empty((max(nh, 1), nl, 2), dtype=torch.int32, device=self.dev) if nh else None
         self.fb_n.zero_()
         nat.call_hip("shifu_csv_gpu_parse", dbuf, starts, ends, nl, self.slot, len(self.kinds), vals, nl, lflags,
-                     self.fb, FB_CAP, self.fb_n, self.dbyte, self.ntok, self.toks, nat.stream_of(dbuf))
+                     self.fb, FB_CAP, self.fb_n, self.dbyte, self.ntok, self.toks, self.mslot, moffs,
+                     nat.stream_of(dbuf))
         nfb = int(self.fb_n.item())
         if nfb > FB_CAP:                         # a mostly non-decimal block: host parse throughout
             self.stats["host_blocks"] += 1
             return parse_block(data, self.delim, self.kinds, self.missing, nthreads)
+        addr = ctypes.addressof(ctypes.c_char.from_buffer(data)) if not data.readonly else host.ctypes.data
         if nfb:
             self.stats["fallback_fields"] += nfb
             fb = self.fb[: 4 * nfb].view(nfb, 4).cpu().numpy()
             fv = np.empty(nfb, np.float64)
-            addr = ctypes.addressof(ctypes.c_char.from_buffer(data)) if not data.readonly else \
-                np.frombuffer(data, np.uint8).ctypes.data
             nat.rt().shifu_parse_fields(addr, fb.ctypes.data, nfb, fv.ctypes.data)
             fbt = torch.as_tensor(fb, device=self.dev)
             vals[fbt[:, 1], fbt[:, 0]] = torch.as_tensor(fv, device=self.dev)
-        blank = (lflags & 1).bool()
-        if bool(blank.any()):
-            vals = vals[:, torch.nonzero(~blank).flatten()]
+        fl = lflags.cpu().numpy()
+        blank = (fl & 1) != 0
+        if blank.any():
+            vals = vals[:, torch.as_tensor(np.flatnonzero(~blank), device=self.dev)]
+        if ((fl & 2) != 0)[~blank].any():
+            # rows with a field count != ncols: the host parser's short / long row rules throughout
+            n, bad, out = self._host_framing(data, nthreads, vals)
+        else:
+            n, bad, out = int((~blank).sum()), 0, {}
+            if nh:
+                mo = moffs.cpu().numpy()
+                cap = int(np.clip(mo[..., 1] - mo[..., 0], 0, None).sum()) + nl * (nh + 3)
+                mini = np.empty(cap, np.uint8)
+                nb = nat.rt().shifu_gather_fields(addr, mo.ctypes.data, nl, nh, fl.ctypes.data,
+                                                  self.delim.encode(), mini.ctypes.data, cap)
+                if nb < 0:
+                    raise RuntimeError("GPU parse: gathering the host columns failed")
+                n2, _, o2 = parse_block(memoryview(mini[:nb]), self.delim, self.kinds_mini, self.missing, nthreads)
+                if n2 != n:
+                    raise RuntimeError(f"GPU parse: {n} rows framed, {n2} host-column rows")
+                out = {c: o2[j] for j, c in enumerate(self.host_cols)}
+            self.stats["gathered_blocks"] = self.stats.get("gathered_blocks", 0) + 1
         if vals.shape[1] != n:
             raise RuntimeError(f"GPU parse framed {vals.shape[1]} rows, host parser {n}")
         blk = DeviceBlock(vals)
         out.update({c: ("num", DevRef(blk, j), []) for j, c in enumerate(self.gpu_cols)})
+        return n, bad, out
+
+    def _host_framing(self, data, nthreads, vals):
+        """The host parser over the whole block for the host columns (row framing, bad rows)."""
+        import torch
+        from .reader import parse_block
+        n, bad, out = parse_block(data, self.delim, self.kinds_host, self.missing, nthreads)
+        if vals is None:
+            blk = DeviceBlock(torch.empty((len(self.gpu_cols), n), dtype=torch.float64, device=self.dev))
+            if n:
+                raise RuntimeError("GPU parse: rows without a device block")
+            out.update({c: ("num", DevRef(blk, j), []) for j, c in enumerate(self.gpu_cols)})
         return n, bad, out

@@ -55,7 +55,7 @@ def byte_ranges(files, rank: int = 0, world: int = 1):
     return sorted(out)
 
 
-READ_THREADS = int(os.environ.get("SHIFU_READ_THREADS", "4"))   # parallel preads per block
+READ_THREADS = int(os.environ.get("SHIFU_READ_THREADS", "8"))   # parallel preads per block
 
 
 def _pread_into(fd: int, mv, off: int, want: int) -> int:

@@ -730,7 +730,8 @@ class TreeTrainer:
         if c is None:
             G, n = self.ngroups, d.n
             need = G * n * FG
-            free = torch.cuda.mem_get_info(self.dev)[0]
+            from ..utils.device import free_hbm
+            free = free_hbm(self.dev)
             if free < need * 1.1 + (6 << 30):
                 _log.info("GBDT root: no room for the [G][N][32] bins copy (%.1f GB); quad records", need / 1e9)
                 self._g32 = False
@@ -1229,7 +1230,8 @@ class TreeTrainer:
         n = max(1, self.data.n)
         b = min(int(os.environ.get("SHIFU_RF_BATCH", "8")), remaining, (2 ** 31 - 1) // n)
         if self.gpu:
-            free, _ = torch.cuda.mem_get_info(self.dev)
+            from ..utils.device import free_hbm
+            free = free_hbm(self.dev)
             b = min(b, int(free // 3 // (40 * n)))
         t = torch.tensor([max(1, b)], dtype=torch.int64, device=self.dev)
         dist.all_reduce_(t, "min")

@@ -554,7 +554,8 @@ class MLPTrainer:
         if self.gpu:
             nbytes = int(np.prod(np.shape(x))) * 2
             if stream is None:
-                free = torch.cuda.mem_get_info(self.device)[0]
+                from ..utils.device import free_hbm
+                free = free_hbm(self.device)
                 stream = nbytes > 0.8 * free
             if stream:
                 n = int(np.shape(x)[0])

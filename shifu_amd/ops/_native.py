@@ -58,7 +58,7 @@ HIP_SIGNATURES = {
     "shifu_cast_bf16": "plpliis",
     "shifu_split_bf16_rows": "plli" "pl" "ii" "s",
     # csv_kernels.hip
-    "shifu_csv_gpu_parse": "pppl" "pi" "pl" "p" "pip" "iiP" "s",
+    "shifu_csv_gpu_parse": "pppl" "pi" "pl" "p" "pip" "iiP" "pp" "s",
     "shifu_transpose_cast": "plpiiis",
     # svm_kernels.hip
     "shifu_svm_smo": "pl" "ppp" "pp" "ii" "dd" "pp" "s",
@@ -121,6 +121,7 @@ RT_SIGNATURES = {
     "shifu_gen_csv": ("Pliildii", "i"),
     "shifu_gen_strong_cols": ("iip", "i"),
     "shifu_parse_fields": ("ppLp", "l"),
+    "shifu_gather_fields": ("pplipPpl", "l"),
 }
 
 

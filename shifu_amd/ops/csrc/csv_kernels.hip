@@ -36,6 +36,8 @@ struct CsvArgs {
   const int* slot; int ncols;                 // header column -> output row (-1: not parsed here)
   double* out; long ldo;                      // out[slot * ldo + line]
   int* lflags;                                // per line: 1 blank, 2 field count != ncols
+  const int* mslot; int* moffs;               // header column -> host-column index (-1) ; its raw
+                                              // field bounds moffs[(k * nl + line) * 2 + {0, 1}]
   long* fb; int fb_cap; int* fb_n;            // fallback fields (line, slot, start, end)
   int d0;
   int ntok;
@@ -51,6 +53,14 @@ __device__ const double kCsvPow10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7,
 // field [a, b) of `line`, header column f -> out (or the fallback list)
 __device__ void csv_field(const CsvArgs& A, long line, int f, long a, long b) {
   if (f >= A.ncols) return;
+  if (A.mslot) {                              // a host-parsed column: hand its bounds back
+    const int k = A.mslot[f];
+    if (k >= 0) {
+      int* o = A.moffs + 2 * ((long)k * A.nl + line);
+      o[0] = (int)a;
+      o[1] = (int)b;
+    }
+  }
   const int s = A.slot[f];
   if (s < 0) return;
   const uint8_t* p = A.buf;
@@ -184,14 +194,18 @@ __global__ __launch_bounds__(256) void csv_parse_kernel(CsvArgs A) {
 // slot[ncols]: output row per header column (-1 skip); out: [nslots][ldo] fp64; lflags[nl];
 // fb: [fb_cap][4] int64 fallback fields, fb_n: int32 counter (zeroed by the caller);
 // toks: ntok '\0'-separated trimmed missing tokens (each < 16 bytes).
+// mslot (nullable): header column -> index of a host-parsed column whose raw field bounds are
+// written to moffs [n_host][nl][2] int32 (block offsets < 2^31), so the host never scans the text.
 SHIFU_API int shifu_csv_gpu_parse(const void* buf, const long* ls, const long* le, long nl, const int* slot,
                                   int ncols, double* out, long ldo, int* lflags, long* fb, int fb_cap, int* fb_n,
-                                  int delim, int ntok, const char* toks, hipStream_t stream) {
+                                  int delim, int ntok, const char* toks, const int* mslot, int* moffs,
+                                  hipStream_t stream) {
   if (nl <= 0) return 0;
-  if (ncols <= 0 || ldo < nl || ntok < 0 || ntok > CSV_MAXTOK || fb_cap < 0) return -1;
+  if (ncols <= 0 || ldo < nl || ntok < 0 || ntok > CSV_MAXTOK || fb_cap < 0 || (mslot && !moffs)) return -1;
   CsvArgs A{};
   A.buf = (const uint8_t*)buf; A.ls = ls; A.le = le; A.nl = nl; A.slot = slot; A.ncols = ncols;
   A.out = out; A.ldo = ldo; A.lflags = lflags; A.fb = fb; A.fb_cap = fb_cap; A.fb_n = fb_n;
+  A.mslot = mslot; A.moffs = moffs;
   A.d0 = delim & 0xff; A.ntok = ntok;
   const char* t = toks;
   for (int i = 0; i < ntok; ++i) {

@@ -572,3 +572,29 @@ SHIFU_RT_API long shifu_parse_fields(const char* buf, const long* fb, long n, do
   }
   return n;
 }
+
+// The host-parsed columns of a GPU-parsed block, from the field bounds the GPU field parser
+// handed back (offs [k][nl][2] int32): one short line "f_0<d>f_1<d>...f_{k-1}<d>x\n" per non-blank
+// line (lflags bit 0 clear; the trailing unparsed "x" field keeps a line of empty fields from
+// reading as blank) -- the host parser then reads only these bytes instead of scanning the whole
+// block.  Returns the bytes written, or -1 when `cap` is too small.
+SHIFU_RT_API long shifu_gather_fields(const char* buf, const int* offs, long nl, int k, const int* lflags,
+                                      const char* delim, char* out, long cap) {
+  long p = 0;
+  const char d = delim && *delim ? delim[0] : '|';
+  for (long l = 0; l < nl; ++l) {
+    if (lflags[l] & 1) continue;
+    for (int j = 0; j < k; ++j) {
+      const int* o = offs + 2 * ((long)j * nl + l);
+      const long n = (long)o[1] - (long)o[0];
+      if (n < 0 || p + n + 1 > cap) return -1;
+      memcpy(out + p, buf + o[0], (size_t)n);
+      p += n;
+      out[p++] = d;
+    }
+    if (p + 2 > cap) return -1;
+    out[p++] = 'x';
+    out[p++] = '\n';
+  }
+  return p;
+}

@@ -839,7 +839,8 @@ class TrainStep:
         if mode in ("false", "0", "off"):
             return False
         need = n_rows * (-(-n_feat // 32) * 32)
-        free, _ = torch.cuda.mem_get_info(self.dev)
+        from ..utils.device import free_hbm
+        free = free_hbm(self.dev)
         return need > 0.6 * free
 
     def _continuous_trees(self, tid, cfg):

@@ -29,3 +29,16 @@ def sync(device: torch.device | None = None) -> None:
 def compute_dtype(device: torch.device) -> torch.dtype:
     """bf16 on MI355X (MFMA), fp32 on the CPU test path."""
     return torch.bfloat16 if device.type == "cuda" else torch.float32
+
+
+def free_hbm(device) -> int:
+    """Bytes of HBM this process can still allocate on ``device``: the driver's free memory plus
+    the blocks the caching allocator holds but no tensor uses (a step that ran earlier in the same
+    process -- e.g. the stats device cache before varsel in one pipeline -- leaves them reserved;
+    the allocator releases them and retries when a new allocation does not fit).  Sizing decisions
+    (resident vs streamed rows, cache budgets) use this, not ``mem_get_info`` alone."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return 0
+    free, _ = torch.cuda.mem_get_info(dev)
+    return int(free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))

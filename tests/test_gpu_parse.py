@@ -35,14 +35,14 @@ def test_device_columns_cpu_semantics():
     assert device_rows([t["c0"], None], "cpu") is None
 
 
-def _adversarial_text(rng, ncols, nrows, crlf=False):
+def _adversarial_text(rng, ncols, nrows, crlf=False, ragged=True):
     toks = ["", "?", "-999", "0", "1.5", "-0.000", "+12.25", "007.50", "12.", "-.5", ".", "-", "1e5", "1.0d",
             "123456789012345", "1234567890123456", "12345678901234567890", "0.1234567890123456789", "3.14159",
             " 4.5", "4.5 ", "\t-2.25", "99999999999999.9", "-0.00001", "1.", "00000000000000001", "NaN", "abc",
             "9007199254740993", "1.7976931348623157e308", "1" * 30, "0." + "0" * 25 + "1"]
     lines = []
     for _ in range(nrows):
-        k = ncols + rng.choice([0] * 12 + [-1, -5, 2])
+        k = ncols + (rng.choice([0] * 12 + [-1, -5, 2]) if ragged else 0)
         f = [rng.choice(toks) if rng.random() < 0.4 else f"{rng.gauss(0, 1000):.{rng.randint(0, 9)}f}"
              for _ in range(max(1, k))]
         lines.append("|".join(f))
@@ -75,6 +75,36 @@ def test_gpu_parse_bit_identical(crlf, miss):
             assert got.tobytes() == ref[c][1].tobytes(), f"column {c}"
         elif kinds[c] == 2:
             assert list(out[c][1]) == list(ref[c][1]) and out[c][2] == ref[c][2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("crlf", [False, True])
+def test_gpu_parse_host_columns_from_field_bounds(crlf):
+    """No ragged rows: the host columns (strings with empty / missing / padded values, a numeric
+    one) are parsed from the field bounds the kernel returns (shifu_gather_fields), blank lines
+    dropped -- same values, codes, dictionaries and row count as the full host parse."""
+    from shifu_amd.data.gpu_parse import GpuBlockParser
+    rng = random.Random(5 + crlf)
+    C = 29
+    data = _adversarial_text(rng, C, 5000, crlf, ragged=False)
+    kinds = [1] * C
+    for c in (0, 7, C - 1):
+        kinds[c] = 2
+    gcols = [c for c in range(C) if kinds[c] == 1 and c != 3]        # column 3: numeric on the host
+    pinned = torch.empty(len(data), dtype=torch.uint8, pin_memory=True).numpy()
+    pinned[:] = np.frombuffer(data, np.uint8)
+    miss = ["", "?", "NA"]
+    gp = GpuBlockParser(kinds, gcols, "|", miss, torch.device("cuda", 0))
+    n, bad, out = gp.parse(memoryview(pinned), 4)
+    n2, bad2, ref = R._parse_native(bytearray(data), "|", kinds, miss, 4)
+    assert (n, bad) == (n2, bad2) == (n, 0) and n == 5000
+    assert gp.stats.get("gathered_blocks") == 1
+    for c in range(C):
+        if kinds[c] == 1:
+            got = out[c][1].host() if c in gcols else out[c][1]
+            assert got.tobytes() == ref[c][1].tobytes(), f"column {c}"
+        else:
+            assert list(out[c][1]) == list(ref[c][1]) and out[c][2] == ref[c][2], f"column {c}"
 
 
 @pytest.mark.gpu

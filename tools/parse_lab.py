@@ -103,7 +103,7 @@ def main():
         gp.fb_n.zero_()
         e0.record()
         nat.call_hip("shifu_csv_gpu_parse", d, starts, ends, nl, gp.slot, ncols, vals, nl, lf, gp.fb, 1 << 20, gp.fb_n,
-                     ord("|"), gp.ntok, gp.toks, nat.stream_of(d))
+                     ord("|"), gp.ntok, gp.toks, None, None, nat.stream_of(d))
         e1.record()
         torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)

@@ -1,9 +1,9 @@
 #!/bin/bash
-# r4h: text-path stage throughputs (parse_lab), stats GPU tests after the pass-D batching, the
+# r4i: text-path stage throughputs (parse_lab), stats GPU tests after the pass-D batching, the
 # 3M x 1600 pipeline again, then the reference's 20M x 1600 shape (one 2.5M-row part listed 8
 # times; the NormalizedData cache on /dev/shm: the box's disk is 79 GB).
 set -o pipefail
-out=gpurun_out/r4h
+out=gpurun_out/r4i
 mkdir -p $out
 (while sleep 50; do date +%T >> $out/heartbeat.txt; done) &
 hb=$!
