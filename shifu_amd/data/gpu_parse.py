@@ -21,6 +21,7 @@ HBM as :class:`DeviceBlock` rows: ``stats`` batches and the ``norm`` K5 pass rea
 from __future__ import annotations
 
 import ctypes
+import time
 
 import numpy as np
 
@@ -143,7 +144,9 @@ class GpuBlockParser:
         self.mslot = torch.as_tensor(mslot, device=self.dev) if self.host_cols else None
         self.fb = torch.empty(4 * FB_CAP, dtype=torch.long, device=self.dev)
         self.fb_n = torch.zeros(1, dtype=torch.int32, device=self.dev)
-        self.stats = {"blocks": 0, "fallback_fields": 0, "host_blocks": 0}
+        self.stream = None
+        self.stats = {"blocks": 0, "fallback_fields": 0, "host_blocks": 0, "bytes": 0}
+        self.times = {"h2d": 0.0, "index": 0.0, "kernel": 0.0, "fallback": 0.0, "host_cols": 0.0}
 
     def parse(self, data, nthreads: int):
         """``data``: a memoryview of complete lines inside a page-locked uint8 ndarray (or any
@@ -152,8 +155,21 @@ class GpuBlockParser:
         import torch
         from ..ops import _native as nat
         from .reader import parse_block
-        with torch.cuda.device(self.dev):          # a reader thread: HIP's current device = ours
-            return self._parse(data, nthreads)
+        # a reader thread: HIP's current device = ours, and a stream of its own, so the block's
+        # host syncs wait for the parse only -- not for the consumer's kernels on the compute
+        # stream (they overlap); the block is complete when handed over (stream synchronized)
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(self.dev)
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
+            n, bad, out = self._parse(data, nthreads)
+            self.stream.synchronize()
+        consumer = torch.cuda.default_stream(self.dev)
+        for c in self.gpu_cols:
+            ref = out[c][1]
+            if isinstance(ref, DevRef):
+                ref.block.D.record_stream(consumer)     # freed by the consumer: reuse waits for it
+                break
+        return n, bad, out
 
     def _parse(self, data, nthreads: int):
         import torch
@@ -163,9 +179,14 @@ class GpuBlockParser:
         self.stats["blocks"] += 1
         if L == 0:
             return self._host_framing(data, nthreads, None)
+        T = self.times
+        t0 = time.perf_counter()
+        self.stats["bytes"] += L
         host = np.frombuffer(data, dtype=np.uint8)
         dbuf = torch.empty(L + 64, dtype=torch.uint8, device=self.dev)
         dbuf[:L].copy_(torch.from_numpy(host))
+        t1 = time.perf_counter()
+        T["h2d"] += t1 - t0
         d = dbuf[:L]
         ends = torch.nonzero(d == 10).flatten()
         if int(host[-1]) != 10:
@@ -179,10 +200,14 @@ class GpuBlockParser:
         nh = len(self.host_cols)
         moffs = torch.empty((max(nh, 1), nl, 2), dtype=torch.int32, device=self.dev) if nh else None
         self.fb_n.zero_()
+        t2 = time.perf_counter()
+        T["index"] += t2 - t1
         nat.call_hip("shifu_csv_gpu_parse", dbuf, starts, ends, nl, self.slot, len(self.kinds), vals, nl, lflags,
                      self.fb, FB_CAP, self.fb_n, self.dbyte, self.ntok, self.toks, self.mslot, moffs,
                      nat.stream_of(dbuf))
         nfb = int(self.fb_n.item())
+        t3 = time.perf_counter()
+        T["kernel"] += t3 - t2
         if nfb > FB_CAP:                         # a mostly non-decimal block: host parse throughout
             self.stats["host_blocks"] += 1
             return parse_block(data, self.delim, self.kinds, self.missing, nthreads)
@@ -195,6 +220,8 @@ class GpuBlockParser:
             fbt = torch.as_tensor(fb, device=self.dev)
             vals[fbt[:, 1], fbt[:, 0]] = torch.as_tensor(fv, device=self.dev)
         fl = lflags.cpu().numpy()
+        t4 = time.perf_counter()
+        T["fallback"] += t4 - t3
         blank = (fl & 1) != 0
         if blank.any():
             vals = vals[:, torch.as_tensor(np.flatnonzero(~blank), device=self.dev)]
@@ -218,9 +245,16 @@ class GpuBlockParser:
             self.stats["gathered_blocks"] = self.stats.get("gathered_blocks", 0) + 1
         if vals.shape[1] != n:
             raise RuntimeError(f"GPU parse framed {vals.shape[1]} rows, host parser {n}")
+        T["host_cols"] += time.perf_counter() - t4
         blk = DeviceBlock(vals)
         out.update({c: ("num", DevRef(blk, j), []) for j, c in enumerate(self.gpu_cols)})
         return n, bad, out
+
+    def summary(self) -> str:
+        s = self.stats
+        tt = " ".join(f"{k} {v:.2f}s" for k, v in self.times.items())
+        return (f"GPU parse: {s['blocks']} blocks, {s['bytes'] / 1e9:.1f} GB, {s['fallback_fields']} fallback fields, "
+                f"{s['host_blocks']} host blocks; {tt}")
 
     def _host_framing(self, data, nthreads, vals):
         """The host parser over the whole block for the host columns (row framing, bad rows)."""

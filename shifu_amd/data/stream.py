@@ -355,6 +355,9 @@ def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTE
             r += n
             if md.n:
                 yield (k, md) if with_keys else md
+        if gp is not None:
+            from ..utils.log import get_logger
+            get_logger("data.stream").info("%s", gp.summary())
     yield from prefetched(produce, int(environment.get("shifu.data.prefetch", 1)))
 
 

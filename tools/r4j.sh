@@ -1,0 +1,18 @@
+#!/bin/bash
+# r4j: GPU parse on its own stream (overlaps the consumer's kernels), parallel cache writes;
+# stats/norm profile at 3M x 1600 (GPU parse stage times in the log), 3M and 20M pipelines.
+set -o pipefail
+out=gpurun_out/r4j
+mkdir -p $out
+(while sleep 50; do date +%T >> $out/heartbeat.txt; done) &
+hb=$!
+trap "kill $hb" EXIT
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_stats_stream.py tests/test_gpu_parse.py tests/test_norm_stream.py > $out/gpu_tests.txt 2>&1 || { tail -40 $out/gpu_tests.txt; exit 1; }
+tail -2 $out/gpu_tests.txt
+timeout -k 10 400 python tools/pipe_lab.py --rows 3000000 --cols 1600 --steps stats norm --top 30 > $out/pipe_lab_3M.txt 2>&1 || { tail -30 $out/pipe_lab_3M.txt; exit 1; }
+grep "^====\|GPU parse:" $out/pipe_lab_3M.txt | cut -c1-250
+timeout -k 10 400 python bench.py --model pipeline --rows 3000000 --cols 1600 --pipeline-epochs 400 > $out/bench_pipeline_3M.json 2> $out/bench_pipeline_3M.err || { tail -30 $out/bench_pipeline_3M.err; exit 1; }
+python -c "import json; d=json.loads(open('$out/bench_pipeline_3M.json').read().strip().splitlines()[-1]); print(d['step_seconds'], d['value'])"
+timeout -k 10 900 python bench.py --model pipeline --rows 20000000 --cols 1600 --pipeline-epochs 400 --pipeline-replicate 8 --pipeline-tmp /dev/shm > $out/bench_pipeline_20M.json 2> $out/bench_pipeline_20M.err || { tail -30 $out/bench_pipeline_20M.err; exit 1; }
+python -c "import json; d=json.loads(open('$out/bench_pipeline_20M.json').read().strip().splitlines()[-1]); print(d['step_seconds'], d['value'], d.get('eval_auc'), d.get('se_recall_of_planted_columns'))"
+grep "GPU parse:" $out/bench_pipeline_20M.err | cut -c1-250
