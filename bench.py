@@ -694,7 +694,8 @@ def bench_pipeline(a, dev, info):
     from shifu_amd.steps import api
     from shifu_amd.steps.create import create_model_set
     rows, F = a.rows, a.cols
-    rows_eval = max(1000, rows // 4)          # disk: the eval set is a quarter of the training set
+    # disk: the eval set is a quarter of the training set unless --pipeline-eval-rows says otherwise
+    rows_eval = a.pipeline_eval_rows or max(1000, rows // 4)
     epochs = max(2, a.pipeline_epochs)
     from shifu_amd.config import environment
     environment.props()["shifu.norm.dtype"] = "bf16"     # GEMM-ready NormalizedData (half the bytes)
@@ -824,7 +825,8 @@ def bench_pipeline(a, dev, info):
                                                                       for k, v in SE_PHASES.items()},
         "step_minutes": {k: round(v / 60.0, 2) for k, v in times.items()},
         "reference_minutes_20M_x_1600 (CHANGES.txt:233-237,264-268)": REF_PIPELINE_MIN,
-        "measured_at_reference_shape": bool(rows * info.world_size >= REF_PIPELINE_ROWS and F >= 1600 and epochs >= 400),
+        "measured_at_reference_shape": bool(rows * info.world_size >= REF_PIPELINE_ROWS and F >= 1600 and epochs >= 400
+                                            and rows_eval * info.world_size >= REF_PIPELINE_ROWS),
         "se_recall_of_planted_columns": recall,
         "eval_auc": perf["areaUnderRoc"] if info.rank == 0 else None,
     }
@@ -908,6 +910,8 @@ def main():
     ap.add_argument("--pipeline-replicate", type=int, default=1,
                     help="pipeline: generate rows/R rows and list the part R times (disk-limited boxes)")
     ap.add_argument("--pipeline-tmp", default=None, help="pipeline: put the model set's tmp/ (NormalizedData) here")
+    ap.add_argument("--pipeline-eval-rows", type=int, default=None,
+                    help="pipeline: eval set rows (default a quarter of --rows; the reference's eval is 20M rows)")
     ap.add_argument("--pipeline-epochs", type=int, default=40,
                     help="pipeline: numTrainEpochs of the NN (varsel SE trains half of them)")
     a = ap.parse_args()

@@ -13,6 +13,6 @@ timeout -k 10 400 python tools/pipe_lab.py --rows 3000000 --cols 1600 --steps st
 grep "^====\|GPU parse:" $out/pipe_lab_3M.txt | cut -c1-250
 timeout -k 10 400 python bench.py --model pipeline --rows 3000000 --cols 1600 --pipeline-epochs 400 > $out/bench_pipeline_3M.json 2> $out/bench_pipeline_3M.err || { tail -30 $out/bench_pipeline_3M.err; exit 1; }
 python -c "import json; d=json.loads(open('$out/bench_pipeline_3M.json').read().strip().splitlines()[-1]); print(d['step_seconds'], d['value'])"
-timeout -k 10 900 python bench.py --model pipeline --rows 20000000 --cols 1600 --pipeline-epochs 400 --pipeline-replicate 8 --pipeline-tmp /dev/shm > $out/bench_pipeline_20M.json 2> $out/bench_pipeline_20M.err || { tail -30 $out/bench_pipeline_20M.err; exit 1; }
+timeout -k 10 900 python bench.py --model pipeline --rows 20000000 --cols 1600 --pipeline-epochs 400 --pipeline-replicate 8 --pipeline-tmp /dev/shm --pipeline-eval-rows 20000000 > $out/bench_pipeline_20M.json 2> $out/bench_pipeline_20M.err || { tail -30 $out/bench_pipeline_20M.err; exit 1; }
 python -c "import json; d=json.loads(open('$out/bench_pipeline_20M.json').read().strip().splitlines()[-1]); print(d['step_seconds'], d['value'], d.get('eval_auc'), d.get('se_recall_of_planted_columns'))"
 grep "GPU parse:" $out/bench_pipeline_20M.err | cut -c1-250
