@@ -179,6 +179,9 @@ class GpuBlockParser:
         self.stats["blocks"] += 1
         if L == 0:
             return self._host_framing(data, nthreads, None)
+        if L >= (1 << 31) - 64:                  # field bounds are int32 block offsets
+            self.stats["host_blocks"] += 1
+            return parse_block(data, self.delim, self.kinds, self.missing, nthreads)
         T = self.times
         t0 = time.perf_counter()
         self.stats["bytes"] += L

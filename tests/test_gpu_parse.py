@@ -168,3 +168,38 @@ def test_streamed_stats_and_norm_same_with_gpu_parse(tmp_path, alg):
         assert ma["n"] == mb["n"] > 0
         for k in xa:
             assert np.asarray(xa[k]).tobytes() == np.asarray(xb[k]).tobytes(), (sub, k)
+
+
+def test_gather_fields_cpu():
+    """shifu_gather_fields (the host half of the GPU parse: the host columns rebuilt from field
+    bounds) on bounds computed here: blank lines skipped, empty / padded fields kept, every line
+    ends with the unparsed "x" field so a line of empty fields never reads as blank."""
+    from shifu_amd.ops import _native as nat
+    lib = nat.rt()
+    if lib is None:
+        pytest.skip("native runtime not built")
+    lines = ["a|1.5|x1", "|2|", "   ", " b |  |q", "c|-3|z"]
+    text = ("\n".join(lines) + "\n").encode()
+    buf = np.frombuffer(bytearray(text), np.uint8)
+    want_cols = [0, 2]                       # host columns
+    offs = np.zeros((len(want_cols), len(lines), 2), np.int32)
+    flags = np.zeros(len(lines), np.int32)
+    pos = 0
+    for li, ln in enumerate(lines):
+        if not ln.strip():
+            flags[li] = 1
+        starts, p = [], pos
+        for f in ln.split("|"):
+            starts.append((p, p + len(f)))
+            p += len(f) + 1
+        for j, c in enumerate(want_cols):
+            offs[j, li] = starts[c] if c < len(starts) else (pos, pos)
+        pos += len(ln) + 1
+    cap = 256
+    out = np.zeros(cap, np.uint8)
+    nb = lib.shifu_gather_fields(buf.ctypes.data, offs.ctypes.data, len(lines), len(want_cols), flags.ctypes.data,
+                                 b"|", out.ctypes.data, cap)
+    got = bytes(out[:nb]).decode()
+    assert got == "a|x1|x\n||x\n b |q|x\nc|z|x\n"
+    assert lib.shifu_gather_fields(buf.ctypes.data, offs.ctypes.data, len(lines), len(want_cols), flags.ctypes.data,
+                                   b"|", out.ctypes.data, 8) == -1        # cap too small
