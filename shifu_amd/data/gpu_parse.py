@@ -145,10 +145,30 @@ class GpuBlockParser:
         self.fb = torch.empty(4 * FB_CAP, dtype=torch.long, device=self.dev)
         self.fb_n = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.stream = None
+        self.h2d_stream = None
         self.stats = {"blocks": 0, "fallback_fields": 0, "host_blocks": 0, "bytes": 0}
         self.times = {"h2d": 0.0, "index": 0.0, "kernel": 0.0, "fallback": 0.0, "host_cols": 0.0}
 
-    def parse(self, data, nthreads: int):
+    def uploads(self, blocks):
+        """(offset, block) -> (offset, block, device copy of the block): the H2D stage of the
+        streamed read (its own thread and stream; a copy is complete when yielded)."""
+        import torch
+        if self.h2d_stream is None:
+            self.h2d_stream = torch.cuda.Stream(self.dev)
+        for off, data in blocks:
+            L = len(data)
+            if L == 0 or L >= (1 << 31) - 64:
+                yield off, data, None
+                continue
+            t0 = time.perf_counter()
+            with torch.cuda.device(self.dev), torch.cuda.stream(self.h2d_stream):
+                dbuf = torch.empty(L + 64, dtype=torch.uint8, device=self.dev)
+                dbuf[:L].copy_(torch.from_numpy(np.frombuffer(data, dtype=np.uint8)), non_blocking=True)
+                self.h2d_stream.synchronize()
+            self.times["h2d"] += time.perf_counter() - t0
+            yield off, data, dbuf
+
+    def parse(self, data, nthreads: int, dbuf=None):
         """``data``: a memoryview of complete lines inside a page-locked uint8 ndarray (or any
         buffer: then it is staged) -> the host parser's (n, bad, {column: (kind, values, dict)})
         with the GPU columns as ``("num", DevRef, [])``."""
@@ -161,7 +181,9 @@ class GpuBlockParser:
         if self.stream is None:
             self.stream = torch.cuda.Stream(self.dev)
         with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
-            n, bad, out = self._parse(data, nthreads)
+            if dbuf is not None:
+                dbuf.record_stream(self.stream)     # the upload stage's block: reuse waits for us
+            n, bad, out = self._parse(data, nthreads, dbuf)
             self.stream.synchronize()
         consumer = torch.cuda.default_stream(self.dev)
         for c in self.gpu_cols:
@@ -171,7 +193,7 @@ class GpuBlockParser:
                 break
         return n, bad, out
 
-    def _parse(self, data, nthreads: int):
+    def _parse(self, data, nthreads: int, dbuf=None):
         import torch
         from ..ops import _native as nat
         from .reader import parse_block
@@ -186,8 +208,9 @@ class GpuBlockParser:
         t0 = time.perf_counter()
         self.stats["bytes"] += L
         host = np.frombuffer(data, dtype=np.uint8)
-        dbuf = torch.empty(L + 64, dtype=torch.uint8, device=self.dev)
-        dbuf[:L].copy_(torch.from_numpy(host))
+        if dbuf is None:
+            dbuf = torch.empty(L + 64, dtype=torch.uint8, device=self.dev)
+            dbuf[:L].copy_(torch.from_numpy(host))
         t1 = time.perf_counter()
         T["h2d"] += t1 - t0
         d = dbuf[:L]
@@ -241,7 +264,8 @@ class GpuBlockParser:
                                                   self.delim.encode(), mini.ctypes.data, cap)
                 if nb < 0:
                     raise RuntimeError("GPU parse: gathering the host columns failed")
-                n2, _, o2 = parse_block(memoryview(mini[:nb]), self.delim, self.kinds_mini, self.missing, nthreads)
+                n2, _, o2 = parse_block(memoryview(mini[:nb]), self.delim, self.kinds_mini, self.missing,
+                                        max(1, min(nthreads, nb >> 20)))
                 if n2 != n:
                     raise RuntimeError(f"GPU parse: {n} rows framed, {n2} host-column rows")
                 out = {c: o2[j] for j, c in enumerate(self.host_cols)}

@@ -204,19 +204,26 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
         # the file reads run on their own thread, PREFETCH_READ blocks ahead of the parse (readinto
         # and the native parser both release the GIL).  PREFETCH_READ + 2 buffers: the block being
         # parsed (its parse copies everything out before the next block is requested), the queued
-        # ones and the one being filled
-        blocks = (prefetched(lambda: _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + 2, pinned=pinned),
-                             PREFETCH_READ)
-                  if PREFETCH_READ > 0 else _lines_in_range(path, a, b, chunk_bytes, pinned=pinned))
-        for off, data in blocks:
-            if plan.skip_header_line and fi == 0 and off == 0:
-                nl = bytes(data[: 1 << 20]).find(b"\n")
-                if nl < 0 and len(data) > (1 << 20):      # a header line wider than 1 MiB
-                    nl = bytes(data).find(b"\n")
-                data = data[nl + 1:] if nl >= 0 else b""
-                if not len(data):
-                    continue
-            yield (fi, off), parse(data)
+        # ones and the one being filled.  GPU parse: a third stage between them copies each block
+        # to HBM on its own thread / stream (read | H2D | parse overlap), two more buffers in flight
+        def lines():
+            for off, data in _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + (4 if pinned else 2),
+                                             pinned=pinned):
+                if plan.skip_header_line and fi == 0 and off == 0:
+                    nl = bytes(data[: 1 << 20]).find(b"\n")
+                    if nl < 0 and len(data) > (1 << 20):      # a header line wider than 1 MiB
+                        nl = bytes(data).find(b"\n")
+                    data = data[nl + 1:] if nl >= 0 else b""
+                    if not len(data):
+                        continue
+                yield off, data
+        blocks = prefetched(lines, PREFETCH_READ) if PREFETCH_READ > 0 else lines()
+        if pinned:
+            for off, data, dbuf in prefetched(lambda: gpu.uploads(blocks), 1):
+                yield (fi, off), gpu.parse(data, nthreads, dbuf)
+        else:
+            for off, data in blocks:
+                yield (fi, off), parse(data)
 
 
 def gpu_parser(plan: DatasetPlan, gpu_cols, dev):

@@ -11,6 +11,8 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method threa
 tail -2 $out/gpu_tests.txt
 timeout -k 10 400 python tools/pipe_lab.py --rows 3000000 --cols 1600 --steps stats norm --top 30 > $out/pipe_lab_3M.txt 2>&1 || { tail -30 $out/pipe_lab_3M.txt; exit 1; }
 grep "^====\|GPU parse:" $out/pipe_lab_3M.txt | cut -c1-250
+timeout -k 10 400 python tools/pipe_lab.py --rows 3000000 --cols 1600 --steps stats norm --top 30 --props shifu.stats.chunkMB=1024 shifu.norm.chunkMB=1024 > $out/pipe_lab_3M_chunk1G.txt 2>&1 || { tail -30 $out/pipe_lab_3M_chunk1G.txt; exit 1; }
+grep "^====\|GPU parse:" $out/pipe_lab_3M_chunk1G.txt | cut -c1-250
 timeout -k 10 400 python bench.py --model pipeline --rows 3000000 --cols 1600 --pipeline-epochs 400 > $out/bench_pipeline_3M.json 2> $out/bench_pipeline_3M.err || { tail -30 $out/bench_pipeline_3M.err; exit 1; }
 python -c "import json; d=json.loads(open('$out/bench_pipeline_3M.json').read().strip().splitlines()[-1]); print(d['step_seconds'], d['value'])"
 timeout -k 10 900 python bench.py --model pipeline --rows 20000000 --cols 1600 --pipeline-epochs 400 --pipeline-replicate 8 --pipeline-tmp /dev/shm --pipeline-eval-rows 20000000 > $out/bench_pipeline_20M.json 2> $out/bench_pipeline_20M.err || { tail -30 $out/bench_pipeline_20M.err; exit 1; }
