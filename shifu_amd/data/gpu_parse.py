@@ -197,6 +197,7 @@ class GpuBlockParser:
         import torch
         from ..ops import _native as nat
         from .reader import parse_block
+        data = memoryview(data)
         L = len(data)
         self.stats["blocks"] += 1
         if L == 0:
