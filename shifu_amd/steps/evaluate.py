@@ -201,7 +201,8 @@ def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, no
     if target and target not in strs and target not in nums:
         strs.append(target)
     plan = plan_dataset(mc, ev.dataSet, nums, strs)
-    chunk = int(float(environment.get("shifu.eval.chunkMB", 256)) * (1 << 20))
+    gpu_run = getattr(runner, "dev", None) is not None and runner.dev.type == "cuda"
+    chunk = int(float(environment.get("shifu.eval.chunkMB", 1024 if gpu_run else 256)) * (1 << 20))
     sel = ev.get("performanceScoreSelector", "mean") or "mean"
     pos = set(str(t) for t in (ev.dataSet.get("posTags") or mc.pos_tags))
     neg = set(str(t) for t in (ev.dataSet.get("negTags") or mc.neg_tags))

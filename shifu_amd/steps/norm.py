@@ -149,7 +149,6 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     info = dist.info()
     plan = plan_dataset(mc, data_conf, [c.name for c in cols if not c.is_categorical()],
                         [c.name for c in cols if c.is_categorical()])
-    chunk = int(float(environment.get("shifu.norm.chunkMB", 256)) * (1 << 20))
     x_dtype = str(environment.get("shifu.norm.dtype", "float32")).lower()
     x_dtype = "bf16" if x_dtype in ("bf16", "bfloat16") else "float32"
     row0 = DS.rank_row_offset(plan, info.rank, info.world_size) if sample_rate < 1.0 else 0
@@ -160,6 +159,7 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     # two rotating pinned output buffers: chunk i is written while chunk i + 1 is normalized
     nplan = N.NormPlan(mc, ms.ccs, cols, want_x=True, want_codes=is_tree, x_dtype=x_dtype, device=dev,
                        pinned_out=2 if dev is not None else 0)
+    chunk = int(float(environment.get("shifu.norm.chunkMB", 1024 if dev is not None else 256)) * (1 << 20))
     outs = [out_x] + ([out_tree] if is_tree else [])
     if info.rank == 0:
         for o in outs:
