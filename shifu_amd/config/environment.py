@@ -28,7 +28,6 @@ DEFAULTS = {
     "shifu.stats.corr.reuse": "false",
     "shifu.stats.streaming": "auto",
     "shifu.stats.streamThresholdGB": "8",
-    "shifu.stats.chunkMB": "256",
     "shifu.stats.binning.parity": "false",
     "shifu.varsel.se.reuse": "false",
     "shifu.tree.regeninput": "false",

@@ -180,7 +180,7 @@ class Bf16Rows:
     ``cols``: the raw columns this view exposes (a model's input subset, :meth:`subset`);
     :meth:`device_rows` moves the bf16 bits to the GPU as they are (no host fp32 expansion)."""
 
-    COPY_THREADS = int(os.environ.get("SHIFU_COPY_THREADS", "8"))
+    COPY_THREADS = int(os.environ.get("SHIFU_COPY_THREADS", "0"))
 
     def __init__(self, raw, width: int, cols=None):
         self.raw = raw
@@ -210,17 +210,18 @@ class Bf16Rows:
     def device_rows(self, device, rows=None, block: int = 1 << 18):
         """bf16 torch tensor [len(rows), width] on ``device``: the raw bits are uploaded in row
         blocks (``rows``: optional SORTED row index array, gathered on the device) and the
-        columns picked on the device.  GPU: each block is copied by ``COPY_THREADS`` threads into
-        one of two page-locked buffers and sent with an async H2D on a copy stream, so the host
-        copy of block i + 1 overlaps the DMA and the device-side pick of block i (a pageable
-        upload of a 20M x 1664 bf16 cache ran at a third of this rate)."""
+        columns picked on the device.  ``COPY_THREADS`` > 0 (``SHIFU_COPY_THREADS``): each block
+        is copied by that many threads into one of two page-locked buffers and sent with an async
+        H2D on a copy stream.  Default 0 = the plain pageable upload: on a 66 GB /dev/shm cache
+        (20M x 1664) it loaded in 8.8 s against 14.5 s for the staged form, although a 13 GB lab
+        file showed them level (profiles/r4/upload_lab_r4m.txt)."""
         import torch
         n = len(self.raw)
         dev = torch.device(device)
         out = torch.empty((n if rows is None else len(rows), self.width), dtype=torch.bfloat16, device=dev)
         cols_d = None if self.cols is None else torch.as_tensor(self.cols, device=dev)
         ridx = None if rows is None else np.asarray(rows, dtype=np.int64)
-        gpu = dev.type == "cuda"
+        gpu = dev.type == "cuda" and self.COPY_THREADS > 0
         if gpu:
             kp = self.raw.shape[1]
             pins = [torch.empty(block * kp, dtype=torch.int16, pin_memory=True) for _ in range(2)]

@@ -323,3 +323,24 @@ def _check_gbt_onehot(tmp_path, norm_type, alg="GBT"):
         assert mb["n"] == ma["n"] and mb.get("streamed")
         for k in xa:
             np.testing.assert_array_equal(np.asarray(xb[k]), xa[k], err_msg=f"{norm_type} {sub} {k}")
+
+
+@pytest.mark.gpu
+def test_bf16rows_device_rows_staged_equals_pageable(monkeypatch):
+    """Bf16Rows.device_rows: the page-locked multi-thread staging (COPY_THREADS > 0) uploads the
+    same rows / columns as the default pageable path (row gathers and column subsets included)."""
+    import numpy as np
+    import torch
+    from shifu_amd.data.rowstore import Bf16Rows
+    rng = np.random.default_rng(9)
+    n, width, kpad = 5000, 37, 128
+    raw = rng.integers(0, 1 << 15, size=(n, kpad)).astype(np.uint16)
+    rows = np.sort(rng.choice(n, 1700, replace=False))
+    dev = torch.device("cuda", 0)
+    for view in (Bf16Rows(raw, width), Bf16Rows(raw, width).subset([3, 0, 36, 10])):
+        monkeypatch.setattr(Bf16Rows, "COPY_THREADS", 0)
+        a = view.device_rows(dev, block=1024)
+        b = view.device_rows(dev, rows=rows, block=1024)
+        monkeypatch.setattr(Bf16Rows, "COPY_THREADS", 4)
+        assert torch.equal(view.device_rows(dev, block=1024).view(torch.int16), a.view(torch.int16))
+        assert torch.equal(view.device_rows(dev, rows=rows, block=1024).view(torch.int16), b.view(torch.int16))

@@ -31,7 +31,7 @@ def main():
     dev = torch.device("cuda", 0)
     gb = a.rows * a.kpad * 2 / 1e9
     res = {"gb": gb}
-    for mode in ("pageable", 1, 4, 8, 16):
+    for mode in ("pageable", 1, 4, 8, 16):  # COPY_THREADS (0 = pageable default)
         raw = np.load(path, mmap_mode="r")
         v = Bf16Rows(raw, a.kpad - 64)
         torch.cuda.synchronize()
