@@ -212,9 +212,8 @@ class Bf16Rows:
         blocks (``rows``: optional SORTED row index array, gathered on the device) and the
         columns picked on the device.  ``COPY_THREADS`` > 0 (``SHIFU_COPY_THREADS``): each block
         is copied by that many threads into one of two page-locked buffers and sent with an async
-        H2D on a copy stream.  Default 0 = the plain pageable upload: on a 66 GB /dev/shm cache
-        (20M x 1664) it loaded in 8.8 s against 14.5 s for the staged form, although a 13 GB lab
-        file showed them level (profiles/r4/upload_lab_r4m.txt)."""
+        H2D on a copy stream, so the host copy of block i + 1 overlaps the DMA of block i.
+        Default 0 = the plain pageable upload (tools/upload_lab.py measures both)."""
         import torch
         n = len(self.raw)
         dev = torch.device(device)
@@ -271,123 +270,6 @@ class Bf16Rows:
                 for e in evs:
                     if e is not None:
                         e.synchronize()
-        return out
-
-    def __getitem__(self, idx):
-        rest = ()
-        if isinstance(idx, tuple):
-            idx, rest = idx[0], idx[1:]
-        if isinstance(idx, slice):
-            lo, hi, step = idx.indices(len(self))
-            if step != 1:
-                return self[np.arange(lo, hi, step)][(slice(None),) + rest] if rest else self[np.arange(lo, hi, step)]
-            blocks = self._rows(lo, hi)
-            if len(blocks) == 1:
-                out = blocks[0]
-            elif blocks:
-                out = np.concatenate(blocks)
-            else:
-                out = np.empty((0,) + self.shape[1:], self.dtype)
-        elif isinstance(idx, (int, np.integer)):
-            i = int(idx) + (len(self) if idx < 0 else 0)
-            k = int(np.searchsorted(self.offsets, i, side="right") - 1)
-            out = self.parts[k][i - self.offsets[k]]
-        else:
-            ix = np.asarray(idx)
-            if ix.dtype == bool:
-                ix = np.nonzero(ix)[0]
-            out = np.empty((len(ix),) + self.shape[1:], self.dtype)
-            k = np.searchsorted(self.offsets, ix, side="right") - 1
-            for pk in np.unique(k):
-                sel = k == pk
-                out[sel] = self.parts[pk][ix[sel] - self.offsets[pk]]
-        return out[(slice(None),) + rest] if rest else out
-
-    def __array__(self, dtype=None, copy=None):
-        a = self[0: len(self)]
-        a = np.array(a) if not isinstance(a, np.ndarray) or isinstance(a, np.memmap) else a
-        return a.astype(dtype) if dtype is not None else a
-
-
-def write_parts_meta(path: str, meta: dict, part_rows: list) -> None:
-    """Top-level meta.json of a partitioned cache (rank 0, after every rank closed its part)."""
-    parts = [{"dir": f"part-{r:05d}", "n": int(n)} for r, n in enumerate(part_rows)]
-    meta = dict(meta, n=int(sum(part_rows)), parts=parts)
-    tmp = os.path.join(path, ".meta.json.tmp")
-    with open(tmp, "w") as f:
-        json.dump(meta, f, indent=1)
-    os.replace(tmp, os.path.join(path, "meta.json"))
-
-
-def load_parts(path: str, meta: dict, mmap: bool = True) -> dict:
-    """name -> RowParts (or the single part's array) of a partitioned cache."""
-    arrays = {}
-    parts = [p for p in meta["parts"] if p["n"] > 0] or meta["parts"][:1]
-    names = sorted({fn[:-4] for p in parts for fn in os.listdir(os.path.join(path, p["dir"])) if fn.endswith(".npy")})
-    for name in names:
-        arrs = [np.load(os.path.join(path, p["dir"], f"{name}.npy"), mmap_mode="r" if mmap else None) for p in parts]
-        arrays[name] = arrs[0] if len(arrs) == 1 else RowParts(arrs)
-    return arrays
-
-
-class Bf16Rows:
-    """Float view of a bf16 GEMM-ready NormalizedData matrix (``Xb``: uint16 bf16 bits
-    [n, kpad], values in the first ``width`` columns, bias column 1.0 at ``width``).  Row /
-    column indexing returns float32 values of the input columns; ``raw`` is the padded
-    bf16 matrix that the MLP trainer streams to HBM without any cast or padding pass.
-    ``cols``: the raw columns this view exposes (a model's input subset, :meth:`subset`);
-    :meth:`device_rows` moves the bf16 bits to the GPU as they are (no host fp32 expansion)."""
-
-    def __init__(self, raw, width: int, cols=None):
-        self.raw = raw
-        self.cols = None if cols is None else np.asarray(cols, dtype=np.int64)
-        self.width = int(width) if self.cols is None else len(self.cols)
-        self.shape = (len(raw), self.width)
-        self.dtype = np.dtype(np.float32)
-        self.ndim = 2
-
-    def __len__(self):
-        return self.shape[0]
-
-    @property
-    def nbytes(self) -> int:
-        return self.shape[0] * self.width * 4
-
-    @staticmethod
-    def to_f32(u16) -> np.ndarray:
-        u = np.ascontiguousarray(u16, dtype=np.uint16)
-        return (u.astype(np.uint32) << 16).view(np.float32)
-
-    def subset(self, idx) -> "Bf16Rows":
-        """The view of input columns ``idx`` (positions in this view)."""
-        base = np.arange(self.width) if self.cols is None else self.cols
-        return Bf16Rows(self.raw, len(idx), base[np.asarray(idx, dtype=np.int64)])
-
-    def device_rows(self, device, rows=None, block: int = 1 << 18):
-        """bf16 torch tensor [len(rows), width] on ``device``: the raw bits are uploaded in row
-        blocks (``rows``: optional SORTED row index array, gathered on the device) and the
-        columns picked on the device."""
-        import torch
-        n = len(self.raw)
-        out = torch.empty((n if rows is None else len(rows), self.width), dtype=torch.bfloat16, device=device)
-        cols_d = None if self.cols is None else torch.as_tensor(self.cols, device=device)
-        ridx = None if rows is None else np.asarray(rows, dtype=np.int64)
-        lo_out = 0
-        for r0 in range(0, n, block):
-            r1 = min(n, r0 + block)
-            if ridx is not None:
-                a, b = np.searchsorted(ridx, r0), np.searchsorted(ridx, r1)
-                if a == b:
-                    continue
-                sel = ridx[a:b]
-                r0, r1 = int(sel[0]), int(sel[-1]) + 1
-            blk = torch.as_tensor(np.ascontiguousarray(self.raw[r0:r1]).view(np.int16), device=device)
-            blk = blk.view(torch.bfloat16)
-            if ridx is not None:
-                blk = blk.index_select(0, torch.as_tensor(sel - r0, device=device))
-            blk = blk[:, : self.width] if cols_d is None else blk.index_select(1, cols_d)
-            out[lo_out: lo_out + len(blk)] = blk
-            lo_out += len(blk)
         return out
 
     def __getitem__(self, idx):
