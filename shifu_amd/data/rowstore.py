@@ -180,7 +180,7 @@ class Bf16Rows:
     ``cols``: the raw columns this view exposes (a model's input subset, :meth:`subset`);
     :meth:`device_rows` moves the bf16 bits to the GPU as they are (no host fp32 expansion)."""
 
-    COPY_THREADS = int(os.environ.get("SHIFU_COPY_THREADS", "0"))
+    COPY_THREADS = int(os.environ.get("SHIFU_COPY_THREADS", "8"))
 
     def __init__(self, raw, width: int, cols=None):
         self.raw = raw
@@ -212,8 +212,9 @@ class Bf16Rows:
         blocks (``rows``: optional SORTED row index array, gathered on the device) and the
         columns picked on the device.  ``COPY_THREADS`` > 0 (``SHIFU_COPY_THREADS``): each block
         is copied by that many threads into one of two page-locked buffers and sent with an async
-        H2D on a copy stream, so the host copy of block i + 1 overlaps the DMA of block i.
-        Default 0 = the plain pageable upload (tools/upload_lab.py measures both)."""
+        H2D on a copy stream, so the host copy of block i + 1 overlaps the DMA of block i:
+        50 GB/s from a /dev/shm cache with 8 threads against 13.6 GB/s for the plain pageable
+        upload (``COPY_THREADS = 0``; profiles/r4/upload_lab_r4n.txt)."""
         import torch
         n = len(self.raw)
         dev = torch.device(device)
