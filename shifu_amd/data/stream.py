@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import gzip
 import os
+import time
 
 from .purifier import DatasetPlan, finish_table
 from .reader import column_kinds, list_data_files, parse_block, table_from_parts, _parse_parquet
@@ -56,6 +57,7 @@ def byte_ranges(files, rank: int = 0, world: int = 1):
 
 
 READ_THREADS = int(os.environ.get("SHIFU_READ_THREADS", "8"))   # parallel preads per block
+READ_STATS = {"read_s": 0.0, "bytes": 0}          # cumulative pread time / bytes (logged per pass)
 
 
 def _pread_into(fd: int, mv, off: int, want: int) -> int:
@@ -147,7 +149,10 @@ def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int
             mv = memoryview(buf)
             c = len(carry)
             mv[:c] = carry
+            t_read = time.perf_counter()
             got = _pread_into(fd, mv[c:], pos + c, want)
+            READ_STATS["read_s"] += time.perf_counter() - t_read
+            READ_STATS["bytes"] += got
             filled = c + got
             if got == 0:
                 if carry:
@@ -354,6 +359,8 @@ def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTE
 
     def produce():
         r = row0 if resume is None else resume[2]
+        r0 = dict(READ_STATS)
+        t0 = time.perf_counter()
         for key, table in iter_tables(plan, chunk_bytes, rank, world,
                                       resume=None if resume is None else resume[:2], gpu=gp):
             n = table.n
@@ -364,7 +371,10 @@ def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTE
                 yield (k, md) if with_keys else md
         if gp is not None:
             from ..utils.log import get_logger
-            get_logger("data.stream").info("%s", gp.summary())
+            rd = READ_STATS["read_s"] - r0["read_s"]
+            gb = (READ_STATS["bytes"] - r0["bytes"]) / 1e9
+            get_logger("data.stream").info("%s; reads %.2fs (%.1f GB); pass %.2fs", gp.summary(), rd, gb,
+                                           time.perf_counter() - t0)
     yield from prefetched(produce, int(environment.get("shifu.data.prefetch", 1)))
 
 
