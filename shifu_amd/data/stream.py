@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import gzip
 import os
+import threading
 import time
 
 from .purifier import DatasetPlan, finish_table
@@ -112,12 +113,31 @@ def _find_nl(buf, lo: int, hi: int, last: bool) -> int:
     return -1
 
 
+_PIN_POOL: list = []            # page-locked block buffers kept for the process (see _new_buf)
+_PIN_LOCK = threading.Lock()
+
+
 def _new_buf(n: int, pinned: bool):
+    """A block buffer of >= n bytes.  Page-locked buffers come from a process-wide pool and are
+    sized to whole 64 MiB steps: pinning 1 GB takes ~0.3 s and holds a HIP runtime lock that stalls
+    every other thread's kernel launches (rocprofv3 trace, profiles/r4/NOTES_r4.md), so a pass must
+    not allocate one per file or whenever a block's carried line makes it a few KB bigger.  A pooled
+    buffer is handed out again only when nothing else references it (no reader, no block view
+    still queued or being parsed downstream)."""
     if not pinned:
         return bytearray(n)
-    import torch
-    # the ndarray's base holds the tensor's storage: views of a block keep its pages alive
-    return torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy()
+    import sys
+    n = -(-n // (64 << 20)) * (64 << 20)
+    with _PIN_LOCK:
+        for arr in _PIN_POOL:
+            # references: the pool list, this loop variable, getrefcount's argument
+            if len(arr) >= n and sys.getrefcount(arr) <= 3:
+                return arr
+        import torch
+        # the ndarray's base holds the tensor's storage: views of a block keep its pages alive
+        arr = torch.empty(n, dtype=torch.uint8, pin_memory=True).numpy()
+        _PIN_POOL.append(arr)
+        return arr
 
 
 def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int = 1, pinned: bool = False):
