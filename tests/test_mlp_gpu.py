@@ -150,6 +150,32 @@ def test_persistent_head_bitwise_equals_per_tile_head(n):
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
 
 
+def test_persistent_forward_bitwise_at_bench_chunk():
+    """The persistent 8-phase forward (tune key 10) at the bench's 2M-row chunk shape (M * ldc * 2
+    >= 2^31, which an old guard sent to the per-tile kernel) writes exactly the per-tile kernel's
+    activations, bias column and padding."""
+    from shifu_amd.ops import _native as nat
+    M, K, N = (1 << 21) + 77, 1024, 512
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    B = (torch.randn(N, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    outs = []
+    for persist in (0, 1):
+        C = torch.full((M, N), 7.0, device="cuda", dtype=torch.bfloat16)
+        nat.call_hip("shifu_gemm_set_tune", 10, persist)
+        try:
+            nat.call_hip("shifu_gemm_nt", A, K, B, K, 500, C, N, None, 0, None, 0, None, 0,
+                         M, N, K, 0, 0, 500, 1, 0.0, nat.stream_of(A))
+            torch.cuda.synchronize()
+        finally:
+            nat.call_hip("shifu_gemm_set_tune", 10, 1)
+        outs.append(C)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    ref = torch.sigmoid(A[-300:].float() @ B[:500].float().t())
+    assert (outs[1][-300:, :500].float() - ref).abs().max().item() < 1e-2
+    assert torch.all(outs[1][:, 500] == 1.0) and torch.all(outs[1][:, 501:] == 0)
+
+
 def test_bench_configuration_tracks_fp32_oracle():
     """The exact bench trainer configuration (bench.py: n_in 1000, hidden 500/200 sigmoid, RPROP,
     chunks >= 2^17 rows) so the 8-phase forward, the fused head, the ring wgrad (incl. the M % 32
