@@ -1244,8 +1244,10 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   if ((g_big == 3 || auto8) && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
     const int grid8 = ((M + 255) / 256) * ((N + 255) / 256);
     const size_t lds8 = 2 * G8_BUF;
-    // (the epilogue's buffer resource spans one 256-row tile: only that range must fit 32 bits)
-    if (g_fwd_persist && epi != EPI_DACT && 256l * ldc * 2 < (1l << 31)) {
+    // persistent only below 2 GiB of output: at the bench's 2M-row x 512 chunk the per-tile
+    // kernel measured 2.57 ms against 3.19 ms persistent (profiles/r4/mlp_lab_persist_r4t.jsonl;
+    // the epilogue's buffer resource itself spans one 256-row tile, so this is a speed choice)
+    if (g_fwd_persist && epi != EPI_DACT && M * (long)ldc * 2 < (1l << 31)) {
       // persistent forward: one block per CU (LDS = the ring + 32 KiB of epilogue staging)
       int dev = 0, ncu = 256;
       hipGetDevice(&dev);
