@@ -185,3 +185,28 @@ def test_streamed_stats_gpu_equal_cpu_in_memory(tmp_path, monkeypatch, method):
         for k in ("mean", "stdDev", "ks", "iv"):
             if sx.get(k) is not None:
                 np.testing.assert_allclose(sx[k], sy[k], rtol=1e-7, atol=1e-9, err_msg=f"{x['columnName']} {k}")
+
+
+def test_block_reader_helpers(tmp_path, monkeypatch):
+    """data/stream.py: the newline search over uint8 ndarrays (page-locked blocks) equals the
+    bytearray search, and the threaded pread fills a block exactly (short reads at end of file)."""
+    from shifu_amd.data import stream as DS
+    rng = np.random.default_rng(0)
+    raw = bytearray(rng.choice(list(b"abc|\n"), size=300_000).astype(np.uint8).tobytes())
+    arr = np.frombuffer(bytes(raw), np.uint8).copy()
+    for lo, hi in ((0, len(raw)), (1000, 250_000), (5, 6), (299_990, 300_000)):
+        for last in (True, False):
+            assert DS._find_nl(arr, lo, hi, last) == DS._find_nl(raw, lo, hi, last), (lo, hi, last)
+    assert DS._find_nl(np.zeros(10, np.uint8), 0, 10, True) == -1
+    p = tmp_path / "blob"
+    data = rng.integers(0, 256, size=(40 << 20) + 12345, dtype=np.uint8).tobytes()
+    p.write_bytes(data)
+    import os
+    fd = os.open(str(p), os.O_RDONLY)
+    try:
+        monkeypatch.setattr(DS, "READ_THREADS", 5)
+        buf = bytearray(len(data) + 100)
+        got = DS._pread_into(fd, memoryview(buf), 7, len(data))          # runs past EOF by 7 bytes
+        assert got == len(data) - 7 and bytes(buf[:got]) == data[7:]
+    finally:
+        os.close(fd)
