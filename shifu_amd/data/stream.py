@@ -376,6 +376,13 @@ def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTE
     stay in HBM as device-block rows (``gpu_parse.device_rows``)."""
     from ..config import environment
     gp = gpu_parser(plan, gpu_cols, dev)
+    sw = os.environ.get("SHIFU_GIL_SWITCH_MS")
+    if gp is not None and sw:
+        # reader / upload / parse / consumer threads hand the GIL over after every C call: a short
+        # switch interval keeps a thread coming back from a pread or a DMA from waiting a whole
+        # interval (5 ms default) behind another thread's Python work
+        import sys
+        sys.setswitchinterval(float(sw) / 1e3)
 
     def produce():
         r = row0 if resume is None else resume[2]
