@@ -234,7 +234,7 @@ def test_streamed_tables_gpu_parse_equal_host_multi_file(tmp_path):
     assert gp is not None and "w" not in [header[c] for c in gp.gpu_cols]
     host = list(DS.iter_tables(plan, 64 << 10))
     dev = list(DS.iter_tables(plan, 64 << 10, gpu=gp))
-    assert len(host) == len(dev) > 10
+    assert len(host) == len(dev) >= 8
     for (ka, ta), (kb, tb) in zip(host, dev):
         assert ka == kb and ta.n == tb.n and ta.bad_rows == tb.bad_rows
         for name in header:
