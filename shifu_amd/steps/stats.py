@@ -184,6 +184,13 @@ def run_correlation(ms: ModelSet, device=None, chunk_rows: int = 1 << 18):
             os.path.exists(cache_c) and json.load(open(cache_c)) == nums:
         _log.info("correlation: reusing %s (shifu.stats.corr.reuse)", cache_m)
         C = np.load(cache_m, allow_pickle=False)
+    elif _use_streaming(ms):
+        C = _correlation_streamed(ms, cols, device)
+        if _writer() and C is not None:
+            os.makedirs(cache_dir, exist_ok=True)
+            np.save(cache_m, C)
+            with open(cache_c, "w") as f:
+                json.dump(nums, f)
     else:
         md = shard_model_data(ms.load_raw(cols))
         # center on the stats step's means (the same on every rank; Pearson is shift invariant)
@@ -223,6 +230,49 @@ def run_correlation(ms: ModelSet, device=None, chunk_rows: int = 1 << 18):
             f.write(f"{c.num},{c.name}," + ", ".join(vals) + "\n")
     _log.info("correlation: %d columns -> %s", len(cols), path)
     return C, [c.num for c in cols]
+
+
+def _correlation_streamed(ms: ModelSet, cols, device=None):
+    """``stats -c`` over this rank's byte range chunk by chunk (the data set never sits in host
+    memory whole: 20M x 1600 fp64 would be 256 GB).  On a GPU the numeric columns are parsed on
+    the device (K0) and fed to the accumulator as [rows, F] views of the parsed block; categorical
+    columns take their pos-rate encoding on the host.  Same rows (purified, all of them) and the
+    same accumulator as the in-memory pass; with the exact int8-digit sums (GPU) the matrix is
+    identical."""
+    import torch
+    from ..config import environment
+    from ..data import stream as DS
+    from ..data.gpu_parse import device_rows
+    from ..data.purifier import plan_dataset
+    from ..parallel import dist
+    mc = ms.mc
+    info = dist.info()
+    plan = plan_dataset(mc, mc.dataSet, [c.name for c in cols if not c.is_categorical()],
+                        [c.name for c in cols if c.is_categorical()])
+    pdev = _parse_device(device)
+    chunk = int(float(environment.get("shifu.stats.chunkMB", 1024 if pdev is not None else 256)) * (1 << 20))
+    shift = [0.0 if c.is_categorical() or not isinstance(c.mean, (int, float)) or not np.isfinite(c.mean)
+             else float(c.mean) for c in cols]
+    acc = S.CorrAccumulator(len(cols), device, shift=shift)
+    num_j = [j for j, c in enumerate(cols) if not c.is_categorical()]
+    cat_j = [j for j, c in enumerate(cols) if c.is_categorical()]
+    for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size,
+                                 gpu_cols=[cols[j].name for j in num_j], dev=pdev):
+        n = md.n
+        dv = device_rows([md.table.columns.get(cols[j].name) for j in num_j], pdev) if pdev is not None and num_j \
+            else None
+        if dv is not None:
+            X = torch.empty((n, len(cols)), dtype=torch.float64, device=dv.device)
+            X[:, num_j] = dv.t()
+        else:
+            X = np.empty((n, len(cols)), np.float64)
+            for j in num_j:
+                X[:, j] = md.table[cols[j].name].numeric()
+        for j in cat_j:
+            v = N.normalize_column(cols[j], md.table[cols[j].name], "OLD_ZSCALE", None)[:, 0]
+            X[:, j] = torch.as_tensor(v, device=X.device) if torch.is_tensor(X) else v
+        acc.update(X)
+    return acc.finalize(0)
 
 
 def read_correlation(path: str):

@@ -210,3 +210,40 @@ def test_block_reader_helpers(tmp_path, monkeypatch):
         assert got == len(data) - 7 and bytes(buf[:got]) == data[7:]
     finally:
         os.close(fd)
+
+
+def _corr_pair(tmp_path, monkeypatch, device):
+    import shutil
+    from shifu_amd.config import environment
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.stats import read_correlation, run_stats
+    from shifu_amd.utils.synthetic import make_model_set
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=4001, n_num=9, n_cat=2)
+    run_init(a)
+    run_stats(a, device=device)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    monkeypatch.setitem(environment.props(), "shifu.stats.streaming", "false")
+    run_stats(a, correlation=True, device=device)
+    monkeypatch.setitem(environment.props(), "shifu.stats.streaming", "true")
+    monkeypatch.setitem(environment.props(), "shifu.stats.chunkMB", str(16 / 1024))   # many blocks
+    run_stats(b, correlation=True, device=device)
+    na, ca = read_correlation(os.path.join(a, "correlation.csv"))
+    nb, cb = read_correlation(os.path.join(b, "correlation.csv"))
+    assert na == nb and len(na) >= 9
+    return np.asarray(ca), np.asarray(cb)
+
+
+def test_correlation_streamed_equals_in_memory(tmp_path, monkeypatch):
+    """`stats -c` streamed chunk by chunk (no whole-table load) == the in-memory pass."""
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    ca, cb = _corr_pair(tmp_path, monkeypatch, "cpu")
+    np.testing.assert_allclose(ca, cb, atol=1e-10)
+
+
+@pytest.mark.gpu
+def test_correlation_streamed_gpu_parse_exact(tmp_path, monkeypatch):
+    """On the GPU: streamed `stats -c` with GPU-parsed blocks fed as device views == the in-memory
+    pass (int8-digit MFMA sums; only the per-chunk digit scales and their fp64 flush order differ)."""
+    ca, cb = _corr_pair(tmp_path, monkeypatch, "cuda")
+    np.testing.assert_allclose(ca, cb, atol=1e-12)
