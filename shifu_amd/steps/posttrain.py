@@ -48,7 +48,12 @@ def _bin_score_sums_gpu(used, table, score, dev, batch: int = 64):
                 b = torch.as_tensor(_bin_num(c, col)).to(dev)
             else:
                 bb = torch.as_tensor(np.asarray(c.bin_boundary or [float("-inf")], np.float64)).to(dev)
-                b = bin_index_torch(torch.as_tensor(col.numeric().astype(np.float64)).to(dev), bb)
+                if getattr(col, "dev", None) is not None and col._values is None and \
+                        col.dev.block.D.device == dev:
+                    v = col.dev.tensor()               # GPU-parsed (K0): already in HBM
+                else:
+                    v = torch.as_tensor(col.numeric().astype(np.float64)).to(dev)
+                b = bin_index_torch(v, bb)
             keys[j] = torch.where(b < 0, nbs[j] - 1, torch.clamp(b, max=nbs[j] - 1)).to(torch.int32)
         cnt, ssum = keyed_hist(keys, max(nbs), sc)
         cnt, ssum = cnt.cpu().numpy(), ssum.cpu().numpy()
@@ -65,13 +70,18 @@ def run_posttrain(root: str = ".", device=None) -> int:
     byname = {c.name: c for c in ms.ccs}
     # data parallel: every rank scores its row shard; the per-(column, bin) score sums and counts
     # are all-reduced once (the PostTrainMapper -> reducer shuffle), then every rank holds them
-    md = shard_model_data(ms.load_raw([byname[n] for n in names if n in byname]))
-    res = runner.score(md.table, 1000.0)
-    score = np.asarray(res["mean"] if "mean" in res else res["class_scores"].max(1))
-    used = [c for c in cols if c.name in md.table]
     dev = torch.device(device) if device is not None else default_device()
-    parts = _bin_score_sums_gpu(used, md.table, score, dev) if dev.type == "cuda" else \
-        [_bin_score_sums_host(c, md.table[c.name], score) for c in used]
+    raw_cols = [byname[n] for n in names if n in byname]
+    from .stats import _use_streaming
+    if _use_streaming(ms):
+        used, parts = _posttrain_streamed(ms, runner, cols, raw_cols, dev)
+    else:
+        md = shard_model_data(ms.load_raw(raw_cols))
+        res = runner.score(md.table, 1000.0)
+        score = np.asarray(res["mean"] if "mean" in res else res["class_scores"].max(1))
+        used = [c for c in cols if c.name in md.table]
+        parts = _bin_score_sums_gpu(used, md.table, score, dev) if dev.type == "cuda" else \
+            [_bin_score_sums_host(c, md.table[c.name], score) for c in used]
     if used and dist.info().world_size > 1:
         flat = dist.all_reduce_np(np.concatenate([p.reshape(-1) for p in parts]))
         off = 0
@@ -97,6 +107,36 @@ def run_posttrain(root: str = ".", device=None) -> int:
                 f.write(f"{k}\t{nm.get(k, k)}\t{v / tot}\n")
     _log.info("posttrain: binAvgScore for %d columns", len(cols))
     return 0
+
+
+def _posttrain_streamed(ms, runner, cols, raw_cols, dev):
+    """The posttrain pass over this rank's byte range chunk by chunk (out of core, SURVEY §5.7;
+    the reference streams rows through PostTrainMapper): each chunk is scored and its per-(column,
+    bin) score sums / counts are added up; on a GPU the model's numeric inputs are parsed on the
+    device (K0) and binned where they land.  -> (columns, [2, n_bins] arrays)."""
+    from ..config import environment
+    from ..data import stream as DS
+    from ..data.purifier import plan_dataset
+    from .stats import _parse_device
+    mc = ms.mc
+    info = dist.info()
+    plan = plan_dataset(mc, mc.dataSet, [c.name for c in raw_cols if not c.is_categorical()],
+                        [c.name for c in raw_cols if c.is_categorical()])
+    pdev = _parse_device(dev) if dev.type == "cuda" else None
+    chunk = int(float(environment.get("shifu.stats.chunkMB", 1024 if pdev is not None else 256)) * (1 << 20))
+    present = set(plan.header)
+    used = [c for c in cols if c.name in present]
+    acc = None
+    for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size,
+                                 gpu_cols=[c.name for c in raw_cols if not c.is_categorical()], dev=pdev):
+        res = runner.score(md.table, 1000.0)
+        score = np.asarray(res["mean"] if "mean" in res else res["class_scores"].max(1))
+        parts = _bin_score_sums_gpu(used, md.table, score, pdev) if pdev is not None else \
+            [_bin_score_sums_host(c, md.table[c.name], score) for c in used]
+        acc = parts if acc is None else [a + p for a, p in zip(acc, parts)]
+    if acc is None:                            # no rows on this rank: zeros for the all-reduce
+        acc = [np.zeros((2, c.n_bins())) for c in used]
+    return used, acc
 
 
 def reason_codes(ccs, table, top_k: int = 3):

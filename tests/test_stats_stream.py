@@ -247,3 +247,49 @@ def test_correlation_streamed_gpu_parse_exact(tmp_path, monkeypatch):
     pass (int8-digit MFMA sums; only the per-chunk digit scales and their fp64 flush order differ)."""
     ca, cb = _corr_pair(tmp_path, monkeypatch, "cuda")
     np.testing.assert_allclose(ca, cb, atol=1e-12)
+
+
+def _posttrain_pair(tmp_path, monkeypatch, device):
+    import json
+    import shutil
+    from shifu_amd.config import environment
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.steps.create import run_init
+    from shifu_amd.steps.norm import run_norm
+    from shifu_amd.steps.posttrain import run_posttrain
+    from shifu_amd.steps.stats import run_stats
+    from shifu_amd.steps.train import run_train
+    from shifu_amd.utils.synthetic import make_model_set
+    a = make_model_set(str(tmp_path), "a", "NN", n_rows=3001, n_num=7, n_cat=2)
+    mc = ModelConfig.load(os.path.join(a, "ModelConfig.json"))
+    mc.train["numTrainEpochs"], mc.train["baggingNum"] = 5, 1
+    mc.save()
+    run_init(a)
+    run_stats(a, device=device)
+    run_norm(a)
+    run_train(a)
+    b = str(tmp_path / "b")
+    shutil.copytree(a, b)
+    monkeypatch.setitem(environment.props(), "shifu.stats.streaming", "false")
+    run_posttrain(a, device=device)
+    monkeypatch.setitem(environment.props(), "shifu.stats.streaming", "true")
+    monkeypatch.setitem(environment.props(), "shifu.stats.chunkMB", str(16 / 1024))
+    run_posttrain(b, device=device)
+    ca = {c["columnName"]: c["columnBinning"].get("binAvgScore") for c in json.load(open(os.path.join(a, "ColumnConfig.json")))}
+    cb = {c["columnName"]: c["columnBinning"].get("binAvgScore") for c in json.load(open(os.path.join(b, "ColumnConfig.json")))}
+    assert any(v for v in ca.values())
+    return ca, cb
+
+
+def test_posttrain_streamed_equals_in_memory(tmp_path, monkeypatch):
+    """posttrain streamed chunk by chunk == the in-memory pass (binAvgScore of every column)."""
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    ca, cb = _posttrain_pair(tmp_path, monkeypatch, "cpu")
+    assert ca == cb
+
+
+@pytest.mark.gpu
+def test_posttrain_streamed_gpu_equals_in_memory(tmp_path, monkeypatch):
+    """On the GPU (GPU-parsed inputs binned in HBM): streamed posttrain == the in-memory pass."""
+    ca, cb = _posttrain_pair(tmp_path, monkeypatch, "cuda")
+    assert ca == cb
