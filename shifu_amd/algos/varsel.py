@@ -188,16 +188,17 @@ def auto_filter(mc, ccs, corr: np.ndarray | None = None, corr_nums=None):
 @torch.no_grad()
 def first_layer_fp32(xb: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, fl_cache: dict | None = None):
     """S = X W1^T + b1 in fp32.  GPU: ONE own-MFMA GEMM (gemm_kernels.hip, EPI_F32 tile) over
-    split-bf16 operands concatenated along K (``ops/gemm_ops.linear_fp32``, 3 part products
-    hi*hi + hi*mid + mid*hi, exact in the fp32 accumulator): the fp32 product to ~2^-17 relative,
-    like K15's split digits.  ``fl_cache`` keeps the split weights and the operand buffer across
+    split-bf16 operands concatenated along K (``ops/gemm_ops.linear_fp32``, the 6 part products
+    hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid, exact in the fp32 accumulator): fp32-accurate, as
+    eval scoring, so near-tied SE scores rank as the reference's float computation does (3 terms,
+    ~2^-17 relative, could reorder them).  ``fl_cache`` keeps the split weights and the operand buffer across
     row chunks."""
     if xb.device.type != "cuda":
         return xb @ W1.t() + b1
     from ..ops.gemm_ops import SplitWeights, linear_fp32
     fl_cache = {} if fl_cache is None else fl_cache
     if fl_cache.get("sw") is None:
-        fl_cache["sw"] = SplitWeights(W1, b1, terms=3)
+        fl_cache["sw"] = SplitWeights(W1, b1, terms=6)
     return linear_fp32(xb, W1, b1, sw=fl_cache["sw"])
 
 

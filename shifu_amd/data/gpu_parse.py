@@ -259,7 +259,11 @@ class GpuBlockParser:
             n, bad, out = int((~blank).sum()), 0, {}
             if nh:
                 mo = moffs.cpu().numpy()
-                cap = int(np.clip(mo[..., 1] - mo[..., 0], 0, None).sum()) + nl * (nh + 3)
+                # the kernel writes only column 0's bounds on a blank line: the other entries are
+                # whatever the allocator left there, so they must not size the gather buffer
+                if blank.any():
+                    mo[:, blank, :] = 0
+                cap =int(np.clip(mo[..., 1] - mo[..., 0], 0, None).sum()) + nl * (nh + 3)
                 mini = np.empty(cap, np.uint8)
                 nb = nat.rt().shifu_gather_fields(addr, mo.ctypes.data, nl, nh, fl.ctypes.data,
                                                   self.delim.encode(), mini.ctypes.data, cap)

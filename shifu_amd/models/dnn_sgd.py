@@ -240,7 +240,7 @@ def train_dnn(X, y: np.ndarray, w: np.ndarray, valid: np.ndarray, params: dict, 
     n_in = int(np.shape(X)[1])
     ref = DNN(n_in, hidden, acts, params.get("WeightInitializer"), seed)      # the TF initialisation
     spec = MLPSpec(n_in, hidden, [_mlp_act(a) for a in acts[: len(hidden)]] or ["sigmoid"], 1, "sigmoid", loss,
-                   flat=False)
+                   flat=False, tf_objective=True)
     if len(spec.acts) < len(hidden):
         spec.acts += [_mlp_act(None)] * (len(hidden) - len(spec.acts))
     tr = MLPTrainer(spec, device=device, propagation="R", seed=seed, chunk_rows=max(1 << 16, batch))
@@ -287,7 +287,8 @@ def train_dnn(X, y: np.ndarray, w: np.ndarray, valid: np.ndarray, params: dict, 
     hist, it = [], 0
     from ..ops import _native as nat
     for ep in range(1, epochs + 1):
-        terr_sum, tcnt = 0.0, 0.0
+        # sum(w * loss) of every batch (TF objective, kept on the device: one host read per epoch)
+        terr_sum, tcnt = torch.zeros((), dtype=torch.float64, device=device), 0.0
         for bi, (a, b) in enumerate(bounds):
             it += 1
             tr.compute_gradients(data, a, b)
@@ -299,9 +300,9 @@ def train_dnn(X, y: np.ndarray, w: np.ndarray, valid: np.ndarray, params: dict, 
                              lr, 0.9, 0.999, 0.9, gscale, 0.01, l2mask, it, nat.stream_of(tr.params.flat))
             else:
                 _tf_step_torch(rule, tr.params.flat, tr.grad, s0, s1, lr, gscale, 0.01, l2mask.float(), it)
-            terr_sum += float(tr.err_acc[0])
+            terr_sum += tr.err_acc[0]
             tcnt += float(cnts[bi])
-        terr = terr_sum / max(tcnt, 1.0)
+        terr = float(terr_sum) / max(tcnt, 1.0)
         v = torch.zeros(2, dtype=torch.float64, device=device)
         if vdata is not None:
             with torch.no_grad():

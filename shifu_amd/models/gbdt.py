@@ -1132,23 +1132,21 @@ class TreeTrainer:
                 finally:
                     self._fuse = None
                 t0 = time.perf_counter()
-                rng = trace_range("gbdt.apply_residual")
-                rng.__enter__()
-                keep = None
-                if tid > 0 and c.dropout_rate > 0.0:
-                    # DTWorker :634-638: each row skips this tree's update with prob. DropoutRate
-                    keep = (torch.rand(d.n, device=self.dev, generator=self.tgen) >= c.dropout_rate).float()
-                    before = self.pred.clone()
-                if not fused or not self._leaf_done:      # (max_depth 1: no level pass ran)
-                    self.apply_tree(tree, d, self.pred, tree.weight, tid == 0)
-                if keep is not None:
-                    self.pred.copy_(before + (self.pred - before) * keep)
-                if self.valid is not None:
-                    self.apply_tree(tree, self.valid, self.vpred, tree.weight, tid == 0)
-                self.timings["apply"] += time.perf_counter() - t0
-                terr = self._residual(self.pred, d, out)
-                verr = self._residual(self.vpred, self.valid, vout) if self.valid is not None else float("nan")
-                rng.__exit__(None, None, None)
+                with trace_range("gbdt.apply_residual"):
+                    keep = None
+                    if tid > 0 and c.dropout_rate > 0.0:
+                        # DTWorker :634-638: each row skips this tree's update with prob. DropoutRate
+                        keep = (torch.rand(d.n, device=self.dev, generator=self.tgen) >= c.dropout_rate).float()
+                        before = self.pred.clone()
+                    if not fused or not self._leaf_done:      # (max_depth 1: no level pass ran)
+                        self.apply_tree(tree, d, self.pred, tree.weight, tid == 0)
+                    if keep is not None:
+                        self.pred.copy_(before + (self.pred - before) * keep)
+                    if self.valid is not None:
+                        self.apply_tree(tree, self.valid, self.vpred, tree.weight, tid == 0)
+                    self.timings["apply"] += time.perf_counter() - t0
+                    terr = self._residual(self.pred, d, out)
+                    verr = self._residual(self.vpred, self.valid, vout) if self.valid is not None else float("nan")
             else:
                 if not self._pending:
                     # RF: the next trees grow together (their subsample weights drawn in tree order,

@@ -123,6 +123,7 @@ class MLPSpec:
     out_act: str = "sigmoid"          # "sigmoid" (classification) or linear/relu/leakyrelu/swish
     loss: str = "squared"
     flat: bool = True                 # Encog's sigmoid flat spot (+0.1 on f'); False for TENSORFLOW
+    tf_objective: bool = False        # error sums = the TF objective sum(w * loss) (same deltas)
 
     def __post_init__(self):
         self.hidden = [int(h) for h in self.hidden]
@@ -134,6 +135,10 @@ class MLPSpec:
         self.loss = (self.loss or "squared").lower()
         if self.loss not in LOSS_IDS:
             self.loss = "squared"
+
+    @property
+    def loss_id(self) -> int:       # kernel loss code: 0-2 Encog error, 3-5 TF objective
+        return LOSS_IDS[self.loss] + (3 if self.tf_objective else 0)
 
     @property
     def layer_in(self):             # logical input width of each weight layer
@@ -766,7 +771,7 @@ class MLPTrainer:
         w1, w2p, w2tp = f2w
         nat.call_hip("shifu_mlp_fused2", x, kp[0], mc, kp[0], w1, kp[0], 512, sp.hidden[0], w2p, w2tp,
                      sp.hidden[1], wv[2], kp[2], y, s, h1, kp[1], d2, kp[2], d1, kp[1], slab, self.err_acc,
-                     ACT_IDS[sp.acts[0]], ACT_IDS[sp.acts[1]], ACT_IDS[sp.out_act], LOSS_IDS[sp.loss],
+                     ACT_IDS[sp.acts[0]], ACT_IDS[sp.acts[1]], ACT_IDS[sp.out_act], sp.loss_id,
                      sp.flat_spot(sp.acts[0]), sp.flat_spot(sp.acts[1]), sp.flat_spot(sp.out_act), st)
         nat.call_hip("shifu_colsum_fixed", slab, tiles, kp[2], part, gv[2], st)
         self._grad_ready(2)
@@ -811,7 +816,7 @@ class MLPTrainer:
             nat.call_hip("shifu_gemm_head", acts[lh].data_ptr(), kp[lh], wb[lh].data_ptr(), kp[lh], sp.hidden[lh],
                          dels[L].data_ptr(), kp[L], mc, kp[L], kp[lh], ACT_IDS[sp.acts[lh]], sp.hidden[lh],
                          wv[L].data_ptr(), y.data_ptr(), nat.ptr(s), gv[L].data_ptr(), self.err_acc.data_ptr(),
-                         kp[L], ACT_IDS[sp.out_act], LOSS_IDS[sp.loss], sp.flat_spot(sp.out_act),
+                         kp[L], ACT_IDS[sp.out_act], sp.loss_id, sp.flat_spot(sp.out_act),
                          sp.flat_spot(sp.acts[lh]), nat.ptr(ws["gw_slab"]), st)
             if ws["gw_slab"] is not None:
                 nat.call_hip("shifu_colsum_fixed", ws["gw_slab"], -(-mc // 256), kp[L], ws["gw_part"],
@@ -822,7 +827,7 @@ class MLPTrainer:
                          wv[L].data_ptr(), y.data_ptr(), sp.n_out, nat.ptr(s),
                          nat.ptr(dels[L]) if L else None, kp[L], gv[L].data_ptr(), self.err_acc.data_ptr(),
                          None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act],
-                         ACT_IDS[sp.acts[L - 1]] if L else 2, LOSS_IDS[sp.loss], sp.flat_spot(sp.out_act),
+                         ACT_IDS[sp.acts[L - 1]] if L else 2, sp.loss_id, sp.flat_spot(sp.out_act),
                          sp.flat_spot(sp.acts[L - 1]) if L else 0.0, st)
         if fwd_event is not None:
             fwd_event.record()                     # forward + head of this chunk enqueued
@@ -874,7 +879,9 @@ class MLPTrainer:
         if sp.loss == "log":
             dl = e * s
             pc = p.clamp(1e-7, 1 - 1e-7)
-            if sp.n_out == 1:
+            if sp.tf_objective:
+                err = (-(torch.log(p + 1e-7) * y + torch.log(1 - p + 1e-7) * (1 - y)) * s).sum()
+            elif sp.n_out == 1:
                 err = -(torch.log(pc) * y + torch.log(1 - pc) * (1 - y)).sum()
             else:
                 err = -(torch.log(pc) * y * s).sum()
@@ -884,7 +891,7 @@ class MLPTrainer:
             err = (e.abs() * s).sum()
         else:
             dl = (act_deriv(sp.out_act, zo, p) + sp.flat_spot(sp.out_act)) * e * s
-            err = ((e * s) ** 2).sum()
+            err = (e * e * s).sum() if sp.tf_objective else ((e * s) ** 2).sum()
         self.err_acc[0] += float(err)
         self.err_acc[1] += float(s.sum())
         gv[L].add_(dl.t() @ acts[L])

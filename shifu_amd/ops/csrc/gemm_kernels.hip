@@ -738,16 +738,18 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
     if (m < p.M) {
       const float y = y_pf, sg = s_pf;
       const float a = act_fwd(h.out_act, z), e = y - a;
-      if (h.loss == 1) {
+      const int lm = h.loss % 3;                       // loss >= 3: TF objective as the error
+      if (lm == 1) {
         dlt = e * sg;
         const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
-        e_c = -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
-      } else if (h.loss == 2) {
+        e_c = h.loss >= 3 ? -(__logf(a + 1e-7f) * y + __logf(1.f - a + 1e-7f) * (1.f - y)) * sg
+                          : -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
+      } else if (lm == 2) {
         dlt = (y < a ? 1.f : -1.f) * (act_deriv_out(h.out_act, a) + h.flat_out) * sg;
         e_c = fabsf(e) * sg;
       } else {
         dlt = (act_deriv_pre(h.out_act, z) + h.flat_out) * e * sg;
-        e_c = (double)(e * sg) * (e * sg);
+        e_c = h.loss >= 3 ? (double)(e * e) * sg : (double)(e * sg) * (e * sg);
       }
       e_w = sg;
     }
@@ -888,16 +890,18 @@ __device__ __forceinline__ void head_epilogue_regs(const GemmArgs& p, const Head
     if (m < p.M) {
       const float y = y_pf, sg = s_pf;
       const float a = act_fwd(h.out_act, z), e = y - a;
-      if (h.loss == 1) {
+      const int lm = h.loss % 3;                       // loss >= 3: TF objective as the error
+      if (lm == 1) {
         dlt = e * sg;
         const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
-        e_c = -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
-      } else if (h.loss == 2) {
+        e_c = h.loss >= 3 ? -(__logf(a + 1e-7f) * y + __logf(1.f - a + 1e-7f) * (1.f - y)) * sg
+                          : -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
+      } else if (lm == 2) {
         dlt = (y < a ? 1.f : -1.f) * (act_deriv_out(h.out_act, a) + h.flat_out) * sg;
         e_c = fabsf(e) * sg;
       } else {
         dlt = (act_deriv_pre(h.out_act, z) + h.flat_out) * e * sg;
-        e_c = (double)(e * sg) * (e * sg);
+        e_c = h.loss >= 3 ? (double)(e * e) * sg : (double)(e * sg) * (e * sg);
       }
       e_w = sg;
     }
@@ -1208,12 +1212,20 @@ static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
 static int g_fwd_persist = 1;     // persistent 8-phase forward (tune key 10; 0 = one tile per block)
 static int g_head_persist = 0;    // persistent fused head (tune key 11 / SHIFU_HEAD_PERSIST=1; measured
                                   // 1.13 vs 1.10 ms per 2M-row chunk: off by default, profiles/r4)
+static int g_ring_nt = 0;         // persistent ring forward (gemm_ring_nt.hip, tune key 12)
+static int g_ring_nt_cap = 0;     // lab: grid cap of the ring forward (tune key 13; 0 = one block per CU)
+// gemm_ring_nt.hip (same library): -1 when the shape is not one it takes
+extern "C" int shifu_ring_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc, int M,
+                             int N, int K, int epi, int act, int n_valid, int bias_col, int grid_cap,
+                             hipStream_t stream);
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
   if (key == 2) { g_wg_interleave = val; return 0; }
   if (key == 9) { g_dbg = val; return 0; }
   if (key == 10) { g_fwd_persist = val; return 0; }
   if (key == 11) { g_head_persist = val; return 0; }
+  if (key == 12) { g_ring_nt = val; return 0; }
+  if (key == 13) { g_ring_nt_cap = val; return 0; }
   return -1;
 }
 SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b == 3 || b == 4) ? b : 0; return 0; }
@@ -1240,6 +1252,11 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;
   const bool dfo_act = act_deriv_from_output(act);
+  if (g_ring_nt && M >= 65536 && (epi == EPI_STORE || (epi == EPI_ACT && dfo_act)) && !g_dbg) {
+    const int r = shifu_ring_nt(A, lda, B, ldb, NB, C, ldc, M, N, K, epi, act, n_valid, bias_col, g_ring_nt_cap,
+                                stream);
+    if (r != -1) return r;          // -1: shape not taken, fall through
+  }
   const bool auto8 = g_big == 0 && M >= 65536 && N >= 512 && K >= 512;
   if ((g_big == 3 || auto8) && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
     const int grid8 = ((M + 255) / 256) * ((N + 255) / 256);

@@ -82,16 +82,18 @@ __global__ __launch_bounds__(256) void mlp_output_kernel(OutArgs p) {
         const float e = y - a;
         if (p.P && valid && li == 0) p.P[(size_t)m * p.ldp + o] = a;
         float contrib;
-        if (p.loss == 1) {          // log
+        const int lm = p.loss % 3;                // loss >= 3: same deltas, TF objective as the error
+        if (lm == 1) {              // log
           dlt[o] = e * s;
           const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
-          contrib = NOUT == 1 ? -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y)) : -(__logf(ac) * y * s);
-        } else if (p.loss == 2) {   // absolute
+          contrib = p.loss >= 3 ? -(__logf(a + 1e-7f) * y + __logf(1.f - a + 1e-7f) * (1.f - y)) * s
+                    : NOUT == 1 ? -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y)) : -(__logf(ac) * y * s);
+        } else if (lm == 2) {       // absolute
           dlt[o] = (y < a ? 1.f : -1.f) * (act_deriv_out(p.out_act, a) + p.flat_out) * s;
           contrib = fabsf(e) * s;
         } else {                    // squared (default)
           dlt[o] = (act_deriv_pre(p.out_act, z) + p.flat_out) * e * s;
-          contrib = (e * s) * (e * s);
+          contrib = p.loss >= 3 ? e * e * s : (e * s) * (e * s);
         }
         if (!valid) dlt[o] = 0.f;
         if (valid && li == 0) esum += contrib;

@@ -741,23 +741,21 @@ class TrainStep:
         # uint8 codes go to the device one 32-feature group at a time (no host int32 staging)
         codes_np = codes if isinstance(codes, np.ndarray) else np.asarray(codes)
         all_rows = len(tri) == codes_np.shape[0]
-        rng = trace_range("train.upload_bins")
-        rng.__enter__()
-        if self._host_bins(len(tri), codes_np.shape[1]):
-            _log.info("tree bins stay in pinned host memory (%d rows x %d features)", len(tri), codes_np.shape[1])
-            d = BinnedData.host_resident(codes_np, y[tri], nb, is_cat, w[tri], device=dev,
-                                         rows=None if all_rows else tri)
-        else:
-            d = BinnedData.from_codes(codes_np, y[tri], nb, is_cat, w[tri], device=dev,
-                                      rows=None if all_rows else tri)
-        vd = None
-        if ts.vcodes is not None:
-            vd = BinnedData.from_codes(np.asarray(ts.vcodes), np.asarray(ts.vy, np.float32), nb, is_cat,
-                                       np.asarray(ts.vw, np.float32), device=dev)
-        elif valid_m.any():
-            vi = np.nonzero(valid_m)[0]
-            vd = BinnedData.from_codes(codes_np, y[vi], nb, is_cat, w[vi], device=dev, rows=vi)
-        rng.__exit__(None, None, None)
+        with trace_range("train.upload_bins"):
+            if self._host_bins(len(tri), codes_np.shape[1]):
+                _log.info("tree bins stay in pinned host memory (%d rows x %d features)", len(tri), codes_np.shape[1])
+                d = BinnedData.host_resident(codes_np, y[tri], nb, is_cat, w[tri], device=dev,
+                                             rows=None if all_rows else tri)
+            else:
+                d = BinnedData.from_codes(codes_np, y[tri], nb, is_cat, w[tri], device=dev,
+                                          rows=None if all_rows else tri)
+            vd = None
+            if ts.vcodes is not None:
+                vd = BinnedData.from_codes(np.asarray(ts.vcodes), np.asarray(ts.vy, np.float32), nb, is_cat,
+                                           np.asarray(ts.vw, np.float32), device=dev)
+            elif valid_m.any():
+                vi = np.nonzero(valid_m)[0]
+                vd = BinnedData.from_codes(codes_np, y[vi], nb, is_cat, w[vi], device=dev, rows=vi)
         tree_num = int(_num(p.get("TreeNum"), 100))
         cfg = TreeConfig(alg, tree_num=tree_num, max_depth=int(_num(p.get("MaxDepth"), 7 if alg == "GBT" else 10)),
                          min_instances_per_node=int(_num(p.get("MinInstancesPerNode"), 5)),

@@ -108,6 +108,33 @@ def test_gpu_parse_host_columns_from_field_bounds(crlf):
 
 
 @pytest.mark.gpu
+def test_gpu_parse_blank_lines_after_poisoned_allocator():
+    """Blank lines leave the host-column bounds of those lines unwritten by the kernel: the gather
+    buffer must be sized without them.  Fill and free a large block with huge int32 values first,
+    so the caching allocator hands that memory back to the parser's bounds tensor."""
+    from shifu_amd.data.gpu_parse import GpuBlockParser
+    rng = random.Random(9)
+    C = 11
+    lines = []
+    for i in range(20000):
+        lines.append("|".join(f"{rng.gauss(0, 10):.3f}" if c != 4 else f"s{i % 13}" for c in range(C)))
+        if i % 7 == 0:
+            lines.append("")
+    data = ("\n".join(lines) + "\n").encode()
+    poison = torch.full((64 << 20,), 0x7ffffff0, dtype=torch.int32, device="cuda")
+    del poison                                              # back to the caching allocator, not zeroed
+    kinds = [1] * C
+    kinds[4] = 2
+    pinned = torch.empty(len(data), dtype=torch.uint8, pin_memory=True).numpy()
+    pinned[:] = np.frombuffer(data, np.uint8)
+    gp = GpuBlockParser(kinds, [c for c in range(C) if c not in (4, 8)], "|", [""], torch.device("cuda", 0))
+    n, bad, out = gp.parse(memoryview(pinned), 4)
+    n2, bad2, ref = R._parse_native(bytearray(data), "|", kinds, [""], 4)
+    assert (n, bad) == (n2, bad2) == (20000, 0)
+    assert list(out[4][1]) == list(ref[4][1]) and out[8][1].tobytes() == ref[8][1].tobytes()
+
+
+@pytest.mark.gpu
 def test_gpu_parse_no_trailing_newline_and_wide_rows():
     from shifu_amd.data.gpu_parse import GpuBlockParser
     rng = np.random.default_rng(3)

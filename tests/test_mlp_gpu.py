@@ -175,6 +175,45 @@ def test_persistent_forward_bitwise_equals_per_tile():
     assert torch.all(outs[1][:, 500] == 1.0) and torch.all(outs[1][:, 501:] == 0)
 
 
+@pytest.mark.parametrize("M,K,N,NB,nv,epi,act", [
+    ((1 << 20) + 77, 1024, 512, 500, 500, 0, 0),       # the bench's first layer (sigmoid + bias column)
+    (70000 + 33, 256, 512, 512, 512, 0, 1),           # K = 8 steps per tile, tanh, no partial columns
+    (65536 + 300, 128, 264, 260, 260, 2, 2),          # store z, partial last column tile (N % 256 != 0)
+])
+def test_ring_forward_matches_8phase_and_oracle(M, K, N, NB, nv, epi, act):
+    """The persistent ring forward (gemm_ring_nt.hip, tune key 12) against the 8-phase / 128x128
+    kernels it replaces (same k order: bitwise equal where the 8-phase kernel runs) and an fp32
+    oracle of the same bf16 inputs: activations, the bias column, zero padding, rows >= M untouched."""
+    from shifu_amd.ops import _native as nat
+    g = torch.Generator(device="cuda").manual_seed(M % 97)
+    A = (torch.randn(M + 64, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    B = (torch.randn(NB, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    outs = []
+    for ring in (0, 1):
+        C = torch.full((M + 64, N), 7.0, device="cuda", dtype=torch.bfloat16)
+        nat.call_hip("shifu_gemm_set_tune", 12, ring)
+        try:
+            nat.call_hip("shifu_gemm_nt", A, K, B, K, NB, C, N, None, 0, None, 0, None, 0,
+                         M, N, K, epi, act, nv, 1, 0.0, nat.stream_of(A))
+            torch.cuda.synchronize()
+        finally:
+            nat.call_hip("shifu_gemm_set_tune", 12, 0)
+        outs.append(C)
+    old, new = outs
+    assert torch.all(new[M:] == 7.0), "rows >= M written"
+    z = A[:M].float() @ B.float().t()
+    ref = {0: torch.sigmoid, 1: torch.tanh, 2: lambda v: v}[act](z)
+    assert (new[:M, :min(nv, NB)].float() - ref[:, :min(nv, NB)]).abs().max().item() < 2e-2
+    if epi == 0 and nv < N:
+        assert torch.all(new[:M, nv] == 1.0) and torch.all(new[:M, nv + 1:] == 0)
+    else:
+        assert torch.all(new[:M, NB:] == 0)
+    if K >= 512 and N >= 512:                         # the 8-phase kernel's shapes: identical bits
+        assert torch.equal(old.view(torch.int16), new.view(torch.int16))
+    else:
+        assert (old.float() - new.float()).abs().max().item() < 2e-2
+
+
 def test_bench_configuration_tracks_fp32_oracle():
     """The exact bench trainer configuration (bench.py: n_in 1000, hidden 500/200 sigmoid, RPROP,
     chunks >= 2^17 rows) so the 8-phase forward, the fused head, the ring wgrad (incl. the M % 32

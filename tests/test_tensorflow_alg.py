@@ -125,6 +125,8 @@ def test_mlp_engine_matches_autograd_oracle(opt, loss, act):
     for a, b in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-4, atol=2e-5)
     np.testing.assert_allclose([v for _, _, v in h1], [v for _, _, v in h2], rtol=1e-4)
+    # the per-epoch training error is the TF objective sum(w * loss) / count(w != 0) in both
+    np.testing.assert_allclose([t for _, t, _ in h1], [t for _, t, _ in h2], rtol=1e-4)
 
 
 @pytest.mark.gpu
@@ -146,5 +148,6 @@ def test_mlp_engine_tf_gpu_tracks_autograd():
     v1, v2 = [v for _, _, v in h1], [v for _, _, v in h2]
     assert v1[-1] < v1[0]
     np.testing.assert_allclose(v1, v2, rtol=0.05)
+    np.testing.assert_allclose([t for _, t, _ in h1], [t for _, t, _ in h2], rtol=0.05)
     for a, b in zip(m1.parameters(), m2.parameters()):
         assert float((a.detach() - b.detach()).abs().max()) < 0.05
