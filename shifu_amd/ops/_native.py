@@ -67,6 +67,7 @@ HIP_SIGNATURES = {
     "shifu_wgrad_ring_ws": ("iii", "l"),
     "shifu_ring_set_stamp": "p",
     "shifu_ring_nt_set_lab": "ip",
+    "shifu_ring_nt_set_variant": "i",
     "shifu_ring_set_mf": "i",
     "shifu_ring_set_dmamma": "i",
     # gbdt_kernels.hip

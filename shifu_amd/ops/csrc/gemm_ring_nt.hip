@@ -84,12 +84,13 @@ struct RingNTArgs {
   int ntiles;                  // ceil(M / 256) * ceil(N / 256)
   // LAB builds only (never the shipped kernel): ablation bits and per-wave segment cycle sums
   //   dbg 1: no epilogue (acc kept live, zeroed), 2: epilogue stores z (no activation),
-  //       4: no MFMAs (fragments kept live), 8: A rows from a 4096-row (L2-resident) window
+  //       4: no MFMAs (fragments kept live), 8: A rows from a 4096-row window (MALL), 16: from a
+  //       256-row window (every block re-reads the same 512 KB: L2-resident)
   int dbg;
   unsigned long long* stamps;  // [blocks][8 waves][8]: epilogue, reads, waits, LD barrier, MMA, MMA barrier, T, lb
 };
 
-template <int EPI, int ACT, bool LAB>
+template <int EPI, int ACT, bool LAB, int VAR>
 __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int G = gridDim.x;
@@ -100,7 +101,9 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
   const int T = ((p.ntiles - 1 - lb) / G + 1) * nk;  // flattened k-steps of this block
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
-  const bool lag = wid >= 4;
+  // the lag group: one barrier behind, so each SIMD pairs a computing wave with a reading one
+  // (VAR bit 3: odd waves instead of waves 4-7 -- lab check of the wave -> SIMD placement)
+  const bool lag = (VAR & 8) ? (wid & 1) != 0 : wid >= 4;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
 
   // ---- LDS-DMA cursor over the flattened (tile, k-step) sequence
@@ -108,16 +111,16 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
   const char* dA;
   const char* dB;
   uint32_t offA[2], offB[2];
-  auto dma_tile = [&](int t) {
+  auto dma_tile = [&](int t) __attribute__((always_inline)) {
     const int m0 = (t / ntn) * 256, n0 = (t % ntn) * 256;
-    const bool win = LAB && (p.dbg & 8);             // lab: rows (m0 + r) & 4095 from A's first rows
+    const bool win = LAB && (p.dbg & 24);            // lab: rows (m0 + r) & 4095 (8) / & 255 (16) of A
     dA = (const char*)(p.A + (size_t)(win ? 0 : m0) * p.lda);
     dB = (const char*)(p.B + (size_t)n0 * p.ldb);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int P = (i * 8 + wid) * 1024 + lane * 16;
       const int row = P >> 6, c = ((P >> 4) & 3) ^ rn_xor(row);
-      const int ra = win ? (min(m0 + row, p.M - 1) & 4095) : min(m0 + row, p.M - 1) - m0;
+      const int ra = win ? (min(m0 + row, p.M - 1) & ((p.dbg & 16) ? 255 : 4095)) : min(m0 + row, p.M - 1) - m0;
       const int rb = min(n0 + row, p.NB - 1) - n0;
       offA[i] = (uint32_t)(ra * p.lda + c * 8) * 2u;
       offB[i] = (uint32_t)(rb * p.ldb + c * 8) * 2u;
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
   };
   dma_tile(d_tile);
   // one of the 4 LDS-DMA instructions of a step (q = 0, 1: A halves; 2, 3: B halves); q == 3 advances
-  auto dma_piece = [&](int slot, int q) {
+  auto dma_piece = [&](int slot, int q) __attribute__((always_inline)) {
     char* base = smem + slot * RN_SLOT + wid_u * 1024 + (q >> 1) * RN_IMG + (q & 1) * 8192;
     const char* src = (q < 2 ? dA + offA[q & 1] : dB + offB[q & 1]) + d_k * 64;
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)base, 16, 0, 0);
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
       if (++d_k == nk) { d_k = 0; d_tile += G; dma_tile(d_tile); }
     }
   };
-  auto dma_step = [&](int slot) { dma_piece(slot, 0); dma_piece(slot, 1); dma_piece(slot, 2); dma_piece(slot, 3); };
+  auto dma_step = [&](int slot) __attribute__((always_inline)) { dma_piece(slot, 0); dma_piece(slot, 1); dma_piece(slot, 2); dma_piece(slot, 3); };
 
   f32x4 acc[4][8];                                   // [n block][m block]
 #pragma unroll
@@ -147,17 +150,29 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
   const uint32_t oA = (uint32_t)((wr * 128 + lr) * 64 + ((lq ^ rn_xor(lr)) << 4));
   const uint32_t oB = (uint32_t)(RN_IMG + (wc * 64 + lr) * 64 + ((lq ^ rn_xor(lr)) << 4));
   bf16x8 af[8], bfr[4];
+  constexpr int DMA_LD = (VAR & 3) == 1 ? 4 : (VAR & 3) == 2 ? 2 : 0;   // DMA pieces issued in the LD segment
+  constexpr bool DEFER = (VAR & 4) != 0;     // epilogue: pack everything, then 16 stores whose data
+                                             // registers stay untouched until the next MMA segment
 
-  // ---- epilogue of tile t from the accumulators (then zeroed)
-  auto epilogue_t = [&](int t, auto FULL, auto USE_ACT) {
+  // ---- epilogue of tile t: activation + bf16 pack + permlane16 widening into pk
+  uint32_t pk[2][8][4];
+  // rows >= M / columns >= N: offsets outside the tile's buffer resource (dropped by the hardware)
+  auto store_one_impl = [&](int t, int np, int mb) __attribute__((always_inline)) {
     const int m0 = (t / ntn) * 256, n0 = (t % ntn) * 256;
     const int rows = min(256, p.M - m0);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.C + (size_t)m0 * p.ldc), (short)0, rows * (int)p.ldc * 2, 0x00020000);
+    const int nl = wc * 64 + np * 32 + 16 * (lq & 1) + 8 * (lq >> 1);
+    const int ml = wr * 128 + mb * 16 + lr;
+    const int off = n0 + nl < p.N ? (int)((ml * p.ldc + n0 + nl) * 2) : (int)0x7ffffff0;
+    const v4i_t v = {(int)pk[np][mb][0], (int)pk[np][mb][1], (int)pk[np][mb][2], (int)pk[np][mb][3]};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+  };
+  (void)store_one_impl;
+  auto pack_tile = [&](int t, auto FULL, auto USE_ACT) __attribute__((always_inline)) {
+    const int n0 = (t % ntn) * 256;
 #pragma unroll
     for (int np = 0; np < 2; ++np) {
-      const int nl = wc * 64 + np * 32 + 16 * (lq & 1) + 8 * (lq >> 1);   // lane's 8 columns after the swap
-      const bool in_n = n0 + nl < p.N;
 #pragma unroll
       for (int mb = 0; mb < 8; ++mb) {
         uint32_t w[2][2];
@@ -187,30 +202,55 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
           w[0][d] = r2[0];
           w[1][d] = r2[1];
         }
-        const int ml = wr * 128 + mb * 16 + lr;
-        const int off = in_n ? (int)((ml * p.ldc + n0 + nl) * 2) : (int)0x7ffffff0;
-        const v4i_t v = {(int)w[0][0], (int)w[0][1], (int)w[1][0], (int)w[1][1]};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+        pk[np][mb][0] = w[0][0]; pk[np][mb][1] = w[0][1]; pk[np][mb][2] = w[1][0]; pk[np][mb][3] = w[1][1];
+        if constexpr (!DEFER) store_one_impl(t, np, mb);
       }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  auto epilogue = [&](int t) {
+  auto pack = [&](int t) __attribute__((always_inline)) {
     const int n0 = (t % ntn) * 256;
+    if (LAB && (p.dbg & 2)) { pack_tile(t, std::integral_constant<bool, true>{}, std::integral_constant<bool, false>{}); return; }
+    if (n0 + 256 <= (EPI == RN_EPI_ACT ? p.n_valid : p.NB))
+      pack_tile(t, std::integral_constant<bool, true>{}, std::integral_constant<bool, true>{});
+    else pack_tile(t, std::integral_constant<bool, false>{}, std::integral_constant<bool, true>{});
+  };
+  // the epilogue of tile t (16 stores per wave); !DEFER: acc zeroed here
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
     if (LAB && (p.dbg & 1)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { asm volatile("" :: "v"(acc[i][j])); acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f}; }
-      return;
+        for (int j = 0; j < 8; ++j) asm volatile("" :: "v"(acc[i][j]));
+#pragma unroll
+      for (int np = 0; np < 2; ++np)
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) pk[np][mb][d] = 0;
+    } else {
+      pack(t);
     }
-    if (LAB && (p.dbg & 2)) { epilogue_t(t, std::integral_constant<bool, true>{}, std::integral_constant<bool, false>{}); return; }
-    if (n0 + 256 <= (EPI == RN_EPI_ACT ? p.n_valid : p.NB))
-      epilogue_t(t, std::integral_constant<bool, true>{}, std::integral_constant<bool, true>{});
-    else epilogue_t(t, std::integral_constant<bool, false>{}, std::integral_constant<bool, true>{});
+    if constexpr (DEFER) {
+#pragma unroll
+      for (int np = 0; np < 2; ++np)
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb) store_one_impl(t, np, mb);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // keeps the stored registers live (unreused) until after the LD segment's barrier
+  auto keep_pk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int np = 0; np < 2; ++np)
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const v4i_t v = {(int)pk[np][mb][0], (int)pk[np][mb][1], (int)pk[np][mb][2], (int)pk[np][mb][3]};
+        asm volatile("" :: "v"(v));
+      }
   };
 
 #define RN_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
@@ -222,7 +262,7 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
   if (lag) RN_BAR();
 
   unsigned long long st_sum[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-  auto stamp = [&](int k) {
+  auto stamp = [&](int k) __attribute__((always_inline)) {
     if constexpr (LAB) {
       __builtin_amdgcn_sched_barrier(0);
       const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -231,33 +271,10 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  // the 32 MFMAs of a k-step (+ the DMA pieces of step t+4 not issued in the LD segment); ZC:
+  // first step of a tile under DEFER -- a zero accumulator input instead of zeroed registers
   int slot = 0, dslot = 4, kk = 0, tile = lb, since_epi = 0;
-  for (int t = 0; t < T; ++t) {
-    // ---- LD segment
-    stamp(-1);
-    if (kk == 0 && t > 0) {
-      __builtin_amdgcn_sched_barrier(0);
-      epilogue(tile - G);
-      since_epi = 3;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    stamp(0);
-    const uint32_t sa = lds0 + slot * RN_SLOT + oA, sb = lds0 + slot * RN_SLOT + oB;
-    rn_for<4>([&](auto I) { bfr[I.v] = rn_read<I.v * 1024>(sb); });
-    rn_for<8>([&](auto I) { af[I.v] = rn_read<I.v * 1024>(sa); });
-    stamp(1);
-    if (since_epi > 0) {
-      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      --since_epi;
-    } else {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    stamp(2);
-    RN_BAR();
-    stamp(3);
-    // ---- MMA segment
-    __builtin_amdgcn_s_setprio(1);
+  auto mma = [&](auto ZC) __attribute__((always_inline)) {
 #pragma unroll
     for (int mb = 0; mb < 8; ++mb) {
       if (LAB && (p.dbg & 4)) {
@@ -269,13 +286,66 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
       } else {
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb)
-          acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nb], af[mb], acc[nb][mb], 0, 0, 0);
+          acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              bfr[nb], af[mb], decltype(ZC)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[nb][mb], 0, 0, 0);
       }
-      if (mb & 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        dma_piece(dslot, mb >> 1);
-        __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DMA_LD < 4) {
+        if ((DMA_LD == 0 && (mb & 1)) || (DMA_LD == 2 && (mb == 3 || mb == 7))) {
+          __builtin_amdgcn_sched_barrier(0);
+          dma_piece(dslot, DMA_LD == 0 ? (mb >> 1) : (mb == 3 ? 2 : 3));
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
+    }
+  };
+  for (int t = 0; t < T; ++t) {
+    // ---- LD segment (opened by the previous tile's epilogue at a tile start)
+    stamp(-1);
+    if (kk == 0 && t > 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      epilogue(tile - G);
+      since_epi = 3;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    stamp(0);
+    if constexpr (DMA_LD > 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      dma_piece(dslot, 0);
+      dma_piece(dslot, 1);
+      if constexpr (DMA_LD == 4) { dma_piece(dslot, 2); dma_piece(dslot, 3); }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const uint32_t sa = lds0 + slot * RN_SLOT + oA, sb = lds0 + slot * RN_SLOT + oB;
+    rn_for<4>([&](auto I) { bfr[I.v] = rn_read<I.v * 1024>(sb); });
+    rn_for<8>([&](auto I) { af[I.v] = rn_read<I.v * 1024>(sa); });
+    stamp(1);
+    // own DMAs of step t+1 landed: younger are steps t+2, t+3 and the pieces of t+4 issued so far
+    // (+16 epilogue stores in the three LD segments after a tile end)
+    if (since_epi > 0) {
+      --since_epi;
+      if constexpr (DMA_LD == 4) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+      else if constexpr (DMA_LD == 2) asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    } else {
+      if constexpr (DMA_LD == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if constexpr (DMA_LD == 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stamp(2);
+    RN_BAR();
+    stamp(3);
+    // ---- MMA segment
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (DEFER) {
+      if (kk == 0) {
+        if (t > 0) keep_pk();
+        mma(std::integral_constant<bool, true>{});
+      } else {
+        mma(std::integral_constant<bool, false>{});
+      }
+    } else {
+      mma(std::integral_constant<bool, false>{});
     }
     __builtin_amdgcn_s_setprio(0);
     stamp(4);
@@ -294,7 +364,8 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
       unsigned long long* d = p.stamps + ((size_t)blockIdx.x * 8 + wid) * 8;
       for (int k = 0; k < 6; ++k) d[k] = st_sum[k];
       d[6] = T;
-      d[7] = lb;
+      // HW_ID: wave slot [3:0], SIMD [5:4], CU [11:8] (gfx9 layout)
+      d[7] = ((unsigned long long)lb << 32) | (unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
     }
   }
 }
@@ -303,12 +374,31 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
 
 static int g_rn_dbg = -1;                    // LAB build switch: >= 0 runs ring_nt_kernel<.., LAB>
 static unsigned long long* g_rn_stamps = nullptr;
+constexpr int RN_DEFAULT_VAR = 0;            // DMA pieces in the MMA segment, per-pair stores
+static int g_rn_var = RN_DEFAULT_VAR;        // sigmoid / store builds: schedule variant (lab A/B)
 // Lab switch (tools/ring_lab.py): dbg >= 0 selects the LAB build (sigmoid / store only) with
 // those ablation bits; buf (>= blocks * 64 u64, nullable) receives the segment cycle sums.
 SHIFU_API int shifu_ring_nt_set_lab(int dbg, void* buf) {
   g_rn_dbg = dbg;
   g_rn_stamps = (unsigned long long*)buf;
   return 0;
+}
+// variant bits: 0-1 DMA placement (0: all 4 pieces in the MMA segment, 1: all in the LD segment,
+// 2: two each), 2: deferred epilogue (pack all, 16 stores, registers untouched until the next MMA)
+SHIFU_API int shifu_ring_nt_set_variant(int v) {
+  if (v < 0 || (v & 4) || (v & 3) == 3 || v > 9) return -1;   // deferred-epilogue builds (bit 2) spill
+  g_rn_var = v;
+  return 0;
+}
+
+template <int EPI, int ACT, bool LAB>
+static void rn_launch(int var, dim3 grid, hipStream_t stream, const RingNTArgs& p) {
+#define RN_V(V) hipLaunchKernelGGL((ring_nt_kernel<EPI, ACT, LAB, V>), grid, dim3(RN_T), RN_LDS, stream, p)
+  switch (var) {
+    case 1: RN_V(1); break; case 2: RN_V(2); break; case 8: RN_V(8); break; case 9: RN_V(9); break;
+    default: RN_V(0); break;
+  }
+#undef RN_V
 }
 
 // C ABI: returns -1 when the shape is not one this engine takes (the caller falls back).
@@ -330,27 +420,24 @@ SHIFU_API int shifu_ring_nt(const void* A, long lda, const void* B, long ldb, in
   if (grid_cap > 0 && grid > grid_cap) grid = grid_cap;
   RingNTArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, M, N, K, NB, n_valid, bias_col,
                (int)ntiles, g_rn_dbg, g_rn_stamps};
+  const dim3 g(grid);
   if (g_rn_dbg >= 0) {
-    if (epi == RN_EPI_ACT && act == 0)
-      hipLaunchKernelGGL((ring_nt_kernel<RN_EPI_ACT, 0, true>), dim3(grid), dim3(RN_T), RN_LDS, stream, p);
-    else if (epi == RN_EPI_STORE)
-      hipLaunchKernelGGL((ring_nt_kernel<RN_EPI_STORE, 2, true>), dim3(grid), dim3(RN_T), RN_LDS, stream, p);
-    else
-      return -1;
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
-  }
-#define RN_L(E, A_) hipLaunchKernelGGL((ring_nt_kernel<E, A_, false>), dim3(grid), dim3(RN_T), RN_LDS, stream, p)
-  if (epi == RN_EPI_ACT) {
-    switch (act) {
-      case 0: RN_L(RN_EPI_ACT, 0); break; case 1: RN_L(RN_EPI_ACT, 1); break; case 2: RN_L(RN_EPI_ACT, 2); break;
-      case 3: RN_L(RN_EPI_ACT, 3); break; case 4: RN_L(RN_EPI_ACT, 4); break; case 6: RN_L(RN_EPI_ACT, 6); break;
-      case 9: RN_L(RN_EPI_ACT, 9); break; default: RN_L(RN_EPI_ACT, 7); break;
-    }
+    if (epi == RN_EPI_ACT && act == 0) rn_launch<RN_EPI_ACT, 0, true>(g_rn_var, g, stream, p);
+    else if (epi == RN_EPI_STORE) rn_launch<RN_EPI_STORE, 2, true>(g_rn_var, g, stream, p);
+    else return -1;
+  } else if (epi == RN_EPI_STORE) {
+    rn_launch<RN_EPI_STORE, 2, false>(g_rn_var, g, stream, p);
+  } else if (act == 0) {
+    rn_launch<RN_EPI_ACT, 0, false>(g_rn_var, g, stream, p);
   } else {
-    RN_L(RN_EPI_STORE, 2);
-  }
+#define RN_L(A_) hipLaunchKernelGGL((ring_nt_kernel<RN_EPI_ACT, A_, false, RN_DEFAULT_VAR>), g, dim3(RN_T), RN_LDS, \
+                                    stream, p)
+    switch (act) {
+      case 1: RN_L(1); break; case 2: RN_L(2); break; case 3: RN_L(3); break; case 4: RN_L(4); break;
+      case 6: RN_L(6); break; case 9: RN_L(9); break; default: RN_L(7); break;
+    }
 #undef RN_L
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--dbg", type=int, nargs="*", default=[1, 2, 4, 8, 5])
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--variants", type=int, nargs="*", default=[0, 1, 2],
+                    help="schedule variants (shifu_ring_nt_set_variant) timed in production and LAB builds")
+    ap.add_argument("--no-lab", action="store_true", help="production builds only (PMC runs), no stamps")
     a = ap.parse_args()
     import torch
     from shifu_amd.ops import _native as nat
@@ -54,26 +57,37 @@ def main():
         return ts[len(ts) // 2], ts[0]
 
     flop = 2.0 * M * K * a.nv
-    variants = [("8phase", 0, -1), ("ring", 1, -1), ("ring_lab_dbg0", 1, 0)] + \
-               [(f"ring_lab_dbg{d}", 1, d) for d in a.dbg]
+    variants = [("8phase", 0, -1, 0)]
+    for v in a.variants:
+        variants += [(f"ring_v{v}", 1, -1, v)]
+        if not a.no_lab:
+            variants += [(f"ring_v{v}_lab_dbg0", 1, 0, v)] + [(f"ring_v{v}_lab_dbg{d}", 1, d, v) for d in a.dbg]
     for rnd in range(a.rounds):
-        for name, ring, dbg in variants:
+        for name, ring, dbg, var in variants:
             nat.call_hip("shifu_gemm_set_tune", 12, ring)
+            nat.call_hip("shifu_ring_nt_set_variant", var)
             nat.call_hip("shifu_ring_nt_set_lab", dbg, None)
             med, mn = timed()
             print(json.dumps({"variant": name, "round": rnd, "ms_median": round(med, 4), "ms_min": round(mn, 4),
                               "tflops_median": round(flop / med / 1e9, 1), "M": M, "K": K, "N": N}), flush=True)
-    # stamps of the LAB build (dbg 0): per wave group, mean cycles per segment
+    for var in ([] if a.no_lab else a.variants):
+        stamp_run(a, nat, torch, dev, launch, var)
+
+
+def stamp_run(a, nat, torch, dev, launch, var):
+    """Stamps of the LAB build (dbg 0): per wave group, mean cycles per segment and k-step."""
     nat.call_hip("shifu_gemm_set_tune", 12, 1)
+    nat.call_hip("shifu_ring_nt_set_variant", var)
     stamps = torch.zeros(256 * 8 * 8, dtype=torch.int64, device=dev)
     nat.call_hip("shifu_ring_nt_set_lab", 0, stamps)
     launch()
     torch.cuda.synchronize()
     nat.call_hip("shifu_ring_nt_set_lab", -1, None)
+    nat.call_hip("shifu_ring_nt_set_variant", 0)
     nat.call_hip("shifu_gemm_set_tune", 12, 0)
     s = stamps.view(-1, 8, 8).double().cpu()
     s = s[s[:, 0, 6] > 0]
-    out = {"variant": "stamps_dbg0", "blocks": int(s.shape[0])}
+    out = {"variant": f"stamps_v{var}_dbg0", "blocks": int(s.shape[0])}
     for grp, sl in (("lead", slice(0, 4)), ("lag", slice(4, 8))):
         seg = s[:, sl, :6].mean(dim=(0, 1))
         tot = float(seg.sum())
@@ -81,6 +95,9 @@ def main():
         out[grp] = {k: round(float(v) / steps, 1) for k, v in zip(SEGS, seg)}
         out[grp]["cycles_per_step"] = round(tot / steps, 1)
         out[grp]["share"] = {k: round(float(v) / tot, 3) for k, v in zip(SEGS, seg)}
+    hw = s[:, :, 7].long() & 0xffffffff
+    out["simd_of_wave"] = [sorted(set(((hw[:, w] >> 4) & 3).tolist())) for w in range(8)]
+    out["waves_per_simd_blk0"] = [int(((hw[0] >> 4) & 3).eq(k).sum()) for k in range(4)]
     print(json.dumps(out), flush=True)
 
 
