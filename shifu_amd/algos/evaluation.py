@@ -221,39 +221,6 @@ def multiclass_confusion(pred: np.ndarray, truth: np.ndarray, n_classes: int, we
     return m
 
 
-def write_gain_chart(path_html: str, path_csv: str, perf: dict, title: str = "Eval"):
-    """Gain / ROC / PR charts (``GainChart`` J/core/eval/GainChart.java:484,814,1205): a self-
-    contained HTML page with inline SVG curves plus the bucket table, and the CSV of the gains."""
-    rows = perf["gains"]
-    with open(path_csv, "w", newline="") as f:
-        wr = csv.writer(f)
-        wr.writerow(["ActionRate", "WeightedActionRate", "Recall", "WeightedRecall", "Precision",
-                     "WeightedPrecision", "FPR", "WeightedFPR", "BinLowestScore"])
-        for po in rows:
-            wr.writerow([po["actionRate"], po["weightedActionRate"], po["recall"], po["weightedRecall"],
-                         po["precision"], po["weightedPrecision"], po["fpr"], po["weightedFpr"],
-                         po["binLowestScore"]])
-
-    def svg(points, xk, yk, label):
-        pts = [(p[xk], p[yk]) for p in points if not (math.isnan(p[xk]) or math.isnan(p[yk]))]
-        path = " ".join(f"{40 + 300 * x:.1f},{330 - 300 * y:.1f}" for x, y in pts)
-        return (f'<svg width="360" height="360"><rect x="40" y="30" width="300" height="300" fill="none" '
-                f'stroke="#999"/><polyline fill="none" stroke="#1f77b4" stroke-width="2" points="{path}"/>'
-                f'<text x="120" y="20">{label}</text></svg>')
-    table = "".join("<tr>" + "".join(f"<td>{po[k]:.4f}</td>" if isinstance(po[k], float) else f"<td>{po[k]}</td>"
-                                     for k in ("actionRate", "recall", "precision", "fpr", "binLowestScore")) + "</tr>"
-                    for po in rows)
-    html = (f"<html><head><title>{title}</title></head><body><h2>{title}</h2>"
-            f"<p>AUC(ROC)={perf['areaUnderRoc']:.6f} AUC(PR)={perf['areaUnderPr']:.6f}</p>"
-            + svg(perf["gains"], "actionRate", "recall", "Gain (recall vs action rate)")
-            + svg(perf["roc"], "fpr", "recall", "ROC")
-            + svg(perf["pr"], "recall", "precision", "Precision-Recall")
-            + "<table border=1><tr><th>ActionRate</th><th>Recall</th><th>Precision</th><th>FPR</th>"
-              "<th>BinLowestScore</th></tr>" + table + "</table></body></html>")
-    with open(path_html, "w") as f:
-        f.write(html)
-
-
 def to_json(obj) -> str:
     def clean(v):
         if isinstance(v, float) and (math.isnan(v) or math.isinf(v)):

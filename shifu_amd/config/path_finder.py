@@ -194,9 +194,6 @@ class PathFinder:
     def eval_meta_score(self, ev):
         return os.path.join(self.eval_dir(ev.get("name")), "EvalMetaScore")
 
-    def eval_gain_chart(self, ev, kind="gainchart", ext="html"):
-        return os.path.join(self.eval_dir(ev.get("name")), f"{ev.get('name')}_{kind}.{ext}")
-
     def eval_models_dir(self, ev):
         return self._custom("modelsPath", ev) or self.models_dir
 

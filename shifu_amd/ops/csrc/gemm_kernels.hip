@@ -1212,7 +1212,8 @@ static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
 static int g_fwd_persist = 1;     // persistent 8-phase forward (tune key 10; 0 = one tile per block)
 static int g_head_persist = 0;    // persistent fused head (tune key 11 / SHIFU_HEAD_PERSIST=1; measured
                                   // 1.13 vs 1.10 ms per 2M-row chunk: off by default, profiles/r4)
-static int g_ring_nt = 0;         // persistent ring forward (gemm_ring_nt.hip, tune key 12)
+static int g_ring_nt = 1;         // persistent ring forward (gemm_ring_nt.hip, tune key 12; 2.2 vs 2.3-2.5 ms
+                                  // for the 8-phase per-tile kernel per 2M-row chunk, profiles/r5)
 static int g_ring_nt_cap = 0;     // lab: grid cap of the ring forward (tune key 13; 0 = one block per CU)
 // gemm_ring_nt.hip (same library): -1 when the shape is not one it takes
 extern "C" int shifu_ring_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc, int M,

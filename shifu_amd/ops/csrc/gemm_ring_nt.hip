@@ -85,7 +85,8 @@ struct RingNTArgs {
   // LAB builds only (never the shipped kernel): ablation bits and per-wave segment cycle sums
   //   dbg 1: no epilogue (acc kept live, zeroed), 2: epilogue stores z (no activation),
   //       4: no MFMAs (fragments kept live), 8: A rows from a 4096-row window (MALL), 16: from a
-  //       256-row window (every block re-reads the same 512 KB: L2-resident)
+  //       256-row window (every block re-reads the same 512 KB: L2-resident), 32: every MFMA
+  //       issued twice (wrong sums; the marginal cost of the MMA segment's MFMAs)
   int dbg;
   unsigned long long* stamps;  // [blocks][8 waves][8]: epilogue, reads, waits, LD barrier, MMA, MMA barrier, T, lb
 };
@@ -288,6 +289,11 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
         for (int nb = 0; nb < 4; ++nb)
           acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               bfr[nb], af[mb], decltype(ZC)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[nb][mb], 0, 0, 0);
+        if (LAB && (p.dbg & 32)) {                   // lab: every MFMA twice (marginal MFMA cost)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nb], af[mb], acc[nb][mb], 0, 0, 0);
+        }
       }
       if constexpr (DMA_LD < 4) {
         if ((DMA_LD == 0 && (mb & 1)) || (DMA_LD == 2 && (mb == 3 || mb == 7))) {

@@ -561,11 +561,11 @@ def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None, lab=N
     if writer:
         with open(ms.pf.eval_performance(ev), "w") as f:
             f.write(E.to_json(perf))
-        E.write_gain_chart(ms.pf.eval_gain_chart(ev, "gainchart", "html"),
-                           ms.pf.eval_gain_chart(ev, "gainchart", "csv"), perf, ev.get("name"))
         _log.info("eval %s: AUC(ROC)=%.6f AUC(PR)=%.6f weighted AUC=%.6f", ev.get("name"), perf["areaUnderRoc"],
                   perf["areaUnderPr"], perf["weightedAreaUnderRoc"])
-    # champion / meta score columns
+    # champion / meta score columns (EvalModelProcessor.runDistEval :911-935): each column's
+    # performance goes to EvalMetaScore/<column>EvalPerformance.json
+    champions = []
     for m in score_meta:
         if m in md.table:
             sv = md.table[m].numeric()[valid]
@@ -575,9 +575,20 @@ def perf_eval(ms: ModelSet, ev, md, res, tags, score_meta=(), device=None, lab=N
                 mx = dist.all_reduce_max_scalar(mx)
             p2 = perf_fn(sv[okm], is_pos[okm], None if w is None else w[okm], nb,
                          max_score=mx if math.isfinite(mx) else 1.0, device=device)
+            champions.append((m, p2))
             if writer:
-                with open(os.path.join(d, f"{m}.EvalPerformance.json"), "w") as f:
+                md_dir = os.path.join(d, "EvalMetaScore")
+                os.makedirs(md_dir, exist_ok=True)
+                with open(os.path.join(md_dir, f"{m}EvalPerformance.json"), "w") as f:
                     f.write(E.to_json(p2))
+    if writer:
+        # gain / PR / ROC pages and the per-series CSVs (ConfusionMatrix.java:543-596 without
+        # champion columns, EvalModelProcessor.java:937-1001 with them)
+        from ..algos.eval_reports import write_eval_reports
+        evn = ev.get("name")
+        model_name = mc.basic.get("name") or "model"
+        series = ([(evn, perf)] if not champions else [(f"{model_name}-{evn}", perf)] + champions)
+        write_eval_reports(d, evn, model_name, series, bool(ev.dataSet.get("weightColumnName")))
     return perf
 
 

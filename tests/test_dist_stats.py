@@ -158,7 +158,7 @@ def _guarded_pipeline(tmp_path, gpu):
     for verb in ("stats", "norm", "varsel", "train", "posttrain", "eval"):
         mp.start_processes(_rank_cli_guarded, args=(2, _port(), root, verb, gpu), nprocs=2, join=True,
                            start_method="spawn")
-    assert os.path.exists(os.path.join(root, "evals", "Eval1", "id.EvalPerformance.json"))
+    assert os.path.exists(os.path.join(root, "evals", "Eval1", "EvalMetaScore", "idEvalPerformance.json"))
     return root
 
 

@@ -159,6 +159,7 @@ def test_persistent_forward_bitwise_equals_per_tile():
     A = (torch.randn(M, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
     B = (torch.randn(N, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
     outs = []
+    nat.call_hip("shifu_gemm_set_tune", 12, 0)              # the 8-phase kernels, not the ring forward
     for persist in (0, 1):
         C = torch.full((M, N), 7.0, device="cuda", dtype=torch.bfloat16)
         nat.call_hip("shifu_gemm_set_tune", 10, persist)
@@ -168,6 +169,8 @@ def test_persistent_forward_bitwise_equals_per_tile():
             torch.cuda.synchronize()
         finally:
             nat.call_hip("shifu_gemm_set_tune", 10, 1)
+            if persist == 1:
+                nat.call_hip("shifu_gemm_set_tune", 12, 1)
         outs.append(C)
     assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
     ref = torch.sigmoid(A[-300:].float() @ B[:500].float().t())
@@ -197,7 +200,7 @@ def test_ring_forward_matches_8phase_and_oracle(M, K, N, NB, nv, epi, act):
                          M, N, K, epi, act, nv, 1, 0.0, nat.stream_of(A))
             torch.cuda.synchronize()
         finally:
-            nat.call_hip("shifu_gemm_set_tune", 12, 0)
+            nat.call_hip("shifu_gemm_set_tune", 12, 1)       # the default
         outs.append(C)
     old, new = outs
     assert torch.all(new[M:] == 7.0), "rows >= M written"

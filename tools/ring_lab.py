@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", type=int, nargs="*", default=[0, 1, 2],
                     help="schedule variants (shifu_ring_nt_set_variant) timed in production and LAB builds")
+    ap.add_argument("--stamp-dbg", type=int, nargs="*", default=[], help="extra LAB ablation bits for stamp runs")
     ap.add_argument("--no-lab", action="store_true", help="production builds only (PMC runs), no stamps")
     a = ap.parse_args()
     import torch
@@ -71,15 +72,16 @@ def main():
             print(json.dumps({"variant": name, "round": rnd, "ms_median": round(med, 4), "ms_min": round(mn, 4),
                               "tflops_median": round(flop / med / 1e9, 1), "M": M, "K": K, "N": N}), flush=True)
     for var in ([] if a.no_lab else a.variants):
-        stamp_run(a, nat, torch, dev, launch, var)
+        for dbg in [0] + a.stamp_dbg:
+            stamp_run(a, nat, torch, dev, launch, var, dbg)
 
 
-def stamp_run(a, nat, torch, dev, launch, var):
+def stamp_run(a, nat, torch, dev, launch, var, dbg=0):
     """Stamps of the LAB build (dbg 0): per wave group, mean cycles per segment and k-step."""
     nat.call_hip("shifu_gemm_set_tune", 12, 1)
     nat.call_hip("shifu_ring_nt_set_variant", var)
     stamps = torch.zeros(256 * 8 * 8, dtype=torch.int64, device=dev)
-    nat.call_hip("shifu_ring_nt_set_lab", 0, stamps)
+    nat.call_hip("shifu_ring_nt_set_lab", dbg, stamps)
     launch()
     torch.cuda.synchronize()
     nat.call_hip("shifu_ring_nt_set_lab", -1, None)
@@ -87,7 +89,7 @@ def stamp_run(a, nat, torch, dev, launch, var):
     nat.call_hip("shifu_gemm_set_tune", 12, 0)
     s = stamps.view(-1, 8, 8).double().cpu()
     s = s[s[:, 0, 6] > 0]
-    out = {"variant": f"stamps_v{var}_dbg0", "blocks": int(s.shape[0])}
+    out = {"variant": f"stamps_v{var}_dbg{dbg}", "blocks": int(s.shape[0])}
     for grp, sl in (("lead", slice(0, 4)), ("lag", slice(4, 8))):
         seg = s[:, sl, :6].mean(dim=(0, 1))
         tot = float(seg.sum())
