@@ -116,13 +116,13 @@ __global__ __launch_bounds__(RN_T, 2) void ring_nt_kernel(RingNTArgs p) {
     const int m0 = (t / ntn) * 256, n0 = (t % ntn) * 256;
     const bool win = LAB && (p.dbg & 24);            // lab: rows (m0 + r) & 4095 (8) / & 255 (16) of A
     dA = (const char*)(p.A + (size_t)(win ? 0 : m0) * p.lda);
-    dB = (const char*)(p.B + (size_t)n0 * p.ldb);
+    dB = (const char*)p.B;                           // absolute rows: a column tile may start at n0 >= NB
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int P = (i * 8 + wid) * 1024 + lane * 16;
       const int row = P >> 6, c = ((P >> 4) & 3) ^ rn_xor(row);
       const int ra = win ? (min(m0 + row, p.M - 1) & ((p.dbg & 16) ? 255 : 4095)) : min(m0 + row, p.M - 1) - m0;
-      const int rb = min(n0 + row, p.NB - 1) - n0;
+      const int rb = min(n0 + row, p.NB - 1);      // rows >= NB read row NB-1 (columns overwritten)
       offA[i] = (uint32_t)(ra * p.lda + c * 8) * 2u;
       offB[i] = (uint32_t)(rb * p.ldb + c * 8) * 2u;
     }
@@ -417,6 +417,7 @@ SHIFU_API int shifu_ring_nt(const void* A, long lda, const void* B, long ldb, in
   if (epi == RN_EPI_ACT && !act_deriv_from_output(act)) return -1;
   if ((long)K * 2 * 256 >= (1l << 31) || 256l * ldc * 2 >= (1l << 31)) return -1;   // 32-bit offsets
   if (lda < K || ldb < K || ldc < N) return -1;
+  if ((long)NB * ldb * 2 >= (1l << 32)) return -1;                                     // B offsets are 32-bit
   const long ntiles = (long)((M + 255) / 256) * ((N + 255) / 256);
   if (ntiles >= (1l << 31)) return -1;
   int dev = 0, ncu = 256;

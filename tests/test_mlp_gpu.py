@@ -182,6 +182,7 @@ def test_persistent_forward_bitwise_equals_per_tile():
     ((1 << 20) + 77, 1024, 512, 500, 500, 0, 0),       # the bench's first layer (sigmoid + bias column)
     (70000 + 33, 256, 512, 512, 512, 0, 1),           # K = 8 steps per tile, tanh, no partial columns
     (65536 + 300, 128, 264, 260, 260, 2, 2),          # store z, partial last column tile (N % 256 != 0)
+    (65536, 384, 384, 256, 256, 0, 0),                # a column tile entirely past the weight rows (n0 >= NB)
 ])
 def test_ring_forward_matches_8phase_and_oracle(M, K, N, NB, nv, epi, act):
     """The persistent ring forward (gemm_ring_nt.hip, tune key 12) against the 8-phase / 128x128
