@@ -43,6 +43,10 @@ IMPURITY_IDS = {"variance": 0, "friedmanmse": 1, "entropy": 2, "gini": 3}
 LOSS_IDS = {"squared": 0, "halfgradsquared": 1, "absolute": 2, "log": 3}
 
 
+# histogram work items per level (node x row-range x 32-feature group); SHIFU_GBDT_ITEMS: lab A/B
+TARGET_ITEMS = int(os.environ.get("SHIFU_GBDT_ITEMS", "2048"))
+
+
 def _strategy_count(strategy, n_feat: int, input_num: int, tree_num: int) -> int:
     """Number of features a node samples (DTMaster.getSubsamplingFeatures); 0 = all."""
     if strategy is None:
@@ -541,7 +545,7 @@ class TreeTrainer:
         """Work items [n, 4] = (node_slot, lo, hi, group) for the built nodes, chunked for
         parallelism, and node_items [n_nodes, n_groups, max_items] (item ids, -1 padded).
         Vectorized per node (numpy), order: node, group, chunk."""
-        target_items = 2048
+        target_items = TARGET_ITEMS
         G = self.ngroups
         rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
         per = self.items_per_node_group

@@ -746,10 +746,18 @@ SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, int rec, const int* pos
     return -1;
   HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, wg_by_pos, rec, items, (long long*)slab, n_items, n_feat,
              (float)scale_w, (float)(mode == 2 ? scale_g / (1 << GSH32) : scale_g), nmod};
-  static const int pf = [] { const char* e = getenv("SHIFU_HIST_PF"); return e ? atoi(e) : 1; }();
+  // SHIFU_HIST_PF: 3 (default) prefetching kernel, 1 row per thread and pass (2.9-3.07 TB/s of codes
+  // below the root vs 2.3-2.5 with 2 rows: profiles/r5/gbdt_variants_r5k.txt); 1: 2 rows; 4: 4 rows;
+  // 0: the non-prefetching kernel (lab A/B switch)
+  static const int pf = [] { const char* e = getenv("SHIFU_HIST_PF"); return e ? atoi(e) : 3; }();
   const size_t lds = 2 * NB * 16 * 8;      // the u32 modes still use 64 KiB for the transposed store
-  if (mode == 1) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 1>), dim3(n_items), dim3(HT), lds, stream, a);
+  static const int root_hu = [] { const char* e = getenv("SHIFU_HIST_ROOT_HU"); return e ? atoi(e) : 2; }();
+  if (mode == 1 && root_hu == 1) hipLaunchKernelGGL((gbdt_hist_kernel<true, 1, 1>), dim3(n_items), dim3(HT), lds, stream, a);
+  else if (mode == 1) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 1>), dim3(n_items), dim3(HT), lds, stream, a);
+  else if (mode == 2 && root_hu == 1) hipLaunchKernelGGL((gbdt_hist_kernel<true, 1, 2>), dim3(n_items), dim3(HT), lds, stream, a);
   else if (mode == 2) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 2>), dim3(n_items), dim3(HT), lds, stream, a);
+  else if (pf == 4) hipLaunchKernelGGL((gbdt_hist_kernel<true, 4, 0>), dim3(n_items), dim3(HT), lds, stream, a);
+  else if (pf == 3) hipLaunchKernelGGL((gbdt_hist_kernel<true, 1, 0>), dim3(n_items), dim3(HT), lds, stream, a);
   else if (pf) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 0>), dim3(n_items), dim3(HT), lds, stream, a);
   else hipLaunchKernelGGL((gbdt_hist_kernel<false, 4, 0>), dim3(n_items), dim3(HT), lds, stream, a);
   CHECK_HIP(hipGetLastError());
@@ -784,6 +792,8 @@ SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const void* b
              (const uint8_t*)is_cat, (unsigned long long*)fbits, wcnt, n, nmod, pred, node_val, child_l_val,
              child_r_val, scale,
              final_level};
+  // (a 4-positions-per-thread variant measured the same, 126.9 vs 127.9 ms per balanced round: the
+  // pass is bound by the split-feature gather's line traffic, not by load parallelism; r5l)
   hipLaunchKernelGGL(gbdt_partition_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
