@@ -124,6 +124,18 @@ RT_SIGNATURES = {
     "shifu_gen_strong_cols": ("iip", "i"),
     "shifu_parse_fields": ("ppLp", "l"),
     "shifu_gather_fields": ("pplipPpl", "l"),
+    # autotype_scan.cpp (init -autotype)
+    "shifu_at_new": ("iiPPP", "p"),
+    "shifu_at_feed": ("pplpi", "l"),
+    "shifu_at_counts": ("pp", "l"),
+    "shifu_at_exact": ("pipl", "l"),
+    "shifu_at_hll_p": ("", "i"),
+    "shifu_at_exact_cap": ("", "i"),
+    "shifu_at_hll": ("pp", "i"),
+    "shifu_at_hll_estimate": ("p", "d"),
+    "shifu_at_items": ("pipl", "l"),
+    "shifu_at_skipped": ("p", "l"),
+    "shifu_at_free": ("p", None),
 }
 
 

@@ -4,11 +4,8 @@
   folder, default ModelConfig.json for the algorithm, ``.HEAD``, empty column-name files.
 * init: ``InitModelProcessor.initColumnConfigList`` (J/core/processor/InitModelProcessor.java:424-502)
   — one ColumnConfig per header field (or per index without a header), flags from the column
-  files; optional auto-type (:289-376 + :143-254): distinct count (exact, on the parsed
-  dictionary instead of HyperLogLog), valid-number ratio > autoTypeThreshold% -> numeric,
-  0/1 columns -> numeric.  (The reference's ``isDoubleFrequentVariable`` only rejects blank
-  sampled items, which makes its threshold branch a no-op; we implement the documented
-  ratio rule.)
+  files; optional auto-type (:105-120, 143-254 + the AutoTypeDistinctCount MapReduce job): one
+  data-parallel streamed pass (algos/autotype.py), see ``auto_type_columns``.
 """
 from __future__ import annotations
 
@@ -19,7 +16,7 @@ import numpy as np
 from ..config.column_config import ColumnConfig, save_column_configs
 from ..config.model_config import create_init_model_config
 from ..config.updater import update_column_flags
-from ..data.reader import first_line_is_header, list_data_files, read_header, read_table
+from ..data.reader import list_data_files, read_header
 from ..utils.log import get_logger
 from .base import ModelSet
 
@@ -98,7 +95,30 @@ def init_column_configs(ms: ModelSet, auto_type: bool | None = None):
     return ccs
 
 
+def _is_binary(distinct: int, items: list) -> bool:
+    """``InitModelProcessor.isBinaryVariable`` (:229-246): two distinct values, both 0 or 1."""
+    if distinct != 2 or len(items) > 2:
+        return False
+    for s in items:
+        try:
+            if float(s) not in (0.0, 1.0):
+                return False
+        except ValueError:
+            return False
+    return True
+
+
 def auto_type_columns(ms: ModelSet, header=None, max_rows: int | None = None):
+    """Distinct counts (+ the column type when autoTypeThreshold > 0) from one data-parallel pass
+    over the training data (algos/autotype.py: every rank streams its byte ranges; counts,
+    hash sets / HyperLogLog registers and frequent items merged over the ranks).  Type rule: a
+    0/1 column is numeric (isBinaryVariable); otherwise numeric when more than autoTypeThreshold %
+    of the non-missing values parse as doubles.  (The reference's isDoubleFrequentVariable
+    (:248-259) only rejects whitespace-only sampled items, which makes its branch a no-op for every
+    column without such an item; the ratio rule here is the documented intent, the counts it uses
+    are the reference mapper's.)  Columns listed in categorical.column.names stay categorical."""
+    from ..algos import autotype
+    from ..parallel import dist
     mc = ms.mc
     ds = mc.dataSet
     data_path = mc.resolve(ds.get("dataPath"))
@@ -106,32 +126,20 @@ def auto_type_columns(ms: ModelSet, header=None, max_rows: int | None = None):
     hpath = ds.get("headerPath")
     header = header or read_header(mc.resolve(hpath) if hpath else None, ds.get("headerDelimiter") or "|",
                                    data_path, delim)
-    skip = (not hpath) and first_line_is_header(data_path, header, delim)
-    todo = [c for c in ms.ccs if not c.is_target() and not c.is_meta() and not c.is_weight()]
-    t = read_table(data_path, header, delim, strings=[header[c.num] for c in todo],
-                   missing=mc.missing_values, skip_header_line=skip, max_rows=max_rows)
+    todo = [c for c in ms.ccs if not c.is_target() and not c.is_meta() and not c.is_weight() and c.num < len(header)]
+    info = dist.info()
+    st = autotype.scan(mc, header, [c.num for c in todo], info.rank, info.world_size)
     thr = float(ds.get("autoTypeThreshold", 0) or 0)
+    user_cat = set(mc.categorical_column_names())
     n_cat = 0
     for c in todo:
-        col = t[header[c.num]]
-        d = col.dictionary
-        counts = np.bincount(col.values[col.values >= 0], minlength=len(d)) if len(d) else np.zeros(0, np.int64)
-        c.stats["distinctCount"] = int(len(d))
-        if thr <= 0 or c.is_categorical() and c.name in set(mc.categorical_column_names()):
+        s = st[c.num]
+        c.stats["distinctCount"] = int(s.distinct)
+        if thr <= 0 or (c.is_categorical() and c.name in user_cat):
             continue
-        valid = 0
-        nums = []
-        for s, k in zip(d, counts):
-            try:
-                nums.append(float(s))
-                valid += int(k)
-            except ValueError:
-                pass
-        nonmiss = int(counts.sum())
-        ratio = valid / nonmiss if nonmiss else 1.0
-        if len(d) == 2 and set(nums) <= {0.0, 1.0} and len(nums) == 2:
-            c.type = "N"
-        elif ratio > thr / 100.0:
+        nonmiss = s.count - s.invalid
+        ratio = s.validnum / nonmiss if nonmiss else 1.0
+        if _is_binary(s.distinct, s.items) or ratio > thr / 100.0:
             c.type = "N"
         else:
             c.type = "C"
@@ -146,10 +154,14 @@ def run_new(name: str, alg: str = "NN", description: str | None = None, parent: 
 
 
 def run_init(root: str = ".", auto_type: bool | None = None) -> int:
+    """Every rank builds the ColumnConfig (the auto-type pass is data parallel); rank 0 writes it."""
+    from ..parallel import dist
     ms = ModelSet(root).setup("INIT", update_flags=False)
     init_column_configs(ms, auto_type)
-    save_column_configs(ms.ccs, ms.pf.column_config)
-    _log.info("init: %d columns -> %s", len(ms.ccs), ms.pf.column_config)
+    if dist.info().rank == 0:
+        save_column_configs(ms.ccs, ms.pf.column_config)
+        _log.info("init: %d columns -> %s", len(ms.ccs), ms.pf.column_config)
+    dist.barrier()
     return 0
 
 
