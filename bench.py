@@ -778,6 +778,30 @@ def bench_pipeline(a, dev, info):
     from shifu_amd.steps.varsel import PHASES as SE_PHASES
     step("train", lambda: api.TrainStep(root).process())
     step("eval", lambda: api.EvalStep(root).process())
+    # --pipeline-extra: steps timed after the pipeline, outside its total (scale checks of the
+    # data-parallel init -autotype scan and the combo score join, data/join.py)
+    extra = {}
+    for x in [e.strip() for e in (a.pipeline_extra or "").split(",") if e.strip()]:
+        if x == "autotype":
+            def _scan():
+                from shifu_amd.algos import autotype
+                from shifu_amd.config.model_config import ModelConfig
+                from shifu_amd.data.reader import read_header
+                mc_ = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+                hp = mc_.resolve(mc_.dataSet["headerPath"])
+                hdr_ = read_header(hp, "|", mc_.resolve(mc_.dataSet["dataPath"]), "|")
+                autotype.scan(mc_, hdr_, list(range(len(hdr_))), info.rank, info.world_size)
+            step("x_autotype_scan", _scan)
+        elif x == "join":
+            def _join():
+                from shifu_amd.steps.base import ModelSet
+                from shifu_amd.steps.combo import _join_scores
+                ms_ = ModelSet(root)
+                _join_scores([("nn", ms_)], [ms_.mc.dataSet], os.path.join(root, "joined"))
+            step("x_combo_join", _join)
+        else:
+            raise ValueError(f"unknown --pipeline-extra step {x}")
+        extra[x] = times.pop("x_autotype_scan" if x == "autotype" else "x_combo_join")
     recall = None
     if info.rank == 0:
         import numpy as np
@@ -819,6 +843,7 @@ def bench_pipeline(a, dev, info):
         "config": {"model": f"default NN {F}-50-1 (tanh), SE varsel filterNum 200", "global_batch": rows * info.world_size,
                    "seq_len": None, "n_cols": F, "rows_per_gpu": rows, "parallelism": f"dp{info.world_size}"},
         "step_seconds": {k: round(v, 2) for k, v in times.items()}, "generation_s": round(t_gen, 1),
+        "extra_step_seconds (outside the total)": {k: round(v, 2) for k, v in extra.items()},
         "train_epoch_s (median epoch interval, metrics.jsonl)": round(ep_train, 4),
         "train_setup_s": round(train_setup, 2),
         "varsel_phases_s (SE: rows load, NN training, sensitivity)": {k: (round(v, 2) if isinstance(v, float) else v)
@@ -917,6 +942,8 @@ def main():
     ap.add_argument("--pipeline-tmp", default=None, help="pipeline: put the model set's tmp/ (NormalizedData) here")
     ap.add_argument("--pipeline-eval-rows", type=int, default=None,
                     help="pipeline: eval set rows (default a quarter of --rows; the reference's eval is 20M rows)")
+    ap.add_argument("--pipeline-extra", default="",
+                    help="pipeline: extra timed steps after it, comma list of autotype, join")
     ap.add_argument("--pipeline-epochs", type=int, default=40,
                     help="pipeline: numTrainEpochs of the NN (varsel SE trains half of them)")
     a = ap.parse_args()

@@ -17,10 +17,10 @@ Ranks merge by all-reduce (counts: sum; HLL registers: max) and by gathering the
 from __future__ import annotations
 
 import ctypes
-import gzip
 
 import numpy as np
 
+from ..data.join import raw_blocks
 from ..utils.log import get_logger
 
 _log = get_logger("algos.autotype")
@@ -43,62 +43,6 @@ def _native():
     if lib is None or not hasattr(lib, "shifu_at_new"):
         raise RuntimeError("auto-type scan needs the native runtime (python -m shifu_amd.build_native)")
     return lib
-
-
-def _blocks(plan, rank: int, world: int, block_bytes: int):
-    """(file index, offset, bytes of complete lines) of this rank's share."""
-    from ..data.reader import list_data_files
-    from ..data.stream import _lines_in_range, byte_ranges
-    files = list_data_files(plan.data_path)
-    if not files:
-        raise FileNotFoundError(f"no data under {plan.data_path}")
-    for fi, path, a, b in byte_ranges(files, rank, world):
-        if a is None:                                       # indivisible unit: gz / parquet
-            if path.endswith(".parquet"):
-                yield fi, 0, _parquet_text(path, plan)
-                continue
-            with gzip.open(path, "rb") as fh:
-                carry = b""
-                first = True
-                while True:
-                    chunk = fh.read(block_bytes)
-                    if not chunk:
-                        if carry:
-                            yield fi, 0, carry
-                        break
-                    data = carry + chunk
-                    cut = data.rfind(b"\n")
-                    if cut < 0:
-                        carry = data
-                        continue
-                    blk, carry = data[:cut + 1], data[cut + 1:]
-                    if first and plan.skip_header_line and fi == 0:
-                        nl = blk.find(b"\n")
-                        blk = blk[nl + 1:]
-                    first = False
-                    yield fi, 0, blk
-            continue
-        for off, data in _lines_in_range(path, a, b, block_bytes, nbuf=1):
-            if plan.skip_header_line and fi == 0 and off == 0:
-                nl = bytes(data[: 1 << 20]).find(b"\n")
-                data = data[nl + 1:] if nl >= 0 else b""
-            if len(data):
-                yield fi, off, data
-
-
-def _parquet_text(path, plan) -> bytes:
-    """A parquet part as delimited text lines (string form of every value; the reader's missing
-    values as empty fields)."""
-    import pyarrow.parquet as pq
-    t = pq.read_table(path)
-    cols = []
-    for h in plan.header:
-        if h in t.column_names:
-            cols.append(["" if v is None else str(v) for v in t.column(h).to_pylist()])
-        else:
-            cols.append([""] * t.num_rows)
-    lines = (plan.delim.join(r) for r in zip(*cols))
-    return ("\n".join(lines) + "\n").encode() if t.num_rows else b""
 
 
 def _filter_mask(plan, data) -> np.ndarray | None:
@@ -135,7 +79,7 @@ def scan(mc, header: list, cols: list, rank: int = 0, world: int = 1, nthreads: 
         raise RuntimeError("auto-type scanner: bad arguments")
     try:
         rows = 0
-        for _, _, data in _blocks(plan, rank, world, block_bytes):
+        for _, _, data in raw_blocks(plan, rank, world, block_bytes):
             mask = _filter_mask(plan, data)
             arr = np.frombuffer(data, dtype=np.uint8)          # the block's bytes, no copy
             got = lib.shifu_at_feed(h, arr.ctypes.data, len(arr), None if mask is None else mask.ctypes.data,

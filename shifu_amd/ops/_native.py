@@ -118,6 +118,8 @@ RT_SIGNATURES = {
     "shifu_spdt_bins": ("pplipl", "l"),
     "shifu_munropat_bins": ("plipl", "l"),
     "shifu_format_rows": ("lipppppplp", "l"),
+    "shifu_format_rows_sep": ("lipppppplpPi", "l"),
+    "shifu_join_lines": ("plPiipplpl", "l"),
     "shifu_merge_runs": ("ippppP", "l"),
     "shifu_gather_lines": ("ppplPp", "l"),
     "shifu_gen_csv": ("Pliildii", "i"),

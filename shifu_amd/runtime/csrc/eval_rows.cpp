@@ -77,14 +77,17 @@ int put_repr(char* p, double x) {
 //   kinds[c]: FIXED6 / REPR / REPR_OR_EMPTY (cols[c] -> double[n]) or DICT (cols[c] -> int32[n],
 //   dict_blob[c] + dict_off[c][k..k+1] = string k, dict_n[c] strings).
 //   line_end[i] = byte offset just past row i's '\n'.  Returns bytes written, or -1 if cap is short.
-SHIFU_RT_API long shifu_format_rows(long n, int ncols, const int* kinds, const void* const* cols,
-                                    const char* const* dict_blob, const long* const* dict_off,
-                                    const long* dict_n, char* out, long cap, long* line_end) {
+//   sep / slen: the field separator (shifu_format_rows: '|').
+SHIFU_RT_API long shifu_format_rows_sep(long n, int ncols, const int* kinds, const void* const* cols,
+                                        const char* const* dict_blob, const long* const* dict_off,
+                                        const long* dict_n, char* out, long cap, long* line_end,
+                                        const char* sep, int slen) {
+  if (slen < 1 || slen > 64) return -1;
   long pos = 0;
   for (long i = 0; i < n; ++i) {
     for (int c = 0; c < ncols; ++c) {
       if (cap - pos < 512) return -1;
-      if (c) out[pos++] = '|';
+      if (c) { std::memcpy(out + pos, sep, (size_t)slen); pos += slen; }
       const int k = kinds[c];
       if (k == DICT) {
         const int code = ((const int32_t*)cols[c])[i];
@@ -104,6 +107,61 @@ SHIFU_RT_API long shifu_format_rows(long n, int ncols, const int* kinds, const v
     line_end[i] = pos;
   }
   return pos;
+}
+
+SHIFU_RT_API long shifu_format_rows(long n, int ncols, const int* kinds, const void* const* cols,
+                                    const char* const* dict_blob, const long* const* dict_off,
+                                    const long* dict_n, char* out, long cap, long* line_end) {
+  return shifu_format_rows_sep(n, ncols, kinds, cols, dict_blob, dict_off, dict_n, out, cap, line_end, "|", 1);
+}
+
+// Joined rows for `combo` (DataJoin of the sub-model scores, ComboModelProcessor.java:278-356) and
+// `encode` (tree leaf-path columns): every non-blank line of a block of complete lines (blank =
+// only ' ', '\t', '\r'; the parser's row framing) is written as its first `nf` fields (a short
+// row padded with empty fields, fields past the header dropped, a trailing '\r' removed), then
+// the separator and suffix line i (from shifu_format_rows_sep, '\n'-terminated).  The raw field
+// bytes pass through untouched.  Returns bytes written, -1 if cap is short, -2 if the block does
+// not hold exactly n non-blank lines.
+SHIFU_RT_API long shifu_join_lines(const char* buf, long len, const char* sep, int slen, int nf,
+                                   const char* suffix, const long* suffix_end, long n, char* out, long cap) {
+  if (slen < 1 || nf < 1) return -2;
+  long pos = 0, row = 0;
+  const char* p = buf;
+  const char* end = buf + len;
+  while (p < end) {
+    const char* nl = (const char*)std::memchr(p, '\n', (size_t)(end - p));
+    const char* le = nl ? nl : end;
+    const char* next = nl ? nl + 1 : end;
+    bool blank = true;
+    for (const char* q = p; q < le; ++q)
+      if (*q != ' ' && *q != '\r' && *q != '\t') { blank = false; break; }
+    if (blank) { p = next; continue; }
+    if (row >= n) return -2;
+    if (le > p && le[-1] == '\r') --le;
+    // the first nf fields: cut before the nf-th separator, if any
+    const char* cut = le;
+    int seen = 1;
+    for (const char* q = p; q + slen <= le;) {
+      if (std::memcmp(q, sep, (size_t)slen) == 0) {
+        if (seen == nf) { cut = q; break; }
+        ++seen;
+        q += slen;
+      } else {
+        ++q;
+      }
+    }
+    const long a = row ? suffix_end[row - 1] : 0, b = suffix_end[row];
+    const long need = (cut - p) + (long)(nf - seen + 1) * slen + (b - a) + 1;
+    if (cap - pos < need) return -1;
+    std::memcpy(out + pos, p, (size_t)(cut - p));
+    pos += cut - p;
+    for (int k = seen; k <= nf; ++k) { std::memcpy(out + pos, sep, (size_t)slen); pos += slen; }
+    std::memcpy(out + pos, suffix + a, (size_t)(b - a));
+    pos += b - a;
+    ++row;
+    p = next;
+  }
+  return row == n ? pos : -2;
 }
 
 // k-way merge of R sorted runs of lines into `out_path` (appending).  Run r: lines blob + line_end

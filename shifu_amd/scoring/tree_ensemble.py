@@ -287,6 +287,22 @@ class TreeScorer:
             cols.append(pad(e.paths[leaf]))
         return np.concatenate(cols, 1) if cols else np.zeros((X.shape[0], 0), dtype=object)
 
+    @torch.no_grad()
+    def encode_fields(self, table, depth: int | None = None) -> list:
+        """:meth:`encode` as row-formatter fields (data/join.py): per tree (DICT, int32 code per
+        row, padded paths of the leaves reached) -- no per-row Python strings.  The leaf walk runs
+        on the scorer's device (HIP tree walk on a GPU)."""
+        from ..data.join import DICT
+        X = self.input_matrix(table)
+        out = []
+        for e in self.ens:
+            d = depth or max(1, e.depth)
+            leaf = e.leaves(X).cpu().numpy()
+            for t in range(leaf.shape[1]):
+                u, inv = np.unique(leaf[:, t], return_inverse=True)
+                out.append((DICT, inv.astype(np.int32), [(p + "L" * d)[:d] for p in e.paths[u]]))
+        return out
+
 
 def _to_float(x):
     try:

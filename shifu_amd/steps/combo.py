@@ -18,7 +18,6 @@ import shutil
 import numpy as np
 
 from ..config.model_config import ModelConfig, create_params_by_alg
-from ..data.reader import first_line_is_header, read_header, read_table
 from ..scoring.model_runner import ModelRunner
 from ..utils.log import get_logger
 from .base import ModelSet
@@ -99,33 +98,29 @@ def _pipeline(root, steps=("init", "stats", "norm", "varsel", "train"), skip_ini
         run_train(root)
 
 
-def _score_rows(ms_sub: ModelSet, data_conf):
-    """Raw rows of a data set + this sub-model's mean score (x1000)."""
-    mc = ms_sub.mc
-    runner = ModelRunner(mc, ms_sub.ccs, ms_sub.pf.models_dir)
-    path = mc.resolve(data_conf.get("dataPath"))
-    delim = data_conf.get("dataDelimiter") or "|"
-    hp = data_conf.get("headerPath")
-    header = read_header(mc.resolve(hp) if hp else None, data_conf.get("headerDelimiter") or "|", path, delim)
-    skip = (not hp) and first_line_is_header(path, header, delim)
-    cats = {c.name for c in ms_sub.ccs if c.is_categorical()}
-    need = runner.raw_columns()
-    t = read_table(path, header, delim, numeric=[h for h in header if h in need and h not in cats],
-                   strings=[h for h in header if h not in need or h in cats], missing=mc.missing_values,
-                   skip_header_line=skip)
-    raw = read_table(path, header, delim, strings=header, missing=mc.missing_values, skip_header_line=skip)
-    return header, raw, runner.score(t, 1000.0)["mean"]
+def _join_scores(subs, confs, out_dir: str) -> str:
+    """Every sub model's mean score (x1000, ``%.6f``) appended to the raw rows of a data set
+    (``confs[i]``: sub model i's view of it), streamed per rank into ``out_dir/part-<rank>``
+    (``data/join.stream_join``) -> the data delimiter (also the ``.pig_header`` delimiter)."""
+    from ..data.join import FIXED6, stream_join
+    from ..data.purifier import plan_dataset
+    from ..data.reader import column_kinds
+    from ..parallel import dist
+    runners = [(f"{name}_score", ModelRunner(sms.mc, sms.ccs, sms.pf.models_dir)) for name, sms in subs]
+    cats = set()
+    need = set()
+    for (_, sms), (_, r) in zip(subs, runners):
+        cats |= {c.name for c in sms.ccs if c.is_categorical()}
+        need |= set(r.raw_columns())
+    mc0 = subs[0][1].mc
+    plan = plan_dataset(mc0, confs[0], [h for h in need if h not in cats], [h for h in need if h in cats])
+    kinds = column_kinds(plan.header, plan.nums, plan.strs)
 
-
-def _write_joined(out_dir, header, raw, score_cols):
-    os.makedirs(out_dir, exist_ok=True)
-    names = list(header) + list(score_cols.keys())
-    with open(os.path.join(out_dir, ".pig_header"), "w") as f:
-        f.write("|".join(names) + "\n")
-    cols = [raw[h].strings() for h in header] + [np.char.mod("%.6f", v) for v in score_cols.values()]
-    with open(os.path.join(out_dir, "part-00000"), "w") as f:
-        for i in range(raw.n):
-            f.write("|".join(str(c[i]) for c in cols) + "\n")
+    def compute(table, n):
+        return [(FIXED6, np.asarray(r.score(table, 1000.0)["mean"], dtype=np.float64)) for _, r in runners]
+    info = dist.info()
+    stream_join(plan, out_dir, [k for k, _ in runners], kinds, compute, info.rank, info.world_size)
+    return plan.delim or "|"
 
 
 def _has_models(d: str) -> bool:
@@ -158,20 +153,17 @@ def combo_run(root: str, shuffle: bool = False, resume: bool = False):
         tasks = [(lambda d=d: _pipeline(d, shuffle=shuffle)) for _, d in todo]
     ExecutorManager(parallel, retries).run(tasks, [sub["modelName"] for sub, _ in todo])
     subs = [(sub["modelName"], ModelSet(d)) for sub, d in zip(cfg["subTrains"], dirs)]
-    scores, header, raw = {}, None, None
-    for name, sms in subs:
-        header, raw, s = _score_rows(sms, sms.mc.dataSet)
-        scores[f"{name}_score"] = s
     asm = cfg["assemble"]
     ad = _sub_dir(ms, asm["modelName"])
     data_dir = os.path.join(ad, "data")
-    _write_joined(data_dir, header, raw, scores)
+    delim = _join_scores(subs, [sms.mc.dataSet for _, sms in subs], data_dir)
     ams = ModelSet(ad)
     ams.mc.dataSet["dataPath"] = data_dir
     ams.mc.dataSet["headerPath"] = os.path.join(data_dir, ".pig_header")
+    ams.mc.dataSet["headerDelimiter"] = delim
     fs = os.path.join(ad, "columns", "forceselect.column.names")
     with open(fs, "w") as f:
-        f.write("\n".join(scores.keys()) + "\n")
+        f.write("\n".join(f"{name}_score" for name, _ in subs) + "\n")
     ams.mc.varSelect["forceSelectColumnNameFile"] = fs
     ams.mc.varSelect["forceEnable"] = True
     ams.save_mc()
@@ -186,17 +178,14 @@ def combo_eval(root: str):
     asm = cfg["assemble"]
     ad = _sub_dir(ms, asm["modelName"])
     ams = ModelSet(ad)
+    subs = [(sub["modelName"], ModelSet(_sub_dir(ms, sub["modelName"]))) for sub in cfg["subTrains"]]
     for ev in ams.mc.evals:
-        scores, header, raw = {}, None, None
-        for sub in cfg["subTrains"]:
-            sms = ModelSet(_sub_dir(ms, sub["modelName"]))
-            sev = [e for e in sms.mc.evals if e.get("name") == ev.get("name")][0]
-            header, raw, s = _score_rows(sms, sev.dataSet)
-            scores[f"{sub['modelName']}_score"] = s
+        confs = [[e for e in sms.mc.evals if e.get("name") == ev.get("name")][0].dataSet for _, sms in subs]
         out = os.path.join(ad, "evaldata", ev.get("name"))
-        _write_joined(out, header, raw, scores)
+        delim = _join_scores(subs, confs, out)
         ev.dataSet["dataPath"] = out
         ev.dataSet["headerPath"] = os.path.join(out, ".pig_header")
+        ev.dataSet["headerDelimiter"] = delim
     ams.save_mc()
     return run_eval(ad)
 

@@ -96,33 +96,30 @@ def run_encode(root=".", target: str | None = None, ref_model: str | None = None
     paths = [os.path.join(mdir, f) for f in sorted(os.listdir(mdir)) if f.endswith((".gbt", ".rf"))]
     if not paths:
         raise FileNotFoundError(f"no GBT/RF model under {mdir}")
-    scorer = TreeScorer(tree_format.read_tree_model(paths[0]), device or "cpu")
+    import torch
+    from ..data.join import stream_join
+    from ..data.purifier import plan_dataset
+    from ..data.reader import column_kinds
+    from ..parallel import dist
+    dev = device or ("cuda" if torch.cuda.is_available() and not os.environ.get("SHIFU_FORCE_CPU") else "cpu")
+    scorer = TreeScorer(tree_format.read_tree_model(paths[0]), dev)
+    m = scorer.model
     depth = int((mc.train.get("params") or {}).get("MaxDepth", 0) or 0) or None
     confs = [("train", mc.dataSet)] if not target else [(e.get("name"), e.dataSet) for e in mc.evals
                                                          if target in ("*", e.get("name"))]
+    ntrees = sum(len(b) for b in m.bags)
+    enc_names = [f"tree_vars_{i}" for i in range(ntrees)]
+    info = dist.info()
     for name, ds in confs:
-        data_path = mc.resolve(ds.get("dataPath"))
-        delim = ds.get("dataDelimiter") or "|"
-        hp = ds.get("headerPath")
-        header = read_header(mc.resolve(hp) if hp else None, ds.get("headerDelimiter") or "|", data_path, delim)
-        t = read_table(data_path, header, delim, strings=header, missing=mc.missing_values,
-                       skip_header_line=(not hp) and first_line_is_header(data_path, header, delim))
-        m = scorer.model
-        num = {m.names[c] for c in m.names if c not in m.categories}
-        tab = read_table(data_path, header, delim, numeric=[h for h in header if h in num],
-                         strings=[h for h in header if h not in num], missing=mc.missing_values,
-                         skip_header_line=(not hp) and first_line_is_header(data_path, header, delim))
-        codes = scorer.encode(tab, depth)
+        # the trees' inputs only: numeric columns parsed as numbers, categorical ones as strings
+        num = [m.names[c] for c in m.names if c not in m.categories]
+        cat = [m.names[c] for c in m.names if c in m.categories]
+        plan = plan_dataset(mc, ds, num, cat)
+        kinds = column_kinds(plan.header, plan.nums, plan.strs)
         out = ms.pf.encoded_train_data if name == "train" else ms.pf.encoded_eval_data(name)
-        os.makedirs(out, exist_ok=True)
-        enc_names = [f"tree_vars_{i}" for i in range(codes.shape[1])]
-        raw = [t[h].strings() for h in header]
-        with open(os.path.join(out, "part-00000"), "w") as f:
-            for i in range(t.n):
-                f.write("|".join([r[i] for r in raw] + list(codes[i])) + "\n")
-        with open(os.path.join(out, ".pig_header"), "w") as f:
-            f.write("|".join(list(header) + enc_names) + "\n")
-        _log.info("encode %s: %d rows, %d tree features -> %s", name, t.n, len(enc_names), out)
+        rows = stream_join(plan, out, enc_names, kinds, lambda t, n: scorer.encode_fields(t, depth),
+                           info.rank, info.world_size)
+        _log.info("encode %s: %d rows (rank %d), %d tree features -> %s", name, rows, info.rank, len(enc_names), out)
     return 0
 
 
