@@ -17,6 +17,7 @@ Ranks merge by all-reduce (counts: sum; HLL registers: max) and by gathering the
 from __future__ import annotations
 
 import ctypes
+import time
 
 import numpy as np
 
@@ -26,6 +27,7 @@ from ..utils.log import get_logger
 _log = get_logger("algos.autotype")
 
 ITEMS_CAP = 200
+STATS: dict = {}          # cumulative native scan seconds (tools/join_lab.py)
 BLOCK_BYTES = 256 << 20
 
 
@@ -61,10 +63,12 @@ def _filter_mask(plan, data) -> np.ndarray | None:
         return None
 
 
-def scan(mc, header: list, cols: list, rank: int = 0, world: int = 1, nthreads: int = 8,
+def scan(mc, header: list, cols: list, rank: int = 0, world: int = 1, nthreads: int | None = None,
          block_bytes: int = BLOCK_BYTES) -> dict:
     """Auto-type statistics of columns ``cols`` (indices into ``header``) over this rank's share,
     merged over the ranks: {column index: ColumnCounts}."""
+    import os
+    nthreads = nthreads or min(16, os.cpu_count() or 4)
     from ..data.purifier import plan_dataset
     from ..parallel import dist
     lib = _native()
@@ -79,14 +83,19 @@ def scan(mc, header: list, cols: list, rank: int = 0, world: int = 1, nthreads: 
         raise RuntimeError("auto-type scanner: bad arguments")
     try:
         rows = 0
-        for _, _, data in raw_blocks(plan, rank, world, block_bytes):
+        from ..data.stream import prefetched
+        # blocks are read on a background thread one ahead of the scan (three rotating buffers)
+        for _, _, data in prefetched(lambda: raw_blocks(plan, rank, world, block_bytes, nbuf=3), 1):
             mask = _filter_mask(plan, data)
             arr = np.frombuffer(data, dtype=np.uint8)          # the block's bytes, no copy
+            t0 = time.perf_counter()
             got = lib.shifu_at_feed(h, arr.ctypes.data, len(arr), None if mask is None else mask.ctypes.data,
                                     int(nthreads))
+            STATS["feed_s"] = STATS.get("feed_s", 0.0) + time.perf_counter() - t0
             if got < 0:
                 raise RuntimeError("auto-type scanner failed on a block")
             rows += got
+        t0 = time.perf_counter()
         F = len(header)
         counts = np.zeros(3 * F, dtype=np.int64)
         lib.shifu_at_counts(h, counts.ctypes.data)
@@ -108,6 +117,7 @@ def scan(mc, header: list, cols: list, rank: int = 0, world: int = 1, nthreads: 
             k = lib.shifu_at_items(h, c, ibuf, len(ibuf))
             items[c] = ibuf.raw[:k].decode("utf-8", "replace").split("\n")[:-1] if k > 0 else []
         skipped = int(lib.shifu_at_skipped(h))
+        STATS["finish_s"] = STATS.get("finish_s", 0.0) + time.perf_counter() - t0
     finally:
         lib.shifu_at_free(h)
     info = dist.info()

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import gzip
 import os
+import time
 
 import numpy as np
 
@@ -35,9 +36,10 @@ def _rt():
     return lib
 
 
-def raw_blocks(plan, rank: int, world: int, block_bytes: int = BLOCK_BYTES):
+def raw_blocks(plan, rank: int, world: int, block_bytes: int = BLOCK_BYTES, nbuf: int = 1):
     """(file index, offset, bytes of complete lines) of this rank's share, header line removed;
-    ``.gz`` parts are decompressed in blocks, ``.parquet`` parts rendered as delimited text."""
+    ``.gz`` parts are decompressed in blocks, ``.parquet`` parts rendered as delimited text.
+    A plain-text block stays valid until ``nbuf - 1`` further blocks have been produced."""
     from .reader import list_data_files
     from .stream import _lines_in_range, byte_ranges
     files = list_data_files(plan.data_path)
@@ -69,7 +71,7 @@ def raw_blocks(plan, rank: int, world: int, block_bytes: int = BLOCK_BYTES):
                     first = False
                     yield fi, 0, blk
             continue
-        for off, data in _lines_in_range(path, a, b, block_bytes, nbuf=1):
+        for off, data in _lines_in_range(path, a, b, block_bytes, nbuf=nbuf):
             if plan.skip_header_line and fi == 0 and off == 0:
                 nl = bytes(data[: 1 << 20]).find(b"\n")
                 if nl < 0 and len(data) > (1 << 20):
@@ -125,33 +127,45 @@ def format_fields(fields, n: int, sep: str = "|"):
     widest = sum(max((len(str(x).encode("utf-8")) for x in f[2]), default=0) for f in fields if f[0] == DICT)
     cap = max(1024, n * (ncols * (26 + len(sb)) + 16 + widest))
     while True:
-        buf = ctypes.create_string_buffer(cap)
+        buf = np.empty(cap, np.uint8)
         got = lib.shifu_format_rows_sep(n, ncols, (ctypes.c_int * ncols)(*kinds), (ctypes.c_void_p * ncols)(*cols),
                                         (ctypes.c_void_p * ncols)(*blobs), (ctypes.c_void_p * ncols)(*offs),
-                                        (ctypes.c_long * ncols)(*dn), buf, cap, ends.ctypes.data, sb, len(sb))
+                                        (ctypes.c_long * ncols)(*dn), buf.ctypes.data, cap, ends.ctypes.data, sb,
+                                        len(sb))
         if got >= 0:
-            return buf.raw[:got], ends
+            return buf[:got], ends
         cap *= 2
 
 
-def join_block(data, sep: str, nf: int, suffix: bytes, ends: np.ndarray, n: int) -> bytes:
-    """The block's non-blank lines, each cut/padded to ``nf`` fields, + ``sep`` + suffix line i."""
-    import ctypes
+def join_block(data, sep: str, nf: int, suffix, ends: np.ndarray, n: int, nthreads: int = 8) -> memoryview:
+    """The block's non-blank lines, each cut/padded to ``nf`` fields, + ``sep`` + suffix line i
+    (``suffix``: bytes or a uint8 array) -> a view of the joined bytes."""
     lib = _rt()
     arr = np.frombuffer(data, dtype=np.uint8)
     sb = sep.encode()
-    sfx = np.frombuffer(suffix or b"\0", dtype=np.uint8)
+    sfx = np.frombuffer(suffix, dtype=np.uint8) if isinstance(suffix, (bytes, bytearray)) else suffix
+    if not len(sfx):
+        sfx = np.zeros(1, np.uint8)
     ends = np.ascontiguousarray(ends, dtype=np.int64)
-    cap = len(arr) + len(suffix) + n * (nf + 2) * len(sb) + 1024
+    cap = len(arr) + len(sfx) + n * (nf + 2) * len(sb) + 1024
     while True:
-        out = ctypes.create_string_buffer(cap)
+        out = np.empty(cap, np.uint8)
         got = lib.shifu_join_lines(arr.ctypes.data, len(arr), sb, len(sb), nf, sfx.ctypes.data, ends.ctypes.data,
-                                   n, out, cap)
+                                   n, out.ctypes.data, cap, int(nthreads))
         if got >= 0:
-            return out.raw[:got]
+            return memoryview(out[:got])
         if got == -2:
             raise RuntimeError(f"row join: the block does not hold the {n} rows its parse produced")
         cap *= 2
+
+
+STATS: dict = {}          # cumulative seconds per stage of stream_join (tools/join_lab.py)
+
+
+def _tick(st, key, t0):
+    t = time.perf_counter()
+    st[key] = st.get(key, 0.0) + t - t0
+    return t
 
 
 def stream_join(plan, out_dir: str, new_names: list, parse_kinds: list, compute, rank: int = 0, world: int = 1,
@@ -175,18 +189,38 @@ def stream_join(plan, out_dir: str, new_names: list, parse_kinds: list, compute,
             f.write(sep.join(list(plan.header) + list(new_names)) + "\n")
     if world > 1:
         dist.barrier()
+    from concurrent.futures import ThreadPoolExecutor
+    from .stream import prefetched
     rows = 0
-    with open(os.path.join(out_dir, f"part-{rank:05d}"), "wb") as out:
-        for _, _, data in raw_blocks(plan, rank, world, block_bytes):
+    st = STATS
+    # the next block is read on a background thread and finished blocks are written on another:
+    # three block buffers (being read, queued, being joined), two joined blocks in flight
+    blocks = prefetched(lambda: raw_blocks(plan, rank, world, block_bytes, nbuf=3), 1)
+    pending = []
+    t = time.perf_counter()
+    with open(os.path.join(out_dir, f"part-{rank:05d}"), "wb") as out, ThreadPoolExecutor(1) as wr:
+        for _, _, data in blocks:
+            t = _tick(st, "read", t)
             part = parse_block(data, sep, parse_kinds, plan.missing, nthreads)
             n = int(part[0])
             if not n:
                 continue
             table = table_from_parts(plan.header, parse_kinds, [part], plan.data_path)
+            t = _tick(st, "parse", t)
             fields = compute(table, n)
+            t = _tick(st, "compute", t)
             suffix, ends = format_fields(fields, n, sep)
-            out.write(join_block(data, sep, nf, suffix, ends, n))
+            t = _tick(st, "format", t)
+            joined = join_block(data, sep, nf, suffix, ends, n, nthreads)
+            t = _tick(st, "join", t)
+            while len(pending) >= 2:
+                pending.pop(0).result()
+            pending.append(wr.submit(out.write, joined))
+            del joined
+            t = _tick(st, "write", t)
             rows += n
+        for f in pending:
+            f.result()
     if world > 1:
         dist.barrier()
     _log.info("join: rank %d wrote %d rows + %d columns -> %s", rank, rows, len(new_names), out_dir)

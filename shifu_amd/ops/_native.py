@@ -119,7 +119,7 @@ RT_SIGNATURES = {
     "shifu_munropat_bins": ("plipl", "l"),
     "shifu_format_rows": ("lipppppplp", "l"),
     "shifu_format_rows_sep": ("lipppppplpPi", "l"),
-    "shifu_join_lines": ("plPiipplpl", "l"),
+    "shifu_join_lines": ("plPiipplpli", "l"),
     "shifu_merge_runs": ("ippppP", "l"),
     "shifu_gather_lines": ("ppplPp", "l"),
     "shifu_gen_csv": ("Pliildii", "i"),
@@ -178,6 +178,12 @@ def hip():
                     f"{HIP_LIB} not built: run `python -m shifu_amd.build_native` (hipcc gfx950)")
             lib = ctypes.CDLL(str(HIP_LIB), mode=ctypes.RTLD_GLOBAL)
             _bind(lib, HIP_SIGNATURES)
+            # SHIFU_GEMM_TUNE="key=value,...": GEMM dispatch knobs (gemm_kernels.hip
+            # shifu_gemm_set_tune; e.g. 12=0 turns the persistent ring forward off) for A/B runs
+            for kv in filter(None, os.environ.get("SHIFU_GEMM_TUNE", "").split(",")):
+                k, v = kv.split("=")
+                if lib.shifu_gemm_set_tune(int(k), int(v)) != 0:
+                    raise ValueError(f"SHIFU_GEMM_TUNE: bad knob {kv}")
             _hip = lib
     return _hip
 

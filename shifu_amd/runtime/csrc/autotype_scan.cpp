@@ -55,6 +55,21 @@ inline uint64_t hash_bytes(const char* p, size_t n) {
   return mix64(h ^ t ^ 0x2545f4914f6cdd1dull);
 }
 
+// The field hash: fields of up to 8 bytes (most numeric text) are one zero-padded little-endian
+// word -- loaded with one 8-byte read when `end` allows, else byte by byte: the same value
+// hashes the same either way.
+inline uint64_t hash_field(const char* p, size_t n, const char* end) {
+  if (n > 8) return hash_bytes(p, n);
+  uint64_t w = 0;
+  if (p + 8 <= end) {
+    memcpy(&w, p, 8);
+    if (n < 8) w &= (1ull << (8 * n)) - 1;
+  } else {
+    for (size_t k = 0; k < n; ++k) w |= (uint64_t)(uint8_t)p[k] << (8 * k);
+  }
+  return mix64(w ^ (n * 0xff51afd7ed558ccdull) ^ 0x2545f4914f6cdd1dull);
+}
+
 // Double.parseDouble's grammar (whitespace-trimmed; NaN / Infinity, a trailing d/D/f/F type
 // suffix; hexadecimal floats are not recognised)
 bool java_double(const char* p, size_t n) {
@@ -85,23 +100,23 @@ bool java_double(const char* p, size_t n) {
   return i == b;
 }
 
+// rank-level state of one column (sketches owned by one thread at a time, see shifu_at_feed)
 struct Col {
   int64_t count = 0, invalid = 0, validnum = 0;
-  std::vector<uint64_t> table;                // open addressing, 0 = empty (hash 0 stored as 1)
+  std::vector<uint64_t> table;                // open addressing, 0 = empty
   int used = 0;
   bool overflow = false;
   std::vector<uint8_t> hll;                   // AT_HLL_M registers (allocated on first value)
   std::vector<std::string> items;
   std::unordered_set<std::string> item_set;
 
-  void add_hash(uint64_t h) {
+  void add_hash(uint64_t h) {                 // h != 0
     if (hll.empty()) hll.assign(AT_HLL_M, 0);
     const uint32_t idx = (uint32_t)(h >> (64 - AT_HLL_P));
     const uint64_t rest = (h << AT_HLL_P) | (1ull << (AT_HLL_P - 1));
     const uint8_t rank = (uint8_t)(__builtin_clzll(rest) + 1);
     if (rank > hll[idx]) hll[idx] = rank;
     if (overflow) return;
-    if (h == 0) h = 1;
     if (table.empty()) table.assign(64, 0);
     if ((used + 1) * 2 > (int)table.size()) {
       if (used + 1 > AT_EXACT_CAP) {
@@ -126,51 +141,16 @@ struct Col {
     table[k] = h;
     ++used;
   }
-  void add_item(const char* p, size_t n, int cap) {
-    if ((int)items.size() >= cap) return;
+};
+
+// first-seen distinct values of one column in one scanner thread (AT_ITEMS_THREAD of them)
+struct Items {
+  std::vector<std::string> items;
+  std::unordered_set<std::string> set;
+  void add(const char* p, size_t n) {
+    if ((int)items.size() >= AT_ITEMS_THREAD) return;
     std::string s(p, n);
-    if (item_set.insert(s).second) items.push_back(std::move(s));
-  }
-  void merge(Col& o, int item_cap) {
-    count += o.count; invalid += o.invalid; validnum += o.validnum;
-    if (!o.hll.empty()) {
-      if (hll.empty()) hll.assign(AT_HLL_M, 0);
-      for (int i = 0; i < AT_HLL_M; ++i) hll[i] = std::max(hll[i], o.hll[i]);
-    }
-    if (o.overflow) {
-      overflow = true;
-      std::vector<uint64_t>().swap(table);
-    } else if (!overflow) {
-      for (uint64_t v : o.table)
-        if (v) {
-          if (overflow) break;
-          // re-insert without touching the HLL (already merged)
-          if (table.empty()) table.assign(64, 0);
-          if ((used + 1) * 2 > (int)table.size()) {
-            if (used + 1 > AT_EXACT_CAP) { overflow = true; std::vector<uint64_t>().swap(table); break; }
-            std::vector<uint64_t> t2(table.size() * 2, 0);
-            for (uint64_t w : table)
-              if (w) {
-                size_t k = w & (t2.size() - 1);
-                while (t2[k]) k = (k + 1) & (t2.size() - 1);
-                t2[k] = w;
-              }
-            table.swap(t2);
-          }
-          size_t k = v & (table.size() - 1);
-          bool dup = false;
-          while (table[k]) {
-            if (table[k] == v) { dup = true; break; }
-            k = (k + 1) & (table.size() - 1);
-          }
-          if (!dup) { table[k] = v; ++used; }
-        }
-    }
-    for (auto& s : o.items) {
-      if ((int)items.size() >= item_cap) break;
-      if (item_set.insert(s).second) items.push_back(s);
-    }
-    o = Col();
+    if (set.insert(s).second) items.push_back(std::move(s));
   }
 };
 
@@ -178,10 +158,12 @@ struct State {
   int ncols = 0, tag_col = -1;
   std::string delim;
   std::vector<std::string> tags;              // trimmed
-  std::unordered_set<std::string> missing;    // compared with the lower-cased raw field
-  std::vector<Col> cols;                      // merged (rank) state
-  std::vector<std::vector<Col>> part;         // per thread, merged on query
+  std::vector<std::string> missing;           // compared with the lower-cased raw field
+  size_t missing_max = 0;                     // longest missing token
+  std::vector<Col> cols;                      // counts and sketches
+  std::vector<std::vector<Items>> part;       // per scanner thread, merged on query
   int64_t rows = 0, skipped_tag = 0;
+  bool dirty = false;                         // per-thread items not merged yet
 };
 
 inline bool is_blank_line(const char* s, const char* e) {
@@ -190,13 +172,30 @@ inline bool is_blank_line(const char* s, const char* e) {
   return true;
 }
 
-// one thread: lines in [s, e) (line-aligned), rows numbered from row0 for the mask
-void scan_range(State& S, std::vector<Col>& cols, const char* s, const char* e, const uint8_t* mask, int64_t row0,
-                int64_t* rows_out, int64_t* skipped_out) {
+// the raw field lower-cased equals one of the missing tokens (no allocation: tokens are short)
+inline bool is_missing(const State& S, const char* v, size_t n) {
+  if (n > S.missing_max) return false;
+  for (const std::string& m : S.missing) {
+    if (m.size() != n) continue;
+    size_t i = 0;
+    while (i < n && (char)tolower((unsigned char)v[i]) == m[i]) ++i;
+    if (i == n) return true;
+  }
+  return false;
+}
+
+// per-field code of the row pass: 0 absent (short row), 1 missing-or-invalid, otherwise
+// (63-bit value hash << 1) | parses-as-a-Java-double
+constexpr uint64_t AT_ABSENT = 0, AT_MISSING = 1;
+
+// Row pass of one thread over lines [s, e): tag / mask filter, field split, per field a code into
+// the column-major buffer codes[c * cap + i] (i = kept row), first-seen items.  Returns kept rows.
+int64_t code_rows(const State& S, std::vector<Items>& items, const char* s, const char* e, const uint8_t* mask,
+                  int64_t row0, uint64_t* codes, int64_t cap, int64_t* skipped_out) {
   const char* d = S.delim.data();
   const size_t dl = S.delim.size();
-  int64_t r = row0, skipped = 0, rows = 0;
-  std::string low;
+  const int NC = S.ncols;
+  int64_t r = row0, skipped = 0, nb = 0;
   std::vector<std::pair<const char*, size_t>> f;
   for (const char* p = s; p < e;) {
     const char* nl = (const char*)memchr(p, '\n', e - p);
@@ -229,25 +228,64 @@ void scan_range(State& S, std::vector<Col>& cols, const char* s, const char* e, 
         if (tg.size() == b - a && !memcmp(tg.data(), t + a, b - a)) { ok = true; break; }
       if (!ok) { ++skipped; p = next; continue; }
     }
-    ++rows;
-    const int nf = std::min((int)f.size(), S.ncols);
+    if (nb >= cap) break;                     // cannot happen: cap = the chunk's line count
+    const int nf = std::min((int)f.size(), NC);
+    uint64_t* cr = codes + nb;
     for (int c = 0; c < nf; ++c) {
-      Col& C = cols[c];
       const char* v = f[c].first;
       const size_t n = f[c].second;
-      C.count += 1;
-      low.assign(v, n);
-      for (auto& ch : low) ch = (char)tolower((unsigned char)ch);
-      if (S.missing.count(low)) { C.invalid += 1; continue; }
-      C.add_hash(hash_bytes(v, n));
-      if (java_double(v, n)) C.validnum += 1;
-      C.add_item(v, n, AT_ITEMS_THREAD);
+      if (is_missing(S, v, n)) { cr[(size_t)c * cap] = AT_MISSING; continue; }
+      uint64_t h = hash_field(v, n, e) >> 1;
+      if (!h) h = 1;
+      cr[(size_t)c * cap] = (h << 1) | (java_double(v, n) ? 1u : 0u);
+      items[c].add(v, n);
     }
+    for (int c = nf; c < NC; ++c) cr[(size_t)c * cap] = AT_ABSENT;
+    ++nb;
     p = next;
   }
-  *rows_out = rows;
   *skipped_out = skipped;
+  return nb;
 }
+
+// Column pass over columns [c0, c1): every chunk's codes (chunk order) into the column's counts,
+// exact set and registers -- each column's sketch is touched by this thread only, for all the
+// rows of the sub-block in a row, so it stays in this core's cache.
+void apply_codes(State& S, int c0, int c1, const std::vector<std::vector<uint64_t>>& codes,
+                 const std::vector<int64_t>& cap, const std::vector<int64_t>& kept) {
+  for (int c = c0; c < c1; ++c) {
+    Col& C = S.cols[c];
+    for (size_t u = 0; u < codes.size(); ++u) {
+      const uint64_t* x = codes[u].data() + (size_t)c * cap[u];
+      for (int64_t i = 0; i < kept[u]; ++i) {
+        const uint64_t v = x[i];
+        if (v == AT_ABSENT) continue;
+        C.count += 1;
+        if (v == AT_MISSING) { C.invalid += 1; continue; }
+        C.validnum += (int64_t)(v & 1);
+        C.add_hash(v | 1);                  // top bits: the hash; odd: never the empty slot
+      }
+    }
+  }
+}
+
+// per-thread item lists -> the rank's (thread order: the lists keep the text order)
+void merge_parts(State& S) {
+  if (!S.dirty) return;
+  S.dirty = false;
+  for (int c = 0; c < S.ncols; ++c) {
+    Col& C = S.cols[c];
+    for (auto& pt : S.part) {
+      for (auto& it : pt[c].items) {
+        if ((int)C.items.size() >= AT_ITEMS_RANK) break;
+        if (C.item_set.insert(it).second) C.items.push_back(it);
+      }
+      pt[c] = Items();
+    }
+  }
+}
+
+constexpr long AT_SUB_BYTES = 32l << 20;      // sub-block: bounds the code buffers (~8 B per field)
 
 std::vector<std::string> split_blob(const char* blob, bool trim) {
   std::vector<std::string> out;
@@ -269,11 +307,6 @@ std::vector<std::string> split_blob(const char* blob, bool trim) {
   return out;
 }
 
-void merge_parts(State& S) {
-  for (auto& pc : S.part)
-    for (int c = 0; c < S.ncols; ++c) S.cols[c].merge(pc[c], AT_ITEMS_RANK);
-}
-
 }  // namespace
 
 // tags / missing: '\n'-joined (missing tokens as configured: the raw field is lower-cased and
@@ -285,53 +318,99 @@ SHIFU_RT_API void* shifu_at_new(int ncols, int tag_col, const char* tags, const 
   S->tag_col = tag_col;
   S->delim = delim;
   S->tags = split_blob(tags, true);
-  for (auto& m : split_blob(missing, false)) S->missing.insert(m);
+  for (auto& m : split_blob(missing, false)) {
+    S->missing_max = std::max(S->missing_max, m.size());
+    S->missing.push_back(m);
+  }
   S->cols.resize(ncols);
   return S;
 }
 
 // Scan a block of complete lines; mask (nullable): keep flag per non-blank line of the block (the
 // purifier's filter expression).  Returns the rows counted (tag filter passed) or -1.
+// Sub-blocks of AT_SUB_BYTES: `nthreads` threads code their line-aligned chunks (row pass), then
+// the same threads each own a slice of the columns and apply every chunk's codes to it.
 SHIFU_RT_API long shifu_at_feed(void* h, const char* buf, long len, const uint8_t* mask, int nthreads) {
   if (!h || len < 0) return -1;
   State& S = *(State*)h;
-  const int T = std::max(1, std::min(nthreads, (int)(len >> 20) + 1));
-  if ((int)S.part.size() < T) {
-    S.part.resize(T);
-    for (auto& pc : S.part)
-      if ((int)pc.size() != S.ncols) pc.resize(S.ncols);
-  }
-  std::vector<const char*> cut(T + 1);
-  cut[0] = buf;
-  cut[T] = buf + len;
-  for (int t = 1; t < T; ++t) {
-    const char* c = buf + (len * t) / T;
-    if (c < cut[t - 1]) c = cut[t - 1];
-    const char* nl = (const char*)memchr(c, '\n', buf + len - c);
-    cut[t] = nl ? nl + 1 : buf + len;
-  }
-  std::vector<int64_t> row0(T, 0);
-  if (mask) {                                   // rows before each chunk (non-blank lines)
-    int64_t r = 0;
-    for (int t = 0; t < T; ++t) {
-      row0[t] = r;
-      for (const char* p = cut[t]; p < cut[t + 1];) {
-        const char* nl = (const char*)memchr(p, '\n', cut[t + 1] - p);
-        const char* le = nl ? nl : cut[t + 1];
-        if (!is_blank_line(p, le)) ++r;
-        p = nl ? nl + 1 : cut[t + 1];
-      }
-    }
-  }
-  std::vector<int64_t> rows(T, 0), skipped(T, 0);
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; ++t)
-    th.emplace_back([&, t] { scan_range(S, S.part[t], cut[t], cut[t + 1], mask, row0[t], &rows[t], &skipped[t]); });
-  scan_range(S, S.part[0], cut[0], cut[1], mask, row0[0], &rows[0], &skipped[0]);
-  for (auto& x : th) x.join();
+  const int NC = S.ncols;
   long tot = 0;
-  for (int t = 0; t < T; ++t) { tot += rows[t]; S.skipped_tag += skipped[t]; }
+  int64_t mrow = 0;                             // mask rows before the sub-block
+  for (long sb0 = 0; sb0 < len;) {
+    long sb1 = std::min(len, sb0 + AT_SUB_BYTES);
+    if (sb1 < len) {
+      const char* nl = (const char*)memchr(buf + sb1, '\n', len - sb1);
+      sb1 = nl ? (long)(nl - buf) + 1 : len;
+    }
+    const char* s0 = buf + sb0;
+    const long sl = sb1 - sb0;
+    const int T = std::max(1, std::min(nthreads, (int)(sl >> 20) + 1));
+    if ((int)S.part.size() < T) {
+      S.part.resize(T);
+      for (auto& pt : S.part)
+        if ((int)pt.size() != NC) pt.resize(NC);
+    }
+    std::vector<const char*> cut(T + 1);
+    cut[0] = s0;
+    cut[T] = s0 + sl;
+    for (int t = 1; t < T; ++t) {
+      const char* c = std::max(s0 + (sl * t) / T, cut[t - 1]);
+      const char* nl = (const char*)memchr(c, '\n', s0 + sl - c);
+      cut[t] = nl ? nl + 1 : s0 + sl;
+    }
+    // lines per chunk (buffer rows) and non-blank rows before each chunk (mask numbering)
+    std::vector<int64_t> lines(T, 0), row0(T, 0);
+    {
+      std::vector<std::thread> th;
+      auto count = [&](int t) {
+        int64_t nlines = 0, nonblank = 0;
+        for (const char* p = cut[t]; p < cut[t + 1];) {
+          const char* nl = (const char*)memchr(p, '\n', cut[t + 1] - p);
+          const char* le = nl ? nl : cut[t + 1];
+          ++nlines;
+          if (mask && !is_blank_line(p, le)) ++nonblank;
+          p = nl ? nl + 1 : cut[t + 1];
+        }
+        lines[t] = nlines;
+        row0[t] = nonblank;                      // prefix-summed below
+      };
+      for (int t = 1; t < T; ++t) th.emplace_back(count, t);
+      count(0);
+      for (auto& x : th) x.join();
+    }
+    int64_t r = mrow;
+    for (int t = 0; t < T; ++t) { const int64_t nbk = row0[t]; row0[t] = r; r += nbk; }
+    mrow = r;
+    std::vector<std::vector<uint64_t>> codes(T);
+    std::vector<int64_t> cap(T), kept(T, 0), skipped(T, 0);
+    for (int t = 0; t < T; ++t) {
+      cap[t] = std::max<int64_t>(1, lines[t]);
+      codes[t].resize((size_t)cap[t] * NC);
+    }
+    {
+      std::vector<std::thread> th;
+      auto rowpass = [&](int t) {
+        kept[t] = code_rows(S, S.part[t], cut[t], cut[t + 1], mask, row0[t], codes[t].data(), cap[t], &skipped[t]);
+      };
+      for (int t = 1; t < T; ++t) th.emplace_back(rowpass, t);
+      rowpass(0);
+      for (auto& x : th) x.join();
+    }
+    {
+      const int TC = std::max(1, std::min(T, (NC + 15) / 16));
+      std::vector<std::thread> th;
+      auto colpass = [&](int t) {
+        apply_codes(S, (int)((int64_t)NC * t / TC), (int)((int64_t)NC * (t + 1) / TC), codes, cap, kept);
+      };
+      for (int t = 1; t < TC; ++t) th.emplace_back(colpass, t);
+      colpass(0);
+      for (auto& x : th) x.join();
+    }
+    for (int t = 0; t < T; ++t) { tot += kept[t]; S.skipped_tag += skipped[t]; }
+    sb0 = sb1;
+  }
   S.rows += tot;
+  S.dirty = true;
   return tot;
 }
 

@@ -15,7 +15,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <queue>
+#include <thread>
 #include <vector>
 
 #define SHIFU_RT_API extern "C" __attribute__((visibility("default")))
@@ -120,48 +122,105 @@ SHIFU_RT_API long shifu_format_rows(long n, int ncols, const int* kinds, const v
 // only ' ', '\t', '\r'; the parser's row framing) is written as its first `nf` fields (a short
 // row padded with empty fields, fields past the header dropped, a trailing '\r' removed), then
 // the separator and suffix line i (from shifu_format_rows_sep, '\n'-terminated).  The raw field
-// bytes pass through untouched.  Returns bytes written, -1 if cap is short, -2 if the block does
-// not hold exactly n non-blank lines.
-SHIFU_RT_API long shifu_join_lines(const char* buf, long len, const char* sep, int slen, int nf,
-                                   const char* suffix, const long* suffix_end, long n, char* out, long cap) {
-  if (slen < 1 || nf < 1) return -2;
-  long pos = 0, row = 0;
-  const char* p = buf;
-  const char* end = buf + len;
-  while (p < end) {
-    const char* nl = (const char*)std::memchr(p, '\n', (size_t)(end - p));
-    const char* le = nl ? nl : end;
-    const char* next = nl ? nl + 1 : end;
-    bool blank = true;
-    for (const char* q = p; q < le; ++q)
-      if (*q != ' ' && *q != '\r' && *q != '\t') { blank = false; break; }
-    if (blank) { p = next; continue; }
-    if (row >= n) return -2;
+// bytes pass through untouched.  Two passes over `nthreads` line-aligned chunks: (1) per line the
+// kept length and the number of padding separators (memchr over the separator's first byte),
+// per chunk the row count and output bytes; (2) every chunk copies to its prefix-summed offset.
+// Returns bytes written, -1 if cap is short, -2 if the block does not hold exactly n non-blank
+// lines.
+namespace {
+
+struct JoinLine { const char* p; int64_t keep; int32_t pad; };
+
+inline bool blank_line(const char* p, const char* le) {
+  for (const char* q = p; q < le; ++q)
+    if (*q != ' ' && *q != '\r' && *q != '\t') return false;
+  return true;
+}
+
+void join_scan(const char* s, const char* e, const char* sep, int slen, int nf, std::vector<JoinLine>& out,
+               int64_t* bytes) {
+  int64_t tot = 0;
+  for (const char* p = s; p < e;) {
+    const char* nl = (const char*)std::memchr(p, '\n', (size_t)(e - p));
+    const char* le = nl ? nl : e;
+    const char* next = nl ? nl + 1 : e;
+    if (blank_line(p, le)) { p = next; continue; }
     if (le > p && le[-1] == '\r') --le;
-    // the first nf fields: cut before the nf-th separator, if any
     const char* cut = le;
     int seen = 1;
     for (const char* q = p; q + slen <= le;) {
-      if (std::memcmp(q, sep, (size_t)slen) == 0) {
-        if (seen == nf) { cut = q; break; }
+      const char* h = (const char*)std::memchr(q, sep[0], (size_t)(le - q));
+      if (!h || h + slen > le) break;
+      if (slen == 1 || std::memcmp(h, sep, (size_t)slen) == 0) {
+        if (seen == nf) { cut = h; break; }
         ++seen;
-        q += slen;
+        q = h + slen;
       } else {
-        ++q;
+        q = h + 1;
       }
     }
-    const long a = row ? suffix_end[row - 1] : 0, b = suffix_end[row];
-    const long need = (cut - p) + (long)(nf - seen + 1) * slen + (b - a) + 1;
-    if (cap - pos < need) return -1;
-    std::memcpy(out + pos, p, (size_t)(cut - p));
-    pos += cut - p;
-    for (int k = seen; k <= nf; ++k) { std::memcpy(out + pos, sep, (size_t)slen); pos += slen; }
-    std::memcpy(out + pos, suffix + a, (size_t)(b - a));
-    pos += b - a;
-    ++row;
+    const int pad = nf - seen + 1;            // separators after the kept bytes (incl. the suffix's)
+    out.push_back({p, (int64_t)(cut - p), pad});
+    tot += (cut - p) + (int64_t)pad * slen;
     p = next;
   }
-  return row == n ? pos : -2;
+  *bytes = tot;
+}
+
+}  // namespace
+
+SHIFU_RT_API long shifu_join_lines(const char* buf, long len, const char* sep, int slen, int nf,
+                                   const char* suffix, const long* suffix_end, long n, char* out, long cap,
+                                   int nthreads) {
+  if (slen < 1 || nf < 1) return -2;
+  const int T = std::max(1, std::min(nthreads, (int)(len >> 20) + 1));
+  std::vector<const char*> cut(T + 1);
+  cut[0] = buf;
+  cut[T] = buf + len;
+  for (int t = 1; t < T; ++t) {
+    const char* c = std::max(buf + (len * t) / T, cut[t - 1]);
+    const char* nl = (const char*)std::memchr(c, '\n', (size_t)(buf + len - c));
+    cut[t] = nl ? nl + 1 : buf + len;
+  }
+  std::vector<std::vector<JoinLine>> lines(T);
+  std::vector<int64_t> raw(T, 0);
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t)
+      th.emplace_back([&, t] { join_scan(cut[t], cut[t + 1], sep, slen, nf, lines[t], &raw[t]); });
+    join_scan(cut[0], cut[1], sep, slen, nf, lines[0], &raw[0]);
+    for (auto& x : th) x.join();
+  }
+  std::vector<int64_t> row0(T + 1, 0), off0(T + 1, 0);
+  for (int t = 0; t < T; ++t) {
+    row0[t + 1] = row0[t] + (int64_t)lines[t].size();
+    if (row0[t + 1] > n) return -2;
+    const int64_t sa = row0[t] ? suffix_end[row0[t] - 1] : 0;
+    const int64_t sb = row0[t + 1] ? suffix_end[row0[t + 1] - 1] : 0;
+    off0[t + 1] = off0[t] + raw[t] + (sb - sa);
+  }
+  if (row0[T] != n) return -2;
+  if (off0[T] > cap) return -1;
+  auto write = [&](int t) {
+    char* o = out + off0[t];
+    int64_t r = row0[t];
+    for (const JoinLine& L : lines[t]) {
+      std::memcpy(o, L.p, (size_t)L.keep);
+      o += L.keep;
+      for (int k = 0; k < L.pad; ++k) { std::memcpy(o, sep, (size_t)slen); o += slen; }
+      const int64_t a = r ? suffix_end[r - 1] : 0, b = suffix_end[r];
+      std::memcpy(o, suffix + a, (size_t)(b - a));
+      o += b - a;
+      ++r;
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(write, t);
+    write(0);
+    for (auto& x : th) x.join();
+  }
+  return (long)off0[T];
 }
 
 // k-way merge of R sorted runs of lines into `out_path` (appending).  Run r: lines blob + line_end

@@ -205,7 +205,7 @@ def test_ranks_match_single_process(tmp_path, world, monkeypatch):
 
 
 def test_host_memory_bounded(tmp_path):
-    """A ~300 MB text file: the scan's peak RSS stays far below the data size (blocks of 64 MB)."""
+    """A ~260 MB text file: the scan's peak RSS stays far below the data size (blocks of 16 MB)."""
     root = make_model_set(str(tmp_path), "r", "NN", n_rows=100)
     d = os.path.join(root, "big")
     os.makedirs(d)
@@ -227,7 +227,7 @@ for k, v in dict(dataPath={d!r}, headerPath=None, targetColumnName="tag", posTag
     mc.dataSet[k] = v
 hdr = ["tag"] + ["c%d" % j for j in range({cols})]
 before = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
-st = autotype.scan(mc, hdr, list(range(1, len(hdr))), block_bytes=64 << 20)
+st = autotype.scan(mc, hdr, list(range(1, len(hdr))), block_bytes=16 << 20)
 assert st[1].count == 860000, st[1].count
 print(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - before)
 """

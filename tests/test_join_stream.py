@@ -55,7 +55,10 @@ def test_join_lines_matches_model(sep):
     v = np.random.default_rng(0).normal(size=n) * 1000
     codes = np.random.default_rng(1).integers(-1, 3, size=n).astype(np.int32)
     suffix, ends = format_fields([(FIXED6, v), (DICT, codes, ["LLR", "R", "LRRLLR"])], n, sep)
-    got = join_block(text.encode(), sep, 5, suffix, ends, n).decode()
+    got = bytes(join_block(text.encode(), sep, 5, suffix, ends, n, nthreads=1)).decode()
+    assert bytes(join_block(text.encode() * 300, sep, 5, np.tile(np.asarray(suffix), 300),
+                            np.concatenate([ends + k * ends[-1] for k in range(300)]), n * 300, nthreads=8)) \
+        == got.encode() * 300
     sfx = [f"{x:.6f}{sep}{['LLR', 'R', 'LRRLLR'][c] if c >= 0 else ''}" for x, c in zip(v, codes)]
     assert got == _model_join(text, sep, 5, sfx)
     with pytest.raises(RuntimeError):

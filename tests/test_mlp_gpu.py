@@ -253,6 +253,42 @@ def test_bench_configuration_tracks_fp32_oracle():
         assert abs(a - b) / a < 1e-2, (ec, eg)
 
 
+@pytest.mark.parametrize("ring", [1, 0])
+def test_pipeline_configuration_tracks_fp32_oracle(ring):
+    """The text pipeline's default NN (bench.py --model pipeline: 1603 inputs, one tanh layer of
+    50, RPROP) on chunks of 2^17 rows, with the ring forward on and off: first gradient and the
+    error trajectory against the fp32 CPU trainer on the same bf16-rounded data."""
+    from shifu_amd.ops import _native as nat
+    spec = MLPSpec(n_in=1603, hidden=[50], acts=["tanh"], n_out=1)
+    n = (1 << 17) + 77
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, spec.n_in, generator=g).bfloat16().float()
+    wt = torch.randn(spec.n_in, 1, generator=g)
+    y = ((x @ wt) > 0).float()
+    nat.call_hip("shifu_gemm_set_tune", 12, ring)
+    try:
+        cpu = MLPTrainer(spec, device="cpu", seed=7, chunk_rows=1 << 17)
+        gpu = MLPTrainer(spec, device="cuda", seed=7, chunk_rows=1 << 17)
+        cpu.params.flat.copy_(cpu.params.flat.bfloat16().float())
+        gpu.params.flat.copy_(cpu.params.flat.cuda())
+        dc, dg = cpu.prepare(x, y), gpu.prepare(x, y)
+        cpu.grad.zero_(); cpu.err_acc.zero_(); cpu.accumulate_gradients(dc)
+        gpu.grad.zero_(); gpu.err_acc.zero_(); gpu.accumulate_gradients(dg)
+        torch.cuda.synchronize()
+        for vc, vg in zip(cpu.params.views(cpu.grad), gpu.params.views(gpu.grad.cpu())):
+            r = (vc - vg).norm() / vc.norm().clamp(min=1e-12)
+            assert r < 3e-2, float(r)
+        ec, eg = [], []
+        for _ in range(4):
+            ec.append(cpu.step(dc))
+            eg.append(gpu.step(dg))
+        torch.cuda.synchronize()
+    finally:
+        nat.call_hip("shifu_gemm_set_tune", 12, 1)
+    for a, b in zip(ec, eg):
+        assert abs(a - b) / a < 1e-2, (ec, eg)
+
+
 def test_ring_wgrad_bitwise_reproducible():
     """The ring wgrad reduces split partials in a fixed order: two runs are bit-identical."""
     from shifu_amd.ops import _native as nat
