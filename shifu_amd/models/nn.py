@@ -489,8 +489,6 @@ class MLPTrainer:
         if self.gpu:
             from ..ops import _native
             _native.require_gpu_native()
-            if "SHIFU_HEAD_PERSIST" in os.environ:     # persistent fused head A/B (gemm_kernels.hip)
-                _native.call_hip("shifu_gemm_set_tune", 11, int(os.environ["SHIFU_HEAD_PERSIST"] == "1"))
             if spec.layer_kpad[-1] > 512 or spec.n_out > 8:
                 raise ValueError("HIP output kernel supports last hidden width <= 511 and n_out <= 8")
         self.params = MLPParams(spec, self.device)
@@ -534,7 +532,6 @@ class MLPTrainer:
         # bitwise reproducible); SHIFU_WGRAD_RING=0 restores the 128x128 split-K atomics kernel
         self.wgrad_ring = os.environ.get("SHIFU_WGRAD_RING", "1") != "0"
         self.fused_head = self._head_eligible()
-        self.fused2 = self._fused2_eligible()
         self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
         # dropout (NNMaster.dropoutNodes :531-556, FloatFlatNetwork.computeLayer :205-215): each
         # iteration drops hidden nodes with DropoutRate and inputs with 0.4*DropoutRate and scales
@@ -612,9 +609,6 @@ class MLPTrainer:
 
     def _weights_bf16(self, train: bool = True):
         """bf16 copies of the hidden-layer weights (+ transposed copies for dgrad)."""
-        if train and self.fused2:      # the fused step reads its own copies (no per-layer GEMMs)
-            self._f2w_cur = self._fused2_weights()
-            return None, None
         ws = self.params.views(self._wflat)
         kp = self.spec.layer_kpad
         L = len(self.spec.hidden)
@@ -721,74 +715,7 @@ class MLPTrainer:
         return bool(sp.n_out == 1 and sp.layer_kpad[L] <= 256 and a in ACT_DERIV_FROM_OUTPUT and
                     sp.acts[L - 1] != "ptanh" and sp.hidden[L - 1] <= 255)
 
-    def _fused2_eligible(self) -> bool:
-        """Row-block fused step (ops/csrc/mlp_fused.hip): layer-1 forward, layer-2 forward,
-        output + loss + deltas and the layer-1 dgrad in ONE kernel per chunk, H1 and the layer-2
-        deltas never re-read from HBM.  Two hidden layers padded to 512 / 256 (widths 257..511 and
-        1..255), one output, an activation pair with an instantiated kernel (sigmoid, tanh, relu
-        pairs).  Opt-in (SHIFU_FUSED_MLP=1) until it beats the per-layer kernels at the bench shape."""
-        sp = self.spec
-        if self.device.type != "cuda" or len(sp.hidden) != 2 or os.environ.get("SHIFU_FUSED_MLP", "0") != "1":
-            return False
-        acts = (ACT_IDS[sp.acts[0]], ACT_IDS[sp.acts[1]])
-        return bool(sp.n_out == 1 and sp.layer_kpad[1] == 512 and sp.layer_kpad[2] == 256 and
-                    sp.layer_kpad[0] % 32 == 0 and sp.hidden[0] <= 511 and sp.hidden[1] <= 255 and
-                    acts in ((0, 0), (1, 1), (3, 3), (3, 0)))
-
-    def _fused2_weights(self):
-        """bf16 W1 padded to 512 rows and the permuted W2 copies of the fused kernel."""
-        from ..ops import _native as nat
-        sp, kp = self.spec, self.spec.layer_kpad
-        wv = self.params.views(self._wflat)
-        st = nat.stream_of(self.params.flat)
-        if getattr(self, "_f2w", None) is None:
-            self._f2w = (torch.zeros(512, kp[0], dtype=torch.bfloat16, device=self.device),
-                         torch.empty(256 * 512, dtype=torch.bfloat16, device=self.device),
-                         torch.empty(512 * 256, dtype=torch.bfloat16, device=self.device))
-        w1, w2p, w2tp = self._f2w
-        nat.call_hip("shifu_cast_bf16", wv[0].data_ptr(), kp[0], w1.data_ptr(), kp[0], sp.hidden[0], kp[0], st)
-        nat.call_hip("shifu_fused_w2_prep", wv[1].data_ptr(), kp[1], sp.hidden[1], w2p, w2tp, st)
-        return w1, w2p, w2tp
-
-    def _chunk_fused2(self, data: TrainData, r0: int, r1: int, f2w, x_dev=None, lane: int = 0):
-        from ..ops import _native as nat
-        sp, kp = self.spec, self.spec.layer_kpad
-        mc = r1 - r0
-        ws = self._workspace(min(self.chunk_rows, data.n), lane)
-        gv = self.params.views(self.grad)
-        wv = self.params.views(self._wflat)
-        x = data.x[r0:r1] if x_dev is None else x_dev
-        st = nat.stream_of(x)
-        h1, d1, d2 = ws["acts"][0][:mc], ws["deltas"][0][:mc], ws["deltas"][1][:mc]
-        tiles = -(-mc // 128)
-        slab, part = ws.get("f2_slab"), ws.get("f2_part")
-        if slab is None or slab.numel() < tiles * kp[2]:
-            t_max = -(-ws["rows"] // 128)
-            ws["f2_slab"] = slab = torch.empty(t_max * kp[2], dtype=torch.float32, device=self.device)
-            ws["f2_part"] = part = torch.empty(-(-t_max // 128) * kp[2], dtype=torch.float32, device=self.device)
-        y = data.y[r0:r1]
-        s = data.s[r0:r1] if data.s is not None else None
-        w1, w2p, w2tp = f2w
-        nat.call_hip("shifu_mlp_fused2", x, kp[0], mc, kp[0], w1, kp[0], 512, sp.hidden[0], w2p, w2tp,
-                     sp.hidden[1], wv[2], kp[2], y, s, h1, kp[1], d2, kp[2], d1, kp[1], slab, self.err_acc,
-                     ACT_IDS[sp.acts[0]], ACT_IDS[sp.acts[1]], ACT_IDS[sp.out_act], sp.loss_id,
-                     sp.flat_spot(sp.acts[0]), sp.flat_spot(sp.acts[1]), sp.flat_spot(sp.out_act), st)
-        nat.call_hip("shifu_colsum_fixed", slab, tiles, kp[2], part, gv[2], st)
-        self._grad_ready(2)
-        for l, dl, al in ((1, d2, h1), (0, d1, x)):
-            if self.wgrad_ring and ws["slab"] is not None and mc >= 4096:
-                nat.call_hip("shifu_wgrad_ring", dl, kp[l + 1], al, kp[l], gv[l], kp[l], mc, sp.hidden[l], kp[l],
-                             ws["slab"], ws["slab"].numel() * 4, st)
-            else:
-                ntiles = math.ceil(sp.hidden[l] / 128) * (kp[l] // 128)
-                spl = max(1, min(mc // 256, 1024 // max(1, ntiles)))
-                nat.call_hip("shifu_wgrad_tn", dl.data_ptr(), kp[l + 1], al.data_ptr(), kp[l], gv[l].data_ptr(),
-                             kp[l], mc, sp.hidden[l], kp[l], spl, st)
-            self._grad_ready(l)
-
     def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None, lane: int = 0, fwd_event=None):
-        if self.fused2 and getattr(self, "_f2w_cur", None) is not None:
-            return self._chunk_fused2(data, r0, r1, self._f2w_cur, x_dev=x_dev, lane=lane)
         from ..ops import _native as nat
         sp, kp = self.spec, self.spec.layer_kpad
         L = len(sp.hidden)

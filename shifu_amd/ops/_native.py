@@ -35,11 +35,6 @@ HIP_SIGNATURES = {
     "shifu_wgrad_tn": "plplpl" "iiiis",
     "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "p" "s",
     "shifu_colsum_fixed": "pii" "pp" "s",
-    # mlp_fused.hip
-    "shifu_mlp_fused2": "pl" "ii" "pli" "i" "pp" "i" "pi" "pp" "pl" "pl" "pl" "pp" "iiii" "fff" "s",
-    "shifu_fused_w2_prep": "pli" "pp" "s",
-    "shifu_mlp_fused2_tiles": ("i", "i"),
-    "shifu_mlp_fused2_set_stamps": ("p", None),
     "shifu_colsum_ws": ("ii", "l"),
     # corr_kernels.hip + gemm_kernels.hip corr_i8_kernel (K15)
     "shifu_corr_planes": "plii" "p" "ii" "pl" "pp" "s",

@@ -413,8 +413,7 @@ __device__ __forceinline__ void gemm8_prologue(const GemmArgs& p, const OffT (&o
 }
 
 // The 8-phase k-loop of one 256 x 256 output tile into acc (see the schedule above), after its
-// prologue DMAs.  extra16: the caller issued 16 vector-memory ops after the prologue (a persistent
-// kernel's epilogue stores of the previous tile), which the first wait leaves in flight.
+// prologue DMAs.
 // I8: the operands are int8 (a k-tile = 128 int8 per row = the same 128 B that hold 64 bf16, so the
 // staging is unchanged; p.K / p.lda stay in 2-byte units) and every MFMA is
 // v_mfma_i32_16x16x64_i8 -- acc then holds int32 bits.  A and B fragments take the same 16 bytes
@@ -422,7 +421,7 @@ __device__ __forceinline__ void gemm8_prologue(const GemmArgs& p, const OffT (&o
 // onto acc (several operand pairs summed into one tile).
 template <bool I8 = false, typename OffT = long>
 __device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8], const OffT (&off)[4][2],
-                                           char* smem, bool extra16 = false, bool zero = true, int extra = -1) {
+                                           char* smem, bool zero = true) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   const int nk = p.K / 64;
@@ -473,14 +472,8 @@ __device__ __forceinline__ void gemm8_loop(const GemmArgs& p, f32x4 (&acc)[4][8]
 #define G8_MMA(mh, nh, bq, on) do { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
     if ((on) && !(p.dbg & 64)) { __builtin_amdgcn_s_setprio(1); mma(mh, nh, bq); __builtin_amdgcn_s_setprio(0); } } while (0)
 
-  // even k-tile 0 landed (its 8 DMAs are the oldest), odd k-tile 1 B halves stay in flight (and
-  // extra16: the 16 epilogue stores a persistent kernel issued after the prologue)
-  // (extra: the number of vector-memory ops a persistent kernel issued after the prologue -- 16
-  // epilogue stores of the forward, 32 of the head -- which this first wait leaves in flight)
-  const int ex = extra >= 0 ? extra : (extra16 ? 16 : 0);
-  if (ex == 32) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-  else if (ex == 16) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  // even k-tile 0 landed (its 8 DMAs are the oldest), odd k-tile 1 B halves stay in flight
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   G8_BAR();
   if (wr == 1) G8_BAR();                      // stagger the two wave rows by one barrier
 
@@ -518,119 +511,6 @@ __device__ __forceinline__ void gemm8_mainloop(const GemmArgs& p, f32x4 (&acc)[4
   gemm8_src(p, m0, n0, off);
   gemm8_prologue(p, off, smem);
   gemm8_loop(p, acc, off, smem);
-}
-
-// ---------------------------------------------------------------------------------------
-// Persistent 8-phase forward (EPI_ACT / EPI_STORE): one block per CU walks its tiles; the next
-// tile's prologue DMAs are issued BEFORE the current tile's epilogue, which stages the bf16 tile
-// through the LDS that the prologue does not touch (buffer 1's A halves + the 32 KiB above the
-// ring) in two 128-row rounds and leaves as 16 bounds-checked buffer stores per thread -- so the
-// next tile's first loads, its launch, and this tile's stores overlap instead of serialising
-// (the fixed per-tile cost of gemm_nt_8ph_kernel: profiles/r3/mlp_lab_ablation_r3d.jsonl).
-// ---------------------------------------------------------------------------------------
-template <int EPI, int ACT>
-__device__ __forceinline__ void epilogue_256_persist(const GemmArgs& p, f32x4 (&acc)[4][8], int m0, int n0,
-                                                     char* smem) {
-  // the thread id through an opaque asm: the per-lane staging / store addresses are then computed
-  // here, not hoisted out of the persistent tile loop (where they would stay live across the
-  // k-loop and spill)
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  // bounds-checked stores (rows >= M dropped by the hardware): the store count is the same on
-  // every tile, which keeps the next loop's counted vmcnt exact
-  const int rows = min(256, p.M - m0);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.C + (size_t)m0 * p.ldc), (short)0, rows * (int)p.ldc * 2, 0x00020000);
-  const bool full = n0 + 256 <= (EPI == EPI_ACT ? p.n_valid : p.NB);
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if (wr == half) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int ml = j * 16 + (lane & 15);                        // row within the half
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = acc[i][j][r];
-            const int n = n0 + nl + r;
-            if (full) o[r] = EPI == EPI_ACT ? act_fwd(ACT, z) : z;
-            else if constexpr (EPI == EPI_ACT) o[r] = n < p.n_valid ? act_fwd(ACT, z) : ((n == p.n_valid && p.bias_col) ? 1.f : 0.f);
-            else o[r] = n < p.NB ? z : 0.f;
-          }
-          uint2 w;
-          w.x = pack_bf16x2(o[0], o[1]);
-          w.y = pack_bf16x2(o[2], o[3]);
-          const int c = nl >> 3, hb = (nl >> 2) & 1;
-          char* region = smem + (ml < 64 ? G8_BUF : 2 * G8_BUF);       // buf1 A halves | above the ring
-          *(uint2*)(region + (ml & 63) * 512 + ((c ^ (ml & 15)) << 4) + hb * 8) = w;
-        }
-      }
-    }
-    // raw barriers: a __syncthreads() would make hipcc drain the next tile's prologue DMAs
-    // (vmcnt(0)) -- only the LDS writes need to be complete (lgkmcnt(0))
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int c = tid & 31;
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int ml = pass * 16 + (tid >> 5);
-      const char* region = smem + (ml < 64 ? G8_BUF : 2 * G8_BUF);
-      const v4i_t v = *(const v4i_t*)(region + (ml & 63) * 512 + ((c ^ (ml & 15)) << 4));
-      const int m = half * 128 + ml;                                  // row within the tile
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)((size_t)m * p.ldc * 2 + (size_t)(n0 + c * 8) * 2), 0, 0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // staging reads done before reuse
-    __builtin_amdgcn_s_barrier();
-  }
-}
-
-template <int EPI, int ACT>
-__global__ __launch_bounds__(G8_T, 1) void gemm_nt_8ph_persist_kernel(GemmArgs p, int ntiles) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntn = (p.N + 255) / 256;
-  // tile t -> (m, n); logical block lb (XCD-remapped) walks t = lb, lb + G, ...: tiles t, t + 1
-  // (the two column tiles of a row block) run on one XCD and share the A rows in its L2
-  const int G = gridDim.x;
-  int t = xcd_remap(blockIdx.x, G);
-  if (t >= ntiles) return;
-  f32x4 acc[4][8];
-  {
-    long o0[4][2];
-    gemm8_src(p, (t / ntn) * 256, (t % ntn) * 256, o0);
-    gemm8_prologue(p, o0, smem);
-  }
-  bool first = true;
-  for (;;) {
-    {
-      long off[4][2];
-      gemm8_src(p, (t / ntn) * 256, (t % ntn) * 256, off);
-      gemm8_loop(p, acc, off, smem, !first);          // 16 stores of the previous epilogue in flight
-    }
-    const int tn = t + G;
-    if (tn < ntiles) {     // next tile's prologue first: lands in buffer 0 + buffer 1's B halves
-      long o2[4][2];
-      gemm8_src(p, (tn / ntn) * 256, (tn % ntn) * 256, o2);
-      gemm8_prologue(p, o2, smem);
-    }
-    if (p.dbg & 2) {                                  // lab: main loop only (acc kept live)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" :: "v"(acc[i][j]));
-    } else if (p.dbg & 128) {
-      epilogue_256_persist<EPI_STORE, 2>(p, acc, (t / ntn) * 256, (t % ntn) * 256, smem);   // lab: no activation
-    } else {
-      epilogue_256_persist<EPI, ACT>(p, acc, (t / ntn) * 256, (t % ntn) * 256, smem);
-    }
-    if (tn >= ntiles) return;
-    t = tn;
-    first = false;
-  }
 }
 
 template <int EPI, int ACT>
@@ -821,187 +701,6 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
     const uint4 v = *(const uint4*)(Cs + ml * 512 + ((c ^ (ml & 15)) << 4));
     if (n + 8 <= p.N) *(uint4*)(p.C + (size_t)m * p.ldc + n) = v;
     else *(uint2*)(p.C + (size_t)m * p.ldc + n) = make_uint2(v.x, v.y);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Persistent fused head: one block per CU walks row tiles t = lb, lb + G, ...; the next tile's
-// prologue DMAs are issued BEFORE this tile's epilogue (as the persistent forward does), and the
-// last-hidden deltas leave straight from the accumulator registers as 32 bounds-checked 8-B buffer
-// stores per lane (no LDS staging: the ring holds the next tile's first k-tile), which drain while
-// the next tile's main loop runs.  The epilogue's row partials / deltas / output-wgrad partials
-// live above the ring.  Same per-row semantics and the same fixed-point-free fp32 math as
-// gemm_head_8ph_kernel (its stage 1-3 arithmetic, in the same order).
-// ---------------------------------------------------------------------------------------
-constexpr int HEADP_STORES = 32;      // D stores per lane per tile (4 column blocks x 8 row blocks)
-
-template <int ACT>
-__device__ __forceinline__ void head_epilogue_regs(const GemmArgs& p, const HeadArgs& h, f32x4 (&acc)[4][8],
-                                                   int m0, float y_pf, float s_pf, char* smem) {
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));        // keep per-lane addressing local to the epilogue
-  const int lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  float* red = (float*)(smem + 2 * G8_BUF);          // [2 wr][4 wc][128] row partials of z_out
-  float* dl = red + 1024;                            // [256] output deltas
-  float* gred = dl + 256;                            // [2 wr][256] output-wgrad partials
-  double* ered = (double*)(gred + 512);              // [8 waves][2]
-  const int nv = p.n_valid;
-  float w3[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = wc * 64 + i * 16 + (lane >> 4) * 4 + r;
-      w3[i][r] = n < h.KH ? h.W[n] : 0.f;
-    }
-  float zp[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = wc * 64 + i * 16 + (lane >> 4) * 4 + r;
-        float a = n < nv ? act_fwd(ACT, acc[i][j][r]) : (n == nv ? 1.f : 0.f);
-        a = bf2f(f2bf(a));
-        acc[i][j][r] = a;
-        t += a * w3[i][r];
-      }
-    t += __shfl_xor(t, 16, 64);
-    t += __shfl_xor(t, 32, 64);
-    zp[j] = t;
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[(wr * 4 + wc) * 128 + j * 16 + lane] = zp[j];
-  }
-  // raw barriers: __syncthreads() would make hipcc drain the next tile's prologue DMAs
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  double e_c = 0.0, e_w = 0.0;
-  if (tid < 256) {
-    const int rw = tid >> 7, rl = tid & 127;
-    const float z = red[(rw * 4 + 0) * 128 + rl] + red[(rw * 4 + 1) * 128 + rl] + red[(rw * 4 + 2) * 128 + rl] +
-                    red[(rw * 4 + 3) * 128 + rl];
-    const int m = m0 + tid;
-    float dlt = 0.f;
-    if (m < p.M) {
-      const float y = y_pf, sg = s_pf;
-      const float a = act_fwd(h.out_act, z), e = y - a;
-      const int lm = h.loss % 3;                       // loss >= 3: TF objective as the error
-      if (lm == 1) {
-        dlt = e * sg;
-        const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
-        e_c = h.loss >= 3 ? -(__logf(a + 1e-7f) * y + __logf(1.f - a + 1e-7f) * (1.f - y)) * sg
-                          : -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y));
-      } else if (lm == 2) {
-        dlt = (y < a ? 1.f : -1.f) * (act_deriv_out(h.out_act, a) + h.flat_out) * sg;
-        e_c = fabsf(e) * sg;
-      } else {
-        dlt = (act_deriv_pre(h.out_act, z) + h.flat_out) * e * sg;
-        e_c = h.loss >= 3 ? (double)(e * e) * sg : (double)(e * sg) * (e * sg);
-      }
-      e_w = sg;
-    }
-    dl[tid] = dlt;
-  }
-  e_c = wave_sum_d(e_c);
-  e_w = wave_sum_d(e_w);
-  if (lane == 0) { ered[wid * 2] = e_c; ered[wid * 2 + 1] = e_w; }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  // D = delta_out * w_out * (f'(a) + flat) straight from registers: lane owns 4 consecutive
-  // columns of one row per (i, j); columns >= N get an out-of-range offset (dropped by the
-  // buffer bounds check: the store count stays uniform for the next tile's counted vmcnt)
-  const int rows = min(256, p.M - m0);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.C + (size_t)m0 * p.ldc), (short)0, rows * (int)p.ldc * 2, 0x00020000);
-  float gw[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) gw[i][r] = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int ml = wr * 128 + j * 16 + (lane & 15);
-    const float d = dl[ml];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nl = wc * 64 + i * 16 + (lane >> 4) * 4;
-      float o[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float a = acc[i][j][r];
-        gw[i][r] += d * a;
-        o[r] = (nl + r < nv) ? d * w3[i][r] * (act_deriv_out(ACT, a) + h.flat_hid) : 0.f;
-      }
-      const uint32_t lo = pack_bf16x2(o[0], o[1]), hi = pack_bf16x2(o[2], o[3]);
-      const int off = nl < p.N ? (int)((ml * p.ldc + nl) * 2) : 0x7ffffff0;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, (uint2){lo, hi}), rs, off, 0, 0);
-    }
-  }
-  if (tid == 0) {
-    double a0 = 0.0, a1 = 0.0;
-    for (int w = 0; w < 8; ++w) { a0 += ered[w * 2]; a1 += ered[w * 2 + 1]; }
-    atomicAdd(h.err, a0);
-    atomicAdd(h.err + 1, a1);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = gw[i][r];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      if ((lane & 15) == 0) gred[wr * 256 + wc * 64 + i * 16 + (lane >> 4) * 4 + r] = v;
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (tid < 256 && tid < h.KH) {
-    const float v = gred[tid] + gred[256 + tid];
-    if (h.GWslab) h.GWslab[(size_t)(m0 >> 8) * h.KH + tid] = v;     // tile index = row block
-    else atomicAdd(h.GW + tid, v);
-  }
-  // the row partials / deltas above the ring are rewritten by the next tile's epilogue only after
-  // its main loop, whose barriers order every wave's reads of this tile's values before it
-}
-
-template <int ACT>
-__global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_persist_kernel(GemmArgs p, HeadArgs h, int ntiles) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int G = gridDim.x;
-  int t = xcd_remap(blockIdx.x, G);
-  if (t >= ntiles) return;
-  {
-    long o0[4][2];
-    gemm8_src(p, t * 256, 0, o0);
-    gemm8_prologue(p, o0, smem);
-  }
-  bool first = true;
-  for (;;) {
-    const int m0 = t * 256;
-    const int my = min(m0 + (int)(threadIdx.x & 255), p.M - 1);
-    const float y_pf = h.Y[my], s_pf = h.S ? h.S[my] : 1.f;
-    f32x4 acc[4][8];
-    {
-      long off[4][2];
-      gemm8_src(p, m0, 0, off);
-      gemm8_loop(p, acc, off, smem, !first, true, first ? 0 : HEADP_STORES);
-    }
-    const int tn = t + G;
-    if (tn < ntiles) {        // next tile's prologue first: lands in buffer 0 + buffer 1's B halves
-      long o2[4][2];
-      gemm8_src(p, tn * 256, 0, o2);
-      gemm8_prologue(p, o2, smem);
-    }
-    head_epilogue_regs<ACT>(p, h, acc, m0, y_pf, s_pf, smem);
-    if (tn >= ntiles) return;
-    t = tn;
-    first = false;
   }
 }
 
@@ -1209,9 +908,6 @@ static int g_big = 0;        // large-M path: 0 = auto (8-phase for M >= 64K, N 
                              // 3 = 8-phase whenever M >= 64K and N >= 256, 4 = 128x128 only
 static int g_wg_interleave = 1;   // wgrad row splits: 1 interleaved 64-row steps (-3% wgrad1 at 1M rows), 0 contiguous
 static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
-static int g_fwd_persist = 1;     // persistent 8-phase forward (tune key 10; 0 = one tile per block)
-static int g_head_persist = 0;    // persistent fused head (tune key 11 / SHIFU_HEAD_PERSIST=1; measured
-                                  // 1.13 vs 1.10 ms per 2M-row chunk: off by default, profiles/r4)
 static int g_ring_nt = 1;         // persistent ring forward (gemm_ring_nt.hip, tune key 12; 2.2 vs 2.3-2.5 ms
                                   // for the 8-phase per-tile kernel per 2M-row chunk, profiles/r5)
 static int g_ring_nt_cap = 0;     // lab: grid cap of the ring forward (tune key 13; 0 = one block per CU)
@@ -1223,8 +919,6 @@ SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
   if (key == 2) { g_wg_interleave = val; return 0; }
   if (key == 9) { g_dbg = val; return 0; }
-  if (key == 10) { g_fwd_persist = val; return 0; }
-  if (key == 11) { g_head_persist = val; return 0; }
   if (key == 12) { g_ring_nt = val; return 0; }
   if (key == 13) { g_ring_nt_cap = val; return 0; }
   return -1;
@@ -1253,6 +947,10 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   if (epi == EPI_DACT && !act_deriv_from_output(act) && Hd == nullptr) return -3;
   if (epi == EPI_DACT && act_deriv_from_output(act) && H == nullptr) return -3;
   const bool dfo_act = act_deriv_from_output(act);
+  // persistent ring engine (forward).  dgrad stays on the 128 x 128 tile kernel: a ring dgrad
+  // (H row segments loaded into registers after the tile's last MMA segment) measured 1.81 vs
+  // 1.23 ms per 2M-row chunk (profiles/r5/NOTES_r5.md) -- with K = 256 a tile has 8 k-steps, and
+  // the H round trip at every tile end is exposed.
   if (g_ring_nt && M >= 65536 && (epi == EPI_STORE || (epi == EPI_ACT && dfo_act)) && !g_dbg) {
     const int r = shifu_ring_nt(A, lda, B, ldb, NB, C, ldc, M, N, K, epi, act, n_valid, bias_col, g_ring_nt_cap,
                                 stream);
@@ -1262,27 +960,6 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   if ((g_big == 3 || auto8) && M >= 65536 && N >= 256 && (epi == EPI_STORE || dfo_act)) {
     const int grid8 = ((M + 255) / 256) * ((N + 255) / 256);
     const size_t lds8 = 2 * G8_BUF;
-    // persistent only below 2 GiB of output: at the bench's 2M-row x 512 chunk the per-tile
-    // kernel measured 2.57 ms against 3.19 ms persistent (profiles/r4/mlp_lab_persist_r4t.jsonl;
-    // the epilogue's buffer resource itself spans one 256-row tile, so this is a speed choice)
-    if (g_fwd_persist && epi != EPI_DACT && M * (long)ldc * 2 < (1l << 31)) {
-      // persistent forward: one block per CU (LDS = the ring + 32 KiB of epilogue staging)
-      int dev = 0, ncu = 256;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      const int gridp = grid8 < ncu ? grid8 : ncu;
-      const size_t ldsp = 2 * G8_BUF + 32768;
-#define GEMMP_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_persist_kernel<E, A>), dim3(gridp), dim3(G8_T), ldsp, stream, p, grid8)
-      if (epi == EPI_ACT) {
-        switch (act) { case 0: GEMMP_L(EPI_ACT, 0); break; case 1: GEMMP_L(EPI_ACT, 1); break;
-          case 2: GEMMP_L(EPI_ACT, 2); break; case 3: GEMMP_L(EPI_ACT, 3); break; case 4: GEMMP_L(EPI_ACT, 4); break;
-          case 6: GEMMP_L(EPI_ACT, 6); break; case 9: GEMMP_L(EPI_ACT, 9); break;
-          default: GEMMP_L(EPI_ACT, 7); break; }
-      } else GEMMP_L(EPI_STORE, 2);
-#undef GEMMP_L
-      CHECK_HIP(hipGetLastError());
-      return 0;
-    }
 #define GEMM8_L(E, A) hipLaunchKernelGGL((gemm_nt_8ph_kernel<E, A>), dim3(grid8), dim3(G8_T), lds8, stream, p)
 #define GEMM8_ACTS(E) switch (act) { case 0: GEMM8_L(E, 0); break; case 1: GEMM8_L(E, 1); break; \
     case 2: GEMM8_L(E, 2); break; case 3: GEMM8_L(E, 3); break; case 4: GEMM8_L(E, 4); break; \
@@ -1325,21 +1002,6 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
              M, N, K, NB, n_valid, act, 1, 0.f, g_dbg};
   HeadArgs h{W, Y, S, GW, GWslab, err, KH, out_act, loss, flat_out, flat_hid};
   const int grid = (M + 255) / 256;
-  if (g_head_persist && !g_dbg && (long)M * ldd * 2 < (1l << 31)) {
-    int dev = 0, ncu = 256;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int gridp = grid < ncu ? grid : ncu;
-#define HEADP_L(A_) hipLaunchKernelGGL((gemm_head_8ph_persist_kernel<A_>), dim3(gridp), dim3(G8_T), HEAD_LDS, stream, \
-                                       p, h, grid)
-    switch (act) {
-      case 0: HEADP_L(0); break; case 1: HEADP_L(1); break; case 2: HEADP_L(2); break;
-      case 3: HEADP_L(3); break; case 4: HEADP_L(4); break; case 9: HEADP_L(9); break; default: HEADP_L(7); break;
-    }
-#undef HEADP_L
-    CHECK_HIP(hipGetLastError());
-    return 0;
-  }
 #define HEAD_L(A_) hipLaunchKernelGGL((gemm_head_8ph_kernel<A_>), dim3(grid), dim3(G8_T), HEAD_LDS, stream, p, h)
   switch (act) {
     case 0: HEAD_L(0); break; case 1: HEAD_L(1); break; case 2: HEAD_L(2); break;

@@ -127,57 +127,6 @@ def test_fused_head_matches_unfused(hidden, acts, loss, monkeypatch):
     assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
 
 
-@pytest.mark.parametrize("n", [70000 + 77, 300000])
-def test_persistent_head_bitwise_equals_per_tile_head(n):
-    """gemm_head_8ph_persist_kernel (next tile's prologue before the epilogue, deltas stored from
-    registers) computes exactly the per-tile head's gradients (same per-element arithmetic); only
-    the fp64 error atomics may differ in summation order."""
-    from shifu_amd.ops import _native as nat
-    spec = MLPSpec(n_in=120, hidden=[300, 200], acts=["sigmoid", "sigmoid"], n_out=1)
-    x, y, s = _mk(spec, n, seed=4)
-    res = []
-    for persist in (0, 1):
-        nat.call_hip("shifu_gemm_set_tune", 11, persist)
-        try:
-            t = MLPTrainer(spec, device="cuda", seed=9, chunk_rows=1 << 20)
-            d = t.prepare(x, y, s)
-            t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
-            torch.cuda.synchronize()
-            res.append((t.grad.clone(), t.err_acc.clone()))
-        finally:
-            nat.call_hip("shifu_gemm_set_tune", 11, 0)
-    assert torch.equal(res[0][0], res[1][0])
-    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-12, atol=0)
-
-
-def test_persistent_forward_bitwise_equals_per_tile():
-    """The persistent 8-phase forward (tune key 10; used below 2 GiB of output) writes exactly the
-    per-tile kernel's activations, bias column and padding."""
-    from shifu_amd.ops import _native as nat
-    M, K, N = (1 << 20) + 77, 1024, 512
-    g = torch.Generator(device="cuda").manual_seed(5)
-    A = (torch.randn(M, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
-    B = (torch.randn(N, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
-    outs = []
-    nat.call_hip("shifu_gemm_set_tune", 12, 0)              # the 8-phase kernels, not the ring forward
-    for persist in (0, 1):
-        C = torch.full((M, N), 7.0, device="cuda", dtype=torch.bfloat16)
-        nat.call_hip("shifu_gemm_set_tune", 10, persist)
-        try:
-            nat.call_hip("shifu_gemm_nt", A, K, B, K, 500, C, N, None, 0, None, 0, None, 0,
-                         M, N, K, 0, 0, 500, 1, 0.0, nat.stream_of(A))
-            torch.cuda.synchronize()
-        finally:
-            nat.call_hip("shifu_gemm_set_tune", 10, 1)
-            if persist == 1:
-                nat.call_hip("shifu_gemm_set_tune", 12, 1)
-        outs.append(C)
-    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
-    ref = torch.sigmoid(A[-300:].float() @ B[:500].float().t())
-    assert (outs[1][-300:, :500].float() - ref).abs().max().item() < 1e-2
-    assert torch.all(outs[1][:, 500] == 1.0) and torch.all(outs[1][:, 501:] == 0)
-
-
 @pytest.mark.parametrize("M,K,N,NB,nv,epi,act", [
     ((1 << 20) + 77, 1024, 512, 500, 500, 0, 0),       # the bench's first layer (sigmoid + bias column)
     (70000 + 33, 256, 512, 512, 512, 0, 1),           # K = 8 steps per tile, tanh, no partial columns
@@ -368,34 +317,3 @@ def test_nn_scoring_bf16_close_to_fp32():
     assert np.abs(a - b).max() <= 2e-2
 
 
-@pytest.mark.parametrize("hidden,acts,loss,n", [([500, 200], ["sigmoid", "sigmoid"], "squared", 70000 + 77),
-                                                ([450, 192], ["tanh", "tanh"], "log", 3 * 4096 + 5),
-                                                ([511, 255], ["relu", "sigmoid"], "absolute", 131072),
-                                                ([500, 200], ["sigmoid", "sigmoid"], "squared", 100)])
-def test_fused_mlp_step_matches_per_layer_kernels(hidden, acts, loss, n, monkeypatch):
-    """mlp_fused2_kernel (layer-1 fwd + layer-2 fwd + output/loss/deltas + layer-1 dgrad in one
-    row-block kernel, H1 / D2 kept on chip) against the per-layer kernels (8-phase forward, fused
-    head, dgrad GEMM): same gradients (bf16 intermediates, different fp32 summation order), same
-    error sums.  Covers a partial last row block, several chunks and a chunk below one block."""
-    spec = MLPSpec(n_in=1000, hidden=hidden, acts=acts, n_out=1, loss=loss)
-    x, y, s = _mk(spec, n, seed=21)
-    monkeypatch.setenv("SHIFU_FUSED_MLP", "1")
-    a = MLPTrainer(spec, device="cuda", seed=4, chunk_rows=65536)
-    monkeypatch.setenv("SHIFU_FUSED_MLP", "0")
-    b = MLPTrainer(spec, device="cuda", seed=4, chunk_rows=65536)
-    assert a.fused2 and not b.fused2
-    b.params.flat.copy_(a.params.flat)
-    da, db = a.prepare(x, y, s), b.prepare(x, y, s)
-    for t, d in ((a, da), (b, db)):
-        t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
-    torch.cuda.synchronize()
-    for va, vb in zip(a.params.views(a.grad), b.params.views(b.grad)):
-        r = (va - vb).norm() / vb.norm().clamp(min=1e-12)
-        assert r < 1e-2, float(r)
-    assert abs(float(a.err_acc[0]) - float(b.err_acc[0])) / float(b.err_acc[0]) < 1e-4
-    assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
-    # and bit-identical run to run (fixed-order output-wgrad partials, no float atomics)
-    g1 = a.grad.clone()
-    a.grad.zero_(); a.accumulate_gradients(da)
-    torch.cuda.synchronize()
-    assert torch.equal(g1, a.grad)

@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--env", nargs="*", default=[])
     ap.add_argument("--tune", nargs="*", default=[],
-                    help="GEMM tune settings applied per run, e.g. 10:0 10:1 (key 10: persistent forward)")
+                    help="GEMM tune settings applied per run, e.g. 12:0 12:1 (key 12: ring forward, 14: ring dgrad)")
     ap.add_argument("--big", type=int, nargs="*", default=[0],
                     help="shifu_gemm_set_big per run (0 auto, 3 8-phase whenever M >= 64K and N >= 256, 4 128x128)")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0],
