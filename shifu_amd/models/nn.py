@@ -599,10 +599,11 @@ class MLPTrainer:
                 ws["slab"] = torch.empty(need // 4, dtype=torch.float32, device=self.device)
         # head output-wgrad partials per 256-row tile + fixed-order reduction scratch (deterministic
         # replacement of the per-tile atomics, ops/csrc/gemm_kernels.hip colsum_fixed)
-        ws["gw_slab"] = ws["gw_part"] = None
+        ws["gw_slab"] = ws["gw_part"] = ws["err_slab"] = None
         if self.gpu and self.fused_head:
             tiles = -(-rows // 256)
             ws["gw_slab"] = torch.empty(tiles * kp[L], dtype=torch.float32, device=self.device)
+            ws["err_slab"] = torch.empty(tiles * 2, dtype=torch.float64, device=self.device)
             ws["gw_part"] = torch.empty(-(-tiles // 128) * kp[L], dtype=torch.float32, device=self.device)
         self._ws[lane] = ws
         return ws
@@ -744,7 +745,7 @@ class MLPTrainer:
                          dels[L].data_ptr(), kp[L], mc, kp[L], kp[lh], ACT_IDS[sp.acts[lh]], sp.hidden[lh],
                          wv[L].data_ptr(), y.data_ptr(), nat.ptr(s), gv[L].data_ptr(), self.err_acc.data_ptr(),
                          kp[L], ACT_IDS[sp.out_act], sp.loss_id, sp.flat_spot(sp.out_act),
-                         sp.flat_spot(sp.acts[lh]), nat.ptr(ws["gw_slab"]), st)
+                         sp.flat_spot(sp.acts[lh]), nat.ptr(ws["gw_slab"]), nat.ptr(ws["err_slab"]), st)
             if ws["gw_slab"] is not None:
                 nat.call_hip("shifu_colsum_fixed", ws["gw_slab"], -(-mc // 256), kp[L], ws["gw_part"],
                              gv[L].data_ptr(), st)

@@ -33,7 +33,7 @@ HIP_SIGNATURES = {
     # mlp_kernels.hip
     "shifu_gemm_nt": "plplipl" "plplpl" "iiiiiiif" "s",
     "shifu_wgrad_tn": "plplpl" "iiiis",
-    "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "p" "s",
+    "shifu_gemm_head": "plplipl" "iiiii" "ppppp" "iii" "ff" "pp" "s",
     "shifu_colsum_fixed": "pii" "pp" "s",
     "shifu_colsum_ws": ("ii", "l"),
     # corr_kernels.hip + gemm_kernels.hip corr_i8_kernel (K15)

@@ -545,7 +545,8 @@ struct HeadArgs {
   const float* S;        // [M] significance (nullable -> 1)
   float* GW;             // [KH] output-weight gradient (atomic; unused when GWslab is set)
   float* GWslab;         // [tiles][KH] per-tile partials (nullable): summed in fixed order afterwards
-  double* err;           // [2] error sum, weight sum (atomic)
+  double* err;           // [2] error sum, weight sum (atomic; unused when errslab is set)
+  double* errslab;       // [tiles][2] per-tile sums (nullable): summed in fixed order afterwards
   int KH, out_act, loss;
   float flat_out, flat_hid;
 };
@@ -642,8 +643,13 @@ __global__ __launch_bounds__(G8_T, 1) void gemm_head_8ph_kernel(GemmArgs p, Head
   if (tid == 0 && !(p.dbg & 1)) {
     double a0 = 0.0, a1 = 0.0;
     for (int w = 0; w < 8; ++w) { a0 += ered[w * 2]; a1 += ered[w * 2 + 1]; }
-    atomicAdd(h.err, a0);
-    atomicAdd(h.err + 1, a1);
+    if (h.errslab) {                                 // 2 fp64 atomics from every tile on one line
+      h.errslab[(size_t)(m0 >> 8) * 2] = a0;         // contended (~0.1 ms per 2M-row chunk)
+      h.errslab[(size_t)(m0 >> 8) * 2 + 1] = a1;
+    } else {
+      atomicAdd(h.err, a0);
+      atomicAdd(h.err + 1, a1);
+    }
   }
   if (p.dbg & 4) return;                             // lab: stages 1-2 only
   // 3. last-hidden deltas (bf16, staged through LDS) and the output-wgrad partials
@@ -988,19 +994,41 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   return 0;
 }
 
+// per-tile (error, weight) sums of the head -> err[0..1] in a fixed order (one block)
+__global__ __launch_bounds__(256) void err_slab_kernel(const double* slab, int T, double* err) {
+  __shared__ double sh[2][256];
+  double a0 = 0.0, a1 = 0.0;
+  for (int t = threadIdx.x; t < T; t += 256) { a0 += slab[2 * t]; a1 += slab[2 * t + 1]; }
+  sh[0][threadIdx.x] = a0;
+  sh[1][threadIdx.x] = a1;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      sh[0][threadIdx.x] += sh[0][threadIdx.x + w];
+      sh[1][threadIdx.x] += sh[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {              // the two chunk lanes add into the same err: atomic
+    atomicAdd(err, sh[0][0]);
+    atomicAdd(err + 1, sh[1][0]);
+  }
+}
+
 // Fused head (see gemm_head_8ph_kernel): A [M, K] last-hidden inputs, B [NB, K] last-hidden
 // weights (bf16), D out [M, N] deltas of the last hidden layer (N = padded width <= 256).
 SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, int NB, void* D, long ldd,
                               int M, int N, int K, int act, int n_valid, const float* W, const float* Y,
                               const float* S, float* GW, double* err, int KH, int out_act, int loss,
-                              float flat_out, float flat_hid, float* GWslab, hipStream_t stream) {
+                              float flat_out, float flat_hid, float* GWslab, double* errslab,
+                              hipStream_t stream) {
   if (K % 64 || N % 8 || N > 256 || KH > 256 || KH < n_valid + 1 || lda % 8 || ldb % 8 || ldd % 8 ||
       M <= 0 || NB <= 0 || NB > 256)
     return -1;
   if (!act_deriv_from_output(act) || act == 6 || out_act < 0 || out_act > 9) return -2;
   GemmArgs p{(const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)D, ldd, nullptr, 0, nullptr, 0, nullptr, 0,
              M, N, K, NB, n_valid, act, 1, 0.f, g_dbg};
-  HeadArgs h{W, Y, S, GW, GWslab, err, KH, out_act, loss, flat_out, flat_hid};
+  HeadArgs h{W, Y, S, GW, GWslab, err, (g_dbg & 1) ? nullptr : errslab, KH, out_act, loss, flat_out, flat_hid};
   const int grid = (M + 255) / 256;
 #define HEAD_L(A_) hipLaunchKernelGGL((gemm_head_8ph_kernel<A_>), dim3(grid), dim3(G8_T), HEAD_LDS, stream, p, h)
   switch (act) {
@@ -1008,6 +1036,7 @@ SHIFU_API int shifu_gemm_head(const void* A, long lda, const void* B, long ldb, 
     case 3: HEAD_L(3); break; case 4: HEAD_L(4); break; case 9: HEAD_L(9); break; default: HEAD_L(7); break;
   }
 #undef HEAD_L
+  if (h.errslab) hipLaunchKernelGGL(err_slab_kernel, dim3(1), dim3(256), 0, stream, h.errslab, grid, err);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
