@@ -47,9 +47,17 @@ def kernel_name(k) -> str:
 
 
 def gram(A: torch.Tensor, B: torch.Tensor, kernel: str, gamma: float, degree: int = 3,
-         coef0: float = 0.0) -> torch.Tensor:
-    """K[i, j] = k(A_i, B_j) (fp32, one GEMM + an elementwise map)."""
-    G = A @ B.t()
+         coef0: float = 0.0, sw=None) -> torch.Tensor:
+    """K[i, j] = k(A_i, B_j) (fp32, one GEMM + an elementwise map).  On the GPU the product is
+    the own MFMA GEMM over split-bf16 operands at fp32 accuracy (ops/gemm_ops.py, 6 terms);
+    ``sw``: B's split operand, built once by the caller for many row blocks of A."""
+    if A.is_cuda:
+        from ..ops.gemm_ops import SplitWeights, linear_fp32
+        A = A.float().contiguous()
+        sw = sw or SplitWeights(B.float(), None, 6)
+        G = linear_fp32(A, B, sw=sw)
+    else:
+        G = A @ B.t()
     if kernel == "linear":
         return G
     if kernel == "poly":
@@ -116,8 +124,12 @@ def train_svm(X, y, kernel="linear", C=1.0, gamma=1.0, degree=3, coef0=0.0, eps=
     n = len(s)
     Xd = torch.as_tensor(X, device=dev)
     K = torch.empty(n, n, dtype=torch.float32, device=dev)
+    sw = None
+    if dev.type == "cuda":
+        from ..ops.gemm_ops import SplitWeights
+        sw = SplitWeights(Xd.float(), None, 6)
     for r0 in range(0, n, 8192):
-        K[r0:r0 + 8192] = gram(Xd[r0:r0 + 8192], Xd, kernel, gamma, degree, coef0)
+        K[r0:r0 + 8192] = gram(Xd[r0:r0 + 8192], Xd, kernel, gamma, degree, coef0, sw=sw)
     Y = torch.as_tensor(s, dtype=torch.float64, device=dev)
     Cv = torch.as_tensor(C * cw, dtype=torch.float64, device=dev)
     alpha = torch.zeros(n, dtype=torch.float64, device=dev)

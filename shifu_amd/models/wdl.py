@@ -123,9 +123,10 @@ class _DeepMFMA(torch.autograd.Function):
             xs.append(C)
             ders.append(C2)
             wbs.append(wb)
-        hL = xs[-1][:, : dims[-1] + 1].float()                   # [n, h_L + 1] incl. the bias column
-        out = hL @ final[0]
-        ctx.save_for_backward(final, hL, *xs, *Ws)
+        # output neuron over [h_L | 1] (the bias column of xs[-1]): one wave per row (wdl_kernels.hip)
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        nat.call_hip("shifu_wdl_rowdot", xs[-1], kp[-1], n, dims[-1] + 1, final[0].float().contiguous(), out, st)
+        ctx.save_for_backward(final, *xs, *Ws)
         ctx.meta = (list(acts), dims, kp, ders, wbs, len(Ws))
         return out
 
@@ -135,14 +136,17 @@ class _DeepMFMA(torch.autograd.Function):
         from .nn import ACT_IDS
         acts, dims, kp, ders, wbs, L = ctx.meta
         saved = ctx.saved_tensors
-        final, hL = saved[0], saved[1]
-        xs, Ws = saved[2: 3 + L], saved[3 + L:]
-        n, dev = hL.shape[0], hL.device
-        st = nat.stream_of(hL)
+        final = saved[0]
+        xs, Ws = saved[1: 2 + L], saved[2 + L:]
+        n, dev = xs[-1].shape[0], xs[-1].device
+        st = nat.stream_of(xs[-1])
         g = g.contiguous().float()
-        g_final = (g @ hL)[None, :]
+        # output-weight gradient sum_i g_i [h_L | 1]_i: per-256-row partials + a fixed-order sum
+        g_final = torch.empty(1, dims[-1] + 1, dtype=torch.float32, device=dev)
+        part = torch.empty(max(1, -(-n // 256)) * (dims[-1] + 1), dtype=torch.float32, device=dev)
+        nat.call_hip("shifu_wdl_coldot", g, xs[-1], kp[-1], n, dims[-1] + 1, part, g_final, st)
         # output delta -> last hidden layer delta (elementwise; the output neuron is linear)
-        aL = hL[:, : dims[-1]]
+        aL = xs[-1][:, : dims[-1]].float()
         dl = ders[-1][:, : dims[-1]].float() if ders[-1] is not None else _deriv_from_out(acts[-1], aL)
         D = torch.zeros(n, kp[-1], dtype=torch.bfloat16, device=dev)
         D[:, : dims[-1]] = (g[:, None] * final[0, : dims[-1]][None, :]) * dl

@@ -91,6 +91,8 @@ HIP_SIGNATURES = {
     "shifu_tree_walk_coded": "pli" "pp" "p" "pi" "pp" "iiii" "pl" "p" "s",
     # wdl_kernels.hip
     "shifu_wdl_gather": "ipipipppppiipplppllls",
+    "shifu_wdl_rowdot": "pllipps",
+    "shifu_wdl_coldot": "ppllipps",
     # quantile_kernels.hip
     "shifu_pack_bits": "plip" "s",
     "shifu_qprep": "pllipid" "pppp" "s",

@@ -105,3 +105,67 @@ SHIFU_API int shifu_wdl_gather(int dir, const float* dense, int nd, const long* 
   CHECK_HIP(hipGetLastError());
   return 0;
 }
+
+// ---- Wide & Deep output neuron (WideAndDeep.java:163-232: a linear unit over [h_L | 1]) --------
+// forward  out[i]   = sum_j H[i][j] w[j]          (bf16 activations, fp32 weights / sums)
+// backward gw[j]    = sum_i g[i] H[i][j]          (per-256-row-block partials, then a fixed-order
+//                                                  sum over blocks: deterministic, no atomics)
+namespace {
+
+__global__ __launch_bounds__(256) void wdl_rowdot_kernel(const bf16_t* __restrict__ H, long ldh, long n, int k,
+                                                         const float* __restrict__ w, float* __restrict__ out) {
+  // one wave per row, lanes over the columns
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int j = lane; j < k; j += 64) s += bf2f(((const uint16_t*)H)[i * ldh + j]) * w[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[i] = s;
+}
+
+__global__ __launch_bounds__(256) void wdl_coldot_part_kernel(const float* __restrict__ g, const bf16_t* __restrict__ H,
+                                                              long ldh, long n, int k, float* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * 256, r1 = min(n, r0 + 256);
+  for (int j = threadIdx.x; j < k; j += 256) {
+    float s = 0.f;
+    for (long i = r0; i < r1; ++i) s += g[i] * bf2f(((const uint16_t*)H)[i * ldh + j]);
+    part[(long)blockIdx.x * k + j] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void wdl_coldot_final_kernel(const float* __restrict__ part, long nb, int k,
+                                                               float* __restrict__ gw) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= k) return;
+  float s = 0.f;
+  for (long b = 0; b < nb; ++b) s += part[b * k + j];
+  gw[j] = s;
+}
+
+}  // namespace
+
+SHIFU_API int shifu_wdl_rowdot(const void* H, long ldh, long n, int k, const float* w, float* out,
+                               hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (k <= 0 || ldh < k) return -1;
+  hipLaunchKernelGGL(wdl_rowdot_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, (const bf16_t*)H, ldh,
+                     n, k, w, out);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// part: >= ceil(n / 256) * k floats of scratch
+SHIFU_API int shifu_wdl_coldot(const float* g, const void* H, long ldh, long n, int k, float* part, float* gw,
+                               hipStream_t stream) {
+  if (k <= 0 || ldh < k || n < 0) return -1;
+  const long nb = (n + 255) / 256;
+  if (nb > 0)
+    hipLaunchKernelGGL(wdl_coldot_part_kernel, dim3((unsigned)nb), dim3(256), 0, stream, g, (const bf16_t*)H, ldh, n,
+                       k, part);
+  hipLaunchKernelGGL(wdl_coldot_final_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, stream, part, nb, k,
+                     gw);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}

@@ -86,3 +86,18 @@ def test_svm_gpu_batched_smo_matches_host_loop(kernel, monkeypatch):
     d = m1.decision(X, device="cuda")
     sgn = 1.0 if ref.classes_[1] == m1.labels[0] else -1.0
     np.testing.assert_allclose(sgn * d, d_ref, atol=5e-3 * max(1.0, float(np.abs(d_ref).max())))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["linear", "poly", "sigmoid", "rbf"])
+def test_gram_gpu_own_gemm_fp32_accurate(kernel):
+    """The GPU kernel matrix runs on the own split-bf16 MFMA GEMM (6 terms, fp32-accurate products):
+    within fp32 rounding of an fp64 reference."""
+    import torch
+    from shifu_amd.models import svm as S
+    g = np.random.default_rng(5)
+    A = g.normal(size=(3000, 37)).astype(np.float32)
+    B = g.normal(size=(1100, 37)).astype(np.float32)
+    K = S.gram(torch.as_tensor(A).cuda(), torch.as_tensor(B).cuda(), kernel, 0.05, 3, 0.5).cpu().double().numpy()
+    ref = S.gram(torch.as_tensor(A).double(), torch.as_tensor(B).double(), kernel, 0.05, 3, 0.5).numpy()
+    np.testing.assert_allclose(K, ref, rtol=2e-5, atol=2e-5 * max(1.0, float(np.abs(ref).max())))
