@@ -261,13 +261,16 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
     if dev.type == "cuda" and len(Ws) == 2 and Ws[1].shape[0] == 1 and W1.shape[0] <= 1024:
         # K14: S cached per row, rank-1 correction + activation + output neuron fused
         from ..ops import stats_ops
+        from ..ops import _native as nat
         acc = torch.zeros(F, 2, dtype=torch.float64, device=dev)
         W1t = W1.t().contiguous()
-        W2 = Ws[1][0, :-1].contiguous()
+        W2 = Ws[1][0, :-1].float().contiguous()
         b2 = float(Ws[1][0, -1])
         for xb in row_chunks(row_chunk * 16):
             S = first_layer(xb).contiguous()
-            base = act_fwd(acts[1], act_fwd(acts[0], S) @ W2 + b2).contiguous()
+            base = torch.empty(S.shape[0], dtype=torch.float32, device=dev)
+            nat.call_hip("shifu_rowdot_f32_act", S, S.stride(0), S.shape[0], S.shape[1], W2, b2, ACT_IDS[acts[0]],
+                         ACT_IDS[acts[1]], base, nat.stream_of(S))
             stats_ops.sensitivity_1h(S, xb, W1t, W2, b2, base, ACT_IDS[acts[0]], ACT_IDS[acts[1]], acc)
             n += xb.shape[0]
         s_abs, s_sq = acc[:, 0], acc[:, 1]
@@ -301,7 +304,8 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
                 for l in range(1, len(Ws)):
                     if l == len(Ws) - 1:          # output neuron: fp32 dot over the bf16 rows (a
                         k = Ws[l].shape[1]        # bf16-rounded output would put a noise floor on d)
-                        z = A[:, :k].float() @ Ws[l][0]
+                        z = torch.empty(M, dtype=torch.float32, device=dev)
+                        nat.call_hip("shifu_rowdot_bf16", A, A.stride(0), M, k, Ws[l][0].float().contiguous(), z, st)
                         return act_fwd(acts[l], z)
                     last = False
                     N, act = kin[l], ACT_IDS[acts[l]]

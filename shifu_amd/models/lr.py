@@ -55,6 +55,9 @@ class LRTrainer:
         return xd, yd, sd
 
     def _score(self, x):
+        if x.is_cuda:                          # own row-dot kernel (wdl_kernels.hip)
+            from ..ops import stats_ops
+            return torch.sigmoid(stats_ops.rowdot(x, self.w[:-1]) + self.w[-1])
         z = (x @ self.w[:-1].to(x.dtype)).float() + self.w[-1]
         return torch.sigmoid(z)
 
@@ -76,7 +79,11 @@ class LRTrainer:
             p = self._score(xb)
             e = yb - p
             d = e * (p * (1 - p) + FLAT_SPOT) * sb
-            g[: self.n_in] += (d.to(xb.dtype) @ xb).float()
+            if xb.is_cuda:                     # above K9's feature limit: own column-dot kernel
+                from ..ops import stats_ops
+                g[: self.n_in] += stats_ops.coldot(d, xb)
+            else:
+                g[: self.n_in] += (d.to(xb.dtype) @ xb).float()
             g[self.n_in] += d.sum()
             tail[0] += (e.double() * e.double()).sum()
         tail[1] = float(x.shape[0])

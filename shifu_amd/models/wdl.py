@@ -125,7 +125,7 @@ class _DeepMFMA(torch.autograd.Function):
             wbs.append(wb)
         # output neuron over [h_L | 1] (the bias column of xs[-1]): one wave per row (wdl_kernels.hip)
         out = torch.empty(n, dtype=torch.float32, device=dev)
-        nat.call_hip("shifu_wdl_rowdot", xs[-1], kp[-1], n, dims[-1] + 1, final[0].float().contiguous(), out, st)
+        nat.call_hip("shifu_rowdot_bf16", xs[-1], kp[-1], n, dims[-1] + 1, final[0].float().contiguous(), out, st)
         ctx.save_for_backward(final, *xs, *Ws)
         ctx.meta = (list(acts), dims, kp, ders, wbs, len(Ws))
         return out
@@ -144,7 +144,7 @@ class _DeepMFMA(torch.autograd.Function):
         # output-weight gradient sum_i g_i [h_L | 1]_i: per-256-row partials + a fixed-order sum
         g_final = torch.empty(1, dims[-1] + 1, dtype=torch.float32, device=dev)
         part = torch.empty(max(1, -(-n // 256)) * (dims[-1] + 1), dtype=torch.float32, device=dev)
-        nat.call_hip("shifu_wdl_coldot", g, xs[-1], kp[-1], n, dims[-1] + 1, part, g_final, st)
+        nat.call_hip("shifu_coldot_bf16", g, xs[-1], kp[-1], n, dims[-1] + 1, part, g_final, st)
         # output delta -> last hidden layer delta (elementwise; the output neuron is linear)
         aL = xs[-1][:, : dims[-1]].float()
         dl = ders[-1][:, : dims[-1]].float() if ders[-1] is not None else _deriv_from_out(acts[-1], aL)

@@ -91,8 +91,10 @@ HIP_SIGNATURES = {
     "shifu_tree_walk_coded": "pli" "pp" "p" "pi" "pp" "iiii" "pl" "p" "s",
     # wdl_kernels.hip
     "shifu_wdl_gather": "ipipipppppiipplppllls",
-    "shifu_wdl_rowdot": "pllipps",
-    "shifu_wdl_coldot": "ppllipps",
+    "shifu_rowdot_bf16": "pllipps",
+    "shifu_coldot_bf16": "ppllipps",
+    "shifu_rowdot_f32_act": "pllipfiips",
+    "shifu_coldot_f32": "ppllipps",
     # quantile_kernels.hip
     "shifu_pack_bits": "plip" "s",
     "shifu_qprep": "pllipid" "pppp" "s",

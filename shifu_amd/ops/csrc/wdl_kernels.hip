@@ -106,7 +106,8 @@ SHIFU_API int shifu_wdl_gather(int dir, const float* dense, int nd, const long* 
   return 0;
 }
 
-// ---- Wide & Deep output neuron (WideAndDeep.java:163-232: a linear unit over [h_L | 1]) --------
+// ---- Output-neuron row / column dots (the WDL output unit, WideAndDeep.java:163-232, a linear
+// unit over [h_L | 1]; the SE output neuron and base score, algos/varsel.py) ---------------------
 // forward  out[i]   = sum_j H[i][j] w[j]          (bf16 activations, fp32 weights / sums)
 // backward gw[j]    = sum_i g[i] H[i][j]          (per-256-row-block partials, then a fixed-order
 //                                                  sum over blocks: deterministic, no atomics)
@@ -135,6 +136,16 @@ __global__ __launch_bounds__(256) void wdl_coldot_part_kernel(const float* __res
   }
 }
 
+__global__ __launch_bounds__(256) void coldot_f32_part_kernel(const float* __restrict__ g, const float* __restrict__ X,
+                                                              long ldx, long n, int k, float* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * 256, r1 = min(n, r0 + 256);
+  for (int j = threadIdx.x; j < k; j += 256) {
+    float s = 0.f;
+    for (long i = r0; i < r1; ++i) s += g[i] * X[i * ldx + j];
+    part[(long)blockIdx.x * k + j] = s;
+  }
+}
+
 __global__ __launch_bounds__(256) void wdl_coldot_final_kernel(const float* __restrict__ part, long nb, int k,
                                                                float* __restrict__ gw) {
   const int j = blockIdx.x * 256 + threadIdx.x;
@@ -144,9 +155,37 @@ __global__ __launch_bounds__(256) void wdl_coldot_final_kernel(const float* __re
   gw[j] = s;
 }
 
+// out[i] = act_out(sum_j act_in(X[i][j]) w[j] + b)   (fp32 rows; act ids as models.nn.ACT_IDS,
+// act_in < 0: identity)
+__global__ __launch_bounds__(256) void rowdot_f32_act_kernel(const float* __restrict__ X, long ldx, long n, int k,
+                                                             const float* __restrict__ w, float b, int act_in,
+                                                             int act_out, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int j = lane; j < k; j += 64) {
+    const float x = X[i * ldx + j];
+    s += (act_in < 0 ? x : act_fwd(act_in, x)) * w[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[i] = act_out < 0 ? s + b : act_fwd(act_out, s + b);
+}
+
 }  // namespace
 
-SHIFU_API int shifu_wdl_rowdot(const void* H, long ldh, long n, int k, const float* w, float* out,
+SHIFU_API int shifu_rowdot_f32_act(const float* X, long ldx, long n, int k, const float* w, float b, int act_in,
+                                   int act_out, float* out, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (k <= 0 || ldx < k) return -1;
+  hipLaunchKernelGGL(rowdot_f32_act_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, X, ldx, n, k, w, b,
+                     act_in, act_out, out);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_rowdot_bf16(const void* H, long ldh, long n, int k, const float* w, float* out,
                                hipStream_t stream) {
   if (n <= 0) return 0;
   if (k <= 0 || ldh < k) return -1;
@@ -157,13 +196,26 @@ SHIFU_API int shifu_wdl_rowdot(const void* H, long ldh, long n, int k, const flo
 }
 
 // part: >= ceil(n / 256) * k floats of scratch
-SHIFU_API int shifu_wdl_coldot(const float* g, const void* H, long ldh, long n, int k, float* part, float* gw,
+SHIFU_API int shifu_coldot_bf16(const float* g, const void* H, long ldh, long n, int k, float* part, float* gw,
                                hipStream_t stream) {
   if (k <= 0 || ldh < k || n < 0) return -1;
   const long nb = (n + 255) / 256;
   if (nb > 0)
     hipLaunchKernelGGL(wdl_coldot_part_kernel, dim3((unsigned)nb), dim3(256), 0, stream, g, (const bf16_t*)H, ldh, n,
                        k, part);
+  hipLaunchKernelGGL(wdl_coldot_final_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, stream, part, nb, k,
+                     gw);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// the same over fp32 rows (LR gradient above K9's feature limit, models/lr.py)
+SHIFU_API int shifu_coldot_f32(const float* g, const float* X, long ldx, long n, int k, float* part, float* gw,
+                               hipStream_t stream) {
+  if (k <= 0 || ldx < k || n < 0) return -1;
+  const long nb = (n + 255) / 256;
+  if (nb > 0)
+    hipLaunchKernelGGL(coldot_f32_part_kernel, dim3((unsigned)nb), dim3(256), 0, stream, g, X, ldx, n, k, part);
   hipLaunchKernelGGL(wdl_coldot_final_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, stream, part, nb, k,
                      gw);
   CHECK_HIP(hipGetLastError());

@@ -214,6 +214,37 @@ def lr_grad(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor, s: torch.Tensor |
     return part.sum(0), ep.sum()
 
 
+def rowdot(x: torch.Tensor, w: torch.Tensor, b: float = 0.0, act_out: int = -1) -> torch.Tensor:
+    """act_out(x [n, k] @ w [k] + b) on the own row-dot kernels (bf16 or fp32 rows; fp32 out)."""
+    nat.require_gpu_native()
+    n, k = x.shape
+    out = torch.empty(n, dtype=torch.float32, device=x.device)
+    w = w.float().contiguous()
+    if x.dtype == torch.bfloat16:
+        nat.call_hip("shifu_rowdot_bf16", x, x.stride(0), n, k, w, out, nat.stream_of(x))
+        if b or act_out >= 0:
+            from ..models.nn import ACT_IDS, act_fwd
+            out = out + b
+            if act_out >= 0:
+                out = act_fwd({v: kk for kk, v in ACT_IDS.items()}[act_out], out)
+    else:
+        nat.call_hip("shifu_rowdot_f32_act", x.float(), x.stride(0), n, k, w, float(b), -1, act_out, out,
+                     nat.stream_of(x))
+    return out
+
+
+def coldot(d: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """sum_i d[i] x[i, :] -> [k] fp32 (per-256-row partials, fixed-order sum: deterministic)."""
+    nat.require_gpu_native()
+    n, k = x.shape
+    part = torch.empty(max(1, -(-n // 256)) * k, dtype=torch.float32, device=x.device)
+    out = torch.empty(k, dtype=torch.float32, device=x.device)
+    d = d.float().contiguous()
+    name = "shifu_coldot_bf16" if x.dtype == torch.bfloat16 else "shifu_coldot_f32"
+    nat.call_hip(name, d, x, x.stride(0), n, k, part, out, nat.stream_of(x))
+    return out
+
+
 def se_perturb(S: torch.Tensor, X: torch.Tensor, W1t: torch.Tensor, f0: int, fc: int, act: int, hpad: int,
                out: torch.Tensor | None = None) -> torch.Tensor:
     """Perturbed first hidden layer of every (row, input in [f0, f0+fc)) pair as bf16 MLP rows

@@ -101,6 +101,41 @@ def test_lr_grad_kernel(dtype, F):
     assert float(err) == pytest.approx(float((e * e).sum()), rel=1e-4)
 
 
+@pytest.mark.parametrize("dtype,F", [(torch.float32, 2500), (torch.bfloat16, 5000)])
+def test_lr_step_above_k9_limit_on_own_dot_kernels(dtype, F):
+    """Feature counts above K9's limit: the LR step's score / gradient run on the own row / column
+    dot kernels (no vendor GEMV), equal to the CPU trainer's step on the same data."""
+    from shifu_amd.models.lr import LRTrainer
+    g = torch.Generator().manual_seed(2)
+    n = 9000
+    x = torch.randn(n, F, generator=g).to(dtype).float()
+    y = (torch.rand(n, generator=g) > 0.5).float()
+    errs = {}
+    ws = {}
+    for dev in ("cpu", "cuda"):
+        t = LRTrainer(F, device=dev, propagation="R")
+        t.w.copy_((torch.randn(F + 1, generator=torch.Generator().manual_seed(3)) * 0.02).to(dev))
+        data = t.prepare(x, y) if hasattr(t, "prepare") else None
+        errs[dev] = [t.step(data) for _ in range(3)]
+        ws[dev] = t.w.cpu()
+    for a, b in zip(errs["cpu"], errs["cuda"]):
+        assert abs(a - b) / a < 1e-3, (errs)
+    assert float((ws["cpu"] - ws["cuda"]).abs().max()) < 1e-3
+
+
+def test_rowdot_coldot_kernels_match_torch():
+    from shifu_amd.ops import stats_ops
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for dt in (torch.float32, torch.bfloat16):
+        x = torch.randn(3001, 700, device="cuda", generator=g).to(dt)
+        w = torch.randn(700, device="cuda", generator=g)
+        d = torch.randn(3001, device="cuda", generator=g)
+        torch.testing.assert_close(stats_ops.rowdot(x, w), x.float() @ w, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(stats_ops.coldot(d, x), d @ x.float(), rtol=1e-4, atol=1e-3)
+        r = stats_ops.rowdot(x, w, 0.5, 0)                       # + bias, sigmoid
+        torch.testing.assert_close(r, torch.sigmoid(x.float() @ w + 0.5), rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("act", ["tanh", "sigmoid", "relu"])
 def test_sensitivity_kernel_matches_torch(act):
     from shifu_amd.algos import varsel as V
