@@ -95,6 +95,9 @@ HIP_SIGNATURES = {
     "shifu_coldot_bf16": "ppllipps",
     "shifu_rowdot_f32_act": "pllipfiips",
     "shifu_coldot_f32": "ppllipps",
+    # ga_kernels.hip
+    "shifu_ga_part_floats": ("llii", "l"),
+    "shifu_ga_head": "plliippppipl" "pp" "ii" "s",
     # quantile_kernels.hip
     "shifu_pack_bits": "plip" "s",
     "shifu_qprep": "pllipid" "pppp" "s",

@@ -5,6 +5,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 import torch
 
 
@@ -27,32 +28,26 @@ def test_generator_bands_and_sizes():
 
 
 def test_population_matches_independent_models():
-    from shifu_amd.algos.ga_varsel import PopulationMLP, population_errors
+    """The batched population (one dense masked first layer, RPROP per weight) trains every seed
+    exactly as that seed alone would: same validation error from the same initial weights."""
+    from shifu_amd.algos.ga_varsel import PopulationData, PopulationTrainer
     g = np.random.default_rng(1)
     X = g.normal(size=(300, 6)).astype(np.float32)
     y = (X[:, 0] + X[:, 3] > 0).astype(np.float32)
     w = np.ones(300, np.float32)
     valid = g.random(300) < 0.3
     masks = np.array([[1, 0, 0, 1, 0, 0], [0, 1, 1, 0, 0, 0], [1, 1, 1, 1, 1, 1]], bool)
-    errs = population_errors(X, y, w, valid, masks, hidden=4, epochs=15, seed=3)
-    # each seed alone (population of one with the same initial weights) gives the same error
-    gen = torch.Generator().manual_seed(3)
-    full = PopulationMLP(torch.as_tensor(masks), 4, "sigmoid", gen)
+    data = PopulationData(X, y, w, valid, "cpu")
+    full = PopulationTrainer(data, masks, 4, "sigmoid", 0.1, torch.Generator().manual_seed(3))
+    init = full.flat.clone()
+    errs = full.train(15)
+    W1 = init[: full.n1].view(full.PH, full.kx)
+    W2 = init[full.n1: full.n1 + full.PH].view(3, 4)
     for p in range(3):
-        m = PopulationMLP(torch.as_tensor(masks[p:p + 1]), 4, "sigmoid", torch.Generator().manual_seed(0))
-        with torch.no_grad():
-            m.W1.copy_(full.W1[p * 4:(p + 1) * 4])
-            m.W2.copy_(full.W2[p:p + 1])
-        opt = torch.optim.Rprop(m.parameters(), lr=0.1, etas=(0.5, 1.2), step_sizes=(1e-6, 50.0))
-        Xt, yt, vm = torch.tensor(X), torch.tensor(y)[:, None], torch.tensor(valid)
-        for _ in range(15):
-            opt.zero_grad()
-            (((m(Xt[~vm]) - yt[~vm]) ** 2).sum()).backward()
-            m.W1.grad.mul_(m.mask)
-            opt.step()
-        with torch.no_grad():
-            e = float(((m(Xt[vm]) - yt[vm]) ** 2).mean())
-        assert abs(e - errs[p]) < 1e-5
+        one = PopulationTrainer(data, masks[p:p + 1], 4, "sigmoid", 0.1, torch.Generator().manual_seed(0))
+        one.W1.copy_(W1[p * 4:(p + 1) * 4])
+        one.W2.copy_(W2[p:p + 1])
+        assert abs(float(one.train(15)[0]) - float(errs[p])) < 1e-6
     assert errs[0] < errs[1]               # the informative subset wins
 
 
@@ -73,3 +68,26 @@ def test_varsel_voted_pipeline(tmp_path, monkeypatch):
         assert main(cmd) == 0
     sel = [c for c in json.load(open("ColumnConfig.json")) if c["finalSelect"]]
     assert len(sel) == 3
+
+
+@pytest.mark.gpu
+def test_population_gpu_matches_cpu_oracle():
+    """The population on the own kernels (MFMA forward, ga_kernels.hip heads, ring wgrad,
+    optimizer_kernel RPROP) against the torch CPU oracle of the same arithmetic: per-seed
+    validation errors within 1e-3 relative."""
+    from shifu_amd.algos.ga_varsel import PopulationData, PopulationTrainer
+    g = np.random.default_rng(4)
+    n, F, P, E, H = 20000, 300, 40, 60, 10
+    X = g.normal(size=(n, F)).astype(np.float32)
+    y = (X[:, 0] - X[:, 7] + 0.5 * X[:, 11] > 0).astype(np.float32)
+    w = (g.random(n) + 0.5).astype(np.float32)
+    valid = g.random(n) < 0.2
+    masks = np.zeros((P, F), bool)
+    for p in range(P):
+        masks[p, g.choice(F, E, replace=False)] = True
+    errs = {}
+    for dev in ("cpu", "cuda"):
+        data = PopulationData(X, y, w, valid, dev)
+        errs[dev] = PopulationTrainer(data, masks, H, "sigmoid", 0.1, torch.Generator().manual_seed(9)).train(5)
+    rel = np.abs(errs["cuda"] - errs["cpu"]) / errs["cpu"]
+    assert rel.max() < 1e-3, (rel.max(), errs)
