@@ -799,9 +799,26 @@ def bench_pipeline(a, dev, info):
                 ms_ = ModelSet(root)
                 _join_scores([("nn", ms_)], [ms_.mc.dataSet], os.path.join(root, "joined"))
             step("x_combo_join", _join)
+        elif x == "encode":
+            # a small GBT on the same data (setup, untimed), then the streamed leaf-path encode
+            from shifu_amd.config.model_config import ModelConfig
+            mc_ = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+            mc_.train["algorithm"] = "GBT"
+            mc_.train["params"] = {"TreeNum": 10, "MaxDepth": 5, "LearningRate": 0.1, "Loss": "squared",
+                                   "Impurity": "variance", "FeatureSubsetStrategy": "ALL", "MinInstancesPerNode": 5}
+            mc_.save()
+            step("x_encode_setup_norm", lambda: api.NormStep(root).process())
+            step("x_encode_setup_train", lambda: api.TrainStep(root).process())
+
+            def _enc():
+                from shifu_amd.steps.misc import run_encode
+                run_encode(root)
+            step("x_encode", _enc)
+            times.pop("x_encode_setup_norm")
+            times.pop("x_encode_setup_train")
         else:
             raise ValueError(f"unknown --pipeline-extra step {x}")
-        extra[x] = times.pop("x_autotype_scan" if x == "autotype" else "x_combo_join")
+        extra[x] = times.pop({"autotype": "x_autotype_scan", "join": "x_combo_join", "encode": "x_encode"}[x])
     recall = None
     if info.rank == 0:
         import numpy as np
@@ -943,7 +960,7 @@ def main():
     ap.add_argument("--pipeline-eval-rows", type=int, default=None,
                     help="pipeline: eval set rows (default a quarter of --rows; the reference's eval is 20M rows)")
     ap.add_argument("--pipeline-extra", default="",
-                    help="pipeline: extra timed steps after it, comma list of autotype, join")
+                    help="pipeline: extra timed steps after it, comma list of autotype, join, encode")
     ap.add_argument("--pipeline-epochs", type=int, default=40,
                     help="pipeline: numTrainEpochs of the NN (varsel SE trains half of them)")
     a = ap.parse_args()

@@ -143,9 +143,9 @@ class Column:
 
 
 def _java_num_str(v: float) -> str:
-    if v == int(v) and abs(v) < 1e15:
-        return str(int(v)) if False else repr(v)
-    return repr(v)
+    """A parsed numeric value as text (shortest round-trip digits, like Double.toString for the
+    common range); a numpy scalar is converted first (numpy 2's repr is 'np.float64(...)')."""
+    return repr(float(v))
 
 
 @dataclass

@@ -107,9 +107,11 @@ def _num(v, default):
 class TrainSet:
     """Host-side (memory-mapped) training arrays of this rank's shard."""
 
-    def __init__(self, X=None, codes=None, y=None, w=None, meta=None, vX=None, vcodes=None, vy=None, vw=None):
+    def __init__(self, X=None, codes=None, y=None, w=None, meta=None, vX=None, vcodes=None, vy=None, vw=None,
+                 row0: int = 0):
         self.X, self.codes, self.y, self.w, self.meta = X, codes, y, w, meta or {}
         self.vX, self.vcodes, self.vy, self.vw = vX, vcodes, vy, vw
+        self.row0 = int(row0)          # global index of this shard's first row (per-row draws)
 
     @property
     def n(self):
@@ -168,8 +170,9 @@ def load_train_set(ms: ModelSet, is_tree: bool) -> TrainSet:
         dist.barrier()
         cache = load_dataset_cache(tmp_t if is_tree else tmp_x)
     meta, arr = cache
+    ntot = len(arr["y"])
     ts = TrainSet(X=_shard(arr.get("X"), info), codes=_shard(arr.get("codes"), info), y=_shard(arr["y"], info),
-                  w=_shard(arr["w"], info), meta=meta)
+                  w=_shard(arr["w"], info), meta=meta, row0=ntot * info.rank // info.world_size)
     vc = load_dataset_cache(ms.pf.cleaned_validation_data if is_tree else ms.pf.normalized_validation_data)
     if vc is not None:
         vc = _subset_cache(*vc, want, is_tree)
@@ -180,34 +183,50 @@ def load_train_set(ms: ModelSet, is_tree: bool) -> TrainSet:
     return ts
 
 
+def _poisson_from_uniform(u: np.ndarray, lam: float) -> np.ndarray:
+    """Poisson(lam) draws by inversion of the given uniforms (per-row, counter-based)."""
+    k = np.zeros(len(u), np.float32)
+    p = np.full(len(u), np.exp(-lam))
+    c = p.copy()
+    for i in range(1, 64):
+        more = u > c
+        if not more.any():
+            break
+        k += more
+        p = p * lam / i
+        c = c + p
+    return k
+
+
 def split_masks(mc, ts: TrainSet, bag: int, n_kfold: int, seed: int):
-    """-> (train_mask, valid_mask, sample_weight) for one bag (AbstractNNWorker :667-800)."""
+    """-> (train_mask, valid_mask, sample_weight) for one bag (AbstractNNWorker :667-800).  Every
+    per-row draw (validation split, bagging) is a counter-based function of the row's GLOBAL index
+    (``purifier.row_uniform``), so the split is the same in one process and over any number of
+    data-parallel ranks (each rank holds rows [ts.row0, ts.row0 + n))."""
+    from ..data.purifier import row_uniform
     n = ts.n
     tr = mc.train
-    rng = np.random.default_rng(seed * 7919 + bag)
+    base = (seed * 7919 + bag) * 4
     y = np.asarray(ts.y)
     if n_kfold and n_kfold > 0:
-        fold = (np.arange(n) * 2654435761 % (1 << 32)) % n_kfold        # row-hash fold id
+        gid = np.arange(ts.row0, ts.row0 + n, dtype=np.uint64)
+        fold = ((gid * np.uint64(2654435761)) % np.uint64(1 << 32)) % np.uint64(n_kfold)   # row-hash fold id
         valid = fold == bag
     elif ts.vy is not None:
         valid = np.zeros(n, dtype=bool)
     else:
+        # stratifiedSample: a per-row draw at the same rate keeps every class's share in
+        # expectation, which is what the reference's per-class sampling does
         rate = float(tr.get("validSetRate", 0.2) or 0.0)
-        if bool(tr.get("stratifiedSample", False)):
-            valid = np.zeros(n, dtype=bool)
-            for cls in np.unique(y):
-                idx = np.nonzero(y == cls)[0]
-                valid[idx] = rng.random(len(idx)) < rate
-        else:
-            valid = rng.random(n) < rate
+        valid = row_uniform(base, ts.row0, n) < rate
     train = ~valid
     rate = float(tr.get("baggingSampleRate", 1.0))
     if n_kfold and n_kfold > 0:
         sw = np.ones(n, np.float32)
     elif bool(tr.get("baggingWithReplacement", False)):
-        sw = rng.poisson(rate, n).astype(np.float32)
+        sw = _poisson_from_uniform(row_uniform(base + 1, ts.row0, n), rate)
     else:
-        sw = (rng.random(n) <= rate).astype(np.float32) if rate < 1.0 else np.ones(n, np.float32)
+        sw = (row_uniform(base + 2, ts.row0, n) <= rate).astype(np.float32) if rate < 1.0 else np.ones(n, np.float32)
     if bool(tr.get("sampleNegOnly", False)) and mc.is_binary():
         sw = np.where(y > 0.5, 1.0, sw).astype(np.float32)
     up = float(tr.get("upSampleWeight", 1.0) or 1.0)

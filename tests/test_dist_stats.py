@@ -142,7 +142,7 @@ def _rank_cli_guarded(rank, world, port, root, verb, gpu):
         raise SystemExit(rc)
 
 
-def _guarded_pipeline(tmp_path, gpu):
+def _guarded_pipeline(tmp_path, gpu, world=2):
     from shifu_amd.config.model_config import ModelConfig
     from shifu_amd.steps.create import run_init
     from shifu_amd.utils.synthetic import make_model_set
@@ -156,7 +156,7 @@ def _guarded_pipeline(tmp_path, gpu):
         f.write("id\n")                                 # a champion score column: the max goes over ranks
     run_init(root)
     for verb in ("stats", "norm", "varsel", "train", "posttrain", "eval"):
-        mp.start_processes(_rank_cli_guarded, args=(2, _port(), root, verb, gpu), nprocs=2, join=True,
+        mp.start_processes(_rank_cli_guarded, args=(world, _port(), root, verb, gpu), nprocs=world, join=True,
                            start_method="spawn")
     assert os.path.exists(os.path.join(root, "evals", "Eval1", "EvalMetaScore", "idEvalPerformance.json"))
     return root
@@ -169,12 +169,13 @@ def test_cli_two_ranks_device_collective_guard(tmp_path):
 
 
 @pytest.mark.gpu
-def test_cli_two_ranks_device_collectives_gpu(tmp_path):
-    """The same two ranks on one GPU (gloo transport, guard on): a collective over a host tensor,
+@pytest.mark.parametrize("world", [2, 4])
+def test_cli_ranks_device_collectives_gpu(tmp_path, world):
+    """2 or 4 ranks on one GPU (gloo transport, guard on): a collective over a host tensor,
     which RCCL would reject (the r3 eval champion-score crash), raises here."""
     import torch
     assert torch.cuda.is_available()
-    _guarded_pipeline(tmp_path, gpu=True)
+    _guarded_pipeline(tmp_path, gpu=True, world=world)
 
 
 @pytest.mark.parametrize("alg,shuffle", [("NN", False), ("NN", True), ("GBT", False)])
