@@ -150,12 +150,16 @@ class GpuBlockParser:
         self.times = {"h2d": 0.0, "index": 0.0, "kernel": 0.0, "fallback": 0.0, "host_cols": 0.0}
 
     def uploads(self, blocks):
-        """(offset, block) -> (offset, block, device copy of the block): the H2D stage of the
-        streamed read (its own thread and stream; a copy is complete when yielded)."""
+        """(key, block) -> (key, block, device copy of the block): the H2D stage of the streamed
+        read (its own thread and stream; a copy is complete when yielded).  A None block (an
+        indivisible gz / parquet unit) passes through."""
         import torch
         if self.h2d_stream is None:
             self.h2d_stream = torch.cuda.Stream(self.dev)
         for off, data in blocks:
+            if data is None:
+                yield off, None, None
+                continue
             L = len(data)
             if L == 0 or L >= (1 << 31) - 64:
                 yield off, data, None
@@ -165,7 +169,11 @@ class GpuBlockParser:
                 dbuf = torch.empty(L + 64, dtype=torch.uint8, device=self.dev)
                 dbuf[:L].copy_(torch.from_numpy(np.frombuffer(data, dtype=np.uint8)), non_blocking=True)
                 self.h2d_stream.synchronize()
-            self.times["h2d"] += time.perf_counter() - t0
+            t1 = time.perf_counter()
+            self.times["h2d"] += t1 - t0
+            from . import stream as _S
+            if _S.TRACE_ON:
+                _S.TRACE.append(("h2d", "upload", t0, t1))
             yield off, data, dbuf
 
     def parse(self, data, nthreads: int, dbuf=None):

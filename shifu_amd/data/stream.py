@@ -58,6 +58,26 @@ def byte_ranges(files, rank: int = 0, world: int = 1):
 
 
 READ_THREADS = int(os.environ.get("SHIFU_READ_THREADS", "8"))   # parallel preads per block
+# SHIFU_STREAM_TRACE=1: every pipeline stage appends (stage, thread, t_start, t_end) per block to
+# TRACE (tools/stream_trace_lab.py turns them into a per-stage overlap table)
+TRACE_ON = os.environ.get("SHIFU_STREAM_TRACE") == "1"
+TRACE: list = []
+
+
+class _span:
+    __slots__ = ("stage", "t0")
+
+    def __init__(self, stage):
+        self.stage = stage
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        if TRACE_ON:
+            TRACE.append((self.stage, threading.current_thread().name, self.t0, time.perf_counter()))
+        return False
 READ_STATS = {"read_s": 0.0, "bytes": 0}          # cumulative pread time / bytes (logged per pass)
 
 
@@ -207,6 +227,7 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
     files = list_data_files(plan.data_path)
     if not files:
         raise FileNotFoundError(f"no data under {plan.data_path}")
+    units = []
     for fi, path, a, b in byte_ranges(files, rank, world):
         if resume is not None:
             if fi < resume[0]:
@@ -215,25 +236,27 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
                 a = max(a, resume[1])
                 if a >= b:
                     continue
-        if a is None:                              # indivisible unit
-            if path.endswith(".parquet"):
-                yield (fi, 0), _parse_parquet(path, plan.header, kinds, plan.missing)
+        units.append((fi, path, a, b))
+
+    # ONE read | upload | parse pipeline over all of the rank's units, so the stages stay busy
+    # across file boundaries (a pipeline per file drained and refilled at every part file:
+    # tools/stream_trace_lab.py).  The reads run on their own thread, PREFETCH_READ blocks ahead
+    # (preads and the native parser release the GIL); PREFETCH_READ + 2 rotating buffers per file
+    # (+2 more with the GPU upload stage in between: block k's buffer is refilled only after
+    # block k has been parsed).  An indivisible unit (gz / parquet) passes through as a marker
+    # and is parsed whole on the host, in order.
+    def blocks():
+        for fi, path, a, b in units:
+            if a is None:
+                yield (fi, 0, path), None
                 continue
-            with gzip.open(path, "rb") as fh:
-                data = fh.read()
-            if plan.skip_header_line and fi == 0:
-                nl = data.find(b"\n")
-                data = data[nl + 1:] if nl >= 0 else b""
-            yield (fi, 0), parse_block(data, plan.delim, kinds, plan.missing, nthreads)
-            continue
-        # the file reads run on their own thread, PREFETCH_READ blocks ahead of the parse (readinto
-        # and the native parser both release the GIL).  PREFETCH_READ + 2 buffers: the block being
-        # parsed (its parse copies everything out before the next block is requested), the queued
-        # ones and the one being filled.  GPU parse: a third stage between them copies each block
-        # to HBM on its own thread / stream (read | H2D | parse overlap), two more buffers in flight
-        def lines():
-            for off, data in _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + (4 if pinned else 2),
-                                             pinned=pinned):
+            it = _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + (4 if pinned else 2), pinned=pinned)
+            while True:
+                with _span("read"):
+                    nxt = next(it, None)
+                if nxt is None:
+                    break
+                off, data = nxt
                 if plan.skip_header_line and fi == 0 and off == 0:
                     nl = bytes(data[: 1 << 20]).find(b"\n")
                     if nl < 0 and len(data) > (1 << 20):      # a header line wider than 1 MiB
@@ -241,14 +264,35 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
                     data = data[nl + 1:] if nl >= 0 else b""
                     if not len(data):
                         continue
-                yield off, data
-        blocks = prefetched(lines, PREFETCH_READ) if PREFETCH_READ > 0 else lines()
-        if pinned:
-            for off, data, dbuf in prefetched(lambda: gpu.uploads(blocks), 1):
-                yield (fi, off), gpu.parse(data, nthreads, dbuf)
-        else:
-            for off, data in blocks:
-                yield (fi, off), parse(data)
+                yield (fi, off, None), data
+
+    def whole_unit(fi, path):
+        if path.endswith(".parquet"):
+            return _parse_parquet(path, plan.header, kinds, plan.missing)
+        with gzip.open(path, "rb") as fh:
+            data = fh.read()
+        if plan.skip_header_line and fi == 0:
+            nl = data.find(b"\n")
+            data = data[nl + 1:] if nl >= 0 else b""
+        return parse_block(data, plan.delim, kinds, plan.missing, nthreads)
+
+    src = prefetched(blocks, PREFETCH_READ) if PREFETCH_READ > 0 else blocks()
+    if pinned:
+        for (fi, off, path), data, dbuf in prefetched(lambda: gpu.uploads(src), 1):
+            if data is None:
+                yield (fi, 0), whole_unit(fi, path)
+                continue
+            with _span("parse"):
+                part = gpu.parse(data, nthreads, dbuf)
+            yield (fi, off), part
+    else:
+        for (fi, off, path), data in src:
+            if data is None:
+                yield (fi, 0), whole_unit(fi, path)
+                continue
+            with _span("parse"):
+                part = parse(data)
+            yield (fi, off), part
 
 
 def gpu_parser(plan: DatasetPlan, gpu_cols, dev):
@@ -391,7 +435,8 @@ def iter_model_data(mc, plan: DatasetPlan, chunk_bytes: int = DEFAULT_CHUNK_BYTE
         for key, table in iter_tables(plan, chunk_bytes, rank, world,
                                       resume=None if resume is None else resume[:2], gpu=gp):
             n = table.n
-            md = finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, r)
+            with _span("purify"):
+                md = finish_table(mc, plan, table, sample_rate, sample_neg_only, seed, require_target, r)
             k = (key[0], key[1], r)
             r += n
             if md.n:

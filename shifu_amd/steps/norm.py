@@ -201,10 +201,12 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
             gpu_cols = [c.name for c in cols if not c.is_categorical()] if dev is not None else None
             for md in DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, sample_rate, neg_only, seed,
                                          row0=row0, gpu_cols=gpu_cols, dev=dev):
-                res = nplan.run(md.table)
-                y, w = md.y.astype(np.float32), md.w.astype(np.float32)
-                if pending is not None:
-                    pending.result()
+                with DS._span("consume"):
+                    res = nplan.run(md.table)
+                    y, w = md.y.astype(np.float32), md.w.astype(np.float32)
+                with DS._span("write_wait"):
+                    if pending is not None:
+                        pending.result()
                 pending = ex.submit(write, res, y, w)
                 n_local += md.n
                 for k, v in md.counters.as_dict().items():
