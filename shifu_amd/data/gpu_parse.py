@@ -222,8 +222,7 @@ class GpuBlockParser:
             dbuf[:L].copy_(torch.from_numpy(host))
         t1 = time.perf_counter()
         T["h2d"] += t1 - t0
-        d = dbuf[:L]
-        ends = torch.nonzero(d == 10).flatten()
+        ends = self._newlines(dbuf, L)
         if int(host[-1]) != 10:
             ends = torch.cat([ends, torch.tensor([L], dtype=torch.long, device=self.dev)])
         nl = int(ends.numel())
@@ -289,6 +288,25 @@ class GpuBlockParser:
         blk = DeviceBlock(vals)
         out.update({c: ("num", DevRef(blk, j), []) for j, c in enumerate(self.gpu_cols)})
         return n, bad, out
+
+    def _newlines(self, dbuf, L: int):
+        """int64 positions of every '\\n' in dbuf[:L] (own kernels, csv_kernels.hip: segment
+        counts, one scan, ordered writes; one host read of the count)."""
+        import torch
+        from ..ops import _native as nat
+        h = nat.hip()
+        need = int(h.shifu_newline_ws_bytes(L))
+        if getattr(self, "_nl_ws", None) is None or self._nl_ws.numel() < need:
+            self._nl_ws = torch.empty(need + 64, dtype=torch.uint8, device=self.dev)
+        ws = self._nl_ws
+        st = nat.stream_of(dbuf)
+        nat.call_hip("shifu_newline_count", dbuf, L, ws, st)
+        o = int(h.shifu_newline_count_offset(L))
+        cnt = int(ws[o:o + 8].view(torch.int64).item())
+        ends = torch.empty(cnt, dtype=torch.long, device=self.dev)
+        if cnt:
+            nat.call_hip("shifu_newline_write", dbuf, L, ws, ends, st)
+        return ends
 
     def summary(self) -> str:
         s = self.stats

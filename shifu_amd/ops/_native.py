@@ -55,6 +55,10 @@ HIP_SIGNATURES = {
     # csv_kernels.hip
     "shifu_csv_gpu_parse": "pppl" "pi" "pl" "p" "pip" "iiP" "pp" "s",
     "shifu_transpose_cast": "plpiiis",
+    "shifu_newline_ws_bytes": ("l", "l"),
+    "shifu_newline_count_offset": ("l", "l"),
+    "shifu_newline_count": "plps",
+    "shifu_newline_write": "plpps",
     # svm_kernels.hip
     "shifu_svm_smo": "pl" "ppp" "pp" "ii" "dd" "pp" "s",
     # gemm_ring.hip

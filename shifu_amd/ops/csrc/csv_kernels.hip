@@ -221,3 +221,132 @@ SHIFU_API int shifu_csv_gpu_parse(const void* buf, const long* ls, const long* l
   CHECK_HIP(hipGetLastError());
   return 0;
 }
+
+// ---- newline index: positions of every '\n' of a block in HBM (the line table the parse kernel
+// takes).  Three launches, all on the device: per 64 KiB segment a count, one exclusive scan of
+// the segment counts (one workgroup), then each segment's positions written in order (per-thread
+// 256-byte runs, workgroup prefix of the run counts).  Replaces torch.nonzero(buf == '\n').
+namespace {
+
+constexpr int NL_SEG = 65536;                 // bytes per segment = 256 threads x 256 bytes
+constexpr int NL_RUN = 256;
+
+__device__ __forceinline__ int nl_count_run(const uint8_t* p, long len) {
+  int c = 0;
+  if (len == NL_RUN) {
+#pragma unroll
+    for (int i = 0; i < NL_RUN / 16; ++i) {
+      const uint4 v = ((const uint4*)p)[i];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x = w[k] ^ 0x0a0a0a0au;                       // zero byte <=> '\n'
+        c += __builtin_popcount(~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu));
+      }
+    }
+  } else {
+    for (long i = 0; i < len; ++i) c += p[i] == '\n';
+  }
+  return c;
+}
+
+__device__ __forceinline__ int nl_block_excl_scan(int v, int* sh, int* total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int u = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += u;
+    __syncthreads();
+  }
+  const int incl = sh[t];
+  *total = sh[255];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ __launch_bounds__(256) void nl_count_kernel(const uint8_t* __restrict__ buf, long L, int* __restrict__ cnt) {
+  __shared__ int sh[256];
+  const long a = (long)blockIdx.x * NL_SEG + (long)threadIdx.x * NL_RUN;
+  const long len = a < L ? min((long)NL_RUN, L - a) : 0;
+  const int c = len > 0 ? nl_count_run(buf + a, len) : 0;
+  int tot;
+  nl_block_excl_scan(c, sh, &tot);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+// exclusive scan of the segment counts in place (+ the total at off[S])
+__global__ __launch_bounds__(1024) void nl_scan_kernel(int* __restrict__ cnt, long S, long* __restrict__ off) {
+  __shared__ long sh[1024];
+  long carry = 0;
+  for (long b = 0; b < S; b += 1024) {
+    const long i = b + threadIdx.x;
+    const long v = i < S ? cnt[i] : 0;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const long u = (int)threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += u;
+      __syncthreads();
+    }
+    if (i < S) off[i] = carry + sh[threadIdx.x] - v;
+    const long last = sh[1023];
+    __syncthreads();
+    carry += last;
+  }
+  if (threadIdx.x == 0) off[S] = carry;
+}
+
+__global__ __launch_bounds__(256) void nl_write_kernel(const uint8_t* __restrict__ buf, long L,
+                                                       const long* __restrict__ off, long* __restrict__ ends) {
+  __shared__ int sh[256];
+  const long a = (long)blockIdx.x * NL_SEG + (long)threadIdx.x * NL_RUN;
+  const long len = a < L ? min((long)NL_RUN, L - a) : 0;
+  const int c = len > 0 ? nl_count_run(buf + a, len) : 0;
+  int tot;
+  const int pre = nl_block_excl_scan(c, sh, &tot);
+  long o = off[blockIdx.x] + pre;
+  for (long i = 0; i < len && c; ++i)
+    if (buf[a + i] == '\n') ends[o++] = a + i;
+}
+
+}  // namespace
+
+SHIFU_API long shifu_newline_ws_bytes(long L) {
+  const long S = (L + NL_SEG - 1) / NL_SEG;
+  return S * 4 + (S + 1) * 8 + 16;
+}
+
+// ws layout (16-B aligned): int32 segment counts [S], then at round16(4 S) the int64 exclusive
+// offsets [S] and the total newline count
+static long nl_off_bytes(long S) { return (S * 4 + 15) & ~15l; }
+static long* nl_off(void* ws, long S) { return (long*)((char*)ws + nl_off_bytes(S)); }
+
+// pass 1 (+ scan): the newline count lands at byte offset shifu_newline_count_offset(L) of ws
+// (an int64; read it after the stream has run)
+SHIFU_API long shifu_newline_count_offset(long L) {
+  const long S = (L + NL_SEG - 1) / NL_SEG;
+  return nl_off_bytes(S) + S * 8;
+}
+
+SHIFU_API int shifu_newline_count(const void* buf, long L, void* ws, hipStream_t stream) {
+  if (L <= 0 || ((uintptr_t)buf & 15) || ((uintptr_t)ws & 15)) return -1;
+  const long S = (L + NL_SEG - 1) / NL_SEG;
+  if (S >= (1l << 31)) return -1;
+  hipLaunchKernelGGL(nl_count_kernel, dim3((unsigned)S), dim3(256), 0, stream, (const uint8_t*)buf, L, (int*)ws);
+  hipLaunchKernelGGL(nl_scan_kernel, dim3(1), dim3(1024), 0, stream, (int*)ws, S, nl_off(ws, S));
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// pass 2: ends[0 .. count) = the '\n' positions in order (ends sized by the count of pass 1)
+SHIFU_API int shifu_newline_write(const void* buf, long L, const void* ws, long* ends, hipStream_t stream) {
+  if (L <= 0) return -1;
+  const long S = (L + NL_SEG - 1) / NL_SEG;
+  hipLaunchKernelGGL(nl_write_kernel, dim3((unsigned)S), dim3(256), 0, stream, (const uint8_t*)buf, L,
+                     nl_off((void*)ws, S), ends);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}

@@ -100,24 +100,46 @@ def _is_binary(distinct: int, items: list) -> bool:
     if distinct != 2 or len(items) > 2:
         return False
     for s in items:
-        try:
-            if float(s) not in (0.0, 1.0):
-                return False
-        except ValueError:
+        v = _java_double(s)
+        if v is None or v not in (0.0, 1.0):
             return False
     return True
+
+
+def _java_double(s: str):
+    """Double.valueOf: surrounding whitespace trimmed, an optional d/D/f/F suffix, NaN / Infinity;
+    None when it would throw NumberFormatException."""
+    t = str(s).strip()
+    if t[-1:] in ("d", "D", "f", "F") and not t.endswith(("Infinity", "NaN")):
+        t = t[:-1]
+    u = t.lstrip("+-")
+    if u in ("NaN", "Infinity"):
+        return float(t.replace("Infinity", "inf"))
+    if not t or any(ch in u.lower() for ch in ("n", "x", "_", "i")):
+        return None
+    try:
+        return float(t)
+    except ValueError:
+        return None
 
 
 def auto_type_columns(ms: ModelSet, header=None, max_rows: int | None = None):
     """Distinct counts (+ the column type when autoTypeThreshold > 0) from one data-parallel pass
     over the training data (algos/autotype.py: every rank streams its byte ranges; counts,
-    hash sets / HyperLogLog registers and frequent items merged over the ranks).  Type rule: a
-    0/1 column is numeric (isBinaryVariable); otherwise numeric when more than autoTypeThreshold %
-    of the non-missing values parse as doubles.  (The reference's isDoubleFrequentVariable
-    (:248-259) only rejects whitespace-only sampled items, which makes its branch a no-op for every
-    column without such an item; the ratio rule here is the documented intent, the counts it uses
-    are the reference mapper's.)  Columns listed in categorical.column.names stay categorical."""
+    hash sets / HyperLogLog registers and frequent items merged over the ranks).
+
+    Type rule (``shifu.autoType.rule``):
+
+    * ``reference`` (default) -- exactly InitModelProcessor.setCategoricalColumnsAndDistinctAccount
+      (:181-219): a 0/1 column is numeric (isBinaryVariable :221-241); otherwise
+      isDoubleFrequentVariable (:243-254) decides, and as written it tries Double.parseDouble only
+      on BLANK sampled items, so a column is categorical exactly when one of its sampled items is
+      whitespace-only, numeric otherwise; user categorical columns are re-typed too, as there;
+    * ``ratio`` -- the intent documented beside it: numeric when more than autoTypeThreshold % of
+      the non-missing values parse as doubles (setCategoricalColumnsByCountInfo :143-179's test),
+      columns listed in categorical.column.names kept categorical."""
     from ..algos import autotype
+    from ..config import environment
     from ..parallel import dist
     mc = ms.mc
     ds = mc.dataSet
@@ -130,21 +152,28 @@ def auto_type_columns(ms: ModelSet, header=None, max_rows: int | None = None):
     info = dist.info()
     st = autotype.scan(mc, header, [c.num for c in todo], info.rank, info.world_size)
     thr = float(ds.get("autoTypeThreshold", 0) or 0)
+    rule = str(environment.get("shifu.autoType.rule", "reference")).lower()
     user_cat = set(mc.categorical_column_names())
     n_cat = 0
     for c in todo:
         s = st[c.num]
         c.stats["distinctCount"] = int(s.distinct)
-        if thr <= 0 or (c.is_categorical() and c.name in user_cat):
+        if thr <= 0:
             continue
-        nonmiss = s.count - s.invalid
-        ratio = s.validnum / nonmiss if nonmiss else 1.0
-        if _is_binary(s.distinct, s.items) or ratio > thr / 100.0:
+        if rule == "ratio":
+            if c.is_categorical() and c.name in user_cat:
+                continue
+            nonmiss = s.count - s.invalid
+            ratio = s.validnum / nonmiss if nonmiss else 1.0
+            numeric = _is_binary(s.distinct, s.items) or ratio > thr / 100.0
+        else:
+            numeric = _is_binary(s.distinct, s.items) or not any(not str(it).strip() for it in s.items)
+        if numeric:
             c.type = "N"
         else:
             c.type = "C"
             n_cat += 1
-    _log.info("auto type: %d categorical columns", n_cat)
+    _log.info("auto type (%s rule): %d categorical columns", "ratio" if rule == "ratio" else "reference", n_cat)
     return n_cat
 
 

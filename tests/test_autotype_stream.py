@@ -47,13 +47,14 @@ def _java_double(s: str) -> bool:
 def _write_data(root, rng, n):
     """A header + n rows: numeric, string, 0/1, mixed, missing-token and short-row columns, some
     invalid tags, blank lines and CRLF endings."""
-    hdr = ["tag", "num", "str", "bin", "mixed", "miss", "wide"]
+    hdr = ["tag", "num", "str", "bin", "mixed", "miss", "wide", "blank"]
     lines = ["|".join(hdr)]
     for i in range(n):
         tag = rng.choice(["1", "0", " 1 ", "0 ", "x"])
         row = [tag, f"{rng.gauss(0, 5):.3f}", rng.choice(["a", "b", "c", "dd", "e f"]), rng.choice(["0", "1"]),
                rng.choice(["1.5", "2e3", "abc", "1.0d", "-7", "NaN", " 4 "]),
-               rng.choice(["NULL", "null", "?", "", "3", "Null"]), f"w{rng.randint(0, 50)}"]
+               rng.choice(["NULL", "null", "?", "", "3", "Null"]), f"w{rng.randint(0, 50)}",
+               rng.choice([" ", "x", "y", "1"])]
         if rng.random() < 0.02:
             row = row[:4]                                    # short row
         lines.append("|".join(row))
@@ -141,15 +142,25 @@ def test_filter_expression_applies(tmp_path, monkeypatch):
         assert st[c].distinct == len(ref[hdr[c]]["vals"]), hdr[c]
 
 
-def test_init_types(tmp_path, monkeypatch):
+@pytest.mark.parametrize("rule", ["reference", "ratio"])
+def test_init_types(tmp_path, monkeypatch, rule):
+    """reference rule (InitModelProcessor.setCategoricalColumnsAndDistinctAccount :181-219, with
+    isDoubleFrequentVariable :243-254 as written): binary columns numeric, otherwise categorical
+    exactly when a sampled item is whitespace-only; ratio rule: the documented valid-double ratio."""
     monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    from shifu_amd.config import environment
     from shifu_amd.steps.create import run_init
+    monkeypatch.setitem(environment.props(), "shifu.autoType.rule", rule)
     root, hdr = _setup(tmp_path)
     run_init(root)
     cc = {c["columnName"]: c for c in json.load(open(os.path.join(root, "ColumnConfig.json")))}
     assert cc["num"]["columnType"] == "N" and cc["bin"]["columnType"] == "N"
-    assert cc["str"]["columnType"] == "C" and cc["wide"]["columnType"] == "C"
     assert cc["miss"]["columnType"] == "N"        # the only non-missing value is "3"
+    if rule == "ratio":
+        assert cc["str"]["columnType"] == "C" and cc["wide"]["columnType"] == "C"
+    else:
+        assert cc["str"]["columnType"] == "N" and cc["wide"]["columnType"] == "N"
+        assert cc["blank"]["columnType"] == "C"      # " " is a sampled item
     assert cc["str"]["columnStats"]["distinctCount"] == 5 and cc["bin"]["columnStats"]["distinctCount"] == 2
 
 

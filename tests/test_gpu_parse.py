@@ -269,3 +269,22 @@ def test_streamed_tables_gpu_parse_equal_host_multi_file(tmp_path):
             assert np.asarray(a.values).tobytes() == np.asarray(b.values).tobytes(), (ka, name)
             assert a.dictionary == b.dictionary, (ka, name)
     assert sum(t.n for _, t in dev) == 6200
+
+
+@pytest.mark.gpu
+def test_newline_index_kernel_matches_nonzero():
+    """The own newline index (csv_kernels.hip: segment counts, scan, ordered writes) equals
+    torch.nonzero over blocks with short / long lines, CR bytes and a tail without a newline."""
+    import torch
+    from shifu_amd.data.gpu_parse import GpuBlockParser
+    rng = np.random.default_rng(3)
+    p = GpuBlockParser([1, 1], [0, 1], "|", [""], "cuda")
+    for L in (1, 300, 65536, 65536 * 3 + 17, 5_000_001):
+        b = rng.integers(32, 127, size=L).astype(np.uint8)
+        nl = rng.random(L) < rng.choice([0.0005, 0.02, 0.3])
+        b[nl] = 10
+        d = torch.zeros(L + 64, dtype=torch.uint8, device="cuda")
+        d[:L] = torch.as_tensor(b, device="cuda")
+        got = p._newlines(d, L)
+        want = torch.nonzero(d[:L] == 10).flatten()
+        assert torch.equal(got, want), L
