@@ -393,17 +393,20 @@ def _cat_update(cc, md, binary, state, missing_acc):
         uniq = {}
         codes = np.array([uniq.setdefault(v, len(uniq)) if v != "" else -1 for v in s], dtype=np.int32)
         dictionary = list(uniq.keys())
-    present = np.unique(codes[codes >= 0])
     y = np.asarray(md.y)
     w = np.asarray(md.w, np.float64)
-    pos = (y > 0.5) if binary else np.ones(md.n, bool)
     nd = len(dictionary)
-    idx = np.where(codes >= 0, codes, nd)
-    cp = np.bincount(idx[pos], minlength=nd + 1)
-    cn = np.bincount(idx[~pos], minlength=nd + 1)
-    wp = np.bincount(idx[pos], weights=w[pos], minlength=nd + 1)
-    wn = np.bincount(idx[~pos], weights=w[~pos], minlength=nd + 1)
-    for d in sorted(present):
+    # one counted and one weighted bincount over (category, positive) keys: no masked copies
+    key = np.where(codes >= 0, codes, nd).astype(np.intp) * 2
+    if binary:
+        key += (y > 0.5)
+    else:
+        key += 1
+    c = np.bincount(key, minlength=2 * (nd + 1)).reshape(nd + 1, 2)
+    ws = np.bincount(key, weights=w, minlength=2 * (nd + 1)).reshape(nd + 1, 2)
+    cp, cn, wp, wn = c[:, 1], c[:, 0], ws[:, 1], ws[:, 0]
+    present = np.flatnonzero(c[:nd].sum(1) > 0)
+    for d in present:
         name = dictionary[d]
         g = index.get(name)
         if g is None:
