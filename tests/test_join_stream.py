@@ -266,3 +266,62 @@ print(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - before)
     grew_kb = int(out.stdout.strip().splitlines()[-1])
     assert grew_kb * 1024 < size * 0.5, (grew_kb, size)
     assert os.path.getsize(tmp_path / "out" / "part-00000") > size
+
+
+@pytest.fixture
+def cj_gpu(tmp_path, monkeypatch):
+    """A synthetic GBT model set trained on the GPU (the join's scorers then run there)."""
+    from shifu_amd.cli import main
+    from shifu_amd.config.model_config import ModelConfig
+    from shifu_amd.utils.synthetic import make_model_set
+    root = make_model_set(str(tmp_path), "g", "GBT", n_rows=4000, n_num=8, n_cat=2)
+    mc = ModelConfig.load(os.path.join(root, "ModelConfig.json"))
+    mc.train["baggingNum"] = 1
+    mc.train["params"] = {"TreeNum": 5, "MaxDepth": 3, "LearningRate": 0.1, "Loss": "squared",
+                          "Impurity": "variance", "FeatureSubsetStrategy": "ALL", "MinInstancesPerNode": 5}
+    mc.save()
+    monkeypatch.chdir(root)
+    for v in ("init", "stats", "norm", "train"):
+        assert main([v]) == 0, v
+    return root
+
+
+@pytest.mark.gpu
+def test_encode_and_combo_join_on_gpu(cj_gpu):
+    """encode (HIP tree walk) and the combo score join (device scoring) on the GPU equal the CPU
+    leaf paths exactly and the CPU scores within fp32 rounding."""
+    from shifu_amd.cli import main
+    from shifu_amd.data.reader import read_header, read_table
+    from shifu_amd.formats.tree_format import read_tree_model
+    from shifu_amd.scoring.model_runner import ModelRunner
+    from shifu_amd.scoring.tree_ensemble import TreeScorer
+    from shifu_amd.steps.base import ModelSet
+    from shifu_amd.steps.combo import _join_scores
+    assert main(["encode"]) == 0
+    ms = ModelSet(".")
+    mc = ms.mc
+    data = mc.resolve(mc.dataSet["dataPath"])
+    header = read_header(mc.resolve(mc.dataSet["headerPath"]), "|", data, "|")
+    scorer = TreeScorer(read_tree_model("models/model0.gbt"), "cpu")
+    m = scorer.model
+    num = {m.names[c] for c in m.names if c not in m.categories}
+    tab = read_table(data, header, "|", numeric=[h for h in header if h in num],
+                     strings=[h for h in header if h not in num], missing=mc.missing_values)
+    codes = scorer.encode(tab, 3)
+    raw = _raw_lines(data)
+    want = ["|".join(raw[i].split("|")[:len(header)] + list(codes[i])) for i in range(len(raw))]
+    assert open(os.path.join(ms.pf.encoded_train_data, "part-00000")).read().splitlines() == want
+    out = os.path.join(str(cj_gpu), "joined")
+    _join_scores([("sub0", ms)], [mc.dataSet], out)
+    r = ModelRunner(mc, ms.ccs, ms.pf.models_dir, device="cpu")
+    need = r.raw_columns()
+    cats = {c.name for c in ms.ccs if c.is_categorical()}
+    t = read_table(data, header, "|", numeric=[h for h in header if h in need and h not in cats],
+                   strings=[h for h in header if h not in need or h in cats], missing=mc.missing_values)
+    s = r.score(t, 1000.0)["mean"]
+    got = open(os.path.join(out, "part-00000")).read().splitlines()
+    assert len(got) == len(raw)
+    for i, line in enumerate(got):
+        f = line.split("|")
+        assert f[:-1] == raw[i].split("|")[:len(header)]
+        assert abs(float(f[-1]) - s[i]) < 2e-3
