@@ -21,6 +21,8 @@ def main():
                     help="GEMM tune settings applied per run, e.g. 12:0 12:1 (key 12: ring forward, 14: ring dgrad)")
     ap.add_argument("--big", type=int, nargs="*", default=[0],
                     help="shifu_gemm_set_big per run (0 auto, 3 8-phase whenever M >= 64K and N >= 256, 4 128x128)")
+    ap.add_argument("--stages", type=int, nargs="*", default=[1],
+                    help="shifu_gemm_set_stages per run (LDS stages of the 128x128 tile kernels: 1 or 2)")
     ap.add_argument("--dbg", type=int, nargs="*", default=[0],
                     help="GEMM lab ablation bits per run (1: no head err atomics, 2: main loops only, 4: head "
                          "stages 1-2 only, 8: no head / 8-phase tile stores, 16: head w_out without loads)")
@@ -63,9 +65,12 @@ def main():
             nat.call_hip("shifu_gemm_set_tune", k, v)
         for big in a.big:
             nat.call_hip("shifu_gemm_set_big", big)
-            for dbg in a.dbg:
-                nat.call_hip("shifu_gemm_set_tune", 9, dbg)
-                run(a, tr, data, wb, wt, timed, real, rec, f"{dbg} tune {tune} big {big}", nat, torch)
+            for stg in a.stages:
+                nat.call_hip("shifu_gemm_set_stages", stg)
+                for dbg in a.dbg:
+                    nat.call_hip("shifu_gemm_set_tune", 9, dbg)
+                    run(a, tr, data, wb, wt, timed, real, rec, f"{dbg} tune {tune} big {big} stages {stg}", nat, torch)
+    nat.call_hip("shifu_gemm_set_stages", 1)
     nat.call_hip("shifu_gemm_set_tune", 9, 0)
 
 
