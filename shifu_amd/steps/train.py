@@ -604,39 +604,38 @@ class TrainStep:
         verr = float("nan")
         # MiniBatchs=k: iteration i trains on slice (i-1) mod k of the rows (SubGradient :326-340)
         mb = max(1, min(1000, int(_num(p.get("MiniBatchs"), 1))))
-        wd = IterationWatchdog(iteration_limit(3600.0), "NN epoch").__enter__()
-        tr.comm_events = []                    # (start, end) of each gradient all-reduce -> allreduce_ms
-        for ep in range(start + 1, epochs + 1):
-            wd.tick()
-            t_ep = time.perf_counter()
-            with trace_range(f"nn.epoch{ep}"):
-                if mb > 1:
-                    b = (ep - 1) % mb
-                    lo, hi = data.n * b // mb, data.n * (b + 1) // mb
-                    terr = tr.step(data, lo, hi)
-                    rows_ep = n_train / mb
-                else:
-                    terr = tr.step(data, num_train_global=n_train)
-                    rows_ep = n_train
-                t_train = time.perf_counter() - t_ep     # step() ends with a host read of the error
-                verr = tr.evaluate(vdata) if vdata is not None else float("nan")
-            check_finite("training error", terr, ep)
-            if not math.isnan(verr) and verr < best_v:
-                best_v, best_w = verr, tr.params.flat.detach().clone()
-            self._log_epoch(tid, ep, terr, verr, extra=self._epoch_extra(tr, rows_ep, t_train))
-            if self.info.rank == 0 and ep % factor == 0 and ep < epochs:
-                self._write_nn(tid, spec, tr, tmp_epoch=ep)
-                os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
-                sd = tr.state_dict()
-                sd.update(epoch=ep, spec_sizes=[n_in] + spec.hidden + [n_out], best_v=best_v,
-                          best_w=None if best_w is None else best_w.cpu())
-                sd.pop("spec", None)
-                torch.save(sd, ckpt)
-            maybe_fault(ep, self.info.rank)
-            if es.update(ep, terr, verr):
-                _log.info("trainer %d early stop at epoch %d", tid, ep)
-                break
-        wd.__exit__(None, None, None)
+        with IterationWatchdog(iteration_limit(3600.0), "NN epoch") as wd:
+            tr.comm_events = []                    # (start, end) of each gradient all-reduce -> allreduce_ms
+            for ep in range(start + 1, epochs + 1):
+                wd.tick()
+                t_ep = time.perf_counter()
+                with trace_range(f"nn.epoch{ep}"):
+                    if mb > 1:
+                        b = (ep - 1) % mb
+                        lo, hi = data.n * b // mb, data.n * (b + 1) // mb
+                        terr = tr.step(data, lo, hi)
+                        rows_ep = n_train / mb
+                    else:
+                        terr = tr.step(data, num_train_global=n_train)
+                        rows_ep = n_train
+                    t_train = time.perf_counter() - t_ep     # step() ends with a host read of the error
+                    verr = tr.evaluate(vdata) if vdata is not None else float("nan")
+                check_finite("training error", terr, ep)
+                if not math.isnan(verr) and verr < best_v:
+                    best_v, best_w = verr, tr.params.flat.detach().clone()
+                self._log_epoch(tid, ep, terr, verr, extra=self._epoch_extra(tr, rows_ep, t_train))
+                if self.info.rank == 0 and ep % factor == 0 and ep < epochs:
+                    self._write_nn(tid, spec, tr, tmp_epoch=ep)
+                    os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
+                    sd = tr.state_dict()
+                    sd.update(epoch=ep, spec_sizes=[n_in] + spec.hidden + [n_out], best_v=best_v,
+                              best_w=None if best_w is None else best_w.cpu())
+                    sd.pop("spec", None)
+                    torch.save(sd, ckpt)
+                maybe_fault(ep, self.info.rank)
+                if es.update(ep, terr, verr):
+                    _log.info("trainer %d early stop at epoch %d", tid, ep)
+                    break
         if best_w is not None and vdata is not None:
             tr.params.flat.copy_(best_w)      # NNOutput keeps the weights of the min validation error
             verr = best_v
@@ -822,20 +821,19 @@ class TrainStep:
             if existing:
                 tt.continue_from(existing)
         interval = checkpoint_interval(p, max(1, tree_num // 10))   # DTOutput: tmp models every treeNum/10
-        wd = IterationWatchdog(iteration_limit(800.0), "tree").__enter__()
-        while len(tt.trees) < tree_num:
-            wd.tick()
-            with trace_range(f"gbdt.tree{len(tt.trees) + 1}"):
-                tt.train(1, callback=cb)
-            n = len(tt.trees)
-            check_finite("training error", tt.train_errors[-1], n)
-            if self.info.rank == 0 and n % interval == 0 and n < tree_num:
-                os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
-                torch.save(tt.state_dict(), ckpt)
-            maybe_fault(n, self.info.rank)
-            if stop[0]:
-                break
-        wd.__exit__(None, None, None)
+        with IterationWatchdog(iteration_limit(800.0), "tree") as wd:
+            while len(tt.trees) < tree_num:
+                wd.tick()
+                with trace_range(f"gbdt.tree{len(tt.trees) + 1}"):
+                    tt.train(1, callback=cb)
+                n = len(tt.trees)
+                check_finite("training error", tt.train_errors[-1], n)
+                if self.info.rank == 0 and n % interval == 0 and n < tree_num:
+                    os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
+                    torch.save(tt.state_dict(), ckpt)
+                maybe_fault(n, self.info.rank)
+                if stop[0]:
+                    break
         if self.info.rank == 0:
             with trace_range("train.write_model"):
                 self._write_trees(tid, tt)

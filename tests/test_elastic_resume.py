@@ -84,3 +84,22 @@ def test_watchdog_aborts_hung_rank(tmp_path):
                        text=True, timeout=120)
     assert r.returncode == 18, r.stderr[-2000:]
     assert "watchdog" in r.stderr
+
+
+def test_watchdog_stops_when_training_raises(tmp_path, monkeypatch):
+    """A training error raised inside the loop (check_finite) ends the watchdog thread too, so a
+    process that catches the error is not aborted one timeout later."""
+    import threading
+    import time
+    from shifu_amd.steps import train as train_mod
+    (a,) = _setup(tmp_path, "NN", ("x",))
+    monkeypatch.setenv("SHIFU_FORCE_CPU", "1")
+    monkeypatch.setenv("SHIFU_ITERATION_TIMEOUT", "1")
+
+    def boom(name, value, it):
+        raise FloatingPointError("forced")
+    monkeypatch.setattr(train_mod, "check_finite", boom)
+    with pytest.raises((FloatingPointError, AssertionError)):   # raised, or a non-zero exit code
+        _run(a, ["train"])
+    time.sleep(1.5)
+    assert not [t for t in threading.enumerate() if t.name == "shifu-watchdog" and t.is_alive()]
