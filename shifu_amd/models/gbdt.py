@@ -723,29 +723,35 @@ class TreeTrainer:
         return best, co
 
     def _root_bins(self):
-        """A [G][N][32] copy of the (quad-blocked) bins for the dense root pass, made once when HBM
-        has room for it (SHIFU_GBDT_ROOT_G32=0: never): the per-group root items then stream
-        contiguous 32-B slices, where the quad records would make each CU fetch whole 128-B lines
-        for a quarter of their bytes (profiles/r3, per-level tables).  None: use the quad records."""
+        """A feature-tiled copy of the (quad-blocked) bins, [G][NT][32][128] with NT = ceil(N/128),
+        made once when HBM has room for it (SHIFU_GBDT_ROOT_G32=0: never).  The dense root pass
+        streams whole 4-KiB tiles (gbdt_root_tile_kernel), and the partition passes read a row's
+        split-feature byte from a 128-B line of 128 consecutive rows of that feature, shared by the
+        node's other rows in the window (the quad records made every row fetch its own line).
+        None: use the quad records."""
         d = self.data
         if not ROOT_G32 or d.bins_dptr is not None or d.bins.device.type != "cuda":
             return None
         c = getattr(self, "_g32", None)
         if c is None:
             G, n = self.ngroups, d.n
-            need = G * n * FG
+            nt = (n + 127) // 128
+            need = G * nt * 4096
             from ..utils.device import free_hbm
             free = free_hbm(self.dev)
             if free < need * 1.1 + (6 << 30):
-                _log.info("GBDT root: no room for the [G][N][32] bins copy (%.1f GB); quad records", need / 1e9)
+                _log.info("GBDT root: no room for the feature-tiled bins copy (%.1f GB); quad records", need / 1e9)
                 self._g32 = False
                 return None
-            b = torch.empty(G, n, FG, dtype=torch.uint8, device=self.dev)
-            for gi in range(G):
-                o = (gi % (QF // FG)) * FG
-                b[gi] = d.bins[gi // (QF // FG), :, o: o + FG]
+            from ..ops import _native as nat
+            b = torch.empty(G, nt * 4096, dtype=torch.uint8, device=self.dev)
+            nat.call_hip("shifu_gbdt_tile_bins", d.kbins, d.group_stride, n, G, b, nt * 4096, nat.stream_of(d.y))
             self._g32 = c = b
         return c if c is not False else None
+
+    def _root_stride(self) -> int:
+        """Group stride (bytes) of the feature-tiled root copy."""
+        return (self.data.n + 127) // 128 * 4096
 
     def _root_slab(self, items, it, w, g, st):
         """Root-level slabs from the two u32 histogram modes: sum w (mode 1) is built once and
@@ -756,18 +762,25 @@ class TreeTrainer:
         d = self.data
         key = (w._version, self.scale_w, hash(items.tobytes()), d.bins.data_ptr(), d.bins_dptr)
         c = getattr(self, "_root_cache", None)
+        rb = self._root_bins()
+        q = None
+        if rb is not None:
+            q = getattr(self, "_root_q", None)
+            if q is None or q.numel() < self._root_stride() // 32:
+                q = self._root_q = torch.empty(self._root_stride() // 32, dtype=torch.int32, device=self.dev)
         if c is None or c[0] is not w or c[1] != key:
             slab = torch.empty(len(items), 2, FG, NB, dtype=torch.int64, device=self.dev)
-            rb = self._root_bins()
-            nat.call_hip("shifu_gbdt_hist", rb if rb is not None else d.kbins,
-                         d.n * FG if rb is not None else d.group_stride, FG if rb is not None else QF, None, w, g, 0,
-                         it, len(items), slab, self.F, self.scale_w, self.scale_g, 0, 1, st)
+            if rb is not None:
+                nat.call_hip("shifu_gbdt_hist_root_tile", rb, self._root_stride(), d.n, w, g, it, len(items), slab,
+                             self.scale_w, self.scale_g, 1, q, st)
+            else:
+                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, QF, None, w, g, 0,
+                             it, len(items), slab, self.F, self.scale_w, self.scale_g, 0, 1, st)
             self._root_cache = (w, key, slab)          # holds w: its storage cannot be re-issued
         slab = self._root_cache[2]
-        rb = self._root_bins()
-        if rb is not None:           # dense root pass over the [G][N][32] copy (every line fully used)
-            nat.call_hip("shifu_gbdt_hist", rb, d.n * FG, FG, None, w, g, 0, it, len(items), slab, self.F,
-                         self.scale_w, self.scale_g, 0, 2, st)
+        if rb is not None:           # dense root pass over the feature tiles (every line fully used)
+            nat.call_hip("shifu_gbdt_hist_root_tile", rb, self._root_stride(), d.n, w, g, it, len(items), slab,
+                         self.scale_w, self.scale_g, 2, q, st)
         elif ROOT_QUAD:
             # sum w*g over whole 128-B records: one block per (row range, quad) consumes every
             # line it fetches (gbdt_kernels.hip gbdt_root_quad_kernel)
@@ -973,7 +986,7 @@ class TreeTrainer:
         pred, scale = fuse
         self._leaf_done = True
         rb = self._root_bins()
-        nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, d.n * FG if rb is not None else 0,
+        nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, self._root_stride() if rb is not None else 0,
                      pos2row, pos_node, sf, sb, cl, self.is_cat_t, None, None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale),
                      1, nat.stream_of(d.y))
 
@@ -998,7 +1011,7 @@ class TreeTrainer:
             lv, (pred, scale) = leaf if leaf is not None else (None, (None, 0.0))
             # non-split nodes' rows get their leaf value here (fused GBT prediction update)
             rb = self._root_bins()        # 32-B records when the root's [G][N][32] copy exists
-            nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, d.n * FG if rb is not None else 0,
+            nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, self._root_stride() if rb is not None else 0,
                          pos2row, pos_node, sf, sb, cl, self.is_cat_t, fbits, wcnt, n, self._nmod, pred, None if lv is None else lv[0], None, None,
                          float(scale), 0, st)
             wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt

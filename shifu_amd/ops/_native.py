@@ -72,6 +72,8 @@ HIP_SIGNATURES = {
     # gbdt_kernels.hip
     "shifu_gbdt_hist": "pli" "ppp" "i" "pipi" "dd" "l" "i" "s",
     "shifu_gbdt_hist_root_quad": "plpppipids",
+    "shifu_gbdt_hist_root_tile": "pllpppipddips",
+    "shifu_gbdt_tile_bins": "pllipls",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
     "shifu_gbdt_partition_flag": "plpl" "pppppppp" "ll" "pppp" "fi" "s",
     "shifu_gbdt_bitrank": "pppip" "s",

@@ -30,6 +30,7 @@
 //     every rank computes the identical split from the all-reduced histograms.
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -469,8 +470,9 @@ __global__ __launch_bounds__(256) void gbdt_split_kernel(SplitArgs a) {
 // ---------------------------------------------------------------------------------------
 struct PartArgs {
   const uint8_t* bins; long gs;   // quad-blocked [Q][N][128]
-  // nullable: the [G][N][32] copy of the same bins (the dense root pass's); a row's split-feature
-  // byte is then read from its 32-B record instead of a 128-B quad record (1/4 of the lines)
+  // nullable: the feature-tiled copy of the same bins ([G][NT][32][128], the dense root pass's):
+  // a row's split-feature byte then sits in a line of 128 consecutive rows of that feature, which
+  // the node's other rows in the window share
   const uint8_t* bins32; long gs32;
   const int* pos2row;
   const int* pos_node;          // [N] node slot of each position (current level)
@@ -498,7 +500,8 @@ __device__ __forceinline__ int partition_flag(const PartArgs& a, long p) {
   int fl = 0;
   if (f >= 0) {
     const long v = a.pos2row[p], row = a.nmod ? v % a.nmod : v;
-    const uint32_t b = a.bins32 ? a.bins32[(f >> 5) * a.gs32 + row * 32 + (f & 31)] : a.bins[bin_off(a.gs, row, f)];
+    const uint32_t b = a.bins32 ? a.bins32[(f >> 5) * a.gs32 + (row >> 7) * 4096 + (f & 31) * 128 + (row & 127)]
+                                : a.bins[bin_off(a.gs, row, f)];
     if (a.is_cat[f]) fl = (a.cat_left[node * 8 + (b >> 5)] >> (b & 31)) & 1;
     else fl = (int)b <= a.split_bin[node] ? 1 : 0;
     if (a.pred && a.final_level) a.pred[row] += a.scale * (fl ? a.child_l_val[node] : a.child_r_val[node]);
@@ -723,9 +726,175 @@ __global__ __launch_bounds__(RQ_T, 1) void gbdt_root_quad_kernel(RootQuadArgs a)
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Root pass over the feature-tiled copy of the bins: [G][NT][32][128], NT = ceil(N / 128).  A
+// 4-KiB tile holds 128 rows x the 32 features of a group, each feature's 128 row bytes in one
+// 128-B line.  The dense root pass streams whole tiles (every fetched byte used), and a
+// partition below the root reads a node's split feature from lines that 128 consecutive rows
+// share: the rows of one node that fall in one tile window hit one line (the row-record layout
+// made every row fetch its own line; gbdt_partition_flag_kernel).
+//
+// Thread (tile slot ts, feature f = u & 31, chunk c = u >> 5) holds 16 row bytes of feature f and
+// adds their per-row u32 q (precomputed by gbdt_root_q_kernel) to LDS [bin][copy][32] with
+// copy = c & 1: the 64 lanes of a wave are 32 features x 2 copies -> 64 distinct banks for any
+// bins (no rotation needed).  Each copy sees 128 of the 256 rows of a pass: 16 passes (2048
+// rows per copy) between the int64 unpacks keep a bin's int32 sum exact (|q| < 2^20 - 1).
+// ---------------------------------------------------------------------------------------
+constexpr int RT_T = 512;                     // 8 waves: 2 tiles (256 rows) per pass
+constexpr int RT_E = NB * FG / RT_T;          // (bin, feature) sums each thread owns (16)
+
+struct RootTileArgs {
+  const uint8_t* bins; long gs;              // [G][NT][32][128]: gs = NT * 4096 bytes per group
+  const int* q;                              // [>= NT * 128] per-row u32 / i32 increment
+  const int* items;                          // [n][4] = {node, lo, hi, group}
+  long long* slab;                           // [n_items][2][FG][NB]
+  int mode;                                  // 1: sum w (stat 0), 2: sum w*g (stat 1, x 2^GSH32)
+};
+
+template <int MODE>
+__global__ __launch_bounds__(RT_T) void gbdt_root_tile_kernel(RootTileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t ht[];    // [NB][2][32]
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
+  for (int i = threadIdx.x; i < NB * 64; i += RT_T) ht[i] = 0u;
+  __syncthreads();
+  const int ts = threadIdx.x >> 8, u = threadIdx.x & 255, f = u & 31, c = u >> 5;
+  const int lb = ((c & 1) << 5) | f;
+  const uint8_t* gb = a.bins + (size_t)grp * a.gs + f * 128 + c * 16;
+  long long acc[RT_E];
+#pragma unroll
+  for (int k = 0; k < RT_E; ++k) acc[k] = 0;
+  auto flush = [&]() {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RT_E; ++k) {
+      const int e = threadIdx.x + k * RT_T, i0 = ((e >> 5) << 6) | (e & 31);    // bin e >> 5, feature e & 31
+      const uint32_t v0 = ht[i0], v1 = ht[i0 + 32];
+      if constexpr (MODE == 1) acc[k] += (long long)v0 + (long long)v1;
+      else acc[k] += ((long long)(int32_t)v0 + (long long)(int32_t)v1) * (1ll << GSH32);
+      ht[i0] = 0u;
+      ht[i0 + 32] = 0u;
+    }
+    __syncthreads();
+  };
+  const int t0 = lo >> 7, t1 = (hi + 127) >> 7;
+  // q of the chunk's 16 rows: lane (f & 3) = k of each 4-lane quad (same chunk) loads rows 4k..4k+3,
+  // the others are broadcast from it by quad-permute DPP moves -- one 16-B q load per pass
+  const int qk = f & 3;
+  auto load = [&](int t, uint4& b, uint4& qv) {
+    const int tc = min(t, t1 - 1);
+    b = *(const uint4*)(gb + (size_t)tc * 4096);
+    const int r0 = tc * 128 + c * 16 + qk * 4;
+    qv = *(const uint4*)(a.q + r0);
+    if (t >= t1 || r0 < lo || r0 + 4 > hi) {                 // rows outside [lo, hi) add nothing
+      const int a0 = t >= t1 ? 4 : max(0, lo - r0), a1 = min(4, hi - r0);
+      qv.x = (0 >= a0 && 0 < a1) ? qv.x : 0u;
+      qv.y = (1 >= a0 && 1 < a1) ? qv.y : 0u;
+      qv.z = (2 >= a0 && 2 < a1) ? qv.z : 0u;
+      qv.w = (3 >= a0 && 3 < a1) ? qv.w : 0u;
+    }
+  };
+  // software pipeline: tiles two passes ahead are in flight while a pass's atomics run
+  uint4 b0, q0, b1, q1;
+  load(t0 + ts, b0, q0);
+  load(t0 + 2 + ts, b1, q1);
+  int passes = 0;
+  for (int t = t0; t < t1; t += 2) {                          // block-uniform trip count
+    uint4 b2, q2;
+    load(t + 4 + ts, b2, q2);
+    const uint32_t B[4] = {b0.x, b0.y, b0.z, b0.w};
+    const int Q[4] = {(int)q0.x, (int)q0.y, (int)q0.z, (int)q0.w};
+    auto rows4 = [&](auto kc) {                               // rows 4k..4k+3 live in quad lane k
+      constexpr int k = decltype(kc)::value;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t qj = (uint32_t)__builtin_amdgcn_mov_dpp(Q[j], k * 0x55, 0xf, 0xf, false);
+        const uint32_t bj = (B[k] >> (j * 8)) & 0xff;
+        atomicAdd(&ht[(bj << 6) | lb], qj);
+      }
+    };
+    rows4(std::integral_constant<int, 0>{});
+    rows4(std::integral_constant<int, 1>{});
+    rows4(std::integral_constant<int, 2>{});
+    rows4(std::integral_constant<int, 3>{});
+    if (++passes == 16) { passes = 0; flush(); }
+    b0 = b1; q0 = q1; b1 = b2; q1 = q2;
+  }
+  flush();
+  // slab [item][st][f][b]: transposed through LDS (32 x 256 int64 = 64 KiB) for coalesced stores
+  long long* tt = (long long*)ht;
+#pragma unroll
+  for (int k = 0; k < RT_E; ++k) {
+    const int e = threadIdx.x + k * RT_T;
+    tt[(e & 31) * NB + (e >> 5)] = acc[k];
+  }
+  __syncthreads();
+  long long* out = a.slab + ((size_t)item * 2 + (MODE == 1 ? 0 : 1)) * FG * NB;
+  for (int i = threadIdx.x; i < FG * NB; i += RT_T) out[i] = tt[i];
+}
+
+// per-row increment of the tiled root pass: mode 1 u32(w * scale_w), mode 2 i32(w * g * scale_g)
+// (scale_g already / 2^GSH32); rows [n, n_pad) get 0
+__global__ void gbdt_root_q_kernel(const float* w, const float* g, long n, long n_pad, float scale, int mode, int* q) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pad) return;
+  int v = 0;
+  if (i < n) {
+    const float wv = w[i];
+    v = mode == 1 ? (int)__float2uint_rn(wv * scale) : __float2int_rn(wv * g[i] * scale);
+  }
+  q[i] = v;
+}
+
+// [Q][N][128] quad records -> [G][NT][32][128] feature tiles (one 4-KiB tile per block)
+__global__ __launch_bounds__(256) void gbdt_tile_bins_kernel(const uint8_t* bins, long gs, long n, int G,
+                                                            uint8_t* out, long gs_t) {
+  __shared__ uint8_t tile[128][33];
+  const long t = blockIdx.x;
+  const int grp = blockIdx.y;
+  const uint8_t* src = bins + (size_t)(grp >> 2) * gs + (grp & 3) * FG;
+  for (int i = threadIdx.x; i < 128 * 32; i += 256) {
+    const int r = i >> 5, f = i & 31;
+    const long row = t * 128 + r;
+    tile[r][f] = row < n ? src[(size_t)row * QF + f] : 0;
+  }
+  __syncthreads();
+  uint8_t* dst = out + (size_t)grp * gs_t + (size_t)t * 4096;
+  for (int i = threadIdx.x; i < 128 * 32; i += 256) {
+    const int f = i >> 7, r = i & 127;
+    dst[i] = tile[r][f];
+  }
+}
+
 }  // namespace
 
 #define CHECK_HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+// root histogram over the feature tiles: q scratch of >= NT * 128 ints (filled here from w, g)
+SHIFU_API int shifu_gbdt_hist_root_tile(const void* tiles, long gs_t, long n, const float* w, const float* g,
+                                        const int* items, int n_items, void* slab, double scale_w, double scale_g,
+                                        int mode, int* q, hipStream_t stream) {
+  const long nt = (n + 127) / 128;
+  if (n <= 0 || n_items <= 0 || (mode != 1 && mode != 2) || gs_t != nt * 4096) return -1;
+  const float sc = mode == 1 ? (float)scale_w : (float)(scale_g / (1 << GSH32));
+  hipLaunchKernelGGL(gbdt_root_q_kernel, dim3((unsigned)((nt * 128 + 255) / 256)), dim3(256), 0, stream, w, g, n,
+                     nt * 128, sc, mode, q);
+  RootTileArgs a{(const uint8_t*)tiles, gs_t, q, items, (long long*)slab, mode};
+  const size_t lds = NB * 64 * 4;                              // 64 KiB (also the int64 transpose)
+  if (mode == 1) hipLaunchKernelGGL(gbdt_root_tile_kernel<1>, dim3(n_items), dim3(RT_T), lds, stream, a);
+  else hipLaunchKernelGGL(gbdt_root_tile_kernel<2>, dim3(n_items), dim3(RT_T), lds, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+SHIFU_API int shifu_gbdt_tile_bins(const void* bins, long gs, long n, int G, void* out, long gs_t, hipStream_t stream) {
+  const long nt = (n + 127) / 128;
+  if (n <= 0 || G <= 0 || gs_t != nt * 4096 || nt > 0x7fffffffL) return -1;
+  hipLaunchKernelGGL(gbdt_tile_bins_kernel, dim3((unsigned)nt, (unsigned)G), dim3(256), 0, stream,
+                     (const uint8_t*)bins, gs, n, G, (uint8_t*)out, gs_t);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
 
 // Root sum w*g over whole quad records (gbdt_root_quad_kernel); qitems [n][4] = {first item, lo,
 // hi, quad}, the items of a quad's groups consecutive in the slab.

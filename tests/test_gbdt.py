@@ -450,3 +450,29 @@ def test_gpu_quantised_splits_vs_fp64_oracle():
     assert total >= 20
     assert same / total >= 0.95
     assert worst > 1 - 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [300001, 257])
+def test_gpu_feature_tiled_root_matches_quad_records(n, monkeypatch):
+    """The feature-tiled root copy ([G][NT][32][128]: tiled root histogram + partition reads) grows
+    the same trees and predictions, bit for bit, as the quad-record root path (no copy), with a
+    row count that leaves a partial last tile and a feature count that leaves a partial group."""
+    import torch
+    from shifu_amd.models import gbdt as gb
+    from shifu_amd.models.gbdt import TreeConfig, TreeTrainer, synthetic_binned
+    data = synthetic_binned(n, 100, "cuda", seed=4, labels="balanced")
+    cfg = TreeConfig("GBT", tree_num=3, max_depth=6, learning_rate=0.1, feature_subset_strategy="ALL",
+                     min_instances_per_node=2)
+    runs = []
+    for tiled in (True, False):
+        monkeypatch.setattr(gb, "ROOT_G32", tiled)
+        tr = TreeTrainer(cfg, data)
+        tr.train()
+        assert (getattr(tr, "_g32", None) is not None and tr._g32 is not False) == tiled
+        runs.append(tr)
+    a, b = runs
+    for x, y in zip(a.trees, b.trees):
+        assert (x.feat == y.feat).all() and (x.thr == y.thr).all()
+        assert np.array_equal(x.value, y.value)
+    assert torch.equal(a.pred, b.pred)
