@@ -394,11 +394,20 @@ class TreeTrainer:
                   "sibling": -1} for t in range(T)]
         hist_prev = None
         # root stats for each root's own value (one all-reduce for the batch)
-        tot = dist.all_reduce_(torch.stack([torch.stack([wt.double().sum(), (wt.double() * g.double()).sum()])
-                                            for wt in ws]))
         # fixed-point scales (powers of two, identical on every rank): per row w*scale_w < 2^16 and
         # |w*g*scale_g| < 2^23, the field widths of the packed LDS histogram entries
-        mx = torch.stack([w.abs().max().double(), (w * gg).abs().max().double()])
+        if self.gpu:        # one read of (w, g) per tree: sums and maxima in one deterministic kernel
+            from ..ops import _native as nat
+            part = torch.empty(4 * 1024, dtype=torch.float64, device=self.dev)
+            wst = torch.empty(T, 4, dtype=torch.float64, device=self.dev)
+            for t, wt in enumerate(ws):
+                nat.call_hip("shifu_gbdt_wg_stats", wt, g, n, part, wst[t], nat.stream_of(d.y))
+            tot = dist.all_reduce_(wst[:, :2].contiguous())
+            mx = torch.stack([wst[:, 2].max(), wst[:, 3].max()])
+        else:
+            tot = dist.all_reduce_(torch.stack([torch.stack([wt.double().sum(), (wt.double() * g.double()).sum()])
+                                                for wt in ws]))
+            mx = torch.stack([w.abs().max().double(), (w * gg).abs().max().double()])
         dist.all_reduce_(mx, "max")
         self.scale_w = _pack_scale(float(mx[0]), W_BITS)
         # margin 2^(GSH32+1): the root's u32 w*g mode quantises at scale_g / 2^GSH32, whose rounded
@@ -977,18 +986,36 @@ class TreeTrainer:
     # ------------------------------------------------------------------------------------
     def _leaf_update(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, leaf_vals, fuse):
         """Final level of a fused GBT tree: pred[row] += scale * value of the row's leaf (split nodes:
-        the child its bin goes to), in the partition-flag kernel without a flag output."""
+        the child its bin goes to).  Default: walked in row windows, each XCD updating its own
+        windows' pred lines in its L2 (gbdt_leaf_window_kernel); SHIFU_GBDT_LEAF_WINDOW=0: the
+        position-ordered partition-flag kernel without a flag output."""
         from ..ops import _native as nat
         d = self.data
-        sf = _h2d(split_feat, self.dev)
-        sb = _h2d(split_bin, self.dev)
-        cl = _h2d(cat_left.view(np.int32), self.dev)
+        nn = len(nodes)
         pred, scale = fuse
         self._leaf_done = True
         rb = self._root_bins()
+        st = nat.stream_of(d.y)
+        if LEAF_WINDOW and self._nmod == 0 and nn <= 1024:
+            starts = np.array([z["start"] for z in nodes], dtype=np.int32)
+            ends = np.array([z["end"] for z in nodes], dtype=np.int32)
+            meta = _h2d(np.concatenate([split_feat.astype(np.int32), split_bin.astype(np.int32),
+                                        cat_left.view(np.int32).reshape(-1), starts, ends]), self.dev)
+            sf, sb, cl = meta[:nn], meta[nn:2 * nn], meta[2 * nn:10 * nn]
+            st_t, en_t = meta[10 * nn:11 * nn], meta[11 * nn:12 * nn]
+            nw = ((d.n + LEAF_W - 1) // LEAF_W + 7) // 8 * 8
+            bounds = torch.empty(nn * (nw + 1), dtype=torch.int32, device=self.dev)
+            nat.call_hip("shifu_gbdt_leaf_window", d.kbins, d.group_stride, rb,
+                         self._root_stride() if rb is not None else 0, pos2row, st_t, en_t, nn, d.n, LEAF_W, LEAF_Y,
+                         bounds, sf, sb, cl, self.is_cat_t, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2],
+                         float(scale), st)
+            return
+        sf = _h2d(split_feat, self.dev)
+        sb = _h2d(split_bin, self.dev)
+        cl = _h2d(cat_left.view(np.int32), self.dev)
         nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, self._root_stride() if rb is not None else 0,
                      pos2row, pos_node, sf, sb, cl, self.is_cat_t, None, None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale),
-                     1, nat.stream_of(d.y))
+                     1, st)
 
     def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots, leaf=None):
         d = self.data
@@ -1000,9 +1027,18 @@ class TreeTrainer:
         if self.gpu:
             from ..ops import _native as nat
             st = nat.stream_of(d.y)
-            sf = _h2d(split_feat, self.dev)
-            sb = _h2d(split_bin, self.dev)
-            cl = _h2d(cat_left.view(np.int32), self.dev)
+            child_l = np.full(nn, -1, np.int32)
+            child_r = np.full(nn, -1, np.int32)
+            for s_, (cl_, cr_) in child_slots.items():
+                child_l[s_], child_r[s_] = cl_, cr_
+            # every per-node array of the level in ONE upload: split feature / bin, categorical
+            # left sets, node position ranges and child slots
+            meta = _h2d(np.concatenate([split_feat.astype(np.int32), split_bin.astype(np.int32),
+                                        cat_left.view(np.int32).reshape(-1), starts.astype(np.int32),
+                                        ends.astype(np.int32), child_l, child_r]), self.dev)
+            sf, sb = meta[:nn], meta[nn:2 * nn]
+            cl = meta[2 * nn:10 * nn]
+            st_t, en_t, chl_t, chr_t = (meta[(10 + k) * nn:(11 + k) * nn] for k in range(4))
             # left bits, one 64-bit word per 64 positions + the words' popcounts (exclusive-scanned):
             # the inclusive left count at p is wpre[p / 64] + popcount of the word's bits <= p
             nw = (n + 63) // 64
@@ -1010,39 +1046,28 @@ class TreeTrainer:
             wcnt = torch.empty(nw, dtype=torch.int32, device=self.dev)
             lv, (pred, scale) = leaf if leaf is not None else (None, (None, 0.0))
             # non-split nodes' rows get their leaf value here (fused GBT prediction update)
-            rb = self._root_bins()        # 32-B records when the root's [G][N][32] copy exists
+            rb = self._root_bins()        # feature-tiled copy when it exists
             nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, self._root_stride() if rb is not None else 0,
                          pos2row, pos_node, sf, sb, cl, self.is_cat_t, fbits, wcnt, n, self._nmod, pred, None if lv is None else lv[0], None, None,
                          float(scale), 0, st)
             wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
-            # per-node: #left = cum[end-1] - cum[start-1]
-            idx = _h2d(np.concatenate([np.maximum(ends - 1, 0), np.maximum(starts - 1, 0)]), self.dev)
-            cum2 = torch.empty(2 * nn, dtype=torch.int32, device=self.dev)
-            nat.call_hip("shifu_gbdt_bitrank", fbits, wpre, idx, 2 * nn, cum2, st)
-            cecb = cum2.view(2, nn).cpu().numpy().astype(np.int64)   # one D2H sync
-            ce, cb = cecb[0], cecb[1]
-            cb = np.where(starts > 0, cb, 0)
-            ce = np.where(ends > starts, ce, cb)
-            nleft = ce - cb
-            child_l = np.full(nn, -1, np.int32)
-            child_r = np.full(nn, -1, np.int32)
-            ranges = {}
-            for z in nodes:
-                s_ = z["slot"]
-                if split_feat[s_] >= 0:
-                    child_l[s_], child_r[s_] = child_slots[s_]
-                ranges[s_] = (int(starts[s_]), int(starts[s_] + nleft[s_]), int(ends[s_]))
+            # per node: left count before its start and #left, on the device; the scatter runs
+            # before the host reads the counts (the D2H overlaps it)
+            cbn = torch.empty(2, nn, dtype=torch.int32, device=self.dev)
+            nat.call_hip("shifu_gbdt_node_counts", fbits, wpre, st_t, en_t, nn, cbn[0], cbn[1], st)
             new_p2r = torch.empty_like(pos2row)
             new_pn = torch.empty_like(pos_node)
-            t = lambda a, dt=np.int32: _h2d(np.ascontiguousarray(a.astype(dt)), self.dev)  # noqa
             # tensors (not .data_ptr() of temporaries) so every buffer outlives the launch
             wg = self._wg_pos
             nw_, ng_ = (torch.empty_like(wg[0]), torch.empty_like(wg[1])) if wg is not None else (None, None)
-            nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, fbits, wpre, t(starts), t(nleft), t(cb),
-                         sf, t(child_l), t(child_r), new_p2r, new_pn, None if wg is None else wg[0],
+            nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, fbits, wpre, st_t, cbn[1], cbn[0],
+                         sf, chl_t, chr_t, new_p2r, new_pn, None if wg is None else wg[0],
                          None if wg is None else wg[1], nw_, ng_, n, st)
             if wg is not None:
                 self._wg_pos = (nw_, ng_)
+            nleft = cbn[1].cpu().numpy().astype(np.int64)     # one D2H sync, behind the scatter
+            ranges = {z["slot"]: (int(starts[z["slot"]]), int(starts[z["slot"]] + nleft[z["slot"]]),
+                                  int(ends[z["slot"]])) for z in nodes}
             # child slot ids follow the order of new_nodes built by the caller (left, right per split)
             return new_p2r, new_pn, ranges
         # CPU path
@@ -1372,6 +1397,10 @@ ROOT_GSH32 = 3               # = gbdt_kernels.hip GSH32
 # the per-group items); SHIFU_GBDT_ROOT_G32=0 never makes the copy
 ROOT_QUAD = os.environ.get("SHIFU_GBDT_ROOT_QUAD", "1") != "0"
 ROOT_G32 = os.environ.get("SHIFU_GBDT_ROOT_G32", "1") != "0"
+# final-level prediction update in row windows of LEAF_W rows, LEAF_Y blocks per window
+LEAF_WINDOW = os.environ.get("SHIFU_GBDT_LEAF_WINDOW", "1") != "0"
+LEAF_W = int(os.environ.get("SHIFU_GBDT_LEAF_W", str(1 << 16)))
+LEAF_Y = int(os.environ.get("SHIFU_GBDT_LEAF_Y", "16"))
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on
 # power-of-two grids (|w*g| < 2^23 of the grid, the root's u32 w*g mode 2^3 coarser), summed
 # exactly in int64 (so every rank and every run finds the same splits)

@@ -74,9 +74,12 @@ HIP_SIGNATURES = {
     "shifu_gbdt_hist_root_quad": "plpppipids",
     "shifu_gbdt_hist_root_tile": "pllpppipddips",
     "shifu_gbdt_tile_bins": "pllipls",
+    "shifu_gbdt_wg_stats": "pplpps",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
     "shifu_gbdt_partition_flag": "plpl" "pppppppp" "ll" "pppp" "fi" "s",
     "shifu_gbdt_bitrank": "pppip" "s",
+    "shifu_gbdt_node_counts": "ppppipps",
+    "shifu_gbdt_leaf_window": "plpl" "ppp" "illi" "p" "pppp" "pppp" "f" "s",
     "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "pppp" "l" "s",
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
     "shifu_gbdt_residual": "pppp" "p" "li" "s",

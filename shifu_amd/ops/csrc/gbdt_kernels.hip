@@ -524,6 +524,79 @@ __global__ void __launch_bounds__(256) gbdt_partition_flag_kernel(PartArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Final-level prediction update, row-window ordered.  Every current node's positions hold
+// ascending rows (the stable partition keeps them so), so the positions of node k whose rows fall
+// in window j = [j W, (j + 1) W) are one sub-range [bounds[k][j], bounds[k][j + 1]).  Block L works
+// on window j = (L & 7) + 8 (L >> 3) / Y: each XCD walks its own windows in order, Y blocks per
+// window, so the pred lines of a window (W x 4 B) are read-modify-written inside one XCD's L2
+// while the window is open -- walking the positions node after node instead scattered
+// 4-B updates over all of pred, one line fetch and one partial write-back per row.
+// ---------------------------------------------------------------------------------------
+struct LeafWinArgs {
+  const uint8_t* bins; long gs;                  // quad-blocked [Q][N][128]
+  const uint8_t* bins32; long gs32;              // nullable: feature-tiled copy
+  const int* pos2row;
+  const int* bounds;                             // [nn][NW + 1]
+  int nn, NW, Y;
+  const int* split_feat; const int* split_bin; const uint32_t* cat_left; const uint8_t* is_cat;
+  float* pred; const float* node_val; const float* child_l_val; const float* child_r_val; float scale;
+};
+
+constexpr int LW_T = 256;
+constexpr int LW_MAXN = 1024;
+
+__global__ __launch_bounds__(LW_T) void gbdt_leaf_window_kernel(LeafWinArgs a) {
+  __shared__ int pre[LW_MAXN + 1];
+  const int L = blockIdx.x, j = (L & 7) + 8 * ((L >> 3) / a.Y), y = (L >> 3) % a.Y;
+  if (j >= a.NW) return;
+  const int nn = a.nn;
+  for (int k = threadIdx.x; k < nn; k += LW_T)
+    pre[k + 1] = a.bounds[(size_t)k * (a.NW + 1) + j + 1] - a.bounds[(size_t)k * (a.NW + 1) + j];
+  if (threadIdx.x == 0) pre[0] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 1; k <= nn; ++k) pre[k] += pre[k - 1];
+  __syncthreads();
+  const int M = pre[nn];
+  for (int v = y * LW_T + threadIdx.x; v < M; v += a.Y * LW_T) {
+    int lo = 0, hi = nn;                                   // node k: pre[k] <= v < pre[k + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] <= v) lo = mid; else hi = mid;
+    }
+    const int k = lo;
+    const long p = a.bounds[(size_t)k * (a.NW + 1) + j] + (v - pre[k]);
+    const long row = a.pos2row[p];
+    const int f = a.split_feat[k];
+    float val;
+    if (f >= 0) {
+      const uint32_t b = a.bins32 ? a.bins32[(f >> 5) * a.gs32 + (row >> 7) * 4096 + (f & 31) * 128 + (row & 127)]
+                                  : a.bins[bin_off(a.gs, row, f)];
+      const bool left = a.is_cat[f] ? ((a.cat_left[k * 8 + (b >> 5)] >> (b & 31)) & 1) : ((int)b <= a.split_bin[k]);
+      val = left ? a.child_l_val[k] : a.child_r_val[k];
+    } else {
+      val = a.node_val[k];
+    }
+    a.pred[row] += a.scale * val;
+  }
+}
+
+// bounds[k][j] = first position of node k (in [start, end), ascending rows) with row >= j W
+__global__ void gbdt_window_bounds_kernel(const int* pos2row, const int* starts, const int* ends, int nn, int NW,
+                                          long W, int* bounds) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)nn * (NW + 1)) return;
+  const int k = (int)(i / (NW + 1)), j = (int)(i % (NW + 1));
+  int lo = starts[k], hi = max(starts[k], ends[k]);
+  const long target = (long)j * W;
+  while (lo < hi) {
+    const int mid = lo + ((hi - lo) >> 1);
+    if ((long)pos2row[mid] < target) lo = mid + 1; else hi = mid;
+  }
+  bounds[i] = lo;
+}
+
 // scatter: positions of split nodes move to [start + rank_left] or [start + n_left + rank_right]
 struct ScatterArgs {
   const int* pos2row; const int* pos_node;
@@ -623,6 +696,64 @@ __global__ __launch_bounds__(256) void gbdt_residual_kernel(ResidArgs a) {
   if (threadIdx.x == 0) {
     atomicAdd(a.err, red[0][0] + red[1][0] + red[2][0] + red[3][0]);
     atomicAdd(a.err + 1, red[0][1] + red[1][1] + red[2][1] + red[3][1]);
+  }
+}
+
+// Per-tree root statistics in one read of (w, g): sum w and sum w*g (f64, products of the f32
+// inputs as in the host path) and max |w|, max |w*g| (the fixed-point scales).  Deterministic: a
+// fixed grid of blocks writes per-block partials, one block sums them in a fixed order.
+constexpr int WS_BLOCKS = 1024;
+
+__device__ __forceinline__ float wave_max_f(float v) {
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__global__ __launch_bounds__(256) void gbdt_wg_stats_kernel(const float* w, const float* g, long n, double* part) {
+  __shared__ double red[4][4];
+  const long chunk = (n + WS_BLOCKS - 1) / WS_BLOCKS, lo = (long)blockIdx.x * chunk, hi = min(n, lo + chunk);
+  double sw = 0.0, swg = 0.0;
+  float mw = 0.f, mwg = 0.f;
+  for (long i = lo + threadIdx.x; i < hi; i += 256) {
+    const float wv = w[i], gv = g[i];
+    sw += (double)wv;
+    swg += (double)wv * (double)gv;
+    mw = fmaxf(mw, fabsf(wv));
+    mwg = fmaxf(mwg, fabsf(wv * gv));
+  }
+  sw = wave_sum_d(sw);
+  swg = wave_sum_d(swg);
+  mw = wave_max_f(mw);
+  mwg = wave_max_f(mwg);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[wv][0] = sw; red[wv][1] = swg; red[wv][2] = mw; red[wv][3] = mwg; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    double v = red[0][k];
+    for (int j = 1; j < 4; ++j) v = k < 2 ? v + red[j][k] : fmax(v, red[j][k]);
+    part[(long)blockIdx.x * 4 + k] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void gbdt_wg_stats_final_kernel(const double* part, double* out) {
+  __shared__ double red[4][4];
+  double s0 = 0.0, s1 = 0.0, m0 = 0.0, m1 = 0.0;
+  for (int b = threadIdx.x; b < WS_BLOCKS; b += 256) {
+    s0 += part[b * 4]; s1 += part[b * 4 + 1];
+    m0 = fmax(m0, part[b * 4 + 2]); m1 = fmax(m1, part[b * 4 + 3]);
+  }
+  s0 = wave_sum_d(s0);
+  s1 = wave_sum_d(s1);
+  for (int off = 32; off > 0; off >>= 1) { m0 = fmax(m0, __shfl_xor(m0, off, 64)); m1 = fmax(m1, __shfl_xor(m1, off, 64)); }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[wv][0] = s0; red[wv][1] = s1; red[wv][2] = m0; red[wv][3] = m1; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    double v = red[0][k];
+    for (int j = 1; j < 4; ++j) v = k < 2 ? v + red[j][k] : fmax(v, red[j][k]);
+    out[k] = v;
   }
 }
 
@@ -887,6 +1018,38 @@ SHIFU_API int shifu_gbdt_hist_root_tile(const void* tiles, long gs_t, long n, co
   return 0;
 }
 
+// out[4] (f64) = sum w, sum w*g, max |w|, max |w*g|; part: >= 4 * 1024 doubles of scratch
+SHIFU_API int shifu_gbdt_wg_stats(const float* w, const float* g, long n, void* part, void* out, hipStream_t stream) {
+  if (n < 0) return -1;
+  hipLaunchKernelGGL(gbdt_wg_stats_kernel, dim3(WS_BLOCKS), dim3(256), 0, stream, w, g, n, (double*)part);
+  hipLaunchKernelGGL(gbdt_wg_stats_final_kernel, dim3(1), dim3(256), 0, stream, (const double*)part, (double*)out);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// final-level fused prediction update in row windows (gbdt_leaf_window_kernel); bounds: scratch
+// of >= nn * (NW + 1) ints, NW = ceil(n_rows / W) rounded up to a multiple of 8
+SHIFU_API int shifu_gbdt_leaf_window(const void* bins, long gs, const void* bins32, long gs32, const int* pos2row,
+                                     const int* starts, const int* ends, int nn, long n_rows, long W, int Y,
+                                     int* bounds, const int* split_feat, const int* split_bin, const void* cat_left,
+                                     const void* is_cat, float* pred, const float* node_val, const float* child_l_val,
+                                     const float* child_r_val, float scale, hipStream_t stream) {
+  if (nn <= 0) return 0;
+  if (nn > LW_MAXN || W <= 0 || Y <= 0 || n_rows <= 0) return -1;
+  const long nw = ((n_rows + W - 1) / W + 7) / 8 * 8;
+  if (nw > (1L << 24) || nw * Y > 0x7fffffffL) return -1;
+  const int NW = (int)nw;
+  const long nb = (long)nn * (NW + 1);
+  hipLaunchKernelGGL(gbdt_window_bounds_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, stream, pos2row,
+                     starts, ends, nn, NW, W, bounds);
+  LeafWinArgs a{(const uint8_t*)bins, gs, (const uint8_t*)bins32, gs32, pos2row, bounds, nn, NW, Y, split_feat,
+                split_bin, (const uint32_t*)cat_left, (const uint8_t*)is_cat, pred, node_val, child_l_val,
+                child_r_val, scale};
+  hipLaunchKernelGGL(gbdt_leaf_window_kernel, dim3((unsigned)(nw * Y)), dim3(LW_T), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 SHIFU_API int shifu_gbdt_tile_bins(const void* bins, long gs, long n, int G, void* out, long gs_t, hipStream_t stream) {
   const long nt = (n + 127) / 128;
   if (n <= 0 || G <= 0 || gs_t != nt * 4096 || nt > 0x7fffffffL) return -1;
@@ -990,6 +1153,33 @@ __global__ void gbdt_bitrank_kernel(const unsigned long long* fbits, const int* 
   const unsigned long long w = fbits[q >> 6];
   const int lane = (int)(q & 63);
   out[i] = wpre[q >> 6] + __popcll(lane == 63 ? w : w & ((2ull << lane) - 1));
+}
+
+// per node [start, end): left count before start (cum0) and #left in the node, from the bits +
+// word prefix -- the scatter's node arrays, computed where the bits are (no host round trip)
+__global__ void gbdt_node_counts_kernel(const unsigned long long* fbits, const int* wpre, const int* starts,
+                                        const int* ends, int nn, int* cum0, int* nleft) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  auto cum = [&](long q) {
+    const unsigned long long w = fbits[q >> 6];
+    const int lane = (int)(q & 63);
+    return wpre[q >> 6] + __popcll(lane == 63 ? w : w & ((2ull << lane) - 1));
+  };
+  const int s = starts[i], e = ends[i];
+  const int cb = s > 0 ? cum(s - 1) : 0;
+  const int ce = e > s ? cum(e - 1) : cb;
+  cum0[i] = cb;
+  nleft[i] = ce - cb;
+}
+
+SHIFU_API int shifu_gbdt_node_counts(const void* fbits, const int* wpre, const int* starts, const int* ends, int nn,
+                                     int* cum0, int* nleft, hipStream_t stream) {
+  if (nn <= 0) return 0;
+  hipLaunchKernelGGL(gbdt_node_counts_kernel, dim3((nn + 255) / 256), dim3(256), 0, stream,
+                     (const unsigned long long*)fbits, wpre, starts, ends, nn, cum0, nleft);
+  CHECK_HIP(hipGetLastError());
+  return 0;
 }
 
 SHIFU_API int shifu_gbdt_bitrank(const void* fbits, const int* wpre, const long* idx, int m, int* out,

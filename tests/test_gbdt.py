@@ -476,3 +476,30 @@ def test_gpu_feature_tiled_root_matches_quad_records(n, monkeypatch):
         assert (x.feat == y.feat).all() and (x.thr == y.thr).all()
         assert np.array_equal(x.value, y.value)
     assert torch.equal(a.pred, b.pred)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w_rows,y_blocks", [(1000, 3), (1 << 16, 16)])
+def test_gpu_leaf_window_update_matches_position_pass(w_rows, y_blocks, monkeypatch):
+    """The final-level prediction update walked in row windows (per-node position sub-ranges found
+    by binary search, XCD-ordered windows) gives the same trees and the same pred, bit for bit, as
+    the position-ordered flag pass; a small window exercises many windows and empty sub-ranges."""
+    import torch
+    from shifu_amd.models import gbdt as gb
+    from shifu_amd.models.gbdt import TreeConfig, TreeTrainer, synthetic_binned
+    data = synthetic_binned(200003, 70, "cuda", seed=9, labels="balanced")
+    cfg = TreeConfig("GBT", tree_num=3, max_depth=6, learning_rate=0.1, feature_subset_strategy="ALL",
+                     min_instances_per_node=2)
+    monkeypatch.setattr(gb, "LEAF_W", w_rows)
+    monkeypatch.setattr(gb, "LEAF_Y", y_blocks)
+    runs = []
+    for win in (True, False):
+        monkeypatch.setattr(gb, "LEAF_WINDOW", win)
+        tr = TreeTrainer(cfg, data)
+        tr.train()
+        runs.append(tr)
+    a, b = runs
+    for x, y in zip(a.trees, b.trees):
+        assert (x.feat == y.feat).all() and (x.thr == y.thr).all()
+        assert np.array_equal(x.value, y.value)
+    assert torch.equal(a.pred, b.pred)
