@@ -220,6 +220,17 @@ def _raw_matrix(cols, table):
     return out
 
 
+def _to_dev(a, dev):
+    """Host array -> ``dev`` without a host stall: page-locked staging (torch's caching host
+    allocator) and a non-blocking copy on the current stream; a pageable ``as_tensor(device=)``
+    waits for the stream's queued kernels first."""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if torch.device(dev).type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def _raw_matrix_dev(cols, table, dev):
     """:func:`_raw_matrix` on ``dev``.  The numeric columns that are rows of the parser's block
     matrix are uploaded in place (the block's spanned rows as one copy, placed by a device-side
@@ -233,11 +244,11 @@ def _raw_matrix_dev(cols, table, dev):
         if len(num_j) == len(cols):
             return blk
         out = torch.empty((len(cols), table.n), dtype=torch.float64, device=dev)
-        out.index_copy_(0, torch.as_tensor(np.asarray(num_j, np.int64), device=dev), blk)
+        out.index_copy_(0, _to_dev(np.asarray(num_j, np.int64), dev), blk)
         in_blk = set(num_j)
         rest = [j for j in range(len(cols)) if j not in in_blk]
         host = _raw_matrix([cols[j] for j in rest], table)
-        out.index_copy_(0, torch.as_tensor(np.asarray(rest, np.int64), device=dev), torch.as_tensor(host, device=dev))
+        out.index_copy_(0, _to_dev(np.asarray(rest, np.int64), dev), _to_dev(host, dev))
         return out
     hit = numeric_rows([table[cols[j].name].values for j in num_j]) if len(num_j) > 1 else None
     if hit is None:
@@ -386,6 +397,7 @@ class NormPlan:
         import torch
         self.mc, self.cols = mc, list(cols)
         self.pinned_out, self._pins, self._pin_i = int(pinned_out), {}, {}
+        self.async_out, self.last_event = False, None     # async D2H into the pinned buffers
         self.nt = norm_type or mc.norm_type
         self.cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
         self.want_x, self.want_codes = want_x, want_codes
@@ -467,7 +479,14 @@ class NormPlan:
         if buf is None or buf.numel() < t.numel():
             buf = self._pins[(key, i)] = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
         h = buf[: t.numel()].view(t.shape)
-        h.copy_(t)
+        if self.async_out:
+            # the caller synchronises on ``last_event`` before reading (streamed norm: the writer
+            # thread), so the consumer queues the next chunk instead of waiting for this DMA
+            h.copy_(t, non_blocking=True)
+            self.last_event = torch.cuda.Event()
+            self.last_event.record(torch.cuda.current_stream(self.dev))
+        else:
+            h.copy_(t)
         return h.numpy()
 
     def _onehot_specs(self):

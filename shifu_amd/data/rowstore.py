@@ -85,6 +85,103 @@ class NpyAppender:
             os.remove(self.path)
 
 
+SEG = "@"                  # segment files of one array: <name>@<k:06d>.npy, rows in k order
+
+
+def _write_npy(path: str, a: np.ndarray) -> None:
+    """One whole .npy file (reserved-size header + the rows) with pwrite, no temporary copy."""
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        os.pwrite(fd, _header(a.dtype, a.shape), 0)
+        mv = memoryview(a.reshape(-1).view(np.uint8)) if a.size else memoryview(b"")
+        off = HEADER_BYTES
+        while len(mv):
+            k = os.pwrite(fd, mv, off)
+            mv, off = mv[k:], off + k
+    finally:
+        os.close(fd)
+
+
+class SegmentAppender:
+    """Append ``[k, *row_shape]`` blocks as a sequence of segment files ``<name>@<k>.npy`` in one
+    directory.  A large block is cut into ``SPLIT`` row slices written by as many threads, each
+    into its own file: tmpfs serialises the writers of one inode (one file took ~5.7 GB/s on the
+    GPU box whatever the thread count; 4 / 8 files at once 21 / 36 GB/s,
+    profiles/r5/write_lab_shm_r5.txt).  Readers concatenate the segments in name order
+    (:func:`part_arrays`)."""
+
+    SPLIT = int(os.environ.get("SHIFU_WRITE_SPLIT", "8"))
+    MIN_SPLIT_BYTES = 64 << 20                   # smaller blocks go out as one file
+
+    def __init__(self, dirpath: str, name: str, dtype, row_shape: tuple = ()):
+        self.dir, self.name = dirpath, name
+        self.dtype, self.row_shape = np.dtype(dtype), tuple(row_shape)
+        self.rows, self.k = 0, 0
+        self._pool = None
+        for fn in os.listdir(dirpath):            # a rewrite replaces every old segment
+            if fn.startswith(name + SEG) and fn.endswith(".npy"):
+                os.remove(os.path.join(dirpath, fn))
+
+    def _path(self, k: int) -> str:
+        return os.path.join(self.dir, f"{self.name}{SEG}{k:06d}.npy")
+
+    def append(self, a) -> None:
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        if a.shape[1:] != self.row_shape:
+            raise ValueError(f"{self.name}: row shape {a.shape[1:]} != {self.row_shape}")
+        if not len(a):
+            return
+        ns = max(1, min(self.SPLIT, len(a))) if a.nbytes >= self.MIN_SPLIT_BYTES else 1
+        cuts = [len(a) * i // ns for i in range(ns + 1)]
+        jobs = [(self._path(self.k + i), a[cuts[i]:cuts[i + 1]]) for i in range(ns)]
+        self.k += ns
+        if ns == 1:
+            _write_npy(*jobs[0])
+        else:
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._pool = ThreadPoolExecutor(self.SPLIT, thread_name_prefix="shifu-seg-write")
+            list(self._pool.map(lambda j: _write_npy(*j), jobs))
+        self.rows += len(a)
+
+    def close(self) -> int:
+        if self.k == 0:                           # an empty array still names its segment
+            _write_npy(self._path(0), np.empty((0,) + self.row_shape, self.dtype))
+            self.k = 1
+        if self._pool is not None:
+            self._pool.shutdown()
+            self._pool = None
+        return self.rows
+
+    def abort(self) -> None:
+        if self._pool is not None:
+            self._pool.shutdown()
+            self._pool = None
+        for fn in os.listdir(self.dir):
+            if fn.startswith(self.name + SEG) and fn.endswith(".npy"):
+                os.remove(os.path.join(self.dir, fn))
+
+
+def part_names(pdir: str) -> list:
+    """Array names in a part directory (plain ``<name>.npy`` or segmented ``<name>@<k>.npy``)."""
+    return sorted({fn[:-4].split(SEG)[0] for fn in os.listdir(pdir) if fn.endswith(".npy")})
+
+
+def part_arrays(pdir: str, name: str, mmap: bool = True) -> list:
+    """The arrays holding ``name`` in a part directory, in row order (segments opened by a
+    thread pool: a 20M-row cache has a few thousand)."""
+    mode = "r" if mmap else None
+    one = os.path.join(pdir, f"{name}.npy")
+    if os.path.exists(one):
+        return [np.load(one, mmap_mode=mode)]
+    segs = sorted(fn for fn in os.listdir(pdir) if fn.startswith(name + SEG) and fn.endswith(".npy"))
+    if len(segs) < 64:
+        return [np.load(os.path.join(pdir, fn), mmap_mode=mode) for fn in segs]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(8) as ex:
+        return list(ex.map(lambda fn: np.load(os.path.join(pdir, fn), mmap_mode=mode), segs))
+
+
 class RowParts:
     """Row-wise concatenation of memory-mapped part arrays (same dtype / trailing shape).
 
@@ -108,12 +205,18 @@ class RowParts:
         return int(np.prod(self.shape)) * self.dtype.itemsize
 
     def _rows(self, lo: int, hi: int):
+        """Views of the parts covering rows [lo, hi), in order."""
         out = []
-        for k, p in enumerate(self.parts):
+        k0 = max(0, int(np.searchsorted(self.offsets, lo, side="right")) - 1)
+        for k in range(k0, len(self.parts)):
+            if self.offsets[k] >= hi:
+                break
             a, b = max(lo, self.offsets[k]), min(hi, self.offsets[k + 1])
             if a < b:
-                out.append(p[a - self.offsets[k]: b - self.offsets[k]])
+                out.append(self.parts[k][a - self.offsets[k]: b - self.offsets[k]])
         return out
+
+    blocks = _rows
 
     def __getitem__(self, idx):
         rest = ()
@@ -165,9 +268,9 @@ def load_parts(path: str, meta: dict, mmap: bool = True) -> dict:
     """name -> RowParts (or the single part's array) of a partitioned cache."""
     arrays = {}
     parts = [p for p in meta["parts"] if p["n"] > 0] or meta["parts"][:1]
-    names = sorted({fn[:-4] for p in parts for fn in os.listdir(os.path.join(path, p["dir"])) if fn.endswith(".npy")})
+    names = sorted({nm for p in parts for nm in part_names(os.path.join(path, p["dir"]))})
     for name in names:
-        arrs = [np.load(os.path.join(path, p["dir"], f"{name}.npy"), mmap_mode="r" if mmap else None) for p in parts]
+        arrs = [x for p in parts for x in part_arrays(os.path.join(path, p["dir"]), name, mmap)]
         arrays[name] = arrs[0] if len(arrs) == 1 else RowParts(arrs)
     return arrays
 
@@ -181,6 +284,7 @@ class Bf16Rows:
     :meth:`device_rows` moves the bf16 bits to the GPU as they are (no host fp32 expansion)."""
 
     COPY_THREADS = int(os.environ.get("SHIFU_COPY_THREADS", "8"))
+    LAST_STATS: dict = {}                        # device_rows: allocation / host copy / DMA wait seconds
 
     def __init__(self, raw, width: int, cols=None):
         self.raw = raw
@@ -215,10 +319,15 @@ class Bf16Rows:
         H2D on a copy stream, so the host copy of block i + 1 overlaps the DMA of block i:
         50 GB/s from a /dev/shm cache with 8 threads against 13.6 GB/s for the plain pageable
         upload (``COPY_THREADS = 0``; profiles/r4/upload_lab_r4n.txt)."""
+        import time
         import torch
+        st = {"alloc_s": 0.0, "copy_s": 0.0, "wait_s": 0.0, "blocks": 0}
+        Bf16Rows.LAST_STATS = st
+        t_a = time.perf_counter()
         n = len(self.raw)
         dev = torch.device(device)
         out = torch.empty((n if rows is None else len(rows), self.width), dtype=torch.bfloat16, device=dev)
+        st["alloc_s"] = time.perf_counter() - t_a
         cols_d = None if self.cols is None else torch.as_tensor(self.cols, device=dev)
         ridx = None if rows is None else np.asarray(rows, dtype=np.int64)
         gpu = dev.type == "cuda" and self.COPY_THREADS > 0
@@ -243,13 +352,25 @@ class Bf16Rows:
                 if gpu:
                     k = i & 1
                     i += 1
+                    t_w = time.perf_counter()
                     if evs[k] is not None:
                         evs[k].synchronize()          # the DMA that last read this buffer is done
+                    t_c = time.perf_counter()
+                    st["wait_s"] += t_c - t_w
+                    st["blocks"] += 1
                     h = pins[k][: (r1 - r0) * kp].numpy().reshape(r1 - r0, kp)
-                    src = self.raw[r0:r1].view(np.int16)
-                    cuts = np.linspace(0, r1 - r0, self.COPY_THREADS + 1).astype(np.int64)
-                    list(pool.map(lambda t: np.copyto(h[cuts[t]:cuts[t + 1]], src[cuts[t]:cuts[t + 1]]),
-                                  range(self.COPY_THREADS)))
+                    # (dst row, source view) pieces: a segmented cache's slice is several views;
+                    # each piece is cut over the copy threads (never concatenated first)
+                    srcs = self.raw.blocks(r0, r1) if hasattr(self.raw, "blocks") else [self.raw[r0:r1]]
+                    jobs, d0 = [], 0
+                    for sv in srcs:
+                        sv = sv.view(np.int16)
+                        cuts = np.linspace(0, len(sv), self.COPY_THREADS + 1).astype(np.int64)
+                        jobs += [(d0 + int(cuts[t]), sv[cuts[t]:cuts[t + 1]]) for t in range(self.COPY_THREADS)
+                                 if cuts[t + 1] > cuts[t]]
+                        d0 += len(sv)
+                    list(pool.map(lambda j: np.copyto(h[j[0]: j[0] + len(j[1])], j[1]), jobs))
+                    st["copy_s"] += time.perf_counter() - t_c
                     with torch.cuda.stream(cstream):
                         blk = torch.empty((r1 - r0, kp), dtype=torch.int16, device=dev)
                         blk.copy_(pins[k][: (r1 - r0) * kp].view(r1 - r0, kp), non_blocking=True)

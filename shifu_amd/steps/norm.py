@@ -143,7 +143,7 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     from ..config import environment
     from ..data import stream as DS
     from ..data.purifier import plan_dataset
-    from ..data.rowstore import NpyAppender, write_parts_meta
+    from ..data.rowstore import SegmentAppender, write_parts_meta
     from ..parallel import dist
     mc = ms.mc
     info = dist.info()
@@ -159,6 +159,7 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     # two rotating pinned output buffers: chunk i is written while chunk i + 1 is normalized
     nplan = N.NormPlan(mc, ms.ccs, cols, want_x=True, want_codes=is_tree, x_dtype=x_dtype, device=dev,
                        pinned_out=2 if dev is not None else 0)
+    nplan.async_out = dev is not None        # the writer waits for the chunk's D2H, not the consumer
     chunk = int(float(environment.get("shifu.norm.chunkMB", 1024 if dev is not None else 256)) * (1 << 20))
     outs = [out_x] + ([out_tree] if is_tree else [])
     if info.rank == 0:
@@ -171,19 +172,24 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     for o in outs:
         os.makedirs(os.path.join(o, pdir), exist_ok=True)
     xname = "Xb" if x_dtype == "bf16" else "X"
-    apx = {xname: NpyAppender(os.path.join(out_x, pdir, f"{xname}.npy"), np.uint16 if x_dtype == "bf16" else np.float32,
-                              (nplan.kpad if x_dtype == "bf16" else nplan.width,)),
-           "y": NpyAppender(os.path.join(out_x, pdir, "y.npy"), np.float32),
-           "w": NpyAppender(os.path.join(out_x, pdir, "w.npy"), np.float32)}
+    # segmented part files: a chunk's rows go out as several files written at once (one tmpfs
+    # inode takes one writer at a time; data/rowstore.SegmentAppender)
+    xd, td = os.path.join(out_x, pdir), os.path.join(out_tree, pdir)
+    apx = {xname: SegmentAppender(xd, xname, np.uint16 if x_dtype == "bf16" else np.float32,
+                                  (nplan.kpad if x_dtype == "bf16" else nplan.width,)),
+           "y": SegmentAppender(xd, "y", np.float32),
+           "w": SegmentAppender(xd, "w", np.float32)}
     apt = {}
     if is_tree:
-        apt = {"codes": NpyAppender(os.path.join(out_tree, pdir, "codes.npy"), nplan.code_dtype, (len(cols),)),
-               "y": NpyAppender(os.path.join(out_tree, pdir, "y.npy"), np.float32),
-               "w": NpyAppender(os.path.join(out_tree, pdir, "w.npy"), np.float32)}
+        apt = {"codes": SegmentAppender(td, "codes", nplan.code_dtype, (len(cols),)),
+               "y": SegmentAppender(td, "y", np.float32),
+               "w": SegmentAppender(td, "w", np.float32)}
     counters = {}
     n_local = 0
 
-    def write(res, y, w):
+    def write(res, y, w, ev):
+        if ev is not None:
+            ev.synchronize()                  # this chunk's D2H into the pinned buffers landed
         apx[xname].append(res[xname])
         apx["y"].append(y)
         apx["w"].append(w)
@@ -207,7 +213,7 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
                 with DS._span("write_wait"):
                     if pending is not None:
                         pending.result()
-                pending = ex.submit(write, res, y, w)
+                pending = ex.submit(write, res, y, w, nplan.last_event)
                 n_local += md.n
                 for k, v in md.counters.as_dict().items():
                     counters[k] = counters.get(k, 0) + v
@@ -216,6 +222,11 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     finally:
         for a in list(apx.values()) + list(apt.values()):
             a.close()
+    if dev is not None:
+        import torch
+        getattr(nplan, "_bufs", {}).clear()
+        getattr(nplan, "_pins", {}).clear()
+        torch.cuda.empty_cache()       # hand the pass's cached blocks back (the next step allocates big)
     got = dist.all_gather_objects((n_local, counters))
     rows = [g[0] for g in got]
     tot_counters = {}
@@ -252,20 +263,20 @@ def _shuffle_parts(path: str, rows: list, seed: int) -> None:
     blocks, then the new parts replace the old ones."""
     import os
     import shutil
-    from ..data.rowstore import NpyAppender, RowParts
+    from ..data.rowstore import NpyAppender, RowParts, part_arrays, part_names
     from ..parallel import dist
     info = dist.info()
     n = int(sum(rows))
     perm = np.random.default_rng(seed).permutation(n)
     parts = [f"part-{r:05d}" for r in range(len(rows))]
-    names = sorted(fn[:-4] for fn in os.listdir(os.path.join(path, parts[info.rank])) if fn.endswith(".npy"))
+    names = part_names(os.path.join(path, parts[info.rank]))
     lo, hi = n * info.rank // info.world_size, n * (info.rank + 1) // info.world_size
     mine = perm[lo:hi]
     newdir = os.path.join(path, f"shuf-{info.rank:05d}")
     os.makedirs(newdir, exist_ok=True)
     block = 1 << 20
     for name in names:
-        arrs = [np.load(os.path.join(path, p, f"{name}.npy"), mmap_mode="r") for p in parts]
+        arrs = [x for p in parts for x in part_arrays(os.path.join(path, p), name)]
         src = RowParts(arrs)
         ap = NpyAppender(os.path.join(newdir, f"{name}.npy"), src.dtype, src.shape[1:])
         try:

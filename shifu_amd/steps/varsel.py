@@ -53,10 +53,12 @@ def _normalized_rows(ms, cols, device=None):
     here avoids a second parse + normalisation of the raw text."""
     from .base import load_dataset_cache
     from .train import _shard
+    t0 = time.perf_counter()
     cache = load_dataset_cache(ms.pf.normalized_data)
     if cache is None:
         return None
     meta, arr = cache
+    t_open = time.perf_counter() - t0
     if meta.get("input_nums") != [c.num for c in cols] or "X" not in arr or "y" not in arr:
         return None
     info = dist.info()
@@ -72,7 +74,9 @@ def _normalized_rows(ms, cols, device=None):
         X = np.asarray(_shard(arr["X"], info), dtype=np.float32)
     y = np.asarray(_shard(arr["y"], info), dtype=np.float32).reshape(len(X), -1)[:, :1]
     w = np.asarray(_shard(arr["w"], info), dtype=np.float32) if "w" in arr else np.ones(len(X), np.float32)
-    _log.info("varsel: sensitivity rows from NormalizedData (%d x %d)", X.shape[0], X.shape[1])
+    _log.info("varsel: sensitivity rows from NormalizedData (%d x %d): open %.2fs, rows %.2fs %s", X.shape[0],
+              X.shape[1], t_open, time.perf_counter() - t0 - t_open,
+              {k: round(v, 2) for k, v in Bf16Rows.LAST_STATS.items()} if isinstance(arr["X"], Bf16Rows) else "")
     return X, y, w
 
 

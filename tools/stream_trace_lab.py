@@ -26,11 +26,53 @@ def overlap_table(ev):
     return {str(k): round(v, 3) for k, v in sorted(busy.items())}
 
 
+def read_back(path):
+    """Seconds to bring the written NormalizedData to HBM: Bf16Rows.device_rows (mmap + threaded
+    copies into page-locked buffers + H2D), and plain 8-thread preads of the segment files into
+    page-locked memory (no page faults) for comparison."""
+    import glob
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    import torch
+    from shifu_amd.steps.base import load_dataset_cache
+    res = {}
+    _, arr = load_dataset_cache(path)
+    t = time.perf_counter()
+    x = arr["X"].device_rows(torch.device("cuda"))
+    torch.cuda.synchronize()
+    res["device_rows_s"] = round(time.perf_counter() - t, 3)
+    res["gb"] = round(x.numel() * 2 / 1e9, 2)
+    del x
+    files = sorted(glob.glob(os.path.join(path, "part-*", "Xb*.npy")))
+    sizes = [os.path.getsize(f) for f in files]
+    buf = torch.empty(max(sizes), dtype=torch.uint8, pin_memory=True)
+    bufs = [torch.empty(max(sizes), dtype=torch.uint8, pin_memory=True) for _ in range(8)]
+
+    def rd(i):
+        f, n = files[i], sizes[i]
+        mv = memoryview(bufs[i % 8].numpy())[:n]
+        fd = os.open(f, os.O_RDONLY)
+        off = 0
+        while off < n:
+            off += os.preadv(fd, [mv[off:]], off)
+        os.close(fd)
+    t = time.perf_counter()
+    with ThreadPoolExecutor(8) as ex:
+        list(ex.map(rd, range(len(files))))
+    res["pread8_s"] = round(time.perf_counter() - t, 3)
+    res["files"] = len(files)
+    del buf
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--cols", type=int, default=1600)
     ap.add_argument("--work", default="/tmp/stream_trace_lab")
+    ap.add_argument("--shm-tmp", action="store_true", help="model set tmp/ (NormalizedData) on /dev/shm")
+    ap.add_argument("--read-back", action="store_true",
+                    help="then time reading the NormalizedData rows back to HBM (device_rows, preads)")
     a = ap.parse_args()
     from shifu_amd.config import environment
     from shifu_amd.config.model_config import ModelConfig
@@ -42,6 +84,12 @@ def main():
     shutil.rmtree(a.work, ignore_errors=True)
     os.makedirs(a.work)
     root = create_model_set("pipe", "NN", parent=a.work)
+    if a.shm_tmp:
+        shm = "/dev/shm/stream_trace_lab_tmp"
+        shutil.rmtree(shm, ignore_errors=True)
+        os.makedirs(shm)
+        shutil.rmtree(os.path.join(root, "tmp"), ignore_errors=True)
+        os.symlink(shm, os.path.join(root, "tmp"))
     d = os.path.join(root, "data", "DataSet1")
     os.makedirs(d)
     if _native.rt().shifu_gen_csv(d.encode(), a.rows, a.cols, 3, 11, 0.02, 20, 16):
@@ -80,8 +128,12 @@ def main():
                   "w") as f:
             json.dump([list(e) for e in ev], f)
         print(json.dumps({step: out[step]}), flush=True)
+    if a.read_back:
+        out["read_back"] = read_back(os.path.join(root, "tmp", "NormalizedData"))
+        print(json.dumps({"read_back": out["read_back"]}), flush=True)
     print(json.dumps(out))
     shutil.rmtree(a.work, ignore_errors=True)
+    shutil.rmtree("/dev/shm/stream_trace_lab_tmp", ignore_errors=True)
 
 
 if __name__ == "__main__":
