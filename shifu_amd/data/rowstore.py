@@ -319,6 +319,12 @@ class Bf16Rows:
         H2D on a copy stream, so the host copy of block i + 1 overlaps the DMA of block i:
         50 GB/s from a /dev/shm cache with 8 threads against 13.6 GB/s for the plain pageable
         upload (``COPY_THREADS = 0``; profiles/r4/upload_lab_r4n.txt)."""
+        return self.device_rows_multi(device, [rows], block)[0]
+
+    def device_rows_multi(self, device, row_sets, block: int = 1 << 18) -> list:
+        """:meth:`device_rows` for several SORTED row sets (None = every row) in ONE pass over the
+        host rows: each block is copied and uploaded once and every set gathers its rows from it
+        (the training and validation rows of a split are one read of the cache, not two)."""
         import time
         import torch
         st = {"alloc_s": 0.0, "copy_s": 0.0, "wait_s": 0.0, "blocks": 0}
@@ -326,10 +332,10 @@ class Bf16Rows:
         t_a = time.perf_counter()
         n = len(self.raw)
         dev = torch.device(device)
-        out = torch.empty((n if rows is None else len(rows), self.width), dtype=torch.bfloat16, device=dev)
+        sets = [None if r is None else np.asarray(r, dtype=np.int64) for r in row_sets]
+        outs = [torch.empty((n if r is None else len(r), self.width), dtype=torch.bfloat16, device=dev) for r in sets]
         st["alloc_s"] = time.perf_counter() - t_a
         cols_d = None if self.cols is None else torch.as_tensor(self.cols, device=dev)
-        ridx = None if rows is None else np.asarray(rows, dtype=np.int64)
         gpu = dev.type == "cuda" and self.COPY_THREADS > 0
         if gpu:
             kp = self.raw.shape[1]
@@ -339,16 +345,23 @@ class Bf16Rows:
             main = torch.cuda.current_stream(dev)
             from concurrent.futures import ThreadPoolExecutor
             pool = ThreadPoolExecutor(self.COPY_THREADS)
-        lo_out, i = 0, 0
+        los, i = [0] * len(sets), 0
         try:
-            for r0 in range(0, n, block):
-                r1 = min(n, r0 + block)
-                if ridx is not None:
-                    a, b = np.searchsorted(ridx, r0), np.searchsorted(ridx, r1)
-                    if a == b:
+            for b0 in range(0, n, block):
+                b1 = min(n, b0 + block)
+                sels = []
+                r0, r1 = b1, b0
+                for r in sets:
+                    if r is None:
+                        sels.append(None)
+                        r0, r1 = b0, b1
                         continue
-                    sel = ridx[a:b]
-                    r0, r1 = int(sel[0]), int(sel[-1]) + 1
+                    a_, c_ = np.searchsorted(r, b0), np.searchsorted(r, b1)
+                    sels.append(r[a_:c_])
+                    if c_ > a_:
+                        r0, r1 = min(r0, int(r[a_])), max(r1, int(r[c_ - 1]) + 1)
+                if r1 <= r0:
+                    continue
                 if gpu:
                     k = i & 1
                     i += 1
@@ -381,18 +394,25 @@ class Bf16Rows:
                 else:
                     blk = torch.as_tensor(np.ascontiguousarray(self.raw[r0:r1]).view(np.int16), device=dev)
                 blk = blk.view(torch.bfloat16)
-                if ridx is not None:
-                    blk = blk.index_select(0, torch.as_tensor(sel - r0, device=dev))
-                blk = blk[:, : self.width] if cols_d is None else blk.index_select(1, cols_d)
-                out[lo_out: lo_out + len(blk)] = blk
-                lo_out += len(blk)
+                for s_, sel in enumerate(sels):
+                    if sel is not None and not len(sel):
+                        continue
+                    if sel is None:
+                        part = blk[b0 - r0: b1 - r0]
+                    else:
+                        ix = torch.from_numpy(sel - r0)
+                        ix = ix.pin_memory().to(dev, non_blocking=True) if gpu else ix.to(dev)
+                        part = blk.index_select(0, ix)
+                    part = part[:, : self.width] if cols_d is None else part.index_select(1, cols_d)
+                    outs[s_][los[s_]: los[s_] + len(part)] = part
+                    los[s_] += len(part)
         finally:
             if gpu:
                 pool.shutdown()
                 for e in evs:
                     if e is not None:
                         e.synchronize()
-        return out
+        return outs
 
     def __getitem__(self, idx):
         rest = ()

@@ -13,6 +13,8 @@ regression value; weights from the weight column/expression.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
 from ..algos import normalize as N
@@ -202,6 +204,7 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     # chunk i+1 is normalized; one write in flight keeps the part files in row order
     from concurrent.futures import ThreadPoolExecutor
     pending = None
+    t_pass = time.perf_counter()
     try:
         with ThreadPoolExecutor(1, thread_name_prefix="shifu-norm-write") as ex:
             gpu_cols = [c.name for c in cols if not c.is_categorical()] if dev is not None else None
@@ -222,11 +225,13 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     finally:
         for a in list(apx.values()) + list(apt.values()):
             a.close()
+    t_rel = time.perf_counter()
     if dev is not None:
         import torch
         getattr(nplan, "_bufs", {}).clear()
         getattr(nplan, "_pins", {}).clear()
         torch.cuda.empty_cache()       # hand the pass's cached blocks back (the next step allocates big)
+    _log.info("norm pass %.2fs (writes closed), buffers released %.2fs", t_rel - t_pass, time.perf_counter() - t_rel)
     got = dist.all_gather_objects((n_local, counters))
     rows = [g[0] for g in got]
     tot_counters = {}

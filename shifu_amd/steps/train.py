@@ -570,7 +570,12 @@ class TrainStep:
             if isinstance(A, Bf16Rows) and tr.gpu:
                 return A.device_rows(tr.device, rows=idx)
             return torch.from_numpy(np.asarray(A[idx] if idx is not None else A, dtype=np.float32))
-        data = tr.prepare(rows_of(X, tri), yy[tri], w[tri])
+        split_dev = (vX is None and valid_m.any() and isinstance(X, Bf16Rows) and tr.gpu)
+        if split_dev:                 # training and validation rows from ONE read of the cache
+            Xt, Xv = X.device_rows_multi(tr.device, [tri, np.nonzero(valid_m)[0]])
+        else:
+            Xt = rows_of(X, tri)
+        data = tr.prepare(Xt, yy[tri], w[tri])
         vdata = None
         if vX is not None:
             vy = np.asarray(ts.vy, np.float32)
@@ -581,7 +586,7 @@ class TrainStep:
             vdata = tr.prepare(rows_of(vX, None), vy.reshape(len(vy), -1), np.asarray(ts.vw, np.float32))
         elif valid_m.any():
             vi = np.nonzero(valid_m)[0]
-            vdata = tr.prepare(rows_of(X, vi), yy[vi], np.asarray(ts.w)[vi])
+            vdata = tr.prepare(Xv if split_dev else rows_of(X, vi), yy[vi], np.asarray(ts.w)[vi])
         n_train = torch.tensor([float(len(tri))], dtype=torch.float64, device=tr.device)
         dist.all_reduce_(n_train)
         n_train = float(n_train.item())

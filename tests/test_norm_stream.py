@@ -225,6 +225,13 @@ def test_bf16rows_subset_and_device_rows():
         np.testing.assert_array_equal(d.float().numpy(), want)
         d = view.device_rows(torch.device("cpu"), rows=rows, block=128)
         np.testing.assert_array_equal(d.float().numpy(), want[rows])
+        # several row sets from one pass (train / validation split), an empty set included
+        rest = np.setdiff1d(np.arange(n), rows)
+        da, db, de, dn = view.device_rows_multi(torch.device("cpu"), [rows, rest, rows[:0], None], block=128)
+        np.testing.assert_array_equal(da.float().numpy(), want[rows])
+        np.testing.assert_array_equal(db.float().numpy(), want[rest])
+        assert de.shape == (0, want.shape[1])
+        np.testing.assert_array_equal(dn.float().numpy(), want)
     np.testing.assert_array_equal(np.asarray(sub.subset([1, 2])), full[:, [0, 36]])
 
 
@@ -254,10 +261,17 @@ def test_bf16_cache_varsel_train_gpu_match_host_expansion(tmp_path, monkeypatch)
     calls = []
     orig = rowstore.Bf16Rows.device_rows
 
+    orig_m = rowstore.Bf16Rows.device_rows_multi
+
     def spy(self, device, rows=None, block=1 << 18):
         calls.append(len(self) if rows is None else len(rows))
         return orig(self, device, rows, block)
+
+    def spy_m(self, device, row_sets, block=1 << 18):
+        calls.extend(len(self) if r is None else len(r) for r in row_sets)
+        return orig_m(self, device, row_sets, block)
     monkeypatch.setattr(rowstore.Bf16Rows, "device_rows", spy)
+    monkeypatch.setattr(rowstore.Bf16Rows, "device_rows_multi", spy_m)
     run_varsel(a)
     run_train(a)
     assert len(calls) >= 2, calls                       # varsel rows + train rows went as bf16
@@ -266,6 +280,8 @@ def test_bf16_cache_varsel_train_gpu_match_host_expansion(tmp_path, monkeypatch)
         x = np.asarray(self) if rows is None else self[rows]
         return torch.from_numpy(np.ascontiguousarray(x)).to(device, torch.bfloat16)
     monkeypatch.setattr(rowstore.Bf16Rows, "device_rows", host)
+    monkeypatch.setattr(rowstore.Bf16Rows, "device_rows_multi",
+                        lambda self, device, row_sets, block=1 << 18: [host(self, device, r) for r in row_sets])
     run_varsel(b)
     run_train(b)
     sa = open(os.path.join(a, "varsel", "se.0")).read().split("\n")
