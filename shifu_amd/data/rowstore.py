@@ -340,6 +340,11 @@ class Bf16Rows:
         if gpu:
             kp = self.raw.shape[1]
             pins = [torch.empty(block * kp, dtype=torch.int16, pin_memory=True) for _ in range(2)]
+            # two device staging blocks reused in turn (a fresh 0.8 GB allocation per block kept
+            # the caching allocator busy): the copy stream waits until the main stream is done
+            # with a block's previous contents before the next DMA into it
+            dbufs = [torch.empty((min(block, n), kp), dtype=torch.int16, device=dev) for _ in range(2)]
+            used = [None, None]
             evs = [None, None]
             cstream = torch.cuda.Stream(dev)
             main = torch.cuda.current_stream(dev)
@@ -385,12 +390,13 @@ class Bf16Rows:
                     list(pool.map(lambda j: np.copyto(h[j[0]: j[0] + len(j[1])], j[1]), jobs))
                     st["copy_s"] += time.perf_counter() - t_c
                     with torch.cuda.stream(cstream):
-                        blk = torch.empty((r1 - r0, kp), dtype=torch.int16, device=dev)
+                        if used[k] is not None:
+                            cstream.wait_event(used[k])
+                        blk = dbufs[k][: r1 - r0]
                         blk.copy_(pins[k][: (r1 - r0) * kp].view(r1 - r0, kp), non_blocking=True)
                         evs[k] = torch.cuda.Event()
                         evs[k].record(cstream)
                     main.wait_event(evs[k])
-                    blk.record_stream(main)
                 else:
                     blk = torch.as_tensor(np.ascontiguousarray(self.raw[r0:r1]).view(np.int16), device=dev)
                 blk = blk.view(torch.bfloat16)
@@ -406,10 +412,13 @@ class Bf16Rows:
                     part = part[:, : self.width] if cols_d is None else part.index_select(1, cols_d)
                     outs[s_][los[s_]: los[s_] + len(part)] = part
                     los[s_] += len(part)
+                if gpu:
+                    used[k] = torch.cuda.Event()
+                    used[k].record(main)
         finally:
             if gpu:
                 pool.shutdown()
-                for e in evs:
+                for e in evs + used:
                     if e is not None:
                         e.synchronize()
         return outs

@@ -226,12 +226,16 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
         for a in list(apx.values()) + list(apt.values()):
             a.close()
     t_rel = time.perf_counter()
+    mem = ""
     if dev is not None:
         import torch
+        mem = " (HBM reserved %.1f GB, peak allocated %.1f GB)" % (torch.cuda.memory_reserved(dev) / 1e9,
+                                                                  torch.cuda.max_memory_allocated(dev) / 1e9)
         getattr(nplan, "_bufs", {}).clear()
         getattr(nplan, "_pins", {}).clear()
         torch.cuda.empty_cache()       # hand the pass's cached blocks back (the next step allocates big)
-    _log.info("norm pass %.2fs (writes closed), buffers released %.2fs", t_rel - t_pass, time.perf_counter() - t_rel)
+    _log.info("norm pass %.2fs (writes closed), buffers released %.2fs%s", t_rel - t_pass, time.perf_counter() - t_rel,
+              mem)
     got = dist.all_gather_objects((n_local, counters))
     rows = [g[0] for g in got]
     tot_counters = {}
