@@ -686,8 +686,20 @@ class TreeTrainer:
                 p2r = None if self._root_level else pos2row      # root: positions are rows
                 by_pos = p2r is not None and self._wg_pos is not None
                 wv, gv = self._wg_pos if by_pos else (w, g)
-                nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, QF, p2r, wv, gv, int(by_pos), it, len(items),
-                             slab, F, self.scale_w, self.scale_g, self._nmod, 0, st)
+                rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
+                if HIST64 and not self._root_level and rows_built >= HIST64_MIN_NODE_ROWS * max(1, n_built):
+                    # half-record blocks: items of groups 2j, 2j + 1 of one node / row range paired
+                    key = np.stack([items[:, 0], items[:, 1], items[:, 2], items[:, 3] >> 1], 1)
+                    uniq, inv = np.unique(key, axis=0, return_inverse=True)
+                    pairs = np.full((len(uniq), 2), -1, np.int32)
+                    pairs[inv.reshape(-1), items[:, 3] & 1] = np.arange(len(items), dtype=np.int32)
+                    pairs_t = _h2d(pairs, self.dev)        # lives until the level's D2H below
+                    nat.call_hip("shifu_gbdt_hist64", d.kbins, d.group_stride, p2r, wv, gv, int(by_pos), it,
+                                 len(items), pairs_t, len(pairs), slab, F, self.scale_w, self.scale_g,
+                                 self._nmod, st)
+                else:
+                    nat.call_hip("shifu_gbdt_hist", d.kbins, d.group_stride, QF, p2r, wv, gv, int(by_pos), it,
+                                 len(items), slab, F, self.scale_w, self.scale_g, self._nmod, 0, st)
             if ls is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev1.record()
@@ -1399,6 +1411,13 @@ ROOT_QUAD = os.environ.get("SHIFU_GBDT_ROOT_QUAD", "1") != "0"
 ROOT_G32 = os.environ.get("SHIFU_GBDT_ROOT_G32", "1") != "0"
 # final-level prediction update in row windows of LEAF_W rows, LEAF_Y blocks per window
 LEAF_WINDOW = os.environ.get("SHIFU_GBDT_LEAF_WINDOW", "1") != "0"
+# below-root histograms over 64-feature half records (gbdt_hist64_kernel); 0 = 32-feature items
+HIST64 = os.environ.get("SHIFU_GBDT_HIST64", "1") != "0"
+# ... on levels whose built nodes average at least this many rows: the 1024-thread blocks (one per
+# CU) win on long row ranges (balanced levels of 11-46M rows per node: 13.9-14.6 vs 15.4-16.2 ms)
+# and lose on short ones (5.6M: even; 8.5M of the favourable labels: 12.6 vs 12.2 ms; 2M: 1.9 vs
+# 1.0 ms), profiles/r5/gbdt/hist64_*
+HIST64_MIN_NODE_ROWS = int(os.environ.get("SHIFU_GBDT_HIST64_MIN_NODE_ROWS", "10000000"))
 LEAF_W = int(os.environ.get("SHIFU_GBDT_LEAF_W", str(1 << 16)))
 LEAF_Y = int(os.environ.get("SHIFU_GBDT_LEAF_Y", "16"))
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on

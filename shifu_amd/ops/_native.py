@@ -75,6 +75,7 @@ HIP_SIGNATURES = {
     "shifu_gbdt_hist_root_tile": "pllpppipddips",
     "shifu_gbdt_tile_bins": "pllipls",
     "shifu_gbdt_wg_stats": "pplpps",
+    "shifu_gbdt_hist64": "plppp" "ipip" "ip" "iddl" "s",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
     "shifu_gbdt_partition_flag": "plpl" "pppppppp" "ll" "pppp" "fi" "s",
     "shifu_gbdt_bitrank": "pppip" "s",

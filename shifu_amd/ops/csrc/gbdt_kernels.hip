@@ -260,6 +260,114 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Below-root histogram over HALF records: one 1024-thread block builds the packed u64
+// histograms of 64 features (two 32-feature group items of one node and row range) for its
+// rows, 4 threads per row each reading 16 B of the row's 64-B half line.  The per-group kernel
+// above has 4 blocks read 32 B each of every 128-B line: its ablations put the non-root levels on
+// that gather (14.4 of 15.7 ms per level with the LDS atomics removed, profiles/r5/gbdt), and
+// every 32-B piece is its own L2 request.  Here a row's 64 B leave L2 as one request.
+// LDS [4 quarters][NB][16] u64 = 128 KiB (one block per CU, 16 waves); the same per-lane byte
+// rotation keeps each 16-lane group on 16 distinct bank pairs; 4096 rows between unpacks.
+// ---------------------------------------------------------------------------------------
+constexpr int H6_T = 1024;
+constexpr int H6_RPP = H6_T / 4;                 // rows per pass
+constexpr int H6_NE = 4 * NB * 16 / H6_T;        // entries each thread unpacks (16)
+
+__global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int* pairs) {
+  constexpr int HFLUSH = 4096 / H6_RPP;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long h6[];    // [4][NB][16]
+  const int pr = xcd_remap(blockIdx.x, gridDim.x);
+  // items of groups 2j (ia) and 2j + 1 (ib) of one node and row range; either may be -1
+  const int ia = pairs[pr * 2], ib = pairs[pr * 2 + 1], i0 = ia >= 0 ? ia : ib;
+  const int lo = a.items[i0 * 4 + 1], hi = a.items[i0 * 4 + 2], grp = a.items[i0 * 4 + 3] & ~1;
+  for (int i = threadIdx.x; i < 4 * NB * 16; i += H6_T) h6[i] = 0ull;
+  __syncthreads();
+  const int qt = threadIdx.x & 3, r = threadIdx.x & 15, t4 = threadIdx.x >> 2;
+  // grp is even: its 64-B half of the quad record starts at byte (grp & 3) * 32 (0 or 64)
+  const uint8_t* gb = a.bins + (size_t)(grp >> 2) * a.gs + (grp & 3) * FG + qt * 16;
+  unsigned long long* base = h6 + qt * NB * 16;
+  auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * QF); };
+  long long accw[H6_NE], accg[H6_NE];
+#pragma unroll
+  for (int k = 0; k < H6_NE; ++k) { accw[k] = 0; accg[k] = 0; }
+  auto update = [&](float wv, float gv, const uint4& bv) {
+    if (wv == 0.f) return;
+    const unsigned long long q = ((unsigned long long)__float2uint_rn(wv * a.scale_w) << PACK_G) +
+                                 (unsigned long long)(long long)__float2int_rn(wv * gv * a.scale_g);
+    const uint32_t W[4] = {bv.x, bv.y, bv.z, bv.w};
+    uint32_t X[4], Y[4], R[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) X[k] = pick(W[k], W[(k + 1) & 3], r & 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Y[k] = pick(X[k], X[(k + 2) & 3], r & 8);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) R[k] = __builtin_amdgcn_alignbyte(Y[(k + 1) & 3], Y[k], r & 3);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
+      atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
+    }
+  };
+  auto flush = [&](int& it) {
+    if (++it == HFLUSH) {
+      it = 0;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < H6_NE; ++k) {
+        const int e = threadIdx.x + k * H6_T;
+        unpack_add(h6[e], accw[k], accg[k]);
+        h6[e] = 0ull;
+      }
+      __syncthreads();
+    }
+  };
+  // software pipeline as gbdt_hist_kernel<PF>: next pass's (bins, w, g) and the pos2row gather
+  // two passes ahead in flight while a pass's atomics run
+  auto row_of = [&](int p) { const int pc = min(p, hi - 1); return a.pos2row ? a.pos2row[pc] : pc; };
+  auto wg_at = [&](int p, int rr) { return a.wg_by_pos ? min(p, hi - 1) : rr; };
+  int it = 0;
+  float wc, gc;
+  uint4 bc;
+  {
+    const int p = lo + t4, rr = row_of(p), k = wg_at(p, rr);
+    wc = a.w[k]; gc = a.g[k]; bc = rec(rr);
+  }
+  int rn = row_of(lo + H6_RPP + t4);
+  for (int p0 = lo; p0 < hi; p0 += H6_RPP) {          // block-uniform trip count (unpack barriers)
+    const int k = wg_at(p0 + H6_RPP + t4, rn);
+    const float wn = a.w[k], gn = a.g[k];
+    const uint4 bn = rec(rn);
+    rn = row_of(p0 + 2 * H6_RPP + t4);
+    update(p0 + t4 < hi ? wc : 0.f, gc, bc);
+    flush(it);
+    wc = wn; gc = gn; bc = bn;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < H6_NE; ++k) unpack_add(h6[threadIdx.x + k * H6_T], accw[k], accg[k]);
+  // slabs: entry e = (quarter e >> 12, bin (e >> 4) & 255, feature 16 quarter + (e & 15)) of the
+  // 64; features 0-31 -> item ia, 32-63 -> item ib.  Transposed through LDS ([64 f][NB] int64 =
+  // 128 KiB) per statistic for coalesced slab stores.
+  long long* tsm = (long long*)h6;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < H6_NE; ++k) {
+      const int e = threadIdx.x + k * H6_T;
+      const int f = (e >> 12) * 16 + (e & 15), b = (e >> 4) & (NB - 1);
+      tsm[f * NB + b] = st ? accg[k] : accw[k];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * FG * NB; i += H6_T) {
+      const int half = i / (FG * NB);
+      const int itm = half ? ib : ia;
+      if (itm >= 0) a.slab[((size_t)itm * 2 + st) * FG * NB + (i % (FG * NB))] = tsm[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Node histograms + split search.  One wave per (node, feature); 64 lanes x 4 bins.
 // mode 0: built node  -> hist = sum of its items' slabs
 // mode 1: derived node -> hist = parent_hist - sibling_hist (sibling built this level)
@@ -1092,6 +1200,20 @@ SHIFU_API int shifu_gbdt_hist(const void* bins, long gs, int rec, const int* pos
   else if (pf == 3) hipLaunchKernelGGL((gbdt_hist_kernel<true, 1, 0>), dim3(n_items), dim3(HT), lds, stream, a);
   else if (pf) hipLaunchKernelGGL((gbdt_hist_kernel<true, 2, 0>), dim3(n_items), dim3(HT), lds, stream, a);
   else hipLaunchKernelGGL((gbdt_hist_kernel<false, 4, 0>), dim3(n_items), dim3(HT), lds, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// below-root histogram over half records (gbdt_hist64_kernel): pairs [n_pairs][2] of item ids
+// (same node / rows, groups 2j and 2j + 1; the second -1 when the group count is odd)
+SHIFU_API int shifu_gbdt_hist64(const void* bins, long gs, const int* pos2row, const float* w, const float* g,
+                                int wg_by_pos, const int* items, int n_items, const int* pairs, int n_pairs,
+                                void* slab, int n_feat, double scale_w, double scale_g, long nmod,
+                                hipStream_t stream) {
+  if (gs % QF || n_items <= 0 || n_pairs <= 0 || (wg_by_pos && nmod)) return -1;
+  HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, wg_by_pos, QF, items, (long long*)slab, n_items, n_feat,
+             (float)scale_w, (float)scale_g, nmod};
+  hipLaunchKernelGGL(gbdt_hist64_kernel, dim3(n_pairs), dim3(H6_T), 4 * NB * 16 * 8, stream, a, pairs);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -503,3 +503,33 @@ def test_gpu_leaf_window_update_matches_position_pass(w_rows, y_blocks, monkeypa
         assert (x.feat == y.feat).all() and (x.thr == y.thr).all()
         assert np.array_equal(x.value, y.value)
     assert torch.equal(a.pred, b.pred)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg,f", [("GBT", 100), ("GBT", 70), ("RF", 45)])
+def test_gpu_hist64_matches_group_items(alg, f, monkeypatch):
+    """Below-root histograms from 64-feature half-record blocks (paired 32-feature items, a lone
+    last group when the group count is odd, forest batches for RF) give the same trees and
+    predictions, bit for bit, as the per-group kernel."""
+    import torch
+    from shifu_amd.models import gbdt as gb
+    from shifu_amd.models.gbdt import TreeConfig, TreeTrainer, synthetic_binned
+    monkeypatch.setenv("SHIFU_RF_BATCH", "2")
+    monkeypatch.setattr(gb, "HIST64_MIN_NODE_ROWS", 0)        # every non-root level
+    data = synthetic_binned(150001, f, "cuda", seed=11, labels="balanced")
+    kw = dict(tree_num=3, max_depth=6, feature_subset_strategy="ALL", min_instances_per_node=2)
+    if alg == "RF":
+        kw.update(bagging_sample_rate=0.7, feature_subset_strategy="HALF")
+    else:
+        kw.update(learning_rate=0.1)
+    runs = []
+    for on in (True, False):
+        monkeypatch.setattr(gb, "HIST64", on)
+        tr = TreeTrainer(TreeConfig(alg, **kw), data)
+        tr.train()
+        runs.append(tr)
+    a, b = runs
+    for x, y in zip(a.trees, b.trees):
+        assert (x.feat == y.feat).all() and (x.thr == y.thr).all()
+        assert np.array_equal(x.value, y.value)
+    assert torch.equal(a.pred, b.pred)
