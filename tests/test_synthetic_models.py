@@ -79,8 +79,12 @@ def test_multiclass_nn(tmp_path, method):
     assert n_models == (3 if method == "ONEVSALL" else 1 * int(mc.train.get("baggingNum", 5)))
 
 
-def test_autotype_rebin_psi(tmp_path):
+def test_autotype_rebin_psi(tmp_path, monkeypatch):
+    """autoTypeThreshold with the documented ratio rule (the reference rule as written types a
+    column categorical only when a sampled item is blank: tests/test_autotype_stream.py)."""
+    from shifu_amd.config import environment
     from shifu_amd.utils.synthetic import make_model_set
+    monkeypatch.setitem(environment.props(), "shifu.autoType.rule", "ratio")
     root = make_model_set(str(tmp_path), "a", "NN", n_rows=1200)
     mc = _mc(root)
     mc.dataSet["autoType"] = True
