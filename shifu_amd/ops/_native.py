@@ -18,7 +18,8 @@ import threading
 from pathlib import Path
 
 LIB_DIR = Path(__file__).resolve().parent / "_lib"
-HIP_LIB = LIB_DIR / "libshifu_hip.so"
+# SHIFU_HIP_LIB: another build of the kernel library (same-box A/B runs of two builds in a lab)
+HIP_LIB = Path(os.environ["SHIFU_HIP_LIB"]) if os.environ.get("SHIFU_HIP_LIB") else LIB_DIR / "libshifu_hip.so"
 RT_LIB = LIB_DIR / "libshifu_rt.so"
 
 _lock = threading.Lock()
