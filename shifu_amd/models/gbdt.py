@@ -1419,7 +1419,7 @@ HIST64 = os.environ.get("SHIFU_GBDT_HIST64", "1") != "0"
 # 1.0 ms), profiles/r5/gbdt/hist64_*
 HIST64_MIN_NODE_ROWS = int(os.environ.get("SHIFU_GBDT_HIST64_MIN_NODE_ROWS", "10000000"))
 LEAF_W = int(os.environ.get("SHIFU_GBDT_LEAF_W", str(1 << 16)))
-LEAF_Y = int(os.environ.get("SHIFU_GBDT_LEAF_Y", "16"))
+LEAF_Y = int(os.environ.get("SHIFU_GBDT_LEAF_Y", "128"))   # 0.96 vs 2.13 ms with 16 (tools/leafwin_sweep.sh)
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on
 # power-of-two grids (|w*g| < 2^23 of the grid, the root's u32 w*g mode 2^3 coarser), summed
 # exactly in int64 (so every rank and every run finds the same splits)

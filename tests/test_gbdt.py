@@ -479,7 +479,7 @@ def test_gpu_feature_tiled_root_matches_quad_records(n, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w_rows,y_blocks", [(1000, 3), (1 << 16, 16)])
+@pytest.mark.parametrize("w_rows,y_blocks", [(1000, 3), (1 << 16, 128)])
 def test_gpu_leaf_window_update_matches_position_pass(w_rows, y_blocks, monkeypatch):
     """The final-level prediction update walked in row windows (per-node position sub-ranges found
     by binary search, XCD-ordered windows) gives the same trees and the same pred, bit for bit, as
