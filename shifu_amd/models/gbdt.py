@@ -553,47 +553,41 @@ class TreeTrainer:
     def _make_items(self, nodes, n_built):
         """Work items [n, 4] = (node_slot, lo, hi, group) for the built nodes, chunked for
         parallelism, and node_items [n_nodes, n_groups, max_items] (item ids, -1 padded).
-        Vectorized per node (numpy), order: node, group, chunk."""
-        target_items = TARGET_ITEMS
+        Vectorized over all nodes at once (it runs on the host between two GPU launches of every
+        level); order: node, quad, chunk, sub-group."""
         G = self.ngroups
+        Q = (G + 3) // 4
+        bz = [z for z in nodes if z["built"] and z["end"] - z["start"] > 0]
+        if not bz:
+            return np.zeros((0, 4), np.int32), np.full((len(nodes), G, 1), -1, np.int32), 1
+        slot = np.array([z["slot"] for z in bz], np.int64)
+        start = np.array([z["start"] for z in bz], np.int64)
+        m = np.array([z["end"] - z["start"] for z in bz], np.int64)
         rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
-        per = self.items_per_node_group
-        blocks, ks = [], []
-        for z in nodes:
-            m = z["end"] - z["start"]
-            if not z["built"] or m <= 0:
-                continue
-            if per is None:
-                k = max(1, int(round(target_items * (m / max(1, rows_built)) / G)))
-                k = min(k, max(1, m // 4096), 64)
-            else:
-                k = per
-            step = (m + k - 1) // k
-            k = (m + step - 1) // step                      # chunks that are non-empty
-            lo = z["start"] + np.arange(k, dtype=np.int64) * step
-            hi = np.minimum(z["end"], lo + step)
-            # order (quad, chunk, sub-group): the 4 groups of one 128-B record and row range are
-            # consecutive items (one XCD, gbdt_kernels.hip xcd_remap) and share every fetched line
-            Q = (G + 3) // 4
-            b = np.empty((Q, k, 4, 4), dtype=np.int32)
-            b[..., 0] = z["slot"]
-            b[..., 1] = lo[None, :, None]
-            b[..., 2] = hi[None, :, None]
-            grp = np.arange(Q, dtype=np.int32)[:, None, None] * 4 + np.arange(4, dtype=np.int32)[None, None, :]
-            b[..., 3] = grp
-            keep = (grp < G).repeat(k, axis=1).reshape(-1)
-            blocks.append((z["slot"], b.reshape(-1, 4)[keep]))
-            ks.append(k)
-        max_items = max(ks + [1])
+        if self.items_per_node_group is None:
+            k = np.maximum(1, np.rint(TARGET_ITEMS * (m / max(1, rows_built)) / G).astype(np.int64))
+            k = np.minimum(np.minimum(k, np.maximum(1, m // 4096)), 64)
+        else:
+            k = np.full(len(bz), int(self.items_per_node_group), np.int64)
+        step = (m + k - 1) // k
+        k = (m + step - 1) // step                          # chunks that are non-empty
+        # one row per (node, quad, chunk, sub-group): the 4 groups of one 128-B record and row
+        # range are consecutive items (one XCD, gbdt_kernels.hip xcd_remap) and share its lines
+        per = Q * k * 4
+        tot = int(per.sum())
+        nd = np.repeat(np.arange(len(bz)), per)
+        r = np.arange(tot) - np.repeat(np.cumsum(per) - per, per)      # index inside the node's block
+        kk = k[nd]
+        q, rem = r // (kk * 4), r % (kk * 4)
+        ch, sg = rem // 4, rem % 4
+        grp = q * 4 + sg
+        lo = start[nd] + ch * step[nd]
+        hi = np.minimum(start[nd] + m[nd], lo + step[nd])
+        keep = grp < G
+        items = np.stack([slot[nd], lo, hi, grp], 1)[keep].astype(np.int32)
+        max_items = int(k.max())
         ni = np.full((len(nodes), G, max_items), -1, dtype=np.int32)
-        off = 0
-        for (slot, b), k in zip(blocks, ks):
-            gi = b[:, 3]
-            # item id of (group, chunk): position of that row in b
-            chunk_of = np.searchsorted(np.unique(b[:, 1]), b[:, 1])
-            ni[slot, gi, chunk_of] = off + np.arange(len(b), dtype=np.int32)
-            off += len(b)
-        items = np.concatenate([b for _, b in blocks]) if blocks else np.zeros((0, 4), np.int32)
+        ni[slot[nd][keep], grp[keep], ch[keep]] = np.arange(len(items), dtype=np.int32)
         return items, ni, max_items
 
     def _hist_allreduce(self, h: torch.Tensor) -> None:
@@ -688,11 +682,7 @@ class TreeTrainer:
                 wv, gv = self._wg_pos if by_pos else (w, g)
                 rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
                 if HIST64 and not self._root_level and rows_built >= HIST64_MIN_NODE_ROWS * max(1, n_built):
-                    # half-record blocks: items of groups 2j, 2j + 1 of one node / row range paired
-                    key = np.stack([items[:, 0], items[:, 1], items[:, 2], items[:, 3] >> 1], 1)
-                    uniq, inv = np.unique(key, axis=0, return_inverse=True)
-                    pairs = np.full((len(uniq), 2), -1, np.int32)
-                    pairs[inv.reshape(-1), items[:, 3] & 1] = np.arange(len(items), dtype=np.int32)
+                    pairs = _group_pairs(items)     # half-record blocks: groups 2j, 2j + 1 paired
                     pairs_t = _h2d(pairs, self.dev)        # lives until the level's D2H below
                     nat.call_hip("shifu_gbdt_hist64", d.kbins, d.group_stride, p2r, wv, gv, int(by_pos), it,
                                  len(items), pairs_t, len(pairs), slab, F, self.scale_w, self.scale_g,
@@ -1379,6 +1369,29 @@ def _apply_classes(tr: "TreeTrainer", t: Tree, data: BinnedData, out: torch.Tens
                      out, 1.0, 1, None, data.n, t.max_nodes, nat.stream_of(out))
     else:
         out.copy_(torch.from_numpy(t.predict_bins(data.codes().numpy(), data.is_cat, classes=True)).float())
+
+
+def _group_pairs(items: np.ndarray) -> np.ndarray:
+    """[n_pairs][2] item ids of groups (2j, 2j + 1) with the same node and row range (-1 where a
+    group has no partner), in item order.  _make_items emits the groups of one (node, chunk) in
+    ascending order and consecutively, so a partner is always the next item: O(n), no sort (a
+    row-wise np.unique took milliseconds per level on the host, between two GPU launches)."""
+    n = len(items)
+    if n == 0:
+        return np.zeros((0, 2), np.int32)
+    slot, lo, hi, grp = items[:, 0], items[:, 1], items[:, 2], items[:, 3]
+    nxt = np.zeros(n, dtype=bool)                 # item i is paired with item i + 1
+    nxt[:-1] = (((grp[:-1] & 1) == 0) & (grp[1:] == grp[:-1] + 1) & (slot[1:] == slot[:-1])
+                & (lo[1:] == lo[:-1]) & (hi[1:] == hi[:-1]))
+    taken = np.zeros(n, dtype=bool)
+    taken[1:] = nxt[:-1]                          # the partner (second) of a pair
+    first = np.flatnonzero(~taken)                # every pair starts at an item not taken
+    pairs = np.full((len(first), 2), -1, np.int32)
+    even = (grp[first] & 1) == 0
+    pairs[even, 0] = first[even]
+    pairs[~even, 1] = first[~even]
+    pairs[nxt[first], 1] = first[nxt[first]] + 1
+    return pairs
 
 
 def _slot_key(z):

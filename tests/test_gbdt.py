@@ -533,3 +533,26 @@ def test_gpu_hist64_matches_group_items(alg, f, monkeypatch):
         assert (x.feat == y.feat).all() and (x.thr == y.thr).all()
         assert np.array_equal(x.value, y.value)
     assert torch.equal(a.pred, b.pred)
+
+
+def test_group_pairs_matches_sorting_construction():
+    """Half-record pairing of histogram items (O(n) scan) equals the pairing by sorting keys, for
+    group counts with and without a lone last group."""
+    from shifu_amd.models.gbdt import _group_pairs
+    rng = np.random.default_rng(0)
+    for G in (32, 31, 3, 1, 7):
+        rows = []
+        for node in range(5):
+            for q in range((G + 3) // 4):
+                for ch in range(int(rng.integers(1, 6))):
+                    for sg in range(4):
+                        if q * 4 + sg < G:
+                            rows.append((node, ch * 1000 + node, ch * 1000 + 1000, q * 4 + sg))
+        items = np.array(rows, np.int32)
+        key = np.stack([items[:, 0], items[:, 1], items[:, 2], items[:, 3] >> 1], 1)
+        uniq, inv = np.unique(key, axis=0, return_inverse=True)
+        ref = np.full((len(uniq), 2), -1, np.int32)
+        ref[inv.reshape(-1), items[:, 3] & 1] = np.arange(len(items), dtype=np.int32)
+        got = _group_pairs(items)
+        assert sorted(map(tuple, got.tolist())) == sorted(map(tuple, ref.tolist()))
+        assert ((got[:, 0] < 0) | (items[np.maximum(got[:, 0], 0), 3] % 2 == 0)).all()
