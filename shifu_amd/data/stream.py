@@ -29,6 +29,7 @@ from .reader import column_kinds, list_data_files, parse_block, table_from_parts
 
 DEFAULT_CHUNK_BYTES = 256 << 20
 PREFETCH_READ = int(os.environ.get("SHIFU_READ_PREFETCH", "1"))   # blocks read ahead of the parse
+PREFETCH_UPLOAD = int(os.environ.get("SHIFU_UPLOAD_PREFETCH", "1"))   # uploaded blocks queued for the parse
 
 
 def _units(files):
@@ -250,7 +251,8 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
             if a is None:
                 yield (fi, 0, path), None
                 continue
-            it = _lines_in_range(path, a, b, chunk_bytes, nbuf=PREFETCH_READ + (4 if pinned else 2), pinned=pinned)
+            it = _lines_in_range(path, a, b, chunk_bytes,
+                                 nbuf=PREFETCH_READ + (3 + PREFETCH_UPLOAD if pinned else 2), pinned=pinned)
             while True:
                 with _span("read"):
                     nxt = next(it, None)
@@ -278,7 +280,7 @@ def _iter_parts(plan: DatasetPlan, chunk_bytes: int, rank: int, world: int, kind
 
     src = prefetched(blocks, PREFETCH_READ) if PREFETCH_READ > 0 else blocks()
     if pinned:
-        for (fi, off, path), data, dbuf in prefetched(lambda: gpu.uploads(src), 1):
+        for (fi, off, path), data, dbuf in prefetched(lambda: gpu.uploads(src), PREFETCH_UPLOAD):
             if data is None:
                 yield (fi, 0), whole_unit(fi, path)
                 continue
