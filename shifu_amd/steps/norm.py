@@ -234,6 +234,9 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
         getattr(nplan, "_bufs", {}).clear()
         getattr(nplan, "_pins", {}).clear()
         torch.cuda.empty_cache()       # hand the pass's cached blocks back (the next step allocates big)
+    if dev is not None:
+        import torch
+        mem += " -> %.1f GB allocated after" % (torch.cuda.memory_allocated(dev) / 1e9)
     _log.info("norm pass %.2fs (writes closed), buffers released %.2fs%s", t_rel - t_pass, time.perf_counter() - t_rel,
               mem)
     got = dist.all_gather_objects((n_local, counters))
