@@ -1426,11 +1426,11 @@ ROOT_G32 = os.environ.get("SHIFU_GBDT_ROOT_G32", "1") != "0"
 LEAF_WINDOW = os.environ.get("SHIFU_GBDT_LEAF_WINDOW", "1") != "0"
 # below-root histograms over 64-feature half records (gbdt_hist64_kernel); 0 = 32-feature items
 HIST64 = os.environ.get("SHIFU_GBDT_HIST64", "1") != "0"
-# ... on levels whose built nodes average at least this many rows: the 1024-thread blocks (one per
-# CU) win on long row ranges (balanced levels of 11-46M rows per node: 13.9-14.6 vs 15.4-16.2 ms)
-# and lose on short ones (5.6M: even; 8.5M of the favourable labels: 12.6 vs 12.2 ms; 2M: 1.9 vs
-# 1.0 ms), profiles/r5/gbdt/hist64_*
-HIST64_MIN_NODE_ROWS = int(os.environ.get("SHIFU_GBDT_HIST64_MIN_NODE_ROWS", "10000000"))
+# ... on levels whose built nodes average at least this many rows.  With 2048 items per level the
+# 1024-thread blocks (one per CU) lost on short row ranges (2M rows: 1.9 vs 1.0 ms); with 4096
+# items they win or tie down to 2.8M rows per node (balanced levels 5 / 6: 13.2 / 14.0 vs 14.5 /
+# 14.8 ms) and tie on the favourable labels' small levels (profiles/r5/gbdt/hist64_threshold_r5.txt)
+HIST64_MIN_NODE_ROWS = int(os.environ.get("SHIFU_GBDT_HIST64_MIN_NODE_ROWS", "2000000"))
 LEAF_W = int(os.environ.get("SHIFU_GBDT_LEAF_W", str(1 << 16)))
 LEAF_Y = int(os.environ.get("SHIFU_GBDT_LEAF_Y", "128"))   # 0.96 vs 2.13 ms with 16 (tools/leafwin_sweep.sh)
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on
