@@ -230,47 +230,69 @@ SHIFU_RT_API long shifu_merge_runs(int R, const char* const* blobs, const long* 
                                    const long* counts, const char* out_path) {
   FILE* f = std::fopen(out_path, "ab");
   if (!f) return -1;
-  std::vector<char> buf(1 << 22);
-  std::setvbuf(f, buf.data(), _IOFBF, buf.size());
-  struct Head { double key; int run; };
-  auto worse = [](const Head& a, const Head& b) {        // priority: larger key, then lower run
-    return a.key < b.key || (a.key == b.key && a.run > b.run);
-  };
-  std::priority_queue<Head, std::vector<Head>, decltype(worse)> pq(worse);
-  std::vector<long> at(R, 0);
+  long total = 0, bytes = 0;
   for (int r = 0; r < R; ++r)
-    if (counts[r] > 0) pq.push({keys[r][0], r});
-  long written = 0;
-  while (!pq.empty()) {
-    const Head h = pq.top();
-    pq.pop();
-    const int r = h.run;
-    const long i = at[r]++;
-    const long a = i ? ends[r][i - 1] : 0, b = ends[r][i];
-    if (std::fwrite(blobs[r] + a, 1, (size_t)(b - a), f) != (size_t)(b - a)) { std::fclose(f); return -1; }
-    ++written;
-    if (at[r] < counts[r]) pq.push({keys[r][at[r]], r});
+    if (counts[r] > 0) { total += counts[r]; bytes += ends[r][counts[r] - 1]; }
+  std::vector<char> out((size_t)bytes);             // merged into memory, written with one call
+  size_t o = 0;
+  int live = 0, only = -1;
+  for (int r = 0; r < R; ++r)
+    if (counts[r] > 0) { ++live; only = r; }
+  if (live == 1) {                                  // one run: it is the merge
+    std::memcpy(out.data(), blobs[only], (size_t)bytes);
+    o = (size_t)bytes;
+  } else {
+    struct Head { double key; int run; };
+    auto worse = [](const Head& a, const Head& b) {        // priority: larger key, then lower run
+      return a.key < b.key || (a.key == b.key && a.run > b.run);
+    };
+    std::priority_queue<Head, std::vector<Head>, decltype(worse)> pq(worse);
+    std::vector<long> at(R, 0);
+    for (int r = 0; r < R; ++r)
+      if (counts[r] > 0) pq.push({keys[r][0], r});
+    while (!pq.empty()) {
+      const Head h = pq.top();
+      pq.pop();
+      const int r = h.run;
+      const long i = at[r]++;
+      const long a = i ? ends[r][i - 1] : 0, b = ends[r][i];
+      std::memcpy(out.data() + o, blobs[r] + a, (size_t)(b - a));
+      o += (size_t)(b - a);
+      if (at[r] < counts[r]) pq.push({keys[r][at[r]], r});
+    }
   }
+  if (o && std::fwrite(out.data(), 1, o, f) != o) { std::fclose(f); return -1; }
   if (std::fclose(f) != 0) return -1;
-  return written;
+  return total;
 }
 
 // Reorder one run's lines: write lines order[0], order[1], ... of (blob, line_end) to out_path and
 // their new end offsets to new_end (the rank-local ORDER BY before the k-way merge).
 SHIFU_RT_API long shifu_gather_lines(const char* blob, const long* ends, const long* order, long n,
                                      const char* out_path, long* new_end) {
-  FILE* f = std::fopen(out_path, "wb");
-  if (!f) return -1;
-  std::vector<char> buf(1 << 22);
-  std::setvbuf(f, buf.data(), _IOFBF, buf.size());
+  // output offsets of the reordered lines (one O(n) pass), then the lines copied into one buffer
+  // by several threads and written with a single call: one fwrite per line was ~1-2 s at 20M
   long pos = 0;
   for (long i = 0; i < n; ++i) {
     const long j = order[i];
-    const long a = j ? ends[j - 1] : 0, b = ends[j];
-    if (std::fwrite(blob + a, 1, (size_t)(b - a), f) != (size_t)(b - a)) { std::fclose(f); return -1; }
-    pos += b - a;
+    pos += ends[j] - (j ? ends[j - 1] : 0);
     new_end[i] = pos;
   }
+  std::vector<char> out((size_t)pos);
+  const long T = std::max(1L, std::min<long>(16, n >> 16));
+  std::vector<std::thread> th;
+  for (long t = 0; t < T; ++t)
+    th.emplace_back([&, t]() {
+      for (long i = n * t / T, e = n * (t + 1) / T; i < e; ++i) {
+        const long j = order[i];
+        const long a = j ? ends[j - 1] : 0, b = ends[j];
+        std::memcpy(out.data() + (i ? new_end[i - 1] : 0), blob + a, (size_t)(b - a));
+      }
+    });
+  for (auto& x : th) x.join();
+  FILE* f = std::fopen(out_path, "wb");
+  if (!f) return -1;
+  if (pos && std::fwrite(out.data(), 1, (size_t)pos, f) != (size_t)pos) { std::fclose(f); return -1; }
   if (std::fclose(f) != 0) return -1;
   return pos;
 }
