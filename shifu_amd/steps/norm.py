@@ -158,6 +158,13 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     if is_gpu_available():
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
+        # blocks a previous step of this process left cached (the stats pass's device cache of
+        # parsed chunks: ~200 GB at 20M x 1600) go back to the driver now, so it has cleared them
+        # by the time a later step makes its big allocation (released at the end of this pass
+        # instead, the varsel 64-GB cache allocation took 0.6-4.4 s)
+        t_e = time.perf_counter()
+        torch.cuda.empty_cache()
+        _log.info("norm: cached HBM of earlier steps released in %.2fs", time.perf_counter() - t_e)
     # two rotating pinned output buffers: chunk i is written while chunk i + 1 is normalized
     nplan = N.NormPlan(mc, ms.ccs, cols, want_x=True, want_codes=is_tree, x_dtype=x_dtype, device=dev,
                        pinned_out=2 if dev is not None else 0)
@@ -233,12 +240,10 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
                                                                   torch.cuda.max_memory_allocated(dev) / 1e9)
         getattr(nplan, "_bufs", {}).clear()
         getattr(nplan, "_pins", {}).clear()
-        torch.cuda.empty_cache()       # hand the pass's cached blocks back (the next step allocates big)
     if dev is not None:
         import torch
         mem += " -> %.1f GB allocated after" % (torch.cuda.memory_allocated(dev) / 1e9)
-    _log.info("norm pass %.2fs (writes closed), buffers released %.2fs%s", t_rel - t_pass, time.perf_counter() - t_rel,
-              mem)
+    _log.info("norm pass %.2fs (writes closed)%s", t_rel - t_pass, mem)
     got = dist.all_gather_objects((n_local, counters))
     rows = [g[0] for g in got]
     tot_counters = {}
