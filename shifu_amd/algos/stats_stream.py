@@ -64,7 +64,10 @@ def _cache_budget(dev) -> int:
     if dev.type == "cuda":
         from ..utils.device import free_hbm
         free = free_hbm(dev)
-        return int(free * 0.7)
+        # everything but ~40 GiB of working room (parse pipeline blocks, per-batch kernels): at
+        # 20M x 1600 the whole 256-GB rank share stays resident and the later passes stop
+        # re-parsing an uncached tail (stats 17.5-19.4 -> 13.0 s; 70 % of free HBM cached 214 GB)
+        return int(max(0.5 * free, min(0.9 * free, free - (40 << 30))))
     return 0
 
 
