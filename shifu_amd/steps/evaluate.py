@@ -202,7 +202,7 @@ def _score_eval_streamed(ms, ev, runner, meta_cols, score_meta, scale, write, no
         strs.append(target)
     plan = plan_dataset(mc, ev.dataSet, nums, strs)
     gpu_run = getattr(runner, "dev", None) is not None and runner.dev.type == "cuda"
-    chunk = int(float(environment.get("shifu.eval.chunkMB", 1024 if gpu_run else 256)) * (1 << 20))
+    chunk = int(float(environment.get("shifu.eval.chunkMB", 2048 if gpu_run else 256)) * (1 << 20))   # 8.1 -> 7.1 s at 20M
     sel = ev.get("performanceScoreSelector", "mean") or "mean"
     pos = set(str(t) for t in (ev.dataSet.get("posTags") or mc.pos_tags))
     neg = set(str(t) for t in (ev.dataSet.get("negTags") or mc.neg_tags))

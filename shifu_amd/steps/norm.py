@@ -169,7 +169,8 @@ def _norm_one_streamed(ms: ModelSet, cols, data_conf, out_x, out_tree, sample_ra
     nplan = N.NormPlan(mc, ms.ccs, cols, want_x=True, want_codes=is_tree, x_dtype=x_dtype, device=dev,
                        pinned_out=2 if dev is not None else 0)
     nplan.async_out = dev is not None        # the writer waits for the chunk's D2H, not the consumer
-    chunk = int(float(environment.get("shifu.norm.chunkMB", 1024 if dev is not None else 256)) * (1 << 20))
+    # 2-GB text chunks on the GPU-parse path: 20M x 1600 norm pass 9.3 -> 8.3 s (profiles/r5/pipeline)
+    chunk = int(float(environment.get("shifu.norm.chunkMB", 2048 if dev is not None else 256)) * (1 << 20))
     outs = [out_x] + ([out_tree] if is_tree else [])
     if info.rank == 0:
         for o in outs:
