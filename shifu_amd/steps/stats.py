@@ -146,8 +146,9 @@ def _stats_streamed(ms: ModelSet, cols, device=None) -> None:
     pdev = _parse_device(device)
     gpu_cols = [c.name for c in cols if not c.is_categorical() and not c.is_target() and not c.is_meta()]
     # 1 GB blocks on the GPU path: per-block fixed costs (parse syncs, per-batch K4/K1 launches)
-    # over 4x fewer blocks (3M x 1600: stats 5.19 -> 4.60 s, profiles/r4/pipe_lab_3Mx1600_chunk1G_r4l.txt)
-    chunk = int(float(environment.get("shifu.stats.chunkMB", 1024 if pdev is not None else 256)) * (1 << 20))
+    # over 4x fewer blocks (3M x 1600: stats 5.19 -> 4.60 s, profiles/r4/pipe_lab_3Mx1600_chunk1G_r4l.txt);
+    # 2 GB since r5 (20M x 1600 with every parsed block resident: 11.9-12.8 -> 10.7-11.0 s)
+    chunk = int(float(environment.get("shifu.stats.chunkMB", 2048 if pdev is not None else 256)) * (1 << 20))
 
     def chunks(resume=None, with_keys=False):
         return DS.iter_model_data(mc, plan, chunk, info.rank, info.world_size, rate, neg_only, row0=row0,
