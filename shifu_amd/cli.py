@@ -39,7 +39,8 @@ _log = get_logger("cli")
 
 # verbs whose every rank takes part (row-sharded data, collectives inside); the other
 # multi-GPU verbs run on rank 0 alone under dist.local_only()
-DP_VERBS = ("train", "stats", "eval", "norm", "normalize", "transform", "varsel", "posttrain", "init")
+DP_VERBS = ("train", "stats", "eval", "norm", "normalize", "transform", "varsel", "posttrain", "init",
+            "encode", "combo")
 
 
 def torch_status(rc: int):
@@ -68,7 +69,7 @@ def main(argv=None) -> int:
         return 0
     cmd, args = argv[0].lower(), argv[1:]
     from .parallel import dist
-    if cmd in ("train", "stats", "norm", "normalize", "transform", "varsel", "eval", "posttrain", "init"):
+    if cmd in DP_VERBS:
         dist.init_from_env()
     from .utils.trace import step_timer
     from .utils.telemetry import record_usage

@@ -489,8 +489,10 @@ class MLPTrainer:
         if self.gpu:
             from ..ops import _native
             _native.require_gpu_native()
-            if spec.layer_kpad[-1] > 512 or spec.n_out > 8:
-                raise ValueError("HIP output kernel supports last hidden width <= 511 and n_out <= 8")
+        # the register-resident output row kernel takes last hidden width <= 511 and n_out <= 8;
+        # any other shape runs the any-shape output kernel + TN wgrad (mlp_kernels.hip)
+        self.wide_out = (spec.layer_kpad[-1] > 512 or spec.n_out > 8 or
+                         os.environ.get("SHIFU_WIDE_OUTPUT") == "1")   # (forced: A/B tests)
         self.params = MLPParams(spec, self.device)
         if init_flat_encog is not None:
             self.params.from_encog_flat(init_flat_encog)
@@ -605,6 +607,10 @@ class MLPTrainer:
             ws["gw_slab"] = torch.empty(tiles * kp[L], dtype=torch.float32, device=self.device)
             ws["err_slab"] = torch.empty(tiles * 2, dtype=torch.float64, device=self.device)
             ws["gw_part"] = torch.empty(-(-tiles // 128) * kp[L], dtype=torch.float32, device=self.device)
+        # bf16 output deltas of the any-shape output path (operand of the output-layer wgrad)
+        ws["ldl"] = round_up(self.spec.n_out, 8)
+        ws["outd"] = (torch.empty(rows, ws["ldl"], dtype=torch.bfloat16, device=self.device)
+                      if self.gpu and self.wide_out else None)
         self._ws[lane] = ws
         return ws
 
@@ -749,6 +755,13 @@ class MLPTrainer:
             if ws["gw_slab"] is not None:
                 nat.call_hip("shifu_colsum_fixed", ws["gw_slab"], -(-mc // 256), kp[L], ws["gw_part"],
                              gv[L].data_ptr(), st)
+        elif self.wide_out:
+            # any-shape output layer: row kernel (deltas, errors) + output wgrad on the TN GEMM
+            nat.call_hip("shifu_mlp_output_wide", acts[L], kp[L], ders[L], kp[L], wv[L].data_ptr(), y,
+                         sp.n_out, s, dels[L] if L else None, kp[L], ws["outd"], ws["ldl"], gv[L].data_ptr(),
+                         self.err_acc, None, 0, mc, kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act],
+                         ACT_IDS[sp.acts[L - 1]] if L else 2, sp.loss_id, sp.flat_spot(sp.out_act),
+                         sp.flat_spot(sp.acts[L - 1]) if L else 0.0, st)
         else:
             # output layer + loss + last hidden delta + output wgrad
             nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], nat.ptr(ders[L]), kp[L],
@@ -956,6 +969,12 @@ class MLPTrainer:
                 nat.call_hip("shifu_gemm_nt", acts[l].data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
                              acts[l + 1].data_ptr(), kp[l + 1], None, 0, None, 0, None, 0, mc, kp[l + 1], kp[l],
                              0, ACT_IDS[sp.acts[l]], sp.hidden[l], 1, 0.0, st)
+            if self.wide_out:
+                nat.call_hip("shifu_mlp_output_wide", acts[L], kp[L], None, kp[L], wv[L].data_ptr(), ydummy,
+                             sp.n_out, None, None, kp[L], None, 0, None, escratch, out[r0:r1], sp.n_out, mc,
+                             kp[L], sp.layer_in[L], sp.n_out, ACT_IDS[sp.out_act],
+                             ACT_IDS[sp.acts[L - 1]] if L else 2, 0, 0.0, 0.0, st)
+                continue
             nat.call_hip("shifu_mlp_output", acts[L].data_ptr(), kp[L], None, kp[L], wv[L].data_ptr(),
                          ydummy.data_ptr(), sp.n_out, None, None, kp[L], gscratch.data_ptr(),
                          escratch.data_ptr(), out[r0:r1].data_ptr(), sp.n_out, mc, kp[L], sp.layer_in[L],

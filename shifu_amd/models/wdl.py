@@ -92,83 +92,92 @@ def _deriv_from_out(act: str, a: torch.Tensor) -> torch.Tensor:
     raise ValueError(act)
 
 
-class _DeepMFMA(torch.autograd.Function):
+def deep_forward(A, final, acts, Ws):
     """Deep tower (dense + activation layers, then the linear output neuron) with every GEMM on
     the MLP's own kernels: forward ``shifu_gemm_nt`` EPI_ACT (activation, bias column and zero
-    padding written by the epilogue as the next layer's bf16 rows -- no per-layer cat), backward
-    ``shifu_gemm_nt`` EPI_DACT (dgrad x f'(a) fused) and ``shifu_wgrad_tn`` (fp32 weight
-    gradients).  bf16 activations / deltas, fp32 accumulation (the NN trainer's precision);
-    WideAndDeep.java:163-232 semantics (no flat spot)."""
+    padding written by the epilogue as the next layer's bf16 rows -- no per-layer cat).  Returns
+    (out [n] fp32, state for ``deep_backward``).  bf16 activations, fp32 accumulation (the NN
+    trainer's precision); WideAndDeep.java:163-232 semantics (no flat spot)."""
+    from ..ops import _native as nat
+    from .nn import ACT_IDS
+    dev, n = A.device, A.shape[0]
+    st = nat.stream_of(A)
+    dims = [A.shape[1]] + [W.shape[0] for W in Ws]
+    kp = [_pad(d + 1) for d in dims]
+    X = torch.zeros(n, kp[0], dtype=torch.bfloat16, device=dev)
+    X[:, : dims[0]] = A
+    X[:, dims[0]] = 1.0
+    xs, ders, wbs = [X], [], []
+    for l, (W, act) in enumerate(zip(Ws, acts)):
+        wb = torch.zeros(dims[l + 1], kp[l], dtype=torch.bfloat16, device=dev)
+        wb[:, : dims[l] + 1] = W
+        C = torch.empty(n, kp[l + 1], dtype=torch.bfloat16, device=dev)
+        aid = ACT_IDS[act]
+        C2 = None if aid in (0, 1, 2, 3, 4, 6, 7) else torch.empty_like(C)
+        nat.call_hip("shifu_gemm_nt", xs[-1], kp[l], wb, kp[l], dims[l + 1], C, kp[l + 1], C2, kp[l + 1], None, 0,
+                     None, 0, n, kp[l + 1], kp[l], 0, aid, dims[l + 1], 1, 0.0, st)
+        xs.append(C)
+        ders.append(C2)
+        wbs.append(wb)
+    # output neuron over [h_L | 1] (the bias column of xs[-1]): one wave per row (wdl_kernels.hip)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    nat.call_hip("shifu_rowdot_bf16", xs[-1], kp[-1], n, dims[-1] + 1, final[0].float().contiguous(), out, st)
+    return out, (list(acts), dims, kp, ders, wbs, final, xs, list(Ws))
+
+
+def deep_backward(state, g):
+    """(dA [n, in] fp32, d final [1, h_L + 1], [dW_l]) of ``sum_i g_i out_i``: ``shifu_gemm_nt``
+    EPI_DACT (dgrad x f'(a) fused) and ``shifu_wgrad_tn`` (fp32 weight gradients)."""
+    from ..ops import _native as nat
+    from .nn import ACT_IDS
+    acts, dims, kp, ders, wbs, final, xs, Ws = state
+    L = len(Ws)
+    n, dev = xs[-1].shape[0], xs[-1].device
+    st = nat.stream_of(xs[-1])
+    g = g.contiguous().float()
+    # output-weight gradient sum_i g_i [h_L | 1]_i: per-256-row partials + a fixed-order sum
+    g_final = torch.empty(1, dims[-1] + 1, dtype=torch.float32, device=dev)
+    part = torch.empty(max(1, -(-n // 256)) * (dims[-1] + 1), dtype=torch.float32, device=dev)
+    nat.call_hip("shifu_coldot_bf16", g, xs[-1], kp[-1], n, dims[-1] + 1, part, g_final, st)
+    # output delta -> last hidden layer delta (elementwise; the output neuron is linear)
+    aL = xs[-1][:, : dims[-1]].float()
+    dl = ders[-1][:, : dims[-1]].float() if ders[-1] is not None else _deriv_from_out(acts[-1], aL)
+    D = torch.zeros(n, kp[-1], dtype=torch.bfloat16, device=dev)
+    D[:, : dims[-1]] = (g[:, None] * final[0, : dims[-1]][None, :]) * dl
+    gWs = [None] * L
+    for l in range(L - 1, -1, -1):
+        G = torch.zeros(dims[l + 1], kp[l], dtype=torch.float32, device=dev)
+        nat.call_hip("shifu_wgrad_tn", D, kp[l + 1], xs[l], kp[l], G, kp[l], n, dims[l + 1], kp[l],
+                     max(1, min(n // 256, 256)), st)
+        gWs[l] = G[:, : dims[l] + 1]
+        # delta of the layer below (or the input gradient): D W_l through W_l^T as B rows
+        wt = torch.zeros(kp[l], kp[l + 1], dtype=torch.bfloat16, device=dev)
+        wt[: dims[l] + 1, : dims[l + 1]] = Ws[l].t()
+        Dn = torch.empty(n, kp[l], dtype=torch.bfloat16, device=dev)
+        if l > 0:
+            aid = ACT_IDS[acts[l - 1]]
+            nat.call_hip("shifu_gemm_nt", D, kp[l + 1], wt, kp[l + 1], kp[l], Dn, kp[l], None, 0,
+                         xs[l], kp[l], ders[l - 1], kp[l], n, kp[l], kp[l + 1], 1, aid, dims[l], 0, 0.0, st)
+        else:
+            nat.call_hip("shifu_gemm_nt", D, kp[1], wt, kp[1], kp[0], Dn, kp[0], None, 0, None, 0, None, 0,
+                         n, kp[0], kp[1], 2, 2, dims[0], 0, 0.0, st)
+        D = Dn
+    return D[:, : dims[0]].float(), g_final, gWs
+
+
+class _DeepMFMA(torch.autograd.Function):
+    """autograd wrapper of ``deep_forward`` / ``deep_backward`` (scoring and the kernel tests)."""
 
     @staticmethod
     def forward(ctx, A, final, acts, *Ws):
-        from ..ops import _native as nat
-        from .nn import ACT_IDS
-        dev, n = A.device, A.shape[0]
-        st = nat.stream_of(A)
-        dims = [A.shape[1]] + [W.shape[0] for W in Ws]
-        kp = [_pad(d + 1) for d in dims]
-        X = torch.zeros(n, kp[0], dtype=torch.bfloat16, device=dev)
-        X[:, : dims[0]] = A
-        X[:, dims[0]] = 1.0
-        xs, ders, wbs = [X], [], []
-        for l, (W, act) in enumerate(zip(Ws, acts)):
-            wb = torch.zeros(dims[l + 1], kp[l], dtype=torch.bfloat16, device=dev)
-            wb[:, : dims[l] + 1] = W
-            C = torch.empty(n, kp[l + 1], dtype=torch.bfloat16, device=dev)
-            aid = ACT_IDS[act]
-            C2 = None if aid in (0, 1, 2, 3, 4, 6, 7) else torch.empty_like(C)
-            nat.call_hip("shifu_gemm_nt", xs[-1], kp[l], wb, kp[l], dims[l + 1], C, kp[l + 1], C2, kp[l + 1], None, 0,
-                         None, 0, n, kp[l + 1], kp[l], 0, aid, dims[l + 1], 1, 0.0, st)
-            xs.append(C)
-            ders.append(C2)
-            wbs.append(wb)
-        # output neuron over [h_L | 1] (the bias column of xs[-1]): one wave per row (wdl_kernels.hip)
-        out = torch.empty(n, dtype=torch.float32, device=dev)
-        nat.call_hip("shifu_rowdot_bf16", xs[-1], kp[-1], n, dims[-1] + 1, final[0].float().contiguous(), out, st)
-        ctx.save_for_backward(final, *xs, *Ws)
-        ctx.meta = (list(acts), dims, kp, ders, wbs, len(Ws))
+        out, state = deep_forward(A, final, acts, Ws)
+        ctx.state = state
         return out
 
     @staticmethod
     def backward(ctx, g):
-        from ..ops import _native as nat
-        from .nn import ACT_IDS
-        acts, dims, kp, ders, wbs, L = ctx.meta
-        saved = ctx.saved_tensors
-        final = saved[0]
-        xs, Ws = saved[1: 2 + L], saved[2 + L:]
-        n, dev = xs[-1].shape[0], xs[-1].device
-        st = nat.stream_of(xs[-1])
-        g = g.contiguous().float()
-        # output-weight gradient sum_i g_i [h_L | 1]_i: per-256-row partials + a fixed-order sum
-        g_final = torch.empty(1, dims[-1] + 1, dtype=torch.float32, device=dev)
-        part = torch.empty(max(1, -(-n // 256)) * (dims[-1] + 1), dtype=torch.float32, device=dev)
-        nat.call_hip("shifu_coldot_bf16", g, xs[-1], kp[-1], n, dims[-1] + 1, part, g_final, st)
-        # output delta -> last hidden layer delta (elementwise; the output neuron is linear)
-        aL = xs[-1][:, : dims[-1]].float()
-        dl = ders[-1][:, : dims[-1]].float() if ders[-1] is not None else _deriv_from_out(acts[-1], aL)
-        D = torch.zeros(n, kp[-1], dtype=torch.bfloat16, device=dev)
-        D[:, : dims[-1]] = (g[:, None] * final[0, : dims[-1]][None, :]) * dl
-        gWs = [None] * L
-        for l in range(L - 1, -1, -1):
-            G = torch.zeros(dims[l + 1], kp[l], dtype=torch.float32, device=dev)
-            nat.call_hip("shifu_wgrad_tn", D, kp[l + 1], xs[l], kp[l], G, kp[l], n, dims[l + 1], kp[l],
-                         max(1, min(n // 256, 256)), st)
-            gWs[l] = G[:, : dims[l] + 1]
-            # delta of the layer below (or the input gradient): D W_l through W_l^T as B rows
-            wt = torch.zeros(kp[l], kp[l + 1], dtype=torch.bfloat16, device=dev)
-            wt[: dims[l] + 1, : dims[l + 1]] = Ws[l].t()
-            Dn = torch.empty(n, kp[l], dtype=torch.bfloat16, device=dev)
-            if l > 0:
-                aid = ACT_IDS[acts[l - 1]]
-                nat.call_hip("shifu_gemm_nt", D, kp[l + 1], wt, kp[l + 1], kp[l], Dn, kp[l], None, 0,
-                             xs[l], kp[l], ders[l - 1], kp[l], n, kp[l], kp[l + 1], 1, aid, dims[l], 0, 0.0, st)
-            else:
-                nat.call_hip("shifu_gemm_nt", D, kp[1], wt, kp[1], kp[0], Dn, kp[0], None, 0, None, 0, None, 0,
-                             n, kp[0], kp[1], 2, 2, dims[0], 0, 0.0, st)
-            D = Dn
-        dA = D[:, : dims[0]].float()
+        dA, g_final, gWs = deep_backward(ctx.state, g)
+        ctx.state = None
         return (dA, g_final, None, *gWs)
 
 

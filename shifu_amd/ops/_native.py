@@ -49,6 +49,7 @@ HIP_SIGNATURES = {
     "shifu_gemm_set_tune": "ii",
     "shifu_mlp_set_out_waves": "i",
     "shifu_mlp_output": "plplppl" "pplpppl" "iiiiiii" "ff" "s",
+    "shifu_mlp_output_wide": "plplppl" "p" "plpl" "pppl" "iiiiiii" "ff" "s",
     "shifu_optimizer_step": "pppppp" "lii" "ffffffffff" "is",
     "shifu_optimizer_step_tf": "pppp" "li" "ffff" "ff" "p" "is",
     "shifu_cast_bf16": "plpliis",
@@ -107,7 +108,7 @@ HIP_SIGNATURES = {
     "shifu_rowdot_f32_act": "pllipfiips",
     "shifu_coldot_f32": "ppllipps",
     # ga_kernels.hip
-    "shifu_ga_part_floats": ("llii", "l"),
+    "shifu_ga_part_floats": ("liii", "l"),
     "shifu_ga_head": "plliippppipl" "pp" "ii" "s",
     # quantile_kernels.hip
     "shifu_pack_bits": "plip" "s",

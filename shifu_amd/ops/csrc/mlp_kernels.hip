@@ -153,6 +153,139 @@ __global__ __launch_bounds__(256) void mlp_output_kernel(OutArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Output layer for ANY last-hidden width and ANY number of outputs (the row kernel above keeps
+// every output's weights and gradient partials in registers: KH <= 512, n_out <= 8).  The
+// reference builds any width / output count (J/core/dtrain/DTrainUtils.java:303-386; one output
+// node per tag for NATIVE multi-class, ModelConfig.java:381-384), so this path has no limit but LDS.
+//
+// One wave per row, grid-stride.  Outputs in groups of 8: z over the row's 8-column groups (lane
+// owns groups lane, lane + 64, ...; the H row is re-read from L1/L2 per output group), summed
+// across the wave by xor shuffles, then activation / loss / output deltas computed redundantly by
+// every lane; lane 0 stages the row's deltas in LDS (one n_out-float strip per wave) and stores
+// them bf16 into L [M, ldl] (zero padded to ldl) for the output wgrad GEMM (GW += L^T H, wgrad_tn,
+// called by the launcher).  Then the hidden deltas D = (sum_o dlt_o W[o]) * (f'(H) + flat) per
+// column group, W rows read fp32 from L2 (n_out x KH x 4 B, shared by every wave).
+// ---------------------------------------------------------------------------------------
+struct WideArgs {
+  const bf16_t* H; long ldh;
+  const bf16_t* Hd; long ldhd;
+  const float* W;                  // [n_out, KH] fp32
+  const float* Y; long ldy;
+  const float* S;
+  bf16_t* D; long ldd;             // hidden deltas (nullable)
+  bf16_t* L; long ldl;             // output deltas bf16 (nullable)
+  double* err;
+  float* P; long ldp;              // predictions (nullable)
+  int M, KH, kh_valid, n_out, out_act, hid_act, loss;
+  float flat_out, flat_hid;
+};
+
+__global__ __launch_bounds__(256) void mlp_output_wide_kernel(WideArgs p) {
+  extern __shared__ float dl_lds[];                 // [4][n_out]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* dl = dl_lds + (size_t)wv * p.n_out;
+  const bool dfo = act_deriv_from_output(p.hid_act);
+  const long wave0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  const int ngroups = p.KH / 8;
+  const int lm = p.loss % 3;
+  double esum = 0.0, wsum = 0.0;
+  for (long m = wave0; m < p.M; m += nwaves) {
+    const bf16_t* hrow = p.H + (size_t)m * p.ldh;
+    const float s = p.S ? p.S[m] : 1.f;
+    for (int og = 0; og < p.n_out; og += 8) {
+      float z[8];
+#pragma unroll
+      for (int o = 0; o < 8; ++o) z[o] = 0.f;
+      for (int g = lane; g < ngroups; g += 64) {
+        float h[8];
+        unpack8(*(const uint4*)(hrow + g * 8), h);
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          const int oo = min(og + o, p.n_out - 1);             // clamped: branch-free loads
+          const float4* wp = (const float4*)(p.W + (size_t)oo * p.KH + g * 8);
+          const float4 w0 = wp[0], w1 = wp[1];
+          z[o] += h[0] * w0.x + h[1] * w0.y + h[2] * w0.z + h[3] * w0.w +
+                  h[4] * w1.x + h[5] * w1.y + h[6] * w1.z + h[7] * w1.w;
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < 8; ++o)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) z[o] += __shfl_xor(z[o], off, 64);
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        const int oi = og + o;
+        if (oi >= p.n_out) {
+          if (p.L && lane == 0 && oi < p.ldl) p.L[(size_t)m * p.ldl + oi] = (bf16_t)0;
+          continue;
+        }
+        const float a = act_fwd(p.out_act, z[o]);
+        const float y = p.Y[(size_t)m * p.ldy + oi];
+        const float e = y - a;
+        float d, contrib;
+        if (lm == 1) {
+          d = e * s;
+          const float ac = fminf(fmaxf(a, 1e-7f), 1.f - 1e-7f);
+          contrib = p.loss >= 3 ? -(__logf(a + 1e-7f) * y + __logf(1.f - a + 1e-7f) * (1.f - y)) * s
+                    : p.n_out == 1 ? -(__logf(ac) * y + __logf(1.f - ac) * (1.f - y)) : -(__logf(ac) * y * s);
+        } else if (lm == 2) {
+          d = (y < a ? 1.f : -1.f) * (act_deriv_out(p.out_act, a) + p.flat_out) * s;
+          contrib = fabsf(e) * s;
+        } else {
+          d = (act_deriv_pre(p.out_act, z[o]) + p.flat_out) * e * s;
+          contrib = p.loss >= 3 ? e * e * s : (e * s) * (e * s);
+        }
+        if (lane == 0) {
+          esum += contrib;
+          dl[oi] = d;
+          if (p.L) p.L[(size_t)m * p.ldl + oi] = f2bf(d);
+          if (p.P) p.P[(size_t)m * p.ldp + oi] = a;
+        }
+      }
+    }
+    if (lane == 0) wsum += s;
+    if (p.D) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);          // lane 0's LDS stores of dl (lgkmcnt(0))
+      __builtin_amdgcn_wave_barrier();
+      for (int g = lane; g < ngroups; g += 64) {
+        float ds[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) ds[c] = 0.f;
+        for (int o = 0; o < p.n_out; ++o) {
+          const float d = dl[o];
+          const float4* wp = (const float4*)(p.W + (size_t)o * p.KH + g * 8);
+          const float4 w0 = wp[0], w1 = wp[1];
+          ds[0] += d * w0.x; ds[1] += d * w0.y; ds[2] += d * w0.z; ds[3] += d * w0.w;
+          ds[4] += d * w1.x; ds[5] += d * w1.y; ds[6] += d * w1.z; ds[7] += d * w1.w;
+        }
+        float h[8], dv[8], outv[8];
+        if (dfo) {
+          unpack8(*(const uint4*)(hrow + g * 8), h);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) dv[c] = act_deriv_out(p.hid_act, h[c]) + p.flat_hid;
+        } else {
+          unpack8(*(const uint4*)(p.Hd + (size_t)m * p.ldhd + g * 8), dv);
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) outv[c] = (g * 8 + c) < p.kh_valid ? ds[c] * dv[c] : 0.f;
+        *(uint4*)(p.D + (size_t)m * p.ldd + g * 8) = pack8(outv);
+      }
+      __builtin_amdgcn_wave_barrier();             // dl reads done before the next row's stores
+    }
+  }
+  __shared__ double ered[4][2];
+  esum = wave_sum_d(esum);
+  wsum = wave_sum_d(wsum);
+  if (lane == 0) { ered[wv][0] = esum; ered[wv][1] = wsum; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(p.err, ered[0][0] + ered[1][0] + ered[2][0] + ered[3][0]);
+    atomicAdd(p.err + 1, ered[0][1] + ered[1][1] + ered[2][1] + ered[3][1]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Optimizer: one fused pass over the flat fp32 weights (J/core/dtrain/Weight.java:194-343,
 // J/core/dtrain/nn/update/*.java).  Gradients are Encog ascent directions: every rule ADDS.
 // ---------------------------------------------------------------------------------------
@@ -282,6 +415,41 @@ SHIFU_API int shifu_mlp_output(const void* H, long ldh, const void* Hd, long ldh
 #undef OUT_LPR
 #undef OUT_L
   CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// gemm_kernels.hip (same library): split-K TN wgrad G[Nv, Kx] += D^T X
+extern "C" int shifu_wgrad_tn(const void* D, long ldd, const void* X, long ldx, float* G, long ldg, int M, int Nv,
+                              int Kx, int splits, hipStream_t stream);
+
+// Any-shape output layer: row kernel (deltas, hidden deltas, errors, predictions) + the output
+// wgrad GW [n_out, KH] += L^T H on the TN GEMM when GW is given (L [M, ldl] bf16 workspace,
+// ldl >= round_up(n_out, 8)).
+SHIFU_API int shifu_mlp_output_wide(const void* H, long ldh, const void* Hd, long ldhd, const float* W,
+                                    const float* Y, long ldy, const float* S, void* D, long ldd, void* L,
+                                    long ldl, float* GW, double* err, float* P, long ldp, int M, int KH,
+                                    int kh_valid, int n_out, int out_act, int hid_act, int loss, float flat_out,
+                                    float flat_hid, hipStream_t stream) {
+  if (KH % 128 || KH < 128 || ldh < KH || ldh % 8 || n_out < 1 || n_out > 8192 || M <= 0) return -1;
+  if (D && (ldd < KH || ldd % 8)) return -1;
+  if (GW && (L == nullptr || ldl < ((n_out + 7) / 8) * 8 || ldl % 8)) return -1;
+  if (D && !act_deriv_from_output(hid_act) && Hd == nullptr) return -3;
+  WideArgs p{(const bf16_t*)H, ldh, (const bf16_t*)Hd, ldhd, W, Y, ldy, S, (bf16_t*)D, ldd,
+             GW ? (bf16_t*)L : nullptr, ldl, err, P, ldp, M, KH, kh_valid, n_out, out_act, hid_act, loss,
+             flat_out, flat_hid};
+  long blocks = (M + 3) / 4;
+  if (blocks > 4096) blocks = 4096;                 // 16 waves per CU, grid-stride over rows
+  const size_t lds = (size_t)4 * n_out * sizeof(float);
+  hipLaunchKernelGGL(mlp_output_wide_kernel, dim3(blocks), dim3(256), lds, stream, p);
+  CHECK_HIP(hipGetLastError());
+  if (GW) {
+    int splits = M / 2048;
+    const int tiles = ((n_out + 127) / 128) * (KH / 128);
+    if (splits > 1024 / tiles) splits = 1024 / tiles;
+    if (splits < 1) splits = 1;
+    const int r = shifu_wgrad_tn(L, ldl, H, ldh, GW, KH, M, n_out, KH, splits, stream);
+    if (r) return r;
+  }
   return 0;
 }
 

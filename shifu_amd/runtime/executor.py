@@ -7,11 +7,15 @@ The reference's ``ExecutorManager`` (a thread pool whose failed tasks are re-sub
 * ``ExecutorManager(workers, retries).run(tasks)`` - runs callables on a thread pool, re-runs a
   failed task up to ``retries`` times, raises the last error of a task that never succeeds;
 * ``run_cli(args, cwd)`` - one ``shifu_amd.cli`` verb in a child process (its own GPU context,
-  so sub-model pipelines can run side by side); returns the exit code.
+  so sub-model pipelines can run side by side); returns the exit code;
+* ``DevicePool`` - the node's GPUs as slots: a child process takes a free GPU for its whole task
+  (``HIP_VISIBLE_DEVICES`` = that one device) and gives it back when done, so two children never
+  share a device (each sizes its HBM caches to the whole card).
 """
 from __future__ import annotations
 
 import os
+import queue
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -50,6 +54,39 @@ class ExecutorManager:
             return [f.result() for f in futs]
 
 
+class DevicePool:
+    """GPU slots for child processes (one child per device at any time)."""
+
+    def __init__(self, ids):
+        self.ids = [str(i) for i in ids]
+        self._free = queue.Queue()
+        for i in self.ids:
+            self._free.put(i)
+
+    def __len__(self):
+        return len(self.ids)
+
+    @classmethod
+    def for_node(cls):
+        """This process's visible GPUs (``HIP_VISIBLE_DEVICES`` order), or None without a GPU.
+        Counting devices does not initialise the GPU in this process."""
+        if os.environ.get("SHIFU_FORCE_CPU") == "1":
+            return None
+        import torch
+        n = torch.cuda.device_count()
+        if n <= 0:
+            return None
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+        ids = [v.strip() for v in vis.split(",") if v.strip()][:n] if vis else list(range(n))
+        return cls(ids)
+
+    def acquire(self) -> str:
+        return self._free.get()
+
+    def release(self, dev: str) -> None:
+        self._free.put(dev)
+
+
 def run_cli(args, cwd: str, env: dict | None = None, log_path: str | None = None) -> int:
     """``python -m shifu_amd.cli <args>`` in ``cwd`` as a child process -> exit code."""
     e = dict(os.environ)
@@ -66,13 +103,20 @@ def run_cli(args, cwd: str, env: dict | None = None, log_path: str | None = None
             out.close()
 
 
-def cli_task(steps, cwd: str, log_path: str | None = None):
-    """A callable running CLI verbs in order in a child process; raises on the first failure."""
+def cli_task(steps, cwd: str, log_path: str | None = None, devices: DevicePool | None = None):
+    """A callable running CLI verbs in order in child processes; raises on the first failure.
+    ``devices``: the task holds one GPU of the pool for all its verbs (the children see only it)."""
     def run():
-        for st in steps:
-            args = st.split() if isinstance(st, str) else list(st)
-            rc = run_cli(args, cwd, log_path=log_path)
-            if rc != 0:
-                raise RuntimeError(f"'shifu {' '.join(args)}' in {cwd} exited with {rc}")
+        dev = devices.acquire() if devices is not None else None
+        env = None if dev is None else {"HIP_VISIBLE_DEVICES": dev, "LOCAL_RANK": "0"}
+        try:
+            for st in steps:
+                args = st.split() if isinstance(st, str) else list(st)
+                rc = run_cli(args, cwd, env=env, log_path=log_path)
+                if rc != 0:
+                    raise RuntimeError(f"'shifu {' '.join(args)}' in {cwd} exited with {rc}")
+        finally:
+            if dev is not None:
+                devices.release(dev)
         return 0
     return run

@@ -84,18 +84,27 @@ def _pipeline(root, steps=("init", "stats", "norm", "varsel", "train"), skip_ini
     from .stats import run_stats
     from .train import run_train
     from .varsel import run_varsel
+    from ..parallel import dist
+    # under torchrun every step ends with a barrier: rank 0 writes the step's outputs (ColumnConfig,
+    # models) that the next step -- or the score join -- reads on every rank
     if "init" in steps and not (skip_init_if_cc and os.path.exists(os.path.join(root, "ColumnConfig.json"))):
         run_init(root)
+        dist.barrier()
     if "stats" in steps:
         run_stats(root)
+        dist.barrier()
     if "norm" in steps:
         run_norm(root, shuffle=shuffle)
+        dist.barrier()
     if "varsel" in steps:
         run_varsel(root)
+        dist.barrier()
     if "train" in steps:
         if shuffle:
             run_norm(root, shuffle=True)        # `train -shuffle` re-shuffles the normalized data
+            dist.barrier()
         run_train(root)
+        dist.barrier()
 
 
 def _join_scores(subs, confs, out_dir: str) -> str:
@@ -129,8 +138,14 @@ def _has_models(d: str) -> bool:
 
 
 def combo_run(root: str, shuffle: bool = False, resume: bool = False):
+    """Under torchrun (world > 1) every sub model's pipeline runs data parallel over all ranks, one
+    after the other -- the reference runs one distributed Guagua job per sub model
+    (ComboModelProcessor.java:278-356) -- then the score join (each rank joins its byte ranges) and
+    the assemble pipeline.  In one process, ``shifu.combo.parallel > 1`` runs sub models side by side
+    as child processes, each pinned to a GPU of its own (``DevicePool``; at most one child per GPU)."""
     from ..config import environment
-    from ..runtime.executor import ExecutorManager, cli_task
+    from ..parallel import dist
+    from ..runtime.executor import DevicePool, ExecutorManager, cli_task
     ms = ModelSet(root)
     cfg = _load_cfg(ms)
     # sub models train with retries (ExecutorManager); shifu.combo.parallel > 1 runs them side by
@@ -144,34 +159,47 @@ def combo_run(root: str, shuffle: bool = False, resume: bool = False):
     todo = [(sub, d) for sub, d in zip(cfg["subTrains"], dirs) if not (resume and _has_models(d))]
     if resume and len(todo) < len(dirs):
         _log.info("combo -resume: %d of %d sub models already trained", len(dirs) - len(todo), len(dirs))
-    if parallel > 1:
+    info = dist.info()
+    if info.world_size > 1:
+        if parallel > 1:
+            _log.info("combo: %d ranks -- sub models run data parallel in turn (shifu.combo.parallel unused)",
+                      info.world_size)
+        for sub, d in todo:          # a failure on one rank must stop every rank: no retries here
+            _pipeline(d, shuffle=shuffle)
+    elif parallel > 1:
         steps = ["init", "stats", "norm -shuffle" if shuffle else "norm", "varsel",
                  "train -shuffle" if shuffle else "train"]
+        devices = DevicePool.for_node()
+        workers = min(parallel, len(devices)) if devices is not None else parallel
         tasks = [cli_task([s for s in steps if not (s == "init" and os.path.exists(os.path.join(d, "ColumnConfig.json")))],
-                          d, os.path.join(d, "combo_sub.log")) for _, d in todo]
+                          d, os.path.join(d, "combo_sub.log"), devices=devices) for _, d in todo]
+        ExecutorManager(workers, retries).run(tasks, [sub["modelName"] for sub, _ in todo])
     else:
         tasks = [(lambda d=d: _pipeline(d, shuffle=shuffle)) for _, d in todo]
-    ExecutorManager(parallel, retries).run(tasks, [sub["modelName"] for sub, _ in todo])
+        ExecutorManager(1, retries).run(tasks, [sub["modelName"] for sub, _ in todo])
     subs = [(sub["modelName"], ModelSet(d)) for sub, d in zip(cfg["subTrains"], dirs)]
     asm = cfg["assemble"]
     ad = _sub_dir(ms, asm["modelName"])
     data_dir = os.path.join(ad, "data")
     delim = _join_scores(subs, [sms.mc.dataSet for _, sms in subs], data_dir)
-    ams = ModelSet(ad)
-    ams.mc.dataSet["dataPath"] = data_dir
-    ams.mc.dataSet["headerPath"] = os.path.join(data_dir, ".pig_header")
-    ams.mc.dataSet["headerDelimiter"] = delim
-    fs = os.path.join(ad, "columns", "forceselect.column.names")
-    with open(fs, "w") as f:
-        f.write("\n".join(f"{name}_score" for name, _ in subs) + "\n")
-    ams.mc.varSelect["forceSelectColumnNameFile"] = fs
-    ams.mc.varSelect["forceEnable"] = True
-    ams.save_mc()
+    if info.rank == 0:
+        ams = ModelSet(ad)
+        ams.mc.dataSet["dataPath"] = data_dir
+        ams.mc.dataSet["headerPath"] = os.path.join(data_dir, ".pig_header")
+        ams.mc.dataSet["headerDelimiter"] = delim
+        fs = os.path.join(ad, "columns", "forceselect.column.names")
+        with open(fs, "w") as f:
+            f.write("\n".join(f"{name}_score" for name, _ in subs) + "\n")
+        ams.mc.varSelect["forceSelectColumnNameFile"] = fs
+        ams.mc.varSelect["forceEnable"] = True
+        ams.save_mc()
+    dist.barrier()
     _pipeline(ad, skip_init_if_cc=False, shuffle=True)   # assemble model: norm -shuffle / train -shuffle
     return 0
 
 
 def combo_eval(root: str):
+    from ..parallel import dist
     from .evaluate import run_eval
     ms = ModelSet(root)
     cfg = _load_cfg(ms)
@@ -186,15 +214,19 @@ def combo_eval(root: str):
         ev.dataSet["dataPath"] = out
         ev.dataSet["headerPath"] = os.path.join(out, ".pig_header")
         ev.dataSet["headerDelimiter"] = delim
-    ams.save_mc()
+    if dist.info().rank == 0:
+        ams.save_mc()
+    dist.barrier()
     return run_eval(ad)
 
 
 def run_combo(root=".", action="run", algs: str | None = None, shuffle: bool = False, resume: bool = False) -> int:
-    if action == "new":
-        combo_new(root, algs or "NN,LR")
-    elif action == "init":
-        combo_init(root)
+    from ..parallel import dist
+    if action in ("new", "init"):      # config writes: rank 0 alone, the others wait for it
+        if dist.info().rank == 0:
+            with dist.local_only():
+                combo_new(root, algs or "NN,LR") if action == "new" else combo_init(root)
+        dist.barrier()
     elif action == "run":
         combo_run(root, shuffle=shuffle, resume=resume)
     elif action == "eval":

@@ -215,8 +215,11 @@ def copy_model_set(src: str, dst: str) -> int:
 def init_model_params(root: str = ".") -> int:
     """``shifu init -model`` (ShifuCLI.initializeModelParam :632-635 ->
     checkAlgorithmParam): fill the default train.params of the configured algorithm."""
+    from ..parallel import dist
     from .base import ModelSet, check_algorithm_params
-    ms = ModelSet(root)
-    check_algorithm_params(ms.mc)
-    ms.save_mc()
+    if dist.info().rank == 0:          # one writer of ModelConfig.json under torchrun
+        ms = ModelSet(root)
+        check_algorithm_params(ms.mc)
+        ms.save_mc()
+    dist.barrier()
     return 0

@@ -71,13 +71,14 @@ def test_varsel_voted_pipeline(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_population_gpu_matches_cpu_oracle():
+@pytest.mark.parametrize("H", [10, 100])
+def test_population_gpu_matches_cpu_oracle(H):
     """The population on the own kernels (MFMA forward, ga_kernels.hip heads, ring wgrad,
     optimizer_kernel RPROP) against the torch CPU oracle of the same arithmetic: per-seed
-    validation errors within 1e-3 relative."""
+    validation errors within 1e-3 relative.  H = 100 runs the any-width head (> 64 hidden)."""
     from shifu_amd.algos.ga_varsel import PopulationData, PopulationTrainer
     g = np.random.default_rng(4)
-    n, F, P, E, H = 20000, 300, 40, 60, 10
+    n, F, P, E = 20000, 300, 40, 60
     X = g.normal(size=(n, F)).astype(np.float32)
     y = (X[:, 0] - X[:, 7] + 0.5 * X[:, 11] > 0).astype(np.float32)
     w = (g.random(n) + 0.5).astype(np.float32)
