@@ -417,7 +417,10 @@ def create_init_model_config(name: str, alg: str = "NN", description: str | None
                                  autoFilterEnable=True, missingRateThreshold=0.98, correlationThreshold=1.0,
                                  minIvThreshold=0.0, minKsThreshold=0.0, postCorrelationMetric="IV",
                                  params=None)
-    d["normalize"] = OrderedDict(stdDevCutOff=6.0, sampleRate=1.0, sampleNegOnly=False, normType="ZSCALE")
+    # WDL trains on z-scored numerics + category indices (the reference pairs WDL with ZSCALE_INDEX,
+    # TrainModelProcessor.java:587; WDLWorker reads a category index per categorical input)
+    d["normalize"] = OrderedDict(stdDevCutOff=6.0, sampleRate=1.0, sampleNegOnly=False,
+                                 normType="ZSCALE_INDEX" if alg == "WDL" else "ZSCALE")
     epochs = {"NN": 200, "SVM": 100, "RF": 20000, "GBT": 20000, "LR": 100, "TENSORFLOW": 100}.get(alg, 100)
     d["train"] = OrderedDict(baggingNum=5, baggingWithReplacement=False, baggingSampleRate=1.0, validSetRate=0.2,
                              numTrainEpochs=epochs, isContinuous=False, workerThreadCount=4, algorithm=alg,

@@ -22,7 +22,10 @@ import torch
 
 from ..formats.javaio import JavaIn, JavaOut
 from ..parallel import dist
+from ..utils.log import get_logger
 from .nn import act_fwd
+
+_log = get_logger("models.wdl")
 
 
 # GPU wide sums + deep input gathers in one pass (ops/csrc/wdl_kernels.hip); SHIFU_WDL_HIP=0: torch ops
@@ -334,17 +337,341 @@ def read_wdl(path: str) -> WDLModel:
     return WDLModel(net, norm, stats, names, cutoff)
 
 
+# ------------------------------------------------------------------------------------------------
+# Training: WDLMaster + WDLWorker semantics (J/core/dtrain/wdl/WDLMaster.java:159-186,
+# WDLWorker.java:679-718, WideAndDeep.java:163-232, the layers' backward, GradientDescent.java:44-63)
+# ------------------------------------------------------------------------------------------------
+class WDLRows:
+    """This rank's training rows as (dense fp32 [m, nd], category indices int64 [m, Fc]) chunks.
+
+    ``X`` is an [n, F] float array (the ZSCALE_INDEX NormalizedData memmap shard, or inputs built
+    from raw columns) whose columns ``num_pos`` are the dense inputs and ``cat_pos`` the category
+    indices (missing / unknown = the category count).  On the GPU the rows are uploaded once and
+    stay resident when they fit in half of the free HBM; otherwise every epoch streams them from
+    the host in chunks (a reader thread fills pinned buffers while the previous chunk computes).
+    On the CPU the chunks are read from the memmap as they are used (bounded host memory)."""
+
+    def __init__(self, X, num_pos, cat_pos, device, chunk_rows: int = 1 << 20):
+        self.X, self.num_pos, self.cat_pos = X, list(num_pos), list(cat_pos)
+        self.n = int(np.shape(X)[0])
+        self.dev = torch.device(device)
+        self.chunk_rows = int(chunk_rows)
+        self.nd, self.fc = len(self.num_pos), len(self.cat_pos)
+        self._resident = None
+        if self.dev.type == "cuda":
+            from ..utils.device import free_hbm
+            need = self.n * (self.nd * 4 + self.fc * 8)
+            force = os.environ.get("SHIFU_WDL_STREAM") == "1"
+            if not force and need < 0.5 * free_hbm(self.dev):
+                self._resident = [self._host_chunk(a, min(self.n, a + self.chunk_rows))
+                                  for a in range(0, self.n, self.chunk_rows)]
+                self._resident = [(d.to(self.dev), c.to(self.dev)) for d, c in self._resident]
+
+    def _host_chunk(self, a, b):
+        blk = np.asarray(self.X[a:b], dtype=np.float32)
+        dense = torch.from_numpy(np.ascontiguousarray(blk[:, self.num_pos]) if self.nd else np.zeros((b - a, 0), np.float32))
+        cats = torch.from_numpy(np.rint(blk[:, self.cat_pos]).astype(np.int64) if self.fc else np.zeros((b - a, 0), np.int64))
+        return dense, cats
+
+    def chunks(self):
+        """-> (row0, row1, dense, cats) over the shard, on the device."""
+        if self._resident is not None:
+            for i, (d, c) in enumerate(self._resident):
+                a = i * self.chunk_rows
+                yield a, a + d.shape[0], d, c
+            return
+        bounds = [(a, min(self.n, a + self.chunk_rows)) for a in range(0, self.n, self.chunk_rows)]
+        if self.dev.type != "cuda":
+            for a, b in bounds:
+                d, c = self._host_chunk(a, b)
+                yield a, b, d, c
+            return
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(1) as ex:            # reader thread: next chunk into pinned memory
+            nxt = ex.submit(lambda ab: [t.pin_memory() for t in self._host_chunk(*ab)], bounds[0]) if bounds else None
+            for i, (a, b) in enumerate(bounds):
+                d, c = nxt.result()
+                if i + 1 < len(bounds):
+                    nxt = ex.submit(lambda ab: [t.pin_memory() for t in self._host_chunk(*ab)], bounds[i + 1])
+                yield a, b, d.to(self.dev, non_blocking=True), c.to(self.dev, non_blocking=True)
+
+
+class WDLTrainer:
+    """Full-batch, data-parallel Wide & Deep training with the reference's master / worker math.
+
+    Per epoch every rank runs ``WideAndDeep.forward`` / ``backward`` over its training rows:
+    ``p = sigmoid(wide + deep)``, the logit gradient ``(p - y) p (1 - p) s`` (s: significance,
+    WideAndDeep.java:203-207), every layer's weight gradients SUMMED over the rows, plus the layers'
+    per-row L2 term (``l2reg * w`` added once per row to the dense layers' and the wide dense
+    layer's weights, and per row to the wide-field weight the row touches; none on biases or
+    embeddings: DenseLayer.java:188-198, WideDenseLayer.java:96-104, WideFieldLayer.java:97-109,
+    EmbedFieldLayer.java:107-117).  The gradients of all ranks are summed by one all-reduce
+    (WDLMaster.aggregateWorkerGradients) and the master's ``GradientDescent(LearningRate)``
+    (``w -= lr * sum_grad``, GradientDescent.java:44-63, hard-wired in WDLMaster.java:175) runs
+    on the replicated weights -- on the GPU in ``optimizer_kernel`` (rule B, momentum 0, on the
+    ascent direction).  ``Optimizer: ADAM / ADAGRAD`` are extensions (the mean gradient through
+    those rules).  The errors are ``sum s (p - y)^2 / row count`` for the training and the
+    validation rows with the epoch's weights (WDLWorker.java:689-706).
+
+    One documented deviation: the reference ASSIGNS the bias gradients per row (DenseLayer.java:197
+    ``bGrads[j] = backInputs[j]``, BiasLayer.java:54), so only a worker's last row reaches the
+    master; here bias gradients are summed over the rows like every other gradient (the assignment
+    makes the result depend on the row order and the worker count).
+
+    GPU: the wide sums / deep input gathers and their scatters are ``wdl_kernels.hip``, the dense
+    wide part and its gradient the row / column dot kernels, the deep tower ``deep_forward`` /
+    ``deep_backward`` (bf16 MFMA GEMMs, fp32 sums); no autograd, no torch.optim."""
+
+    def __init__(self, net: WideDeepNet, device, lr: float, l2: float = 0.0, optimizer: str = "GD"):
+        from .nn import Optimizer
+        self.dev = torch.device(device)
+        self.gpu = self.dev.type == "cuda"
+        self.net = net.to(self.dev)
+        # explicit order (Module.parameters() lists a module's own parameters before its lists')
+        ps = list(net.wide_tables) + [net.wide_dense, net.bias] + list(net.embeds) + list(net.layers) + [net.final]
+        self.params = ps
+        sizes = [p.numel() for p in ps]
+        self.flat = torch.empty(sum(sizes), dtype=torch.float32, device=self.dev)
+        self.offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        for p, a, b in zip(ps, self.offs[:-1], self.offs[1:]):
+            self.flat[a:b].copy_(p.data.reshape(-1))
+            p.data = self.flat[a:b].view_as(p.data)
+        self.grad = torch.zeros_like(self.flat)
+        self.gviews = [self.grad[a:b].view_as(p) for p, a, b in zip(ps, self.offs[:-1], self.offs[1:])]
+        fc, E, L = len(net.wide_tables), len(net.embeds), len(net.layers)
+        self.i_wide, self.i_wd, self.i_bias = 0, fc, fc + 1
+        self.i_emb, self.i_layers, self.i_final = fc + 2, fc + 2 + E, fc + 2 + E + L
+        # rows whose weights take the per-row L2 term: wide dense, dense layers and final layer
+        # weights (not their bias columns)
+        l2row = torch.zeros_like(self.flat)
+        mv = [l2row[a:b].view_as(p) for p, a, b in zip(ps, self.offs[:-1], self.offs[1:])]
+        mv[self.i_wd].fill_(1.0)
+        for i in list(range(self.i_layers, self.i_layers + L)) + [self.i_final]:
+            mv[i][:, :-1] = 1.0
+        self.l2row = l2row
+        self.l2 = float(l2)
+        self.lr = float(lr)
+        self.opt_name = (optimizer or "GD").upper()
+        rule = {"ADAM": "ADAM", "ADAGRAD": "ADAGRAD"}.get(self.opt_name, "B")
+        self.opt = Optimizer(self.flat.numel(), self.dev, rule, learning_rate=self.lr, momentum=0.0)
+        self.wide_cnt = None                     # per wide-table entry: training rows of this rank
+        self.n_train = 0.0
+
+    # ---- forward / backward of one chunk ------------------------------------------------------
+    def _tables(self):
+        net = self.net
+        fc, E = len(net.wide_tables), len(net.embeds)
+        wt = self.flat[self.offs[self.i_wide]: self.offs[self.i_wide + fc]] if fc else self.flat.new_zeros(1)
+        et = self.flat[self.offs[self.i_emb]: self.offs[self.i_emb + E]] if E else self.flat.new_zeros(1)
+        return wt, et
+
+    def _forward_backward(self, dense, cats, y, s_tr):
+        """logit of every row; accumulates the (ascent-direction) gradients of sum_i s_i * loss_i
+        into self.grad.  Returns p."""
+        net = self.net
+        if self.gpu and WDL_HIP:
+            return self._fb_hip(dense, cats, y, s_tr)
+        n = dense.shape[0]
+        gv = self.gviews
+        logit = torch.zeros(n, device=self.dev)
+        if net.wide_on:
+            logit = logit + (dense @ net.wide_dense if net.n_dense else 0.0) + net.bias
+            for f, t in enumerate(net.wide_tables):
+                logit = logit + t[cats[:, f]]
+        acts_out, zs = [], []
+        if net.deep_on:
+            parts = [dense] + [e[cats[:, f]] for e, f in zip(net.embeds, net.embed_fields)]
+            a = torch.cat(parts, 1) if len(parts) > 1 else dense
+            acts_out = [a]
+            for W, act in zip(net.layers, net.acts):
+                z = a @ W[:, :-1].t() + W[:, -1]
+                a = act_fwd(act, z)
+                zs.append(z)
+                acts_out.append(a)
+            logit = logit + (a @ net.final[0, :-1] + net.final[0, -1])
+        p = torch.sigmoid(logit)
+        g = (y - p) * p * (1 - p) * s_tr                      # ascent on the logit
+        if net.wide_on:
+            if net.n_dense:
+                gv[self.i_wd].add_(g @ dense)
+            gv[self.i_bias].add_(g.sum())
+            for f in range(len(net.wide_tables)):
+                gv[self.i_wide + f].index_add_(0, cats[:, f], g)
+        if net.deep_on:
+            from .nn import act_deriv
+            aL = acts_out[-1]
+            gv[self.i_final][0, :-1].add_(g @ aL)
+            gv[self.i_final][0, -1].add_(g.sum())
+            d = g[:, None] * net.final[0, :-1][None, :]
+            for l in range(len(net.layers) - 1, -1, -1):
+                a_in = acts_out[l]
+                d = d * act_deriv(net.acts[l], zs[l], acts_out[l + 1])
+                gv[self.i_layers + l][:, :-1].add_(d.t() @ a_in)
+                gv[self.i_layers + l][:, -1].add_(d.sum(0))
+                d = d @ net.layers[l][:, :-1]
+            off = net.n_dense
+            for k, f in enumerate(net.embed_fields):
+                D = net.embed_dim
+                gv[self.i_emb + k].index_add_(0, cats[:, f], d[:, off + k * D: off + (k + 1) * D])
+        return p
+
+    def _fb_hip(self, dense, cats, y, s_tr):
+        from ..ops import _native as nat
+        net = self.net
+        n = dense.shape[0]
+        st = nat.stream_of(dense)
+        woff, eoff, efield = self._offsets()
+        fc, E, D = len(net.wide_tables), len(net.embed_fields), net.embed_dim
+        wt, et = self._tables()
+        want_wide = net.wide_on and fc > 0
+        wide = torch.zeros(n, device=self.dev)
+        A = torch.empty(n, net.n_dense + E * D, device=self.dev) if net.deep_on else None
+        ef = efield if (net.deep_on and E) else efield[:0]
+        nat.call_hip("shifu_wdl_gather", 0, dense, net.n_dense, cats, fc, wt, woff, et, eoff, ef,
+                     len(ef), D, wide if want_wide else None, A, net.n_dense + E * D, None, None, wt.numel(),
+                     et.numel(), n, st)
+        logit = wide
+        if net.wide_on:
+            if net.n_dense:
+                lin = torch.empty(n, device=self.dev)
+                nat.call_hip("shifu_rowdot_f32_act", dense, net.n_dense, n, net.n_dense, net.wide_dense, 0.0, -1, -1,
+                             lin, st)
+                logit = logit + lin
+            logit = logit + net.bias
+        state = None
+        if net.deep_on:
+            out, state = deep_forward(A, net.final, tuple(net.acts), tuple(net.layers))
+            logit = logit + out
+        p = torch.sigmoid(logit)
+        g = ((y - p) * p * (1 - p) * s_tr).contiguous()
+        gv = self.gviews
+        if net.wide_on:
+            if net.n_dense:
+                tmp = torch.empty(net.n_dense, device=self.dev)
+                part = torch.empty(max(1, -(-n // 256)) * net.n_dense, device=self.dev)
+                nat.call_hip("shifu_coldot_f32", g, dense, net.n_dense, n, net.n_dense, part, tmp, st)
+                gv[self.i_wd].add_(tmp)
+            gv[self.i_bias].add_(g.sum())
+        dwt = self.grad[self.offs[self.i_wide]: self.offs[self.i_wide + fc]] if want_wide else None
+        dA = None
+        if net.deep_on:
+            dA, g_final, gWs = deep_backward(state, g)
+            gv[self.i_final].add_(g_final)
+            for l, G in enumerate(gWs):
+                gv[self.i_layers + l].add_(G)
+        det = self.grad[self.offs[self.i_emb]: self.offs[self.i_emb + len(net.embeds)]] if (dA is not None and E) else None
+        if dwt is not None or det is not None:
+            nat.call_hip("shifu_wdl_gather", 1, None, net.n_dense, cats, fc, None, woff, None, eoff, ef, len(ef), D,
+                         g if dwt is not None else None, dA.contiguous() if det is not None else None,
+                         net.n_dense + E * D, dwt, det, wt.numel(), et.numel(), n, st)
+        return p
+
+    def _offsets(self):
+        net = self.net
+        if getattr(self, "_offs", None) is None:
+            ws = [s + 1 for s in net.cat_sizes]
+            woff = torch.tensor(np.concatenate([[0], np.cumsum(ws)[:-1]]) if ws else [0], dtype=torch.int32)
+            es = [(net.cat_sizes[f] + 1) for f in net.embed_fields]
+            eoff = torch.tensor(np.concatenate([[0], np.cumsum(es)[:-1]]) if es else [0], dtype=torch.int32)
+            ef = torch.tensor(net.embed_fields or [0], dtype=torch.int32)
+            if not net.embed_fields:
+                ef = ef[:0]
+            self._offs = (woff.to(self.dev), eoff.to(self.dev), ef.to(self.dev))
+        return self._offs
+
+    # ---- one epoch ------------------------------------------------------------------------------
+    def epoch(self, rows: WDLRows, y: np.ndarray, s_tr: np.ndarray, s_va: np.ndarray, n_tr: float, n_va: float):
+        """One full-batch iteration.  y / s_tr / s_va: per-row labels, training significance (0 off
+        the training set), validation weight (0 off the validation set).  Returns (train error,
+        validation error) of the weights the epoch started from."""
+        if self.wide_cnt is None:
+            self._count_wide(rows, s_tr)
+        self.grad.zero_()
+        err = torch.zeros(2, dtype=torch.float64, device=self.dev)
+        yt, st_, sv = (torch.from_numpy(np.asarray(a, np.float32)) for a in (y, s_tr, s_va))
+        with torch.no_grad():
+            for a, b, dense, cats in rows.chunks():
+                yy = yt[a:b].to(self.dev, non_blocking=True)
+                tr = st_[a:b].to(self.dev, non_blocking=True)
+                va = sv[a:b].to(self.dev, non_blocking=True)
+                p = self._forward_backward(dense, cats, yy, tr)
+                e2 = (p - yy) ** 2
+                err[0] += (e2 * tr).sum().double()
+                err[1] += (e2 * va).sum().double()
+            if self.l2 > 0:                       # per-row L2 of the layers (ascent: minus)
+                self.grad.add_(-self.l2 * (self.n_train * self.l2row + self.wide_cnt) * self.flat)
+            dist.all_reduce_(self.grad)
+            dist.all_reduce_(err)
+            tot = torch.tensor([n_tr, n_va], dtype=torch.float64, device=self.dev)
+            dist.all_reduce_(tot)
+            n_all = float(tot[0])
+            g = self.grad if self.opt_name not in ("ADAM", "ADAGRAD") else self.grad / max(n_all, 1.0)
+            self.opt.step(self.flat, g, n_all)
+        terr = float(err[0]) / max(n_all, 1.0)
+        verr = float(err[1]) / float(tot[1]) if float(tot[1]) > 0 else float("nan")
+        return terr, verr
+
+    def _count_wide(self, rows: WDLRows, s_tr: np.ndarray):
+        """Training rows per wide-table entry on this rank (the wide fields' per-row L2 term)."""
+        net = self.net
+        cnt = torch.zeros_like(self.flat)
+        on = torch.from_numpy((np.asarray(s_tr) != 0).astype(np.float32))
+        self.n_train = float(on.sum())
+        if net.wide_on and len(net.wide_tables):
+            cv = [cnt[a:b] for a, b in zip(self.offs[:-1], self.offs[1:])]
+            with torch.no_grad():
+                for a, b, _, cats in rows.chunks():
+                    w = on[a:b].to(self.dev)
+                    for f in range(len(net.wide_tables)):
+                        cv[self.i_wide + f].index_add_(0, cats[:, f], w)
+        self.wide_cnt = cnt
+
+
+def wdl_rows_from_cache(ms, ts):
+    """(X, num_pos, cat_pos) of a ZSCALE_INDEX-family NormalizedData shard (``ts.X``), or None."""
+    from ..config.enums import is_index_norm
+    if ts.X is None or not is_index_norm(ms.mc.norm_type):
+        return None
+    nums = list(ts.meta.get("input_nums") or [])
+    cols = ms.input_columns()
+    pos = {n: i for i, n in enumerate(nums)}
+    if len(nums) != np.shape(ts.X)[1] or any(c.num not in pos for c in cols):
+        return None
+    num_pos = [pos[c.num] for c in cols if not c.is_categorical()]
+    cat_pos = [pos[c.num] for c in cols if c.is_categorical()]
+    return ts.X, num_pos, cat_pos
+
+
 def train_wdl_step(step, tid, p, ts, y, train_m, valid_m, sw):
-    """Train one WDL bag inside ``TrainStep`` (re-reads raw columns: WDL needs category indices)."""
+    """Train one WDL bag inside ``TrainStep``.  Rows: this rank's shard of the ZSCALE_INDEX
+    NormalizedData (z-scored numerics, category indices) with the step's counter-based split;
+    other norm types: the inputs are rebuilt from this rank's shard of the raw columns."""
+    from ..steps.base import shard_model_data
+    from ..steps.train import TrainSet, split_masks
     ms, mc = step.ms, step.mc
     cols = ms.input_columns()
-    md = ms.load_raw(cols)
+    num = [c for c in cols if not c.is_categorical()]
+    cat = [c for c in cols if c.is_categorical()]
     cutoff = float(mc.normalize.get("stdDevCutOff", 6.0))
-    dense, idx, sizes, num, cat = wdl_inputs(ms.ccs, md.table, cols, cutoff)
-    y = md.y.astype(np.float32)
-    w = md.w.astype(np.float32)
-    rng = np.random.default_rng(tid)
-    valid = rng.random(md.n) < float(mc.train.get("validSetRate", 0.2) or 0.0)
+    src = wdl_rows_from_cache(ms, ts)
+    if src is not None:
+        X, num_pos, cat_pos = src
+        w = np.asarray(ts.w, np.float32)
+        yy = np.asarray(y, np.float32)
+        tr_m, va_m, sw_ = train_m, valid_m, sw
+    else:
+        info = dist.info()
+        full = ms.load_raw(cols)
+        md = shard_model_data(full)
+        dense, idx, _, _, _ = wdl_inputs(ms.ccs, md.table, cols, cutoff)
+        X = np.concatenate([dense, idx.astype(np.float32)], 1)
+        num_pos, cat_pos = list(range(dense.shape[1])), list(range(dense.shape[1], X.shape[1]))
+        w, yy = md.w.astype(np.float32), md.y.astype(np.float32)
+        fake = TrainSet(y=yy, w=w, row0=full.n * info.rank // info.world_size)
+        n_kfold = int(mc.train.get("numKFold", -1) or -1)
+        seed = max(0, int(mc.train.get("baggingSampleSeed", -1)))
+        tr_m, va_m, sw_ = split_masks(mc, fake, tid, n_kfold, seed)
+    sizes = [len(c.bin_category or []) for c in cat]
     embed_ids = p.get("NumEmbedColumnIds")
     cat_nums = [c.num for c in cat]
     embed_fields = [cat_nums.index(c) for c in embed_ids if c in cat_nums] if embed_ids else list(range(len(cat)))
@@ -352,39 +679,24 @@ def train_wdl_step(step, tid, p, ts, y, train_m, valid_m, sw):
     acts = list(p.get("ActivationFunc") or ["relu"])
     while len(acts) < len(hidden):
         acts.append(acts[-1])
-    net = WideDeepNet(dense.shape[1], sizes, embed_fields, int(p.get("NumEmbedOuputs", 8) or 8), hidden,
-                      acts[: len(hidden)]).to(step.dev)
+    net = WideDeepNet(len(num), sizes, embed_fields, int(p.get("NumEmbedOuputs", p.get("EmbedOutputs", 8)) or 8),
+                      hidden, acts[: len(hidden)])
     for prm in net.parameters():
         dist.broadcast_(prm.data, 0)
-    lr = float(p.get("LearningRate", 0.01))
     l2 = float(p.get("WDLL2Reg", 0.0) or 0.0)
-    opt_name = str(p.get("Optimizer", "ADAM")).upper()
-    opt = {"ADAGRAD": torch.optim.Adagrad, "SGD": torch.optim.SGD, "GD": torch.optim.SGD}.get(
-        opt_name, torch.optim.Adam)(net.parameters(), lr=lr)
-    dv = lambda a: torch.from_numpy(a).to(step.dev)   # noqa: E731
-    td, ti, ty, tw = dv(dense[~valid]), dv(idx[~valid]), dv(y[~valid]), dv(w[~valid])
-    vd, vi, vy = dv(dense[valid]), dv(idx[valid]), dv(y[valid])
+    trainer = WDLTrainer(net, step.dev, float(p.get("LearningRate", 0.1)), l2, str(p.get("Optimizer", "GD")))
+    rows = WDLRows(X, num_pos, cat_pos, step.dev)
+    _log.info("WDL trainer %d: %d rows on rank %d from %s (%s on the device), %s lr %g, L2 %g", tid, rows.n,
+              dist.info().rank, "the NormalizedData cache" if src is not None else "the raw columns",
+              "resident" if rows._resident is not None else ("streamed" if rows.dev.type == "cuda" else "host"),
+              trainer.opt_name, trainer.lr, l2)
+    s_tr = (w * np.asarray(sw_, np.float32) * np.asarray(tr_m, np.float32)).astype(np.float32)
+    s_va = (w * np.asarray(va_m, np.float32)).astype(np.float32)
+    n_tr, n_va = float(np.count_nonzero(np.asarray(tr_m) & (np.asarray(sw_) > 0))), float(np.count_nonzero(va_m))
     epochs = int(mc.train.get("numTrainEpochs", 100))
     verr = float("nan")
     for ep in range(1, epochs + 1):
-        opt.zero_grad()
-        pr = torch.sigmoid(net(td, ti))
-        loss = 0.5 * ((pr - ty) ** 2 * tw).sum()
-        if l2 > 0:
-            loss = loss + 0.5 * l2 * sum((q ** 2).sum() for q in net.parameters())
-        loss.backward()
-        flat = torch.cat([q.grad.reshape(-1) for q in net.parameters()])
-        tail = torch.tensor([float(((pr.detach() - ty) ** 2).sum()), float(len(ty))], device=step.dev)
-        buf = torch.cat([flat, tail])
-        dist.all_reduce_(buf)
-        off = 0
-        for q in net.parameters():
-            q.grad.copy_(buf[off: off + q.numel()].view_as(q) / max(float(buf[-1]), 1.0))
-            off += q.numel()
-        opt.step()
-        terr = float(buf[-2] / max(float(buf[-1]), 1.0))
-        with torch.no_grad():
-            verr = float(((torch.sigmoid(net(vd, vi)) - vy) ** 2).mean()) if len(vy) else float("nan")
+        terr, verr = trainer.epoch(rows, yy, s_tr, s_va, n_tr, n_va)
         step._log_epoch(tid, ep, terr, verr)
     if step.info.rank == 0:
         from ..steps.train import nn_column_stats

@@ -152,7 +152,7 @@ def test_wdl_pipeline_on_gpu(tmp_path):
     mc.train["numTrainEpochs"] = 60
     mc.train["baggingNum"] = 1
     mc.train["params"] = {"NumHiddenLayers": 1, "NumHiddenNodes": [16], "ActivationFunc": ["relu"],
-                          "LearningRate": 0.05, "NumEmbedOuputs": 4, "WDLL2Reg": 0.0}
+                          "LearningRate": 0.01, "NumEmbedOuputs": 4, "WDLL2Reg": 0.0}
     mc.save()
     _run(root, ("init", "stats", "varsel", "norm", "train", "eval"))
     assert _auc(root) > 0.8, _auc(root)

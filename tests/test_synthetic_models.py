@@ -35,7 +35,7 @@ def test_wdl_pipeline(tmp_path):
     mc.train["numTrainEpochs"] = 60
     mc.train["baggingNum"] = 1
     mc.train["params"] = {"NumHiddenLayers": 1, "NumHiddenNodes": [16], "ActivationFunc": ["relu"],
-                          "LearningRate": 0.05, "NumEmbedOuputs": 4, "WDLL2Reg": 0.0}
+                          "LearningRate": 0.01, "NumEmbedOuputs": 4, "WDLL2Reg": 0.0}
     mc.save()
     _run(root, ["init", "stats", "varsel", "norm", "train", "eval"])
     assert os.path.exists(os.path.join(root, "models/model0.wdl"))
