@@ -29,6 +29,8 @@ from ..utils.log import get_logger
 
 _log = get_logger("data.gpu_parse")
 
+# largest block the device parse takes: field bounds are int32 offsets into the block (+64 B pad)
+BLOCK_LIMIT = (1 << 31) - 64
 FB_CAP = 1 << 20          # fallback fields per block before the whole block is parsed on the host
 MAX_TOKENS, TOKEN_BYTES = 8, 15
 
@@ -161,7 +163,7 @@ class GpuBlockParser:
                 yield off, None, None
                 continue
             L = len(data)
-            if L == 0 or L >= (1 << 31) - 64:
+            if L == 0 or L >= BLOCK_LIMIT:
                 yield off, data, None
                 continue
             t0 = time.perf_counter()
@@ -210,7 +212,7 @@ class GpuBlockParser:
         self.stats["blocks"] += 1
         if L == 0:
             return self._host_framing(data, nthreads, None)
-        if L >= (1 << 31) - 64:                  # field bounds are int32 block offsets
+        if L >= BLOCK_LIMIT:                     # field bounds are int32 block offsets
             self.stats["host_blocks"] += 1
             return parse_block(data, self.delim, self.kinds, self.missing, nthreads)
         T = self.times

@@ -183,6 +183,9 @@ def _lines_in_range(path: str, start: int, end: int, chunk_bytes: int, nbuf: int
             # never read (much) past the range: the line straddling `end` is completed by the
             # small follow-up reads of the carry logic
             want = min(chunk_bytes, max(end - pos - len(carry), 0) + (1 << 16))
+            if pinned:                         # device-parse blocks: carry + read < the parser's limit
+                from .gpu_parse import BLOCK_LIMIT
+                want = max(1, min(want, BLOCK_LIMIT - 1 - len(carry)))
             need = len(carry) + want
             buf = bufs[k]
             if buf is None or len(buf) < need:

@@ -17,16 +17,28 @@ import numpy as np
 import torch
 
 from ..parallel import dist
+from ..utils.log import get_logger
 from .nn import Optimizer
+
+_log = get_logger("models.lr")
 
 FLAT_SPOT = 0.1
 
 
 class LRTrainer:
     def __init__(self, n_in: int, device=None, propagation="R", learning_rate=0.1, reg=0.0, reg_level="NONE",
-                 learning_decay=0.0, momentum=0.5, adam_beta1=0.9, adam_beta2=0.999, seed=0, init=None):
+                 learning_decay=0.0, momentum=0.5, adam_beta1=0.9, adam_beta2=0.999, seed=0, init=None,
+                 input_dtype: str | None = None):
+        from ..config import environment
         from ..utils.device import default_device
         self.device = torch.device(device) if device is not None else default_device()
+        # resident input rows: fp32 (the reference LR is double throughout, LogisticRegressionWorker
+        # :302-352); "auto" keeps fp32 unless the fp32 rows would not fit in HBM, then stores bf16
+        # rows (fp32 sums) and says so; "bf16" forces that mode (shifu.lr.inputDtype)
+        self.input_dtype_request = str(input_dtype or environment.get("shifu.lr.inputDtype", "auto") or "auto").lower()
+        if self.input_dtype_request not in ("auto", "fp32", "float32", "bf16", "bfloat16"):
+            raise ValueError(f"shifu.lr.inputDtype must be auto, fp32 or bf16, not {self.input_dtype_request}")
+        self.input_dtype = "fp32"
         self.n_in = n_in
         g = torch.Generator().manual_seed(seed)
         w = (torch.rand(n_in + 1, generator=g, dtype=torch.float32) - 0.5) if init is None else \
@@ -41,7 +53,7 @@ class LRTrainer:
     def prepare(self, x, y, s=None):
         x = torch.as_tensor(x)
         n = x.shape[0]
-        dt = torch.bfloat16 if (self.device.type == "cuda" and x.numel() > (1 << 30)) else torch.float32
+        dt = self._row_dtype(n, x.shape[1])
         if self.device.type == "cuda":      # pad rows to a 16-byte multiple for the vector loads of K9
             fp = (x.shape[1] + 7) // 8 * 8
             xp = torch.zeros(n, fp, dtype=dt, device=self.device)
@@ -53,6 +65,23 @@ class LRTrainer:
         sd = torch.ones(n, device=self.device) if s is None else \
             torch.as_tensor(s, dtype=torch.float32).reshape(n).to(self.device)
         return xd, yd, sd
+
+    def _row_dtype(self, n: int, f: int) -> torch.dtype:
+        req = self.input_dtype_request
+        if self.device.type != "cuda" or req in ("fp32", "float32"):
+            self.input_dtype = "fp32"
+            return torch.float32
+        if req in ("bf16", "bfloat16"):
+            self.input_dtype = "bf16"
+        else:
+            from ..utils.device import free_hbm
+            fp32_bytes = n * ((f + 7) // 8 * 8) * 4
+            self.input_dtype = "bf16" if fp32_bytes > 0.8 * free_hbm(self.device) else "fp32"
+        if self.input_dtype == "bf16":
+            _log.warning("LR: %d x %d input rows kept as bf16 in HBM (fp32 rows: %.1f GB); dot products and "
+                         "gradient sums stay fp32 (shifu.lr.inputDtype=%s)", n, f, n * f * 4 / 1e9, req)
+            return torch.bfloat16
+        return torch.float32
 
     def _score(self, x):
         if x.is_cuda:                          # own row-dot kernel (wdl_kernels.hip)

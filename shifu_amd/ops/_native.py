@@ -136,6 +136,7 @@ RT_SIGNATURES = {
     "shifu_join_lines": ("plPiipplpli", "l"),
     "shifu_merge_runs": ("ippppP", "l"),
     "shifu_gather_lines": ("ppplPp", "l"),
+    "shifu_eval_set_flush_bytes": ("l", "l"),
     "shifu_gen_csv": ("Pliildii", "i"),
     "shifu_gen_strong_cols": ("iip", "i"),
     "shifu_parse_fields": ("ppLp", "l"),

@@ -226,43 +226,63 @@ SHIFU_RT_API long shifu_join_lines(const char* buf, long len, const char* sep, i
 // k-way merge of R sorted runs of lines into `out_path` (appending).  Run r: lines blob + line_end
 // offsets (ascending) + keys (the run's order: descending key); ties go to the lower run index,
 // so runs = ranks in order reproduces a stable single-process sort.  Returns lines written or -1.
+// Output staging of the merge / gather below: lines are copied into a fixed-size buffer that is
+// written out whenever it fills (the merging rank's memory stays bounded whatever the score file's
+// size; one fwrite per line was ~1-2 s at 20M rows).
+static size_t kFlushBytes = (size_t)256 << 20;
+SHIFU_RT_API long shifu_eval_set_flush_bytes(long b) {      // tests: a small buffer (flush paths)
+  const long old = (long)kFlushBytes;
+  if (b > 0) kFlushBytes = (size_t)b;
+  return old;
+}
+
 SHIFU_RT_API long shifu_merge_runs(int R, const char* const* blobs, const long* const* ends, const double* const* keys,
                                    const long* counts, const char* out_path) {
   FILE* f = std::fopen(out_path, "ab");
   if (!f) return -1;
-  long total = 0, bytes = 0;
-  for (int r = 0; r < R; ++r)
-    if (counts[r] > 0) { total += counts[r]; bytes += ends[r][counts[r] - 1]; }
-  std::vector<char> out((size_t)bytes);             // merged into memory, written with one call
-  size_t o = 0;
+  long total = 0;
   int live = 0, only = -1;
   for (int r = 0; r < R; ++r)
-    if (counts[r] > 0) { ++live; only = r; }
-  if (live == 1) {                                  // one run: it is the merge
-    std::memcpy(out.data(), blobs[only], (size_t)bytes);
-    o = (size_t)bytes;
-  } else {
-    struct Head { double key; int run; };
-    auto worse = [](const Head& a, const Head& b) {        // priority: larger key, then lower run
-      return a.key < b.key || (a.key == b.key && a.run > b.run);
-    };
-    std::priority_queue<Head, std::vector<Head>, decltype(worse)> pq(worse);
-    std::vector<long> at(R, 0);
-    for (int r = 0; r < R; ++r)
-      if (counts[r] > 0) pq.push({keys[r][0], r});
-    while (!pq.empty()) {
-      const Head h = pq.top();
-      pq.pop();
-      const int r = h.run;
-      const long i = at[r]++;
-      const long a = i ? ends[r][i - 1] : 0, b = ends[r][i];
-      std::memcpy(out.data() + o, blobs[r] + a, (size_t)(b - a));
-      o += (size_t)(b - a);
-      if (at[r] < counts[r]) pq.push({keys[r][at[r]], r});
-    }
+    if (counts[r] > 0) { total += counts[r]; ++live; only = r; }
+  if (live == 1) {                                  // one run: it is the merge, written from the blob
+    const size_t bytes = (size_t)ends[only][counts[only] - 1];
+    if (bytes && std::fwrite(blobs[only], 1, bytes, f) != bytes) { std::fclose(f); return -1; }
+    return std::fclose(f) == 0 ? total : -1;
   }
-  if (o && std::fwrite(out.data(), 1, o, f) != o) { std::fclose(f); return -1; }
-  if (std::fclose(f) != 0) return -1;
+  std::vector<char> out(kFlushBytes);
+  size_t o = 0;
+  bool ok = true;
+  auto put = [&](const char* p, size_t len) {
+    if (o + len > out.size()) {
+      if (o && std::fwrite(out.data(), 1, o, f) != o) ok = false;
+      o = 0;
+      if (len > out.size()) {                       // a line longer than the buffer: straight out
+        if (std::fwrite(p, 1, len, f) != len) ok = false;
+        return;
+      }
+    }
+    std::memcpy(out.data() + o, p, len);
+    o += len;
+  };
+  struct Head { double key; int run; };
+  auto worse = [](const Head& a, const Head& b) {        // priority: larger key, then lower run
+    return a.key < b.key || (a.key == b.key && a.run > b.run);
+  };
+  std::priority_queue<Head, std::vector<Head>, decltype(worse)> pq(worse);
+  std::vector<long> at(R, 0);
+  for (int r = 0; r < R; ++r)
+    if (counts[r] > 0) pq.push({keys[r][0], r});
+  while (!pq.empty() && ok) {
+    const Head h = pq.top();
+    pq.pop();
+    const int r = h.run;
+    const long i = at[r]++;
+    const long a = i ? ends[r][i - 1] : 0, b = ends[r][i];
+    put(blobs[r] + a, (size_t)(b - a));
+    if (at[r] < counts[r]) pq.push({keys[r][at[r]], r});
+  }
+  if (ok && o && std::fwrite(out.data(), 1, o, f) != o) ok = false;
+  if (std::fclose(f) != 0 || !ok) return -1;
   return total;
 }
 
@@ -270,29 +290,52 @@ SHIFU_RT_API long shifu_merge_runs(int R, const char* const* blobs, const long* 
 // their new end offsets to new_end (the rank-local ORDER BY before the k-way merge).
 SHIFU_RT_API long shifu_gather_lines(const char* blob, const long* ends, const long* order, long n,
                                      const char* out_path, long* new_end) {
-  // output offsets of the reordered lines (one O(n) pass), then the lines copied into one buffer
-  // by several threads and written with a single call: one fwrite per line was ~1-2 s at 20M
+  // output offsets of the reordered lines (one O(n) pass), then the lines copied by several threads
+  // into a fixed-size buffer, written whenever it fills (a window of lines per fill)
   long pos = 0;
   for (long i = 0; i < n; ++i) {
     const long j = order[i];
     pos += ends[j] - (j ? ends[j - 1] : 0);
     new_end[i] = pos;
   }
-  std::vector<char> out((size_t)pos);
-  const long T = std::max(1L, std::min<long>(16, n >> 16));
-  std::vector<std::thread> th;
-  for (long t = 0; t < T; ++t)
-    th.emplace_back([&, t]() {
-      for (long i = n * t / T, e = n * (t + 1) / T; i < e; ++i) {
-        const long j = order[i];
-        const long a = j ? ends[j - 1] : 0, b = ends[j];
-        std::memcpy(out.data() + (i ? new_end[i - 1] : 0), blob + a, (size_t)(b - a));
-      }
-    });
-  for (auto& x : th) x.join();
   FILE* f = std::fopen(out_path, "wb");
   if (!f) return -1;
-  if (pos && std::fwrite(out.data(), 1, (size_t)pos, f) != (size_t)pos) { std::fclose(f); return -1; }
+  std::vector<char> out(std::min<size_t>(kFlushBytes, (size_t)std::max(pos, 1L)));
+  long i0 = 0;
+  while (i0 < n) {
+    // the window [i0, i1): as many whole lines as fit (at least one)
+    const long base = i0 ? new_end[i0 - 1] : 0;
+    long i1 = i0 + 1;
+    {
+      long lo = i0 + 1, hi = n;                     // largest i1 with new_end[i1 - 1] - base <= size
+      while (lo <= hi) {
+        const long mid = lo + (hi - lo) / 2;
+        if (new_end[mid - 1] - base <= (long)out.size()) { i1 = mid; lo = mid + 1; } else hi = mid - 1;
+      }
+    }
+    const long wbytes = new_end[i1 - 1] - base;
+    if (wbytes > (long)out.size()) {                 // one line longer than the buffer
+      const long j = order[i0];
+      const long a = j ? ends[j - 1] : 0;
+      if (std::fwrite(blob + a, 1, (size_t)wbytes, f) != (size_t)wbytes) { std::fclose(f); return -1; }
+      i0 = i1;
+      continue;
+    }
+    const long cnt = i1 - i0;
+    const long T = std::max(1L, std::min<long>(16, cnt >> 16));
+    std::vector<std::thread> th;
+    for (long t = 0; t < T; ++t)
+      th.emplace_back([&, t]() {
+        for (long i = i0 + cnt * t / T, e = i0 + cnt * (t + 1) / T; i < e; ++i) {
+          const long j = order[i];
+          const long a = j ? ends[j - 1] : 0, b = ends[j];
+          std::memcpy(out.data() + ((i ? new_end[i - 1] : 0) - base), blob + a, (size_t)(b - a));
+        }
+      });
+    for (auto& x : th) x.join();
+    if (wbytes && std::fwrite(out.data(), 1, (size_t)wbytes, f) != (size_t)wbytes) { std::fclose(f); return -1; }
+    i0 = i1;
+  }
   if (std::fclose(f) != 0) return -1;
   return pos;
 }

@@ -198,6 +198,20 @@ def _poisson_from_uniform(u: np.ndarray, lam: float) -> np.ndarray:
     return k
 
 
+# Version of the train / validation / bagging draws stored in checkpoints: 2 = counter-based per
+# global row (row_uniform); 1 (absent) = the per-rank default_rng draws of rounds <= 4.  A resume
+# across versions keeps training but warns: rows may have moved between the two sets.
+SPLIT_SCHEME = 2
+
+
+def _check_split_scheme(st: dict, what: str) -> None:
+    v = int(st.get("split_scheme", 1)) if isinstance(st, dict) else 1
+    if v != SPLIT_SCHEME:
+        _log.warning("%s: checkpoint written with train/validation split scheme %d, resuming with scheme %d "
+                     "(counter-based per-row draws): some rows move between the training and the validation "
+                     "set", what, v, SPLIT_SCHEME)
+
+
 def split_masks(mc, ts: TrainSet, bag: int, n_kfold: int, seed: int):
     """-> (train_mask, valid_mask, sample_weight) for one bag (AbstractNNWorker :667-800).  Every
     per-row draw (validation split, bagging) is a counter-based function of the row's GLOBAL index
@@ -600,6 +614,7 @@ class TrainStep:
         if self.resume and os.path.exists(ckpt):
             st = torch.load(ckpt, weights_only=True)
             if st.get("spec_sizes") == [n_in] + spec.hidden + [n_out]:
+                _check_split_scheme(st, f"trainer {tid}")
                 tr.load_state_dict(st)
                 start = int(st["epoch"])
                 best_v = float(st.get("best_v", math.inf))
@@ -633,7 +648,7 @@ class TrainStep:
                     self._write_nn(tid, spec, tr, tmp_epoch=ep)
                     os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
                     sd = tr.state_dict()
-                    sd.update(epoch=ep, spec_sizes=[n_in] + spec.hidden + [n_out], best_v=best_v,
+                    sd.update(epoch=ep, spec_sizes=[n_in] + spec.hidden + [n_out], best_v=best_v, split_scheme=SPLIT_SCHEME,
                               best_w=None if best_w is None else best_w.cpu())
                     sd.pop("spec", None)
                     torch.save(sd, ckpt)
@@ -817,7 +832,10 @@ class TrainStep:
                 stop[0] = True
         ckpt = os.path.join(ms.pf.checkpoint_dir, f"tree_trainer{tid}.pt")
         if self.resume and os.path.exists(ckpt):
-            tt.load_state_dict(torch.load(ckpt, weights_only=True))
+            st = torch.load(ckpt, weights_only=True)
+            _check_split_scheme(st, f"trainer {tid}")
+            st.pop("split_scheme", None)
+            tt.load_state_dict(st)
             _log.info("resumed trainer %d from checkpoint with %d trees", tid, len(tt.trees))
         else:
             existing = self._continuous_trees(tid, cfg)
@@ -835,7 +853,7 @@ class TrainStep:
                 check_finite("training error", tt.train_errors[-1], n)
                 if self.info.rank == 0 and n % interval == 0 and n < tree_num:
                     os.makedirs(ms.pf.checkpoint_dir, exist_ok=True)
-                    torch.save(tt.state_dict(), ckpt)
+                    torch.save({**tt.state_dict(), "split_scheme": SPLIT_SCHEME}, ckpt)
                 maybe_fault(n, self.info.rank)
                 if stop[0]:
                     break

@@ -155,3 +155,50 @@ def test_streamed_eval_host_memory_bounded_by_chunk(tmp_path, monkeypatch):
           % (s_small / 1e6, s_big / 1e6, m_big / 1e6))
     assert s_big - s_small < 30e6, (s_small, s_big, m_big)   # 600K more rows: +17 B/row metric columns
     assert m_big - s_big > 20e6, (s_small, s_big, m_big)     # the in-memory eval grows with the data
+
+
+def test_gather_and_merge_with_small_flush_buffer(tmp_path):
+    """shifu_gather_lines / shifu_merge_runs stage their output in a fixed-size buffer flushed when
+    full (bounded memory on the merging rank): with a 100-byte buffer the files equal the ones
+    written with the default 256-MB buffer."""
+    import ctypes
+    from shifu_amd.ops import _native
+    lib = _native.rt()
+    g = np.random.default_rng(0)
+    runs = []
+    for r in range(3):
+        n = 400 + 50 * r
+        key = np.round(g.random(n), 4)
+        lines = [("%d|%s|%.4f\n" % (r, "y" * int(g.integers(0, 300)), v)).encode() for v in key]
+        blob = np.frombuffer(b"".join(lines), dtype=np.uint8).copy()
+        ends = np.cumsum([len(l) for l in lines]).astype(np.int64)
+        runs.append((blob, ends, key))
+
+    def write(flush, tag):
+        lib.shifu_eval_set_flush_bytes(flush)
+        sorted_runs = []
+        for i, (blob, ends, key) in enumerate(runs):
+            order = np.argsort(-key, kind="stable").astype(np.int64)
+            new_end = np.zeros(len(key), np.int64)
+            out = str(tmp_path / f"{tag}_s{i}.bin")
+            assert lib.shifu_gather_lines(blob.ctypes.data, ends.ctypes.data, order.ctypes.data, len(key),
+                                          out.encode(), new_end.ctypes.data) == ends[-1]
+            sorted_runs.append((np.fromfile(out, dtype=np.uint8), new_end, np.ascontiguousarray(key[order])))
+        path = str(tmp_path / f"{tag}_merged")
+        open(path, "w").close()
+        R = len(sorted_runs)
+        assert lib.shifu_merge_runs(R, (ctypes.c_void_p * R)(*[b.ctypes.data for b, _, _ in sorted_runs]),
+                                    (ctypes.c_void_p * R)(*[e.ctypes.data for _, e, _ in sorted_runs]),
+                                    (ctypes.c_void_p * R)(*[k.ctypes.data for _, _, k in sorted_runs]),
+                                    (ctypes.c_long * R)(*[len(k) for _, _, k in sorted_runs]),
+                                    path.encode()) == sum(len(k) for _, _, k in sorted_runs)
+        return [open(str(tmp_path / f"{tag}_s{i}.bin"), "rb").read() for i in range(R)], open(path, "rb").read()
+    try:
+        big = write(256 << 20, "big")
+        small = write(100, "small")
+    finally:
+        lib.shifu_eval_set_flush_bytes(256 << 20)
+    assert small == big
+    merged = big[1].decode().strip().split("\n")
+    keys = [float(l.rsplit("|", 1)[1]) for l in merged]
+    assert len(merged) == 1350 and keys == sorted(keys, reverse=True)

@@ -169,7 +169,7 @@ def test_ring_forward_matches_8phase_and_oracle(M, K, N, NB, nv, epi, act):
 
 def test_bench_configuration_tracks_fp32_oracle():
     """The exact bench trainer configuration (bench.py: n_in 1000, hidden 500/200 sigmoid, RPROP,
-    chunks >= 2^17 rows) so the 8-phase forward, the fused head, the ring wgrad (incl. the M % 32
+    chunks >= 2^17 rows) so the persistent ring forward, the fused head, the ring wgrad (incl. the M % 32
     tail) and dgrad all run, for 8 full-batch epochs against the fp32 torch oracle on the same
     bf16-rounded rows and weights: the training-error trajectory agrees within 1e-2 relative and
     the final weights stay close."""
@@ -279,7 +279,7 @@ def test_two_chunk_lanes_match_one_lane(monkeypatch):
 
 
 def test_bench_configuration_gradient_bitwise_reproducible():
-    """The bench trainer path (8-phase forward, fused head, ring wgrad, dgrad; full chunks) gives
+    """The bench trainer path (ring forward, fused head, ring wgrad, dgrad; full chunks) gives
     bit-identical gradients run to run: the head's output-layer wgrad goes through per-tile
     partials + a fixed-order reduction (colsum_fixed) instead of float atomics."""
     spec = MLPSpec(n_in=1000, hidden=[500, 200], acts=["sigmoid", "sigmoid"], n_out=1)

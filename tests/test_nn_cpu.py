@@ -151,3 +151,15 @@ def test_activation_derivatives(act):
     mask = z.detach().abs() > 1e-3   # kinks at 0
     assert torch.allclose(d[mask], z.grad[mask], atol=1e-6)
     assert flat_spot(act) == (0.1 if act == "sigmoid" else 0.0)
+
+
+def test_lr_input_dtype_option():
+    """shifu.lr.inputDtype: auto / fp32 / bf16 (bf16 rows only on the GPU); anything else fails."""
+    import pytest
+    import torch
+    from shifu_amd.models.lr import LRTrainer
+    t = LRTrainer(5, device="cpu", input_dtype="bf16")
+    x, y, s = t.prepare(torch.randn(10, 5), torch.zeros(10))
+    assert x.dtype == torch.float32 and t.input_dtype == "fp32"
+    with pytest.raises(ValueError):
+        LRTrainer(5, device="cpu", input_dtype="fp16")

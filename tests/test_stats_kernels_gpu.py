@@ -113,9 +113,12 @@ def test_lr_step_above_k9_limit_on_own_dot_kernels(dtype, F):
     errs = {}
     ws = {}
     for dev in ("cpu", "cuda"):
-        t = LRTrainer(F, device=dev, propagation="R")
+        t = LRTrainer(F, device=dev, propagation="R", input_dtype="bf16" if dtype == torch.bfloat16 else "auto")
         t.w.copy_((torch.randn(F + 1, generator=torch.Generator().manual_seed(3)) * 0.02).to(dev))
         data = t.prepare(x, y) if hasattr(t, "prepare") else None
+        # the row dtype is explicit: fp32 unless bf16 is asked for (or fp32 rows do not fit in HBM)
+        want = "bf16" if (dev == "cuda" and dtype == torch.bfloat16) else "fp32"
+        assert t.input_dtype == want and data[0].dtype == (torch.bfloat16 if want == "bf16" else torch.float32)
         errs[dev] = [t.step(data) for _ in range(3)]
         ws[dev] = t.w.cpu()
     for a, b in zip(errs["cpu"], errs["cuda"]):

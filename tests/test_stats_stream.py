@@ -293,3 +293,21 @@ def test_posttrain_streamed_gpu_equals_in_memory(tmp_path, monkeypatch):
     """On the GPU (GPU-parsed inputs binned in HBM): streamed posttrain == the in-memory pass."""
     ca, cb = _posttrain_pair(tmp_path, monkeypatch, "cuda")
     assert ca == cb
+
+
+def test_pinned_blocks_stay_below_the_device_parse_limit(tmp_path, monkeypatch):
+    """Blocks read for the GPU parse (pinned) are carry + read bytes: the read is capped so every
+    block stays below the parser's int32 limit (a block at or above it would fall back to a host
+    parse).  The limit is scaled down here; chunk_bytes equals it, as with 2-GB chunks."""
+    from shifu_amd.data import gpu_parse, stream
+    monkeypatch.setattr(gpu_parse, "BLOCK_LIMIT", 5000)
+    monkeypatch.setattr(stream, "_new_buf", lambda n, pinned: bytearray(n))
+    lines = [("%d|%s|%.3f\n" % (i, "x" * (i % 23), i * 0.37)).encode() for i in range(6000)]
+    path = tmp_path / "t.csv"
+    path.write_bytes(b"".join(lines))
+    got = []
+    for off, blk in stream._lines_in_range(str(path), 0, path.stat().st_size, 5000, nbuf=2, pinned=True):
+        assert len(blk) < 5000
+        got.append(bytes(blk))
+    assert b"".join(got) == path.read_bytes()
+    assert len(got) > 20
