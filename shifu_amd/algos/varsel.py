@@ -199,7 +199,15 @@ def first_layer_fp32(xb: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor, fl_ca
     fl_cache = {} if fl_cache is None else fl_cache
     if fl_cache.get("sw") is None:
         fl_cache["sw"] = SplitWeights(W1, b1, terms=6)
-    return linear_fp32(xb, W1, b1, sw=fl_cache["sw"])
+    sw = fl_cache["sw"]
+    # the split operand is 6 x K bf16 per row (~120 KB at 10k inputs): at most ~4 GB of it at once
+    step = max(4096, (4 << 30) // (sw.kp * 2))
+    if xb.shape[0] <= step:
+        return linear_fp32(xb, W1, b1, sw=sw)
+    out = torch.empty(xb.shape[0], sw.N, dtype=torch.float32, device=xb.device)
+    for r0 in range(0, xb.shape[0], step):
+        out[r0: r0 + step] = linear_fp32(xb[r0: r0 + step], W1, b1, sw=sw)
+    return out
 
 
 def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, row_chunk: int = 1 << 16,
@@ -238,8 +246,10 @@ def sensitivity(network, X, y=None, w=None, device=None, feat_chunk: int = 64, r
         """device fp32 [m, F] row blocks (HostRows: pinned staging + H2D on a copy stream)."""
         if isinstance(X, HostRows):
             k0 = ((F + 1 + 127) // 128) * 128
+            sub = max(4096, min(rc, (8 << 30) // (4 * F)))     # fp32 blocks of <= ~8 GB
             for _, _, xd in X.chunks(0, n_rows, rc, k0, dev):
-                yield xd[:, :F].float()
+                for s0 in range(0, xd.shape[0], sub):
+                    yield xd[s0: s0 + sub, :F].float()
             return
         for r0 in range(0, n_rows, rc):
             xb = X[r0: r0 + rc]

@@ -69,6 +69,8 @@ HIP_SIGNATURES = {
     "shifu_ring_set_stamp": "p",
     "shifu_ring_nt_set_lab": "ip",
     "shifu_ring_nt_set_variant": "i",
+    "shifu_strip_nt": "plplipl" "iii" "iiiii" "s",
+    "shifu_strip_nt_set_lab": "i",
     "shifu_ring_set_mf": "i",
     "shifu_ring_set_dmamma": "i",
     # gbdt_kernels.hip

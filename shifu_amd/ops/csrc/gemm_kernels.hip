@@ -917,16 +917,21 @@ static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
 static int g_ring_nt = 1;         // persistent ring forward (gemm_ring_nt.hip, tune key 12; 2.2 vs 2.3-2.5 ms
                                   // for the 8-phase per-tile kernel per 2M-row chunk, profiles/r5)
 static int g_ring_nt_cap = 0;     // lab: grid cap of the ring forward (tune key 13; 0 = one block per CU)
+static int g_strip_nt = 0;        // row-strip forward engine (gemm_strip_nt.hip, tune key 14): 1 = before the ring
 // gemm_ring_nt.hip (same library): -1 when the shape is not one it takes
 extern "C" int shifu_ring_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc, int M,
                              int N, int K, int epi, int act, int n_valid, int bias_col, int grid_cap,
                              hipStream_t stream);
+extern "C" int shifu_strip_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc, int M,
+                              int N, int K, int epi, int act, int n_valid, int bias_col, int grid_cap,
+                              hipStream_t stream);
 SHIFU_API int shifu_gemm_set_stages(int s) { g_stages = (s == 2) ? 2 : 1; return 0; }
 SHIFU_API int shifu_gemm_set_tune(int key, int val) {
   if (key == 2) { g_wg_interleave = val; return 0; }
   if (key == 9) { g_dbg = val; return 0; }
   if (key == 12) { g_ring_nt = val; return 0; }
   if (key == 13) { g_ring_nt_cap = val; return 0; }
+  if (key == 14) { g_strip_nt = val; return 0; }
   return -1;
 }
 SHIFU_API int shifu_gemm_set_big(int b) { g_big = (b == 3 || b == 4) ? b : 0; return 0; }
@@ -957,6 +962,11 @@ SHIFU_API int shifu_gemm_nt(const void* A, long lda, const void* B, long ldb, in
   // (H row segments loaded into registers after the tile's last MMA segment) measured 1.81 vs
   // 1.23 ms per 2M-row chunk (profiles/r5/NOTES_r5.md) -- with K = 256 a tile has 8 k-steps, and
   // the H round trip at every tile end is exposed.
+  if (g_strip_nt && M >= 65536 && (epi == EPI_STORE || (epi == EPI_ACT && dfo_act)) && !g_dbg) {
+    const int r = shifu_strip_nt(A, lda, B, ldb, NB, C, ldc, M, N, K, epi, act, n_valid, bias_col, g_ring_nt_cap,
+                                 stream);
+    if (r != -1) return r;          // -1: shape not taken, fall through
+  }
   if (g_ring_nt && M >= 65536 && (epi == EPI_STORE || (epi == EPI_ACT && dfo_act)) && !g_dbg) {
     const int r = shifu_ring_nt(A, lda, B, ldb, NB, C, ldc, M, N, K, epi, act, n_valid, bias_col, g_ring_nt_cap,
                                 stream);

@@ -5,6 +5,7 @@ import torch
 from shifu_amd.models.nn import MLPSpec, MLPTrainer, TrainData
 
 pytestmark = pytest.mark.gpu
+STRIP_DEFAULT = 0          # gemm_kernels.hip g_strip_nt (tune key 14) as built
 
 
 def _mk(spec, n, seed=0, loss="squared"):
@@ -165,6 +166,43 @@ def test_ring_forward_matches_8phase_and_oracle(M, K, N, NB, nv, epi, act):
         assert torch.equal(old.view(torch.int16), new.view(torch.int16))
     else:
         assert (old.float() - new.float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("M,K,N,NB,nv,act", [
+    ((1 << 21), 1024, 512, 500, 500, 0),               # the bench's first layer (sigmoid + bias column)
+    ((1 << 20) + 77, 1024, 512, 500, 500, 0),           # a partial last row tile
+    (70000 + 33, 256, 512, 512, 512, 3),                # K = 4 steps per tile, relu, no partial columns
+    (65536 + 300, 128, 264, 260, 260, 0),               # partial last column tile (N % 256 != 0)
+    (65536, 384, 384, 256, 256, 2),                     # a column tile entirely past the weight rows
+    (131072, 512, 1024, 1000, 1000, 7),                 # four column tiles, log activation
+])
+def test_strip_forward_bitwise_equals_ring(M, K, N, NB, nv, act):
+    """The row-strip forward (gemm_strip_nt.hip, tune key 14: A fragments global -> VGPR, B by
+    LDS-DMA in 64-deep k-steps) against the ring engine: the same k order per accumulator, so the
+    outputs are identical bits, rows >= M untouched."""
+    from shifu_amd.ops import _native as nat
+    g = torch.Generator(device="cuda").manual_seed(M % 89)
+    A = (torch.randn(M + 64, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    B = (torch.randn(NB, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    outs = []
+    for strip in (0, 1):
+        C = torch.full((M + 64, N), 7.0, device="cuda", dtype=torch.bfloat16)
+        nat.call_hip("shifu_gemm_set_tune", 14, strip)
+        try:
+            nat.call_hip("shifu_gemm_nt", A, K, B, K, NB, C, N, None, 0, None, 0, None, 0,
+                         M, N, K, 0, act, nv, 1, 0.0, nat.stream_of(A))
+            torch.cuda.synchronize()
+        finally:
+            nat.call_hip("shifu_gemm_set_tune", 14, STRIP_DEFAULT)
+        outs.append(C)
+    ring, strip = outs
+    assert torch.all(strip[M:] == 7.0), "rows >= M written"
+    if act in (0, 2, 3):
+        assert torch.equal(ring.view(torch.int16), strip.view(torch.int16))
+    else:       # __logf / v_log_f32 codegen may differ by an fp32 ulp between the two kernels
+        d = (ring.float() - strip.float()).abs()
+        assert float(d.max()) <= 2 ** -7 * max(1.0, float(ring.float().abs().max()))
+        assert int((d > 0).sum()) < 1e-3 * d.numel()
 
 
 def test_bench_configuration_tracks_fp32_oracle():
