@@ -917,7 +917,7 @@ static int g_dbg = 0;             // lab ablation bits (GemmArgs::dbg)
 static int g_ring_nt = 1;         // persistent ring forward (gemm_ring_nt.hip, tune key 12; 2.2 vs 2.3-2.5 ms
                                   // for the 8-phase per-tile kernel per 2M-row chunk, profiles/r5)
 static int g_ring_nt_cap = 0;     // lab: grid cap of the ring forward (tune key 13; 0 = one block per CU)
-static int g_strip_nt = 0;        // row-strip forward engine (gemm_strip_nt.hip, tune key 14): 1 = before the ring
+static int g_strip_nt = 1;        // row-strip forward engine (gemm_strip_nt.hip, tune key 14): 1 = before the ring
 // gemm_ring_nt.hip (same library): -1 when the shape is not one it takes
 extern "C" int shifu_ring_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc, int M,
                              int N, int K, int epi, int act, int n_valid, int bias_col, int grid_cap,

@@ -13,10 +13,10 @@
 //   * wave w of the 512-thread block owns the 32-row strip [32w, 32w + 32) of the 256-row tile and
 //     all 256 columns, so no other wave needs its A rows: each lane loads its A fragments global ->
 //     VGPR (4 global_load_dwordx4 per k-step: two m-blocks x the two 32-deep halves, the halves of a
-//     row issued back to back = one whole line), SN_P k-steps ahead into a register ring;
+//     row issued back to back = one whole line), 2 k-steps ahead into a 2-entry register ring;
 //   * only the B tile (256 weight rows x 128 B = 32 KiB per k-step, shared by the 8 waves) goes
-//     through LDS: 32 LDS-DMA pieces of 8 rows x 128 B per k-step, 4 per wave, into a 5-slot ring
-//     running SN_P k-steps ahead across tile boundaries (the (tile, k-step) sequence is flattened);
+//     through LDS: 32 LDS-DMA pieces of 8 rows x 128 B per k-step, 4 per wave, into a 4-slot ring
+//     running 2 k-steps ahead across tile boundaries (the (tile, k-step) sequence is flattened);
 //     16-B chunk c of row r sits at c ^ ((r >> 1) & 7): every ds_read_b128 lane group hits 16
 //     distinct bank slots;
 //   * per k-step 32 B fragments are read (eight double-buffered groups of 4) and feed 64 x
@@ -29,16 +29,16 @@
 // Numerics: every accumulator adds its 32-deep halves in ascending k order, like the ring and the
 // 8-phase kernels, so the outputs are bitwise identical to theirs.
 //
-// Schedule per wave (P = SN_P = 3, step t of the flattened sequence padded to a multiple of P,
-// e = t mod P; padded steps only load):
-//   prologue: groups 0 .. P-1 (DMA x4, A x4 each); vmcnt(8(P-1)); barrier
-//   step t:   B fragment groups / MFMAs from slot t mod (P+2) with A ring entry e;
-//             group t+P: DMA x4 into slot (t+P) mod (P+2), A x4 into ring entry e;
+// Schedule per wave (D = 2 steps ahead, A ring of 2 entries; e = t mod 2):
+//   prologue: groups 0, 1 (DMA x4, A x4 each); vmcnt(8); barrier
+//   step t:   8 MMA groups (B fragments from slot t mod 4, A ring entry e);
+//             group t+2: DMA x4 into slot (t+2) mod 4, A x4 into ring entry e;
 //             [last k-step of a tile: epilogue, 16 stores];
-//             vmcnt(8(P-1)) (+16 in the P steps after an epilogue) -> own group t+1 landed; barrier
+//             vmcnt(8) (24 in the 2 steps after an epilogue) -> own group t+1 landed; barrier
 // RAW: a wave's own pieces of step t+1 landed before the barrier that precedes every wave's reads
-// of that slot.  WAR: slot (t+P) mod (P+2) was last read in step t-2, whose reads were waited for
-// (lgkmcnt(0)) before the barrier that ended it.
+// of that slot.  WAR: slot (t+2) mod 4 was last read in step t-2, behind the barrier that ended
+// step t-1.  (Issuing step t+2's loads between the MMA groups, with a 3-entry ring, measured the
+// same: 2.19 ms vs 2.18-2.20, strip_lab_d.)
 #include "common.h"
 #include <type_traits>
 #include <utility>
@@ -49,10 +49,11 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((ext_vector_type(4))) int v4i_t;
 
 constexpr int SN_T = 512;
-constexpr int SN_P = 3;                      // k-steps in flight (A ring entries, B slots ahead)
-constexpr int SN_NSLOT = SN_P + 2;           // + the slot being read + the one landed / waiting
+constexpr int SN_D = 2;                      // k-steps ahead: step t issues the loads of step t+D
+constexpr int SN_P = SN_D;                   // A ring entries = unroll (entry t mod 2 reloaded after use)
+constexpr int SN_NSLOT = SN_D + 2;           // B slots: + the slot being read + the one landed
 constexpr int SN_SLOT = 256 * 128;           // 32 KiB: B image [256 rows][64 bf16]
-constexpr int SN_LDS = SN_NSLOT * SN_SLOT;   // 160 KiB
+constexpr int SN_LDS = SN_NSLOT * SN_SLOT;   // 128 KiB
 enum { SN_EPI_ACT = 0, SN_EPI_STORE = 2 };   // same codes as gemm_kernels.hip's Epi
 
 __device__ __forceinline__ int sn_xcd_remap(int bid, int nwg) {
@@ -66,11 +67,11 @@ __device__ __forceinline__ bf16x8 sn_read(uint32_t a) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
   return v;
 }
+// "+v": the load's destination is tied to the ring entry's current register (the entry is
+// overwritten in place; hipcc has no new value to place elsewhere)
 template <int OFF>
-__device__ __forceinline__ bf16x8 sn_gload(const void* p) {
-  bf16x8 v;
-  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(v) : "v"(p), "n"(OFF) : "memory");
-  return v;
+__device__ __forceinline__ void sn_gload(bf16x8& v, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "+v"(v) : "v"(p), "n"(OFF) : "memory");
 }
 
 template <int I> struct SnIC { static constexpr int v = I; };
@@ -97,7 +98,6 @@ __global__ __launch_bounds__(SN_T, 2) void strip_nt_kernel(StripArgs p) {
   const int ntn = (p.N + 255) >> 8;
   const int nk = p.K >> 6;
   const int T = ((p.ntiles - 1 - lb) / G + 1) * nk;  // flattened k-steps of this block
-  const int TP = (T + SN_P - 1) / SN_P * SN_P;       // padded to the unroll: the tail steps only load
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   const int lr = lane & 15, lq = lane >> 4;
@@ -122,23 +122,28 @@ __global__ __launch_bounds__(SN_T, 2) void strip_nt_kernel(StripArgs p) {
     }
   };
   cursor_tile(c_tile);
-  // issue the loads of the cursor's step: 4 DMA pieces into `slot`, 4 A fragments into a[mb][h]
-  auto issue = [&](int slot, bf16x8 (&a)[2][2]) __attribute__((always_inline)) {
-    const int ko = c_k * 128;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      char* dst = smem + slot * SN_SLOT + (wid_u * 4 + i) * 1024;
-      __builtin_amdgcn_global_load_lds((const void*)(bptr[i] + ko), (lds_ptr_t)dst, 16, 0, 0);
-    }
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {               // the two halves of each row line back to back
-      a[mb][0] = sn_gload<0>(aptr[mb] + ko);
-      a[mb][1] = sn_gload<64>(aptr[mb] + ko);
-    }
+  // the loads of the cursor's step: 4 DMA pieces into `slot`, 4 A fragments into a[mb][h] (the
+  // two halves of a row's line back to back); advance() moves the cursor on afterwards
+  auto issue_dma = [&](int slot, int i) __attribute__((always_inline)) {
+    char* dst = smem + slot * SN_SLOT + (wid_u * 4 + i) * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)(bptr[i] + c_k * 128), (lds_ptr_t)dst, 16, 0, 0);
+  };
+  auto issue_a = [&](bf16x8 (&a)[2][2], int mb) __attribute__((always_inline)) {
+    sn_gload<0>(a[mb][0], aptr[mb] + c_k * 128);
+    sn_gload<64>(a[mb][1], aptr[mb] + c_k * 128);
+  };
+  auto advance = [&]() __attribute__((always_inline)) {
     if (c_left > 0) {                                // past the end: re-issue the last step
       --c_left;
       if (++c_k == nk) { c_k = 0; c_tile += G; cursor_tile(c_tile); }
     }
+  };
+  auto issue = [&](int slot, bf16x8 (&a)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) issue_dma(slot, i);
+    issue_a(a, 0);
+    issue_a(a, 1);
+    advance();
   };
 
   f32x4 acc[16][2];                                  // [n block of 16][m block of 16]
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(SN_T, 2) void strip_nt_kernel(StripArgs p) {
   for (int i = 0; i < 16; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ar[SN_P][2][2];                             // A register ring [entry][m block][k half]
+  bf16x8 ar[SN_P][2][2] = {};                        // A register ring [entry][m block][k half]
 
   const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   const int sx = (lr >> 1) & 7;                      // the row swizzle of this lane's fragment rows
@@ -218,12 +223,23 @@ __global__ __launch_bounds__(SN_T, 2) void strip_nt_kernel(StripArgs p) {
 
 #define SN_BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
                       __builtin_amdgcn_sched_barrier(0); } while (0)
-#define SN_WAIT_A(N, E) asm volatile("s_waitcnt vmcnt(" #N ")" : "+v"(ar[E][0][0]), "+v"(ar[E][0][1]), \
-                                     "+v"(ar[E][1][0]), "+v"(ar[E][1][1]) :: "memory")
+  // Every vmcnt wait names EVERY A ring register ("+v"): an asm load's destination counts as
+  // written at the asm statement, so a loaded value that no later statement reads (the last
+  // re-issued steps past the end of the sequence) would be dead to hipcc and its registers handed
+  // to other values while the data is still in flight -- the late write then corrupts them (seen as
+  // rare wrong last tiles before this).  Named here, each ring entry stays live and in place from
+  // its load to the wait that retires it.
+#define SN_WAIT_A(N, E) asm volatile("s_waitcnt vmcnt(" #N ")" \
+    : "+v"(ar[0][0][0]), "+v"(ar[0][0][1]), "+v"(ar[0][1][0]), "+v"(ar[0][1][1]), \
+      "+v"(ar[1][0][0]), "+v"(ar[1][0][1]), "+v"(ar[1][1][0]), "+v"(ar[1][1][1]) :: "memory")
+#define SN_KEEP_A() asm volatile("" \
+    : "+v"(ar[0][0][0]), "+v"(ar[0][0][1]), "+v"(ar[0][1][0]), "+v"(ar[0][1][1]), \
+      "+v"(ar[1][0][0]), "+v"(ar[1][0][1]), "+v"(ar[1][1][0]), "+v"(ar[1][1][1]) :: "memory")
+  static_assert(SN_P == 2, "SN_WAIT_A names a 2-entry ring");
 
-  // prologue: steps 0 .. P-1 in flight
-  sn_for<SN_P>([&](auto I) { issue(I.v, ar[I.v]); });
-  SN_WAIT_A(16, 0);
+  // prologue: steps 0 .. D-1 in flight
+  sn_for<SN_D>([&](auto I) { issue(I.v, ar[I.v]); });
+  SN_WAIT_A(8, 0);
   SN_BAR();
 
   // B fragments of n blocks 2g, 2g+1 (both k halves) x the wave's A fragments: 8 MFMAs, k ascending
@@ -251,64 +267,70 @@ __global__ __launch_bounds__(SN_T, 2) void strip_nt_kernel(StripArgs p) {
   };
 #define SN_WAIT_B(N, b) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) \
                                      :: "memory")
-  int kk = 0, tile = lb, since_epi = 0, rslot = 0, dslot = SN_P;
-  for (int t0 = 0; t0 < TP; t0 += SN_P) {
+  int kk = 0, tile = lb, since_epi = 0, rslot = 0, dslot = SN_D;
+  for (int t0 = 0; t0 < T; t0 += SN_P) {          // T is a multiple of 2 (K % 128 == 0)
     sn_for<SN_P>([&](auto E) {
       constexpr int e = E.v;
       const int t = t0 + e;
       const uint32_t sb = lds0 + (uint32_t)(rslot * SN_SLOT);
-      const bool live = t < T;                       // wave-uniform: padded tail steps only load
       bf16x8 b0[4], b1[4];
-      if (live) {
-      read_group(b0, sb, SnIC<0>{});
-      read_group(b1, sb, SnIC<1>{});
-      __builtin_amdgcn_s_setprio(1);
-      sn_for<8>([&](auto Gi) {
-        constexpr int g = Gi.v;
-        if constexpr ((g & 1) == 0) {
-          if constexpr (g < 7) SN_WAIT_B(4, b0); else SN_WAIT_B(0, b0);
-          __builtin_amdgcn_sched_barrier(0);
-          mma(b0, g, ar[e]);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (g + 2 < 8) read_group(b0, sb, SnIC<g + 2>{});
-        } else {
-          if constexpr (g < 7) SN_WAIT_B(4, b1); else SN_WAIT_B(0, b1);
-          __builtin_amdgcn_sched_barrier(0);
-          mma(b1, g, ar[e]);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (g + 2 < 8) read_group(b1, sb, SnIC<g + 2>{});
-        }
-      });
-      __builtin_amdgcn_s_setprio(0);
+      {
+        read_group(b0, sb, SnIC<0>{});
+        read_group(b1, sb, SnIC<1>{});
+        __builtin_amdgcn_s_setprio(1);
+        sn_for<8>([&](auto Gi) {
+          constexpr int g = Gi.v;
+          if constexpr ((g & 1) == 0) {
+            if constexpr (g < 7) SN_WAIT_B(4, b0); else SN_WAIT_B(0, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(b0, g, ar[e]);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g + 2 < 8) read_group(b0, sb, SnIC<g + 2>{});
+          } else {
+            if constexpr (g < 7) SN_WAIT_B(4, b1); else SN_WAIT_B(0, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(b1, g, ar[e]);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g + 2 < 8) read_group(b1, sb, SnIC<g + 2>{});
+          }
+        });
+        __builtin_amdgcn_s_setprio(0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      // group t+P: B pieces into slot (t+P) mod (P+2) (last read in step t-2), A into ring entry e
+      // the loads of step t+2: B pieces into slot (t+2) mod 4 (last read in step t-2), A into the
+      // ring entry e this step's MFMAs have just read
       issue(dslot, ar[e]);
+      __builtin_amdgcn_sched_barrier(0);
       rslot = rslot == SN_NSLOT - 1 ? 0 : rslot + 1;
       dslot = dslot == SN_NSLOT - 1 ? 0 : dslot + 1;
       __builtin_amdgcn_sched_barrier(0);
-      if (live && ++kk == nk) {
+      if (++kk == nk) {
         kk = 0;
         epilogue(tile);
         tile += G;
-        since_epi = SN_P;
+        since_epi = SN_D;
         __builtin_amdgcn_sched_barrier(0);
       }
-      // own group t+1 landed (A ring entry (e+1) mod P, B pieces of slot t+1); younger: groups
-      // t+2 .. t+P (+16 epilogue stores in the P steps after a tile end)
-      constexpr int en = (e + 1) % SN_P;
+      // own group t+1 landed (A ring entry (e+1) mod P, B pieces of slot t+1); younger: group
+      // t+2 (+16 epilogue stores in the D steps after a tile end).  The waits carry no operands;
+      // the statement naming the ring registers sits after the join: "+v" operands on waits in
+      // two arms made hipcc give each arm its own register assignment and copy the in-flight ring
+      // between them.  (A CFG audit of this reports the MFMAs after the join on the infeasible
+      // path "since_epi > 0 without an epilogue"; tools/asm_vmcnt_audit.py --copies checks the rest.)
       if (since_epi > 0) {
         --since_epi;
-        SN_WAIT_A(32, en);
+        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
       } else {
-        SN_WAIT_A(16, en);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       }
+      SN_KEEP_A();
       SN_BAR();
     });
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  SN_WAIT_A(0, 0);                                   // the trailing loads land before the exit
 #undef SN_WAIT_B
 #undef SN_WAIT_A
+#undef SN_KEEP_A
 #undef SN_BAR
 }
 
@@ -322,7 +344,7 @@ SHIFU_API int shifu_strip_nt_set_lab(int dbg) { g_sn_dbg = dbg; return 0; }
 SHIFU_API int shifu_strip_nt(const void* A, long lda, const void* B, long ldb, int NB, void* C, long ldc, int M,
                              int N, int K, int epi, int act, int n_valid, int bias_col, int grid_cap,
                              hipStream_t stream) {
-  if (K % 64 || K < 128 || lda % 8 || ldb % 8 || ldc % 8 || N % 8 || M <= 0 || N <= 0 || NB <= 0) return -1;
+  if (K % 128 || K < 128 || lda % 8 || ldb % 8 || ldc % 8 || N % 8 || M <= 0 || N <= 0 || NB <= 0) return -1;
   if (epi != SN_EPI_ACT) return -1;                  // the store-z and tanh builds spill VGPRs: the A ring
   if (act == 1) return -1;                           // lives in asm-loaded registers, so those stay on the ring
   if (epi == SN_EPI_ACT && !act_deriv_from_output(act)) return -1;

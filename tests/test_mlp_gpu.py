@@ -5,7 +5,7 @@ import torch
 from shifu_amd.models.nn import MLPSpec, MLPTrainer, TrainData
 
 pytestmark = pytest.mark.gpu
-STRIP_DEFAULT = 0          # gemm_kernels.hip g_strip_nt (tune key 14) as built
+STRIP_DEFAULT = 1          # gemm_kernels.hip g_strip_nt (tune key 14) as built
 
 
 def _mk(spec, n, seed=0, loss="squared"):
