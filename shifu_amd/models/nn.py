@@ -534,6 +534,7 @@ class MLPTrainer:
         # bitwise reproducible); SHIFU_WGRAD_RING=0 restores the 128x128 split-K atomics kernel
         self.wgrad_ring = os.environ.get("SHIFU_WGRAD_RING", "1") != "0"
         self.fused_head = self._head_eligible()
+        self.strip_head = self.fused_head and self._strip_head_eligible()
         self.err_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
         # dropout (NNMaster.dropoutNodes :531-556, FloatFlatNetwork.computeLayer :205-215): each
         # iteration drops hidden nodes with DropoutRate and inputs with 0.4*DropoutRate and scales
@@ -603,7 +604,7 @@ class MLPTrainer:
         # replacement of the per-tile atomics, ops/csrc/gemm_kernels.hip colsum_fixed)
         ws["gw_slab"] = ws["gw_part"] = ws["err_slab"] = None
         if self.gpu and self.fused_head:
-            tiles = -(-rows // 256)
+            tiles = max(-(-rows // 256), 8 * 256 if self.strip_head else 0)   # strip head: grid x 8 waves
             ws["gw_slab"] = torch.empty(tiles * kp[L], dtype=torch.float32, device=self.device)
             ws["err_slab"] = torch.empty(tiles * 2, dtype=torch.float64, device=self.device)
             ws["gw_part"] = torch.empty(-(-tiles // 128) * kp[L], dtype=torch.float32, device=self.device)
@@ -722,6 +723,21 @@ class MLPTrainer:
         return bool(sp.n_out == 1 and sp.layer_kpad[L] <= 256 and a in ACT_DERIV_FROM_OUTPUT and
                     sp.acts[L - 1] != "ptanh" and sp.hidden[L - 1] <= 255)
 
+    def _strip_head_eligible(self) -> bool:
+        """Fused head + the layer-below dgrad in one persistent kernel (gemm_strip_head.hip): the
+        head layer's deltas stay in registers as the dgrad's MFMA operand.  Needs >= 2 hidden
+        layers, the head layer padded to 256 (128 < width + 1 <= 256), the layer below padded to
+        256 or 512, and the same activation on both layers (one instantiation per activation).
+        SHIFU_STRIP_HEAD=0 keeps the separate head + dgrad kernels."""
+        sp = self.spec
+        L = len(sp.hidden)
+        if L < 2 or os.environ.get("SHIFU_STRIP_HEAD", "1") == "0":
+            return False
+        kp = sp.layer_kpad
+        a2, a1 = sp.acts[L - 1], sp.acts[L - 2]
+        return bool(kp[L] == 256 and kp[L - 1] in (256, 512) and a1 == a2 and
+                    ACT_IDS[a1] in ACT_DERIV_FROM_OUTPUT and a1 != "ptanh")
+
     def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None, lane: int = 0, fwd_event=None):
         from ..ops import _native as nat
         sp, kp = self.spec, self.spec.layer_kpad
@@ -744,7 +760,21 @@ class MLPTrainer:
             nat.call_hip("shifu_gemm_nt", a_in.data_ptr(), kp[l], wb[l].data_ptr(), kp[l], sp.hidden[l],
                          a_out.data_ptr(), kp[l + 1], nat.ptr(ders[l + 1]), kp[l + 1], None, 0, None, 0,
                          mc, kp[l + 1], kp[l], 0, act, sp.hidden[l], 1, sp.flat_spot(sp.acts[l]), st)
-        if head:
+        fused_dgrad = False
+        if head and self.strip_head:
+            # last hidden forward + output + loss + deltas + output wgrad + the dgrad of the layer
+            # below in one persistent kernel (the head deltas never leave the chip)
+            lh = L - 1
+            nat.call_hip("shifu_strip_head", acts[lh], kp[lh], wb[lh], kp[lh], sp.hidden[lh], wt[lh], kp[L],
+                              dels[L], kp[L], dels[lh], kp[lh], mc, kp[lh], sp.hidden[lh], sp.hidden[lh - 1],
+                              wv[L].data_ptr(), kp[L], y, s, ws["gw_slab"], ws["err_slab"], self.err_acc,
+                              ACT_IDS[sp.acts[lh]], ACT_IDS[sp.acts[lh - 1]], ACT_IDS[sp.out_act], sp.loss_id,
+                              sp.flat_spot(sp.out_act), sp.flat_spot(sp.acts[lh]), sp.flat_spot(sp.acts[lh - 1]),
+                              st)
+            nat.call_hip("shifu_colsum_fixed", ws["gw_slab"], nat.hip().shifu_strip_head_rows(mc), kp[L],
+                         ws["gw_part"], gv[L].data_ptr(), st)
+            fused_dgrad = True
+        elif head:
             # last hidden forward + output layer + loss + deltas + output wgrad in one GEMM epilogue
             lh = L - 1
             nat.call_hip("shifu_gemm_head", acts[lh].data_ptr(), kp[lh], wb[lh].data_ptr(), kp[lh], sp.hidden[lh],
@@ -788,7 +818,7 @@ class MLPTrainer:
                 nat.call_hip("shifu_wgrad_tn", dels[l + 1].data_ptr(), kp[l + 1], acts[l].data_ptr(), kp[l],
                              gv[l].data_ptr(), kp[l], mc, sp.hidden[l], kp[l], spl, st)
             self._grad_ready(l)
-            if l >= 1:
+            if l >= 1 and not (fused_dgrad and l == L - 1):
                 # dgrad: D_l = (D_{l+1} W_l) * (f'(A_l)+flat)
                 act = ACT_IDS[sp.acts[l - 1]]
                 nat.call_hip("shifu_gemm_nt", dels[l + 1].data_ptr(), kp[l + 1], wt[l].data_ptr(), kp[l + 1],

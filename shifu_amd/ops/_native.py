@@ -70,6 +70,10 @@ HIP_SIGNATURES = {
     "shifu_ring_nt_set_lab": "ip",
     "shifu_ring_nt_set_variant": "i",
     "shifu_strip_nt": "plplipl" "iii" "iiiii" "s",
+    # fused head + layer-below dgrad (gemm_strip_head.hip)
+    "shifu_strip_head": "plpli" "pl" "plpl" "iiii" "pi" "ppppp" "iiii" "fff" "s",
+    "shifu_strip_head_rows": ("i", "i"),
+    "shifu_strip_head_set_dbg_rows": "p",
     "shifu_strip_nt_set_lab": "i",
     "shifu_ring_set_mf": "i",
     "shifu_ring_set_dmamma": "i",

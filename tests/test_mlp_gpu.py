@@ -128,6 +128,39 @@ def test_fused_head_matches_unfused(hidden, acts, loss, monkeypatch):
     assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
 
 
+@pytest.mark.parametrize("hidden,acts,loss,n", [
+    ([500, 200], ["sigmoid", "sigmoid"], "squared", 70000 + 77),     # the bench's head + layer-1 dgrad
+    ([255, 150], ["tanh", "tanh"], "log", 65536 + 1000),             # K1 = 256 (4 + 4 steps per tile)
+    ([400, 250], ["relu", "relu"], "absolute", 300000 + 5),          # several tiles per block
+])
+def test_strip_head_matches_head_plus_dgrad(hidden, acts, loss, n, monkeypatch):
+    """gemm_strip_head.hip (head forward + output + loss + head deltas + output wgrad + the layer
+    below's dgrad in one persistent kernel, the head deltas kept in registers as the dgrad operand)
+    against the 8-phase head kernel + the dgrad tile kernel: same gradients / errors (k order inside
+    the MFMA blocks differs: not bitwise), and bitwise reproducible run to run."""
+    spec = MLPSpec(n_in=120, hidden=hidden, acts=acts, n_out=1, loss=loss)
+    x, y, s = _mk(spec, n, seed=4)
+    monkeypatch.setenv("SHIFU_STRIP_HEAD", "1")
+    a = MLPTrainer(spec, device="cuda", seed=11, chunk_rows=1 << 20)
+    monkeypatch.setenv("SHIFU_STRIP_HEAD", "0")
+    b = MLPTrainer(spec, device="cuda", seed=11, chunk_rows=1 << 20)
+    assert a.strip_head and b.fused_head and not b.strip_head
+    b.params.flat.copy_(a.params.flat)
+    da, db = a.prepare(x, y, s), b.prepare(x, y, s)
+    for t, d in ((a, da), (b, db)):
+        t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
+    torch.cuda.synchronize()
+    g1, e1 = a.grad.clone(), a.err_acc.clone()
+    for va, vb in zip(a.params.views(a.grad), b.params.views(b.grad)):
+        r = (va - vb).norm() / vb.norm().clamp(min=1e-12)
+        assert r < 1e-2, float(r)
+    assert abs(float(a.err_acc[0]) - float(b.err_acc[0])) / float(b.err_acc[0]) < 1e-4
+    assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
+    a.grad.zero_(); a.err_acc.zero_(); a.accumulate_gradients(da)
+    torch.cuda.synchronize()
+    assert torch.equal(a.grad, g1) and torch.equal(a.err_acc, e1)
+
+
 @pytest.mark.parametrize("M,K,N,NB,nv,epi,act", [
     ((1 << 20) + 77, 1024, 512, 500, 500, 0, 0),       # the bench's first layer (sigmoid + bias column)
     (70000 + 33, 256, 512, 512, 512, 0, 1),           # K = 8 steps per tile, tanh, no partial columns
