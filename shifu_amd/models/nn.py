@@ -727,7 +727,7 @@ class MLPTrainer:
         """Fused head + the layer-below dgrad in one persistent kernel (gemm_strip_head.hip): the
         head layer's deltas stay in registers as the dgrad's MFMA operand.  Needs >= 2 hidden
         layers, the head layer padded to 256 (128 < width + 1 <= 256), the layer below padded to
-        256 or 512, and the same activation on both layers (one instantiation per activation).
+        512, and the same activation on both layers (one instantiation per activation).
         SHIFU_STRIP_HEAD=0 keeps the separate head + dgrad kernels."""
         sp = self.spec
         L = len(sp.hidden)
@@ -735,7 +735,7 @@ class MLPTrainer:
             return False
         kp = sp.layer_kpad
         a2, a1 = sp.acts[L - 1], sp.acts[L - 2]
-        return bool(kp[L] == 256 and kp[L - 1] in (256, 512) and a1 == a2 and
+        return bool(kp[L] == 256 and kp[L - 1] == 512 and a1 == a2 and
                     ACT_IDS[a1] in ACT_DERIV_FROM_OUTPUT and a1 != "ptanh")
 
     def _chunk_hip(self, data: TrainData, r0: int, r1: int, wb, wt, x_dev=None, lane: int = 0, fwd_event=None):

@@ -618,8 +618,8 @@ __global__ __launch_bounds__(256) void sh_err_kernel(const double* slab, int T, 
 
 int sh_grid(int M) {
   int dev = 0, ncu = 256;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int ntiles = (M + 255) / 256;
   return ntiles < ncu ? ntiles : ncu;
 }
@@ -634,14 +634,17 @@ SHIFU_API int shifu_strip_head_set_dbg_rows(float* p) { g_sh_dbg_rows = p; retur
 SHIFU_API int shifu_strip_head_rows(int M) { return M > 0 ? sh_grid(M) * 8 : 0; }
 
 // Fused head + layer-below dgrad (see above).  Returns -1 for shapes it does not take (the caller
-// keeps the head + dgrad kernels): K1 in {256, 512}, head width padded to 256 (ldd = ldwt = 256),
+// keeps the head + dgrad kernels): K1 = 512, head width padded to 256 (ldd = ldwt = 256),
 // ACT == HACT (one instantiation per activation), both derivable from the output, not ptanh.
 SHIFU_API int shifu_strip_head(const void* H, long ldh, const void* W, long ldw, int NB, const void* WT, long ldwt,
                                void* D, long ldd, void* DZ, long lddz, int M, int K1, int nv, int nv1,
                                const float* Wo, int KH, const float* Y, const float* S, float* gw_slab,
                                double* err_slab, double* err, int act, int hact, int out_act, int loss,
                                float flat_out, float flat_hid, float flat1, hipStream_t stream) {
-  if (M <= 0 || (K1 != 256 && K1 != 512) || ldh < K1 || ldh % 8 || ldw < K1 || ldw % 8 || ldd != 256 ||
+  // K1 = 256 (4 + 4 steps per tile) is not taken: that build computed wrong, run-to-run different
+  // head deltas for every block's second tile even with every wait made vmcnt(0) (a register-level
+  // fault the ISA audit does not see; profiles/r6/NOTES_r6.md) -- its shapes keep the two kernels
+  if (M <= 0 || K1 != 512 || ldh < K1 || ldh % 8 || ldw < K1 || ldw % 8 || ldd != 256 ||
       ldwt != 256 || lddz < K1 || lddz % 8 || NB <= 0 || NB > 256 || nv > 255 || nv < 0 || KH > 256 ||
       KH < nv + 1 || nv1 > K1)
     return -1;
@@ -659,9 +662,9 @@ SHIFU_API int shifu_strip_head(const void* H, long ldh, const void* W, long ldw,
     case 7: SH_L(7, N_); break; case 9: SH_L(9, N_); break; default: return -1; }
 #ifdef SH_ONE                                        // lab builds: one instantiation
   if (act != 0) return -1;
-  if (K1 == 512) { SH_L(0, 8); } else { SH_L(0, 4); }
+  SH_L(0, 8);
 #else
-  if (K1 == 256) { SH_ACTS(4) } else { SH_ACTS(8) }
+  SH_ACTS(8)
 #endif
 #undef SH_ACTS
 #undef SH_L

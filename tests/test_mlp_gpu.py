@@ -130,7 +130,7 @@ def test_fused_head_matches_unfused(hidden, acts, loss, monkeypatch):
 
 @pytest.mark.parametrize("hidden,acts,loss,n", [
     ([500, 200], ["sigmoid", "sigmoid"], "squared", 70000 + 77),     # the bench's head + layer-1 dgrad
-    ([255, 150], ["tanh", "tanh"], "log", 65536 + 1000),             # K1 = 256 (4 + 4 steps per tile)
+    ([500, 150], ["tanh", "tanh"], "log", 65536 + 1000),             # a partial last tile, two tiles on a few blocks
     ([400, 250], ["relu", "relu"], "absolute", 300000 + 5),          # several tiles per block
 ])
 def test_strip_head_matches_head_plus_dgrad(hidden, acts, loss, n, monkeypatch):
@@ -145,6 +145,8 @@ def test_strip_head_matches_head_plus_dgrad(hidden, acts, loss, n, monkeypatch):
     monkeypatch.setenv("SHIFU_STRIP_HEAD", "0")
     b = MLPTrainer(spec, device="cuda", seed=11, chunk_rows=1 << 20)
     assert a.strip_head and b.fused_head and not b.strip_head
+    # a 256-wide layer below (K1 = 256) keeps the head + dgrad kernels (gemm_strip_head.hip)
+    assert not MLPTrainer(MLPSpec(n_in=120, hidden=[255, 150], acts=acts, n_out=1), device="cuda").strip_head
     b.params.flat.copy_(a.params.flat)
     da, db = a.prepare(x, y, s), b.prepare(x, y, s)
     for t, d in ((a, da), (b, db)):

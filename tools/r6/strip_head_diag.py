@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--nv", type=int, default=200)
     ap.add_argument("--nv1", type=int, default=500)
     ap.add_argument("--act", type=int, default=0, help="0 sigmoid, 1 tanh (both layers)")
+    ap.add_argument("--repeat", type=int, default=0, help="extra launches compared bitwise with the first")
     a = ap.parse_args()
     import torch
     from shifu_amd.ops import _native as nat
@@ -111,6 +112,20 @@ def main():
     rep("gw", gws.sum(0), gw)
     print(json.dumps({"err": [float(err[0]), float(err[1])], "ref_err": [float((e * e).sum()), float(M)],
                       "slab_rows": T}), flush=True)
+    if a.repeat:
+        D0, Z0, g0 = D.clone(), DZ.clone(), gws.clone()
+        nrep = []
+        for _ in range(a.repeat):
+            D.fill_(7.0); DZ.fill_(7.0)
+            nat.call_hip("shifu_strip_head", H, K1, W, K1, nv, WT, 256, D, 256, DZ, K1, M, K1, nv, nv1, Wo, 256, Y,
+                         None, gws, ers, err, a.act, a.act, 0, 0, 0.0, 0.0, 0.0, st)
+            torch.cuda.synchronize()
+            bd = (D != D0).nonzero()
+            bz = (DZ != Z0).nonzero()
+            nrep.append({"D2_diff": int(bd.shape[0]), "DZ_diff": int(bz.shape[0]), "gw_equal": bool(torch.equal(gws, g0)),
+                         "DZ_diff_tiles": torch.unique(bz[:, 0] // 256).tolist()[:10] if bz.shape[0] else [],
+                         "DZ_diff_cols": torch.unique(bz[:, 1] // 64).tolist() if bz.shape[0] else []})
+        print(json.dumps({"repeat": nrep}), flush=True)
     # first rows in detail
     print(json.dumps({"D2_row0_got": [float(v) for v in D[0, :8]], "D2_row0_ref": [float(v) for v in d2b[0, :8]],
                       "DZ_row0_got": [float(v) for v in DZ[0, :8]], "DZ_row0_ref": [float(v) for v in dz[0, :8]]}))
