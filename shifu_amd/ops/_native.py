@@ -56,6 +56,12 @@ HIP_SIGNATURES = {
     "shifu_split_bf16_rows": "plli" "pl" "ii" "s",
     # csv_kernels.hip
     "shifu_csv_gpu_parse": "pppl" "pi" "pl" "p" "pip" "iiP" "pp" "s",
+    # autotype_kernels.hip (init -autotype on the device)
+    "shifu_at_gpu_caps": "p",
+    "shifu_at_gpu_codes": "pppl" "i" "pl" "p" "iiP" "iiP" "s",
+    "shifu_at_gpu_apply": "pll" "pl" "pi" "pppppp" "s",
+    "shifu_at_gpu_items": "pi" "ppp" "s",
+    "shifu_at_gpu_hll_from_sets": "pi" "pp" "s",
     "shifu_transpose_cast": "plpiiis",
     "shifu_newline_ws_bytes": ("l", "l"),
     "shifu_newline_count_offset": ("l", "l"),
