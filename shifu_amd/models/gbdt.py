@@ -384,7 +384,7 @@ class TreeTrainer:
         # single GPU tree: (w, g) travel in position order with pos2row (the partition scatter moves
         # them), so below the root the histogram reads them contiguously and gathers only the bins;
         # at the root positions are rows
-        self._wg_pos = (w, gg) if (self.gpu and T == 1 and not c.is_multiclass) else None
+        self._wg_pos = (w, gg) if (self.gpu and T == 1 and not c.is_multiclass and WG_POS) else None
         trees = [Tree(c.max_depth, weight) for _ in range(T)]
         rngs = [np.random.default_rng([c.seed, int(t)]) for t in tids]
         pos2row = torch.arange(P, dtype=torch.int32, device=self.dev)
@@ -433,6 +433,10 @@ class TreeTrainer:
         n_leaves = [1] * T
         level_log = []
         self.last_tree_stats = {"levels": level_log}
+        if self._pipelined(T):
+            self._grow_levels_dev(trees, rngs, nodes, pos2row, pos_node, w, gg, level_log, n_leaves)
+            self._nmod, self._npos = 0, n
+            return trees
         for level in range(1, c.max_depth):
             if not nodes:
                 break
@@ -492,7 +496,8 @@ class TreeTrainer:
                 if d.is_cat[f]:
                     order = hist["cat_order"][s_][f]
                     left_bins = order[: int(b) + 1]
-                    for lb in left_bins:
+                    for lb in left_bins:       # (int: a uint8 shift stays uint8 under NumPy 2)
+                        lb = int(lb)
                         cat_left[s_, lb >> 5] |= np.uint32(1 << (lb & 31))
                     tree.cat_left[nid] = cat_left[s_]
                     tree.thr[nid] = -1
@@ -550,20 +555,253 @@ class TreeTrainer:
         return trees
 
     # ------------------------------------------------------------------------------------
-    def _make_items(self, nodes, n_built):
+    def _pipelined(self, T: int) -> bool:
+        """Device decisions + device node ranges for this growth (see _grow_levels_dev)."""
+        c = self.cfg
+        return (DEV_DECIDE and self.gpu and not c.is_multiclass and c.max_leaves <= 0
+                and T * 2 ** max(0, c.max_depth - 2) <= 512)
+
+    def _grow_levels_dev(self, trees, rngs, nodes, pos2row, pos_node, w, gg, level_log, n_leaves):
+        """The level loop with one host sync per level, hidden behind the partition.
+
+        Per level the GPU runs, back to back: histogram items resolved to row ranges on the device
+        (shifu_gbdt_items_fix), the histograms, the split scan, the decisions (shifu_gbdt_decide:
+        best feature per node, split bin / categorical set, leaf values, the children's next-level
+        slots), the partition (flags, per-node counts + the children's row ranges, scatter) -- or
+        on the last level the fused leaf update.  The host waits only for the decisions' copy,
+        then mirrors them into the Tree objects and builds the next level's items while the
+        partition runs.  Items are sized from estimated child sizes (parent rows x child weight
+        share) because the exact counts are still on the GPU; the chunking only balances work,
+        the integer histograms do not depend on it.  The exact counts arrive one level later
+        (pinned copy behind the scatter) for the row statistics.  Same trees as the host path
+        (tests/test_gbdt.py: pipelined vs SHIFU_GBDT_DEV_DECIDE=0)."""
+        from ..ops import _native as nat
+        c, d, dev = self.cfg, self.data, self.dev
+        st = nat.stream_of(d.y)
+        fuse = self._fuse if len(trees) == 1 else None
+        cat_any = bool(d.is_cat.any())
+        nodes.sort(key=_slot_key)
+        for s_, z in enumerate(nodes):
+            z["slot"] = s_
+        rng = _h2d(np.array([[z["start"] for z in nodes], [z["end"] for z in nodes]], np.int32), dev)
+        nval = _h2d(np.array([trees[z["tree"]].value[z["id"]] for z in nodes], np.float32), dev)
+        hist_prev = None
+        nleft_prev = None            # pinned per-node left counts of the previous partition
+        for level in range(1, c.max_depth):
+            nn = len(nodes)
+            last = level + 1 >= c.max_depth
+            slot_of = {(z["tree"], z["id"]): z["slot"] for z in nodes}
+            for z in nodes:
+                if not z["built"]:
+                    z["sib_slot"] = slot_of[(z["tree"], z["id"] ^ 1)]
+            n_built = sum(1 for z in nodes if z["built"])
+            self._root_level = level == 1
+            self._level = level
+            self._level_rngs = [rngs[z["tree"]] for z in nodes]
+            t0 = time.perf_counter()
+            with trace_range(f"gbdt.level{level}.hist_split"):
+                h = self._build_and_split(nodes, n_built, gg, w, pos2row, hist_prev,
+                                          rng=rng if level > 1 else None, raw=True)
+                meta = _h2d(np.array([[z["tree"] for z in nodes], [z["id"] for z in nodes],
+                                      [int(z["built"]) for z in nodes]], np.int32), dev)
+                i32 = dict(dtype=torch.int32, device=dev)
+                sf, sb, chl, chr_ = (torch.empty(nn, **i32) for _ in range(4))
+                cl = torch.empty(nn, 8, **i32)
+                lv = torch.empty(3, nn, dtype=torch.float32, device=dev)
+                nxt = torch.empty(max(1, 2 * nn), dtype=torch.float32, device=dev)
+                best_d = torch.empty(nn, 8, dtype=torch.float32, device=dev)
+                nat.call_hip("shifu_gbdt_decide", h["cand"], self.F, nn, meta, nval, h["cat_order"], self.is_cat_t,
+                             int(last), best_d, sf, sb, cl, chl, chr_, lv, nxt, st)
+                best_h = torch.empty(nn, 8, dtype=torch.float32, pin_memory=True)
+                best_h.copy_(best_d, non_blocking=True)
+                cl_h = None
+                if cat_any:
+                    cl_h = torch.empty(nn, 8, dtype=torch.int32, pin_memory=True)
+                    cl_h.copy_(cl, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            self.timings["split"] += time.perf_counter() - t0
+            t1 = time.perf_counter()
+            part = None
+            with trace_range(f"gbdt.level{level}.partition"):
+                if not last:
+                    part = self._partition_dev(nn, rng, sf, sb, cl, chl, chr_, lv, pos2row, pos_node, fuse)
+                elif fuse is not None:
+                    self._leaf_update_dev(nn, rng, sf, sb, cl, lv, pos2row, pos_node, fuse)
+            self.timings["partition"] += time.perf_counter() - t1
+            ev.synchronize()
+            # exact ranges of this level's nodes (the previous partition's counts came before ev)
+            if nleft_prev is not None:
+                nl = nleft_prev.numpy()
+                for z in nodes:
+                    lo, hi = z["prange"]
+                    k = int(nl[z["parent"]])
+                    z["start"], z["end"] = (lo, lo + k) if z["id"] % 2 == 0 else (lo + k, hi)
+                    z.pop("m", None)
+            lv_rows = int(sum(_zm(z) for z in nodes if z["built"]))
+            self.hist_rows_total += lv_rows
+            level_log.append({"level": level, "nodes": nn, "built": int(n_built), "hist_rows": lv_rows,
+                              "hist_split_ms": (time.perf_counter() - t0) * 1e3})
+            # the host mirror of the device decisions
+            b = best_h.numpy().astype(np.float64)
+            clh = cl_h.numpy().view(np.uint32) if cl_h is not None else None
+            if DECIDE_CHECK:
+                self._check_decisions(h, nodes, b, clh, sf, sb, chl, chr_, last)
+            children = []
+            for z in nodes:
+                s_ = z["slot"]
+                f, bn, gain, lw, ls, rw, rs, ok = b[s_]
+                if not ok:
+                    continue
+                tree = trees[z["tree"]]
+                nid = z["id"]
+                n_leaves[z["tree"]] += 1
+                f = int(f)
+                tree.feat[nid] = f
+                tree.gain[nid] = gain
+                tree.features_used.append(f)
+                if d.is_cat[f]:
+                    tree.cat_left[nid] = clh[s_].copy()
+                    tree.thr[nid] = -1
+                else:
+                    tree.thr[nid] = int(bn)
+                for cid, cw, cs in ((2 * nid, lw, ls), (2 * nid + 1, rw, rs)):
+                    tree.exists[cid] = True
+                    tree.value[cid] = cs / cw if cw != 0 else 0.0
+                    tree.wgt_cnt[cid] = cw
+                children.append((z, lw, rw))
+            if last or not children:
+                # fused: the leaf update (last level) or the partition's flag pass (no split: every
+                # row got its node's value) already moved pred
+                if fuse is not None:
+                    self._leaf_done = True
+                break
+            new_nodes = []
+            for z, lw, rw in children:
+                pm, tot = _zm(z), lw + rw
+                for side, cw in ((0, lw), (1, rw)):
+                    built = (lw <= rw) if side == 0 else not (lw <= rw)
+                    est = (int(round(pm * cw / tot)) if tot > 0 else pm // 2)
+                    if cw > 0:
+                        est = max(1, est)
+                    new_nodes.append({"tree": z["tree"], "id": 2 * z["id"] + side, "built": built,
+                                      "parent": z["slot"], "prange": (z["start"], z["end"]), "m": min(est, pm)})
+            new_nodes.sort(key=_slot_key)
+            for s_, nz in enumerate(new_nodes):
+                nz["slot"] = s_
+            pos2row, pos_node, rng, nleft_prev = part
+            nval = nxt
+            hist_prev = h["hist"]
+            nodes = new_nodes
+
+    def _check_decisions(self, h, nodes, b, clh, sf, sb, chl, chr_, last):
+        """SHIFU_GBDT_DECIDE_CHECK=1: the device decisions against _select_best + the host's
+        categorical sets and slot order on the same candidates (debug; syncs)."""
+        nn = len(nodes)
+        ref = self._select_best(h["cand"], nn)
+        co = None if h["cat_order"] is None else h["cat_order"].cpu().numpy()
+        sf_d, sb_d = sf.cpu().numpy(), sb.cpu().numpy()
+        chl_d, chr_d = chl.cpu().numpy(), chr_.cpu().numpy()
+        kids = []
+        for z in nodes:
+            s_ = z["slot"]
+            f, bn, gain, lw, ls, rw, rs, ok = ref[s_]
+            got = tuple(float(v) for v in b[s_])
+            want = (float(f), float(bn), gain, lw, ls, rw, rs, float(ok))
+            if ok and got != want:
+                raise AssertionError(f"decide: slot {s_} best {got} != host {want}")
+            if bool(got[7]) != ok:
+                raise AssertionError(f"decide: slot {s_} ok {got[7]} != host {ok}")
+            exp_sf = f if ok else -1
+            exp_sb = int(bn) if ok and not self.data.is_cat[f] else -1
+            if sf_d[s_] != exp_sf or sb_d[s_] != exp_sb:
+                raise AssertionError(f"decide: slot {s_} split ({sf_d[s_]}, {sb_d[s_]}) != host ({exp_sf}, {exp_sb})")
+            words = np.zeros(8, np.uint32)
+            if ok and self.data.is_cat[f]:
+                for lb in co[s_][f][: int(bn) + 1]:
+                    words[lb >> 5] |= np.uint32(1 << (int(lb) & 31))
+            if clh is not None and not np.array_equal(words, clh[s_]):
+                raise AssertionError(f"decide: slot {s_} cat set {clh[s_].tolist()} != host {words.tolist()} "
+                                     f"(f {f} bin {bn} order {co[s_][f][:int(bn) + 1].tolist()})")
+            if ok and not last:
+                for side, built in ((0, lw <= rw), (1, not lw <= rw)):
+                    kids.append(((not built, z["tree"], 2 * z["id"] + side), s_, side))
+        kids.sort()
+        for slot, (_, s_, side) in enumerate(kids):
+            got = chl_d[s_] if side == 0 else chr_d[s_]
+            if got != slot:
+                raise AssertionError(f"decide: slot {s_} side {side} child slot {got} != host {slot}")
+
+    def _partition_dev(self, nn, rng, sf, sb, cl, chl, chr_, lv, pos2row, pos_node, fuse):
+        """The partition with every per-node input on the device (decide kernel outputs, node
+        ranges): flags, per-node counts + the children's ranges, scatter.  Returns the new
+        position arrays, the next level's ranges [2, 2 nn] and a pinned copy of the left counts."""
+        from ..ops import _native as nat
+        d = self.data
+        st = nat.stream_of(d.y)
+        n = self._npos
+        nw = (n + 63) // 64
+        fbits = torch.empty(nw, dtype=torch.int64, device=self.dev)
+        wcnt = torch.empty(nw, dtype=torch.int32, device=self.dev)
+        pred, scale = fuse if fuse is not None else (None, 0.0)
+        rb = self._root_bins()
+        nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb,
+                     self._root_stride() if rb is not None else 0, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
+                     fbits, wcnt, n, self._nmod, pred, lv[0] if pred is not None else None, None, None,
+                     float(scale), 0, st)
+        wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
+        cbn = torch.empty(2, nn, dtype=torch.int32, device=self.dev)
+        new_rng = torch.empty(2, 2 * nn, dtype=torch.int32, device=self.dev)
+        nat.call_hip("shifu_gbdt_node_counts", fbits, wpre, rng[0], rng[1], nn, cbn[0], cbn[1], chl, chr_,
+                     new_rng[0], new_rng[1], st)
+        new_p2r = torch.empty_like(pos2row)
+        new_pn = torch.empty_like(pos_node)
+        wg = self._wg_pos
+        nw_, ng_ = (torch.empty_like(wg[0]), torch.empty_like(wg[1])) if wg is not None else (None, None)
+        nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, fbits, wpre, rng[0], cbn[1], cbn[0],
+                     sf, chl, chr_, new_p2r, new_pn, None if wg is None else wg[0],
+                     None if wg is None else wg[1], nw_, ng_, n, st)
+        if wg is not None:
+            self._wg_pos = (nw_, ng_)
+        nleft = torch.empty(nn, dtype=torch.int32, pin_memory=True)
+        nleft.copy_(cbn[1], non_blocking=True)
+        return new_p2r, new_pn, new_rng, nleft
+
+    def _leaf_update_dev(self, nn, rng, sf, sb, cl, lv, pos2row, pos_node, fuse):
+        """_leaf_update with the decisions and node ranges on the device."""
+        from ..ops import _native as nat
+        d = self.data
+        pred, scale = fuse
+        rb = self._root_bins()
+        st = nat.stream_of(d.y)
+        if LEAF_WINDOW and self._nmod == 0 and nn <= 1024:
+            nw = ((d.n + LEAF_W - 1) // LEAF_W + 7) // 8 * 8
+            bounds = torch.empty(nn * (nw + 1), dtype=torch.int32, device=self.dev)
+            nat.call_hip("shifu_gbdt_leaf_window", d.kbins, d.group_stride, rb,
+                         self._root_stride() if rb is not None else 0, pos2row, rng[0], rng[1], nn, d.n, LEAF_W,
+                         LEAF_Y, bounds, sf, sb, cl, self.is_cat_t, pred, lv[0], lv[1], lv[2], float(scale), st)
+            return
+        nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb,
+                     self._root_stride() if rb is not None else 0, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
+                     None, None, self._npos, self._nmod, pred, lv[0], lv[1], lv[2], float(scale), 1, st)
+
+    # ------------------------------------------------------------------------------------
+    def _make_items(self, nodes, n_built, est=False):
         """Work items [n, 4] = (node_slot, lo, hi, group) for the built nodes, chunked for
         parallelism, and node_items [n_nodes, n_groups, max_items] (item ids, -1 padded).
         Vectorized over all nodes at once (it runs on the host between two GPU launches of every
-        level); order: node, quad, chunk, sub-group."""
+        level); order: node, quad, chunk, sub-group.  ``est``: the node sizes z["m"] are estimates
+        and the row ranges live on the device -- items hold (slot, chunk, n_chunks, group) and
+        shifu_gbdt_items_fix turns them into row ranges before the histogram launch."""
         G = self.ngroups
         Q = (G + 3) // 4
-        bz = [z for z in nodes if z["built"] and z["end"] - z["start"] > 0]
+        bz = [z for z in nodes if z["built"] and _zm(z) > 0]
         if not bz:
             return np.zeros((0, 4), np.int32), np.full((len(nodes), G, 1), -1, np.int32), 1
         slot = np.array([z["slot"] for z in bz], np.int64)
-        start = np.array([z["start"] for z in bz], np.int64)
-        m = np.array([z["end"] - z["start"] for z in bz], np.int64)
-        rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
+        start = np.zeros(len(bz), np.int64) if est else np.array([z["start"] for z in bz], np.int64)
+        m = np.array([_zm(z) for z in bz], np.int64)
+        rows_built = sum(_zm(z) for z in nodes if z["built"])
         if self.items_per_node_group is None:
             k = np.maximum(1, np.rint(TARGET_ITEMS * (m / max(1, rows_built)) / G).astype(np.int64))
             k = np.minimum(np.minimum(k, np.maximum(1, m // 4096)), 64)
@@ -581,8 +819,11 @@ class TreeTrainer:
         q, rem = r // (kk * 4), r % (kk * 4)
         ch, sg = rem // 4, rem % 4
         grp = q * 4 + sg
-        lo = start[nd] + ch * step[nd]
-        hi = np.minimum(start[nd] + m[nd], lo + step[nd])
+        if est:
+            lo, hi = ch, kk
+        else:
+            lo = start[nd] + ch * step[nd]
+            hi = np.minimum(start[nd] + m[nd], lo + step[nd])
         keep = grp < G
         items = np.stack([slot[nd], lo, hi, grp], 1)[keep].astype(np.int32)
         max_items = int(k.max())
@@ -619,7 +860,10 @@ class TreeTrainer:
         self._ar_events = []
         return ms
 
-    def _build_and_split(self, nodes, n_built, g, w, pos2row, hist_prev):
+    def _build_and_split(self, nodes, n_built, g, w, pos2row, hist_prev, rng=None, raw=False):
+        """raw (GPU): return the split candidates [nn, F, 8] and the categorical orders on the
+        device (the decisions are made by shifu_gbdt_decide); rng: the level's node row ranges
+        [2, nn] on the device (histogram items sized from estimates)."""
         F = self.F
         nn = len(nodes)
         mask = self._node_feature_mask(nn)
@@ -632,6 +876,10 @@ class TreeTrainer:
         # so no zero fill of the level's histograms (up to 64 nodes x 4 MB)
         alloc = torch.empty if self.gpu else torch.zeros
         hist = alloc(nn, 2, F, NB, dtype=torch.int64, device=self.dev)
+        if self.gpu and raw:
+            cand, cat_order = self._build_and_split_hip(nodes, n_built, g, w, pos2row, hist_prev, hist, mask,
+                                                        imp, min_inst, min_gain, rng=rng, raw=True)
+            return {"hist": hist, "cand": cand, "cat_order": cat_order}
         if self.gpu:
             best, cat_order = self._build_and_split_hip(nodes, n_built, g, w, pos2row, hist_prev, hist, mask,
                                                         imp, min_inst, min_gain)
@@ -656,12 +904,13 @@ class TreeTrainer:
             res.append((int(f), int(b), float(gain), float(lw), float(ls), float(rw), float(rs), bool(ok[i])))
         return res
 
-    def _build_and_split_hip(self, nodes, n_built, g, w, pos2row, hist_prev, hist, mask, imp, min_inst, min_gain):
+    def _build_and_split_hip(self, nodes, n_built, g, w, pos2row, hist_prev, hist, mask, imp, min_inst, min_gain,
+                             rng=None, raw=False):
         from ..ops import _native as nat
         d = self.data
         F, nn = self.F, len(nodes)
         st = nat.stream_of(d.y)
-        items, ni, max_items = self._make_items(nodes, n_built)
+        items, ni, max_items = self._make_items(nodes, n_built, est=rng is not None)
         ni_t = _h2d(ni, self.dev)
         feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
         cand = torch.zeros(nn, F, 8, dtype=torch.float32, device=self.dev)
@@ -669,6 +918,8 @@ class TreeTrainer:
         t0 = time.perf_counter()
         if len(items):
             it = _h2d(items, self.dev)
+            if rng is not None:
+                nat.call_hip("shifu_gbdt_items_fix", it, len(items), rng[0], rng[1], st)
             ls = self.level_stats
             if ls is not None:          # per-level histogram roofline (bench --gbdt-levels)
                 ev0 = torch.cuda.Event(enable_timing=True)
@@ -680,7 +931,7 @@ class TreeTrainer:
                 p2r = None if self._root_level else pos2row      # root: positions are rows
                 by_pos = p2r is not None and self._wg_pos is not None
                 wv, gv = self._wg_pos if by_pos else (w, g)
-                rows_built = sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"])
+                rows_built = sum(_zm(z) for z in nodes if z["built"])
                 if HIST64 and not self._root_level and rows_built >= HIST64_MIN_NODE_ROWS * max(1, n_built):
                     pairs = _group_pairs(items)     # half-record blocks: groups 2j, 2j + 1 paired
                     pairs_t = _h2d(pairs, self.dev)        # lives until the level's D2H below
@@ -693,7 +944,7 @@ class TreeTrainer:
             if ls is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev1.record()
-                rows = int(sum(max(0, z["end"] - z["start"]) for z in nodes if z["built"]))
+                rows = int(sum(_zm(z) for z in nodes if z["built"]))
                 ls.append({"level": self._level, "nodes_built": int(n_built), "rows": rows, "ev": (ev0, ev1)})
         else:
             slab = torch.zeros(1, 2, FG, NB, dtype=torch.int64, device=self.dev)
@@ -729,6 +980,8 @@ class TreeTrainer:
                          feat_list.data_ptr(), F, self.nbins_t.data_ptr(), self.is_cat_t.data_ptr(), mptr,
                          cand.data_ptr(), cptr, F, 1, imp, 1, min_inst, min_gain, 1.0 / self.scale_w,
                          1.0 / self.scale_g, st)
+        if raw:
+            return cand, cat_order
         best = self._select_best(cand, nn)
         co = None if cat_order is None else cat_order.cpu().numpy()
         return best, co
@@ -1056,7 +1309,7 @@ class TreeTrainer:
             # per node: left count before its start and #left, on the device; the scatter runs
             # before the host reads the counts (the D2H overlaps it)
             cbn = torch.empty(2, nn, dtype=torch.int32, device=self.dev)
-            nat.call_hip("shifu_gbdt_node_counts", fbits, wpre, st_t, en_t, nn, cbn[0], cbn[1], st)
+            nat.call_hip("shifu_gbdt_node_counts", fbits, wpre, st_t, en_t, nn, cbn[0], cbn[1], None, None, None, None, st)
             new_p2r = torch.empty_like(pos2row)
             new_pn = torch.empty_like(pos_node)
             # tensors (not .data_ptr() of temporaries) so every buffer outlives the launch
@@ -1394,6 +1647,12 @@ def _group_pairs(items: np.ndarray) -> np.ndarray:
     return pairs
 
 
+def _zm(z) -> int:
+    """Rows of a node: exact (end - start) or the estimate "m" of a node whose range is still on
+    the device."""
+    return max(0, int(z["m"])) if "m" in z else max(0, z["end"] - z["start"])
+
+
 def _slot_key(z):
     """Slot order of a level's nodes: built first (one contiguous all-reduce), then by tree, id."""
     return (not z["built"], z["tree"], z["id"])
@@ -1431,6 +1690,15 @@ HIST64 = os.environ.get("SHIFU_GBDT_HIST64", "1") != "0"
 # items they win or tie down to 2.8M rows per node (balanced levels 5 / 6: 13.2 / 14.0 vs 14.5 /
 # 14.8 ms) and tie on the favourable labels' small levels (profiles/r5/gbdt/hist64_threshold_r5.txt)
 HIST64_MIN_NODE_ROWS = int(os.environ.get("SHIFU_GBDT_HIST64_MIN_NODE_ROWS", "2000000"))
+# split decisions on the device, queued ahead of the partition (one host sync per level, which
+# the partition hides); SHIFU_GBDT_DEV_DECIDE=0: host decisions between the split scan and the
+# partition (two syncs per level).  Trees with MaxLeaves, native multi-class trees and levels of
+# more than 512 nodes always take the host path.
+DEV_DECIDE = os.environ.get("SHIFU_GBDT_DEV_DECIDE", "1") != "0"
+DECIDE_CHECK = os.environ.get("SHIFU_GBDT_DECIDE_CHECK", "0") == "1"
+# single-tree builds move (w, g) with the rows in the partition scatter so the histograms read
+# them in position order; SHIFU_GBDT_WG_POS=0: the histograms gather w[row], g[row] instead
+WG_POS = os.environ.get("SHIFU_GBDT_WG_POS", "1") != "0"
 LEAF_W = int(os.environ.get("SHIFU_GBDT_LEAF_W", str(1 << 16)))
 LEAF_Y = int(os.environ.get("SHIFU_GBDT_LEAF_Y", "128"))   # 0.96 vs 2.13 ms with 16 (tools/leafwin_sweep.sh)
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on

@@ -107,6 +107,12 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   uint32_t* hsm32 = (uint32_t*)hsm;
   const int item = xcd_remap(blockIdx.x, gridDim.x);     // a quad's 4 group items share an XCD
   const int lo = a.items[item * 4 + 1], hi = a.items[item * 4 + 2], grp = a.items[item * 4 + 3];
+  if (lo >= hi) {        // an item past its node's rows (ranges resolved on the device): zero slab
+    long long* out = a.slab + (size_t)item * 2 * FG * NB;
+    for (int i = threadIdx.x; i < 2 * FG * NB; i += HT)
+      if (!((MODE == 1 && i >= FG * NB) || (MODE == 2 && i < FG * NB))) out[i] = 0;
+    return;
+  }
   for (int i = threadIdx.x; i < 2 * NB * 16; i += HT) hsm[i] = 0ull;
   __syncthreads();
   const int half = threadIdx.x & 1, r = threadIdx.x & 15, t2 = threadIdx.x >> 1;
@@ -177,37 +183,41 @@ __global__ __launch_bounds__(HT) void gbdt_hist_kernel(HistArgs a) {
   int it = 0;
   constexpr int STEP = RPP * HU;
   if constexpr (PF) {
-    // Software pipeline: pass i+1's loads (bins, w, g) and pass i+2's pos2row gather are issued
-    // before pass i's LDS atomics, so HBM latency hides behind the atomics.  Positions past `hi`
-    // are clamped to hi - 1 (valid memory, no branch around a load: a branch would make the
-    // compiler wait for the outstanding loads early) and get weight 0 when consumed.
+    // Software pipeline over two static slots (as gbdt_hist64_kernel): slot k's (bins, w, g) are
+    // added, then the slot is refilled with the pass two ahead whose row ids were gathered two
+    // passes earlier.  Positions past `hi` are clamped to hi - 1 (valid memory, no branch around
+    // a load) and get weight 0 when consumed.
+    constexpr int SL = 2;
     auto row_of = [&](int p) { const int pc = min(p, hi - 1); return a.pos2row ? a.pos2row[pc] : pc; };
     auto wg_at = [&](int p, int rr) { return a.wg_by_pos ? min(p, hi - 1) : rr; };
-    int rn[HU];
-    float wc[HU], gc[HU];
-    uint4 bc[HU];
+    int rn[SL][HU];
+    float wc[SL][HU], gc[SL][HU];
+    uint4 bc[SL][HU];
 #pragma unroll
-    for (int u = 0; u < HU; ++u) {
-      const int p = lo + t2 + u * RPP, rr = row_of(p), k = wg_at(p, rr);
-      wc[u] = a.w[k]; gc[u] = a.g[k]; bc[u] = rec(rr);
-    }
-#pragma unroll
-    for (int u = 0; u < HU; ++u) rn[u] = row_of(lo + STEP + t2 + u * RPP);
-    for (int p0 = lo; p0 < hi; p0 += STEP) {          // block-uniform trip count (unpack barriers)
-      float wn[HU], gn[HU];
-      uint4 bn[HU];
+    for (int k = 0; k < SL; ++k)
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
-        const int k = wg_at(p0 + STEP + t2 + u * RPP, rn[u]);
-        wn[u] = a.w[k]; gn[u] = a.g[k]; bn[u] = rec(rn[u]);
+        const int p = lo + k * STEP + t2 + u * RPP, rr = row_of(p), kk = wg_at(p, rr);
+        wc[k][u] = a.w[kk]; gc[k][u] = a.g[kk]; bc[k][u] = rec(rr);
       }
 #pragma unroll
-      for (int u = 0; u < HU; ++u) rn[u] = row_of(p0 + 2 * STEP + t2 + u * RPP);
+    for (int k = 0; k < SL; ++k)
 #pragma unroll
-      for (int u = 0; u < HU; ++u) update(p0 + t2 + u * RPP < hi ? wc[u] : 0.f, gc[u], bc[u]);
-      flush(it);
+      for (int u = 0; u < HU; ++u) rn[k][u] = row_of(lo + (SL + k) * STEP + t2 + u * RPP);
+    for (int p0 = lo; p0 < hi; p0 += SL * STEP) {     // block-uniform trip count (unpack barriers)
 #pragma unroll
-      for (int u = 0; u < HU; ++u) { wc[u] = wn[u]; gc[u] = gn[u]; bc[u] = bn[u]; }
+      for (int k = 0; k < SL; ++k) {
+        const int pk = p0 + k * STEP;
+#pragma unroll
+        for (int u = 0; u < HU; ++u) update(pk + t2 + u * RPP < hi ? wc[k][u] : 0.f, gc[k][u], bc[k][u]);
+        flush(it);
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          const int kk = wg_at(pk + SL * STEP + t2 + u * RPP, rn[k][u]);
+          wc[k][u] = a.w[kk]; gc[k][u] = a.g[kk]; bc[k][u] = rec(rn[k][u]);
+          rn[k][u] = row_of(pk + 2 * SL * STEP + t2 + u * RPP);
+        }
+      }
     }
   } else {
     for (int p0 = lo; p0 < hi; p0 += STEP) {          // block-uniform trip count (unpack barriers)
@@ -273,6 +283,10 @@ constexpr int H6_T = 1024;
 constexpr int H6_RPP = H6_T / 4;                 // rows per pass
 constexpr int H6_NE = 4 * NB * 16 / H6_T;        // entries each thread unpacks (16)
 
+// PD: passes of (bins, w, g) in flight ahead of the one being added (row ids PD passes further):
+// with one block of 16 waves per CU a single pass ahead keeps ~4 MB of gathers in flight over the
+// chip, short of what HBM latency x bandwidth asks for
+template <int PD>
 __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int* pairs) {
   constexpr int HFLUSH = 4096 / H6_RPP;
   extern __shared__ __attribute__((aligned(16))) unsigned long long h6[];    // [4][NB][16]
@@ -280,6 +294,13 @@ __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int
   // items of groups 2j (ia) and 2j + 1 (ib) of one node and row range; either may be -1
   const int ia = pairs[pr * 2], ib = pairs[pr * 2 + 1], i0 = ia >= 0 ? ia : ib;
   const int lo = a.items[i0 * 4 + 1], hi = a.items[i0 * 4 + 2], grp = a.items[i0 * 4 + 3] & ~1;
+  if (lo >= hi) {        // empty row range (device-resolved items): zero slabs
+    for (int i = threadIdx.x; i < 2 * 2 * FG * NB; i += H6_T) {
+      const int itm = (i / (2 * FG * NB)) ? ib : ia;
+      if (itm >= 0) a.slab[(size_t)itm * 2 * FG * NB + (i % (2 * FG * NB))] = 0;
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < 4 * NB * 16; i += H6_T) h6[i] = 0ull;
   __syncthreads();
   const int qt = threadIdx.x & 3, r = threadIdx.x & 15, t4 = threadIdx.x >> 2;
@@ -326,21 +347,28 @@ __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int
   auto row_of = [&](int p) { const int pc = min(p, hi - 1); return a.pos2row ? a.pos2row[pc] : pc; };
   auto wg_at = [&](int p, int rr) { return a.wg_by_pos ? min(p, hi - 1) : rr; };
   int it = 0;
-  float wc, gc;
-  uint4 bc;
-  {
-    const int p = lo + t4, rr = row_of(p), k = wg_at(p, rr);
-    wc = a.w[k]; gc = a.g[k]; bc = rec(rr);
+  // PD static slots: slot k is added, then refilled with the pass PD ahead (its row id was
+  // gathered PD passes earlier; the slot's next row id is gathered now)
+  float wr[PD], gr[PD];
+  uint4 br[PD];
+  int rn[PD];
+#pragma unroll
+  for (int j = 0; j < PD; ++j) {
+    const int p = lo + j * H6_RPP + t4, rr = row_of(p), k = wg_at(p, rr);
+    wr[j] = a.w[k]; gr[j] = a.g[k]; br[j] = rec(rr);
   }
-  int rn = row_of(lo + H6_RPP + t4);
-  for (int p0 = lo; p0 < hi; p0 += H6_RPP) {          // block-uniform trip count (unpack barriers)
-    const int k = wg_at(p0 + H6_RPP + t4, rn);
-    const float wn = a.w[k], gn = a.g[k];
-    const uint4 bn = rec(rn);
-    rn = row_of(p0 + 2 * H6_RPP + t4);
-    update(p0 + t4 < hi ? wc : 0.f, gc, bc);
-    flush(it);
-    wc = wn; gc = gn; bc = bn;
+#pragma unroll
+  for (int j = 0; j < PD; ++j) rn[j] = row_of(lo + (PD + j) * H6_RPP + t4);
+  for (int p0 = lo; p0 < hi; p0 += PD * H6_RPP) {     // block-uniform trip count (unpack barriers)
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int pk = p0 + k * H6_RPP;                  // passes past hi add nothing (weight 0)
+      update(pk + t4 < hi ? wr[k] : 0.f, gr[k], br[k]);
+      flush(it);
+      const int kw = wg_at(pk + PD * H6_RPP + t4, rn[k]);
+      wr[k] = a.w[kw]; gr[k] = a.g[kw]; br[k] = rec(rn[k]);
+      rn[k] = row_of(pk + 2 * PD * H6_RPP + t4);
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -1009,7 +1037,7 @@ struct RootTileArgs {
   int mode;                                  // 1: sum w (stat 0), 2: sum w*g (stat 1, x 2^GSH32)
 };
 
-template <int MODE>
+template <int MODE, int PD>
 __global__ __launch_bounds__(RT_T) void gbdt_root_tile_kernel(RootTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ht[];    // [NB][2][32]
   const int item = xcd_remap(blockIdx.x, gridDim.x);
@@ -1042,9 +1070,14 @@ __global__ __launch_bounds__(RT_T) void gbdt_root_tile_kernel(RootTileArgs a) {
   auto load = [&](int t, uint4& b, uint4& qv) {
     const int tc = min(t, t1 - 1);
     b = *(const uint4*)(gb + (size_t)tc * 4096);
-    const int r0 = tc * 128 + c * 16 + qk * 4;
-    qv = *(const uint4*)(a.q + r0);
-    if (t >= t1 || r0 < lo || r0 + 4 > hi) {                 // rows outside [lo, hi) add nothing
+    qv = *(const uint4*)(a.q + tc * 128 + c * 16 + qk * 4);
+  };
+  // rows outside [lo, hi) add nothing -- applied when the pass is consumed: a select on the
+  // loaded values right after the load made the compiler wait for it there (vmcnt(0) per pass:
+  // no load was ever in flight across a pass's atomics)
+  auto mask = [&](int t, uint4& qv) {
+    const int tc = min(t, t1 - 1), r0 = tc * 128 + c * 16 + qk * 4;
+    if (t >= t1 || r0 < lo || r0 + 4 > hi) {
       const int a0 = t >= t1 ? 4 : max(0, lo - r0), a1 = min(4, hi - r0);
       qv.x = (0 >= a0 && 0 < a1) ? qv.x : 0u;
       qv.y = (1 >= a0 && 1 < a1) ? qv.y : 0u;
@@ -1052,31 +1085,37 @@ __global__ __launch_bounds__(RT_T) void gbdt_root_tile_kernel(RootTileArgs a) {
       qv.w = (3 >= a0 && 3 < a1) ? qv.w : 0u;
     }
   };
-  // software pipeline: tiles two passes ahead are in flight while a pass's atomics run
-  uint4 b0, q0, b1, q1;
-  load(t0 + ts, b0, q0);
-  load(t0 + 2 + ts, b1, q1);
-  int passes = 0;
-  for (int t = t0; t < t1; t += 2) {                          // block-uniform trip count
-    uint4 b2, q2;
-    load(t + 4 + ts, b2, q2);
-    const uint32_t B[4] = {b0.x, b0.y, b0.z, b0.w};
-    const int Q[4] = {(int)q0.x, (int)q0.y, (int)q0.z, (int)q0.w};
-    auto rows4 = [&](auto kc) {                               // rows 4k..4k+3 live in quad lane k
-      constexpr int k = decltype(kc)::value;
+  // software pipeline over PD static slots: slot k is consumed and then refilled with the pass PD
+  // ahead, so the other PD - 1 slots' loads stay in flight across its atomics (rotating the slots
+  // through register copies made the compiler wait for every load at the copy)
+  uint4 br[PD], qr[PD];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t qj = (uint32_t)__builtin_amdgcn_mov_dpp(Q[j], k * 0x55, 0xf, 0xf, false);
-        const uint32_t bj = (B[k] >> (j * 8)) & 0xff;
-        atomicAdd(&ht[(bj << 6) | lb], qj);
-      }
-    };
-    rows4(std::integral_constant<int, 0>{});
-    rows4(std::integral_constant<int, 1>{});
-    rows4(std::integral_constant<int, 2>{});
-    rows4(std::integral_constant<int, 3>{});
-    if (++passes == 16) { passes = 0; flush(); }
-    b0 = b1; q0 = q1; b1 = b2; q1 = q2;
+  for (int j = 0; j < PD; ++j) load(t0 + 2 * j + ts, br[j], qr[j]);
+  int passes = 0;
+  for (int t = t0; t < t1; t += 2 * PD) {                     // block-uniform trip count
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int tt = t + 2 * k;                               // passes past t1 add zeros (mask)
+      uint4 q0 = qr[k];
+      mask(tt + ts, q0);
+      const uint32_t B[4] = {br[k].x, br[k].y, br[k].z, br[k].w};
+      const int Q[4] = {(int)q0.x, (int)q0.y, (int)q0.z, (int)q0.w};
+      auto rows4 = [&](auto kc) {                             // rows 4k..4k+3 live in quad lane k
+        constexpr int kq = decltype(kc)::value;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t qj = (uint32_t)__builtin_amdgcn_mov_dpp(Q[j], kq * 0x55, 0xf, 0xf, false);
+          const uint32_t bj = (B[kq] >> (j * 8)) & 0xff;
+          atomicAdd(&ht[(bj << 6) | lb], qj);
+        }
+      };
+      rows4(std::integral_constant<int, 0>{});
+      rows4(std::integral_constant<int, 1>{});
+      rows4(std::integral_constant<int, 2>{});
+      rows4(std::integral_constant<int, 3>{});
+      load(tt + 2 * PD + ts, br[k], qr[k]);
+      if (++passes == 16) { passes = 0; flush(); }
+    }
   }
   flush();
   // slab [item][st][f][b]: transposed through LDS (32 x 256 int64 = 64 KiB) for coalesced stores
@@ -1139,8 +1178,13 @@ SHIFU_API int shifu_gbdt_hist_root_tile(const void* tiles, long gs_t, long n, co
                      nt * 128, sc, mode, q);
   RootTileArgs a{(const uint8_t*)tiles, gs_t, q, items, (long long*)slab, mode};
   const size_t lds = NB * 64 * 4;                              // 64 KiB (also the int64 transpose)
-  if (mode == 1) hipLaunchKernelGGL(gbdt_root_tile_kernel<1>, dim3(n_items), dim3(RT_T), lds, stream, a);
-  else hipLaunchKernelGGL(gbdt_root_tile_kernel<2>, dim3(n_items), dim3(RT_T), lds, stream, a);
+  // SHIFU_GBDT_ROOT_PD: tile passes in flight (lab A/B)
+  static const int pd = [] { const char* e = getenv("SHIFU_GBDT_ROOT_PD"); return e ? atoi(e) : 4; }();
+  if (mode == 1) hipLaunchKernelGGL((gbdt_root_tile_kernel<1, 2>), dim3(n_items), dim3(RT_T), lds, stream, a);
+  else if (pd >= 6) hipLaunchKernelGGL((gbdt_root_tile_kernel<2, 6>), dim3(n_items), dim3(RT_T), lds, stream, a);
+  else if (pd >= 4) hipLaunchKernelGGL((gbdt_root_tile_kernel<2, 4>), dim3(n_items), dim3(RT_T), lds, stream, a);
+  else if (pd == 3) hipLaunchKernelGGL((gbdt_root_tile_kernel<2, 3>), dim3(n_items), dim3(RT_T), lds, stream, a);
+  else hipLaunchKernelGGL((gbdt_root_tile_kernel<2, 2>), dim3(n_items), dim3(RT_T), lds, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -1232,7 +1276,13 @@ SHIFU_API int shifu_gbdt_hist64(const void* bins, long gs, const int* pos2row, c
   if (gs % QF || n_items <= 0 || n_pairs <= 0 || (wg_by_pos && nmod)) return -1;
   HistArgs a{(const uint8_t*)bins, gs, pos2row, w, g, wg_by_pos, QF, items, (long long*)slab, n_items, n_feat,
              (float)scale_w, (float)scale_g, nmod};
-  hipLaunchKernelGGL(gbdt_hist64_kernel, dim3(n_pairs), dim3(H6_T), 4 * NB * 16 * 8, stream, a, pairs);
+  // SHIFU_GBDT_H64_PD: passes in flight (lab A/B)
+  static const int pd = [] { const char* e = getenv("SHIFU_GBDT_H64_PD"); return e ? atoi(e) : 3; }();
+  const size_t lds = 4 * NB * 16 * 8;
+  if (pd >= 4) hipLaunchKernelGGL(gbdt_hist64_kernel<4>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else if (pd == 3) hipLaunchKernelGGL(gbdt_hist64_kernel<3>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else if (pd == 2) hipLaunchKernelGGL(gbdt_hist64_kernel<2>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else hipLaunchKernelGGL(gbdt_hist64_kernel<1>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -1298,8 +1348,11 @@ __global__ void gbdt_bitrank_kernel(const unsigned long long* fbits, const int* 
 
 // per node [start, end): left count before start (cum0) and #left in the node, from the bits +
 // word prefix -- the scatter's node arrays, computed where the bits are (no host round trip)
+// (chl / chr non-null: also the next level's node ranges, new_st / new_en by child slot -- the
+// next level's histogram items resolve their row ranges from these on the device)
 __global__ void gbdt_node_counts_kernel(const unsigned long long* fbits, const int* wpre, const int* starts,
-                                        const int* ends, int nn, int* cum0, int* nleft) {
+                                        const int* ends, int nn, int* cum0, int* nleft, const int* chl,
+                                        const int* chr, int* new_st, int* new_en) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nn) return;
   auto cum = [&](long q) {
@@ -1312,13 +1365,19 @@ __global__ void gbdt_node_counts_kernel(const unsigned long long* fbits, const i
   const int ce = e > s ? cum(e - 1) : cb;
   cum0[i] = cb;
   nleft[i] = ce - cb;
+  if (chl && chl[i] >= 0) {
+    new_st[chl[i]] = s; new_en[chl[i]] = s + (ce - cb);
+    new_st[chr[i]] = s + (ce - cb); new_en[chr[i]] = e;
+  }
 }
 
 SHIFU_API int shifu_gbdt_node_counts(const void* fbits, const int* wpre, const int* starts, const int* ends, int nn,
-                                     int* cum0, int* nleft, hipStream_t stream) {
+                                     int* cum0, int* nleft, const int* chl, const int* chr, int* new_st, int* new_en,
+                                     hipStream_t stream) {
   if (nn <= 0) return 0;
+  if (chl && (!chr || !new_st || !new_en)) return -1;
   hipLaunchKernelGGL(gbdt_node_counts_kernel, dim3((nn + 255) / 256), dim3(256), 0, stream,
-                     (const unsigned long long*)fbits, wpre, starts, ends, nn, cum0, nleft);
+                     (const unsigned long long*)fbits, wpre, starts, ends, nn, cum0, nleft, chl, chr, new_st, new_en);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -1351,6 +1410,152 @@ SHIFU_API int shifu_gbdt_residual(const float* pred, const float* y, const float
   long blocks = (n + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(gbdt_residual_kernel, dim3(blocks), dim3(256), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Split decisions on the device.  After the split scan, one block turns the level's candidates
+// into the partition's inputs (best feature per node with the lowest index on ties, split bin /
+// categorical left set, leaf values, the children's next-level slots and values), so the
+// partition is queued behind it at once and the host reads the same decisions later -- the
+// level no longer waits on a host round trip between the split scan and the partition
+// (DTMaster.java:298-355 makes these decisions on the master between two worker passes).
+// The host applies the identical rules to the copied `best` rows (TreeTrainer._grow_levels_dev).
+// ---------------------------------------------------------------------------------------
+constexpr int DC_T = 1024;
+constexpr int DC_MAXN = 512;
+
+struct DecideArgs {
+  const float* cand; int F, nn;                 // cand [nn][F][8]
+  const int* meta;                              // [3][nn]: tree, node id, built
+  const float* node_val;                        // [nn] leaf value of each node (fused prediction update)
+  const uint8_t* cat_order;                     // [nn][F][NB] nullable
+  const uint8_t* is_cat;
+  int last;
+  float* best;                                  // [nn][8]: feature, bin, gain, lw, ls, rw, rs, ok
+  int* split_feat; int* split_bin; uint32_t* cat_left;   // [nn], [nn], [nn][8]
+  int* child_l; int* child_r;                   // [nn] next-level slots (-1: leaf)
+  float* lv;                                    // [3][nn]: node value, left / right child value
+  float* next_val;                              // [2 nn] child values by next-level slot
+};
+
+__device__ __forceinline__ float leaf_value(float s, float w) {
+  return w != 0.f ? (float)((double)s / (double)w) : 0.f;
+}
+
+__global__ __launch_bounds__(DC_T) void gbdt_decide_kernel(DecideArgs a) {
+  __shared__ int s_ok[DC_MAXN];
+  __shared__ int s_lb[DC_MAXN];                 // left child built (lw <= rw)
+  __shared__ float s_cv[DC_MAXN][2];
+  __shared__ long long s_key[2 * DC_MAXN];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, nn = a.nn;
+  for (int node = wv; node < nn; node += DC_T / 64) {
+    float bg = -INFINITY;
+    int bf = 0x7fffffff;
+    for (int fi = lane; fi < a.F; fi += 64) {
+      const float* c = a.cand + ((size_t)node * a.F + fi) * 8;
+      const float gg = c[6] > 0.f ? c[0] : -INFINITY;
+      if (gg > bg || (gg == bg && fi < bf)) { bg = gg; bf = fi; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const float og = __shfl_xor(bg, off, 64);
+      const int of = __shfl_xor(bf, off, 64);
+      if (og > bg || (og == bg && of < bf)) { bg = og; bf = of; }
+    }
+    const int ok = bg > -INFINITY ? 1 : 0;
+    if (!ok) bf = 0;
+    const float* c = a.cand + ((size_t)node * a.F + bf) * 8;
+    const int cat = ok && a.is_cat[bf];
+    const int bin = (int)c[1];
+    // categorical left set: the first bin + 1 entries of the node's mean-target order of bf
+    uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (cat && a.cat_order) {
+      const uint8_t* o = a.cat_order + ((size_t)node * a.F + bf) * NB;
+      for (int k = lane * 4; k < lane * 4 + 4; ++k)
+        if (k <= bin) { const int b = o[k]; words[b >> 5] |= 1u << (b & 31); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        for (int off = 32; off > 0; off >>= 1) words[j] |= __shfl_xor(words[j], off, 64);
+    }
+    if (lane < 8) a.cat_left[node * 8 + lane] = words[lane];
+    if (lane == 0) {
+      float* b = a.best + (size_t)node * 8;
+      b[0] = (float)bf; b[1] = c[1]; b[2] = c[0]; b[3] = c[2]; b[4] = c[3]; b[5] = c[4]; b[6] = c[5];
+      b[7] = (float)ok;
+      a.split_feat[node] = ok ? bf : -1;
+      a.split_bin[node] = ok && !cat ? bin : -1;
+      const float vl = ok ? leaf_value(c[3], c[2]) : 0.f, vr = ok ? leaf_value(c[5], c[4]) : 0.f;
+      a.lv[node] = a.node_val[node];
+      a.lv[nn + node] = vl;
+      a.lv[2 * nn + node] = vr;
+      s_ok[node] = ok;
+      s_lb[node] = c[2] <= c[4];
+      s_cv[node][0] = vl; s_cv[node][1] = vr;
+    }
+  }
+  __syncthreads();
+  if (a.last) {
+    for (int i = threadIdx.x; i < nn; i += DC_T) { a.child_l[i] = -1; a.child_r[i] = -1; }
+    return;
+  }
+  // next-level slot of child j = (node j / 2, side j % 2): its rank among the children by
+  // (not built, tree, id) -- the host's _slot_key order
+  for (int j = threadIdx.x; j < 2 * nn; j += DC_T) {
+    const int node = j >> 1, side = j & 1;
+    long long key = -1;
+    if (s_ok[node]) {
+      const int built = side == 0 ? s_lb[node] : !s_lb[node];
+      key = ((long long)(built ? 0 : 1) << 62) | ((long long)a.meta[node] << 32) |
+            (long long)(2 * a.meta[nn + node] + side);
+    }
+    s_key[j] = key;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * nn; j += DC_T) {
+    const long long key = s_key[j];
+    const int node = j >> 1, side = j & 1;
+    if (key < 0) {
+      if (side == 0) a.child_l[node] = -1; else a.child_r[node] = -1;
+      continue;
+    }
+    int slot = 0;
+    for (int t = 0; t < 2 * nn; ++t) slot += (s_key[t] >= 0 && s_key[t] < key) ? 1 : 0;
+    if (side == 0) a.child_l[node] = slot; else a.child_r[node] = slot;
+    a.next_val[slot] = s_cv[node][side];
+  }
+}
+
+SHIFU_API int shifu_gbdt_decide(const float* cand, int F, int nn, const int* meta, const float* node_val,
+                                const void* cat_order, const void* is_cat, int last, float* best, int* split_feat,
+                                int* split_bin, void* cat_left, int* child_l, int* child_r, float* lv,
+                                float* next_val, hipStream_t stream) {
+  if (nn <= 0) return 0;
+  if (nn > DC_MAXN || F <= 0 || F > (1 << 24)) return -1;
+  DecideArgs a{cand, F, nn, meta, node_val, (const uint8_t*)cat_order, (const uint8_t*)is_cat, last, best,
+               split_feat, split_bin, (uint32_t*)cat_left, child_l, child_r, lv, next_val};
+  hipLaunchKernelGGL(gbdt_decide_kernel, dim3(1), dim3(DC_T), 0, stream, a);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// histogram items whose row ranges live on the device: items [n][4] = {slot, chunk, k, group} ->
+// {slot, lo, hi, group}, chunk `chunk` of k equal pieces of the node's [start, end)
+__global__ void gbdt_items_fix_kernel(int* items, int n, const int* starts, const int* ends) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int* it = items + (size_t)i * 4;
+  const int slot = it[0], ch = it[1], k = max(1, it[2]);
+  const int s = starts[slot], m = max(0, ends[slot] - s);
+  const int step = (m + k - 1) / k;
+  const long lo = min((long)m, (long)ch * step), hi = min((long)m, lo + step);
+  it[1] = s + (int)lo;
+  it[2] = s + (int)hi;
+}
+
+SHIFU_API int shifu_gbdt_items_fix(int* items, int n, const int* starts, const int* ends, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gbdt_items_fix_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, items, n, starts, ends);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

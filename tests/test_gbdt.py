@@ -556,3 +556,68 @@ def test_group_pairs_matches_sorting_construction():
         got = _group_pairs(items)
         assert sorted(map(tuple, got.tolist())) == sorted(map(tuple, ref.tolist()))
         assert ((got[:, 0] < 0) | (items[np.maximum(got[:, 0], 0), 3] % 2 == 0)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["gbt_balanced", "gbt_categorical", "rf_forest_poisson"])
+def test_gpu_device_decisions_match_host_path(case, monkeypatch):
+    """Split decisions made on the device ahead of the partition (shifu_gbdt_decide), node row
+    ranges kept on the device and histogram items sized from estimated child sizes
+    (shifu_gbdt_items_fix, empty chunks included) grow the same trees, categorical left sets and
+    predictions, bit for bit, as the host-decision path with two syncs per level."""
+    from shifu_amd.models import gbdt as gb
+    from shifu_amd.models.gbdt import synthetic_binned
+    monkeypatch.setenv("SHIFU_RF_BATCH", "3")
+    if case == "gbt_categorical":
+        _, codes, y = _data(n=40000, f=40, nb=64, seed=7, cat_cols=(1, 3, 17))
+        nbins = np.full(40, 64)
+        is_cat = np.zeros(40, np.uint8)
+        is_cat[[1, 3, 17]] = 1
+        data = BinnedData.from_codes(codes, y, nbins, is_cat, device="cuda")
+        cfg = TreeConfig("GBT", tree_num=3, max_depth=6, learning_rate=0.2, feature_subset_strategy="ALL",
+                         min_instances_per_node=2)
+    elif case == "gbt_balanced":
+        data = synthetic_binned(200003, 70, "cuda", seed=12, labels="balanced")
+        cfg = TreeConfig("GBT", tree_num=3, max_depth=7, learning_rate=0.1, feature_subset_strategy="ALL",
+                         min_instances_per_node=2)
+    else:
+        data = synthetic_binned(120001, 45, "cuda", seed=13, labels="balanced")
+        cfg = TreeConfig("RF", tree_num=4, max_depth=6, feature_subset_strategy="HALF", min_instances_per_node=2,
+                         bagging_sample_rate=0.6, sample_with_replacement=True, seed=5)
+    runs = []
+    for dev_dec in (True, False):
+        monkeypatch.setattr(gb, "DEV_DECIDE", dev_dec)
+        tr = TreeTrainer(cfg, data)
+        assert tr._pipelined(1) == dev_dec
+        tr.train()
+        runs.append(tr)
+    a, b = runs
+    assert a.hist_rows_total == b.hist_rows_total
+    for x, y_ in zip(a.trees, b.trees):
+        assert (x.feat == y_.feat).all() and (x.thr == y_.thr).all()
+        assert np.array_equal(x.value, y_.value) and np.array_equal(x.wgt_cnt, y_.wgt_cnt)
+        assert np.array_equal(np.asarray(x.cat_left), np.asarray(y_.cat_left))
+    if case == "gbt_categorical":
+        assert any((np.asarray(t.cat_left) != 0).any() for t in a.trees)
+    assert torch.equal(a.pred, b.pred)
+    # (the residual kernel's error sum uses float64 atomics: equal up to summation order)
+    assert np.allclose(a.train_errors, b.train_errors, rtol=1e-9, atol=0)
+
+
+def test_categorical_split_with_many_categories_partitions_rows():
+    """A categorical split whose left set holds categories >= 8: every left category's rows go
+    left (the host's left-set bits were once built with a uint8 shift that dropped them)."""
+    rng = np.random.default_rng(4)
+    n = 4000
+    cat = rng.integers(0, 40, n)
+    pos = np.array([9, 13, 22, 31, 38])
+    y = np.isin(cat, pos).astype(np.float32)
+    codes = np.stack([cat, rng.integers(0, 8, n)], 1)
+    data = BinnedData.from_codes(codes, y, np.array([41, 8]), np.array([1, 0]))
+    tr = TreeTrainer(TreeConfig("GBT", tree_num=1, max_depth=2, feature_subset_strategy="ALL"), data)
+    tr.train()
+    t = tr.trees[0]
+    assert t.feat[1] == 0
+    left = {c for c in range(41) if (int(t.cat_left[1][c >> 5]) >> (c & 31)) & 1}
+    assert left == set(pos.tolist()) or left.isdisjoint(pos.tolist())
+    assert abs(tr.train_errors[0]) < 1e-6
