@@ -409,6 +409,9 @@ class TreeTrainer:
                                                 for wt in ws]))
             mx = torch.stack([w.abs().max().double(), (w * gg).abs().max().double()])
         dist.all_reduce_(mx, "max")
+        # the root sums and the scales' maxima in one device-to-host copy (one sync per tree here)
+        hv = torch.cat([tot.reshape(-1).double(), mx.double()]).cpu().numpy()
+        tot, mx = hv[:2 * T].reshape(T, 2), hv[2 * T:]
         self.scale_w = _pack_scale(float(mx[0]), W_BITS)
         # margin 2^(GSH32+1): the root's u32 w*g mode quantises at scale_g / 2^GSH32, whose rounded
         # |q| must stay < 2^20 - 1 so 2048 rows in one bin cannot reach 2^31 (gbdt_kernels.hip)
@@ -583,6 +586,8 @@ class TreeTrainer:
         nodes.sort(key=_slot_key)
         for s_, z in enumerate(nodes):
             z["slot"] = s_
+        if RANGE_NODES:          # positions find their node from the sorted node ranges
+            pos_node = None
         rng = _h2d(np.array([[z["start"] for z in nodes], [z["end"] for z in nodes]], np.int32), dev)
         nval = _h2d(np.array([trees[z["tree"]].value[z["id"]] for z in nodes], np.float32), dev)
         hist_prev = None
@@ -745,22 +750,23 @@ class TreeTrainer:
         wcnt = torch.empty(nw, dtype=torch.int32, device=self.dev)
         pred, scale = fuse if fuse is not None else (None, 0.0)
         rb = self._root_bins()
+        ri = self._range_index(nn, rng) if pos_node is None else (None, None, None, 0)
         nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb,
                      self._root_stride() if rb is not None else 0, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
                      fbits, wcnt, n, self._nmod, pred, lv[0] if pred is not None else None, None, None,
-                     float(scale), 0, st)
+                     float(scale), 0, *ri, st)
         wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
         cbn = torch.empty(2, nn, dtype=torch.int32, device=self.dev)
         new_rng = torch.empty(2, 2 * nn, dtype=torch.int32, device=self.dev)
         nat.call_hip("shifu_gbdt_node_counts", fbits, wpre, rng[0], rng[1], nn, cbn[0], cbn[1], chl, chr_,
                      new_rng[0], new_rng[1], st)
         new_p2r = torch.empty_like(pos2row)
-        new_pn = torch.empty_like(pos_node)
+        new_pn = torch.empty_like(pos_node) if pos_node is not None else None
         wg = self._wg_pos
         nw_, ng_ = (torch.empty_like(wg[0]), torch.empty_like(wg[1])) if wg is not None else (None, None)
         nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, fbits, wpre, rng[0], cbn[1], cbn[0],
                      sf, chl, chr_, new_p2r, new_pn, None if wg is None else wg[0],
-                     None if wg is None else wg[1], nw_, ng_, n, st)
+                     None if wg is None else wg[1], nw_, ng_, n, *ri, st)
         if wg is not None:
             self._wg_pos = (nw_, ng_)
         nleft = torch.empty(nn, dtype=torch.int32, pin_memory=True)
@@ -781,12 +787,22 @@ class TreeTrainer:
                          self._root_stride() if rb is not None else 0, pos2row, rng[0], rng[1], nn, d.n, LEAF_W,
                          LEAF_Y, bounds, sf, sb, cl, self.is_cat_t, pred, lv[0], lv[1], lv[2], float(scale), st)
             return
+        ri = self._range_index(nn, rng) if pos_node is None else (None, None, None, 0)
         nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb,
                      self._root_stride() if rb is not None else 0, pos2row, pos_node, sf, sb, cl, self.is_cat_t,
-                     None, None, self._npos, self._nmod, pred, lv[0], lv[1], lv[2], float(scale), 1, st)
+                     None, None, self._npos, self._nmod, pred, lv[0], lv[1], lv[2], float(scale), 1, *ri, st)
+
+    def _range_index(self, nn, rng):
+        """The level's node ranges sorted by start (range_node in gbdt_kernels.hip): the partition
+        finds a position's node from these instead of a per-position node array."""
+        from ..ops import _native as nat
+        r_start = torch.empty(nn, dtype=torch.int32, device=self.dev)
+        r_slot = torch.empty(nn, dtype=torch.int32, device=self.dev)
+        nat.call_hip("shifu_gbdt_range_index", rng[0], rng[1], nn, r_start, r_slot, nat.stream_of(self.data.y))
+        return r_start, r_slot, rng[1], nn
 
     # ------------------------------------------------------------------------------------
-    def _make_items(self, nodes, n_built, est=False):
+    def _make_items(self, nodes, n_built, est=False, align=1):
         """Work items [n, 4] = (node_slot, lo, hi, group) for the built nodes, chunked for
         parallelism, and node_items [n_nodes, n_groups, max_items] (item ids, -1 padded).
         Vectorized over all nodes at once (it runs on the host between two GPU launches of every
@@ -808,6 +824,8 @@ class TreeTrainer:
         else:
             k = np.full(len(bz), int(self.items_per_node_group), np.int64)
         step = (m + k - 1) // k
+        if align > 1:       # chunk boundaries on whole row tiles (the tiled root pass skips its row mask)
+            step = (step + align - 1) // align * align
         k = (m + step - 1) // step                          # chunks that are non-empty
         # one row per (node, quad, chunk, sub-group): the 4 groups of one 128-B record and row
         # range are consecutive items (one XCD, gbdt_kernels.hip xcd_remap) and share its lines
@@ -910,7 +928,8 @@ class TreeTrainer:
         d = self.data
         F, nn = self.F, len(nodes)
         st = nat.stream_of(d.y)
-        items, ni, max_items = self._make_items(nodes, n_built, est=rng is not None)
+        tiled_root = self._root_level and self._nmod == 0 and ROOT_U32 and self._root_bins() is not None
+        items, ni, max_items = self._make_items(nodes, n_built, est=rng is not None, align=128 if tiled_root else 1)
         ni_t = _h2d(ni, self.dev)
         feat_list = torch.arange(F, dtype=torch.int32, device=self.dev)
         cand = torch.zeros(nn, F, 8, dtype=torch.float32, device=self.dev)
@@ -1270,7 +1289,7 @@ class TreeTrainer:
         cl = _h2d(cat_left.view(np.int32), self.dev)
         nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, self._root_stride() if rb is not None else 0,
                      pos2row, pos_node, sf, sb, cl, self.is_cat_t, None, None, self._npos, self._nmod, pred, leaf_vals[0], leaf_vals[1], leaf_vals[2], float(scale),
-                     1, st)
+                     1, None, None, None, 0, st)
 
     def _partition(self, nodes, split_feat, split_bin, cat_left, pos2row, pos_node, child_slots, leaf=None):
         d = self.data
@@ -1304,7 +1323,7 @@ class TreeTrainer:
             rb = self._root_bins()        # feature-tiled copy when it exists
             nat.call_hip("shifu_gbdt_partition_flag", d.kbins, d.group_stride, rb, self._root_stride() if rb is not None else 0,
                          pos2row, pos_node, sf, sb, cl, self.is_cat_t, fbits, wcnt, n, self._nmod, pred, None if lv is None else lv[0], None, None,
-                         float(scale), 0, st)
+                         float(scale), 0, None, None, None, 0, st)
             wpre = torch.cumsum(wcnt, 0, dtype=torch.int32) - wcnt
             # per node: left count before its start and #left, on the device; the scatter runs
             # before the host reads the counts (the D2H overlaps it)
@@ -1317,7 +1336,7 @@ class TreeTrainer:
             nw_, ng_ = (torch.empty_like(wg[0]), torch.empty_like(wg[1])) if wg is not None else (None, None)
             nat.call_hip("shifu_gbdt_partition_scatter", pos2row, pos_node, fbits, wpre, st_t, cbn[1], cbn[0],
                          sf, chl_t, chr_t, new_p2r, new_pn, None if wg is None else wg[0],
-                         None if wg is None else wg[1], nw_, ng_, n, st)
+                         None if wg is None else wg[1], nw_, ng_, n, None, None, None, 0, st)
             if wg is not None:
                 self._wg_pos = (nw_, ng_)
             nleft = cbn[1].cpu().numpy().astype(np.int64)     # one D2H sync, behind the scatter
@@ -1392,7 +1411,8 @@ class TreeTrainer:
             err[0] = (s.double() * e.double()).sum()
             err[1] = s.double().sum()
         dist.all_reduce_(err)
-        return float(err[0] / max(err[1], 1e-12))
+        e = err.cpu().numpy()                      # one device-to-host copy
+        return float(e[0] / max(e[1], 1e-12))
 
     # ------------------------------------------------------------------------------------
     def train(self, n_trees: int | None = None, callback=None):
@@ -1699,6 +1719,10 @@ DECIDE_CHECK = os.environ.get("SHIFU_GBDT_DECIDE_CHECK", "0") == "1"
 # single-tree builds move (w, g) with the rows in the partition scatter so the histograms read
 # them in position order; SHIFU_GBDT_WG_POS=0: the histograms gather w[row], g[row] instead
 WG_POS = os.environ.get("SHIFU_GBDT_WG_POS", "1") != "0"
+# device-decision levels: the partition finds a position's node by searching the level's node
+# ranges (sorted by start) instead of reading / writing a per-position node array (8-12 B per
+# position per level less); SHIFU_GBDT_RANGE_NODES=0 keeps the array
+RANGE_NODES = os.environ.get("SHIFU_GBDT_RANGE_NODES", "1") != "0"
 LEAF_W = int(os.environ.get("SHIFU_GBDT_LEAF_W", str(1 << 16)))
 LEAF_Y = int(os.environ.get("SHIFU_GBDT_LEAF_Y", "128"))   # 0.96 vs 2.13 ms with 16 (tools/leafwin_sweep.sh)
 # what the histograms really hold (bench label): per-row w and w*g quantised to fixed point on

@@ -91,13 +91,14 @@ HIP_SIGNATURES = {
     "shifu_gbdt_wg_stats": "pplpps",
     "shifu_gbdt_hist64": "plppp" "ipip" "ip" "iddl" "s",
     "shifu_gbdt_split": "ppipppp" "pipipp" "ppp" "iiii" "ff" "dd" "s",
-    "shifu_gbdt_partition_flag": "plpl" "pppppppp" "ll" "pppp" "fi" "s",
+    "shifu_gbdt_partition_flag": "plpl" "pppppppp" "ll" "pppp" "fi" "pppi" "s",
+    "shifu_gbdt_range_index": "ppi" "pp" "s",
     "shifu_gbdt_bitrank": "pppip" "s",
     "shifu_gbdt_node_counts": "ppppipp" "pppp" "s",
     "shifu_gbdt_decide": "pii" "pp" "pp" "i" "p" "ppp" "pp" "pp" "s",
     "shifu_gbdt_items_fix": "pi" "pp" "s",
     "shifu_gbdt_leaf_window": "plpl" "ppp" "illi" "p" "pppp" "pppp" "f" "s",
-    "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "pppp" "l" "s",
+    "shifu_gbdt_partition_scatter": "pppp" "ppp" "ppp" "pp" "pppp" "l" "pppi" "s",
     "shifu_gbdt_apply_tree": "plppppppp" "fi" "p" "li" "s",
     "shifu_gbdt_residual": "pppp" "p" "li" "s",
     # stats_kernels.hip

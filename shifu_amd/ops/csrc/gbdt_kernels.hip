@@ -31,6 +31,7 @@
 #include "common.h"
 #include <cstdlib>
 #include <type_traits>
+typedef __attribute__((ext_vector_type(4))) int v4i_t;
 
 namespace {
 
@@ -627,13 +628,42 @@ struct PartArgs {
   // split nodes get the value of the child they go to
   float* pred; const float* node_val; const float* child_l_val; const float* child_r_val;
   float scale; int final_level;
+  // pos_node == nullptr: the node of a position comes from the level's node ranges sorted by
+  // start (gbdt_range_index_kernel): r_start ascending, r_slot, node ends by slot
+  const int* r_start; const int* r_slot; const int* r_end; int r_n;
 };
+
+// index r of the last sorted range starting at or before p (-1: none)
+__device__ __forceinline__ int range_find(const int* rs, int nn, int p) {
+  int lo = 0, hi = nn;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (rs[mid] <= p) lo = mid + 1; else hi = mid;
+  }
+  return lo - 1;
+}
+
+// node slot of position p from the sorted ranges (-1: a finished node's position).  The search
+// runs once per wave on the first active lane's position (uniform operands: scalar loads of the
+// small index); lanes outside that node (a wave straddling a node boundary) search on their own
+__device__ __forceinline__ int range_node(const int* rs, const int* rslot, const int* ren, int nn, int p) {
+  const int p0 = __builtin_amdgcn_readfirstlane(p);
+  const int r0 = range_find(rs, nn, p0);
+  int s0 = -1, b0 = 0, e0 = 0;
+  if (r0 >= 0) { s0 = rslot[r0]; b0 = rs[r0]; e0 = ren[s0]; }
+  const bool in0 = r0 >= 0 && p >= b0 && p < e0;
+  if (__all(in0)) return s0;
+  const int r = range_find(rs, nn, p);
+  if (r < 0) return -1;
+  const int sl = rslot[r];
+  return p < ren[sl] ? sl : -1;
+}
 
 // left bit of position p (+ the fused prediction update).  The node's parameters come from scalar
 // loads of the wave's first lane's node when all 64 positions lie in it (nearly always), as in
 // the scatter kernel
 __device__ __forceinline__ int partition_flag(const PartArgs& a, long p) {
-  const int node = a.pos_node[p];
+  const int node = a.pos_node ? a.pos_node[p] : range_node(a.r_start, a.r_slot, a.r_end, a.r_n, (int)p);
   const long v = a.pos2row[p], row = a.nmod ? v % a.nmod : v;
   const int nu = __builtin_amdgcn_readfirstlane(node);
   const int nd = __all(node == nu) ? nu : node;
@@ -747,6 +777,7 @@ struct ScatterArgs {
   // nullable: position-ordered per-row floats (w, g) moved with their rows (a pair of src / dst)
   const float* w_src; const float* g_src; float* w_dst; float* g_dst;
   long n;
+  const int* r_start; const int* r_slot; const int* r_end; int r_n;   // pos_node == nullptr (as PartArgs)
 };
 
 __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
@@ -756,7 +787,7 @@ __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
   // 64 positions almost always lie in one node, so those come from scalar loads of the wave's
   // first lane's node (vector loads only when the wave straddles a node boundary): 1.16 ->
   // 0.68 ms per 100M positions (profiles/r5/gbdt/partition_uniform_ab.txt)
-  const int node = a.pos_node[p];
+  const int node = a.pos_node ? a.pos_node[p] : range_node(a.r_start, a.r_slot, a.r_end, a.r_n, (int)p);
   const int row = a.pos2row[p];
   float wv = 0.f, gv = 0.f;
   if (a.w_dst) { wv = a.w_src[p]; gv = a.g_src[p]; }
@@ -785,7 +816,7 @@ __global__ void gbdt_partition_scatter_kernel(ScatterArgs a) {
     else { np = s + nleft + (int)(p - s) - before; child = cr; }
   }
   a.new_pos2row[np] = row;
-  a.new_pos_node[np] = child;
+  if (a.new_pos_node) a.new_pos_node[np] = child;
   if (a.w_dst) { a.w_dst[np] = wv; a.g_dst[np] = gv; }
 }
 
@@ -1031,10 +1062,11 @@ constexpr int RT_E = NB * FG / RT_T;          // (bin, feature) sums each thread
 
 struct RootTileArgs {
   const uint8_t* bins; long gs;              // [G][NT][32][128]: gs = NT * 4096 bytes per group
-  const int* q;                              // [>= NT * 128] per-row u32 / i32 increment
+  const int* q;                              // [>= NT * 128] per-row u32 / i32 increment (0 past n)
   const int* items;                          // [n][4] = {node, lo, hi, group}
   long long* slab;                           // [n_items][2][FG][NB]
   int mode;                                  // 1: sum w (stat 0), 2: sum w*g (stat 1, x 2^GSH32)
+  long n;                                    // rows (q is zero-padded past n to the tile end)
 };
 
 template <int MODE, int PD>
@@ -1064,17 +1096,33 @@ __global__ __launch_bounds__(RT_T) void gbdt_root_tile_kernel(RootTileArgs a) {
     __syncthreads();
   };
   const int t0 = lo >> 7, t1 = (hi + 127) >> 7;
+  if (t1 <= t0) {                                             // no rows: zero slab
+    long long* out = a.slab + ((size_t)item * 2 + (MODE == 1 ? 0 : 1)) * FG * NB;
+    for (int i = threadIdx.x; i < FG * NB; i += RT_T) out[i] = 0;
+    return;
+  }
   // q of the chunk's 16 rows: lane (f & 3) = k of each 4-lane quad (same chunk) loads rows 4k..4k+3,
-  // the others are broadcast from it by quad-permute DPP moves -- one 16-B q load per pass
+  // the others are broadcast from it by quad-permute DPP moves -- one 16-B q load per pass.
+  // Loads are raw buffer loads: the per-lane part of the address in voffset (constant), the
+  // wave-uniform tile in soffset (scalar arithmetic: no 64-bit VALU address math per pass)
   const int qk = f & 3;
-  auto load = [&](int t, uint4& b, uint4& qv) {
-    const int tc = min(t, t1 - 1);
-    b = *(const uint4*)(gb + (size_t)tc * 4096);
-    qv = *(const uint4*)(a.q + tc * 128 + c * 16 + qk * 4);
+  // Resources based at the item's first tile: the buffer offsets (and the range check) then span
+  // only the item's own tiles, whatever the size of the copy (a group of 100M rows is 3.2 GB: a
+  // whole-group resource clipped to 2^31 bytes read zeros past 67M rows)
+  const long nt_item = (long)(t1 - t0);
+  const __amdgpu_buffer_rsrc_t rb_bins = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.bins + (size_t)grp * a.gs + (size_t)t0 * 4096), (short)0, (int)(nt_item * 4096), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb_q = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.q + (size_t)t0 * 128), (short)0, (int)(nt_item * 512), 0x00020000);
+  const int vo_b = f * 128 + c * 16, vo_q = (c * 16 + qk * 4) * 4;
+  auto load = [&](int t, uint4& b, uint4& qv) {             // t: wave-uniform tile (clamped)
+    const int tc = __builtin_amdgcn_readfirstlane(min(t, t1 - 1) - t0);
+    const v4i_t bv = __builtin_amdgcn_raw_buffer_load_b128(rb_bins, vo_b, tc * 4096, 0);
+    const v4i_t qq = __builtin_amdgcn_raw_buffer_load_b128(rb_q, vo_q, tc * 512, 0);
+    b = make_uint4((uint32_t)bv[0], (uint32_t)bv[1], (uint32_t)bv[2], (uint32_t)bv[3]);
+    qv = make_uint4((uint32_t)qq[0], (uint32_t)qq[1], (uint32_t)qq[2], (uint32_t)qq[3]);
   };
-  // rows outside [lo, hi) add nothing -- applied when the pass is consumed: a select on the
-  // loaded values right after the load made the compiler wait for it there (vmcnt(0) per pass:
-  // no load was ever in flight across a pass's atomics)
+  // rows outside [lo, hi) add nothing (unaligned items only; applied when the pass is consumed)
   auto mask = [&](int t, uint4& qv) {
     const int tc = min(t, t1 - 1), r0 = tc * 128 + c * 16 + qk * 4;
     if (t >= t1 || r0 < lo || r0 + 4 > hi) {
@@ -1085,38 +1133,65 @@ __global__ __launch_bounds__(RT_T) void gbdt_root_tile_kernel(RootTileArgs a) {
       qv.w = (3 >= a0 && 3 < a1) ? qv.w : 0u;
     }
   };
-  // software pipeline over PD static slots: slot k is consumed and then refilled with the pass PD
-  // ahead, so the other PD - 1 slots' loads stay in flight across its atomics (rotating the slots
-  // through register copies made the compiler wait for every load at the copy)
-  uint4 br[PD], qr[PD];
+  // The pass is VALU-bound (PMC: ~5.2 VALU per LDS atomic before, r6): each atomic's LDS byte
+  // address bin * 256 + lane * 4 is ONE v_perm_b32 of the bin byte and the lane's byte offset, fed
+  // to ds_add_u32 directly (the dynamic LDS array starts at byte 0: the kernel has no static LDS),
+  // and items whose rows start and end on tile boundaries (the root items are chunked that way; q
+  // is zero past n) skip the row mask: 2 VALU per atomic (perm + the q broadcast) plus the loop.
+  const uint32_t lbyte = (uint32_t)lb * 4u;                   // < 256: byte 0 of every address
+  auto consume = [&](const uint4& b, uint4 q0, int tt, auto masked) {
+    if constexpr (decltype(masked)::value) mask(tt + ts, q0);
+    const uint32_t B[4] = {b.x, b.y, b.z, b.w};
+    const int Q[4] = {(int)q0.x, (int)q0.y, (int)q0.z, (int)q0.w};
+    auto rows4 = [&](auto kc) {                               // rows 4k..4k+3 live in quad lane k
+      constexpr int kq = decltype(kc)::value;
 #pragma unroll
-  for (int j = 0; j < PD; ++j) load(t0 + 2 * j + ts, br[j], qr[j]);
-  int passes = 0;
-  for (int t = t0; t < t1; t += 2 * PD) {                     // block-uniform trip count
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t qj = (uint32_t)__builtin_amdgcn_mov_dpp(Q[j], kq * 0x55, 0xf, 0xf, false);
+        // bytes {lbyte, bin j of B[kq], 0, 0}: selector 0 = byte 0 of src1, 4 + j = byte j of src0
+        const uint32_t addr = __builtin_amdgcn_perm(B[kq], lbyte, 0x0c0c0000u | ((4u + j) << 8));
+        asm volatile("ds_add_u32 %0, %1" : : "v"(addr), "v"(qj) : "memory");
+      }
+    };
+    rows4(std::integral_constant<int, 0>{});
+    rows4(std::integral_constant<int, 1>{});
+    rows4(std::integral_constant<int, 2>{});
+    rows4(std::integral_constant<int, 3>{});
+  };
+  // the asm atomics are invisible to the compiler's LDS counter: drain them before the unpacks
+  auto flush_asm = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); flush(); };
+  // software pipeline over PD static slots: slot k is consumed, then refilled with the pass PD
+  // ahead, so the other PD - 1 slots' loads stay in flight across its atomics.  Whole groups of PD
+  // passes run branch-free; the last npass % PD passes are consumed after the loop.
+  const int npass = (t1 - t0 + 1) >> 1;
+  const bool aligned = (lo & 127) == 0 && ((hi & 127) == 0 || (long)hi == a.n);
+  auto run = [&](auto masked) {
+    uint4 br[PD], qr[PD];
 #pragma unroll
-    for (int k = 0; k < PD; ++k) {
-      const int tt = t + 2 * k;                               // passes past t1 add zeros (mask)
-      uint4 q0 = qr[k];
-      mask(tt + ts, q0);
-      const uint32_t B[4] = {br[k].x, br[k].y, br[k].z, br[k].w};
-      const int Q[4] = {(int)q0.x, (int)q0.y, (int)q0.z, (int)q0.w};
-      auto rows4 = [&](auto kc) {                             // rows 4k..4k+3 live in quad lane k
-        constexpr int kq = decltype(kc)::value;
+    for (int j = 0; j < PD; ++j) load(t0 + 2 * j + ts, br[j], qr[j]);
+    int passes = 0, pi = 0;
+    // the last pass stays out of the branch-free loop: its second tile (waves with ts = 1) may lie
+    // past t1 when the item has an odd tile count (the load clamps it to tile t1 - 1)
+    for (; pi + PD < npass; pi += PD) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t qj = (uint32_t)__builtin_amdgcn_mov_dpp(Q[j], kq * 0x55, 0xf, 0xf, false);
-          const uint32_t bj = (B[kq] >> (j * 8)) & 0xff;
-          atomicAdd(&ht[(bj << 6) | lb], qj);
-        }
-      };
-      rows4(std::integral_constant<int, 0>{});
-      rows4(std::integral_constant<int, 1>{});
-      rows4(std::integral_constant<int, 2>{});
-      rows4(std::integral_constant<int, 3>{});
-      load(tt + 2 * PD + ts, br[k], qr[k]);
-      if (++passes == 16) { passes = 0; flush(); }
+      for (int k = 0; k < PD; ++k) {
+        const int tt = t0 + 2 * (pi + k);
+        consume(br[k], qr[k], tt, masked);
+        load(tt + 2 * PD + ts, br[k], qr[k]);
+        if (++passes == 16) { passes = 0; flush_asm(); }
+      }
     }
-  }
+#pragma unroll
+    for (int k = 0; k < PD; ++k)
+      if (pi + k < npass) {
+        const int tt = t0 + 2 * (pi + k);
+        if (tt + ts < t1) consume(br[k], qr[k], tt, masked);       // wave-uniform
+        if (++passes == 16) { passes = 0; flush_asm(); }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  if (aligned) run(std::false_type{});
+  else run(std::true_type{});
   flush();
   // slab [item][st][f][b]: transposed through LDS (32 x 256 int64 = 64 KiB) for coalesced stores
   long long* tt = (long long*)ht;
@@ -1173,10 +1248,11 @@ SHIFU_API int shifu_gbdt_hist_root_tile(const void* tiles, long gs_t, long n, co
                                         int mode, int* q, hipStream_t stream) {
   const long nt = (n + 127) / 128;
   if (n <= 0 || n_items <= 0 || (mode != 1 && mode != 2) || gs_t != nt * 4096) return -1;
+  if (nt * 128 > 0x7fffffffL) return -1;                      // row ids are int (items, q offsets)
   const float sc = mode == 1 ? (float)scale_w : (float)(scale_g / (1 << GSH32));
   hipLaunchKernelGGL(gbdt_root_q_kernel, dim3((unsigned)((nt * 128 + 255) / 256)), dim3(256), 0, stream, w, g, n,
                      nt * 128, sc, mode, q);
-  RootTileArgs a{(const uint8_t*)tiles, gs_t, q, items, (long long*)slab, mode};
+  RootTileArgs a{(const uint8_t*)tiles, gs_t, q, items, (long long*)slab, mode, n};
   const size_t lds = NB * 64 * 4;                              // 64 KiB (also the int64 transpose)
   // SHIFU_GBDT_ROOT_PD: tile passes in flight (lab A/B)
   static const int pd = [] { const char* e = getenv("SHIFU_GBDT_ROOT_PD"); return e ? atoi(e) : 4; }();
@@ -1310,11 +1386,14 @@ SHIFU_API int shifu_gbdt_partition_flag(const void* bins, long gs, const void* b
                                         const void* is_cat, void* fbits, int* wcnt, long n, long nmod, float* pred,
                                         const float* node_val, const float* child_l_val,
                                         const float* child_r_val, float scale, int final_level,
+                                        const int* r_start, const int* r_slot, const int* r_end, int r_n,
                                         hipStream_t stream) {
+  if (!pos_node && (!r_start || !r_slot || !r_end || r_n <= 0)) return -1;
+  if (!pos_node && n >= 0x7fffffffL) return -1;
   PartArgs a{(const uint8_t*)bins, gs, (const uint8_t*)bins32, gs32, pos2row, pos_node, split_feat, split_bin, (const uint32_t*)cat_left,
              (const uint8_t*)is_cat, (unsigned long long*)fbits, wcnt, n, nmod, pred, node_val, child_l_val,
              child_r_val, scale,
-             final_level};
+             final_level, r_start, r_slot, r_end, r_n};
   // (a 4-positions-per-thread variant measured the same, 126.9 vs 127.9 ms per balanced round: the
   // pass is bound by the split-feature gather's line traffic, not by load parallelism; r5l)
   hipLaunchKernelGGL(gbdt_partition_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
@@ -1327,10 +1406,12 @@ SHIFU_API int shifu_gbdt_partition_scatter(const int* pos2row, const int* pos_no
                                            const int* split_feat, const int* child_left, const int* child_right,
                                            int* new_pos2row, int* new_pos_node, const float* w_src,
                                            const float* g_src, float* w_dst, float* g_dst, long n,
+                                           const int* r_start, const int* r_slot, const int* r_end, int r_n,
                                            hipStream_t stream) {
   if ((w_dst != nullptr) != (g_dst != nullptr) || (w_dst && (!w_src || !g_src))) return -1;
+  if (!pos_node && (!r_start || !r_slot || !r_end || r_n <= 0 || n >= 0x7fffffffL)) return -1;
   ScatterArgs a{pos2row, pos_node, (const unsigned long long*)fbits, wpre, node_start, node_nleft, node_cum0, split_feat, child_left,
-                child_right, new_pos2row, new_pos_node, w_src, g_src, w_dst, g_dst, n};
+                child_right, new_pos2row, new_pos_node, w_src, g_src, w_dst, g_dst, n, r_start, r_slot, r_end, r_n};
   hipLaunchKernelGGL(gbdt_partition_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a);
   CHECK_HIP(hipGetLastError());
   return 0;
@@ -1556,6 +1637,30 @@ __global__ void gbdt_items_fix_kernel(int* items, int n, const int* starts, cons
 SHIFU_API int shifu_gbdt_items_fix(int* items, int n, const int* starts, const int* ends, hipStream_t stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(gbdt_items_fix_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, items, n, starts, ends);
+  CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// The level's node ranges sorted by start for range_node: empty ranges sort last (start INT_MAX).
+// One block; nn <= DC_MAXN.
+__global__ __launch_bounds__(256) void gbdt_range_index_kernel(const int* starts, const int* ends, int nn,
+                                                               int* r_start, int* r_slot) {
+  for (int i = threadIdx.x; i < nn; i += 256) {
+    const int si = ends[i] > starts[i] ? starts[i] : 0x7fffffff;
+    int rank = 0;
+    for (int j = 0; j < nn; ++j) {
+      const int sj = ends[j] > starts[j] ? starts[j] : 0x7fffffff;
+      rank += (sj < si || (sj == si && j < i)) ? 1 : 0;
+    }
+    r_start[rank] = si;
+    r_slot[rank] = i;
+  }
+}
+
+SHIFU_API int shifu_gbdt_range_index(const int* starts, const int* ends, int nn, int* r_start, int* r_slot,
+                                     hipStream_t stream) {
+  if (nn <= 0 || nn > DC_MAXN) return -1;
+  hipLaunchKernelGGL(gbdt_range_index_kernel, dim3(1), dim3(256), 0, stream, starts, ends, nn, r_start, r_slot);
   CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -99,7 +99,8 @@ struct StripHeadArgs {
   const float* Y;                // [M] targets
   const float* S;                // [M] significance (nullable -> 1)
   float* gw_slab;                // [grid * 8][KH] per-wave output-wgrad partials
-  double* err_slab;              // [grid * 8][2] per-wave (error, weight) sums
+  double* err_slab;              // [grid * 8][2] per-wave (error, weight) sums (err == nullptr)
+  double* err;                   // non-null: per-wave sums added straight into err[2] (double atomics)
   int M, K1, NB, nv, nv1, KH, out_act, loss;
   float flat_out, flat_hid, flat1;
   int ntiles;
@@ -589,7 +590,8 @@ __global__ __launch_bounds__(SH_T, 2) void strip_head_kernel(StripHeadArgs p) {
   if (lane < 2) {
     double a = 0.0;
     for (int l = 0; l < 64; ++l) a += er_s[(wid * 64 + l) * 2 + lane];
-    p.err_slab[srow * 2 + lane] = a;
+    if (p.err) atomicAdd(p.err + lane, a);
+    else p.err_slab[srow * 2 + lane] = a;
   }
 #undef SH_VMWAIT
 #undef SH_KEEP
@@ -654,8 +656,15 @@ SHIFU_API int shifu_strip_head(const void* H, long ldh, const void* W, long ldw,
     return -1;
   const int grid = sh_grid(M);
   StripHeadArgs p{(const bf16_t*)H, ldh, (const bf16_t*)W, ldw, (const bf16_t*)WT, ldwt, (bf16_t*)D, ldd,
-                  (bf16_t*)DZ, lddz, Wo, Y, S, gw_slab, err_slab, M, K1, NB, nv, nv1, KH, out_act, loss,
-                  flat_out, flat_hid, flat1, (M + 255) / 256, g_sh_dbg_rows};
+                  (bf16_t*)DZ, lddz, Wo, Y, S, gw_slab, err_slab, nullptr, M, K1, NB, nv, nv1, KH, out_act,
+                  loss, flat_out, flat_hid, flat1, (M + 255) / 256, g_sh_dbg_rows};
+  // the error sums: each wave's (error, weight) pair added into err by double atomics in the
+  // kernel's tail (the two chunk lanes add into the same err already: order-free up to rounding).
+  // A one-block reduction kernel after it sat on its lane's critical path for up to 1.5 ms per
+  // chunk, waiting for a CU slot behind the other lane's persistent kernel (r6 MLP kernel trace).
+  // SHIFU_SH_ERR_SLAB=1: per-wave slabs + the reduction kernel (lab A/B)
+  static const bool err_slab_path = [] { const char* e = getenv("SHIFU_SH_ERR_SLAB"); return e && atoi(e) == 1; }();
+  if (!err_slab_path) p.err = err;
 #define SH_L(A_, N_) hipLaunchKernelGGL((strip_head_kernel<A_, A_, N_>), dim3(grid), dim3(SH_T), SH_LDS, stream, p)
 #define SH_ACTS(N_) switch (act) { case 0: SH_L(0, N_); break; case 1: SH_L(1, N_); break; \
     case 2: SH_L(2, N_); break; case 3: SH_L(3, N_); break; case 4: SH_L(4, N_); break; \
@@ -668,7 +677,7 @@ SHIFU_API int shifu_strip_head(const void* H, long ldh, const void* W, long ldw,
 #endif
 #undef SH_ACTS
 #undef SH_L
-  hipLaunchKernelGGL(sh_err_kernel, dim3(1), dim3(256), 0, stream, err_slab, grid * 8, err);
+  if (err_slab_path) hipLaunchKernelGGL(sh_err_kernel, dim3(1), dim3(256), 0, stream, err_slab, grid * 8, err);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }

@@ -585,23 +585,26 @@ def test_gpu_device_decisions_match_host_path(case, monkeypatch):
         cfg = TreeConfig("RF", tree_num=4, max_depth=6, feature_subset_strategy="HALF", min_instances_per_node=2,
                          bagging_sample_rate=0.6, sample_with_replacement=True, seed=5)
     runs = []
-    for dev_dec in (True, False):
+    # device decisions with the node-range lookup, with the per-position node array, host path
+    for dev_dec, ranges in ((True, True), (True, False), (False, False)):
         monkeypatch.setattr(gb, "DEV_DECIDE", dev_dec)
+        monkeypatch.setattr(gb, "RANGE_NODES", ranges)
         tr = TreeTrainer(cfg, data)
         assert tr._pipelined(1) == dev_dec
         tr.train()
         runs.append(tr)
-    a, b = runs
-    assert a.hist_rows_total == b.hist_rows_total
-    for x, y_ in zip(a.trees, b.trees):
-        assert (x.feat == y_.feat).all() and (x.thr == y_.thr).all()
-        assert np.array_equal(x.value, y_.value) and np.array_equal(x.wgt_cnt, y_.wgt_cnt)
-        assert np.array_equal(np.asarray(x.cat_left), np.asarray(y_.cat_left))
-    if case == "gbt_categorical":
-        assert any((np.asarray(t.cat_left) != 0).any() for t in a.trees)
-    assert torch.equal(a.pred, b.pred)
-    # (the residual kernel's error sum uses float64 atomics: equal up to summation order)
-    assert np.allclose(a.train_errors, b.train_errors, rtol=1e-9, atol=0)
+    b = runs[-1]
+    for a in runs[:-1]:
+        assert a.hist_rows_total == b.hist_rows_total
+        for x, y_ in zip(a.trees, b.trees):
+            assert (x.feat == y_.feat).all() and (x.thr == y_.thr).all()
+            assert np.array_equal(x.value, y_.value) and np.array_equal(x.wgt_cnt, y_.wgt_cnt)
+            assert np.array_equal(np.asarray(x.cat_left), np.asarray(y_.cat_left))
+        if case == "gbt_categorical":
+            assert any((np.asarray(t.cat_left) != 0).any() for t in a.trees)
+        assert torch.equal(a.pred, b.pred)
+        # (the residual kernel's error sum uses float64 atomics: equal up to summation order)
+        assert np.allclose(a.train_errors, b.train_errors, rtol=1e-9, atol=0)
 
 
 def test_categorical_split_with_many_categories_partitions_rows():

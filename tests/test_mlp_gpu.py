@@ -160,7 +160,8 @@ def test_strip_head_matches_head_plus_dgrad(hidden, acts, loss, n, monkeypatch):
     assert abs(float(a.err_acc[1]) - float(b.err_acc[1])) / float(b.err_acc[1]) < 1e-6
     a.grad.zero_(); a.err_acc.zero_(); a.accumulate_gradients(da)
     torch.cuda.synchronize()
-    assert torch.equal(a.grad, g1) and torch.equal(a.err_acc, e1)
+    # gradients bitwise; the error sums are per-wave double atomics (equal up to summation order)
+    assert torch.equal(a.grad, g1) and torch.allclose(a.err_acc, e1, rtol=1e-12, atol=0)
 
 
 @pytest.mark.parametrize("M,K,N,NB,nv,epi,act", [
