@@ -761,7 +761,10 @@ class MLPTrainer:
                          a_out.data_ptr(), kp[l + 1], nat.ptr(ders[l + 1]), kp[l + 1], None, 0, None, 0,
                          mc, kp[l + 1], kp[l], 0, act, sp.hidden[l], 1, sp.flat_spot(sp.acts[l]), st)
         fused_dgrad = False
-        if head and self.strip_head:
+        # the strip head addresses the chunk's H1 / DZ1 / D2 with 32-bit buffer offsets: chunks of
+        # 4M+ rows at K1 = 512 take the 8-phase head + the dgrad kernel instead
+        strip = self.strip_head and mc * max(kp[L - 1], kp[L]) * 2 < (1 << 32) if L >= 1 else False
+        if head and strip:
             # last hidden forward + output + loss + deltas + output wgrad + the dgrad of the layer
             # below in one persistent kernel (the head deltas never leave the chip)
             lh = L - 1
