@@ -86,7 +86,8 @@ struct StripArgs {
   bf16_t* C; long ldc;         // [M, N]
   int M, N, K, NB, n_valid, bias_col;
   int ntiles;                  // ceil(M / 256) * ceil(N / 256)
-  int dbg;                     // LAB builds only: 1 no epilogue, 4 no MFMAs (operands kept live)
+  int dbg;                     // LAB builds only: 1 no epilogue, 4 no MFMAs (operands kept live),
+                               // 8 no B LDS-DMA, 16 no A loads (timing ablations: results invalid)
 };
 
 template <int EPI, int ACT, bool LAB>
@@ -139,10 +140,14 @@ __global__ __launch_bounds__(SN_T, 2) void strip_nt_kernel(StripArgs p) {
     }
   };
   auto issue = [&](int slot, bf16x8 (&a)[2][2]) __attribute__((always_inline)) {
+    if (!(LAB && (p.dbg & 8))) {                     // LAB dbg 8: no B LDS-DMA pieces
 #pragma unroll
-    for (int i = 0; i < 4; ++i) issue_dma(slot, i);
-    issue_a(a, 0);
-    issue_a(a, 1);
+      for (int i = 0; i < 4; ++i) issue_dma(slot, i);
+    }
+    if (!(LAB && (p.dbg & 16))) {                    // LAB dbg 16: no A loads
+      issue_a(a, 0);
+      issue_a(a, 1);
+    }
     advance();
   };
 
