@@ -287,10 +287,16 @@ constexpr int H6_NE = 4 * NB * 16 / H6_T;        // entries each thread unpacks 
 // PD: passes of (bins, w, g) in flight ahead of the one being added (row ids PD passes further):
 // with one block of 16 waves per CU a single pass ahead keeps ~4 MB of gathers in flight over the
 // chip, short of what HBM latency x bandwidth asks for
-template <int PD>
+//
+// PERM: LDS laid out [quarter pair][NB][2][16] instead of [quarter][NB][16], so a bin's row is 256
+// bytes and each atomic's byte address {lane/step constant, bin, quarter pair, 0} is ONE v_perm_b32
+// of the rotated record word and a per-(lane, step) constant (the [4][NB][16] layout needed a byte
+// extract + shift-add per atomic).  Banks: a 16-lane group still hits 16 distinct bank pairs
+// ((qt & 1) * 32 + 2 f for its 16 features, any bins).
+template <int PD, bool PERM>
 __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int* pairs) {
   constexpr int HFLUSH = 4096 / H6_RPP;
-  extern __shared__ __attribute__((aligned(16))) unsigned long long h6[];    // [4][NB][16]
+  extern __shared__ __attribute__((aligned(16))) unsigned long long h6[];    // [4][NB][16] (see PERM)
   const int pr = xcd_remap(blockIdx.x, gridDim.x);
   // items of groups 2j (ia) and 2j + 1 (ib) of one node and row range; either may be -1
   const int ia = pairs[pr * 2], ib = pairs[pr * 2 + 1], i0 = ia >= 0 ? ia : ib;
@@ -308,6 +314,7 @@ __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int
   // grp is even: its 64-B half of the quad record starts at byte (grp & 3) * 32 (0 or 64)
   const uint8_t* gb = a.bins + (size_t)(grp >> 2) * a.gs + (grp & 3) * FG + qt * 16;
   unsigned long long* base = h6 + qt * NB * 16;
+  const uint32_t cq = ((uint32_t)(qt >> 1) << 16) | ((uint32_t)(qt & 1) << 7);   // PERM layout
   auto rec = [&](int v) { return *(const uint4*)(gb + (size_t)(a.nmod ? (long)v % a.nmod : (long)v) * QF); };
   long long accw[H6_NE], accg[H6_NE];
 #pragma unroll
@@ -326,13 +333,21 @@ __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int
     for (int k = 0; k < 4; ++k) R[k] = __builtin_amdgcn_alignbyte(Y[(k + 1) & 3], Y[k], r & 3);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
-      atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
+      if constexpr (PERM) {
+        // {cq byte 0 + 8 f, bin, quarter pair, 0}: selector bytes 0 / 2 from src1, 4 + (j & 3) = the bin
+        const uint32_t cj = cq | ((((uint32_t)(j + r)) & 15u) << 3);
+        const uint32_t addr = __builtin_amdgcn_perm(R[j >> 2], cj, 0x0c020000u | ((4u + (j & 3)) << 8));
+        asm volatile("ds_add_u64 %0, %1" : : "v"(addr), "v"(q) : "memory");
+      } else {
+        const uint32_t b = (R[j >> 2] >> ((j & 3) * 8)) & 0xff;
+        atomicAdd(&base[(b << 4) | ((j + r) & 15)], q);
+      }
     }
   };
   auto flush = [&](int& it) {
     if (++it == HFLUSH) {
       it = 0;
+      if constexpr (PERM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm atomics
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < H6_NE; ++k) {
@@ -371,6 +386,7 @@ __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int
       rn[k] = row_of(pk + 2 * PD * H6_RPP + t4);
     }
   }
+  if constexpr (PERM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < H6_NE; ++k) unpack_add(h6[threadIdx.x + k * H6_T], accw[k], accg[k]);
@@ -384,7 +400,9 @@ __global__ __launch_bounds__(H6_T) void gbdt_hist64_kernel(HistArgs a, const int
 #pragma unroll
     for (int k = 0; k < H6_NE; ++k) {
       const int e = threadIdx.x + k * H6_T;
-      const int f = (e >> 12) * 16 + (e & 15), b = (e >> 4) & (NB - 1);
+      // PERM: e = (pair, bin, quarter & 1, feature) -> quarter ((e >> 13) << 1) | ((e >> 4) & 1)
+      const int f = PERM ? ((((e >> 13) << 1) | ((e >> 4) & 1)) * 16 + (e & 15)) : ((e >> 12) * 16 + (e & 15));
+      const int b = PERM ? ((e >> 5) & (NB - 1)) : ((e >> 4) & (NB - 1));
       tsm[f * NB + b] = st ? accg[k] : accw[k];
     }
     __syncthreads();
@@ -1354,11 +1372,15 @@ SHIFU_API int shifu_gbdt_hist64(const void* bins, long gs, const int* pos2row, c
              (float)scale_w, (float)scale_g, nmod};
   // SHIFU_GBDT_H64_PD: passes in flight (lab A/B)
   static const int pd = [] { const char* e = getenv("SHIFU_GBDT_H64_PD"); return e ? atoi(e) : 3; }();
+  // SHIFU_GBDT_H64_PERM=0: the [quarter][NB][16] layout with extract + shift-add addresses (lab A/B)
+  static const bool perm = [] { const char* e = getenv("SHIFU_GBDT_H64_PERM"); return !e || atoi(e) != 0; }();
   const size_t lds = 4 * NB * 16 * 8;
-  if (pd >= 4) hipLaunchKernelGGL(gbdt_hist64_kernel<4>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
-  else if (pd == 3) hipLaunchKernelGGL(gbdt_hist64_kernel<3>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
-  else if (pd == 2) hipLaunchKernelGGL(gbdt_hist64_kernel<2>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
-  else hipLaunchKernelGGL(gbdt_hist64_kernel<1>, dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  if (perm && pd >= 3) hipLaunchKernelGGL((gbdt_hist64_kernel<3, true>), dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else if (perm) hipLaunchKernelGGL((gbdt_hist64_kernel<2, true>), dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else if (pd >= 4) hipLaunchKernelGGL((gbdt_hist64_kernel<4, false>), dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else if (pd == 3) hipLaunchKernelGGL((gbdt_hist64_kernel<3, false>), dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else if (pd == 2) hipLaunchKernelGGL((gbdt_hist64_kernel<2, false>), dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
+  else hipLaunchKernelGGL((gbdt_hist64_kernel<1, false>), dim3(n_pairs), dim3(H6_T), lds, stream, a, pairs);
   CHECK_HIP(hipGetLastError());
   return 0;
 }
