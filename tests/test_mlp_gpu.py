@@ -391,3 +391,25 @@ def test_nn_scoring_bf16_close_to_fp32():
     assert np.abs(a - b).max() <= 2e-2
 
 
+
+
+def test_strip_head_falls_back_on_4m_row_chunks():
+    """A 4M-row chunk puts the strip head's H1 / DZ1 operands past 32-bit buffer offsets at
+    K1 = 512: the trainer takes the 8-phase head + dgrad kernels for that chunk (the launcher used
+    to surface as an error) and the gradients match 1M-row chunks (strip head) up to summation
+    order."""
+    spec = MLPSpec(n_in=60, hidden=[500, 200], acts=["sigmoid", "sigmoid"], n_out=1)
+    n = (1 << 22) + 4096
+    x, y, s = _mk(spec, n, seed=9)
+    big = MLPTrainer(spec, device="cuda", seed=3, chunk_rows=1 << 22)
+    small = MLPTrainer(spec, device="cuda", seed=3, chunk_rows=1 << 20)
+    assert big.strip_head and small.strip_head
+    small.params.flat.copy_(big.params.flat)
+    for t in (big, small):
+        d = t.prepare(x, y, s)
+        t.grad.zero_(); t.err_acc.zero_(); t.accumulate_gradients(d)
+    torch.cuda.synchronize()
+    for va, vb in zip(big.params.views(big.grad), small.params.views(small.grad)):
+        r = (va - vb).norm() / vb.norm().clamp(min=1e-12)
+        assert r < 1e-2, float(r)
+    assert abs(float(big.err_acc[0]) - float(small.err_acc[0])) / float(small.err_acc[0]) < 1e-4
