@@ -45,6 +45,7 @@ LOSS_IDS = {"squared": 0, "halfgradsquared": 1, "absolute": 2, "log": 3}
 
 # histogram work items per level (node x row-range x 32-feature group); SHIFU_GBDT_ITEMS: lab A/B
 TARGET_ITEMS = int(os.environ.get("SHIFU_GBDT_ITEMS", "4096"))   # favourable +2.3 %, balanced even vs 2048 (profiles/r5/gbdt/items_sweep_r5.txt)
+TARGET_ITEMS_FEW = int(os.environ.get("SHIFU_GBDT_ITEMS_FEW", str(TARGET_ITEMS // 2)))   # non-root levels, <= 4 built nodes
 
 
 def _strategy_count(strategy, n_feat: int, input_num: int, tree_num: int) -> int:
@@ -819,7 +820,11 @@ class TreeTrainer:
         m = np.array([_zm(z) for z in bz], np.int64)
         rows_built = sum(_zm(z) for z in nodes if z["built"])
         if self.items_per_node_group is None:
-            k = np.maximum(1, np.rint(TARGET_ITEMS * (m / max(1, rows_built)) / G).astype(np.int64))
+            # below the root, levels with few built nodes run fewer, longer items (less per-item LDS
+            # zeroing and slab traffic; levels 3 / 4 of the balanced bench 13.1 / 12.3 vs 13.9 /
+            # 12.5 ms, levels with 8+ nodes lose with it: profiles/r6/gbdt/items_per_level_r6.txt)
+            target = TARGET_ITEMS_FEW if (not getattr(self, "_root_level", True) and n_built <= 4) else TARGET_ITEMS
+            k = np.maximum(1, np.rint(target * (m / max(1, rows_built)) / G).astype(np.int64))
             k = np.minimum(np.minimum(k, np.maximum(1, m // 4096)), 64)
         else:
             k = np.full(len(bz), int(self.items_per_node_group), np.int64)
