@@ -624,3 +624,40 @@ def test_categorical_split_with_many_categories_partitions_rows():
     left = {c for c in range(41) if (int(t.cat_left[1][c >> 5]) >> (c & 31)) & 1}
     assert left == set(pos.tolist()) or left.isdisjoint(pos.tolist())
     assert abs(tr.train_errors[0]) < 1e-6
+
+
+def test_estimated_items_cover_each_node_exactly_once():
+    """Histogram items sized from estimated child sizes (TreeTrainer._make_items(est=True): rows
+    (slot, chunk, n_chunks, group)) resolved against the real node ranges the way
+    gbdt_items_fix_kernel does: every (node, group) covers its node's rows exactly once, whether
+    the estimate is high, low or the node is empty."""
+    from shifu_amd.models.gbdt import TreeTrainer, TreeConfig
+    data, _, _ = _data(n=500, f=70)
+    tr = TreeTrainer(TreeConfig("GBT", tree_num=1, max_depth=3, feature_subset_strategy="ALL"), data)
+    tr._root_level = False
+    real = [(0, 3_000_000), (3_000_000, 3_000_000), (3_000_000, 3_900_000), (5_000_000, 5_000_017)]
+    est = [2_000_000, 40_000, 5_000_000, 1]
+    nodes = [{"slot": s, "built": True, "m": e} for s, e in enumerate(est)]
+    nodes.append({"slot": 4, "built": False, "m": 123})
+    items, ni, max_items = tr._make_items(nodes, 4, est=True)
+    assert items.shape[1] == 4 and len(items)
+    G = tr.ngroups
+    starts = np.array([r[0] for r in real] + [0])
+    ends = np.array([r[1] for r in real] + [0])
+    cover = {}
+    for slot, ch, k, grp in items:                    # gbdt_items_fix_kernel
+        s, m = starts[slot], max(0, ends[slot] - starts[slot])
+        step = (m + k - 1) // k
+        lo, hi = min(m, ch * step), min(m, min(m, ch * step) + step)
+        cover.setdefault((slot, grp), []).append((s + lo, s + hi))
+    for slot in range(4):
+        for grp in range(G):
+            segs = sorted(cover.get((slot, grp), []))
+            tot = sum(h - l for l, h in segs)
+            assert tot == ends[slot] - starts[slot], (slot, grp, tot)
+            for (l0, h0), (l1, h1) in zip(segs, segs[1:]):
+                assert h0 <= l1                        # no overlap
+            ids = ni[slot, grp]
+            assert sorted(int(i) for i in ids if i >= 0) == sorted(
+                int(i) for i in np.flatnonzero((items[:, 0] == slot) & (items[:, 3] == grp)))
+    assert (ni[4] < 0).all()                          # derived node: no items
