@@ -1714,7 +1714,10 @@ HIST64 = os.environ.get("SHIFU_GBDT_HIST64", "1") != "0"
 # 1024-thread blocks (one per CU) lost on short row ranges (2M rows: 1.9 vs 1.0 ms); with 4096
 # items they win or tie down to 2.8M rows per node (balanced levels 5 / 6: 13.2 / 14.0 vs 14.5 /
 # 14.8 ms) and tie on the favourable labels' small levels (profiles/r5/gbdt/hist64_threshold_r5.txt)
-HIST64_MIN_NODE_ROWS = int(os.environ.get("SHIFU_GBDT_HIST64_MIN_NODE_ROWS", "2000000"))
+# (r6, with the static-slot prefetch and v_perm addressing: 500K rows per built node -- favourable
+# levels 3 / 5 / 6 at 2.26 / 3.33 / 4.07 vs 2.36 / 3.51 / 4.22 ms, balanced unchanged;
+# profiles/r6/gbdt/hist64_threshold_r6.txt)
+HIST64_MIN_NODE_ROWS = int(os.environ.get("SHIFU_GBDT_HIST64_MIN_NODE_ROWS", "500000"))
 # split decisions on the device, queued ahead of the partition (one host sync per level, which
 # the partition hides); SHIFU_GBDT_DEV_DECIDE=0: host decisions between the split scan and the
 # partition (two syncs per level).  Trees with MaxLeaves, native multi-class trees and levels of
