@@ -1273,7 +1273,7 @@ SHIFU_API int shifu_gbdt_hist_root_tile(const void* tiles, long gs_t, long n, co
   RootTileArgs a{(const uint8_t*)tiles, gs_t, q, items, (long long*)slab, mode, n};
   const size_t lds = NB * 64 * 4;                              // 64 KiB (also the int64 transpose)
   // SHIFU_GBDT_ROOT_PD: tile passes in flight (lab A/B)
-  static const int pd = [] { const char* e = getenv("SHIFU_GBDT_ROOT_PD"); return e ? atoi(e) : 4; }();
+  static const int pd = [] { const char* e = getenv("SHIFU_GBDT_ROOT_PD"); return e ? atoi(e) : 6; }();   // 6: root 19.5-19.7 vs 19.8-20.0 ms with 4 (r6 gbdtenv_pd3)
   if (mode == 1) hipLaunchKernelGGL((gbdt_root_tile_kernel<1, 2>), dim3(n_items), dim3(RT_T), lds, stream, a);
   else if (pd >= 6) hipLaunchKernelGGL((gbdt_root_tile_kernel<2, 6>), dim3(n_items), dim3(RT_T), lds, stream, a);
   else if (pd >= 4) hipLaunchKernelGGL((gbdt_root_tile_kernel<2, 4>), dim3(n_items), dim3(RT_T), lds, stream, a);
